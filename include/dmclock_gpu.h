@@ -1,0 +1,218 @@
+/* SPDX-License-Identifier: LGPL-2.1
+ *
+ * dmclock_gpu.h -- C-ABI of the MI355X-native dmClock server queue.
+ *
+ * This is the drop-in boundary for the hot path named by BASELINE.json's
+ * north_star: the server-side dmClock priority queue of the reference
+ * (crimson::dmclock::PullPriorityQueue / PushPriorityQueue,
+ * /root/reference/src/dmclock_server.h).  The reference's boundary is a C++
+ * template API, not an FFI; every entry point below names the reference member
+ * it replaces (file:line).  The C++ facade in
+ * dmclock_amd/include/dmclock_server.h re-exports the reference's template
+ * names on top of these functions, so existing callers compile unchanged.
+ *
+ * Conventions
+ *  - plain pointers and sizes only; no torch / HIP types in signatures.
+ *  - a queue lives on one HIP device; every call on one queue handle must be
+ *    serialised by the caller (the facade holds a mutex, mirroring the
+ *    reference's data_mtx, dmclock_server.h:762).
+ *  - clients are dense "slots" [0, max_clients); the facade maps the
+ *    reference's client id type C to slots.
+ *  - every function returns a status code (DMC_OK or a negative DMC_E*);
+ *    nothing aborts.  Where the reference asserts, we return a code.
+ *  - *_device variants take device pointers and run asynchronously on the
+ *    queue's HIP stream (dmc_queue_stream); the others take host pointers and
+ *    return when results are in host memory.
+ */
+#ifndef DMCLOCK_GPU_H
+#define DMCLOCK_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------ status codes */
+#define DMC_OK 0
+#define DMC_EAGAIN 11          /* AtLimit::Reject rejected the request (errno EAGAIN, dmclock_server.h:989-993) */
+#define DMC_EINVAL (-1)        /* bad argument (unknown slot, bad params, ...) */
+#define DMC_ENOMEM (-2)        /* device allocation failed */
+#define DMC_EDEVICE (-3)       /* HIP runtime error */
+#define DMC_EBADTAG (-1001)    /* cost==0 or r and w both 0 (reference asserts, dmclock_server.h:158,182) */
+#define DMC_EBADPARAMS (-1002) /* rho > delta (reference asserts, dmclock_recs.h:51) */
+#define DMC_EQUEUEFULL (-1004) /* the client's request ring is full (documented deviation: the
+                                  reference's per-client std::deque is unbounded, :360) */
+#define DMC_ENOTREG (-1005)    /* slot not registered */
+
+/* ------------------------------------------------------------ enums */
+/* AtLimit, dmclock_server.h:74-84 */
+#define DMC_AT_LIMIT_WAIT 0
+#define DMC_AT_LIMIT_ALLOW 1
+#define DMC_AT_LIMIT_REJECT 2
+
+/* NextReqType, dmclock_server.h:506 */
+#define DMC_NEXT_RETURNING 0
+#define DMC_NEXT_FUTURE 1
+#define DMC_NEXT_NONE 2
+
+/* PhaseType, dmclock_recs.h:33 */
+#define DMC_PHASE_RESERVATION 0
+#define DMC_PHASE_PRIORITY 1
+
+/* ------------------------------------------------------------ records */
+
+/* Queue construction parameters.  Replaces the PullPriorityQueue /
+ * PushPriorityQueue constructors (dmclock_server.h:1314-1341, 1545-1580) and
+ * their template parameters IsDelayed and U1 (:1279, :1505).  The heap
+ * branching factor B has no meaning on the device (there are no heaps). */
+typedef struct dmc_queue_params {
+  uint32_t max_clients;      /* slot capacity of the client table            */
+  uint32_t ring_capacity;    /* per-client request ring, power of two        */
+  uint32_t max_batch;        /* max requests per add batch and decisions per pull batch */
+  int32_t delayed;           /* IsDelayed (DelayedTagCalc), :277-280          */
+  int32_t dynamic_info;      /* U1: ClientInfo re-read at every tag, :870-875 */
+  int32_t at_limit;          /* DMC_AT_LIMIT_*                                */
+  double reject_threshold;   /* RejectThreshold (AtLimitParam variant), :86-93 */
+  double anticipation_timeout; /* :151-161                                    */
+  int32_t device;            /* HIP device ordinal                            */
+  int32_t reserved;
+} dmc_queue_params;
+
+/* One request of an add batch.  Replaces the arguments of
+ * add_request(RequestRef&&, const C&, const ReqParams&, Time, Cost)
+ * (dmclock_server.h:1398-1417; ReqParams dmclock_recs.h:40-72).  `handle`
+ * stands for the RequestRef: the device never sees R, only this handle, which
+ * comes back in the decision that dispatches the request. */
+typedef struct dmc_request {
+  uint32_t slot;   /* client slot                                           */
+  uint32_t cost;   /* Cost, dmclock_recs.h:31                               */
+  double time;     /* arrival Time, dmclock_util.h:33                       */
+  uint32_t delta;  /* ReqParams::delta                                      */
+  uint32_t rho;    /* ReqParams::rho                                        */
+  uint64_t handle; /* opaque request handle                                 */
+} dmc_request;     /* 32 bytes */
+
+/* One dispatch decision of a pull batch.  Replaces PullReq::Retn
+ * (dmclock_server.h:1287-1292): client, request, phase, cost; plus the tag
+ * the request was dispatched with (before reduce_reservation_tags) so that
+ * parity can be checked at the tag level. */
+typedef struct dmc_decision {
+  uint64_t handle;     /* the request's handle                                */
+  double tag_r;        /* RequestTag::reservation at dispatch                 */
+  double tag_p;        /* RequestTag::proportion                              */
+  double tag_l;        /* RequestTag::limit                                   */
+  uint32_t slot;       /* client slot                                         */
+  uint32_t cost;       /* Cost                                                */
+  uint32_t phase;      /* DMC_PHASE_*                                         */
+  uint32_t flags;      /* bit0: the key tied with another client's (GPU: lowest slot won) */
+} dmc_decision;        /* 48 bytes */
+
+/* Outcome of a pull batch: how many decisions were returned and, when the
+ * batch stopped early, what the stopping pull_request(now) returned
+ * (PullReq::type and its Time, dmclock_server.h:1294-1305). */
+typedef struct dmc_pull_result {
+  uint32_t n_decisions; /* decisions written                                 */
+  uint32_t next_type;   /* DMC_NEXT_RETURNING if k decisions were made, else
+                           DMC_NEXT_FUTURE / DMC_NEXT_NONE of the stopping pull */
+  double when;          /* future time when next_type == DMC_NEXT_FUTURE     */
+  uint32_t n_reservation; /* decisions in the reservation phase              */
+  uint32_t n_priority;    /* decisions in the priority phase                 */
+} dmc_pull_result;
+
+/* Per-client state snapshot for tests and debugging (ClientRec, :355-393). */
+typedef struct dmc_client_state {
+  double prev_r, prev_p, prev_l, prev_arrival; /* prev_tag                   */
+  double prop_delta;
+  double front_r, front_p, front_l, front_arrival; /* next_request().tag     */
+  double r_inv, w_inv, l_inv;                  /* ClientInfo inverses        */
+  uint64_t last_tick;
+  uint32_t count;       /* queued requests                                   */
+  uint32_t cur_delta, cur_rho;
+  uint8_t idle, front_ready, registered, pad;
+} dmc_client_state;
+
+/* Queue counters, dmclock_server.h:806-812 */
+typedef struct dmc_stats {
+  uint64_t tick;
+  uint64_t reserv_sched_count;
+  uint64_t prop_sched_count;
+  uint64_t limit_break_sched_count;
+  uint64_t clients;   /* registered slots (client_count, :551-554)           */
+  uint64_t requests;  /* queued requests (request_count, :557-564)           */
+} dmc_stats;
+
+typedef struct dmc_queue dmc_queue;
+
+/* ------------------------------------------------------------ lifecycle */
+
+/* Replaces PullPriorityQueue(ClientInfoFunc, AtLimitParam, double)
+ * (dmclock_server.h:1314-1341).  Allocates the HBM client table and rings. */
+int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out);
+int dmc_queue_destroy(dmc_queue* q);
+/* The HIP stream (hipStream_t) every *_device call runs on. */
+void* dmc_queue_stream(dmc_queue* q);
+int dmc_queue_sync(dmc_queue* q);
+const char* dmc_strerror(int code);
+
+/* ------------------------------------------------------------ clients */
+
+/* First sight of a client: do_add_request's client_map.emplace +
+ * client_info_f + ClientRec(idle=true) (dmclock_server.h:920-932, 381-393).
+ * active != 0 is the bulk-registration deviation used for 1M-client
+ * populations (idle=false, prop_delta=0), applied identically to the oracle. */
+int dmc_client_register(dmc_queue* q, uint32_t slot, double reservation,
+                        double weight, double limit, int active);
+int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                              const double* reservation, const double* weight,
+                              const double* limit, int active);
+/* update_client_info(s) after client_info_f returns new values
+ * (dmclock_server.h:633-648; ClientInfo::update :111-118). */
+int dmc_client_update_info(dmc_queue* q, uint32_t slot, double reservation,
+                           double weight, double limit);
+/* do_clean's idle marking and erase, as explicit calls (dmclock_server.h
+ * :1206-1255): mark_idle sets idle=true; erase drops the client and its
+ * queued requests (their handles are written to handles_out, capacity cap). */
+int dmc_client_mark_idle(dmc_queue* q, uint32_t slot);
+int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
+                     uint32_t cap, uint32_t* n_out);
+int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* out);
+/* last_tick of every slot in [0, n) (for the facade's do_clean). */
+int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out);
+
+/* ------------------------------------------------------------ hot path */
+
+/* A batch of add_request_time calls in order (dmclock_server.h:1368-1417,
+ * do_add_request :913-1018).  rc_out[i] gets 0, DMC_EAGAIN, or an error. */
+int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
+                  int32_t* rc_out);
+int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
+                         int32_t* d_rc_out);
+
+/* Up to k successive pull_request(now) calls (dmclock_server.h:1425-1489),
+ * stopping after the first that does not return a request. */
+int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
+                   dmc_pull_result* result);
+int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
+                          dmc_decision* d_out, dmc_pull_result* d_result);
+
+/* ------------------------------------------------------------ maintenance */
+
+/* remove_by_client (dmclock_server.h:594-625): queued handles in FIFO order
+ * (reverse != 0: LIFO) are written to handles_out; the queue is cleared. */
+int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
+                         uint64_t* handles_out, uint32_t cap, uint32_t* n_out);
+/* Queued handles of one client, FIFO order (for remove_by_req_filter, :567-585). */
+int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
+                        uint32_t cap, uint32_t* n_out);
+/* Keep only the requests whose keep[i] != 0 (i in FIFO order, n == count):
+ * ClientRec::remove_by_req_filter's erase (:440-480). */
+int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
+                      const uint8_t* keep);
+int dmc_stats_get(dmc_queue* q, dmc_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DMCLOCK_GPU_H */
