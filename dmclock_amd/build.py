@@ -1,0 +1,37 @@
+"""Build the HIP engine in-tree: dmclock_amd/libdmclock_gpu.so (gfx950)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libdmclock_gpu.so")
+SOURCES = [os.path.join(HERE, "csrc", "dmc_engine.hip")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", "dmc_device.h"),
+                  os.path.join(ROOT, "include", "dmclock_gpu.h")]
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               # exact IEEE double tag arithmetic: no FMA contraction
+               "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+
+
+def up_to_date():
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", LIB] + SOURCES
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,327 @@
+// SPDX-License-Identifier: LGPL-2.1
+//
+// dmc_device.h -- device-side data layout and per-client arithmetic of the
+// MI355X dmClock engine.  Everything here is exact IEEE-754 double arithmetic
+// in the reference's order (no FMA contraction: explicit __d*_rn intrinsics,
+// and the library is built with -ffp-contract=off).
+//
+// Layout (per queue, N client slots, ring capacity Q):
+//   client table, struct-of-arrays in HBM: prev_{r,p,l,arr}, {r,w,l}_inv,
+//     prop_delta, front_{r,p,l} (the heap keys of the reference, cached),
+//     head/count (ring cursor), cur_{delta,rho}, last_tick, flags.
+//   request rings: ring[slot * Q + i], one 64-byte ReqEntry per request.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmc {
+
+constexpr double kInf = __builtin_huge_val();
+constexpr uint64_t kMaxKey = ~0ull;
+
+enum : uint8_t { F_IDLE = 1, F_READY = 2, F_REG = 4 };
+
+// One queued request: its tag (RequestTag, dmclock_server.h:135-143) plus the
+// opaque handle that stands for the RequestRef.
+struct alignas(16) ReqEntry {
+  double r, p, l, arrival;
+  uint64_t handle;
+  uint32_t cost, delta, rho, pad;
+  uint64_t pad2;
+};
+static_assert(sizeof(ReqEntry) == 64, "ReqEntry must be 64 bytes");
+
+// Client table pointers (passed by value to kernels).
+struct Table {
+  uint32_t n;      // slots
+  uint32_t q;      // ring capacity (power of two, <= 64)
+  uint32_t qmask;
+  int32_t delayed;
+  int32_t at_limit;
+  double reject_thr;
+  double antic;
+  double *prev_r, *prev_p, *prev_l, *prev_arr;
+  double *r_inv, *w_inv, *l_inv;
+  double *pd;
+  double *front_r, *front_p, *front_l;
+  uint32_t *head, *count, *cur_delta, *cur_rho;
+  uint64_t *last_tick;
+  uint8_t *flags;
+  ReqEntry *ring;
+};
+
+__host__ __device__ inline uint64_t dbits(double x) {
+  uint64_t u;
+  __builtin_memcpy(&u, &x, 8);
+  return u;
+}
+__host__ __device__ inline double bitsd(uint64_t u) {
+  double x;
+  __builtin_memcpy(&x, &u, 8);
+  return x;
+}
+// order-preserving map double -> u64 (ascending)
+__host__ __device__ inline uint64_t okey(double x) {
+  uint64_t u = dbits(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__host__ __device__ inline double from_okey(uint64_t k) {
+  return bitsd((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+
+// tag_calc, dmclock_server.h:246-259
+__device__ inline double tag_step(double time, double prev, double inc,
+                                  uint32_t dist, bool high, uint32_t cost) {
+  if (inc == 0.0) return high ? kInf : -kInf;
+  double units = (double)((uint64_t)dist + (uint64_t)cost);
+  double cand = __dadd_rn(prev, __dmul_rn(inc, units));
+  return (time < cand) ? cand : time;
+}
+
+struct Tag3 {
+  double r, p, l, arrival;
+};
+
+// RequestTag(prev, info, delta, rho, time, cost, antic), :145-183.
+// Returns false where the reference asserts.
+__device__ inline bool make_tag(const Tag3& prev, double rinv, double winv,
+                                double linv, uint32_t delta, uint32_t rho,
+                                double time, uint32_t cost, double antic,
+                                Tag3* out) {
+  if (cost == 0) return false;
+  double max_time = time;
+  if (__dsub_rn(time, antic) < prev.arrival) max_time = __dsub_rn(max_time, antic);
+  Tag3 t;
+  t.r = tag_step(max_time, prev.r, rinv, rho, true, cost);
+  t.p = tag_step(max_time, prev.p, winv, delta, true, cost);
+  t.l = tag_step(max_time, prev.l, linv, delta, false, cost);
+  t.arrival = time;
+  if (!(t.r < kInf || t.p < kInf)) return false;
+  *out = t;
+  return true;
+}
+
+// assign_unpinned_tag / update_req_tag, :399-412 (prev in registers)
+__device__ inline void assign_unpinned(double& lhs, double rhs) {
+  if (rhs != kInf && rhs != -kInf) lhs = rhs;
+}
+
+// reduce_reservation_tags offset, :1090-1091: uint32 (cost + rho) first
+__device__ inline double resv_offset(double rinv, uint32_t cost,
+                                     uint32_t rho) {
+  return __dmul_rn(rinv, (double)(uint32_t)(cost + rho));
+}
+
+// Per-client sequence of pops inside one pull batch at fixed `now` is a pure
+// function of that client's own state ("Batched pulls").
+// The walkers below enumerate it; the three kernels that call them (count,
+// emit, apply) run the same arithmetic, so what is applied is exactly what
+// was ranked.
+
+// Visitor callbacks used by the walkers.
+struct NullVisit {
+  __device__ void pop(uint32_t /*i*/, const Tag3& /*t*/, uint32_t /*cost*/,
+                      uint64_t /*h*/, bool /*prio*/) {}
+  __device__ void group(uint64_t /*key*/, uint32_t /*run*/) {}
+};
+
+// Reservation phase walk (R-prefix): entries whose reservation tag is
+// <= min(now, thr) and whose ordered key <= T, popped without reductions.
+// Immediate mode reads stored tags; Delayed mode recomputes each new front
+// with update_next_tag (:1021-1036).  `limit` bounds the pops (apply mode).
+// Returns the number of pops; leaves the final prev tag in *prev (delayed).
+template <typename V>
+__device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
+                                  uint64_t T, uint32_t limit, V& vis,
+                                  Tag3* prev_io, Tag3* front_out,
+                                  uint32_t* front_cost) {
+  uint32_t h = tb.head[s], c = tb.count[s];
+  uint32_t n = 0;
+  if (c == 0) return 0;
+  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  if (!tb.delayed) {
+    while (n < c && n < limit) {
+      const ReqEntry& e = ring[(h + n) & tb.qmask];
+      if (!(e.r <= now) || okey(e.r) > T) break;
+      vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false);
+      ++n;
+    }
+    if (front_out && n < c) {
+      const ReqEntry& e = ring[(h + n) & tb.qmask];
+      *front_out = Tag3{e.r, e.p, e.l, e.arrival};
+      *front_cost = e.cost;
+    }
+    return n;
+  }
+  // delayed: front tag is stored; later tags are computed at pop time
+  const ReqEntry& e0 = ring[h & tb.qmask];
+  Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
+  uint32_t cur_cost = e0.cost, cur_rho = e0.rho;
+  uint64_t cur_h = e0.handle;
+  double rinv = tb.r_inv[s], winv = tb.w_inv[s], linv = tb.l_inv[s];
+  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
+  while (n < c && n < limit) {
+    if (!(cur.r <= now) || okey(cur.r) > T) break;
+    vis.pop(n, cur, cur_cost, cur_h, false);
+    ++n;
+    if (n < c) {
+      const ReqEntry& e = ring[(h + n) & tb.qmask];
+      Tag3 nt;
+      if (!make_tag(cur, rinv, winv, linv, cd, cr, e.arrival, e.cost,
+                    tb.antic, &nt))
+        nt = Tag3{e.r, e.p, e.l, e.arrival};
+      if (prev_io) {
+        assign_unpinned(prev_io->r, nt.r);
+        assign_unpinned(prev_io->l, nt.l);
+        assign_unpinned(prev_io->p, nt.p);
+        prev_io->arrival = nt.arrival;
+      }
+      cur = nt;
+      cur_cost = e.cost;
+      cur_rho = cr;
+      cur_h = e.handle;
+    }
+  }
+  (void)cur_rho;
+  if (front_out && n < c) {
+    *front_out = cur;
+    *front_cost = cur_cost;
+  }
+  return n;
+}
+
+// Priority phase walk: a sequence of groups, each a priority pop of the
+// front (eligible if ready and proportion < inf; the first front's ready
+// flag comes from the table, later fronts become ready at the next limit
+// scan iff limit <= now) with key p + prop_delta <= T, followed by the
+// reservation pops its reduce_reservation_tags exposes (r <= now).
+// `limit` bounds the total pops (apply mode).  On return *pmask has bit i set
+// for every entry popped by priority (immediate mode), used to recompute the
+// reduced reservation tags of the entries behind them.
+struct WalkP {
+  uint32_t pops;
+  uint32_t groups;
+  uint64_t pmask;
+};
+
+// immediate-mode reservation tag of entry i after the reductions of the
+// priority pops before it, applied in order (:1088-1095)
+__device__ inline double reduced_r(const ReqEntry* ring, uint32_t h,
+                                   uint32_t qmask, uint32_t i, uint64_t pmask,
+                                   double rinv) {
+  double r = ring[(h + i) & qmask].r;
+  for (uint32_t j = 0; j < i; ++j)
+    if ((pmask >> j) & 1ull) {
+      const ReqEntry& ej = ring[(h + j) & qmask];
+      r = __dsub_rn(r, resv_offset(rinv, ej.cost, ej.rho));
+    }
+  return r;
+}
+
+template <typename V>
+__device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
+                               uint64_t T, uint32_t limit, V& vis,
+                               Tag3* prev_io, Tag3* front_out,
+                               uint32_t* front_cost) {
+  WalkP w{0, 0, 0};
+  uint32_t h = tb.head[s], c = tb.count[s];
+  if (c == 0) return w;
+  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  double pdv = tb.pd[s];
+  double rinv = tb.r_inv[s];
+  bool ready0 = (tb.flags[s] & F_READY) != 0;
+  if (!tb.delayed) {
+    uint32_t i = 0;
+    while (i < c && w.pops < limit) {
+      const ReqEntry& e = ring[(h + i) & tb.qmask];
+      bool rdy = (i == 0) ? (ready0 || e.l <= now) : (e.l <= now);
+      if (!rdy || !(e.p < kInf)) break;
+      uint64_t key = okey(__dadd_rn(e.p, pdv));
+      if (key > T) break;
+      double r_now = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
+      vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true);
+      w.pmask |= 1ull << i;
+      ++i;
+      ++w.pops;
+      uint32_t run = 0;
+      while (i < c && w.pops < limit) {
+        double ri = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
+        if (!(ri <= now)) break;
+        const ReqEntry& er = ring[(h + i) & tb.qmask];
+        vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, false);
+        ++i;
+        ++w.pops;
+        ++run;
+      }
+      vis.group(key, run);
+      ++w.groups;
+    }
+    if (front_out && i < c) {
+      const ReqEntry& e = ring[(h + i) & tb.qmask];
+      *front_out = Tag3{reduced_r(ring, h, tb.qmask, i, w.pmask, rinv), e.p,
+                        e.l, e.arrival};
+      *front_cost = e.cost;
+    }
+    return w;
+  }
+  // delayed mode
+  double winv = tb.w_inv[s], linv = tb.l_inv[s];
+  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
+  const ReqEntry& e0 = ring[h & tb.qmask];
+  Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
+  uint32_t cur_cost = e0.cost, cur_rho = e0.rho;
+  uint64_t cur_h = e0.handle;
+  uint32_t i = 0;
+  auto advance = [&](bool prio) {
+    // pop entry i (tag `cur`), compute the next front by update_next_tag and,
+    // after a priority pop, reduce it and prev (:1021-1036, :1077-1085)
+    double off = prio ? resv_offset(rinv, cur_cost, cur_rho) : 0.0;
+    ++i;
+    if (i < c) {
+      const ReqEntry& e = ring[(h + i) & tb.qmask];
+      Tag3 nt;
+      if (!make_tag(cur, rinv, winv, linv, cd, cr, e.arrival, e.cost,
+                    tb.antic, &nt))
+        nt = Tag3{e.r, e.p, e.l, e.arrival};
+      if (prev_io) {
+        assign_unpinned(prev_io->r, nt.r);
+        assign_unpinned(prev_io->l, nt.l);
+        assign_unpinned(prev_io->p, nt.p);
+        prev_io->arrival = nt.arrival;
+      }
+      if (prio) nt.r = __dsub_rn(nt.r, off);
+      cur = nt;
+      cur_cost = e.cost;
+      cur_rho = cr;
+      cur_h = e.handle;
+    }
+    if (prio && prev_io) prev_io->r = __dsub_rn(prev_io->r, off);
+  };
+  while (i < c && w.pops < limit) {
+    bool rdy = (i == 0) ? (ready0 || cur.l <= now) : (cur.l <= now);
+    if (!rdy || !(cur.p < kInf)) break;
+    uint64_t key = okey(__dadd_rn(cur.p, pdv));
+    if (key > T) break;
+    vis.pop(i, cur, cur_cost, cur_h, true);
+    advance(true);
+    ++w.pops;
+    uint32_t run = 0;
+    while (i < c && w.pops < limit) {
+      if (!(cur.r <= now)) break;
+      vis.pop(i, cur, cur_cost, cur_h, false);
+      advance(false);
+      ++w.pops;
+      ++run;
+    }
+    vis.group(key, run);
+    ++w.groups;
+  }
+  if (front_out && i < c) {
+    *front_out = cur;
+    *front_cost = cur_cost;
+  }
+  return w;
+}
+
+}  // namespace dmc

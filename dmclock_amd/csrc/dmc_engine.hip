@@ -1,0 +1,1783 @@
+// SPDX-License-Identifier: LGPL-2.1
+//
+// dmc_engine.hip -- MI355X (gfx950) dmClock server-queue engine behind the
+// C-ABI of include/dmclock_gpu.h.
+//
+// Reference path replaced: crimson::dmclock::PriorityQueueBase /
+// PullPriorityQueue (/root/reference/src/dmclock_server.h:283-1501):
+//   add path     do_add_request          :913-1018   -> add pipeline below
+//   select path  do_next_request         :1115-1186  -> pull pipeline below
+//   pop/reduce   pop_process_request     :1046-1073,
+//                reduce_reservation_tags :1077-1111  -> apply kernels
+// The three IndIntruHeaps are replaced by data-parallel scans over a
+// struct-of-arrays client table plus a per-batch radix sort of the candidate
+// pops; see DESIGN.md for why the result is the reference's dispatch order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <vector>
+
+#include "../../include/dmclock_gpu.h"
+#include "dmc_device.h"
+
+using namespace dmc;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kHistBins = 2048;
+constexpr uint32_t kNone = 0xffffffffu;
+
+#define HIP_OK(expr)                                              \
+  do {                                                            \
+    hipError_t e_ = (expr);                                       \
+    if (e_ != hipSuccess) {                                       \
+      std::fprintf(stderr, "dmclock_gpu: %s failed: %s (%s:%d)\n", \
+                   #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return DMC_EDEVICE;                                         \
+    }                                                             \
+  } while (0)
+
+// Per-phase selection / bookkeeping block (device resident).
+struct Sel {
+  uint32_t n_elig;
+  uint32_t pad0;
+  uint64_t kmin, kmax;
+  uint64_t T;           // ordered-key threshold for this phase
+  uint32_t n_entries;   // emitted pops (R) / groups (P)
+  uint32_t n_dec_phase; // decisions taken by this phase
+  uint32_t g_last;      // last priority (limit-scan) pull index, kNone if none
+  uint32_t terminal;    // 1 if this phase ended the batch early
+  uint32_t ties;
+  uint32_t pad1;
+};
+
+// Single-step (one do_next_request) reduction record.
+struct ArgMin {
+  uint64_t key;
+  uint32_t slot;
+  uint32_t cnt;  // how many slots share the minimum key
+};
+
+struct StepRed {
+  ArgMin r;       // min front reservation over clients with requests
+  ArgMin p;       // min p+pd over ready (after marking) fronts with p < inf
+  ArgMin pnr;     // min p+pd over not-ready fronts (Allow: ready-heap top)
+  uint64_t lmin_nr, lmin_rd;  // min limit (ordered) over not-ready / ready
+  uint32_t n_any, n_ready, n_notready, pad;
+};
+
+struct StepCtl {
+  int32_t type;    // DMC_NEXT_*
+  int32_t prio;    // 1: ready-heap pop (reduce), 0: reservation-heap pop
+  uint32_t slot;
+  uint32_t mark;   // the limit scan ran: commit ready marks
+  uint32_t tie;
+  uint32_t pad;
+  double when;
+};
+
+__device__ inline ArgMin argmin_combine(ArgMin a, ArgMin b) {
+  if (a.key < b.key) return a;
+  if (b.key < a.key) return b;
+  ArgMin o;
+  o.key = a.key;
+  o.slot = a.slot < b.slot ? a.slot : b.slot;
+  o.cnt = a.cnt + b.cnt;
+  return o;
+}
+
+__device__ inline uint64_t shfl_u64(uint64_t v, int src) {
+  uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t shfl_down_u64(uint64_t v, int d) {
+  uint32_t lo = __shfl_down((uint32_t)v, d), hi = __shfl_down((uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ inline ArgMin wave_argmin(ArgMin a) {
+  for (int d = 32; d > 0; d >>= 1) {
+    ArgMin b;
+    b.key = shfl_down_u64(a.key, d);
+    b.slot = __shfl_down(a.slot, d);
+    b.cnt = __shfl_down(a.cnt, d);
+    a = argmin_combine(a, b);
+  }
+  return a;
+}
+__device__ inline uint64_t wave_min_u64(uint64_t v) {
+  for (int d = 32; d > 0; d >>= 1) {
+    uint64_t o = shfl_down_u64(v, d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ inline uint64_t wave_max_u64(uint64_t v) {
+  for (int d = 32; d > 0; d >>= 1) {
+    uint64_t o = shfl_down_u64(v, d);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
+  return v;
+}
+
+// ------------------------------------------------------------------ register
+__global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
+                           const double* rinv, const double* winv,
+                           const double* linv, int active, uint64_t tick) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = slots[i];
+  if (s >= tb.n) return;
+  // ClientRec(client, info, tick), dmclock_server.h:381-393
+  tb.prev_r[s] = 0.0;
+  tb.prev_p[s] = 0.0;
+  tb.prev_l[s] = 0.0;
+  tb.prev_arr[s] = 0.0;
+  tb.r_inv[s] = rinv[i];
+  tb.w_inv[s] = winv[i];
+  tb.l_inv[s] = linv[i];
+  tb.pd[s] = 0.0;
+  tb.front_r[s] = 0.0;
+  tb.front_p[s] = 0.0;
+  tb.front_l[s] = 0.0;
+  tb.head[s] = 0;
+  tb.count[s] = 0;
+  tb.cur_delta[s] = 1;
+  tb.cur_rho[s] = 1;
+  tb.last_tick[s] = tick;
+  tb.flags[s] = F_REG | (active ? 0 : F_IDLE);
+}
+
+// ------------------------------------------------------------------ add path
+__global__ void k_add_keys(const dmc_request* reqs, uint32_t n,
+                           uint32_t* keys, uint32_t* vals) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = reqs[i].slot;
+  vals[i] = i;
+}
+
+// One thread per client segment of the slot-sorted batch walks that client's
+// requests in arrival order: do_add_request minus the idle reset (handled
+// before, per activation), initial_tag (:878-907), the Reject check
+// (:989-993), the enqueue and cur_rho/cur_delta (:995-1009).
+__global__ void k_add_chain(Table tb, const uint32_t* sslot,
+                            const uint32_t* spos, const dmc_request* reqs,
+                            uint32_t n, uint64_t tick_base, int32_t* rc) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = sslot[i];
+  if (i > 0 && sslot[i - 1] == s) return;  // not a segment head
+  uint32_t end = i + 1;
+  while (end < n && sslot[end] == s) ++end;
+  if (s >= tb.n || !(tb.flags[s] & F_REG)) {
+    for (uint32_t j = i; j < end; ++j) rc[spos[j]] = DMC_ENOTREG;
+    return;
+  }
+  Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
+  double rinv = tb.r_inv[s], winv = tb.w_inv[s], linv = tb.l_inv[s];
+  uint32_t head = tb.head[s], count = tb.count[s];
+  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
+  uint64_t last_tick = tb.last_tick[s];
+  uint8_t flags = tb.flags[s];
+  bool front_set = false;
+  Tag3 front{};
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  for (uint32_t j = i; j < end; ++j) {
+    uint32_t pos = spos[j];
+    const dmc_request rq = reqs[pos];
+    uint64_t tick = tick_base + pos + 1;  // ++tick, :918
+    if (rq.rho > rq.delta) {  // ReqParams asserts rho <= delta
+      rc[pos] = DMC_EBADPARAMS;
+      continue;
+    }
+    if (count >= tb.q) {  // documented deviation: bounded ring
+      rc[pos] = DMC_EQUEUEFULL;
+      continue;
+    }
+    Tag3 tag;
+    if (!tb.delayed || count == 0) {
+      if (!make_tag(prev, rinv, winv, linv, rq.delta, rq.rho, rq.time,
+                    rq.cost, tb.antic, &tag)) {
+        rc[pos] = DMC_EBADTAG;
+        continue;
+      }
+      // update_req_tag, :405-412
+      assign_unpinned(prev.r, tag.r);
+      assign_unpinned(prev.l, tag.l);
+      assign_unpinned(prev.p, tag.p);
+      prev.arrival = tag.arrival;
+      last_tick = tick;
+    } else {
+      if (rq.cost == 0) {
+        rc[pos] = DMC_EBADTAG;
+        continue;
+      }
+      tag = Tag3{0.0, 0.0, 0.0, rq.time};  // placeholder, :880
+    }
+    if (tb.at_limit == DMC_AT_LIMIT_REJECT &&
+        tag.l > __dadd_rn(rq.time, tb.reject_thr)) {
+      rc[pos] = DMC_EAGAIN;
+      continue;
+    }
+    ReqEntry e;
+    e.r = tag.r;
+    e.p = tag.p;
+    e.l = tag.l;
+    e.arrival = tag.arrival;
+    e.handle = rq.handle;
+    e.cost = rq.cost;
+    e.delta = (tb.delayed && count > 0) ? 0u : rq.delta;
+    e.rho = (tb.delayed && count > 0) ? 0u : rq.rho;
+    e.pad = 0;
+    e.pad2 = 0;
+    ring[(head + count) & tb.qmask] = e;
+    if (count == 0) {
+      front = tag;
+      front_set = true;
+      flags &= (uint8_t)~F_READY;  // a new tag is not ready, :155
+    }
+    ++count;
+    cd = rq.delta;
+    cr = rq.rho;
+    rc[pos] = DMC_OK;
+  }
+  tb.prev_r[s] = prev.r;
+  tb.prev_p[s] = prev.p;
+  tb.prev_l[s] = prev.l;
+  tb.prev_arr[s] = prev.arrival;
+  tb.count[s] = count;
+  tb.cur_delta[s] = cd;
+  tb.cur_rho[s] = cr;
+  tb.last_tick[s] = last_tick;
+  tb.flags[s] = flags;
+  if (front_set) {
+    tb.front_r[s] = front.r;
+    tb.front_p[s] = front.p;
+    tb.front_l[s] = front.l;
+  }
+}
+
+// idle reset, :937-985: L = min over non-idle clients of
+// (has_request ? front.p : prev.p) + prop_delta
+__global__ void k_contrib_min(Table tb, uint64_t* out) {
+  uint64_t m = kMaxKey;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    uint8_t f = tb.flags[s];
+    if ((f & F_REG) && !(f & F_IDLE)) {
+      double p = tb.count[s] ? tb.front_p[s] : tb.prev_p[s];
+      uint64_t k = okey(__dadd_rn(p, tb.pd[s]));
+      m = k < m ? k : m;
+    }
+  }
+  m = wave_min_u64(m);
+  if ((threadIdx.x & 63) == 0) atomicMin((unsigned long long*)out, (unsigned long long)m);
+}
+
+__global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* lmin) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  constexpr double trigger = 1.7976931348623157e308 / 3.0;  // DBL_MAX / 3, :957
+  double lowest = 1.7976931348623157e308;                    // DBL_MAX, :960
+  if (*lmin != kMaxKey) {
+    double L = from_okey(*lmin);
+    if (L < lowest) lowest = L;
+  }
+  if (lowest < trigger) tb.pd[s] = __dsub_rn(lowest, t);
+  tb.flags[s] &= (uint8_t)~F_IDLE;
+}
+
+// ------------------------------------------------------------------ pull: scans
+// Phase R scan: key = front reservation tag, eligible iff r <= now.
+// Phase P scan: first commits the limit scan of the first priority pull
+// (:1135-1144: every front with limit <= now becomes ready), then
+// key = p + prop_delta, eligible iff ready and p < inf (:1146-1151).
+template <int PH>
+__global__ void k_scan(Table tb, double now, uint64_t* keys, Sel* sel) {
+  uint32_t cnt = 0;
+  uint64_t mn = kMaxKey, mx = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    uint64_t k = kMaxKey;
+    uint32_t c = tb.count[s];
+    if (c) {
+      if (PH == 0) {
+        double r = tb.front_r[s];
+        if (r <= now) k = okey(r);
+      } else {
+        uint8_t f = tb.flags[s];
+        bool rdy = (f & F_READY) != 0;
+        if (!rdy && tb.front_l[s] <= now) {
+          rdy = true;
+          tb.flags[s] = f | F_READY;
+        }
+        double p = tb.front_p[s];
+        if (rdy && p < kInf) k = okey(__dadd_rn(p, tb.pd[s]));
+      }
+    }
+    keys[s] = k;
+    if (k != kMaxKey) {
+      ++cnt;
+      mn = k < mn ? k : mn;
+      mx = k > mx ? k : mx;
+    }
+  }
+  cnt = wave_sum_u32(cnt);
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(&sel->n_elig, cnt);
+    atomicMin((unsigned long long*)&sel->kmin, (unsigned long long)mn);
+    atomicMax((unsigned long long*)&sel->kmax, (unsigned long long)mx);
+  }
+}
+
+__device__ inline uint32_t hist_shift(uint64_t range) {
+  // smallest shift with (range >> shift) < kHistBins
+  uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
+  uint32_t hb = 11;  // log2(kHistBins)
+  return bits > hb ? bits - hb : 0;
+}
+
+// Histogram of eligible keys over [kmin, kmax] in kHistBins integer buckets
+// of the ordered-key space (monotone in the key), with the max key per bucket.
+__global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
+                       uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
+  if (sel->n_elig <= k_rem) return;
+  __shared__ uint32_t sh[kHistBins];
+  __shared__ unsigned long long smx[kHistBins];
+  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+    sh[b] = 0;
+    smx[b] = 0;
+  }
+  __syncthreads();
+  uint64_t kmin = sel->kmin;
+  uint32_t sh_ = hist_shift(sel->kmax - kmin);
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += gridDim.x * blockDim.x) {
+    uint64_t k = keys[s];
+    if (k == kMaxKey) continue;
+    uint32_t b = (uint32_t)((k - kmin) >> sh_);
+    atomicAdd(&sh[b], 1u);
+    atomicMax(&smx[b], (unsigned long long)k);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+    if (sh[b]) {
+      atomicAdd(&hist[b], sh[b]);
+      atomicMax((unsigned long long*)&hmax[b], smx[b]);
+    }
+  }
+}
+
+// Pick the threshold T: every key <= T is a candidate and at least k_rem
+// eligible fronts are <= T (T is the largest key of the bucket holding the
+// k_rem-th smallest), or take everything when there are no more than k_rem.
+__global__ void k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist,
+                       uint64_t* hmax) {
+  __shared__ uint64_t T;
+  if (threadIdx.x == 0) {
+    uint32_t ne = sel->n_elig;
+    if (ne == 0) {
+      T = 0;  // nothing
+    } else if (ne <= k_rem) {
+      T = kMaxKey - 1;  // all eligible
+    } else {
+      uint32_t cum = 0;
+      T = sel->kmax;
+      for (int b = 0; b < kHistBins; ++b) {
+        cum += hist[b];
+        if (cum >= k_rem) {
+          T = hmax[b];
+          break;
+        }
+      }
+    }
+    sel->T = T;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+    hist[b] = 0;
+    hmax[b] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ pull: walks
+struct CountVisit {
+  uint32_t pops = 0, groups = 0;
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
+  __device__ void group(uint64_t, uint32_t) { ++groups; }
+};
+
+template <int PH>
+__global__ void k_count(Table tb, double now, const uint64_t* keys,
+                        const Sel* sel, uint32_t* cnt) {
+  uint64_t T = sel->T;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    uint32_t c = 0;
+    if (keys[s] <= T) {
+      CountVisit v;
+      if (PH == 0)
+        c = walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+      else
+        c = walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr).groups;
+    }
+    cnt[s] = c;
+  }
+}
+
+__global__ void k_total(uint32_t n, const uint32_t* cnt, const uint32_t* off,
+                        Sel* sel) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    sel->n_entries = n ? off[n - 1] + cnt[n - 1] : 0;
+}
+
+struct EmitVisit {
+  uint64_t* ekey;
+  uint32_t* eval;
+  uint32_t* eslot;
+  uint32_t* erun;
+  uint32_t base, slot, n = 0;
+  int ph;
+  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
+    if (ph == 0) {
+      uint32_t e = base + n++;
+      ekey[e] = okey(t.r);
+      eval[e] = e;
+      eslot[e] = slot;
+    }
+  }
+  __device__ void group(uint64_t key, uint32_t run) {
+    uint32_t e = base + n++;
+    ekey[e] = key;
+    eval[e] = e;
+    eslot[e] = slot;
+    erun[e] = run;
+  }
+};
+
+template <int PH>
+__global__ void k_emit(Table tb, double now, const Sel* sel,
+                       const uint32_t* cnt, const uint32_t* off,
+                       uint64_t* ekey, uint32_t* eval, uint32_t* eslot,
+                       uint32_t* erun) {
+  uint64_t T = sel->T;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    if (!cnt[s]) continue;
+    EmitVisit v{ekey, eval, eslot, erun, off[s], s, 0, PH};
+    if (PH == 0)
+      walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+    else
+      walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+  }
+}
+
+__device__ inline bool tie_at(const uint64_t* skey, const uint32_t* sval,
+                              const uint32_t* eslot, uint32_t n, uint32_t pos) {
+  uint32_t me = eslot[sval[pos]];
+  if (pos > 0 && skey[pos - 1] == skey[pos] && eslot[sval[pos - 1]] != me)
+    return true;
+  if (pos + 1 < n && skey[pos + 1] == skey[pos] && eslot[sval[pos + 1]] != me)
+    return true;
+  return false;
+}
+
+// R: the first k_rem sorted pops are dispatched in sorted order.
+__global__ void k_decide_r(uint32_t n, uint32_t k_rem, uint32_t n_dec,
+                           const uint64_t* skey, const uint32_t* sval,
+                           const uint32_t* eslot, uint32_t* eoff,
+                           uint8_t* etie, uint32_t* applied, Sel* sel) {
+  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos == 0) {
+    uint32_t d = n < k_rem ? n : k_rem;
+    sel->n_dec_phase = d;
+    sel->terminal = 0;
+    sel->g_last = kNone;
+  }
+  if (pos >= n) return;
+  uint32_t e = sval[pos];
+  if (pos < k_rem) {
+    eoff[e] = n_dec + pos;
+    etie[e] = tie_at(skey, sval, eslot, n, pos) ? 1 : 0;
+    atomicAdd(&applied[eslot[e]], 1u);
+  } else {
+    eoff[e] = kNone;
+  }
+}
+
+__global__ void k_group_sizes(uint32_t n, const uint32_t* sval,
+                              const uint32_t* erun, uint32_t* gsz) {
+  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos < n) gsz[pos] = 1 + erun[sval[pos]];
+}
+
+// P: groups (priority pop + the reservation run it exposes) in key order;
+// decisions are the prefix of their concatenation up to k_rem.
+__global__ void k_decide_p(uint32_t n, uint32_t k_rem, uint32_t n_dec,
+                           const uint64_t* skey, const uint32_t* sval,
+                           const uint32_t* eslot, const uint32_t* gsz,
+                           const uint32_t* goff, uint32_t* eoff, uint8_t* etie,
+                           uint32_t* applied, Sel* sel) {
+  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= n) return;
+  uint32_t e = sval[pos];
+  uint32_t o = goff[pos];
+  if (pos == n - 1) {
+    uint32_t tot = o + gsz[pos];
+    sel->n_dec_phase = tot < k_rem ? tot : k_rem;
+    sel->terminal = tot < k_rem ? 1 : 0;
+  }
+  if (o < k_rem) {
+    eoff[e] = n_dec + o;
+    etie[e] = tie_at(skey, sval, eslot, n, pos) ? 1 : 0;
+    uint32_t na = gsz[pos];
+    if (na > k_rem - o) na = k_rem - o;
+    atomicAdd(&applied[eslot[e]], na);
+    atomicMax(&sel->g_last, n_dec + o);  // g_last initialised to 0 by host
+  } else {
+    eoff[e] = kNone;
+  }
+}
+
+struct ApplyVisit {
+  dmc_decision* out;
+  const uint32_t* eoff;
+  const uint8_t* etie;
+  uint32_t base;    // first entry index of this client
+  uint32_t slot;
+  int ph;
+  uint32_t npop = 0, ngroup = 0, inrun = 0;
+  uint32_t last_idx = 0;
+  uint32_t n_res = 0, n_prio = 0;
+  __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
+                      bool prio) {
+    uint32_t idx, tie;
+    if (ph == 0) {
+      uint32_t e = base + npop;
+      idx = eoff[e];
+      tie = etie[e];
+    } else {
+      uint32_t e = base + ngroup;
+      if (prio) inrun = 0;
+      idx = eoff[e] + inrun;
+      tie = prio ? etie[e] : 0;
+      ++inrun;
+    }
+    dmc_decision d;
+    d.handle = h;
+    d.tag_r = t.r;
+    d.tag_p = t.p;
+    d.tag_l = t.l;
+    d.slot = slot;
+    d.cost = cost;
+    d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+    d.flags = tie;
+    out[idx] = d;
+    last_idx = idx;
+    ++npop;
+    if (prio) ++n_prio; else ++n_res;
+  }
+  __device__ void group(uint64_t, uint32_t) { ++ngroup; }
+};
+
+// Replays each candidate client's walk for exactly the pops that were
+// dispatched, writes their decision records, and stores the client's new
+// state: ring head/count, front cache, reduced reservation tags (immediate:
+// every queued request, :1088-1095; delayed: the front, :1077-1085), prev tag,
+// and the front's ready flag (set iff a later limit scan saw it with
+// limit <= now).
+template <int PH>
+__global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
+                        const uint32_t* cnt, const uint32_t* off,
+                        const uint32_t* eoff, const uint8_t* etie,
+                        uint32_t* applied, dmc_decision* out,
+                        unsigned long long* sched) {
+  uint32_t g_last = sel->g_last;
+  uint32_t terminal = sel->terminal;
+  uint64_t T = sel->T;
+  uint32_t nres = 0, nprio = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    if (!cnt[s]) continue;
+    uint32_t a = applied[s];
+    if (!a) continue;
+    applied[s] = 0;
+    ApplyVisit v{out, eoff, etie, off[s], s, PH};
+    Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
+    Tag3 front{};
+    uint32_t fcost = 0;
+    uint32_t c = tb.count[s], h = tb.head[s];
+    uint64_t pmask = 0;
+    uint32_t pops;
+    if (PH == 0) {
+      pops = walk_r(tb, s, now, T, a, v, &prev, &front, &fcost);
+    } else {
+      WalkP w = walk_p(tb, s, now, T, a, v, &prev, &front, &fcost);
+      pops = w.pops;
+      pmask = w.pmask;
+    }
+    nres += v.n_res;
+    nprio += v.n_prio;
+    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+    uint32_t nc = c - pops, nh = (h + pops) & tb.qmask;
+    if (!tb.delayed) {
+      if (PH == 1 && pmask) {
+        double rinv = tb.r_inv[s];
+        // remaining requests: all reductions, in order
+        for (uint32_t i = pops; i < c; ++i)
+          ring[(h + i) & tb.qmask].r = reduced_r(ring, h, tb.qmask, i, pmask, rinv);
+        double pr = prev.r;
+        for (uint32_t j = 0; j < pops; ++j)
+          if ((pmask >> j) & 1ull) {
+            const ReqEntry& ej = ring[(h + j) & tb.qmask];
+            pr = __dsub_rn(pr, resv_offset(rinv, ej.cost, ej.rho));
+          }
+        tb.prev_r[s] = pr;
+      }
+      if (nc) {
+        const ReqEntry& f = ring[nh];
+        front = Tag3{f.r, f.p, f.l, f.arrival};
+      }
+    } else {
+      // delayed: the walk recomputed the new front and prev
+      if (nc) {
+        ReqEntry& f = ring[nh];
+        f.r = front.r;
+        f.p = front.p;
+        f.l = front.l;
+        f.delta = tb.cur_delta[s];
+        f.rho = tb.cur_rho[s];
+      }
+      tb.prev_r[s] = prev.r;
+      tb.prev_p[s] = prev.p;
+      tb.prev_l[s] = prev.l;
+      tb.prev_arr[s] = prev.arrival;
+      if (c >= 2) tb.last_tick[s] = tick;
+    }
+    tb.head[s] = nh;
+    tb.count[s] = nc;
+    uint8_t f = tb.flags[s] & (uint8_t)~F_READY;
+    if (nc) {
+      tb.front_r[s] = front.r;
+      tb.front_p[s] = front.p;
+      tb.front_l[s] = front.l;
+      bool later_scan = PH == 1 && (terminal || (g_last != kNone && v.last_idx < g_last));
+      if (later_scan && front.l <= now) f |= F_READY;
+    }
+    tb.flags[s] = f;
+  }
+  nres = wave_sum_u32(nres);
+  nprio = wave_sum_u32(nprio);
+  if ((threadIdx.x & 63) == 0) {
+    if (nres) atomicAdd(&sched[0], (unsigned long long)nres);
+    if (nprio) atomicAdd(&sched[1], (unsigned long long)nprio);
+  }
+}
+
+// ------------------------------------------------------------------ future
+// Terminal pull of a Wait/Reject batch: min_not_0 over the reservation-heap
+// top and the limit-heap top (:1170-1185).
+__global__ void k_future_scan(Table tb, StepRed* red) {
+  uint64_t rmin = kMaxKey, lnr = kMaxKey, lrd = kMaxKey;
+  uint32_t nany = 0, nnr = 0, nrd = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    if (!tb.count[s]) continue;
+    ++nany;
+    uint64_t kr = okey(tb.front_r[s]);
+    rmin = kr < rmin ? kr : rmin;
+    uint64_t kl = okey(tb.front_l[s]);
+    if (tb.flags[s] & F_READY) {
+      ++nrd;
+      lrd = kl < lrd ? kl : lrd;
+    } else {
+      ++nnr;
+      lnr = kl < lnr ? kl : lnr;
+    }
+  }
+  rmin = wave_min_u64(rmin);
+  lnr = wave_min_u64(lnr);
+  lrd = wave_min_u64(lrd);
+  nany = wave_sum_u32(nany);
+  nnr = wave_sum_u32(nnr);
+  nrd = wave_sum_u32(nrd);
+  if ((threadIdx.x & 63) == 0 && nany) {
+    atomicMin((unsigned long long*)&red->r.key, (unsigned long long)rmin);
+    atomicMin((unsigned long long*)&red->lmin_nr, (unsigned long long)lnr);
+    atomicMin((unsigned long long*)&red->lmin_rd, (unsigned long long)lrd);
+    atomicAdd(&red->n_any, nany);
+    atomicAdd(&red->n_notready, nnr);
+    atomicAdd(&red->n_ready, nrd);
+  }
+}
+
+__device__ inline double min_not_0(double cur, double possible) {
+  return possible == 0.0 ? cur : (possible < cur ? possible : cur);
+}
+
+__global__ void k_future_final(const StepRed* red, StepCtl* sc) {
+  if (threadIdx.x || blockIdx.x) return;
+  const double tmax = 1.7976931348623157e308;
+  double next = tmax;
+  if (red->n_any) {
+    next = min_not_0(next, from_okey(red->r.key));
+    double lt = red->n_notready ? from_okey(red->lmin_nr) : from_okey(red->lmin_rd);
+    next = min_not_0(next, lt);
+  }
+  if (next < tmax) {
+    sc->type = DMC_NEXT_FUTURE;
+    sc->when = next;
+  } else {
+    sc->type = DMC_NEXT_NONE;
+    sc->when = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------ single step
+// General do_next_request(now) one pull at a time (used for small k and for
+// AtLimit::Allow limit breaks, :1157-1165).  Reductions are per block, then
+// one block combines them.
+__global__ void k_step_scan(Table tb, double now, StepRed* part) {
+  ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
+  uint64_t lnr = kMaxKey, lrd = kMaxKey;
+  uint32_t nany = 0, nrd = 0, nnr = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    if (!tb.count[s]) continue;
+    ++nany;
+    ArgMin a{okey(tb.front_r[s]), s, 1};
+    r = argmin_combine(r, a);
+    double l = tb.front_l[s];
+    bool rdy = (tb.flags[s] & F_READY) || l <= now;
+    double pv = tb.front_p[s];
+    uint64_t kp = okey(__dadd_rn(pv, tb.pd[s]));
+    uint64_t kl = okey(l);
+    if (rdy) {
+      ++nrd;
+      lrd = kl < lrd ? kl : lrd;
+      if (pv < kInf) p = argmin_combine(p, ArgMin{kp, s, 1});
+    } else {
+      ++nnr;
+      lnr = kl < lnr ? kl : lnr;
+      pnr = argmin_combine(pnr, ArgMin{kp, s, 1});
+    }
+  }
+  r = wave_argmin(r);
+  p = wave_argmin(p);
+  pnr = wave_argmin(pnr);
+  lnr = wave_min_u64(lnr);
+  lrd = wave_min_u64(lrd);
+  nany = wave_sum_u32(nany);
+  nrd = wave_sum_u32(nrd);
+  nnr = wave_sum_u32(nnr);
+  __shared__ StepRed sh[kBlock / 64];
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w].r = r;
+    sh[w].p = p;
+    sh[w].pnr = pnr;
+    sh[w].lmin_nr = lnr;
+    sh[w].lmin_rd = lrd;
+    sh[w].n_any = nany;
+    sh[w].n_ready = nrd;
+    sh[w].n_notready = nnr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    StepRed o = sh[0];
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) {
+      o.r = argmin_combine(o.r, sh[i].r);
+      o.p = argmin_combine(o.p, sh[i].p);
+      o.pnr = argmin_combine(o.pnr, sh[i].pnr);
+      o.lmin_nr = sh[i].lmin_nr < o.lmin_nr ? sh[i].lmin_nr : o.lmin_nr;
+      o.lmin_rd = sh[i].lmin_rd < o.lmin_rd ? sh[i].lmin_rd : o.lmin_rd;
+      o.n_any += sh[i].n_any;
+      o.n_ready += sh[i].n_ready;
+      o.n_notready += sh[i].n_notready;
+    }
+    part[blockIdx.x] = o;
+  }
+}
+
+__global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
+                              int at_limit, uint32_t nregistered,
+                              StepCtl* sc) {
+  if (threadIdx.x || blockIdx.x) return;
+  StepRed o = part[0];
+  for (uint32_t i = 1; i < nparts; ++i) {
+    o.r = argmin_combine(o.r, part[i].r);
+    o.p = argmin_combine(o.p, part[i].p);
+    o.pnr = argmin_combine(o.pnr, part[i].pnr);
+    o.lmin_nr = part[i].lmin_nr < o.lmin_nr ? part[i].lmin_nr : o.lmin_nr;
+    o.lmin_rd = part[i].lmin_rd < o.lmin_rd ? part[i].lmin_rd : o.lmin_rd;
+    o.n_any += part[i].n_any;
+    o.n_ready += part[i].n_ready;
+    o.n_notready += part[i].n_notready;
+  }
+  StepCtl c{};
+  c.type = DMC_NEXT_NONE;
+  c.slot = kNone;
+  if (nregistered == 0) {  // resv_heap.empty(), :1118-1120
+    *sc = c;
+    return;
+  }
+  double rtop = o.n_any ? from_okey(o.r.key) : kInf;
+  if (o.n_any && rtop <= now) {  // :1124-1128
+    c.type = DMC_NEXT_RETURNING;
+    c.prio = 0;
+    c.slot = o.r.slot;
+    c.tie = o.r.cnt > 1;
+    *sc = c;
+    return;
+  }
+  c.mark = 1;  // the limit scan ran
+  if (o.p.slot != kNone) {  // :1146-1151
+    c.type = DMC_NEXT_RETURNING;
+    c.prio = 1;
+    c.slot = o.p.slot;
+    c.tie = o.p.cnt > 1;
+    *sc = c;
+    return;
+  }
+  if (at_limit == DMC_AT_LIMIT_ALLOW && o.n_any) {  // :1157-1165
+    // ready-heap top: ready fronts first (all have p == inf here), else the
+    // min p+pd over not-ready fronts
+    bool top_ready = o.n_ready > 0;
+    if (!top_ready && o.pnr.slot != kNone &&
+        from_okey(o.pnr.key) < kInf) {
+      c.type = DMC_NEXT_RETURNING;
+      c.prio = 1;
+      c.slot = o.pnr.slot;
+      c.tie = o.pnr.cnt > 1;
+      *sc = c;
+      return;
+    }
+    if (rtop < kInf) {
+      c.type = DMC_NEXT_RETURNING;
+      c.prio = 0;
+      c.slot = o.r.slot;
+      c.tie = o.r.cnt > 1;
+      *sc = c;
+      return;
+    }
+  }
+  const double tmax = 1.7976931348623157e308;
+  double next = tmax;
+  if (o.n_any) {
+    next = min_not_0(next, rtop);
+    double lt = o.n_notready ? from_okey(o.lmin_nr) : from_okey(o.lmin_rd);
+    next = min_not_0(next, lt);
+  }
+  if (next < tmax) {
+    c.type = DMC_NEXT_FUTURE;
+    c.when = next;
+  }
+  *sc = c;
+}
+
+__global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
+  if (!sc->mark) return;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    if (tb.count[s] && !(tb.flags[s] & F_READY) && tb.front_l[s] <= now)
+      tb.flags[s] |= F_READY;
+  }
+}
+
+// pop_process_request (+ reduce_reservation_tags for ready-heap pops) of the
+// chosen client, :1046-1111.
+__global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
+                             dmc_decision* out, uint32_t out_idx,
+                             unsigned long long* sched) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (sc->type != DMC_NEXT_RETURNING) return;
+  uint32_t s = sc->slot;
+  bool prio = sc->prio != 0;
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  uint32_t h = tb.head[s], c = tb.count[s];
+  ReqEntry popped = ring[h];
+  dmc_decision d;
+  d.handle = popped.handle;
+  d.tag_r = popped.r;
+  d.tag_p = popped.p;
+  d.tag_l = popped.l;
+  d.slot = s;
+  d.cost = popped.cost;
+  d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+  d.flags = sc->tie ? 1u : 0u;
+  out[out_idx] = d;
+  uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
+  double rinv = tb.r_inv[s];
+  if (tb.delayed && nc) {  // update_next_tag, :1021-1036
+    ReqEntry& f = ring[nh];
+    Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
+    Tag3 nt;
+    uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
+    if (make_tag(pt, rinv, tb.w_inv[s], tb.l_inv[s], cd, cr, f.arrival, f.cost,
+                 tb.antic, &nt)) {
+      f.r = nt.r;
+      f.p = nt.p;
+      f.l = nt.l;
+      f.delta = cd;
+      f.rho = cr;
+      double pr = tb.prev_r[s], pp = tb.prev_p[s], pl = tb.prev_l[s];
+      assign_unpinned(pr, nt.r);
+      assign_unpinned(pl, nt.l);
+      assign_unpinned(pp, nt.p);
+      tb.prev_r[s] = pr;
+      tb.prev_p[s] = pp;
+      tb.prev_l[s] = pl;
+      tb.prev_arr[s] = nt.arrival;
+      tb.last_tick[s] = tick;
+    }
+  }
+  if (prio) {  // reduce_reservation_tags, :1077-1111
+    double o = resv_offset(rinv, popped.cost, popped.rho);
+    if (tb.delayed) {
+      if (nc) ring[nh].r = __dsub_rn(ring[nh].r, o);
+    } else {
+      for (uint32_t i = 1; i < c; ++i) {
+        ReqEntry& e = ring[(h + i) & tb.qmask];
+        e.r = __dsub_rn(e.r, o);
+      }
+    }
+    tb.prev_r[s] = __dsub_rn(tb.prev_r[s], o);
+  }
+  tb.head[s] = nh;
+  tb.count[s] = nc;
+  tb.flags[s] &= (uint8_t)~F_READY;
+  if (nc) {
+    const ReqEntry& f = ring[nh];
+    tb.front_r[s] = f.r;
+    tb.front_p[s] = f.p;
+    tb.front_l[s] = f.l;
+  }
+  atomicAdd(&sched[prio ? 1 : 0], 1ull);
+}
+
+// ------------------------------------------------------------------ stats
+__global__ void k_count_requests(Table tb, unsigned long long* out) {
+  unsigned long long t = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x)
+    t += tb.count[s];
+  for (int d = 32; d > 0; d >>= 1) t += shfl_down_u64(t, d);
+  if ((threadIdx.x & 63) == 0 && t) atomicAdd(out, t);
+}
+
+uint32_t grid_for(uint32_t n, uint32_t cap = 4096) {
+  uint32_t g = (n + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  return g > cap ? cap : g;
+}
+
+}  // namespace
+
+// ====================================================================== host
+struct dmc_queue {
+  dmc_queue_params p{};
+  hipStream_t stream = nullptr;
+  Table tb{};
+  std::mutex mtx;  // C-ABI calls on one handle are serialised (data_mtx, :762)
+  // host mirrors
+  std::vector<uint8_t> reg_h, idle_h;
+  uint32_t n_registered = 0;
+  uint32_t n_idle = 0;
+  uint64_t tick = 0;
+  // device scratch
+  uint64_t* keys = nullptr;   // N
+  uint32_t* cnt = nullptr;    // N
+  uint32_t* off = nullptr;    // N
+  uint32_t* applied = nullptr;// N
+  uint32_t* hist = nullptr;
+  uint64_t* hmax = nullptr;
+  Sel* sel = nullptr;
+  StepRed* red = nullptr;     // step partials (grid) + future record
+  StepCtl* sctl = nullptr;
+  uint64_t* act_min = nullptr;
+  unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
+  unsigned long long* reqcount = nullptr;
+  // entries (grown on demand)
+  uint32_t ecap = 0;
+  uint64_t *ekey = nullptr, *skey = nullptr;
+  uint32_t *eval = nullptr, *sval = nullptr, *eslot = nullptr, *erun = nullptr;
+  uint32_t *eoff = nullptr, *gsz = nullptr, *goff = nullptr;
+  uint8_t* etie = nullptr;
+  // add batch buffers
+  uint32_t bcap = 0;
+  dmc_request* d_reqs = nullptr;
+  int32_t* d_rc = nullptr;
+  uint32_t *akeys = nullptr, *avals = nullptr, *skeys = nullptr, *svals = nullptr;
+  // decisions (host API)
+  uint32_t dcap = 0;
+  dmc_decision* d_dec = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  uint32_t step_grid = 0;
+  uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
+};
+
+namespace {
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+int ensure_temp(dmc_queue* q, size_t need) {
+  if (need <= q->temp_bytes) return DMC_OK;
+  if (q->temp) dfree(q->temp);
+  q->temp = nullptr;
+  size_t sz = need + (need >> 2) + 4096;
+  HIP_OK(hipMalloc(&q->temp, sz));
+  q->temp_bytes = sz;
+  return DMC_OK;
+}
+
+int ensure_entries(dmc_queue* q, uint32_t n) {
+  if (n <= q->ecap) return DMC_OK;
+  uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
+  dfree(q->ekey); dfree(q->skey); dfree(q->eval); dfree(q->sval);
+  dfree(q->eslot); dfree(q->erun); dfree(q->eoff); dfree(q->gsz);
+  dfree(q->goff); dfree(q->etie);
+  HIP_OK(hipMalloc(&q->ekey, sizeof(uint64_t) * cap));
+  HIP_OK(hipMalloc(&q->skey, sizeof(uint64_t) * cap));
+  HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eslot, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->erun, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eoff, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->etie, cap));
+  q->ecap = cap;
+  size_t t1 = 0, t2 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ekey, q->skey, q->eval,
+                                     q->sval, (int)cap, 0, 64, q->stream);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
+                                   q->stream);
+  return ensure_temp(q, std::max(t1, t2));
+}
+
+int ensure_batch(dmc_queue* q, uint32_t n) {
+  if (n <= q->bcap) return DMC_OK;
+  uint32_t cap = std::max<uint32_t>(n, 1024);
+  dfree(q->d_reqs); dfree(q->d_rc); dfree(q->akeys); dfree(q->avals);
+  dfree(q->skeys); dfree(q->svals);
+  HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
+  HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
+  HIP_OK(hipMalloc(&q->akeys, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->avals, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->skeys, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->svals, sizeof(uint32_t) * cap));
+  q->bcap = cap;
+  size_t t = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, q->akeys, q->skeys, q->avals,
+                                     q->svals, (int)cap, 0, 32, q->stream);
+  return ensure_temp(q, t);
+}
+
+int ensure_dec(dmc_queue* q, uint32_t n) {
+  if (n <= q->dcap) return DMC_OK;
+  dfree(q->d_dec);
+  uint32_t cap = std::max<uint32_t>(n, 1024);
+  HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
+  q->dcap = cap;
+  return DMC_OK;
+}
+
+int slot_bits(uint32_t n) {
+  int b = 1;
+  while (b < 32 && (1u << b) < n) ++b;
+  return b;
+}
+
+// Add a contiguous run of requests that contains no activation except,
+// possibly, its first request (which has already been activated).
+int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
+                int32_t* d_rc, uint64_t tick_base) {
+  if (!n) return DMC_OK;
+  uint32_t g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_add_keys, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
+                     q->akeys, q->avals);
+  size_t tb = q->temp_bytes;
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tb, q->akeys, q->skeys,
+                                            q->avals, q->svals, (int)n, 0,
+                                            slot_bits(q->p.max_clients),
+                                            q->stream));
+  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     q->skeys, q->svals, d_reqs, n, tick_base, d_rc);
+  return DMC_OK;
+}
+
+int activate(dmc_queue* q, uint32_t slot, double t) {
+  HIP_OK(hipMemsetAsync(q->act_min, 0xff, sizeof(uint64_t), q->stream));
+  hipLaunchKernelGGL(k_contrib_min, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock),
+                     0, q->stream, q->tb, q->act_min);
+  hipLaunchKernelGGL(k_activate, dim3(1), dim3(64), 0, q->stream, q->tb, slot,
+                     t, (const uint64_t*)q->act_min);
+  return DMC_OK;
+}
+
+// Host-ordered add: split the batch at activations (first request of an idle
+// client); each activation's idle reset sees the state left by everything
+// before it, exactly as the sequential reference does.
+int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
+                   const dmc_request* d_reqs, int32_t* d_rc) {
+  uint32_t start = 0;
+  uint64_t tick0 = q->tick;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = h_reqs[i].slot;
+    bool act = s < q->p.max_clients && q->reg_h[s] && q->idle_h[s] &&
+               h_reqs[i].rho <= h_reqs[i].delta;
+    if (!act) continue;
+    int rc = add_segment(q, d_reqs + start, i - start, d_rc + start, tick0 + start);
+    if (rc) return rc;
+    rc = activate(q, s, h_reqs[i].time);
+    if (rc) return rc;
+    q->idle_h[s] = 0;
+    --q->n_idle;
+    start = i;
+  }
+  return add_segment(q, d_reqs + start, n - start, d_rc + start, tick0 + start);
+}
+
+// --------------------------------------------------------------- pull phases
+struct PhaseOut {
+  uint32_t n_dec;
+  uint32_t terminal;
+};
+
+template <int PH>
+int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
+              dmc_decision* d_out, PhaseOut* po) {
+  const Table& tb = q->tb;
+  uint32_t N = tb.n;
+  uint32_t gN = grid_for(N, 2048);
+  Sel init{};
+  init.kmin = kMaxKey;
+  init.kmax = 0;
+  init.g_last = 0;
+  HIP_OK(hipMemcpyAsync(q->sel, &init, sizeof(Sel), hipMemcpyHostToDevice, q->stream));
+  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
+                     q->keys, q->sel);
+  hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
+                     (const uint64_t*)q->keys, (const Sel*)q->sel, k_rem, q->hist,
+                     q->hmax);
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, q->stream, q->sel, k_rem,
+                     q->hist, q->hmax);
+  hipLaunchKernelGGL(k_count<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
+                     (const uint64_t*)q->keys, (const Sel*)q->sel, q->cnt);
+  size_t tbytes = q->temp_bytes;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->cnt, q->off, (int)N,
+                                          q->stream));
+  hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, q->stream, N,
+                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, q->sel);
+  Sel hs;
+  HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  uint32_t ne = hs.n_entries;
+  po->n_dec = 0;
+  po->terminal = (PH == 1) ? 1 : 0;
+  if (ne == 0) return DMC_OK;
+  int rc = ensure_entries(q, ne);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_emit<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
+                     (const Sel*)q->sel, (const uint32_t*)q->cnt,
+                     (const uint32_t*)q->off, q->ekey, q->eval, q->eslot, q->erun);
+  tbytes = q->temp_bytes;
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ekey, q->skey,
+                                            q->eval, q->sval, (int)ne, 0, 64,
+                                            q->stream));
+  uint32_t ge = (ne + kBlock - 1) / kBlock;
+  if (PH == 0) {
+    hipLaunchKernelGGL(k_decide_r, dim3(ge), dim3(kBlock), 0, q->stream, ne,
+                       k_rem, n_dec, (const uint64_t*)q->skey,
+                       (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                       q->eoff, q->etie, q->applied, q->sel);
+  } else {
+    hipLaunchKernelGGL(k_group_sizes, dim3(ge), dim3(kBlock), 0, q->stream, ne,
+                       (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
+    tbytes = q->temp_bytes;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
+                                            (int)ne, q->stream));
+    hipLaunchKernelGGL(k_decide_p, dim3(ge), dim3(kBlock), 0, q->stream, ne,
+                       k_rem, n_dec, (const uint64_t*)q->skey,
+                       (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                       (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
+                       q->etie, q->applied, q->sel);
+  }
+  hipLaunchKernelGGL(k_apply<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
+                     q->tick, (const Sel*)q->sel, (const uint32_t*)q->cnt,
+                     (const uint32_t*)q->off, (const uint32_t*)q->eoff,
+                     (const uint8_t*)q->etie, q->applied, d_out, q->sched);
+  HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  po->n_dec = hs.n_dec_phase;
+  po->terminal = (PH == 1) ? hs.terminal : 0;
+  return DMC_OK;
+}
+
+// one general pull_request(now); returns the NextReqType in *type
+int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
+              int* type, double* when) {
+  const Table& tb = q->tb;
+  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
+                     tb, now, q->red);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, q->stream,
+                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
+                     q->n_registered, q->sctl);
+  hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
+                     q->stream, tb, now, (const StepCtl*)q->sctl);
+  hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
+                     (const StepCtl*)q->sctl, d_out, idx, q->sched);
+  StepCtl sc;
+  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  *type = sc.type;
+  *when = sc.when;
+  return DMC_OK;
+}
+
+int future_of(dmc_queue* q, int* type, double* when) {
+  StepRed init{};
+  init.r.key = kMaxKey;
+  init.lmin_nr = kMaxKey;
+  init.lmin_rd = kMaxKey;
+  HIP_OK(hipMemcpyAsync(q->red, &init, sizeof(init), hipMemcpyHostToDevice, q->stream));
+  hipLaunchKernelGGL(k_future_scan, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock), 0,
+                     q->stream, q->tb, q->red);
+  hipLaunchKernelGGL(k_future_final, dim3(1), dim3(64), 0, q->stream,
+                     (const StepRed*)q->red, q->sctl);
+  StepCtl sc;
+  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  *type = sc.type;
+  *when = sc.when;
+  return DMC_OK;
+}
+
+int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
+              dmc_pull_result* res) {
+  dmc_pull_result r{};
+  r.next_type = DMC_NEXT_RETURNING;
+  uint32_t n_dec = 0;
+  bool allow = q->p.at_limit == DMC_AT_LIMIT_ALLOW;
+  while (n_dec < k) {
+    if (q->n_registered == 0) {
+      r.next_type = DMC_NEXT_NONE;
+      break;
+    }
+    if (k - n_dec <= q->small_k) {
+      int type;
+      double when;
+      int rc = step_once(q, now, d_out, n_dec, &type, &when);
+      if (rc) return rc;
+      if (type != DMC_NEXT_RETURNING) {
+        r.next_type = type;
+        r.when = when;
+        break;
+      }
+      ++n_dec;
+      continue;
+    }
+    PhaseOut po;
+    int rc = run_phase<0>(q, now, k - n_dec, n_dec, d_out, &po);
+    if (rc) return rc;
+    n_dec += po.n_dec;
+    if (n_dec >= k) break;
+    rc = run_phase<1>(q, now, k - n_dec, n_dec, d_out, &po);
+    if (rc) return rc;
+    n_dec += po.n_dec;
+    if (n_dec >= k) break;
+    // every normally eligible request is dispatched; the next pull is the
+    // terminal one (or an Allow limit break)
+    if (allow) {
+      int type;
+      double when;
+      rc = step_once(q, now, d_out, n_dec, &type, &when);
+      if (rc) return rc;
+      if (type != DMC_NEXT_RETURNING) {
+        r.next_type = type;
+        r.when = when;
+        break;
+      }
+      ++n_dec;
+      continue;
+    }
+    int type;
+    double when;
+    rc = future_of(q, &type, &when);
+    if (rc) return rc;
+    r.next_type = type;
+    r.when = when;
+    break;
+  }
+  r.n_decisions = n_dec;
+  if (res) *res = r;
+  return DMC_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+const char* dmc_strerror(int code) {
+  switch (code) {
+    case DMC_OK: return "ok";
+    case DMC_EAGAIN: return "rejected at limit (EAGAIN)";
+    case DMC_EINVAL: return "invalid argument";
+    case DMC_ENOMEM: return "out of device memory";
+    case DMC_EDEVICE: return "HIP runtime error";
+    case DMC_EBADTAG: return "bad tag (cost 0, or reservation and weight both 0)";
+    case DMC_EBADPARAMS: return "bad ReqParams (rho > delta)";
+    case DMC_EQUEUEFULL: return "client request ring full";
+    case DMC_ENOTREG: return "client slot not registered";
+    default: return "unknown error";
+  }
+}
+
+int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
+  if (!params || !out) return DMC_EINVAL;
+  const dmc_queue_params& p = *params;
+  if (p.max_clients == 0 || p.ring_capacity == 0 || p.ring_capacity > 64 ||
+      (p.ring_capacity & (p.ring_capacity - 1)))
+    return DMC_EINVAL;
+  if (p.at_limit < 0 || p.at_limit > 2) return DMC_EINVAL;
+  // AtLimit::Reject depends on ImmediateTagCalc, :856-857
+  if (p.at_limit == DMC_AT_LIMIT_REJECT && p.delayed) return DMC_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DMC_EDEVICE;
+  if (p.device < 0 || p.device >= ndev) return DMC_EINVAL;
+  HIP_OK(hipSetDevice(p.device));
+  dmc_queue* q = new dmc_queue;
+  q->p = p;
+  HIP_OK(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
+  uint32_t N = p.max_clients;
+  Table& t = q->tb;
+  t.n = N;
+  t.q = p.ring_capacity;
+  t.qmask = p.ring_capacity - 1;
+  t.delayed = p.delayed;
+  t.at_limit = p.at_limit;
+  t.reject_thr = p.at_limit == DMC_AT_LIMIT_REJECT ? p.reject_threshold : 0.0;
+  t.antic = p.anticipation_timeout;
+  auto A = [&](auto** ptr, size_t elems) -> int {
+    if (hipMalloc((void**)ptr, elems * sizeof(**ptr)) != hipSuccess) return DMC_ENOMEM;
+    return hipMemsetAsync(*ptr, 0, elems * sizeof(**ptr), q->stream) == hipSuccess
+               ? DMC_OK : DMC_EDEVICE;
+  };
+  int rc = 0;
+  rc |= A(&t.prev_r, N); rc |= A(&t.prev_p, N); rc |= A(&t.prev_l, N);
+  rc |= A(&t.prev_arr, N); rc |= A(&t.r_inv, N); rc |= A(&t.w_inv, N);
+  rc |= A(&t.l_inv, N); rc |= A(&t.pd, N); rc |= A(&t.front_r, N);
+  rc |= A(&t.front_p, N); rc |= A(&t.front_l, N); rc |= A(&t.head, N);
+  rc |= A(&t.count, N); rc |= A(&t.cur_delta, N); rc |= A(&t.cur_rho, N);
+  rc |= A(&t.last_tick, N); rc |= A(&t.flags, N);
+  rc |= A(&t.ring, (size_t)N * p.ring_capacity);
+  rc |= A(&q->keys, N); rc |= A(&q->cnt, N); rc |= A(&q->off, N);
+  rc |= A(&q->applied, N);
+  rc |= A(&q->hist, kHistBins); rc |= A(&q->hmax, kHistBins);
+  rc |= A(&q->sel, 1);
+  q->step_grid = grid_for(N, 1024);
+  rc |= A(&q->red, q->step_grid + 1);
+  rc |= A(&q->sctl, 1);
+  rc |= A(&q->act_min, 1);
+  rc |= A(&q->sched, 2);
+  rc |= A(&q->reqcount, 1);
+  if (rc) {
+    dmc_queue_destroy(q);
+    return DMC_ENOMEM;
+  }
+  size_t tscan = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, q->cnt, q->off, (int)N, q->stream);
+  if (ensure_temp(q, tscan) || ensure_entries(q, std::max<uint32_t>(p.max_batch, 1u << 16)) ||
+      ensure_batch(q, std::max<uint32_t>(p.max_batch, 1024)) ||
+      ensure_dec(q, std::max<uint32_t>(p.max_batch, 1024))) {
+    dmc_queue_destroy(q);
+    return DMC_ENOMEM;
+  }
+  q->reg_h.assign(N, 0);
+  q->idle_h.assign(N, 0);
+  if (hipStreamSynchronize(q->stream) != hipSuccess) {
+    dmc_queue_destroy(q);
+    return DMC_EDEVICE;
+  }
+  *out = q;
+  return DMC_OK;
+}
+
+int dmc_queue_destroy(dmc_queue* q) {
+  if (!q) return DMC_EINVAL;
+  if (q->stream) (void)hipStreamSynchronize(q->stream);
+  Table& t = q->tb;
+  void* ptrs[] = {t.prev_r, t.prev_p, t.prev_l, t.prev_arr, t.r_inv, t.w_inv,
+                  t.l_inv, t.pd, t.front_r, t.front_p, t.front_l, t.head,
+                  t.count, t.cur_delta, t.cur_rho, t.last_tick, t.flags, t.ring,
+                  q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sel,
+                  q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->ekey,
+                  q->skey, q->eval, q->sval, q->eslot, q->erun, q->eoff, q->gsz,
+                  q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
+                  q->skeys, q->svals, q->d_dec, q->temp};
+  for (void* p : ptrs)
+    dfree(p);
+  if (q->stream) (void)hipStreamDestroy(q->stream);
+  delete q;
+  return DMC_OK;
+}
+
+void* dmc_queue_stream(dmc_queue* q) { return q ? (void*)q->stream : nullptr; }
+
+int dmc_queue_sync(dmc_queue* q) {
+  if (!q) return DMC_EINVAL;
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+static double inv_of(double x) { return x == 0.0 ? 0.0 : 1.0 / x; }  // :115-117
+
+int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                              const double* r, const double* w, const double* l,
+                              int active) {
+  if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  for (uint32_t i = 0; i < n; ++i)
+    if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
+  if (!n) return DMC_OK;
+  std::vector<double> ri(n), wi(n), li(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    ri[i] = inv_of(r[i]);
+    wi[i] = inv_of(w[i]);
+    li[i] = inv_of(l[i]);
+  }
+  uint32_t* d_slots;
+  double *d_r, *d_w, *d_l;
+  HIP_OK(hipMalloc(&d_slots, 4ull * n));
+  HIP_OK(hipMalloc(&d_r, 8ull * n));
+  HIP_OK(hipMalloc(&d_w, 8ull * n));
+  HIP_OK(hipMalloc(&d_l, 8ull * n));
+  HIP_OK(hipMemcpyAsync(d_slots, slots, 4ull * n, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(d_r, ri.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(d_w, wi.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(d_l, li.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
+  hipLaunchKernelGGL(k_register, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, n, d_slots, d_r, d_w, d_l, active, q->tick);
+  HIP_OK(hipStreamSynchronize(q->stream));
+  dfree(d_slots); dfree(d_r); dfree(d_w); dfree(d_l);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = slots[i];
+    if (!q->reg_h[s]) ++q->n_registered;
+    if (q->idle_h[s]) --q->n_idle;
+    q->reg_h[s] = 1;
+    q->idle_h[s] = active ? 0 : 1;
+    if (!active) ++q->n_idle;
+  }
+  return DMC_OK;
+}
+
+int dmc_client_register(dmc_queue* q, uint32_t slot, double r, double w,
+                        double l, int active) {
+  return dmc_client_register_batch(q, 1, &slot, &r, &w, &l, active);
+}
+
+int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
+                           double l) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) return DMC_ENOTREG;
+  double v[3] = {inv_of(r), inv_of(w), inv_of(l)};
+  HIP_OK(hipMemcpyAsync(q->tb.r_inv + slot, &v[0], 8, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(q->tb.w_inv + slot, &v[1], 8, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(q->tb.l_inv + slot, &v[2], 8, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) return DMC_ENOTREG;
+  uint8_t f;
+  HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  f |= F_IDLE;
+  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  if (!q->idle_h[slot]) {
+    q->idle_h[slot] = 1;
+    ++q->n_idle;
+  }
+  return DMC_OK;
+}
+
+static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
+                        uint32_t* head) {
+  uint32_t h, c;
+  HIP_OK(hipMemcpyAsync(&h, q->tb.head + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&c, q->tb.count + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  std::vector<ReqEntry> ring(q->p.ring_capacity);
+  HIP_OK(hipMemcpyAsync(ring.data(), q->tb.ring + (size_t)slot * q->p.ring_capacity,
+                        sizeof(ReqEntry) * q->p.ring_capacity, hipMemcpyDeviceToHost,
+                        q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  ents->clear();
+  for (uint32_t i = 0; i < c; ++i) ents->push_back(ring[(h + i) & q->tb.qmask]);
+  *head = h;
+  return DMC_OK;
+}
+
+// rewrite a client's queue (after filtering), keeping the front's ready flag
+// only if the front survived
+static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>& ents,
+                       bool front_kept) {
+  uint32_t Q = q->p.ring_capacity;
+  std::vector<ReqEntry> ring(Q);
+  for (size_t i = 0; i < ents.size(); ++i) ring[i] = ents[i];
+  HIP_OK(hipMemcpyAsync(q->tb.ring + (size_t)slot * Q, ring.data(), sizeof(ReqEntry) * Q,
+                        hipMemcpyHostToDevice, q->stream));
+  uint32_t z = 0, c = (uint32_t)ents.size();
+  HIP_OK(hipMemcpyAsync(q->tb.head + slot, &z, 4, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(q->tb.count + slot, &c, 4, hipMemcpyHostToDevice, q->stream));
+  if (c) {
+    HIP_OK(hipMemcpyAsync(q->tb.front_r + slot, &ring[0].r, 8, hipMemcpyHostToDevice, q->stream));
+    HIP_OK(hipMemcpyAsync(q->tb.front_p + slot, &ring[0].p, 8, hipMemcpyHostToDevice, q->stream));
+    HIP_OK(hipMemcpyAsync(q->tb.front_l + slot, &ring[0].l, 8, hipMemcpyHostToDevice, q->stream));
+  }
+  uint8_t f;
+  HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  if (!front_kept || !c) f &= (uint8_t)~F_READY;
+  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
+                     uint32_t cap, uint32_t* n_out) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) return DMC_ENOTREG;
+  std::vector<ReqEntry> ents;
+  uint32_t h;
+  int rc = read_handles(q, slot, &ents, &h);
+  if (rc) return rc;
+  for (size_t i = 0; i < ents.size() && i < cap; ++i)
+    if (handles_out) handles_out[i] = ents[i].handle;
+  if (n_out) *n_out = (uint32_t)ents.size();
+  uint32_t z = 0;
+  uint8_t f = 0;
+  HIP_OK(hipMemcpyAsync(q->tb.count + slot, &z, 4, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  if (q->idle_h[slot]) --q->n_idle;
+  q->reg_h[slot] = 0;
+  q->idle_h[slot] = 0;
+  --q->n_registered;
+  return DMC_OK;
+}
+
+int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
+  if (!q || !s || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  std::memset(s, 0, sizeof(*s));
+  const Table& t = q->tb;
+  auto D = [&](double* dst, const double* src) {
+    return hipMemcpyAsync(dst, src + slot, 8, hipMemcpyDeviceToHost, q->stream);
+  };
+  uint32_t head = 0;
+  uint8_t f = 0;
+  HIP_OK(D(&s->prev_r, t.prev_r)); HIP_OK(D(&s->prev_p, t.prev_p));
+  HIP_OK(D(&s->prev_l, t.prev_l)); HIP_OK(D(&s->prev_arrival, t.prev_arr));
+  HIP_OK(D(&s->prop_delta, t.pd)); HIP_OK(D(&s->front_r, t.front_r));
+  HIP_OK(D(&s->front_p, t.front_p)); HIP_OK(D(&s->front_l, t.front_l));
+  HIP_OK(D(&s->r_inv, t.r_inv)); HIP_OK(D(&s->w_inv, t.w_inv));
+  HIP_OK(D(&s->l_inv, t.l_inv));
+  HIP_OK(hipMemcpyAsync(&s->last_tick, t.last_tick + slot, 8, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&s->count, t.count + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&head, t.head + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&s->cur_delta, t.cur_delta + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&s->cur_rho, t.cur_rho + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&f, t.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  if (s->count) {
+    ReqEntry e;
+    HIP_OK(hipMemcpyAsync(&e, t.ring + (size_t)slot * t.q + head, sizeof(e),
+                          hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    s->front_arrival = e.arrival;
+  } else {
+    s->front_r = s->front_p = s->front_l = 0.0;
+  }
+  s->idle = (f & F_IDLE) ? 1 : 0;
+  s->front_ready = (f & F_READY) && s->count ? 1 : 0;
+  s->registered = (f & F_REG) ? 1 : 0;
+  return s->registered ? DMC_OK : DMC_ENOTREG;
+}
+
+int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
+  if (!q || !out || n > q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  HIP_OK(hipMemcpyAsync(out, q->tb.last_tick, 8ull * n, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
+                  int32_t* rc_out) {
+  if (!q || (n && !reqs)) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!n) return DMC_OK;
+  int rc = ensure_batch(q, n);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(q->d_reqs, reqs, sizeof(dmc_request) * n,
+                        hipMemcpyHostToDevice, q->stream));
+  rc = q->n_idle ? add_host_split(q, reqs, n, q->d_reqs, q->d_rc)
+                 : add_segment(q, q->d_reqs, n, q->d_rc, q->tick);
+  if (rc) return rc;
+  q->tick += n;
+  if (rc_out)
+    HIP_OK(hipMemcpyAsync(rc_out, q->d_rc, 4ull * n, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
+                         int32_t* d_rc_out) {
+  if (!q || (n && (!d_reqs || !d_rc_out))) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!n) return DMC_OK;
+  int rc = ensure_batch(q, n);
+  if (rc) return rc;
+  if (q->n_idle) {
+    // activations need the host-ordered split: stage the batch on the host
+    std::vector<dmc_request> h(n);
+    HIP_OK(hipMemcpyAsync(h.data(), d_reqs, sizeof(dmc_request) * n,
+                          hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    rc = add_host_split(q, h.data(), n, d_reqs, d_rc_out);
+  } else {
+    rc = add_segment(q, d_reqs, n, d_rc_out, q->tick);
+  }
+  if (rc) return rc;
+  q->tick += n;
+  return DMC_OK;
+}
+
+int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
+                   dmc_pull_result* result) {
+  if (!q || (k && !out)) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  int rc = ensure_dec(q, k);
+  if (rc) return rc;
+  dmc_pull_result r{};
+  rc = pull_impl(q, now, k, q->d_dec, &r);
+  if (rc) return rc;
+  if (r.n_decisions)
+    HIP_OK(hipMemcpyAsync(out, q->d_dec, sizeof(dmc_decision) * r.n_decisions,
+                          hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  for (uint32_t i = 0; i < r.n_decisions; ++i)
+    (out[i].phase == DMC_PHASE_RESERVATION ? r.n_reservation : r.n_priority)++;
+  if (result) *result = r;
+  return DMC_OK;
+}
+
+int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
+                          dmc_decision* d_out, dmc_pull_result* d_result) {
+  if (!q || (k && !d_out)) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  dmc_pull_result r{};
+  int rc = pull_impl(q, now, k, d_out, &r);
+  if (rc) return rc;
+  if (d_result)
+    HIP_OK(hipMemcpyAsync(d_result, &r, sizeof(r), hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
+                         uint64_t* handles_out, uint32_t cap, uint32_t* n_out) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) {
+    if (n_out) *n_out = 0;
+    return DMC_OK;  // client_map.find fails -> return, :599-601
+  }
+  std::vector<ReqEntry> ents;
+  uint32_t h;
+  int rc = read_handles(q, slot, &ents, &h);
+  if (rc) return rc;
+  uint32_t n = (uint32_t)ents.size();
+  for (uint32_t i = 0; i < n && i < cap; ++i)
+    if (handles_out) handles_out[i] = ents[reverse ? n - 1 - i : i].handle;
+  if (n_out) *n_out = n;
+  return write_queue(q, slot, {}, false);
+}
+
+int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
+                        uint32_t cap, uint32_t* n_out) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) return DMC_ENOTREG;
+  std::vector<ReqEntry> ents;
+  uint32_t h;
+  int rc = read_handles(q, slot, &ents, &h);
+  if (rc) return rc;
+  for (size_t i = 0; i < ents.size() && i < cap; ++i)
+    if (handles_out) handles_out[i] = ents[i].handle;
+  if (n_out) *n_out = (uint32_t)ents.size();
+  return DMC_OK;
+}
+
+int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
+                      const uint8_t* keep) {
+  if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (!q->reg_h[slot]) return DMC_ENOTREG;
+  std::vector<ReqEntry> ents;
+  uint32_t h;
+  int rc = read_handles(q, slot, &ents, &h);
+  if (rc) return rc;
+  if (n != ents.size() || (n && !keep)) return DMC_EINVAL;
+  std::vector<ReqEntry> kept;
+  for (uint32_t i = 0; i < n; ++i)
+    if (keep[i]) kept.push_back(ents[i]);
+  if (kept.size() == ents.size()) return DMC_OK;
+  return write_queue(q, slot, kept, n > 0 && keep[0]);
+}
+
+int dmc_stats_get(dmc_queue* q, dmc_stats* out) {
+  if (!q || !out) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  unsigned long long sc[2];
+  HIP_OK(hipMemsetAsync(q->reqcount, 0, 8, q->stream));
+  hipLaunchKernelGGL(k_count_requests, dim3(grid_for(q->tb.n, 1024)), dim3(kBlock),
+                     0, q->stream, q->tb, q->reqcount);
+  unsigned long long rq = 0;
+  HIP_OK(hipMemcpyAsync(&rq, q->reqcount, 8, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(sc, q->sched, 16, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  out->tick = q->tick;
+  out->reserv_sched_count = sc[0];
+  out->prop_sched_count = sc[1];
+  out->limit_break_sched_count = 0;  // never incremented by the reference, :812
+  out->clients = q->n_registered;
+  out->requests = rq;
+  return DMC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,324 @@
+"""ctypes binding of the HIP engine's C-ABI (include/dmclock_gpu.h).
+
+`GpuQueue` exposes the same Python surface as the CPU restatement used by the
+tests (set_info / add / pull / pull_batch / ...), so that one driver can run a
+trace through both.  Like the C++ facade (dmclock_amd/include/dmclock_server.h)
+it maps the reference's client ids to dense device slots and models
+client_info_f: the ClientInfo a client maps to can be mutated in place (seen at
+once, as through the reference's cached pointer) or replaced by a fresh object
+(seen after update_client_info, or at every tag with dynamic_info / U1).
+
+There is no CPU fallback: the engine library must be present and a HIP device
+must exist, or construction fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from ._abi import (DECISION_DTYPE, REQUEST_DTYPE, ClientState, PullResult,
+                   QueueParams, Stats, make_requests)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdmclock_gpu.so")
+_lib = None
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_i32 = ctypes.c_int
+_f64 = ctypes.c_double
+
+EXPORTS = {
+    "dmc_queue_create": (_i32, [ctypes.POINTER(QueueParams), ctypes.POINTER(_vp)]),
+    "dmc_queue_destroy": (_i32, [_vp]),
+    "dmc_queue_stream": (_vp, [_vp]),
+    "dmc_queue_sync": (_i32, [_vp]),
+    "dmc_strerror": (ctypes.c_char_p, [_i32]),
+    "dmc_client_register": (_i32, [_vp, _u32, _f64, _f64, _f64, _i32]),
+    "dmc_client_register_batch": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _i32]),
+    "dmc_client_update_info": (_i32, [_vp, _u32, _f64, _f64, _f64]),
+    "dmc_client_mark_idle": (_i32, [_vp, _u32]),
+    "dmc_client_erase": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
+    "dmc_client_get_state": (_i32, [_vp, _u32, ctypes.POINTER(ClientState)]),
+    "dmc_client_last_ticks": (_i32, [_vp, _u32, _vp]),
+    "dmc_add_batch": (_i32, [_vp, _u32, _vp, _vp]),
+    "dmc_add_batch_device": (_i32, [_vp, _u32, _vp, _vp]),
+    "dmc_pull_batch": (_i32, [_vp, _f64, _u32, _vp, ctypes.POINTER(PullResult)]),
+    "dmc_pull_batch_device": (_i32, [_vp, _f64, _u32, _vp, _vp]),
+    "dmc_remove_by_client": (_i32, [_vp, _u32, _i32, _vp, _u32,
+                                    ctypes.POINTER(_u32)]),
+    "dmc_client_requests": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
+    "dmc_client_filter": (_i32, [_vp, _u32, _u32, _vp]),
+    "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
+}
+
+
+class DmcError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the engine library (no fallback: raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DmcError(
+                f"{LIB_PATH} is missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().dmc_strerror(rc).decode()
+        raise DmcError(f"{what}: {msg} ({rc})")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class GpuQueue:
+    """One dmClock server queue on one HIP device."""
+
+    def __init__(self, max_clients=1024, ring_capacity=64, max_batch=1 << 16,
+                 delayed=False, dynamic_info=False, at_limit=0,
+                 reject_threshold=0.0, anticipation=0.0, device=0,
+                 branching=2, track_ties=True):
+        del branching, track_ties  # no heaps on the device
+        self.L = lib()
+        p = QueueParams()
+        p.max_clients = max_clients
+        p.ring_capacity = ring_capacity
+        p.max_batch = max_batch
+        p.delayed = int(delayed)
+        p.dynamic_info = int(dynamic_info)
+        p.at_limit = at_limit
+        p.reject_threshold = float(reject_threshold)
+        p.anticipation_timeout = float(anticipation)
+        p.device = device
+        h = _vp()
+        _check(self.L.dmc_queue_create(ctypes.byref(p), ctypes.byref(h)),
+               "dmc_queue_create")
+        self.h = h
+        self.params = p
+        self.dynamic = bool(dynamic_info)
+        self.slot_of = {}      # client id -> slot
+        self.client_of = []    # slot -> client id
+        self.info_cur = {}     # client -> (r, w, l) client_info_f returns now
+        self.info_dev = {}     # client -> (r, w, l) the device uses
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.dmc_queue_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- client_info_f model
+    def set_info(self, client, r, w, l, fresh=False):
+        self.info_cur[client] = (float(r), float(w), float(l))
+        if not fresh and client in self.slot_of:
+            self._push_info(client)
+
+    def _push_info(self, client):
+        v = self.info_cur[client]
+        if self.info_dev.get(client) != v:
+            _check(self.L.dmc_client_update_info(self.h, self.slot_of[client],
+                                                 *v), "update_info")
+            self.info_dev[client] = v
+
+    def _slot(self, client):
+        s = self.slot_of.get(client)
+        if s is None:
+            s = len(self.client_of)
+            r, w, l = self.info_cur[client]
+            _check(self.L.dmc_client_register(self.h, s, r, w, l, 0),
+                   "register")
+            self.slot_of[client] = s
+            self.client_of.append(client)
+            self.info_dev[client] = (r, w, l)
+        return s
+
+    def register_active(self, slots, r, w, l):
+        """Bulk registration (deviation shared with the oracle): client id ==
+        slot, idle=false, prop_delta=0."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        l = np.ascontiguousarray(l, dtype=np.float64)
+        _check(self.L.dmc_client_register_batch(self.h, len(slots), _ptr(slots),
+                                                _ptr(r), _ptr(w), _ptr(l), 1),
+               "register_batch")
+        for i, s in enumerate(slots.tolist()):
+            self.slot_of[s] = s
+            self.info_cur[s] = self.info_dev[s] = (r[i], w[i], l[i])
+        if len(self.client_of) < int(slots.max()) + 1:
+            self.client_of.extend(range(len(self.client_of),
+                                        int(slots.max()) + 1))
+
+    def register(self, slots, r, w, l, active):
+        """Register clients with client id == slot (trace drivers)."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        l = np.ascontiguousarray(l, dtype=np.float64)
+        _check(self.L.dmc_client_register_batch(self.h, len(slots), _ptr(slots),
+                                                _ptr(r), _ptr(w), _ptr(l),
+                                                int(active)), "register_batch")
+        top = int(slots.max()) + 1 if len(slots) else 0
+        if len(self.client_of) < top:
+            self.client_of.extend(range(len(self.client_of), top))
+        for i, s in enumerate(slots.tolist()):
+            self.slot_of[s] = s
+            self.info_cur[s] = self.info_dev[s] = (r[i], w[i], l[i])
+
+    # ---- hot path
+    def add(self, client, time, delta=1, rho=1, cost=1, handle=0):
+        s = self._slot(client)
+        if self.dynamic:
+            self._push_info(client)
+        req = make_requests([s], [time], [cost], [delta], [rho], [handle])
+        return int(self.add_batch(req)[0])
+
+    def add_batch(self, reqs):
+        """reqs: REQUEST_DTYPE array whose `slot` field holds device slots."""
+        reqs = np.ascontiguousarray(reqs, dtype=REQUEST_DTYPE)
+        rc = np.zeros(len(reqs), dtype=np.int32)
+        _check(self.L.dmc_add_batch(self.h, len(reqs), _ptr(reqs), _ptr(rc)),
+               "add_batch")
+        return rc
+
+    def _refresh_dynamic(self):
+        if self.dynamic:
+            for c in self.slot_of:
+                self._push_info(c)
+
+    def pull(self, now):
+        d, res = self.pull_batch(now, 1)
+        if res.n_decisions:
+            rec = d[0].copy()
+            rec["slot"] = self.client_of[int(rec["slot"])]
+            return 0, rec, 0.0
+        return res.next_type, None, res.when
+
+    def pull_batch(self, now, k):
+        self._refresh_dynamic()
+        out = np.zeros(max(k, 1), dtype=DECISION_DTYPE)
+        res = PullResult()
+        _check(self.L.dmc_pull_batch(self.h, float(now), k, _ptr(out),
+                                     ctypes.byref(res)), "pull_batch")
+        return out[:res.n_decisions].copy(), res
+
+    # ---- device-pointer variants (bench)
+    def add_batch_device(self, d_reqs_ptr, n, d_rc_ptr):
+        _check(self.L.dmc_add_batch_device(self.h, n, d_reqs_ptr, d_rc_ptr),
+               "add_batch_device")
+
+    def pull_batch_device(self, now, k, d_out_ptr, d_res_ptr=None):
+        _check(self.L.dmc_pull_batch_device(self.h, float(now), k, d_out_ptr,
+                                            d_res_ptr), "pull_batch_device")
+
+    def stream(self):
+        return self.L.dmc_queue_stream(self.h)
+
+    # ---- maintenance
+    def stats(self):
+        st = Stats()
+        _check(self.L.dmc_stats_get(self.h, ctypes.byref(st)), "stats")
+        return st
+
+    def request_count(self):
+        return self.stats().requests
+
+    def client_count(self):
+        return self.stats().clients
+
+    def sched_counts(self):
+        st = self.stats()
+        return st.reserv_sched_count, st.prop_sched_count
+
+    def tick(self):
+        return self.stats().tick
+
+    def update_client_info(self, client):
+        if client in self.slot_of:
+            self._push_info(client)
+
+    def update_client_infos(self):
+        for c in self.slot_of:
+            self._push_info(c)
+
+    def remove_by_client(self, client, reverse=False):
+        if client not in self.slot_of:
+            return np.zeros(0, dtype=np.uint64)
+        cap = self.params.ring_capacity
+        out = np.zeros(cap, dtype=np.uint64)
+        n = _u32(0)
+        _check(self.L.dmc_remove_by_client(self.h, self.slot_of[client],
+                                           int(reverse), _ptr(out), cap,
+                                           ctypes.byref(n)), "remove_by_client")
+        return out[:n.value].copy()
+
+    def client_requests(self, client):
+        cap = self.params.ring_capacity
+        out = np.zeros(cap, dtype=np.uint64)
+        n = _u32(0)
+        _check(self.L.dmc_client_requests(self.h, self.slot_of[client],
+                                          _ptr(out), cap, ctypes.byref(n)),
+               "client_requests")
+        return out[:n.value].copy()
+
+    def remove_by_req_filter(self, fn, backwards=False):
+        """remove_by_req_filter (dmclock_server.h:567-585): clients visited in
+        ascending client-id order (std::map), each client's requests front to
+        back, or back to front when `backwards`."""
+        any_removed = False
+        for c in sorted(self.slot_of):
+            hs = self.client_requests(c).tolist()
+            if not hs:
+                continue
+            keep = np.ones(len(hs), dtype=np.uint8)
+            order = range(len(hs) - 1, -1, -1) if backwards else range(len(hs))
+            for i in order:
+                if fn(int(hs[i])):
+                    keep[i] = 0
+            if not keep.all():
+                any_removed = True
+                _check(self.L.dmc_client_filter(self.h, self.slot_of[c],
+                                                len(hs), _ptr(keep)), "filter")
+        return any_removed
+
+    def mark_idle(self, client):
+        _check(self.L.dmc_client_mark_idle(self.h, self.slot_of[client]),
+               "mark_idle")
+
+    def erase(self, client):
+        if client not in self.slot_of:
+            return False
+        n = _u32(0)
+        _check(self.L.dmc_client_erase(self.h, self.slot_of[client], None, 0,
+                                       ctypes.byref(n)), "erase")
+        return True
+
+    def client_state(self, client):
+        s = ClientState()
+        slot = self.slot_of.get(client, client)
+        rc = self.L.dmc_client_get_state(self.h, slot, ctypes.byref(s))
+        return s if rc == 0 else None
+
+    def last_ticks(self, n):
+        out = np.zeros(n, dtype=np.uint64)
+        _check(self.L.dmc_client_last_ticks(self.h, n, _ptr(out)), "last_ticks")
+        return out
+

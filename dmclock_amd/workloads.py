@@ -1,0 +1,151 @@
+"""Deterministic synthetic dmClock traces (BASELINE.json configs 3-4 and the
+parity-test traces).
+
+A trace is a client table plus a list of operations, replayed identically on
+the HIP engine and on the CPU restatement:
+    ("add", reqs)            REQUEST_DTYPE array, in arrival order
+    ("pull", now, k)         up to k pull_request(now)
+    ("idle", slots)          do_clean's idle marking for these clients
+    ("info", slot, r, w, l)  client_info_f changes + update_client_info
+
+Time base t0 = 1.0 s (epoch-scale times create rounding
+ties between tags).  Client ids are slots.
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._abi import REQUEST_DTYPE
+
+
+@dataclass
+class ClientTable:
+    slots: np.ndarray
+    r: np.ndarray
+    w: np.ndarray
+    l: np.ndarray
+    active: bool = True
+
+
+@dataclass
+class Trace:
+    clients: ClientTable
+    ops: list = field(default_factory=list)
+    params: dict = field(default_factory=dict)
+
+
+def client_table(rng, n, frac_r=0.5, r_range=(1.0, 10.0), w_range=(0.5, 1.5),
+                 frac_l=0.3, l_range=(5.0, 25.0), active=True):
+    """Config 3 mix: r ~ U[1,10] for frac_r of clients (else 0);
+    w ~ U[0.5,1.5]; l ~ U[5,25] for frac_l (else 0)."""
+    slots = np.arange(n, dtype=np.uint32)
+    r = np.where(rng.random(n) < frac_r, rng.uniform(*r_range, n), 0.0)
+    w = rng.uniform(*w_range, n)
+    l = np.where(rng.random(n) < frac_l, rng.uniform(*l_range, n), 0.0)
+    return ClientTable(slots, r, w, l, active)
+
+
+def arrivals(rng, n_clients, n, t_start, rate, costs=(1, 2, 3),
+             delta_rho="ones", handle_base=0, clients=None):
+    """n requests of a Poisson process of aggregate `rate` over uniformly
+    chosen clients (or the given client subset)."""
+    gaps = rng.exponential(1.0 / rate, n)
+    times = t_start + np.cumsum(gaps)
+    out = np.zeros(n, dtype=REQUEST_DTYPE)
+    if clients is None:
+        out["slot"] = rng.integers(0, n_clients, n, dtype=np.uint32)
+    else:
+        out["slot"] = rng.choice(clients, n)
+    out["time"] = times
+    out["cost"] = rng.choice(np.asarray(costs, dtype=np.uint32), n)
+    if delta_rho == "ones":
+        out["delta"] = 1
+        out["rho"] = 1
+    else:
+        d = rng.integers(0, 4, n, dtype=np.uint32)
+        out["delta"] = d
+        out["rho"] = (rng.random(n) * (d + 1)).astype(np.uint32)
+    out["handle"] = np.arange(handle_base, handle_base + n, dtype=np.uint64)
+    return out
+
+
+def steady_trace(seed, n_clients, n_steps, adds_per_step, pulls_per_step,
+                 rate=None, depth=4, t0=1.0, delta_rho="ones", costs=(1, 2, 3),
+                 table_kw=None, k_choices=None):
+    """Config-3-style trace: bulk-registered active clients, a pre-population
+    of `depth` requests per client, then steps of `adds_per_step` arrivals
+    followed by pulls at the step's end time."""
+    rng = np.random.default_rng(seed)
+    tab = client_table(rng, n_clients, **(table_kw or {}))
+    rate = rate or 2.0 * n_clients
+    tr = Trace(tab, params=dict(seed=seed, n_clients=n_clients, rate=rate))
+    handle = 0
+    t = t0
+    pre = depth * n_clients
+    if pre:
+        reqs = arrivals(rng, n_clients, pre, t, rate, costs, delta_rho, handle)
+        handle += pre
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+    for _ in range(n_steps):
+        reqs = arrivals(rng, n_clients, adds_per_step, t, rate, costs,
+                        delta_rho, handle)
+        handle += adds_per_step
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+        k = pulls_per_step if k_choices is None else int(rng.choice(k_choices))
+        tr.ops.append(("pull", t, k))
+    return tr
+
+
+def churn_trace(seed, n_clients, n_steps, adds_per_step, pulls_per_step,
+                idle_frac=0.1, rate=None, t0=1.0, delta_rho="random",
+                k_choices=None):
+    """Config-4-style trace: like steady_trace but each step marks a random
+    fraction of clients idle first; their next request re-activates them
+    through the idle reset (prop_delta = L - t, dmclock_server.h:937-985)."""
+    rng = np.random.default_rng(seed)
+    tr = steady_trace(seed, n_clients, 0, 0, 0, rate=rate, depth=2, t0=t0,
+                      delta_rho=delta_rho)
+    rate = tr.params["rate"]
+    handle = 2 * n_clients
+    t = float(tr.ops[-1][1]["time"][-1])
+    for _ in range(n_steps):
+        idle = rng.choice(n_clients, max(1, int(idle_frac * n_clients)),
+                          replace=False).astype(np.uint32)
+        tr.ops.append(("idle", np.sort(idle)))
+        reqs = arrivals(rng, n_clients, adds_per_step, t, rate, (1, 2, 3),
+                        delta_rho, handle)
+        handle += adds_per_step
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+        k = pulls_per_step if k_choices is None else int(rng.choice(k_choices))
+        tr.ops.append(("pull", t, k))
+    return tr
+
+
+def replay(q, trace, check=None):
+    """Replay a trace on a queue exposing register/add_batch/pull_batch/
+    mark_idle/set_info/update_client_info.  Yields per-op outputs."""
+    c = trace.clients
+    q.register(c.slots, c.r, c.w, c.l, c.active)
+    outs = []
+    for op in trace.ops:
+        if op[0] == "add":
+            outs.append(("add", q.add_batch(op[1])))
+        elif op[0] == "pull":
+            d, res = q.pull_batch(op[1], op[2])
+            outs.append(("pull", d, (res.n_decisions, res.next_type,
+                                     res.when if res.next_type == 1 else 0.0)))
+        elif op[0] == "idle":
+            for s in op[1].tolist():
+                q.mark_idle(s)
+            outs.append(("idle", None))
+        elif op[0] == "info":
+            _, s, r, w, l = op
+            q.set_info(s, r, w, l)
+            q.update_client_info(s)
+            outs.append(("info", None))
+        if check is not None:
+            check(op, outs[-1])
+    return outs

@@ -136,6 +136,16 @@ class OracleQueue:
                                               _ptr(l))
         assert rc == 0, rc
 
+    def register(self, clients, r, w, l, active):
+        """Trace-driver registration: active -> bulk registration; inactive
+        -> only client_info_f is defined (the record is created, idle, by the
+        client's first add_request, dmclock_server.h:920-932)."""
+        if active:
+            self.register_active(clients, r, w, l)
+        else:
+            for c, a, b, d in zip(np.asarray(clients).tolist(), r, w, l):
+                self.set_info(c, float(a), float(b), float(d))
+
     def add(self, client, time, delta=1, rho=1, cost=1, handle=0):
         return self.L.dmo_add(self.h, handle, client, delta, rho, time, cost)
 

@@ -1,0 +1,68 @@
+"""Trace-level parity between the HIP engine and the oracle (test helper)."""
+import numpy as np
+
+import pyoracle
+from dmclock_amd import workloads
+
+STATE_FIELDS = ("prev_r", "prev_p", "prev_l", "prev_arrival", "prop_delta",
+                "front_r", "front_p", "front_l", "front_arrival", "count",
+                "cur_delta", "cur_rho", "idle", "front_ready")
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def compare_decisions(dg, do, where):
+    assert len(dg) == len(do), (where, len(dg), len(do))
+    for f in ("slot", "phase", "cost", "handle"):
+        bad = np.nonzero(dg[f] != do[f])[0]
+        assert bad.size == 0, (where, f, int(bad[0]), dg[bad[0]], do[bad[0]])
+    for f in ("tag_r", "tag_p", "tag_l"):
+        bad = np.nonzero(bits(dg[f]) != bits(do[f]))[0]
+        assert bad.size == 0, (where, f, int(bad[0]), dg[bad[0]], do[bad[0]])
+
+
+def compare_states(qg, qo, slots, where=""):
+    for s in slots:
+        sg, so = qg.client_state(int(s)), qo.client_state(int(s))
+        assert (sg is None) == (so is None), (where, s)
+        if sg is None:
+            continue
+        for f in STATE_FIELDS:
+            a, b = getattr(sg, f), getattr(so, f)
+            if isinstance(a, float):
+                if f.startswith("front") and not so.count:
+                    continue
+                assert np.float64(a).view(np.uint64) == \
+                    np.float64(b).view(np.uint64), (where, s, f, a, b)
+            else:
+                assert a == b, (where, s, f, a, b)
+
+
+def run_parity(trace, mk_gpu, queue_kw=None, state_sample=64, require_tie_free=True):
+    """Replay `trace` on both engines op by op and compare every output."""
+    queue_kw = queue_kw or {}
+    qo = pyoracle.OracleQueue(**queue_kw)
+    qg = mk_gpu(max_clients=int(trace.clients.slots.max()) + 1, **queue_kw)
+    outs_o = workloads.replay(qo, trace)
+    ties = qo.ties
+    if require_tie_free:
+        assert ties == 0, f"trace has {ties} tied decisions; pick another seed"
+    outs_g = workloads.replay(qg, trace)
+    n_dec = 0
+    for i, (a, b) in enumerate(zip(outs_g, outs_o)):
+        assert a[0] == b[0]
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), (i, np.nonzero(a[1] != b[1]))
+        elif a[0] == "pull":
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], (i, a[2], b[2])
+            n_dec += len(a[1])
+    rng = np.random.default_rng(0)
+    slots = trace.clients.slots
+    sample = rng.choice(slots, min(state_sample, len(slots)), replace=False)
+    compare_states(qg, qo, sample, "final")
+    assert qg.request_count() == qo.request_count()
+    assert tuple(qg.sched_counts()) == tuple(qo.sched_counts())
+    return n_dec, qg, qo

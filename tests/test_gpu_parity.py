@@ -1,0 +1,112 @@
+"""Parity of the HIP engine against the oracle (needs an MI355X).
+
+Bar: bit-exact.  Every decision (client, phase, cost, request handle and the
+dispatched tag's bits), every add status, every stopping pull's type and
+future time, the scheduling counters, and sampled per-client state (prev tag,
+prop_delta, front tag, ready/idle flags) must equal the oracle's.  Traces are
+checked tie-free by the oracle first (among equal keys
+the reference's winner is its heap history; the engine breaks ties by lowest
+slot and flags them).
+"""
+import numpy as np
+import pytest
+
+import kats
+from dmclock_amd import workloads
+from dmclock_amd._abi import AT_LIMIT_ALLOW, AT_LIMIT_REJECT, AT_LIMIT_WAIT
+from parity import run_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def mk_gpu(**kw):
+    from dmclock_amd.gpu import GpuQueue
+    kw.setdefault("max_clients", 256)
+    kw.setdefault("ring_capacity", 64)
+    return GpuQueue(**kw)
+
+
+@pytest.mark.parametrize("kat", kats.SERVER_KATS, ids=lambda f: f.__name__)
+def test_server_kat_gpu(kat):
+    kat(mk_gpu)
+
+
+MODES = [
+    dict(at_limit=AT_LIMIT_WAIT),
+    dict(at_limit=AT_LIMIT_WAIT, delayed=True),
+    dict(at_limit=AT_LIMIT_ALLOW),
+    dict(at_limit=AT_LIMIT_REJECT, reject_threshold=0.5),
+]
+
+
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "-".join(
+    f"{k}={v}" for k, v in m.items()))
+@pytest.mark.parametrize("seed", [1, 2])
+def test_steady_trace_parity(mode, seed):
+    tr = workloads.steady_trace(seed, 300, 12, 200, 150, depth=3,
+                                delta_rho="random",
+                                k_choices=[1, 2, 7, 40, 150, 600, 5000])
+    n, _, _ = run_parity(tr, mk_gpu, mode)
+    assert n > 500
+
+
+@pytest.mark.parametrize("mode", MODES[:2], ids=["imm", "delayed"])
+def test_churn_trace_parity(mode):
+    tr = workloads.churn_trace(7, 300, 10, 250, 200, idle_frac=0.15,
+                               k_choices=[1, 9, 64, 200, 1000])
+    run_parity(tr, mk_gpu, mode, require_tie_free=False)
+
+
+def test_mixed_reservation_priority_mix():
+    """A trace tuned so that both phases and the R-runs after priority pops
+    (reduce_reservation_tags re-exposing reservations) occur."""
+    tr = workloads.steady_trace(11, 500, 15, 400, 380, depth=2,
+                                table_kw=dict(frac_r=0.4, r_range=(0.2, 2.0),
+                                              frac_l=0.4, l_range=(0.5, 4.0)),
+                                k_choices=[380, 2000])
+    n, qg, qo = run_parity(tr, mk_gpu, dict(at_limit=AT_LIMIT_WAIT))
+    res, prio = qo.sched_counts()
+    assert res > 100 and prio > 100
+
+
+def test_non_monotone_now_ready_flags():
+    """pull_request(now) with now going backwards: fronts marked ready at a
+    later `now` stay ready (the flag lives on the tag, :1139)."""
+    tr = workloads.steady_trace(5, 200, 6, 150, 0, depth=2,
+                                table_kw=dict(frac_l=0.8, l_range=(0.3, 2.0)))
+    t_end = float(tr.ops[-1][1]["time"][-1])
+    ops = [op for op in tr.ops if op[0] == "add"]
+    for i, t in enumerate([t_end, t_end - 1.0, t_end + 0.5, t_end - 2.0,
+                           t_end + 1.0, t_end + 3.0]):
+        ops.append(("pull", t, [3, 50, 1, 200, 17, 10000][i]))
+    tr.ops = ops
+    run_parity(tr, mk_gpu, dict(at_limit=AT_LIMIT_WAIT))
+
+
+def test_edge_empty_and_none():
+    """pull on an empty queue -> none; registered clients with no requests ->
+    none; limit-0 clients (limit tag -inf) with reservation r > now -> a
+    future at -inf (min_not_0_time excludes only 0.0, :1192-1195)."""
+    import pyoracle
+    from parity import compare_decisions
+    q = mk_gpu()
+    assert q.pull(1.0)[0] == 2
+    for qq in (q, pyoracle.OracleQueue()):
+        qq.register(np.array([0, 1], np.uint32), [1.0, 1.0], [0.0, 0.0],
+                    [0.0, 0.0], True)
+        assert qq.pull(1.0)[0] == 2
+    reqs = workloads.arrivals(np.random.default_rng(0), 2, 6, 5.0, 10.0)
+    outs = []
+    for qq in (q, pyoracle.OracleQueue()):
+        if not isinstance(qq, type(q)):
+            qq.register(np.array([0, 1], np.uint32), [1.0, 1.0], [0.0, 0.0],
+                        [0.0, 0.0], True)
+        qq.add_batch(reqs)
+        outs.append([qq.pull_batch(now, k) for now, k in
+                     ((5.0, 10), (5.5, 1), (6.0, 3), (9.0, 100))])
+    for (dg, rg), (do, ro) in zip(*outs):
+        compare_decisions(dg, do, "edge")
+        assert (rg.n_decisions, rg.next_type) == (ro.n_decisions, ro.next_type)
+        if rg.next_type == 1:
+            assert np.float64(rg.when).view(np.uint64) == \
+                np.float64(ro.when).view(np.uint64)
