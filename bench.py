@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json config 3 on the HIP engine.
+
+Workload ("step"): one dmClock server queue with 1M bulk-registered clients
+(r ~ U[1,10] for 50 %, w ~ U[0.5,1.5], l ~ U[5,25] for 30 %, cost in {1,2,3},
+delta = rho = 1), pre-populated with ~4 queued requests per client from a
+Poisson process of 2M req/s; each step adds the next 64K arrivals
+(tag updates) and then makes up to 64K pull_request(now) decisions at the
+step's last arrival time.  Inputs of every step are resident in HBM before
+the timed region; each step runs dmc_add_batch_device + dmc_pull_batch_device.
+
+metric = BASELINE.json metric: dispatch decisions/s + tag updates/s, whole job.
+With --gpus N each rank runs its own server queue (dmClock servers are
+independent: SURVEY.md section 8(e)), so scaling is weak and there is no
+collective on the data path.
+
+Extra fields: roofline (dominant stage, HIP-event timed inside the timed
+region on the engine's stream), cpu_baseline (the CPU restatement timed on
+this host, rank 0, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "dispatch decisions/sec + tag updates/sec at 1M clients; % of HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# Algorithmic bytes per unit for the single-kernel stages (DESIGN.md,
+# "Roofline accounting").  unit: "client" = one slot of the client table
+# scanned; "request" = one request of the add batch.
+STAGE_BYTES = {
+    # k_scan<1>: count 4 + flags 1 + front_l 8 + front_p 8 + prop_delta 8
+    #            read, key 8 written
+    "p_scan": ("client", 37),
+    # k_scan<0>: count 4 + front_r 8 read, key 8 written
+    "r_scan": ("client", 20),
+    # k_count: key 8 read, count 4 written (walks of candidates not counted)
+    "r_count": ("client", 12),
+    "p_count": ("client", 12),
+    # k_apply: candidate count 4 read
+    "r_apply": ("client", 4),
+    "p_apply": ("client", 4),
+    # k_add_chain: request 32 + sorted (slot,pos) 8 + rc 4 + ring entry 64
+    #              + client state read 81 / written 57
+    "add_chain": ("request", 246),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=1 << 16)
+    ap.add_argument("--pulls", type=int, default=None,
+                    help="decisions per step (default: = --batch)")
+    ap.add_argument("--depth", type=int, default=4)
+    ap.add_argument("--ring", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="do not record stage timers in the timed region")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles",
+                                                      "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def make_workload(args, seed):
+    from dmclock_amd import workloads
+    rng = np.random.default_rng(seed)
+    n = args.clients
+    tab = workloads.client_table(rng, n)
+    rate = 2.0 * n
+    pre = workloads.arrivals(rng, n, args.depth * n, 1.0, rate)
+    t = float(pre["time"][-1])
+    steps = []
+    handle = len(pre)
+    for _ in range(args.warmup + args.steps):
+        reqs = workloads.arrivals(rng, n, args.batch, t, rate,
+                                  handle_base=handle)
+        handle += args.batch
+        t = float(reqs["time"][-1])
+        steps.append(reqs)
+    return tab, pre, steps
+
+
+def cpu_baseline(args, tab, pre, steps):
+    """The oracle (CPU restatement of the reference queue, one core) on a
+    bounded sample of the same workload: same 1M clients and pre-population,
+    timed over --cpu-steps steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    q = pyoracle.OracleQueue(track_ties=False)
+    q.register_active(tab.slots, tab.r, tab.w, tab.l)
+    chunk = 1 << 20
+    for i in range(0, len(pre), chunk):
+        q.add_batch(pre[i:i + chunk])
+    k = args.pulls or args.batch
+    ops = 0
+    t0 = time.perf_counter()
+    for reqs in steps[:args.cpu_steps]:
+        q.add_batch(reqs)
+        d, res = q.pull_batch(float(reqs["time"][-1]), k)
+        ops += len(reqs) + res.n_decisions
+    dt = time.perf_counter() - t0
+    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
+                       f"{args.clients} clients pre-populated with "
+                       f"{len(pre)} requests, {args.cpu_steps} steps of "
+                       f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    from dmclock_amd.gpu import GpuQueue
+    from dmclock_amd._abi import DECISION_DTYPE, PullResult
+
+    tab, pre, steps = make_workload(args, args.seed + rank)
+    k = args.pulls or args.batch
+    q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
+                 max_batch=max(args.batch, k, 1 << 20), device=local)
+    q.register_active(tab.slots, tab.r, tab.w, tab.l)
+    chunk = 1 << 20
+    for i in range(0, len(pre), chunk):
+        rc = q.add_batch(pre[i:i + chunk])
+        assert (rc == 0).all(), np.unique(rc)
+
+    dev = torch.device("cuda", local)
+    d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r in steps]
+    d_rc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+    d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8,
+                        device=dev)
+    res_sz = 24
+    d_res = torch.zeros((len(steps), res_sz), dtype=torch.uint8, device=dev)
+    nows = [float(r["time"][-1]) for r in steps]
+    torch.cuda.synchronize()
+
+    def step(i):
+        q.add_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr())
+        q.pull_batch_device(nows[i], k, d_out.data_ptr(),
+                            d_res[i].data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+    if not args.no_profile:
+        q.profile(True)
+        q.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    q.profile(False)
+    prof = q.profile_read()
+
+    res = d_res[args.warmup:].cpu().numpy()
+    n_dec = 0
+    n_res = 0
+    for row in res:
+        pr = PullResult.from_buffer_copy(row.tobytes())
+        n_dec += pr.n_decisions
+    rc_last = d_rc.cpu().numpy()
+    assert (rc_last == 0).all(), np.unique(rc_last, return_counts=True)
+    st = q.stats()
+    n_adds = args.steps * args.batch
+    local_ops = n_dec + n_adds
+
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        o = torch.tensor([local_ops, n_dec, n_adds], dtype=torch.float64,
+                         device=dev)
+        dist.all_reduce(o, op=dist.ReduceOp.SUM)
+        local_ops, n_dec, n_adds = (float(x) for x in o.tolist())
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # roofline: the dominant single-kernel stage of the timed region
+    roof = None
+    cand = [(ms, name) for name, (c, ms) in prof.items()
+            if name in STAGE_BYTES and c > 0]
+    if cand:
+        ms, name = max(cand)
+        c = prof[name][0]
+        unit, per = STAGE_BYTES[name]
+        units = args.clients if unit == "client" else args.batch
+        per_launch = per * units
+        avg_s = ms / c / 1e3
+        achieved = per_launch / avg_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                traffic = json.load(open(args.traffic)).get(name)
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "kernel": name,
+                "bytes_per_launch": per_launch,
+                "avg_launch_us": round(avg_s * 1e6, 2)}
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(args, tab, pre, steps[args.warmup:])
+
+    ms_step = dt / args.steps * 1e3
+    out = {
+        "metric": METRIC,
+        "value": round(local_ops / dt, 1),
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "config3: single server queue, synthetic 1M "
+                               "clients mixed r/w/l, 64K adds + 64K pulls "
+                               "per step",
+                   "clients": args.clients, "adds_per_step": args.batch,
+                   "pulls_per_step": k, "prepopulated": len(pre),
+                   "ring_capacity": args.ring,
+                   "parallelism": f"{world} independent server queue(s)"},
+        "decisions_per_s": round(n_dec / dt, 1),
+        "tag_updates_per_s": round(n_adds / dt, 1),
+        "reservation_decisions": int(st.reserv_sched_count),
+        "priority_decisions": int(st.prop_sched_count),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "stages_ms_per_step": {n: round(ms / max(args.steps, 1), 4)
+                               for n, (c, ms) in prof.items() if c},
+    }
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

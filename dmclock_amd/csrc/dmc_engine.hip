@@ -1028,9 +1028,60 @@ struct dmc_queue {
   size_t temp_bytes = 0;
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
+  // stage timers (HIP events on the queue's stream), see dmc_profile_*
+  struct ProfRec {
+    hipEvent_t a, b;
+    int stage;
+  };
+  bool prof_on = false;
+  std::vector<ProfRec> prof_pool;
+  size_t prof_n = 0;
+  double prof_ms[DMC_PROF_NSTAGES] = {};
+  uint64_t prof_cnt[DMC_PROF_NSTAGES] = {};
 };
 
 namespace {
+
+const char* kStageNames[DMC_PROF_NSTAGES] = {
+    "add_sort", "add_chain", "activate",
+    "r_scan", "r_select", "r_count", "r_offsets", "r_emit", "r_sort",
+    "r_decide", "r_apply",
+    "p_scan", "p_select", "p_count", "p_offsets", "p_emit", "p_sort",
+    "p_decide", "p_apply",
+    "step", "future"};
+
+void pb(dmc_queue* q, int stage) {
+  if (!q->prof_on) return;
+  if (q->prof_n == q->prof_pool.size()) {
+    dmc_queue::ProfRec r;
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) {
+      q->prof_on = false;
+      return;
+    }
+    q->prof_pool.push_back(r);
+  }
+  q->prof_pool[q->prof_n].stage = stage;
+  (void)hipEventRecord(q->prof_pool[q->prof_n].a, q->stream);
+}
+
+void pe(dmc_queue* q) {
+  if (!q->prof_on) return;
+  (void)hipEventRecord(q->prof_pool[q->prof_n].b, q->stream);
+  ++q->prof_n;
+}
+
+void pflush(dmc_queue* q) {
+  if (!q->prof_on || !q->prof_n) return;
+  (void)hipEventSynchronize(q->prof_pool[q->prof_n - 1].b);
+  for (size_t i = 0; i < q->prof_n; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, q->prof_pool[i].a, q->prof_pool[i].b) == hipSuccess) {
+      q->prof_ms[q->prof_pool[i].stage] += ms;
+      q->prof_cnt[q->prof_pool[i].stage] += 1;
+    }
+  }
+  q->prof_n = 0;
+}
 
 void dfree(void* p) {
   if (p) (void)hipFree(p);
@@ -1110,6 +1161,7 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
                 int32_t* d_rc, uint64_t tick_base) {
   if (!n) return DMC_OK;
   uint32_t g = (n + kBlock - 1) / kBlock;
+  pb(q, DMC_PROF_ADD_SORT);
   hipLaunchKernelGGL(k_add_keys, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
                      q->akeys, q->avals);
   size_t tb = q->temp_bytes;
@@ -1117,17 +1169,22 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
                                             q->avals, q->svals, (int)n, 0,
                                             slot_bits(q->p.max_clients),
                                             q->stream));
+  pe(q);
+  pb(q, DMC_PROF_ADD_CHAIN);
   hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
                      q->skeys, q->svals, d_reqs, n, tick_base, d_rc);
+  pe(q);
   return DMC_OK;
 }
 
 int activate(dmc_queue* q, uint32_t slot, double t) {
+  pb(q, DMC_PROF_ACTIVATE);
   HIP_OK(hipMemsetAsync(q->act_min, 0xff, sizeof(uint64_t), q->stream));
   hipLaunchKernelGGL(k_contrib_min, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock),
                      0, q->stream, q->tb, q->act_min);
   hipLaunchKernelGGL(k_activate, dim3(1), dim3(64), 0, q->stream, q->tb, slot,
                      t, (const uint64_t*)q->act_min);
+  pe(q);
   return DMC_OK;
 }
 
@@ -1166,42 +1223,59 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = grid_for(N, 2048);
+  const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
   Sel init{};
   init.kmin = kMaxKey;
   init.kmax = 0;
   init.g_last = 0;
   HIP_OK(hipMemcpyAsync(q->sel, &init, sizeof(Sel), hipMemcpyHostToDevice, q->stream));
+  pb(q, S0 + 0);
   hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
                      q->keys, q->sel);
+  pe(q);
+  pb(q, S0 + 1);
   hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
                      (const uint64_t*)q->keys, (const Sel*)q->sel, k_rem, q->hist,
                      q->hmax);
   hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, q->stream, q->sel, k_rem,
                      q->hist, q->hmax);
+  pe(q);
+  pb(q, S0 + 2);
   hipLaunchKernelGGL(k_count<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
                      (const uint64_t*)q->keys, (const Sel*)q->sel, q->cnt);
+  pe(q);
+  pb(q, S0 + 3);
   size_t tbytes = q->temp_bytes;
   HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->cnt, q->off, (int)N,
                                           q->stream));
   hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, q->stream, N,
                      (const uint32_t*)q->cnt, (const uint32_t*)q->off, q->sel);
+  pe(q);
   Sel hs;
   HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   uint32_t ne = hs.n_entries;
   po->n_dec = 0;
   po->terminal = (PH == 1) ? 1 : 0;
-  if (ne == 0) return DMC_OK;
+  if (ne == 0) {
+    pflush(q);
+    return DMC_OK;
+  }
   int rc = ensure_entries(q, ne);
   if (rc) return rc;
+  pb(q, S0 + 4);
   hipLaunchKernelGGL(k_emit<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
                      (const Sel*)q->sel, (const uint32_t*)q->cnt,
                      (const uint32_t*)q->off, q->ekey, q->eval, q->eslot, q->erun);
+  pe(q);
+  pb(q, S0 + 5);
   tbytes = q->temp_bytes;
   HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ekey, q->skey,
                                             q->eval, q->sval, (int)ne, 0, 64,
                                             q->stream));
+  pe(q);
   uint32_t ge = (ne + kBlock - 1) / kBlock;
+  pb(q, S0 + 6);
   if (PH == 0) {
     hipLaunchKernelGGL(k_decide_r, dim3(ge), dim3(kBlock), 0, q->stream, ne,
                        k_rem, n_dec, (const uint64_t*)q->skey,
@@ -1219,12 +1293,16 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
                        (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
                        q->etie, q->applied, q->sel);
   }
+  pe(q);
+  pb(q, S0 + 7);
   hipLaunchKernelGGL(k_apply<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
                      q->tick, (const Sel*)q->sel, (const uint32_t*)q->cnt,
                      (const uint32_t*)q->off, (const uint32_t*)q->eoff,
                      (const uint8_t*)q->etie, q->applied, d_out, q->sched);
+  pe(q);
   HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  pflush(q);
   po->n_dec = hs.n_dec_phase;
   po->terminal = (PH == 1) ? hs.terminal : 0;
   return DMC_OK;
@@ -1234,6 +1312,7 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
 int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
               int* type, double* when) {
   const Table& tb = q->tb;
+  pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
                      tb, now, q->red);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, q->stream,
@@ -1243,9 +1322,11 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
                      q->stream, tb, now, (const StepCtl*)q->sctl);
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
                      (const StepCtl*)q->sctl, d_out, idx, q->sched);
+  pe(q);
   StepCtl sc;
   HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  pflush(q);
   *type = sc.type;
   *when = sc.when;
   return DMC_OK;
@@ -1257,13 +1338,16 @@ int future_of(dmc_queue* q, int* type, double* when) {
   init.lmin_nr = kMaxKey;
   init.lmin_rd = kMaxKey;
   HIP_OK(hipMemcpyAsync(q->red, &init, sizeof(init), hipMemcpyHostToDevice, q->stream));
+  pb(q, DMC_PROF_FUTURE);
   hipLaunchKernelGGL(k_future_scan, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock), 0,
                      q->stream, q->tb, q->red);
   hipLaunchKernelGGL(k_future_final, dim3(1), dim3(64), 0, q->stream,
                      (const StepRed*)q->red, q->sctl);
+  pe(q);
   StepCtl sc;
   HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  pflush(q);
   *type = sc.type;
   *when = sc.when;
   return DMC_OK;
@@ -1434,6 +1518,10 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->skeys, q->svals, q->d_dec, q->temp};
   for (void* p : ptrs)
     dfree(p);
+  for (auto& r : q->prof_pool) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
   if (q->stream) (void)hipStreamDestroy(q->stream);
   delete q;
   return DMC_OK;
@@ -1652,6 +1740,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   if (rc_out)
     HIP_OK(hipMemcpyAsync(rc_out, q->d_rc, 4ull * n, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  pflush(q);
   return DMC_OK;
 }
 
@@ -1674,6 +1763,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   }
   if (rc) return rc;
   q->tick += n;
+  pflush(q);  // no-op unless profiling (then it waits for the add kernels)
   return DMC_OK;
 }
 
@@ -1758,6 +1848,37 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
     if (keep[i]) kept.push_back(ents[i]);
   if (kept.size() == ents.size()) return DMC_OK;
   return write_queue(q, slot, kept, n > 0 && keep[0]);
+}
+
+int dmc_profile_enable(dmc_queue* q, int on) {
+  if (!q) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  q->prof_on = on != 0;
+  q->prof_n = 0;
+  return DMC_OK;
+}
+
+int dmc_profile_reset(dmc_queue* q) {
+  if (!q) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  for (int i = 0; i < DMC_PROF_NSTAGES; ++i) {
+    q->prof_ms[i] = 0.0;
+    q->prof_cnt[i] = 0;
+  }
+  return DMC_OK;
+}
+
+int dmc_profile_read(dmc_queue* q, uint32_t stage, uint64_t* count,
+                     double* total_ms) {
+  if (!q || stage >= DMC_PROF_NSTAGES) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  if (count) *count = q->prof_cnt[stage];
+  if (total_ms) *total_ms = q->prof_ms[stage];
+  return DMC_OK;
+}
+
+const char* dmc_profile_stage_name(uint32_t stage) {
+  return stage < DMC_PROF_NSTAGES ? kStageNames[stage] : "";
 }
 
 int dmc_stats_get(dmc_queue* q, dmc_stats* out) {

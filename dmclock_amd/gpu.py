@@ -50,7 +50,13 @@ EXPORTS = {
     "dmc_client_requests": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
     "dmc_client_filter": (_i32, [_vp, _u32, _u32, _vp]),
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
+    "dmc_profile_enable": (_i32, [_vp, _i32]),
+    "dmc_profile_reset": (_i32, [_vp]),
+    "dmc_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.POINTER(_f64)]),
+    "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
+PROF_NSTAGES = 21
 
 
 class DmcError(RuntimeError):
@@ -231,6 +237,22 @@ class GpuQueue:
 
     def stream(self):
         return self.L.dmc_queue_stream(self.h)
+
+    # ---- stage timers (HIP events on the queue's stream)
+    def profile(self, on=True):
+        _check(self.L.dmc_profile_enable(self.h, int(on)), "profile_enable")
+
+    def profile_reset(self):
+        _check(self.L.dmc_profile_reset(self.h), "profile_reset")
+
+    def profile_read(self):
+        out = {}
+        for st in range(PROF_NSTAGES):
+            c, ms = ctypes.c_uint64(0), _f64(0.0)
+            _check(self.L.dmc_profile_read(self.h, st, ctypes.byref(c),
+                                           ctypes.byref(ms)), "profile_read")
+            out[self.L.dmc_profile_stage_name(st).decode()] = (c.value, ms.value)
+        return out
 
     # ---- maintenance
     def stats(self):

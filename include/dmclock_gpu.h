@@ -211,6 +211,26 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep);
 int dmc_stats_get(dmc_queue* q, dmc_stats* out);
 
+/* ------------------------------------------------------------ profiling
+ * Stage timers: HIP events recorded on the queue's stream around each stage
+ * of the add and pull pipelines (an extension of this library; the reference
+ * has compile-time PROFILE timers around add/pull instead,
+ * dmclock_server.h:1309-1312, support/src/profile.h). */
+#define DMC_PROF_ADD_SORT 0
+#define DMC_PROF_ADD_CHAIN 1
+#define DMC_PROF_ACTIVATE 2
+#define DMC_PROF_R_SCAN 3   /* r_scan r_select r_count r_offsets r_emit r_sort r_decide r_apply */
+#define DMC_PROF_P_SCAN 11  /* p_scan ... p_apply, same order */
+#define DMC_PROF_STEP 19
+#define DMC_PROF_FUTURE 20
+#define DMC_PROF_NSTAGES 21
+
+int dmc_profile_enable(dmc_queue* q, int on);
+int dmc_profile_reset(dmc_queue* q);
+int dmc_profile_read(dmc_queue* q, uint32_t stage, uint64_t* count,
+                     double* total_ms);
+const char* dmc_profile_stage_name(uint32_t stage);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,8 +74,8 @@ def test_non_monotone_now_ready_flags():
     later `now` stay ready (the flag lives on the tag, :1139)."""
     tr = workloads.steady_trace(5, 200, 6, 150, 0, depth=2,
                                 table_kw=dict(frac_l=0.8, l_range=(0.3, 2.0)))
-    t_end = float(tr.ops[-1][1]["time"][-1])
     ops = [op for op in tr.ops if op[0] == "add"]
+    t_end = float(ops[-1][1]["time"][-1])
     for i, t in enumerate([t_end, t_end - 1.0, t_end + 0.5, t_end - 2.0,
                            t_end + 1.0, t_end + 3.0]):
         ops.append(("pull", t, [3, 50, 1, 200, 17, 10000][i]))
