@@ -384,32 +384,52 @@ __global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
 // Pick the threshold T: every key <= T is a candidate and at least k_rem
 // eligible fronts are <= T (T is the largest key of the bucket holding the
 // k_rem-th smallest), or take everything when there are no more than k_rem.
-__global__ void k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist,
-                       uint64_t* hmax) {
-  __shared__ uint64_t T;
-  if (threadIdx.x == 0) {
-    uint32_t ne = sel->n_elig;
-    if (ne == 0) {
-      T = 0;  // nothing
-    } else if (ne <= k_rem) {
-      T = kMaxKey - 1;  // all eligible
-    } else {
-      uint32_t cum = 0;
-      T = sel->kmax;
-      for (int b = 0; b < kHistBins; ++b) {
-        cum += hist[b];
-        if (cum >= k_rem) {
-          T = hmax[b];
-          break;
-        }
+// launched with kPickThreads threads; each owns kHistBins / kPickThreads
+// consecutive bins; a block-wide exclusive scan finds the bin that holds the
+// k_rem-th smallest eligible key.
+constexpr int kPickThreads = 1024;
+constexpr int kBinsPerThread = kHistBins / kPickThreads;
+__global__ void __launch_bounds__(kPickThreads)
+k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
+  __shared__ uint32_t wsum[kPickThreads / 64];
+  uint32_t ne = sel->n_elig;
+  int t = threadIdx.x;
+  uint32_t h[kBinsPerThread];
+  uint32_t local = 0;
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    h[j] = hist[t * kBinsPerThread + j];
+    local += h[j];
+  }
+  // inclusive scan of `local` across the block
+  uint32_t incl = local;
+  int lane = t & 63, w = t >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int i = 0; i < w; ++i) wbase += wsum[i];
+  uint32_t before = wbase + incl - local;  // exclusive prefix
+  if (ne == 0) {
+    if (t == 0) sel->T = 0;  // nothing eligible
+  } else if (ne <= k_rem) {
+    if (t == 0) sel->T = kMaxKey - 1;  // everything eligible
+  } else if (before < k_rem && before + local >= k_rem) {
+    uint32_t cum = before;
+    for (int j = 0; j < kBinsPerThread; ++j) {
+      cum += h[j];
+      if (cum >= k_rem) {
+        sel->T = hmax[t * kBinsPerThread + j];
+        break;
       }
     }
-    sel->T = T;
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
-    hist[b] = 0;
-    hmax[b] = 0;
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    hist[t * kBinsPerThread + j] = 0;
+    hmax[t * kBinsPerThread + j] = 0;
   }
 }
 
@@ -812,21 +832,41 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part) {
   }
 }
 
+__device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
+  o.r = argmin_combine(o.r, b.r);
+  o.p = argmin_combine(o.p, b.p);
+  o.pnr = argmin_combine(o.pnr, b.pnr);
+  o.lmin_nr = b.lmin_nr < o.lmin_nr ? b.lmin_nr : o.lmin_nr;
+  o.lmin_rd = b.lmin_rd < o.lmin_rd ? b.lmin_rd : o.lmin_rd;
+  o.n_any += b.n_any;
+  o.n_ready += b.n_ready;
+  o.n_notready += b.n_notready;
+}
+
+// launched with one block of kBlock threads; combines the per-block partials
+// (tree reduction in LDS), then thread 0 decides
 __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
                               int at_limit, uint32_t nregistered,
                               StepCtl* sc) {
-  if (threadIdx.x || blockIdx.x) return;
-  StepRed o = part[0];
-  for (uint32_t i = 1; i < nparts; ++i) {
-    o.r = argmin_combine(o.r, part[i].r);
-    o.p = argmin_combine(o.p, part[i].p);
-    o.pnr = argmin_combine(o.pnr, part[i].pnr);
-    o.lmin_nr = part[i].lmin_nr < o.lmin_nr ? part[i].lmin_nr : o.lmin_nr;
-    o.lmin_rd = part[i].lmin_rd < o.lmin_rd ? part[i].lmin_rd : o.lmin_rd;
-    o.n_any += part[i].n_any;
-    o.n_ready += part[i].n_ready;
-    o.n_notready += part[i].n_notready;
+  __shared__ StepRed sh[kBlock];
+  StepRed acc;
+  acc.r = ArgMin{kMaxKey, kNone, 0};
+  acc.p = acc.r;
+  acc.pnr = acc.r;
+  acc.lmin_nr = kMaxKey;
+  acc.lmin_rd = kMaxKey;
+  acc.n_any = acc.n_ready = acc.n_notready = 0;
+  acc.pad = 0;
+  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+    stepred_combine(acc, part[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) stepred_combine(sh[threadIdx.x], sh[threadIdx.x + d]);
+    __syncthreads();
   }
+  if (threadIdx.x) return;
+  StepRed o = sh[0];
   StepCtl c{};
   c.type = DMC_NEXT_NONE;
   c.slot = kNone;
@@ -1237,8 +1277,8 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
   hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
                      (const uint64_t*)q->keys, (const Sel*)q->sel, k_rem, q->hist,
                      q->hmax);
-  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kBlock), 0, q->stream, q->sel, k_rem,
-                     q->hist, q->hmax);
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream, q->sel,
+                     k_rem, q->hist, q->hmax);
   pe(q);
   pb(q, S0 + 2);
   hipLaunchKernelGGL(k_count<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
@@ -1315,7 +1355,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
                      tb, now, q->red);
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, q->stream,
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
                      q->n_registered, q->sctl);
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
