@@ -58,6 +58,24 @@ struct Sel {
   uint32_t pad1;
 };
 
+// Per-pull-batch control block (device resident): the batched phases read
+// their remaining budget from it, so a whole batch runs without host round
+// trips.
+struct Ctl {
+  uint32_t k_total;    // pulls requested
+  uint32_t n_dec;      // decisions made so far
+  uint32_t overflow;   // an entry buffer was too small: later kernels no-op
+  uint32_t terminal;   // eligible work ran out before k_total
+  uint32_t ne[2];      // entries emitted by phase R / P (capacity hints)
+  uint32_t next_type;  // DMC_NEXT_* of the stopping pull
+  uint32_t pad;
+  double when;
+};
+
+__device__ inline uint32_t k_left(const Ctl* c) {
+  return c->overflow ? 0u : c->k_total - c->n_dec;
+}
+
 // Single-step (one do_next_request) reduction record.
 struct ArgMin {
   uint64_t key;
@@ -299,12 +317,24 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* lmin)
 }
 
 // ------------------------------------------------------------------ pull: scans
+__global__ void k_phase_init(Sel* sel) {
+  if (threadIdx.x || blockIdx.x) return;
+  Sel z{};
+  z.kmin = kMaxKey;
+  z.kmax = 0;
+  z.g_last = 0;
+  *sel = z;
+}
+
 // Phase R scan: key = front reservation tag, eligible iff r <= now.
 // Phase P scan: first commits the limit scan of the first priority pull
 // (:1135-1144: every front with limit <= now becomes ready), then
 // key = p + prop_delta, eligible iff ready and p < inf (:1146-1151).
+// Nothing runs once the batch is complete (no further pull took place).
 template <int PH>
-__global__ void k_scan(Table tb, double now, uint64_t* keys, Sel* sel) {
+__global__ void k_scan(Table tb, double now, uint64_t* keys, Sel* sel,
+                       const Ctl* ctl) {
+  if (k_left(ctl) == 0) return;
   uint32_t cnt = 0;
   uint64_t mn = kMaxKey, mx = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
@@ -353,8 +383,9 @@ __device__ inline uint32_t hist_shift(uint64_t range) {
 // Histogram of eligible keys over [kmin, kmax] in kHistBins integer buckets
 // of the ordered-key space (monotone in the key), with the max key per bucket.
 __global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
-                       uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
-  if (sel->n_elig <= k_rem) return;
+                       const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
+  uint32_t k_rem = k_left(ctl);
+  if (k_rem == 0 || sel->n_elig <= k_rem) return;
   __shared__ uint32_t sh[kHistBins];
   __shared__ unsigned long long smx[kHistBins];
   for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
@@ -381,17 +412,16 @@ __global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
   }
 }
 
-// Pick the threshold T: every key <= T is a candidate and at least k_rem
-// eligible fronts are <= T (T is the largest key of the bucket holding the
-// k_rem-th smallest), or take everything when there are no more than k_rem.
-// launched with kPickThreads threads; each owns kHistBins / kPickThreads
-// consecutive bins; a block-wide exclusive scan finds the bin that holds the
-// k_rem-th smallest eligible key.
+// Threshold T: every key <= T is a candidate and at least k_rem eligible
+// fronts are <= T (T is the largest key of the bin holding the k_rem-th
+// smallest), or everything when no more than k_rem are eligible.  Launched
+// with kPickThreads threads; each owns kHistBins / kPickThreads bins.
 constexpr int kPickThreads = 1024;
 constexpr int kBinsPerThread = kHistBins / kPickThreads;
 __global__ void __launch_bounds__(kPickThreads)
-k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
+k_pick(Sel* sel, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
   __shared__ uint32_t wsum[kPickThreads / 64];
+  uint32_t k_rem = k_left(ctl);
   uint32_t ne = sel->n_elig;
   int t = threadIdx.x;
   uint32_t h[kBinsPerThread];
@@ -400,7 +430,6 @@ k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
     h[j] = hist[t * kBinsPerThread + j];
     local += h[j];
   }
-  // inclusive scan of `local` across the block
   uint32_t incl = local;
   int lane = t & 63, w = t >> 6;
   for (int d = 1; d < 64; d <<= 1) {
@@ -412,8 +441,8 @@ k_pick(Sel* sel, uint32_t k_rem, uint32_t* hist, uint64_t* hmax) {
   uint32_t wbase = 0;
   for (int i = 0; i < w; ++i) wbase += wsum[i];
   uint32_t before = wbase + incl - local;  // exclusive prefix
-  if (ne == 0) {
-    if (t == 0) sel->T = 0;  // nothing eligible
+  if (k_rem == 0 || ne == 0) {
+    if (t == 0) sel->T = 0;  // nothing
   } else if (ne <= k_rem) {
     if (t == 0) sel->T = kMaxKey - 1;  // everything eligible
   } else if (before < k_rem && before + local >= k_rem) {
@@ -458,10 +487,18 @@ __global__ void k_count(Table tb, double now, const uint64_t* keys,
   }
 }
 
+template <int PH>
 __global__ void k_total(uint32_t n, const uint32_t* cnt, const uint32_t* off,
-                        Sel* sel) {
-  if (threadIdx.x == 0 && blockIdx.x == 0)
-    sel->n_entries = n ? off[n - 1] + cnt[n - 1] : 0;
+                        uint32_t cap, Sel* sel, Ctl* ctl) {
+  if (threadIdx.x || blockIdx.x) return;
+  uint32_t ne = n ? off[n - 1] + cnt[n - 1] : 0;
+  if (ctl->overflow || k_left(ctl) == 0) ne = 0;
+  sel->n_entries = ne;
+  ctl->ne[PH] = ne;
+  if (ne > cap) {
+    ctl->overflow = 1;
+    sel->n_entries = 0;
+  }
 }
 
 struct EmitVisit {
@@ -488,14 +525,24 @@ struct EmitVisit {
   }
 };
 
+// Writes the candidates' entries in slot order, and pads [n_entries, cap)
+// with maximal keys so that a fixed-size sort leaves them at the end.
 template <int PH>
-__global__ void k_emit(Table tb, double now, const Sel* sel,
-                       const uint32_t* cnt, const uint32_t* off,
+__global__ void k_emit(Table tb, double now, const Sel* sel, const Ctl* ctl,
+                       uint32_t cap, const uint32_t* cnt, const uint32_t* off,
                        uint64_t* ekey, uint32_t* eval, uint32_t* eslot,
                        uint32_t* erun) {
+  if (ctl->overflow) return;
   uint64_t T = sel->T;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
+  uint32_t ne = sel->n_entries;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = ne + tid; e < cap; e += stride) {
+    ekey[e] = kMaxKey;
+    eval[e] = e;
+  }
+  if (!ne) return;
+  for (uint32_t s = tid; s < tb.n; s += stride) {
     if (!cnt[s]) continue;
     EmitVisit v{ekey, eval, eslot, erun, off[s], s, 0, PH};
     if (PH == 0)
@@ -516,14 +563,15 @@ __device__ inline bool tie_at(const uint64_t* skey, const uint32_t* sval,
 }
 
 // R: the first k_rem sorted pops are dispatched in sorted order.
-__global__ void k_decide_r(uint32_t n, uint32_t k_rem, uint32_t n_dec,
-                           const uint64_t* skey, const uint32_t* sval,
-                           const uint32_t* eslot, uint32_t* eoff,
-                           uint8_t* etie, uint32_t* applied, Sel* sel) {
+__global__ void k_decide_r(const Ctl* ctl, const uint64_t* skey,
+                           const uint32_t* sval, const uint32_t* eslot,
+                           uint32_t* eoff, uint8_t* etie, uint32_t* applied,
+                           Sel* sel) {
+  if (ctl->overflow) return;
+  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
   uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
   if (pos == 0) {
-    uint32_t d = n < k_rem ? n : k_rem;
-    sel->n_dec_phase = d;
+    sel->n_dec_phase = n < k_rem ? n : k_rem;
     sel->terminal = 0;
     sel->g_last = kNone;
   }
@@ -538,20 +586,31 @@ __global__ void k_decide_r(uint32_t n, uint32_t k_rem, uint32_t n_dec,
   }
 }
 
-__global__ void k_group_sizes(uint32_t n, const uint32_t* sval,
-                              const uint32_t* erun, uint32_t* gsz) {
+__global__ void k_group_sizes(const Ctl* ctl, const Sel* sel, uint32_t cap,
+                              const uint32_t* sval, const uint32_t* erun,
+                              uint32_t* gsz) {
   uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pos < n) gsz[pos] = 1 + erun[sval[pos]];
+  if (pos >= cap) return;
+  gsz[pos] = (!ctl->overflow && pos < sel->n_entries) ? 1 + erun[sval[pos]] : 0;
 }
 
 // P: groups (priority pop + the reservation run it exposes) in key order;
 // decisions are the prefix of their concatenation up to k_rem.
-__global__ void k_decide_p(uint32_t n, uint32_t k_rem, uint32_t n_dec,
-                           const uint64_t* skey, const uint32_t* sval,
-                           const uint32_t* eslot, const uint32_t* gsz,
-                           const uint32_t* goff, uint32_t* eoff, uint8_t* etie,
-                           uint32_t* applied, Sel* sel) {
+__global__ void k_decide_p(const Ctl* ctl, const uint64_t* skey,
+                           const uint32_t* sval, const uint32_t* eslot,
+                           const uint32_t* gsz, const uint32_t* goff,
+                           uint32_t* eoff, uint8_t* etie, uint32_t* applied,
+                           Sel* sel) {
+  if (ctl->overflow) return;
+  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
   uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n == 0) {
+    if (pos == 0) {
+      sel->n_dec_phase = 0;
+      sel->terminal = k_rem > 0 ? 1 : 0;
+    }
+    return;
+  }
   if (pos >= n) return;
   uint32_t e = sval[pos];
   uint32_t o = goff[pos];
@@ -566,7 +625,7 @@ __global__ void k_decide_p(uint32_t n, uint32_t k_rem, uint32_t n_dec,
     uint32_t na = gsz[pos];
     if (na > k_rem - o) na = k_rem - o;
     atomicAdd(&applied[eslot[e]], na);
-    atomicMax(&sel->g_last, n_dec + o);  // g_last initialised to 0 by host
+    atomicMax(&sel->g_last, n_dec + o);  // g_last starts at 0
   } else {
     eoff[e] = kNone;
   }
@@ -621,10 +680,11 @@ struct ApplyVisit {
 // limit <= now).
 template <int PH>
 __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
-                        const uint32_t* cnt, const uint32_t* off,
-                        const uint32_t* eoff, const uint8_t* etie,
-                        uint32_t* applied, dmc_decision* out,
-                        unsigned long long* sched) {
+                        const Ctl* ctl, const uint32_t* cnt,
+                        const uint32_t* off, const uint32_t* eoff,
+                        const uint8_t* etie, uint32_t* applied,
+                        dmc_decision* out, unsigned long long* sched) {
+  if (ctl->overflow || sel->n_entries == 0) return;
   uint32_t g_last = sel->g_last;
   uint32_t terminal = sel->terminal;
   uint64_t T = sel->T;
@@ -707,10 +767,36 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
   }
 }
 
+__global__ void k_ctl_init(Ctl* ctl, uint32_t k_total) {
+  if (threadIdx.x || blockIdx.x) return;
+  Ctl c{};
+  c.k_total = k_total;
+  c.next_type = DMC_NEXT_RETURNING;
+  *ctl = c;
+}
+
+__global__ void k_red_init(StepRed* red) {
+  if (threadIdx.x || blockIdx.x) return;
+  StepRed z{};
+  z.r.key = kMaxKey;
+  z.lmin_nr = kMaxKey;
+  z.lmin_rd = kMaxKey;
+  *red = z;
+}
+
+template <int PH>
+__global__ void k_phase_end(const Sel* sel, Ctl* ctl) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (ctl->overflow || k_left(ctl) == 0) return;
+  ctl->n_dec += sel->n_entries ? sel->n_dec_phase : 0;
+  if (PH == 1 && ctl->n_dec < ctl->k_total) ctl->terminal = 1;
+}
+
 // ------------------------------------------------------------------ future
 // Terminal pull of a Wait/Reject batch: min_not_0 over the reservation-heap
 // top and the limit-heap top (:1170-1185).
-__global__ void k_future_scan(Table tb, StepRed* red) {
+__global__ void k_future_scan(Table tb, StepRed* red, const Ctl* ctl) {
+  if (ctl && (ctl->overflow || !ctl->terminal)) return;
   uint64_t rmin = kMaxKey, lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nnr = 0, nrd = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
@@ -748,8 +834,9 @@ __device__ inline double min_not_0(double cur, double possible) {
   return possible == 0.0 ? cur : (possible < cur ? possible : cur);
 }
 
-__global__ void k_future_final(const StepRed* red, StepCtl* sc) {
+__global__ void k_future_final(const StepRed* red, StepCtl* sc, Ctl* ctl) {
   if (threadIdx.x || blockIdx.x) return;
+  if (ctl && (ctl->overflow || !ctl->terminal)) return;
   const double tmax = 1.7976931348623157e308;
   double next = tmax;
   if (red->n_any) {
@@ -763,6 +850,10 @@ __global__ void k_future_final(const StepRed* red, StepCtl* sc) {
   } else {
     sc->type = DMC_NEXT_NONE;
     sc->when = 0.0;
+  }
+  if (ctl) {
+    ctl->next_type = sc->type;
+    ctl->when = sc->when;
   }
 }
 
@@ -1068,6 +1159,8 @@ struct dmc_queue {
   size_t temp_bytes = 0;
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
+  Ctl* ctl = nullptr;
+  uint32_t cap_hint[2] = {4096, 4096};  // entry capacity per phase (adaptive)
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
   struct ProfRec {
     hipEvent_t a, b;
@@ -1252,33 +1345,32 @@ int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
 }
 
 // --------------------------------------------------------------- pull phases
-struct PhaseOut {
-  uint32_t n_dec;
-  uint32_t terminal;
-};
+uint32_t pow2_at_least(uint32_t x) {
+  uint32_t p = 4096;
+  while (p < x && p < (1u << 31)) p <<= 1;
+  return p;
+}
 
+// Enqueue one batched phase; no host synchronisation.  `cap` is the entry
+// capacity the sort runs over (entries beyond it set ctl->overflow and the
+// rest of the batch no-ops; the host retries with a larger capacity).
 template <int PH>
-int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
-              dmc_decision* d_out, PhaseOut* po) {
+int launch_phase(dmc_queue* q, double now, uint32_t cap, dmc_decision* d_out) {
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = grid_for(N, 2048);
   const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
-  Sel init{};
-  init.kmin = kMaxKey;
-  init.kmax = 0;
-  init.g_last = 0;
-  HIP_OK(hipMemcpyAsync(q->sel, &init, sizeof(Sel), hipMemcpyHostToDevice, q->stream));
+  hipLaunchKernelGGL(k_phase_init, dim3(1), dim3(64), 0, q->stream, q->sel);
   pb(q, S0 + 0);
   hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     q->keys, q->sel);
+                     q->keys, q->sel, (const Ctl*)q->ctl);
   pe(q);
   pb(q, S0 + 1);
   hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
-                     (const uint64_t*)q->keys, (const Sel*)q->sel, k_rem, q->hist,
-                     q->hmax);
+                     (const uint64_t*)q->keys, (const Sel*)q->sel,
+                     (const Ctl*)q->ctl, q->hist, q->hmax);
   hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream, q->sel,
-                     k_rem, q->hist, q->hmax);
+                     (const Ctl*)q->ctl, q->hist, q->hmax);
   pe(q);
   pb(q, S0 + 2);
   hipLaunchKernelGGL(k_count<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
@@ -1288,47 +1380,38 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
   size_t tbytes = q->temp_bytes;
   HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->cnt, q->off, (int)N,
                                           q->stream));
-  hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, q->stream, N,
-                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, q->sel);
+  hipLaunchKernelGGL(k_total<PH>, dim3(1), dim3(64), 0, q->stream, N,
+                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, cap, q->sel,
+                     q->ctl);
   pe(q);
-  Sel hs;
-  HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));
-  uint32_t ne = hs.n_entries;
-  po->n_dec = 0;
-  po->terminal = (PH == 1) ? 1 : 0;
-  if (ne == 0) {
-    pflush(q);
-    return DMC_OK;
-  }
-  int rc = ensure_entries(q, ne);
-  if (rc) return rc;
   pb(q, S0 + 4);
   hipLaunchKernelGGL(k_emit<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     (const Sel*)q->sel, (const uint32_t*)q->cnt,
-                     (const uint32_t*)q->off, q->ekey, q->eval, q->eslot, q->erun);
+                     (const Sel*)q->sel, (const Ctl*)q->ctl, cap,
+                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, q->ekey,
+                     q->eval, q->eslot, q->erun);
   pe(q);
   pb(q, S0 + 5);
   tbytes = q->temp_bytes;
   HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ekey, q->skey,
-                                            q->eval, q->sval, (int)ne, 0, 64,
+                                            q->eval, q->sval, (int)cap, 0, 64,
                                             q->stream));
   pe(q);
-  uint32_t ge = (ne + kBlock - 1) / kBlock;
+  uint32_t ge = (cap + kBlock - 1) / kBlock;
   pb(q, S0 + 6);
   if (PH == 0) {
-    hipLaunchKernelGGL(k_decide_r, dim3(ge), dim3(kBlock), 0, q->stream, ne,
-                       k_rem, n_dec, (const uint64_t*)q->skey,
+    hipLaunchKernelGGL(k_decide_r, dim3(ge), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const uint64_t*)q->skey,
                        (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
                        q->eoff, q->etie, q->applied, q->sel);
   } else {
-    hipLaunchKernelGGL(k_group_sizes, dim3(ge), dim3(kBlock), 0, q->stream, ne,
+    hipLaunchKernelGGL(k_group_sizes, dim3(ge), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const Sel*)q->sel, cap,
                        (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
     tbytes = q->temp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
-                                            (int)ne, q->stream));
-    hipLaunchKernelGGL(k_decide_p, dim3(ge), dim3(kBlock), 0, q->stream, ne,
-                       k_rem, n_dec, (const uint64_t*)q->skey,
+                                            (int)cap, q->stream));
+    hipLaunchKernelGGL(k_decide_p, dim3(ge), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const uint64_t*)q->skey,
                        (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
                        (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
                        q->etie, q->applied, q->sel);
@@ -1336,15 +1419,25 @@ int run_phase(dmc_queue* q, double now, uint32_t k_rem, uint32_t n_dec,
   pe(q);
   pb(q, S0 + 7);
   hipLaunchKernelGGL(k_apply<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     q->tick, (const Sel*)q->sel, (const uint32_t*)q->cnt,
-                     (const uint32_t*)q->off, (const uint32_t*)q->eoff,
-                     (const uint8_t*)q->etie, q->applied, d_out, q->sched);
+                     q->tick, (const Sel*)q->sel, (const Ctl*)q->ctl,
+                     (const uint32_t*)q->cnt, (const uint32_t*)q->off,
+                     (const uint32_t*)q->eoff, (const uint8_t*)q->etie,
+                     q->applied, d_out, q->sched);
   pe(q);
-  HIP_OK(hipMemcpyAsync(&hs, q->sel, sizeof(Sel), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));
-  pflush(q);
-  po->n_dec = hs.n_dec_phase;
-  po->terminal = (PH == 1) ? hs.terminal : 0;
+  hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
+                     (const Sel*)q->sel, q->ctl);
+  return DMC_OK;
+}
+
+// Terminal pull of a Wait/Reject batch (no-op unless ctl->terminal).
+int launch_future(dmc_queue* q, Ctl* ctl) {
+  hipLaunchKernelGGL(k_red_init, dim3(1), dim3(64), 0, q->stream, q->red);
+  pb(q, DMC_PROF_FUTURE);
+  hipLaunchKernelGGL(k_future_scan, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock), 0,
+                     q->stream, q->tb, q->red, (const Ctl*)ctl);
+  hipLaunchKernelGGL(k_future_final, dim3(1), dim3(64), 0, q->stream,
+                     (const StepRed*)q->red, q->sctl, ctl);
+  pe(q);
   return DMC_OK;
 }
 
@@ -1372,27 +1465,10 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   return DMC_OK;
 }
 
-int future_of(dmc_queue* q, int* type, double* when) {
-  StepRed init{};
-  init.r.key = kMaxKey;
-  init.lmin_nr = kMaxKey;
-  init.lmin_rd = kMaxKey;
-  HIP_OK(hipMemcpyAsync(q->red, &init, sizeof(init), hipMemcpyHostToDevice, q->stream));
-  pb(q, DMC_PROF_FUTURE);
-  hipLaunchKernelGGL(k_future_scan, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock), 0,
-                     q->stream, q->tb, q->red);
-  hipLaunchKernelGGL(k_future_final, dim3(1), dim3(64), 0, q->stream,
-                     (const StepRed*)q->red, q->sctl);
-  pe(q);
-  StepCtl sc;
-  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));
-  pflush(q);
-  *type = sc.type;
-  *when = sc.when;
-  return DMC_OK;
-}
-
+// k successive pull_request(now).  Batched phases run with one host
+// synchronisation per round; a round ends the batch unless an entry buffer
+// overflowed (retry with more capacity) or, with AtLimit::Allow, the eligible
+// work ran out (one general limit-break step, then another round).
 int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
               dmc_pull_result* res) {
   dmc_pull_result r{};
@@ -1404,7 +1480,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       r.next_type = DMC_NEXT_NONE;
       break;
     }
-    if (k - n_dec <= q->small_k) {
+    uint32_t kk = k - n_dec;
+    if (kk <= q->small_k) {
       int type;
       double when;
       int rc = step_once(q, now, d_out, n_dec, &type, &when);
@@ -1417,17 +1494,34 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       ++n_dec;
       continue;
     }
-    PhaseOut po;
-    int rc = run_phase<0>(q, now, k - n_dec, n_dec, d_out, &po);
+    uint32_t cap[2];
+    for (int ph = 0; ph < 2; ++ph) {
+      cap[ph] = std::max(q->cap_hint[ph], pow2_at_least(std::min(kk, 1u << 16)));
+      int rc = ensure_entries(q, cap[ph]);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk);
+    int rc = launch_phase<0>(q, now, cap[0], d_out + n_dec);
     if (rc) return rc;
-    n_dec += po.n_dec;
-    if (n_dec >= k) break;
-    rc = run_phase<1>(q, now, k - n_dec, n_dec, d_out, &po);
+    rc = launch_phase<1>(q, now, cap[1], d_out + n_dec);
     if (rc) return rc;
-    n_dec += po.n_dec;
-    if (n_dec >= k) break;
-    // every normally eligible request is dispatched; the next pull is the
-    // terminal one (or an Allow limit break)
+    if (!allow) {
+      rc = launch_future(q, q->ctl);
+      if (rc) return rc;
+    }
+    Ctl c;
+    HIP_OK(hipMemcpyAsync(&c, q->ctl, sizeof(c), hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    pflush(q);
+    n_dec += c.n_dec;
+    for (int ph = 0; ph < 2; ++ph) {
+      uint32_t want = pow2_at_least(c.ne[ph] + (c.ne[ph] >> 2) + 1);
+      // grow at once, shrink slowly
+      q->cap_hint[ph] = want > q->cap_hint[ph] ? want
+                        : std::max(want, q->cap_hint[ph] / 2);
+    }
+    if (c.overflow) continue;  // state before the overflowing phase is intact
+    if (n_dec >= k || !c.terminal) break;
     if (allow) {
       int type;
       double when;
@@ -1441,12 +1535,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       ++n_dec;
       continue;
     }
-    int type;
-    double when;
-    rc = future_of(q, &type, &when);
-    if (rc) return rc;
-    r.next_type = type;
-    r.when = when;
+    r.next_type = c.next_type;
+    r.when = c.when;
     break;
   }
   r.n_decisions = n_dec;
@@ -1519,6 +1609,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
+  rc |= A(&q->ctl, 1);
   rc |= A(&q->act_min, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
@@ -1555,7 +1646,7 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->ekey,
                   q->skey, q->eval, q->sval, q->eslot, q->erun, q->eoff, q->gsz,
                   q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
-                  q->skeys, q->svals, q->d_dec, q->temp};
+                  q->skeys, q->svals, q->d_dec, q->temp, q->ctl};
   for (void* p : ptrs)
     dfree(p);
   for (auto& r : q->prof_pool) {
