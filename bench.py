@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--pulls", type=int, default=None,
                     help="decisions per step (default: = --batch)")
     ap.add_argument("--depth", type=int, default=4)
+    ap.add_argument("--settle", type=int, default=None,
+                    help="pulls at the pre-population's end time before the "
+                         "steps (default: depth/2 per client), which drain "
+                         "the reservation backlog so that steps run in "
+                         "steady state with both phases")
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -93,6 +98,27 @@ def make_workload(args, seed):
     return tab, pre, steps
 
 
+def prepare(q, args, tab, pre):
+    """Same setup on either engine: bulk registration, pre-population,
+    settle pulls."""
+    q.register_active(tab.slots, tab.r, tab.w, tab.l)
+    chunk = 1 << 20
+    for i in range(0, len(pre), chunk):
+        rc = q.add_batch(pre[i:i + chunk])
+        assert (rc == 0).all(), np.unique(rc)
+    settle = args.settle if args.settle is not None else \
+        args.depth * args.clients // 2
+    t_pre = float(pre["time"][-1])
+    done = 0
+    while done < settle:
+        k = min(settle - done, 1 << 20)
+        d, res = q.pull_batch(t_pre, k)
+        done += k
+        if res.n_decisions < k:
+            break
+    return settle
+
+
 def cpu_baseline(args, tab, pre, steps):
     """The oracle (CPU restatement of the reference queue, one core) on a
     bounded sample of the same workload: same 1M clients and pre-population,
@@ -100,10 +126,7 @@ def cpu_baseline(args, tab, pre, steps):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     q = pyoracle.OracleQueue(track_ties=False)
-    q.register_active(tab.slots, tab.r, tab.w, tab.l)
-    chunk = 1 << 20
-    for i in range(0, len(pre), chunk):
-        q.add_batch(pre[i:i + chunk])
+    prepare(q, args, tab, pre)
     k = args.pulls or args.batch
     ops = 0
     t0 = time.perf_counter()
@@ -114,8 +137,8 @@ def cpu_baseline(args, tab, pre, steps):
     dt = time.perf_counter() - t0
     return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
             "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
-                       f"{args.clients} clients pre-populated with "
-                       f"{len(pre)} requests, {args.cpu_steps} steps of "
+                       f"the same {args.clients}-client queue after the same "
+                       f"pre-population and settle, {args.cpu_steps} steps of "
                        f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
 
 
@@ -137,11 +160,7 @@ def main():
     k = args.pulls or args.batch
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
                  max_batch=max(args.batch, k, 1 << 20), device=local)
-    q.register_active(tab.slots, tab.r, tab.w, tab.l)
-    chunk = 1 << 20
-    for i in range(0, len(pre), chunk):
-        rc = q.add_batch(pre[i:i + chunk])
-        assert (rc == 0).all(), np.unique(rc)
+    settle = prepare(q, args, tab, pre)
 
     dev = torch.device("cuda", local)
     d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r in steps]
@@ -160,6 +179,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    st_t0 = q.stats()
     if not args.no_profile:
         q.profile(True)
         q.profile_reset()
@@ -250,12 +270,14 @@ def main():
                                "per step",
                    "clients": args.clients, "adds_per_step": args.batch,
                    "pulls_per_step": k, "prepopulated": len(pre),
+                   "settle_pulls": settle,
                    "ring_capacity": args.ring,
                    "parallelism": f"{world} independent server queue(s)"},
         "decisions_per_s": round(n_dec / dt, 1),
         "tag_updates_per_s": round(n_adds / dt, 1),
-        "reservation_decisions": int(st.reserv_sched_count),
-        "priority_decisions": int(st.prop_sched_count),
+        "reservation_decisions": int(st.reserv_sched_count - st_t0.reserv_sched_count),
+        "priority_decisions": int(st.prop_sched_count - st_t0.prop_sched_count),
+        "queued_after": int(st.requests),
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms_per_step": {n: round(ms / max(args.steps, 1), 4)

@@ -55,7 +55,7 @@ struct Sel {
   uint32_t g_last;      // last priority (limit-scan) pull index, kNone if none
   uint32_t terminal;    // 1 if this phase ended the batch early
   uint32_t ties;
-  uint32_t pad1;
+  uint32_t n_prio_groups; // priority pops applied by phase P
 };
 
 // Per-pull-batch control block (device resident): the batched phases read
@@ -70,6 +70,11 @@ struct Ctl {
   uint32_t next_type;  // DMC_NEXT_* of the stopping pull
   uint32_t pad;
   double when;
+};
+
+struct ScanPart {
+  uint32_t cnt, pad;
+  uint64_t mn, mx;
 };
 
 __device__ inline uint32_t k_left(const Ctl* c) {
@@ -289,7 +294,7 @@ __global__ void k_add_chain(Table tb, const uint32_t* sslot,
 
 // idle reset, :937-985: L = min over non-idle clients of
 // (has_request ? front.p : prev.p) + prop_delta
-__global__ void k_contrib_min(Table tb, uint64_t* out) {
+__global__ void k_contrib_min(Table tb, uint64_t* parts) {
   uint64_t m = kMaxKey;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
@@ -301,11 +306,30 @@ __global__ void k_contrib_min(Table tb, uint64_t* out) {
     }
   }
   m = wave_min_u64(m);
-  if ((threadIdx.x & 63) == 0) atomicMin((unsigned long long*)out, (unsigned long long)m);
+  __shared__ uint64_t sh[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) m = sh[i] < m ? sh[i] : m;
+    parts[blockIdx.x] = m;
+  }
 }
 
-__global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* lmin) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts,
+                           uint32_t nparts) {
+  __shared__ uint64_t sh[kBlock];
+  uint64_t m = kMaxKey;
+  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+    m = parts[i] < m ? parts[i] : m;
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d && sh[threadIdx.x + d] < sh[threadIdx.x])
+      sh[threadIdx.x] = sh[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x) return;
+  const uint64_t* lmin = &sh[0];
   constexpr double trigger = 1.7976931348623157e308 / 3.0;  // DBL_MAX / 3, :957
   double lowest = 1.7976931348623157e308;                    // DBL_MAX, :960
   if (*lmin != kMaxKey) {
@@ -332,7 +356,7 @@ __global__ void k_phase_init(Sel* sel) {
 // key = p + prop_delta, eligible iff ready and p < inf (:1146-1151).
 // Nothing runs once the batch is complete (no further pull took place).
 template <int PH>
-__global__ void k_scan(Table tb, double now, uint64_t* keys, Sel* sel,
+__global__ void k_scan(Table tb, double now, uint64_t* keys, ScanPart* parts,
                        const Ctl* ctl) {
   if (k_left(ctl) == 0) return;
   uint32_t cnt = 0;
@@ -363,13 +387,54 @@ __global__ void k_scan(Table tb, double now, uint64_t* keys, Sel* sel,
       mx = k > mx ? k : mx;
     }
   }
+  // per-block partial (no same-address atomics: thousands of waves hitting
+  // one word serialise at the memory side); k_scan_final combines them
   cnt = wave_sum_u32(cnt);
   mn = wave_min_u64(mn);
   mx = wave_max_u64(mx);
-  if ((threadIdx.x & 63) == 0 && cnt) {
-    atomicAdd(&sel->n_elig, cnt);
-    atomicMin((unsigned long long*)&sel->kmin, (unsigned long long)mn);
-    atomicMax((unsigned long long*)&sel->kmax, (unsigned long long)mx);
+  __shared__ ScanPart sh[kBlock / 64];
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = ScanPart{cnt, 0, mn, mx};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ScanPart o = sh[0];
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) {
+      o.cnt += sh[i].cnt;
+      o.mn = sh[i].mn < o.mn ? sh[i].mn : o.mn;
+      o.mx = sh[i].mx > o.mx ? sh[i].mx : o.mx;
+    }
+    parts[blockIdx.x] = o;
+  }
+}
+
+// combines the scan's per-block partials into the phase's Sel
+__global__ void k_scan_final(const ScanPart* parts, uint32_t nparts, Sel* sel,
+                             const Ctl* ctl) {
+  __shared__ ScanPart sh[kBlock];
+  ScanPart o{0, 0, kMaxKey, 0};
+  if (k_left(ctl))
+    for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+      ScanPart b = parts[i];
+      o.cnt += b.cnt;
+      o.mn = b.mn < o.mn ? b.mn : o.mn;
+      o.mx = b.mx > o.mx ? b.mx : o.mx;
+    }
+  sh[threadIdx.x] = o;
+  __syncthreads();
+  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) {
+      ScanPart& a = sh[threadIdx.x];
+      const ScanPart& b = sh[threadIdx.x + d];
+      a.cnt += b.cnt;
+      a.mn = b.mn < a.mn ? b.mn : a.mn;
+      a.mx = b.mx > a.mx ? b.mx : a.mx;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sel->n_elig = sh[0].cnt;
+    sel->kmin = sh[0].mn;
+    sel->kmax = sh[0].mx;
   }
 }
 
@@ -625,7 +690,12 @@ __global__ void k_decide_p(const Ctl* ctl, const uint64_t* skey,
     uint32_t na = gsz[pos];
     if (na > k_rem - o) na = k_rem - o;
     atomicAdd(&applied[eslot[e]], na);
-    atomicMax(&sel->g_last, n_dec + o);  // g_last starts at 0
+    if (pos == n - 1 || goff[pos + 1] >= k_rem) {
+      // the last applied group: its priority pop is this phase's last
+      // limit-scanning pull
+      sel->g_last = n_dec + o;
+      sel->n_prio_groups = pos + 1;
+    }
   } else {
     eoff[e] = kNone;
   }
@@ -759,12 +829,9 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
     }
     tb.flags[s] = f;
   }
-  nres = wave_sum_u32(nres);
-  nprio = wave_sum_u32(nprio);
-  if ((threadIdx.x & 63) == 0) {
-    if (nres) atomicAdd(&sched[0], (unsigned long long)nres);
-    if (nprio) atomicAdd(&sched[1], (unsigned long long)nprio);
-  }
+  (void)nres;
+  (void)nprio;
+  (void)sched;  // counted once per phase in k_phase_end
 }
 
 __global__ void k_ctl_init(Ctl* ctl, uint32_t k_total) {
@@ -775,93 +842,34 @@ __global__ void k_ctl_init(Ctl* ctl, uint32_t k_total) {
   *ctl = c;
 }
 
-__global__ void k_red_init(StepRed* red) {
-  if (threadIdx.x || blockIdx.x) return;
-  StepRed z{};
-  z.r.key = kMaxKey;
-  z.lmin_nr = kMaxKey;
-  z.lmin_rd = kMaxKey;
-  *red = z;
-}
-
+// the phase's decisions are counted once here (sched[0] reservation,
+// sched[1] priority: one per applied group), :1469,1479
 template <int PH>
-__global__ void k_phase_end(const Sel* sel, Ctl* ctl) {
+__global__ void k_phase_end(const Sel* sel, Ctl* ctl,
+                            unsigned long long* sched) {
   if (threadIdx.x || blockIdx.x) return;
   if (ctl->overflow || k_left(ctl) == 0) return;
-  ctl->n_dec += sel->n_entries ? sel->n_dec_phase : 0;
+  uint32_t d = sel->n_entries ? sel->n_dec_phase : 0;
+  uint32_t np = PH == 1 && sel->n_entries ? sel->n_prio_groups : 0;
+  ctl->n_dec += d;
+  sched[0] += d - np;
+  sched[1] += np;
   if (PH == 1 && ctl->n_dec < ctl->k_total) ctl->terminal = 1;
 }
 
 // ------------------------------------------------------------------ future
-// Terminal pull of a Wait/Reject batch: min_not_0 over the reservation-heap
-// top and the limit-heap top (:1170-1185).
-__global__ void k_future_scan(Table tb, StepRed* red, const Ctl* ctl) {
-  if (ctl && (ctl->overflow || !ctl->terminal)) return;
-  uint64_t rmin = kMaxKey, lnr = kMaxKey, lrd = kMaxKey;
-  uint32_t nany = 0, nnr = 0, nrd = 0;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    if (!tb.count[s]) continue;
-    ++nany;
-    uint64_t kr = okey(tb.front_r[s]);
-    rmin = kr < rmin ? kr : rmin;
-    uint64_t kl = okey(tb.front_l[s]);
-    if (tb.flags[s] & F_READY) {
-      ++nrd;
-      lrd = kl < lrd ? kl : lrd;
-    } else {
-      ++nnr;
-      lnr = kl < lnr ? kl : lnr;
-    }
-  }
-  rmin = wave_min_u64(rmin);
-  lnr = wave_min_u64(lnr);
-  lrd = wave_min_u64(lrd);
-  nany = wave_sum_u32(nany);
-  nnr = wave_sum_u32(nnr);
-  nrd = wave_sum_u32(nrd);
-  if ((threadIdx.x & 63) == 0 && nany) {
-    atomicMin((unsigned long long*)&red->r.key, (unsigned long long)rmin);
-    atomicMin((unsigned long long*)&red->lmin_nr, (unsigned long long)lnr);
-    atomicMin((unsigned long long*)&red->lmin_rd, (unsigned long long)lrd);
-    atomicAdd(&red->n_any, nany);
-    atomicAdd(&red->n_notready, nnr);
-    atomicAdd(&red->n_ready, nrd);
-  }
-}
-
-__device__ inline double min_not_0(double cur, double possible) {
+__device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
   return possible == 0.0 ? cur : (possible < cur ? possible : cur);
-}
-
-__global__ void k_future_final(const StepRed* red, StepCtl* sc, Ctl* ctl) {
-  if (threadIdx.x || blockIdx.x) return;
-  if (ctl && (ctl->overflow || !ctl->terminal)) return;
-  const double tmax = 1.7976931348623157e308;
-  double next = tmax;
-  if (red->n_any) {
-    next = min_not_0(next, from_okey(red->r.key));
-    double lt = red->n_notready ? from_okey(red->lmin_nr) : from_okey(red->lmin_rd);
-    next = min_not_0(next, lt);
-  }
-  if (next < tmax) {
-    sc->type = DMC_NEXT_FUTURE;
-    sc->when = next;
-  } else {
-    sc->type = DMC_NEXT_NONE;
-    sc->when = 0.0;
-  }
-  if (ctl) {
-    ctl->next_type = sc->type;
-    ctl->when = sc->when;
-  }
 }
 
 // ------------------------------------------------------------------ single step
 // General do_next_request(now) one pull at a time (used for small k and for
 // AtLimit::Allow limit breaks, :1157-1165).  Reductions are per block, then
 // one block combines them.
-__global__ void k_step_scan(Table tb, double now, StepRed* part) {
+__global__ void k_step_scan(Table tb, double now, StepRed* part,
+                            const Ctl* ctl) {
+  // as the terminal pull of a batch: only if the batch ran out of work
+  if (ctl && (ctl->overflow || !ctl->terminal)) return;
   ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
   uint64_t lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nrd = 0, nnr = 0;
@@ -938,7 +946,8 @@ __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
 // (tree reduction in LDS), then thread 0 decides
 __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
                               int at_limit, uint32_t nregistered,
-                              StepCtl* sc) {
+                              StepCtl* sc, Ctl* ctl) {
+  if (ctl && (ctl->overflow || !ctl->terminal)) return;
   __shared__ StepRed sh[kBlock];
   StepRed acc;
   acc.r = ArgMin{kMaxKey, kNone, 0};
@@ -963,6 +972,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
   c.slot = kNone;
   if (nregistered == 0) {  // resv_heap.empty(), :1118-1120
     *sc = c;
+    if (ctl) {
+      ctl->next_type = c.type;
+      ctl->when = c.when;
+    }
     return;
   }
   double rtop = o.n_any ? from_okey(o.r.key) : kInf;
@@ -972,6 +985,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
     c.slot = o.r.slot;
     c.tie = o.r.cnt > 1;
     *sc = c;
+    if (ctl) {
+      ctl->next_type = c.type;
+      ctl->when = c.when;
+    }
     return;
   }
   c.mark = 1;  // the limit scan ran
@@ -981,6 +998,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
     c.slot = o.p.slot;
     c.tie = o.p.cnt > 1;
     *sc = c;
+    if (ctl) {
+      ctl->next_type = c.type;
+      ctl->when = c.when;
+    }
     return;
   }
   if (at_limit == DMC_AT_LIMIT_ALLOW && o.n_any) {  // :1157-1165
@@ -994,6 +1015,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
       c.slot = o.pnr.slot;
       c.tie = o.pnr.cnt > 1;
       *sc = c;
+      if (ctl) {
+        ctl->next_type = c.type;
+        ctl->when = c.when;
+      }
       return;
     }
     if (rtop < kInf) {
@@ -1002,6 +1027,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
       c.slot = o.r.slot;
       c.tie = o.r.cnt > 1;
       *sc = c;
+      if (ctl) {
+        ctl->next_type = c.type;
+        ctl->when = c.when;
+      }
       return;
     }
   }
@@ -1017,6 +1046,10 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
     c.when = next;
   }
   *sc = c;
+  if (ctl) {
+    ctl->next_type = c.type;
+    ctl->when = c.when;
+  }
 }
 
 __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
@@ -1106,7 +1139,13 @@ __global__ void k_count_requests(Table tb, unsigned long long* out) {
        s += gridDim.x * blockDim.x)
     t += tb.count[s];
   for (int d = 32; d > 0; d >>= 1) t += shfl_down_u64(t, d);
-  if ((threadIdx.x & 63) == 0 && t) atomicAdd(out, t);
+  __shared__ unsigned long long sh[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) t += sh[i];
+    if (t) atomicAdd(out, t);
+  }
 }
 
 uint32_t grid_for(uint32_t n, uint32_t cap = 4096) {
@@ -1160,6 +1199,7 @@ struct dmc_queue {
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   Ctl* ctl = nullptr;
+  ScanPart* parts = nullptr;  // per-block scan partials
   uint32_t cap_hint[2] = {4096, 4096};  // entry capacity per phase (adaptive)
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
   struct ProfRec {
@@ -1312,11 +1352,11 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
 
 int activate(dmc_queue* q, uint32_t slot, double t) {
   pb(q, DMC_PROF_ACTIVATE);
-  HIP_OK(hipMemsetAsync(q->act_min, 0xff, sizeof(uint64_t), q->stream));
-  hipLaunchKernelGGL(k_contrib_min, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock),
-                     0, q->stream, q->tb, q->act_min);
-  hipLaunchKernelGGL(k_activate, dim3(1), dim3(64), 0, q->stream, q->tb, slot,
-                     t, (const uint64_t*)q->act_min);
+  uint32_t g = grid_for(q->tb.n, 2048);
+  hipLaunchKernelGGL(k_contrib_min, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     (uint64_t*)q->parts);
+  hipLaunchKernelGGL(k_activate, dim3(1), dim3(kBlock), 0, q->stream, q->tb, slot,
+                     t, (const uint64_t*)q->parts, g);
   pe(q);
   return DMC_OK;
 }
@@ -1363,7 +1403,9 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap, dmc_decision* d_out) {
   hipLaunchKernelGGL(k_phase_init, dim3(1), dim3(64), 0, q->stream, q->sel);
   pb(q, S0 + 0);
   hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     q->keys, q->sel, (const Ctl*)q->ctl);
+                     q->keys, q->parts, (const Ctl*)q->ctl);
+  hipLaunchKernelGGL(k_scan_final, dim3(1), dim3(kBlock), 0, q->stream,
+                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl);
   pe(q);
   pb(q, S0 + 1);
   hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
@@ -1425,18 +1467,20 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap, dmc_decision* d_out) {
                      q->applied, d_out, q->sched);
   pe(q);
   hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
-                     (const Sel*)q->sel, q->ctl);
+                     (const Sel*)q->sel, q->ctl, q->sched);
   return DMC_OK;
 }
 
-// Terminal pull of a Wait/Reject batch (no-op unless ctl->terminal).
-int launch_future(dmc_queue* q, Ctl* ctl) {
-  hipLaunchKernelGGL(k_red_init, dim3(1), dim3(64), 0, q->stream, q->red);
+// Terminal pull of a Wait/Reject batch: one general do_next_request, which
+// (nothing being eligible) computes min_not_0 over the reservation- and
+// limit-heap tops, :1170-1185.  No-op unless ctl->terminal.
+int launch_future(dmc_queue* q, double now, Ctl* ctl) {
   pb(q, DMC_PROF_FUTURE);
-  hipLaunchKernelGGL(k_future_scan, dim3(grid_for(q->tb.n, 2048)), dim3(kBlock), 0,
-                     q->stream, q->tb, q->red, (const Ctl*)ctl);
-  hipLaunchKernelGGL(k_future_final, dim3(1), dim3(64), 0, q->stream,
-                     (const StepRed*)q->red, q->sctl, ctl);
+  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
+                     q->tb, now, q->red, (const Ctl*)ctl);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
+                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
+                     q->n_registered, q->sctl, ctl);
   pe(q);
   return DMC_OK;
 }
@@ -1447,10 +1491,10 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   const Table& tb = q->tb;
   pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     tb, now, q->red);
+                     tb, now, q->red, (const Ctl*)nullptr);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl);
+                     q->n_registered, q->sctl, (Ctl*)nullptr);
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
                      q->stream, tb, now, (const StepCtl*)q->sctl);
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
@@ -1506,7 +1550,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     rc = launch_phase<1>(q, now, cap[1], d_out + n_dec);
     if (rc) return rc;
     if (!allow) {
-      rc = launch_future(q, q->ctl);
+      rc = launch_future(q, now, q->ctl);
       if (rc) return rc;
     }
     Ctl c;
@@ -1610,6 +1654,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
   rc |= A(&q->ctl, 1);
+  rc |= A(&q->parts, 4096);
   rc |= A(&q->act_min, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
@@ -1646,7 +1691,8 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->ekey,
                   q->skey, q->eval, q->sval, q->eslot, q->erun, q->eoff, q->gsz,
                   q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
-                  q->skeys, q->svals, q->d_dec, q->temp, q->ctl};
+                  q->skeys, q->svals, q->d_dec, q->temp, q->ctl,
+                  q->parts};
   for (void* p : ptrs)
     dfree(p);
   for (auto& r : q->prof_pool) {

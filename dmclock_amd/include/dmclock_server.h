@@ -506,12 +506,10 @@ class PullPriorityQueue : public PriorityQueueBase<C, R, IsDelayed, U1, B> {
                   const ReqParams& req_params, const Time time,
                   const Cost cost = 1u) {
     std::lock_guard<std::mutex> g(this->data_mtx);
-    RequestRef held = std::move(request);
-    R* raw = held.get();
-    int rc = this->do_add_request(std::move(held), client_id, req_params, time,
-                                  cost);
-    if (rc != DMC_OK) request.reset(raw);  // hand ownership back
-    return rc;
+    // do_add_request moves from `request` only on success, so on EAGAIN the
+    // caller keeps ownership (test_dmclock_server.cc:1329-1335)
+    return this->do_add_request(std::move(request), client_id, req_params,
+                                time, cost);
   }
 
   inline PullReq pull_request() { return pull_request(get_time()); }
@@ -637,14 +635,9 @@ class PushPriorityQueue : public PriorityQueueBase<C, R, IsDelayed, U1, B> {
                   const ReqParams& req_params, const Time time,
                   const Cost cost = 1u) {  // :1627-1648
     std::lock_guard<std::mutex> g(this->data_mtx);
-    RequestRef held = std::move(request);
-    R* raw = held.get();
-    int rc = this->do_add_request(std::move(held), client_id, req_params, time,
-                                  cost);
-    if (rc != DMC_OK) {
-      request.reset(raw);
-      return rc;
-    }
+    int rc = this->do_add_request(std::move(request), client_id, req_params,
+                                  time, cost);
+    if (rc != DMC_OK) return rc;
     schedule_request();
     return rc;
   }
