@@ -34,7 +34,18 @@ static std::string g_test;
                    __LINE__, #c);                                             \
     }                                                                         \
   } while (0)
-#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
+#define EXPECT_EQ(a, b)                                                       \
+  do {                                                                        \
+    ++g_checks;                                                               \
+    auto va_ = (a);                                                           \
+    auto vb_ = (b);                                                           \
+    if (!(va_ == vb_)) {                                                      \
+      ++g_fail;                                                               \
+      std::fprintf(stderr, "FAIL %s %s:%d: %s == %s (%s vs %s)\n",           \
+                   g_test.c_str(), __FILE__, __LINE__, #a, #b,                \
+                   std::to_string(va_).c_str(), std::to_string(vb_).c_str()); \
+    }                                                                         \
+  } while (0)
 
 struct Request {};
 
@@ -528,21 +539,23 @@ TEST(add_req_pushprio_queue) {  // :188-270: handle_f sees every request
 TEST(push_sched_ahead_fires) {
   // A limit-throttled request must be dispatched by the sched-ahead timer
   // (the reference's timer never fires on time, dmclock_server.h:1771-1773).
+  // limit 5/s: the 2nd and 3rd requests become eligible 0.4 s and 0.8 s
+  // after the 1st; without completions only the timer can dispatch them.
   using Queue = dmc::PushPriorityQueue<int, Request>;
-  dmc::ClientInfo ci(0.0, 1.0, 5.0);  // limit 5/s: 0.4 s per request
+  dmc::ClientInfo ci(0.0, 1.0, 5.0);
   std::atomic<int> handled{0};
-  std::atomic<bool> busy{false};
-  Queue* qp = nullptr;
-  Queue pq([&](int) { return &ci; }, [&]() { return !busy.load(); },
+  Queue pq([&](int) { return &ci; }, []() { return true; },
            [&](const int&, std::unique_ptr<Request>, dmc::PhaseType, uint64_t) {
              ++handled;
            },
            AtLimit::Wait);
-  qp = &pq;
-  (void)qp;
   for (int i = 0; i < 3; ++i)
     EXPECT_EQ(0, pq.add_request(Request{}, 17, ReqParams(1, 1)));
-  std::this_thread::sleep_for(std::chrono::milliseconds(1500));
+  EXPECT_EQ(1, handled.load());  // the first goes out at once
+  std::this_thread::sleep_for(std::chrono::milliseconds(600));
+  EXPECT_EQ(2, handled.load());  // the timer dispatched the second
+  pq.request_completed();        // schedules the third for t0 + 0.8 s
+  std::this_thread::sleep_for(std::chrono::milliseconds(600));
   EXPECT_EQ(3, handled.load());
 }
 
