@@ -41,12 +41,9 @@ STAGE_BYTES = {
     "p_scan": ("client", 37),
     # k_scan<0>: count 4 + front_r 8 read, key 8 written
     "r_scan": ("client", 20),
-    # k_count: key 8 read, count 4 written (walks of candidates not counted)
-    "r_count": ("client", 12),
-    "p_count": ("client", 12),
-    # k_apply: candidate count 4 read
-    "r_apply": ("client", 4),
-    "p_apply": ("client", 4),
+    # k_cand: key 8 read per slot (candidate ids written are negligible)
+    "r_cand": ("client", 8),
+    "p_cand": ("client", 8),
     # k_add_chain: request 32 + sorted (slot,pos) 8 + rc 4 + ring entry 64
     #              + client state read 81 / written 57
     "add_chain": ("request", 246),

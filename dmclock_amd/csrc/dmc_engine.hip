@@ -46,15 +46,17 @@ constexpr uint32_t kNone = 0xffffffffu;
 
 // Per-phase selection / bookkeeping block (device resident).
 struct Sel {
-  uint32_t n_elig;
-  uint32_t pad0;
-  uint64_t kmin, kmax;
-  uint64_t T;           // ordered-key threshold for this phase
-  uint32_t n_entries;   // emitted pops (R) / groups (P)
+  uint32_t n_elig;      // eligible fronts
+  uint32_t phase;       // 0 = R, 1 = P
+  uint64_t kmin, kmax;  // ordered-key range of eligible fronts
+  uint64_t T;           // ordered-key threshold (0: nothing, ~0-1: all)
+  uint32_t n_cand;      // candidate clients (key <= T)
+  uint32_t n_extra;     // entries beyond each candidate's first
+  uint32_t n_entries;   // pops (R) / groups (P) to rank
+  uint32_t shift;       // 32-bit sort key scaling
   uint32_t n_dec_phase; // decisions taken by this phase
   uint32_t g_last;      // last priority (limit-scan) pull index, kNone if none
   uint32_t terminal;    // 1 if this phase ended the batch early
-  uint32_t ties;
   uint32_t n_prio_groups; // priority pops applied by phase P
 };
 
@@ -66,7 +68,8 @@ struct Ctl {
   uint32_t n_dec;      // decisions made so far
   uint32_t overflow;   // an entry buffer was too small: later kernels no-op
   uint32_t terminal;   // eligible work ran out before k_total
-  uint32_t ne[2];      // entries emitted by phase R / P (capacity hints)
+  uint32_t nc[2];      // candidates of phase R / P (capacity hints)
+  uint32_t nx[2];      // extra entries of phase R / P
   uint32_t next_type;  // DMC_NEXT_* of the stopping pull
   uint32_t pad;
   double when;
@@ -341,20 +344,13 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
 }
 
 // ------------------------------------------------------------------ pull: scans
-__global__ void k_phase_init(Sel* sel) {
-  if (threadIdx.x || blockIdx.x) return;
-  Sel z{};
-  z.kmin = kMaxKey;
-  z.kmax = 0;
-  z.g_last = 0;
-  *sel = z;
-}
-
 // Phase R scan: key = front reservation tag, eligible iff r <= now.
 // Phase P scan: first commits the limit scan of the first priority pull
 // (:1135-1144: every front with limit <= now becomes ready), then
 // key = p + prop_delta, eligible iff ready and p < inf (:1146-1151).
 // Nothing runs once the batch is complete (no further pull took place).
+// Per-block partials (count, min, max) go to `parts`: no same-address
+// atomics (thousands of waves hitting one word serialise at the memory side).
 template <int PH>
 __global__ void k_scan(Table tb, double now, uint64_t* keys, ScanPart* parts,
                        const Ctl* ctl) {
@@ -387,8 +383,6 @@ __global__ void k_scan(Table tb, double now, uint64_t* keys, ScanPart* parts,
       mx = k > mx ? k : mx;
     }
   }
-  // per-block partial (no same-address atomics: thousands of waves hitting
-  // one word serialise at the memory side); k_scan_final combines them
   cnt = wave_sum_u32(cnt);
   mn = wave_min_u64(mn);
   mx = wave_max_u64(mx);
@@ -407,18 +401,16 @@ __global__ void k_scan(Table tb, double now, uint64_t* keys, ScanPart* parts,
   }
 }
 
-// combines the scan's per-block partials into the phase's Sel
-__global__ void k_scan_final(const ScanPart* parts, uint32_t nparts, Sel* sel,
-                             const Ctl* ctl) {
-  __shared__ ScanPart sh[kBlock];
+// block-wide reduction of the scan partials (every thread gets the result)
+__device__ inline ScanPart reduce_parts(const ScanPart* parts, uint32_t nparts) {
+  __shared__ ScanPart sh[1024];
   ScanPart o{0, 0, kMaxKey, 0};
-  if (k_left(ctl))
-    for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
-      ScanPart b = parts[i];
-      o.cnt += b.cnt;
-      o.mn = b.mn < o.mn ? b.mn : o.mn;
-      o.mx = b.mx > o.mx ? b.mx : o.mx;
-    }
+  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+    ScanPart b = parts[i];
+    o.cnt += b.cnt;
+    o.mn = b.mn < o.mn ? b.mn : o.mn;
+    o.mx = b.mx > o.mx ? b.mx : o.mx;
+  }
   sh[threadIdx.x] = o;
   __syncthreads();
   for (int d = blockDim.x / 2; d > 0; d >>= 1) {
@@ -431,11 +423,9 @@ __global__ void k_scan_final(const ScanPart* parts, uint32_t nparts, Sel* sel,
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    sel->n_elig = sh[0].cnt;
-    sel->kmin = sh[0].mn;
-    sel->kmax = sh[0].mx;
-  }
+  ScanPart r = sh[0];
+  __syncthreads();
+  return r;
 }
 
 __device__ inline uint32_t hist_shift(uint64_t range) {
@@ -446,11 +436,17 @@ __device__ inline uint32_t hist_shift(uint64_t range) {
 }
 
 // Histogram of eligible keys over [kmin, kmax] in kHistBins integer buckets
-// of the ordered-key space (monotone in the key), with the max key per bucket.
-__global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
-                       const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
+// of the ordered-key space (monotone in the key), with the max key per
+// bucket.  kHistBlocks blocks of 1024 threads: few enough that the global
+// flush (one atomic per non-empty bin per block) stays cheap.
+constexpr int kHistBlocks = 128;
+__global__ void __launch_bounds__(1024)
+k_hist(uint32_t n, const uint64_t* keys, const ScanPart* parts,
+       uint32_t nparts, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
   uint32_t k_rem = k_left(ctl);
-  if (k_rem == 0 || sel->n_elig <= k_rem) return;
+  if (k_rem == 0) return;
+  ScanPart tot = reduce_parts(parts, nparts);
+  if (tot.cnt <= k_rem) return;
   __shared__ uint32_t sh[kHistBins];
   __shared__ unsigned long long smx[kHistBins];
   for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
@@ -458,8 +454,8 @@ __global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
     smx[b] = 0;
   }
   __syncthreads();
-  uint64_t kmin = sel->kmin;
-  uint32_t sh_ = hist_shift(sel->kmax - kmin);
+  uint64_t kmin = tot.mn;
+  uint32_t sh_ = hist_shift(tot.mx - kmin);
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n;
        s += gridDim.x * blockDim.x) {
     uint64_t k = keys[s];
@@ -479,16 +475,29 @@ __global__ void k_hist(uint32_t n, const uint64_t* keys, const Sel* sel,
 
 // Threshold T: every key <= T is a candidate and at least k_rem eligible
 // fronts are <= T (T is the largest key of the bin holding the k_rem-th
-// smallest), or everything when no more than k_rem are eligible.  Launched
-// with kPickThreads threads; each owns kHistBins / kPickThreads bins.
+// smallest), or everything when no more than k_rem are eligible.  Also
+// (re)initialises the phase's Sel.  kPickThreads threads; each owns
+// kHistBins / kPickThreads bins.
 constexpr int kPickThreads = 1024;
 constexpr int kBinsPerThread = kHistBins / kPickThreads;
 __global__ void __launch_bounds__(kPickThreads)
-k_pick(Sel* sel, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
+k_pick(const ScanPart* parts, uint32_t nparts, Sel* sel, const Ctl* ctl,
+       uint32_t* hist, uint64_t* hmax, uint32_t phase) {
   __shared__ uint32_t wsum[kPickThreads / 64];
   uint32_t k_rem = k_left(ctl);
-  uint32_t ne = sel->n_elig;
+  ScanPart tot = reduce_parts(parts, nparts);
+  uint32_t ne = k_rem ? tot.cnt : 0;
   int t = threadIdx.x;
+  if (t == 0) {
+    Sel z{};
+    z.n_elig = ne;
+    z.phase = phase;
+    z.kmin = tot.mn;
+    z.kmax = tot.mx;
+    z.g_last = kNone;
+    z.T = (k_rem == 0 || ne == 0) ? 0 : kMaxKey - 1;
+    *sel = z;
+  }
   uint32_t h[kBinsPerThread];
   uint32_t local = 0;
   for (int j = 0; j < kBinsPerThread; ++j) {
@@ -506,11 +515,7 @@ k_pick(Sel* sel, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
   uint32_t wbase = 0;
   for (int i = 0; i < w; ++i) wbase += wsum[i];
   uint32_t before = wbase + incl - local;  // exclusive prefix
-  if (k_rem == 0 || ne == 0) {
-    if (t == 0) sel->T = 0;  // nothing
-  } else if (ne <= k_rem) {
-    if (t == 0) sel->T = kMaxKey - 1;  // everything eligible
-  } else if (before < k_rem && before + local >= k_rem) {
+  if (k_rem && ne > k_rem && before < k_rem && before + local >= k_rem) {
     uint32_t cum = before;
     for (int j = 0; j < kBinsPerThread; ++j) {
       cum += h[j];
@@ -527,6 +532,40 @@ k_pick(Sel* sel, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
   }
 }
 
+// Candidates = slots whose key <= T, compacted (any order: the final order
+// is fixed by the sort on full keys).  kCandBlocks blocks, one atomic each.
+constexpr int kCandBlocks = 256;
+__global__ void k_cand(uint32_t n, const uint64_t* keys, Sel* sel,
+                       uint32_t* cand) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t base;
+  uint64_t T = sel->T;
+  if (T == 0) return;
+  uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint32_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  // pass 1: count
+  uint32_t c = 0;
+  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x) c += keys[s] <= T;
+  uint32_t incl = c;
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+  for (int i = 0; i < (int)(blockDim.x / 64); ++i) {
+    if (i < w) wb += wsum[i];
+    tot += wsum[i];
+  }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(&sel->n_cand, tot) : 0;
+  __syncthreads();
+  uint32_t o = base + wb + incl - c;
+  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
+    if (keys[s] <= T) cand[o++] = s;
+}
+
 // ------------------------------------------------------------------ pull: walks
 struct CountVisit {
   uint32_t pops = 0, groups = 0;
@@ -534,170 +573,254 @@ struct CountVisit {
   __device__ void group(uint64_t, uint32_t) { ++groups; }
 };
 
-template <int PH>
-__global__ void k_count(Table tb, double now, const uint64_t* keys,
-                        const Sel* sel, uint32_t* cnt) {
-  uint64_t T = sel->T;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    uint32_t c = 0;
-    if (keys[s] <= T) {
-      CountVisit v;
-      if (PH == 0)
-        c = walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
-      else
-        c = walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr).groups;
-    }
-    cnt[s] = c;
-  }
-}
-
-template <int PH>
-__global__ void k_total(uint32_t n, const uint32_t* cnt, const uint32_t* off,
-                        uint32_t cap, Sel* sel, Ctl* ctl) {
-  if (threadIdx.x || blockIdx.x) return;
-  uint32_t ne = n ? off[n - 1] + cnt[n - 1] : 0;
-  if (ctl->overflow || k_left(ctl) == 0) ne = 0;
-  sel->n_entries = ne;
-  ctl->ne[PH] = ne;
-  if (ne > cap) {
-    ctl->overflow = 1;
-    sel->n_entries = 0;
-  }
+// Entry id of the j-th entry of candidate i: the first lives at i, the rest
+// in the extras region (after cap1) at the candidate's extras base.
+__device__ inline uint32_t entry_id(uint32_t i, uint32_t j, uint32_t cap1,
+                                    uint32_t xbase) {
+  return j == 0 ? i : cap1 + xbase + j - 1;
 }
 
 struct EmitVisit {
-  uint64_t* ekey;
-  uint32_t* eval;
+  uint64_t* eokey;
   uint32_t* eslot;
+  uint32_t* eseq;
   uint32_t* erun;
-  uint32_t base, slot, n = 0;
+  uint32_t i, cap1, xbase, cap2, slot;
   int ph;
-  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
-    if (ph == 0) {
-      uint32_t e = base + n++;
-      ekey[e] = okey(t.r);
-      eval[e] = e;
+  uint32_t n = 0;
+  uint64_t kmax = 0;
+  __device__ void put(uint64_t key, uint32_t run) {
+    if (n == 0 ? i < cap1 : xbase + n - 1 < cap2) {
+      uint32_t e = entry_id(i, n, cap1, xbase);
+      eokey[e] = key;
       eslot[e] = slot;
+      eseq[e] = n;
+      erun[e] = run;
     }
+    kmax = key > kmax ? key : kmax;
+    ++n;
   }
-  __device__ void group(uint64_t key, uint32_t run) {
-    uint32_t e = base + n++;
-    ekey[e] = key;
-    eval[e] = e;
-    eslot[e] = slot;
-    erun[e] = run;
+  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
+    if (ph == 0) put(okey(t.r), 0);
   }
+  __device__ void group(uint64_t key, uint32_t run) { put(key, run); }
 };
 
-// Writes the candidates' entries in slot order, and pads [n_entries, cap)
-// with maximal keys so that a fixed-size sort leaves them at the end.
+// One thread per candidate: count its entries (R: pops with r <= min(now,T);
+// P: groups with key <= T), allocate its extras (one atomic per block), then
+// emit (key, slot, seq, run).  Per-block max key goes to emax[] for the
+// 32-bit sort-key scaling.
 template <int PH>
-__global__ void k_emit(Table tb, double now, const Sel* sel, const Ctl* ctl,
-                       uint32_t cap, const uint32_t* cnt, const uint32_t* off,
-                       uint64_t* ekey, uint32_t* eval, uint32_t* eslot,
-                       uint32_t* erun) {
-  if (ctl->overflow) return;
+__global__ void k_emit(Table tb, double now, Sel* sel, const Ctl* ctl,
+                       const uint32_t* cand, uint32_t cap1, uint32_t cap2,
+                       uint32_t* cxbase, uint64_t* eokey, uint32_t* eslot,
+                       uint32_t* eseq, uint32_t* erun, uint64_t* emax) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t base;
+  __shared__ unsigned long long bmax;
+  uint32_t nc = sel->n_cand;
+  if (blockIdx.x * blockDim.x >= nc || ctl->overflow) return;
   uint64_t T = sel->T;
-  uint32_t ne = sel->n_entries;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t e = ne + tid; e < cap; e += stride) {
-    ekey[e] = kMaxKey;
-    eval[e] = e;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t s = i < nc ? cand[i] : 0;
+  uint32_t c = 0;
+  if (i < nc) {
+    CountVisit v;
+    c = PH == 0 ? walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr)
+                : walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr).groups;
   }
-  if (!ne) return;
-  for (uint32_t s = tid; s < tb.n; s += stride) {
-    if (!cnt[s]) continue;
-    EmitVisit v{ekey, eval, eslot, erun, off[s], s, 0, PH};
+  uint32_t x = c ? c - 1 : 0;
+  uint32_t incl = x;
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  if (threadIdx.x == 0) bmax = 0;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+  for (int k = 0; k < (int)(blockDim.x / 64); ++k) {
+    if (k < w) wb += wsum[k];
+    tot += wsum[k];
+  }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(&sel->n_extra, tot) : 0;
+  __syncthreads();
+  uint32_t xb = base + wb + incl - x;
+  if (i < nc) {
+    cxbase[i] = xb;
+    EmitVisit v{eokey, eslot, eseq, erun, i, cap1, xb, cap2, s, PH};
     if (PH == 0)
       walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
     else
       walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+    atomicMax(&bmax, (unsigned long long)v.kmax);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) emax[blockIdx.x] = bmax;
+}
+
+// 32-bit sort keys: (okey - kmin) >> shift with the smallest shift that keeps
+// every real key below 0xffffffff; padding entries get 0xffffffff.  Pads are
+// region-1 ids in [n_cand, cap1) and region-2 ids past the extras.
+__global__ void k_key32(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
+                        const uint64_t* emax, uint32_t nemax,
+                        const uint64_t* eokey, uint32_t* ek32, uint32_t* eval) {
+  __shared__ unsigned long long sh[kBlock];
+  uint32_t nc = sel->n_cand, nx = sel->n_extra;
+  bool ovf = ctl->overflow || nc > cap1 || nx > cap2;
+  uint64_t m = 0;
+  uint32_t nb = (nc + kBlock - 1) / kBlock;  // emit blocks that ran
+  if (nb < nemax) nemax = nb;
+  for (uint32_t b = threadIdx.x; b < nemax; b += blockDim.x)
+    m = emax[b] > m ? emax[b] : m;
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d && sh[threadIdx.x + d] > sh[threadIdx.x])
+      sh[threadIdx.x] = sh[threadIdx.x + d];
+    __syncthreads();
+  }
+  uint64_t kmin = sel->kmin;
+  uint64_t range = sh[0] > kmin ? sh[0] - kmin : 0;
+  uint32_t shift = 0;
+  while ((range >> shift) >= 0xffffffffull) ++shift;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) {
+    sel->n_entries = ovf ? 0 : nc + nx;
+    sel->shift = shift;
+    ctl->nc[sel->phase] = nc;
+    ctl->nx[sel->phase] = nx;
+    if (ovf) ctl->overflow = 1;
+  }
+  uint32_t E = cap1 + cap2;
+  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
+    bool real = !ovf && (e < nc || (e >= cap1 && e < cap1 + nx));
+    uint64_t k = real ? eokey[e] : 0;
+    ek32[e] = !real ? 0xffffffffu
+                    : (k > kmin ? (uint32_t)((k - kmin) >> shift) : 0u);
+    eval[e] = e;
   }
 }
 
-__device__ inline bool tie_at(const uint64_t* skey, const uint32_t* sval,
+// Full order among entries: (okey, slot, seq).
+__device__ inline bool ent_less(uint32_t a, uint32_t b, const uint64_t* eokey,
+                                const uint32_t* eslot, const uint32_t* eseq) {
+  if (eokey[a] != eokey[b]) return eokey[a] < eokey[b];
+  if (eslot[a] != eslot[b]) return eslot[a] < eslot[b];
+  return eseq[a] < eseq[b];
+}
+
+// After the 32-bit radix sort, runs of equal 32-bit keys are ordered by the
+// full key (insertion sort by the run's first thread; runs are short).
+__global__ void k_fixup(const Sel* sel, const uint32_t* sk32, uint32_t* sval,
+                        const uint64_t* eokey, const uint32_t* eslot,
+                        const uint32_t* eseq) {
+  uint32_t n = sel->n_entries;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += gridDim.x * blockDim.x) {
+    if (p > 0 && sk32[p - 1] == sk32[p]) continue;
+    uint32_t q = p + 1;
+    while (q < n && sk32[q] == sk32[p]) ++q;
+    for (uint32_t a = p + 1; a < q; ++a) {
+      uint32_t v = sval[a];
+      uint32_t b = a;
+      while (b > p && ent_less(v, sval[b - 1], eokey, eslot, eseq)) {
+        sval[b] = sval[b - 1];
+        --b;
+      }
+      sval[b] = v;
+    }
+  }
+}
+
+__device__ inline bool tie_at(const uint64_t* eokey, const uint32_t* sval,
                               const uint32_t* eslot, uint32_t n, uint32_t pos) {
-  uint32_t me = eslot[sval[pos]];
-  if (pos > 0 && skey[pos - 1] == skey[pos] && eslot[sval[pos - 1]] != me)
-    return true;
-  if (pos + 1 < n && skey[pos + 1] == skey[pos] && eslot[sval[pos + 1]] != me)
-    return true;
+  uint32_t e = sval[pos];
+  if (pos > 0) {
+    uint32_t f = sval[pos - 1];
+    if (eokey[f] == eokey[e] && eslot[f] != eslot[e]) return true;
+  }
+  if (pos + 1 < n) {
+    uint32_t f = sval[pos + 1];
+    if (eokey[f] == eokey[e] && eslot[f] != eslot[e]) return true;
+  }
   return false;
 }
 
 // R: the first k_rem sorted pops are dispatched in sorted order.
-__global__ void k_decide_r(const Ctl* ctl, const uint64_t* skey,
+__global__ void k_decide_r(const Ctl* ctl, const uint64_t* eokey,
                            const uint32_t* sval, const uint32_t* eslot,
                            uint32_t* eoff, uint8_t* etie, uint32_t* applied,
                            Sel* sel) {
   if (ctl->overflow) return;
   uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pos == 0) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) {
     sel->n_dec_phase = n < k_rem ? n : k_rem;
     sel->terminal = 0;
-    sel->g_last = kNone;
   }
-  if (pos >= n) return;
-  uint32_t e = sval[pos];
-  if (pos < k_rem) {
-    eoff[e] = n_dec + pos;
-    etie[e] = tie_at(skey, sval, eslot, n, pos) ? 1 : 0;
-    atomicAdd(&applied[eslot[e]], 1u);
-  } else {
-    eoff[e] = kNone;
+  for (uint32_t pos = tid; pos < n; pos += gridDim.x * blockDim.x) {
+    uint32_t e = sval[pos];
+    if (pos < k_rem) {
+      eoff[e] = n_dec + pos;
+      etie[e] = tie_at(eokey, sval, eslot, n, pos) ? 1 : 0;
+      atomicAdd(&applied[eslot[e]], 1u);
+    } else {
+      eoff[e] = kNone;
+    }
   }
 }
 
-__global__ void k_group_sizes(const Ctl* ctl, const Sel* sel, uint32_t cap,
+__global__ void k_group_sizes(const Ctl* ctl, const Sel* sel, uint32_t E,
                               const uint32_t* sval, const uint32_t* erun,
                               uint32_t* gsz) {
-  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pos >= cap) return;
-  gsz[pos] = (!ctl->overflow && pos < sel->n_entries) ? 1 + erun[sval[pos]] : 0;
+  uint32_t n = (!ctl->overflow) ? sel->n_entries : 0;
+  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < E;
+       pos += gridDim.x * blockDim.x)
+    gsz[pos] = pos < n ? 1 + erun[sval[pos]] : 0;
 }
 
 // P: groups (priority pop + the reservation run it exposes) in key order;
 // decisions are the prefix of their concatenation up to k_rem.
-__global__ void k_decide_p(const Ctl* ctl, const uint64_t* skey,
+__global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
                            const uint32_t* sval, const uint32_t* eslot,
                            const uint32_t* gsz, const uint32_t* goff,
                            uint32_t* eoff, uint8_t* etie, uint32_t* applied,
                            Sel* sel) {
   if (ctl->overflow) return;
   uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (n == 0) {
-    if (pos == 0) {
+    if (tid == 0) {
       sel->n_dec_phase = 0;
       sel->terminal = k_rem > 0 ? 1 : 0;
     }
     return;
   }
-  if (pos >= n) return;
-  uint32_t e = sval[pos];
-  uint32_t o = goff[pos];
-  if (pos == n - 1) {
-    uint32_t tot = o + gsz[pos];
-    sel->n_dec_phase = tot < k_rem ? tot : k_rem;
-    sel->terminal = tot < k_rem ? 1 : 0;
-  }
-  if (o < k_rem) {
-    eoff[e] = n_dec + o;
-    etie[e] = tie_at(skey, sval, eslot, n, pos) ? 1 : 0;
-    uint32_t na = gsz[pos];
-    if (na > k_rem - o) na = k_rem - o;
-    atomicAdd(&applied[eslot[e]], na);
-    if (pos == n - 1 || goff[pos + 1] >= k_rem) {
-      // the last applied group: its priority pop is this phase's last
-      // limit-scanning pull
-      sel->g_last = n_dec + o;
-      sel->n_prio_groups = pos + 1;
+  for (uint32_t pos = tid; pos < n; pos += gridDim.x * blockDim.x) {
+    uint32_t e = sval[pos];
+    uint32_t o = goff[pos];
+    if (pos == n - 1) {
+      uint32_t tot = o + gsz[pos];
+      sel->n_dec_phase = tot < k_rem ? tot : k_rem;
+      sel->terminal = tot < k_rem ? 1 : 0;
     }
-  } else {
-    eoff[e] = kNone;
+    if (o < k_rem) {
+      eoff[e] = n_dec + o;
+      etie[e] = tie_at(eokey, sval, eslot, n, pos) ? 1 : 0;
+      uint32_t na = gsz[pos];
+      if (na > k_rem - o) na = k_rem - o;
+      atomicAdd(&applied[eslot[e]], na);
+      if (pos == n - 1 || goff[pos + 1] >= k_rem) {
+        // the last applied group: its priority pop is this phase's last
+        // limit-scanning pull
+        sel->g_last = n_dec + o;
+        sel->n_prio_groups = pos + 1;
+      }
+    } else {
+      eoff[e] = kNone;
+    }
   }
 }
 
@@ -705,21 +828,20 @@ struct ApplyVisit {
   dmc_decision* out;
   const uint32_t* eoff;
   const uint8_t* etie;
-  uint32_t base;    // first entry index of this client
+  uint32_t i, cap1, xbase;  // candidate index, region-2 layout
   uint32_t slot;
   int ph;
   uint32_t npop = 0, ngroup = 0, inrun = 0;
   uint32_t last_idx = 0;
-  uint32_t n_res = 0, n_prio = 0;
   __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
                       bool prio) {
     uint32_t idx, tie;
     if (ph == 0) {
-      uint32_t e = base + npop;
+      uint32_t e = entry_id(i, npop, cap1, xbase);
       idx = eoff[e];
       tie = etie[e];
     } else {
-      uint32_t e = base + ngroup;
+      uint32_t e = entry_id(i, ngroup, cap1, xbase);
       if (prio) inrun = 0;
       idx = eoff[e] + inrun;
       tie = prio ? etie[e] : 0;
@@ -737,12 +859,11 @@ struct ApplyVisit {
     out[idx] = d;
     last_idx = idx;
     ++npop;
-    if (prio) ++n_prio; else ++n_res;
   }
   __device__ void group(uint64_t, uint32_t) { ++ngroup; }
 };
 
-// Replays each candidate client's walk for exactly the pops that were
+// One thread per candidate replays its walk for exactly the pops that were
 // dispatched, writes their decision records, and stores the client's new
 // state: ring head/count, front cache, reduced reservation tags (immediate:
 // every queued request, :1088-1095; delayed: the front, :1077-1085), prev tag,
@@ -750,22 +871,22 @@ struct ApplyVisit {
 // limit <= now).
 template <int PH>
 __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
-                        const Ctl* ctl, const uint32_t* cnt,
-                        const uint32_t* off, const uint32_t* eoff,
-                        const uint8_t* etie, uint32_t* applied,
-                        dmc_decision* out, unsigned long long* sched) {
+                        const Ctl* ctl, const uint32_t* cand,
+                        const uint32_t* cxbase, uint32_t cap1,
+                        const uint32_t* eoff, const uint8_t* etie,
+                        uint32_t* applied, dmc_decision* out) {
   if (ctl->overflow || sel->n_entries == 0) return;
+  uint32_t nc = sel->n_cand;
   uint32_t g_last = sel->g_last;
   uint32_t terminal = sel->terminal;
   uint64_t T = sel->T;
-  uint32_t nres = 0, nprio = 0;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    if (!cnt[s]) continue;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nc;
+       i += gridDim.x * blockDim.x) {
+    uint32_t s = cand[i];
     uint32_t a = applied[s];
     if (!a) continue;
     applied[s] = 0;
-    ApplyVisit v{out, eoff, etie, off[s], s, PH};
+    ApplyVisit v{out, eoff, etie, i, cap1, cxbase[i], s, PH};
     Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
     Tag3 front{};
     uint32_t fcost = 0;
@@ -779,16 +900,14 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
       pops = w.pops;
       pmask = w.pmask;
     }
-    nres += v.n_res;
-    nprio += v.n_prio;
     ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-    uint32_t nc = c - pops, nh = (h + pops) & tb.qmask;
+    uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
     if (!tb.delayed) {
       if (PH == 1 && pmask) {
         double rinv = tb.r_inv[s];
         // remaining requests: all reductions, in order
-        for (uint32_t i = pops; i < c; ++i)
-          ring[(h + i) & tb.qmask].r = reduced_r(ring, h, tb.qmask, i, pmask, rinv);
+        for (uint32_t k = pops; k < c; ++k)
+          ring[(h + k) & tb.qmask].r = reduced_r(ring, h, tb.qmask, k, pmask, rinv);
         double pr = prev.r;
         for (uint32_t j = 0; j < pops; ++j)
           if ((pmask >> j) & 1ull) {
@@ -797,13 +916,13 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
           }
         tb.prev_r[s] = pr;
       }
-      if (nc) {
+      if (nc2) {
         const ReqEntry& f = ring[nh];
         front = Tag3{f.r, f.p, f.l, f.arrival};
       }
     } else {
       // delayed: the walk recomputed the new front and prev
-      if (nc) {
+      if (nc2) {
         ReqEntry& f = ring[nh];
         f.r = front.r;
         f.p = front.p;
@@ -818,9 +937,9 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
       if (c >= 2) tb.last_tick[s] = tick;
     }
     tb.head[s] = nh;
-    tb.count[s] = nc;
+    tb.count[s] = nc2;
     uint8_t f = tb.flags[s] & (uint8_t)~F_READY;
-    if (nc) {
+    if (nc2) {
       tb.front_r[s] = front.r;
       tb.front_p[s] = front.p;
       tb.front_l[s] = front.l;
@@ -829,9 +948,6 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
     }
     tb.flags[s] = f;
   }
-  (void)nres;
-  (void)nprio;
-  (void)sched;  // counted once per phase in k_phase_end
 }
 
 __global__ void k_ctl_init(Ctl* ctl, uint32_t k_total) {
@@ -1182,8 +1298,10 @@ struct dmc_queue {
   unsigned long long* reqcount = nullptr;
   // entries (grown on demand)
   uint32_t ecap = 0;
-  uint64_t *ekey = nullptr, *skey = nullptr;
+  uint64_t* eokey = nullptr;  // full ordered key per entry
+  uint32_t *ek32 = nullptr, *sk32 = nullptr;  // 32-bit sort keys
   uint32_t *eval = nullptr, *sval = nullptr, *eslot = nullptr, *erun = nullptr;
+  uint32_t *eseq = nullptr;
   uint32_t *eoff = nullptr, *gsz = nullptr, *goff = nullptr;
   uint8_t* etie = nullptr;
   // add batch buffers
@@ -1200,7 +1318,11 @@ struct dmc_queue {
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   Ctl* ctl = nullptr;
   ScanPart* parts = nullptr;  // per-block scan partials
-  uint32_t cap_hint[2] = {4096, 4096};  // entry capacity per phase (adaptive)
+  // entry capacities per phase: [0] first entries (= candidates), [1] extras
+  uint32_t cap_hint[2][2] = {{4096, 4096}, {4096, 4096}};
+  uint32_t* cand = nullptr;    // N
+  uint32_t* cxbase = nullptr;  // N
+  uint64_t* emax = nullptr;    // N / kBlock + 1
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
   struct ProfRec {
     hipEvent_t a, b;
@@ -1217,9 +1339,9 @@ namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
     "add_sort", "add_chain", "activate",
-    "r_scan", "r_select", "r_count", "r_offsets", "r_emit", "r_sort",
+    "r_scan", "r_select", "r_cand", "r_emit", "r_key32", "r_sort",
     "r_decide", "r_apply",
-    "p_scan", "p_select", "p_count", "p_offsets", "p_emit", "p_sort",
+    "p_scan", "p_select", "p_cand", "p_emit", "p_key32", "p_sort",
     "p_decide", "p_apply",
     "step", "future"};
 
@@ -1273,25 +1395,27 @@ int ensure_temp(dmc_queue* q, size_t need) {
 int ensure_entries(dmc_queue* q, uint32_t n) {
   if (n <= q->ecap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
-  dfree(q->ekey); dfree(q->skey); dfree(q->eval); dfree(q->sval);
-  dfree(q->eslot); dfree(q->erun); dfree(q->eoff); dfree(q->gsz);
-  dfree(q->goff); dfree(q->etie);
-  HIP_OK(hipMalloc(&q->ekey, sizeof(uint64_t) * cap));
-  HIP_OK(hipMalloc(&q->skey, sizeof(uint64_t) * cap));
+  dfree(q->eokey); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
+  dfree(q->sval); dfree(q->eslot); dfree(q->erun); dfree(q->eseq);
+  dfree(q->eoff); dfree(q->gsz); dfree(q->goff); dfree(q->etie);
+  HIP_OK(hipMalloc(&q->eokey, sizeof(uint64_t) * cap));
+  HIP_OK(hipMalloc(&q->ek32, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sk32, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->eslot, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->erun, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eseq, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->eoff, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->etie, cap));
   q->ecap = cap;
   size_t t1 = 0, t2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ekey, q->skey, q->eval,
-                                     q->sval, (int)cap, 0, 64, q->stream);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
+                                           q->sval, (int)cap, 0, 32, q->stream);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
-                                   q->stream);
+                                         q->stream);
   return ensure_temp(q, std::max(t1, t2));
 }
 
@@ -1395,76 +1519,78 @@ uint32_t pow2_at_least(uint32_t x) {
 // capacity the sort runs over (entries beyond it set ctl->overflow and the
 // rest of the batch no-ops; the host retries with a larger capacity).
 template <int PH>
-int launch_phase(dmc_queue* q, double now, uint32_t cap, dmc_decision* d_out) {
+int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
+                 dmc_decision* d_out) {
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = grid_for(N, 2048);
+  uint32_t E = cap1 + cap2;
+  uint32_t gE = grid_for(E, 1024);
+  uint32_t gC = (N + kBlock - 1) / kBlock;  // one thread per candidate
   const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
-  hipLaunchKernelGGL(k_phase_init, dim3(1), dim3(64), 0, q->stream, q->sel);
   pb(q, S0 + 0);
   hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
                      q->keys, q->parts, (const Ctl*)q->ctl);
-  hipLaunchKernelGGL(k_scan_final, dim3(1), dim3(kBlock), 0, q->stream,
-                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl);
   pe(q);
   pb(q, S0 + 1);
-  hipLaunchKernelGGL(k_hist, dim3(gN), dim3(kBlock), 0, q->stream, N,
-                     (const uint64_t*)q->keys, (const Sel*)q->sel,
+  hipLaunchKernelGGL(k_hist, dim3(kHistBlocks), dim3(1024), 0, q->stream, N,
+                     (const uint64_t*)q->keys, (const ScanPart*)q->parts, gN,
                      (const Ctl*)q->ctl, q->hist, q->hmax);
-  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream, q->sel,
-                     (const Ctl*)q->ctl, q->hist, q->hmax);
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream,
+                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl,
+                     q->hist, q->hmax, (uint32_t)PH);
   pe(q);
   pb(q, S0 + 2);
-  hipLaunchKernelGGL(k_count<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     (const uint64_t*)q->keys, (const Sel*)q->sel, q->cnt);
+  hipLaunchKernelGGL(k_cand, dim3(kCandBlocks), dim3(kBlock), 0, q->stream, N,
+                     (const uint64_t*)q->keys, q->sel, q->cand);
   pe(q);
   pb(q, S0 + 3);
-  size_t tbytes = q->temp_bytes;
-  HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->cnt, q->off, (int)N,
-                                          q->stream));
-  hipLaunchKernelGGL(k_total<PH>, dim3(1), dim3(64), 0, q->stream, N,
-                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, cap, q->sel,
-                     q->ctl);
+  hipLaunchKernelGGL(k_emit<PH>, dim3(gC), dim3(kBlock), 0, q->stream, tb, now,
+                     q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand, cap1,
+                     cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
+                     q->emax);
   pe(q);
   pb(q, S0 + 4);
-  hipLaunchKernelGGL(k_emit<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     (const Sel*)q->sel, (const Ctl*)q->ctl, cap,
-                     (const uint32_t*)q->cnt, (const uint32_t*)q->off, q->ekey,
-                     q->eval, q->eslot, q->erun);
+  hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
+                     q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
+                     (const uint64_t*)q->eokey, q->ek32, q->eval);
   pe(q);
   pb(q, S0 + 5);
-  tbytes = q->temp_bytes;
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ekey, q->skey,
-                                            q->eval, q->sval, (int)cap, 0, 64,
+  size_t tbytes = q->temp_bytes;
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
+                                            q->eval, q->sval, (int)E, 0, 32,
                                             q->stream));
+  hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
+                     (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
+                     (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
+                     (const uint32_t*)q->eseq);
   pe(q);
-  uint32_t ge = (cap + kBlock - 1) / kBlock;
   pb(q, S0 + 6);
   if (PH == 0) {
-    hipLaunchKernelGGL(k_decide_r, dim3(ge), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const uint64_t*)q->skey,
+    hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
                        (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
                        q->eoff, q->etie, q->applied, q->sel);
   } else {
-    hipLaunchKernelGGL(k_group_sizes, dim3(ge), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const Sel*)q->sel, cap,
+    hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const Sel*)q->sel, E,
                        (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
     tbytes = q->temp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
-                                            (int)cap, q->stream));
-    hipLaunchKernelGGL(k_decide_p, dim3(ge), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const uint64_t*)q->skey,
+                                            (int)E, q->stream));
+    hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
                        (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
                        (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
                        q->etie, q->applied, q->sel);
   }
   pe(q);
   pb(q, S0 + 7);
-  hipLaunchKernelGGL(k_apply<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
-                     q->tick, (const Sel*)q->sel, (const Ctl*)q->ctl,
-                     (const uint32_t*)q->cnt, (const uint32_t*)q->off,
-                     (const uint32_t*)q->eoff, (const uint8_t*)q->etie,
-                     q->applied, d_out, q->sched);
+  hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
+                     q->stream, tb, now, q->tick, (const Sel*)q->sel,
+                     (const Ctl*)q->ctl, (const uint32_t*)q->cand,
+                     (const uint32_t*)q->cxbase, cap1, (const uint32_t*)q->eoff,
+                     (const uint8_t*)q->etie, q->applied, d_out);
   pe(q);
   hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
                      (const Sel*)q->sel, q->ctl, q->sched);
@@ -1538,16 +1664,17 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       ++n_dec;
       continue;
     }
-    uint32_t cap[2];
+    uint32_t cap1[2], cap2[2];
     for (int ph = 0; ph < 2; ++ph) {
-      cap[ph] = std::max(q->cap_hint[ph], pow2_at_least(std::min(kk, 1u << 16)));
-      int rc = ensure_entries(q, cap[ph]);
+      cap1[ph] = std::max(q->cap_hint[ph][0], pow2_at_least(std::min(kk, 1u << 16)));
+      cap2[ph] = q->cap_hint[ph][1];
+      int rc = ensure_entries(q, cap1[ph] + cap2[ph]);
       if (rc) return rc;
     }
     hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk);
-    int rc = launch_phase<0>(q, now, cap[0], d_out + n_dec);
+    int rc = launch_phase<0>(q, now, cap1[0], cap2[0], d_out + n_dec);
     if (rc) return rc;
-    rc = launch_phase<1>(q, now, cap[1], d_out + n_dec);
+    rc = launch_phase<1>(q, now, cap1[1], cap2[1], d_out + n_dec);
     if (rc) return rc;
     if (!allow) {
       rc = launch_future(q, now, q->ctl);
@@ -1559,10 +1686,12 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     pflush(q);
     n_dec += c.n_dec;
     for (int ph = 0; ph < 2; ++ph) {
-      uint32_t want = pow2_at_least(c.ne[ph] + (c.ne[ph] >> 2) + 1);
-      // grow at once, shrink slowly
-      q->cap_hint[ph] = want > q->cap_hint[ph] ? want
-                        : std::max(want, q->cap_hint[ph] / 2);
+      uint32_t need[2] = {c.nc[ph], c.nx[ph]};
+      for (int r = 0; r < 2; ++r) {
+        uint32_t want = pow2_at_least(need[r] + (need[r] >> 2) + 1);
+        uint32_t& h = q->cap_hint[ph][r];
+        h = want > h ? want : std::max(want, h / 2);  // grow at once, shrink slowly
+      }
     }
     if (c.overflow) continue;  // state before the overflowing phase is intact
     if (n_dec >= k || !c.terminal) break;
@@ -1655,6 +1784,9 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->sctl, 1);
   rc |= A(&q->ctl, 1);
   rc |= A(&q->parts, 4096);
+  rc |= A(&q->cand, N);
+  rc |= A(&q->cxbase, N);
+  rc |= A(&q->emax, N / kBlock + 2);
   rc |= A(&q->act_min, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
@@ -1688,11 +1820,11 @@ int dmc_queue_destroy(dmc_queue* q) {
                   t.l_inv, t.pd, t.front_r, t.front_p, t.front_l, t.head,
                   t.count, t.cur_delta, t.cur_rho, t.last_tick, t.flags, t.ring,
                   q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sel,
-                  q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->ekey,
-                  q->skey, q->eval, q->sval, q->eslot, q->erun, q->eoff, q->gsz,
-                  q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
+                  q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->eokey,
+                  q->ek32, q->sk32, q->eval, q->sval, q->eslot, q->erun, q->eseq,
+                  q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
                   q->skeys, q->svals, q->d_dec, q->temp, q->ctl,
-                  q->parts};
+                  q->parts, q->cand, q->cxbase, q->emax};
   for (void* p : ptrs)
     dfree(p);
   for (auto& r : q->prof_pool) {

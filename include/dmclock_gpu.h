@@ -219,7 +219,7 @@ int dmc_stats_get(dmc_queue* q, dmc_stats* out);
 #define DMC_PROF_ADD_SORT 0
 #define DMC_PROF_ADD_CHAIN 1
 #define DMC_PROF_ACTIVATE 2
-#define DMC_PROF_R_SCAN 3   /* r_scan r_select r_count r_offsets r_emit r_sort r_decide r_apply */
+#define DMC_PROF_R_SCAN 3   /* r_scan r_select r_cand r_emit r_key32 r_sort r_decide r_apply */
 #define DMC_PROF_P_SCAN 11  /* p_scan ... p_apply, same order */
 #define DMC_PROF_STEP 19
 #define DMC_PROF_FUTURE 20

@@ -11,6 +11,9 @@ rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/p
 timeout -k 10 400 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; [ $rc -eq 0 ] || { echo "bench failed $rc"; tail -30 gpurun_out/bench.err; exit $rc; }
 cat gpurun_out/bench.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-profile --no-cpu-baseline > gpurun_out/bench_noprof.json 2> gpurun_out/bench_noprof.err
+rc=$?; [ $rc -eq 0 ] || { echo "bench2 failed $rc"; tail -30 gpurun_out/bench_noprof.err; exit $rc; }
+cat gpurun_out/bench_noprof.json
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err
