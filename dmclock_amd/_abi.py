@@ -28,6 +28,10 @@ NEXT_RETURNING = 0
 NEXT_FUTURE = 1
 NEXT_NONE = 2
 
+# engine options (dmc_queue_set_option)
+OPT_SMALL_K = 1
+OPT_FORCE_RADIX = 2
+
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0
 PHASE_PRIORITY = 1

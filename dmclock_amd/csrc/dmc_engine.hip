@@ -824,6 +824,216 @@ __global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
   }
 }
 
+// ---------------------------------------------------------- pull: bin-rank
+// Ranking the entries without a general sort: entries are counted into kNB
+// bins of the ordered-key range (monotone), bucketed, and each entry's rank
+// is its bin's offset plus the number of entries of its own bin that precede
+// it in the full order (okey, slot, seq).  The same pass yields the
+// group-size prefix (P) and the tie flag, and decides.  A bin with more than
+// kBigBin entries aborts the batch (ctl->overflow = 2); the host then redoes
+// it through the radix-sort path.
+constexpr int kNB = 4096;
+constexpr uint32_t kBigBin = 2048;
+
+__device__ inline uint64_t emax_reduce(const uint64_t* emax, uint32_t nemax,
+                                       uint32_t nc) {
+  __shared__ unsigned long long sh[kBlock];
+  uint64_t m = 0;
+  uint32_t nb = (nc + kBlock - 1) / kBlock;  // emit blocks that ran
+  if (nb < nemax) nemax = nb;
+  for (uint32_t b = threadIdx.x; b < nemax; b += blockDim.x)
+    m = emax[b] > m ? emax[b] : m;
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d && sh[threadIdx.x + d] > sh[threadIdx.x])
+      sh[threadIdx.x] = sh[threadIdx.x + d];
+    __syncthreads();
+  }
+  uint64_t r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+template <int PH>
+__global__ void k_bin(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
+                      const uint64_t* emax, uint32_t nemax,
+                      const uint64_t* eokey, const uint32_t* erun,
+                      uint32_t* ebin, uint32_t* bcount, uint32_t* bsize) {
+  __shared__ uint32_t sc[kNB];
+  __shared__ uint32_t ss[kNB];
+  uint32_t nc = sel->n_cand, nx = sel->n_extra;
+  bool ovf = ctl->overflow || nc > cap1 || nx > cap2;
+  uint64_t kmin = sel->kmin;
+  uint64_t mx = emax_reduce(emax, nemax, nc);
+  uint64_t range = mx > kmin ? mx - kmin : 0;
+  uint32_t shift = 0;
+  while ((range >> shift) >= (uint64_t)kNB) ++shift;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) {
+    sel->n_entries = ovf ? 0 : nc + nx;
+    sel->shift = shift;
+    ctl->nc[PH] = nc;
+    ctl->nx[PH] = nx;
+    if (ovf && !ctl->overflow) ctl->overflow = 1;
+  }
+  if (ovf) return;
+  for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
+    sc[b] = 0;
+    ss[b] = 0;
+  }
+  __syncthreads();
+  uint32_t E = cap1 + cap2;
+  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
+    bool real = e < nc || (e >= cap1 && e < cap1 + nx);
+    if (!real) continue;
+    uint64_t k = eokey[e];
+    uint32_t b = k > kmin ? (uint32_t)((k - kmin) >> shift) : 0u;
+    if (b >= (uint32_t)kNB) b = kNB - 1;
+    ebin[e] = b;
+    atomicAdd(&sc[b], 1u);
+    atomicAdd(&ss[b], PH == 0 ? 1u : 1u + erun[e]);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kNB; b += blockDim.x)
+    if (sc[b]) {
+      atomicAdd(&bcount[b], sc[b]);
+      atomicAdd(&bsize[b], ss[b]);
+    }
+}
+
+// exclusive scans of the bin counts and of the bins' total group sizes; the
+// phase's decision count; skew check.  One block of 1024 threads.
+template <int PH>
+__global__ void __launch_bounds__(1024)
+k_bscan(Sel* sel, Ctl* ctl, const uint32_t* bcount, const uint32_t* bsize,
+        uint32_t* boff, uint32_t* bsoff, uint32_t* bfill) {
+  constexpr int per = kNB / 1024;
+  __shared__ uint32_t wc[16], wsz[16];
+  __shared__ uint32_t big;
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) big = 0;
+  uint32_t c[per], z[per], lc = 0, lz = 0, mx = 0;
+  for (int j = 0; j < per; ++j) {
+    c[j] = bcount[t * per + j];
+    z[j] = bsize[t * per + j];
+    lc += c[j];
+    lz += z[j];
+    mx = c[j] > mx ? c[j] : mx;
+    bfill[t * per + j] = 0;
+  }
+  uint32_t ic = lc, iz = lz;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d);
+    if (lane >= d) {
+      ic += oc;
+      iz += oz;
+    }
+  }
+  if (lane == 63) {
+    wc[w] = ic;
+    wsz[w] = iz;
+  }
+  __syncthreads();
+  if (mx > kBigBin) atomicOr(&big, 1u);
+  uint32_t bc = 0, bz = 0, tc = 0, tz = 0;
+  for (int i = 0; i < 16; ++i) {
+    if (i < w) {
+      bc += wc[i];
+      bz += wsz[i];
+    }
+    tc += wc[i];
+    tz += wsz[i];
+  }
+  uint32_t oc = bc + ic - lc, oz = bz + iz - lz;
+  for (int j = 0; j < per; ++j) {
+    boff[t * per + j] = oc;
+    bsoff[t * per + j] = oz;
+    oc += c[j];
+    oz += z[j];
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (ctl->overflow) return;
+    if (big) {
+      ctl->overflow = 2;  // skewed bins: redo through the radix-sort path
+      sel->n_entries = 0;
+      return;
+    }
+    uint32_t k_rem = k_left(ctl);
+    uint32_t n = sel->n_entries;
+    (void)tc;
+    sel->n_dec_phase = tz < k_rem ? tz : k_rem;
+    sel->terminal = (PH == 1 && tz < k_rem) ? 1 : 0;
+    if (n == 0) sel->terminal = (PH == 1 && k_rem > 0) ? 1 : 0;
+  }
+}
+
+__global__ void k_bucket(const Sel* sel, const Ctl* ctl, uint32_t cap1,
+                         uint32_t cap2, const uint32_t* ebin,
+                         const uint32_t* boff, uint32_t* bfill,
+                         uint32_t* bucketed) {
+  if (ctl->overflow) return;
+  uint32_t nc = sel->n_cand, nx = sel->n_extra;
+  uint32_t E = cap1 + cap2;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += gridDim.x * blockDim.x) {
+    bool real = e < nc || (e >= cap1 && e < cap1 + nx);
+    if (!real) continue;
+    uint32_t b = ebin[e];
+    bucketed[boff[b] + atomicAdd(&bfill[b], 1u)] = e;
+  }
+}
+
+// rank within the bin by the full order; decide.
+template <int PH>
+__global__ void k_rank(Sel* sel, const Ctl* ctl, const uint32_t* bucketed,
+                       const uint32_t* ebin, const uint32_t* boff,
+                       const uint32_t* bcount, const uint32_t* bsoff,
+                       const uint64_t* eokey, const uint32_t* eslot,
+                       const uint32_t* eseq, const uint32_t* erun,
+                       uint32_t* eoff, uint8_t* etie, uint32_t* applied) {
+  if (ctl->overflow) return;
+  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += gridDim.x * blockDim.x) {
+    uint32_t e = bucketed[p];
+    uint32_t b = ebin[e];
+    uint32_t lo = boff[b], hi = lo + bcount[b];
+    uint64_t ke = eokey[e];
+    uint32_t se = eslot[e], qe = eseq[e];
+    uint32_t rank = lo, goff = bsoff[b];
+    bool tie = false;
+    for (uint32_t q = lo; q < hi; ++q) {
+      uint32_t f = bucketed[q];
+      if (f == e) continue;
+      uint64_t kf = eokey[f];
+      uint32_t sf = eslot[f];
+      bool less = kf < ke || (kf == ke && (sf < se || (sf == se && eseq[f] < qe)));
+      if (less) {
+        ++rank;
+        goff += PH == 0 ? 1u : 1u + erun[f];
+      }
+      if (kf == ke && sf != se) tie = true;
+    }
+    uint32_t size = PH == 0 ? 1u : 1u + erun[e];
+    if (goff < k_rem) {
+      eoff[e] = n_dec + goff;
+      etie[e] = tie ? 1 : 0;
+      uint32_t na = size < k_rem - goff ? size : k_rem - goff;
+      atomicAdd(&applied[se], na);
+      if (PH == 1 && (goff + size >= k_rem || rank == n - 1)) {
+        // the last applied group: its priority pop is this phase's last
+        // limit-scanning pull
+        sel->g_last = n_dec + goff;
+        sel->n_prio_groups = rank + 1;
+      }
+    } else {
+      eoff[e] = kNone;
+    }
+  }
+}
+
 struct ApplyVisit {
   dmc_decision* out;
   const uint32_t* eoff;
@@ -874,7 +1084,13 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
                         const Ctl* ctl, const uint32_t* cand,
                         const uint32_t* cxbase, uint32_t cap1,
                         const uint32_t* eoff, const uint8_t* etie,
-                        uint32_t* applied, dmc_decision* out) {
+                        uint32_t* applied, dmc_decision* out, uint32_t* bcount,
+                        uint32_t* bsize) {
+  if (blockIdx.x == 0)  // the bin-rank counters are consumed: reset them
+    for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
+      bcount[b] = 0;
+      bsize[b] = 0;
+    }
   if (ctl->overflow || sel->n_entries == 0) return;
   uint32_t nc = sel->n_cand;
   uint32_t g_last = sel->g_last;
@@ -1321,6 +1537,11 @@ struct dmc_queue {
   // entry capacities per phase: [0] first entries (= candidates), [1] extras
   uint32_t cap_hint[2][2] = {{4096, 4096}, {4096, 4096}};
   uint32_t* cand = nullptr;    // N
+  bool use_radix = false;      // rank entries with the radix sort (fallback)
+  bool force_radix = false;    // DMC_OPT_FORCE_RADIX
+  uint32_t radix_batches = 0;  // batches left on the fallback path
+  uint32_t *ebin = nullptr, *bcount = nullptr, *bsize = nullptr;
+  uint32_t *boff = nullptr, *bsoff = nullptr, *bfill = nullptr;
   uint32_t* cxbase = nullptr;  // N
   uint64_t* emax = nullptr;    // N / kBlock + 1
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
@@ -1410,6 +1631,8 @@ int ensure_entries(dmc_queue* q, uint32_t n) {
   HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->etie, cap));
+  dfree(q->ebin);
+  HIP_OK(hipMalloc(&q->ebin, sizeof(uint32_t) * cap));
   q->ecap = cap;
   size_t t1 = 0, t2 = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
@@ -1550,47 +1773,76 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
                      cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
                      q->emax);
   pe(q);
-  pb(q, S0 + 4);
-  hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
-                     q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
-                     (const uint64_t*)q->eokey, q->ek32, q->eval);
-  pe(q);
-  pb(q, S0 + 5);
-  size_t tbytes = q->temp_bytes;
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
-                                            q->eval, q->sval, (int)E, 0, 32,
-                                            q->stream));
-  hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
-                     (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
-                     (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
-                     (const uint32_t*)q->eseq);
-  pe(q);
-  pb(q, S0 + 6);
-  if (PH == 0) {
-    hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                       (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                       q->eoff, q->etie, q->applied, q->sel);
+  if (!q->use_radix) {
+    uint32_t gB = grid_for(E, 256);
+    pb(q, S0 + 4);
+    hipLaunchKernelGGL(k_bin<PH>, dim3(gB), dim3(kBlock), 0, q->stream, q->sel,
+                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
+                       (const uint64_t*)q->eokey, (const uint32_t*)q->erun,
+                       q->ebin, q->bcount, q->bsize);
+    pe(q);
+    pb(q, S0 + 5);
+    hipLaunchKernelGGL(k_bscan<PH>, dim3(1), dim3(1024), 0, q->stream, q->sel,
+                       q->ctl, (const uint32_t*)q->bcount,
+                       (const uint32_t*)q->bsize, q->boff, q->bsoff, q->bfill);
+    hipLaunchKernelGGL(k_bucket, dim3(gB), dim3(kBlock), 0, q->stream,
+                       (const Sel*)q->sel, (const Ctl*)q->ctl, cap1, cap2,
+                       (const uint32_t*)q->ebin, (const uint32_t*)q->boff,
+                       q->bfill, q->sval);
+    pe(q);
+    pb(q, S0 + 6);
+    hipLaunchKernelGGL(k_rank<PH>, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
+                       (const Ctl*)q->ctl, (const uint32_t*)q->sval,
+                       (const uint32_t*)q->ebin, (const uint32_t*)q->boff,
+                       (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
+                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
+                       (const uint32_t*)q->eseq, (const uint32_t*)q->erun, q->eoff,
+                       q->etie, q->applied);
+    pe(q);
   } else {
-    hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const Sel*)q->sel, E,
-                       (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
-    tbytes = q->temp_bytes;
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
-                                            (int)E, q->stream));
-    hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                       (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                       (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
-                       q->etie, q->applied, q->sel);
+    pb(q, S0 + 4);
+    hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
+                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
+                       (const uint64_t*)q->eokey, q->ek32, q->eval);
+    pe(q);
+    pb(q, S0 + 5);
+    size_t tbytes = q->temp_bytes;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
+                                              q->eval, q->sval, (int)E, 0, 32,
+                                              q->stream));
+    hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
+                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
+                       (const uint32_t*)q->eseq);
+    pe(q);
+    pb(q, S0 + 6);
+    if (PH == 0) {
+      hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                         q->eoff, q->etie, q->applied, q->sel);
+    } else {
+      hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const Sel*)q->sel, E,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
+      tbytes = q->temp_bytes;
+      HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
+                                              (int)E, q->stream));
+      hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                         (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
+                         q->etie, q->applied, q->sel);
+    }
+    pe(q);
   }
-  pe(q);
   pb(q, S0 + 7);
   hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
                      q->stream, tb, now, q->tick, (const Sel*)q->sel,
                      (const Ctl*)q->ctl, (const uint32_t*)q->cand,
                      (const uint32_t*)q->cxbase, cap1, (const uint32_t*)q->eoff,
-                     (const uint8_t*)q->etie, q->applied, d_out);
+                     (const uint8_t*)q->etie, q->applied, d_out, q->bcount,
+                     q->bsize);
   pe(q);
   hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
                      (const Sel*)q->sel, q->ctl, q->sched);
@@ -1671,6 +1923,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       int rc = ensure_entries(q, cap1[ph] + cap2[ph]);
       if (rc) return rc;
     }
+    q->use_radix = q->force_radix || q->radix_batches > 0;
+    if (q->radix_batches) --q->radix_batches;
     hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk);
     int rc = launch_phase<0>(q, now, cap1[0], cap2[0], d_out + n_dec);
     if (rc) return rc;
@@ -1693,6 +1947,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
         h = want > h ? want : std::max(want, h / 2);  // grow at once, shrink slowly
       }
     }
+    if (c.overflow == 2) q->radix_batches = 8;  // skewed keys: sort instead
     if (c.overflow) continue;  // state before the overflowing phase is intact
     if (n_dec >= k || !c.terminal) break;
     if (allow) {
@@ -1785,6 +2040,11 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->ctl, 1);
   rc |= A(&q->parts, 4096);
   rc |= A(&q->cand, N);
+  rc |= A(&q->bcount, kNB);
+  rc |= A(&q->bsize, kNB);
+  rc |= A(&q->boff, kNB);
+  rc |= A(&q->bsoff, kNB);
+  rc |= A(&q->bfill, kNB);
   rc |= A(&q->cxbase, N);
   rc |= A(&q->emax, N / kBlock + 2);
   rc |= A(&q->act_min, 1);
@@ -1824,7 +2084,8 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->ek32, q->sk32, q->eval, q->sval, q->eslot, q->erun, q->eseq,
                   q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
                   q->skeys, q->svals, q->d_dec, q->temp, q->ctl,
-                  q->parts, q->cand, q->cxbase, q->emax};
+                  q->parts, q->cand, q->cxbase, q->emax, q->ebin, q->bcount,
+                  q->bsize, q->boff, q->bsoff, q->bfill};
   for (void* p : ptrs)
     dfree(p);
   for (auto& r : q->prof_pool) {
@@ -2157,6 +2418,22 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
     if (keep[i]) kept.push_back(ents[i]);
   if (kept.size() == ents.size()) return DMC_OK;
   return write_queue(q, slot, kept, n > 0 && keep[0]);
+}
+
+int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
+  if (!q) return DMC_EINVAL;
+  std::lock_guard<std::mutex> g(q->mtx);
+  switch (option) {
+    case DMC_OPT_SMALL_K:
+      if (value < 0) return DMC_EINVAL;
+      q->small_k = (uint32_t)value;
+      return DMC_OK;
+    case DMC_OPT_FORCE_RADIX:
+      q->force_radix = value != 0;
+      return DMC_OK;
+    default:
+      return DMC_EINVAL;
+  }
 }
 
 int dmc_profile_enable(dmc_queue* q, int on) {

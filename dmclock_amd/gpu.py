@@ -50,6 +50,7 @@ EXPORTS = {
     "dmc_client_requests": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
     "dmc_client_filter": (_i32, [_vp, _u32, _u32, _vp]),
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
+    "dmc_queue_set_option": (_i32, [_vp, _i32, ctypes.c_int64]),
     "dmc_profile_enable": (_i32, [_vp, _i32]),
     "dmc_profile_reset": (_i32, [_vp]),
     "dmc_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),
@@ -237,6 +238,10 @@ class GpuQueue:
 
     def stream(self):
         return self.L.dmc_queue_stream(self.h)
+
+    def set_option(self, option, value):
+        _check(self.L.dmc_queue_set_option(self.h, option, int(value)),
+               "set_option")
 
     # ---- stage timers (HIP events on the queue's stream)
     def profile(self, on=True):

@@ -211,6 +211,14 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep);
 int dmc_stats_get(dmc_queue* q, dmc_stats* out);
 
+/* ------------------------------------------------------------ tuning
+ * Engine options (no reference counterpart): pulls with k <= SMALL_K run one
+ * general do_next_request at a time (default 8); FORCE_RADIX ranks batched
+ * pulls with a radix sort instead of the bin-rank pass (both exact). */
+#define DMC_OPT_SMALL_K 1
+#define DMC_OPT_FORCE_RADIX 2
+int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
+
 /* ------------------------------------------------------------ profiling
  * Stage timers: HIP events recorded on the queue's stream around each stage
  * of the add and pull pipelines (an extension of this library; the reference

@@ -26,6 +26,23 @@ def mk_gpu(**kw):
     return GpuQueue(**kw)
 
 
+def mk_variant(variant):
+    """engine paths: default (bin-rank batches, single steps for k <= 8),
+    radix-sorted batches, and single steps for every pull"""
+    from dmclock_amd._abi import OPT_FORCE_RADIX, OPT_SMALL_K
+
+    def mk(**kw):
+        q = mk_gpu(**kw)
+        if variant == "radix":
+            q.set_option(OPT_FORCE_RADIX, 1)
+        elif variant == "steps":
+            q.set_option(OPT_SMALL_K, 1 << 30)
+        elif variant == "batched":
+            q.set_option(OPT_SMALL_K, 0)
+        return q
+    return mk
+
+
 @pytest.mark.parametrize("kat", kats.SERVER_KATS, ids=lambda f: f.__name__)
 def test_server_kat_gpu(kat):
     kat(mk_gpu)
@@ -48,6 +65,17 @@ def test_steady_trace_parity(mode, seed):
                                 k_choices=[1, 2, 7, 40, 150, 600, 5000])
     n, _, _ = run_parity(tr, mk_gpu, mode)
     assert n > 500
+
+
+@pytest.mark.parametrize("variant", ["radix", "steps", "batched"])
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "-".join(
+    f"{k}={v}" for k, v in m.items()))
+def test_engine_paths_parity(mode, variant):
+    """The three ways the engine answers pulls give the same decisions."""
+    tr = workloads.steady_trace(3, 200, 8, 150, 120, depth=2,
+                                delta_rho="random",
+                                k_choices=[1, 3, 9, 64, 120, 2000])
+    run_parity(tr, mk_variant(variant), mode)
 
 
 @pytest.mark.parametrize("mode", MODES[:2], ids=["imm", "delayed"])
