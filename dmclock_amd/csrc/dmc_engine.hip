@@ -58,6 +58,8 @@ struct Sel {
   uint32_t g_last;      // last priority (limit-scan) pull index, kNone if none
   uint32_t terminal;    // 1 if this phase ended the batch early
   uint32_t n_prio_groups; // priority pops applied by phase P
+  uint32_t hshift;      // histogram bin of key k: (k - kmin) >> hshift
+  uint32_t tbin;        // histogram bin holding T (last bin of the rank table)
 };
 
 // Per-pull-batch control block (device resident): the batched phases read
@@ -446,7 +448,7 @@ k_hist(uint32_t n, const uint64_t* keys, const ScanPart* parts,
   uint32_t k_rem = k_left(ctl);
   if (k_rem == 0) return;
   ScanPart tot = reduce_parts(parts, nparts);
-  if (tot.cnt <= k_rem) return;
+  if (tot.cnt == 0) return;  // (also feeds the rank bins when cnt <= k_rem)
   __shared__ uint32_t sh[kHistBins];
   __shared__ unsigned long long smx[kHistBins];
   for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
@@ -476,18 +478,45 @@ k_hist(uint32_t n, const uint64_t* keys, const ScanPart* parts,
 // Threshold T: every key <= T is a candidate and at least k_rem eligible
 // fronts are <= T (T is the largest key of the bin holding the k_rem-th
 // smallest), or everything when no more than k_rem are eligible.  Also
-// (re)initialises the phase's Sel.  kPickThreads threads; each owns
-// kHistBins / kPickThreads bins.
+// (re)initialises the phase's Sel and builds the rank-bin table: the kNB rank
+// bins are spread over the histogram bins up to T's bin in proportion to
+// their counts (each gets 1 + its share), so that the rank bins stay small
+// however the keys are distributed (the rank pass is quadratic per bin).
+// kPickThreads threads; each owns kHistBins / kPickThreads bins.
+constexpr int kNB = 4096;  // rank bins
 constexpr int kPickThreads = 1024;
 constexpr int kBinsPerThread = kHistBins / kPickThreads;
+__device__ inline uint32_t block_excl_scan_1024(uint32_t v, uint32_t* wsum,
+                                                uint32_t* total) {
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t incl = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, tot = 0;
+  for (int i = 0; i < kPickThreads / 64; ++i) {
+    if (i < w) wbase += wsum[i];
+    tot += wsum[i];
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return wbase + incl - v;
+}
+
 __global__ void __launch_bounds__(kPickThreads)
 k_pick(const ScanPart* parts, uint32_t nparts, Sel* sel, const Ctl* ctl,
-       uint32_t* hist, uint64_t* hmax, uint32_t phase) {
+       uint32_t* hist, uint64_t* hmax, uint32_t phase, uint32_t* sbase,
+       uint32_t* snum) {
   __shared__ uint32_t wsum[kPickThreads / 64];
+  __shared__ uint32_t s_tb, s_C;
   uint32_t k_rem = k_left(ctl);
   ScanPart tot = reduce_parts(parts, nparts);
   uint32_t ne = k_rem ? tot.cnt : 0;
   int t = threadIdx.x;
+  uint32_t sh1 = hist_shift(tot.mx - tot.mn);
   if (t == 0) {
     Sel z{};
     z.n_elig = ne;
@@ -496,7 +525,11 @@ k_pick(const ScanPart* parts, uint32_t nparts, Sel* sel, const Ctl* ctl,
     z.kmax = tot.mx;
     z.g_last = kNone;
     z.T = (k_rem == 0 || ne == 0) ? 0 : kMaxKey - 1;
+    z.hshift = sh1;
+    z.tbin = ne ? (uint32_t)((tot.mx - tot.mn) >> sh1) : 0;
     *sel = z;
+    s_tb = z.tbin;
+    s_C = 0;
   }
   uint32_t h[kBinsPerThread];
   uint32_t local = 0;
@@ -504,32 +537,61 @@ k_pick(const ScanPart* parts, uint32_t nparts, Sel* sel, const Ctl* ctl,
     h[j] = hist[t * kBinsPerThread + j];
     local += h[j];
   }
-  uint32_t incl = local;
-  int lane = t & 63, w = t >> 6;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (int i = 0; i < w; ++i) wbase += wsum[i];
-  uint32_t before = wbase + incl - local;  // exclusive prefix
+  uint32_t before = block_excl_scan_1024(local, wsum, nullptr);
   if (k_rem && ne > k_rem && before < k_rem && before + local >= k_rem) {
     uint32_t cum = before;
     for (int j = 0; j < kBinsPerThread; ++j) {
       cum += h[j];
       if (cum >= k_rem) {
         sel->T = hmax[t * kBinsPerThread + j];
+        sel->tbin = t * kBinsPerThread + j;
+        s_tb = t * kBinsPerThread + j;
         break;
       }
     }
   }
   __syncthreads();
-  for (int j = 0; j < kBinsPerThread; ++j) {
-    hist[t * kBinsPerThread + j] = 0;
-    hmax[t * kBinsPerThread + j] = 0;
+  uint32_t tb = s_tb;
+  {
+    uint32_t cum = before;
+    for (int j = 0; j < kBinsPerThread; ++j) {
+      cum += h[j];
+      if ((uint32_t)(t * kBinsPerThread + j) == tb) s_C = cum;
+    }
   }
+  __syncthreads();
+  uint32_t C = s_C > 0 ? s_C : 1;
+  uint32_t S = kNB - (tb + 1);
+  uint32_t ns[kBinsPerThread], lns = 0;
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    uint32_t b = t * kBinsPerThread + j;
+    ns[j] = b <= tb ? 1u + (uint32_t)((uint64_t)h[j] * S / C) : 0u;
+    lns += ns[j];
+  }
+  uint32_t nb = block_excl_scan_1024(lns, wsum, nullptr);
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    uint32_t b = t * kBinsPerThread + j;
+    sbase[b] = nb;
+    snum[b] = ns[j];
+    nb += ns[j];
+    hist[b] = 0;
+    hmax[b] = 0;
+  }
+}
+
+// Rank bin of an entry key (monotone in the key): its histogram bin's share
+// of the kNB rank bins, split linearly (k_pick's table).
+__device__ inline uint32_t rank_bin(uint64_t k, uint64_t kmin, uint32_t sh1,
+                                    uint32_t tb, const uint32_t* sbase,
+                                    const uint32_t* snum) {
+  uint64_t d = k > kmin ? k - kmin : 0;
+  uint64_t hb = d >> sh1;
+  uint32_t h = hb > tb ? tb : (uint32_t)hb;
+  uint64_t lo = d - ((uint64_t)h << sh1);
+  uint32_t ns = snum[h];
+  uint64_t sub = sh1 <= 51 ? (lo * ns) >> sh1 : ((lo >> 12) * ns) >> (sh1 - 12);
+  if (sub >= ns) sub = ns - 1;
+  return sbase[h] + (uint32_t)sub;
 }
 
 // Candidates = slots whose key <= T, compacted (any order: the final order
@@ -832,47 +894,24 @@ __global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
 // group-size prefix (P) and the tie flag, and decides.  A bin with more than
 // kBigBin entries aborts the batch (ctl->overflow = 2); the host then redoes
 // it through the radix-sort path.
-constexpr int kNB = 4096;
 constexpr uint32_t kBigBin = 2048;
-
-__device__ inline uint64_t emax_reduce(const uint64_t* emax, uint32_t nemax,
-                                       uint32_t nc) {
-  __shared__ unsigned long long sh[kBlock];
-  uint64_t m = 0;
-  uint32_t nb = (nc + kBlock - 1) / kBlock;  // emit blocks that ran
-  if (nb < nemax) nemax = nb;
-  for (uint32_t b = threadIdx.x; b < nemax; b += blockDim.x)
-    m = emax[b] > m ? emax[b] : m;
-  sh[threadIdx.x] = m;
-  __syncthreads();
-  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d && sh[threadIdx.x + d] > sh[threadIdx.x])
-      sh[threadIdx.x] = sh[threadIdx.x + d];
-    __syncthreads();
-  }
-  uint64_t r = sh[0];
-  __syncthreads();
-  return r;
-}
 
 template <int PH>
 __global__ void k_bin(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
-                      const uint64_t* emax, uint32_t nemax,
+                      const uint32_t* sbase_g, const uint32_t* snum_g,
                       const uint64_t* eokey, const uint32_t* erun,
                       uint32_t* ebin, uint32_t* bcount, uint32_t* bsize) {
   __shared__ uint32_t sc[kNB];
   __shared__ uint32_t ss[kNB];
+  __shared__ uint32_t sbase[kHistBins], snum[kHistBins];
   uint32_t nc = sel->n_cand, nx = sel->n_extra;
   bool ovf = ctl->overflow || nc > cap1 || nx > cap2;
   uint64_t kmin = sel->kmin;
-  uint64_t mx = emax_reduce(emax, nemax, nc);
-  uint64_t range = mx > kmin ? mx - kmin : 0;
-  uint32_t shift = 0;
-  while ((range >> shift) >= (uint64_t)kNB) ++shift;
+  uint32_t sh1 = sel->hshift, tb = sel->tbin;
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid == 0) {
     sel->n_entries = ovf ? 0 : nc + nx;
-    sel->shift = shift;
+    sel->shift = 0;
     ctl->nc[PH] = nc;
     ctl->nx[PH] = nx;
     if (ovf && !ctl->overflow) ctl->overflow = 1;
@@ -882,14 +921,16 @@ __global__ void k_bin(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
     sc[b] = 0;
     ss[b] = 0;
   }
+  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+    sbase[b] = sbase_g[b];
+    snum[b] = snum_g[b];
+  }
   __syncthreads();
   uint32_t E = cap1 + cap2;
   for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
     bool real = e < nc || (e >= cap1 && e < cap1 + nx);
     if (!real) continue;
-    uint64_t k = eokey[e];
-    uint32_t b = k > kmin ? (uint32_t)((k - kmin) >> shift) : 0u;
-    if (b >= (uint32_t)kNB) b = kNB - 1;
+    uint32_t b = rank_bin(eokey[e], kmin, sh1, tb, sbase, snum);
     ebin[e] = b;
     atomicAdd(&sc[b], 1u);
     atomicAdd(&ss[b], PH == 0 ? 1u : 1u + erun[e]);
@@ -1506,6 +1547,7 @@ struct dmc_queue {
   uint32_t* applied = nullptr;// N
   uint32_t* hist = nullptr;
   uint64_t* hmax = nullptr;
+  uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin table (k_pick)
   Sel* sel = nullptr;
   StepRed* red = nullptr;     // step partials (grid) + future record
   StepCtl* sctl = nullptr;
@@ -1761,7 +1803,7 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
                      (const Ctl*)q->ctl, q->hist, q->hmax);
   hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream,
                      (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl,
-                     q->hist, q->hmax, (uint32_t)PH);
+                     q->hist, q->hmax, (uint32_t)PH, q->sbase, q->snum);
   pe(q);
   pb(q, S0 + 2);
   hipLaunchKernelGGL(k_cand, dim3(kCandBlocks), dim3(kBlock), 0, q->stream, N,
@@ -1777,7 +1819,8 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
     uint32_t gB = grid_for(E, 256);
     pb(q, S0 + 4);
     hipLaunchKernelGGL(k_bin<PH>, dim3(gB), dim3(kBlock), 0, q->stream, q->sel,
-                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
+                       q->ctl, cap1, cap2, (const uint32_t*)q->sbase,
+                       (const uint32_t*)q->snum,
                        (const uint64_t*)q->eokey, (const uint32_t*)q->erun,
                        q->ebin, q->bcount, q->bsize);
     pe(q);
@@ -2033,6 +2076,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->keys, N); rc |= A(&q->cnt, N); rc |= A(&q->off, N);
   rc |= A(&q->applied, N);
   rc |= A(&q->hist, kHistBins); rc |= A(&q->hmax, kHistBins);
+  rc |= A(&q->sbase, kHistBins); rc |= A(&q->snum, kHistBins);
   rc |= A(&q->sel, 1);
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
@@ -2079,7 +2123,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.prev_r, t.prev_p, t.prev_l, t.prev_arr, t.r_inv, t.w_inv,
                   t.l_inv, t.pd, t.front_r, t.front_p, t.front_l, t.head,
                   t.count, t.cur_delta, t.cur_rho, t.last_tick, t.flags, t.ring,
-                  q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sel,
+                  q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sbase, q->snum, q->sel,
                   q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->eokey,
                   q->ek32, q->sk32, q->eval, q->sval, q->eslot, q->erun, q->eseq,
                   q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,

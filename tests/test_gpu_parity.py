@@ -138,3 +138,38 @@ def test_edge_empty_and_none():
         if rg.next_type == 1:
             assert np.float64(rg.when).view(np.uint64) == \
                 np.float64(ro.when).view(np.uint64)
+
+
+def bench_shaped_trace(seed, n_clients, n_steps, batch, depth=4):
+    """bench.py's workload (BASELINE config 3) at a reduced client count:
+    bulk-registered clients, `depth` requests per client, a settle pull of
+    depth/2 per client at the pre-population's end, then steps of `batch`
+    adds + `batch` pulls.  Its priority keys are heavily skewed (a dense
+    cluster just above the reservation backlog), which is what the rank-bin
+    table of k_pick exists for."""
+    rng = np.random.default_rng(seed)
+    tab = workloads.client_table(rng, n_clients)
+    rate = 2.0 * n_clients
+    tr = workloads.Trace(tab, params=dict(seed=seed))
+    pre = workloads.arrivals(rng, n_clients, depth * n_clients, 1.0, rate)
+    t = float(pre["time"][-1])
+    tr.ops.append(("add", pre))
+    tr.ops.append(("pull", t, depth * n_clients // 2))
+    h = len(pre)
+    for _ in range(n_steps):
+        reqs = workloads.arrivals(rng, n_clients, batch, t, rate,
+                                  handle_base=h)
+        h += batch
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+        tr.ops.append(("pull", t, batch))
+    return tr
+
+
+@pytest.mark.parametrize("variant", ["default", "radix"])
+def test_bench_shaped_parity(variant):
+    """The benchmark's own key distributions, 64K clients, bit-exact."""
+    tr = bench_shaped_trace(42, 1 << 16, 4, 1 << 12)
+    n, qg, qo = run_parity(tr, mk_variant(variant),
+                           dict(at_limit=AT_LIMIT_WAIT), state_sample=256)
+    assert n > 100000
