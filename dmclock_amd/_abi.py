@@ -31,6 +31,7 @@ NEXT_NONE = 2
 # engine options (dmc_queue_set_option)
 OPT_SMALL_K = 1
 OPT_FORCE_RADIX = 2
+OPT_GRAPHS = 3
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0

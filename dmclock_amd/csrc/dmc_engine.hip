@@ -75,6 +75,10 @@ struct Ctl {
   uint32_t next_type;  // DMC_NEXT_* of the stopping pull
   uint32_t pad;
   double when;
+  // per-call parameters, written by k_ctl_init (the graph's parameter node)
+  double now;
+  dmc_decision* out;
+  uint64_t tick;
 };
 
 struct ScanPart {
@@ -354,9 +358,10 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
 // Per-block partials (count, min, max) go to `parts`: no same-address
 // atomics (thousands of waves hitting one word serialise at the memory side).
 template <int PH>
-__global__ void k_scan(Table tb, double now, uint64_t* keys, ScanPart* parts,
+__global__ void k_scan(Table tb, uint64_t* keys, ScanPart* parts,
                        const Ctl* ctl) {
   if (k_left(ctl) == 0) return;
+  const double now = ctl->now;
   uint32_t cnt = 0;
   uint64_t mn = kMaxKey, mx = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
@@ -673,7 +678,7 @@ struct EmitVisit {
 // emit (key, slot, seq, run).  Per-block max key goes to emax[] for the
 // 32-bit sort-key scaling.
 template <int PH>
-__global__ void k_emit(Table tb, double now, Sel* sel, const Ctl* ctl,
+__global__ void k_emit(Table tb, Sel* sel, const Ctl* ctl,
                        const uint32_t* cand, uint32_t cap1, uint32_t cap2,
                        uint32_t* cxbase, uint64_t* eokey, uint32_t* eslot,
                        uint32_t* eseq, uint32_t* erun, uint64_t* emax) {
@@ -682,6 +687,7 @@ __global__ void k_emit(Table tb, double now, Sel* sel, const Ctl* ctl,
   __shared__ unsigned long long bmax;
   uint32_t nc = sel->n_cand;
   if (blockIdx.x * blockDim.x >= nc || ctl->overflow) return;
+  const double now = ctl->now;
   uint64_t T = sel->T;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t s = i < nc ? cand[i] : 0;
@@ -1121,18 +1127,20 @@ struct ApplyVisit {
 // and the front's ready flag (set iff a later limit scan saw it with
 // limit <= now).
 template <int PH>
-__global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
-                        const Ctl* ctl, const uint32_t* cand,
-                        const uint32_t* cxbase, uint32_t cap1,
-                        const uint32_t* eoff, const uint8_t* etie,
-                        uint32_t* applied, dmc_decision* out, uint32_t* bcount,
-                        uint32_t* bsize) {
+__global__ void k_apply(Table tb, const Sel* sel, const Ctl* ctl,
+                        const uint32_t* cand, const uint32_t* cxbase,
+                        uint32_t cap1, const uint32_t* eoff,
+                        const uint8_t* etie, uint32_t* applied,
+                        uint32_t* bcount, uint32_t* bsize) {
   if (blockIdx.x == 0)  // the bin-rank counters are consumed: reset them
     for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
       bcount[b] = 0;
       bsize[b] = 0;
     }
   if (ctl->overflow || sel->n_entries == 0) return;
+  const double now = ctl->now;
+  const uint64_t tick = ctl->tick;
+  dmc_decision* out = ctl->out;
   uint32_t nc = sel->n_cand;
   uint32_t g_last = sel->g_last;
   uint32_t terminal = sel->terminal;
@@ -1207,11 +1215,17 @@ __global__ void k_apply(Table tb, double now, uint64_t tick, const Sel* sel,
   }
 }
 
-__global__ void k_ctl_init(Ctl* ctl, uint32_t k_total) {
+// The first node of a pull round: its arguments are the round's per-call
+// parameters (updated in place on graph replays).
+__global__ void k_ctl_init(Ctl* ctl, uint32_t k_total, double now,
+                           dmc_decision* out, uint64_t tick) {
   if (threadIdx.x || blockIdx.x) return;
   Ctl c{};
   c.k_total = k_total;
   c.next_type = DMC_NEXT_RETURNING;
+  c.now = now;
+  c.out = out;
+  c.tick = tick;
   *ctl = c;
 }
 
@@ -1243,6 +1257,7 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
                             const Ctl* ctl) {
   // as the terminal pull of a batch: only if the batch ran out of work
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
+  if (ctl) now = ctl->now;
   ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
   uint64_t lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nrd = 0, nnr = 0;
@@ -1321,6 +1336,7 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
                               int at_limit, uint32_t nregistered,
                               StepCtl* sc, Ctl* ctl) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
+  if (ctl) now = ctl->now;
   __shared__ StepRed sh[kBlock];
   StepRed acc;
   acc.r = ArgMin{kMaxKey, kNone, 0};
@@ -1530,6 +1546,15 @@ uint32_t grid_for(uint32_t n, uint32_t cap = 4096) {
 }  // namespace
 
 // ====================================================================== host
+struct GraphRec {
+  uint64_t key = 0;
+  uint64_t last_use = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipGraphNode_t param_node = nullptr;
+  hipKernelNodeParams kp{};
+};
+
 struct dmc_queue {
   dmc_queue_params p{};
   hipStream_t stream = nullptr;
@@ -1586,6 +1611,12 @@ struct dmc_queue {
   uint32_t *boff = nullptr, *bsoff = nullptr, *bfill = nullptr;
   uint32_t* cxbase = nullptr;  // N
   uint64_t* emax = nullptr;    // N / kBlock + 1
+  // captured pull rounds / add segments (see launch_round)
+  bool use_graphs = true;
+  std::vector<GraphRec> graphs = std::vector<GraphRec>(8);
+  std::vector<uint64_t> graph_seen = std::vector<uint64_t>(8, 0);
+  uint32_t graph_seen_pos = 0;
+  uint64_t graph_clock = 0;
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
   struct ProfRec {
     hipEvent_t a, b;
@@ -1645,8 +1676,16 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
+void graph_destroy(GraphRec& g);
+
+// Buffers captured into graphs are about to move: drop every graph.
+void invalidate_graphs(dmc_queue* q) {
+  for (auto& g : q->graphs) graph_destroy(g);
+}
+
 int ensure_temp(dmc_queue* q, size_t need) {
   if (need <= q->temp_bytes) return DMC_OK;
+  invalidate_graphs(q);
   if (q->temp) dfree(q->temp);
   q->temp = nullptr;
   size_t sz = need + (need >> 2) + 4096;
@@ -1658,6 +1697,7 @@ int ensure_temp(dmc_queue* q, size_t need) {
 int ensure_entries(dmc_queue* q, uint32_t n) {
   if (n <= q->ecap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
+  invalidate_graphs(q);
   dfree(q->eokey); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
   dfree(q->sval); dfree(q->eslot); dfree(q->erun); dfree(q->eseq);
   dfree(q->eoff); dfree(q->gsz); dfree(q->goff); dfree(q->etie);
@@ -1687,6 +1727,7 @@ int ensure_entries(dmc_queue* q, uint32_t n) {
 int ensure_batch(dmc_queue* q, uint32_t n) {
   if (n <= q->bcap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n, 1024);
+  invalidate_graphs(q);
   dfree(q->d_reqs); dfree(q->d_rc); dfree(q->akeys); dfree(q->avals);
   dfree(q->skeys); dfree(q->svals);
   HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
@@ -1784,8 +1825,7 @@ uint32_t pow2_at_least(uint32_t x) {
 // capacity the sort runs over (entries beyond it set ctl->overflow and the
 // rest of the batch no-ops; the host retries with a larger capacity).
 template <int PH>
-int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
-                 dmc_decision* d_out) {
+int launch_phase(dmc_queue* q, uint32_t cap1, uint32_t cap2) {
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = grid_for(N, 2048);
@@ -1794,7 +1834,7 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
   uint32_t gC = (N + kBlock - 1) / kBlock;  // one thread per candidate
   const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
   pb(q, S0 + 0);
-  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb, now,
+  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb,
                      q->keys, q->parts, (const Ctl*)q->ctl);
   pe(q);
   pb(q, S0 + 1);
@@ -1810,7 +1850,7 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
                      (const uint64_t*)q->keys, q->sel, q->cand);
   pe(q);
   pb(q, S0 + 3);
-  hipLaunchKernelGGL(k_emit<PH>, dim3(gC), dim3(kBlock), 0, q->stream, tb, now,
+  hipLaunchKernelGGL(k_emit<PH>, dim3(gC), dim3(kBlock), 0, q->stream, tb,
                      q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand, cap1,
                      cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
                      q->emax);
@@ -1881,10 +1921,10 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
   }
   pb(q, S0 + 7);
   hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
-                     q->stream, tb, now, q->tick, (const Sel*)q->sel,
+                     q->stream, tb, (const Sel*)q->sel,
                      (const Ctl*)q->ctl, (const uint32_t*)q->cand,
                      (const uint32_t*)q->cxbase, cap1, (const uint32_t*)q->eoff,
-                     (const uint8_t*)q->etie, q->applied, d_out, q->bcount,
+                     (const uint8_t*)q->etie, q->applied, q->bcount,
                      q->bsize);
   pe(q);
   hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
@@ -1895,7 +1935,8 @@ int launch_phase(dmc_queue* q, double now, uint32_t cap1, uint32_t cap2,
 // Terminal pull of a Wait/Reject batch: one general do_next_request, which
 // (nothing being eligible) computes min_not_0 over the reservation- and
 // limit-heap tops, :1170-1185.  No-op unless ctl->terminal.
-int launch_future(dmc_queue* q, double now, Ctl* ctl) {
+int launch_future(dmc_queue* q, Ctl* ctl) {
+  const double now = 0.0;  // read from ctl by the kernels
   pb(q, DMC_PROF_FUTURE);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
                      q->tb, now, q->red, (const Ctl*)ctl);
@@ -1928,6 +1969,117 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   *type = sc.type;
   *when = sc.when;
   return DMC_OK;
+}
+
+// One pull round: k_ctl_init + phase R + phase P (+ the terminal pull).  The
+// sequence depends on the per-call parameters only through k_ctl_init's
+// arguments, so it is captured once per shape (entry capacities, ranking
+// path, terminal pull) into a hipGraph and replayed with k_ctl_init's
+// arguments updated: one graph launch instead of ~25 kernel launches, which
+// removes the host's per-launch cost from the critical path.  A shape is
+// captured the second time it is seen; profiling runs eagerly (the stage
+// timers are events between kernels).
+void enqueue_round(dmc_queue* q, uint32_t kk, double now, dmc_decision* out,
+                   const uint32_t* cap1, const uint32_t* cap2, bool future) {
+  hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk, now,
+                     out, q->tick);
+  launch_phase<0>(q, cap1[0], cap2[0]);
+  launch_phase<1>(q, cap1[1], cap2[1]);
+  if (future) launch_future(q, q->ctl);
+}
+
+int graph_replay(dmc_queue* q, GraphRec& g, void** args) {
+  hipKernelNodeParams kp = g.kp;
+  kp.kernelParams = args;
+  kp.extra = nullptr;
+  HIP_OK(hipGraphExecKernelNodeSetParams(g.exec, g.param_node, &kp));
+  HIP_OK(hipGraphLaunch(g.exec, q->stream));
+  return DMC_OK;
+}
+
+// Capture `enqueue` (which must start with the parameter kernel) as a graph.
+template <typename F>
+int graph_capture(dmc_queue* q, GraphRec& g, F enqueue) {
+  HIP_OK(hipStreamBeginCapture(q->stream, hipStreamCaptureModeThreadLocal));
+  enqueue();
+  hipGraph_t graph = nullptr;
+  HIP_OK(hipStreamEndCapture(q->stream, &graph));
+  size_t nroot = 0;
+  HIP_OK(hipGraphGetRootNodes(graph, nullptr, &nroot));
+  if (nroot != 1) {
+    (void)hipGraphDestroy(graph);
+    return DMC_EDEVICE;
+  }
+  hipGraphNode_t root;
+  HIP_OK(hipGraphGetRootNodes(graph, &root, &nroot));
+  hipGraphNodeType ty;
+  HIP_OK(hipGraphNodeGetType(root, &ty));
+  if (ty != hipGraphNodeTypeKernel) {
+    (void)hipGraphDestroy(graph);
+    return DMC_EDEVICE;
+  }
+  HIP_OK(hipGraphKernelNodeGetParams(root, &g.kp));
+  HIP_OK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+  g.graph = graph;
+  g.param_node = root;
+  return DMC_OK;
+}
+
+void graph_destroy(GraphRec& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g = GraphRec{};
+}
+
+// Find (or, on the second sighting, build) the graph for `key`; nullptr if the
+// caller should launch eagerly this time.
+template <typename F>
+GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
+  if (!q->use_graphs || q->prof_on) return nullptr;
+  for (auto& g : q->graphs)
+    if (g.exec && g.key == key) {
+      g.last_use = ++q->graph_clock;
+      return &g;
+    }
+  bool seen = false;
+  for (uint64_t k : q->graph_seen) seen |= (k == key);
+  if (!seen) {
+    q->graph_seen[q->graph_seen_pos++ % q->graph_seen.size()] = key;
+    return nullptr;
+  }
+  GraphRec* slot = &q->graphs[0];
+  for (auto& g : q->graphs)
+    if (!g.exec || g.last_use < slot->last_use) slot = &g;
+  graph_destroy(*slot);
+  if (graph_capture(q, *slot, enqueue) != DMC_OK) {
+    graph_destroy(*slot);
+    q->use_graphs = false;  // capture unsupported: stay eager
+    return nullptr;
+  }
+  slot->key = key;
+  slot->last_use = ++q->graph_clock;
+  return slot;
+}
+
+int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
+                 const uint32_t* cap1, const uint32_t* cap2, bool future) {
+  uint64_t key = 1;  // shape: capacities (powers of two), ranking path, future
+  for (int ph = 0; ph < 2; ++ph)
+    key = key * 64 + (uint64_t)__builtin_ctz(cap1[ph]),
+    key = key * 64 + (uint64_t)__builtin_ctz(cap2[ph]);
+  key = key * 4 + (q->use_radix ? 2 : 0) + (future ? 1 : 0);
+  GraphRec* g = graph_for(q, key, [&] {
+    enqueue_round(q, kk, now, out, cap1, cap2, future);
+  });
+  if (!g) {
+    enqueue_round(q, kk, now, out, cap1, cap2, future);
+    HIP_OK(hipGetLastError());
+    return DMC_OK;
+  }
+  Ctl* ctl = q->ctl;
+  uint64_t tick = q->tick;
+  void* args[] = {&ctl, &kk, &now, &out, &tick};
+  return graph_replay(q, *g, args);
 }
 
 // k successive pull_request(now).  Batched phases run with one host
@@ -1968,15 +2120,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     q->use_radix = q->force_radix || q->radix_batches > 0;
     if (q->radix_batches) --q->radix_batches;
-    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk);
-    int rc = launch_phase<0>(q, now, cap1[0], cap2[0], d_out + n_dec);
+    int rc = launch_round(q, now, kk, d_out + n_dec, cap1, cap2, !allow);
     if (rc) return rc;
-    rc = launch_phase<1>(q, now, cap1[1], cap2[1], d_out + n_dec);
-    if (rc) return rc;
-    if (!allow) {
-      rc = launch_future(q, now, q->ctl);
-      if (rc) return rc;
-    }
     Ctl c;
     HIP_OK(hipMemcpyAsync(&c, q->ctl, sizeof(c), hipMemcpyDeviceToHost, q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
@@ -2119,6 +2264,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   if (q->stream) (void)hipStreamSynchronize(q->stream);
+  invalidate_graphs(q);
   Table& t = q->tb;
   void* ptrs[] = {t.prev_r, t.prev_p, t.prev_l, t.prev_arr, t.r_inv, t.w_inv,
                   t.l_inv, t.pd, t.front_r, t.front_p, t.front_l, t.head,
@@ -2474,6 +2620,10 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_FORCE_RADIX:
       q->force_radix = value != 0;
+      return DMC_OK;
+    case DMC_OPT_GRAPHS:
+      q->use_graphs = value != 0;
+      if (!q->use_graphs) invalidate_graphs(q);
       return DMC_OK;
     default:
       return DMC_EINVAL;

@@ -217,6 +217,7 @@ int dmc_stats_get(dmc_queue* q, dmc_stats* out);
  * pulls with a radix sort instead of the bin-rank pass (both exact). */
 #define DMC_OPT_SMALL_K 1
 #define DMC_OPT_FORCE_RADIX 2
+#define DMC_OPT_GRAPHS 3       /* 0: launch every kernel eagerly (default 1: replay captured hipGraphs) */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
 /* ------------------------------------------------------------ profiling

@@ -29,7 +29,7 @@ def mk_gpu(**kw):
 def mk_variant(variant):
     """engine paths: default (bin-rank batches, single steps for k <= 8),
     radix-sorted batches, and single steps for every pull"""
-    from dmclock_amd._abi import OPT_FORCE_RADIX, OPT_SMALL_K
+    from dmclock_amd._abi import OPT_FORCE_RADIX, OPT_GRAPHS, OPT_SMALL_K
 
     def mk(**kw):
         q = mk_gpu(**kw)
@@ -39,6 +39,8 @@ def mk_variant(variant):
             q.set_option(OPT_SMALL_K, 1 << 30)
         elif variant == "batched":
             q.set_option(OPT_SMALL_K, 0)
+        elif variant == "eager":
+            q.set_option(OPT_GRAPHS, 0)
         return q
     return mk
 
@@ -67,7 +69,7 @@ def test_steady_trace_parity(mode, seed):
     assert n > 500
 
 
-@pytest.mark.parametrize("variant", ["radix", "steps", "batched"])
+@pytest.mark.parametrize("variant", ["radix", "steps", "batched", "eager"])
 @pytest.mark.parametrize("mode", MODES, ids=lambda m: "-".join(
     f"{k}={v}" for k, v in m.items()))
 def test_engine_paths_parity(mode, variant):
@@ -166,7 +168,7 @@ def bench_shaped_trace(seed, n_clients, n_steps, batch, depth=4):
     return tr
 
 
-@pytest.mark.parametrize("variant", ["default", "radix"])
+@pytest.mark.parametrize("variant", ["default", "radix", "eager"])
 def test_bench_shaped_parity(variant):
     """The benchmark's own key distributions, 64K clients, bit-exact."""
     tr = bench_shaped_trace(42, 1 << 16, 4, 1 << 12)
