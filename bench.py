@@ -44,9 +44,12 @@ STAGE_BYTES = {
     # k_cand: key 8 read per slot (candidate ids written are negligible)
     "r_cand": ("client", 8),
     "p_cand": ("client", 8),
-    # k_add_chain: request 32 + sorted (slot,pos) 8 + rc 4 + ring entry 64
-    #              + client state read 81 / written 57
-    "add_chain": ("request", 246),
+    # k_add_chain (one request per client): apos/aslot 8 + acnt 8 + abuf 4
+    #   + request 32 + rc 4 + ring entry 64 + client state read 81
+    #   (prev tag 32, inverses 24, head/count/cur_delta/cur_rho 16,
+    #   last_tick 8, flags 1) and written 77 (prev 32, count/cur_* 12,
+    #   last_tick 8, flags 1, front tag 24)
+    "add_chain": ("request", 278),
 }
 
 

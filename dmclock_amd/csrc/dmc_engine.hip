@@ -60,6 +60,7 @@ struct Sel {
   uint32_t n_prio_groups; // priority pops applied by phase P
   uint32_t hshift;      // histogram bin of key k: (k - kmin) >> hshift
   uint32_t tbin;        // histogram bin holding T (last bin of the rank table)
+  uint32_t bin_ovf;     // a rank bin outgrew kBinCap (skewed keys)
 };
 
 // Per-pull-batch control block (device resident): the batched phases read
@@ -75,7 +76,7 @@ struct Ctl {
   uint32_t next_type;  // DMC_NEXT_* of the stopping pull
   uint32_t pad;
   double when;
-  // per-call parameters, written by k_ctl_init (the graph's parameter node)
+  // per-call parameters, published by k_scan<0> (the graph's parameter node)
   double now;
   dmc_decision* out;
   uint64_t tick;
@@ -89,6 +90,16 @@ struct ScanPart {
 __device__ inline uint32_t k_left(const Ctl* c) {
   return c->overflow ? 0u : c->k_total - c->n_dec;
 }
+
+// Per-call parameters of a pull round: the arguments of its first kernel
+// (k_scan<0>, the graph's parameter node), published through Ctl.
+struct CallParams {
+  uint32_t k_total;
+  uint32_t pad;
+  double now;
+  dmc_decision* out;
+  uint64_t tick;
+};
 
 // Single-step (one do_next_request) reduction record.
 struct ArgMin {
@@ -192,112 +203,187 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
 }
 
 // ------------------------------------------------------------------ add path
-__global__ void k_add_keys(const dmc_request* reqs, uint32_t n,
-                           uint32_t* keys, uint32_t* vals) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  keys[i] = reqs[i].slot;
-  vals[i] = i;
-}
+// A batch (a run of add_request_time calls with no activation inside) is
+// grouped by client without sorting: k_add_link counts each client's requests
+// with one atomic per request and files the first kAddSlots batch positions
+// in the client's slot buffer; k_add_chain then lets one thread per client
+// replay that client's requests in batch order.  Clients with more than
+// kAddSlots requests in the batch (rare: 64K requests over 1M clients is
+// Poisson(1/16)) are replayed by a scan of the batch's slot column, in order.
+constexpr uint32_t kAddSlots = 16;
 
-// One thread per client segment of the slot-sorted batch walks that client's
-// requests in arrival order: do_add_request minus the idle reset (handled
-// before, per activation), initial_tag (:878-907), the Reject check
-// (:989-993), the enqueue and cur_rho/cur_delta (:995-1009).
-__global__ void k_add_chain(Table tb, const uint32_t* sslot,
-                            const uint32_t* spos, const dmc_request* reqs,
-                            uint32_t n, uint64_t tick_base, int32_t* rc) {
+struct AddParams {
+  const dmc_request* reqs;
+  int32_t* rc;
+  uint64_t tick_base;
+  uint32_t n;
+  uint32_t pad;
+};
+
+// The first node of an add segment: its arguments are the segment's per-call
+// parameters (updated in place on graph replays); block 0 publishes them for
+// k_add_chain.
+__global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
+                           uint32_t* abuf, uint32_t* apos, uint32_t* aslot,
+                           AddParams* pblk) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t s = sslot[i];
-  if (i > 0 && sslot[i - 1] == s) return;  // not a segment head
-  uint32_t end = i + 1;
-  while (end < n && sslot[end] == s) ++end;
-  if (s >= tb.n || !(tb.flags[s] & F_REG)) {
-    for (uint32_t j = i; j < end; ++j) rc[spos[j]] = DMC_ENOTREG;
+  if (i == 0) *pblk = p;
+  if (i >= p.n) return;
+  uint32_t s = p.reqs[i].slot;
+  aslot[i] = s;
+  if (s >= tb.n) {
+    apos[i] = kNone;
     return;
   }
-  Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
-  double rinv = tb.r_inv[s], winv = tb.w_inv[s], linv = tb.l_inv[s];
-  uint32_t head = tb.head[s], count = tb.count[s];
-  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
-  uint64_t last_tick = tb.last_tick[s];
-  uint8_t flags = tb.flags[s];
-  bool front_set = false;
-  Tag3 front{};
-  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  for (uint32_t j = i; j < end; ++j) {
-    uint32_t pos = spos[j];
-    const dmc_request rq = reqs[pos];
-    uint64_t tick = tick_base + pos + 1;  // ++tick, :918
-    if (rq.rho > rq.delta) {  // ReqParams asserts rho <= delta
-      rc[pos] = DMC_EBADPARAMS;
-      continue;
-    }
-    if (count >= tb.q) {  // documented deviation: bounded ring
-      rc[pos] = DMC_EQUEUEFULL;
-      continue;
-    }
-    Tag3 tag;
-    if (!tb.delayed || count == 0) {
-      if (!make_tag(prev, rinv, winv, linv, rq.delta, rq.rho, rq.time,
-                    rq.cost, tb.antic, &tag)) {
-        rc[pos] = DMC_EBADTAG;
-        continue;
-      }
-      // update_req_tag, :405-412
-      assign_unpinned(prev.r, tag.r);
-      assign_unpinned(prev.l, tag.l);
-      assign_unpinned(prev.p, tag.p);
-      prev.arrival = tag.arrival;
-      last_tick = tick;
-    } else {
-      if (rq.cost == 0) {
-        rc[pos] = DMC_EBADTAG;
-        continue;
-      }
-      tag = Tag3{0.0, 0.0, 0.0, rq.time};  // placeholder, :880
-    }
-    if (tb.at_limit == DMC_AT_LIMIT_REJECT &&
-        tag.l > __dadd_rn(rq.time, tb.reject_thr)) {
-      rc[pos] = DMC_EAGAIN;
-      continue;
-    }
-    ReqEntry e;
-    e.r = tag.r;
-    e.p = tag.p;
-    e.l = tag.l;
-    e.arrival = tag.arrival;
-    e.handle = rq.handle;
-    e.cost = rq.cost;
-    e.delta = (tb.delayed && count > 0) ? 0u : rq.delta;
-    e.rho = (tb.delayed && count > 0) ? 0u : rq.rho;
-    e.pad = 0;
-    e.pad2 = 0;
-    ring[(head + count) & tb.qmask] = e;
-    if (count == 0) {
-      front = tag;
-      front_set = true;
-      flags &= (uint8_t)~F_READY;  // a new tag is not ready, :155
-    }
-    ++count;
-    cd = rq.delta;
-    cr = rq.rho;
-    rc[pos] = DMC_OK;
+  uint32_t pos = atomicAdd(&acnt[s], 1u);
+  apos[i] = pos;
+  if (pos < kAddSlots) abuf[(size_t)s * kAddSlots + pos] = i;
+}
+
+// do_add_request for one client's requests of the batch, in batch order:
+// minus the idle reset (handled before, per activation), initial_tag
+// (:878-907), the Reject check (:989-993), the enqueue and cur_rho/cur_delta
+// (:995-1009).
+struct AddState {
+  Tag3 prev;
+  double rinv, winv, linv;
+  uint32_t head, count, cd, cr;
+  uint64_t last_tick;
+  uint8_t flags;
+  bool front_set;
+  Tag3 front;
+};
+
+__device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
+                               const AddParams& p, uint32_t pos) {
+  const dmc_request rq = p.reqs[pos];
+  uint64_t tick = p.tick_base + pos + 1;  // ++tick, :918
+  if (rq.rho > rq.delta) {  // ReqParams asserts rho <= delta
+    p.rc[pos] = DMC_EBADPARAMS;
+    return;
   }
-  tb.prev_r[s] = prev.r;
-  tb.prev_p[s] = prev.p;
-  tb.prev_l[s] = prev.l;
-  tb.prev_arr[s] = prev.arrival;
-  tb.count[s] = count;
-  tb.cur_delta[s] = cd;
-  tb.cur_rho[s] = cr;
-  tb.last_tick[s] = last_tick;
-  tb.flags[s] = flags;
-  if (front_set) {
-    tb.front_r[s] = front.r;
-    tb.front_p[s] = front.p;
-    tb.front_l[s] = front.l;
+  if (st.count >= tb.q) {  // documented deviation: bounded ring
+    p.rc[pos] = DMC_EQUEUEFULL;
+    return;
+  }
+  Tag3 tag;
+  if (!tb.delayed || st.count == 0) {
+    if (!make_tag(st.prev, st.rinv, st.winv, st.linv, rq.delta, rq.rho, rq.time,
+                  rq.cost, tb.antic, &tag)) {
+      p.rc[pos] = DMC_EBADTAG;
+      return;
+    }
+    // update_req_tag, :405-412
+    assign_unpinned(st.prev.r, tag.r);
+    assign_unpinned(st.prev.l, tag.l);
+    assign_unpinned(st.prev.p, tag.p);
+    st.prev.arrival = tag.arrival;
+    st.last_tick = tick;
+  } else {
+    if (rq.cost == 0) {
+      p.rc[pos] = DMC_EBADTAG;
+      return;
+    }
+    tag = Tag3{0.0, 0.0, 0.0, rq.time};  // placeholder, :880
+  }
+  if (tb.at_limit == DMC_AT_LIMIT_REJECT &&
+      tag.l > __dadd_rn(rq.time, tb.reject_thr)) {
+    p.rc[pos] = DMC_EAGAIN;
+    return;
+  }
+  ReqEntry e;
+  e.r = tag.r;
+  e.p = tag.p;
+  e.l = tag.l;
+  e.arrival = tag.arrival;
+  e.handle = rq.handle;
+  e.cost = rq.cost;
+  e.delta = (tb.delayed && st.count > 0) ? 0u : rq.delta;
+  e.rho = (tb.delayed && st.count > 0) ? 0u : rq.rho;
+  e.pad = 0;
+  e.pad2 = 0;
+  ring[(st.head + st.count) & tb.qmask] = e;
+  if (st.count == 0) {
+    st.front = tag;
+    st.front_set = true;
+    st.flags &= (uint8_t)~F_READY;  // a new tag is not ready, :155
+  }
+  ++st.count;
+  st.cd = rq.delta;
+  st.cr = rq.rho;
+  p.rc[pos] = DMC_OK;
+}
+
+__global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
+                            const uint32_t* abuf, const uint32_t* apos,
+                            const uint32_t* aslot) {
+  const AddParams p = *pblk;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  uint32_t pos0 = apos[i];
+  if (pos0 == kNone) {
+    p.rc[i] = DMC_ENOTREG;
+    return;
+  }
+  if (pos0 != 0) return;  // the client's first filer replays its requests
+  uint32_t s = aslot[i];
+  uint32_t m = acnt[s];
+  acnt[s] = 0;  // ready for the next batch
+  if (!(tb.flags[s] & F_REG)) {
+    if (m <= kAddSlots) {
+      for (uint32_t j = 0; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
+    } else {
+      for (uint32_t j = 0; j < p.n; ++j)
+        if (aslot[j] == s) p.rc[j] = DMC_ENOTREG;
+    }
+    return;
+  }
+  AddState st;
+  st.prev = Tag3{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
+  st.rinv = tb.r_inv[s];
+  st.winv = tb.w_inv[s];
+  st.linv = tb.l_inv[s];
+  st.head = tb.head[s];
+  st.count = tb.count[s];
+  st.cd = tb.cur_delta[s];
+  st.cr = tb.cur_rho[s];
+  st.last_tick = tb.last_tick[s];
+  st.flags = tb.flags[s];
+  st.front_set = false;
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  if (m == 1) {
+    add_one(tb, st, ring, p, i);
+  } else if (m <= kAddSlots) {
+    // the client's batch positions in ascending order, by repeated selection
+    // over its (L2-resident) slot-buffer row
+    const uint32_t* row = abuf + (size_t)s * kAddSlots;
+    uint32_t last = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      uint32_t next = 0xffffffffu;
+      for (uint32_t k = 0; k < m; ++k) {
+        uint32_t v = row[k];
+        if ((j == 0 || v > last) && v < next) next = v;
+      }
+      add_one(tb, st, ring, p, next);
+      last = next;
+    }
+  } else {
+    for (uint32_t j = 0; j < p.n; ++j)
+      if (aslot[j] == s) add_one(tb, st, ring, p, j);
+  }
+  tb.prev_r[s] = st.prev.r;
+  tb.prev_p[s] = st.prev.p;
+  tb.prev_l[s] = st.prev.l;
+  tb.prev_arr[s] = st.prev.arrival;
+  tb.count[s] = st.count;
+  tb.cur_delta[s] = st.cd;
+  tb.cur_rho[s] = st.cr;
+  tb.last_tick[s] = st.last_tick;
+  tb.flags[s] = st.flags;
+  if (st.front_set) {
+    tb.front_r[s] = st.front.r;
+    tb.front_p[s] = st.front.p;
+    tb.front_l[s] = st.front.l;
   }
 }
 
@@ -358,10 +444,23 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
 // Per-block partials (count, min, max) go to `parts`: no same-address
 // atomics (thousands of waves hitting one word serialise at the memory side).
 template <int PH>
-__global__ void k_scan(Table tb, uint64_t* keys, ScanPart* parts,
-                       const Ctl* ctl) {
-  if (k_left(ctl) == 0) return;
-  const double now = ctl->now;
+__global__ void k_scan(Table tb, uint64_t* keys, ScanPart* parts, Ctl* ctl,
+                       CallParams cp) {
+  if (PH == 0) {  // the round's first kernel: publish the call's parameters
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      Ctl c{};
+      c.k_total = cp.k_total;
+      c.next_type = DMC_NEXT_RETURNING;
+      c.now = cp.now;
+      c.out = cp.out;
+      c.tick = cp.tick;
+      *ctl = c;
+    }
+    if (cp.k_total == 0) return;
+  } else if (k_left(ctl) == 0) {
+    return;
+  }
+  const double now = PH == 0 ? cp.now : ctl->now;
   uint32_t cnt = 0;
   uint64_t mn = kMaxKey, mx = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
@@ -599,8 +698,82 @@ __device__ inline uint32_t rank_bin(uint64_t k, uint64_t kmin, uint32_t sh1,
   return sbase[h] + (uint32_t)sub;
 }
 
+// ------------------------------------------------------------------ pull: walks
+struct CountVisit {
+  uint32_t pops = 0, groups = 0;
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
+  __device__ void group(uint64_t, uint32_t) { ++groups; }
+};
+
+// Entry id of the j-th entry of candidate i: the first lives at i, the rest
+// in the extras region (after cap1) at the candidate's extras base.
+__device__ inline uint32_t entry_id(uint32_t i, uint32_t j, uint32_t cap1,
+                                    uint32_t xbase) {
+  return j == 0 ? i : cap1 + xbase + j - 1;
+}
+
+// Rank-bin record of one entry (bin-rank path): the full order key
+// (okey, slot, seq), the group's run (P) and the entry id.
+constexpr uint32_t kBinCap = 256;  // entries per rank bin (more: bin_ovf)
+struct BRec {
+  uint64_t okey;
+  uint32_t slot;
+  uint32_t e;
+  uint32_t seq;
+  uint32_t run;
+};
+
+struct EmitVisit {
+  uint64_t* eokey;
+  uint32_t* eslot;
+  uint32_t* eseq;
+  uint32_t* erun;
+  uint32_t i, cap1, xbase, cap2, slot;
+  int ph;
+  // bin-rank path (brec != nullptr): k_pick's rank-bin table
+  BRec* brec;
+  uint32_t* bcount;
+  uint32_t* bsize;
+  const uint32_t* sbase;
+  const uint32_t* snum;
+  uint64_t kmin;
+  uint32_t sh1, tbin;
+  Sel* sel;
+  uint32_t n = 0;
+  uint64_t kmax = 0;
+  uint32_t q = 0;  // bin-rank path: entry id = candidate * q + n
+  __device__ void put(uint64_t key, uint32_t run) {
+    if (brec) {
+      if (i < cap1) {
+        uint32_t e = i * q + n;
+        uint32_t b = rank_bin(key, kmin, sh1, tbin, sbase, snum);
+        uint32_t pos = atomicAdd(&bcount[b], 1u);
+        atomicAdd(&bsize[b], ph == 0 ? 1u : 1u + run);
+        if (pos < kBinCap)
+          brec[(size_t)b * kBinCap + pos] = BRec{key, slot, e, n, run};
+        else
+          sel->bin_ovf = 1;
+      }
+    } else if (n == 0 ? i < cap1 : xbase + n - 1 < cap2) {
+      uint32_t e = entry_id(i, n, cap1, xbase);
+      {
+        eokey[e] = key;
+        eslot[e] = slot;
+        eseq[e] = n;
+        erun[e] = run;
+      }
+    }
+    kmax = key > kmax ? key : kmax;
+    ++n;
+  }
+  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
+    if (ph == 0) put(okey(t.r), 0);
+  }
+  __device__ void group(uint64_t key, uint32_t run) { put(key, run); }
+};
+
 // Candidates = slots whose key <= T, compacted (any order: the final order
-// is fixed by the sort on full keys).  kCandBlocks blocks, one atomic each.
+// is fixed by the ranking on full keys).  kCandBlocks blocks, one atomic each.
 constexpr int kCandBlocks = 256;
 __global__ void k_cand(uint32_t n, const uint64_t* keys, Sel* sel,
                        uint32_t* cand) {
@@ -633,55 +806,19 @@ __global__ void k_cand(uint32_t n, const uint64_t* keys, Sel* sel,
     if (keys[s] <= T) cand[o++] = s;
 }
 
-// ------------------------------------------------------------------ pull: walks
-struct CountVisit {
-  uint32_t pops = 0, groups = 0;
-  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
-  __device__ void group(uint64_t, uint32_t) { ++groups; }
-};
-
-// Entry id of the j-th entry of candidate i: the first lives at i, the rest
-// in the extras region (after cap1) at the candidate's extras base.
-__device__ inline uint32_t entry_id(uint32_t i, uint32_t j, uint32_t cap1,
-                                    uint32_t xbase) {
-  return j == 0 ? i : cap1 + xbase + j - 1;
-}
-
-struct EmitVisit {
-  uint64_t* eokey;
-  uint32_t* eslot;
-  uint32_t* eseq;
-  uint32_t* erun;
-  uint32_t i, cap1, xbase, cap2, slot;
-  int ph;
-  uint32_t n = 0;
-  uint64_t kmax = 0;
-  __device__ void put(uint64_t key, uint32_t run) {
-    if (n == 0 ? i < cap1 : xbase + n - 1 < cap2) {
-      uint32_t e = entry_id(i, n, cap1, xbase);
-      eokey[e] = key;
-      eslot[e] = slot;
-      eseq[e] = n;
-      erun[e] = run;
-    }
-    kmax = key > kmax ? key : kmax;
-    ++n;
-  }
-  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
-    if (ph == 0) put(okey(t.r), 0);
-  }
-  __device__ void group(uint64_t key, uint32_t run) { put(key, run); }
-};
-
-// One thread per candidate: count its entries (R: pops with r <= min(now,T);
-// P: groups with key <= T), allocate its extras (one atomic per block), then
-// emit (key, slot, seq, run).  Per-block max key goes to emax[] for the
-// 32-bit sort-key scaling.
-template <int PH>
-__global__ void k_emit(Table tb, Sel* sel, const Ctl* ctl,
-                       const uint32_t* cand, uint32_t cap1, uint32_t cap2,
-                       uint32_t* cxbase, uint64_t* eokey, uint32_t* eslot,
-                       uint32_t* eseq, uint32_t* erun, uint64_t* emax) {
+// One thread per candidate enumerates its entries (R: pops with
+// r <= min(now, T); P: groups with key <= T) and emits (key, slot, seq, run).
+// Bin-rank path (BIN): each entry goes straight to its rank bin, with entry id
+// candidate * q + seq (no allocation needed).  Radix path: a counting walk
+// first, extras allocated with one atomic per block, then the entries go to
+// the entry arrays; per-block max key to emax[] for the 32-bit key scaling.
+template <int PH, bool BIN>
+__global__ void __launch_bounds__(kBlock)
+k_emit(Table tb, Sel* sel, const Ctl* ctl, const uint32_t* cand, uint32_t cap1,
+       uint32_t cap2, uint32_t* cxbase, uint64_t* eokey, uint32_t* eslot,
+       uint32_t* eseq, uint32_t* erun, uint64_t* emax, BRec* brec,
+       uint32_t* bcount, uint32_t* bsize, const uint32_t* sbase,
+       const uint32_t* snum) {
   __shared__ uint32_t wsum[kBlock / 64];
   __shared__ uint32_t base;
   __shared__ unsigned long long bmax;
@@ -691,6 +828,18 @@ __global__ void k_emit(Table tb, Sel* sel, const Ctl* ctl,
   uint64_t T = sel->T;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t s = i < nc ? cand[i] : 0;
+  if (BIN) {
+    if (i >= nc) return;
+    EmitVisit v{nullptr, nullptr, nullptr, nullptr, i, cap1, 0, cap2, s, PH,
+                brec, bcount, bsize, sbase, snum, sel->kmin, sel->hshift,
+                sel->tbin, sel};
+    v.q = tb.q;
+    if (PH == 0)
+      walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+    else
+      walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
+    return;
+  }
   uint32_t c = 0;
   if (i < nc) {
     CountVisit v;
@@ -717,7 +866,8 @@ __global__ void k_emit(Table tb, Sel* sel, const Ctl* ctl,
   uint32_t xb = base + wb + incl - x;
   if (i < nc) {
     cxbase[i] = xb;
-    EmitVisit v{eokey, eslot, eseq, erun, i, cap1, xb, cap2, s, PH};
+    EmitVisit v{eokey, eslot, eseq, erun, i, cap1, xb, cap2, s, PH,
+                nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, sel};
     if (PH == 0)
       walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
     else
@@ -893,191 +1043,131 @@ __global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
 }
 
 // ---------------------------------------------------------- pull: bin-rank
-// Ranking the entries without a general sort: entries are counted into kNB
-// bins of the ordered-key range (monotone), bucketed, and each entry's rank
-// is its bin's offset plus the number of entries of its own bin that precede
-// it in the full order (okey, slot, seq).  The same pass yields the
-// group-size prefix (P) and the tie flag, and decides.  A bin with more than
-// kBigBin entries aborts the batch (ctl->overflow = 2); the host then redoes
-// it through the radix-sort path.
-constexpr uint32_t kBigBin = 2048;
-
+// Ranking the entries without a general sort: k_emit files each entry in its
+// rank bin (k_pick's table: monotone in the key, balanced over the keys'
+// histogram); an entry's rank is the number of entries in earlier bins plus
+// those of its own bin that precede it in the full order (okey, slot, seq).
+// One wave per bin ranks it in LDS; each block first sums the counts and
+// group sizes of all earlier bins.  The same pass yields the group-size prefix
+// (P) and the tie flag, and decides.  A bin past kBinCap (bin_ovf) aborts the
+// batch (ctl->overflow = 2); the host then redoes it through the radix path.
+constexpr int kRankBins = 16;                 // bins per block (4 per wave)
+constexpr int kRankBlocks = kNB / kRankBins;  // 256
 template <int PH>
-__global__ void k_bin(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
-                      const uint32_t* sbase_g, const uint32_t* snum_g,
-                      const uint64_t* eokey, const uint32_t* erun,
-                      uint32_t* ebin, uint32_t* bcount, uint32_t* bsize) {
-  __shared__ uint32_t sc[kNB];
-  __shared__ uint32_t ss[kNB];
-  __shared__ uint32_t sbase[kHistBins], snum[kHistBins];
-  uint32_t nc = sel->n_cand, nx = sel->n_extra;
-  bool ovf = ctl->overflow || nc > cap1 || nx > cap2;
-  uint64_t kmin = sel->kmin;
-  uint32_t sh1 = sel->hshift, tb = sel->tbin;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0) {
-    sel->n_entries = ovf ? 0 : nc + nx;
-    sel->shift = 0;
-    ctl->nc[PH] = nc;
-    ctl->nx[PH] = nx;
-    if (ovf && !ctl->overflow) ctl->overflow = 1;
-  }
-  if (ovf) return;
-  for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
-    sc[b] = 0;
-    ss[b] = 0;
-  }
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
-    sbase[b] = sbase_g[b];
-    snum[b] = snum_g[b];
-  }
-  __syncthreads();
-  uint32_t E = cap1 + cap2;
-  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
-    bool real = e < nc || (e >= cap1 && e < cap1 + nx);
-    if (!real) continue;
-    uint32_t b = rank_bin(eokey[e], kmin, sh1, tb, sbase, snum);
-    ebin[e] = b;
-    atomicAdd(&sc[b], 1u);
-    atomicAdd(&ss[b], PH == 0 ? 1u : 1u + erun[e]);
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < kNB; b += blockDim.x)
-    if (sc[b]) {
-      atomicAdd(&bcount[b], sc[b]);
-      atomicAdd(&bsize[b], ss[b]);
-    }
-}
-
-// exclusive scans of the bin counts and of the bins' total group sizes; the
-// phase's decision count; skew check.  One block of 1024 threads.
-template <int PH>
-__global__ void __launch_bounds__(1024)
-k_bscan(Sel* sel, Ctl* ctl, const uint32_t* bcount, const uint32_t* bsize,
-        uint32_t* boff, uint32_t* bsoff, uint32_t* bfill) {
-  constexpr int per = kNB / 1024;
-  __shared__ uint32_t wc[16], wsz[16];
-  __shared__ uint32_t big;
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) big = 0;
-  uint32_t c[per], z[per], lc = 0, lz = 0, mx = 0;
-  for (int j = 0; j < per; ++j) {
-    c[j] = bcount[t * per + j];
-    z[j] = bsize[t * per + j];
-    lc += c[j];
-    lz += z[j];
-    mx = c[j] > mx ? c[j] : mx;
-    bfill[t * per + j] = 0;
-  }
-  uint32_t ic = lc, iz = lz;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d);
-    if (lane >= d) {
-      ic += oc;
-      iz += oz;
-    }
-  }
-  if (lane == 63) {
-    wc[w] = ic;
-    wsz[w] = iz;
-  }
-  __syncthreads();
-  if (mx > kBigBin) atomicOr(&big, 1u);
-  uint32_t bc = 0, bz = 0, tc = 0, tz = 0;
-  for (int i = 0; i < 16; ++i) {
-    if (i < w) {
-      bc += wc[i];
-      bz += wsz[i];
-    }
-    tc += wc[i];
-    tz += wsz[i];
-  }
-  uint32_t oc = bc + ic - lc, oz = bz + iz - lz;
-  for (int j = 0; j < per; ++j) {
-    boff[t * per + j] = oc;
-    bsoff[t * per + j] = oz;
-    oc += c[j];
-    oz += z[j];
-  }
-  __syncthreads();
-  if (t == 0) {
-    if (ctl->overflow) return;
-    if (big) {
-      ctl->overflow = 2;  // skewed bins: redo through the radix-sort path
+__global__ void __launch_bounds__(kBlock)
+k_rank(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2, const uint32_t* bcount,
+       const uint32_t* bsize, const BRec* brec, uint32_t* eoff, uint8_t* etie,
+       uint32_t* applied) {
+  __shared__ BRec sh[kBlock / 64][kBinCap];
+  __shared__ uint32_t s_off[kRankBins], s_soff[kRankBins], s_cnt[kRankBins];
+  __shared__ uint32_t s_pc[kBlock / 64], s_ps[kBlock / 64];
+  __shared__ uint32_t s_tc[kBlock / 64], s_ts[kBlock / 64], s_ne;
+  uint32_t nc = sel->n_cand, nx = 0;  // (no extra-entry region on this path)
+  bool ovf = ctl->overflow || nc > cap1 || sel->bin_ovf;
+  bool last = blockIdx.x == 0;
+  uint32_t k_rem = k_left(ctl), n_dec = ctl->n_dec;
+  if (ovf) {
+    if (last && threadIdx.x == 0) {
       sel->n_entries = 0;
-      return;
+      ctl->nc[PH] = nc;
+      ctl->nx[PH] = nx;
+      if (!ctl->overflow)
+        ctl->overflow = nc <= cap1 ? 2u : 1u;
     }
-    uint32_t k_rem = k_left(ctl);
-    uint32_t n = sel->n_entries;
-    (void)tc;
-    sel->n_dec_phase = tz < k_rem ? tz : k_rem;
-    sel->terminal = (PH == 1 && tz < k_rem) ? 1 : 0;
-    if (n == 0) sel->terminal = (PH == 1 && k_rem > 0) ? 1 : 0;
+    return;
   }
-}
-
-__global__ void k_bucket(const Sel* sel, const Ctl* ctl, uint32_t cap1,
-                         uint32_t cap2, const uint32_t* ebin,
-                         const uint32_t* boff, uint32_t* bfill,
-                         uint32_t* bucketed) {
-  if (ctl->overflow) return;
-  uint32_t nc = sel->n_cand, nx = sel->n_extra;
-  uint32_t E = cap1 + cap2;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E;
-       e += gridDim.x * blockDim.x) {
-    bool real = e < nc || (e >= cap1 && e < cap1 + nx);
-    if (!real) continue;
-    uint32_t b = ebin[e];
-    bucketed[boff[b] + atomicAdd(&bfill[b], 1u)] = e;
+  uint32_t b0 = blockIdx.x * kRankBins;
+  // entries and group sizes of all bins before b0, and in all bins
+  uint32_t pc = 0, ps = 0, tc = 0, ts = 0;
+  for (uint32_t b = threadIdx.x; b < (uint32_t)kNB; b += kBlock) {
+    uint32_t c = bcount[b], z = bsize[b];
+    if (b < b0) {
+      pc += c;
+      ps += z;
+    }
+    tc += c;
+    ts += z;
   }
-}
-
-// rank within the bin by the full order; decide.
-template <int PH>
-__global__ void k_rank(Sel* sel, const Ctl* ctl, const uint32_t* bucketed,
-                       const uint32_t* ebin, const uint32_t* boff,
-                       const uint32_t* bcount, const uint32_t* bsoff,
-                       const uint64_t* eokey, const uint32_t* eslot,
-                       const uint32_t* eseq, const uint32_t* erun,
-                       uint32_t* eoff, uint8_t* etie, uint32_t* applied) {
-  if (ctl->overflow) return;
-  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
-       p += gridDim.x * blockDim.x) {
-    uint32_t e = bucketed[p];
-    uint32_t b = ebin[e];
-    uint32_t lo = boff[b], hi = lo + bcount[b];
-    uint64_t ke = eokey[e];
-    uint32_t se = eslot[e], qe = eseq[e];
-    uint32_t rank = lo, goff = bsoff[b];
-    bool tie = false;
-    for (uint32_t q = lo; q < hi; ++q) {
-      uint32_t f = bucketed[q];
-      if (f == e) continue;
-      uint64_t kf = eokey[f];
-      uint32_t sf = eslot[f];
-      bool less = kf < ke || (kf == ke && (sf < se || (sf == se && eseq[f] < qe)));
-      if (less) {
-        ++rank;
-        goff += PH == 0 ? 1u : 1u + erun[f];
-      }
-      if (kf == ke && sf != se) tie = true;
+  pc = wave_sum_u32(pc);
+  ps = wave_sum_u32(ps);
+  tc = wave_sum_u32(tc);
+  ts = wave_sum_u32(ts);
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_pc[w] = pc;
+    s_ps[w] = ps;
+    s_tc[w] = tc;
+    s_ts[w] = ts;
+  }
+  if (threadIdx.x < kRankBins) s_cnt[threadIdx.x] = bcount[b0 + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t PC = 0, PS = 0, TC = 0, TS = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+      PC += s_pc[k];
+      PS += s_ps[k];
+      TC += s_tc[k];
+      TS += s_ts[k];
     }
-    uint32_t size = PH == 0 ? 1u : 1u + erun[e];
-    if (goff < k_rem) {
-      eoff[e] = n_dec + goff;
-      etie[e] = tie ? 1 : 0;
-      uint32_t na = size < k_rem - goff ? size : k_rem - goff;
-      atomicAdd(&applied[se], na);
-      if (PH == 1 && (goff + size >= k_rem || rank == n - 1)) {
-        // the last applied group: its priority pop is this phase's last
-        // limit-scanning pull
-        sel->g_last = n_dec + goff;
-        sel->n_prio_groups = rank + 1;
-      }
-    } else {
-      eoff[e] = kNone;
+    s_ne = TC;
+    for (int k = 0; k < kRankBins; ++k) {
+      s_off[k] = PC;
+      s_soff[k] = PS;
+      PC += s_cnt[k];
+      PS += bsize[b0 + k];
     }
+    if (last) {  // totals: the phase's decision count, terminal flag
+      sel->n_entries = TC;
+      ctl->nc[PH] = nc;
+      ctl->nx[PH] = nx;
+      sel->n_dec_phase = TS < k_rem ? TS : k_rem;
+      sel->terminal = (PH == 1 && TS < k_rem) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t ne = s_ne;
+  for (int j = 0; j < kRankBins / (kBlock / 64); ++j) {
+    uint32_t lb = w * (kRankBins / (kBlock / 64)) + j;
+    uint32_t b = b0 + lb;
+    uint32_t cnt = s_cnt[lb];
+    const BRec* src = brec + (size_t)b * kBinCap;
+    for (uint32_t q = lane; q < cnt; q += 64) sh[w][q] = src[q];
+    __syncthreads();
+    for (uint32_t q = lane; q < cnt; q += 64) {
+      BRec me = sh[w][q];
+      uint32_t rank = 0, gl = 0;
+      bool tie = false;
+      for (uint32_t f = 0; f < cnt; ++f) {
+        if (f == q) continue;
+        const BRec& o = sh[w][f];
+        bool less = o.okey < me.okey ||
+                    (o.okey == me.okey &&
+                     (o.slot < me.slot || (o.slot == me.slot && o.seq < me.seq)));
+        if (less) {
+          ++rank;
+          gl += PH == 0 ? 1u : 1u + o.run;
+        }
+        if (o.okey == me.okey && o.slot != me.slot) tie = true;
+      }
+      uint32_t grank = s_off[lb] + rank;
+      uint32_t goff = PH == 0 ? grank : s_soff[lb] + gl;
+      uint32_t size = PH == 0 ? 1u : 1u + me.run;
+      if (goff < k_rem) {
+        eoff[me.e] = n_dec + goff;
+        etie[me.e] = tie ? 1 : 0;
+        uint32_t na = size < k_rem - goff ? size : k_rem - goff;
+        atomicAdd(&applied[me.slot], na);
+        if (PH == 1 && (goff + size >= k_rem || grank == ne - 1)) {
+          // the last applied group: its priority pop is this phase's last
+          // limit-scanning pull
+          sel->g_last = n_dec + goff;
+          sel->n_prio_groups = grank + 1;
+        }
+      } else {
+        eoff[me.e] = kNone;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1088,17 +1178,21 @@ struct ApplyVisit {
   uint32_t i, cap1, xbase;  // candidate index, region-2 layout
   uint32_t slot;
   int ph;
+  uint32_t qbin;  // bin-rank path: entry id = i * qbin + seq (else region layout)
+  __device__ uint32_t id(uint32_t j) const {
+    return qbin ? i * qbin + j : entry_id(i, j, cap1, xbase);
+  }
   uint32_t npop = 0, ngroup = 0, inrun = 0;
   uint32_t last_idx = 0;
   __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
                       bool prio) {
     uint32_t idx, tie;
     if (ph == 0) {
-      uint32_t e = entry_id(i, npop, cap1, xbase);
+      uint32_t e = id(npop);
       idx = eoff[e];
       tie = etie[e];
     } else {
-      uint32_t e = entry_id(i, ngroup, cap1, xbase);
+      uint32_t e = id(ngroup);
       if (prio) inrun = 0;
       idx = eoff[e] + inrun;
       tie = prio ? etie[e] : 0;
@@ -1127,16 +1221,30 @@ struct ApplyVisit {
 // and the front's ready flag (set iff a later limit scan saw it with
 // limit <= now).
 template <int PH>
-__global__ void k_apply(Table tb, const Sel* sel, const Ctl* ctl,
+__global__ void k_apply(Table tb, const Sel* sel, Ctl* ctl,
                         const uint32_t* cand, const uint32_t* cxbase,
                         uint32_t cap1, const uint32_t* eoff,
                         const uint8_t* etie, uint32_t* applied,
-                        uint32_t* bcount, uint32_t* bsize) {
-  if (blockIdx.x == 0)  // the bin-rank counters are consumed: reset them
+                        uint32_t* bcount, uint32_t* bsize,
+                        unsigned long long* sched, uint32_t qbin) {
+  if (blockIdx.x == 0) {
+    // the bin-rank counters are consumed: reset them
     for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
       bcount[b] = 0;
       bsize[b] = 0;
     }
+    // end of phase: the phase's decisions are counted once here (sched[0]
+    // reservation, sched[1] priority: one per applied group), :1469,1479.
+    // No other block of this kernel reads the fields written here.
+    if (threadIdx.x == 0 && !ctl->overflow && k_left(ctl) != 0) {
+      uint32_t d = sel->n_entries ? sel->n_dec_phase : 0;
+      uint32_t np = PH == 1 && sel->n_entries ? sel->n_prio_groups : 0;
+      ctl->n_dec += d;
+      sched[0] += d - np;
+      sched[1] += np;
+      if (PH == 1 && ctl->n_dec < ctl->k_total) ctl->terminal = 1;
+    }
+  }
   if (ctl->overflow || sel->n_entries == 0) return;
   const double now = ctl->now;
   const uint64_t tick = ctl->tick;
@@ -1151,7 +1259,7 @@ __global__ void k_apply(Table tb, const Sel* sel, const Ctl* ctl,
     uint32_t a = applied[s];
     if (!a) continue;
     applied[s] = 0;
-    ApplyVisit v{out, eoff, etie, i, cap1, cxbase[i], s, PH};
+    ApplyVisit v{out, eoff, etie, i, cap1, qbin ? 0u : cxbase[i], s, PH, qbin};
     Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
     Tag3 front{};
     uint32_t fcost = 0;
@@ -1213,35 +1321,6 @@ __global__ void k_apply(Table tb, const Sel* sel, const Ctl* ctl,
     }
     tb.flags[s] = f;
   }
-}
-
-// The first node of a pull round: its arguments are the round's per-call
-// parameters (updated in place on graph replays).
-__global__ void k_ctl_init(Ctl* ctl, uint32_t k_total, double now,
-                           dmc_decision* out, uint64_t tick) {
-  if (threadIdx.x || blockIdx.x) return;
-  Ctl c{};
-  c.k_total = k_total;
-  c.next_type = DMC_NEXT_RETURNING;
-  c.now = now;
-  c.out = out;
-  c.tick = tick;
-  *ctl = c;
-}
-
-// the phase's decisions are counted once here (sched[0] reservation,
-// sched[1] priority: one per applied group), :1469,1479
-template <int PH>
-__global__ void k_phase_end(const Sel* sel, Ctl* ctl,
-                            unsigned long long* sched) {
-  if (threadIdx.x || blockIdx.x) return;
-  if (ctl->overflow || k_left(ctl) == 0) return;
-  uint32_t d = sel->n_entries ? sel->n_dec_phase : 0;
-  uint32_t np = PH == 1 && sel->n_entries ? sel->n_prio_groups : 0;
-  ctl->n_dec += d;
-  sched[0] += d - np;
-  sched[1] += np;
-  if (PH == 1 && ctl->n_dec < ctl->k_total) ctl->terminal = 1;
 }
 
 // ------------------------------------------------------------------ future
@@ -1587,11 +1666,14 @@ struct dmc_queue {
   uint32_t *eseq = nullptr;
   uint32_t *eoff = nullptr, *gsz = nullptr, *goff = nullptr;
   uint8_t* etie = nullptr;
+  size_t idcap = 0;           // eoff / etie capacity
   // add batch buffers
   uint32_t bcap = 0;
   dmc_request* d_reqs = nullptr;
   int32_t* d_rc = nullptr;
-  uint32_t *akeys = nullptr, *avals = nullptr, *skeys = nullptr, *svals = nullptr;
+  uint32_t *apos = nullptr, *aslot = nullptr;   // per batch request
+  uint32_t *acnt = nullptr, *abuf = nullptr;    // per client (N, N * kAddSlots)
+  AddParams* apblk = nullptr;
   // decisions (host API)
   uint32_t dcap = 0;
   dmc_decision* d_dec = nullptr;
@@ -1607,9 +1689,9 @@ struct dmc_queue {
   bool use_radix = false;      // rank entries with the radix sort (fallback)
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
   uint32_t radix_batches = 0;  // batches left on the fallback path
-  uint32_t *ebin = nullptr, *bcount = nullptr, *bsize = nullptr;
-  uint32_t *boff = nullptr, *bsoff = nullptr, *bfill = nullptr;
+  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNB rank-bin counters
   uint32_t* cxbase = nullptr;  // N
+  BRec* brec = nullptr;        // kNB * kBinCap rank-bin records
   uint64_t* emax = nullptr;    // N / kBlock + 1
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
@@ -1632,7 +1714,7 @@ struct dmc_queue {
 namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
-    "add_sort", "add_chain", "activate",
+    "add_link", "add_chain", "activate",
     "r_scan", "r_select", "r_cand", "r_emit", "r_key32", "r_sort",
     "r_decide", "r_apply",
     "p_scan", "p_select", "p_cand", "p_emit", "p_key32", "p_sort",
@@ -1674,318 +1756,6 @@ void pflush(dmc_queue* q) {
 
 void dfree(void* p) {
   if (p) (void)hipFree(p);
-}
-
-void graph_destroy(GraphRec& g);
-
-// Buffers captured into graphs are about to move: drop every graph.
-void invalidate_graphs(dmc_queue* q) {
-  for (auto& g : q->graphs) graph_destroy(g);
-}
-
-int ensure_temp(dmc_queue* q, size_t need) {
-  if (need <= q->temp_bytes) return DMC_OK;
-  invalidate_graphs(q);
-  if (q->temp) dfree(q->temp);
-  q->temp = nullptr;
-  size_t sz = need + (need >> 2) + 4096;
-  HIP_OK(hipMalloc(&q->temp, sz));
-  q->temp_bytes = sz;
-  return DMC_OK;
-}
-
-int ensure_entries(dmc_queue* q, uint32_t n) {
-  if (n <= q->ecap) return DMC_OK;
-  uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
-  invalidate_graphs(q);
-  dfree(q->eokey); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
-  dfree(q->sval); dfree(q->eslot); dfree(q->erun); dfree(q->eseq);
-  dfree(q->eoff); dfree(q->gsz); dfree(q->goff); dfree(q->etie);
-  HIP_OK(hipMalloc(&q->eokey, sizeof(uint64_t) * cap));
-  HIP_OK(hipMalloc(&q->ek32, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->sk32, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eslot, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->erun, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eseq, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eoff, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->etie, cap));
-  dfree(q->ebin);
-  HIP_OK(hipMalloc(&q->ebin, sizeof(uint32_t) * cap));
-  q->ecap = cap;
-  size_t t1 = 0, t2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
-                                           q->sval, (int)cap, 0, 32, q->stream);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
-                                         q->stream);
-  return ensure_temp(q, std::max(t1, t2));
-}
-
-int ensure_batch(dmc_queue* q, uint32_t n) {
-  if (n <= q->bcap) return DMC_OK;
-  uint32_t cap = std::max<uint32_t>(n, 1024);
-  invalidate_graphs(q);
-  dfree(q->d_reqs); dfree(q->d_rc); dfree(q->akeys); dfree(q->avals);
-  dfree(q->skeys); dfree(q->svals);
-  HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
-  HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
-  HIP_OK(hipMalloc(&q->akeys, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->avals, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->skeys, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->svals, sizeof(uint32_t) * cap));
-  q->bcap = cap;
-  size_t t = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, q->akeys, q->skeys, q->avals,
-                                     q->svals, (int)cap, 0, 32, q->stream);
-  return ensure_temp(q, t);
-}
-
-int ensure_dec(dmc_queue* q, uint32_t n) {
-  if (n <= q->dcap) return DMC_OK;
-  dfree(q->d_dec);
-  uint32_t cap = std::max<uint32_t>(n, 1024);
-  HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
-  q->dcap = cap;
-  return DMC_OK;
-}
-
-int slot_bits(uint32_t n) {
-  int b = 1;
-  while (b < 32 && (1u << b) < n) ++b;
-  return b;
-}
-
-// Add a contiguous run of requests that contains no activation except,
-// possibly, its first request (which has already been activated).
-int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
-                int32_t* d_rc, uint64_t tick_base) {
-  if (!n) return DMC_OK;
-  uint32_t g = (n + kBlock - 1) / kBlock;
-  pb(q, DMC_PROF_ADD_SORT);
-  hipLaunchKernelGGL(k_add_keys, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
-                     q->akeys, q->avals);
-  size_t tb = q->temp_bytes;
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tb, q->akeys, q->skeys,
-                                            q->avals, q->svals, (int)n, 0,
-                                            slot_bits(q->p.max_clients),
-                                            q->stream));
-  pe(q);
-  pb(q, DMC_PROF_ADD_CHAIN);
-  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     q->skeys, q->svals, d_reqs, n, tick_base, d_rc);
-  pe(q);
-  return DMC_OK;
-}
-
-int activate(dmc_queue* q, uint32_t slot, double t) {
-  pb(q, DMC_PROF_ACTIVATE);
-  uint32_t g = grid_for(q->tb.n, 2048);
-  hipLaunchKernelGGL(k_contrib_min, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     (uint64_t*)q->parts);
-  hipLaunchKernelGGL(k_activate, dim3(1), dim3(kBlock), 0, q->stream, q->tb, slot,
-                     t, (const uint64_t*)q->parts, g);
-  pe(q);
-  return DMC_OK;
-}
-
-// Host-ordered add: split the batch at activations (first request of an idle
-// client); each activation's idle reset sees the state left by everything
-// before it, exactly as the sequential reference does.
-int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
-                   const dmc_request* d_reqs, int32_t* d_rc) {
-  uint32_t start = 0;
-  uint64_t tick0 = q->tick;
-  for (uint32_t i = 0; i < n; ++i) {
-    uint32_t s = h_reqs[i].slot;
-    bool act = s < q->p.max_clients && q->reg_h[s] && q->idle_h[s] &&
-               h_reqs[i].rho <= h_reqs[i].delta;
-    if (!act) continue;
-    int rc = add_segment(q, d_reqs + start, i - start, d_rc + start, tick0 + start);
-    if (rc) return rc;
-    rc = activate(q, s, h_reqs[i].time);
-    if (rc) return rc;
-    q->idle_h[s] = 0;
-    --q->n_idle;
-    start = i;
-  }
-  return add_segment(q, d_reqs + start, n - start, d_rc + start, tick0 + start);
-}
-
-// --------------------------------------------------------------- pull phases
-uint32_t pow2_at_least(uint32_t x) {
-  uint32_t p = 4096;
-  while (p < x && p < (1u << 31)) p <<= 1;
-  return p;
-}
-
-// Enqueue one batched phase; no host synchronisation.  `cap` is the entry
-// capacity the sort runs over (entries beyond it set ctl->overflow and the
-// rest of the batch no-ops; the host retries with a larger capacity).
-template <int PH>
-int launch_phase(dmc_queue* q, uint32_t cap1, uint32_t cap2) {
-  const Table& tb = q->tb;
-  uint32_t N = tb.n;
-  uint32_t gN = grid_for(N, 2048);
-  uint32_t E = cap1 + cap2;
-  uint32_t gE = grid_for(E, 1024);
-  uint32_t gC = (N + kBlock - 1) / kBlock;  // one thread per candidate
-  const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
-  pb(q, S0 + 0);
-  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb,
-                     q->keys, q->parts, (const Ctl*)q->ctl);
-  pe(q);
-  pb(q, S0 + 1);
-  hipLaunchKernelGGL(k_hist, dim3(kHistBlocks), dim3(1024), 0, q->stream, N,
-                     (const uint64_t*)q->keys, (const ScanPart*)q->parts, gN,
-                     (const Ctl*)q->ctl, q->hist, q->hmax);
-  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream,
-                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl,
-                     q->hist, q->hmax, (uint32_t)PH, q->sbase, q->snum);
-  pe(q);
-  pb(q, S0 + 2);
-  hipLaunchKernelGGL(k_cand, dim3(kCandBlocks), dim3(kBlock), 0, q->stream, N,
-                     (const uint64_t*)q->keys, q->sel, q->cand);
-  pe(q);
-  pb(q, S0 + 3);
-  hipLaunchKernelGGL(k_emit<PH>, dim3(gC), dim3(kBlock), 0, q->stream, tb,
-                     q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand, cap1,
-                     cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
-                     q->emax);
-  pe(q);
-  if (!q->use_radix) {
-    uint32_t gB = grid_for(E, 256);
-    pb(q, S0 + 4);
-    hipLaunchKernelGGL(k_bin<PH>, dim3(gB), dim3(kBlock), 0, q->stream, q->sel,
-                       q->ctl, cap1, cap2, (const uint32_t*)q->sbase,
-                       (const uint32_t*)q->snum,
-                       (const uint64_t*)q->eokey, (const uint32_t*)q->erun,
-                       q->ebin, q->bcount, q->bsize);
-    pe(q);
-    pb(q, S0 + 5);
-    hipLaunchKernelGGL(k_bscan<PH>, dim3(1), dim3(1024), 0, q->stream, q->sel,
-                       q->ctl, (const uint32_t*)q->bcount,
-                       (const uint32_t*)q->bsize, q->boff, q->bsoff, q->bfill);
-    hipLaunchKernelGGL(k_bucket, dim3(gB), dim3(kBlock), 0, q->stream,
-                       (const Sel*)q->sel, (const Ctl*)q->ctl, cap1, cap2,
-                       (const uint32_t*)q->ebin, (const uint32_t*)q->boff,
-                       q->bfill, q->sval);
-    pe(q);
-    pb(q, S0 + 6);
-    hipLaunchKernelGGL(k_rank<PH>, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
-                       (const Ctl*)q->ctl, (const uint32_t*)q->sval,
-                       (const uint32_t*)q->ebin, (const uint32_t*)q->boff,
-                       (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
-                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
-                       (const uint32_t*)q->eseq, (const uint32_t*)q->erun, q->eoff,
-                       q->etie, q->applied);
-    pe(q);
-  } else {
-    pb(q, S0 + 4);
-    hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
-                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gC,
-                       (const uint64_t*)q->eokey, q->ek32, q->eval);
-    pe(q);
-    pb(q, S0 + 5);
-    size_t tbytes = q->temp_bytes;
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
-                                              q->eval, q->sval, (int)E, 0, 32,
-                                              q->stream));
-    hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
-                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
-                       (const uint32_t*)q->eseq);
-    pe(q);
-    pb(q, S0 + 6);
-    if (PH == 0) {
-      hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                         q->eoff, q->etie, q->applied, q->sel);
-    } else {
-      hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const Sel*)q->sel, E,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
-      tbytes = q->temp_bytes;
-      HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
-                                              (int)E, q->stream));
-      hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                         (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
-                         q->etie, q->applied, q->sel);
-    }
-    pe(q);
-  }
-  pb(q, S0 + 7);
-  hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
-                     q->stream, tb, (const Sel*)q->sel,
-                     (const Ctl*)q->ctl, (const uint32_t*)q->cand,
-                     (const uint32_t*)q->cxbase, cap1, (const uint32_t*)q->eoff,
-                     (const uint8_t*)q->etie, q->applied, q->bcount,
-                     q->bsize);
-  pe(q);
-  hipLaunchKernelGGL(k_phase_end<PH>, dim3(1), dim3(64), 0, q->stream,
-                     (const Sel*)q->sel, q->ctl, q->sched);
-  return DMC_OK;
-}
-
-// Terminal pull of a Wait/Reject batch: one general do_next_request, which
-// (nothing being eligible) computes min_not_0 over the reservation- and
-// limit-heap tops, :1170-1185.  No-op unless ctl->terminal.
-int launch_future(dmc_queue* q, Ctl* ctl) {
-  const double now = 0.0;  // read from ctl by the kernels
-  pb(q, DMC_PROF_FUTURE);
-  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     q->tb, now, q->red, (const Ctl*)ctl);
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
-                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, ctl);
-  pe(q);
-  return DMC_OK;
-}
-
-// one general pull_request(now); returns the NextReqType in *type
-int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
-              int* type, double* when) {
-  const Table& tb = q->tb;
-  pb(q, DMC_PROF_STEP);
-  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     tb, now, q->red, (const Ctl*)nullptr);
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
-                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, (Ctl*)nullptr);
-  hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
-                     q->stream, tb, now, (const StepCtl*)q->sctl);
-  hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
-                     (const StepCtl*)q->sctl, d_out, idx, q->sched);
-  pe(q);
-  StepCtl sc;
-  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));
-  pflush(q);
-  *type = sc.type;
-  *when = sc.when;
-  return DMC_OK;
-}
-
-// One pull round: k_ctl_init + phase R + phase P (+ the terminal pull).  The
-// sequence depends on the per-call parameters only through k_ctl_init's
-// arguments, so it is captured once per shape (entry capacities, ranking
-// path, terminal pull) into a hipGraph and replayed with k_ctl_init's
-// arguments updated: one graph launch instead of ~25 kernel launches, which
-// removes the host's per-launch cost from the critical path.  A shape is
-// captured the second time it is seen; profiling runs eagerly (the stage
-// timers are events between kernels).
-void enqueue_round(dmc_queue* q, uint32_t kk, double now, dmc_decision* out,
-                   const uint32_t* cap1, const uint32_t* cap2, bool future) {
-  hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, q->stream, q->ctl, kk, now,
-                     out, q->tick);
-  launch_phase<0>(q, cap1[0], cap2[0]);
-  launch_phase<1>(q, cap1[1], cap2[1]);
-  if (future) launch_future(q, q->ctl);
 }
 
 int graph_replay(dmc_queue* q, GraphRec& g, void** args) {
@@ -2061,6 +1831,323 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
   return slot;
 }
 
+// Buffers captured into graphs are about to move: drop every graph.
+void invalidate_graphs(dmc_queue* q) {
+  for (auto& g : q->graphs) graph_destroy(g);
+}
+
+int ensure_temp(dmc_queue* q, size_t need) {
+  if (need <= q->temp_bytes) return DMC_OK;
+  invalidate_graphs(q);
+  if (q->temp) dfree(q->temp);
+  q->temp = nullptr;
+  size_t sz = need + (need >> 2) + 4096;
+  HIP_OK(hipMalloc(&q->temp, sz));
+  q->temp_bytes = sz;
+  return DMC_OK;
+}
+
+// decision offset / tie flag per entry id: region layout (cap1 + cap2) on the
+// radix path, candidate * ring capacity + seq on the bin-rank path
+int ensure_ids(dmc_queue* q, size_t n) {
+  if (n <= q->idcap) return DMC_OK;
+  size_t cap = std::max<size_t>(n + (n >> 2), 1u << 16);
+  invalidate_graphs(q);
+  dfree(q->eoff);
+  dfree(q->etie);
+  q->eoff = nullptr;
+  q->etie = nullptr;
+  HIP_OK(hipMalloc(&q->eoff, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->etie, cap));
+  q->idcap = cap;
+  return DMC_OK;
+}
+
+int ensure_entries(dmc_queue* q, uint32_t n) {
+  if (n <= q->ecap) return DMC_OK;
+  uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
+  invalidate_graphs(q);
+  dfree(q->eokey); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
+  dfree(q->sval); dfree(q->eslot); dfree(q->erun); dfree(q->eseq);
+  dfree(q->gsz); dfree(q->goff);
+  HIP_OK(hipMalloc(&q->eokey, sizeof(uint64_t) * cap));
+  HIP_OK(hipMalloc(&q->ek32, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sk32, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eslot, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->erun, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->eseq, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
+  q->ecap = cap;
+  int rc = ensure_ids(q, cap);
+  if (rc) return rc;
+  size_t t1 = 0, t2 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
+                                           q->sval, (int)cap, 0, 32, q->stream);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
+                                         q->stream);
+  return ensure_temp(q, std::max(t1, t2));
+}
+
+int ensure_batch(dmc_queue* q, uint32_t n) {
+  if (n <= q->bcap) return DMC_OK;
+  uint32_t cap = std::max<uint32_t>(n, 1024);
+  invalidate_graphs(q);
+  dfree(q->d_reqs); dfree(q->d_rc); dfree(q->apos); dfree(q->aslot);
+  HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
+  HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
+  HIP_OK(hipMalloc(&q->apos, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->aslot, sizeof(uint32_t) * cap));
+  q->bcap = cap;
+  return DMC_OK;
+}
+
+int ensure_dec(dmc_queue* q, uint32_t n) {
+  if (n <= q->dcap) return DMC_OK;
+  dfree(q->d_dec);
+  uint32_t cap = std::max<uint32_t>(n, 1024);
+  HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
+  q->dcap = cap;
+  return DMC_OK;
+}
+
+int slot_bits(uint32_t n) {
+  int b = 1;
+  while (b < 32 && (1u << b) < n) ++b;
+  return b;
+}
+
+// Add a contiguous run of requests that contains no activation except,
+// possibly, its first request (which has already been activated).
+// Add a contiguous run of requests that contains no activation except,
+// possibly, its first request (which has already been activated).  The two
+// kernels are captured once per batch size and replayed with k_add_link's
+// arguments updated (see launch_round).
+void enqueue_add(dmc_queue* q, const AddParams& ap) {
+  uint32_t g = (ap.n + kBlock - 1) / kBlock;
+  pb(q, DMC_PROF_ADD_LINK);
+  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
+                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk);
+  pe(q);
+  pb(q, DMC_PROF_ADD_CHAIN);
+  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot);
+  pe(q);
+}
+
+int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
+                int32_t* d_rc, uint64_t tick_base) {
+  if (!n) return DMC_OK;
+  AddParams ap{d_reqs, d_rc, tick_base, n, 0};
+  uint64_t key = (2ull << 56) | n;
+  GraphRec* g = graph_for(q, key, [&] { enqueue_add(q, ap); });
+  if (!g) {
+    enqueue_add(q, ap);
+    HIP_OK(hipGetLastError());
+    return DMC_OK;
+  }
+  Table tb = q->tb;
+  void* args[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk};
+  return graph_replay(q, *g, args);
+}
+
+int activate(dmc_queue* q, uint32_t slot, double t) {
+  pb(q, DMC_PROF_ACTIVATE);
+  uint32_t g = grid_for(q->tb.n, 2048);
+  hipLaunchKernelGGL(k_contrib_min, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     (uint64_t*)q->parts);
+  hipLaunchKernelGGL(k_activate, dim3(1), dim3(kBlock), 0, q->stream, q->tb, slot,
+                     t, (const uint64_t*)q->parts, g);
+  pe(q);
+  return DMC_OK;
+}
+
+// Host-ordered add: split the batch at activations (first request of an idle
+// client); each activation's idle reset sees the state left by everything
+// before it, exactly as the sequential reference does.
+int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
+                   const dmc_request* d_reqs, int32_t* d_rc) {
+  uint32_t start = 0;
+  uint64_t tick0 = q->tick;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = h_reqs[i].slot;
+    bool act = s < q->p.max_clients && q->reg_h[s] && q->idle_h[s] &&
+               h_reqs[i].rho <= h_reqs[i].delta;
+    if (!act) continue;
+    int rc = add_segment(q, d_reqs + start, i - start, d_rc + start, tick0 + start);
+    if (rc) return rc;
+    rc = activate(q, s, h_reqs[i].time);
+    if (rc) return rc;
+    q->idle_h[s] = 0;
+    --q->n_idle;
+    start = i;
+  }
+  return add_segment(q, d_reqs + start, n - start, d_rc + start, tick0 + start);
+}
+
+// --------------------------------------------------------------- pull phases
+// Larger pulls rank through the radix path: the kNB x kBinCap rank bins hold
+// about a million entries when balanced.
+constexpr uint32_t kBinRankMaxK = 1u << 18;
+
+uint32_t pow2_at_least(uint32_t x) {
+  uint32_t p = 4096;
+  while (p < x && p < (1u << 31)) p <<= 1;
+  return p;
+}
+
+// Enqueue one batched phase; no host synchronisation.  `cap` is the entry
+// capacity the sort runs over (entries beyond it set ctl->overflow and the
+// rest of the batch no-ops; the host retries with a larger capacity).
+template <int PH>
+int launch_phase(dmc_queue* q, uint32_t cap1, uint32_t cap2, const CallParams& cp) {
+  const Table& tb = q->tb;
+  uint32_t N = tb.n;
+  uint32_t gN = grid_for(N, 2048);
+  uint32_t E = cap1 + cap2;
+  uint32_t gE = grid_for(E, 1024);
+  const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
+  pb(q, S0 + 0);
+  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb,
+                     q->keys, q->parts, q->ctl, cp);
+  pe(q);
+  pb(q, S0 + 1);
+  hipLaunchKernelGGL(k_hist, dim3(kHistBlocks), dim3(1024), 0, q->stream, N,
+                     (const uint64_t*)q->keys, (const ScanPart*)q->parts, gN,
+                     (const Ctl*)q->ctl, q->hist, q->hmax);
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream,
+                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl,
+                     q->hist, q->hmax, (uint32_t)PH, q->sbase, q->snum);
+  pe(q);
+  uint32_t gX = (N + kBlock - 1) / kBlock;  // one thread per candidate
+  pb(q, S0 + 2);
+  hipLaunchKernelGGL(k_cand, dim3(kCandBlocks), dim3(kBlock), 0, q->stream, N,
+                     (const uint64_t*)q->keys, q->sel, q->cand);
+  pe(q);
+  pb(q, S0 + 3);
+  if (q->use_radix)
+    hipLaunchKernelGGL((k_emit<PH, false>), dim3(gX), dim3(kBlock), 0, q->stream,
+                       tb, q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand,
+                       cap1, cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
+                       q->emax, nullptr, nullptr, nullptr, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((k_emit<PH, true>), dim3(gX), dim3(kBlock), 0, q->stream,
+                       tb, q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand,
+                       cap1, cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
+                       q->emax, q->brec, q->bcount, q->bsize,
+                       (const uint32_t*)q->sbase, (const uint32_t*)q->snum);
+  pe(q);
+  if (!q->use_radix) {
+    pb(q, S0 + 6);
+    hipLaunchKernelGGL(k_rank<PH>, dim3(kRankBlocks), dim3(kBlock), 0, q->stream,
+                       q->sel, q->ctl, cap1, cap2, (const uint32_t*)q->bcount,
+                       (const uint32_t*)q->bsize, (const BRec*)q->brec, q->eoff,
+                       q->etie, q->applied);
+    pe(q);
+  } else {
+    pb(q, S0 + 4);
+    hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
+                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gX,
+                       (const uint64_t*)q->eokey, q->ek32, q->eval);
+    pe(q);
+    pb(q, S0 + 5);
+    size_t tbytes = q->temp_bytes;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
+                                              q->eval, q->sval, (int)E, 0, 32,
+                                              q->stream));
+    hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
+                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
+                       (const uint32_t*)q->eseq);
+    pe(q);
+    pb(q, S0 + 6);
+    if (PH == 0) {
+      hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                         q->eoff, q->etie, q->applied, q->sel);
+    } else {
+      hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const Sel*)q->sel, E,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
+      tbytes = q->temp_bytes;
+      HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
+                                              (int)E, q->stream));
+      hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
+                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
+                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
+                         (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
+                         q->etie, q->applied, q->sel);
+    }
+    pe(q);
+  }
+  pb(q, S0 + 7);
+  hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
+                     q->stream, tb, (const Sel*)q->sel, q->ctl,
+                     (const uint32_t*)q->cand, (const uint32_t*)q->cxbase, cap1,
+                     (const uint32_t*)q->eoff, (const uint8_t*)q->etie, q->applied,
+                     q->bcount, q->bsize, q->sched, q->use_radix ? 0u : tb.q);
+  pe(q);
+  return DMC_OK;
+}
+
+// Terminal pull of a Wait/Reject batch: one general do_next_request, which
+// (nothing being eligible) computes min_not_0 over the reservation- and
+// limit-heap tops, :1170-1185.  No-op unless ctl->terminal.
+int launch_future(dmc_queue* q, Ctl* ctl) {
+  const double now = 0.0;  // read from ctl by the kernels
+  pb(q, DMC_PROF_FUTURE);
+  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
+                     q->tb, now, q->red, (const Ctl*)ctl);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
+                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
+                     q->n_registered, q->sctl, ctl);
+  pe(q);
+  return DMC_OK;
+}
+
+// one general pull_request(now); returns the NextReqType in *type
+int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
+              int* type, double* when) {
+  const Table& tb = q->tb;
+  pb(q, DMC_PROF_STEP);
+  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
+                     tb, now, q->red, (const Ctl*)nullptr);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
+                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
+                     q->n_registered, q->sctl, (Ctl*)nullptr);
+  hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
+                     q->stream, tb, now, (const StepCtl*)q->sctl);
+  hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
+                     (const StepCtl*)q->sctl, d_out, idx, q->sched);
+  pe(q);
+  StepCtl sc;
+  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  pflush(q);
+  *type = sc.type;
+  *when = sc.when;
+  return DMC_OK;
+}
+
+// One pull round: phase R + phase P (+ the terminal pull).  The sequence
+// depends on the per-call parameters only through k_scan<0>'s
+// arguments, so it is captured once per shape (entry capacities, ranking
+// path, terminal pull) into a hipGraph and replayed with k_scan<0>'s
+// arguments updated: one graph launch instead of ~25 kernel launches, which
+// removes the host's per-launch cost from the critical path.  A shape is
+// captured the second time it is seen; profiling runs eagerly (the stage
+// timers are events between kernels).
+void enqueue_round(dmc_queue* q, const CallParams& cp, const uint32_t* cap1,
+                   const uint32_t* cap2, bool future) {
+  launch_phase<0>(q, cap1[0], cap2[0], cp);
+  launch_phase<1>(q, cap1[1], cap2[1], cp);
+  if (future) launch_future(q, q->ctl);
+}
+
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
                  const uint32_t* cap1, const uint32_t* cap2, bool future) {
   uint64_t key = 1;  // shape: capacities (powers of two), ranking path, future
@@ -2068,17 +2155,15 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
     key = key * 64 + (uint64_t)__builtin_ctz(cap1[ph]),
     key = key * 64 + (uint64_t)__builtin_ctz(cap2[ph]);
   key = key * 4 + (q->use_radix ? 2 : 0) + (future ? 1 : 0);
-  GraphRec* g = graph_for(q, key, [&] {
-    enqueue_round(q, kk, now, out, cap1, cap2, future);
-  });
+  CallParams cp{kk, 0, now, out, q->tick};
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, cap1, cap2, future); });
   if (!g) {
-    enqueue_round(q, kk, now, out, cap1, cap2, future);
+    enqueue_round(q, cp, cap1, cap2, future);
     HIP_OK(hipGetLastError());
     return DMC_OK;
   }
-  Ctl* ctl = q->ctl;
-  uint64_t tick = q->tick;
-  void* args[] = {&ctl, &kk, &now, &out, &tick};
+  Table tb = q->tb;
+  void* args[] = {&tb, &q->keys, &q->parts, &q->ctl, &cp};
   return graph_replay(q, *g, args);
 }
 
@@ -2118,8 +2203,12 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       int rc = ensure_entries(q, cap1[ph] + cap2[ph]);
       if (rc) return rc;
     }
-    q->use_radix = q->force_radix || q->radix_batches > 0;
+    q->use_radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
     if (q->radix_batches) --q->radix_batches;
+    if (!q->use_radix) {
+      int rc = ensure_ids(q, (size_t)std::max(cap1[0], cap1[1]) * q->tb.q);
+      if (rc) return rc;
+    }
     int rc = launch_round(q, now, kk, d_out + n_dec, cap1, cap2, !allow);
     if (rc) return rc;
     Ctl c;
@@ -2231,12 +2320,13 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->cand, N);
   rc |= A(&q->bcount, kNB);
   rc |= A(&q->bsize, kNB);
-  rc |= A(&q->boff, kNB);
-  rc |= A(&q->bsoff, kNB);
-  rc |= A(&q->bfill, kNB);
   rc |= A(&q->cxbase, N);
+  rc |= A(&q->brec, (size_t)kNB * kBinCap);
   rc |= A(&q->emax, N / kBlock + 2);
   rc |= A(&q->act_min, 1);
+  rc |= A(&q->acnt, N);
+  rc |= A(&q->abuf, (size_t)N * kAddSlots);
+  rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
   if (rc) {
@@ -2272,10 +2362,10 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sbase, q->snum, q->sel,
                   q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->eokey,
                   q->ek32, q->sk32, q->eval, q->sval, q->eslot, q->erun, q->eseq,
-                  q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->akeys, q->avals,
-                  q->skeys, q->svals, q->d_dec, q->temp, q->ctl,
-                  q->parts, q->cand, q->cxbase, q->emax, q->ebin, q->bcount,
-                  q->bsize, q->boff, q->bsoff, q->bfill};
+                  q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->apos, q->aslot,
+                  q->acnt, q->abuf, q->apblk, q->d_dec, q->temp, q->ctl,
+                  q->parts, q->cand, q->cxbase, q->brec, q->emax, q->bcount,
+                  q->bsize};
   for (void* p : ptrs)
     dfree(p);
   for (auto& r : q->prof_pool) {

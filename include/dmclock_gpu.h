@@ -225,7 +225,7 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
  * of the add and pull pipelines (an extension of this library; the reference
  * has compile-time PROFILE timers around add/pull instead,
  * dmclock_server.h:1309-1312, support/src/profile.h). */
-#define DMC_PROF_ADD_SORT 0
+#define DMC_PROF_ADD_LINK 0
 #define DMC_PROF_ADD_CHAIN 1
 #define DMC_PROF_ACTIVATE 2
 #define DMC_PROF_R_SCAN 3   /* r_scan r_select r_cand r_emit r_key32 r_sort r_decide r_apply */
