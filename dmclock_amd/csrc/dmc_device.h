@@ -141,11 +141,15 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
   if (c == 0) return 0;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   if (!tb.delayed) {
+    // one entry loaded ahead: the walk's loads are not a dependent chain
+    ReqEntry e = ring[h & tb.qmask];
+    ReqEntry nx = ring[(h + 1) & tb.qmask];
     while (n < c && n < limit) {
-      const ReqEntry& e = ring[(h + n) & tb.qmask];
       if (!(e.r <= now) || okey(e.r) > T) break;
       vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false);
       ++n;
+      e = nx;
+      nx = ring[(h + n + 1) & tb.qmask];
     }
     if (front_out && n < c) {
       const ReqEntry& e = ring[(h + n) & tb.qmask];

@@ -1051,8 +1051,8 @@ __global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
 // group sizes of all earlier bins.  The same pass yields the group-size prefix
 // (P) and the tie flag, and decides.  A bin past kBinCap (bin_ovf) aborts the
 // batch (ctl->overflow = 2); the host then redoes it through the radix path.
-constexpr int kRankBins = 16;                 // bins per block (4 per wave)
-constexpr int kRankBlocks = kNB / kRankBins;  // 256
+constexpr int kRankBins = kBlock / 64;        // bins per block (one per wave)
+constexpr int kRankBlocks = kNB / kRankBins;  // 1024
 template <int PH>
 __global__ void __launch_bounds__(kBlock)
 k_rank(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2, const uint32_t* bcount,
@@ -1667,6 +1667,8 @@ struct dmc_queue {
   uint32_t *eoff = nullptr, *gsz = nullptr, *goff = nullptr;
   uint8_t* etie = nullptr;
   size_t idcap = 0;           // eoff / etie capacity
+  Ctl* h_ctl = nullptr;              // pinned: round control readback
+  dmc_pull_result* h_res = nullptr;  // pinned: device-API result staging
   // add batch buffers
   uint32_t bcap = 0;
   dmc_request* d_reqs = nullptr;
@@ -2211,9 +2213,11 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     int rc = launch_round(q, now, kk, d_out + n_dec, cap1, cap2, !allow);
     if (rc) return rc;
-    Ctl c;
-    HIP_OK(hipMemcpyAsync(&c, q->ctl, sizeof(c), hipMemcpyDeviceToHost, q->stream));
+    // one host round trip per round, through pinned memory
+    HIP_OK(hipMemcpyAsync(q->h_ctl, q->ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+                          q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
+    const Ctl c = *q->h_ctl;
     pflush(q);
     n_dec += c.n_dec;
     for (int ph = 0; ph < 2; ++ph) {
@@ -2329,6 +2333,9 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
+  if (hipHostMalloc((void**)&q->h_ctl, sizeof(Ctl), 0) != hipSuccess ||
+      hipHostMalloc((void**)&q->h_res, sizeof(dmc_pull_result), 0) != hipSuccess)
+    rc |= DMC_ENOMEM;
   if (rc) {
     dmc_queue_destroy(q);
     return DMC_ENOMEM;
@@ -2368,6 +2375,8 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->bsize};
   for (void* p : ptrs)
     dfree(p);
+  if (q->h_ctl) (void)hipHostFree(q->h_ctl);
+  if (q->h_res) (void)hipHostFree(q->h_res);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -2643,9 +2652,13 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
   dmc_pull_result r{};
   int rc = pull_impl(q, now, k, d_out, &r);
   if (rc) return rc;
-  if (d_result)
-    HIP_OK(hipMemcpyAsync(d_result, &r, sizeof(r), hipMemcpyHostToDevice, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));
+  if (d_result) {
+    // stream-ordered: pull_impl has synchronised, so the pinned staging
+    // record is free, and the copy completes before any later work
+    *q->h_res = r;
+    HIP_OK(hipMemcpyAsync(d_result, q->h_res, sizeof(r), hipMemcpyHostToDevice,
+                          q->stream));
+  }
   return DMC_OK;
 }
 
