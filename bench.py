@@ -32,24 +32,34 @@ sys.path.insert(0, ROOT)
 METRIC = "dispatch decisions/sec + tag updates/sec at 1M clients; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-# Algorithmic bytes per unit for the single-kernel stages (DESIGN.md,
-# "Roofline accounting").  unit: "client" = one slot of the client table
-# scanned; "request" = one request of the add batch.
+# Algorithmic bytes of each stage: (per client slot of the table, per added
+# request, per decision) -- DESIGN.md section 6.  A pull round streams the
+# client-table columns it needs once per kernel and touches the candidates'
+# rings and state; the add path touches one client record per request.
 STAGE_BYTES = {
-    # k_scan<1>: count 4 + flags 1 + front_l 8 + front_p 8 + prop_delta 8
-    #            read, key 8 written
-    "p_scan": ("client", 37),
-    # k_scan<0>: count 4 + front_r 8 read, key 8 written
-    "r_scan": ("client", 20),
-    # k_cand: key 8 read per slot (candidate ids written are negligible)
-    "r_cand": ("client", 8),
-    "p_cand": ("client", 8),
+    # k_rscan: count 4 + front_r 8 + flags 1 + front_p 8 + front_l 8 +
+    #   prop_delta 8 read, keyr 8 + keyp 8 + R-prefix length 1 written
+    "scan": (54, 0, 0),
+    # k_rhist: keyr + keyp read (k_rpick: one block, 2 x 2048 bins)
+    "select": (16, 0, 0),
+    # k_remit: keyr + keyp read; per dispatched entry its ring entry 64 read
+    #   and rank record 24 written
+    "emit": (16, 0, 88),
+    # k_rrank: rank record 24 read, decision offset + tie 8 written into the
+    #   ring entry
+    "rank": (0, 0, 32),
+    # k_rapply: applied 4 + flags 1 per slot; per decision its ring entry 64
+    #   read, decision record 48 written, client state ~120 read/written
+    "apply": (5, 0, 232),
+    # k_add_link: request slot 32 (line) read, apos/aslot 8 written, slot
+    #   counter 4 + slot buffer 4
+    "add_link": (0, 48, 0),
     # k_add_chain (one request per client): apos/aslot 8 + acnt 8 + abuf 4
     #   + request 32 + rc 4 + ring entry 64 + client state read 81
     #   (prev tag 32, inverses 24, head/count/cur_delta/cur_rho 16,
     #   last_tick 8, flags 1) and written 77 (prev 32, count/cur_* 12,
     #   last_tick 8, flags 1, front tag 24)
-    "add_chain": ("request", 278),
+    "add_chain": (0, 278, 0),
 }
 
 
@@ -238,16 +248,19 @@ def main():
             dist.destroy_process_group()
         return
 
-    # roofline: the dominant single-kernel stage of the timed region
+    # roofline: the dominant stage (largest time per step) of the stage-timed
+    # pass, its algorithmic bytes per launch over its mean launch duration
     roof = None
     cand = [(ms, name) for name, (c, ms) in prof.items()
             if name in STAGE_BYTES and c > 0]
     if cand:
         ms, name = max(cand)
         c = prof[name][0]
-        unit, per = STAGE_BYTES[name]
-        units = args.clients if unit == "client" else args.batch
-        per_launch = per * units
+        per_client, per_req, per_dec = STAGE_BYTES[name]
+        launches_per_step = c / max(prof_steps, 1)
+        per_launch = (per_client * args.clients
+                      + (per_req * args.batch + per_dec * k)
+                      / launches_per_step)
         avg_s = ms / c / 1e3
         achieved = per_launch / avg_s / 1e9
         traffic = None
@@ -260,7 +273,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "kernel": name,
-                "bytes_per_launch": per_launch,
+                "bytes_per_launch": int(per_launch),
                 "avg_launch_us": round(avg_s * 1e6, 2)}
 
     cpu = None

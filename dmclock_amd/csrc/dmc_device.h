@@ -6,9 +6,10 @@
 // and the library is built with -ffp-contract=off).
 //
 // Layout (per queue, N client slots, ring capacity Q):
-//   client table, struct-of-arrays in HBM: prev_{r,p,l,arr}, {r,w,l}_inv,
-//     prop_delta, front_{r,p,l} (the heap keys of the reference, cached),
-//     head/count (ring cursor), cur_{delta,rho}, last_tick, flags.
+//   random-access records: ClientRec (64 B: prev tag, inverses, last_tick)
+//     and QState (16 B: head, count, cur_delta, cur_rho) per client;
+//   scanned struct-of-arrays columns: prop_delta, front_{r,p,l} (the heap
+//     keys of the reference, cached), flags;
 //   request rings: ring[slot * Q + i], one 64-byte ReqEntry per request.
 #pragma once
 
@@ -27,10 +28,27 @@ enum : uint8_t { F_IDLE = 1, F_READY = 2, F_REG = 4 };
 struct alignas(16) ReqEntry {
   double r, p, l, arrival;
   uint64_t handle;
-  uint32_t cost, delta, rho, pad;
-  uint64_t pad2;
+  uint32_t cost, delta, rho;
+  uint32_t dec;  // pull round scratch: decision offset of this pop
+  uint32_t tie;  // pull round scratch: tie flag of this pop
+  uint32_t pad;
 };
 static_assert(sizeof(ReqEntry) == 64, "ReqEntry must be 64 bytes");
+
+// Per-client state touched at random by the add, emit and apply kernels,
+// kept together so that one client costs one or two cache lines (the
+// struct-of-arrays columns below are the ones the table scans stream).
+struct alignas(64) ClientRec {
+  double prev_r, prev_p, prev_l, prev_arr;  // ClientRec::prev_tag
+  double r_inv, w_inv, l_inv;                // ClientInfo inverses
+  uint64_t last_tick;
+};
+static_assert(sizeof(ClientRec) == 64, "ClientRec must be 64 bytes");
+struct alignas(16) QState {
+  uint32_t head, count;         // request ring cursor
+  uint32_t cur_delta, cur_rho;  // last ReqParams
+};
+static_assert(sizeof(QState) == 16, "QState must be 16 bytes");
 
 // Client table pointers (passed by value to kernels).
 struct Table {
@@ -41,14 +59,12 @@ struct Table {
   int32_t at_limit;
   double reject_thr;
   double antic;
-  double *prev_r, *prev_p, *prev_l, *prev_arr;
-  double *r_inv, *w_inv, *l_inv;
-  double *pd;
-  double *front_r, *front_p, *front_l;
-  uint32_t *head, *count, *cur_delta, *cur_rho;
-  uint64_t *last_tick;
-  uint8_t *flags;
-  ReqEntry *ring;
+  ClientRec* rec;  // N
+  QState* qs;      // N
+  double* pd;      // prop_delta (scanned)
+  double *front_r, *front_p, *front_l;  // front tag = heap keys (scanned)
+  uint8_t* flags;
+  ReqEntry* ring;
 };
 
 __host__ __device__ inline uint64_t dbits(double x) {
@@ -136,7 +152,7 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
                                   uint64_t T, uint32_t limit, V& vis,
                                   Tag3* prev_io, Tag3* front_out,
                                   uint32_t* front_cost) {
-  uint32_t h = tb.head[s], c = tb.count[s];
+  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
   uint32_t n = 0;
   if (c == 0) return 0;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
@@ -163,8 +179,8 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
   Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
   uint32_t cur_cost = e0.cost, cur_rho = e0.rho;
   uint64_t cur_h = e0.handle;
-  double rinv = tb.r_inv[s], winv = tb.w_inv[s], linv = tb.l_inv[s];
-  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
+  double rinv = tb.rec[s].r_inv, winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
+  uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
   while (n < c && n < limit) {
     if (!(cur.r <= now) || okey(cur.r) > T) break;
     vis.pop(n, cur, cur_cost, cur_h, false);
@@ -223,23 +239,27 @@ __device__ inline double reduced_r(const ReqEntry* ring, uint32_t h,
   return r;
 }
 
+// The walk starts at ring offset `start` (the front left after the round's
+// reservation pops); `start_tag` is that entry's tag in delayed mode (the
+// walk_r front, used iff use_start_tag), `ready0` its ready flag (only the untouched front can carry
+// one: a front exposed by a reservation pop is ready iff limit <= now).
 template <typename V>
 __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
                                uint64_t T, uint32_t limit, V& vis,
                                Tag3* prev_io, Tag3* front_out,
-                               uint32_t* front_cost) {
+                               uint32_t* front_cost, uint32_t start,
+                               Tag3 start_tag, bool use_start_tag, bool ready0) {
   WalkP w{0, 0, 0};
-  uint32_t h = tb.head[s], c = tb.count[s];
-  if (c == 0) return w;
+  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
+  if (start >= c) return w;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   double pdv = tb.pd[s];
-  double rinv = tb.r_inv[s];
-  bool ready0 = (tb.flags[s] & F_READY) != 0;
+  double rinv = tb.rec[s].r_inv;
   if (!tb.delayed) {
-    uint32_t i = 0;
+    uint32_t i = start;
     while (i < c && w.pops < limit) {
       const ReqEntry& e = ring[(h + i) & tb.qmask];
-      bool rdy = (i == 0) ? (ready0 || e.l <= now) : (e.l <= now);
+      bool rdy = (i == start) ? (ready0 || e.l <= now) : (e.l <= now);
       if (!rdy || !(e.p < kInf)) break;
       uint64_t key = okey(__dadd_rn(e.p, pdv));
       if (key > T) break;
@@ -270,13 +290,14 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
     return w;
   }
   // delayed mode
-  double winv = tb.w_inv[s], linv = tb.l_inv[s];
-  uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
-  const ReqEntry& e0 = ring[h & tb.qmask];
-  Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
-  uint32_t cur_cost = e0.cost, cur_rho = e0.rho;
+  double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
+  uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
+  const ReqEntry& e0 = ring[(h + start) & tb.qmask];
+  Tag3 cur = use_start_tag ? start_tag : Tag3{e0.r, e0.p, e0.l, e0.arrival};
+  uint32_t cur_cost = e0.cost;
+  uint32_t cur_rho = start ? cr : e0.rho;  // a recomputed front carries cur_rho
   uint64_t cur_h = e0.handle;
-  uint32_t i = 0;
+  uint32_t i = start;
   auto advance = [&](bool prio) {
     // pop entry i (tag `cur`), compute the next front by update_next_tag and,
     // after a priority pop, reduce it and prev (:1021-1036, :1077-1085)
@@ -303,7 +324,7 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
     if (prio && prev_io) prev_io->r = __dsub_rn(prev_io->r, off);
   };
   while (i < c && w.pops < limit) {
-    bool rdy = (i == 0) ? (ready0 || cur.l <= now) : (cur.l <= now);
+    bool rdy = (i == start) ? (ready0 || cur.l <= now) : (cur.l <= now);
     if (!rdy || !(cur.p < kInf)) break;
     uint64_t key = okey(__dadd_rn(cur.p, pdv));
     if (key > T) break;

@@ -25,13 +25,13 @@
 
 #include "../../include/dmclock_gpu.h"
 #include "dmc_device.h"
+#include "dmc_round.h"
 
 using namespace dmc;
 
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kHistBins = 2048;
 constexpr uint32_t kNone = 0xffffffffu;
 
 #define HIP_OK(expr)                                              \
@@ -43,63 +43,6 @@ constexpr uint32_t kNone = 0xffffffffu;
       return DMC_EDEVICE;                                         \
     }                                                             \
   } while (0)
-
-// Per-phase selection / bookkeeping block (device resident).
-struct Sel {
-  uint32_t n_elig;      // eligible fronts
-  uint32_t phase;       // 0 = R, 1 = P
-  uint64_t kmin, kmax;  // ordered-key range of eligible fronts
-  uint64_t T;           // ordered-key threshold (0: nothing, ~0-1: all)
-  uint32_t n_cand;      // candidate clients (key <= T)
-  uint32_t n_extra;     // entries beyond each candidate's first
-  uint32_t n_entries;   // pops (R) / groups (P) to rank
-  uint32_t shift;       // 32-bit sort key scaling
-  uint32_t n_dec_phase; // decisions taken by this phase
-  uint32_t g_last;      // last priority (limit-scan) pull index, kNone if none
-  uint32_t terminal;    // 1 if this phase ended the batch early
-  uint32_t n_prio_groups; // priority pops applied by phase P
-  uint32_t hshift;      // histogram bin of key k: (k - kmin) >> hshift
-  uint32_t tbin;        // histogram bin holding T (last bin of the rank table)
-  uint32_t bin_ovf;     // a rank bin outgrew kBinCap (skewed keys)
-};
-
-// Per-pull-batch control block (device resident): the batched phases read
-// their remaining budget from it, so a whole batch runs without host round
-// trips.
-struct Ctl {
-  uint32_t k_total;    // pulls requested
-  uint32_t n_dec;      // decisions made so far
-  uint32_t overflow;   // an entry buffer was too small: later kernels no-op
-  uint32_t terminal;   // eligible work ran out before k_total
-  uint32_t nc[2];      // candidates of phase R / P (capacity hints)
-  uint32_t nx[2];      // extra entries of phase R / P
-  uint32_t next_type;  // DMC_NEXT_* of the stopping pull
-  uint32_t pad;
-  double when;
-  // per-call parameters, published by k_scan<0> (the graph's parameter node)
-  double now;
-  dmc_decision* out;
-  uint64_t tick;
-};
-
-struct ScanPart {
-  uint32_t cnt, pad;
-  uint64_t mn, mx;
-};
-
-__device__ inline uint32_t k_left(const Ctl* c) {
-  return c->overflow ? 0u : c->k_total - c->n_dec;
-}
-
-// Per-call parameters of a pull round: the arguments of its first kernel
-// (k_scan<0>, the graph's parameter node), published through Ctl.
-struct CallParams {
-  uint32_t k_total;
-  uint32_t pad;
-  double now;
-  dmc_decision* out;
-  uint64_t tick;
-};
 
 // Single-step (one do_next_request) reduction record.
 struct ArgMin {
@@ -183,22 +126,22 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
   uint32_t s = slots[i];
   if (s >= tb.n) return;
   // ClientRec(client, info, tick), dmclock_server.h:381-393
-  tb.prev_r[s] = 0.0;
-  tb.prev_p[s] = 0.0;
-  tb.prev_l[s] = 0.0;
-  tb.prev_arr[s] = 0.0;
-  tb.r_inv[s] = rinv[i];
-  tb.w_inv[s] = winv[i];
-  tb.l_inv[s] = linv[i];
+  tb.rec[s].prev_r = 0.0;
+  tb.rec[s].prev_p = 0.0;
+  tb.rec[s].prev_l = 0.0;
+  tb.rec[s].prev_arr = 0.0;
+  tb.rec[s].r_inv = rinv[i];
+  tb.rec[s].w_inv = winv[i];
+  tb.rec[s].l_inv = linv[i];
   tb.pd[s] = 0.0;
   tb.front_r[s] = 0.0;
   tb.front_p[s] = 0.0;
   tb.front_l[s] = 0.0;
-  tb.head[s] = 0;
-  tb.count[s] = 0;
-  tb.cur_delta[s] = 1;
-  tb.cur_rho[s] = 1;
-  tb.last_tick[s] = tick;
+  tb.qs[s].head = 0;
+  tb.qs[s].count = 0;
+  tb.qs[s].cur_delta = 1;
+  tb.qs[s].cur_rho = 1;
+  tb.rec[s].last_tick = tick;
   tb.flags[s] = F_REG | (active ? 0 : F_IDLE);
 }
 
@@ -300,8 +243,9 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   e.cost = rq.cost;
   e.delta = (tb.delayed && st.count > 0) ? 0u : rq.delta;
   e.rho = (tb.delayed && st.count > 0) ? 0u : rq.rho;
+  e.dec = 0;
+  e.tie = 0;
   e.pad = 0;
-  e.pad2 = 0;
   ring[(st.head + st.count) & tb.qmask] = e;
   if (st.count == 0) {
     st.front = tag;
@@ -339,15 +283,15 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
     return;
   }
   AddState st;
-  st.prev = Tag3{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
-  st.rinv = tb.r_inv[s];
-  st.winv = tb.w_inv[s];
-  st.linv = tb.l_inv[s];
-  st.head = tb.head[s];
-  st.count = tb.count[s];
-  st.cd = tb.cur_delta[s];
-  st.cr = tb.cur_rho[s];
-  st.last_tick = tb.last_tick[s];
+  st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
+  st.rinv = tb.rec[s].r_inv;
+  st.winv = tb.rec[s].w_inv;
+  st.linv = tb.rec[s].l_inv;
+  st.head = tb.qs[s].head;
+  st.count = tb.qs[s].count;
+  st.cd = tb.qs[s].cur_delta;
+  st.cr = tb.qs[s].cur_rho;
+  st.last_tick = tb.rec[s].last_tick;
   st.flags = tb.flags[s];
   st.front_set = false;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
@@ -371,14 +315,14 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
     for (uint32_t j = 0; j < p.n; ++j)
       if (aslot[j] == s) add_one(tb, st, ring, p, j);
   }
-  tb.prev_r[s] = st.prev.r;
-  tb.prev_p[s] = st.prev.p;
-  tb.prev_l[s] = st.prev.l;
-  tb.prev_arr[s] = st.prev.arrival;
-  tb.count[s] = st.count;
-  tb.cur_delta[s] = st.cd;
-  tb.cur_rho[s] = st.cr;
-  tb.last_tick[s] = st.last_tick;
+  tb.rec[s].prev_r = st.prev.r;
+  tb.rec[s].prev_p = st.prev.p;
+  tb.rec[s].prev_l = st.prev.l;
+  tb.rec[s].prev_arr = st.prev.arrival;
+  tb.qs[s].count = st.count;
+  tb.qs[s].cur_delta = st.cd;
+  tb.qs[s].cur_rho = st.cr;
+  tb.rec[s].last_tick = st.last_tick;
   tb.flags[s] = st.flags;
   if (st.front_set) {
     tb.front_r[s] = st.front.r;
@@ -395,7 +339,7 @@ __global__ void k_contrib_min(Table tb, uint64_t* parts) {
        s += gridDim.x * blockDim.x) {
     uint8_t f = tb.flags[s];
     if ((f & F_REG) && !(f & F_IDLE)) {
-      double p = tb.count[s] ? tb.front_p[s] : tb.prev_p[s];
+      double p = tb.qs[s].count ? tb.front_p[s] : tb.rec[s].prev_p;
       uint64_t k = okey(__dadd_rn(p, tb.pd[s]));
       m = k < m ? k : m;
     }
@@ -435,894 +379,6 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
   tb.flags[s] &= (uint8_t)~F_IDLE;
 }
 
-// ------------------------------------------------------------------ pull: scans
-// Phase R scan: key = front reservation tag, eligible iff r <= now.
-// Phase P scan: first commits the limit scan of the first priority pull
-// (:1135-1144: every front with limit <= now becomes ready), then
-// key = p + prop_delta, eligible iff ready and p < inf (:1146-1151).
-// Nothing runs once the batch is complete (no further pull took place).
-// Per-block partials (count, min, max) go to `parts`: no same-address
-// atomics (thousands of waves hitting one word serialise at the memory side).
-template <int PH>
-__global__ void k_scan(Table tb, uint64_t* keys, ScanPart* parts, Ctl* ctl,
-                       CallParams cp) {
-  if (PH == 0) {  // the round's first kernel: publish the call's parameters
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      Ctl c{};
-      c.k_total = cp.k_total;
-      c.next_type = DMC_NEXT_RETURNING;
-      c.now = cp.now;
-      c.out = cp.out;
-      c.tick = cp.tick;
-      *ctl = c;
-    }
-    if (cp.k_total == 0) return;
-  } else if (k_left(ctl) == 0) {
-    return;
-  }
-  const double now = PH == 0 ? cp.now : ctl->now;
-  uint32_t cnt = 0;
-  uint64_t mn = kMaxKey, mx = 0;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    uint64_t k = kMaxKey;
-    uint32_t c = tb.count[s];
-    if (c) {
-      if (PH == 0) {
-        double r = tb.front_r[s];
-        if (r <= now) k = okey(r);
-      } else {
-        uint8_t f = tb.flags[s];
-        bool rdy = (f & F_READY) != 0;
-        if (!rdy && tb.front_l[s] <= now) {
-          rdy = true;
-          tb.flags[s] = f | F_READY;
-        }
-        double p = tb.front_p[s];
-        if (rdy && p < kInf) k = okey(__dadd_rn(p, tb.pd[s]));
-      }
-    }
-    keys[s] = k;
-    if (k != kMaxKey) {
-      ++cnt;
-      mn = k < mn ? k : mn;
-      mx = k > mx ? k : mx;
-    }
-  }
-  cnt = wave_sum_u32(cnt);
-  mn = wave_min_u64(mn);
-  mx = wave_max_u64(mx);
-  __shared__ ScanPart sh[kBlock / 64];
-  int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sh[w] = ScanPart{cnt, 0, mn, mx};
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ScanPart o = sh[0];
-    for (int i = 1; i < (int)(blockDim.x / 64); ++i) {
-      o.cnt += sh[i].cnt;
-      o.mn = sh[i].mn < o.mn ? sh[i].mn : o.mn;
-      o.mx = sh[i].mx > o.mx ? sh[i].mx : o.mx;
-    }
-    parts[blockIdx.x] = o;
-  }
-}
-
-// block-wide reduction of the scan partials (every thread gets the result)
-__device__ inline ScanPart reduce_parts(const ScanPart* parts, uint32_t nparts) {
-  __shared__ ScanPart sh[1024];
-  ScanPart o{0, 0, kMaxKey, 0};
-  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
-    ScanPart b = parts[i];
-    o.cnt += b.cnt;
-    o.mn = b.mn < o.mn ? b.mn : o.mn;
-    o.mx = b.mx > o.mx ? b.mx : o.mx;
-  }
-  sh[threadIdx.x] = o;
-  __syncthreads();
-  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d) {
-      ScanPart& a = sh[threadIdx.x];
-      const ScanPart& b = sh[threadIdx.x + d];
-      a.cnt += b.cnt;
-      a.mn = b.mn < a.mn ? b.mn : a.mn;
-      a.mx = b.mx > a.mx ? b.mx : a.mx;
-    }
-    __syncthreads();
-  }
-  ScanPart r = sh[0];
-  __syncthreads();
-  return r;
-}
-
-__device__ inline uint32_t hist_shift(uint64_t range) {
-  // smallest shift with (range >> shift) < kHistBins
-  uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
-  uint32_t hb = 11;  // log2(kHistBins)
-  return bits > hb ? bits - hb : 0;
-}
-
-// Histogram of eligible keys over [kmin, kmax] in kHistBins integer buckets
-// of the ordered-key space (monotone in the key), with the max key per
-// bucket.  kHistBlocks blocks of 1024 threads: few enough that the global
-// flush (one atomic per non-empty bin per block) stays cheap.
-constexpr int kHistBlocks = 128;
-__global__ void __launch_bounds__(1024)
-k_hist(uint32_t n, const uint64_t* keys, const ScanPart* parts,
-       uint32_t nparts, const Ctl* ctl, uint32_t* hist, uint64_t* hmax) {
-  uint32_t k_rem = k_left(ctl);
-  if (k_rem == 0) return;
-  ScanPart tot = reduce_parts(parts, nparts);
-  if (tot.cnt == 0) return;  // (also feeds the rank bins when cnt <= k_rem)
-  __shared__ uint32_t sh[kHistBins];
-  __shared__ unsigned long long smx[kHistBins];
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
-    sh[b] = 0;
-    smx[b] = 0;
-  }
-  __syncthreads();
-  uint64_t kmin = tot.mn;
-  uint32_t sh_ = hist_shift(tot.mx - kmin);
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += gridDim.x * blockDim.x) {
-    uint64_t k = keys[s];
-    if (k == kMaxKey) continue;
-    uint32_t b = (uint32_t)((k - kmin) >> sh_);
-    atomicAdd(&sh[b], 1u);
-    atomicMax(&smx[b], (unsigned long long)k);
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
-    if (sh[b]) {
-      atomicAdd(&hist[b], sh[b]);
-      atomicMax((unsigned long long*)&hmax[b], smx[b]);
-    }
-  }
-}
-
-// Threshold T: every key <= T is a candidate and at least k_rem eligible
-// fronts are <= T (T is the largest key of the bin holding the k_rem-th
-// smallest), or everything when no more than k_rem are eligible.  Also
-// (re)initialises the phase's Sel and builds the rank-bin table: the kNB rank
-// bins are spread over the histogram bins up to T's bin in proportion to
-// their counts (each gets 1 + its share), so that the rank bins stay small
-// however the keys are distributed (the rank pass is quadratic per bin).
-// kPickThreads threads; each owns kHistBins / kPickThreads bins.
-constexpr int kNB = 4096;  // rank bins
-constexpr int kPickThreads = 1024;
-constexpr int kBinsPerThread = kHistBins / kPickThreads;
-__device__ inline uint32_t block_excl_scan_1024(uint32_t v, uint32_t* wsum,
-                                                uint32_t* total) {
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t incl = v;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t wbase = 0, tot = 0;
-  for (int i = 0; i < kPickThreads / 64; ++i) {
-    if (i < w) wbase += wsum[i];
-    tot += wsum[i];
-  }
-  __syncthreads();
-  if (total) *total = tot;
-  return wbase + incl - v;
-}
-
-__global__ void __launch_bounds__(kPickThreads)
-k_pick(const ScanPart* parts, uint32_t nparts, Sel* sel, const Ctl* ctl,
-       uint32_t* hist, uint64_t* hmax, uint32_t phase, uint32_t* sbase,
-       uint32_t* snum) {
-  __shared__ uint32_t wsum[kPickThreads / 64];
-  __shared__ uint32_t s_tb, s_C;
-  uint32_t k_rem = k_left(ctl);
-  ScanPart tot = reduce_parts(parts, nparts);
-  uint32_t ne = k_rem ? tot.cnt : 0;
-  int t = threadIdx.x;
-  uint32_t sh1 = hist_shift(tot.mx - tot.mn);
-  if (t == 0) {
-    Sel z{};
-    z.n_elig = ne;
-    z.phase = phase;
-    z.kmin = tot.mn;
-    z.kmax = tot.mx;
-    z.g_last = kNone;
-    z.T = (k_rem == 0 || ne == 0) ? 0 : kMaxKey - 1;
-    z.hshift = sh1;
-    z.tbin = ne ? (uint32_t)((tot.mx - tot.mn) >> sh1) : 0;
-    *sel = z;
-    s_tb = z.tbin;
-    s_C = 0;
-  }
-  uint32_t h[kBinsPerThread];
-  uint32_t local = 0;
-  for (int j = 0; j < kBinsPerThread; ++j) {
-    h[j] = hist[t * kBinsPerThread + j];
-    local += h[j];
-  }
-  uint32_t before = block_excl_scan_1024(local, wsum, nullptr);
-  if (k_rem && ne > k_rem && before < k_rem && before + local >= k_rem) {
-    uint32_t cum = before;
-    for (int j = 0; j < kBinsPerThread; ++j) {
-      cum += h[j];
-      if (cum >= k_rem) {
-        sel->T = hmax[t * kBinsPerThread + j];
-        sel->tbin = t * kBinsPerThread + j;
-        s_tb = t * kBinsPerThread + j;
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  uint32_t tb = s_tb;
-  {
-    uint32_t cum = before;
-    for (int j = 0; j < kBinsPerThread; ++j) {
-      cum += h[j];
-      if ((uint32_t)(t * kBinsPerThread + j) == tb) s_C = cum;
-    }
-  }
-  __syncthreads();
-  uint32_t C = s_C > 0 ? s_C : 1;
-  uint32_t S = kNB - (tb + 1);
-  uint32_t ns[kBinsPerThread], lns = 0;
-  for (int j = 0; j < kBinsPerThread; ++j) {
-    uint32_t b = t * kBinsPerThread + j;
-    ns[j] = b <= tb ? 1u + (uint32_t)((uint64_t)h[j] * S / C) : 0u;
-    lns += ns[j];
-  }
-  uint32_t nb = block_excl_scan_1024(lns, wsum, nullptr);
-  for (int j = 0; j < kBinsPerThread; ++j) {
-    uint32_t b = t * kBinsPerThread + j;
-    sbase[b] = nb;
-    snum[b] = ns[j];
-    nb += ns[j];
-    hist[b] = 0;
-    hmax[b] = 0;
-  }
-}
-
-// Rank bin of an entry key (monotone in the key): its histogram bin's share
-// of the kNB rank bins, split linearly (k_pick's table).
-__device__ inline uint32_t rank_bin(uint64_t k, uint64_t kmin, uint32_t sh1,
-                                    uint32_t tb, const uint32_t* sbase,
-                                    const uint32_t* snum) {
-  uint64_t d = k > kmin ? k - kmin : 0;
-  uint64_t hb = d >> sh1;
-  uint32_t h = hb > tb ? tb : (uint32_t)hb;
-  uint64_t lo = d - ((uint64_t)h << sh1);
-  uint32_t ns = snum[h];
-  uint64_t sub = sh1 <= 51 ? (lo * ns) >> sh1 : ((lo >> 12) * ns) >> (sh1 - 12);
-  if (sub >= ns) sub = ns - 1;
-  return sbase[h] + (uint32_t)sub;
-}
-
-// ------------------------------------------------------------------ pull: walks
-struct CountVisit {
-  uint32_t pops = 0, groups = 0;
-  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
-  __device__ void group(uint64_t, uint32_t) { ++groups; }
-};
-
-// Entry id of the j-th entry of candidate i: the first lives at i, the rest
-// in the extras region (after cap1) at the candidate's extras base.
-__device__ inline uint32_t entry_id(uint32_t i, uint32_t j, uint32_t cap1,
-                                    uint32_t xbase) {
-  return j == 0 ? i : cap1 + xbase + j - 1;
-}
-
-// Rank-bin record of one entry (bin-rank path): the full order key
-// (okey, slot, seq), the group's run (P) and the entry id.
-constexpr uint32_t kBinCap = 256;  // entries per rank bin (more: bin_ovf)
-struct BRec {
-  uint64_t okey;
-  uint32_t slot;
-  uint32_t e;
-  uint32_t seq;
-  uint32_t run;
-};
-
-struct EmitVisit {
-  uint64_t* eokey;
-  uint32_t* eslot;
-  uint32_t* eseq;
-  uint32_t* erun;
-  uint32_t i, cap1, xbase, cap2, slot;
-  int ph;
-  // bin-rank path (brec != nullptr): k_pick's rank-bin table
-  BRec* brec;
-  uint32_t* bcount;
-  uint32_t* bsize;
-  const uint32_t* sbase;
-  const uint32_t* snum;
-  uint64_t kmin;
-  uint32_t sh1, tbin;
-  Sel* sel;
-  uint32_t n = 0;
-  uint64_t kmax = 0;
-  uint32_t q = 0;  // bin-rank path: entry id = candidate * q + n
-  __device__ void put(uint64_t key, uint32_t run) {
-    if (brec) {
-      if (i < cap1) {
-        uint32_t e = i * q + n;
-        uint32_t b = rank_bin(key, kmin, sh1, tbin, sbase, snum);
-        uint32_t pos = atomicAdd(&bcount[b], 1u);
-        atomicAdd(&bsize[b], ph == 0 ? 1u : 1u + run);
-        if (pos < kBinCap)
-          brec[(size_t)b * kBinCap + pos] = BRec{key, slot, e, n, run};
-        else
-          sel->bin_ovf = 1;
-      }
-    } else if (n == 0 ? i < cap1 : xbase + n - 1 < cap2) {
-      uint32_t e = entry_id(i, n, cap1, xbase);
-      {
-        eokey[e] = key;
-        eslot[e] = slot;
-        eseq[e] = n;
-        erun[e] = run;
-      }
-    }
-    kmax = key > kmax ? key : kmax;
-    ++n;
-  }
-  __device__ void pop(uint32_t, const Tag3& t, uint32_t, uint64_t, bool) {
-    if (ph == 0) put(okey(t.r), 0);
-  }
-  __device__ void group(uint64_t key, uint32_t run) { put(key, run); }
-};
-
-// Candidates = slots whose key <= T, compacted (any order: the final order
-// is fixed by the ranking on full keys).  kCandBlocks blocks, one atomic each.
-constexpr int kCandBlocks = 256;
-__global__ void k_cand(uint32_t n, const uint64_t* keys, Sel* sel,
-                       uint32_t* cand) {
-  __shared__ uint32_t wsum[kBlock / 64];
-  __shared__ uint32_t base;
-  uint64_t T = sel->T;
-  if (T == 0) return;
-  uint32_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint32_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
-  // pass 1: count
-  uint32_t c = 0;
-  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x) c += keys[s] <= T;
-  uint32_t incl = c;
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t wb = 0, tot = 0;
-  for (int i = 0; i < (int)(blockDim.x / 64); ++i) {
-    if (i < w) wb += wsum[i];
-    tot += wsum[i];
-  }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(&sel->n_cand, tot) : 0;
-  __syncthreads();
-  uint32_t o = base + wb + incl - c;
-  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
-    if (keys[s] <= T) cand[o++] = s;
-}
-
-// One thread per candidate enumerates its entries (R: pops with
-// r <= min(now, T); P: groups with key <= T) and emits (key, slot, seq, run).
-// Bin-rank path (BIN): each entry goes straight to its rank bin, with entry id
-// candidate * q + seq (no allocation needed).  Radix path: a counting walk
-// first, extras allocated with one atomic per block, then the entries go to
-// the entry arrays; per-block max key to emax[] for the 32-bit key scaling.
-template <int PH, bool BIN>
-__global__ void __launch_bounds__(kBlock)
-k_emit(Table tb, Sel* sel, const Ctl* ctl, const uint32_t* cand, uint32_t cap1,
-       uint32_t cap2, uint32_t* cxbase, uint64_t* eokey, uint32_t* eslot,
-       uint32_t* eseq, uint32_t* erun, uint64_t* emax, BRec* brec,
-       uint32_t* bcount, uint32_t* bsize, const uint32_t* sbase,
-       const uint32_t* snum) {
-  __shared__ uint32_t wsum[kBlock / 64];
-  __shared__ uint32_t base;
-  __shared__ unsigned long long bmax;
-  uint32_t nc = sel->n_cand;
-  if (blockIdx.x * blockDim.x >= nc || ctl->overflow) return;
-  const double now = ctl->now;
-  uint64_t T = sel->T;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t s = i < nc ? cand[i] : 0;
-  if (BIN) {
-    if (i >= nc) return;
-    EmitVisit v{nullptr, nullptr, nullptr, nullptr, i, cap1, 0, cap2, s, PH,
-                brec, bcount, bsize, sbase, snum, sel->kmin, sel->hshift,
-                sel->tbin, sel};
-    v.q = tb.q;
-    if (PH == 0)
-      walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
-    else
-      walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
-    return;
-  }
-  uint32_t c = 0;
-  if (i < nc) {
-    CountVisit v;
-    c = PH == 0 ? walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr)
-                : walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr).groups;
-  }
-  uint32_t x = c ? c - 1 : 0;
-  uint32_t incl = x;
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  if (threadIdx.x == 0) bmax = 0;
-  __syncthreads();
-  uint32_t wb = 0, tot = 0;
-  for (int k = 0; k < (int)(blockDim.x / 64); ++k) {
-    if (k < w) wb += wsum[k];
-    tot += wsum[k];
-  }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(&sel->n_extra, tot) : 0;
-  __syncthreads();
-  uint32_t xb = base + wb + incl - x;
-  if (i < nc) {
-    cxbase[i] = xb;
-    EmitVisit v{eokey, eslot, eseq, erun, i, cap1, xb, cap2, s, PH,
-                nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, sel};
-    if (PH == 0)
-      walk_r(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
-    else
-      walk_p(tb, s, now, T, 0xffffffffu, v, nullptr, nullptr, nullptr);
-    atomicMax(&bmax, (unsigned long long)v.kmax);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) emax[blockIdx.x] = bmax;
-}
-
-// 32-bit sort keys: (okey - kmin) >> shift with the smallest shift that keeps
-// every real key below 0xffffffff; padding entries get 0xffffffff.  Pads are
-// region-1 ids in [n_cand, cap1) and region-2 ids past the extras.
-__global__ void k_key32(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2,
-                        const uint64_t* emax, uint32_t nemax,
-                        const uint64_t* eokey, uint32_t* ek32, uint32_t* eval) {
-  __shared__ unsigned long long sh[kBlock];
-  uint32_t nc = sel->n_cand, nx = sel->n_extra;
-  bool ovf = ctl->overflow || nc > cap1 || nx > cap2;
-  uint64_t m = 0;
-  uint32_t nb = (nc + kBlock - 1) / kBlock;  // emit blocks that ran
-  if (nb < nemax) nemax = nb;
-  for (uint32_t b = threadIdx.x; b < nemax; b += blockDim.x)
-    m = emax[b] > m ? emax[b] : m;
-  sh[threadIdx.x] = m;
-  __syncthreads();
-  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d && sh[threadIdx.x + d] > sh[threadIdx.x])
-      sh[threadIdx.x] = sh[threadIdx.x + d];
-    __syncthreads();
-  }
-  uint64_t kmin = sel->kmin;
-  uint64_t range = sh[0] > kmin ? sh[0] - kmin : 0;
-  uint32_t shift = 0;
-  while ((range >> shift) >= 0xffffffffull) ++shift;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0) {
-    sel->n_entries = ovf ? 0 : nc + nx;
-    sel->shift = shift;
-    ctl->nc[sel->phase] = nc;
-    ctl->nx[sel->phase] = nx;
-    if (ovf) ctl->overflow = 1;
-  }
-  uint32_t E = cap1 + cap2;
-  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
-    bool real = !ovf && (e < nc || (e >= cap1 && e < cap1 + nx));
-    uint64_t k = real ? eokey[e] : 0;
-    ek32[e] = !real ? 0xffffffffu
-                    : (k > kmin ? (uint32_t)((k - kmin) >> shift) : 0u);
-    eval[e] = e;
-  }
-}
-
-// Full order among entries: (okey, slot, seq).
-__device__ inline bool ent_less(uint32_t a, uint32_t b, const uint64_t* eokey,
-                                const uint32_t* eslot, const uint32_t* eseq) {
-  if (eokey[a] != eokey[b]) return eokey[a] < eokey[b];
-  if (eslot[a] != eslot[b]) return eslot[a] < eslot[b];
-  return eseq[a] < eseq[b];
-}
-
-// After the 32-bit radix sort, runs of equal 32-bit keys are ordered by the
-// full key (insertion sort by the run's first thread; runs are short).
-__global__ void k_fixup(const Sel* sel, const uint32_t* sk32, uint32_t* sval,
-                        const uint64_t* eokey, const uint32_t* eslot,
-                        const uint32_t* eseq) {
-  uint32_t n = sel->n_entries;
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
-       p += gridDim.x * blockDim.x) {
-    if (p > 0 && sk32[p - 1] == sk32[p]) continue;
-    uint32_t q = p + 1;
-    while (q < n && sk32[q] == sk32[p]) ++q;
-    for (uint32_t a = p + 1; a < q; ++a) {
-      uint32_t v = sval[a];
-      uint32_t b = a;
-      while (b > p && ent_less(v, sval[b - 1], eokey, eslot, eseq)) {
-        sval[b] = sval[b - 1];
-        --b;
-      }
-      sval[b] = v;
-    }
-  }
-}
-
-__device__ inline bool tie_at(const uint64_t* eokey, const uint32_t* sval,
-                              const uint32_t* eslot, uint32_t n, uint32_t pos) {
-  uint32_t e = sval[pos];
-  if (pos > 0) {
-    uint32_t f = sval[pos - 1];
-    if (eokey[f] == eokey[e] && eslot[f] != eslot[e]) return true;
-  }
-  if (pos + 1 < n) {
-    uint32_t f = sval[pos + 1];
-    if (eokey[f] == eokey[e] && eslot[f] != eslot[e]) return true;
-  }
-  return false;
-}
-
-// R: the first k_rem sorted pops are dispatched in sorted order.
-__global__ void k_decide_r(const Ctl* ctl, const uint64_t* eokey,
-                           const uint32_t* sval, const uint32_t* eslot,
-                           uint32_t* eoff, uint8_t* etie, uint32_t* applied,
-                           Sel* sel) {
-  if (ctl->overflow) return;
-  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0) {
-    sel->n_dec_phase = n < k_rem ? n : k_rem;
-    sel->terminal = 0;
-  }
-  for (uint32_t pos = tid; pos < n; pos += gridDim.x * blockDim.x) {
-    uint32_t e = sval[pos];
-    if (pos < k_rem) {
-      eoff[e] = n_dec + pos;
-      etie[e] = tie_at(eokey, sval, eslot, n, pos) ? 1 : 0;
-      atomicAdd(&applied[eslot[e]], 1u);
-    } else {
-      eoff[e] = kNone;
-    }
-  }
-}
-
-__global__ void k_group_sizes(const Ctl* ctl, const Sel* sel, uint32_t E,
-                              const uint32_t* sval, const uint32_t* erun,
-                              uint32_t* gsz) {
-  uint32_t n = (!ctl->overflow) ? sel->n_entries : 0;
-  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < E;
-       pos += gridDim.x * blockDim.x)
-    gsz[pos] = pos < n ? 1 + erun[sval[pos]] : 0;
-}
-
-// P: groups (priority pop + the reservation run it exposes) in key order;
-// decisions are the prefix of their concatenation up to k_rem.
-__global__ void k_decide_p(const Ctl* ctl, const uint64_t* eokey,
-                           const uint32_t* sval, const uint32_t* eslot,
-                           const uint32_t* gsz, const uint32_t* goff,
-                           uint32_t* eoff, uint8_t* etie, uint32_t* applied,
-                           Sel* sel) {
-  if (ctl->overflow) return;
-  uint32_t n = sel->n_entries, k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n == 0) {
-    if (tid == 0) {
-      sel->n_dec_phase = 0;
-      sel->terminal = k_rem > 0 ? 1 : 0;
-    }
-    return;
-  }
-  for (uint32_t pos = tid; pos < n; pos += gridDim.x * blockDim.x) {
-    uint32_t e = sval[pos];
-    uint32_t o = goff[pos];
-    if (pos == n - 1) {
-      uint32_t tot = o + gsz[pos];
-      sel->n_dec_phase = tot < k_rem ? tot : k_rem;
-      sel->terminal = tot < k_rem ? 1 : 0;
-    }
-    if (o < k_rem) {
-      eoff[e] = n_dec + o;
-      etie[e] = tie_at(eokey, sval, eslot, n, pos) ? 1 : 0;
-      uint32_t na = gsz[pos];
-      if (na > k_rem - o) na = k_rem - o;
-      atomicAdd(&applied[eslot[e]], na);
-      if (pos == n - 1 || goff[pos + 1] >= k_rem) {
-        // the last applied group: its priority pop is this phase's last
-        // limit-scanning pull
-        sel->g_last = n_dec + o;
-        sel->n_prio_groups = pos + 1;
-      }
-    } else {
-      eoff[e] = kNone;
-    }
-  }
-}
-
-// ---------------------------------------------------------- pull: bin-rank
-// Ranking the entries without a general sort: k_emit files each entry in its
-// rank bin (k_pick's table: monotone in the key, balanced over the keys'
-// histogram); an entry's rank is the number of entries in earlier bins plus
-// those of its own bin that precede it in the full order (okey, slot, seq).
-// One wave per bin ranks it in LDS; each block first sums the counts and
-// group sizes of all earlier bins.  The same pass yields the group-size prefix
-// (P) and the tie flag, and decides.  A bin past kBinCap (bin_ovf) aborts the
-// batch (ctl->overflow = 2); the host then redoes it through the radix path.
-constexpr int kRankBins = kBlock / 64;        // bins per block (one per wave)
-constexpr int kRankBlocks = kNB / kRankBins;  // 1024
-template <int PH>
-__global__ void __launch_bounds__(kBlock)
-k_rank(Sel* sel, Ctl* ctl, uint32_t cap1, uint32_t cap2, const uint32_t* bcount,
-       const uint32_t* bsize, const BRec* brec, uint32_t* eoff, uint8_t* etie,
-       uint32_t* applied) {
-  __shared__ BRec sh[kBlock / 64][kBinCap];
-  __shared__ uint32_t s_off[kRankBins], s_soff[kRankBins], s_cnt[kRankBins];
-  __shared__ uint32_t s_pc[kBlock / 64], s_ps[kBlock / 64];
-  __shared__ uint32_t s_tc[kBlock / 64], s_ts[kBlock / 64], s_ne;
-  uint32_t nc = sel->n_cand, nx = 0;  // (no extra-entry region on this path)
-  bool ovf = ctl->overflow || nc > cap1 || sel->bin_ovf;
-  bool last = blockIdx.x == 0;
-  uint32_t k_rem = k_left(ctl), n_dec = ctl->n_dec;
-  if (ovf) {
-    if (last && threadIdx.x == 0) {
-      sel->n_entries = 0;
-      ctl->nc[PH] = nc;
-      ctl->nx[PH] = nx;
-      if (!ctl->overflow)
-        ctl->overflow = nc <= cap1 ? 2u : 1u;
-    }
-    return;
-  }
-  uint32_t b0 = blockIdx.x * kRankBins;
-  // entries and group sizes of all bins before b0, and in all bins
-  uint32_t pc = 0, ps = 0, tc = 0, ts = 0;
-  for (uint32_t b = threadIdx.x; b < (uint32_t)kNB; b += kBlock) {
-    uint32_t c = bcount[b], z = bsize[b];
-    if (b < b0) {
-      pc += c;
-      ps += z;
-    }
-    tc += c;
-    ts += z;
-  }
-  pc = wave_sum_u32(pc);
-  ps = wave_sum_u32(ps);
-  tc = wave_sum_u32(tc);
-  ts = wave_sum_u32(ts);
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) {
-    s_pc[w] = pc;
-    s_ps[w] = ps;
-    s_tc[w] = tc;
-    s_ts[w] = ts;
-  }
-  if (threadIdx.x < kRankBins) s_cnt[threadIdx.x] = bcount[b0 + threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t PC = 0, PS = 0, TC = 0, TS = 0;
-    for (int k = 0; k < kBlock / 64; ++k) {
-      PC += s_pc[k];
-      PS += s_ps[k];
-      TC += s_tc[k];
-      TS += s_ts[k];
-    }
-    s_ne = TC;
-    for (int k = 0; k < kRankBins; ++k) {
-      s_off[k] = PC;
-      s_soff[k] = PS;
-      PC += s_cnt[k];
-      PS += bsize[b0 + k];
-    }
-    if (last) {  // totals: the phase's decision count, terminal flag
-      sel->n_entries = TC;
-      ctl->nc[PH] = nc;
-      ctl->nx[PH] = nx;
-      sel->n_dec_phase = TS < k_rem ? TS : k_rem;
-      sel->terminal = (PH == 1 && TS < k_rem) ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  const uint32_t ne = s_ne;
-  for (int j = 0; j < kRankBins / (kBlock / 64); ++j) {
-    uint32_t lb = w * (kRankBins / (kBlock / 64)) + j;
-    uint32_t b = b0 + lb;
-    uint32_t cnt = s_cnt[lb];
-    const BRec* src = brec + (size_t)b * kBinCap;
-    for (uint32_t q = lane; q < cnt; q += 64) sh[w][q] = src[q];
-    __syncthreads();
-    for (uint32_t q = lane; q < cnt; q += 64) {
-      BRec me = sh[w][q];
-      uint32_t rank = 0, gl = 0;
-      bool tie = false;
-      for (uint32_t f = 0; f < cnt; ++f) {
-        if (f == q) continue;
-        const BRec& o = sh[w][f];
-        bool less = o.okey < me.okey ||
-                    (o.okey == me.okey &&
-                     (o.slot < me.slot || (o.slot == me.slot && o.seq < me.seq)));
-        if (less) {
-          ++rank;
-          gl += PH == 0 ? 1u : 1u + o.run;
-        }
-        if (o.okey == me.okey && o.slot != me.slot) tie = true;
-      }
-      uint32_t grank = s_off[lb] + rank;
-      uint32_t goff = PH == 0 ? grank : s_soff[lb] + gl;
-      uint32_t size = PH == 0 ? 1u : 1u + me.run;
-      if (goff < k_rem) {
-        eoff[me.e] = n_dec + goff;
-        etie[me.e] = tie ? 1 : 0;
-        uint32_t na = size < k_rem - goff ? size : k_rem - goff;
-        atomicAdd(&applied[me.slot], na);
-        if (PH == 1 && (goff + size >= k_rem || grank == ne - 1)) {
-          // the last applied group: its priority pop is this phase's last
-          // limit-scanning pull
-          sel->g_last = n_dec + goff;
-          sel->n_prio_groups = grank + 1;
-        }
-      } else {
-        eoff[me.e] = kNone;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-struct ApplyVisit {
-  dmc_decision* out;
-  const uint32_t* eoff;
-  const uint8_t* etie;
-  uint32_t i, cap1, xbase;  // candidate index, region-2 layout
-  uint32_t slot;
-  int ph;
-  uint32_t qbin;  // bin-rank path: entry id = i * qbin + seq (else region layout)
-  __device__ uint32_t id(uint32_t j) const {
-    return qbin ? i * qbin + j : entry_id(i, j, cap1, xbase);
-  }
-  uint32_t npop = 0, ngroup = 0, inrun = 0;
-  uint32_t last_idx = 0;
-  __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
-                      bool prio) {
-    uint32_t idx, tie;
-    if (ph == 0) {
-      uint32_t e = id(npop);
-      idx = eoff[e];
-      tie = etie[e];
-    } else {
-      uint32_t e = id(ngroup);
-      if (prio) inrun = 0;
-      idx = eoff[e] + inrun;
-      tie = prio ? etie[e] : 0;
-      ++inrun;
-    }
-    dmc_decision d;
-    d.handle = h;
-    d.tag_r = t.r;
-    d.tag_p = t.p;
-    d.tag_l = t.l;
-    d.slot = slot;
-    d.cost = cost;
-    d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
-    d.flags = tie;
-    out[idx] = d;
-    last_idx = idx;
-    ++npop;
-  }
-  __device__ void group(uint64_t, uint32_t) { ++ngroup; }
-};
-
-// One thread per candidate replays its walk for exactly the pops that were
-// dispatched, writes their decision records, and stores the client's new
-// state: ring head/count, front cache, reduced reservation tags (immediate:
-// every queued request, :1088-1095; delayed: the front, :1077-1085), prev tag,
-// and the front's ready flag (set iff a later limit scan saw it with
-// limit <= now).
-template <int PH>
-__global__ void k_apply(Table tb, const Sel* sel, Ctl* ctl,
-                        const uint32_t* cand, const uint32_t* cxbase,
-                        uint32_t cap1, const uint32_t* eoff,
-                        const uint8_t* etie, uint32_t* applied,
-                        uint32_t* bcount, uint32_t* bsize,
-                        unsigned long long* sched, uint32_t qbin) {
-  if (blockIdx.x == 0) {
-    // the bin-rank counters are consumed: reset them
-    for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
-      bcount[b] = 0;
-      bsize[b] = 0;
-    }
-    // end of phase: the phase's decisions are counted once here (sched[0]
-    // reservation, sched[1] priority: one per applied group), :1469,1479.
-    // No other block of this kernel reads the fields written here.
-    if (threadIdx.x == 0 && !ctl->overflow && k_left(ctl) != 0) {
-      uint32_t d = sel->n_entries ? sel->n_dec_phase : 0;
-      uint32_t np = PH == 1 && sel->n_entries ? sel->n_prio_groups : 0;
-      ctl->n_dec += d;
-      sched[0] += d - np;
-      sched[1] += np;
-      if (PH == 1 && ctl->n_dec < ctl->k_total) ctl->terminal = 1;
-    }
-  }
-  if (ctl->overflow || sel->n_entries == 0) return;
-  const double now = ctl->now;
-  const uint64_t tick = ctl->tick;
-  dmc_decision* out = ctl->out;
-  uint32_t nc = sel->n_cand;
-  uint32_t g_last = sel->g_last;
-  uint32_t terminal = sel->terminal;
-  uint64_t T = sel->T;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nc;
-       i += gridDim.x * blockDim.x) {
-    uint32_t s = cand[i];
-    uint32_t a = applied[s];
-    if (!a) continue;
-    applied[s] = 0;
-    ApplyVisit v{out, eoff, etie, i, cap1, qbin ? 0u : cxbase[i], s, PH, qbin};
-    Tag3 prev{tb.prev_r[s], tb.prev_p[s], tb.prev_l[s], tb.prev_arr[s]};
-    Tag3 front{};
-    uint32_t fcost = 0;
-    uint32_t c = tb.count[s], h = tb.head[s];
-    uint64_t pmask = 0;
-    uint32_t pops;
-    if (PH == 0) {
-      pops = walk_r(tb, s, now, T, a, v, &prev, &front, &fcost);
-    } else {
-      WalkP w = walk_p(tb, s, now, T, a, v, &prev, &front, &fcost);
-      pops = w.pops;
-      pmask = w.pmask;
-    }
-    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-    uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
-    if (!tb.delayed) {
-      if (PH == 1 && pmask) {
-        double rinv = tb.r_inv[s];
-        // remaining requests: all reductions, in order
-        for (uint32_t k = pops; k < c; ++k)
-          ring[(h + k) & tb.qmask].r = reduced_r(ring, h, tb.qmask, k, pmask, rinv);
-        double pr = prev.r;
-        for (uint32_t j = 0; j < pops; ++j)
-          if ((pmask >> j) & 1ull) {
-            const ReqEntry& ej = ring[(h + j) & tb.qmask];
-            pr = __dsub_rn(pr, resv_offset(rinv, ej.cost, ej.rho));
-          }
-        tb.prev_r[s] = pr;
-      }
-      if (nc2) {
-        const ReqEntry& f = ring[nh];
-        front = Tag3{f.r, f.p, f.l, f.arrival};
-      }
-    } else {
-      // delayed: the walk recomputed the new front and prev
-      if (nc2) {
-        ReqEntry& f = ring[nh];
-        f.r = front.r;
-        f.p = front.p;
-        f.l = front.l;
-        f.delta = tb.cur_delta[s];
-        f.rho = tb.cur_rho[s];
-      }
-      tb.prev_r[s] = prev.r;
-      tb.prev_p[s] = prev.p;
-      tb.prev_l[s] = prev.l;
-      tb.prev_arr[s] = prev.arrival;
-      if (c >= 2) tb.last_tick[s] = tick;
-    }
-    tb.head[s] = nh;
-    tb.count[s] = nc2;
-    uint8_t f = tb.flags[s] & (uint8_t)~F_READY;
-    if (nc2) {
-      tb.front_r[s] = front.r;
-      tb.front_p[s] = front.p;
-      tb.front_l[s] = front.l;
-      bool later_scan = PH == 1 && (terminal || (g_last != kNone && v.last_idx < g_last));
-      if (later_scan && front.l <= now) f |= F_READY;
-    }
-    tb.flags[s] = f;
-  }
-}
-
 // ------------------------------------------------------------------ future
 __device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
   return possible == 0.0 ? cur : (possible < cur ? possible : cur);
@@ -1333,7 +389,7 @@ __device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
 // AtLimit::Allow limit breaks, :1157-1165).  Reductions are per block, then
 // one block combines them.
 __global__ void k_step_scan(Table tb, double now, StepRed* part,
-                            const Ctl* ctl) {
+                            const Round* ctl) {
   // as the terminal pull of a batch: only if the batch ran out of work
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
   if (ctl) now = ctl->now;
@@ -1342,7 +398,7 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
   uint32_t nany = 0, nrd = 0, nnr = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    if (!tb.count[s]) continue;
+    if (!tb.qs[s].count) continue;
     ++nany;
     ArgMin a{okey(tb.front_r[s]), s, 1};
     r = argmin_combine(r, a);
@@ -1413,7 +469,7 @@ __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
 // (tree reduction in LDS), then thread 0 decides
 __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
                               int at_limit, uint32_t nregistered,
-                              StepCtl* sc, Ctl* ctl) {
+                              StepCtl* sc, Round* ctl) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
   if (ctl) now = ctl->now;
   __shared__ StepRed sh[kBlock];
@@ -1524,7 +580,7 @@ __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
   if (!sc->mark) return;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    if (tb.count[s] && !(tb.flags[s] & F_READY) && tb.front_l[s] <= now)
+    if (tb.qs[s].count && !(tb.flags[s] & F_READY) && tb.front_l[s] <= now)
       tb.flags[s] |= F_READY;
   }
 }
@@ -1539,7 +595,7 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
   uint32_t s = sc->slot;
   bool prio = sc->prio != 0;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  uint32_t h = tb.head[s], c = tb.count[s];
+  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
   ReqEntry popped = ring[h];
   dmc_decision d;
   d.handle = popped.handle;
@@ -1552,28 +608,28 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
   d.flags = sc->tie ? 1u : 0u;
   out[out_idx] = d;
   uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
-  double rinv = tb.r_inv[s];
+  double rinv = tb.rec[s].r_inv;
   if (tb.delayed && nc) {  // update_next_tag, :1021-1036
     ReqEntry& f = ring[nh];
     Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
     Tag3 nt;
-    uint32_t cd = tb.cur_delta[s], cr = tb.cur_rho[s];
-    if (make_tag(pt, rinv, tb.w_inv[s], tb.l_inv[s], cd, cr, f.arrival, f.cost,
+    uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
+    if (make_tag(pt, rinv, tb.rec[s].w_inv, tb.rec[s].l_inv, cd, cr, f.arrival, f.cost,
                  tb.antic, &nt)) {
       f.r = nt.r;
       f.p = nt.p;
       f.l = nt.l;
       f.delta = cd;
       f.rho = cr;
-      double pr = tb.prev_r[s], pp = tb.prev_p[s], pl = tb.prev_l[s];
+      double pr = tb.rec[s].prev_r, pp = tb.rec[s].prev_p, pl = tb.rec[s].prev_l;
       assign_unpinned(pr, nt.r);
       assign_unpinned(pl, nt.l);
       assign_unpinned(pp, nt.p);
-      tb.prev_r[s] = pr;
-      tb.prev_p[s] = pp;
-      tb.prev_l[s] = pl;
-      tb.prev_arr[s] = nt.arrival;
-      tb.last_tick[s] = tick;
+      tb.rec[s].prev_r = pr;
+      tb.rec[s].prev_p = pp;
+      tb.rec[s].prev_l = pl;
+      tb.rec[s].prev_arr = nt.arrival;
+      tb.rec[s].last_tick = tick;
     }
   }
   if (prio) {  // reduce_reservation_tags, :1077-1111
@@ -1586,10 +642,10 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
         e.r = __dsub_rn(e.r, o);
       }
     }
-    tb.prev_r[s] = __dsub_rn(tb.prev_r[s], o);
+    tb.rec[s].prev_r = __dsub_rn(tb.rec[s].prev_r, o);
   }
-  tb.head[s] = nh;
-  tb.count[s] = nc;
+  tb.qs[s].head = nh;
+  tb.qs[s].count = nc;
   tb.flags[s] &= (uint8_t)~F_READY;
   if (nc) {
     const ReqEntry& f = ring[nh];
@@ -1605,7 +661,7 @@ __global__ void k_count_requests(Table tb, unsigned long long* out) {
   unsigned long long t = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x)
-    t += tb.count[s];
+    t += tb.qs[s].count;
   for (int d = 32; d > 0; d >>= 1) t += shfl_down_u64(t, d);
   __shared__ unsigned long long sh[kBlock / 64];
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
@@ -1645,29 +701,30 @@ struct dmc_queue {
   uint32_t n_idle = 0;
   uint64_t tick = 0;
   // device scratch
-  uint64_t* keys = nullptr;   // N
-  uint32_t* cnt = nullptr;    // N
-  uint32_t* off = nullptr;    // N
-  uint32_t* applied = nullptr;// N
-  uint32_t* hist = nullptr;
-  uint64_t* hmax = nullptr;
-  uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin table (k_pick)
-  Sel* sel = nullptr;
+  uint32_t* applied = nullptr;// N: pops dispatched this round (R | P << 16)
+  uint32_t* cand = nullptr;   // N: candidate slots of the round
+  uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
+  uint8_t* mr = nullptr;      // N: R prefix length
+  RoundPart* rparts = nullptr;
+  Round* rd = nullptr;
+  Round* h_rd = nullptr;      // pinned: round readback
+  uint32_t* hist = nullptr;   // 2 x kHistBinsR
+  uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin tables (k_rpick)
+  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters
+  uint32_t *bsoff = nullptr, *bpoff = nullptr;   // their prefixes (k_rbscan)
+  BRecR* brec = nullptr;      // kNBR * kBinCapR rank-bin records
   StepRed* red = nullptr;     // step partials (grid) + future record
   StepCtl* sctl = nullptr;
+  StepCtl* h_sctl = nullptr;  // pinned
   uint64_t* act_min = nullptr;
   unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
   unsigned long long* reqcount = nullptr;
-  // entries (grown on demand)
-  uint32_t ecap = 0;
-  uint64_t* eokey = nullptr;  // full ordered key per entry
+  // radix path (grown on demand)
+  uint32_t ecap = 0, dense_hint = 1u << 16;
+  DEnt* dense = nullptr;
   uint32_t *ek32 = nullptr, *sk32 = nullptr;  // 32-bit sort keys
-  uint32_t *eval = nullptr, *sval = nullptr, *eslot = nullptr, *erun = nullptr;
-  uint32_t *eseq = nullptr;
-  uint32_t *eoff = nullptr, *gsz = nullptr, *goff = nullptr;
-  uint8_t* etie = nullptr;
-  size_t idcap = 0;           // eoff / etie capacity
-  Ctl* h_ctl = nullptr;              // pinned: round control readback
+  uint32_t *eval = nullptr, *sval = nullptr;
+  uint32_t *gsz = nullptr, *goff = nullptr, *gisp = nullptr, *gpoff = nullptr;
   dmc_pull_result* h_res = nullptr;  // pinned: device-API result staging
   // add batch buffers
   uint32_t bcap = 0;
@@ -1683,18 +740,8 @@ struct dmc_queue {
   size_t temp_bytes = 0;
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
-  Ctl* ctl = nullptr;
-  ScanPart* parts = nullptr;  // per-block scan partials
-  // entry capacities per phase: [0] first entries (= candidates), [1] extras
-  uint32_t cap_hint[2][2] = {{4096, 4096}, {4096, 4096}};
-  uint32_t* cand = nullptr;    // N
-  bool use_radix = false;      // rank entries with the radix sort (fallback)
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
-  uint32_t radix_batches = 0;  // batches left on the fallback path
-  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNB rank-bin counters
-  uint32_t* cxbase = nullptr;  // N
-  BRec* brec = nullptr;        // kNB * kBinCap rank-bin records
-  uint64_t* emax = nullptr;    // N / kBlock + 1
+  uint32_t radix_batches = 0;  // rounds left on the fallback path
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
   std::vector<GraphRec> graphs = std::vector<GraphRec>(8);
@@ -1716,12 +763,8 @@ struct dmc_queue {
 namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
-    "add_link", "add_chain", "activate",
-    "r_scan", "r_select", "r_cand", "r_emit", "r_key32", "r_sort",
-    "r_decide", "r_apply",
-    "p_scan", "p_select", "p_cand", "p_emit", "p_key32", "p_sort",
-    "p_decide", "p_apply",
-    "step", "future"};
+    "add_link", "add_chain", "activate", "scan", "select", "emit", "sort",
+    "rank", "apply", "step", "future"};
 
 void pb(dmc_queue* q, int stage) {
   if (!q->prof_on) return;
@@ -1849,42 +892,23 @@ int ensure_temp(dmc_queue* q, size_t need) {
   return DMC_OK;
 }
 
-// decision offset / tie flag per entry id: region layout (cap1 + cap2) on the
-// radix path, candidate * ring capacity + seq on the bin-rank path
-int ensure_ids(dmc_queue* q, size_t n) {
-  if (n <= q->idcap) return DMC_OK;
-  size_t cap = std::max<size_t>(n + (n >> 2), 1u << 16);
-  invalidate_graphs(q);
-  dfree(q->eoff);
-  dfree(q->etie);
-  q->eoff = nullptr;
-  q->etie = nullptr;
-  HIP_OK(hipMalloc(&q->eoff, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->etie, cap));
-  q->idcap = cap;
-  return DMC_OK;
-}
-
 int ensure_entries(dmc_queue* q, uint32_t n) {
   if (n <= q->ecap) return DMC_OK;
-  uint32_t cap = std::max<uint32_t>(n + (n >> 1), 1u << 16);
+  uint32_t cap = std::max<uint32_t>(n, 1u << 16);
   invalidate_graphs(q);
-  dfree(q->eokey); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
-  dfree(q->sval); dfree(q->eslot); dfree(q->erun); dfree(q->eseq);
-  dfree(q->gsz); dfree(q->goff);
-  HIP_OK(hipMalloc(&q->eokey, sizeof(uint64_t) * cap));
+  dfree(q->dense); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
+  dfree(q->sval); dfree(q->gsz); dfree(q->goff); dfree(q->gisp); dfree(q->gpoff);
+  q->ecap = 0;
+  HIP_OK(hipMalloc(&q->dense, sizeof(DEnt) * cap));
   HIP_OK(hipMalloc(&q->ek32, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->sk32, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eslot, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->erun, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eseq, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->gisp, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->gpoff, sizeof(uint32_t) * cap));
   q->ecap = cap;
-  int rc = ensure_ids(q, cap);
-  if (rc) return rc;
   size_t t1 = 0, t2 = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
                                            q->sval, (int)cap, 0, 32, q->stream);
@@ -1960,9 +984,9 @@ int activate(dmc_queue* q, uint32_t slot, double t) {
   pb(q, DMC_PROF_ACTIVATE);
   uint32_t g = grid_for(q->tb.n, 2048);
   hipLaunchKernelGGL(k_contrib_min, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     (uint64_t*)q->parts);
+                     q->act_min);
   hipLaunchKernelGGL(k_activate, dim3(1), dim3(kBlock), 0, q->stream, q->tb, slot,
-                     t, (const uint64_t*)q->parts, g);
+                     t, (const uint64_t*)q->act_min, g);
   pe(q);
   return DMC_OK;
 }
@@ -1990,9 +1014,9 @@ int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   return add_segment(q, d_reqs + start, n - start, d_rc + start, tick0 + start);
 }
 
-// --------------------------------------------------------------- pull phases
-// Larger pulls rank through the radix path: the kNB x kBinCap rank bins hold
-// about a million entries when balanced.
+// --------------------------------------------------------------- pull rounds
+// Larger pulls rank through the radix path: the kNBR x kBinCapR rank bins
+// hold about a million entries when balanced.
 constexpr uint32_t kBinRankMaxK = 1u << 18;
 
 uint32_t pow2_at_least(uint32_t x) {
@@ -2001,114 +1025,18 @@ uint32_t pow2_at_least(uint32_t x) {
   return p;
 }
 
-// Enqueue one batched phase; no host synchronisation.  `cap` is the entry
-// capacity the sort runs over (entries beyond it set ctl->overflow and the
-// rest of the batch no-ops; the host retries with a larger capacity).
-template <int PH>
-int launch_phase(dmc_queue* q, uint32_t cap1, uint32_t cap2, const CallParams& cp) {
-  const Table& tb = q->tb;
-  uint32_t N = tb.n;
-  uint32_t gN = grid_for(N, 2048);
-  uint32_t E = cap1 + cap2;
-  uint32_t gE = grid_for(E, 1024);
-  const int S0 = PH == 0 ? DMC_PROF_R_SCAN : DMC_PROF_P_SCAN;  // stage base
-  pb(q, S0 + 0);
-  hipLaunchKernelGGL(k_scan<PH>, dim3(gN), dim3(kBlock), 0, q->stream, tb,
-                     q->keys, q->parts, q->ctl, cp);
-  pe(q);
-  pb(q, S0 + 1);
-  hipLaunchKernelGGL(k_hist, dim3(kHistBlocks), dim3(1024), 0, q->stream, N,
-                     (const uint64_t*)q->keys, (const ScanPart*)q->parts, gN,
-                     (const Ctl*)q->ctl, q->hist, q->hmax);
-  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kPickThreads), 0, q->stream,
-                     (const ScanPart*)q->parts, gN, q->sel, (const Ctl*)q->ctl,
-                     q->hist, q->hmax, (uint32_t)PH, q->sbase, q->snum);
-  pe(q);
-  uint32_t gX = (N + kBlock - 1) / kBlock;  // one thread per candidate
-  pb(q, S0 + 2);
-  hipLaunchKernelGGL(k_cand, dim3(kCandBlocks), dim3(kBlock), 0, q->stream, N,
-                     (const uint64_t*)q->keys, q->sel, q->cand);
-  pe(q);
-  pb(q, S0 + 3);
-  if (q->use_radix)
-    hipLaunchKernelGGL((k_emit<PH, false>), dim3(gX), dim3(kBlock), 0, q->stream,
-                       tb, q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand,
-                       cap1, cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
-                       q->emax, nullptr, nullptr, nullptr, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL((k_emit<PH, true>), dim3(gX), dim3(kBlock), 0, q->stream,
-                       tb, q->sel, (const Ctl*)q->ctl, (const uint32_t*)q->cand,
-                       cap1, cap2, q->cxbase, q->eokey, q->eslot, q->eseq, q->erun,
-                       q->emax, q->brec, q->bcount, q->bsize,
-                       (const uint32_t*)q->sbase, (const uint32_t*)q->snum);
-  pe(q);
-  if (!q->use_radix) {
-    pb(q, S0 + 6);
-    hipLaunchKernelGGL(k_rank<PH>, dim3(kRankBlocks), dim3(kBlock), 0, q->stream,
-                       q->sel, q->ctl, cap1, cap2, (const uint32_t*)q->bcount,
-                       (const uint32_t*)q->bsize, (const BRec*)q->brec, q->eoff,
-                       q->etie, q->applied);
-    pe(q);
-  } else {
-    pb(q, S0 + 4);
-    hipLaunchKernelGGL(k_key32, dim3(gE), dim3(kBlock), 0, q->stream, q->sel,
-                       q->ctl, cap1, cap2, (const uint64_t*)q->emax, gX,
-                       (const uint64_t*)q->eokey, q->ek32, q->eval);
-    pe(q);
-    pb(q, S0 + 5);
-    size_t tbytes = q->temp_bytes;
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
-                                              q->eval, q->sval, (int)E, 0, 32,
-                                              q->stream));
-    hipLaunchKernelGGL(k_fixup, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Sel*)q->sel, (const uint32_t*)q->sk32, q->sval,
-                       (const uint64_t*)q->eokey, (const uint32_t*)q->eslot,
-                       (const uint32_t*)q->eseq);
-    pe(q);
-    pb(q, S0 + 6);
-    if (PH == 0) {
-      hipLaunchKernelGGL(k_decide_r, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                         q->eoff, q->etie, q->applied, q->sel);
-    } else {
-      hipLaunchKernelGGL(k_group_sizes, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const Sel*)q->sel, E,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->erun, q->gsz);
-      tbytes = q->temp_bytes;
-      HIP_OK(hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff,
-                                              (int)E, q->stream));
-      hipLaunchKernelGGL(k_decide_p, dim3(gE), dim3(kBlock), 0, q->stream,
-                         (const Ctl*)q->ctl, (const uint64_t*)q->eokey,
-                         (const uint32_t*)q->sval, (const uint32_t*)q->eslot,
-                         (const uint32_t*)q->gsz, (const uint32_t*)q->goff, q->eoff,
-                         q->etie, q->applied, q->sel);
-    }
-    pe(q);
-  }
-  pb(q, S0 + 7);
-  hipLaunchKernelGGL(k_apply<PH>, dim3(grid_for(N, 1024)), dim3(kBlock), 0,
-                     q->stream, tb, (const Sel*)q->sel, q->ctl,
-                     (const uint32_t*)q->cand, (const uint32_t*)q->cxbase, cap1,
-                     (const uint32_t*)q->eoff, (const uint8_t*)q->etie, q->applied,
-                     q->bcount, q->bsize, q->sched, q->use_radix ? 0u : tb.q);
-  pe(q);
-  return DMC_OK;
-}
-
 // Terminal pull of a Wait/Reject batch: one general do_next_request, which
 // (nothing being eligible) computes min_not_0 over the reservation- and
-// limit-heap tops, :1170-1185.  No-op unless ctl->terminal.
-int launch_future(dmc_queue* q, Ctl* ctl) {
-  const double now = 0.0;  // read from ctl by the kernels
+// limit-heap tops, :1170-1185.  No-op unless the round is terminal.
+void launch_future(dmc_queue* q) {
+  const double now = 0.0;  // read from the round by the kernels
   pb(q, DMC_PROF_FUTURE);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     q->tb, now, q->red, (const Ctl*)ctl);
+                     q->tb, now, q->red, (const Round*)q->rd);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, ctl);
+                     q->n_registered, q->sctl, q->rd);
   pe(q);
-  return DMC_OK;
 }
 
 // one general pull_request(now); returns the NextReqType in *type
@@ -2117,62 +1045,133 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   const Table& tb = q->tb;
   pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     tb, now, q->red, (const Ctl*)nullptr);
+                     tb, now, q->red, (const Round*)nullptr);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, (Ctl*)nullptr);
+                     q->n_registered, q->sctl, (Round*)nullptr);
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
                      q->stream, tb, now, (const StepCtl*)q->sctl);
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
                      (const StepCtl*)q->sctl, d_out, idx, q->sched);
   pe(q);
-  StepCtl sc;
-  HIP_OK(hipMemcpyAsync(&sc, q->sctl, sizeof(sc), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(q->h_sctl, q->sctl, sizeof(StepCtl), hipMemcpyDeviceToHost,
+                        q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   pflush(q);
-  *type = sc.type;
-  *when = sc.when;
+  *type = q->h_sctl->type;
+  *when = q->h_sctl->when;
   return DMC_OK;
 }
 
-// One pull round: phase R + phase P (+ the terminal pull).  The sequence
-// depends on the per-call parameters only through k_scan<0>'s
-// arguments, so it is captured once per shape (entry capacities, ranking
-// path, terminal pull) into a hipGraph and replayed with k_scan<0>'s
-// arguments updated: one graph launch instead of ~25 kernel launches, which
-// removes the host's per-launch cost from the critical path.  A shape is
-// captured the second time it is seen; profiling runs eagerly (the stage
-// timers are events between kernels).
-void enqueue_round(dmc_queue* q, const CallParams& cp, const uint32_t* cap1,
-                   const uint32_t* cap2, bool future) {
-  launch_phase<0>(q, cap1[0], cap2[0], cp);
-  launch_phase<1>(q, cap1[1], cap2[1], cp);
-  if (future) launch_future(q, q->ctl);
+// One pull round (dmc_round.h): scan, histograms, thresholds, emission,
+// ranking, apply (+ the terminal pull).  The sequence depends on the
+// per-call parameters only through k_rscan's arguments, so it is captured
+// once per shape (ranking path, dense capacity, terminal pull) into a hipGraph
+// and replayed with k_rscan's arguments updated: one graph launch instead of
+// 8-13 kernel launches, which takes the host's per-launch cost off the
+// critical path.  A shape is captured the second time it is seen; profiling
+// runs eagerly (the stage timers are events between kernels).
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) {
+  const Table& tb = q->tb;
+  uint32_t N = tb.n;
+  uint32_t gN = grid_for(N, 4096);  // k_rscan: one slot per thread up to 1M
+  // walking kernels: grid-stride over the candidate list, sized so that
+  // a typical round's candidates are resident at once
+  uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, 1024);
+  pb(q, DMC_PROF_SCAN);
+  hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kBlockR), 0, q->stream, tb, q->keyr,
+                     q->keyp, q->mr, q->rparts, q->rd, cp);
+  pe(q);
+  pb(q, DMC_PROF_SELECT);
+  hipLaunchKernelGGL(k_rreduce, dim3(1), dim3(1024), 0, q->stream,
+                     (const RoundPart*)q->rparts, gN, q->rd);
+  hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
+                     (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
+                     (const Round*)q->rd, q->hist);
+  hipLaunchKernelGGL(k_rpick, dim3(2), dim3(kPickThreadsR), 0, q->stream, q->rd,
+                     q->hist, q->sbase, q->snum);
+  pe(q);
+  pb(q, DMC_PROF_EMIT);
+  hipLaunchKernelGGL(k_rcand, dim3(kCandBlocksR), dim3(kBlockR), 0, q->stream, N,
+                     q->rd, (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
+                     q->cand);
+  hipLaunchKernelGGL(k_remit, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
+                     (const uint32_t*)q->cand,
+                     (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
+                     (const uint8_t*)q->mr, radix ? nullptr : q->brec, q->bcount,
+                     q->bsize, (const uint32_t*)q->sbase, (const uint32_t*)q->snum,
+                     q->dense, q->ecap);
+  pe(q);
+  if (!radix) {
+    pb(q, DMC_PROF_RANK);
+    hipLaunchKernelGGL(k_rbscan, dim3(1), dim3(1024), 0, q->stream, q->rd,
+                       (const uint32_t*)q->bcount, (const uint32_t*)q->bsize,
+                       q->bsoff, q->bpoff);
+    hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
+                       q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
+                       (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
+                       q->applied);
+    pe(q);
+  } else {
+    uint32_t E = q->ecap;
+    uint32_t gE = grid_for(E, 1024);
+    pb(q, DMC_PROF_SORT);
+    hipLaunchKernelGGL(k_dkey32, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E,
+                       (const DEnt*)q->dense, E, q->ek32, q->eval);
+    size_t tbytes = q->temp_bytes;
+    (void)hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
+                                             q->eval, q->sval, (int)E, 0, 32,
+                                             q->stream);
+    hipLaunchKernelGGL(k_dfixup, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Round*)q->rd, E, (const uint32_t*)q->sk32, q->sval,
+                       (const DEnt*)q->dense);
+    pe(q);
+    pb(q, DMC_PROF_RANK);
+    hipLaunchKernelGGL(k_dsizes, dim3(gE), dim3(kBlock), 0, q->stream,
+                       (const Round*)q->rd, E, E, (const uint32_t*)q->sval,
+                       (const DEnt*)q->dense, q->gsz, q->gisp);
+    tbytes = q->temp_bytes;
+    (void)hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff, (int)E,
+                                           q->stream);
+    tbytes = q->temp_bytes;
+    (void)hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gisp, q->gpoff,
+                                           (int)E, q->stream);
+    hipLaunchKernelGGL(k_ddecide, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E,
+                       (const uint32_t*)q->sval, (const DEnt*)q->dense,
+                       (const uint32_t*)q->gsz, (const uint32_t*)q->goff,
+                       (const uint32_t*)q->gpoff, tb.ring, q->applied);
+    pe(q);
+  }
+  pb(q, DMC_PROF_APPLY);
+  hipLaunchKernelGGL(k_rapply, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
+                     (const uint32_t*)q->cand, (const uint64_t*)q->keyr,
+                     (const uint64_t*)q->keyp, q->applied, q->bcount, q->bsize,
+                     q->sched);
+  pe(q);
+  if (future) launch_future(q);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
-                 const uint32_t* cap1, const uint32_t* cap2, bool future) {
-  uint64_t key = 1;  // shape: capacities (powers of two), ranking path, future
-  for (int ph = 0; ph < 2; ++ph)
-    key = key * 64 + (uint64_t)__builtin_ctz(cap1[ph]),
-    key = key * 64 + (uint64_t)__builtin_ctz(cap2[ph]);
-  key = key * 4 + (q->use_radix ? 2 : 0) + (future ? 1 : 0);
+                 bool radix, bool future) {
+  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 2) | (radix ? 2 : 0) |
+                 (future ? 1 : 0);
   CallParams cp{kk, 0, now, out, q->tick};
-  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, cap1, cap2, future); });
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, future); });
   if (!g) {
-    enqueue_round(q, cp, cap1, cap2, future);
+    enqueue_round(q, cp, radix, future);
     HIP_OK(hipGetLastError());
     return DMC_OK;
   }
   Table tb = q->tb;
-  void* args[] = {&tb, &q->keys, &q->parts, &q->ctl, &cp};
+  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->rparts, &q->rd, &cp};
   return graph_replay(q, *g, args);
 }
 
-// k successive pull_request(now).  Batched phases run with one host
-// synchronisation per round; a round ends the batch unless an entry buffer
-// overflowed (retry with more capacity) or, with AtLimit::Allow, the eligible
-// work ran out (one general limit-break step, then another round).
+// k successive pull_request(now).  Each round is one graph launch and one
+// host round trip; a round ends the batch unless the radix path's dense
+// buffer overflowed (retry with more capacity), a rank bin overflowed (retry
+// on the radix path) or, with AtLimit::Allow, the eligible work ran out (one
+// general limit-break step, then another round).
 int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
               dmc_pull_result* res) {
   dmc_pull_result r{};
@@ -2198,38 +1197,29 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       ++n_dec;
       continue;
     }
-    uint32_t cap1[2], cap2[2];
-    for (int ph = 0; ph < 2; ++ph) {
-      cap1[ph] = std::max(q->cap_hint[ph][0], pow2_at_least(std::min(kk, 1u << 16)));
-      cap2[ph] = q->cap_hint[ph][1];
-      int rc = ensure_entries(q, cap1[ph] + cap2[ph]);
-      if (rc) return rc;
-    }
-    q->use_radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
+    bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
     if (q->radix_batches) --q->radix_batches;
-    if (!q->use_radix) {
-      int rc = ensure_ids(q, (size_t)std::max(cap1[0], cap1[1]) * q->tb.q);
+    if (radix) {
+      int rc = ensure_entries(q, q->dense_hint);
       if (rc) return rc;
     }
-    int rc = launch_round(q, now, kk, d_out + n_dec, cap1, cap2, !allow);
+    int rc = launch_round(q, now, kk, d_out + n_dec, radix, !allow);
     if (rc) return rc;
     // one host round trip per round, through pinned memory
-    HIP_OK(hipMemcpyAsync(q->h_ctl, q->ctl, sizeof(Ctl), hipMemcpyDeviceToHost,
+    HIP_OK(hipMemcpyAsync(q->h_rd, q->rd, sizeof(Round), hipMemcpyDeviceToHost,
                           q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
-    const Ctl c = *q->h_ctl;
     pflush(q);
-    n_dec += c.n_dec;
-    for (int ph = 0; ph < 2; ++ph) {
-      uint32_t need[2] = {c.nc[ph], c.nx[ph]};
-      for (int r = 0; r < 2; ++r) {
-        uint32_t want = pow2_at_least(need[r] + (need[r] >> 2) + 1);
-        uint32_t& h = q->cap_hint[ph][r];
-        h = want > h ? want : std::max(want, h / 2);  // grow at once, shrink slowly
-      }
+    const Round c = *q->h_rd;
+    if (c.overflow == 1) {  // dense entries: grow and retry
+      q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
+      continue;
     }
-    if (c.overflow == 2) q->radix_batches = 8;  // skewed keys: sort instead
-    if (c.overflow) continue;  // state before the overflowing phase is intact
+    if (c.overflow == 2) {  // massively tied keys: rank by sorting instead
+      q->radix_batches = 8;
+      continue;
+    }
+    n_dec += c.n_dec;
     if (n_dec >= k || !c.terminal) break;
     if (allow) {
       int type;
@@ -2304,45 +1294,42 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
                ? DMC_OK : DMC_EDEVICE;
   };
   int rc = 0;
-  rc |= A(&t.prev_r, N); rc |= A(&t.prev_p, N); rc |= A(&t.prev_l, N);
-  rc |= A(&t.prev_arr, N); rc |= A(&t.r_inv, N); rc |= A(&t.w_inv, N);
-  rc |= A(&t.l_inv, N); rc |= A(&t.pd, N); rc |= A(&t.front_r, N);
-  rc |= A(&t.front_p, N); rc |= A(&t.front_l, N); rc |= A(&t.head, N);
-  rc |= A(&t.count, N); rc |= A(&t.cur_delta, N); rc |= A(&t.cur_rho, N);
-  rc |= A(&t.last_tick, N); rc |= A(&t.flags, N);
+  rc |= A(&t.rec, N); rc |= A(&t.qs, N);
+  rc |= A(&t.pd, N); rc |= A(&t.front_r, N);
+  rc |= A(&t.front_p, N); rc |= A(&t.front_l, N); rc |= A(&t.flags, N);
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
-  rc |= A(&q->keys, N); rc |= A(&q->cnt, N); rc |= A(&q->off, N);
   rc |= A(&q->applied, N);
-  rc |= A(&q->hist, kHistBins); rc |= A(&q->hmax, kHistBins);
-  rc |= A(&q->sbase, kHistBins); rc |= A(&q->snum, kHistBins);
-  rc |= A(&q->sel, 1);
+  rc |= A(&q->cand, N);
+  rc |= A(&q->keyr, N);
+  rc |= A(&q->keyp, N);
+  rc |= A(&q->mr, N);
+  rc |= A(&q->hist, 2 * kHistBinsR);
+  rc |= A(&q->sbase, 2 * kHistBinsR); rc |= A(&q->snum, 2 * kHistBinsR);
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
-  rc |= A(&q->ctl, 1);
-  rc |= A(&q->parts, 4096);
-  rc |= A(&q->cand, N);
-  rc |= A(&q->bcount, kNB);
-  rc |= A(&q->bsize, kNB);
-  rc |= A(&q->cxbase, N);
-  rc |= A(&q->brec, (size_t)kNB * kBinCap);
-  rc |= A(&q->emax, N / kBlock + 2);
-  rc |= A(&q->act_min, 1);
+  rc |= A(&q->rd, 1);
+  rc |= A(&q->rparts, 4096);
+  rc |= A(&q->bcount, kNBR);
+  rc |= A(&q->bsize, kNBR);
+  rc |= A(&q->bsoff, kNBR);
+  rc |= A(&q->bpoff, kNBR);
+  rc |= A(&q->brec, (size_t)kNBR * kBinCapR);
+  rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
   rc |= A(&q->acnt, N);
   rc |= A(&q->abuf, (size_t)N * kAddSlots);
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
-  if (hipHostMalloc((void**)&q->h_ctl, sizeof(Ctl), 0) != hipSuccess ||
+  if (hipHostMalloc((void**)&q->h_rd, sizeof(Round), 0) != hipSuccess ||
+      hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess ||
       hipHostMalloc((void**)&q->h_res, sizeof(dmc_pull_result), 0) != hipSuccess)
     rc |= DMC_ENOMEM;
   if (rc) {
     dmc_queue_destroy(q);
     return DMC_ENOMEM;
   }
-  size_t tscan = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, q->cnt, q->off, (int)N, q->stream);
-  if (ensure_temp(q, tscan) || ensure_entries(q, std::max<uint32_t>(p.max_batch, 1u << 16)) ||
+  if (ensure_entries(q, 1u << 16) ||
       ensure_batch(q, std::max<uint32_t>(p.max_batch, 1024)) ||
       ensure_dec(q, std::max<uint32_t>(p.max_batch, 1024))) {
     dmc_queue_destroy(q);
@@ -2363,19 +1350,18 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
-  void* ptrs[] = {t.prev_r, t.prev_p, t.prev_l, t.prev_arr, t.r_inv, t.w_inv,
-                  t.l_inv, t.pd, t.front_r, t.front_p, t.front_l, t.head,
-                  t.count, t.cur_delta, t.cur_rho, t.last_tick, t.flags, t.ring,
-                  q->keys, q->cnt, q->off, q->applied, q->hist, q->hmax, q->sbase, q->snum, q->sel,
-                  q->red, q->sctl, q->act_min, q->sched, q->reqcount, q->eokey,
-                  q->ek32, q->sk32, q->eval, q->sval, q->eslot, q->erun, q->eseq,
-                  q->eoff, q->gsz, q->goff, q->etie, q->d_reqs, q->d_rc, q->apos, q->aslot,
-                  q->acnt, q->abuf, q->apblk, q->d_dec, q->temp, q->ctl,
-                  q->parts, q->cand, q->cxbase, q->brec, q->emax, q->bcount,
-                  q->bsize};
+  void* ptrs[] = {t.rec, t.qs, t.pd, t.front_r, t.front_p, t.front_l, t.flags,
+                  t.ring,
+                  q->applied, q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
+                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize,
+                  q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
+                  q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
+                  q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
+                  q->apblk, q->d_dec, q->temp};
   for (void* p : ptrs)
     dfree(p);
-  if (q->h_ctl) (void)hipHostFree(q->h_ctl);
+  if (q->h_rd) (void)hipHostFree(q->h_rd);
+  if (q->h_sctl) (void)hipHostFree(q->h_sctl);
   if (q->h_res) (void)hipHostFree(q->h_res);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
@@ -2446,9 +1432,9 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
   std::lock_guard<std::mutex> g(q->mtx);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   double v[3] = {inv_of(r), inv_of(w), inv_of(l)};
-  HIP_OK(hipMemcpyAsync(q->tb.r_inv + slot, &v[0], 8, hipMemcpyHostToDevice, q->stream));
-  HIP_OK(hipMemcpyAsync(q->tb.w_inv + slot, &v[1], 8, hipMemcpyHostToDevice, q->stream));
-  HIP_OK(hipMemcpyAsync(q->tb.l_inv + slot, &v[2], 8, hipMemcpyHostToDevice, q->stream));
+  // r_inv, w_inv, l_inv are contiguous in ClientRec
+  HIP_OK(hipMemcpyAsync(&q->tb.rec[slot].r_inv, v, sizeof(v), hipMemcpyHostToDevice,
+                        q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
 }
@@ -2472,10 +1458,11 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
 
 static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
                         uint32_t* head) {
-  uint32_t h, c;
-  HIP_OK(hipMemcpyAsync(&h, q->tb.head + slot, 4, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&c, q->tb.count + slot, 4, hipMemcpyDeviceToHost, q->stream));
+  QState qs;
+  HIP_OK(hipMemcpyAsync(&qs, q->tb.qs + slot, sizeof(qs), hipMemcpyDeviceToHost,
+                        q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  uint32_t h = qs.head, c = qs.count;
   std::vector<ReqEntry> ring(q->p.ring_capacity);
   HIP_OK(hipMemcpyAsync(ring.data(), q->tb.ring + (size_t)slot * q->p.ring_capacity,
                         sizeof(ReqEntry) * q->p.ring_capacity, hipMemcpyDeviceToHost,
@@ -2496,9 +1483,10 @@ static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>&
   for (size_t i = 0; i < ents.size(); ++i) ring[i] = ents[i];
   HIP_OK(hipMemcpyAsync(q->tb.ring + (size_t)slot * Q, ring.data(), sizeof(ReqEntry) * Q,
                         hipMemcpyHostToDevice, q->stream));
-  uint32_t z = 0, c = (uint32_t)ents.size();
-  HIP_OK(hipMemcpyAsync(q->tb.head + slot, &z, 4, hipMemcpyHostToDevice, q->stream));
-  HIP_OK(hipMemcpyAsync(q->tb.count + slot, &c, 4, hipMemcpyHostToDevice, q->stream));
+  uint32_t hc[2] = {0, (uint32_t)ents.size()};  // head, count
+  uint32_t c = hc[1];
+  HIP_OK(hipMemcpyAsync(&q->tb.qs[slot].head, hc, sizeof(hc), hipMemcpyHostToDevice,
+                        q->stream));
   if (c) {
     HIP_OK(hipMemcpyAsync(q->tb.front_r + slot, &ring[0].r, 8, hipMemcpyHostToDevice, q->stream));
     HIP_OK(hipMemcpyAsync(q->tb.front_p + slot, &ring[0].p, 8, hipMemcpyHostToDevice, q->stream));
@@ -2527,7 +1515,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
   if (n_out) *n_out = (uint32_t)ents.size();
   uint32_t z = 0;
   uint8_t f = 0;
-  HIP_OK(hipMemcpyAsync(q->tb.count + slot, &z, 4, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(&q->tb.qs[slot].count, &z, 4, hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   if (q->idle_h[slot]) --q->n_idle;
@@ -2545,21 +1533,27 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   auto D = [&](double* dst, const double* src) {
     return hipMemcpyAsync(dst, src + slot, 8, hipMemcpyDeviceToHost, q->stream);
   };
-  uint32_t head = 0;
   uint8_t f = 0;
-  HIP_OK(D(&s->prev_r, t.prev_r)); HIP_OK(D(&s->prev_p, t.prev_p));
-  HIP_OK(D(&s->prev_l, t.prev_l)); HIP_OK(D(&s->prev_arrival, t.prev_arr));
+  ClientRec cr;
+  QState qs;
+  HIP_OK(hipMemcpyAsync(&cr, t.rec + slot, sizeof(cr), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&qs, t.qs + slot, sizeof(qs), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(D(&s->prop_delta, t.pd)); HIP_OK(D(&s->front_r, t.front_r));
   HIP_OK(D(&s->front_p, t.front_p)); HIP_OK(D(&s->front_l, t.front_l));
-  HIP_OK(D(&s->r_inv, t.r_inv)); HIP_OK(D(&s->w_inv, t.w_inv));
-  HIP_OK(D(&s->l_inv, t.l_inv));
-  HIP_OK(hipMemcpyAsync(&s->last_tick, t.last_tick + slot, 8, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&s->count, t.count + slot, 4, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&head, t.head + slot, 4, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&s->cur_delta, t.cur_delta + slot, 4, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&s->cur_rho, t.cur_rho + slot, 4, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipMemcpyAsync(&f, t.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  s->prev_r = cr.prev_r;
+  s->prev_p = cr.prev_p;
+  s->prev_l = cr.prev_l;
+  s->prev_arrival = cr.prev_arr;
+  s->r_inv = cr.r_inv;
+  s->w_inv = cr.w_inv;
+  s->l_inv = cr.l_inv;
+  s->last_tick = cr.last_tick;
+  s->count = qs.count;
+  s->cur_delta = qs.cur_delta;
+  s->cur_rho = qs.cur_rho;
+  uint32_t head = qs.head;
   if (s->count) {
     ReqEntry e;
     HIP_OK(hipMemcpyAsync(&e, t.ring + (size_t)slot * t.q + head, sizeof(e),
@@ -2578,7 +1572,10 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
 int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
   if (!q || !out || n > q->p.max_clients) return DMC_EINVAL;
   std::lock_guard<std::mutex> g(q->mtx);
-  HIP_OK(hipMemcpyAsync(out, q->tb.last_tick, 8ull * n, hipMemcpyDeviceToHost, q->stream));
+  if (n)
+    HIP_OK(hipMemcpy2DAsync(out, sizeof(uint64_t), &q->tb.rec[0].last_tick,
+                            sizeof(ClientRec), sizeof(uint64_t), n,
+                            hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
 }

@@ -1,0 +1,1065 @@
+// SPDX-License-Identifier: LGPL-2.1
+//
+// dmc_round.h -- one batched pull round: k successive pull_request(now)
+// (dmclock_server.h:1420-1489, do_next_request :1115-1186) as six
+// data-parallel kernels over the client table.
+//
+// Why one round covers both heaps.  Within a batch of pulls at one `now`:
+//  * while some front has r <= now the pulls are reservation pops in
+//    ascending r (:1124-1128), with no reductions: each client contributes a
+//    prefix of its queue ("R prefix": the entries with r <= now);
+//  * once none is left, every pull runs the limit scan (:1135-1144) and pops
+//    the ready front with the smallest p + prop_delta (:1146-1151); its
+//    reduce_reservation_tags (:1077-1111) can expose reservation pops of that
+//    client only, taken by the very next pulls.  Each client contributes a
+//    sequence of *groups* (a priority pop + the reservation run it exposes)
+//    with non-decreasing keys, starting from its state after its R prefix.
+// So the first k pulls are: if the R prefixes hold n_R >= k entries, the k
+// smallest of them; otherwise all n_R of them followed by the P groups in key
+// order up to k - n_R pops.  Each client's R prefix and group sequence is a
+// pure function of its own state, enumerated by one thread (walk_r / walk_p),
+// and the global order comes from ranking (phase, key, slot, ring position).
+//
+// Kernels (one thread per client slot unless noted):
+//   k_rscan   R prefix length + first R key, first P key of the post-R front,
+//             pending limit-scan mark; per-block counts and key ranges
+//   k_rhist   key histograms of both phases (2048 bins each)
+//   k_rpick   one block: thresholds T_R / T_P (every key <= T is a candidate,
+//             at least the needed number of keys are <= T) and the rank-bin
+//             tables (R bins [0, 2048), P bins [2048, 4096))
+//   k_remit   candidates enumerate their entries into rank bins
+//   k_rrank   one wave per rank bin: rank in LDS, decide, count applied pops
+//   k_rapply  replays each client's dispatched pops with the same arithmetic,
+//             writes the decision records and the new client state
+// A rank bin that outgrows kBinCap (massively tied keys) aborts the round
+// (overflow = 2): the host replays it on the radix path (dense entries,
+// 32-bit radix sort + exact fix-up).
+#pragma once
+
+#include "dmc_device.h"
+
+namespace dmc {
+
+constexpr int kBlockR = 256;
+constexpr int kHistBinsR = 2048;        // per phase
+constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
+constexpr int kNBPhase = kNBR / 2;
+constexpr uint32_t kBinCapR = 256;      // entries per rank bin
+constexpr uint32_t kNoneR = 0xffffffffu;
+constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
+
+// Per-phase selection state.
+struct PhaseSel {
+  uint64_t kmin, kmax;  // ordered-key range of the first keys
+  uint64_t T;           // candidates: first key <= T (0: none)
+  uint32_t n_elig;      // clients with an eligible first key
+  uint32_t hshift;      // histogram bin of key k: (k - kmin) >> hshift
+  uint32_t tbin;        // histogram bin holding T (last bin of the table)
+  uint32_t pad;
+};
+
+struct RoundPart {  // per-block partials of k_rscan
+  uint32_t cnt[2];
+  uint64_t n_r;
+  uint64_t mn[2], mx[2];
+};
+
+// Round state (device resident).
+struct Round {
+  PhaseSel ph[2];
+  uint64_t n_r;          // entries in all R prefixes
+  uint32_t k_total;      // pulls requested
+  uint32_t p_runs;       // the R prefixes hold fewer than k_total entries
+  uint32_t bin_ovf;      // a rank bin outgrew kBinCapR
+  uint32_t dense_n;      // radix path: dense entries emitted
+  uint32_t n_dec;        // decisions of the round
+  uint32_t n_prio;       // priority pops (= applied P groups)
+  uint32_t g_last;       // decision index of the last applied P group's pop
+  uint32_t terminal;     // eligible work ran out before k_total
+  uint32_t overflow;     // 1: dense capacity, 2: rank bin (retry on radix)
+  uint32_t next_type;    // DMC_NEXT_* of the stopping pull (terminal)
+  double when;
+  unsigned long long dmax[2];  // radix path: largest emitted key per phase
+  uint32_t n_cand;       // candidate clients (k_rcand)
+  uint32_t n_pgroups;    // P groups emitted (k_rbscan)
+  RoundPart tot;         // reduced scan partials (k_rreduce)
+  // per-call parameters, published by k_rscan (the graph's parameter node)
+  double now;
+  dmc_decision* out;
+  uint64_t tick;
+};
+
+struct CallParams {
+  uint32_t k_total;
+  uint32_t pad;
+  double now;
+  dmc_decision* out;
+  uint64_t tick;
+};
+
+__device__ inline uint64_t shfl_down_u64r(uint64_t v, int d) {
+  uint32_t lo = __shfl_down((uint32_t)v, d), hi = __shfl_down((uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t wmin64(uint64_t v) {
+  for (int d = 32; d > 0; d >>= 1) {
+    uint64_t o = shfl_down_u64r(v, d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ inline uint64_t wmax64(uint64_t v) {
+  for (int d = 32; d > 0; d >>= 1) {
+    uint64_t o = shfl_down_u64r(v, d);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ inline uint64_t wsum64(uint64_t v) {
+  for (int d = 32; d > 0; d >>= 1) v += shfl_down_u64r(v, d);
+  return v;
+}
+__device__ inline uint32_t wsum32(uint32_t v) {
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
+  return v;
+}
+
+struct CountV {
+  uint32_t pops = 0, groups = 0;
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
+  __device__ void group(uint64_t, uint32_t) { ++groups; }
+};
+
+// ---------------------------------------------------------------- k_rscan
+// Per slot: R key = front r if r <= now (its R prefix is walked for its
+// length and, in delayed mode, the post-R front tag); P key = p + prop_delta of
+// the post-R front if it is ready (flag, or limit <= now: the first priority
+// pull's limit scan) and p < inf.  An untouched front that this scan would
+// mark gets F_PMARK; k_rapply turns it into F_READY iff the priority pulls ran.
+__global__ void __launch_bounds__(kBlockR)
+k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
+        Round* rd, CallParams cp) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Round z{};
+    z.k_total = cp.k_total;
+    z.g_last = kNoneR;
+    z.next_type = DMC_NEXT_RETURNING;
+    z.now = cp.now;
+    z.out = cp.out;
+    z.tick = cp.tick;
+    *rd = z;
+  }
+  const double now = cp.now;
+  uint32_t cnt0 = 0, cnt1 = 0;
+  uint64_t nr = 0, mn0 = kMaxKey, mx0 = 0, mn1 = kMaxKey, mx1 = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    uint64_t kr = kMaxKey, kp = kMaxKey;
+    uint32_t m = 0;
+    uint32_t c = tb.qs[s].count;
+    uint32_t h = tb.qs[s].head;  // loaded with the columns: the walk below
+                              // starts one dependent load later
+    if (c) {
+      double fr = tb.front_r[s];
+      uint8_t f = tb.flags[s];
+      Tag3 pf;
+      bool have_pf = true, ready;
+      if (fr <= now) {
+        kr = okey(fr);
+        if (!tb.delayed) {
+          // the front (r == fr) is in the prefix; walk on from entry 1
+          const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+          m = 1;
+          while (m < c) {
+            const ReqEntry& e = ring[(h + m) & tb.qmask];
+            if (!(e.r <= now)) {
+              pf = Tag3{e.r, e.p, e.l, e.arrival};
+              break;
+            }
+            ++m;
+          }
+        } else {
+          CountV v;
+          uint32_t fc;
+          m = walk_r(tb, s, now, kMaxKey, 0xffffffffu, v, nullptr, &pf, &fc);
+        }
+        have_pf = m < c;
+        ready = pf.l <= now;
+      } else {
+        pf.p = tb.front_p[s];
+        pf.l = tb.front_l[s];
+        ready = (f & F_READY) || pf.l <= now;
+        if (!(f & F_READY) && pf.l <= now) tb.flags[s] = f | F_PMARK;
+      }
+      if (have_pf && ready && pf.p < kInf) kp = okey(__dadd_rn(pf.p, tb.pd[s]));
+    }
+    keyr[s] = kr;
+    keyp[s] = kp;
+    mr[s] = (uint8_t)m;
+    if (kr != kMaxKey) {
+      ++cnt0;
+      nr += m;
+      mn0 = kr < mn0 ? kr : mn0;
+      mx0 = kr > mx0 ? kr : mx0;
+    }
+    if (kp != kMaxKey) {
+      ++cnt1;
+      mn1 = kp < mn1 ? kp : mn1;
+      mx1 = kp > mx1 ? kp : mx1;
+    }
+  }
+  cnt0 = wsum32(cnt0);
+  cnt1 = wsum32(cnt1);
+  nr = wsum64(nr);
+  mn0 = wmin64(mn0);
+  mx0 = wmax64(mx0);
+  mn1 = wmin64(mn1);
+  mx1 = wmax64(mx1);
+  __shared__ RoundPart sh[kBlockR / 64];
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = RoundPart{{cnt0, cnt1}, nr, {mn0, mn1}, {mx0, mx1}};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    RoundPart o = sh[0];
+    for (int i = 1; i < kBlockR / 64; ++i) {
+      for (int p = 0; p < 2; ++p) {
+        o.cnt[p] += sh[i].cnt[p];
+        o.mn[p] = sh[i].mn[p] < o.mn[p] ? sh[i].mn[p] : o.mn[p];
+        o.mx[p] = sh[i].mx[p] > o.mx[p] ? sh[i].mx[p] : o.mx[p];
+      }
+      o.n_r += sh[i].n_r;
+    }
+    parts[blockIdx.x] = o;
+  }
+}
+
+__device__ inline void rpart_combine(RoundPart& a, const RoundPart& b) {
+  for (int p = 0; p < 2; ++p) {
+    a.cnt[p] += b.cnt[p];
+    a.mn[p] = b.mn[p] < a.mn[p] ? b.mn[p] : a.mn[p];
+    a.mx[p] = b.mx[p] > a.mx[p] ? b.mx[p] : a.mx[p];
+  }
+  a.n_r += b.n_r;
+}
+
+// block-wide reduction of the scan partials (every thread gets the result):
+// strided per thread, then across the wave by shuffles, then across waves
+__device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t nparts) {
+  __shared__ RoundPart sh[1024 / 64];
+  RoundPart o{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
+  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) rpart_combine(o, parts[i]);
+  for (int p = 0; p < 2; ++p) {
+    o.cnt[p] = wsum32(o.cnt[p]);
+    o.mn[p] = wmin64(o.mn[p]);
+    o.mx[p] = wmax64(o.mx[p]);
+  }
+  o.n_r = wsum64(o.n_r);
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = o;
+  __syncthreads();
+  RoundPart r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) rpart_combine(r, sh[i]);
+  __syncthreads();
+  return r;
+}
+
+// one block: the scan partials reduced once (k_rhist's blocks and k_rpick
+// read the result instead of each reducing them again)
+__global__ void __launch_bounds__(1024)
+k_rreduce(const RoundPart* parts, uint32_t nparts, Round* rd) {
+  RoundPart tot = reduce_rparts(parts, nparts);
+  if (threadIdx.x == 0) rd->tot = tot;
+}
+
+__device__ inline uint32_t hist_shift_r(uint64_t range) {
+  // smallest shift with (range >> shift) < kHistBinsR
+  uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
+  return bits > 11 ? bits - 11 : 0;
+}
+
+// ---------------------------------------------------------------- k_rhist
+// Histograms of both phases' first keys over their [kmin, kmax].
+// kHistBlocksR blocks of 1024 threads: few enough that the global flush (one
+// atomic per non-empty bin per block) stays cheap.
+constexpr int kHistBlocksR = 256;
+__global__ void __launch_bounds__(1024)
+k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp,
+        const Round* rd, uint32_t* hist) {
+  const RoundPart tot = rd->tot;
+  if (tot.cnt[0] == 0 && tot.cnt[1] == 0) return;
+  __shared__ uint32_t sh[2][kHistBinsR];
+  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x)
+    for (int p = 0; p < 2; ++p) sh[p][b] = 0;
+  __syncthreads();
+  uint32_t sh0 = hist_shift_r(tot.mx[0] - tot.mn[0]);
+  uint32_t sh1 = hist_shift_r(tot.mx[1] - tot.mn[1]);
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += gridDim.x * blockDim.x) {
+    uint64_t k = keyr[s];
+    if (k != kMaxKey) {
+      atomicAdd(&sh[0][(uint32_t)((k - tot.mn[0]) >> sh0)], 1u);
+    }
+    k = keyp[s];
+    if (k != kMaxKey) {
+      atomicAdd(&sh[1][(uint32_t)((k - tot.mn[1]) >> sh1)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x)
+    for (int p = 0; p < 2; ++p)
+      if (sh[p][b]) atomicAdd(&hist[p * kHistBinsR + b], sh[p][b]);
+}
+
+// ---------------------------------------------------------------- k_rpick
+constexpr int kPickThreadsR = 1024;
+constexpr int kBinsPerThreadR = kHistBinsR / kPickThreadsR;
+
+__device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t incl = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int i = 0; i < w; ++i) wbase += wsum[i];
+  __syncthreads();
+  return wbase + incl - v;
+}
+
+// One phase: threshold T for `need` first keys (everything if fewer are
+// eligible), and its kNBPhase rank bins spread over the histogram bins up to
+// T's bin in proportion to their counts (each gets 1 + its share), so that
+// the rank bins stay small however the keys are distributed.
+__device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
+                                  Round* rd, uint32_t* hist,
+                                  uint32_t* sbase, uint32_t* snum,
+                                  uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
+                                  uint64_t* s_T) {
+  int t = threadIdx.x;
+  uint32_t ne = tot.cnt[p];
+  uint32_t sh1 = hist_shift_r(tot.mx[p] - tot.mn[p]);
+  uint32_t* hp = hist + p * kHistBinsR;
+  if (t == 0) {
+    *s_tb = ne ? (uint32_t)((tot.mx[p] - tot.mn[p]) >> sh1) : 0;
+    *s_C = 0;
+    *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
+  }
+  uint32_t h[kBinsPerThreadR];
+  uint32_t local = 0;
+  for (int j = 0; j < kBinsPerThreadR; ++j) {
+    h[j] = hp[t * kBinsPerThreadR + j];
+    local += h[j];
+  }
+  uint32_t before = block_excl_scan_r(local, wsum);
+  if (need && ne > need && before < need && before + local >= need) {
+    uint32_t cum = before;
+    for (int j = 0; j < kBinsPerThreadR; ++j) {
+      cum += h[j];
+      if (cum >= need) {
+        // the bin's upper edge: the same candidate set as its largest key
+        uint32_t b = t * kBinsPerThreadR + j;
+        uint64_t edge = ((uint64_t)b << sh1) | ((1ull << sh1) - 1);
+        *s_T = edge >= kMaxKey - 1 - tot.mn[p] ? kMaxKey - 1 : tot.mn[p] + edge;
+        *s_tb = b;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t tb = *s_tb;
+  {
+    uint32_t cum = before;
+    for (int j = 0; j < kBinsPerThreadR; ++j) {
+      cum += h[j];
+      if ((uint32_t)(t * kBinsPerThreadR + j) == tb) *s_C = cum;
+    }
+  }
+  __syncthreads();
+  uint32_t C = *s_C > 0 ? *s_C : 1;
+  uint32_t S = kNBPhase - (tb + 1);
+  uint32_t ns[kBinsPerThreadR], lns = 0;
+  for (int j = 0; j < kBinsPerThreadR; ++j) {
+    uint32_t b = t * kBinsPerThreadR + j;
+    ns[j] = b <= tb ? 1u + (uint32_t)((uint64_t)h[j] * S / C) : 0u;
+    lns += ns[j];
+  }
+  uint32_t nb = block_excl_scan_r(lns, wsum);
+  for (int j = 0; j < kBinsPerThreadR; ++j) {
+    uint32_t b = t * kBinsPerThreadR + j;
+    sbase[p * kHistBinsR + b] = p * kNBPhase + nb;
+    snum[p * kHistBinsR + b] = ns[j];
+    nb += ns[j];
+    hp[b] = 0;
+  }
+  if (t == 0) {
+    PhaseSel z{};
+    z.kmin = tot.mn[p];
+    z.kmax = tot.mx[p];
+    z.T = *s_T;
+    z.n_elig = ne;
+    z.hshift = sh1;
+    z.tbin = tb;
+    rd->ph[p] = z;
+  }
+  __syncthreads();
+}
+
+// Two blocks, one per phase.
+__global__ void __launch_bounds__(kPickThreadsR)
+k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
+  __shared__ uint32_t wsum[kPickThreadsR / 64];
+  __shared__ uint32_t s_tb, s_C;
+  __shared__ uint64_t s_T;
+  const RoundPart tot = rd->tot;
+  uint32_t k = rd->k_total;
+  bool p_runs = tot.n_r < (uint64_t)k;
+  if (blockIdx.x == 0) {
+    // R: all prefixes when they hold fewer than k entries; else every client
+    // whose first key is at or below the k-th smallest first key's bucket
+    // (each such client contributes at least one entry <= T)
+    pick_phase(0, p_runs ? 0xffffffffu : k, tot, rd, hist, sbase, snum, wsum,
+               &s_tb, &s_C, &s_T);
+    if (threadIdx.x == 0) {
+      rd->n_r = tot.n_r;
+      rd->p_runs = p_runs ? 1 : 0;
+    }
+  } else {
+    pick_phase(1, p_runs ? k - (uint32_t)tot.n_r : 0, tot, rd, hist, sbase,
+               snum, wsum, &s_tb, &s_C, &s_T);
+  }
+}
+
+// Rank bin of an entry key (monotone in the key): its histogram bin's share
+// of the phase's rank bins, split linearly (k_rpick's table).
+__device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
+                                      const uint32_t* sbase, const uint32_t* snum) {
+  uint64_t d = k > ps.kmin ? k - ps.kmin : 0;
+  uint32_t sh1 = ps.hshift;
+  uint64_t hb = d >> sh1;
+  uint32_t h = hb > ps.tbin ? ps.tbin : (uint32_t)hb;
+  uint64_t lo = d - ((uint64_t)h << sh1);
+  uint32_t ns = snum[p * kHistBinsR + h];
+  uint64_t sub = sh1 <= 51 ? (lo * ns) >> sh1 : ((lo >> 12) * ns) >> (sh1 - 12);
+  if (sub >= ns) sub = ns - 1;
+  return sbase[p * kHistBinsR + h] + (uint32_t)sub;
+}
+
+// Rank-bin record of one entry: the order key (phase by bin, okey, slot,
+// queue position), the group's run (P) and the entry's ring index.  The
+// decision offset and tie flag are written into the ring entry itself
+// (ReqEntry::dec / ::tie), where k_rapply's walk reads them.
+struct BRecR {
+  uint64_t okey;
+  uint32_t slot;
+  uint32_t seq;
+  uint32_t run;
+  uint32_t ridx;  // slot * q + ring index
+};
+
+// Dense entry (radix path).
+struct DEnt {
+  uint64_t okey;
+  uint32_t slot;
+  uint32_t seq;   // queue position | phase << 31
+  uint32_t run;
+  uint32_t ridx;  // slot * q + ring index
+};
+
+struct EmitV {
+  int ph;
+  uint32_t slot;
+  const PhaseSel* ps;
+  // bin-rank path
+  BRecR* brec;
+  uint32_t* bcount;
+  uint32_t* bsize;
+  const uint32_t* sbase;
+  const uint32_t* snum;
+  Round* rd;
+  // radix path
+  DEnt* dense;
+  uint32_t dcap;
+  uint32_t rbase, head, qmask;  // ring index of queue position i
+  __device__ void put(uint64_t key, uint32_t pos, uint32_t run) {
+    uint32_t ridx = rbase + ((head + pos) & qmask);
+    if (brec) {
+      uint32_t b = rank_bin_r(key, *ps, ph, sbase, snum);
+      uint32_t at = atomicAdd(&bcount[b], 1u);
+      atomicAdd(&bsize[b], ph == 0 ? 1u : 1u + run);
+      if (at < kBinCapR)
+        brec[(size_t)b * kBinCapR + at] = BRecR{key, slot, pos, run, ridx};
+      else
+        rd->bin_ovf = 1;
+    } else {
+      atomicMax(&rd->dmax[ph], (unsigned long long)key);
+      uint32_t at = atomicAdd(&rd->dense_n, 1u);
+      if (at < dcap) dense[at] = DEnt{key, slot, pos | ((uint32_t)ph << 31), run, ridx};
+    }
+  }
+  uint32_t gpos = 0;
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, bool prio) {
+    if (ph == 0) put(okey(t.r), i, 0);
+    else if (prio) gpos = i;
+  }
+  __device__ void group(uint64_t key, uint32_t run) { put(key, gpos, run); }
+};
+
+// A client is a candidate iff its first R key is <= T_R or (the priority
+// pulls run and) its first P key is <= T_P.
+struct CandPred {
+  uint64_t TR, TP;  // 0: no candidates in that phase
+  __device__ explicit CandPred(const Round* rd)
+      : TR(rd->ph[0].T), TP(rd->p_runs ? rd->ph[1].T : 0) {}
+  __device__ bool operator()(uint64_t kr, uint64_t kp) const {
+    return (TR && kr <= TR) || (TP && kp <= TP);
+  }
+};
+__device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
+  return CandPred(rd)(kr, kp);
+}
+
+// ---------------------------------------------------------------- k_rcand
+// Candidates compacted into a dense list, so that the walking kernels run
+// dense waves: kCandBlocksR blocks, each owning a contiguous slot range, one
+// atomic each (list order is irrelevant: the ranking fixes the order).
+constexpr int kCandBlocksR = 256;
+__global__ void __launch_bounds__(kBlockR)
+k_rcand(uint32_t n, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
+        uint32_t* cand) {
+  __shared__ uint32_t wsum[kBlockR / 64];
+  __shared__ uint32_t base;
+  uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint32_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  const CandPred pred(rd);
+  uint32_t c = 0;
+  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
+    c += pred(keyr[s], keyp[s]);
+  uint32_t incl = c;
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+  for (int i = 0; i < kBlockR / 64; ++i) {
+    if (i < w) wb += wsum[i];
+    tot += wsum[i];
+  }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(&rd->n_cand, tot) : 0;
+  __syncthreads();
+  uint32_t o = base + wb + incl - c;
+  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
+    if (pred(keyr[s], keyp[s])) cand[o++] = s;
+}
+
+__device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
+                                const uint64_t* keyr, const uint64_t* keyp,
+                                const uint8_t* mr, BRecR* brec,
+                                uint32_t* bcount, uint32_t* bsize,
+                                const uint32_t* sbase, const uint32_t* snum,
+                                DEnt* dense, uint32_t dcap) {
+  const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
+  uint64_t kr = keyr[s], kp = keyp[s];
+  bool cr = TR && kr <= TR;
+  bool cp = rd->p_runs && TP && kp <= TP;
+  if (!cr && !cp) return;
+  const double now = rd->now;
+  Tag3 pf;
+  uint32_t fc;
+  uint32_t h = tb.qs[s].head;
+  if (cr) {
+    EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
+            s * tb.q, h, tb.qmask};
+    walk_r(tb, s, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
+  }
+  if (cp) {
+    uint32_t m = mr[s];  // the priority pulls run only after every R pop
+    bool ready0 = m == 0 && (tb.flags[s] & F_READY);
+    EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
+            s * tb.q, h, tb.qmask};
+    walk_p(tb, s, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
+           pf, m && tb.delayed, ready0);
+  }
+}
+
+// ---------------------------------------------------------------- k_remit
+// Candidates (first key <= T) enumerate their entries: R pops with
+// r <= min(now, T_R); then, if the priority pulls run, the P groups with key
+// <= T_P from the post-R state.  Bin-rank path: into the rank bins; radix
+// path: appended to the dense entry list.
+__global__ void __launch_bounds__(kBlockR)
+k_remit(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
+        const uint64_t* keyp, const uint8_t* mr, BRecR* brec, uint32_t* bcount,
+        uint32_t* bsize, const uint32_t* sbase, const uint32_t* snum,
+        DEnt* dense, uint32_t dcap) {
+  const uint32_t nc = rd->n_cand;
+  for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < nc;
+       ci += gridDim.x * blockDim.x)
+    emit_one(tb, rd, cand[ci], keyr, keyp, mr, brec, bcount, bsize, sbase, snum,
+             dense, dcap);
+}
+
+// ---------------------------------------------------------------- k_rrank
+// One wave per rank bin ranks it in LDS by (okey, slot, position); R bins
+// precede P bins, so the decision offset of an entry is the sum of the group
+// sizes (1 for R pops, 1 + run for P groups) of all earlier bins plus those
+// of its own bin that precede it.  Each block first sums the counts and sizes
+// of all earlier bins.  Decides: entry ids slot * q + position get their
+// decision offset (eoff) and tie flag; applied[slot] counts the dispatched
+// pops (low 16 bits R, high 16 bits P).
+// one block: exclusive prefixes over the rank bins of the entry counts, the
+// group sizes and the P-group counts; the round's decision count and
+// terminal flag.  A rank bin past kBinCapR aborts the round (overflow = 2).
+__global__ void __launch_bounds__(1024)
+k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
+         uint32_t* bsoff, uint32_t* bpoff) {
+  constexpr int per = kNBR / 1024;
+  __shared__ uint32_t wc[16], wz[16], wp[16];
+  if (rd->bin_ovf) {
+    if (threadIdx.x == 0) rd->overflow = 2;
+    return;
+  }
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
+  for (int j = 0; j < per; ++j) {
+    uint32_t b = t * per + j;
+    c[j] = bcount[b];
+    z[j] = bsize[b];
+    lc += c[j];
+    lz += z[j];
+    lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
+  }
+  uint32_t ic = lc, iz = lz, ip = lp;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d);
+    if (lane >= d) {
+      ic += oc;
+      iz += oz;
+      ip += op;
+    }
+  }
+  if (lane == 63) {
+    wc[w] = ic;
+    wz[w] = iz;
+    wp[w] = ip;
+  }
+  __syncthreads();
+  uint32_t bc = 0, bz = 0, bp = 0, tz = 0, tp = 0;
+  for (int i = 0; i < 16; ++i) {
+    if (i < w) {
+      bc += wc[i];
+      bz += wz[i];
+      bp += wp[i];
+    }
+    tz += wz[i];
+    tp += wp[i];
+  }
+  uint32_t oz = bz + iz - lz, op = bp + ip - lp;
+  (void)bc;
+  for (int j = 0; j < per; ++j) {
+    uint32_t b = t * per + j;
+    bsoff[b] = oz;
+    bpoff[b] = op;
+    oz += z[j];
+    if (b >= (uint32_t)kNBPhase) op += c[j];
+  }
+  if (t == 0) {
+    uint32_t k = rd->k_total;
+    rd->n_dec = tz < k ? tz : k;
+    rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
+    rd->n_pgroups = tp;
+  }
+}
+
+constexpr int kRankBinsR = kBlockR / 64;
+constexpr int kRankBlocksR = kNBR / kRankBinsR;
+__global__ void __launch_bounds__(kBlockR)
+k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
+        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
+        uint32_t* applied) {
+  __shared__ BRecR sh[kBlockR / 64][kBinCapR];
+  if (rd->overflow) return;
+  const uint32_t k = rd->k_total;
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t n_pgroups = rd->n_pgroups;
+  uint32_t b = blockIdx.x * kRankBinsR + w;
+  bool isp = b >= (uint32_t)kNBPhase;
+  uint32_t cnt = bcount[b];
+  const uint32_t soff = bsoff[b], poff = bpoff[b];
+  const BRecR* src = brec + (size_t)b * kBinCapR;
+  for (uint32_t i = lane; i < cnt; i += 64) sh[w][i] = src[i];
+  __syncthreads();
+
+  for (uint32_t i = lane; i < cnt; i += 64) {
+    BRecR me = sh[w][i];
+    uint32_t rank = 0, gl = 0;
+    bool tie = false;
+    for (uint32_t f = 0; f < cnt; ++f) {
+      if (f == i) continue;
+      const BRecR& o = sh[w][f];
+      bool less = o.okey < me.okey ||
+                  (o.okey == me.okey &&
+                   (o.slot < me.slot || (o.slot == me.slot && o.seq < me.seq)));
+      if (less) {
+        ++rank;
+        gl += isp ? 1u + o.run : 1u;
+      }
+      if (o.okey == me.okey && o.slot != me.slot) tie = true;
+    }
+    uint32_t goff = soff + gl;
+    uint32_t size = isp ? 1u + me.run : 1u;
+    if (goff < k) {
+      ring[me.ridx].dec = goff;
+      ring[me.ridx].tie = tie ? 1 : 0;
+      uint32_t na = size < k - goff ? size : k - goff;
+      atomicAdd(&applied[me.slot], isp ? na << 16 : na);
+      if (isp) {
+        uint32_t prank = poff + rank;  // among P groups
+        if (goff + size >= k || prank == n_pgroups - 1) {
+          // the last applied group: its priority pop is the round's last
+          // limit-scanning pull
+          rd->g_last = goff;
+          rd->n_prio = prank + 1;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- radix path
+// 32-bit sort keys: phase in the top bit, then (okey - kmin) >> shift with the
+// smallest shift that keeps every key of the phase below 2^31; padding gets
+// 0xffffffff.  Runs of equal 32-bit keys are ordered exactly by k_dfixup.
+__global__ void k_dkey32(Round* rd, uint32_t dcap, const DEnt* dense,
+                         uint32_t E, uint32_t* ek32, uint32_t* eval) {
+  uint32_t nd = rd->dense_n;
+  bool ovf = nd > dcap || rd->overflow;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0 && ovf && !rd->overflow) rd->overflow = 1;
+  uint32_t shift[2];
+  for (int p = 0; p < 2; ++p) {
+    const PhaseSel& ps = rd->ph[p];
+    uint64_t hi = rd->dmax[p];
+    uint64_t range = hi > ps.kmin ? hi - ps.kmin : 0;
+    uint32_t sh = 0;
+    while ((range >> sh) >= 0x7fffffffull) ++sh;
+    shift[p] = sh;
+  }
+  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
+    bool real = !ovf && e < nd;
+    uint32_t k32 = 0xffffffffu;
+    if (real) {
+      const DEnt& d = dense[e];
+      int p = d.seq >> 31;
+      uint64_t km = rd->ph[p].kmin;
+      uint64_t v = d.okey > km ? (d.okey - km) >> shift[p] : 0;
+      if (v > 0x7ffffffeull) v = 0x7ffffffeull;
+      k32 = ((uint32_t)p << 31) | (uint32_t)v;
+    }
+    ek32[e] = k32;
+    eval[e] = e;
+  }
+}
+
+__device__ inline bool dent_less(const DEnt& a, const DEnt& b) {
+  uint32_t pa = a.seq >> 31, pb = b.seq >> 31;
+  if (pa != pb) return pa < pb;
+  if (a.okey != b.okey) return a.okey < b.okey;
+  if (a.slot != b.slot) return a.slot < b.slot;
+  return (a.seq & 0x7fffffffu) < (b.seq & 0x7fffffffu);
+}
+
+__global__ void k_dfixup(const Round* rd, uint32_t dcap, const uint32_t* sk32,
+                         uint32_t* sval, const DEnt* dense) {
+  if (rd->overflow) return;
+  uint32_t n = rd->dense_n;
+  if (n > dcap) return;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
+       p += gridDim.x * blockDim.x) {
+    if (p > 0 && sk32[p - 1] == sk32[p]) continue;
+    uint32_t q = p + 1;
+    while (q < n && sk32[q] == sk32[p]) ++q;
+    for (uint32_t a = p + 1; a < q; ++a) {
+      uint32_t v = sval[a];
+      uint32_t b = a;
+      while (b > p && dent_less(dense[v], dense[sval[b - 1]])) {
+        sval[b] = sval[b - 1];
+        --b;
+      }
+      sval[b] = v;
+    }
+  }
+}
+
+__global__ void k_dsizes(const Round* rd, uint32_t dcap, uint32_t E,
+                         const uint32_t* sval, const DEnt* dense, uint32_t* gsz,
+                         uint32_t* isp) {
+  uint32_t n = (!rd->overflow && rd->dense_n <= dcap) ? rd->dense_n : 0;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < E;
+       p += gridDim.x * blockDim.x) {
+    uint32_t g = 0, ip = 0;
+    if (p < n) {
+      const DEnt& d = dense[sval[p]];
+      ip = d.seq >> 31;
+      g = ip ? 1 + d.run : 1;
+    }
+    gsz[p] = g;
+    isp[p] = ip;
+  }
+}
+
+__device__ inline bool dtie_at(const DEnt* dense, const uint32_t* sval,
+                               uint32_t n, uint32_t pos) {
+  const DEnt& e = dense[sval[pos]];
+  for (int d = -1; d <= 1; d += 2) {
+    int64_t o = (int64_t)pos + d;
+    if (o < 0 || o >= (int64_t)n) continue;
+    const DEnt& f = dense[sval[o]];
+    if ((f.seq >> 31) == (e.seq >> 31) && f.okey == e.okey && f.slot != e.slot)
+      return true;
+  }
+  return false;
+}
+
+// decisions are the prefix of the sorted entries' groups up to k
+__global__ void k_ddecide(Round* rd, uint32_t dcap, const uint32_t* sval,
+                          const DEnt* dense, const uint32_t* gsz,
+                          const uint32_t* goff, const uint32_t* gp,
+                          ReqEntry* ring, uint32_t* applied) {
+  if (rd->overflow || rd->dense_n > dcap) return;
+  uint32_t n = rd->dense_n, k = rd->k_total;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n == 0) {
+    if (tid == 0) {
+      rd->n_dec = 0;
+      rd->terminal = rd->p_runs && k > 0 ? 1 : 0;
+    }
+    return;
+  }
+  uint32_t np = gp[n - 1] + (dense[sval[n - 1]].seq >> 31);  // P groups (incl.)
+  for (uint32_t pos = tid; pos < n; pos += gridDim.x * blockDim.x) {
+    const DEnt& d = dense[sval[pos]];
+    uint32_t o = goff[pos];
+    bool isp = d.seq >> 31;
+    if (pos == n - 1) {
+      uint32_t tot = o + gsz[pos];
+      rd->n_dec = tot < k ? tot : k;
+      rd->terminal = (rd->p_runs && tot < k) ? 1 : 0;
+    }
+    if (o < k) {
+      ring[d.ridx].dec = o;
+      ring[d.ridx].tie = dtie_at(dense, sval, n, pos) ? 1 : 0;
+      uint32_t na = gsz[pos];
+      if (na > k - o) na = k - o;
+      atomicAdd(&applied[d.slot], isp ? na << 16 : na);
+      if (isp && (pos == n - 1 || goff[pos + 1] >= k)) {
+        rd->g_last = o;
+        rd->n_prio = gp[pos] + 1;  // exclusive P count before + this one
+      }
+    }
+  }
+  (void)np;
+}
+
+// ---------------------------------------------------------------- k_rapply
+struct ApplyV {
+  dmc_decision* out;
+  const ReqEntry* ring;  // this client's ring
+  uint32_t head, qmask;
+  uint32_t slot;
+  uint32_t inrun = 0, gidx = 0;
+  uint32_t last_idx = 0;
+  bool any = false;
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t cost, uint64_t h,
+                      bool prio, bool pphase) {
+    uint32_t idx, tie;
+    const ReqEntry& e = ring[(head + i) & qmask];
+    if (!pphase) {
+      idx = e.dec;
+      tie = e.tie;
+    } else {
+      if (prio) {
+        gidx = e.dec;
+        inrun = 0;
+      }
+      idx = gidx + inrun;
+      tie = prio ? e.tie : 0;
+      ++inrun;
+    }
+    dmc_decision d;
+    d.handle = h;
+    d.tag_r = t.r;
+    d.tag_p = t.p;
+    d.tag_l = t.l;
+    d.slot = slot;
+    d.cost = cost;
+    d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+    d.flags = tie;
+    out[idx] = d;
+    last_idx = idx;
+    any = true;
+  }
+};
+struct ApplyVR {
+  ApplyV* a;
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p) {
+    a->pop(i, t, c, h, p, false);
+  }
+  __device__ void group(uint64_t, uint32_t) {}
+};
+struct ApplyVP {
+  ApplyV* a;
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p) {
+    a->pop(i, t, c, h, p, true);
+  }
+  __device__ void group(uint64_t, uint32_t) {}
+};
+
+// One thread per slot.  Clients with dispatched pops replay their walks for
+// exactly those pops (R pops, then P groups from the post-R state), write the
+// decision records and store the new state: ring head/count, front cache,
+// reduced reservation tags (immediate: every queued request, in order,
+// :1088-1095; delayed: the front, :1077-1085), prev tag, and the front's ready
+// flag: a front left by reservation pops only was seen by the round's first
+// limit scan iff the priority pulls ran; one left by priority pops iff a later
+// limit-scanning pull happened (or the round's terminal pull).  Untouched
+// fronts turn their pending mark into F_READY iff the priority pulls ran.
+// Block 0 also counts the round's decisions (sched[0] reservation, sched[1]
+// priority, :1469,1479) and resets the rank-bin counters.
+__device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
+                                 uint32_t* applied) {
+  const bool ovf = rd->overflow != 0;
+  const bool p_runs = rd->p_runs != 0;
+  uint32_t a = applied[s];
+  if (a) applied[s] = 0;
+  if (!a || ovf) {
+    uint8_t f = tb.flags[s];
+    if (f & F_PMARK) {
+      f &= (uint8_t)~F_PMARK;
+      if (p_runs && !ovf) f |= F_READY;
+      tb.flags[s] = f;
+    }
+    return;
+  }
+  const double now = rd->now;
+  const uint64_t tick = rd->tick;
+  const uint32_t g_last = rd->g_last;
+  const uint32_t terminal = rd->terminal;
+  uint32_t aR = a & 0xffffu, aP = a >> 16;
+  uint32_t c = tb.qs[s].count, h = tb.qs[s].head;
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  ApplyV v{rd->out, ring, h, tb.qmask, s};
+  uint8_t f0 = tb.flags[s];
+  Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
+  Tag3 front{};
+  uint32_t fcost = 0;
+  uint32_t popsR = 0, popsP = 0;
+  uint64_t pmask = 0;
+  if (aR) {
+    ApplyVR vr{&v};
+    popsR = walk_r(tb, s, now, kMaxKey, aR, vr, &prev, &front, &fcost);
+  }
+  if (aP) {
+    ApplyVP vp{&v};
+    bool ready0 = popsR == 0 && (f0 & F_READY);
+    WalkP w = walk_p(tb, s, now, kMaxKey, aP, vp, &prev, &front, &fcost, popsR,
+                     front, popsR && tb.delayed, ready0);
+    popsP = w.pops;
+    pmask = w.pmask;
+  }
+  uint32_t pops = popsR + popsP;
+  uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
+  if (!tb.delayed) {
+    if (pmask) {
+      double rinv = tb.rec[s].r_inv;
+      // remaining requests: all reductions, in order
+      for (uint32_t k = pops; k < c; ++k)
+        ring[(h + k) & tb.qmask].r = reduced_r(ring, h, tb.qmask, k, pmask, rinv);
+      double pr = prev.r;
+      for (uint32_t j = 0; j < pops; ++j)
+        if ((pmask >> j) & 1ull) {
+          const ReqEntry& ej = ring[(h + j) & tb.qmask];
+          pr = __dsub_rn(pr, resv_offset(rinv, ej.cost, ej.rho));
+        }
+      tb.rec[s].prev_r = pr;
+    }
+    if (nc2) {
+      const ReqEntry& fe = ring[nh];
+      front = Tag3{fe.r, fe.p, fe.l, fe.arrival};
+    }
+  } else {
+    // delayed: the walks recomputed the new front and prev
+    if (nc2) {
+      ReqEntry& fe = ring[nh];
+      fe.r = front.r;
+      fe.p = front.p;
+      fe.l = front.l;
+      fe.delta = tb.qs[s].cur_delta;
+      fe.rho = tb.qs[s].cur_rho;
+    }
+    tb.rec[s].prev_r = prev.r;
+    tb.rec[s].prev_p = prev.p;
+    tb.rec[s].prev_l = prev.l;
+    tb.rec[s].prev_arr = prev.arrival;
+    if (c >= 2) tb.rec[s].last_tick = tick;
+  }
+  tb.qs[s].head = nh;
+  tb.qs[s].count = nc2;
+  uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
+  if (nc2) {
+    tb.front_r[s] = front.r;
+    tb.front_p[s] = front.p;
+    tb.front_l[s] = front.l;
+    bool seen = popsP ? (terminal || (g_last != kNoneR && v.last_idx < g_last))
+                      : p_runs;
+    if (seen && front.l <= now) f |= F_READY;
+  }
+  tb.flags[s] = f;
+}
+
+// Candidates (the dense list) with dispatched pops replay their walks for
+// exactly those pops (R pops, then P groups from the post-R state), write the
+// decision records and store the new state: ring head/count, front cache,
+// reduced reservation tags (immediate: every queued request, in order,
+// :1088-1095; delayed: the front, :1077-1085), prev tag, and the front's
+// ready flag: a front left by reservation pops only was seen by the round's
+// first limit scan iff the priority pulls ran; one left by priority pops iff
+// a later limit-scanning pull happened (or the round's terminal pull).  Then
+// every other slot turns its pending mark into F_READY iff the priority pulls
+// ran.  Block 0 also counts the round's decisions (sched[0] reservation,
+// sched[1] priority, :1469,1479) and resets the rank-bin counters.
+__global__ void __launch_bounds__(kBlockR)
+k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
+         const uint64_t* keyp, uint32_t* applied, uint32_t* bcount,
+         uint32_t* bsize, unsigned long long* sched) {
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < kNBR; b += blockDim.x) {
+      bcount[b] = 0;
+      bsize[b] = 0;
+    }
+    if (threadIdx.x == 0 && !rd->overflow) {
+      sched[0] += rd->n_dec - rd->n_prio;
+      sched[1] += rd->n_prio;
+    }
+  }
+  const uint32_t nc = rd->n_cand;
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t ci = tid; ci < nc; ci += stride) apply_one(tb, rd, cand[ci], applied);
+  const bool p_runs = rd->p_runs && !rd->overflow;
+  const CandPred pred(rd);
+  for (uint32_t s = tid; s < tb.n; s += stride) {
+    uint8_t f = tb.flags[s];
+    if (!(f & F_PMARK) || pred(keyr[s], keyp[s])) continue;
+    f &= (uint8_t)~F_PMARK;
+    if (p_runs) f |= F_READY;
+    tb.flags[s] = f;
+  }
+}
+
+}  // namespace dmc

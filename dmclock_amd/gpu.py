@@ -57,7 +57,7 @@ EXPORTS = {
                                 ctypes.POINTER(_f64)]),
     "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
-PROF_NSTAGES = 21
+PROF_NSTAGES = 11
 
 
 class DmcError(RuntimeError):

@@ -228,11 +228,15 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 #define DMC_PROF_ADD_LINK 0
 #define DMC_PROF_ADD_CHAIN 1
 #define DMC_PROF_ACTIVATE 2
-#define DMC_PROF_R_SCAN 3   /* r_scan r_select r_cand r_emit r_key32 r_sort r_decide r_apply */
-#define DMC_PROF_P_SCAN 11  /* p_scan ... p_apply, same order */
-#define DMC_PROF_STEP 19
-#define DMC_PROF_FUTURE 20
-#define DMC_PROF_NSTAGES 21
+#define DMC_PROF_SCAN 3     /* pull round: k_rscan */
+#define DMC_PROF_SELECT 4   /* k_rhist + k_rpick */
+#define DMC_PROF_EMIT 5     /* k_remit */
+#define DMC_PROF_SORT 6     /* radix path: key32 + sort + fix-up */
+#define DMC_PROF_RANK 7     /* k_rrank (radix path: sizes + scans + decide) */
+#define DMC_PROF_APPLY 8    /* k_rapply */
+#define DMC_PROF_STEP 9     /* one general pull_request */
+#define DMC_PROF_FUTURE 10  /* a round's terminal pull */
+#define DMC_PROF_NSTAGES 11
 
 int dmc_profile_enable(dmc_queue* q, int on);
 int dmc_profile_reset(dmc_queue* q);
