@@ -207,8 +207,8 @@ def main():
     st_t1 = q.stats()
     res = d_res[args.warmup:args.warmup + args.steps].cpu().numpy()
 
-    # stage-timed pass: the next prof_steps batches, kernels launched eagerly
-    # with HIP events on the engine's stream around each stage
+    # stage-timed pass: the next prof_steps batches, launched eagerly behind
+    # a GPU-side gate with HIP events on the engine's stream around each stage
     prof = {}
     prof_steps = 0
     if not args.no_profile and args.prof_steps > 0:
@@ -312,8 +312,10 @@ def main():
         "stages_ms_per_step": {n: round(ms / max(prof_steps, 1), 4)
                                for n, (c, ms) in prof.items() if c},
         "stages_note": "stage times from a second pass of prof_steps steps "
-                       "launched eagerly with HIP events between kernels; "
-                       "the timed region replays captured hipGraphs",
+                       "launched eagerly behind a GPU-side gate (all of a "
+                       "call's kernels queued before the first starts) with "
+                       "HIP events around each stage; the timed region "
+                       "replays captured hipGraphs",
         "prof_steps": prof_steps,
     }
     print(json.dumps(out))

@@ -7,8 +7,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libdmclock_gpu.so")
 SOURCES = [os.path.join(HERE, "csrc", "dmc_engine.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "dmc_device.h"),
-                  os.path.join(ROOT, "include", "dmclock_gpu.h")]
+# every source and header under csrc/ plus the C-ABI header
+DEPS = SOURCES + sorted(
+    os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
+    if f.endswith((".h", ".hip"))) + [os.path.join(ROOT, "include", "dmclock_gpu.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                # exact IEEE double tag arithmetic: no FMA contraction

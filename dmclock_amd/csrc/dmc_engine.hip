@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <mutex>
@@ -681,6 +682,12 @@ uint32_t grid_for(uint32_t n, uint32_t cap = 4096) {
 }  // namespace
 
 // ====================================================================== host
+// A stage timer: HIP events around a stage on the queue's stream.
+struct ProfRec {
+  hipEvent_t a, b;
+  int stage;
+};
+
 struct GraphRec {
   uint64_t key = 0;
   uint64_t last_use = 0;
@@ -741,6 +748,9 @@ struct dmc_queue {
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
+  bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
+  uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
+  uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
   uint32_t radix_batches = 0;  // rounds left on the fallback path
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
@@ -749,10 +759,6 @@ struct dmc_queue {
   uint32_t graph_seen_pos = 0;
   uint64_t graph_clock = 0;
   // stage timers (HIP events on the queue's stream), see dmc_profile_*
-  struct ProfRec {
-    hipEvent_t a, b;
-    int stage;
-  };
   bool prof_on = false;
   std::vector<ProfRec> prof_pool;
   size_t prof_n = 0;
@@ -766,11 +772,27 @@ const char* kStageNames[DMC_PROF_NSTAGES] = {
     "add_link", "add_chain", "activate", "scan", "select", "emit", "sort",
     "rank", "apply", "step", "future"};
 
+// Profiling launches eagerly; a short GPU-side delay queued ahead of a
+// profiled call lets the host enqueue all of the call's kernels before the
+// first one starts, so that each stage timer brackets GPU time only (kernel
+// plus its launch boundary), not the host's per-launch cost.
+__global__ void k_prof_gate(uint32_t iters) {
+  for (uint32_t i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+void prof_gate(dmc_queue* q) {
+  if (q->prof_on)
+    hipLaunchKernelGGL(k_prof_gate, dim3(1), dim3(64), 0, q->stream, 50u);  // ~170 us
+}
+
 void pb(dmc_queue* q, int stage) {
   if (!q->prof_on) return;
   if (q->prof_n == q->prof_pool.size()) {
-    dmc_queue::ProfRec r;
-    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) {
+    ProfRec r;
+    // timing-only events: no system-scope fence (no L2 writeback/invalidate
+    // between the stages they bracket)
+    if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
       q->prof_on = false;
       return;
     }
@@ -786,16 +808,22 @@ void pe(dmc_queue* q) {
   ++q->prof_n;
 }
 
-void pflush(dmc_queue* q) {
-  if (!q->prof_on || !q->prof_n) return;
-  (void)hipEventSynchronize(q->prof_pool[q->prof_n - 1].b);
-  for (size_t i = 0; i < q->prof_n; ++i) {
+void prof_accumulate(dmc_queue* q, const ProfRec* recs, size_t n) {
+  if (!n) return;
+  (void)hipEventSynchronize(recs[n - 1].b);
+  for (size_t i = 0; i < n; ++i) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, q->prof_pool[i].a, q->prof_pool[i].b) == hipSuccess) {
-      q->prof_ms[q->prof_pool[i].stage] += ms;
-      q->prof_cnt[q->prof_pool[i].stage] += 1;
+    if (hipEventElapsedTime(&ms, recs[i].a, recs[i].b) == hipSuccess) {
+      q->prof_ms[recs[i].stage] += ms;
+      q->prof_cnt[recs[i].stage] += 1;
     }
   }
+}
+
+// Collect the stage timers of everything enqueued since the last flush.
+void pflush(dmc_queue* q) {
+  if (!q->prof_on || !q->prof_n) return;
+  prof_accumulate(q, q->prof_pool.data(), q->prof_n);
   q->prof_n = 0;
 }
 
@@ -850,6 +878,8 @@ void graph_destroy(GraphRec& g) {
 // caller should launch eagerly this time.
 template <typename F>
 GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
+  // stage timers run eagerly: event-record nodes inside a replayed graph do
+  // not bracket the kernels they were captured between
   if (!q->use_graphs || q->prof_on) return nullptr;
   for (auto& g : q->graphs)
     if (g.exec && g.key == key) {
@@ -878,6 +908,7 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
 
 // Buffers captured into graphs are about to move: drop every graph.
 void invalidate_graphs(dmc_queue* q) {
+  pflush(q);
   for (auto& g : q->graphs) graph_destroy(g);
 }
 
@@ -952,6 +983,7 @@ int slot_bits(uint32_t n) {
 // kernels are captured once per batch size and replayed with k_add_link's
 // arguments updated (see launch_round).
 void enqueue_add(dmc_queue* q, const AddParams& ap) {
+  prof_gate(q);
   uint32_t g = (ap.n + kBlock - 1) / kBlock;
   pb(q, DMC_PROF_ADD_LINK);
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
@@ -1072,6 +1104,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
 // critical path.  A shape is captured the second time it is seen; profiling
 // runs eagerly (the stage timers are events between kernels).
 void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) {
+  prof_gate(q);
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = grid_for(N, 4096);  // k_rscan: one slot per thread up to 1M
@@ -1107,10 +1140,18 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
     hipLaunchKernelGGL(k_rbscan, dim3(1), dim3(1024), 0, q->stream, q->rd,
                        (const uint32_t*)q->bcount, (const uint32_t*)q->bsize,
                        q->bsoff, q->bpoff);
+    if (q->debug)
+      (void)hipMemcpyAsync(q->dbg_bins, q->bcount, kNBR * sizeof(uint32_t),
+                           hipMemcpyDeviceToDevice, q->stream);
+    if (getenv("DMC_DEBUG_RANK2"))
+      hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
+                         q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
+                         (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
+                         q->applied, 1);
     hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
                        q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
                        (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
-                       q->applied);
+                       q->applied, 0, q->debug ? q->dbg_wtime : nullptr);
     pe(q);
   } else {
     uint32_t E = q->ecap;
@@ -1211,6 +1252,27 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     HIP_OK(hipStreamSynchronize(q->stream));
     pflush(q);
     const Round c = *q->h_rd;
+    if (q->debug && getenv("DMC_DEBUG_BINS")) {
+      std::vector<uint32_t> hb(kNBR);
+      (void)hipMemcpy(hb.data(), q->dbg_bins, hb.size() * 4, hipMemcpyDeviceToHost);
+      std::vector<uint64_t> wt(2 * kNBR);
+      (void)hipMemcpy(wt.data(), q->dbg_wtime, wt.size() * 8, hipMemcpyDeviceToHost);
+      FILE* f = std::fopen(getenv("DMC_DEBUG_BINS"), "ab");
+      if (f) {
+        std::fwrite(hb.data(), 4, hb.size(), f);
+        std::fwrite(wt.data(), 8, wt.size(), f);
+        std::fclose(f);
+      }
+    }
+    if (q->debug)
+      std::fprintf(stderr,
+                   "dmc round: k=%u n_r=%llu p_runs=%u cand=%u R(elig=%u T=%s) "
+                   "P(elig=%u) dec=%u prio=%u bins max R %u P %u sumsq %llu "
+                   "ovf=%u radix=%d\n",
+                   kk, (unsigned long long)c.n_r, c.p_runs, c.n_cand,
+                   c.ph[0].n_elig, c.ph[0].T == kMaxKey - 1 ? "all" : "thr",
+                   c.ph[1].n_elig, c.n_dec, c.n_prio, c.bin_max[0], c.bin_max[1],
+                   c.bin_sq, c.overflow, (int)radix);
     if (c.overflow == 1) {  // dense entries: grow and retry
       q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
       continue;
@@ -1314,6 +1376,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->bsize, kNBR);
   rc |= A(&q->bsoff, kNBR);
   rc |= A(&q->bpoff, kNBR);
+  if (q->debug) rc |= A(&q->dbg_bins, kNBR);
+  if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   rc |= A(&q->brec, (size_t)kNBR * kBinCapR);
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
   rc |= A(&q->acnt, N);
@@ -1353,7 +1417,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.qs, t.pd, t.front_r, t.front_p, t.front_l, t.flags,
                   t.ring,
                   q->applied, q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
-                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize,
+                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,

@@ -26,7 +26,7 @@
 //   k_rhist   key histograms of both phases (2048 bins each)
 //   k_rpick   one block: thresholds T_R / T_P (every key <= T is a candidate,
 //             at least the needed number of keys are <= T) and the rank-bin
-//             tables (R bins [0, 2048), P bins [2048, 4096))
+//             tables (R bins [0, kNBPhase), P bins [kNBPhase, kNBR))
 //   k_remit   candidates enumerate their entries into rank bins
 //   k_rrank   one wave per rank bin: rank in LDS, decide, count applied pops
 //   k_rapply  replays each client's dispatched pops with the same arithmetic,
@@ -44,7 +44,7 @@ constexpr int kBlockR = 256;
 constexpr int kHistBinsR = 2048;        // per phase
 constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
 constexpr int kNBPhase = kNBR / 2;
-constexpr uint32_t kBinCapR = 256;      // entries per rank bin
+constexpr uint32_t kBinCapR = 256;      // entries per rank bin (4 per lane)
 constexpr uint32_t kNoneR = 0xffffffffu;
 constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
 
@@ -82,6 +82,8 @@ struct Round {
   unsigned long long dmax[2];  // radix path: largest emitted key per phase
   uint32_t n_cand;       // candidate clients (k_rcand)
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
+  uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
+  unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
   // per-call parameters, published by k_rscan (the graph's parameter node)
   double now;
@@ -668,6 +670,40 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
     oz += z[j];
     if (b >= (uint32_t)kNBPhase) op += c[j];
   }
+  // diagnostics: largest bin per phase, sum of squared bin counts (the rank
+  // pass's work), reduced through the wave partial slots
+  {
+    uint32_t mx = 0;
+    unsigned long long sq = 0;
+    for (int j = 0; j < per; ++j) {
+      mx = c[j] > mx ? c[j] : mx;
+      sq += (unsigned long long)c[j] * c[j];
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+      uint32_t o = __shfl_down(mx, d);
+      mx = o > mx ? o : mx;
+      sq += shfl_down_u64r(sq, d);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      wc[w] = mx;
+      wz[w] = (uint32_t)sq;
+      wp[w] = (uint32_t)(sq >> 32);
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t m0 = 0, m1 = 0;
+      unsigned long long S = 0;
+      for (int i = 0; i < 16; ++i) {
+        if (i < 8) m0 = wc[i] > m0 ? wc[i] : m0;  // threads 0..511: R bins
+        else m1 = wc[i] > m1 ? wc[i] : m1;
+        S += ((unsigned long long)wp[i] << 32) | wz[i];
+      }
+      rd->bin_max[0] = m0;
+      rd->bin_max[1] = m1;
+      rd->bin_sq = S;
+    }
+  }
   if (t == 0) {
     uint32_t k = rd->k_total;
     rd->n_dec = tz < k ? tz : k;
@@ -676,46 +712,63 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
   }
 }
 
-constexpr int kRankBinsR = kBlockR / 64;
-constexpr int kRankBlocksR = kNBR / kRankBinsR;
+// One block per rank bin.  The bin's records are staged in LDS; each record
+// is ranked against all of them by `parts` adjacent lanes, each comparing a
+// slice (parts = the largest power of two with cnt * parts <= 256, at most
+// 64), and the slices' counts are summed by shuffles: a big bin (skewed keys)
+// costs cnt^2 / 256 compare steps per lane instead of cnt.  The comparison is
+// branchless (wave-uniform trip counts, broadcast LDS reads).
+constexpr int kRankBlocksR = kNBR;
 __global__ void __launch_bounds__(kBlockR)
 k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
         const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
-        uint32_t* applied) {
-  __shared__ BRecR sh[kBlockR / 64][kBinCapR];
-  if (rd->overflow) return;
+        uint32_t* applied, int dry = 0, uint64_t* wtime = nullptr) {
+  __shared__ BRecR sh[kBinCapR];
+  uint64_t t0 = wall_clock64();
+  const uint32_t b = blockIdx.x;
+  const uint32_t cnt = bcount[b];
+  if (cnt == 0 || rd->overflow) return;
   const uint32_t k = rd->k_total;
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t n_pgroups = rd->n_pgroups;
-  uint32_t b = blockIdx.x * kRankBinsR + w;
-  bool isp = b >= (uint32_t)kNBPhase;
-  uint32_t cnt = bcount[b];
+  const bool isp = b >= (uint32_t)kNBPhase;
   const uint32_t soff = bsoff[b], poff = bpoff[b];
   const BRecR* src = brec + (size_t)b * kBinCapR;
-  for (uint32_t i = lane; i < cnt; i += 64) sh[w][i] = src[i];
+  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
+  uint32_t parts = 1;
+  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
+  const uint32_t per = (cnt + parts - 1) / parts;
   __syncthreads();
-
-  for (uint32_t i = lane; i < cnt; i += 64) {
-    BRecR me = sh[w][i];
-    uint32_t rank = 0, gl = 0;
-    bool tie = false;
-    for (uint32_t f = 0; f < cnt; ++f) {
-      if (f == i) continue;
-      const BRecR& o = sh[w][f];
-      bool less = o.okey < me.okey ||
-                  (o.okey == me.okey &&
-                   (o.slot < me.slot || (o.slot == me.slot && o.seq < me.seq)));
-      if (less) {
-        ++rank;
-        gl += isp ? 1u + o.run : 1u;
-      }
-      if (o.okey == me.okey && o.slot != me.slot) tie = true;
-    }
+  const uint32_t t = threadIdx.x;
+  const uint32_t i = t / parts, part = t % parts;
+  const bool valid = i < cnt;
+  BRecR me = sh[valid ? i : 0];
+  uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
+  if (!valid) f1 = f0;  // inactive lanes still take part in the shuffles
+  uint32_t rank = 0, gl = 0, tie = 0;
+#pragma unroll 4
+  for (uint32_t f = f0; f < f1; ++f) {
+    const BRecR o = sh[f];
+    uint32_t eqk = o.okey == me.okey;
+    uint32_t less = (uint32_t)(o.okey < me.okey) |
+                    (eqk & ((uint32_t)(o.slot < me.slot) |
+                            ((uint32_t)(o.slot == me.slot) & (uint32_t)(o.seq < me.seq))));
+    rank += less;
+    gl += less * (isp ? 1u + o.run : 1u);
+    tie |= eqk & (uint32_t)(o.slot != me.slot);
+  }
+  for (uint32_t d = 1; d < parts; d <<= 1) {
+    rank += __shfl_xor(rank, d);
+    gl += __shfl_xor(gl, d);
+    tie |= __shfl_xor(tie, d);
+  }
+  if (valid && part == 0) {
     uint32_t goff = soff + gl;
     uint32_t size = isp ? 1u + me.run : 1u;
-    if (goff < k) {
+    if (dry) {
+      if (rank == 0xffffffffu) applied[0] = gl;  // keep the work alive
+    } else if (goff < k) {
       ring[me.ridx].dec = goff;
-      ring[me.ridx].tie = tie ? 1 : 0;
+      ring[me.ridx].tie = tie;
       uint32_t na = size < k - goff ? size : k - goff;
       atomicAdd(&applied[me.slot], isp ? na << 16 : na);
       if (isp) {
@@ -728,6 +781,10 @@ k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
         }
       }
     }
+  }
+  if (wtime && threadIdx.x == 0) {
+    wtime[2 * b] = t0;
+    wtime[2 * b + 1] = wall_clock64();
   }
 }
 
