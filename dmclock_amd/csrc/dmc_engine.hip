@@ -1107,22 +1107,20 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   prof_gate(q);
   const Table& tb = q->tb;
   uint32_t N = tb.n;
-  uint32_t gN = grid_for(N, 4096);  // k_rscan: one slot per thread up to 1M
+  uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // walking kernels: grid-stride over the candidate list, sized so that
   // a typical round's candidates are resident at once
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, 1024);
   pb(q, DMC_PROF_SCAN);
-  hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kBlockR), 0, q->stream, tb, q->keyr,
+  hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
                      q->keyp, q->mr, q->rparts, q->rd, cp);
   pe(q);
   pb(q, DMC_PROF_SELECT);
-  hipLaunchKernelGGL(k_rreduce, dim3(1), dim3(1024), 0, q->stream,
-                     (const RoundPart*)q->rparts, gN, q->rd);
   hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
                      (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const Round*)q->rd, q->hist);
+                     (const RoundPart*)q->rparts, gN, q->hist);
   hipLaunchKernelGGL(k_rpick, dim3(2), dim3(kPickThreadsR), 0, q->stream, q->rd,
-                     q->hist, q->sbase, q->snum);
+                     (const RoundPart*)q->rparts, gN, q->hist, q->sbase, q->snum);
   pe(q);
   pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_rcand, dim3(kCandBlocksR), dim3(kBlockR), 0, q->stream, N,
@@ -1371,7 +1369,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
   rc |= A(&q->rd, 1);
-  rc |= A(&q->rparts, 4096);
+  rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
   rc |= A(&q->bcount, kNBR);
   rc |= A(&q->bsize, kNBR);
   rc |= A(&q->bsoff, kNBR);

@@ -138,7 +138,72 @@ struct CountV {
 // the post-R front if it is ready (flag, or limit <= now: the first priority
 // pull's limit scan) and p < inf.  An untouched front that this scan would
 // mark gets F_PMARK; k_rapply turns it into F_READY iff the priority pulls ran.
-__global__ void __launch_bounds__(kBlockR)
+// Each thread takes kScanSlots slots and issues all their column loads before
+// any walk; blocks of kScanBlock threads, so that the per-block partials
+// (counts, key ranges) that k_rhist's blocks and k_rpick reduce stay few.
+constexpr int kScanSlots = 2;
+constexpr int kScanBlock = 1024;
+
+struct ScanCols {
+  uint32_t c, h;
+  double fr, fp, fl, pd;
+  uint8_t f;
+};
+
+__device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
+                                 double now, uint64_t* keyr, uint64_t* keyp,
+                                 uint8_t* mr, RoundPart& acc) {
+  uint64_t kr = kMaxKey, kp = kMaxKey;
+  uint32_t m = 0;
+  if (x.c) {
+    Tag3 pf;
+    bool have_pf = true, ready;
+    if (x.fr <= now) {
+      kr = okey(x.fr);
+      if (!tb.delayed) {
+        // the front (r == fr) is in the prefix; walk on from entry 1
+        const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+        m = 1;
+        while (m < x.c) {
+          const ReqEntry& e = ring[(x.h + m) & tb.qmask];
+          if (!(e.r <= now)) {
+            pf = Tag3{e.r, e.p, e.l, e.arrival};
+            break;
+          }
+          ++m;
+        }
+      } else {
+        CountV v;
+        uint32_t fc;
+        m = walk_r(tb, s, now, kMaxKey, 0xffffffffu, v, nullptr, &pf, &fc);
+      }
+      have_pf = m < x.c;
+      ready = pf.l <= now;
+    } else {
+      pf.p = x.fp;
+      pf.l = x.fl;
+      ready = (x.f & F_READY) || pf.l <= now;
+      if (!(x.f & F_READY) && pf.l <= now) tb.flags[s] = x.f | F_PMARK;
+    }
+    if (have_pf && ready && pf.p < kInf) kp = okey(__dadd_rn(pf.p, x.pd));
+  }
+  keyr[s] = kr;
+  keyp[s] = kp;
+  mr[s] = (uint8_t)m;
+  if (kr != kMaxKey) {
+    ++acc.cnt[0];
+    acc.n_r += m;
+    acc.mn[0] = kr < acc.mn[0] ? kr : acc.mn[0];
+    acc.mx[0] = kr > acc.mx[0] ? kr : acc.mx[0];
+  }
+  if (kp != kMaxKey) {
+    ++acc.cnt[1];
+    acc.mn[1] = kp < acc.mn[1] ? kp : acc.mn[1];
+    acc.mx[1] = kp > acc.mx[1] ? kp : acc.mx[1];
+  }
+}
+
+__global__ void __launch_bounds__(kScanBlock)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
         Round* rd, CallParams cp) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -152,78 +217,39 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     *rd = z;
   }
   const double now = cp.now;
-  uint32_t cnt0 = 0, cnt1 = 0;
-  uint64_t nr = 0, mn0 = kMaxKey, mx0 = 0, mn1 = kMaxKey, mx1 = 0;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    uint64_t kr = kMaxKey, kp = kMaxKey;
-    uint32_t m = 0;
-    uint32_t c = tb.qs[s].count;
-    uint32_t h = tb.qs[s].head;  // loaded with the columns: the walk below
-                              // starts one dependent load later
-    if (c) {
-      double fr = tb.front_r[s];
-      uint8_t f = tb.flags[s];
-      Tag3 pf;
-      bool have_pf = true, ready;
-      if (fr <= now) {
-        kr = okey(fr);
-        if (!tb.delayed) {
-          // the front (r == fr) is in the prefix; walk on from entry 1
-          const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-          m = 1;
-          while (m < c) {
-            const ReqEntry& e = ring[(h + m) & tb.qmask];
-            if (!(e.r <= now)) {
-              pf = Tag3{e.r, e.p, e.l, e.arrival};
-              break;
-            }
-            ++m;
-          }
-        } else {
-          CountV v;
-          uint32_t fc;
-          m = walk_r(tb, s, now, kMaxKey, 0xffffffffu, v, nullptr, &pf, &fc);
-        }
-        have_pf = m < c;
-        ready = pf.l <= now;
-      } else {
-        pf.p = tb.front_p[s];
-        pf.l = tb.front_l[s];
-        ready = (f & F_READY) || pf.l <= now;
-        if (!(f & F_READY) && pf.l <= now) tb.flags[s] = f | F_PMARK;
-      }
-      if (have_pf && ready && pf.p < kInf) kp = okey(__dadd_rn(pf.p, tb.pd[s]));
-    }
-    keyr[s] = kr;
-    keyp[s] = kp;
-    mr[s] = (uint8_t)m;
-    if (kr != kMaxKey) {
-      ++cnt0;
-      nr += m;
-      mn0 = kr < mn0 ? kr : mn0;
-      mx0 = kr > mx0 ? kr : mx0;
-    }
-    if (kp != kMaxKey) {
-      ++cnt1;
-      mn1 = kp < mn1 ? kp : mn1;
-      mx1 = kp > mx1 ? kp : mx1;
+  RoundPart acc{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
+  const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
+  ScanCols x[kScanSlots];
+#pragma unroll
+  for (int j = 0; j < kScanSlots; ++j) {
+    uint32_t s = base + j * blockDim.x;
+    x[j].c = 0;
+    if (s < tb.n) {
+      x[j].c = tb.qs[s].count;
+      x[j].h = tb.qs[s].head;
+      x[j].fr = tb.front_r[s];
+      x[j].fp = tb.front_p[s];
+      x[j].fl = tb.front_l[s];
+      x[j].pd = tb.pd[s];
+      x[j].f = tb.flags[s];
     }
   }
-  cnt0 = wsum32(cnt0);
-  cnt1 = wsum32(cnt1);
-  nr = wsum64(nr);
-  mn0 = wmin64(mn0);
-  mx0 = wmax64(mx0);
-  mn1 = wmin64(mn1);
-  mx1 = wmax64(mx1);
-  __shared__ RoundPart sh[kBlockR / 64];
+#pragma unroll
+  for (int j = 0; j < kScanSlots; ++j) {
+    uint32_t s = base + j * blockDim.x;
+    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, acc);
+  }
+  uint32_t cnt0 = wsum32(acc.cnt[0]), cnt1 = wsum32(acc.cnt[1]);
+  uint64_t nr = wsum64(acc.n_r);
+  uint64_t mn0 = wmin64(acc.mn[0]), mx0 = wmax64(acc.mx[0]);
+  uint64_t mn1 = wmin64(acc.mn[1]), mx1 = wmax64(acc.mx[1]);
+  __shared__ RoundPart sh[kScanBlock / 64];
   int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) sh[w] = RoundPart{{cnt0, cnt1}, nr, {mn0, mn1}, {mx0, mx1}};
   __syncthreads();
   if (threadIdx.x == 0) {
     RoundPart o = sh[0];
-    for (int i = 1; i < kBlockR / 64; ++i) {
+    for (int i = 1; i < kScanBlock / 64; ++i) {
       for (int p = 0; p < 2; ++p) {
         o.cnt[p] += sh[i].cnt[p];
         o.mn[p] = sh[i].mn[p] < o.mn[p] ? sh[i].mn[p] : o.mn[p];
@@ -265,14 +291,6 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
   return r;
 }
 
-// one block: the scan partials reduced once (k_rhist's blocks and k_rpick
-// read the result instead of each reducing them again)
-__global__ void __launch_bounds__(1024)
-k_rreduce(const RoundPart* parts, uint32_t nparts, Round* rd) {
-  RoundPart tot = reduce_rparts(parts, nparts);
-  if (threadIdx.x == 0) rd->tot = tot;
-}
-
 __device__ inline uint32_t hist_shift_r(uint64_t range) {
   // smallest shift with (range >> shift) < kHistBinsR
   uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
@@ -286,8 +304,8 @@ __device__ inline uint32_t hist_shift_r(uint64_t range) {
 constexpr int kHistBlocksR = 256;
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp,
-        const Round* rd, uint32_t* hist) {
-  const RoundPart tot = rd->tot;
+        const RoundPart* parts, uint32_t nparts, uint32_t* hist) {
+  const RoundPart tot = reduce_rparts(parts, nparts);
   if (tot.cnt[0] == 0 && tot.cnt[1] == 0) return;
   __shared__ uint32_t sh[2][kHistBinsR];
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x)
@@ -411,11 +429,13 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
 
 // Two blocks, one per phase.
 __global__ void __launch_bounds__(kPickThreadsR)
-k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
+k_rpick(Round* rd, const RoundPart* parts, uint32_t nparts, uint32_t* hist,
+        uint32_t* sbase, uint32_t* snum) {
   __shared__ uint32_t wsum[kPickThreadsR / 64];
   __shared__ uint32_t s_tb, s_C;
   __shared__ uint64_t s_T;
-  const RoundPart tot = rd->tot;
+  const RoundPart tot = reduce_rparts(parts, nparts);
+  if (blockIdx.x == 0 && threadIdx.x == 0) rd->tot = tot;
   uint32_t k = rd->k_total;
   bool p_runs = tot.n_r < (uint64_t)k;
   if (blockIdx.x == 0) {
@@ -1090,7 +1110,7 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
 // every other slot turns its pending mark into F_READY iff the priority pulls
 // ran.  Block 0 also counts the round's decisions (sched[0] reservation,
 // sched[1] priority, :1469,1479) and resets the rank-bin counters.
-__global__ void __launch_bounds__(kBlockR)
+__global__ void __launch_bounds__(kBlockR, 5)
 k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
          const uint64_t* keyp, uint32_t* applied, uint32_t* bcount,
          uint32_t* bsize, unsigned long long* sched) {
