@@ -1,0 +1,63 @@
+"""HBM traffic per launch of each bench stage from two rocprofv3 PMC passes
+(FETCH_SIZE and WRITE_SIZE, collected in separate runs by scripts/gpu_pmc.sh).
+
+Units and corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM):
+FETCH_SIZE / WRITE_SIZE are reported in KiB; on gfx950 FETCH_SIZE counts half
+the bytes of a wide coalesced read, so fetched bytes = 2 x FETCH_SIZE (the
+guide's calibration is for 16-B-per-lane streaming; other access widths are
+uncalibrated and the raw values are kept beside the corrected ones).
+Only the last `--steps` dispatches of each kernel (the bench's timed steps)
+are used.  Writes {stage: {...}} JSON (bench.py reads "hbm_bytes").
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+STAGES = {
+    "scan": ["k_rscan"],
+    "select": ["k_rhist", "k_rpick"],
+    "emit": ["k_rcand", "k_remit"],
+    "rank": ["k_rbscan", "k_rrank"],
+    "apply": ["k_rapply"],
+    "add_link": ["k_add_link"],
+    "add_chain": ["k_add_chain"],
+}
+
+
+def per_kernel(path, steps):
+    vals = defaultdict(list)
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda x: int(x["Dispatch_Id"]))
+    for r in rows:
+        name = r["Kernel_Name"]
+        for ks in STAGES.values():
+            for k in ks:
+                if k + "(" in name or name.endswith(k):
+                    vals[k].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: v[-steps:] for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", default="gpurun_out/pmc_FETCH_SIZE/run_counter_collection.csv")
+    ap.add_argument("--write", default="gpurun_out/pmc_WRITE_SIZE/run_counter_collection.csv")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--out", default="profiles/traffic_r01.json")
+    a = ap.parse_args()
+    fe = per_kernel(a.fetch, a.steps)
+    wr = per_kernel(a.write, a.steps)
+    out = {}
+    for stage, ks in STAGES.items():
+        f = sum(sum(fe.get(k, [])) / max(len(fe.get(k, [])), 1) for k in ks)
+        w = sum(sum(wr.get(k, [])) / max(len(wr.get(k, [])), 1) for k in ks)
+        out[stage] = {"fetch_size_bytes_raw": round(f), "write_size_bytes": round(w),
+                      "hbm_bytes": round(2 * f + w),
+                      "kernels": ks, "launches_averaged": a.steps}
+    json.dump(out, open(a.out, "w"), indent=1)
+    for k, v in out.items():
+        print(f"{k:10s} fetch(raw) {v['fetch_size_bytes_raw']/1e6:8.2f} MB  write {v['write_size_bytes']/1e6:8.2f} MB  hbm(corr) {v['hbm_bytes']/1e6:8.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
