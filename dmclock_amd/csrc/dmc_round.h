@@ -545,20 +545,32 @@ __device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
 
 // ---------------------------------------------------------------- k_rcand
 // Candidates compacted into a dense list, so that the walking kernels run
-// dense waves: kCandBlocksR blocks, each owning a contiguous slot range, one
-// atomic each (list order is irrelevant: the ranking fixes the order).
+// dense waves: kCandBlocksR blocks of kCandThreads, each owning a contiguous
+// slot range, one atomic each (list order is irrelevant: the ranking fixes the
+// order).  The same pass settles the pending limit-scan marks of every
+// non-candidate (F_PMARK -> F_READY iff the priority pulls run); candidates
+// settle theirs in k_rapply.
 constexpr int kCandBlocksR = 256;
-__global__ void __launch_bounds__(kBlockR)
-k_rcand(uint32_t n, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
+constexpr int kCandThreads = 1024;
+__global__ void __launch_bounds__(kCandThreads)
+k_rcand(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
         uint32_t* cand) {
-  __shared__ uint32_t wsum[kBlockR / 64];
+  __shared__ uint32_t wsum[kCandThreads / 64];
   __shared__ uint32_t base;
+  const uint32_t n = tb.n;
   uint32_t per = (n + gridDim.x - 1) / gridDim.x;
   uint32_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
   const CandPred pred(rd);
+  const bool p_runs = rd->p_runs != 0;
   uint32_t c = 0;
-  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
-    c += pred(keyr[s], keyp[s]);
+  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
+    bool isc = pred(keyr[s], keyp[s]);
+    c += isc;
+    if (!isc) {
+      uint8_t f = tb.flags[s];
+      if (f & F_PMARK) tb.flags[s] = (uint8_t)((f & ~F_PMARK) | (p_runs ? F_READY : 0));
+    }
+  }
   uint32_t incl = c;
   int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int d = 1; d < 64; d <<= 1) {
@@ -568,7 +580,7 @@ k_rcand(uint32_t n, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   uint32_t wb = 0, tot = 0;
-  for (int i = 0; i < kBlockR / 64; ++i) {
+  for (int i = 0; i < kCandThreads / 64; ++i) {
     if (i < w) wb += wsum[i];
     tot += wsum[i];
   }
@@ -1106,9 +1118,8 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
 // :1088-1095; delayed: the front, :1077-1085), prev tag, and the front's
 // ready flag: a front left by reservation pops only was seen by the round's
 // first limit scan iff the priority pulls ran; one left by priority pops iff
-// a later limit-scanning pull happened (or the round's terminal pull).  Then
-// every other slot turns its pending mark into F_READY iff the priority pulls
-// ran.  Block 0 also counts the round's decisions (sched[0] reservation,
+// a later limit-scanning pull happened (or the round's terminal pull).
+// (Non-candidates settled their pending marks in k_rcand.)  Block 0 also counts the round's decisions (sched[0] reservation,
 // sched[1] priority, :1469,1479) and resets the rank-bin counters.
 __global__ void __launch_bounds__(kBlockR, 5)
 k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
@@ -1128,15 +1139,6 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t ci = tid; ci < nc; ci += stride) apply_one(tb, rd, cand[ci], applied);
-  const bool p_runs = rd->p_runs && !rd->overflow;
-  const CandPred pred(rd);
-  for (uint32_t s = tid; s < tb.n; s += stride) {
-    uint8_t f = tb.flags[s];
-    if (!(f & F_PMARK) || pred(keyr[s], keyp[s])) continue;
-    f &= (uint8_t)~F_PMARK;
-    if (p_runs) f |= F_READY;
-    tb.flags[s] = f;
-  }
 }
 
 }  // namespace dmc
