@@ -8,8 +8,8 @@
 // Layout (per queue, N client slots, ring capacity Q):
 //   random-access records: ClientRec (64 B: prev tag, inverses, last_tick)
 //     and QState (16 B: head, count, cur_delta, cur_rho) per client;
-//   scanned struct-of-arrays columns: prop_delta, front_{r,p,l} (the heap
-//     keys of the reference, cached), flags;
+//   scanned columns: FrontRec (32 B: front r/p/l -- the heap keys of the
+//     reference, cached -- and prop_delta) and flags;
 //   request rings: ring[slot * Q + i], one 64-byte ReqEntry per request.
 #pragma once
 
@@ -50,6 +50,14 @@ struct alignas(16) QState {
 };
 static_assert(sizeof(QState) == 16, "QState must be 16 bytes");
 
+// The front request's tag (the three heaps' keys, cached) and the client's
+// prop_delta: every pull scan streams all four; the add and apply kernels
+// rewrite them together.
+struct alignas(32) FrontRec {
+  double r, p, l, pd;
+};
+static_assert(sizeof(FrontRec) == 32, "FrontRec must be 32 bytes");
+
 // Client table pointers (passed by value to kernels).
 struct Table {
   uint32_t n;      // slots
@@ -61,8 +69,7 @@ struct Table {
   double antic;
   ClientRec* rec;  // N
   QState* qs;      // N
-  double* pd;      // prop_delta (scanned)
-  double *front_r, *front_p, *front_l;  // front tag = heap keys (scanned)
+  FrontRec* fr;    // N: front tag + prop_delta (scanned; one line per 4)
   uint8_t* flags;
   ReqEntry* ring;
 };
@@ -253,7 +260,7 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
   uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
   if (start >= c) return w;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  double pdv = tb.pd[s];
+  double pdv = tb.fr[s].pd;
   double rinv = tb.rec[s].r_inv;
   if (!tb.delayed) {
     uint32_t i = start;

@@ -134,10 +134,10 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
   tb.rec[s].r_inv = rinv[i];
   tb.rec[s].w_inv = winv[i];
   tb.rec[s].l_inv = linv[i];
-  tb.pd[s] = 0.0;
-  tb.front_r[s] = 0.0;
-  tb.front_p[s] = 0.0;
-  tb.front_l[s] = 0.0;
+  tb.fr[s].pd = 0.0;
+  tb.fr[s].r = 0.0;
+  tb.fr[s].p = 0.0;
+  tb.fr[s].l = 0.0;
   tb.qs[s].head = 0;
   tb.qs[s].count = 0;
   tb.qs[s].cur_delta = 1;
@@ -326,9 +326,9 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
   tb.rec[s].last_tick = st.last_tick;
   tb.flags[s] = st.flags;
   if (st.front_set) {
-    tb.front_r[s] = st.front.r;
-    tb.front_p[s] = st.front.p;
-    tb.front_l[s] = st.front.l;
+    tb.fr[s].r = st.front.r;
+    tb.fr[s].p = st.front.p;
+    tb.fr[s].l = st.front.l;
   }
 }
 
@@ -340,8 +340,8 @@ __global__ void k_contrib_min(Table tb, uint64_t* parts) {
        s += gridDim.x * blockDim.x) {
     uint8_t f = tb.flags[s];
     if ((f & F_REG) && !(f & F_IDLE)) {
-      double p = tb.qs[s].count ? tb.front_p[s] : tb.rec[s].prev_p;
-      uint64_t k = okey(__dadd_rn(p, tb.pd[s]));
+      double p = tb.qs[s].count ? tb.fr[s].p : tb.rec[s].prev_p;
+      uint64_t k = okey(__dadd_rn(p, tb.fr[s].pd));
       m = k < m ? k : m;
     }
   }
@@ -376,7 +376,7 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
     double L = from_okey(*lmin);
     if (L < lowest) lowest = L;
   }
-  if (lowest < trigger) tb.pd[s] = __dsub_rn(lowest, t);
+  if (lowest < trigger) tb.fr[s].pd = __dsub_rn(lowest, t);
   tb.flags[s] &= (uint8_t)~F_IDLE;
 }
 
@@ -401,12 +401,12 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
        s += gridDim.x * blockDim.x) {
     if (!tb.qs[s].count) continue;
     ++nany;
-    ArgMin a{okey(tb.front_r[s]), s, 1};
+    ArgMin a{okey(tb.fr[s].r), s, 1};
     r = argmin_combine(r, a);
-    double l = tb.front_l[s];
+    double l = tb.fr[s].l;
     bool rdy = (tb.flags[s] & F_READY) || l <= now;
-    double pv = tb.front_p[s];
-    uint64_t kp = okey(__dadd_rn(pv, tb.pd[s]));
+    double pv = tb.fr[s].p;
+    uint64_t kp = okey(__dadd_rn(pv, tb.fr[s].pd));
     uint64_t kl = okey(l);
     if (rdy) {
       ++nrd;
@@ -581,7 +581,7 @@ __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
   if (!sc->mark) return;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    if (tb.qs[s].count && !(tb.flags[s] & F_READY) && tb.front_l[s] <= now)
+    if (tb.qs[s].count && !(tb.flags[s] & F_READY) && tb.fr[s].l <= now)
       tb.flags[s] |= F_READY;
   }
 }
@@ -650,9 +650,9 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
   tb.flags[s] &= (uint8_t)~F_READY;
   if (nc) {
     const ReqEntry& f = ring[nh];
-    tb.front_r[s] = f.r;
-    tb.front_p[s] = f.p;
-    tb.front_l[s] = f.l;
+    tb.fr[s].r = f.r;
+    tb.fr[s].p = f.p;
+    tb.fr[s].l = f.l;
   }
   atomicAdd(&sched[prio ? 1 : 0], 1ull);
 }
@@ -1355,8 +1355,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   };
   int rc = 0;
   rc |= A(&t.rec, N); rc |= A(&t.qs, N);
-  rc |= A(&t.pd, N); rc |= A(&t.front_r, N);
-  rc |= A(&t.front_p, N); rc |= A(&t.front_l, N); rc |= A(&t.flags, N);
+  rc |= A(&t.fr, N); rc |= A(&t.flags, N);
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
   rc |= A(&q->applied, N);
   rc |= A(&q->cand, N);
@@ -1412,7 +1411,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
-  void* ptrs[] = {t.rec, t.qs, t.pd, t.front_r, t.front_p, t.front_l, t.flags,
+  void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
                   q->applied, q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
                   q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime,
@@ -1550,9 +1549,9 @@ static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>&
   HIP_OK(hipMemcpyAsync(&q->tb.qs[slot].head, hc, sizeof(hc), hipMemcpyHostToDevice,
                         q->stream));
   if (c) {
-    HIP_OK(hipMemcpyAsync(q->tb.front_r + slot, &ring[0].r, 8, hipMemcpyHostToDevice, q->stream));
-    HIP_OK(hipMemcpyAsync(q->tb.front_p + slot, &ring[0].p, 8, hipMemcpyHostToDevice, q->stream));
-    HIP_OK(hipMemcpyAsync(q->tb.front_l + slot, &ring[0].l, 8, hipMemcpyHostToDevice, q->stream));
+    // r, p, l are contiguous in FrontRec and in ReqEntry
+    HIP_OK(hipMemcpyAsync(&q->tb.fr[slot].r, &ring[0].r, 24, hipMemcpyHostToDevice,
+                          q->stream));
   }
   uint8_t f;
   HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
@@ -1592,18 +1591,19 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   std::lock_guard<std::mutex> g(q->mtx);
   std::memset(s, 0, sizeof(*s));
   const Table& t = q->tb;
-  auto D = [&](double* dst, const double* src) {
-    return hipMemcpyAsync(dst, src + slot, 8, hipMemcpyDeviceToHost, q->stream);
-  };
   uint8_t f = 0;
   ClientRec cr;
   QState qs;
   HIP_OK(hipMemcpyAsync(&cr, t.rec + slot, sizeof(cr), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipMemcpyAsync(&qs, t.qs + slot, sizeof(qs), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(D(&s->prop_delta, t.pd)); HIP_OK(D(&s->front_r, t.front_r));
-  HIP_OK(D(&s->front_p, t.front_p)); HIP_OK(D(&s->front_l, t.front_l));
+  FrontRec fr;
+  HIP_OK(hipMemcpyAsync(&fr, t.fr + slot, sizeof(fr), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipMemcpyAsync(&f, t.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
+  s->prop_delta = fr.pd;
+  s->front_r = fr.r;
+  s->front_p = fr.p;
+  s->front_l = fr.l;
   s->prev_r = cr.prev_r;
   s->prev_p = cr.prev_p;
   s->prev_l = cr.prev_l;

@@ -227,10 +227,10 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     if (s < tb.n) {
       x[j].c = tb.qs[s].count;
       x[j].h = tb.qs[s].head;
-      x[j].fr = tb.front_r[s];
-      x[j].fp = tb.front_p[s];
-      x[j].fl = tb.front_l[s];
-      x[j].pd = tb.pd[s];
+      x[j].fr = tb.fr[s].r;
+      x[j].fp = tb.fr[s].p;
+      x[j].fl = tb.fr[s].l;
+      x[j].pd = tb.fr[s].pd;
       x[j].f = tb.flags[s];
     }
   }
@@ -1101,9 +1101,9 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
   tb.qs[s].count = nc2;
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
   if (nc2) {
-    tb.front_r[s] = front.r;
-    tb.front_p[s] = front.p;
-    tb.front_l[s] = front.l;
+    tb.fr[s].r = front.r;
+    tb.fr[s].p = front.p;
+    tb.fr[s].l = front.l;
     bool seen = popsP ? (terminal || (g_last != kNoneR && v.last_idx < g_last))
                       : p_runs;
     if (seen && front.l <= now) f |= F_READY;
