@@ -137,16 +137,40 @@ __device__ inline double resv_offset(double rinv, uint32_t cost,
 }
 
 // Per-client sequence of pops inside one pull batch at fixed `now` is a pure
-// function of that client's own state ("Batched pulls").
-// The walkers below enumerate it; the three kernels that call them (count,
-// emit, apply) run the same arithmetic, so what is applied is exactly what
-// was ranked.
+// function of that client's own state (see dmc_round.h).  The walkers below
+// enumerate it; the kernels that call them (scan, emit, apply) run the same
+// arithmetic, so what is applied is exactly what was ranked.
 
-// Visitor callbacks used by the walkers.
+// A client's queue state as the walkers need it, loaded once by the caller
+// (all loads issued together, before the first ring access).
+struct CView {
+  uint32_t h, c;          // ring head, queued requests
+  uint32_t cd, cr;        // cur_delta, cur_rho (delayed mode)
+  double rinv, winv, linv;
+  double pd;              // prop_delta
+};
+
+__device__ inline CView load_view(const Table& tb, uint32_t s) {
+  const QState q = tb.qs[s];
+  CView v;
+  v.h = q.head;
+  v.c = q.count;
+  v.cd = q.cur_delta;
+  v.cr = q.cur_rho;
+  v.rinv = tb.rec[s].r_inv;
+  v.winv = tb.rec[s].w_inv;
+  v.linv = tb.rec[s].l_inv;
+  v.pd = tb.fr[s].pd;
+  return v;
+}
+
+// Visitor callbacks: pop(i, tag, cost, handle, prio, dec, tie) for each pop
+// (i = queue position, dec/tie = the ring entry's round scratch), and
+// group(key, run) after each priority group.
 struct NullVisit {
-  __device__ void pop(uint32_t /*i*/, const Tag3& /*t*/, uint32_t /*cost*/,
-                      uint64_t /*h*/, bool /*prio*/) {}
-  __device__ void group(uint64_t /*key*/, uint32_t /*run*/) {}
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool, uint32_t,
+                      uint32_t) {}
+  __device__ void group(uint64_t, uint32_t) {}
 };
 
 // Reservation phase walk (R-prefix): entries whose reservation tag is
@@ -155,11 +179,11 @@ struct NullVisit {
 // with update_next_tag (:1021-1036).  `limit` bounds the pops (apply mode).
 // Returns the number of pops; leaves the final prev tag in *prev (delayed).
 template <typename V>
-__device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
-                                  uint64_t T, uint32_t limit, V& vis,
+__device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
+                                  double now, uint64_t T, uint32_t limit, V& vis,
                                   Tag3* prev_io, Tag3* front_out,
                                   uint32_t* front_cost) {
-  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
+  const uint32_t h = cv.h, c = cv.c;
   uint32_t n = 0;
   if (c == 0) return 0;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
@@ -169,34 +193,32 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
     ReqEntry nx = ring[(h + 1) & tb.qmask];
     while (n < c && n < limit) {
       if (!(e.r <= now) || okey(e.r) > T) break;
-      vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false);
+      vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false, e.dec,
+              e.tie);
       ++n;
       e = nx;
       nx = ring[(h + n + 1) & tb.qmask];
     }
     if (front_out && n < c) {
-      const ReqEntry& e = ring[(h + n) & tb.qmask];
       *front_out = Tag3{e.r, e.p, e.l, e.arrival};
       *front_cost = e.cost;
     }
     return n;
   }
   // delayed: front tag is stored; later tags are computed at pop time
-  const ReqEntry& e0 = ring[h & tb.qmask];
+  ReqEntry e0 = ring[h & tb.qmask];
   Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
-  uint32_t cur_cost = e0.cost, cur_rho = e0.rho;
+  uint32_t cur_cost = e0.cost, cur_dec = e0.dec, cur_tie = e0.tie;
   uint64_t cur_h = e0.handle;
-  double rinv = tb.rec[s].r_inv, winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
-  uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
   while (n < c && n < limit) {
     if (!(cur.r <= now) || okey(cur.r) > T) break;
-    vis.pop(n, cur, cur_cost, cur_h, false);
+    vis.pop(n, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
     ++n;
     if (n < c) {
-      const ReqEntry& e = ring[(h + n) & tb.qmask];
+      const ReqEntry e = ring[(h + n) & tb.qmask];
       Tag3 nt;
-      if (!make_tag(cur, rinv, winv, linv, cd, cr, e.arrival, e.cost,
-                    tb.antic, &nt))
+      if (!make_tag(cur, cv.rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival,
+                    e.cost, tb.antic, &nt))
         nt = Tag3{e.r, e.p, e.l, e.arrival};
       if (prev_io) {
         assign_unpinned(prev_io->r, nt.r);
@@ -206,11 +228,11 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, double now,
       }
       cur = nt;
       cur_cost = e.cost;
-      cur_rho = cr;
       cur_h = e.handle;
+      cur_dec = e.dec;
+      cur_tie = e.tie;
     }
   }
-  (void)cur_rho;
   if (front_out && n < c) {
     *front_out = cur;
     *front_cost = cur_cost;
@@ -248,30 +270,31 @@ __device__ inline double reduced_r(const ReqEntry* ring, uint32_t h,
 
 // The walk starts at ring offset `start` (the front left after the round's
 // reservation pops); `start_tag` is that entry's tag in delayed mode (the
-// walk_r front, used iff use_start_tag), `ready0` its ready flag (only the untouched front can carry
-// one: a front exposed by a reservation pop is ready iff limit <= now).
+// walk_r front, used iff use_start_tag), `ready0` its ready flag (only the
+// untouched front can carry one: a front exposed by a reservation pop is ready
+// iff limit <= now).
 template <typename V>
-__device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
-                               uint64_t T, uint32_t limit, V& vis,
+__device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
+                               double now, uint64_t T, uint32_t limit, V& vis,
                                Tag3* prev_io, Tag3* front_out,
                                uint32_t* front_cost, uint32_t start,
                                Tag3 start_tag, bool use_start_tag, bool ready0) {
   WalkP w{0, 0, 0};
-  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
+  const uint32_t h = cv.h, c = cv.c;
   if (start >= c) return w;
   const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  double pdv = tb.fr[s].pd;
-  double rinv = tb.rec[s].r_inv;
+  const double pdv = cv.pd, rinv = cv.rinv;
   if (!tb.delayed) {
     uint32_t i = start;
     while (i < c && w.pops < limit) {
-      const ReqEntry& e = ring[(h + i) & tb.qmask];
+      const ReqEntry e = ring[(h + i) & tb.qmask];
       bool rdy = (i == start) ? (ready0 || e.l <= now) : (e.l <= now);
       if (!rdy || !(e.p < kInf)) break;
       uint64_t key = okey(__dadd_rn(e.p, pdv));
       if (key > T) break;
       double r_now = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
-      vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true);
+      vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true, e.dec,
+              e.tie);
       w.pmask |= 1ull << i;
       ++i;
       ++w.pops;
@@ -279,8 +302,9 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
       while (i < c && w.pops < limit) {
         double ri = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
         if (!(ri <= now)) break;
-        const ReqEntry& er = ring[(h + i) & tb.qmask];
-        vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, false);
+        const ReqEntry er = ring[(h + i) & tb.qmask];
+        vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, false,
+                er.dec, er.tie);
         ++i;
         ++w.pops;
         ++run;
@@ -297,12 +321,10 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
     return w;
   }
   // delayed mode
-  double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
-  uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
-  const ReqEntry& e0 = ring[(h + start) & tb.qmask];
+  const ReqEntry e0 = ring[(h + start) & tb.qmask];
   Tag3 cur = use_start_tag ? start_tag : Tag3{e0.r, e0.p, e0.l, e0.arrival};
-  uint32_t cur_cost = e0.cost;
-  uint32_t cur_rho = start ? cr : e0.rho;  // a recomputed front carries cur_rho
+  uint32_t cur_cost = e0.cost, cur_dec = e0.dec, cur_tie = e0.tie;
+  uint32_t cur_rho = start ? cv.cr : e0.rho;  // a recomputed front carries cur_rho
   uint64_t cur_h = e0.handle;
   uint32_t i = start;
   auto advance = [&](bool prio) {
@@ -311,9 +333,9 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
     double off = prio ? resv_offset(rinv, cur_cost, cur_rho) : 0.0;
     ++i;
     if (i < c) {
-      const ReqEntry& e = ring[(h + i) & tb.qmask];
+      const ReqEntry e = ring[(h + i) & tb.qmask];
       Tag3 nt;
-      if (!make_tag(cur, rinv, winv, linv, cd, cr, e.arrival, e.cost,
+      if (!make_tag(cur, rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival, e.cost,
                     tb.antic, &nt))
         nt = Tag3{e.r, e.p, e.l, e.arrival};
       if (prev_io) {
@@ -325,8 +347,10 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
       if (prio) nt.r = __dsub_rn(nt.r, off);
       cur = nt;
       cur_cost = e.cost;
-      cur_rho = cr;
+      cur_rho = cv.cr;
       cur_h = e.handle;
+      cur_dec = e.dec;
+      cur_tie = e.tie;
     }
     if (prio && prev_io) prev_io->r = __dsub_rn(prev_io->r, off);
   };
@@ -335,13 +359,13 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, double now,
     if (!rdy || !(cur.p < kInf)) break;
     uint64_t key = okey(__dadd_rn(cur.p, pdv));
     if (key > T) break;
-    vis.pop(i, cur, cur_cost, cur_h, true);
+    vis.pop(i, cur, cur_cost, cur_h, true, cur_dec, cur_tie);
     advance(true);
     ++w.pops;
     uint32_t run = 0;
     while (i < c && w.pops < limit) {
       if (!(cur.r <= now)) break;
-      vis.pop(i, cur, cur_cost, cur_h, false);
+      vis.pop(i, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
       advance(false);
       ++w.pops;
       ++run;

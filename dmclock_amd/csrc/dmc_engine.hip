@@ -751,6 +751,7 @@ struct dmc_queue {
   bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
   uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
+  uint64_t* dbg_atime = nullptr; // debug: per-candidate apply start/end clocks
   uint32_t radix_batches = 0;  // rounds left on the fallback path
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
@@ -1185,7 +1186,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   hipLaunchKernelGGL(k_rapply, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
                      (const uint32_t*)q->cand, (const uint64_t*)q->keyr,
                      (const uint64_t*)q->keyp, q->applied, q->bcount, q->bsize,
-                     q->sched);
+                     q->sched, q->debug ? q->dbg_atime : nullptr);
   pe(q);
   if (future) launch_future(q);
 }
@@ -1255,10 +1256,14 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       (void)hipMemcpy(hb.data(), q->dbg_bins, hb.size() * 4, hipMemcpyDeviceToHost);
       std::vector<uint64_t> wt(2 * kNBR);
       (void)hipMemcpy(wt.data(), q->dbg_wtime, wt.size() * 8, hipMemcpyDeviceToHost);
+      std::vector<uint64_t> at(2 * 262144);
+      (void)hipMemcpy(at.data(), q->dbg_atime, at.size() * 8, hipMemcpyDeviceToHost);
       FILE* f = std::fopen(getenv("DMC_DEBUG_BINS"), "ab");
       if (f) {
         std::fwrite(hb.data(), 4, hb.size(), f);
         std::fwrite(wt.data(), 8, wt.size(), f);
+        std::fwrite(at.data(), 8, at.size(), f);
+        std::fwrite(&c.n_cand, 4, 1, f);
         std::fclose(f);
       }
     }
@@ -1375,6 +1380,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->bpoff, kNBR);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
+  if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
   rc |= A(&q->brec, (size_t)kNBR * kBinCapR);
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
   rc |= A(&q->acnt, N);
@@ -1414,7 +1420,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
                   q->applied, q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
-                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime,
+                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,

@@ -128,7 +128,10 @@ __device__ inline uint32_t wsum32(uint32_t v) {
 
 struct CountV {
   uint32_t pops = 0, groups = 0;
-  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool) { ++pops; }
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool, uint32_t,
+                      uint32_t) {
+    ++pops;
+  }
   __device__ void group(uint64_t, uint32_t) { ++groups; }
 };
 
@@ -175,7 +178,8 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
       } else {
         CountV v;
         uint32_t fc;
-        m = walk_r(tb, s, now, kMaxKey, 0xffffffffu, v, nullptr, &pf, &fc);
+        m = walk_r(tb, s, load_view(tb, s), now, kMaxKey, 0xffffffffu, v, nullptr,
+                   &pf, &fc);
       }
       have_pf = m < x.c;
       ready = pf.l <= now;
@@ -522,7 +526,8 @@ struct EmitV {
     }
   }
   uint32_t gpos = 0;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, bool prio) {
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, bool prio,
+                      uint32_t, uint32_t) {
     if (ph == 0) put(okey(t.r), i, 0);
     else if (prio) gpos = i;
   }
@@ -605,18 +610,20 @@ __device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
   const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
-  uint32_t h = tb.qs[s].head;
+  const CView cv = load_view(tb, s);
+  const uint32_t h = cv.h;
+  const uint8_t f0 = tb.flags[s];
   if (cr) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
-    walk_r(tb, s, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
+    walk_r(tb, s, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
   if (cp) {
     uint32_t m = mr[s];  // the priority pulls run only after every R pop
-    bool ready0 = m == 0 && (tb.flags[s] & F_READY);
+    bool ready0 = m == 0 && (f0 & F_READY);
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
-    walk_p(tb, s, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
+    walk_p(tb, s, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
   }
 }
@@ -958,26 +965,23 @@ __global__ void k_ddecide(Round* rd, uint32_t dcap, const uint32_t* sval,
 // ---------------------------------------------------------------- k_rapply
 struct ApplyV {
   dmc_decision* out;
-  const ReqEntry* ring;  // this client's ring
-  uint32_t head, qmask;
   uint32_t slot;
   uint32_t inrun = 0, gidx = 0;
   uint32_t last_idx = 0;
   bool any = false;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t cost, uint64_t h,
-                      bool prio, bool pphase) {
+  __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
+                      bool prio, bool pphase, uint32_t edec, uint32_t etie) {
     uint32_t idx, tie;
-    const ReqEntry& e = ring[(head + i) & qmask];
     if (!pphase) {
-      idx = e.dec;
-      tie = e.tie;
+      idx = edec;
+      tie = etie;
     } else {
       if (prio) {
-        gidx = e.dec;
+        gidx = edec;
         inrun = 0;
       }
       idx = gidx + inrun;
-      tie = prio ? e.tie : 0;
+      tie = prio ? etie : 0;
       ++inrun;
     }
     dmc_decision d;
@@ -996,15 +1000,17 @@ struct ApplyV {
 };
 struct ApplyVR {
   ApplyV* a;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p) {
-    a->pop(i, t, c, h, p, false);
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p,
+                      uint32_t d, uint32_t ti) {
+    a->pop(i, t, c, h, p, false, d, ti);
   }
   __device__ void group(uint64_t, uint32_t) {}
 };
 struct ApplyVP {
   ApplyV* a;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p) {
-    a->pop(i, t, c, h, p, true);
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p,
+                      uint32_t d, uint32_t ti) {
+    a->pop(i, t, c, h, p, true, d, ti);
   }
   __device__ void group(uint64_t, uint32_t) {}
 };
@@ -1020,43 +1026,51 @@ struct ApplyVP {
 // fronts turn their pending mark into F_READY iff the priority pulls ran.
 // Block 0 also counts the round's decisions (sched[0] reservation, sched[1]
 // priority, :1469,1479) and resets the rank-bin counters.
-__device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
+// The round's scalars, read once per thread (stores through the table could
+// alias the round record, which would force re-loads inside the walks).
+struct RoundC {
+  double now;
+  uint64_t tick;
+  dmc_decision* out;
+  uint32_t g_last, terminal;
+  bool p_runs, ovf;
+};
+
+__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
                                  uint32_t* applied) {
-  const bool ovf = rd->overflow != 0;
-  const bool p_runs = rd->p_runs != 0;
-  uint32_t a = applied[s];
+  // every load that depends only on the slot is issued before the first
+  // branch: one memory round trip for all of them
+  const uint32_t a = applied[s];
+  const uint8_t f0 = tb.flags[s];
+  const CView cv = load_view(tb, s);
+  Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   if (a) applied[s] = 0;
-  if (!a || ovf) {
-    uint8_t f = tb.flags[s];
-    if (f & F_PMARK) {
-      f &= (uint8_t)~F_PMARK;
-      if (p_runs && !ovf) f |= F_READY;
-      tb.flags[s] = f;
-    }
+  if (!a || rc.ovf) {
+    if (f0 & F_PMARK)
+      tb.flags[s] = (uint8_t)((f0 & ~F_PMARK) | (rc.p_runs && !rc.ovf ? F_READY : 0));
     return;
   }
-  const double now = rd->now;
-  const uint64_t tick = rd->tick;
-  const uint32_t g_last = rd->g_last;
-  const uint32_t terminal = rd->terminal;
+  const double now = rc.now;
+  const uint64_t tick = rc.tick;
+  const uint32_t g_last = rc.g_last;
+  const uint32_t terminal = rc.terminal;
+  const bool p_runs = rc.p_runs;
   uint32_t aR = a & 0xffffu, aP = a >> 16;
-  uint32_t c = tb.qs[s].count, h = tb.qs[s].head;
+  const uint32_t c = cv.c, h = cv.h;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  ApplyV v{rd->out, ring, h, tb.qmask, s};
-  uint8_t f0 = tb.flags[s];
-  Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
+  ApplyV v{rc.out, s};
   Tag3 front{};
   uint32_t fcost = 0;
   uint32_t popsR = 0, popsP = 0;
   uint64_t pmask = 0;
   if (aR) {
     ApplyVR vr{&v};
-    popsR = walk_r(tb, s, now, kMaxKey, aR, vr, &prev, &front, &fcost);
+    popsR = walk_r(tb, s, cv, now, kMaxKey, aR, vr, &prev, &front, &fcost);
   }
   if (aP) {
     ApplyVP vp{&v};
     bool ready0 = popsR == 0 && (f0 & F_READY);
-    WalkP w = walk_p(tb, s, now, kMaxKey, aP, vp, &prev, &front, &fcost, popsR,
+    WalkP w = walk_p(tb, s, cv, now, kMaxKey, aP, vp, &prev, &front, &fcost, popsR,
                      front, popsR && tb.delayed, ready0);
     popsP = w.pops;
     pmask = w.pmask;
@@ -1065,7 +1079,7 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
   if (!tb.delayed) {
     if (pmask) {
-      double rinv = tb.rec[s].r_inv;
+      double rinv = cv.rinv;
       // remaining requests: all reductions, in order
       for (uint32_t k = pops; k < c; ++k)
         ring[(h + k) & tb.qmask].r = reduced_r(ring, h, tb.qmask, k, pmask, rinv);
@@ -1088,8 +1102,8 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
       fe.r = front.r;
       fe.p = front.p;
       fe.l = front.l;
-      fe.delta = tb.qs[s].cur_delta;
-      fe.rho = tb.qs[s].cur_rho;
+      fe.delta = cv.cd;
+      fe.rho = cv.cr;
     }
     tb.rec[s].prev_r = prev.r;
     tb.rec[s].prev_p = prev.p;
@@ -1124,7 +1138,7 @@ __device__ inline void apply_one(Table tb, Round* rd, uint32_t s,
 __global__ void __launch_bounds__(kBlockR, 5)
 k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
          const uint64_t* keyp, uint32_t* applied, uint32_t* bcount,
-         uint32_t* bsize, unsigned long long* sched) {
+         uint32_t* bsize, unsigned long long* sched, uint64_t* dbg = nullptr) {
   if (blockIdx.x == 0) {
     for (int b = threadIdx.x; b < kNBR; b += blockDim.x) {
       bcount[b] = 0;
@@ -1138,7 +1152,16 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
   const uint32_t nc = rd->n_cand;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t ci = tid; ci < nc; ci += stride) apply_one(tb, rd, cand[ci], applied);
+  const RoundC rc{rd->now, rd->tick, rd->out, rd->g_last, rd->terminal,
+                  rd->p_runs != 0, rd->overflow != 0};
+  for (uint32_t ci = tid; ci < nc; ci += stride) {
+    uint64_t t0 = dbg ? wall_clock64() : 0;
+    apply_one(tb, rc, cand[ci], applied);
+    if (dbg && ci < 262144) {
+      dbg[2 * ci] = t0;
+      dbg[2 * ci + 1] = wall_clock64();
+    }
+  }
 }
 
 }  // namespace dmc
