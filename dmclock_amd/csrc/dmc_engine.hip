@@ -27,6 +27,7 @@
 #include "../../include/dmclock_gpu.h"
 #include "dmc_device.h"
 #include "dmc_round.h"
+#include "dmc_tracker.h"
 
 using namespace dmc;
 
@@ -1776,6 +1777,52 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
     if (keep[i]) kept.push_back(ents[i]);
   if (kept.size() == ents.size()) return DMC_OK;
   return write_queue(q, slot, kept, n > 0 && keep[0]);
+}
+
+int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
+                      const dmc_pull_result* d_result, uint32_t cap,
+                      uint32_t* d_comp_delta, uint32_t* d_comp_rho) {
+  if (!q || !d_result || (cap && (!d_dec || !d_comp_delta || !d_comp_rho)))
+    return DMC_EINVAL;
+  if (!cap) return DMC_OK;
+  hipLaunchKernelGGL(k_tally, dim3(grid_for(cap, 1024)), dim3(kBlock), 0, q->stream,
+                     d_dec, d_result, cap, d_comp_delta, d_comp_rho);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
+}
+
+int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
+                     const uint32_t* d_gdelta, const uint32_t* d_grho,
+                     uint32_t* d_xd, uint32_t* d_xr, uint8_t* d_known,
+                     uint32_t* d_first) {
+  if (!q || (n && (!d_reqs || !d_gdelta || !d_grho || !d_xd || !d_xr ||
+                   !d_known || !d_first)))
+    return DMC_EINVAL;
+  if (!n) return DMC_OK;
+  uint32_t g = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_track_first, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
+                     q->p.max_clients, d_first);
+  hipLaunchKernelGGL(k_track_params, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
+                     q->p.max_clients, d_gdelta, d_grho, d_xd, d_xr, d_known,
+                     d_first);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
+}
+
+int dmc_tracker_deliver(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd,
+                        uint32_t* d_xr, uint32_t* d_comp_delta,
+                        uint32_t* d_comp_rho, uint32_t* d_gdelta,
+                        uint32_t* d_grho, const uint32_t* d_sum_delta,
+                        const uint32_t* d_sum_rho) {
+  if (!q || n_slots > q->p.max_clients) return DMC_EINVAL;
+  if (d_xd && (!d_xr || !d_comp_delta || !d_comp_rho)) return DMC_EINVAL;
+  if (d_gdelta && (!d_grho || !d_sum_delta || !d_sum_rho)) return DMC_EINVAL;
+  if (!n_slots || (!d_xd && !d_gdelta)) return DMC_OK;
+  hipLaunchKernelGGL(k_track_deliver, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0,
+                     q->stream, n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho,
+                     d_gdelta, d_grho, d_sum_delta, d_sum_rho);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
 }
 
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {

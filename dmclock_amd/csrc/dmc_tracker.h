@@ -1,0 +1,102 @@
+// SPDX-License-Identifier: LGPL-2.1
+//
+// dmc_tracker.h -- the client side of multi-server dmClock on the device:
+// ServiceTracker<S, OrigTracker> (/root/reference/src/dmclock_client.h:39-84,
+// 163-287) for simulated clients whose responses are delivered in bulk at
+// epoch boundaries (multi-GPU deployment).
+//
+// Per (server s, client c) the OrigTracker holds delta_prev_req, rho_prev_req
+// and my_delta, my_rho; prepare_req returns delta = the_delta -
+// delta_prev_req - my_delta.  Only the sum X = delta_prev_req + my_delta
+// matters, so the state per (s, c) is X_delta, X_rho (uint32, modular like
+// the reference's uint32 cast of the Counter difference) and a `known` byte
+// (s is in the client's server_map).  Per client c: the global
+// delta_counter / rho_counter (start at 1, ServiceTracker ctor :186-187).
+//
+//   get_req_params(s)  (:241-251)  unknown: known = 1, X = counters, (1, 1);
+//                                  else (D - X_d, R - X_r), X = counters
+//   track_resp(s, ph, cost) (:221-235), delivered per epoch:
+//                                  D += cost, X_d(s) += cost (my_delta);
+//                                  reservation: R += cost, X_r(s) += cost
+// Requests of one client to one server inside a batch are served in batch
+// order: the first gets the epoch's delta, later ones 0 (the counters did
+// not move in between), exactly as the sequential reference would.
+#pragma once
+
+#include "dmc_device.h"
+
+namespace dmc {
+
+// per-slot completion tallies of one server's decisions (track_resp's cost)
+__global__ void k_tally(const dmc_decision* dec, const dmc_pull_result* res,
+                        uint32_t cap, uint32_t* comp_d, uint32_t* comp_r) {
+  uint32_t n = res->n_decisions < cap ? res->n_decisions : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += gridDim.x * blockDim.x) {
+    const dmc_decision& d = dec[i];
+    atomicAdd(&comp_d[d.slot], d.cost);
+    if (d.phase == DMC_PHASE_RESERVATION) atomicAdd(&comp_r[d.slot], d.cost);
+  }
+}
+
+// first batch position of each (server, client) in the batch
+__global__ void k_track_first(const dmc_request* reqs, uint32_t n, uint32_t nslots,
+                              uint32_t* first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = reqs[i].slot;
+  if (s < nslots) atomicMin(&first[s], i);
+}
+
+// get_req_params for every request of the batch (one server)
+__global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
+                               const uint32_t* gd, const uint32_t* gr,
+                               uint32_t* xd, uint32_t* xr, uint8_t* known,
+                               uint32_t* first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = reqs[i].slot;
+  if (s >= nslots) return;
+  uint32_t delta = 0, rho = 0;  // a later request of the same client: no new responses
+  if (first[s] == i) {
+    uint32_t D = gd[s], R = gr[s];
+    if (!known[s]) {
+      known[s] = 1;
+      delta = 1;
+      rho = 1;
+    } else {
+      delta = D - xd[s];
+      rho = R - xr[s];
+    }
+    xd[s] = D;
+    xr[s] = R;
+    first[s] = 0xffffffffu;  // ready for the next batch
+  } else if (!known[s]) {
+    // cannot happen: the batch's first request made the server known
+  }
+  reqs[i].delta = delta;
+  reqs[i].rho = rho;
+}
+
+// epoch delivery for one server: my_delta / my_rho of its responses (X += own)
+// and, once per client table, the global counters (D += all servers' sums)
+__global__ void k_track_deliver(uint32_t nslots, uint32_t* xd, uint32_t* xr,
+                                uint32_t* comp_d, uint32_t* comp_r,
+                                uint32_t* gd, uint32_t* gr, const uint32_t* sum_d,
+                                const uint32_t* sum_r) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    if (xd) {
+      xd[s] += comp_d[s];
+      xr[s] += comp_r[s];
+      comp_d[s] = 0;
+      comp_r[s] = 0;
+    }
+    if (gd) {
+      gd[s] += sum_d[s];
+      gr[s] += sum_r[s];
+    }
+  }
+}
+
+}  // namespace dmc

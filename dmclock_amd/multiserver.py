@@ -1,0 +1,110 @@
+"""Multi-server dmClock on the device (BASELINE config 5).
+
+dmClock servers are independent queues (sim/src/simulate.h:118-136; one queue
+per server, sim/src/sim_server.h:84,123-130); the only coupling between them
+is client side: every request carries delta/rho, the responses the client got
+from the *other* servers since its previous request to this one
+(ServiceTracker<S, OrigTracker>, dmclock_client.h:39-84, 163-287).
+
+Here the clients' trackers live on the device next to the server queues
+(dmclock_amd/csrc/dmc_tracker.h) and responses are delivered at epoch
+boundaries: per epoch each server's decisions are tallied per client, the
+per-client sums over all servers are combined across ranks with one
+all-reduce (RCCL over xGMI for one process per GPU; gloo on CPU), and each
+tracker advances by its own responses.  That all-reduce is the one exchange
+step of the deployment; the dispatch path itself has no collective.
+
+Arrays are torch tensors (device memory and the collective); every
+computation on them is an engine kernel behind the C-ABI.
+"""
+import ctypes
+
+import numpy as np
+
+from .gpu import GpuQueue, _check, lib
+
+U32_NONE = -1  # 0xffffffff as int32
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class DeviceTrackers:
+    """Client trackers for the S servers (queues) of one rank over a table of
+    N client slots; one instance per rank."""
+
+    def __init__(self, queues, n_clients, device):
+        import torch
+        self.torch = torch
+        self.queues = list(queues)
+        S, N = len(self.queues), n_clients
+        i32 = torch.int32
+        self.N = N
+        self.gd = torch.ones(N, dtype=i32, device=device)
+        self.gr = torch.ones(N, dtype=i32, device=device)
+        self.xd = torch.zeros((S, N), dtype=i32, device=device)
+        self.xr = torch.zeros((S, N), dtype=i32, device=device)
+        self.known = torch.zeros((S, N), dtype=torch.uint8, device=device)
+        self.first = torch.full((S, N), U32_NONE, dtype=i32, device=device)
+        self.comp_d = torch.zeros((S, N), dtype=i32, device=device)
+        self.comp_r = torch.zeros((S, N), dtype=i32, device=device)
+        self.sum_d = torch.zeros(N, dtype=i32, device=device)
+        self.sum_r = torch.zeros(N, dtype=i32, device=device)
+        self.L = lib()
+        torch.cuda.synchronize(device)
+
+    def fill(self, s, d_reqs_ptr, n):
+        """get_req_params for a batch of n requests to server s (device
+        dmc_request array), on that queue's stream."""
+        q = self.queues[s]
+        _check(self.L.dmc_tracker_fill(q.h, ctypes.c_void_p(d_reqs_ptr), n,
+                                       _p(self.gd), _p(self.gr), _p(self.xd[s]),
+                                       _p(self.xr[s]), _p(self.known[s]),
+                                       _p(self.first[s])), "dmc_tracker_fill")
+
+    def tally(self, s, d_dec_ptr, d_res_ptr, cap):
+        q = self.queues[s]
+        _check(self.L.dmc_tracker_tally(q.h, ctypes.c_void_p(d_dec_ptr),
+                                        ctypes.c_void_p(d_res_ptr), cap,
+                                        _p(self.comp_d[s]), _p(self.comp_r[s])),
+               "dmc_tracker_tally")
+
+    def deliver(self, group=None):
+        """Epoch boundary: per-client sums over this rank's servers, one
+        all-reduce over the ranks (sum, modular int32), then every tracker
+        advances."""
+        torch = self.torch
+        for q in self.queues:
+            q.sync()
+        torch.sum(self.comp_d, 0, dtype=torch.int32, out=self.sum_d)
+        torch.sum(self.comp_r, 0, dtype=torch.int32, out=self.sum_r)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            both = torch.stack([self.sum_d, self.sum_r])
+            dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
+            self.sum_d.copy_(both[0])
+            self.sum_r.copy_(both[1])
+        torch.cuda.synchronize(self.gd.device)
+        for s, q in enumerate(self.queues):
+            _check(self.L.dmc_tracker_deliver(q.h, self.N, _p(self.xd[s]),
+                                              _p(self.xr[s]), _p(self.comp_d[s]),
+                                              _p(self.comp_r[s]), None, None, None,
+                                              None), "dmc_tracker_deliver")
+        q0 = self.queues[0]
+        _check(self.L.dmc_tracker_deliver(q0.h, self.N, None, None, None, None,
+                                          _p(self.gd), _p(self.gr), _p(self.sum_d),
+                                          _p(self.sum_r)), "dmc_tracker_deliver")
+        for q in self.queues:
+            q.sync()
+
+    def state(self):
+        """host copies (tests)"""
+        f = lambda t: t.cpu().numpy().view(np.uint32)
+        return {"gd": f(self.gd), "gr": f(self.gr), "xd": f(self.xd),
+                "xr": f(self.xr), "known": self.known.cpu().numpy().astype(bool)}
+
+
+def make_queues(n_servers, n_clients, device=0, **kw):
+    return [GpuQueue(max_clients=n_clients, device=device, **kw)
+            for _ in range(n_servers)]

@@ -211,6 +211,38 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep);
 int dmc_stats_get(dmc_queue* q, dmc_stats* out);
 
+/* ------------------------------------------------------------ client side
+ * Multi-server epochs: the reference's client-side
+ * ServiceTracker<S, OrigTracker> (dmclock_client.h:39-84, 163-287) for
+ * simulated clients, on the device, with responses delivered at epoch
+ * boundaries.  All arrays are device memory indexed by client slot, owned by
+ * the caller; they run on the queue's stream.  The caller sums the per-server
+ * tallies over all servers of all ranks (an all-reduce) between tally and
+ * deliver. */
+/* track_resp's counting: comp_delta[slot] += cost for each of the
+ * d_result->n_decisions (<= cap) decisions, comp_rho[slot] += cost for the
+ * reservation-phase ones. */
+int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
+                      const dmc_pull_result* d_result, uint32_t cap,
+                      uint32_t* d_comp_delta, uint32_t* d_comp_rho);
+/* get_req_params (dmclock_client.h:241-251) for every request of a batch to
+ * this queue's server, in batch order: writes d_reqs[i].delta / .rho.
+ * xd/xr/known: this server's per-client tracker state; gdelta/grho: the
+ * clients' global counters (start at 1); first: scratch, all 0xffffffff
+ * initially (left so). */
+int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
+                     const uint32_t* d_gdelta, const uint32_t* d_grho,
+                     uint32_t* d_xd, uint32_t* d_xr, uint8_t* d_known,
+                     uint32_t* d_first);
+/* Epoch delivery (track_resp, :221-235): xd += comp_delta, xr += comp_rho,
+ * comp_* = 0 (when d_xd != NULL); gdelta += sum_delta, grho += sum_rho (when
+ * d_gdelta != NULL; once per client table, with the all-reduced sums). */
+int dmc_tracker_deliver(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd,
+                        uint32_t* d_xr, uint32_t* d_comp_delta,
+                        uint32_t* d_comp_rho, uint32_t* d_gdelta,
+                        uint32_t* d_grho, const uint32_t* d_sum_delta,
+                        const uint32_t* d_sum_rho);
+
 /* ------------------------------------------------------------ tuning
  * Engine options (no reference counterpart): pulls with k <= SMALL_K run one
  * general do_next_request at a time (default 8); FORCE_RADIX ranks batched

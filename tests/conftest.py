@@ -3,6 +3,14 @@ import sys
 
 import pytest
 
+# Load torch (and the HIP runtime it ships) before the engine library: a
+# process must resolve one HIP runtime, and the GPU tests that use torch
+# tensors (multi-server) need torch's to be the one.
+import torch  # noqa: E402
+
+if torch.cuda.is_available():  # initialise torch's HIP context first, too
+    torch.cuda.init()
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -1,0 +1,184 @@
+"""Multi-server dmClock with epoch-delivered client trackers (BASELINE config
+5).
+
+CPU: the epoch restatement (oracle/epoch_tracker.py) equals the sequential
+ServiceTracker<S, OrigTracker> restatement (oracle pyoracle.Tracker) driven
+with the same calls; the per-rank sums combined with a world-size-2 gloo
+all-reduce equal the single-process sums.
+GPU: the device trackers equal the restatement bit for bit, and S server
+queues driven by them make the same decisions as S oracle queues driven by
+the restatement.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import pyoracle
+from epoch_tracker import EpochTrackers
+from dmclock_amd import workloads
+from dmclock_amd._abi import DECISION_DTYPE, REQUEST_DTYPE
+
+
+def epoch_batches(rng, n_servers, n_clients, n_epochs, per_server, t0=1.0,
+                  rate=None):
+    """Per epoch, per server: a batch of requests (Poisson arrivals over all
+    clients), delta/rho left for the trackers."""
+    rate = rate or 2.0 * n_clients
+    t = t0
+    h = 0
+    out = []
+    for _ in range(n_epochs):
+        ep = []
+        for _s in range(n_servers):
+            r = workloads.arrivals(rng, n_clients, per_server, t, rate, handle_base=h)
+            h += per_server
+            ep.append(r)
+        t = max(float(b["time"][-1]) for b in ep)
+        out.append((t, ep))
+    return out
+
+
+def test_epoch_restatement_matches_sequential_tracker():
+    rng = np.random.default_rng(3)
+    S, N = 3, 40
+    et = EpochTrackers(S, N)
+    seq = [pyoracle.Tracker("orig") for _ in range(N)]
+    for epoch in range(6):
+        batches = []
+        for s in range(S):
+            reqs = np.zeros(rng.integers(5, 60), dtype=REQUEST_DTYPE)
+            reqs["slot"] = rng.integers(0, N, len(reqs))
+            et.fill(s, reqs)
+            for i in range(len(reqs)):
+                d, r = seq[reqs["slot"][i]].get_req_params(s)
+                assert (d, r) == (reqs["delta"][i], reqs["rho"][i]), (epoch, s, i)
+            batches.append(reqs)
+        for s in range(S):
+            n = len(batches[s])
+            dec = np.zeros(n, dtype=DECISION_DTYPE)
+            dec["slot"] = batches[s]["slot"]
+            dec["cost"] = rng.integers(1, 4, n)
+            dec["phase"] = rng.integers(0, 2, n)
+            et.tally(s, dec)
+            for x in dec:
+                seq[x["slot"]].track_resp(s, int(x["phase"]), int(x["cost"]))
+        et.deliver()
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(11)
+        S_total, N = 4, 64
+        S = S_total // world
+        et = EpochTrackers(S, N)
+        for epoch in range(4):
+            for s in range(S):
+                gs = rank * S + s
+                r2 = np.random.default_rng(100 * epoch + gs)
+                dec = np.zeros(50, dtype=DECISION_DTYPE)
+                dec["slot"] = r2.integers(0, N, 50)
+                dec["cost"] = r2.integers(1, 4, 50)
+                dec["phase"] = r2.integers(0, 2, 50)
+                et.tally(s, dec)
+            sd, sr = et.local_sums()
+            both = torch.from_numpy(np.stack([sd, sr]).view(np.int32).copy())
+            dist.all_reduce(both, op=dist.ReduceOp.SUM)
+            allr = both.numpy().view(np.uint32)
+            et.deliver(allr[0], allr[1])
+        q.put((rank, et.gd.copy(), et.gr.copy(), et.xd.copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_epoch_allreduce_gloo_world2():
+    """Per-rank sums + all-reduce == one process holding every server."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict()
+    for _ in procs:
+        rank, gd, gr, xd = q.get(timeout=120)
+        res[rank] = (gd, gr, xd)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process, all 4 servers
+    S_total, N = 4, 64
+    et = EpochTrackers(S_total, N)
+    for epoch in range(4):
+        for gs in range(S_total):
+            r2 = np.random.default_rng(100 * epoch + gs)
+            dec = np.zeros(50, dtype=DECISION_DTYPE)
+            dec["slot"] = r2.integers(0, N, 50)
+            dec["cost"] = r2.integers(1, 4, 50)
+            dec["phase"] = r2.integers(0, 2, 50)
+            et.tally(gs, dec)
+        et.deliver()
+    for rank in (0, 1):
+        gd, gr, xd = res[rank]
+        assert np.array_equal(gd, et.gd) and np.array_equal(gr, et.gr)
+        assert np.array_equal(xd, et.xd[rank * 2:(rank + 1) * 2])
+
+
+@pytest.mark.gpu
+def test_device_trackers_and_multiserver_parity():
+    """S GPU server queues + device trackers vs S oracle queues + the
+    restatement: bit-exact delta/rho, decisions and tracker state."""
+    import torch
+    from dmclock_amd.multiserver import DeviceTrackers, make_queues
+    from parity import compare_decisions
+    S, N = 4, 300
+    rng = np.random.default_rng(5)
+    tab = workloads.client_table(rng, N)
+    qg = make_queues(S, N, device=0, ring_capacity=64)
+    qo = [pyoracle.OracleQueue() for _ in range(S)]
+    for q in qg + qo:
+        q.register(tab.slots, tab.r, tab.w, tab.l, True)
+    dev = torch.device("cuda", 0)
+    dt = DeviceTrackers(qg, N, dev)
+    et = EpochTrackers(S, N)
+    n_dec = 0
+    for t, ep in epoch_batches(rng, S, N, n_epochs=6, per_server=250):
+        for s in range(S):
+            reqs = ep[s].copy()
+            d_reqs = torch.from_numpy(reqs.view(np.uint8)).to(dev)
+            dt.fill(s, d_reqs.data_ptr(), len(reqs))
+            qg[s].sync()
+            got = d_reqs.cpu().numpy().view(REQUEST_DTYPE)
+            et.fill(s, reqs)
+            assert np.array_equal(got["delta"], reqs["delta"])
+            assert np.array_equal(got["rho"], reqs["rho"])
+            rc_g = qg[s].add_batch(got)
+            rc_o = qo[s].add_batch(reqs)
+            assert np.array_equal(rc_g, rc_o)
+        for s in range(S):
+            k = 200
+            d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            d_res = torch.zeros(24, dtype=torch.uint8, device=dev)
+            qg[s].pull_batch_device(t, k, d_out.data_ptr(), d_res.data_ptr())
+            dt.tally(s, d_out.data_ptr(), d_res.data_ptr(), k)
+            qg[s].sync()
+            from dmclock_amd._abi import PullResult
+            res = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+            dg = d_out.cpu().numpy().view(DECISION_DTYPE)[:res.n_decisions]
+            do, ro = qo[s].pull_batch(t, k)
+            compare_decisions(dg, do, f"server {s}")
+            et.tally(s, do)
+            n_dec += len(do)
+        dt.deliver()
+        et.deliver()
+        st = dt.state()
+        for f in ("gd", "gr", "xd", "xr", "known"):
+            assert np.array_equal(st[f], getattr(et, f)), f
+    assert n_dec > 1000
