@@ -90,7 +90,19 @@ def parse():
                          "region, on the following batches)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles",
                                                       "traffic_r01.json"))
-    return ap.parse_args()
+    ap.add_argument("--config", type=int, default=3, choices=(3, 5),
+                    help="3: one server queue (default); 5: multi-server "
+                         "dmClock, --servers queues per GPU with device client "
+                         "trackers and a per-epoch all-reduce")
+    ap.add_argument("--servers", type=int, default=8,
+                    help="config 5: server queues per GPU")
+    ap.add_argument("--epoch-steps", type=int, default=16,
+                    help="config 5: steps per delta/rho epoch (16 x 64K = 1M "
+                         "decisions per server)")
+    args = ap.parse_args()
+    if args.config == 5 and "--clients" not in sys.argv:
+        args.clients = 1 << 21  # 2M client slots per server table
+    return args
 
 
 def make_workload(args, seed):
@@ -158,6 +170,9 @@ def cpu_baseline(args, tab, pre, steps):
 
 def main():
     args = parse()
+    if args.config == 5:
+        import bench_multiserver
+        return bench_multiserver.main(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

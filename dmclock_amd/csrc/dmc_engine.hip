@@ -768,6 +768,14 @@ struct dmc_queue {
   uint64_t prof_cnt[DMC_PROF_NSTAGES] = {};
 };
 
+// Every entry point of a queue holds its mutex (the reference's data_mtx) and
+// makes the queue's device current for the calling thread, so that servers
+// of one rank can be driven from one host thread each.
+struct QueueLock {
+  std::lock_guard<std::mutex> l;
+  explicit QueueLock(dmc_queue* q) : l(q->mtx) { (void)hipSetDevice(q->p.device); }
+};
+
 namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
@@ -1415,6 +1423,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
+  (void)hipSetDevice(q->p.device);
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
@@ -1454,7 +1463,7 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                               const double* r, const double* w, const double* l,
                               int active) {
   if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
   if (!n) return DMC_OK;
@@ -1497,7 +1506,7 @@ int dmc_client_register(dmc_queue* q, uint32_t slot, double r, double w,
 int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
                            double l) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   double v[3] = {inv_of(r), inv_of(w), inv_of(l)};
   // r_inv, w_inv, l_inv are contiguous in ClientRec
@@ -1509,7 +1518,7 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
 
 int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   uint8_t f;
   HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
@@ -1572,7 +1581,7 @@ static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>&
 int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -1595,7 +1604,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
 
 int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   if (!q || !s || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   std::memset(s, 0, sizeof(*s));
   const Table& t = q->tb;
   uint8_t f = 0;
@@ -1640,7 +1649,7 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
 
 int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
   if (!q || !out || n > q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (n)
     HIP_OK(hipMemcpy2DAsync(out, sizeof(uint64_t), &q->tb.rec[0].last_tick,
                             sizeof(ClientRec), sizeof(uint64_t), n,
@@ -1652,7 +1661,7 @@ int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
 int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
                   int32_t* rc_out) {
   if (!q || (n && !reqs)) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
@@ -1672,7 +1681,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
 int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
                          int32_t* d_rc_out) {
   if (!q || (n && (!d_reqs || !d_rc_out))) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
@@ -1695,7 +1704,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
 int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                    dmc_pull_result* result) {
   if (!q || (k && !out)) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   int rc = ensure_dec(q, k);
   if (rc) return rc;
   dmc_pull_result r{};
@@ -1714,7 +1723,7 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
 int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
                           dmc_decision* d_out, dmc_pull_result* d_result) {
   if (!q || (k && !d_out)) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   dmc_pull_result r{};
   int rc = pull_impl(q, now, k, d_out, &r);
   if (rc) return rc;
@@ -1731,7 +1740,7 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
 int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
                          uint64_t* handles_out, uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) {
     if (n_out) *n_out = 0;
     return DMC_OK;  // client_map.find fails -> return, :599-601
@@ -1750,7 +1759,7 @@ int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
 int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                         uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -1765,7 +1774,7 @@ int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
 int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -1782,6 +1791,8 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
 int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
                       const dmc_pull_result* d_result, uint32_t cap,
                       uint32_t* d_comp_delta, uint32_t* d_comp_rho) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
   if (!q || !d_result || (cap && (!d_dec || !d_comp_delta || !d_comp_rho)))
     return DMC_EINVAL;
   if (!cap) return DMC_OK;
@@ -1792,9 +1803,11 @@ int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
 }
 
 int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
-                     const uint32_t* d_gdelta, const uint32_t* d_grho,
-                     uint32_t* d_xd, uint32_t* d_xr, uint8_t* d_known,
-                     uint32_t* d_first) {
+                     const uint32_t* d_client_of_slot, const uint32_t* d_gdelta,
+                     const uint32_t* d_grho, uint32_t* d_xd, uint32_t* d_xr,
+                     uint8_t* d_known, uint32_t* d_first) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
   if (!q || (n && (!d_reqs || !d_gdelta || !d_grho || !d_xd || !d_xr ||
                    !d_known || !d_first)))
     return DMC_EINVAL;
@@ -1803,31 +1816,45 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
   hipLaunchKernelGGL(k_track_first, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
                      q->p.max_clients, d_first);
   hipLaunchKernelGGL(k_track_params, dim3(g), dim3(kBlock), 0, q->stream, d_reqs, n,
-                     q->p.max_clients, d_gdelta, d_grho, d_xd, d_xr, d_known,
-                     d_first);
+                     q->p.max_clients, d_client_of_slot, d_gdelta, d_grho, d_xd,
+                     d_xr, d_known, d_first);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
 
-int dmc_tracker_deliver(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd,
-                        uint32_t* d_xr, uint32_t* d_comp_delta,
-                        uint32_t* d_comp_rho, uint32_t* d_gdelta,
-                        uint32_t* d_grho, const uint32_t* d_sum_delta,
-                        const uint32_t* d_sum_rho) {
+int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
+                        const uint32_t* d_client_of_slot, uint32_t* d_xd,
+                        uint32_t* d_xr, uint32_t* d_comp_delta, uint32_t* d_comp_rho,
+                        uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
   if (!q || n_slots > q->p.max_clients) return DMC_EINVAL;
-  if (d_xd && (!d_xr || !d_comp_delta || !d_comp_rho)) return DMC_EINVAL;
-  if (d_gdelta && (!d_grho || !d_sum_delta || !d_sum_rho)) return DMC_EINVAL;
-  if (!n_slots || (!d_xd && !d_gdelta)) return DMC_OK;
-  hipLaunchKernelGGL(k_track_deliver, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0,
-                     q->stream, n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho,
-                     d_gdelta, d_grho, d_sum_delta, d_sum_rho);
+  if (!n_slots) return DMC_OK;
+  if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho)
+    return DMC_EINVAL;
+  hipLaunchKernelGGL(k_track_collect, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0,
+                     q->stream, n_slots, d_client_of_slot, d_xd, d_xr, d_comp_delta,
+                     d_comp_rho, d_sum_delta, d_sum_rho);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
+}
+
+int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
+                        uint32_t* d_grho, uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
+  if (!q) return DMC_EINVAL;
+  if (!n_clients) return DMC_OK;
+  if (!d_gdelta || !d_grho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
+  hipLaunchKernelGGL(k_track_advance, dim3(grid_for(n_clients, 2048)), dim3(kBlock), 0,
+                     q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
 
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
   if (!q) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   switch (option) {
     case DMC_OPT_SMALL_K:
       if (value < 0) return DMC_EINVAL;
@@ -1847,7 +1874,7 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
 
 int dmc_profile_enable(dmc_queue* q, int on) {
   if (!q) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   q->prof_on = on != 0;
   q->prof_n = 0;
   return DMC_OK;
@@ -1855,7 +1882,7 @@ int dmc_profile_enable(dmc_queue* q, int on) {
 
 int dmc_profile_reset(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   for (int i = 0; i < DMC_PROF_NSTAGES; ++i) {
     q->prof_ms[i] = 0.0;
     q->prof_cnt[i] = 0;
@@ -1866,7 +1893,7 @@ int dmc_profile_reset(dmc_queue* q) {
 int dmc_profile_read(dmc_queue* q, uint32_t stage, uint64_t* count,
                      double* total_ms) {
   if (!q || stage >= DMC_PROF_NSTAGES) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   if (count) *count = q->prof_cnt[stage];
   if (total_ms) *total_ms = q->prof_ms[stage];
   return DMC_OK;
@@ -1878,7 +1905,7 @@ const char* dmc_profile_stage_name(uint32_t stage) {
 
 int dmc_stats_get(dmc_queue* q, dmc_stats* out) {
   if (!q || !out) return DMC_EINVAL;
-  std::lock_guard<std::mutex> g(q->mtx);
+  QueueLock g(q);
   unsigned long long sc[2];
   HIP_OK(hipMemsetAsync(q->reqcount, 0, 8, q->stream));
   hipLaunchKernelGGL(k_count_requests, dim3(grid_for(q->tb.n, 1024)), dim3(kBlock),

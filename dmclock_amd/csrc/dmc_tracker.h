@@ -21,6 +21,10 @@
 // Requests of one client to one server inside a batch are served in batch
 // order: the first gets the epoch's delta, later ones 0 (the counters did
 // not move in between), exactly as the sequential reference would.
+//
+// A server's table slot s holds global client client_of_slot[s] (identity
+// when the map is null): the per-(server, slot) state is slot-indexed, the
+// global counters client-indexed (config 5: 16M clients, 2M per table).
 #pragma once
 
 #include "dmc_device.h"
@@ -50,6 +54,7 @@ __global__ void k_track_first(const dmc_request* reqs, uint32_t n, uint32_t nslo
 
 // get_req_params for every request of the batch (one server)
 __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
+                               const uint32_t* client_of_slot,
                                const uint32_t* gd, const uint32_t* gr,
                                uint32_t* xd, uint32_t* xr, uint8_t* known,
                                uint32_t* first) {
@@ -59,7 +64,8 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
   if (s >= nslots) return;
   uint32_t delta = 0, rho = 0;  // a later request of the same client: no new responses
   if (first[s] == i) {
-    uint32_t D = gd[s], R = gr[s];
+    uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    uint32_t D = gd[c], R = gr[c];
     if (!known[s]) {
       known[s] = 1;
       delta = 1;
@@ -71,31 +77,42 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
     xd[s] = D;
     xr[s] = R;
     first[s] = 0xffffffffu;  // ready for the next batch
-  } else if (!known[s]) {
-    // cannot happen: the batch's first request made the server known
   }
   reqs[i].delta = delta;
   reqs[i].rho = rho;
 }
 
-// epoch delivery for one server: my_delta / my_rho of its responses (X += own)
-// and, once per client table, the global counters (D += all servers' sums)
-__global__ void k_track_deliver(uint32_t nslots, uint32_t* xd, uint32_t* xr,
-                                uint32_t* comp_d, uint32_t* comp_r,
-                                uint32_t* gd, uint32_t* gr, const uint32_t* sum_d,
-                                const uint32_t* sum_r) {
+// epoch end, per server: my_delta / my_rho of its responses (X += own) and
+// the server's contribution to the per-client sums (atomics: the servers of
+// a rank collect concurrently on their own streams)
+__global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
+                                uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
+                                uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r) {
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
        s += gridDim.x * blockDim.x) {
-    if (xd) {
-      xd[s] += comp_d[s];
-      xr[s] += comp_r[s];
-      comp_d[s] = 0;
-      comp_r[s] = 0;
-    }
-    if (gd) {
-      gd[s] += sum_d[s];
-      gr[s] += sum_r[s];
-    }
+    uint32_t cd = comp_d[s];
+    if (!cd) continue;  // comp_r <= comp_d: nothing delivered to this slot
+    uint32_t cr = comp_r[s];
+    xd[s] += cd;
+    xr[s] += cr;
+    comp_d[s] = 0;
+    comp_r[s] = 0;
+    uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    atomicAdd(&sum_d[c], cd);
+    if (cr) atomicAdd(&sum_r[c], cr);
+  }
+}
+
+// after the all-reduce of the sums: the global counters advance (D += all
+// servers' responses to the client), sums cleared for the next epoch
+__global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
+                                uint32_t* sum_d, uint32_t* sum_r) {
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nclients;
+       c += gridDim.x * blockDim.x) {
+    gd[c] += sum_d[c];
+    gr[c] += sum_r[c];
+    sum_d[c] = 0;
+    sum_r[c] = 0;
   }
 }
 

@@ -52,9 +52,10 @@ EXPORTS = {
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "dmc_queue_set_option": (_i32, [_vp, _i32, ctypes.c_int64]),
     "dmc_tracker_tally": (_i32, [_vp, _vp, _vp, _u32, _vp, _vp]),
-    "dmc_tracker_fill": (_i32, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "dmc_tracker_deliver": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp]),
+    "dmc_tracker_fill": (_i32, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp]),
+    "dmc_tracker_collect": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dmc_tracker_advance": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "dmc_profile_enable": (_i32, [_vp, _i32]),
     "dmc_profile_reset": (_i32, [_vp]),
     "dmc_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),

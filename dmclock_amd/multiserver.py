@@ -31,37 +31,53 @@ def _p(t):
 
 
 class DeviceTrackers:
-    """Client trackers for the S servers (queues) of one rank over a table of
-    N client slots; one instance per rank."""
+    """Client trackers for the S servers (queues) of one rank.
 
-    def __init__(self, queues, n_clients, device):
+    Each server table has n_slots client slots; client_of_slot (S x n_slots,
+    int32, optional; identity when None) names the global client of each
+    slot, of n_clients global clients (default n_slots).  Per (server, slot):
+    X_delta, X_rho, known; per global client: the delta/rho counters."""
+
+    def __init__(self, queues, n_slots, device, n_clients=None, client_of_slot=None):
         import torch
         self.torch = torch
         self.queues = list(queues)
-        S, N = len(self.queues), n_clients
+        S, N = len(self.queues), n_slots
+        G = n_clients if n_clients is not None else n_slots
         i32 = torch.int32
-        self.N = N
-        self.gd = torch.ones(N, dtype=i32, device=device)
-        self.gr = torch.ones(N, dtype=i32, device=device)
+        self.N, self.G = N, G
+        if client_of_slot is not None:
+            client_of_slot = torch.as_tensor(client_of_slot, dtype=i32).to(device)
+            if tuple(client_of_slot.shape) != (S, N):
+                raise ValueError("client_of_slot must be (servers, n_slots)")
+            if int(client_of_slot.min()) < 0 or int(client_of_slot.max()) >= G:
+                raise ValueError("client_of_slot out of range")
+        self.cmap = client_of_slot
+        self.gd = torch.ones(G, dtype=i32, device=device)
+        self.gr = torch.ones(G, dtype=i32, device=device)
+        self.sum_d = torch.zeros(G, dtype=i32, device=device)
+        self.sum_r = torch.zeros(G, dtype=i32, device=device)
         self.xd = torch.zeros((S, N), dtype=i32, device=device)
         self.xr = torch.zeros((S, N), dtype=i32, device=device)
         self.known = torch.zeros((S, N), dtype=torch.uint8, device=device)
         self.first = torch.full((S, N), U32_NONE, dtype=i32, device=device)
         self.comp_d = torch.zeros((S, N), dtype=i32, device=device)
         self.comp_r = torch.zeros((S, N), dtype=i32, device=device)
-        self.sum_d = torch.zeros(N, dtype=i32, device=device)
-        self.sum_r = torch.zeros(N, dtype=i32, device=device)
         self.L = lib()
         torch.cuda.synchronize(device)
+
+    def _map(self, s):
+        return None if self.cmap is None else _p(self.cmap[s])
 
     def fill(self, s, d_reqs_ptr, n):
         """get_req_params for a batch of n requests to server s (device
         dmc_request array), on that queue's stream."""
         q = self.queues[s]
         _check(self.L.dmc_tracker_fill(q.h, ctypes.c_void_p(d_reqs_ptr), n,
-                                       _p(self.gd), _p(self.gr), _p(self.xd[s]),
-                                       _p(self.xr[s]), _p(self.known[s]),
-                                       _p(self.first[s])), "dmc_tracker_fill")
+                                       self._map(s), _p(self.gd), _p(self.gr),
+                                       _p(self.xd[s]), _p(self.xr[s]),
+                                       _p(self.known[s]), _p(self.first[s])),
+               "dmc_tracker_fill")
 
     def tally(self, s, d_dec_ptr, d_res_ptr, cap):
         q = self.queues[s]
@@ -70,33 +86,33 @@ class DeviceTrackers:
                                         _p(self.comp_d[s]), _p(self.comp_r[s])),
                "dmc_tracker_tally")
 
+    def collect(self):
+        """Epoch end, every server of the rank on its own stream: X += own
+        responses, per-client sums += this server's responses."""
+        for s, q in enumerate(self.queues):
+            _check(self.L.dmc_tracker_collect(q.h, self.N, self._map(s),
+                                              _p(self.xd[s]), _p(self.xr[s]),
+                                              _p(self.comp_d[s]), _p(self.comp_r[s]),
+                                              _p(self.sum_d), _p(self.sum_r)),
+                   "dmc_tracker_collect")
+
     def deliver(self, group=None):
-        """Epoch boundary: per-client sums over this rank's servers, one
-        all-reduce over the ranks (sum, modular int32), then every tracker
-        advances."""
+        """Epoch boundary: collect, one all-reduce of the per-client sums over
+        the ranks (sum, modular int32), then the global counters advance."""
         torch = self.torch
+        self.collect()
         for q in self.queues:
             q.sync()
-        torch.sum(self.comp_d, 0, dtype=torch.int32, out=self.sum_d)
-        torch.sum(self.comp_r, 0, dtype=torch.int32, out=self.sum_r)
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            both = torch.stack([self.sum_d, self.sum_r])
-            dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
-            self.sum_d.copy_(both[0])
-            self.sum_r.copy_(both[1])
-        torch.cuda.synchronize(self.gd.device)
-        for s, q in enumerate(self.queues):
-            _check(self.L.dmc_tracker_deliver(q.h, self.N, _p(self.xd[s]),
-                                              _p(self.xr[s]), _p(self.comp_d[s]),
-                                              _p(self.comp_r[s]), None, None, None,
-                                              None), "dmc_tracker_deliver")
+            dist.all_reduce(self.sum_d, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(self.sum_r, op=dist.ReduceOp.SUM, group=group)
+            torch.cuda.synchronize(self.gd.device)
         q0 = self.queues[0]
-        _check(self.L.dmc_tracker_deliver(q0.h, self.N, None, None, None, None,
-                                          _p(self.gd), _p(self.gr), _p(self.sum_d),
-                                          _p(self.sum_r)), "dmc_tracker_deliver")
-        for q in self.queues:
-            q.sync()
+        _check(self.L.dmc_tracker_advance(q0.h, self.G, _p(self.gd), _p(self.gr),
+                                          _p(self.sum_d), _p(self.sum_r)),
+               "dmc_tracker_advance")
+        q0.sync()
 
     def state(self):
         """host copies (tests)"""

@@ -227,21 +227,25 @@ int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
                       uint32_t* d_comp_delta, uint32_t* d_comp_rho);
 /* get_req_params (dmclock_client.h:241-251) for every request of a batch to
  * this queue's server, in batch order: writes d_reqs[i].delta / .rho.
- * xd/xr/known: this server's per-client tracker state; gdelta/grho: the
- * clients' global counters (start at 1); first: scratch, all 0xffffffff
- * initially (left so). */
+ * client_of_slot: the global client of each table slot (NULL: identity);
+ * xd/xr/known: this server's per-slot tracker state; gdelta/grho: the
+ * clients' global counters (start at 1); first: per-slot scratch, all
+ * 0xffffffff initially (left so). */
 int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
-                     const uint32_t* d_gdelta, const uint32_t* d_grho,
-                     uint32_t* d_xd, uint32_t* d_xr, uint8_t* d_known,
-                     uint32_t* d_first);
-/* Epoch delivery (track_resp, :221-235): xd += comp_delta, xr += comp_rho,
- * comp_* = 0 (when d_xd != NULL); gdelta += sum_delta, grho += sum_rho (when
- * d_gdelta != NULL; once per client table, with the all-reduced sums). */
-int dmc_tracker_deliver(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd,
-                        uint32_t* d_xr, uint32_t* d_comp_delta,
-                        uint32_t* d_comp_rho, uint32_t* d_gdelta,
-                        uint32_t* d_grho, const uint32_t* d_sum_delta,
-                        const uint32_t* d_sum_rho);
+                     const uint32_t* d_client_of_slot, const uint32_t* d_gdelta,
+                     const uint32_t* d_grho, uint32_t* d_xd, uint32_t* d_xr,
+                     uint8_t* d_known, uint32_t* d_first);
+/* Epoch end for one server (track_resp, :221-235): xd += comp_delta, xr +=
+ * comp_rho (my_delta / my_rho), sum_*[client_of_slot[s]] += comp_* (atomic;
+ * the servers of a rank may collect concurrently), comp_* = 0. */
+int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
+                        const uint32_t* d_client_of_slot, uint32_t* d_xd,
+                        uint32_t* d_xr, uint32_t* d_comp_delta, uint32_t* d_comp_rho,
+                        uint32_t* d_sum_delta, uint32_t* d_sum_rho);
+/* After the sums are all-reduced over the ranks: gdelta += sum_delta, grho
+ * += sum_rho (the_delta / the_rho of track_resp), sums cleared. */
+int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
+                        uint32_t* d_grho, uint32_t* d_sum_delta, uint32_t* d_sum_rho);
 
 /* ------------------------------------------------------------ tuning
  * Engine options (no reference counterpart): pulls with k <= SMALL_K run one

@@ -9,23 +9,28 @@ with responses delivered in bulk at epoch boundaries; tests pin it against the
 sequential restatement of the tracker (oracle/pyoracle.Tracker).
 
 State (uint32, modular like the reference's uint32 cast of Counter
-differences): per client the global delta/rho counters (start at 1), per
-(server, client) X = delta_prev_req + my_delta (and the rho analogue) and a
-`known` flag (server in server_map).
+differences): per global client the delta/rho counters (start at 1), per
+(server, table slot) X = delta_prev_req + my_delta (and the rho analogue) and
+a `known` flag (server in server_map); client_of_slot[s][slot] names the
+global client of a server's table slot (identity when None).
 """
 import numpy as np
 
 
 class EpochTrackers:
-    def __init__(self, n_servers, n_clients):
-        self.S, self.N = n_servers, n_clients
-        self.gd = np.ones(n_clients, np.uint32)
-        self.gr = np.ones(n_clients, np.uint32)
-        self.xd = np.zeros((n_servers, n_clients), np.uint32)
-        self.xr = np.zeros((n_servers, n_clients), np.uint32)
-        self.known = np.zeros((n_servers, n_clients), bool)
-        self.comp_d = np.zeros((n_servers, n_clients), np.uint32)
-        self.comp_r = np.zeros((n_servers, n_clients), np.uint32)
+    def __init__(self, n_servers, n_slots, n_clients=None, client_of_slot=None):
+        G = n_slots if n_clients is None else n_clients
+        self.S, self.N, self.G = n_servers, n_slots, G
+        if client_of_slot is None:
+            client_of_slot = np.tile(np.arange(n_slots, dtype=np.int64), (n_servers, 1))
+        self.cmap = np.asarray(client_of_slot, np.int64)
+        self.gd = np.ones(G, np.uint32)
+        self.gr = np.ones(G, np.uint32)
+        self.xd = np.zeros((n_servers, n_slots), np.uint32)
+        self.xr = np.zeros((n_servers, n_slots), np.uint32)
+        self.known = np.zeros((n_servers, n_slots), bool)
+        self.comp_d = np.zeros((n_servers, n_slots), np.uint32)
+        self.comp_r = np.zeros((n_servers, n_slots), np.uint32)
 
     def fill(self, s, reqs):
         """get_req_params(s) for every request of `reqs` (batch order); sets
@@ -35,15 +40,16 @@ class EpochTrackers:
         rho = np.zeros(len(reqs), np.uint32)
         _, first = np.unique(slots, return_index=True)
         c = slots[first]
+        g = self.cmap[s, c]
         new = ~self.known[s, c]
         with np.errstate(over="ignore"):
-            d = np.where(new, np.uint32(1), self.gd[c] - self.xd[s, c])
-            r = np.where(new, np.uint32(1), self.gr[c] - self.xr[s, c])
+            d = np.where(new, np.uint32(1), self.gd[g] - self.xd[s, c])
+            r = np.where(new, np.uint32(1), self.gr[g] - self.xr[s, c])
         delta[first] = d
         rho[first] = r
         self.known[s, c] = True
-        self.xd[s, c] = self.gd[c]
-        self.xr[s, c] = self.gr[c]
+        self.xd[s, c] = self.gd[g]
+        self.xr[s, c] = self.gr[g]
         reqs["delta"] = delta
         reqs["rho"] = rho
 
@@ -57,9 +63,12 @@ class EpochTrackers:
             np.add.at(self.comp_r[s], slots[res], cost[res])
 
     def local_sums(self):
-        with np.errstate(over="ignore"):
-            return (self.comp_d.sum(0, dtype=np.uint64).astype(np.uint32),
-                    self.comp_r.sum(0, dtype=np.uint64).astype(np.uint32))
+        """per global client: the responses of this object's servers"""
+        sd = np.zeros(self.G, np.uint64)
+        sr = np.zeros(self.G, np.uint64)
+        np.add.at(sd, self.cmap.ravel(), self.comp_d.ravel().astype(np.uint64))
+        np.add.at(sr, self.cmap.ravel(), self.comp_r.ravel().astype(np.uint64))
+        return sd.astype(np.uint32), sr.astype(np.uint32)
 
     def deliver(self, sum_d=None, sum_r=None):
         """Epoch boundary: the global counters advance by every server's

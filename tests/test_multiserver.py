@@ -40,11 +40,19 @@ def epoch_batches(rng, n_servers, n_clients, n_epochs, per_server, t0=1.0,
     return out
 
 
-def test_epoch_restatement_matches_sequential_tracker():
+def client_maps(rng, n_servers, n_slots, n_clients):
+    """each server table: n_slots distinct global clients in random order"""
+    return np.stack([rng.permutation(n_clients)[:n_slots] for _ in range(n_servers)])
+
+
+@pytest.mark.parametrize("mapped", [False, True])
+def test_epoch_restatement_matches_sequential_tracker(mapped):
     rng = np.random.default_rng(3)
     S, N = 3, 40
-    et = EpochTrackers(S, N)
-    seq = [pyoracle.Tracker("orig") for _ in range(N)]
+    G = 70 if mapped else N
+    cmap = client_maps(rng, S, N, G) if mapped else np.tile(np.arange(N), (S, 1))
+    et = EpochTrackers(S, N, G, cmap if mapped else None)
+    seq = [pyoracle.Tracker("orig") for _ in range(G)]
     for epoch in range(6):
         batches = []
         for s in range(S):
@@ -52,7 +60,7 @@ def test_epoch_restatement_matches_sequential_tracker():
             reqs["slot"] = rng.integers(0, N, len(reqs))
             et.fill(s, reqs)
             for i in range(len(reqs)):
-                d, r = seq[reqs["slot"][i]].get_req_params(s)
+                d, r = seq[cmap[s, reqs["slot"][i]]].get_req_params(s)
                 assert (d, r) == (reqs["delta"][i], reqs["rho"][i]), (epoch, s, i)
             batches.append(reqs)
         for s in range(S):
@@ -63,7 +71,7 @@ def test_epoch_restatement_matches_sequential_tracker():
             dec["phase"] = rng.integers(0, 2, n)
             et.tally(s, dec)
             for x in dec:
-                seq[x["slot"]].track_resp(s, int(x["phase"]), int(x["cost"]))
+                seq[cmap[s, x["slot"]]].track_resp(s, int(x["phase"]), int(x["cost"]))
         et.deliver()
 
 
@@ -138,16 +146,17 @@ def test_device_trackers_and_multiserver_parity():
     import torch
     from dmclock_amd.multiserver import DeviceTrackers, make_queues
     from parity import compare_decisions
-    S, N = 4, 300
+    S, N, G = 4, 300, 500
     rng = np.random.default_rng(5)
+    cmap = client_maps(rng, S, N, G)
     tab = workloads.client_table(rng, N)
     qg = make_queues(S, N, device=0, ring_capacity=64)
     qo = [pyoracle.OracleQueue() for _ in range(S)]
     for q in qg + qo:
         q.register(tab.slots, tab.r, tab.w, tab.l, True)
     dev = torch.device("cuda", 0)
-    dt = DeviceTrackers(qg, N, dev)
-    et = EpochTrackers(S, N)
+    dt = DeviceTrackers(qg, N, dev, n_clients=G, client_of_slot=cmap)
+    et = EpochTrackers(S, N, G, cmap)
     n_dec = 0
     for t, ep in epoch_batches(rng, S, N, n_epochs=6, per_server=250):
         for s in range(S):
