@@ -16,6 +16,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -715,7 +716,11 @@ struct dmc_queue {
   uint8_t* mr = nullptr;      // N: R prefix length
   RoundPart* rparts = nullptr;
   Round* rd = nullptr;
-  Round* h_rd = nullptr;      // pinned: round readback
+  Round h_rd_copy{};          // host copy of the last round's summary
+  Round* h_rd = &h_rd_copy;
+  HostRound* h_round = nullptr;  // fine-grained pinned, written by k_rfinish
+  HostRound* d_hround = nullptr; // its device address
+  uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
   uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin tables (k_rpick)
   uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters
@@ -733,7 +738,6 @@ struct dmc_queue {
   uint32_t *ek32 = nullptr, *sk32 = nullptr;  // 32-bit sort keys
   uint32_t *eval = nullptr, *sval = nullptr;
   uint32_t *gsz = nullptr, *goff = nullptr, *gisp = nullptr, *gpoff = nullptr;
-  dmc_pull_result* h_res = nullptr;  // pinned: device-API result staging
   // add batch buffers
   uint32_t bcap = 0;
   dmc_request* d_reqs = nullptr;
@@ -1198,13 +1202,15 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                      q->sched, q->debug ? q->dbg_atime : nullptr);
   pe(q);
   if (future) launch_future(q);
+  hipLaunchKernelGGL(k_rfinish, dim3(1), dim3(64), 0, q->stream, (const Round*)q->rd,
+                     q->d_hround);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
-                 bool radix, bool future) {
+                 dmc_pull_result* d_result, bool radix, bool future) {
   uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 2) | (radix ? 2 : 0) |
                  (future ? 1 : 0);
-  CallParams cp{kk, 0, now, out, q->tick};
+  CallParams cp{kk, 0, now, out, q->tick, d_result, ++q->round_seq};
   GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, future); });
   if (!g) {
     enqueue_round(q, cp, radix, future);
@@ -1216,13 +1222,38 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   return graph_replay(q, *g, args);
 }
 
+// Wait for round `seq`'s summary in host memory (k_rfinish).  Polls; after
+// 2 ms (a long round, or a device fault) blocks on the stream instead, which
+// reports errors.
+int wait_round(dmc_queue* q, uint64_t seq) {
+  const volatile uint64_t* flag = &q->h_round->seq;
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 255) == 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      HIP_OK(hipStreamSynchronize(q->stream));
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) return DMC_EDEVICE;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  std::memcpy(q->h_rd, (const void*)&q->h_round->r, sizeof(Round));
+  return DMC_OK;
+}
+
 // k successive pull_request(now).  Each round is one graph launch and one
 // host round trip; a round ends the batch unless the radix path's dense
 // buffer overflowed (retry with more capacity), a rank bin overflowed (retry
 // on the radix path) or, with AtLimit::Allow, the eligible work ran out (one
-// general limit-break step, then another round).
+// general limit-break step, then another round).  d_result (device API) is
+// written by the first round's k_rfinish when that round ends the call;
+// *dev_wrote says so.
 int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
-              dmc_pull_result* res) {
+              dmc_pull_result* res, dmc_pull_result* d_result = nullptr,
+              bool* dev_wrote = nullptr) {
+  if (dev_wrote) *dev_wrote = false;
+  bool first_round = true;
   dmc_pull_result r{};
   r.next_type = DMC_NEXT_RETURNING;
   uint32_t n_dec = 0;
@@ -1244,6 +1275,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
         break;
       }
       ++n_dec;
+      (q->h_sctl->prio ? r.n_priority : r.n_reservation)++;
       continue;
     }
     bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
@@ -1252,14 +1284,17 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       int rc = ensure_entries(q, q->dense_hint);
       if (rc) return rc;
     }
-    int rc = launch_round(q, now, kk, d_out + n_dec, radix, !allow);
+    // the first round of a call may end it: its k_rfinish writes d_result
+    dmc_pull_result* dres = (first_round && n_dec == 0) ? d_result : nullptr;
+    int rc = launch_round(q, now, kk, d_out + n_dec, dres, radix, !allow);
     if (rc) return rc;
-    // one host round trip per round, through pinned memory
-    HIP_OK(hipMemcpyAsync(q->h_rd, q->rd, sizeof(Round), hipMemcpyDeviceToHost,
-                          q->stream));
-    HIP_OK(hipStreamSynchronize(q->stream));
+    // one host round trip per round, through host-mapped memory
+    rc = wait_round(q, q->round_seq);
+    if (rc) return rc;
     pflush(q);
     const Round c = *q->h_rd;
+    bool wrote = dres && !c.overflow;
+    first_round = false;
     if (q->debug && getenv("DMC_DEBUG_BINS")) {
       std::vector<uint32_t> hb(kNBR);
       (void)hipMemcpy(hb.data(), q->dbg_bins, hb.size() * 4, hipMemcpyDeviceToHost);
@@ -1294,7 +1329,12 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       continue;
     }
     n_dec += c.n_dec;
-    if (n_dec >= k || !c.terminal) break;
+    r.n_priority += c.n_prio;
+    r.n_reservation += c.n_dec - c.n_prio;
+    if (n_dec >= k || !c.terminal) {
+      if (dev_wrote) *dev_wrote = wrote;
+      break;
+    }
     if (allow) {
       int type;
       double when;
@@ -1306,10 +1346,12 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
         break;
       }
       ++n_dec;
+      (q->h_sctl->prio ? r.n_priority : r.n_reservation)++;
       continue;
     }
     r.next_type = c.next_type;
     r.when = c.when;
+    if (dev_wrote) *dev_wrote = wrote;
     break;
   }
   r.n_decisions = n_dec;
@@ -1397,10 +1439,13 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->reqcount, 1);
-  if (hipHostMalloc((void**)&q->h_rd, sizeof(Round), 0) != hipSuccess ||
-      hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess ||
-      hipHostMalloc((void**)&q->h_res, sizeof(dmc_pull_result), 0) != hipSuccess)
+  if (hipHostMalloc((void**)&q->h_round, sizeof(HostRound),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&q->d_hround, q->h_round, 0) != hipSuccess ||
+      hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess)
     rc |= DMC_ENOMEM;
+  else
+    std::memset((void*)q->h_round, 0, sizeof(HostRound));
   if (rc) {
     dmc_queue_destroy(q);
     return DMC_ENOMEM;
@@ -1437,9 +1482,8 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->apblk, q->d_dec, q->temp};
   for (void* p : ptrs)
     dfree(p);
-  if (q->h_rd) (void)hipHostFree(q->h_rd);
+  if (q->h_round) (void)hipHostFree(q->h_round);
   if (q->h_sctl) (void)hipHostFree(q->h_sctl);
-  if (q->h_res) (void)hipHostFree(q->h_res);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -1714,8 +1758,6 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
     HIP_OK(hipMemcpyAsync(out, q->d_dec, sizeof(dmc_decision) * r.n_decisions,
                           hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
-  for (uint32_t i = 0; i < r.n_decisions; ++i)
-    (out[i].phase == DMC_PHASE_RESERVATION ? r.n_reservation : r.n_priority)++;
   if (result) *result = r;
   return DMC_OK;
 }
@@ -1725,14 +1767,12 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
   if (!q || (k && !d_out)) return DMC_EINVAL;
   QueueLock g(q);
   dmc_pull_result r{};
-  int rc = pull_impl(q, now, k, d_out, &r);
+  bool dev_wrote = false;
+  int rc = pull_impl(q, now, k, d_out, &r, d_result, &dev_wrote);
   if (rc) return rc;
-  if (d_result) {
-    // stream-ordered: pull_impl has synchronised, so the pinned staging
-    // record is free, and the copy completes before any later work
-    *q->h_res = r;
-    HIP_OK(hipMemcpyAsync(d_result, q->h_res, sizeof(r), hipMemcpyHostToDevice,
-                          q->stream));
+  if (d_result && !dev_wrote) {  // stream-ordered after the call's rounds
+    hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, d_result, r);
+    HIP_OK(hipGetLastError());
   }
   return DMC_OK;
 }

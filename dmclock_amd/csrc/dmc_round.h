@@ -89,6 +89,8 @@ struct Round {
   double now;
   dmc_decision* out;
   uint64_t tick;
+  dmc_pull_result* res;  // device-API result record (null: the host writes it)
+  uint64_t seq;          // round sequence number, published to the host
 };
 
 struct CallParams {
@@ -97,6 +99,17 @@ struct CallParams {
   double now;
   dmc_decision* out;
   uint64_t tick;
+  dmc_pull_result* res;
+  uint64_t seq;
+};
+
+// Host-mapped (fine-grained pinned) round summary: the round's last kernel
+// copies Round here and then publishes seq, so the host learns the outcome
+// by polling host memory instead of a device-to-host copy and a stream
+// synchronisation (two command-processor round trips per call).
+struct HostRound {
+  Round r;
+  uint64_t seq;
 };
 
 __device__ inline uint64_t shfl_down_u64r(uint64_t v, int d) {
@@ -218,6 +231,8 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     z.now = cp.now;
     z.out = cp.out;
     z.tick = cp.tick;
+    z.res = cp.res;
+    z.seq = cp.seq;
     *rd = z;
   }
   const double now = cp.now;
@@ -1163,5 +1178,33 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
     }
   }
 }
+
+// Round end (one block of 64): the device-API result record when the host
+// expects this round to end the call (no overflow retry; a terminal round
+// under AtLimit::Allow is followed by host-driven steps, which rewrite it),
+// then the Round summary to host memory and its sequence number last.
+__global__ void k_rfinish(const Round* rd, HostRound* h) {
+  constexpr uint32_t W = sizeof(Round) / 4;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x == 0 && rd->res && !rd->overflow) {
+    dmc_pull_result r{};
+    r.n_decisions = rd->n_dec;
+    bool stop = rd->terminal && rd->n_dec < rd->k_total;
+    r.next_type = stop ? rd->next_type : DMC_NEXT_RETURNING;
+    r.when = stop ? rd->when : 0.0;
+    r.n_priority = rd->n_prio;
+    r.n_reservation = rd->n_dec - rd->n_prio;
+    *rd->res = r;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&h->seq, rd->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// device-API result written by the host's view of a multi-round call
+__global__ void k_put_result(dmc_pull_result* res, dmc_pull_result r) { *res = r; }
 
 }  // namespace dmc

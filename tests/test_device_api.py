@@ -1,0 +1,75 @@
+"""The device-resident API (dmc_add_batch_device / dmc_pull_batch_device, the
+path bench.py times) against the host API on the same trace: identical
+decisions and add statuses, and the device result record
+(n_decisions, next_type, when, n_reservation, n_priority) equal to the host
+call's, with the phase counts equal to the decisions' phases.  The result is
+written on the device by the round's last kernel when one round ends the
+call, and by the host's view otherwise (overflow retries, AtLimit::Allow
+steps, small-k steps): every path is exercised.
+"""
+import numpy as np
+import pytest
+
+from dmclock_amd import workloads
+from dmclock_amd._abi import (AT_LIMIT_ALLOW, AT_LIMIT_WAIT, DECISION_DTYPE,
+                              OPT_FORCE_RADIX, OPT_GRAPHS, OPT_SMALL_K, PullResult)
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(variant, **kw):
+    from dmclock_amd.gpu import GpuQueue
+    q = GpuQueue(max_clients=kw.pop("n"), ring_capacity=64, **kw)
+    if variant == "radix":
+        q.set_option(OPT_FORCE_RADIX, 1)
+    elif variant == "steps":
+        q.set_option(OPT_SMALL_K, 1 << 30)
+    elif variant == "eager":
+        q.set_option(OPT_GRAPHS, 0)
+    return q
+
+
+@pytest.mark.parametrize("variant", ["default", "radix", "steps", "eager"])
+@pytest.mark.parametrize("at_limit", [AT_LIMIT_WAIT, AT_LIMIT_ALLOW],
+                         ids=["wait", "allow"])
+def test_device_api_matches_host_api(variant, at_limit):
+    import torch
+    n = 400
+    tr = workloads.steady_trace(7, n, 10, 300, 0, depth=2, delta_rho="random",
+                                k_choices=(1, 5, 40, 300, 900, 5000))
+    qh = _mk(variant, n=n, at_limit=at_limit)
+    qd = _mk(variant, n=n, at_limit=at_limit)
+    c = tr.clients
+    for q in (qh, qd):
+        q.register(c.slots, c.r, c.w, c.l, c.active)
+    dev = torch.device("cuda", 0)
+    res_sz = 24
+    kinds = set()
+    for op in tr.ops:
+        if op[0] == "add":
+            reqs = op[1]
+            rc_h = qh.add_batch(reqs)
+            d_reqs = torch.from_numpy(reqs.view(np.uint8).copy()).to(dev)
+            d_rc = torch.full((len(reqs),), -7, dtype=torch.int32, device=dev)
+            qd.add_batch_device(d_reqs.data_ptr(), len(reqs), d_rc.data_ptr())
+            qd.sync()
+            assert np.array_equal(d_rc.cpu().numpy(), rc_h)
+            continue
+        _, now, k = op
+        dh, rh = qh.pull_batch(now, k)
+        d_out = torch.zeros(max(k, 1) * DECISION_DTYPE.itemsize, dtype=torch.uint8,
+                            device=dev)
+        d_res = torch.full((res_sz,), 0xAB, dtype=torch.uint8, device=dev)
+        qd.pull_batch_device(now, k, d_out.data_ptr(), d_res.data_ptr())
+        qd.sync()
+        rd = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+        dd = d_out.cpu().numpy().view(DECISION_DTYPE)[:rd.n_decisions]
+        assert (rd.n_decisions, rd.next_type) == (rh.n_decisions, rh.next_type)
+        if rh.next_type == 1:
+            assert rd.when == rh.when
+        assert np.array_equal(dd, dh)
+        n_res = int((dh["phase"] == 0).sum())
+        assert (rd.n_reservation, rd.n_priority) == (n_res, len(dh) - n_res)
+        assert (rh.n_reservation, rh.n_priority) == (n_res, len(dh) - n_res)
+        kinds.add(rd.next_type)
+    assert 0 in kinds  # some pulls returned k decisions
