@@ -40,7 +40,7 @@ STAGE_BYTES = {
     # k_rscan: count 4 + front_r 8 + flags 1 + front_p 8 + front_l 8 +
     #   prop_delta 8 read, keyr 8 + keyp 8 + R-prefix length 1 written
     "scan": (54, 0, 0),
-    # k_rhist: keyr + keyp read (k_rpick: one block, 2 x 2048 bins)
+    # k_rhist: keyr + keyp read (its last block: 2 x 2048-bin thresholds)
     "select": (16, 0, 0),
     # k_remit: keyr + keyp read; per dispatched entry its ring entry 64 read
     #   and rank record 24 written

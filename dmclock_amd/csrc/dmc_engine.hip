@@ -470,9 +470,9 @@ __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
 
 // launched with one block of kBlock threads; combines the per-block partials
 // (tree reduction in LDS), then thread 0 decides
-__global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
-                              int at_limit, uint32_t nregistered,
-                              StepCtl* sc, Round* ctl) {
+__device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
+                            int at_limit, uint32_t nregistered,
+                            StepCtl* sc, Round* ctl) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
   if (ctl) now = ctl->now;
   __shared__ StepRed sh[kBlock];
@@ -576,6 +576,18 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
   if (ctl) {
     ctl->next_type = c.type;
     ctl->when = c.when;
+  }
+}
+
+// The general decision; a round's terminal pull also ends the round (h: the
+// host-mapped summary, k_rfinish's work folded in).
+__global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
+                              int at_limit, uint32_t nregistered,
+                              StepCtl* sc, Round* ctl, HostRound* h) {
+  step_decide(nparts, part, now, at_limit, nregistered, sc, ctl);
+  if (h) {
+    __syncthreads();
+    rfinish_body(ctl, h);
   }
 }
 
@@ -714,7 +726,7 @@ struct dmc_queue {
   uint32_t* cand = nullptr;   // N: candidate slots of the round
   uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
   uint8_t* mr = nullptr;      // N: R prefix length
-  RoundPart* rparts = nullptr;
+  RoundPart* rparts = nullptr; // k_rscan's per-block partials
   Round* rd = nullptr;
   Round h_rd_copy{};          // host copy of the last round's summary
   Round* h_rd = &h_rd_copy;
@@ -1081,7 +1093,7 @@ void launch_future(dmc_queue* q) {
                      q->tb, now, q->red, (const Round*)q->rd);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, q->rd);
+                     q->n_registered, q->sctl, q->rd, q->d_hround);
   pe(q);
 }
 
@@ -1094,7 +1106,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
                      tb, now, q->red, (const Round*)nullptr);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, (Round*)nullptr);
+                     q->n_registered, q->sctl, (Round*)nullptr, (HostRound*)nullptr);
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
                      q->stream, tb, now, (const StepCtl*)q->sctl);
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
@@ -1132,9 +1144,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   pb(q, DMC_PROF_SELECT);
   hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
                      (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const RoundPart*)q->rparts, gN, q->hist);
+                     (const RoundPart*)q->rparts, gN, q->rd, q->hist);
   hipLaunchKernelGGL(k_rpick, dim3(2), dim3(kPickThreadsR), 0, q->stream, q->rd,
-                     (const RoundPart*)q->rparts, gN, q->hist, q->sbase, q->snum);
+                     q->hist, q->sbase, q->snum);
   pe(q);
   pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_rcand, dim3(kCandBlocksR), dim3(kCandThreads), 0, q->stream,
@@ -1201,9 +1213,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                      (const uint64_t*)q->keyp, q->applied, q->bcount, q->bsize,
                      q->sched, q->debug ? q->dbg_atime : nullptr);
   pe(q);
-  if (future) launch_future(q);
-  hipLaunchKernelGGL(k_rfinish, dim3(1), dim3(64), 0, q->stream, (const Round*)q->rd,
-                     q->d_hround);
+  if (future)
+    launch_future(q);  // its decide kernel ends the round
+  else
+    hipLaunchKernelGGL(k_rfinish, dim3(1), dim3(64), 0, q->stream, (const Round*)q->rd,
+                       q->d_hround);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
@@ -1418,7 +1432,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->keyr, N);
   rc |= A(&q->keyp, N);
   rc |= A(&q->mr, N);
-  rc |= A(&q->hist, 2 * kHistBinsR);
+  rc |= A(&q->hist, kShards * 2 * kHistBinsR);
   rc |= A(&q->sbase, 2 * kHistBinsR); rc |= A(&q->snum, 2 * kHistBinsR);
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);

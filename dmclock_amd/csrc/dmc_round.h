@@ -23,14 +23,20 @@
 // Kernels (one thread per client slot unless noted):
 //   k_rscan   R prefix length + first R key, first P key of the post-R front,
 //             pending limit-scan mark; per-block counts and key ranges
-//   k_rhist   key histograms of both phases (2048 bins each)
-//   k_rpick   one block: thresholds T_R / T_P (every key <= T is a candidate,
+//             (the graph's parameter node: publishes the call's parameters)
+//   k_rhist   the round's totals; key histograms of both phases (2048 bins
+//             each, over the exact key ranges, flushed into kShards shards)
+//   k_rpick   two blocks: thresholds T_R / T_P (every key <= T is a candidate,
 //             at least the needed number of keys are <= T) and the rank-bin
 //             tables (R bins [0, kNBPhase), P bins [kNBPhase, kNBR))
+//   k_rcand   compacts the candidate slots, settles the others' pending marks
 //   k_remit   candidates enumerate their entries into rank bins
-//   k_rrank   one wave per rank bin: rank in LDS, decide, count applied pops
-//   k_rapply  replays each client's dispatched pops with the same arithmetic,
-//             writes the decision records and the new client state
+//   k_rbscan  one block: prefix sums of the rank-bin sizes, decision count
+//   k_rrank   one block per rank bin: rank in LDS, decide, count applied pops
+//   k_rapply  replays each candidate's dispatched pops with the same
+//             arithmetic, writes the decision records and the new state
+//   k_rfinish round summary to host-mapped memory (folded into the terminal
+//             pull's k_step_decide when the round has one)
 // A rank bin that outgrows kBinCap (massively tied keys) aborts the round
 // (overflow = 2): the host replays it on the radix path (dense entries,
 // 32-bit radix sort + exact fix-up).
@@ -44,6 +50,10 @@ constexpr int kBlockR = 256;
 constexpr int kHistBinsR = 2048;        // per phase
 constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
 constexpr int kNBPhase = kNBR / 2;
+// Same-address atomics from every block of a launch serialise at the memory
+// side (~12 ns each): the histogram is sharded 8 ways (block % 8, one shard
+// per XCD) and the pick combines the shards.
+constexpr int kShards = 8;
 constexpr uint32_t kBinCapR = 256;      // entries per rank bin (4 per lane)
 constexpr uint32_t kNoneR = 0xffffffffu;
 constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
@@ -53,8 +63,18 @@ struct PhaseSel {
   uint64_t kmin, kmax;  // ordered-key range of the first keys
   uint64_t T;           // candidates: first key <= T (0: none)
   uint32_t n_elig;      // clients with an eligible first key
-  uint32_t hshift;      // histogram bin of key k: (k - kmin) >> hshift
+  uint32_t hshift;      // histogram bin of key k: hist_bin(k, hmin, hshift)
   uint32_t tbin;        // histogram bin holding T (last bin of the table)
+  uint32_t pad;
+  uint64_t hmin;        // histogram base
+  uint64_t lo0, hitop;  // key span of the open-ended first / last bin
+};
+
+// Histogram range of a phase: base key and bin shift (bins 0 and
+// kHistBinsR - 1 are open-ended).
+struct HistRange {
+  uint64_t hmin;
+  uint32_t shift;
   uint32_t pad;
 };
 
@@ -156,7 +176,7 @@ struct CountV {
 // mark gets F_PMARK; k_rapply turns it into F_READY iff the priority pulls ran.
 // Each thread takes kScanSlots slots and issues all their column loads before
 // any walk; blocks of kScanBlock threads, so that the per-block partials
-// (counts, key ranges) that k_rhist's blocks and k_rpick reduce stay few.
+// (counts, key ranges) stay few.
 constexpr int kScanSlots = 2;
 constexpr int kScanBlock = 1024;
 
@@ -220,6 +240,52 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
   }
 }
 
+__device__ inline void rpart_combine(RoundPart& a, const RoundPart& b) {
+  for (int p = 0; p < 2; ++p) {
+    a.cnt[p] += b.cnt[p];
+    a.mn[p] = b.mn[p] < a.mn[p] ? b.mn[p] : a.mn[p];
+    a.mx[p] = b.mx[p] > a.mx[p] ? b.mx[p] : a.mx[p];
+  }
+  a.n_r += b.n_r;
+}
+
+__device__ inline RoundPart rpart_ident() {
+  return RoundPart{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
+}
+
+// one wave's partials combined across its lanes (result in every lane)
+__device__ inline RoundPart wave_reduce_rpart(const RoundPart& a) {
+  RoundPart o;
+  o.cnt[0] = wsum32(a.cnt[0]);
+  o.cnt[1] = wsum32(a.cnt[1]);
+  o.n_r = wsum64(a.n_r);
+  o.mn[0] = wmin64(a.mn[0]);
+  o.mn[1] = wmin64(a.mn[1]);
+  o.mx[0] = wmax64(a.mx[0]);
+  o.mx[1] = wmax64(a.mx[1]);
+  return o;
+}
+
+__device__ inline uint32_t hist_shift_r(uint64_t range) {
+  // smallest shift with (range >> shift) < kHistBinsR
+  uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
+  return bits > 11 ? bits - 11 : 0;
+}
+
+// histogram bin of a key (bins 0 and kHistBinsR - 1 are open-ended)
+__device__ inline uint32_t hist_bin(uint64_t k, uint64_t hmin, uint32_t sh) {
+  if (k <= hmin) return 0;
+  uint64_t b = (k - hmin) >> sh;
+  return b >= (uint64_t)kHistBinsR ? kHistBinsR - 1 : (uint32_t)b;
+}
+
+__device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
+  return a + b < a ? ~0ull : a + b;
+}
+
+// Scan.  Per-block counts and key ranges (parts), staged in LDS and combined
+// by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
+// for a RoundPart, too many to run in every wave of the block).
 __global__ void __launch_bounds__(kScanBlock)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
         Round* rd, CallParams cp) {
@@ -235,8 +301,9 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     z.seq = cp.seq;
     *rd = z;
   }
+  __shared__ RoundPart sh[kScanBlock];
   const double now = cp.now;
-  RoundPart acc{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
+  RoundPart acc = rpart_ident();
   const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
   ScanCols x[kScanSlots];
 #pragma unroll
@@ -258,98 +325,94 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     uint32_t s = base + j * blockDim.x;
     if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, acc);
   }
-  uint32_t cnt0 = wsum32(acc.cnt[0]), cnt1 = wsum32(acc.cnt[1]);
-  uint64_t nr = wsum64(acc.n_r);
-  uint64_t mn0 = wmin64(acc.mn[0]), mx0 = wmax64(acc.mx[0]);
-  uint64_t mn1 = wmin64(acc.mn[1]), mx1 = wmax64(acc.mx[1]);
-  __shared__ RoundPart sh[kScanBlock / 64];
-  int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sh[w] = RoundPart{{cnt0, cnt1}, nr, {mn0, mn1}, {mx0, mx1}};
+  sh[threadIdx.x] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    RoundPart o = sh[0];
-    for (int i = 1; i < kScanBlock / 64; ++i) {
-      for (int p = 0; p < 2; ++p) {
-        o.cnt[p] += sh[i].cnt[p];
-        o.mn[p] = sh[i].mn[p] < o.mn[p] ? sh[i].mn[p] : o.mn[p];
-        o.mx[p] = sh[i].mx[p] > o.mx[p] ? sh[i].mx[p] : o.mx[p];
-      }
-      o.n_r += sh[i].n_r;
-    }
-    parts[blockIdx.x] = o;
+  if (threadIdx.x < 64) {
+    RoundPart o = sh[threadIdx.x];
+    for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
+    o = wave_reduce_rpart(o);
+    if (threadIdx.x == 0) parts[blockIdx.x] = o;
   }
 }
 
-__device__ inline void rpart_combine(RoundPart& a, const RoundPart& b) {
-  for (int p = 0; p < 2; ++p) {
-    a.cnt[p] += b.cnt[p];
-    a.mn[p] = b.mn[p] < a.mn[p] ? b.mn[p] : a.mn[p];
-    a.mx[p] = b.mx[p] > a.mx[p] ? b.mx[p] : a.mx[p];
-  }
-  a.n_r += b.n_r;
-}
-
-// block-wide reduction of the scan partials (every thread gets the result):
-// strided per thread, then across the wave by shuffles, then across waves
+// The round's totals from the scan's per-block partials (every thread gets
+// them): wave 0 combines them, 8 per lane for 512 partials with the loads in
+// flight together, and reduces across its lanes; the other waves wait.
 __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t nparts) {
-  __shared__ RoundPart sh[1024 / 64];
-  RoundPart o{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
-  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) rpart_combine(o, parts[i]);
-  for (int p = 0; p < 2; ++p) {
-    o.cnt[p] = wsum32(o.cnt[p]);
-    o.mn[p] = wmin64(o.mn[p]);
-    o.mx[p] = wmax64(o.mx[p]);
+  __shared__ RoundPart sh_tot;
+  if (threadIdx.x < 64) {
+    RoundPart o = rpart_ident();
+    for (uint32_t i = threadIdx.x; i < nparts; i += 64) rpart_combine(o, parts[i]);
+    o = wave_reduce_rpart(o);
+    if (threadIdx.x == 0) sh_tot = o;
   }
-  o.n_r = wsum64(o.n_r);
-  int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sh[w] = o;
   __syncthreads();
-  RoundPart r = sh[0];
-  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) rpart_combine(r, sh[i]);
+  RoundPart r = sh_tot;
   __syncthreads();
   return r;
 }
 
-__device__ inline uint32_t hist_shift_r(uint64_t range) {
-  // smallest shift with (range >> shift) < kHistBinsR
-  uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
-  return bits > 11 ? bits - 11 : 0;
-}
-
-// ---------------------------------------------------------------- k_rhist
-// Histograms of both phases' first keys over their [kmin, kmax].
-// kHistBlocksR blocks of 1024 threads: few enough that the global flush (one
-// atomic per non-empty bin per block) stays cheap.
+// Histograms of both phases' first keys over their exact [kmin, kmax]:
+// kHistBlocksR blocks of 1024 threads, 4 consecutive slots per thread and
+// iteration with every key load issued before the first LDS atomic; the
+// block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
 __global__ void __launch_bounds__(1024)
-k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp,
-        const RoundPart* parts, uint32_t nparts, uint32_t* hist) {
-  const RoundPart tot = reduce_rparts(parts, nparts);
+k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
+        uint32_t nparts, Round* rd, uint32_t* hist) {
+  __shared__ uint32_t lh[2][kHistBinsR];
+  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
+    lh[0][b] = 0;
+    lh[1][b] = 0;
+  }
+  // this thread's first keys are loaded before the totals are reduced (the
+  // two latencies overlap); further iterations only when n > 4 x threads
+  const uint32_t stride = gridDim.x * blockDim.x * 4;
+  uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  uint64_t kr[4], kp[4];
+  auto load = [&](uint32_t s0) {
+    if (s0 + 4 <= n) {
+      const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
+      const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
+      ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
+      kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
+      kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kr[j] = s0 + j < n ? keyr[s0 + j] : kMaxKey;
+        kp[j] = s0 + j < n ? keyp[s0 + j] : kMaxKey;
+      }
+    }
+  };
+  if (s < n) load(s);
+  const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    bool p_runs = tot.n_r < (uint64_t)rd->k_total;
+    rd->tot = tot;
+    rd->n_r = tot.n_r;
+    rd->p_runs = p_runs ? 1 : 0;
+  }
   if (tot.cnt[0] == 0 && tot.cnt[1] == 0) return;
-  __shared__ uint32_t sh[2][kHistBinsR];
-  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x)
-    for (int p = 0; p < 2; ++p) sh[p][b] = 0;
-  __syncthreads();
-  uint32_t sh0 = hist_shift_r(tot.mx[0] - tot.mn[0]);
-  uint32_t sh1 = hist_shift_r(tot.mx[1] - tot.mn[1]);
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n;
-       s += gridDim.x * blockDim.x) {
-    uint64_t k = keyr[s];
-    if (k != kMaxKey) {
-      atomicAdd(&sh[0][(uint32_t)((k - tot.mn[0]) >> sh0)], 1u);
+  const uint64_t mn0 = tot.mn[0], mn1 = tot.mn[1];
+  const uint32_t sh0 = hist_shift_r(tot.mx[0] - mn0);
+  const uint32_t sh1 = hist_shift_r(tot.mx[1] - mn1);
+  for (; s < n; s += stride) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(kr[j], mn0, sh0)], 1u);
+      if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(kp[j], mn1, sh1)], 1u);
     }
-    k = keyp[s];
-    if (k != kMaxKey) {
-      atomicAdd(&sh[1][(uint32_t)((k - tot.mn[1]) >> sh1)], 1u);
-    }
+    if (s + stride < n) load(s + stride);
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x)
-    for (int p = 0; p < 2; ++p)
-      if (sh[p][b]) atomicAdd(&hist[p * kHistBinsR + b], sh[p][b]);
+  uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
+  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
+    if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
+    if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
+  }
 }
 
-// ---------------------------------------------------------------- k_rpick
 constexpr int kPickThreadsR = 1024;
 constexpr int kBinsPerThreadR = kHistBinsR / kPickThreadsR;
 
@@ -373,23 +436,26 @@ __device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
 // T's bin in proportion to their counts (each gets 1 + its share), so that
 // the rank bins stay small however the keys are distributed.
 __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
-                                  Round* rd, uint32_t* hist,
+                                  const HistRange& hr, Round* rd, uint32_t* hist,
                                   uint32_t* sbase, uint32_t* snum,
                                   uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
                                   uint64_t* s_T) {
   int t = threadIdx.x;
   uint32_t ne = tot.cnt[p];
-  uint32_t sh1 = hist_shift_r(tot.mx[p] - tot.mn[p]);
-  uint32_t* hp = hist + p * kHistBinsR;
+  const uint32_t sh1 = hr.shift;
+  const uint64_t hmin = hr.hmin;
+  uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   if (t == 0) {
-    *s_tb = ne ? (uint32_t)((tot.mx[p] - tot.mn[p]) >> sh1) : 0;
+    *s_tb = ne ? hist_bin(tot.mx[p], hmin, sh1) : 0;
     *s_C = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
   }
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0;
   for (int j = 0; j < kBinsPerThreadR; ++j) {
-    h[j] = hp[t * kBinsPerThreadR + j];
+    h[j] = 0;
+#pragma unroll
+    for (int i = 0; i < kShards; ++i) h[j] += hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
     local += h[j];
   }
   uint32_t before = block_excl_scan_r(local, wsum);
@@ -399,9 +465,12 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
       cum += h[j];
       if (cum >= need) {
         // the bin's upper edge: the same candidate set as its largest key
+        // (the open-ended last bin: the largest key)
         uint32_t b = t * kBinsPerThreadR + j;
-        uint64_t edge = ((uint64_t)b << sh1) | ((1ull << sh1) - 1);
-        *s_T = edge >= kMaxKey - 1 - tot.mn[p] ? kMaxKey - 1 : tot.mn[p] + edge;
+        uint64_t edge = b == kHistBinsR - 1
+                            ? tot.mx[p]
+                            : sat_add_u64(hmin, ((uint64_t)(b + 1) << sh1) - 1);
+        *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : edge;
         *s_tb = b;
         break;
       }
@@ -431,7 +500,8 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     sbase[p * kHistBinsR + b] = p * kNBPhase + nb;
     snum[p * kHistBinsR + b] = ns[j];
     nb += ns[j];
-    hp[b] = 0;
+#pragma unroll
+    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + b] = 0;
   }
   if (t == 0) {
     PhaseSel z{};
@@ -441,51 +511,55 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     z.n_elig = ne;
     z.hshift = sh1;
     z.tbin = tb;
+    z.hmin = hmin;
+    z.lo0 = tot.mn[p] < hmin ? tot.mn[p] : hmin;
+    uint64_t top = sat_add_u64(hmin, (uint64_t)(kHistBinsR - 1) << sh1);
+    z.hitop = tot.mx[p] > top ? tot.mx[p] : top;
     rd->ph[p] = z;
   }
   __syncthreads();
 }
 
-// Two blocks, one per phase.
+
+// Thresholds and rank-bin tables: two blocks, one per phase.
 __global__ void __launch_bounds__(kPickThreadsR)
-k_rpick(Round* rd, const RoundPart* parts, uint32_t nparts, uint32_t* hist,
-        uint32_t* sbase, uint32_t* snum) {
+k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
   __shared__ uint32_t wsum[kPickThreadsR / 64];
   __shared__ uint32_t s_tb, s_C;
   __shared__ uint64_t s_T;
-  const RoundPart tot = reduce_rparts(parts, nparts);
-  if (blockIdx.x == 0 && threadIdx.x == 0) rd->tot = tot;
+  const RoundPart tot = rd->tot;
+  const int p = blockIdx.x;
   uint32_t k = rd->k_total;
-  bool p_runs = tot.n_r < (uint64_t)k;
-  if (blockIdx.x == 0) {
-    // R: all prefixes when they hold fewer than k entries; else every client
-    // whose first key is at or below the k-th smallest first key's bucket
-    // (each such client contributes at least one entry <= T)
-    pick_phase(0, p_runs ? 0xffffffffu : k, tot, rd, hist, sbase, snum, wsum,
-               &s_tb, &s_C, &s_T);
-    if (threadIdx.x == 0) {
-      rd->n_r = tot.n_r;
-      rd->p_runs = p_runs ? 1 : 0;
-    }
-  } else {
-    pick_phase(1, p_runs ? k - (uint32_t)tot.n_r : 0, tot, rd, hist, sbase,
-               snum, wsum, &s_tb, &s_C, &s_T);
-  }
+  bool p_runs = rd->p_runs;
+  // R: all prefixes when they hold fewer than k entries; else every client
+  // whose first key is at or below the k-th smallest first key's bucket
+  // (each such client contributes at least one entry <= T).  P: the rest.
+  uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
+                         : (p_runs ? k - (uint32_t)tot.n_r : 0);
+  const HistRange h{tot.mn[p], hist_shift_r(tot.mx[p] - tot.mn[p]), 0};
+  pick_phase(p, need, tot, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
-// of the phase's rank bins, split linearly (k_rpick's table).
+// of the phase's rank bins, split linearly over the bin's key span (k_rpick's
+// table; the open-ended first and last bins span the keys actually seen).
 __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
                                       const uint32_t* sbase, const uint32_t* snum) {
-  uint64_t d = k > ps.kmin ? k - ps.kmin : 0;
-  uint32_t sh1 = ps.hshift;
-  uint64_t hb = d >> sh1;
-  uint32_t h = hb > ps.tbin ? ps.tbin : (uint32_t)hb;
-  uint64_t lo = d - ((uint64_t)h << sh1);
+  uint32_t h = hist_bin(k, ps.hmin, ps.hshift);
+  if (h > ps.tbin) h = ps.tbin;
   uint32_t ns = snum[p * kHistBinsR + h];
-  uint64_t sub = sh1 <= 51 ? (lo * ns) >> sh1 : ((lo >> 12) * ns) >> (sh1 - 12);
-  if (sub >= ns) sub = ns - 1;
-  return sbase[p * kHistBinsR + h] + (uint32_t)sub;
+  uint32_t sub = 0;
+  if (ns > 1) {
+    uint64_t lo = h == 0 ? ps.lo0 : ps.hmin + ((uint64_t)h << ps.hshift);
+    uint64_t hi = h == kHistBinsR - 1 ? ps.hitop
+                                      : ps.hmin + ((uint64_t)(h + 1) << ps.hshift) - 1;
+    uint64_t off = k > lo ? k - lo : 0;
+    uint64_t w = hi > lo ? hi - lo : 0;
+    double f = (double)off / ((double)w + 1.0);
+    sub = (uint32_t)(f * (double)ns);
+    if (sub >= ns) sub = ns - 1;
+  }
+  return sbase[p * kHistBinsR + h] + sub;
 }
 
 // Rank-bin record of one entry: the order key (phase by bin, okey, slot,
@@ -1183,7 +1257,7 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
 // expects this round to end the call (no overflow retry; a terminal round
 // under AtLimit::Allow is followed by host-driven steps, which rewrite it),
 // then the Round summary to host memory and its sequence number last.
-__global__ void k_rfinish(const Round* rd, HostRound* h) {
+__device__ inline void rfinish_body(const Round* rd, HostRound* h) {
   constexpr uint32_t W = sizeof(Round) / 4;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
@@ -1203,6 +1277,7 @@ __global__ void k_rfinish(const Round* rd, HostRound* h) {
   if (threadIdx.x == 0)
     __hip_atomic_store(&h->seq, rd->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__global__ void k_rfinish(const Round* rd, HostRound* h) { rfinish_body(rd, h); }
 
 // device-API result written by the host's view of a multi-round call
 __global__ void k_put_result(dmc_pull_result* res, dmc_pull_result r) { *res = r; }
