@@ -1149,7 +1149,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                      q->hist, q->sbase, q->snum);
   pe(q);
   pb(q, DMC_PROF_EMIT);
-  hipLaunchKernelGGL(k_rcand, dim3(kCandBlocksR), dim3(kCandThreads), 0, q->stream,
+  hipLaunchKernelGGL(k_rcand, dim3((N + kCandChunk - 1) / kCandChunk), dim3(kCandThreads), 0, q->stream,
                      tb, q->rd, (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
                      q->cand);
   hipLaunchKernelGGL(k_remit, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,

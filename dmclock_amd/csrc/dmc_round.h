@@ -639,32 +639,52 @@ __device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
 
 // ---------------------------------------------------------------- k_rcand
 // Candidates compacted into a dense list, so that the walking kernels run
-// dense waves: kCandBlocksR blocks of kCandThreads, each owning a contiguous
-// slot range, one atomic each (list order is irrelevant: the ranking fixes the
-// order).  The same pass settles the pending limit-scan marks of every
-// non-candidate (F_PMARK -> F_READY iff the priority pulls run); candidates
-// settle theirs in k_rapply.
-constexpr int kCandBlocksR = 256;
+// dense waves: blocks of kCandThreads own kCandChunk consecutive slots, 4 per
+// thread with every load issued up front, one atomic per block (list order
+// is irrelevant: the ranking fixes the order).  The same pass settles the
+// pending limit-scan marks of every non-candidate (k_rapply settles the
+// candidates').
 constexpr int kCandThreads = 1024;
+constexpr uint32_t kCandChunk = kCandThreads * 4;
 __global__ void __launch_bounds__(kCandThreads)
 k_rcand(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
         uint32_t* cand) {
   __shared__ uint32_t wsum[kCandThreads / 64];
   __shared__ uint32_t base;
   const uint32_t n = tb.n;
-  uint32_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint32_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  const uint32_t s0 = blockIdx.x * kCandChunk + threadIdx.x * 4;
   const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
-  uint32_t c = 0;
-  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
-    bool isc = pred(keyr[s], keyp[s]);
-    c += isc;
-    if (!isc) {
-      uint8_t f = tb.flags[s];
-      if (f & F_PMARK) tb.flags[s] = (uint8_t)((f & ~F_PMARK) | (p_runs ? F_READY : 0));
+  uint64_t kr[4], kp[4];
+  uint8_t f[4];
+  if (s0 + 4 <= n) {
+    const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
+    const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
+    ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
+    uchar4 f4 = *reinterpret_cast<const uchar4*>(tb.flags + s0);
+    kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
+    kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
+    f[0] = f4.x; f[1] = f4.y; f[2] = f4.z; f[3] = f4.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bool in = s0 + j < n;
+      kr[j] = in ? keyr[s0 + j] : kMaxKey;
+      kp[j] = in ? keyp[s0 + j] : kMaxKey;
+      f[j] = in ? tb.flags[s0 + j] : 0;
     }
   }
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (s0 + j >= n) continue;
+    if (pred(kr[j], kp[j])) {
+      bits |= 1u << j;
+    } else if (f[j] & F_PMARK) {
+      tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
+    }
+  }
+  const uint32_t c = __popc(bits);
   uint32_t incl = c;
   int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int d = 1; d < 64; d <<= 1) {
@@ -681,8 +701,9 @@ k_rcand(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   if (threadIdx.x == 0) base = tot ? atomicAdd(&rd->n_cand, tot) : 0;
   __syncthreads();
   uint32_t o = base + wb + incl - c;
-  for (uint32_t s = lo + threadIdx.x; s < hi; s += blockDim.x)
-    if (pred(keyr[s], keyp[s])) cand[o++] = s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (bits & (1u << j)) cand[o++] = s0 + j;
 }
 
 __device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
