@@ -7,7 +7,8 @@ delta = rho = 1), pre-populated with ~4 queued requests per client from a
 Poisson process of 2M req/s; each step adds the next 64K arrivals
 (tag updates) and then makes up to 64K pull_request(now) decisions at the
 step's last arrival time.  Inputs of every step are resident in HBM before
-the timed region; each step runs dmc_add_batch_device + dmc_pull_batch_device.
+the timed region; each step runs dmc_add_pull_batch_device (= dmc_add_batch_device
++ dmc_pull_batch_device, fused into one graph launch; --separate-calls for two).
 
 metric = BASELINE.json metric: dispatch decisions/s + tag updates/s, whole job.
 With --gpus N each rank runs its own server queue (dmClock servers are
@@ -80,7 +81,10 @@ def parse():
                          "steady state with both phases")
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=30)
+    ap.add_argument("--separate-calls", action="store_true",
+                    help="dmc_add_batch_device + dmc_pull_batch_device per step "
+                         "instead of dmc_add_pull_batch_device")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the second, stage-timed pass")
@@ -202,9 +206,12 @@ def main():
     torch.cuda.synchronize()
 
     def step(i):
-        q.add_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr())
-        q.pull_batch_device(nows[i], k, d_out.data_ptr(),
-                            d_res[i].data_ptr())
+        if args.separate_calls:
+            q.add_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr())
+            q.pull_batch_device(nows[i], k, d_out.data_ptr(), d_res[i].data_ptr())
+        else:  # the same two operations, one graph launch
+            q.add_pull_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr(),
+                                    nows[i], k, d_out.data_ptr(), d_res[i].data_ptr())
 
     for i in range(args.warmup):
         step(i)

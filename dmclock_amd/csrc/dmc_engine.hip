@@ -709,6 +709,8 @@ struct GraphRec {
   hipGraphExec_t exec = nullptr;
   hipGraphNode_t param_node = nullptr;
   hipKernelNodeParams kp{};
+  hipGraphNode_t param_node2 = nullptr;  // fused add + pull: the round's k_rscan
+  hipKernelNodeParams kp2{};
 };
 
 struct dmc_queue {
@@ -857,18 +859,24 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
-int graph_replay(dmc_queue* q, GraphRec& g, void** args) {
+int graph_replay(dmc_queue* q, GraphRec& g, void** args, void** args2 = nullptr) {
   hipKernelNodeParams kp = g.kp;
   kp.kernelParams = args;
   kp.extra = nullptr;
   HIP_OK(hipGraphExecKernelNodeSetParams(g.exec, g.param_node, &kp));
+  if (args2) {
+    hipKernelNodeParams kp2 = g.kp2;
+    kp2.kernelParams = args2;
+    kp2.extra = nullptr;
+    HIP_OK(hipGraphExecKernelNodeSetParams(g.exec, g.param_node2, &kp2));
+  }
   HIP_OK(hipGraphLaunch(g.exec, q->stream));
   return DMC_OK;
 }
 
 // Capture `enqueue` (which must start with the parameter kernel) as a graph.
 template <typename F>
-int graph_capture(dmc_queue* q, GraphRec& g, F enqueue) {
+int graph_capture(dmc_queue* q, GraphRec& g, F enqueue, const void* func2 = nullptr) {
   HIP_OK(hipStreamBeginCapture(q->stream, hipStreamCaptureModeThreadLocal));
   enqueue();
   hipGraph_t graph = nullptr;
@@ -888,6 +896,28 @@ int graph_capture(dmc_queue* q, GraphRec& g, F enqueue) {
     return DMC_EDEVICE;
   }
   HIP_OK(hipGraphKernelNodeGetParams(root, &g.kp));
+  if (func2) {  // the second parameter node: the kernel node running func2
+    size_t nn = 0;
+    HIP_OK(hipGraphGetNodes(graph, nullptr, &nn));
+    std::vector<hipGraphNode_t> nodes(nn);
+    HIP_OK(hipGraphGetNodes(graph, nodes.data(), &nn));
+    for (auto nd : nodes) {
+      hipGraphNodeType t2;
+      HIP_OK(hipGraphNodeGetType(nd, &t2));
+      if (t2 != hipGraphNodeTypeKernel) continue;
+      hipKernelNodeParams kp{};
+      HIP_OK(hipGraphKernelNodeGetParams(nd, &kp));
+      if (kp.func == func2) {
+        g.param_node2 = nd;
+        g.kp2 = kp;
+        break;
+      }
+    }
+    if (!g.param_node2) {
+      (void)hipGraphDestroy(graph);
+      return DMC_EDEVICE;
+    }
+  }
   HIP_OK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
   g.graph = graph;
   g.param_node = root;
@@ -903,7 +933,7 @@ void graph_destroy(GraphRec& g) {
 // Find (or, on the second sighting, build) the graph for `key`; nullptr if the
 // caller should launch eagerly this time.
 template <typename F>
-GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
+GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = nullptr) {
   // stage timers run eagerly: event-record nodes inside a replayed graph do
   // not bracket the kernels they were captured between
   if (!q->use_graphs || q->prof_on) return nullptr;
@@ -922,7 +952,7 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue) {
   for (auto& g : q->graphs)
     if (!g.exec || g.last_use < slot->last_use) slot = &g;
   graph_destroy(*slot);
-  if (graph_capture(q, *slot, enqueue) != DMC_OK) {
+  if (graph_capture(q, *slot, enqueue, func2) != DMC_OK) {
     graph_destroy(*slot);
     q->use_graphs = false;  // capture unsupported: stay eager
     return nullptr;
@@ -1265,7 +1295,7 @@ int wait_round(dmc_queue* q, uint64_t seq) {
 // *dev_wrote says so.
 int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
               dmc_pull_result* res, dmc_pull_result* d_result = nullptr,
-              bool* dev_wrote = nullptr) {
+              bool* dev_wrote = nullptr, bool pre_launched = false) {
   if (dev_wrote) *dev_wrote = false;
   bool first_round = true;
   dmc_pull_result r{};
@@ -1278,7 +1308,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       break;
     }
     uint32_t kk = k - n_dec;
-    if (kk <= q->small_k) {
+    if (kk <= q->small_k && !pre_launched) {
       int type;
       double when;
       int rc = step_once(q, now, d_out, n_dec, &type, &when);
@@ -1293,15 +1323,21 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       continue;
     }
     bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
-    if (q->radix_batches) --q->radix_batches;
-    if (radix) {
-      int rc = ensure_entries(q, q->dense_hint);
-      if (rc) return rc;
-    }
     // the first round of a call may end it: its k_rfinish writes d_result
     dmc_pull_result* dres = (first_round && n_dec == 0) ? d_result : nullptr;
-    int rc = launch_round(q, now, kk, d_out + n_dec, dres, radix, !allow);
-    if (rc) return rc;
+    int rc = DMC_OK;
+    if (pre_launched) {  // the fused add + pull graph launched this round
+      pre_launched = false;
+      radix = false;
+    } else {
+      if (q->radix_batches) --q->radix_batches;
+      if (radix) {
+        rc = ensure_entries(q, q->dense_hint);
+        if (rc) return rc;
+      }
+      rc = launch_round(q, now, kk, d_out + n_dec, dres, radix, !allow);
+      if (rc) return rc;
+    }
     // one host round trip per round, through host-mapped memory
     rc = wait_round(q, q->round_seq);
     if (rc) return rc;
@@ -1789,6 +1825,59 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
     HIP_OK(hipGetLastError());
   }
   return DMC_OK;
+}
+
+// add_batch followed by pull_batch(now, k), both device-resident: one graph
+// launch for the add kernels and the first pull round when nothing needs the
+// host in between (no idle client to activate, a batched bin-ranked round),
+// otherwise exactly the two calls.
+int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
+                              int32_t* d_rc_out, double now, uint32_t k,
+                              dmc_decision* d_out, dmc_pull_result* d_result) {
+  if (!q || (n && (!d_reqs || !d_rc_out)) || (k && !d_out)) return DMC_EINVAL;
+  bool fuse;
+  {
+    QueueLock g(q);
+    fuse = n && k && q->n_idle == 0 && q->n_registered > 0 && k > q->small_k &&
+           !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
+           q->use_graphs && !q->prof_on;
+    if (fuse) {
+      int rc = ensure_batch(q, n);
+      if (rc) return rc;
+      const bool future = q->p.at_limit != DMC_AT_LIMIT_ALLOW;
+      AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
+      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq};
+      auto enqueue = [&] {
+        enqueue_add(q, ap);
+        enqueue_round(q, cp, false, future);
+      };
+      uint64_t key = (4ull << 56) | ((uint64_t)n << 1) | (future ? 1 : 0);
+      GraphRec* gr = graph_for(q, key, enqueue, (const void*)k_rscan);
+      if (!gr) {
+        enqueue();
+        HIP_OK(hipGetLastError());
+      } else {
+        Table tb = q->tb;
+        void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk};
+        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->rparts, &q->rd, &cp};
+        int rc = graph_replay(q, *gr, a1, a2);
+        if (rc) return rc;
+      }
+      q->tick += n;
+      dmc_pull_result r{};
+      bool dev_wrote = false;
+      rc = pull_impl(q, now, k, d_out, &r, d_result, &dev_wrote, true);
+      if (rc) return rc;
+      if (d_result && !dev_wrote) {
+        hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, d_result, r);
+        HIP_OK(hipGetLastError());
+      }
+      return DMC_OK;
+    }
+  }
+  int rc = dmc_add_batch_device(q, n, d_reqs, d_rc_out);
+  if (rc) return rc;
+  return dmc_pull_batch_device(q, now, k, d_out, d_result);
 }
 
 int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,

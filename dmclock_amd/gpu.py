@@ -45,6 +45,7 @@ EXPORTS = {
     "dmc_add_batch_device": (_i32, [_vp, _u32, _vp, _vp]),
     "dmc_pull_batch": (_i32, [_vp, _f64, _u32, _vp, ctypes.POINTER(PullResult)]),
     "dmc_pull_batch_device": (_i32, [_vp, _f64, _u32, _vp, _vp]),
+    "dmc_add_pull_batch_device": (_i32, [_vp, _u32, _vp, _vp, _f64, _u32, _vp, _vp]),
     "dmc_remove_by_client": (_i32, [_vp, _u32, _i32, _vp, _u32,
                                     ctypes.POINTER(_u32)]),
     "dmc_client_requests": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
@@ -240,6 +241,14 @@ class GpuQueue:
     def pull_batch_device(self, now, k, d_out_ptr, d_res_ptr=None):
         _check(self.L.dmc_pull_batch_device(self.h, float(now), k, d_out_ptr,
                                             d_res_ptr), "pull_batch_device")
+
+    def add_pull_batch_device(self, d_reqs_ptr, n, d_rc_ptr, now, k, d_out_ptr,
+                              d_res_ptr=None):
+        """add_batch_device then pull_batch_device(now, k), fused into one
+        graph launch when possible"""
+        _check(self.L.dmc_add_pull_batch_device(self.h, n, d_reqs_ptr, d_rc_ptr,
+                                                float(now), k, d_out_ptr, d_res_ptr),
+               "add_pull_batch_device")
 
     def stream(self):
         return self.L.dmc_queue_stream(self.h)

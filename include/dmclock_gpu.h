@@ -195,6 +195,14 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                    dmc_pull_result* result);
 int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
                           dmc_decision* d_out, dmc_pull_result* d_result);
+/* dmc_add_batch_device then dmc_pull_batch_device(now, k): the same results
+ * as the two calls (the reference's add_request_time x n then
+ * pull_request(now) x k, :1344-1489).  When no idle client must be
+ * activated and the pull is one batched round, the add kernels and that round
+ * run as one graph launch. */
+int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
+                              int32_t* d_rc, double now, uint32_t k,
+                              dmc_decision* d_out, dmc_pull_result* d_result);
 
 /* ------------------------------------------------------------ maintenance */
 

@@ -29,10 +29,29 @@ def _mk(variant, **kw):
     return q
 
 
+def _res(d_res):
+    return PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+
+
+def _check_pull(qh, now, k, d_out, d_res):
+    dh, rh = qh.pull_batch(now, k)
+    rd = _res(d_res)
+    dd = d_out.cpu().numpy().view(DECISION_DTYPE)[:rd.n_decisions]
+    assert (rd.n_decisions, rd.next_type) == (rh.n_decisions, rh.next_type)
+    if rh.next_type == 1:
+        assert rd.when == rh.when
+    assert np.array_equal(dd, dh)
+    n_res = int((dh["phase"] == 0).sum())
+    assert (rd.n_reservation, rd.n_priority) == (n_res, len(dh) - n_res)
+    assert (rh.n_reservation, rh.n_priority) == (n_res, len(dh) - n_res)
+    return rd.next_type
+
+
+@pytest.mark.parametrize("api", ["separate", "fused"])
 @pytest.mark.parametrize("variant", ["default", "radix", "steps", "eager"])
 @pytest.mark.parametrize("at_limit", [AT_LIMIT_WAIT, AT_LIMIT_ALLOW],
                          ids=["wait", "allow"])
-def test_device_api_matches_host_api(variant, at_limit):
+def test_device_api_matches_host_api(variant, at_limit, api):
     import torch
     n = 400
     tr = workloads.steady_trace(7, n, 10, 300, 0, depth=2, delta_rho="random",
@@ -43,33 +62,39 @@ def test_device_api_matches_host_api(variant, at_limit):
     for q in (qh, qd):
         q.register(c.slots, c.r, c.w, c.l, c.active)
     dev = torch.device("cuda", 0)
-    res_sz = 24
     kinds = set()
-    for op in tr.ops:
+    ops = list(tr.ops)
+    i = 0
+    while i < len(ops):
+        op = ops[i]
         if op[0] == "add":
             reqs = op[1]
             rc_h = qh.add_batch(reqs)
             d_reqs = torch.from_numpy(reqs.view(np.uint8).copy()).to(dev)
             d_rc = torch.full((len(reqs),), -7, dtype=torch.int32, device=dev)
+            if api == "fused" and i + 1 < len(ops) and ops[i + 1][0] == "pull":
+                _, now, k = ops[i + 1]
+                d_out = torch.zeros(max(k, 1) * DECISION_DTYPE.itemsize,
+                                    dtype=torch.uint8, device=dev)
+                d_res = torch.full((24,), 0xAB, dtype=torch.uint8, device=dev)
+                qd.add_pull_batch_device(d_reqs.data_ptr(), len(reqs), d_rc.data_ptr(),
+                                         now, k, d_out.data_ptr(), d_res.data_ptr())
+                qd.sync()
+                assert np.array_equal(d_rc.cpu().numpy(), rc_h)
+                kinds.add(_check_pull(qh, now, k, d_out, d_res))
+                i += 2
+                continue
             qd.add_batch_device(d_reqs.data_ptr(), len(reqs), d_rc.data_ptr())
             qd.sync()
             assert np.array_equal(d_rc.cpu().numpy(), rc_h)
+            i += 1
             continue
         _, now, k = op
-        dh, rh = qh.pull_batch(now, k)
         d_out = torch.zeros(max(k, 1) * DECISION_DTYPE.itemsize, dtype=torch.uint8,
                             device=dev)
-        d_res = torch.full((res_sz,), 0xAB, dtype=torch.uint8, device=dev)
+        d_res = torch.full((24,), 0xAB, dtype=torch.uint8, device=dev)
         qd.pull_batch_device(now, k, d_out.data_ptr(), d_res.data_ptr())
         qd.sync()
-        rd = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
-        dd = d_out.cpu().numpy().view(DECISION_DTYPE)[:rd.n_decisions]
-        assert (rd.n_decisions, rd.next_type) == (rh.n_decisions, rh.next_type)
-        if rh.next_type == 1:
-            assert rd.when == rh.when
-        assert np.array_equal(dd, dh)
-        n_res = int((dh["phase"] == 0).sum())
-        assert (rd.n_reservation, rd.n_priority) == (n_res, len(dh) - n_res)
-        assert (rh.n_reservation, rh.n_priority) == (n_res, len(dh) - n_res)
-        kinds.add(rd.next_type)
+        kinds.add(_check_pull(qh, now, k, d_out, d_res))
+        i += 1
     assert 0 in kinds  # some pulls returned k decisions

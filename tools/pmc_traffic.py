@@ -16,7 +16,7 @@ from collections import defaultdict
 
 STAGES = {
     "scan": ["k_rscan"],
-    "select": ["k_rhist"],
+    "select": ["k_rhist", "k_rpick"],
     "emit": ["k_rcand", "k_remit"],
     "rank": ["k_rbscan", "k_rrank"],
     "apply": ["k_rapply"],
