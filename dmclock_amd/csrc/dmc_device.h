@@ -20,6 +20,8 @@ namespace dmc {
 
 constexpr double kInf = __builtin_huge_val();
 constexpr uint64_t kMaxKey = ~0ull;
+// ReqEntry::dec of a request no pull round has dispatched (set at add)
+constexpr uint32_t kNoDec = 0xffffffffu;
 
 enum : uint8_t { F_IDLE = 1, F_READY = 2, F_REG = 4 };
 
@@ -29,7 +31,7 @@ struct alignas(16) ReqEntry {
   double r, p, l, arrival;
   uint64_t handle;
   uint32_t cost, delta, rho;
-  uint32_t dec;  // pull round scratch: decision offset of this pop
+  uint32_t dec;  // pull round stamp: decision offset of this pop (kNoDec: none)
   uint32_t tie;  // pull round scratch: tie flag of this pop
   uint32_t pad;
 };
@@ -178,11 +180,12 @@ struct NullVisit {
 // Immediate mode reads stored tags; Delayed mode recomputes each new front
 // with update_next_tag (:1021-1036).  `limit` bounds the pops (apply mode).
 // Returns the number of pops; leaves the final prev tag in *prev (delayed).
+// `stamped` (apply): walk exactly the entries the ranking stamped.
 template <typename V>
 __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
                                   double now, uint64_t T, uint32_t limit, V& vis,
                                   Tag3* prev_io, Tag3* front_out,
-                                  uint32_t* front_cost) {
+                                  uint32_t* front_cost, bool stamped = false) {
   const uint32_t h = cv.h, c = cv.c;
   uint32_t n = 0;
   if (c == 0) return 0;
@@ -192,7 +195,7 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
     ReqEntry e = ring[h & tb.qmask];
     ReqEntry nx = ring[(h + 1) & tb.qmask];
     while (n < c && n < limit) {
-      if (!(e.r <= now) || okey(e.r) > T) break;
+      if (!(e.r <= now) || okey(e.r) > T || (stamped && e.dec == kNoDec)) break;
       vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false, e.dec,
               e.tie);
       ++n;
@@ -211,7 +214,7 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
   uint32_t cur_cost = e0.cost, cur_dec = e0.dec, cur_tie = e0.tie;
   uint64_t cur_h = e0.handle;
   while (n < c && n < limit) {
-    if (!(cur.r <= now) || okey(cur.r) > T) break;
+    if (!(cur.r <= now) || okey(cur.r) > T || (stamped && cur_dec == kNoDec)) break;
     vis.pop(n, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
     ++n;
     if (n < c) {
@@ -273,12 +276,16 @@ __device__ inline double reduced_r(const ReqEntry* ring, uint32_t h,
 // walk_r front, used iff use_start_tag), `ready0` its ready flag (only the
 // untouched front can carry one: a front exposed by a reservation pop is ready
 // iff limit <= now).
+// `kstamp` != 0 (apply, kstamp = the round's k): walk exactly the groups the
+// ranking stamped; a group stamped at decision offset o keeps at most
+// kstamp - o pops (the round's last group can be cut inside its run).
 template <typename V>
 __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
                                double now, uint64_t T, uint32_t limit, V& vis,
                                Tag3* prev_io, Tag3* front_out,
                                uint32_t* front_cost, uint32_t start,
-                               Tag3 start_tag, bool use_start_tag, bool ready0) {
+                               Tag3 start_tag, bool use_start_tag, bool ready0,
+                               uint32_t kstamp = 0) {
   WalkP w{0, 0, 0};
   const uint32_t h = cv.h, c = cv.c;
   if (start >= c) return w;
@@ -291,7 +298,8 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
       bool rdy = (i == start) ? (ready0 || e.l <= now) : (e.l <= now);
       if (!rdy || !(e.p < kInf)) break;
       uint64_t key = okey(__dadd_rn(e.p, pdv));
-      if (key > T) break;
+      if (key > T || (kstamp && e.dec == kNoDec)) break;
+      const uint32_t glim = kstamp ? kstamp - e.dec : 0xffffffffu;  // pops in group
       double r_now = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
       vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true, e.dec,
               e.tie);
@@ -299,7 +307,7 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
       ++i;
       ++w.pops;
       uint32_t run = 0;
-      while (i < c && w.pops < limit) {
+      while (i < c && w.pops < limit && run + 1 < glim) {
         double ri = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
         if (!(ri <= now)) break;
         const ReqEntry er = ring[(h + i) & tb.qmask];
@@ -358,12 +366,13 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
     bool rdy = (i == start) ? (ready0 || cur.l <= now) : (cur.l <= now);
     if (!rdy || !(cur.p < kInf)) break;
     uint64_t key = okey(__dadd_rn(cur.p, pdv));
-    if (key > T) break;
+    if (key > T || (kstamp && cur_dec == kNoDec)) break;
+    const uint32_t glim = kstamp ? kstamp - cur_dec : 0xffffffffu;  // pops in group
     vis.pop(i, cur, cur_cost, cur_h, true, cur_dec, cur_tie);
     advance(true);
     ++w.pops;
     uint32_t run = 0;
-    while (i < c && w.pops < limit) {
+    while (i < c && w.pops < limit && run + 1 < glim) {
       if (!(cur.r <= now)) break;
       vis.pop(i, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
       advance(false);

@@ -246,7 +246,7 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   e.cost = rq.cost;
   e.delta = (tb.delayed && st.count > 0) ? 0u : rq.delta;
   e.rho = (tb.delayed && st.count > 0) ? 0u : rq.rho;
-  e.dec = 0;
+  e.dec = kNoDec;
   e.tie = 0;
   e.pad = 0;
   ring[(st.head + st.count) & tb.qmask] = e;
@@ -724,7 +724,6 @@ struct dmc_queue {
   uint32_t n_idle = 0;
   uint64_t tick = 0;
   // device scratch
-  uint32_t* applied = nullptr;// N: pops dispatched this round (R | P << 16)
   uint32_t* cand = nullptr;   // N: candidate slots of the round
   uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
   uint8_t* mr = nullptr;      // N: R prefix length
@@ -1197,15 +1196,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcount, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
-    if (getenv("DMC_DEBUG_RANK2"))
-      hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
-                         q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
-                         (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
-                         q->applied, 1);
     hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
                        q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
                        (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
-                       q->applied, 0, q->debug ? q->dbg_wtime : nullptr);
+                       q->debug ? q->dbg_wtime : nullptr);
     pe(q);
   } else {
     uint32_t E = q->ecap;
@@ -1234,14 +1228,13 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
     hipLaunchKernelGGL(k_ddecide, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E,
                        (const uint32_t*)q->sval, (const DEnt*)q->dense,
                        (const uint32_t*)q->gsz, (const uint32_t*)q->goff,
-                       (const uint32_t*)q->gpoff, tb.ring, q->applied);
+                       (const uint32_t*)q->gpoff, tb.ring);
     pe(q);
   }
   pb(q, DMC_PROF_APPLY);
   hipLaunchKernelGGL(k_rapply, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
-                     (const uint32_t*)q->cand, (const uint64_t*)q->keyr,
-                     (const uint64_t*)q->keyp, q->applied, q->bcount, q->bsize,
-                     q->sched, q->debug ? q->dbg_atime : nullptr);
+                     (const uint32_t*)q->cand, q->bcount, q->bsize, q->sched,
+                     q->debug ? q->dbg_atime : nullptr);
   pe(q);
   if (future)
     launch_future(q);  // its decide kernel ends the round
@@ -1463,7 +1456,6 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&t.rec, N); rc |= A(&t.qs, N);
   rc |= A(&t.fr, N); rc |= A(&t.flags, N);
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
-  rc |= A(&q->applied, N);
   rc |= A(&q->cand, N);
   rc |= A(&q->keyr, N);
   rc |= A(&q->keyp, N);
@@ -1524,7 +1516,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   Table& t = q->tb;
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
-                  q->applied, q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
+                  q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
                   q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,

@@ -32,7 +32,7 @@
 //   k_rcand   compacts the candidate slots, settles the others' pending marks
 //   k_remit   candidates enumerate their entries into rank bins
 //   k_rbscan  one block: prefix sums of the rank-bin sizes, decision count
-//   k_rrank   one block per rank bin: rank in LDS, decide, count applied pops
+//   k_rrank   one block per rank bin: rank in LDS, decide, stamp the ring entries
 //   k_rapply  replays each candidate's dispatched pops with the same
 //             arithmetic, writes the decision records and the new state
 //   k_rfinish round summary to host-mapped memory (folded into the terminal
@@ -761,8 +761,8 @@ k_remit(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
 // sizes (1 for R pops, 1 + run for P groups) of all earlier bins plus those
 // of its own bin that precede it.  Each block first sums the counts and sizes
 // of all earlier bins.  Decides: entry ids slot * q + position get their
-// decision offset (eoff) and tie flag; applied[slot] counts the dispatched
-// pops (low 16 bits R, high 16 bits P).
+// decision offset (eoff) and tie flag, stamped into the ring entry (the
+// priority pop's entry for a P group).
 // one block: exclusive prefixes over the rank bins of the entry counts, the
 // group sizes and the P-group counts; the round's decision count and
 // terminal flag.  A rank bin past kBinCapR aborts the round (overflow = 2).
@@ -871,7 +871,7 @@ constexpr int kRankBlocksR = kNBR;
 __global__ void __launch_bounds__(kBlockR)
 k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
         const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
-        uint32_t* applied, int dry = 0, uint64_t* wtime = nullptr) {
+        uint64_t* wtime = nullptr) {
   __shared__ BRecR sh[kBinCapR];
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
@@ -913,13 +913,9 @@ k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
   if (valid && part == 0) {
     uint32_t goff = soff + gl;
     uint32_t size = isp ? 1u + me.run : 1u;
-    if (dry) {
-      if (rank == 0xffffffffu) applied[0] = gl;  // keep the work alive
-    } else if (goff < k) {
-      ring[me.ridx].dec = goff;
+    if (goff < k) {
+      ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
       ring[me.ridx].tie = tie;
-      uint32_t na = size < k - goff ? size : k - goff;
-      atomicAdd(&applied[me.slot], isp ? na << 16 : na);
       if (isp) {
         uint32_t prank = poff + rank;  // among P groups
         if (goff + size >= k || prank == n_pgroups - 1) {
@@ -1036,7 +1032,7 @@ __device__ inline bool dtie_at(const DEnt* dense, const uint32_t* sval,
 __global__ void k_ddecide(Round* rd, uint32_t dcap, const uint32_t* sval,
                           const DEnt* dense, const uint32_t* gsz,
                           const uint32_t* goff, const uint32_t* gp,
-                          ReqEntry* ring, uint32_t* applied) {
+                          ReqEntry* ring) {
   if (rd->overflow || rd->dense_n > dcap) return;
   uint32_t n = rd->dense_n, k = rd->k_total;
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1060,9 +1056,6 @@ __global__ void k_ddecide(Round* rd, uint32_t dcap, const uint32_t* sval,
     if (o < k) {
       ring[d.ridx].dec = o;
       ring[d.ridx].tie = dtie_at(dense, sval, n, pos) ? 1 : 0;
-      uint32_t na = gsz[pos];
-      if (na > k - o) na = k - o;
-      atomicAdd(&applied[d.slot], isp ? na << 16 : na);
       if (isp && (pos == n - 1 || goff[pos + 1] >= k)) {
         rd->g_last = o;
         rd->n_prio = gp[pos] + 1;  // exclusive P count before + this one
@@ -1143,21 +1136,18 @@ struct RoundC {
   uint64_t tick;
   dmc_decision* out;
   uint32_t g_last, terminal;
+  uint32_t k;
   bool p_runs, ovf;
 };
 
-__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
-                                 uint32_t* applied) {
+__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) {
   // every load that depends only on the slot is issued before the first
   // branch: one memory round trip for all of them
-  const uint32_t a = applied[s];
   const uint8_t f0 = tb.flags[s];
   const CView cv = load_view(tb, s);
   Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
-  if (a) applied[s] = 0;
-  if (!a || rc.ovf) {
-    if (f0 & F_PMARK)
-      tb.flags[s] = (uint8_t)((f0 & ~F_PMARK) | (rc.p_runs && !rc.ovf ? F_READY : 0));
+  if (rc.ovf) {
+    if (f0 & F_PMARK) tb.flags[s] = (uint8_t)(f0 & ~F_PMARK);
     return;
   }
   const double now = rc.now;
@@ -1165,7 +1155,6 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
   const uint32_t g_last = rc.g_last;
   const uint32_t terminal = rc.terminal;
   const bool p_runs = rc.p_runs;
-  uint32_t aR = a & 0xffffu, aP = a >> 16;
   const uint32_t c = cv.c, h = cv.h;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s};
@@ -1173,19 +1162,26 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
   uint32_t fcost = 0;
   uint32_t popsR = 0, popsP = 0;
   uint64_t pmask = 0;
-  if (aR) {
+  // exactly the pops the ranking stamped: the R prefix's, then the P groups'
+  {
     ApplyVR vr{&v};
-    popsR = walk_r(tb, s, cv, now, kMaxKey, aR, vr, &prev, &front, &fcost);
+    popsR = walk_r(tb, s, cv, now, kMaxKey, 0xffffffffu, vr, &prev, &front, &fcost,
+                   true);
   }
-  if (aP) {
+  if (p_runs) {
     ApplyVP vp{&v};
     bool ready0 = popsR == 0 && (f0 & F_READY);
-    WalkP w = walk_p(tb, s, cv, now, kMaxKey, aP, vp, &prev, &front, &fcost, popsR,
-                     front, popsR && tb.delayed, ready0);
+    WalkP w = walk_p(tb, s, cv, now, kMaxKey, 0xffffffffu, vp, &prev, &front, &fcost,
+                     popsR, front, popsR && tb.delayed, ready0, rc.k);
     popsP = w.pops;
     pmask = w.pmask;
   }
   uint32_t pops = popsR + popsP;
+  if (pops == 0) {  // a candidate none of whose entries was dispatched
+    if (f0 & F_PMARK)
+      tb.flags[s] = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
+    return;
+  }
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
   if (!tb.delayed) {
     if (pmask) {
@@ -1246,8 +1242,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
 // (Non-candidates settled their pending marks in k_rcand.)  Block 0 also counts the round's decisions (sched[0] reservation,
 // sched[1] priority, :1469,1479) and resets the rank-bin counters.
 __global__ void __launch_bounds__(kBlockR, 5)
-k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
-         const uint64_t* keyp, uint32_t* applied, uint32_t* bcount,
+k_rapply(Table tb, Round* rd, const uint32_t* cand, uint32_t* bcount,
          uint32_t* bsize, unsigned long long* sched, uint64_t* dbg = nullptr) {
   if (blockIdx.x == 0) {
     for (int b = threadIdx.x; b < kNBR; b += blockDim.x) {
@@ -1262,11 +1257,11 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
   const uint32_t nc = rd->n_cand;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  const RoundC rc{rd->now, rd->tick, rd->out, rd->g_last, rd->terminal,
+  const RoundC rc{rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
                   rd->p_runs != 0, rd->overflow != 0};
   for (uint32_t ci = tid; ci < nc; ci += stride) {
     uint64_t t0 = dbg ? wall_clock64() : 0;
-    apply_one(tb, rc, cand[ci], applied);
+    apply_one(tb, rc, cand[ci]);
     if (dbg && ci < 262144) {
       dbg[2 * ci] = t0;
       dbg[2 * ci + 1] = wall_clock64();
