@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-steps", type=int, default=30)
+    ap.add_argument("--cpu-sub", type=int, default=None,
+                    help="config 4: only the first CPU_SUB requests (and pulls) "
+                         "of each CPU-baseline step (default: all)")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -94,10 +97,17 @@ def parse():
                          "region, on the following batches)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles",
                                                       "traffic_r01.json"))
-    ap.add_argument("--config", type=int, default=3, choices=(3, 5),
-                    help="3: one server queue (default); 5: multi-server "
+    ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5),
+                    help="3: one server queue (default); 4: config 3 with "
+                         "idle/active churn (do_clean idle marking before "
+                         "every step, activations with the prop_delta reset) "
+                         "and 10%% limit-throttled tenants; 5: multi-server "
                          "dmClock, --servers queues per GPU with device client "
                          "trackers and a per-epoch all-reduce")
+    ap.add_argument("--idle-frac", type=float, default=0.10,
+                    help="config 4: fraction of the clients marked idle before "
+                         "each step, drawn from those without an arrival in "
+                         "the previous two steps")
     ap.add_argument("--servers", type=int, default=8,
                     help="config 5: server queues per GPU")
     ap.add_argument("--epoch-steps", type=int, default=16,
@@ -114,6 +124,10 @@ def make_workload(args, seed):
     rng = np.random.default_rng(seed)
     n = args.clients
     tab = workloads.client_table(rng, n)
+    if args.config == 4:
+        # 10 % of the tenants limited below their arrival rate (2 req/s each)
+        thr = rng.random(n) < 0.10
+        tab.l = np.where(thr, rng.uniform(0.5, 1.5, n), tab.l)
     rate = 2.0 * n
     pre = workloads.arrivals(rng, n, args.depth * n, 1.0, rate)
     t = float(pre["time"][-1])
@@ -125,7 +139,25 @@ def make_workload(args, seed):
         handle += args.batch
         t = float(reqs["time"][-1])
         steps.append(reqs)
-    return tab, pre, steps
+    idle = None
+    if args.config == 4:
+        # do_clean's idle pass before each step (:1230-1250): clients without
+        # an arrival in the two previous batches, a random idle_frac of all
+        idle = []
+        last = np.full(n, -1, np.int64)
+        is_idle = np.zeros(n, bool)
+        args.activations = []
+        for i, reqs in enumerate(steps):
+            quiet = np.flatnonzero(last < i - 2)
+            m = min(len(quiet), int(args.idle_frac * n))
+            sel = np.sort(rng.choice(quiet, m, replace=False)).astype(np.uint32)
+            idle.append(sel)
+            is_idle[sel] = True
+            u = np.unique(reqs["slot"])
+            args.activations.append(int(is_idle[u].sum()))  # first arrivals of idle clients
+            is_idle[u] = False
+            last[reqs["slot"]] = i
+    return tab, pre, steps, idle
 
 
 def prepare(q, args, tab, pre):
@@ -149,7 +181,7 @@ def prepare(q, args, tab, pre):
     return settle
 
 
-def cpu_baseline(args, tab, pre, steps):
+def cpu_baseline(args, tab, pre, steps, idle=None):
     """The oracle (CPU restatement of the reference queue, one core) on a
     bounded sample of the same workload: same 1M clients and pre-population,
     timed over --cpu-steps steps."""
@@ -160,16 +192,28 @@ def cpu_baseline(args, tab, pre, steps):
     k = args.pulls or args.batch
     ops = 0
     t0 = time.perf_counter()
-    for reqs in steps[:args.cpu_steps]:
+    for i, reqs in enumerate(steps[:args.cpu_steps]):
+        kk = k
+        if idle is not None:
+            # config 4: every activation scans all clients (O(N), SURVEY
+            # finding 4): a bounded prefix of the step
+            for c in idle[i].tolist():
+                q.mark_idle(c)
+            if args.cpu_sub:
+                reqs = reqs[:args.cpu_sub]
+                kk = args.cpu_sub
         q.add_batch(reqs)
-        d, res = q.pull_batch(float(reqs["time"][-1]), k)
+        d, res = q.pull_batch(float(reqs["time"][-1]), kk)
         ops += len(reqs) + res.n_decisions
     dt = time.perf_counter() - t0
     return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
             "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
                        f"the same {args.clients}-client queue after the same "
                        f"pre-population and settle, {args.cpu_steps} steps of "
-                       f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+                       + (f"{args.batch} adds + {k} pulls" if args.config != 4 else
+                          f"idle marking + {args.cpu_sub or args.batch} adds + "
+                          f"{args.cpu_sub or k} pulls")
+                       + f", {dt:.2f} s")}
 
 
 def main():
@@ -189,7 +233,7 @@ def main():
     from dmclock_amd.gpu import GpuQueue
     from dmclock_amd._abi import DECISION_DTYPE, PullResult
 
-    tab, pre, steps = make_workload(args, args.seed + rank)
+    tab, pre, steps, idle = make_workload(args, args.seed + rank)
     k = args.pulls or args.batch
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
                  max_batch=max(args.batch, k, 1 << 20), device=local)
@@ -206,6 +250,8 @@ def main():
     torch.cuda.synchronize()
 
     def step(i):
+        if idle is not None:
+            q.mark_idle_batch(idle[i])
         if args.separate_calls:
             q.add_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr())
             q.pull_batch_device(nows[i], k, d_out.data_ptr(), d_res[i].data_ptr())
@@ -305,7 +351,8 @@ def main():
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(args, tab, pre, steps[args.warmup:])
+        cpu = cpu_baseline(args, tab, pre, steps[args.warmup:],
+                           None if idle is None else idle[args.warmup:])
 
     ms_step = dt / args.steps * 1e3
     out = {
@@ -321,15 +368,22 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "config3: single server queue, synthetic 1M "
-                               "clients mixed r/w/l, 64K adds + 64K pulls "
-                               "per step",
+        "config": {"workload": ("config3: single server queue, synthetic 1M "
+                                "clients mixed r/w/l, 64K adds + 64K pulls "
+                                "per step") if args.config == 3 else
+                               ("config4: config 3 + do_clean idle marking of "
+                                f"{args.idle_frac:.0%} of the clients before each "
+                                "step (activations with the prop_delta reset) "
+                                "+ 10% limit-throttled tenants"),
                    "clients": args.clients, "adds_per_step": args.batch,
                    "pulls_per_step": k, "prepopulated": len(pre),
                    "settle_pulls": settle,
                    "ring_capacity": args.ring,
                    "parallelism": f"{world} independent server queue(s)"},
         "decisions_per_s": round(n_dec / dt, 1),
+        "activations_per_step": (None if args.config != 4 else
+                                 round(float(np.mean(args.activations[args.warmup:
+                                       args.warmup + args.steps])), 1)),
         "tag_updates_per_s": round(n_adds / dt, 1),
         "reservation_decisions": int(st.reserv_sched_count - st_t0.reserv_sched_count),
         "priority_decisions": int(st.prop_sched_count - st_t0.prop_sched_count),

@@ -1619,6 +1619,43 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   return DMC_OK;
 }
 
+__global__ void k_mark_idle(Table tb, uint32_t n, const uint32_t* slots) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tb.flags[slots[i]] |= F_IDLE;
+}
+
+int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) {
+  if (!q || (n && !slots)) return DMC_EINVAL;
+  QueueLock g(q);
+  std::vector<uint32_t> mark;
+  mark.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = slots[i];
+    if (s >= q->p.max_clients) return DMC_EINVAL;
+    if (!q->reg_h[s]) return DMC_ENOTREG;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = slots[i];
+    if (!q->idle_h[s]) {
+      q->idle_h[s] = 1;
+      ++q->n_idle;
+      mark.push_back(s);
+    }
+  }
+  if (mark.empty()) return DMC_OK;
+  uint32_t m = (uint32_t)mark.size();
+  uint32_t* d_slots;
+  HIP_OK(hipMallocAsync((void**)&d_slots, 4ull * m, q->stream));
+  HIP_OK(hipMemcpyAsync(d_slots, mark.data(), 4ull * m, hipMemcpyHostToDevice,
+                        q->stream));
+  hipLaunchKernelGGL(k_mark_idle, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, m, (const uint32_t*)d_slots);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipFreeAsync(d_slots, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));  // the host vector is freed on return
+  return DMC_OK;
+}
+
 static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
                         uint32_t* head) {
   QState qs;

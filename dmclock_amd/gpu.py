@@ -38,6 +38,7 @@ EXPORTS = {
     "dmc_client_register_batch": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _i32]),
     "dmc_client_update_info": (_i32, [_vp, _u32, _f64, _f64, _f64]),
     "dmc_client_mark_idle": (_i32, [_vp, _u32]),
+    "dmc_client_mark_idle_batch": (_i32, [_vp, _u32, _vp]),
     "dmc_client_erase": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
     "dmc_client_get_state": (_i32, [_vp, _u32, ctypes.POINTER(ClientState)]),
     "dmc_client_last_ticks": (_i32, [_vp, _u32, _vp]),
@@ -342,6 +343,11 @@ class GpuQueue:
                 _check(self.L.dmc_client_filter(self.h, self.slot_of[c],
                                                 len(hs), _ptr(keep)), "filter")
         return any_removed
+
+    def mark_idle_batch(self, slots):
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        _check(self.L.dmc_client_mark_idle_batch(self.h, len(slots), _ptr(slots)),
+               "mark_idle_batch")
 
     def mark_idle(self, client):
         _check(self.L.dmc_client_mark_idle(self.h, self.slot_of[client]),

@@ -174,6 +174,9 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double reservation,
  * :1206-1255): mark_idle sets idle=true; erase drops the client and its
  * queued requests (their handles are written to handles_out, capacity cap). */
 int dmc_client_mark_idle(dmc_queue* q, uint32_t slot);
+/* The same for n registered clients (do_clean's idle pass over a client
+ * set, :1230-1250); slots in host memory. */
+int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots);
 int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out);
 int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* out);
