@@ -84,7 +84,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=30)
     ap.add_argument("--cpu-sub", type=int, default=None,
                     help="config 4: only the first CPU_SUB requests (and pulls) "
-                         "of each CPU-baseline step (default: all)")
+                         "of each CPU-baseline step (default 4096)")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -199,9 +199,9 @@ def cpu_baseline(args, tab, pre, steps, idle=None):
             # finding 4): a bounded prefix of the step
             for c in idle[i].tolist():
                 q.mark_idle(c)
-            if args.cpu_sub:
-                reqs = reqs[:args.cpu_sub]
-                kk = args.cpu_sub
+            sub = args.cpu_sub or 4096  # activations are O(N) each on the CPU
+            reqs = reqs[:sub]
+            kk = sub
         q.add_batch(reqs)
         d, res = q.pull_batch(float(reqs["time"][-1]), kk)
         ops += len(reqs) + res.n_decisions
@@ -211,8 +211,8 @@ def cpu_baseline(args, tab, pre, steps, idle=None):
                        f"the same {args.clients}-client queue after the same "
                        f"pre-population and settle, {args.cpu_steps} steps of "
                        + (f"{args.batch} adds + {k} pulls" if args.config != 4 else
-                          f"idle marking + {args.cpu_sub or args.batch} adds + "
-                          f"{args.cpu_sub or k} pulls")
+                          f"idle marking + the first {args.cpu_sub or 4096} "
+                          f"adds + as many pulls")
                        + f", {dt:.2f} s")}
 
 

@@ -32,6 +32,7 @@ NEXT_NONE = 2
 OPT_SMALL_K = 1
 OPT_FORCE_RADIX = 2
 OPT_GRAPHS = 3
+OPT_ACT_SPLIT = 4
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0

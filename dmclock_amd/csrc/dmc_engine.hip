@@ -86,6 +86,10 @@ __device__ inline uint64_t shfl_u64(uint64_t v, int src) {
   uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
+  uint32_t lo = __shfl_up((uint32_t)v, d), hi = __shfl_up((uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline uint64_t shfl_down_u64(uint64_t v, int d) {
   uint32_t lo = __shfl_down((uint32_t)v, d), hi = __shfl_down((uint32_t)(v >> 32), d);
   return ((uint64_t)hi << 32) | lo;
@@ -166,15 +170,38 @@ struct AddParams {
   uint32_t pad;
 };
 
+// Batched activations (the idle reset of every idle client's first request
+// in one batch, resolved on the device; see k_act_resolve).  Per batch
+// position: the proportion contribution (ordered key) a non-idle client with
+// an empty queue had before its first accepted request there (cold, stored
+// at index n - 1 - position) and has after it (cnew); at an activation position the post-add proportion basis
+// (actp: front p if the client has a request, else prev p).
+struct ActBuf {
+  uint64_t* cold;
+  uint64_t* cnew;
+  double* actp;
+  uint64_t* pre;     // exclusive prefix minima of cnew
+  uint64_t* suf;     // exclusive prefix minima of cold (reversed): suffix minima
+  const uint32_t* idx;  // activation positions, ascending
+  uint32_t m;
+  const uint64_t* parts;  // k_act_base partials
+  uint32_t nparts;
+  uint64_t* extra;   // contributions of touched empty clients left unchanged
+};
+
 // The first node of an add segment: its arguments are the segment's per-call
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
 __global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
                            uint32_t* abuf, uint32_t* apos, uint32_t* aslot,
-                           AddParams* pblk) {
+                           AddParams* pblk, ActBuf act = ActBuf{}) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *pblk = p;
   if (i >= p.n) return;
+  if (act.cold) {
+    act.cold[i] = kMaxKey;
+    act.cnew[i] = kMaxKey;
+  }
   uint32_t s = p.reqs[i].slot;
   aslot[i] = s;
   if (s >= tb.n) {
@@ -263,7 +290,7 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
 
 __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
                             const uint32_t* abuf, const uint32_t* apos,
-                            const uint32_t* aslot) {
+                            const uint32_t* aslot, ActBuf act = ActBuf{}) {
   const AddParams p = *pblk;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
@@ -298,8 +325,31 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
   st.flags = tb.flags[s];
   st.front_set = false;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  // batched activations: this client's contribution to the idle reset before
+  // and after its requests (see ActBuf)
+  const bool idle0 = (st.flags & F_IDLE) != 0;
+  const uint32_t count0 = st.count;
+  const double pd = act.cold ? tb.fr[s].pd : 0.0;
+  const double front_p0 = (act.cold && count0) ? tb.fr[s].p : 0.0;
+  const double prev_p0 = st.prev.p;
+  bool act_done = false, chg_done = false;
+  auto step = [&](uint32_t pos) {
+    add_one(tb, st, ring, p, pos);
+    if (!act.cold) return;
+    if (idle0) {
+      const dmc_request& rq = p.reqs[pos];
+      if (!act_done && rq.rho <= rq.delta) {  // the activating request
+        act_done = true;
+        act.actp[pos] = st.count ? (count0 ? front_p0 : st.front.p) : st.prev.p;
+      }
+    } else if (count0 == 0 && !chg_done && st.count) {
+      chg_done = true;
+      act.cold[p.n - 1 - pos] = okey(__dadd_rn(prev_p0, pd));  // reversed order
+      act.cnew[pos] = okey(__dadd_rn(st.front.p, pd));
+    }
+  };
   if (m == 1) {
-    add_one(tb, st, ring, p, i);
+    step(i);
   } else if (m <= kAddSlots) {
     // the client's batch positions in ascending order, by repeated selection
     // over its (L2-resident) slot-buffer row
@@ -311,13 +361,16 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
         uint32_t v = row[k];
         if ((j == 0 || v > last) && v < next) next = v;
       }
-      add_one(tb, st, ring, p, next);
+      step(next);
       last = next;
     }
   } else {
     for (uint32_t j = 0; j < p.n; ++j)
-      if (aslot[j] == s) add_one(tb, st, ring, p, j);
+      if (aslot[j] == s) step(j);
   }
+  if (act.cold && !idle0 && count0 == 0 && !chg_done)  // nothing accepted
+    atomicMin((unsigned long long*)act.extra,
+              (unsigned long long)okey(__dadd_rn(prev_p0, pd)));
   tb.rec[s].prev_r = st.prev.r;
   tb.rec[s].prev_p = st.prev.p;
   tb.rec[s].prev_l = st.prev.l;
@@ -380,6 +433,219 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
   }
   if (lowest < trigger) tb.fr[s].pd = __dsub_rn(lowest, t);
   tb.flags[s] &= (uint8_t)~F_IDLE;
+}
+
+// Batched activations, step 1 (after k_add_link, before k_add_chain): the
+// idle reset's minimum over the clients whose contribution the batch does
+// not change: registered, non-idle, and not (empty and touched by the batch).
+__global__ void k_act_base(Table tb, const uint32_t* acnt, uint64_t* parts) {
+  uint64_t m = kMaxKey;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    uint8_t f = tb.flags[s];
+    if ((f & F_REG) && !(f & F_IDLE)) {
+      uint32_t c = tb.qs[s].count;
+      if (c == 0 && acnt[s]) continue;  // changes inside the batch: positions
+      double p = c ? tb.fr[s].p : tb.rec[s].prev_p;
+      uint64_t k = okey(__dadd_rn(p, tb.fr[s].pd));
+      m = k < m ? k : m;
+    }
+  }
+  m = wave_min_u64(m);
+  __shared__ uint64_t sh[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x / 64); ++i) m = sh[i] < m ? sh[i] : m;
+    parts[blockIdx.x] = m;
+  }
+}
+
+constexpr int kActThreads = 1024;
+
+struct MinKey {
+  __host__ __device__ uint64_t operator()(uint64_t a, uint64_t b) const {
+    return a < b ? a : b;
+  }
+};
+
+// block-wide inclusive min-scan of one value per thread (u64 ordered keys)
+__device__ inline uint64_t block_incl_min(uint64_t v, uint64_t* wpart) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t o = shfl_up_u64(v, d);
+    if (lane >= d && o < v) v = o;
+  }
+  if (lane == 63) wpart[w] = v;
+  __syncthreads();
+  uint64_t b = kMaxKey;
+  for (int i = 0; i < w; ++i) b = wpart[i] < b ? wpart[i] : b;
+  __syncthreads();
+  return b < v ? b : v;
+}
+
+// the idle reset's value for minimum key x (:957-969): lowest_prop_tag starts
+// at DBL_MAX and takes x if smaller; prop_delta = lowest - t iff below the
+// trigger, else unchanged
+__device__ inline double act_pd(uint64_t x, double t, double pd_old) {
+  constexpr double trigger = 1.7976931348623157e308 / 3.0;
+  double lowest = 1.7976931348623157e308;
+  if (x != kMaxKey) {
+    double L = from_okey(x);
+    if (L < lowest) lowest = L;
+  }
+  return lowest < trigger ? __dsub_rn(lowest, t) : pd_old;
+}
+
+// Batched activations, step 2 (after k_add_chain and two min-scans over the
+// batch positions: pre = exclusive prefix minima of cnew, sufr = exclusive
+// prefix minima of cold in reversed position order, i.e. suffix minima).
+// The idle reset of the k-th activating request (batch position q_k, time
+// t_k) is L_k = min over the clients non-idle at that moment of their
+// contribution: unchanged clients (k_act_base), touched empty clients before
+// their first accepted request (cold at positions > q_k) or after it (cnew
+// at positions < q_k), and the clients activated earlier in the batch
+// (M_{k-1} = min_{j<k} p_j + pd_j, pd_j = L_j - t_j).  This kernel gathers
+// each activation's inputs (one thread per activation).
+__global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
+                             uint64_t* ax, double* ap, double* at, double* apd,
+                             uint32_t* aslot) {
+  const AddParams p = *pblk;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < act.m;
+       k += gridDim.x * blockDim.x) {
+    uint32_t q = act.idx[k];
+    uint64_t a = act.pre[q], b = act.suf[p.n - 1 - q];
+    ax[k] = a < b ? a : b;
+    const dmc_request& rq = p.reqs[q];
+    ap[k] = act.actp[q];
+    at[k] = rq.time;
+    aslot[k] = rq.slot;
+    apd[k] = tb.fr[rq.slot].pd;
+  }
+}
+
+// Step 3 (one block): only the M term is sequential.  Every L_k is first
+// taken as X_k = min(unchanged, pre, suf), which is exact as long as
+// M_{k-1} >= X_k for all k (checked chunk by chunk); from the first k where
+// an earlier activation undercuts (an idle client whose old front tag lies
+// behind the clock contributes below the reset it got) the recurrence runs
+// on one thread over LDS-staged inputs.
+__global__ void __launch_bounds__(kActThreads)
+k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
+              const double* at, const double* apd, const uint32_t* aslot) {
+  __shared__ uint64_t wpart[kActThreads / 64];
+  __shared__ uint64_t s_base, s_carry, s_minpre;
+  __shared__ uint32_t s_fail;
+  __shared__ uint64_t sv[kActThreads];
+  const uint32_t t = threadIdx.x, m = act.m;
+  uint64_t b = kMaxKey;
+  for (uint32_t i = t; i < act.nparts; i += kActThreads) b = act.parts[i] < b ? act.parts[i] : b;
+  b = block_incl_min(b, wpart);
+  if (t == kActThreads - 1) {
+    uint64_t e = *act.extra;
+    s_base = e < b ? e : b;
+    s_carry = kMaxKey;  // M over the activations handled so far
+    s_fail = 0xffffffffu;
+  }
+  __syncthreads();
+  const uint64_t base = s_base;
+  uint32_t k0 = 0;
+  // speculative: L_k = X_k
+  for (; k0 < m; k0 += kActThreads) {
+    const uint32_t k = k0 + t;
+    const bool in = k < m;
+    uint64_t x = kMaxKey, c = kMaxKey;
+    double pd = 0.0;
+    if (in) {
+      x = ax[k] < base ? ax[k] : base;
+      pd = act_pd(x, at[k], apd[k]);
+      c = okey(__dadd_rn(ap[k], pd));
+    }
+    const uint64_t incl = block_incl_min(c, wpart);
+    sv[t] = incl;
+    __syncthreads();
+    const uint64_t carry = s_carry;
+    uint64_t mprev = t ? sv[t - 1] : kMaxKey;
+    mprev = carry < mprev ? carry : mprev;
+    if (in && mprev < x) atomicMin(&s_fail, k);
+    __syncthreads();
+    const uint32_t fail = s_fail;
+    if (in && k < fail) {
+      tb.fr[aslot[k]].pd = pd;
+      tb.flags[aslot[k]] &= (uint8_t)~F_IDLE;
+    }
+    if (fail != 0xffffffffu) {
+      if (fail > k0 && t == fail - k0 - 1) s_minpre = incl;
+      break;
+    }
+    if (t == kActThreads - 1) s_carry = carry < incl ? carry : incl;
+    __syncthreads();
+  }
+  __syncthreads();
+  const uint32_t fail = s_fail;
+  if (fail != 0xffffffffu) {
+    // the recurrence in doubles (okey order is the double order): a short
+    // dependent chain of min / compare / sub / add per activation
+    __shared__ double cx[kActThreads], cp[kActThreads], ct[kActThreads],
+        cpd[kActThreads];
+    __shared__ double s_M;
+    if (t == 0) {
+      uint64_t M = s_carry;
+      if (fail > k0) M = s_minpre < M ? s_minpre : M;
+      s_M = M == kMaxKey ? kInf : from_okey(M);
+    }
+    __syncthreads();
+    for (uint32_t c0 = fail; c0 < m; c0 += kActThreads) {
+      const uint32_t k = c0 + t;
+      if (k < m) {
+        uint64_t x = ax[k] < base ? ax[k] : base;
+        cx[t] = x == kMaxKey ? kInf : from_okey(x);
+        cp[t] = ap[k];
+        ct[t] = at[k];
+        cpd[t] = apd[k];
+      }
+      __syncthreads();
+      if (t == 0) {
+        constexpr double dmax = 1.7976931348623157e308;  // :960
+        constexpr double trigger = dmax / 3.0;            // :957
+        double M = s_M;
+        const uint32_t e = m - c0 < (uint32_t)kActThreads ? m - c0 : kActThreads;
+        for (uint32_t j0 = 0; j0 < e; j0 += 8) {
+          double rx[8], rp[8], rt[8], rpd[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            uint32_t j = j0 + u < e ? j0 + u : e - 1;
+            rx[u] = cx[j];
+            rp[u] = cp[j];
+            rt[u] = ct[j];
+            rpd[u] = cpd[j];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (j0 + u < e) {
+              double L = M < rx[u] ? M : rx[u];
+              double lowest = L < dmax ? L : dmax;
+              double pd = lowest < trigger ? __dsub_rn(lowest, rt[u]) : rpd[u];
+              rpd[u] = pd;
+              double c = __dadd_rn(rp[u], pd);
+              M = c < M ? c : M;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (j0 + u < e) cpd[j0 + u] = rpd[u];
+        }
+        s_M = M;
+      }
+      __syncthreads();
+      if (k < m) {
+        tb.fr[aslot[k]].pd = cpd[t];
+        tb.flags[aslot[k]] &= (uint8_t)~F_IDLE;
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) *act.extra = kMaxKey;  // ready for the next batch
 }
 
 // ------------------------------------------------------------------ future
@@ -743,6 +1009,17 @@ struct dmc_queue {
   StepCtl* sctl = nullptr;
   StepCtl* h_sctl = nullptr;  // pinned
   uint64_t* act_min = nullptr;
+  // batched activations (k_act_base / k_act_resolve), grown on demand
+  uint32_t acap = 0;
+  uint64_t *act_cold = nullptr, *act_cnew = nullptr, *act_pre = nullptr,
+           *act_suf = nullptr, *act_extra = nullptr, *act_parts = nullptr;
+  double* act_p = nullptr;
+  uint32_t* act_idx = nullptr;
+  uint64_t* act_x = nullptr;   // per activation: X_k without the unchanged term
+  double *act_ip = nullptr, *act_it = nullptr, *act_ipd = nullptr;
+  uint32_t* act_islot = nullptr;
+  uint32_t* h_act = nullptr;  // pinned staging of the activation positions
+  bool act_split = false;     // DMC_OPT_ACT_SPLIT: one host split per activation
   unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
   unsigned long long* reqcount = nullptr;
   // radix path (grown on demand)
@@ -1063,7 +1340,8 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
     return DMC_OK;
   }
   Table tb = q->tb;
-  void* args[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk};
+  ActBuf noact{};
+  void* args[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk, &noact};
   return graph_replay(q, *g, args);
 }
 
@@ -1099,6 +1377,112 @@ int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
     start = i;
   }
   return add_segment(q, d_reqs + start, n - start, d_rc + start, tick0 + start);
+}
+
+int ensure_act(dmc_queue* q, uint32_t n) {
+  if (n <= q->acap) return DMC_OK;
+  uint32_t cap = std::max<uint32_t>(n, 4096);
+  dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
+  dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
+  dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot);
+  if (q->h_act) (void)hipHostFree(q->h_act);
+  q->h_act = nullptr;
+  HIP_OK(hipMalloc(&q->act_cold, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_cnew, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_pre, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_suf, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_p, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_idx, 4ull * cap));
+  HIP_OK(hipMalloc(&q->act_x, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_ip, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_it, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_ipd, 8ull * cap));
+  HIP_OK(hipMalloc(&q->act_islot, 4ull * cap));
+  HIP_OK(hipHostMalloc((void**)&q->h_act, 4ull * cap, 0));
+  {
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveScan(nullptr, tb, q->act_cnew, q->act_pre,
+                                            MinKey{}, kMaxKey, (int)cap, q->stream);
+    int rc = ensure_temp(q, tb);
+    if (rc) return rc;
+  }
+  if (!q->act_extra) {
+    HIP_OK(hipMalloc(&q->act_extra, 8));
+    const uint64_t mx = kMaxKey;
+    HIP_OK(hipMemcpyAsync(q->act_extra, &mx, 8, hipMemcpyHostToDevice, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+  }
+  if (!q->act_parts) HIP_OK(hipMalloc(&q->act_parts, 8ull * 2048));
+  q->acap = cap;
+  return DMC_OK;
+}
+
+// A batch with activations in one pass (AtLimit Wait / Allow): the host only
+// finds the activating requests (to keep its idle mirror); the idle resets
+// are resolved on the device by k_act_base + k_add_chain's bookkeeping +
+// k_act_resolve, exactly as a sequential replay would compute them.
+int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
+                  const dmc_request* d_reqs, int32_t* d_rc) {
+  int rc = ensure_act(q, n);
+  if (rc) return rc;
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = h_reqs[i].slot;
+    if (s < q->p.max_clients && q->reg_h[s] && q->idle_h[s] &&
+        h_reqs[i].rho <= h_reqs[i].delta) {
+      q->h_act[m++] = i;
+      q->idle_h[s] = 0;
+      --q->n_idle;
+    }
+  }
+  if (m == 0) return add_segment(q, d_reqs, n, d_rc, q->tick);
+  HIP_OK(hipMemcpyAsync(q->act_idx, q->h_act, 4ull * m, hipMemcpyHostToDevice,
+                        q->stream));
+  prof_gate(q);
+  const uint32_t gb = grid_for(q->tb.n, 2048);
+  ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
+             q->act_idx, m, q->act_parts, gb, q->act_extra};
+  AddParams ap{d_reqs, d_rc, q->tick, n, 0};
+  uint32_t g = (n + kBlock - 1) / kBlock;
+  pb(q, DMC_PROF_ADD_LINK);
+  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
+                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk, act);
+  pe(q);
+  pb(q, DMC_PROF_ACTIVATE);
+  hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
+                     (const uint32_t*)q->acnt, q->act_parts);
+  pe(q);
+  pb(q, DMC_PROF_ADD_CHAIN);
+  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
+  pe(q);
+  pb(q, DMC_PROF_ACTIVATE);
+  size_t tbytes = q->temp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cnew, q->act_pre,
+                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  tbytes = q->temp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cold, q->act_suf,
+                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(m, 1024)), dim3(kBlock), 0, q->stream,
+                     (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
+                     q->act_it, q->act_ipd, q->act_islot);
+  hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
+                     act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
+                     (const double*)q->act_it, (const double*)q->act_ipd,
+                     (const uint32_t*)q->act_islot);
+  pe(q);
+  HIP_OK(hipGetLastError());
+  // the pinned staging is reused by the next batch: wait for the copy
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
+                  const dmc_request* d_reqs, int32_t* d_rc) {
+  if (q->act_split || q->p.at_limit == DMC_AT_LIMIT_REJECT)
+    return add_host_split(q, h_reqs, n, d_reqs, d_rc);
+  return add_act_batch(q, h_reqs, n, d_reqs, d_rc);
 }
 
 // --------------------------------------------------------------- pull rounds
@@ -1525,6 +1909,10 @@ int dmc_queue_destroy(dmc_queue* q) {
   for (void* p : ptrs)
     dfree(p);
   if (q->h_round) (void)hipHostFree(q->h_round);
+  if (q->h_act) (void)hipHostFree(q->h_act);
+  dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
+  dfree(q->act_p); dfree(q->act_idx); dfree(q->act_extra); dfree(q->act_parts);
+  dfree(q->act_x); dfree(q->act_ip); dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot);
   if (q->h_sctl) (void)hipHostFree(q->h_sctl);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
@@ -1790,7 +2178,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(q->d_reqs, reqs, sizeof(dmc_request) * n,
                         hipMemcpyHostToDevice, q->stream));
-  rc = q->n_idle ? add_host_split(q, reqs, n, q->d_reqs, q->d_rc)
+  rc = q->n_idle ? add_with_idle(q, reqs, n, q->d_reqs, q->d_rc)
                  : add_segment(q, q->d_reqs, n, q->d_rc, q->tick);
   if (rc) return rc;
   q->tick += n;
@@ -1814,7 +2202,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
     HIP_OK(hipMemcpyAsync(h.data(), d_reqs, sizeof(dmc_request) * n,
                           hipMemcpyDeviceToHost, q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
-    rc = add_host_split(q, h.data(), n, d_reqs, d_rc_out);
+    rc = add_with_idle(q, h.data(), n, d_reqs, d_rc_out);
   } else {
     rc = add_segment(q, d_reqs, n, d_rc_out, q->tick);
   }
@@ -1887,7 +2275,9 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         HIP_OK(hipGetLastError());
       } else {
         Table tb = q->tb;
-        void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk};
+        ActBuf noact{};
+        void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk,
+                      &noact};
         void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->rparts, &q->rd, &cp};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
@@ -2038,6 +2428,9 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
     case DMC_OPT_GRAPHS:
       q->use_graphs = value != 0;
       if (!q->use_graphs) invalidate_graphs(q);
+      return DMC_OK;
+    case DMC_OPT_ACT_SPLIT:
+      q->act_split = value != 0;
       return DMC_OK;
     default:
       return DMC_EINVAL;

@@ -265,6 +265,8 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
 #define DMC_OPT_SMALL_K 1
 #define DMC_OPT_FORCE_RADIX 2
 #define DMC_OPT_GRAPHS 3       /* 0: launch every kernel eagerly (default 1: replay captured hipGraphs) */
+#define DMC_OPT_ACT_SPLIT 4    /* 1: resolve each activation's idle reset by splitting the batch on the
+                                  host (default 0: all of a batch's activations on the device) */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
 /* ------------------------------------------------------------ profiling

@@ -175,3 +175,84 @@ def test_bench_shaped_parity(variant):
     n, qg, qo = run_parity(tr, mk_variant(variant),
                            dict(at_limit=AT_LIMIT_WAIT), state_sample=256)
     assert n > 100000
+
+
+# ------------------------------------------------ batched activations
+MODES_ACT = [dict(at_limit=AT_LIMIT_WAIT), dict(at_limit=AT_LIMIT_WAIT, delayed=True),
+             dict(at_limit=AT_LIMIT_ALLOW)]
+
+
+def mk_act(split):
+    from dmclock_amd._abi import OPT_ACT_SPLIT
+
+    def mk(**kw):
+        q = mk_gpu(**kw)
+        q.set_option(OPT_ACT_SPLIT, int(split))
+        return q
+    return mk
+
+
+@pytest.mark.parametrize("mode", MODES_ACT, ids=["imm", "delayed", "allow"])
+@pytest.mark.parametrize("seed", [3, 11, 19])
+def test_churn_activations_parity(mode, seed):
+    """Many activations per batch (a third of the clients idle before every
+    step): the device-resolved idle resets equal the sequential ones (the
+    host split, one activation at a time) in every decision and every
+    client's state; and both equal the oracle when its run is tie-free
+    (activations align proportion keys, p + L - t, so ties are frequent and
+    then the heap's history picks)."""
+    from parity import compare_decisions, compare_states
+    tr = workloads.churn_trace(seed, 400, 8, 600, 300, idle_frac=0.35,
+                               k_choices=[1, 9, 64, 300, 2000])
+    qa = mk_act(0)(max_clients=400, **mode)
+    qb = mk_act(1)(max_clients=400, **mode)
+    oa, ob = workloads.replay(qa, tr), workloads.replay(qb, tr)
+    for i, (a, b) in enumerate(zip(oa, ob)):
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), i
+        elif a[0] == "pull":
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], i
+    compare_states(qa, qb, np.arange(400), "final")
+    import pyoracle
+    qo = pyoracle.OracleQueue(**mode)
+    workloads.replay(qo, tr)
+    if qo.ties == 0:
+        run_parity(tr, mk_act(0), mode, state_sample=400)
+
+
+def test_activation_undercut_by_earlier_activation():
+    """An activated client's contribution undercuts the minimum a later
+    activation sees once the former minimum client gets its first request
+    (k_act_resolve's sequential fallback)."""
+    from dmclock_amd._abi import make_requests
+    n = 30
+    slots = np.arange(n, dtype=np.uint32)
+    r = np.zeros(n)
+    w = np.linspace(0.6, 1.4, n)
+    l = np.zeros(n)
+    tr = workloads.Trace(workloads.ClientTable(slots, r, w, l, True))
+    # clients 1..9 queued (contributions ~ their tags); client 0 empty with
+    # prev p = 0: the initial minimum
+    tr.ops.append(("add", make_requests(np.arange(1, 10), 1.0 + 0.01 * np.arange(9),
+                                        handles=np.arange(9))))
+    tr.ops.append(("idle", np.arange(10, 30, dtype=np.uint32)))
+    order = [10, 0, 11, 12, 0, 13, 14, 15, 16, 17, 18, 19, 20]
+    times = 2.0 + 0.1 * np.arange(len(order))
+    tr.ops.append(("add", make_requests(order, times, handles=100 + np.arange(len(order)))))
+    tr.ops.append(("pull", 5.0, 40))
+    tr.ops.append(("add", make_requests(np.arange(20, 30), 6.0 + 0.03 * np.arange(10),
+                                        handles=200 + np.arange(10))))
+    tr.ops.append(("pull", 20.0, 100))
+    # activations align keys (ties): device vs one-at-a-time host split
+    from parity import compare_decisions, compare_states
+    qa = mk_act(0)(max_clients=n, at_limit=AT_LIMIT_WAIT)
+    qb = mk_act(1)(max_clients=n, at_limit=AT_LIMIT_WAIT)
+    oa, ob = workloads.replay(qa, tr), workloads.replay(qb, tr)
+    for i, (a, b) in enumerate(zip(oa, ob)):
+        if a[0] == "pull":
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], i
+        elif a[0] == "add":
+            assert np.array_equal(a[1], b[1]), i
+    compare_states(qa, qb, slots, "final")
