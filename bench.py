@@ -82,9 +82,8 @@ def parse():
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-steps", type=int, default=30)
-    ap.add_argument("--cpu-sub", type=int, default=None,
-                    help="config 4: only the first CPU_SUB requests (and pulls) "
-                         "of each CPU-baseline step (default 4096)")
+    ap.add_argument("--cpu-budget", type=float, default=20.0,
+                    help="config 4: seconds of oracle work in the CPU sample")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -191,29 +190,62 @@ def cpu_baseline(args, tab, pre, steps, idle=None):
     prepare(q, args, tab, pre)
     k = args.pulls or args.batch
     ops = 0
+    if idle is not None:
+        return cpu_baseline_churn(args, q, steps, idle)
     t0 = time.perf_counter()
     for i, reqs in enumerate(steps[:args.cpu_steps]):
-        kk = k
-        if idle is not None:
-            # config 4: every activation scans all clients (O(N), SURVEY
-            # finding 4): a bounded prefix of the step
-            for c in idle[i].tolist():
-                q.mark_idle(c)
-            sub = args.cpu_sub or 4096  # activations are O(N) each on the CPU
-            reqs = reqs[:sub]
-            kk = sub
         q.add_batch(reqs)
-        d, res = q.pull_batch(float(reqs["time"][-1]), kk)
+        d, res = q.pull_batch(float(reqs["time"][-1]), k)
         ops += len(reqs) + res.n_decisions
     dt = time.perf_counter() - t0
     return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
             "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
                        f"the same {args.clients}-client queue after the same "
                        f"pre-population and settle, {args.cpu_steps} steps of "
-                       + (f"{args.batch} adds + {k} pulls" if args.config != 4 else
-                          f"idle marking + the first {args.cpu_sub or 4096} "
-                          f"adds + as many pulls")
-                       + f", {dt:.2f} s")}
+                       f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+
+
+def cpu_baseline_churn(args, q, steps, idle):
+    """Config 4 on the oracle: every activation scans all clients (O(N),
+    SURVEY finding 4), so the sample is the first step's idle marking and
+    then its adds in chunks of 256, each followed by as many pulls, until
+    --cpu-budget seconds have passed."""
+    budget = args.cpu_budget
+    ops = acts = 0
+    i0 = next((i for i, s in enumerate(idle) if len(s)), 0)
+    t0 = time.perf_counter()
+    for c in idle[i0].tolist():
+        q.mark_idle(c)
+    reqs = steps[i0]
+    idle_set = np.zeros(args.clients, bool)
+    idle_set[idle[i0]] = True
+    n_add = 0
+    last = t0
+    for j in range(0, len(reqs), 256):
+        sub = reqs[j:j + 256]
+        u = np.unique(sub["slot"])
+        acts += int(idle_set[u].sum())
+        idle_set[u] = False
+        q.add_batch(sub)
+        d, res = q.pull_batch(float(sub["time"][-1]), len(sub))
+        ops += len(sub) + res.n_decisions
+        n_add += len(sub)
+        now = time.perf_counter()
+        if now - last > 20:
+            print(f"cpu baseline: {n_add} adds, {now - t0:.0f} s", file=sys.stderr,
+                  flush=True)
+            last = now
+        if now - t0 > budget:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
+                       f"the same {args.clients}-client queue after the same "
+                       f"pre-population and settle: a step's idle "
+                       f"marking ({len(idle[i0])} clients), then its first "
+                       f"{n_add} adds ({acts} activations, each an O(N) scan) "
+                       f"in chunks of 256, each followed by as many pulls, "
+                       f"{dt:.2f} s")}
 
 
 def main():

@@ -605,37 +605,33 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
         cpd[t] = apd[k];
       }
       __syncthreads();
-      if (t == 0) {
+      if (t < 64) {
+        // one wave steps the recurrence: with M fixed, every lane evaluates
+        // its activation; the first lane whose contribution undercuts M (a
+        // new minimum) ends the step, lanes up to it commit (their M was
+        // exact), and M takes that lane's value.  The number of steps is the
+        // number of new minima plus e / 64, not e.
         constexpr double dmax = 1.7976931348623157e308;  // :960
         constexpr double trigger = dmax / 3.0;            // :957
         double M = s_M;
         const uint32_t e = m - c0 < (uint32_t)kActThreads ? m - c0 : kActThreads;
-        for (uint32_t j0 = 0; j0 < e; j0 += 8) {
-          double rx[8], rp[8], rt[8], rpd[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            uint32_t j = j0 + u < e ? j0 + u : e - 1;
-            rx[u] = cx[j];
-            rp[u] = cp[j];
-            rt[u] = ct[j];
-            rpd[u] = cpd[j];
+        for (uint32_t j0 = 0; j0 < e;) {
+          const uint32_t j = j0 + t;
+          const bool in = j < e;
+          double pd = 0.0, c = kInf;
+          if (in) {
+            double L = M < cx[j] ? M : cx[j];
+            double lowest = L < dmax ? L : dmax;
+            pd = lowest < trigger ? __dsub_rn(lowest, ct[j]) : cpd[j];
+            c = __dadd_rn(cp[j], pd);
           }
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            if (j0 + u < e) {
-              double L = M < rx[u] ? M : rx[u];
-              double lowest = L < dmax ? L : dmax;
-              double pd = lowest < trigger ? __dsub_rn(lowest, rt[u]) : rpd[u];
-              rpd[u] = pd;
-              double c = __dadd_rn(rp[u], pd);
-              M = c < M ? c : M;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (j0 + u < e) cpd[j0 + u] = rpd[u];
+          const uint64_t rec = __ballot(in && c < M);
+          const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
+          if (in && t <= r) cpd[j] = pd;
+          if (rec) M = __shfl(c, (int)r);
+          j0 += r == 64u ? 64u : r + 1;
         }
-        s_M = M;
+        if (t == 0) s_M = M;
       }
       __syncthreads();
       if (k < m) {

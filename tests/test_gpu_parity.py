@@ -256,3 +256,49 @@ def test_activation_undercut_by_earlier_activation():
         elif a[0] == "add":
             assert np.array_equal(a[1], b[1]), i
     compare_states(qa, qb, slots, "final")
+
+
+@pytest.mark.parametrize("queued_frac", [1.0, 0.5, 0.05])
+def test_activation_records_across_chunks(queued_frac):
+    """Thousands of activations in one batch, across several 1024-entry
+    chunks of k_act_resolve, where every activated client with a queued
+    front behind the clock lowers the running minimum (each one a new
+    minimum for the wave-stepped recurrence; queued_frac = 1 makes every
+    activation one).  Device resolution equals the host split, one
+    activation at a time, in every decision and every client's state."""
+    from dmclock_amd._abi import make_requests
+    from parity import compare_decisions, compare_states
+    rng = np.random.default_rng(7)
+    n = 5000
+    slots = np.arange(n, dtype=np.uint32)
+    r = np.where(rng.random(n) < 0.3, rng.uniform(1, 5, n), 0.0)
+    w = rng.uniform(0.5, 1.5, n)
+    l = np.zeros(n)
+    tr = workloads.Trace(workloads.ClientTable(slots, r, w, l, True))
+    # a base of non-idle clients with queued requests, and idle clients of
+    # which queued_frac hold an old front far behind the later clock
+    base = slots[:200]
+    queued = slots[200:][rng.random(n - 200) < queued_frac]
+    first = np.concatenate([base, queued])
+    tr.ops.append(("add", make_requests(first, 1.0 + 1e-4 * rng.random(len(first)),
+                                        handles=np.arange(len(first)))))
+    tr.ops.append(("idle", slots[200:]))
+    order = rng.permutation(slots[200:])
+    tr.ops.append(("add", make_requests(order, 50.0 + 1e-5 * np.arange(len(order)),
+                                        handles=10000 + np.arange(len(order)))))
+    tr.ops.append(("pull", 60.0, 3000))
+    tr.ops.append(("idle", slots[1000:4000]))
+    order = rng.permutation(slots[1000:4000])
+    tr.ops.append(("add", make_requests(order, 61.0 + 1e-5 * np.arange(len(order)),
+                                        handles=20000 + np.arange(len(order)))))
+    tr.ops.append(("pull", 70.0, 20000))
+    qa = mk_act(0)(max_clients=n, at_limit=AT_LIMIT_WAIT)
+    qb = mk_act(1)(max_clients=n, at_limit=AT_LIMIT_WAIT)
+    oa, ob = workloads.replay(qa, tr), workloads.replay(qb, tr)
+    for i, (a, b) in enumerate(zip(oa, ob)):
+        if a[0] == "pull":
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], i
+        elif a[0] == "add":
+            assert np.array_equal(a[1], b[1]), i
+    compare_states(qa, qb, slots, "final")
