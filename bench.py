@@ -43,9 +43,12 @@ STAGE_BYTES = {
     "scan": (54, 0, 0),
     # k_rhist: keyr + keyp read (its last block: 2 x 2048-bin thresholds)
     "select": (16, 0, 0),
-    # k_remit: keyr + keyp read; per dispatched entry its ring entry 64 read
-    #   and rank record 24 written
-    "emit": (16, 0, 88),
+    # k_rcand: keyr + keyp + flags read per slot; per candidate (about one
+    #   per decision) its slot written to the candidate list
+    "cand": (17, 0, 4),
+    # k_remit: per candidate its slot 4 and keyr + keyp 16 read; per
+    #   dispatched entry its ring entry 64 read and rank record 24 written
+    "emit": (0, 0, 108),
     # k_rrank: rank record 24 read, decision offset + tie 8 written into the
     #   ring entry
     "rank": (0, 0, 32),

@@ -653,11 +653,8 @@ __device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
 // General do_next_request(now) one pull at a time (used for small k and for
 // AtLimit::Allow limit breaks, :1157-1165).  Reductions are per block, then
 // one block combines them.
-__global__ void k_step_scan(Table tb, double now, StepRed* part,
-                            const Round* ctl) {
-  // as the terminal pull of a batch: only if the batch ran out of work
-  if (ctl && (ctl->overflow || !ctl->terminal)) return;
-  if (ctl) now = ctl->now;
+template <int THREADS = kBlock>
+__device__ inline void step_scan_body(const Table& tb, double now, StepRed* part) {
   ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
   uint64_t lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nrd = 0, nnr = 0;
@@ -690,7 +687,7 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
   nany = wave_sum_u32(nany);
   nrd = wave_sum_u32(nrd);
   nnr = wave_sum_u32(nnr);
-  __shared__ StepRed sh[kBlock / 64];
+  __shared__ StepRed sh[THREADS / 64];
   int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     sh[w].r = r;
@@ -705,7 +702,7 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
   __syncthreads();
   if (threadIdx.x == 0) {
     StepRed o = sh[0];
-    for (int i = 1; i < (int)(blockDim.x / 64); ++i) {
+    for (int i = 1; i < THREADS / 64; ++i) {
       o.r = argmin_combine(o.r, sh[i].r);
       o.p = argmin_combine(o.p, sh[i].p);
       o.pnr = argmin_combine(o.pnr, sh[i].pnr);
@@ -717,6 +714,10 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part,
     }
     part[blockIdx.x] = o;
   }
+}
+
+__global__ void k_step_scan(Table tb, double now, StepRed* part) {
+  step_scan_body(tb, now, part);
 }
 
 __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
@@ -732,12 +733,13 @@ __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
 
 // launched with one block of kBlock threads; combines the per-block partials
 // (tree reduction in LDS), then thread 0 decides
+template <int THREADS = kBlock>
 __device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
                             int at_limit, uint32_t nregistered,
                             StepCtl* sc, Round* ctl) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
   if (ctl) now = ctl->now;
-  __shared__ StepRed sh[kBlock];
+  __shared__ StepRed sh[THREADS];
   StepRed acc;
   acc.r = ArgMin{kMaxKey, kNone, 0};
   acc.p = acc.r;
@@ -750,7 +752,7 @@ __device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
     stepred_combine(acc, part[i]);
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int d = blockDim.x / 2; d > 0; d >>= 1) {
+  for (int d = THREADS / 2; d > 0; d >>= 1) {
     if ((int)threadIdx.x < d) stepred_combine(sh[threadIdx.x], sh[threadIdx.x + d]);
     __syncthreads();
   }
@@ -851,6 +853,42 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
     __syncthreads();
     rfinish_body(ctl, h);
   }
+}
+
+// A round's terminal pull in one kernel: one block of kFutThreads per CU
+// scans the table and writes its partial, and the last block to finish (one
+// ticket counter; lane-0 agent-scope release before the ticket, acquire after
+// it: MI355X_MICROARCH.md, inter-workgroup visibility) combines the partials,
+// decides and ends the round.  When the round did not run out of work (the
+// common case) block 0 only ends the round: one kernel boundary per round
+// instead of two.
+constexpr int kFutThreads = 1024;
+constexpr uint32_t kFutBlocks = 256;
+__global__ void __launch_bounds__(kFutThreads)
+k_round_future(Table tb, StepRed* part, int at_limit, uint32_t nregistered,
+               StepCtl* sc, Round* ctl, HostRound* h, uint32_t* done) {
+  if (ctl->overflow || !ctl->terminal) {
+    if (blockIdx.x == 0) rfinish_body(ctl, h);
+    return;
+  }
+  step_scan_body<kFutThreads>(tb, ctl->now, part);  // thread 0 stores the partial
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool last = atomicAdd(done, 1u) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  step_decide<kFutThreads>(gridDim.x, part, 0.0, at_limit, nregistered, sc, ctl);
+  __syncthreads();
+  if (threadIdx.x == 0) *done = 0;  // ready for the next round
+  rfinish_body(ctl, h);
 }
 
 __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
@@ -1003,6 +1041,7 @@ struct dmc_queue {
   BRecR* brec = nullptr;      // kNBR * kBinCapR rank-bin records
   StepRed* red = nullptr;     // step partials (grid) + future record
   StepCtl* sctl = nullptr;
+  uint32_t* fut_done = nullptr;   // k_round_future's block ticket counter
   StepCtl* h_sctl = nullptr;  // pinned
   uint64_t* act_min = nullptr;
   // batched activations (k_act_base / k_act_resolve), grown on demand
@@ -1070,7 +1109,7 @@ namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
     "add_link", "add_chain", "activate", "scan", "select", "emit", "sort",
-    "rank", "apply", "step", "future"};
+    "rank", "apply", "step", "future", "cand"};
 
 // Profiling launches eagerly; a short GPU-side delay queued ahead of a
 // profiled call lets the host enqueue all of the call's kernels before the
@@ -1498,11 +1537,11 @@ uint32_t pow2_at_least(uint32_t x) {
 void launch_future(dmc_queue* q) {
   const double now = 0.0;  // read from the round by the kernels
   pb(q, DMC_PROF_FUTURE);
-  hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     q->tb, now, q->red, (const Round*)q->rd);
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
-                     q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
-                     q->n_registered, q->sctl, q->rd, q->d_hround);
+  (void)now;
+  hipLaunchKernelGGL(k_round_future, dim3(std::min(q->step_grid, kFutBlocks)),
+                     dim3(kFutThreads), 0, q->stream,
+                     q->tb, q->red, q->p.at_limit, q->n_registered, q->sctl, q->rd,
+                     q->d_hround, q->fut_done);
   pe(q);
 }
 
@@ -1512,7 +1551,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   const Table& tb = q->tb;
   pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
-                     tb, now, q->red, (const Round*)nullptr);
+                     tb, now, q->red);
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
                      q->n_registered, q->sctl, (Round*)nullptr, (HostRound*)nullptr);
@@ -1557,10 +1596,12 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   hipLaunchKernelGGL(k_rpick, dim3(2), dim3(kPickThreadsR), 0, q->stream, q->rd,
                      q->hist, q->sbase, q->snum);
   pe(q);
-  pb(q, DMC_PROF_EMIT);
+  pb(q, DMC_PROF_CAND);
   hipLaunchKernelGGL(k_rcand, dim3((N + kCandChunk - 1) / kCandChunk), dim3(kCandThreads), 0, q->stream,
                      tb, q->rd, (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
                      q->cand);
+  pe(q);
+  pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_remit, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
                      (const uint32_t*)q->cand,
                      (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
@@ -1845,6 +1886,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
+  rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
   rc |= A(&q->bcount, kNBR);
@@ -1897,7 +1939,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
                   q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
-                  q->snum, q->red, q->sctl, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->snum, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,

@@ -35,8 +35,9 @@
 //   k_rrank   one block per rank bin: rank in LDS, decide, stamp the ring entries
 //   k_rapply  replays each candidate's dispatched pops with the same
 //             arithmetic, writes the decision records and the new state
-//   k_rfinish round summary to host-mapped memory (folded into the terminal
-//             pull's k_step_decide when the round has one)
+//   k_rfinish round summary to host-mapped memory (AtLimit::Allow; under
+//             Wait / Reject k_round_future ends the round, running the
+//             terminal pull first when the round ran out of work)
 // A rank bin that outgrows kBinCap (massively tied keys) aborts the round
 // (overflow = 2): the host replays it on the radix path (dense entries,
 // 32-bit radix sort + exact fix-up).

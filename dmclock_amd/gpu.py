@@ -64,7 +64,7 @@ EXPORTS = {
                                 ctypes.POINTER(_f64)]),
     "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
-PROF_NSTAGES = 11
+PROF_NSTAGES = 12
 
 
 class DmcError(RuntimeError):

@@ -285,7 +285,8 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 #define DMC_PROF_APPLY 8    /* k_rapply */
 #define DMC_PROF_STEP 9     /* one general pull_request */
 #define DMC_PROF_FUTURE 10  /* a round's terminal pull */
-#define DMC_PROF_NSTAGES 11
+#define DMC_PROF_CAND 11    /* k_rcand */
+#define DMC_PROF_NSTAGES 12
 
 int dmc_profile_enable(dmc_queue* q, int on);
 int dmc_profile_reset(dmc_queue* q);

@@ -17,7 +17,8 @@ from collections import defaultdict
 STAGES = {
     "scan": ["k_rscan"],
     "select": ["k_rhist", "k_rpick"],
-    "emit": ["k_rcand", "k_remit"],
+    "cand": ["k_rcand"],
+    "emit": ["k_remit"],
     "rank": ["k_rbscan", "k_rrank"],
     "apply": ["k_rapply"],
     "add_link": ["k_add_link"],
