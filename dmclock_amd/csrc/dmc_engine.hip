@@ -1779,11 +1779,14 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       std::fprintf(stderr,
                    "dmc round: k=%u n_r=%llu p_runs=%u cand=%u R(elig=%u T=%s) "
                    "P(elig=%u) dec=%u prio=%u bins max R %u P %u sumsq %llu "
-                   "ovf=%u radix=%d\n",
+                   "ovf=%u radix=%d dense=%u pgroups=%u P keys [%.9g, %.9g] T %.9g "
+                   "now %.9g\n",
                    kk, (unsigned long long)c.n_r, c.p_runs, c.n_cand,
                    c.ph[0].n_elig, c.ph[0].T == kMaxKey - 1 ? "all" : "thr",
                    c.ph[1].n_elig, c.n_dec, c.n_prio, c.bin_max[0], c.bin_max[1],
-                   c.bin_sq, c.overflow, (int)radix);
+                   c.bin_sq, c.overflow, (int)radix, c.dense_n, c.n_pgroups,
+                   from_okey(c.ph[1].kmin), from_okey(c.ph[1].kmax),
+                   c.ph[1].T ? from_okey(c.ph[1].T) : 0.0, c.now);
     if (c.overflow == 1) {  // dense entries: grow and retry
       q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
       continue;

@@ -67,8 +67,9 @@ struct PhaseSel {
   uint32_t hshift;      // histogram bin of key k: hist_bin(k, hmin, hshift)
   uint32_t tbin;        // histogram bin holding T (last bin of the table)
   uint32_t pad;
-  uint64_t hmin;        // histogram base
-  uint64_t lo0, hitop;  // key span of the open-ended first / last bin
+  uint64_t hmin;        // histogram base (histogram coordinates, KeyMap)
+  uint64_t lo0, hitop;  // coordinate span of the open-ended first / last bin
+  double vmin, scale;   // the phase's KeyMap (with kmin)
 };
 
 // Histogram range of a phase: base key and bin shift (bins 0 and
@@ -273,7 +274,54 @@ __device__ inline uint32_t hist_shift_r(uint64_t range) {
   return bits > 11 ? bits - 11 : 0;
 }
 
-// histogram bin of a key (bins 0 and kHistBinsR - 1 are open-ended)
+// Histogram coordinate of an ordered key: linear in the key's value over the
+// phase's [kmin, kmax].  Ordered-key offsets are linear in the bit pattern,
+// so a key range that straddles zero or spans binades (the negative
+// proportion keys of activations, :957-969) would pile most keys into a few
+// bins and the threshold would admit most clients.  Monotone non-decreasing
+// in the key (every step rounds monotonically), which is all the selection
+// and the rank bins need.  Used only for such ranges (the value map costs a
+// binary search per threshold and piles the keys near `now` into fewer bins
+// than the bit-pattern map does for a range of a few binades); scale == 0:
+// ordered-key offsets (also for degenerate or non-finite ranges).
+struct KeyMap {
+  uint64_t kmin;
+  double vmin, scale;
+  __device__ KeyMap(uint64_t mn, uint64_t mx) : kmin(mn), vmin(0.0), scale(0.0) {
+    const double a = from_okey(mn), b = from_okey(mx);
+    const double r = __dsub_rn(b, a);
+    const int ea = (int)((dbits(a) >> 52) & 0x7ff), eb = (int)((dbits(b) >> 52) & 0x7ff);
+    const bool wide = (a < 0.0 && b > 0.0) || ea - eb > 12 || eb - ea > 12;
+    if (wide && r > 0.0 && r < kInf) {
+      const double sc = __ddiv_rn(0x1p62, r);
+      if (sc < kInf) {
+        vmin = a;
+        scale = sc;
+      }
+    }
+  }
+  __device__ KeyMap(uint64_t mn, double vm, double sc) : kmin(mn), vmin(vm), scale(sc) {}
+  __device__ uint64_t operator()(uint64_t k) const {
+    if (k <= kmin) return 0;
+    if (scale == 0.0) return k - kmin;
+    const double x = __dmul_rn(__dsub_rn(from_okey(k), vmin), scale);
+    return x < 0x1p63 ? (uint64_t)x : (1ull << 63);
+  }
+  // the largest ordered key in [kmin, kmax] whose coordinate is <= c
+  __device__ uint64_t max_key_at(uint64_t c, uint64_t kmax) const {
+    if ((*this)(kmax) <= c) return kmax;
+    if (scale == 0.0) return kmin + c;  // < kmax here
+    uint64_t lo = kmin, hi = kmax;  // (*this)(lo) <= c < (*this)(hi)
+    while (hi - lo > 1) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if ((*this)(mid) <= c) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+};
+
+// histogram bin of a coordinate (bins 0 and kHistBinsR - 1 are open-ended)
 __device__ inline uint32_t hist_bin(uint64_t k, uint64_t hmin, uint32_t sh) {
   if (k <= hmin) return 0;
   uint64_t b = (k - hmin) >> sh;
@@ -395,14 +443,14 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
     rd->p_runs = p_runs ? 1 : 0;
   }
   if (tot.cnt[0] == 0 && tot.cnt[1] == 0) return;
-  const uint64_t mn0 = tot.mn[0], mn1 = tot.mn[1];
-  const uint32_t sh0 = hist_shift_r(tot.mx[0] - mn0);
-  const uint32_t sh1 = hist_shift_r(tot.mx[1] - mn1);
+  const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
+  const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
+  const uint32_t sh1 = hist_shift_r(m1(tot.mx[1]));
   for (; s < n; s += stride) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(kr[j], mn0, sh0)], 1u);
-      if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(kp[j], mn1, sh1)], 1u);
+      if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(m0(kr[j]), 0, sh0)], 1u);
+      if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(m1(kp[j]), 0, sh1)], 1u);
     }
     if (s + stride < n) load(s + stride);
   }
@@ -437,7 +485,8 @@ __device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
 // T's bin in proportion to their counts (each gets 1 + its share), so that
 // the rank bins stay small however the keys are distributed.
 __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
-                                  const HistRange& hr, Round* rd, uint32_t* hist,
+                                  const KeyMap& km, const HistRange& hr, Round* rd,
+                                  uint32_t* hist,
                                   uint32_t* sbase, uint32_t* snum,
                                   uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
                                   uint64_t* s_T) {
@@ -447,7 +496,7 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
   const uint64_t hmin = hr.hmin;
   uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   if (t == 0) {
-    *s_tb = ne ? hist_bin(tot.mx[p], hmin, sh1) : 0;
+    *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
     *s_C = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
   }
@@ -465,12 +514,14 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       cum += h[j];
       if (cum >= need) {
-        // the bin's upper edge: the same candidate set as its largest key
-        // (the open-ended last bin: the largest key)
+        // the bin's upper edge: the largest key mapped into it, the same
+        // candidate set as its largest key present (the open-ended last
+        // bin: the largest key)
         uint32_t b = t * kBinsPerThreadR + j;
         uint64_t edge = b == kHistBinsR - 1
                             ? tot.mx[p]
-                            : sat_add_u64(hmin, ((uint64_t)(b + 1) << sh1) - 1);
+                            : km.max_key_at(sat_add_u64(hmin, ((uint64_t)(b + 1) << sh1) - 1),
+                                            tot.mx[p]);
         *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : edge;
         *s_tb = b;
         break;
@@ -513,9 +564,12 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     z.hshift = sh1;
     z.tbin = tb;
     z.hmin = hmin;
-    z.lo0 = tot.mn[p] < hmin ? tot.mn[p] : hmin;
+    z.lo0 = hmin;
+    const uint64_t cmax = km(tot.mx[p]);
     uint64_t top = sat_add_u64(hmin, (uint64_t)(kHistBinsR - 1) << sh1);
-    z.hitop = tot.mx[p] > top ? tot.mx[p] : top;
+    z.hitop = cmax > top ? cmax : top;
+    z.vmin = km.vmin;
+    z.scale = km.scale;
     rd->ph[p] = z;
   }
   __syncthreads();
@@ -537,8 +591,9 @@ k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
   // (each such client contributes at least one entry <= T).  P: the rest.
   uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                          : (p_runs ? k - (uint32_t)tot.n_r : 0);
-  const HistRange h{tot.mn[p], hist_shift_r(tot.mx[p] - tot.mn[p]), 0};
-  pick_phase(p, need, tot, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
+  const KeyMap km(tot.mn[p], tot.mx[p]);
+  const HistRange h{0, hist_shift_r(km(tot.mx[p])), 0};
+  pick_phase(p, need, tot, km, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -546,7 +601,8 @@ k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
 // table; the open-ended first and last bins span the keys actually seen).
 __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
                                       const uint32_t* sbase, const uint32_t* snum) {
-  uint32_t h = hist_bin(k, ps.hmin, ps.hshift);
+  const uint64_t c = KeyMap(ps.kmin, ps.vmin, ps.scale)(k);
+  uint32_t h = hist_bin(c, ps.hmin, ps.hshift);
   if (h > ps.tbin) h = ps.tbin;
   uint32_t ns = snum[p * kHistBinsR + h];
   uint32_t sub = 0;
@@ -554,7 +610,7 @@ __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
     uint64_t lo = h == 0 ? ps.lo0 : ps.hmin + ((uint64_t)h << ps.hshift);
     uint64_t hi = h == kHistBinsR - 1 ? ps.hitop
                                       : ps.hmin + ((uint64_t)(h + 1) << ps.hshift) - 1;
-    uint64_t off = k > lo ? k - lo : 0;
+    uint64_t off = c > lo ? c - lo : 0;
     uint64_t w = hi > lo ? hi - lo : 0;
     double f = (double)off / ((double)w + 1.0);
     sub = (uint32_t)(f * (double)ns);
@@ -610,8 +666,28 @@ struct EmitV {
       else
         rd->bin_ovf = 1;
     } else {
-      atomicMax(&rd->dmax[ph], (unsigned long long)key);
-      uint32_t at = atomicAdd(&rd->dense_n, 1u);
+      // wave-aggregated: one counter add and one max per phase per wave
+      // (massively tied rounds emit every entry here; per-entry atomics on
+      // two addresses serialise)
+      const uint64_t m = __ballot(1);
+      const int lane = threadIdx.x & 63;
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      const unsigned long long k0 = ph == 0 ? key : 0ull, k1 = ph == 1 ? key : 0ull;
+      unsigned long long mx0 = 0, mx1 = 0;
+      for (uint64_t mm = m; mm; mm &= mm - 1) {
+        const int l = __ffsll((unsigned long long)mm) - 1;
+        const unsigned long long a = __shfl(k0, l), b = __shfl(k1, l);
+        mx0 = a > mx0 ? a : mx0;
+        mx1 = b > mx1 ? b : mx1;
+      }
+      uint32_t base = 0;
+      if (lane == leader) {
+        if (mx0) atomicMax(&rd->dmax[0], mx0);
+        if (mx1) atomicMax(&rd->dmax[1], mx1);
+        base = atomicAdd(&rd->dense_n, (uint32_t)__popcll(m));
+      }
+      base = __shfl(base, leader);
+      const uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
       if (at < dcap) dense[at] = DEnt{key, slot, pos | ((uint32_t)ph << 31), run, ridx};
     }
   }

@@ -302,3 +302,25 @@ def test_activation_records_across_chunks(queued_frac):
         elif a[0] == "add":
             assert np.array_equal(a[1], b[1]), i
     compare_states(qa, qb, slots, "final")
+
+
+@pytest.mark.parametrize("seed", [1, 3, 5])
+def test_key_range_straddles_zero(seed):
+    """Forty idle clients with queued fronts are activated 100 s later: the
+    idle reset gives them prop_delta ~ -600 s, so the proportion keys of the
+    next pulls straddle zero and the histogram coordinates switch from
+    bit-pattern offsets to the value-linear map (KeyMap, dmc_round.h) with
+    binary-searched thresholds.  Tie-free; bit-exact against the oracle
+    through the bin-ranked path (k = 50 / 700 / 2500)."""
+    from dmclock_amd._abi import make_requests
+    rng = np.random.default_rng(seed)
+    tr = workloads.steady_trace(seed, 3000, 3, 1500, 0, depth=3)
+    t = max(float(o[1]["time"][-1]) for o in tr.ops if o[0] == "add")
+    idle = rng.choice(3000, 40, replace=False).astype(np.uint32)
+    tr.ops.append(("idle", np.sort(idle)))
+    tr.ops.append(("add", make_requests(idle, t + 100 + 0.37 * np.arange(40),
+                                        handles=10**6 + np.arange(40))))
+    t2 = t + 100 + 0.37 * 40
+    for i in range(4):
+        tr.ops.append(("pull", t2 + 0.5 * i, int(rng.choice([50, 700, 2500]))))
+    run_parity(tr, mk_gpu, state_sample=3000)
