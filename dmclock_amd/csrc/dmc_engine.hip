@@ -187,6 +187,10 @@ struct ActBuf {
   const uint64_t* parts;  // k_act_base partials
   uint32_t nparts;
   uint64_t* extra;   // contributions of touched empty clients left unchanged
+  // device-detected activations (dmc_add_batch_device): k_add_chain flags
+  // each activating position, a compaction builds idx and the count *dm
+  uint32_t* flag = nullptr;
+  const uint32_t* dm = nullptr;
 };
 
 // The first node of an add segment: its arguments are the segment's per-call
@@ -201,6 +205,7 @@ __global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
   if (act.cold) {
     act.cold[i] = kMaxKey;
     act.cnew[i] = kMaxKey;
+    if (act.flag) act.flag[i] = 0;
   }
   uint32_t s = p.reqs[i].slot;
   aslot[i] = s;
@@ -341,6 +346,7 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
       if (!act_done && rq.rho <= rq.delta) {  // the activating request
         act_done = true;
         act.actp[pos] = st.count ? (count0 ? front_p0 : st.front.p) : st.prev.p;
+        if (act.flag) act.flag[pos] = 1;
       }
     } else if (count0 == 0 && !chg_done && st.count) {
       chg_done = true;
@@ -511,7 +517,8 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
                              uint64_t* ax, double* ap, double* at, double* apd,
                              uint32_t* aslot) {
   const AddParams p = *pblk;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < act.m;
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m;
        k += gridDim.x * blockDim.x) {
     uint32_t q = act.idx[k];
     uint64_t a = act.pre[q], b = act.suf[p.n - 1 - q];
@@ -537,7 +544,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
   __shared__ uint64_t s_base, s_carry, s_minpre;
   __shared__ uint32_t s_fail;
   __shared__ uint64_t sv[kActThreads];
-  const uint32_t t = threadIdx.x, m = act.m;
+  const uint32_t t = threadIdx.x, m = act.dm ? *act.dm : act.m;
   uint64_t b = kMaxKey;
   for (uint32_t i = t; i < act.nparts; i += kActThreads) b = act.parts[i] < b ? act.parts[i] : b;
   b = block_incl_min(b, wpart);
@@ -1053,6 +1060,16 @@ struct dmc_queue {
   uint64_t* act_x = nullptr;   // per activation: X_k without the unchanged term
   double *act_ip = nullptr, *act_it = nullptr, *act_ipd = nullptr;
   uint32_t* act_islot = nullptr;
+  uint32_t* act_flag = nullptr;  // device-detected activations: position flags
+  uint32_t* act_dm = nullptr;    // and their count
+  uint32_t* h_actm = nullptr;    // pinned copy of the count
+  bool act_pending = false;      // h_act / h_actm hold a batch the idle mirror has not seen
+  // dmc_client_mark_idle_batch staging (pinned) and device list
+  uint32_t* h_mark = nullptr;
+  uint32_t* d_mark = nullptr;
+  uint32_t mark_cap = 0;
+  hipEvent_t mark_ev = nullptr;
+  bool mark_ev_live = false;
   uint32_t* h_act = nullptr;  // pinned staging of the activation positions
   bool act_split = false;     // DMC_OPT_ACT_SPLIT: one host split per activation
   unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
@@ -1419,7 +1436,7 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   uint32_t cap = std::max<uint32_t>(n, 4096);
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
-  dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot);
+  dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot); dfree(q->act_flag);
   if (q->h_act) (void)hipHostFree(q->h_act);
   q->h_act = nullptr;
   HIP_OK(hipMalloc(&q->act_cold, 8ull * cap));
@@ -1433,12 +1450,24 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   HIP_OK(hipMalloc(&q->act_it, 8ull * cap));
   HIP_OK(hipMalloc(&q->act_ipd, 8ull * cap));
   HIP_OK(hipMalloc(&q->act_islot, 4ull * cap));
+  HIP_OK(hipMalloc(&q->act_flag, 4ull * cap));
   HIP_OK(hipHostMalloc((void**)&q->h_act, 4ull * cap, 0));
+  if (!q->act_dm) {
+    HIP_OK(hipMalloc(&q->act_dm, 4));
+    HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
+  }
   {
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveScan(nullptr, tb, q->act_cnew, q->act_pre,
                                             MinKey{}, kMaxKey, (int)cap, q->stream);
     int rc = ensure_temp(q, tb);
+    if (rc) return rc;
+    tb = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, tb,
+                                        hipcub::CountingInputIterator<uint32_t>(0),
+                                        q->act_flag, q->act_idx, q->act_dm, (int)cap,
+                                        q->stream);
+    rc = ensure_temp(q, tb);
     if (rc) return rc;
   }
   if (!q->act_extra) {
@@ -1510,6 +1539,77 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   HIP_OK(hipGetLastError());
   // the pinned staging is reused by the next batch: wait for the copy
   HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+// The device API's batch with activations: k_add_chain flags the activating
+// requests itself, so the requests never travel to the host; the host's idle
+// mirror learns the activated slots lazily (settle_act) before anything reads
+// it, with no synchronisation between the add and the pulls that follow.
+int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
+                      int32_t* d_rc) {
+  int rc = ensure_act(q, n);
+  if (rc) return rc;
+  prof_gate(q);
+  const uint32_t gb = grid_for(q->tb.n, 2048);
+  ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
+             q->act_idx, 0, q->act_parts, gb, q->act_extra, q->act_flag, q->act_dm};
+  AddParams ap{d_reqs, d_rc, q->tick, n, 0};
+  uint32_t g = (n + kBlock - 1) / kBlock;
+  pb(q, DMC_PROF_ADD_LINK);
+  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
+                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk, act);
+  pe(q);
+  pb(q, DMC_PROF_ACTIVATE);
+  hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
+                     (const uint32_t*)q->acnt, q->act_parts);
+  pe(q);
+  pb(q, DMC_PROF_ADD_CHAIN);
+  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
+                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
+  pe(q);
+  pb(q, DMC_PROF_ACTIVATE);
+  size_t tbytes = q->temp_bytes;
+  (void)hipcub::DeviceSelect::Flagged(q->temp, tbytes,
+                                      hipcub::CountingInputIterator<uint32_t>(0),
+                                      q->act_flag, q->act_idx, q->act_dm, (int)n,
+                                      q->stream);
+  tbytes = q->temp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cnew, q->act_pre,
+                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  tbytes = q->temp_bytes;
+  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cold, q->act_suf,
+                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
+                     (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
+                     q->act_it, q->act_ipd, q->act_islot);
+  hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
+                     act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
+                     (const double*)q->act_it, (const double*)q->act_ipd,
+                     (const uint32_t*)q->act_islot);
+  pe(q);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(q->h_actm, q->act_dm, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(q->h_act, q->act_islot, 4ull * n, hipMemcpyDeviceToHost,
+                        q->stream));
+  q->act_pending = true;
+  return DMC_OK;
+}
+
+// the idle mirror catches up with the last device-detected activations
+int settle_act(dmc_queue* q) {
+  if (!q->act_pending) return DMC_OK;
+  HIP_OK(hipStreamSynchronize(q->stream));
+  q->act_pending = false;
+  const uint32_t m = *q->h_actm;
+  for (uint32_t k = 0; k < m; ++k) {
+    const uint32_t s = q->h_act[k];
+    if (q->idle_h[s]) {
+      q->idle_h[s] = 0;
+      --q->n_idle;
+    }
+  }
   return DMC_OK;
 }
 
@@ -1954,6 +2054,11 @@ int dmc_queue_destroy(dmc_queue* q) {
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_extra); dfree(q->act_parts);
   dfree(q->act_x); dfree(q->act_ip); dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot);
+  dfree(q->act_flag); dfree(q->act_dm);
+  if (q->h_actm) (void)hipHostFree(q->h_actm);
+  dfree(q->d_mark);
+  if (q->h_mark) (void)hipHostFree(q->h_mark);
+  if (q->mark_ev) (void)hipEventDestroy(q->mark_ev);
   if (q->h_sctl) (void)hipHostFree(q->h_sctl);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
@@ -1979,6 +2084,7 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                               int active) {
   if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
   QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
   if (!n) return DMC_OK;
@@ -2034,6 +2140,7 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
 int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   uint8_t f;
   HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
@@ -2056,32 +2163,47 @@ __global__ void k_mark_idle(Table tb, uint32_t n, const uint32_t* slots) {
 int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) {
   if (!q || (n && !slots)) return DMC_EINVAL;
   QueueLock g(q);
-  std::vector<uint32_t> mark;
-  mark.reserve(n);
+  if (int rc0 = settle_act(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s = slots[i];
     if (s >= q->p.max_clients) return DMC_EINVAL;
     if (!q->reg_h[s]) return DMC_ENOTREG;
   }
+  // pinned staging and a device list kept across calls; the previous
+  // call's copy must have left the staging before it is rewritten
+  if (q->mark_ev_live) {
+    HIP_OK(hipEventSynchronize(q->mark_ev));
+    q->mark_ev_live = false;
+  }
+  if (n > q->mark_cap) {
+    if (q->h_mark) (void)hipHostFree(q->h_mark);
+    dfree(q->d_mark);
+    q->h_mark = nullptr;
+    q->d_mark = nullptr;
+    q->mark_cap = 0;
+    const uint32_t cap = std::max<uint32_t>(n, 4096);
+    HIP_OK(hipHostMalloc((void**)&q->h_mark, 4ull * cap, 0));
+    HIP_OK(hipMalloc(&q->d_mark, 4ull * cap));
+    q->mark_cap = cap;
+  }
+  if (!q->mark_ev) HIP_OK(hipEventCreateWithFlags(&q->mark_ev, hipEventDisableTiming));
+  uint32_t m = 0;
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s = slots[i];
     if (!q->idle_h[s]) {
       q->idle_h[s] = 1;
       ++q->n_idle;
-      mark.push_back(s);
+      q->h_mark[m++] = s;
     }
   }
-  if (mark.empty()) return DMC_OK;
-  uint32_t m = (uint32_t)mark.size();
-  uint32_t* d_slots;
-  HIP_OK(hipMallocAsync((void**)&d_slots, 4ull * m, q->stream));
-  HIP_OK(hipMemcpyAsync(d_slots, mark.data(), 4ull * m, hipMemcpyHostToDevice,
+  if (m == 0) return DMC_OK;
+  HIP_OK(hipMemcpyAsync(q->d_mark, q->h_mark, 4ull * m, hipMemcpyHostToDevice,
                         q->stream));
   hipLaunchKernelGGL(k_mark_idle, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                     q->stream, q->tb, m, (const uint32_t*)d_slots);
+                     q->stream, q->tb, m, (const uint32_t*)q->d_mark);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipFreeAsync(d_slots, q->stream));
-  HIP_OK(hipStreamSynchronize(q->stream));  // the host vector is freed on return
+  HIP_OK(hipEventRecord(q->mark_ev, q->stream));
+  q->mark_ev_live = true;
   return DMC_OK;
 }
 
@@ -2134,6 +2256,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -2214,6 +2337,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
                   int32_t* rc_out) {
   if (!q || (n && !reqs)) return DMC_EINVAL;
   QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
@@ -2237,8 +2361,12 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
-  if (q->n_idle) {
-    // activations need the host-ordered split: stage the batch on the host
+  rc = settle_act(q);
+  if (rc) return rc;
+  if (q->n_idle && !q->act_split && q->p.at_limit != DMC_AT_LIMIT_REJECT) {
+    rc = add_act_batch_dev(q, n, d_reqs, d_rc_out);
+  } else if (q->n_idle) {
+    // the host split (Reject, or forced): stage the batch on the host
     std::vector<dmc_request> h(n);
     HIP_OK(hipMemcpyAsync(h.data(), d_reqs, sizeof(dmc_request) * n,
                           hipMemcpyDeviceToHost, q->stream));
@@ -2296,6 +2424,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
   bool fuse;
   {
     QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
     fuse = n && k && q->n_idle == 0 && q->n_registered > 0 && k > q->small_k &&
            !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
            q->use_graphs && !q->prof_on;
