@@ -166,6 +166,22 @@ __device__ inline CView load_view(const Table& tb, uint32_t s) {
   return v;
 }
 
+// Touch the client's queued entries past the first two (up to kTouch) so
+// that their lines are requested together with the walk's first loads: the
+// walkers, reduced_r and the apply reductions then hit the cache instead of
+// paying one dependent memory round trip per entry.  Returns a value the
+// caller consumes once the walk is done (keeps the loads alive).
+constexpr uint32_t kTouch = 8;
+__device__ inline double touch_ring(const Table& tb, uint32_t s, uint32_t h,
+                                    uint32_t c) {
+  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  const uint32_t n = c < kTouch ? c : kTouch;
+  double acc = 0.0;
+  for (uint32_t j = 2; j < n; ++j) acc += ring[(h + j) & tb.qmask].arrival;
+  return acc;
+}
+__device__ inline void keep(double v) { asm volatile("" ::"v"(v)); }
+
 // Visitor callbacks: pop(i, tag, cost, handle, prio, dec, tie) for each pop
 // (i = queue position, dec/tie = the ring entry's round scratch), and
 // group(key, run) after each priority group.

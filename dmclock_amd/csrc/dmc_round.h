@@ -1233,6 +1233,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) 
   const uint32_t terminal = rc.terminal;
   const bool p_runs = rc.p_runs;
   const uint32_t c = cv.c, h = cv.h;
+  const double touched = touch_ring(tb, s, h, c);
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s};
   Tag3 front{};
@@ -1253,6 +1254,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) 
     popsP = w.pops;
     pmask = w.pmask;
   }
+  keep(touched);
   uint32_t pops = popsR + popsP;
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
