@@ -617,26 +617,34 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
         // its activation; the first lane whose contribution undercuts M (a
         // new minimum) ends the step, lanes up to it commit (their M was
         // exact), and M takes that lane's value.  The number of steps is the
-        // number of new minima plus e / 64, not e.
+        // number of new minima plus e / 64, not e.  Each lane keeps its
+        // activation's inputs in registers for the whole 64-wide window, so
+        // a step's critical path is the arithmetic, the ballot and one
+        // readlane (no LDS round trip).
         constexpr double dmax = 1.7976931348623157e308;  // :960
         constexpr double trigger = dmax / 3.0;            // :957
         double M = s_M;
         const uint32_t e = m - c0 < (uint32_t)kActThreads ? m - c0 : kActThreads;
-        for (uint32_t j0 = 0; j0 < e;) {
+        for (uint32_t j0 = 0; j0 < e; j0 += 64) {
           const uint32_t j = j0 + t;
           const bool in = j < e;
-          double pd = 0.0, c = kInf;
-          if (in) {
-            double L = M < cx[j] ? M : cx[j];
+          const double rx = in ? cx[j] : kInf, rp = in ? cp[j] : 0.0,
+                       rt = in ? ct[j] : 0.0, rpd0 = in ? cpd[j] : 0.0;
+          const uint32_t w = e - j0 < 64u ? e - j0 : 64u;
+          double out = rpd0;
+          for (uint32_t done = 0; done < w;) {
+            const bool act = in && t >= done;
+            double L = M < rx ? M : rx;
             double lowest = L < dmax ? L : dmax;
-            pd = lowest < trigger ? __dsub_rn(lowest, ct[j]) : cpd[j];
-            c = __dadd_rn(cp[j], pd);
+            const double pd = lowest < trigger ? __dsub_rn(lowest, rt) : rpd0;
+            const double c = __dadd_rn(rp, pd);
+            const uint64_t rec = __ballot(act && c < M);
+            const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
+            if (act && t <= r) out = pd;
+            if (rec) M = __shfl(c, (int)r);
+            done = r == 64u ? 64u : r + 1;
           }
-          const uint64_t rec = __ballot(in && c < M);
-          const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
-          if (in && t <= r) cpd[j] = pd;
-          if (rec) M = __shfl(c, (int)r);
-          j0 += r == 64u ? 64u : r + 1;
+          if (in) cpd[j] = out;
         }
         if (t == 0) s_M = M;
       }
