@@ -284,9 +284,21 @@ def main():
     nows = [float(r["time"][-1]) for r in steps]
     torch.cuda.synchronize()
 
+    host_t = {"mark_idle": 0.0, "add_pull": 0.0}
+    timing = os.environ.get("BENCH_HOST_TIMING") is not None
+
     def step(i):
         if idle is not None:
+            t_a = time.perf_counter()
             q.mark_idle_batch(idle[i])
+            if timing:
+                host_t["mark_idle"] += time.perf_counter() - t_a
+        t_b = time.perf_counter()
+        _step_calls(i)
+        if timing:
+            host_t["add_pull"] += time.perf_counter() - t_b
+
+    def _step_calls(i):
         if args.separate_calls:
             q.add_batch_device(d_reqs[i].data_ptr(), args.batch, d_rc.data_ptr())
             q.pull_batch_device(nows[i], k, d_out.data_ptr(), d_res[i].data_ptr())
@@ -309,6 +321,10 @@ def main():
     dt = time.perf_counter() - t0
     st_t1 = q.stats()
     res = d_res[args.warmup:args.warmup + args.steps].cpu().numpy()
+    if timing:
+        print("host time per step (ms): " + ", ".join(
+            f"{k} {v / args.steps * 1e3:.3f}" for k, v in host_t.items())
+            + f", wall {dt / args.steps * 1e3:.3f}", file=sys.stderr)
 
     # stage-timed pass: the next prof_steps batches, launched eagerly behind
     # a GPU-side gate with HIP events on the engine's stream around each stage
