@@ -228,7 +228,11 @@ class GpuQueue:
 
     def pull_batch(self, now, k):
         self._refresh_dynamic()
-        out = np.zeros(max(k, 1), dtype=DECISION_DTYPE)
+        # a reused output buffer (first-touch page faults on a fresh 3 MB
+        # array per call cost as much as the transfer); callers get a copy
+        if getattr(self, "_out", None) is None or len(self._out) < max(k, 1):
+            self._out = np.empty(max(k, 1), dtype=DECISION_DTYPE)
+        out = self._out
         res = PullResult()
         _check(self.L.dmc_pull_batch(self.h, float(now), k, _ptr(out),
                                      ctypes.byref(res)), "pull_batch")
