@@ -177,6 +177,17 @@ def test_bench_shaped_parity(variant):
     assert n > 100000
 
 
+def test_full_size_parity_1m_clients():
+    """BASELINE config 3 at its full size: 1,048,576 bulk-registered clients,
+    2M pre-populated requests, a 1M-pull settle round, then two steps of
+    64K adds + 64K pulls — every decision (≈1.18M) and every add status
+    bit-exact against the oracle, the trace tie-free (oracle ≈13 s)."""
+    tr = bench_shaped_trace(42, 1 << 20, 2, 1 << 16, depth=2)
+    n, qg, qo = run_parity(tr, mk_variant("default"),
+                           dict(at_limit=AT_LIMIT_WAIT), state_sample=4096)
+    assert n > 1_000_000
+
+
 # ------------------------------------------------ batched activations
 MODES_ACT = [dict(at_limit=AT_LIMIT_WAIT), dict(at_limit=AT_LIMIT_WAIT, delayed=True),
              dict(at_limit=AT_LIMIT_ALLOW)]
