@@ -32,6 +32,10 @@
 
 using namespace dmc;
 
+#ifndef DMC_WALK_GRID_CAP
+#define DMC_WALK_GRID_CAP 1024
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -1108,6 +1112,7 @@ struct dmc_queue {
   uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
   uint64_t* dbg_atime = nullptr; // debug: per-candidate apply start/end clocks
   uint32_t radix_batches = 0;  // rounds left on the fallback path
+  uint32_t ovf_streak = 0;     // bin-rank rounds in a row that overflowed
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
   std::vector<GraphRec> graphs = std::vector<GraphRec>(8);
@@ -1692,7 +1697,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // walking kernels: grid-stride over the candidate list, sized so that
   // a typical round's candidates are resident at once
-  uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, 1024);
+  uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
   pb(q, DMC_PROF_SCAN);
   hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
                      q->keyp, q->mr, q->rparts, q->rd, cp);
@@ -1820,6 +1825,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
               bool* dev_wrote = nullptr, bool pre_launched = false) {
   if (dev_wrote) *dev_wrote = false;
   bool first_round = true;
+  bool retry_radix = false;  // re-run an overflowed round on the radix path
   dmc_pull_result r{};
   r.next_type = DMC_NEXT_RETURNING;
   uint32_t n_dec = 0;
@@ -1844,7 +1850,9 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       (q->h_sctl->prio ? r.n_priority : r.n_reservation)++;
       continue;
     }
-    bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK;
+    const bool retry = retry_radix;
+    retry_radix = false;
+    bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK || retry;
     // the first round of a call may end it: its k_rfinish writes d_result
     dmc_pull_result* dres = (first_round && n_dec == 0) ? d_result : nullptr;
     int rc = DMC_OK;
@@ -1852,7 +1860,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       pre_launched = false;
       radix = false;
     } else {
-      if (q->radix_batches) --q->radix_batches;
+      if (q->radix_batches && !retry) --q->radix_batches;
       if (radix) {
         rc = ensure_entries(q, q->dense_hint);
         if (rc) return rc;
@@ -1899,10 +1907,17 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
       continue;
     }
-    if (c.overflow == 2) {  // massively tied keys: rank by sorting instead
-      q->radix_batches = 8;
+    if (c.overflow == 2) {
+      // a rank bin outgrew kBinCapR: this round is re-run on the radix path.
+      // An isolated skewed round costs only that; massively tied keys
+      // (overflows in a row) keep the next 1, 2, 4, then 8 calls on it
+      retry_radix = true;
+      ++q->ovf_streak;
+      if (q->ovf_streak > 1)
+        q->radix_batches = std::min<uint32_t>(8, 1u << (q->ovf_streak - 2));
       continue;
     }
+    if (!radix) q->ovf_streak = 0;
     n_dec += c.n_dec;
     r.n_priority += c.n_prio;
     r.n_reservation += c.n_dec - c.n_prio;

@@ -55,7 +55,7 @@ constexpr int kNBPhase = kNBR / 2;
 // side (~12 ns each): the histogram is sharded 8 ways (block % 8, one shard
 // per XCD) and the pick combines the shards.
 constexpr int kShards = 8;
-constexpr uint32_t kBinCapR = 256;      // entries per rank bin (4 per lane)
+constexpr uint32_t kBinCapR = 512;      // entries per rank bin (2 per thread of k_rrank)
 constexpr uint32_t kNoneR = 0xffffffffu;
 constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
 
@@ -179,8 +179,15 @@ struct CountV {
 // Each thread takes kScanSlots slots and issues all their column loads before
 // any walk; blocks of kScanBlock threads, so that the per-block partials
 // (counts, key ranges) stay few.
-constexpr int kScanSlots = 2;
-constexpr int kScanBlock = 1024;
+// (build-time overridable for launch-shape sweeps: results do not depend on them)
+#ifndef DMC_SCAN_SLOTS
+#define DMC_SCAN_SLOTS 2
+#endif
+#ifndef DMC_SCAN_BLOCK
+#define DMC_SCAN_BLOCK 1024
+#endif
+constexpr int kScanSlots = DMC_SCAN_SLOTS;
+constexpr int kScanBlock = DMC_SCAN_BLOCK;
 
 struct ScanCols {
   uint32_t c, h;
@@ -820,7 +827,10 @@ __device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
 // r <= min(now, T_R); then, if the priority pulls run, the P groups with key
 // <= T_P from the post-R state.  Bin-rank path: into the rank bins; radix
 // path: appended to the dense entry list.
-__global__ void __launch_bounds__(kBlockR)
+#ifndef DMC_EMIT_MINB
+#define DMC_EMIT_MINB 1
+#endif
+__global__ void __launch_bounds__(kBlockR, DMC_EMIT_MINB)
 k_remit(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
         const uint64_t* keyp, const uint8_t* mr, BRecR* brec, uint32_t* bcount,
         uint32_t* bsize, const uint32_t* sbase, const uint32_t* snum,
@@ -938,38 +948,19 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
   }
 }
 
-// One block per rank bin.  The bin's records are staged in LDS; each record
-// is ranked against all of them by `parts` adjacent lanes, each comparing a
-// slice (parts = the largest power of two with cnt * parts <= 256, at most
-// 64), and the slices' counts are summed by shuffles: a big bin (skewed keys)
-// costs cnt^2 / 256 compare steps per lane instead of cnt.  The comparison is
-// branchless (wave-uniform trip counts, broadcast LDS reads).
-constexpr int kRankBlocksR = kNBR;
-__global__ void __launch_bounds__(kBlockR)
-k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
-        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
-        uint64_t* wtime = nullptr) {
-  __shared__ BRecR sh[kBinCapR];
-  uint64_t t0 = wall_clock64();
-  const uint32_t b = blockIdx.x;
-  const uint32_t cnt = bcount[b];
-  if (cnt == 0 || rd->overflow) return;
-  const uint32_t k = rd->k_total;
-  const uint32_t n_pgroups = rd->n_pgroups;
-  const bool isp = b >= (uint32_t)kNBPhase;
-  const uint32_t soff = bsoff[b], poff = bpoff[b];
-  const BRecR* src = brec + (size_t)b * kBinCapR;
-  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
-  uint32_t parts = 1;
-  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
-  const uint32_t per = (cnt + parts - 1) / parts;
-  __syncthreads();
-  const uint32_t t = threadIdx.x;
-  const uint32_t i = t / parts, part = t % parts;
+// Rank of record i of a bin among all `cnt` of them, compared in `parts`
+// slices of `per` records by adjacent lanes whose counts are summed by
+// shuffles; lanes with i >= cnt take part in the shuffles only.  Decides:
+// the entry's decision offset and tie flag stamped into its ring entry.
+__device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
+                                uint32_t parts, uint32_t per, uint32_t i,
+                                uint32_t part, bool isp, uint32_t k,
+                                uint32_t n_pgroups, uint32_t soff, uint32_t poff,
+                                ReqEntry* ring) {
   const bool valid = i < cnt;
   BRecR me = sh[valid ? i : 0];
   uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
-  if (!valid) f1 = f0;  // inactive lanes still take part in the shuffles
+  if (!valid) f1 = f0;
   uint32_t rank = 0, gl = 0, tie = 0;
 #pragma unroll 4
   for (uint32_t f = f0; f < f1; ++f) {
@@ -1004,6 +995,39 @@ k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
       }
     }
   }
+}
+
+// One block per rank bin.  The bin's records are staged in LDS; each record
+// is ranked against all of them by `parts` adjacent lanes, each comparing a
+// slice (parts = the largest power of two with cnt * parts <= 256, at most
+// 64): a big bin (skewed keys) costs cnt^2 / 256 compare steps per lane
+// instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
+// ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
+// branchless (wave-uniform trip counts, broadcast LDS reads).
+constexpr int kRankBlocksR = kNBR;
+__global__ void __launch_bounds__(kBlockR)
+k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
+        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
+        uint64_t* wtime = nullptr) {
+  __shared__ BRecR sh[kBinCapR];
+  uint64_t t0 = wall_clock64();
+  const uint32_t b = blockIdx.x;
+  const uint32_t cnt = bcount[b];
+  if (cnt == 0 || rd->overflow) return;
+  const uint32_t k = rd->k_total;
+  const uint32_t n_pgroups = rd->n_pgroups;
+  const bool isp = b >= (uint32_t)kNBPhase;
+  const uint32_t soff = bsoff[b], poff = bpoff[b];
+  const BRecR* src = brec + (size_t)b * kBinCapR;
+  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
+  uint32_t parts = 1;
+  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
+  const uint32_t per = (cnt + parts - 1) / parts;
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
+    rank_rec(rd, sh, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
+             soff, poff, ring);
   if (wtime && threadIdx.x == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
@@ -1320,7 +1344,10 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) 
 // a later limit-scanning pull happened (or the round's terminal pull).
 // (Non-candidates settled their pending marks in k_rcand.)  Block 0 also counts the round's decisions (sched[0] reservation,
 // sched[1] priority, :1469,1479) and resets the rank-bin counters.
-__global__ void __launch_bounds__(kBlockR, 5)
+#ifndef DMC_APPLY_MINB
+#define DMC_APPLY_MINB 5
+#endif
+__global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const uint32_t* cand, uint32_t* bcount,
          uint32_t* bsize, unsigned long long* sched, uint64_t* dbg = nullptr) {
   if (blockIdx.x == 0) {

@@ -335,3 +335,44 @@ def test_key_range_straddles_zero(seed):
     for i in range(4):
         tr.ops.append(("pull", t2 + 0.5 * i, int(rng.choice([50, 700, 2500]))))
     run_parity(tr, mk_gpu, state_sample=3000)
+
+
+@pytest.mark.parametrize("n", [200, 300, 500, 700])
+def test_tied_rank_bins(n):
+    """Massively tied keys put every entry of a round into one rank bin:
+    n = 300 and 500 exceed one k_rrank block (multi-pass ranking), n = 700
+    exceeds kBinCapR = 512 (the round is re-run on the radix path, then the
+    next call tries the bins again).  The bin-ranked, radix-sorted and
+    single-step engines must give the same decisions bit for bit (ties broken
+    by lowest slot)."""
+    from dmclock_amd._abi import REQUEST_DTYPE
+
+    def run(variant):
+        q = mk_variant(variant)(max_clients=1024)
+        slots = np.arange(n, dtype=np.uint32)
+        q.register_active(slots, np.zeros(n), np.ones(n), np.zeros(n))
+        out = []
+        for call in range(3):
+            reqs = np.zeros(3 * n, REQUEST_DTYPE)
+            reqs["slot"] = np.tile(slots, 3)
+            reqs["cost"] = 1
+            reqs["time"] = 1.0 + call
+            reqs["delta"] = 1
+            reqs["rho"] = 1
+            reqs["handle"] = np.arange(3 * n) + call * 3 * n
+            rc = q.add_batch(reqs)
+            assert (rc == 0).all()
+            d, res = q.pull_batch(10.0 + call, 2 * n + 7)
+            assert res.n_decisions == 2 * n + 7
+            out.append(d[:res.n_decisions].copy())
+        q.close()
+        return np.concatenate(out)
+
+    base = run("default")
+    assert (base["flags"] != 0).mean() > 0.5  # tied and flagged
+    assert base.tobytes() == run("radix").tobytes()
+    # single steps flag a tie among the fronts of one pull, not a round's
+    # entries: every other field must match
+    steps = run("steps")
+    for f in ("handle", "tag_r", "tag_p", "tag_l", "slot", "cost", "phase"):
+        assert base[f].tobytes() == steps[f].tobytes(), f
