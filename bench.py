@@ -33,38 +33,82 @@ sys.path.insert(0, ROOT)
 METRIC = "dispatch decisions/sec + tag updates/sec at 1M clients; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-# Algorithmic bytes of each stage: (per client slot of the table, per added
-# request, per decision) -- DESIGN.md section 6.  A pull round streams the
-# client-table columns it needs once per kernel and touches the candidates'
-# rings and state; the add path touches one client record per request.
-STAGE_BYTES = {
-    # k_rscan: count 4 + front_r 8 + flags 1 + front_p 8 + front_l 8 +
-    #   prop_delta 8 read, keyr 8 + keyp 8 + R-prefix length 1 written
-    "scan": (54, 0, 0),
-    # k_rhist: keyr + keyp read (its last block: 2 x 2048-bin thresholds)
-    "select": (16, 0, 0),
-    # k_rcand: keyr + keyp + flags read per slot; per candidate (about one
-    #   per decision) its slot written to the candidate list
-    "cand": (17, 0, 4),
-    # k_remit: per candidate its slot 4 and keyr + keyp 16 read; per
-    #   dispatched entry its ring entry 64 read and rank record 24 written
-    "emit": (0, 0, 108),
-    # k_rrank: rank record 24 read, decision offset + tie 8 written into the
-    #   ring entry
-    "rank": (0, 0, 32),
-    # k_rapply: applied 4 + flags 1 per slot; per decision its ring entry 64
-    #   read, decision record 48 written, client state ~120 read/written
-    "apply": (5, 0, 232),
-    # k_add_link: request slot 32 (line) read, apos/aslot 8 written, slot
-    #   counter 4 + slot buffer 4
-    "add_link": (0, 48, 0),
-    # k_add_chain (one request per client): apos/aslot 8 + acnt 8 + abuf 4
-    #   + request 32 + rc 4 + ring entry 64 + client state read 81
-    #   (prev tag 32, inverses 24, head/count/cur_delta/cur_rho 16,
-    #   last_tick 8, flags 1) and written 77 (prev 32, count/cur_* 12,
-    #   last_tick 8, flags 1, front tag 24)
-    "add_chain": (0, 278, 0),
-}
+# Algorithmic bytes of each stage per step, from the step's counts: N client
+# slots, R added requests, D decisions, C candidate clients, E rank records
+# emitted, A activations.  The pull-round stages stream
+# the client-table columns they need once per kernel and touch the
+# candidates' state and rings; the add path touches one client record per
+# request.
+def _stage_bytes(N, R, D, C, E, A):
+    return {
+        # k_rscan: count 4 + head 4 + front r/p/l 24 + prop_delta 8 + flags 1
+        #   read; keyr 8 + keyp 8 + R-prefix length 1 written
+        "scan": 58 * N,
+        # k_rhist + k_rpick: keyr + keyp read
+        "select": 16 * N,
+        # k_rcand: keyr + keyp + flags read per slot; candidate slot written
+        "cand": 17 * N + 4 * C,
+        # k_remit: per candidate its slot 4, keyr/keyp 16, R-prefix length 1,
+        #   QState 16, inverses 24, prop_delta 8, flags 1 read; per record its
+        #   ring entry 64 read and the 24-byte rank record written
+        "emit": 70 * C + 88 * E,
+        # k_rbscan + k_rrank: rank records read, the decision offset and tie
+        #   flag (8) stamped into each dispatched ring entry
+        "rank": 24 * E + 8 * D,
+        # k_rapply: per candidate its slot 4, flags 1, QState 16, ClientRec
+        #   64, prop_delta 8 read; per decision its ring entry 64 read and the
+        #   48-byte decision written, and the popped client's new state
+        #   (head/count 8, front r/p/l 24, prev r 8, flags 1) written
+        "apply": 93 * C + 153 * D,
+        # k_add_link: request slot 4 read, apos/aslot 8 written, the
+        #   client's counter 4 (atomic) and slot-buffer entry 4
+        "add_link": 20 * R,
+        # k_add_chain (one request per client): link records 16 + request 32
+        #   + status 4 + ring entry 64 written + client state read 73
+        #   (prev tag 32, inverses 24, head/count/cur_delta/cur_rho 16, flags
+        #   1) and written 85 (prev 32, count/cur_* 12, last_tick 8, flags 1,
+        #   front tag 24, counter reset 4, ...)
+        "add_chain": 278 * R,
+        # activations (config 4): k_act_base streams flags 1, count 4, front
+        #   p 8, prop_delta 8, prev p 8 and the batch counter 4 per slot; per
+        #   request the cold/new contributions and their two min-scans (4 x 8
+        #   written + read); per activation its inputs and result (~56)
+        "activate": 33 * N + 64 * R + 56 * A,
+    }
+
+
+def roofline(args, prof, prof_steps, ctr, k, n_clients=None, n_adds=None,
+             activations=None):
+    """The dominant stage (largest time per step) of the stage-timed pass:
+    its algorithmic bytes per launch (_stage_bytes over that pass's counts)
+    over its mean launch duration, against the HBM peak."""
+    cand = [(ms, name) for name, (c, ms) in prof.items() if c > 0]
+    if not cand or not prof_steps or ctr is None:
+        return None
+    N = n_clients or args.clients
+    R = n_adds if n_adds is not None else args.batch
+    per_step = lambda key: ctr[key] / prof_steps
+    D, C, E = per_step("decisions"), per_step("candidates"), per_step("entries")
+    A = activations or 0.0
+    model = _stage_bytes(N, R, D, C, E, A)
+    cand = [(ms, name) for ms, name in cand if name in model]
+    if not cand:
+        return None
+    ms, name = max(cand)
+    c = prof[name][0]
+    launches_per_step = c / prof_steps
+    per_launch = model[name] / launches_per_step
+    avg_s = ms / c / 1e3
+    achieved = per_launch / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None, "kernel": name,
+            "bytes_per_launch": int(per_launch),
+            "avg_launch_us": round(avg_s * 1e6, 2),
+            "counts_per_step": {"clients": N, "adds": R, "decisions": round(D, 1),
+                                "candidates": round(C, 1), "records": round(E, 1),
+                                "activations": A}}
 
 
 def parse():
@@ -256,20 +300,55 @@ def cpu_baseline_churn(args, q, steps, idle):
                        f"{dt:.2f} s")}
 
 
-def main():
-    args = parse()
-    if args.config == 5:
-        import bench_multiserver
-        return bench_multiserver.main(args)
+def rank_env():
+    """(rank, world, local device, backend) from the torchrun environment.
+    BENCH_SHARE_DEVICE=1 rehearses a multi-rank run on a one-GPU box: every
+    rank on device 0, gloo for the barrier and the reductions (RCCL needs a
+    device per rank)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = "nccl"
+    if os.environ.get("BENCH_SHARE_DEVICE") == "1":
+        local, backend = 0, "gloo"
+    return rank, world, local, backend
+
+
+def spawn_ranks(n):
+    """bench.py --gpus N run directly (no torchrun environment): launch the N
+    ranks as child processes through torch.distributed.run, one per GPU,
+    before this process touches a GPU, and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus and "WORLD_SIZE" in os.environ:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; "
+              f"running {world_env} ranks", file=sys.stderr)
+    if args.config == 5:
+        import bench_multiserver
+        return bench_multiserver.main(args)
+    rank, world, local, backend = rank_env()
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     from dmclock_amd.gpu import GpuQueue
     from dmclock_amd._abi import DECISION_DTYPE, PullResult
 
@@ -320,6 +399,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     st_t0 = q.stats()
+    q.counters(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -331,6 +411,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     st_t1 = q.stats()
+    ctr_timed = q.counters()
     res = d_res[args.warmup:args.warmup + args.steps].cpu().numpy()
     if timing:
         print("host time per step (ms): " + ", ".join(
@@ -341,9 +422,11 @@ def main():
     # a GPU-side gate with HIP events on the engine's stream around each stage
     prof = {}
     prof_steps = 0
+    prof_ctr = None
     if not args.no_profile and args.prof_steps > 0:
         q.profile(True)
         q.profile_reset()
+        q.counters(reset=True)
         torch.cuda.synchronize()
         for i in range(args.warmup + args.steps,
                        args.warmup + args.steps + args.prof_steps):
@@ -351,6 +434,7 @@ def main():
         torch.cuda.synchronize()
         q.profile(False)
         prof = q.profile_read()
+        prof_ctr = q.counters()
         prof_steps = args.prof_steps
 
     n_dec = 0
@@ -366,11 +450,12 @@ def main():
     local_ops = n_dec + n_adds
 
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        rdev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         o = torch.tensor([local_ops, n_dec, n_adds], dtype=torch.float64,
-                         device=dev)
+                         device=rdev)
         dist.all_reduce(o, op=dist.ReduceOp.SUM)
         local_ops, n_dec, n_adds = (float(x) for x in o.tolist())
 
@@ -379,38 +464,23 @@ def main():
             dist.destroy_process_group()
         return
 
-    # roofline: the dominant stage (largest time per step) of the stage-timed
-    # pass, its algorithmic bytes per launch over its mean launch duration
-    roof = None
-    cand = [(ms, name) for name, (c, ms) in prof.items()
-            if name in STAGE_BYTES and c > 0]
-    if cand:
-        ms, name = max(cand)
-        c = prof[name][0]
-        per_client, per_req, per_dec = STAGE_BYTES[name]
-        launches_per_step = c / max(prof_steps, 1)
-        per_launch = (per_client * args.clients
-                      + (per_req * args.batch + per_dec * k)
-                      / launches_per_step)
-        avg_s = ms / c / 1e3
-        achieved = per_launch / avg_s / 1e9
+    acts = None
+    if args.config == 4 and prof_steps:
+        i0 = args.warmup + args.steps
+        acts = float(np.mean(args.activations[i0:i0 + prof_steps]))
+    roof = roofline(args, prof, prof_steps, prof_ctr, k, activations=acts)
+    if roof is not None:
         # HBM bytes per launch of the same stage from the PMC passes of
-        # scripts/gpu_pmc.sh (tools/pmc_traffic.py: 2 x FETCH_SIZE +
-        # WRITE_SIZE, the guide's gfx950 correction), committed under
-        # profiles/; null if that file is absent
+        # scripts/gpu_pmc.sh (tools/pmc_traffic.py), committed under
+        # profiles/; null if that file is absent or lacks the stage
         traffic = None
         if os.path.exists(args.traffic):
             try:
-                t = json.load(open(args.traffic)).get(name)
+                t = json.load(open(args.traffic)).get(roof["kernel"])
                 traffic = t["hbm_bytes"] if t else None
             except Exception:
                 traffic = None
-        roof = {"bound": "hbm", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "kernel": name,
-                "bytes_per_launch": int(per_launch),
-                "avg_launch_us": round(avg_s * 1e6, 2)}
+        roof["traffic"] = traffic
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -445,7 +515,9 @@ def main():
                    "api": ("host buffers (dmc_add_batch + dmc_pull_batch, PCIe "
                            "inclusive)" if args.host_api else
                            "device buffers (dmc_add_pull_batch_device)"),
-                   "parallelism": f"{world} independent server queue(s)"},
+                   "parallelism": f"{world} independent server queue(s)"
+                                  + ("" if backend == "nccl" else
+                                     " (rehearsal: ranks share device 0, gloo)")},
         "decisions_per_s": round(n_dec / dt, 1),
         "activations_per_step": (None if args.config != 4 else
                                  round(float(np.mean(args.activations[args.warmup:
@@ -464,6 +536,7 @@ def main():
                        "HIP events around each stage; the timed region "
                        "replays captured hipGraphs",
         "prof_steps": prof_steps,
+        "engine_counters": ctr_timed,
     }
     print(json.dumps(out))
     if dist:

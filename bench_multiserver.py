@@ -58,28 +58,73 @@ def server_workload(args, rank, s, n_steps):
     return tab, cmap, pre, steps
 
 
+def cpu_baseline_multi(args, wl, n_steps):
+    """The oracle (CPU restatement of the reference queue, one thread per
+    server queue, C = min(servers, 16) threads: the box's CPU share per GPU)
+    on a bounded sample of the same workload: each thread builds server s's
+    queue (same table, pre-population and settle pulls; delta = rho = 1 as
+    the requests carry them, the device trackers' fill is not restated) and
+    is then timed over --cpu-steps steps of 64K adds + 64K pulls.  ctypes
+    releases the GIL inside the oracle's calls, so the queues run in
+    parallel."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from bench import prepare
+    S = len(wl)
+    C = min(S, 16)
+    k = args.pulls or args.batch
+    steps = min(args.cpu_steps, n_steps)
+
+    def one(s):
+        tab, _, pre, bat = wl[s]
+        q = pyoracle.OracleQueue(track_ties=False)
+        prepare(q, args, tab, pre)
+        t0 = time.perf_counter()
+        ops = 0
+        for reqs in bat[:steps]:
+            q.add_batch(reqs)
+            d, res = q.pull_batch(float(reqs["time"][-1]), k)
+            ops += len(reqs) + res.n_decisions
+        t1 = time.perf_counter()
+        q.close()
+        return ops, t0, t1
+
+    with ThreadPoolExecutor(C) as ex:
+        out = list(ex.map(one, range(S)))
+    ops = sum(o[0] for o in out)
+    span = max(o[2] for o in out) - min(o[1] for o in out)
+    busy = sum(o[2] - o[1] for o in out)
+    return {"value": ops / span, "unit": "ops/s", "cores": C, "kind": "port",
+            "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps), "
+                       f"{S} server queues of {args.clients} clients on {C} host "
+                       f"threads, each after the same pre-population and settle, "
+                       f"{steps} steps of {args.batch} adds + {k} pulls per queue; "
+                       f"{span:.1f} s wall ({busy:.1f} thread-s)")}
+
+
 def main(args):
     import torch
     from dmclock_amd._abi import DECISION_DTYPE, PullResult
     from dmclock_amd.multiserver import DeviceTrackers, make_queues
     from bench import METRIC
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from bench import rank_env
+    rank, world, local, backend = rank_env()
     dist = None
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     S, N, E = args.servers, args.clients, args.epoch_steps
     k = args.pulls or args.batch
     n_steps = args.warmup + args.steps
+    n_prof = 0 if args.no_profile else args.prof_steps
     t_gen = time.perf_counter()
     with ThreadPoolExecutor(min(S, 8)) as ex:
-        wl = list(ex.map(lambda s: server_workload(args, rank, s, n_steps), range(S)))
+        wl = list(ex.map(lambda s: server_workload(args, rank, s, n_steps + n_prof),
+                         range(S)))
     t_gen = time.perf_counter() - t_gen
 
     queues = make_queues(S, N, device=local, ring_capacity=args.ring,
@@ -91,7 +136,7 @@ def main(args):
     d_rc = [torch.zeros(chunk, dtype=torch.int32, device=dev) for _ in range(S)]
     d_out = [torch.zeros(max(k, chunk) * DECISION_DTYPE.itemsize, dtype=torch.uint8,
                          device=dev) for _ in range(S)]
-    d_res = torch.zeros((S, n_steps + 64, 24), dtype=torch.uint8, device=dev)
+    d_res = torch.zeros((S, n_steps + n_prof + 64, 24), dtype=torch.uint8, device=dev)
     d_steps = [[torch.from_numpy(r.view(np.uint8)).to(dev) for r in w[3]] for w in wl]
     nows = [[float(r["time"][-1]) for r in w[3]] for w in wl]
 
@@ -109,7 +154,7 @@ def main(args):
             assert int((d_rc[s][:n] != 0).sum()) == 0
         settle = args.settle if args.settle is not None else args.depth * N // 2
         t_pre = float(pre["time"][-1])
-        done, j = 0, n_steps
+        done, j = 0, n_steps + n_prof
         while done < settle:
             kk = min(settle - done, chunk)
             q.pull_batch_device(t_pre, kk, d_out[s].data_ptr(), d_res[s, j].data_ptr())
@@ -167,6 +212,25 @@ def main(args):
     dt = time.perf_counter() - t0
     pool.shutdown()
 
+    # roofline: server 0's next n_prof steps alone (no other queue running),
+    # stage-timed like config 3 (HIP events around each stage on its stream)
+    from bench import roofline
+    roof = None
+    if n_prof:
+        q0 = queues[0]
+        q0.profile(True)
+        q0.profile_reset()
+        q0.counters(reset=True)
+        torch.cuda.synchronize()
+        run(0, n_steps, n_steps + n_prof)
+        torch.cuda.synchronize()
+        q0.profile(False)
+        roof = roofline(args, q0.profile_read(), n_prof, q0.counters(), k,
+                        n_clients=N)
+        if roof is not None:
+            roof["note"] = ("server 0 alone after the timed region: its "
+                            "dominant stage per launch")
+
     res = d_res[:, args.warmup:n_steps].cpu().numpy()
     n_dec = sum(PullResult.from_buffer_copy(row.tobytes()).n_decisions
                 for srv in res for row in srv)
@@ -177,10 +241,11 @@ def main(args):
     local_ops = n_dec + n_adds
     ep_ms = 1e3 * float(np.mean(epochs)) if epochs else None
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        rdev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        o = torch.tensor([local_ops, n_dec, n_adds], dtype=torch.float64, device=dev)
+        o = torch.tensor([local_ops, n_dec, n_adds], dtype=torch.float64, device=rdev)
         dist.all_reduce(o, op=dist.ReduceOp.SUM)
         local_ops, n_dec, n_adds = (float(x) for x in o.tolist())
     st = trk.state() if rank == 0 else None
@@ -223,8 +288,9 @@ def main(args):
         "allreduce_bytes_per_epoch": ar_bytes,
         "tracker_known_frac": round(float(st["known"].mean()), 4),
         "setup_s": {"generate": round(t_gen, 1), "prepopulate": round(t_prep, 1)},
-        "roofline": None,
-        "cpu_baseline": None,
+        "roofline": roof,
+        "cpu_baseline": (None if args.no_cpu_baseline or world > 1 else
+                         cpu_baseline_multi(args, wl, n_steps)),
     }
     print(json.dumps(out))
     if dist:

@@ -107,6 +107,28 @@ class Stats(ctypes.Structure):
     ]
 
 
+class Counters(ctypes.Structure):
+    """dmc_counters: engine path counters (dmc_queue_counters)."""
+    _fields_ = [
+        ("rounds", ctypes.c_uint64),
+        ("radix_rounds", ctypes.c_uint64),
+        ("bin_overflows", ctypes.c_uint64),
+        ("dense_overflows", ctypes.c_uint64),
+        ("single_steps", ctypes.c_uint64),
+        ("candidates", ctypes.c_uint64),
+        ("entries", ctypes.c_uint64),
+        ("decisions", ctypes.c_uint64),
+        ("graph_replays", ctypes.c_uint64),
+        ("fused_calls", ctypes.c_uint64),
+        ("max_bin", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_
+                if name != "reserved"}
+
+
 def make_requests(slots, times, costs=1, deltas=1, rhos=1, handles=None):
     """Build a REQUEST_DTYPE array (broadcasting scalars)."""
     slots = np.asarray(slots, dtype=np.uint32)

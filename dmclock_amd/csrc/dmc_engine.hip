@@ -1112,7 +1112,8 @@ struct dmc_queue {
   uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
   uint64_t* dbg_atime = nullptr; // debug: per-candidate apply start/end clocks
   uint32_t radix_batches = 0;  // rounds left on the fallback path
-  uint32_t ovf_streak = 0;     // bin-rank rounds in a row that overflowed
+  uint32_t ovf_streak = 0;     // bin-rank rounds in a row that overflowed (saturates at 5)
+  dmc_counters ctr{};          // dmc_queue_counters
   // captured pull rounds / add segments (see launch_round)
   bool use_graphs = true;
   std::vector<GraphRec> graphs = std::vector<GraphRec>(8);
@@ -1201,6 +1202,7 @@ void dfree(void* p) {
 }
 
 int graph_replay(dmc_queue* q, GraphRec& g, void** args, void** args2 = nullptr) {
+  ++q->ctr.graph_replays;
   hipKernelNodeParams kp = g.kp;
   kp.kernelParams = args;
   kp.extra = nullptr;
@@ -1343,6 +1345,15 @@ int ensure_entries(dmc_queue* q, uint32_t n) {
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
                                          q->stream);
   return ensure_temp(q, std::max(t1, t2));
+}
+
+// The rank-bin records (kNBR x kBinCapR x 24 B = 48 MiB per queue), allocated
+// by the first bin-ranked round: queues that only ever take single steps or
+// the radix path do not pay for them.
+int ensure_brec(dmc_queue* q) {
+  if (q->brec) return DMC_OK;
+  HIP_OK(hipMalloc(&q->brec, sizeof(BRecR) * (size_t)kNBR * kBinCapR));
+  return DMC_OK;
 }
 
 int ensure_batch(dmc_queue* q, uint32_t n) {
@@ -1662,6 +1673,7 @@ void launch_future(dmc_queue* q) {
 int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
               int* type, double* when) {
   const Table& tb = q->tb;
+  ++q->ctr.single_steps;
   pb(q, DMC_PROF_STEP);
   hipLaunchKernelGGL(k_step_scan, dim3(q->step_grid), dim3(kBlock), 0, q->stream,
                      tb, now, q->red);
@@ -1861,10 +1873,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       radix = false;
     } else {
       if (q->radix_batches && !retry) --q->radix_batches;
-      if (radix) {
-        rc = ensure_entries(q, q->dense_hint);
-        if (rc) return rc;
-      }
+      rc = radix ? ensure_entries(q, q->dense_hint) : ensure_brec(q);
+      if (rc) return rc;
       rc = launch_round(q, now, kk, d_out + n_dec, dres, radix, !allow);
       if (rc) return rc;
     }
@@ -1903,21 +1913,37 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
                    c.bin_sq, c.overflow, (int)radix, c.dense_n, c.n_pgroups,
                    from_okey(c.ph[1].kmin), from_okey(c.ph[1].kmax),
                    c.ph[1].T ? from_okey(c.ph[1].T) : 0.0, c.now);
+    ++q->ctr.rounds;
+    if (radix) ++q->ctr.radix_rounds;
+    if (!radix && c.bin_max[0] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[0];
+    if (!radix && c.bin_max[1] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[1];
     if (c.overflow == 1) {  // dense entries: grow and retry
+      ++q->ctr.dense_overflows;
       q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
+      // a radix retry of a bin-overflowed round stays a retry: without this
+      // the next round would try the bins again, overflow again, and the
+      // streak would send the following call to the radix path as well
+      retry_radix = retry;
       continue;
     }
     if (c.overflow == 2) {
       // a rank bin outgrew kBinCapR: this round is re-run on the radix path.
       // An isolated skewed round costs only that; massively tied keys
-      // (overflows in a row) keep the next 1, 2, 4, then 8 calls on it
+      // (overflows in a row) keep the next 1, 2, 4, then 8 calls on it.
+      // k_rbscan left the round's emitted-entry total in dense_n: the retry's
+      // dense buffer is sized for it up front.
+      ++q->ctr.bin_overflows;
       retry_radix = true;
-      ++q->ovf_streak;
+      q->dense_hint = std::max(q->dense_hint, pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1));
+      q->ovf_streak = std::min<uint32_t>(q->ovf_streak + 1, 5);
       if (q->ovf_streak > 1)
         q->radix_batches = std::min<uint32_t>(8, 1u << (q->ovf_streak - 2));
       continue;
     }
     if (!radix) q->ovf_streak = 0;
+    q->ctr.candidates += c.n_cand;
+    q->ctr.entries += radix ? c.dense_n : c.n_emit;
+    q->ctr.decisions += c.n_dec;
     n_dec += c.n_dec;
     r.n_priority += c.n_prio;
     r.n_reservation += c.n_dec - c.n_prio;
@@ -2022,7 +2048,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
-  rc |= A(&q->brec, (size_t)kNBR * kBinCapR);
+  // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
+  // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
   rc |= A(&q->acnt, N);
   rc |= A(&q->abuf, (size_t)N * kAddSlots);
@@ -2453,6 +2480,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
            q->use_graphs && !q->prof_on;
     if (fuse) {
       int rc = ensure_batch(q, n);
+      if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       const bool future = q->p.at_limit != DMC_AT_LIMIT_ALLOW;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
@@ -2461,6 +2489,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         enqueue_add(q, ap);
         enqueue_round(q, cp, false, future);
       };
+      ++q->ctr.fused_calls;
       uint64_t key = (4ull << 56) | ((uint64_t)n << 1) | (future ? 1 : 0);
       GraphRec* gr = graph_for(q, key, enqueue, (const void*)k_rscan);
       if (!gr) {
@@ -2628,6 +2657,14 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
     default:
       return DMC_EINVAL;
   }
+}
+
+int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset) {
+  if (!q || !out) return DMC_EINVAL;
+  QueueLock g(q);
+  *out = q->ctr;
+  if (reset) q->ctr = dmc_counters{};
+  return DMC_OK;
 }
 
 int dmc_profile_enable(dmc_queue* q, int on) {

@@ -104,6 +104,7 @@ struct Round {
   unsigned long long dmax[2];  // radix path: largest emitted key per phase
   uint32_t n_cand;       // candidate clients (k_rcand)
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
+  uint32_t n_emit;       // rank records emitted (k_rbscan)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
   unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
@@ -858,11 +859,24 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
          uint32_t* bsoff, uint32_t* bpoff) {
   constexpr int per = kNBR / 1024;
   __shared__ uint32_t wc[16], wz[16], wp[16];
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (rd->bin_ovf) {
-    if (threadIdx.x == 0) rd->overflow = 2;
+    // the round is re-run on the radix path: report how many entries it
+    // emitted (sum of the bin counts, overflowed ones included) so that the
+    // retry's dense buffer is sized for them
+    uint32_t s = 0;
+    for (int j = 0; j < per; ++j) s += bcount[t * per + j];
+    s = wsum32(s);
+    if (lane == 0) wc[w] = s;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t tot = 0;
+      for (int i = 0; i < 16; ++i) tot += wc[i];
+      rd->dense_n = tot;
+      rd->overflow = 2;
+    }
     return;
   }
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
   for (int j = 0; j < per; ++j) {
     uint32_t b = t * per + j;
@@ -945,6 +959,20 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
     rd->n_dec = tz < k ? tz : k;
     rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
     rd->n_pgroups = tp;
+  }
+  {
+    // the round's emitted records (diagnostics: bench.py's bytes model)
+    uint32_t e = 0;
+    for (int j = 0; j < per; ++j) e += c[j];
+    e = wsum32(e);
+    __syncthreads();
+    if (lane == 0) wc[w] = e;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t tot = 0;
+      for (int i = 0; i < 16; ++i) tot += wc[i];
+      rd->n_emit = tot;
+    }
   }
 }
 

@@ -16,8 +16,8 @@ import os
 
 import numpy as np
 
-from ._abi import (DECISION_DTYPE, REQUEST_DTYPE, ClientState, PullResult,
-                   QueueParams, Stats, make_requests)
+from ._abi import (DECISION_DTYPE, REQUEST_DTYPE, ClientState, Counters,
+                   PullResult, QueueParams, Stats, make_requests)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdmclock_gpu.so")
@@ -53,6 +53,7 @@ EXPORTS = {
     "dmc_client_filter": (_i32, [_vp, _u32, _u32, _vp]),
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "dmc_queue_set_option": (_i32, [_vp, _i32, ctypes.c_int64]),
+    "dmc_queue_counters": (_i32, [_vp, ctypes.POINTER(Counters), _i32]),
     "dmc_tracker_tally": (_i32, [_vp, _vp, _vp, _u32, _vp, _vp]),
     "dmc_tracker_fill": (_i32, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp,
                                 _vp]),
@@ -264,6 +265,14 @@ class GpuQueue:
     def set_option(self, option, value):
         _check(self.L.dmc_queue_set_option(self.h, option, int(value)),
                "set_option")
+
+    def counters(self, reset=False):
+        """engine path counters (rounds, radix rounds, overflows, largest
+        rank bin) since creation or the last reset"""
+        c = Counters()
+        _check(self.L.dmc_queue_counters(self.h, ctypes.byref(c), int(reset)),
+               "queue_counters")
+        return c.as_dict()
 
     # ---- stage timers (HIP events on the queue's stream)
     def profile(self, on=True):

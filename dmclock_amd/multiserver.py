@@ -98,15 +98,26 @@ class DeviceTrackers:
 
     def deliver(self, group=None):
         """Epoch boundary: collect, one all-reduce of the per-client sums over
-        the ranks (sum, modular int32), then the global counters advance."""
+        the ranks (sum, modular int32), then the global counters advance.
+        Under RCCL ("nccl") the all-reduce runs on the device buffers over
+        xGMI; under gloo (CPU tests, or ranks sharing one GPU) the sums are
+        staged through host memory."""
         torch = self.torch
         self.collect()
         for q in self.queues:
             q.sync()
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.sum_d, op=dist.ReduceOp.SUM, group=group)
-            dist.all_reduce(self.sum_r, op=dist.ReduceOp.SUM, group=group)
+        if dist.is_available() and dist.is_initialized() and \
+                dist.get_world_size(group) > 1:
+            both = torch.stack([self.sum_d, self.sum_r])
+            if dist.get_backend(group) == "gloo":
+                host = both.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+                both.copy_(host)
+            else:
+                dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
+            self.sum_d.copy_(both[0])
+            self.sum_r.copy_(both[1])
             torch.cuda.synchronize(self.gd.device)
         q0 = self.queues[0]
         _check(self.L.dmc_tracker_advance(q0.h, self.G, _p(self.gd), _p(self.gr),

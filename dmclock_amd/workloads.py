@@ -124,6 +124,64 @@ def churn_trace(seed, n_clients, n_steps, adds_per_step, pulls_per_step,
     return tr
 
 
+def config3_trace(seed, n_clients, n_steps, batch, depth=4, settle=None, t0=1.0):
+    """bench.py's workload (BASELINE config 3) at any client count:
+    bulk-registered clients in the config-3 mix, `depth` requests per client
+    from a Poisson process of 2 req/s per client, a settle pull of depth/2 per
+    client at the pre-population's end, then steps of `batch` adds + `batch`
+    pulls at the step's last arrival."""
+    rng = np.random.default_rng(seed)
+    tab = client_table(rng, n_clients)
+    rate = 2.0 * n_clients
+    tr = Trace(tab, params=dict(seed=seed, config=3))
+    pre = arrivals(rng, n_clients, depth * n_clients, t0, rate)
+    t = float(pre["time"][-1])
+    tr.ops.append(("add", pre))
+    tr.ops.append(("pull", t, depth * n_clients // 2 if settle is None else settle))
+    h = len(pre)
+    for _ in range(n_steps):
+        reqs = arrivals(rng, n_clients, batch, t, rate, handle_base=h)
+        h += batch
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+        tr.ops.append(("pull", t, batch))
+    return tr
+
+
+def config4_trace(seed, n_clients, n_steps, batch, depth=4, idle_frac=0.10,
+                  throttled=0.10):
+    """bench.py --config 4 (BASELINE config 4) at any client count: config 3
+    plus `throttled` of the tenants limited below their arrival rate (l ~
+    U[0.5, 1.5] against 2 req/s, AtLimit::Wait throttles them) and, before
+    every step, do_clean's idle marking of `idle_frac` of all clients drawn
+    from those without an arrival in the two previous steps (their next
+    request re-activates them through the idle reset, :937-985)."""
+    rng = np.random.default_rng(seed)
+    tab = client_table(rng, n_clients)
+    thr = rng.random(n_clients) < throttled
+    tab.l = np.where(thr, rng.uniform(0.5, 1.5, n_clients), tab.l)
+    rate = 2.0 * n_clients
+    tr = Trace(tab, params=dict(seed=seed, config=4))
+    pre = arrivals(rng, n_clients, depth * n_clients, 1.0, rate)
+    t = float(pre["time"][-1])
+    tr.ops.append(("add", pre))
+    tr.ops.append(("pull", t, depth * n_clients // 2))
+    h = len(pre)
+    last = np.full(n_clients, -1, np.int64)
+    for i in range(n_steps):
+        quiet = np.flatnonzero(last < i - 2)
+        m = min(len(quiet), int(idle_frac * n_clients))
+        sel = np.sort(rng.choice(quiet, m, replace=False)).astype(np.uint32)
+        tr.ops.append(("idle", sel))
+        reqs = arrivals(rng, n_clients, batch, t, rate, handle_base=h)
+        h += batch
+        t = float(reqs["time"][-1])
+        last[reqs["slot"]] = i
+        tr.ops.append(("add", reqs))
+        tr.ops.append(("pull", t, batch))
+    return tr
+
+
 def replay(q, trace, check=None):
     """Replay a trace on a queue exposing register/add_batch/pull_batch/
     mark_idle/set_info/update_client_info.  Yields per-op outputs."""
@@ -138,8 +196,11 @@ def replay(q, trace, check=None):
             outs.append(("pull", d, (res.n_decisions, res.next_type,
                                      res.when if res.next_type == 1 else 0.0)))
         elif op[0] == "idle":
-            for s in op[1].tolist():
-                q.mark_idle(s)
+            if hasattr(q, "mark_idle_batch"):
+                q.mark_idle_batch(op[1])
+            else:
+                for s in op[1].tolist():
+                    q.mark_idle(s)
             outs.append(("idle", None))
         elif op[0] == "info":
             _, s, r, w, l = op

@@ -269,6 +269,25 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   host (default 0: all of a batch's activations on the device) */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
+/* Engine path counters since creation (or the last reset): which ranking
+ * path the batched pull rounds took and how often a round was re-run.  No
+ * reference counterpart; for tests and the benchmark's records. */
+typedef struct dmc_counters {
+  uint64_t rounds;          /* batched pull rounds run (re-runs included)          */
+  uint64_t radix_rounds;    /* of which ranked by the radix path                    */
+  uint64_t bin_overflows;   /* rounds aborted by a rank-bin overflow (re-run on the radix path) */
+  uint64_t dense_overflows; /* radix rounds re-run with a larger dense buffer       */
+  uint64_t single_steps;    /* general single pull_request steps                    */
+  uint64_t candidates;      /* candidate clients visited by completed rounds         */
+  uint64_t entries;         /* rank records (bin path) / dense entries (radix path) they emitted */
+  uint64_t decisions;       /* decisions of completed rounds                         */
+  uint64_t graph_replays;   /* captured hipGraphs replayed (add segments, rounds, fused calls) */
+  uint64_t fused_calls;     /* dmc_add_pull_batch_device calls run as one add + round launch */
+  uint32_t max_bin;         /* largest rank bin of a bin-ranked round (records)     */
+  uint32_t reserved;
+} dmc_counters;
+int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
+
 /* ------------------------------------------------------------ profiling
  * Stage timers: HIP events recorded on the queue's stream around each stage
  * of the add and pull pipelines (an extension of this library; the reference

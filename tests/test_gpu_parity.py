@@ -203,15 +203,19 @@ def mk_act(split):
     return mk
 
 
+CHURN_ORACLE_SEEDS = (3, 19)
+
+
 @pytest.mark.parametrize("mode", MODES_ACT, ids=["imm", "delayed", "allow"])
 @pytest.mark.parametrize("seed", [3, 11, 19])
 def test_churn_activations_parity(mode, seed):
     """Many activations per batch (a third of the clients idle before every
     step): the device-resolved idle resets equal the sequential ones (the
     host split, one activation at a time) in every decision and every
-    client's state; and both equal the oracle when its run is tie-free
-    (activations align proportion keys, p + L - t, so ties are frequent and
-    then the heap's history picks)."""
+    client's state; and for seeds 3 and 19, verified tie-free, both equal
+    the oracle (activations align proportion keys, p + L - t, so ties occur
+    -- seed 11 has one -- and then the heap's history picks, SURVEY.md
+    section 7)."""
     from parity import compare_decisions, compare_states
     tr = workloads.churn_trace(seed, 400, 8, 600, 300, idle_frac=0.35,
                                k_choices=[1, 9, 64, 300, 2000])
@@ -228,8 +232,14 @@ def test_churn_activations_parity(mode, seed):
     import pyoracle
     qo = pyoracle.OracleQueue(**mode)
     workloads.replay(qo, tr)
-    if qo.ties == 0:
+    if seed in CHURN_ORACLE_SEEDS:
+        # verified tie-free (checked on the CPU): the oracle leg runs
+        assert qo.ties == 0, (seed, qo.ties)
         run_parity(tr, mk_act(0), mode, state_sample=400)
+    else:
+        # seed 11 has one tied decision under the oracle (the heap's history
+        # picks among equal keys); it stays a device-vs-host-split check
+        assert qo.ties > 0, seed
 
 
 def test_activation_undercut_by_earlier_activation():
@@ -337,40 +347,63 @@ def test_key_range_straddles_zero(seed):
     run_parity(tr, mk_gpu, state_sample=3000)
 
 
-@pytest.mark.parametrize("n", [200, 300, 500, 700])
+@pytest.mark.parametrize("n", [200, 300, 500, 700, 1400])
 def test_tied_rank_bins(n):
     """Massively tied keys put every entry of a round into one rank bin:
     n = 300 and 500 exceed one k_rrank block (multi-pass ranking), n = 700
     exceeds kBinCapR = 512 (the round is re-run on the radix path, then the
-    next call tries the bins again).  The bin-ranked, radix-sorted and
-    single-step engines must give the same decisions bit for bit (ties broken
-    by lowest slot)."""
+    next call tries the bins again), n = 1400 also emits more entries than
+    the radix path's initial dense buffer holds (65,536 after a retry sized
+    from the overflowed round's total, no dense overflow).  The bin-ranked,
+    radix-sorted and single-step engines must give the same decisions bit
+    for bit (ties broken by lowest slot), and the engine counters show which
+    path each round took."""
     from dmclock_amd._abi import REQUEST_DTYPE
+    ctrs = {}
 
     def run(variant):
-        q = mk_variant(variant)(max_clients=1024)
+        q = mk_variant(variant)(max_clients=max(1024, n))
         slots = np.arange(n, dtype=np.uint32)
         q.register_active(slots, np.zeros(n), np.ones(n), np.zeros(n))
         out = []
+        depth = 3 if n <= 700 else 48
         for call in range(3):
-            reqs = np.zeros(3 * n, REQUEST_DTYPE)
-            reqs["slot"] = np.tile(slots, 3)
+            reqs = np.zeros(depth * n, REQUEST_DTYPE)
+            reqs["slot"] = np.tile(slots, depth)
             reqs["cost"] = 1
             reqs["time"] = 1.0 + call
             reqs["delta"] = 1
             reqs["rho"] = 1
-            reqs["handle"] = np.arange(3 * n) + call * 3 * n
+            reqs["handle"] = np.arange(depth * n) + call * depth * n
             rc = q.add_batch(reqs)
             assert (rc == 0).all()
-            d, res = q.pull_batch(10.0 + call, 2 * n + 7)
-            assert res.n_decisions == 2 * n + 7
+            k = 2 * n + 7 if n <= 700 else 40 * n
+            d, res = q.pull_batch(10.0 + call, k)
+            assert res.n_decisions == k
             out.append(d[:res.n_decisions].copy())
+        ctrs[variant] = q.counters()
         q.close()
         return np.concatenate(out)
 
     base = run("default")
+    c = ctrs["default"]
+    print(f"n={n} counters {c}")
+    if n <= 500:
+        # one round's tied entries: ranked in passes (a bin above one k_rrank
+        # block of 256 records), within the 512-record capacity
+        assert c["bin_overflows"] == 0, c
+        if n >= 300:
+            assert c["max_bin"] > 256, c
+    else:
+        # a bin overflows and the round is re-run on the radix path; the
+        # retry is sized from the overflowed round: no dense overflow
+        assert c["bin_overflows"] >= 1, c
+        assert c["radix_rounds"] >= c["bin_overflows"], c
+        assert c["dense_overflows"] == 0, c
     assert (base["flags"] != 0).mean() > 0.5  # tied and flagged
     assert base.tobytes() == run("radix").tobytes()
+    if n > 700:
+        return  # the single-step variant would take 40 x n general steps
     # single steps flag a tie among the fronts of one pull, not a round's
     # entries: every other field must match
     steps = run("steps")

@@ -191,3 +191,135 @@ def test_device_trackers_and_multiserver_parity():
         for f in ("gd", "gr", "xd", "xr", "known"):
             assert np.array_equal(st[f], getattr(et, f)), f
     assert n_dec > 1000
+
+
+# ---------------------------------------------------- world size 2 on the GPU
+W2 = dict(S_total=4, N=300, G=500, epochs=5, per_server=250, k=200, seed=9)
+
+
+def _w2_workload():
+    """the same global workload in every process: maps, table, batches"""
+    rng = np.random.default_rng(W2["seed"])
+    cmap = client_maps(rng, W2["S_total"], W2["N"], W2["G"])
+    tab = workloads.client_table(rng, W2["N"])
+    eps = epoch_batches(rng, W2["S_total"], W2["N"], W2["epochs"], W2["per_server"])
+    return cmap, tab, eps
+
+
+def _device_trackers_worker(rank, world, port, out_q):
+    """One rank: servers [rank * S, (rank + 1) * S) as GPU queues on cuda:0
+    with DeviceTrackers, the per-epoch delivery all-reducing over gloo (the
+    product's DeviceTrackers.deliver, host-staged)."""
+    import torch
+    import torch.distributed as dist
+    from dmclock_amd._abi import PullResult
+    from dmclock_amd.multiserver import DeviceTrackers, make_queues
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        cmap, tab, eps = _w2_workload()
+        S = W2["S_total"] // world
+        mine = list(range(rank * S, (rank + 1) * S))
+        qg = make_queues(S, W2["N"], device=0, ring_capacity=64)
+        for q in qg:
+            q.register(tab.slots, tab.r, tab.w, tab.l, True)
+        dt = DeviceTrackers(qg, W2["N"], dev, n_clients=W2["G"],
+                            client_of_slot=cmap[mine])
+        decs = []
+        k = W2["k"]
+        for t, ep in eps:
+            for j, s in enumerate(mine):
+                reqs = ep[s].copy()
+                d_reqs = torch.from_numpy(reqs.view(np.uint8)).to(dev)
+                torch.cuda.synchronize()
+                dt.fill(j, d_reqs.data_ptr(), len(reqs))
+                qg[j].sync()
+                got = d_reqs.cpu().numpy().view(REQUEST_DTYPE).copy()
+                rc = qg[j].add_batch(got)
+                assert (rc == 0).all()
+                decs.append(("req", s, got["delta"].copy(), got["rho"].copy()))
+            for j, s in enumerate(mine):
+                d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8,
+                                    device=dev)
+                d_res = torch.zeros(24, dtype=torch.uint8, device=dev)
+                torch.cuda.synchronize()
+                qg[j].pull_batch_device(t, k, d_out.data_ptr(), d_res.data_ptr())
+                dt.tally(j, d_out.data_ptr(), d_res.data_ptr(), k)
+                qg[j].sync()
+                res = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+                dg = d_out.cpu().numpy().view(DECISION_DTYPE)[:res.n_decisions].copy()
+                decs.append(("dec", s, dg))
+            dt.deliver()
+        st = dt.state()
+        out_q.put((rank, st, decs))
+        for q in qg:
+            q.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_device_trackers_world2_gloo():
+    """Two ranks sharing GPU 0, two server queues each, device trackers with
+    the per-epoch all-reduce of DeviceTrackers.deliver over gloo: every
+    request's delta/rho, every decision and the final tracker state equal one
+    process running all four oracle queues with the epoch restatement."""
+    import torch.multiprocessing as mp
+    from parity import compare_decisions
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_device_trackers_worker, args=(r, 2, port, out_q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            rank, st, decs = out_q.get(timeout=240)
+            res[rank] = (st, decs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    # one process: all four servers on the oracle, epoch restatement
+    cmap, tab, eps = _w2_workload()
+    S_total, N, G, k = W2["S_total"], W2["N"], W2["G"], W2["k"]
+    qo = [pyoracle.OracleQueue() for _ in range(S_total)]
+    for q in qo:
+        q.register(tab.slots, tab.r, tab.w, tab.l, True)
+    et = EpochTrackers(S_total, N, G, cmap)
+    want = {}
+    for e, (t, ep) in enumerate(eps):
+        for s in range(S_total):
+            reqs = ep[s].copy()
+            et.fill(s, reqs)
+            want[("req", e, s)] = (reqs["delta"].copy(), reqs["rho"].copy())
+            assert (qo[s].add_batch(reqs) == 0).all()
+        for s in range(S_total):
+            do, _ = qo[s].pull_batch(t, k)
+            et.tally(s, do)
+            want[("dec", e, s)] = do
+        et.deliver()
+    n_dec = 0
+    for rank, (st, decs) in res.items():
+        S = S_total // 2
+        it = iter(decs)
+        for e in range(len(eps)):
+            for _ in range(S):
+                kind, s, d, r = next(it)
+                wd, wr = want[("req", e, s)]
+                assert np.array_equal(d, wd) and np.array_equal(r, wr), (rank, e, s)
+            for _ in range(S):
+                kind, s, dg = next(it)
+                compare_decisions(dg, want[("dec", e, s)], f"rank {rank} epoch {e} server {s}")
+                n_dec += len(dg)
+        assert np.array_equal(st["gd"], et.gd) and np.array_equal(st["gr"], et.gr)
+        sl = slice(rank * S, (rank + 1) * S)
+        for f in ("xd", "xr", "known"):
+            assert np.array_equal(st[f], getattr(et, f)[sl]), (rank, f)
+    assert n_dec > 1000
