@@ -349,12 +349,13 @@ def test_key_range_straddles_zero(seed):
 
 @pytest.mark.parametrize("n", [200, 300, 500, 700, 1400])
 def test_tied_rank_bins(n):
-    """Massively tied keys put every entry of a round into one rank bin:
-    n = 300 and 500 exceed one k_rrank block (multi-pass ranking), n = 700
-    exceeds kBinCapR = 512 (the round is re-run on the radix path, then the
-    next call tries the bins again), n = 1400 also emits more entries than
-    the radix path's initial dense buffer holds (65,536 after a retry sized
-    from the overflowed round's total, no dense overflow).  The bin-ranked,
+    """Massively tied keys put a round's entries into two rank bins (the tied
+    first keys, and every later entry in the last bin): n = 200's first call
+    ranks a 400-record bin in passes (above one k_rrank block of 256); bins
+    past kBinCapR = 512 abort the round, which is re-run on the radix path
+    (then the next call tries the bins again); n = 1400 also emits more
+    entries than the radix path's initial dense buffer holds (65,536; the
+    retry is sized from the overflowed round's total, no dense overflow).  The bin-ranked,
     radix-sorted and single-step engines must give the same decisions bit
     for bit (ties broken by lowest slot), and the engine counters show which
     path each round took."""
@@ -388,18 +389,18 @@ def test_tied_rank_bins(n):
     base = run("default")
     c = ctrs["default"]
     print(f"n={n} counters {c}")
-    if n <= 500:
-        # one round's tied entries: ranked in passes (a bin above one k_rrank
-        # block of 256 records), within the 512-record capacity
-        assert c["bin_overflows"] == 0, c
-        if n >= 300:
-            assert c["max_bin"] > 256, c
-    else:
-        # a bin overflows and the round is re-run on the radix path; the
-        # retry is sized from the overflowed round: no dense overflow
-        assert c["bin_overflows"] >= 1, c
-        assert c["radix_rounds"] >= c["bin_overflows"], c
-        assert c["dense_overflows"] == 0, c
+    # the first keys tie in one bin and every later entry lands in the last
+    # rank bin of the threshold's histogram bin: as the queues deepen over
+    # the three calls that bin outgrows its 512 records and the round is
+    # re-run on the radix path, its dense buffer sized from the overflowed
+    # round (no dense overflow)
+    assert c["bin_overflows"] >= 1, c
+    assert c["radix_rounds"] >= c["bin_overflows"], c
+    assert c["dense_overflows"] == 0, c
+    if n == 200:
+        # the first call's last bin holds 400 records: ranked in passes of
+        # one record per thread (above one k_rrank block of 256)
+        assert c["max_bin"] > 256, c
     assert (base["flags"] != 0).mean() > 0.5  # tied and flagged
     assert base.tobytes() == run("radix").tobytes()
     if n > 700:
