@@ -1043,7 +1043,7 @@ struct dmc_queue {
   uint32_t n_idle = 0;
   uint64_t tick = 0;
   // device scratch
-  uint32_t* cand = nullptr;   // N: candidate slots of the round
+  CandRec* cand = nullptr;    // N: candidates of the round (k_remit)
   uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
   uint8_t* mr = nullptr;      // N: R prefix length
   RoundPart* rparts = nullptr; // k_rscan's per-block partials
@@ -1055,7 +1055,10 @@ struct dmc_queue {
   uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
   uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin tables (k_rpick)
-  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters
+  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics)
+  uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
+  uint32_t* hist_done = nullptr;  // k_rhist's block ticket counter
+  uint32_t* emit_done = nullptr;  // k_remit's block ticket counter
   uint32_t *bsoff = nullptr, *bpoff = nullptr;   // their prefixes (k_rbscan)
   BRecR* brec = nullptr;      // kNBR * kBinCapR rank-bin records
   StepRed* red = nullptr;     // step partials (grid) + future record
@@ -1717,33 +1720,24 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   pb(q, DMC_PROF_SELECT);
   hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
                      (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const RoundPart*)q->rparts, gN, q->rd, q->hist);
-  hipLaunchKernelGGL(k_rpick, dim3(2), dim3(kPickThreadsR), 0, q->stream, q->rd,
-                     q->hist, q->sbase, q->snum);
-  pe(q);
-  pb(q, DMC_PROF_CAND);
-  hipLaunchKernelGGL(k_rcand, dim3((N + kCandChunk - 1) / kCandChunk), dim3(kCandThreads), 0, q->stream,
-                     tb, q->rd, (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     q->cand);
+                     (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbase, q->snum,
+                     q->hist_done);
   pe(q);
   pb(q, DMC_PROF_EMIT);
-  hipLaunchKernelGGL(k_remit, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
-                     (const uint32_t*)q->cand,
-                     (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const uint8_t*)q->mr, radix ? nullptr : q->brec, q->bcount,
-                     q->bsize, (const uint32_t*)q->sbase, (const uint32_t*)q->snum,
-                     q->dense, q->ecap);
+  hipLaunchKernelGGL(k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk), dim3(kEmitThreads),
+                     0, q->stream, tb, q->rd, (const uint64_t*)q->keyr,
+                     (const uint64_t*)q->keyp, (const uint8_t*)q->mr, q->cand,
+                     radix ? nullptr : q->brec, q->bcount, q->bsize,
+                     (const uint32_t*)q->sbase, (const uint32_t*)q->snum, q->dense,
+                     q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done);
   pe(q);
   if (!radix) {
     pb(q, DMC_PROF_RANK);
-    hipLaunchKernelGGL(k_rbscan, dim3(1), dim3(1024), 0, q->stream, q->rd,
-                       (const uint32_t*)q->bcount, (const uint32_t*)q->bsize,
-                       q->bsoff, q->bpoff);
     if (q->debug)
-      (void)hipMemcpyAsync(q->dbg_bins, q->bcount, kNBR * sizeof(uint32_t),
+      (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
     hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
-                       q->rd, (const uint32_t*)q->bcount, (const uint32_t*)q->bsoff,
+                       q->rd, (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff,
                        (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
                        q->debug ? q->dbg_wtime : nullptr);
     pe(q);
@@ -1779,8 +1773,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   }
   pb(q, DMC_PROF_APPLY);
   hipLaunchKernelGGL(k_rapply, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
-                     (const uint32_t*)q->cand, q->bcount, q->bsize, q->sched,
-                     q->debug ? q->dbg_atime : nullptr);
+                     (const CandRec*)q->cand, q->sched, q->debug ? q->dbg_atime : nullptr);
   pe(q);
   if (future)
     launch_future(q);  // its decide kernel ends the round
@@ -2043,6 +2036,9 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
   rc |= A(&q->bcount, kNBR);
   rc |= A(&q->bsize, kNBR);
+  rc |= A(&q->bcnt, kNBR);
+  rc |= A(&q->hist_done, 1);
+  rc |= A(&q->emit_done, 1);
   rc |= A(&q->bsoff, kNBR);
   rc |= A(&q->bpoff, kNBR);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
@@ -2092,7 +2088,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
                   q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
-                  q->snum, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->snum, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,

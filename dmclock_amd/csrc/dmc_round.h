@@ -25,13 +25,14 @@
 //             pending limit-scan mark; per-block counts and key ranges
 //             (the graph's parameter node: publishes the call's parameters)
 //   k_rhist   the round's totals; key histograms of both phases (2048 bins
-//             each, over the exact key ranges, flushed into kShards shards)
-//   k_rpick   two blocks: thresholds T_R / T_P (every key <= T is a candidate,
-//             at least the needed number of keys are <= T) and the rank-bin
-//             tables (R bins [0, kNBPhase), P bins [kNBPhase, kNBR))
-//   k_rcand   compacts the candidate slots, settles the others' pending marks
-//   k_remit   candidates enumerate their entries into rank bins
-//   k_rbscan  one block: prefix sums of the rank-bin sizes, decision count
+//             each, over the exact key ranges, flushed into kShards shards);
+//             its last block: thresholds T_R / T_P (every key <= T is a
+//             candidate, at least the needed number of keys are <= T) and the
+//             rank-bin tables (R bins [0, kNBPhase), P bins [kNBPhase, kNBR))
+//   k_remit   candidates (first key <= T) selected and compacted per wave,
+//             the others' pending marks settled; candidates enumerate their
+//             entries into rank bins; its last block: the bins' prefix sums,
+//             the decision count
 //   k_rrank   one block per rank bin: rank in LDS, decide, stamp the ring entries
 //   k_rapply  replays each candidate's dispatched pops with the same
 //             arithmetic, writes the decision records and the new state
@@ -414,10 +415,15 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // iteration with every key load issued before the first LDS atomic; the
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
+constexpr int kPickThreadsR = 1024;
+__device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
+                          uint32_t* sbase, uint32_t* snum);
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist) {
+        uint32_t nparts, Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum,
+        uint32_t* done) {
   __shared__ uint32_t lh[2][kHistBinsR];
+  __shared__ uint32_t s_last;
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
     lh[0][b] = 0;
     lh[1][b] = 0;
@@ -450,27 +456,39 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
     rd->n_r = tot.n_r;
     rd->p_runs = p_runs ? 1 : 0;
   }
-  if (tot.cnt[0] == 0 && tot.cnt[1] == 0) return;
-  const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
-  const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
-  const uint32_t sh1 = hist_shift_r(m1(tot.mx[1]));
-  for (; s < n; s += stride) {
+  if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
+    const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
+    const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
+    const uint32_t sh1 = hist_shift_r(m1(tot.mx[1]));
+    for (; s < n; s += stride) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(m0(kr[j]), 0, sh0)], 1u);
-      if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(m1(kp[j]), 0, sh1)], 1u);
+      for (int j = 0; j < 4; ++j) {
+        if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(m0(kr[j]), 0, sh0)], 1u);
+        if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(m1(kp[j]), 0, sh1)], 1u);
+      }
+      if (s + stride < n) load(s + stride);
     }
-    if (s + stride < n) load(s + stride);
+    __syncthreads();
+    uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
+    for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
+      if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
+      if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
+    }
   }
+  // ticket: the block's histogram atomics have completed (every wave waits
+  // for its own) before one lane takes it; the last block picks.  Only
+  // memory-side atomics cross blocks here (the shards, the ticket), so no
+  // release / acquire fence is needed (MI355X_MICROARCH.md, inter-workgroup
+  // visibility: nothing this kernel hands over sits in an L2)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
-  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
-    if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
-    if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
-  }
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) atomicExch(done, 0u);  // ready for the next round
+  pick_both(rd, tot, hist, sbase, snum);
 }
 
-constexpr int kPickThreadsR = 1024;
 constexpr int kBinsPerThreadR = kHistBinsR / kPickThreadsR;
 
 __device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
@@ -508,12 +526,20 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     *s_C = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
   }
+  // the shards were filled by every k_rhist block with device-scope atomics
+  // (performed at the memory side): read them the same way, clearing them
+  // for the next round in the same operation (no plain load can see a stale
+  // L2 line of another XCD's, and no plain store is left to write back)
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0;
   for (int j = 0; j < kBinsPerThreadR; ++j) {
+    uint32_t v[kShards];
+#pragma unroll
+    for (int i = 0; i < kShards; ++i)
+      v[i] = atomicExch(&hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j], 0u);
     h[j] = 0;
 #pragma unroll
-    for (int i = 0; i < kShards; ++i) h[j] += hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
+    for (int i = 0; i < kShards; ++i) h[j] += v[i];
     local += h[j];
   }
   uint32_t before = block_excl_scan_r(local, wsum);
@@ -560,8 +586,6 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     sbase[p * kHistBinsR + b] = p * kNBPhase + nb;
     snum[p * kHistBinsR + b] = ns[j];
     nb += ns[j];
-#pragma unroll
-    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + b] = 0;
   }
   if (t == 0) {
     PhaseSel z{};
@@ -584,24 +608,25 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
 }
 
 
-// Thresholds and rank-bin tables: two blocks, one per phase.
-__global__ void __launch_bounds__(kPickThreadsR)
-k_rpick(Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum) {
+// Thresholds and rank-bin tables of both phases, by the last k_rhist block
+// (1024 threads), one phase after the other.
+__device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
+                          uint32_t* sbase, uint32_t* snum) {
   __shared__ uint32_t wsum[kPickThreadsR / 64];
   __shared__ uint32_t s_tb, s_C;
   __shared__ uint64_t s_T;
-  const RoundPart tot = rd->tot;
-  const int p = blockIdx.x;
-  uint32_t k = rd->k_total;
-  bool p_runs = rd->p_runs;
-  // R: all prefixes when they hold fewer than k entries; else every client
-  // whose first key is at or below the k-th smallest first key's bucket
-  // (each such client contributes at least one entry <= T).  P: the rest.
-  uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
-                         : (p_runs ? k - (uint32_t)tot.n_r : 0);
-  const KeyMap km(tot.mn[p], tot.mx[p]);
-  const HistRange h{0, hist_shift_r(km(tot.mx[p])), 0};
-  pick_phase(p, need, tot, km, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
+  const uint32_t k = rd->k_total;
+  const bool p_runs = tot.n_r < (uint64_t)k;
+  for (int p = 0; p < 2; ++p) {
+    // R: all prefixes when they hold fewer than k entries; else every client
+    // whose first key is at or below the k-th smallest first key's bucket
+    // (each such client contributes at least one entry <= T).  P: the rest.
+    uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
+                           : (p_runs ? k - (uint32_t)tot.n_r : 0);
+    const KeyMap km(tot.mn[p], tot.mx[p]);
+    const HistRange h{0, hist_shift_r(km(tot.mx[p])), 0};
+    pick_phase(p, need, tot, km, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
+  }
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -672,7 +697,7 @@ struct EmitV {
       if (at < kBinCapR)
         brec[(size_t)b * kBinCapR + at] = BRecR{key, slot, pos, run, ridx};
       else
-        rd->bin_ovf = 1;
+        atomicOr(&rd->bin_ovf, 1u);  // read by the last block (memory side)
     } else {
       // wave-aggregated: one counter add and one max per phase per wave
       // (massively tied rounds emit every entry here; per-entry atomics on
@@ -722,99 +747,29 @@ __device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
   return CandPred(rd)(kr, kp);
 }
 
-// ---------------------------------------------------------------- k_rcand
-// Candidates compacted into a dense list, so that the walking kernels run
-// dense waves: blocks of kCandThreads own kCandChunk consecutive slots, 4 per
-// thread with every load issued up front, one atomic per block (list order
-// is irrelevant: the ranking fixes the order).  The same pass settles the
-// pending limit-scan marks of every non-candidate (k_rapply settles the
-// candidates').
-constexpr int kCandThreads = 1024;
-constexpr uint32_t kCandChunk = kCandThreads * 4;
-__global__ void __launch_bounds__(kCandThreads)
-k_rcand(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
-        uint32_t* cand) {
-  __shared__ uint32_t wsum[kCandThreads / 64];
-  __shared__ uint32_t base;
-  const uint32_t n = tb.n;
-  const uint32_t s0 = blockIdx.x * kCandChunk + threadIdx.x * 4;
-  const CandPred pred(rd);
-  const bool p_runs = rd->p_runs != 0;
-  uint64_t kr[4], kp[4];
-  uint8_t f[4];
-  if (s0 + 4 <= n) {
-    const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
-    const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
-    ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
-    uchar4 f4 = *reinterpret_cast<const uchar4*>(tb.flags + s0);
-    kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
-    kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
-    f[0] = f4.x; f[1] = f4.y; f[2] = f4.z; f[3] = f4.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bool in = s0 + j < n;
-      kr[j] = in ? keyr[s0 + j] : kMaxKey;
-      kp[j] = in ? keyp[s0 + j] : kMaxKey;
-      f[j] = in ? tb.flags[s0 + j] : 0;
-    }
-  }
-  uint32_t bits = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (s0 + j >= n) continue;
-    if (pred(kr[j], kp[j])) {
-      bits |= 1u << j;
-    } else if (f[j] & F_PMARK) {
-      tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
-    }
-  }
-  const uint32_t c = __popc(bits);
-  uint32_t incl = c;
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t wb = 0, tot = 0;
-  for (int i = 0; i < kCandThreads / 64; ++i) {
-    if (i < w) wb += wsum[i];
-    tot += wsum[i];
-  }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(&rd->n_cand, tot) : 0;
-  __syncthreads();
-  uint32_t o = base + wb + incl - c;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (bits & (1u << j)) cand[o++] = s0 + j;
-}
-
-__device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
-                                const uint64_t* keyr, const uint64_t* keyp,
-                                const uint8_t* mr, BRecR* brec,
+// One candidate's entries: R pops with r <= min(now, T_R); then, if the
+// priority pulls run, the P groups with key <= T_P from the post-R state.
+// cr / cp: its first R / P key is at or below the threshold; m: its R-prefix
+// length (k_rscan); f0: its flags.  Bin-rank path: into the rank bins; radix
+// path: appended to the dense entry list.
+__device__ inline void emit_one(const Table& tb, Round* rd, uint32_t s, bool cr,
+                                bool cp, uint32_t m, uint8_t f0, BRecR* brec,
                                 uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbase, const uint32_t* snum,
                                 DEnt* dense, uint32_t dcap) {
   const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
-  uint64_t kr = keyr[s], kp = keyp[s];
-  bool cr = TR && kr <= TR;
-  bool cp = rd->p_runs && TP && kp <= TP;
-  if (!cr && !cp) return;
   const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
   const CView cv = load_view(tb, s);
   const uint32_t h = cv.h;
-  const uint8_t f0 = tb.flags[s];
   if (cr) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
     walk_r(tb, s, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
   if (cp) {
-    uint32_t m = mr[s];  // the priority pulls run only after every R pop
+    // the priority pulls run only after every R pop
     bool ready0 = m == 0 && (f0 & F_READY);
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
@@ -823,69 +778,38 @@ __device__ inline void emit_one(Table tb, Round* rd, uint32_t s,
   }
 }
 
-// ---------------------------------------------------------------- k_remit
-// Candidates (first key <= T) enumerate their entries: R pops with
-// r <= min(now, T_R); then, if the priority pulls run, the P groups with key
-// <= T_P from the post-R state.  Bin-rank path: into the rank bins; radix
-// path: appended to the dense entry list.
-#ifndef DMC_EMIT_MINB
-#define DMC_EMIT_MINB 1
-#endif
-__global__ void __launch_bounds__(kBlockR, DMC_EMIT_MINB)
-k_remit(Table tb, Round* rd, const uint32_t* cand, const uint64_t* keyr,
-        const uint64_t* keyp, const uint8_t* mr, BRecR* brec, uint32_t* bcount,
-        uint32_t* bsize, const uint32_t* sbase, const uint32_t* snum,
-        DEnt* dense, uint32_t dcap) {
-  const uint32_t nc = rd->n_cand;
-  for (uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x; ci < nc;
-       ci += gridDim.x * blockDim.x)
-    emit_one(tb, rd, cand[ci], keyr, keyp, mr, brec, bcount, bsize, sbase, snum,
-             dense, dcap);
-}
+// A candidate as compacted by k_remit: slot, its first-key predicates
+// (bit 0: R, bit 1: P), R-prefix length and flags.
+struct CandRec {
+  uint32_t slot;
+  uint8_t bits, m, f, pad;
+};
 
-// ---------------------------------------------------------------- k_rrank
-// One wave per rank bin ranks it in LDS by (okey, slot, position); R bins
-// precede P bins, so the decision offset of an entry is the sum of the group
-// sizes (1 for R pops, 1 + run for P groups) of all earlier bins plus those
-// of its own bin that precede it.  Each block first sums the counts and sizes
-// of all earlier bins.  Decides: entry ids slot * q + position get their
-// decision offset (eoff) and tie flag, stamped into the ring entry (the
-// priority pop's entry for a P group).
-// one block: exclusive prefixes over the rank bins of the entry counts, the
-// group sizes and the P-group counts; the round's decision count and
-// terminal flag.  A rank bin past kBinCapR aborts the round (overflow = 2).
-__global__ void __launch_bounds__(1024)
-k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
-         uint32_t* bsoff, uint32_t* bpoff) {
+// Exclusive prefixes over the rank bins of the record counts, the group
+// sizes and the P-group counts; the round's decision count and terminal
+// flag; diagnostics.  Run by the last k_remit block (1024 threads) over the
+// counters every block filled with memory-side atomics, read and cleared the
+// same way (atomicExch).  A rank bin past kBinCapR aborts the round
+// (overflow = 2): the host re-runs it on the radix path.
+__device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
+                           uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff) {
   constexpr int per = kNBR / 1024;
   __shared__ uint32_t wc[16], wz[16], wp[16];
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (rd->bin_ovf) {
-    // the round is re-run on the radix path: report how many entries it
-    // emitted (sum of the bin counts, overflowed ones included) so that the
-    // retry's dense buffer is sized for them
-    uint32_t s = 0;
-    for (int j = 0; j < per; ++j) s += bcount[t * per + j];
-    s = wsum32(s);
-    if (lane == 0) wc[w] = s;
-    __syncthreads();
-    if (t == 0) {
-      uint32_t tot = 0;
-      for (int i = 0; i < 16; ++i) tot += wc[i];
-      rd->dense_n = tot;
-      rd->overflow = 2;
-    }
-    return;
-  }
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
+#pragma unroll
   for (int j = 0; j < per; ++j) {
-    uint32_t b = t * per + j;
-    c[j] = bcount[b];
-    z[j] = bsize[b];
+    const uint32_t b = t * per + j;
+    c[j] = atomicExch(&bcount[b], 0u);
+    z[j] = atomicExch(&bsize[b], 0u);
+  }
+  for (int j = 0; j < per; ++j) {
+    const uint32_t b = t * per + j;
     lc += c[j];
     lz += z[j];
     lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
   }
+  const bool ovf = atomicOr(&rd->bin_ovf, 0u) != 0;
   uint32_t ic = lc, iz = lz, ip = lp;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d);
@@ -901,20 +825,33 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
     wp[w] = ip;
   }
   __syncthreads();
-  uint32_t bc = 0, bz = 0, bp = 0, tz = 0, tp = 0;
+  uint32_t bc = 0, bz = 0, bp = 0, tc = 0, tz = 0, tp = 0;
   for (int i = 0; i < 16; ++i) {
     if (i < w) {
       bc += wc[i];
       bz += wz[i];
       bp += wp[i];
     }
+    tc += wc[i];
     tz += wz[i];
     tp += wp[i];
+  }
+  if (ovf) {
+    // the round is re-run on the radix path: report how many entries it
+    // emitted (the bin counts, overflowed ones included) so that the retry's
+    // dense buffer is sized for them
+    if (t == 0) {
+      rd->bin_ovf = 0;
+      rd->dense_n = tc;
+      rd->overflow = 2;
+    }
+    return;
   }
   uint32_t oz = bz + iz - lz, op = bp + ip - lp;
   (void)bc;
   for (int j = 0; j < per; ++j) {
-    uint32_t b = t * per + j;
+    const uint32_t b = t * per + j;
+    bcnt[b] = c[j];
     bsoff[b] = oz;
     bpoff[b] = op;
     oz += z[j];
@@ -922,59 +859,142 @@ k_rbscan(Round* rd, const uint32_t* bcount, const uint32_t* bsize,
   }
   // diagnostics: largest bin per phase, sum of squared bin counts (the rank
   // pass's work), reduced through the wave partial slots
-  {
-    uint32_t mx = 0;
-    unsigned long long sq = 0;
-    for (int j = 0; j < per; ++j) {
-      mx = c[j] > mx ? c[j] : mx;
-      sq += (unsigned long long)c[j] * c[j];
-    }
-    for (int d = 32; d > 0; d >>= 1) {
-      uint32_t o = __shfl_down(mx, d);
-      mx = o > mx ? o : mx;
-      sq += shfl_down_u64r(sq, d);
-    }
-    __syncthreads();
-    if (lane == 0) {
-      wc[w] = mx;
-      wz[w] = (uint32_t)sq;
-      wp[w] = (uint32_t)(sq >> 32);
-    }
-    __syncthreads();
-    if (t == 0) {
-      uint32_t m0 = 0, m1 = 0;
-      unsigned long long S = 0;
-      for (int i = 0; i < 16; ++i) {
-        if (i < 8) m0 = wc[i] > m0 ? wc[i] : m0;  // threads 0..511: R bins
-        else m1 = wc[i] > m1 ? wc[i] : m1;
-        S += ((unsigned long long)wp[i] << 32) | wz[i];
-      }
-      rd->bin_max[0] = m0;
-      rd->bin_max[1] = m1;
-      rd->bin_sq = S;
-    }
+  uint32_t mx = 0;
+  unsigned long long sq = 0;
+  for (int j = 0; j < per; ++j) {
+    mx = c[j] > mx ? c[j] : mx;
+    sq += (unsigned long long)c[j] * c[j];
   }
+  for (int d = 32; d > 0; d >>= 1) {
+    uint32_t o = __shfl_down(mx, d);
+    mx = o > mx ? o : mx;
+    sq += shfl_down_u64r(sq, d);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    wc[w] = mx;
+    wz[w] = (uint32_t)sq;
+    wp[w] = (uint32_t)(sq >> 32);
+  }
+  __syncthreads();
   if (t == 0) {
-    uint32_t k = rd->k_total;
+    uint32_t m0 = 0, m1 = 0;
+    unsigned long long S = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (i < 8) m0 = wc[i] > m0 ? wc[i] : m0;  // threads 0..511: R bins
+      else m1 = wc[i] > m1 ? wc[i] : m1;
+      S += ((unsigned long long)wp[i] << 32) | wz[i];
+    }
+    rd->bin_max[0] = m0;
+    rd->bin_max[1] = m1;
+    rd->bin_sq = S;
+    const uint32_t k = rd->k_total;
     rd->n_dec = tz < k ? tz : k;
     rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
     rd->n_pgroups = tp;
-  }
-  {
-    // the round's emitted records (diagnostics: bench.py's bytes model)
-    uint32_t e = 0;
-    for (int j = 0; j < per; ++j) e += c[j];
-    e = wsum32(e);
-    __syncthreads();
-    if (lane == 0) wc[w] = e;
-    __syncthreads();
-    if (t == 0) {
-      uint32_t tot = 0;
-      for (int i = 0; i < 16; ++i) tot += wc[i];
-      rd->n_emit = tot;
-    }
+    rd->n_emit = tc;
   }
 }
+
+// ---------------------------------------------------------------- k_remit
+// Candidate selection and emission in one pass over the client table:
+// blocks of kEmitThreads own kEmitChunk consecutive slots, 4 per thread,
+// with the first keys, R-prefix lengths and flags loaded coalesced.  A slot
+// is a candidate iff its first R key is <= T_R or (the priority pulls run
+// and) its first P key is <= T_P; non-candidates settle their pending
+// limit-scan marks here (k_rapply settles the candidates').  Each wave
+// compacts its candidates (about 17 of its 256 slots in a config-3 round)
+// in LDS, appends them to the candidate list with one atomic, and its lanes
+// walk one candidate each: 16 waves per CU hide each other's dependent
+// loads.  Bin-rank path: the last block to finish computes the rank-bin
+// prefixes (k_rrank's offsets); radix path: entries go to the dense list.
+constexpr int kEmitThreads = 1024;
+constexpr uint32_t kEmitChunk = kEmitThreads * 4;
+__global__ void __launch_bounds__(kEmitThreads)
+k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
+        const uint8_t* mr, CandRec* cand, BRecR* brec, uint32_t* bcount,
+        uint32_t* bsize, const uint32_t* sbase, const uint32_t* snum,
+        DEnt* dense, uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff,
+        uint32_t* bpoff, uint32_t* done) {
+  __shared__ CandRec wl[kEmitThreads / 64][256];
+  __shared__ uint32_t s_last;
+  const uint32_t n = tb.n;
+  const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * 4;
+  const CandPred pred(rd);
+  const bool p_runs = rd->p_runs != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t kr[4], kp[4];
+  uint8_t f[4], m[4];
+  if (s0 + 4 <= n) {
+    const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
+    const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
+    ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
+    uchar4 f4 = *reinterpret_cast<const uchar4*>(tb.flags + s0);
+    uchar4 m4 = *reinterpret_cast<const uchar4*>(mr + s0);
+    kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
+    kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
+    f[0] = f4.x; f[1] = f4.y; f[2] = f4.z; f[3] = f4.w;
+    m[0] = m4.x; m[1] = m4.y; m[2] = m4.z; m[3] = m4.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bool in = s0 + j < n;
+      kr[j] = in ? keyr[s0 + j] : kMaxKey;
+      kp[j] = in ? keyp[s0 + j] : kMaxKey;
+      f[j] = in ? tb.flags[s0 + j] : 0;
+      m[j] = in ? mr[s0 + j] : 0;
+    }
+  }
+  uint32_t cnt = 0;
+  CandRec mine[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (s0 + j >= n) continue;
+    const bool cr = pred.TR && kr[j] <= pred.TR;
+    const bool cp = pred.TP && kp[j] <= pred.TP;
+    if (cr || cp) {
+      mine[cnt++] = CandRec{s0 + j, (uint8_t)((cr ? 1 : 0) | (cp ? 2 : 0)), m[j], f[j], 0};
+    } else if (f[j] & F_PMARK) {
+      tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
+    }
+  }
+  // wave compaction
+  uint32_t incl = cnt;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  const uint32_t wtot = __shfl(incl, 63);
+  for (uint32_t j = 0, o = incl - cnt; j < cnt; ++j, ++o) wl[w][o] = mine[j];
+  uint32_t base = 0;
+  if (lane == 0 && wtot) base = atomicAdd(&rd->n_cand, wtot);
+  base = __shfl(base, 0);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (uint32_t i = lane; i < wtot; i += 64) {
+    const CandRec c = wl[w][i];
+    cand[base + i] = c;
+    emit_one(tb, rd, c.slot, c.bits & 1, (c.bits >> 1) & 1, c.m, c.f, brec, bcount,
+             bsize, sbase, snum, dense, dcap);
+  }
+  if (!brec) return;
+  // ticket (see k_rhist): the last block computes the rank-bin prefixes
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) atomicExch(done, 0u);
+  bin_prefix(rd, bcount, bsize, bcnt, bsoff, bpoff);
+}
+
+// ---------------------------------------------------------------- k_rrank
+// One block per rank bin ranks it in LDS by (okey, slot, position); R bins
+// precede P bins, so the decision offset of an entry is the sum of the group
+// sizes (1 for R pops, 1 + run for P groups) of all earlier bins (bin_prefix)
+// plus those of its own bin that precede it.  Decides: entry ids slot * q +
+// position get their decision offset and tie flag, stamped into the ring
+// entry (the priority pop's entry for a P group).
 
 // Rank of record i of a bin among all `cnt` of them, compared in `parts`
 // slices of `per` records by adjacent lanes whose counts are summed by
@@ -1034,13 +1054,13 @@ __device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
 // branchless (wave-uniform trip counts, broadcast LDS reads).
 constexpr int kRankBlocksR = kNBR;
 __global__ void __launch_bounds__(kBlockR)
-k_rrank(Round* rd, const uint32_t* bcount, const uint32_t* bsoff,
+k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
         const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
         uint64_t* wtime = nullptr) {
   __shared__ BRecR sh[kBinCapR];
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
-  const uint32_t cnt = bcount[b];
+  const uint32_t cnt = bcnt[b];
   if (cnt == 0 || rd->overflow) return;
   const uint32_t k = rd->k_total;
   const uint32_t n_pgroups = rd->n_pgroups;
@@ -1257,7 +1277,7 @@ struct ApplyVP {
 // limit-scanning pull happened (or the round's terminal pull).  Untouched
 // fronts turn their pending mark into F_READY iff the priority pulls ran.
 // Block 0 also counts the round's decisions (sched[0] reservation, sched[1]
-// priority, :1469,1479) and resets the rank-bin counters.
+// priority, :1469,1479).
 // The round's scalars, read once per thread (stores through the table could
 // alias the round record, which would force re-loads inside the walks).
 struct RoundC {
@@ -1269,10 +1289,11 @@ struct RoundC {
   bool p_runs, ovf;
 };
 
-__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) {
+__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
+                                 uint8_t f0) {
   // every load that depends only on the slot is issued before the first
-  // branch: one memory round trip for all of them
-  const uint8_t f0 = tb.flags[s];
+  // branch: one memory round trip for all of them (f0: the flags k_remit
+  // loaded; nothing between the two kernels changes a candidate's flags)
   const CView cv = load_view(tb, s);
   Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   if (rc.ovf) {
@@ -1370,23 +1391,18 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s) 
 // ready flag: a front left by reservation pops only was seen by the round's
 // first limit scan iff the priority pulls ran; one left by priority pops iff
 // a later limit-scanning pull happened (or the round's terminal pull).
-// (Non-candidates settled their pending marks in k_rcand.)  Block 0 also counts the round's decisions (sched[0] reservation,
-// sched[1] priority, :1469,1479) and resets the rank-bin counters.
+// (Non-candidates settled their pending marks in k_remit.)  Block 0 also
+// counts the round's decisions (sched[0] reservation, sched[1] priority,
+// :1469,1479).
 #ifndef DMC_APPLY_MINB
 #define DMC_APPLY_MINB 5
 #endif
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
-k_rapply(Table tb, Round* rd, const uint32_t* cand, uint32_t* bcount,
-         uint32_t* bsize, unsigned long long* sched, uint64_t* dbg = nullptr) {
-  if (blockIdx.x == 0) {
-    for (int b = threadIdx.x; b < kNBR; b += blockDim.x) {
-      bcount[b] = 0;
-      bsize[b] = 0;
-    }
-    if (threadIdx.x == 0 && !rd->overflow) {
-      sched[0] += rd->n_dec - rd->n_prio;
-      sched[1] += rd->n_prio;
-    }
+k_rapply(Table tb, Round* rd, const CandRec* cand, unsigned long long* sched,
+         uint64_t* dbg = nullptr) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow) {
+    sched[0] += rd->n_dec - rd->n_prio;
+    sched[1] += rd->n_prio;
   }
   const uint32_t nc = rd->n_cand;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1395,7 +1411,8 @@ k_rapply(Table tb, Round* rd, const uint32_t* cand, uint32_t* bcount,
                   rd->p_runs != 0, rd->overflow != 0};
   for (uint32_t ci = tid; ci < nc; ci += stride) {
     uint64_t t0 = dbg ? wall_clock64() : 0;
-    apply_one(tb, rc, cand[ci]);
+    const CandRec c = cand[ci];
+    apply_one(tb, rc, c.slot, c.f);
     if (dbg && ci < 262144) {
       dbg[2 * ci] = t0;
       dbg[2 * ci + 1] = wall_clock64();
