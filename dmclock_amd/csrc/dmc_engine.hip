@@ -1054,7 +1054,8 @@ struct dmc_queue {
   HostRound* d_hround = nullptr; // its device address
   uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
-  uint32_t *sbase = nullptr, *snum = nullptr;  // rank-bin tables (k_rpick)
+  uint32_t* sbn = nullptr;    // rank-bin table per phase and histogram bin (k_rhist's pick)
+  uint16_t* hc = nullptr;     // N: ring head | count << 8 as k_rscan saw them
   uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics)
   uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
   uint32_t* hist_done = nullptr;  // k_rhist's block ticket counter
@@ -1715,21 +1716,21 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
   pb(q, DMC_PROF_SCAN);
   hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
-                     q->keyp, q->mr, q->rparts, q->rd, cp);
+                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp);
   pe(q);
   pb(q, DMC_PROF_SELECT);
   hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
                      (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbase, q->snum,
+                     (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn,
                      q->hist_done);
   pe(q);
   pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk), dim3(kEmitThreads),
                      0, q->stream, tb, q->rd, (const uint64_t*)q->keyr,
-                     (const uint64_t*)q->keyp, (const uint8_t*)q->mr, q->cand,
-                     radix ? nullptr : q->brec, q->bcount, q->bsize,
-                     (const uint32_t*)q->sbase, (const uint32_t*)q->snum, q->dense,
-                     q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done);
+                     (const uint64_t*)q->keyp, (const uint8_t*)q->mr,
+                     (const uint16_t*)q->hc, q->cand, radix ? nullptr : q->brec,
+                     q->bcount, q->bsize, (const uint32_t*)q->sbn, q->dense, q->ecap,
+                     q->bcnt, q->bsoff, q->bpoff, q->emit_done);
   pe(q);
   if (!radix) {
     pb(q, DMC_PROF_RANK);
@@ -1794,7 +1795,7 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
     return DMC_OK;
   }
   Table tb = q->tb;
-  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->rparts, &q->rd, &cp};
+  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp};
   return graph_replay(q, *g, args);
 }
 
@@ -1910,6 +1911,12 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (radix) ++q->ctr.radix_rounds;
     if (!radix && c.bin_max[0] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[0];
     if (!radix && c.bin_max[1] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[1];
+#ifdef DMC_TAIL_TIMING
+    if (q->debug)
+      std::fprintf(stderr, "dmc tails (us): hist body %.2f pick %.2f | emit body %.2f prefix %.2f\n",
+                   (c.tdbg[1] - c.tdbg[0]) / 100.0, (c.tdbg[2] - c.tdbg[1]) / 100.0,
+                   (c.tdbg[4] - c.tdbg[3]) / 100.0, (c.tdbg[5] - c.tdbg[4]) / 100.0);
+#endif
     if (c.overflow == 1) {  // dense entries: grow and retry
       ++q->ctr.dense_overflows;
       q->dense_hint = pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1);
@@ -2027,7 +2034,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->keyp, N);
   rc |= A(&q->mr, N);
   rc |= A(&q->hist, kShards * 2 * kHistBinsR);
-  rc |= A(&q->sbase, 2 * kHistBinsR); rc |= A(&q->snum, 2 * kHistBinsR);
+  rc |= A(&q->sbn, 2 * kHistBinsR);
+  rc |= A(&q->hc, N);
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
@@ -2087,8 +2095,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   Table& t = q->tb;
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
-                  q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbase,
-                  q->snum, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbn,
+                  q->hc, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
@@ -2496,7 +2504,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         ActBuf noact{};
         void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk,
                       &noact};
-        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->rparts, &q->rd, &cp};
+        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }

@@ -71,6 +71,7 @@ struct PhaseSel {
   uint64_t hmin;        // histogram base (histogram coordinates, KeyMap)
   uint64_t lo0, hitop;  // coordinate span of the open-ended first / last bin
   double vmin, scale;   // the phase's KeyMap (with kmin)
+  double inv_w, inv_last;  // rank_bin_r's split scales (interior / last bin)
 };
 
 // Histogram range of a phase: base key and bin shift (bins 0 and
@@ -109,6 +110,11 @@ struct Round {
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
   unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
+  // diagnostics (DMC_TAIL_TIMING builds): wall clocks of the kernels with a
+  // last-block tail: [0] first k_rhist block start, [1] its last block's
+  // ticket, [2] pick done; [3] first k_remit block start, [4] its last
+  // block's ticket, [5] bin prefixes done
+  unsigned long long tdbg[6];
   // per-call parameters, published by k_rscan (the graph's parameter node)
   double now;
   dmc_decision* out;
@@ -199,7 +205,7 @@ struct ScanCols {
 
 __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
                                  double now, uint64_t* keyr, uint64_t* keyp,
-                                 uint8_t* mr, RoundPart& acc) {
+                                 uint8_t* mr, uint16_t* hc, RoundPart& acc) {
   uint64_t kr = kMaxKey, kp = kMaxKey;
   uint32_t m = 0;
   if (x.c) {
@@ -238,6 +244,7 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
   keyr[s] = kr;
   keyp[s] = kp;
   mr[s] = (uint8_t)m;
+  hc[s] = (uint16_t)((x.c ? x.h : 0u) | (x.c << 8));
   if (kr != kMaxKey) {
     ++acc.cnt[0];
     acc.n_r += m;
@@ -345,8 +352,8 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
 // for a RoundPart, too many to run in every wave of the block).
 __global__ void __launch_bounds__(kScanBlock)
-k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
-        Round* rd, CallParams cp) {
+k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
+        RoundPart* parts, Round* rd, CallParams cp) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -357,6 +364,7 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
     z.tick = cp.tick;
     z.res = cp.res;
     z.seq = cp.seq;
+    z.tdbg[0] = z.tdbg[3] = ~0ull;
     *rd = z;
   }
   __shared__ RoundPart sh[kScanBlock];
@@ -381,7 +389,7 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, RoundPart* parts,
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, acc);
+    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, hc, acc);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
@@ -415,15 +423,17 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // iteration with every key load issued before the first LDS atomic; the
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
-constexpr int kPickThreadsR = 1024;
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbase, uint32_t* snum);
+                          uint32_t* sbn);
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist, uint32_t* sbase, uint32_t* snum,
+        uint32_t nparts, Round* rd, uint32_t* hist, uint32_t* sbn,
         uint32_t* done) {
   __shared__ uint32_t lh[2][kHistBinsR];
   __shared__ uint32_t s_last;
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) atomicMin(&rd->tdbg[0], (unsigned long long)wall_clock64());
+#endif
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
     lh[0][b] = 0;
     lh[1][b] = 0;
@@ -486,13 +496,28 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) atomicExch(done, 0u);  // ready for the next round
-  pick_both(rd, tot, hist, sbase, snum);
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
+#endif
+  pick_both(rd, tot, hist, sbn);
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[2] = wall_clock64();
+#endif
 }
 
-constexpr int kBinsPerThreadR = kHistBinsR / kPickThreadsR;
-
-__device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
-  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+// Threshold and rank-bin table of one phase, by one half (kPickHalf
+// threads) of the last k_rhist block; the other half does the other phase
+// at the same time (the block barriers line up: both halves run this code).
+// T: the largest key of the bin holding the need-th first key (any T at or
+// above the k-th smallest entry key is exact; a bin edge only admits extra
+// candidates).  The phase's kNBPhase rank bins are spread over the
+// histogram bins up to T's bin in proportion to their counts (each gets 1 +
+// its share), so that the rank bins stay small however the keys are
+// distributed.  Table entry: first rank bin | rank bins << 16.
+constexpr int kPickHalf = 512;
+constexpr int kBinsPerThreadR = kHistBinsR / kPickHalf;
+__device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
+  const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
   uint32_t incl = v;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t o = __shfl_up(incl, d);
@@ -506,20 +531,13 @@ __device__ inline uint32_t block_excl_scan_r(uint32_t v, uint32_t* wsum) {
   return wbase + incl - v;
 }
 
-// One phase: threshold T for `need` first keys (everything if fewer are
-// eligible), and its kNBPhase rank bins spread over the histogram bins up to
-// T's bin in proportion to their counts (each gets 1 + its share), so that
-// the rank bins stay small however the keys are distributed.
 __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
-                                  const KeyMap& km, const HistRange& hr, Round* rd,
-                                  uint32_t* hist,
-                                  uint32_t* sbase, uint32_t* snum,
-                                  uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
-                                  uint64_t* s_T) {
-  int t = threadIdx.x;
-  uint32_t ne = tot.cnt[p];
-  const uint32_t sh1 = hr.shift;
-  const uint64_t hmin = hr.hmin;
+                                  const KeyMap& km, uint32_t sh1, Round* rd,
+                                  uint32_t* hist, uint32_t* sbn, uint32_t* wsum,
+                                  uint32_t* s_tb, uint32_t* s_C, uint64_t* s_T) {
+  const int t = threadIdx.x & (kPickHalf - 1);
+  const uint32_t ne = tot.cnt[p];
+  const uint64_t hmin = 0;
   uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   if (t == 0) {
     *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
@@ -532,19 +550,25 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
   // L2 line of another XCD's, and no plain store is left to write back)
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0;
-  for (int j = 0; j < kBinsPerThreadR; ++j) {
-    uint32_t v[kShards];
+  {
+    uint32_t v[kBinsPerThreadR][kShards];
 #pragma unroll
-    for (int i = 0; i < kShards; ++i)
-      v[i] = atomicExch(&hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j], 0u);
-    h[j] = 0;
+    for (int j = 0; j < kBinsPerThreadR; ++j)
 #pragma unroll
-    for (int i = 0; i < kShards; ++i) h[j] += v[i];
-    local += h[j];
+      for (int i = 0; i < kShards; ++i)
+        v[j][i] = atomicExch(&hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j], 0u);
+#pragma unroll
+    for (int j = 0; j < kBinsPerThreadR; ++j) {
+      h[j] = 0;
+#pragma unroll
+      for (int i = 0; i < kShards; ++i) h[j] += v[j][i];
+      local += h[j];
+    }
   }
-  uint32_t before = block_excl_scan_r(local, wsum);
+  const uint32_t before = half_excl_scan(local, wsum);
   if (need && ne > need && before < need && before + local >= need) {
     uint32_t cum = before;
+#pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       cum += h[j];
       if (cum >= need) {
@@ -563,28 +587,45 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     }
   }
   __syncthreads();
-  uint32_t tb = *s_tb;
+  const uint32_t tb = *s_tb;
   {
     uint32_t cum = before;
+#pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       cum += h[j];
       if ((uint32_t)(t * kBinsPerThreadR + j) == tb) *s_C = cum;
     }
   }
   __syncthreads();
-  uint32_t C = *s_C > 0 ? *s_C : 1;
-  uint32_t S = kNBPhase - (tb + 1);
+  const uint32_t C = *s_C > 0 ? *s_C : 1;
+  const uint32_t S = kNBPhase - (tb + 1);
+  // spare rank bins in proportion to the counts, h * S / C in single
+  // precision (any split is correct; only the balance depends on it), each
+  // clipped to S so that the phase cannot pass its kNBPhase rank bins
+  const float q = (float)S / (float)C;
   uint32_t ns[kBinsPerThreadR], lns = 0;
+#pragma unroll
   for (int j = 0; j < kBinsPerThreadR; ++j) {
-    uint32_t b = t * kBinsPerThreadR + j;
-    ns[j] = b <= tb ? 1u + (uint32_t)((uint64_t)h[j] * S / C) : 0u;
+    const uint32_t b = t * kBinsPerThreadR + j;
+    uint32_t e = (uint32_t)((float)h[j] * q);
+    e = e > S ? S : e;
+    ns[j] = b <= tb ? 1u + e : 0u;
     lns += ns[j];
   }
-  uint32_t nb = block_excl_scan_r(lns, wsum);
+  uint32_t nb = half_excl_scan(lns, wsum);
+#pragma unroll
   for (int j = 0; j < kBinsPerThreadR; ++j) {
-    uint32_t b = t * kBinsPerThreadR + j;
-    sbase[p * kHistBinsR + b] = p * kNBPhase + nb;
-    snum[p * kHistBinsR + b] = ns[j];
+    const uint32_t b = t * kBinsPerThreadR + j;
+    // float rounding may overshoot S by a few bins in all: the tail bins
+    // are folded into the phase's last rank bin (monotone, still exact)
+    uint32_t first = nb, num = ns[j];
+    if (first >= (uint32_t)kNBPhase) {
+      first = kNBPhase - 1;
+      num = num ? 1 : 0;
+    } else if (first + num > (uint32_t)kNBPhase) {
+      num = kNBPhase - first;
+    }
+    sbn[p * kHistBinsR + b] = (p * kNBPhase + first) | (num << 16);
     nb += ns[j];
   }
   if (t == 0) {
@@ -598,58 +639,59 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     z.hmin = hmin;
     z.lo0 = hmin;
     const uint64_t cmax = km(tot.mx[p]);
-    uint64_t top = sat_add_u64(hmin, (uint64_t)(kHistBinsR - 1) << sh1);
+    const uint64_t top = sat_add_u64(hmin, (uint64_t)(kHistBinsR - 1) << sh1);
     z.hitop = cmax > top ? cmax : top;
     z.vmin = km.vmin;
     z.scale = km.scale;
+    // the rank-bin split inside a histogram bin (rank_bin_r): the interior
+    // bins are 2^shift wide (an exact power-of-two scale); the open-ended
+    // last bin spans [top, hitop]
+    z.inv_w = bitsd((uint64_t)(1023 - sh1) << 52);
+    z.inv_last = 1.0 / ((double)(z.hitop - top) + 1.0);
     rd->ph[p] = z;
   }
-  __syncthreads();
 }
 
-
 // Thresholds and rank-bin tables of both phases, by the last k_rhist block
-// (1024 threads), one phase after the other.
+// (1024 threads): phase 0 in threads [0, 512), phase 1 in [512, 1024).
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbase, uint32_t* snum) {
-  __shared__ uint32_t wsum[kPickThreadsR / 64];
-  __shared__ uint32_t s_tb, s_C;
-  __shared__ uint64_t s_T;
+                          uint32_t* sbn) {
+  __shared__ uint32_t wsum[2][kPickHalf / 64];
+  __shared__ uint32_t s_tb[2], s_C[2];
+  __shared__ uint64_t s_T[2];
   const uint32_t k = rd->k_total;
   const bool p_runs = tot.n_r < (uint64_t)k;
-  for (int p = 0; p < 2; ++p) {
-    // R: all prefixes when they hold fewer than k entries; else every client
-    // whose first key is at or below the k-th smallest first key's bucket
-    // (each such client contributes at least one entry <= T).  P: the rest.
-    uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
-                           : (p_runs ? k - (uint32_t)tot.n_r : 0);
-    const KeyMap km(tot.mn[p], tot.mx[p]);
-    const HistRange h{0, hist_shift_r(km(tot.mx[p])), 0};
-    pick_phase(p, need, tot, km, h, rd, hist, sbase, snum, wsum, &s_tb, &s_C, &s_T);
-  }
+  const int p = threadIdx.x / kPickHalf;
+  // R: all prefixes when they hold fewer than k entries; else every client
+  // whose first key is at or below the k-th smallest first key's bucket
+  // (each such client contributes at least one entry <= T).  P: the rest.
+  const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
+                               : (p_runs ? k - (uint32_t)tot.n_r : 0);
+  const KeyMap km(tot.mn[p], tot.mx[p]);
+  pick_phase(p, need, tot, km, hist_shift_r(km(tot.mx[p])), rd, hist, sbn, wsum[p],
+             &s_tb[p], &s_C[p], &s_T[p]);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
-// of the phase's rank bins, split linearly over the bin's key span (k_rpick's
-// table; the open-ended first and last bins span the keys actually seen).
+// of the phase's rank bins (the pick's table: first rank bin | count << 16),
+// split linearly over the bin's key span -- interior bins 2^shift wide, an
+// exact power-of-two scale; the open-ended last bin up to the keys seen.
 __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
-                                      const uint32_t* sbase, const uint32_t* snum) {
+                                      const uint32_t* sbn) {
   const uint64_t c = KeyMap(ps.kmin, ps.vmin, ps.scale)(k);
   uint32_t h = hist_bin(c, ps.hmin, ps.hshift);
   if (h > ps.tbin) h = ps.tbin;
-  uint32_t ns = snum[p * kHistBinsR + h];
+  const uint32_t e = sbn[p * kHistBinsR + h];
+  const uint32_t ns = e >> 16;
   uint32_t sub = 0;
   if (ns > 1) {
-    uint64_t lo = h == 0 ? ps.lo0 : ps.hmin + ((uint64_t)h << ps.hshift);
-    uint64_t hi = h == kHistBinsR - 1 ? ps.hitop
-                                      : ps.hmin + ((uint64_t)(h + 1) << ps.hshift) - 1;
-    uint64_t off = c > lo ? c - lo : 0;
-    uint64_t w = hi > lo ? hi - lo : 0;
-    double f = (double)off / ((double)w + 1.0);
+    const uint64_t lo = ps.hmin + ((uint64_t)h << ps.hshift);
+    const uint64_t off = c > lo ? c - lo : 0;
+    const double f = (double)off * (h == kHistBinsR - 1 ? ps.inv_last : ps.inv_w);
     sub = (uint32_t)(f * (double)ns);
     if (sub >= ns) sub = ns - 1;
   }
-  return sbase[p * kHistBinsR + h] + sub;
+  return (e & 0xffffu) + sub;
 }
 
 // Rank-bin record of one entry: the order key (phase by bin, okey, slot,
@@ -681,8 +723,7 @@ struct EmitV {
   BRecR* brec;
   uint32_t* bcount;
   uint32_t* bsize;
-  const uint32_t* sbase;
-  const uint32_t* snum;
+  const uint32_t* sbn;  // the rank-bin table, staged in LDS
   Round* rd;
   // radix path
   DEnt* dense;
@@ -691,7 +732,7 @@ struct EmitV {
   __device__ void put(uint64_t key, uint32_t pos, uint32_t run) {
     uint32_t ridx = rbase + ((head + pos) & qmask);
     if (brec) {
-      uint32_t b = rank_bin_r(key, *ps, ph, sbase, snum);
+      uint32_t b = rank_bin_r(key, *ps, ph, sbn);
       uint32_t at = atomicAdd(&bcount[b], 1u);
       atomicAdd(&bsize[b], ph == 0 ? 1u : 1u + run);
       if (at < kBinCapR)
@@ -747,43 +788,68 @@ __device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
   return CandPred(rd)(kr, kp);
 }
 
+// A candidate as compacted by k_remit: slot; flags (low nibble) and its
+// first-key predicates (bit 4: R, bit 5: P); R-prefix length; ring head and
+// count as k_rscan saw them (nothing changes them before k_rapply), so that
+// the walkers request the ring entries together with the client record.
+struct CandRec {
+  uint32_t slot;
+  uint8_t fb, m, h, c;
+  __device__ uint8_t f() const { return fb & 0x0f; }
+  __device__ bool cr() const { return (fb >> 4) & 1; }
+  __device__ bool cp() const { return (fb >> 5) & 1; }
+};
+static_assert(sizeof(CandRec) == 8, "CandRec must be 8 bytes");
+
+// The walkers' view of a candidate: head / count from its CandRec, the
+// inverses and prop_delta from the table (one level of loads with the ring
+// entries), cur_delta / cur_rho only in delayed mode.
+__device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
+  const uint32_t s = cr.slot;
+  CView v;
+  v.h = cr.h;
+  v.c = cr.c;
+  v.cd = v.cr = 0;
+  if (tb.delayed) {
+    const QState q = tb.qs[s];
+    v.cd = q.cur_delta;
+    v.cr = q.cur_rho;
+  }
+  v.rinv = tb.rec[s].r_inv;
+  v.winv = tb.rec[s].w_inv;
+  v.linv = tb.rec[s].l_inv;
+  v.pd = tb.fr[s].pd;
+  return v;
+}
+
 // One candidate's entries: R pops with r <= min(now, T_R); then, if the
 // priority pulls run, the P groups with key <= T_P from the post-R state.
-// cr / cp: its first R / P key is at or below the threshold; m: its R-prefix
-// length (k_rscan); f0: its flags.  Bin-rank path: into the rank bins; radix
-// path: appended to the dense entry list.
-__device__ inline void emit_one(const Table& tb, Round* rd, uint32_t s, bool cr,
-                                bool cp, uint32_t m, uint8_t f0, BRecR* brec,
-                                uint32_t* bcount, uint32_t* bsize,
-                                const uint32_t* sbase, const uint32_t* snum,
-                                DEnt* dense, uint32_t dcap) {
+// Bin-rank path: into the rank bins; radix path: appended to the dense list.
+__device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
+                                BRecR* brec, uint32_t* bcount, uint32_t* bsize,
+                                const uint32_t* sbn, DEnt* dense, uint32_t dcap) {
+  const uint32_t s = c.slot;
   const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
   const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
-  const CView cv = load_view(tb, s);
+  const CView cv = cand_view(tb, c);
   const uint32_t h = cv.h;
-  if (cr) {
-    EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
+  if (c.cr()) {
+    EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
     walk_r(tb, s, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
-  if (cp) {
+  if (c.cp()) {
     // the priority pulls run only after every R pop
-    bool ready0 = m == 0 && (f0 & F_READY);
-    EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbase, snum, rd, dense, dcap,
+    const uint32_t m = c.m;
+    bool ready0 = m == 0 && (c.f() & F_READY);
+    EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
     walk_p(tb, s, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
   }
 }
-
-// A candidate as compacted by k_remit: slot, its first-key predicates
-// (bit 0: R, bit 1: P), R-prefix length and flags.
-struct CandRec {
-  uint32_t slot;
-  uint8_t bits, m, f, pad;
-};
 
 // Exclusive prefixes over the rank bins of the record counts, the group
 // sizes and the P-group counts; the round's decision count and terminal
@@ -899,42 +965,53 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 // ---------------------------------------------------------------- k_remit
 // Candidate selection and emission in one pass over the client table:
 // blocks of kEmitThreads own kEmitChunk consecutive slots, 4 per thread,
-// with the first keys, R-prefix lengths and flags loaded coalesced.  A slot
-// is a candidate iff its first R key is <= T_R or (the priority pulls run
-// and) its first P key is <= T_P; non-candidates settle their pending
-// limit-scan marks here (k_rapply settles the candidates').  Each wave
-// compacts its candidates (about 17 of its 256 slots in a config-3 round)
-// in LDS, appends them to the candidate list with one atomic, and its lanes
-// walk one candidate each: 16 waves per CU hide each other's dependent
-// loads.  Bin-rank path: the last block to finish computes the rank-bin
-// prefixes (k_rrank's offsets); radix path: entries go to the dense list.
+// with the first keys, R-prefix lengths, ring head / count and flags loaded
+// coalesced.  A slot is a candidate iff its first R key is <= T_R or (the
+// priority pulls run and) its first P key is <= T_P; non-candidates settle
+// their pending limit-scan marks here (k_rapply settles the candidates').
+// The block compacts its candidates in LDS (about 270 of its 4096 slots in
+// a config-3 round) and appends them to the candidate list with one atomic;
+// its first threads then walk one candidate each, full waves, with the
+// rank-bin table staged in LDS.  Bin-rank path: the last block to finish
+// computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
+// to the dense list.
 constexpr int kEmitThreads = 1024;
 constexpr uint32_t kEmitChunk = kEmitThreads * 4;
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
-        const uint8_t* mr, CandRec* cand, BRecR* brec, uint32_t* bcount,
-        uint32_t* bsize, const uint32_t* sbase, const uint32_t* snum,
-        DEnt* dense, uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff,
-        uint32_t* bpoff, uint32_t* done) {
-  __shared__ CandRec wl[kEmitThreads / 64][256];
-  __shared__ uint32_t s_last;
+        const uint8_t* mr, const uint16_t* hc, CandRec* cand, BRecR* brec,
+        uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
+        uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
+        uint32_t* done) {
+  __shared__ CandRec bl[kEmitChunk];
+  __shared__ uint32_t ltab[2 * kHistBinsR];
+  __shared__ uint32_t wsum[kEmitThreads / 64];
+  __shared__ uint32_t s_base, s_tot, s_last;
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
+#endif
   const uint32_t n = tb.n;
   const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * 4;
   const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (brec)
+    for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
   uint64_t kr[4], kp[4];
   uint8_t f[4], m[4];
+  uint16_t hcv[4];
   if (s0 + 4 <= n) {
     const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
     const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
     ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
     uchar4 f4 = *reinterpret_cast<const uchar4*>(tb.flags + s0);
     uchar4 m4 = *reinterpret_cast<const uchar4*>(mr + s0);
+    ushort4 h4 = *reinterpret_cast<const ushort4*>(hc + s0);
     kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
     kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
     f[0] = f4.x; f[1] = f4.y; f[2] = f4.z; f[3] = f4.w;
     m[0] = m4.x; m[1] = m4.y; m[2] = m4.z; m[3] = m4.w;
+    hcv[0] = h4.x; hcv[1] = h4.y; hcv[2] = h4.z; hcv[3] = h4.w;
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -943,49 +1020,76 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
       kp[j] = in ? keyp[s0 + j] : kMaxKey;
       f[j] = in ? tb.flags[s0 + j] : 0;
       m[j] = in ? mr[s0 + j] : 0;
+      hcv[j] = in ? hc[s0 + j] : 0;
     }
   }
-  uint32_t cnt = 0;
-  CandRec mine[4];
+  uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (s0 + j >= n) continue;
     const bool cr = pred.TR && kr[j] <= pred.TR;
     const bool cp = pred.TP && kp[j] <= pred.TP;
     if (cr || cp) {
-      mine[cnt++] = CandRec{s0 + j, (uint8_t)((cr ? 1 : 0) | (cp ? 2 : 0)), m[j], f[j], 0};
+      bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
     } else if (f[j] & F_PMARK) {
       tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
-  // wave compaction
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cnt += ((bits >> (2 * j)) & 3u) ? 1u : 0u;
+  // block compaction (static indices only: no private-memory arrays)
   uint32_t incl = cnt;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t o = __shfl_up(incl, d);
     if (lane >= d) incl += o;
   }
-  const uint32_t wtot = __shfl(incl, 63);
-  for (uint32_t j = 0, o = incl - cnt; j < cnt; ++j, ++o) wl[w][o] = mine[j];
-  uint32_t base = 0;
-  if (lane == 0 && wtot) base = atomicAdd(&rd->n_cand, wtot);
-  base = __shfl(base, 0);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  for (uint32_t i = lane; i < wtot; i += 64) {
-    const CandRec c = wl[w][i];
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, btot = 0;
+  for (int i = 0; i < kEmitThreads / 64; ++i) {
+    wbase += i < w ? wsum[i] : 0u;
+    btot += wsum[i];
+  }
+  {
+    uint32_t o = wbase + incl - cnt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t b = (bits >> (2 * j)) & 3u;
+      if (b)
+        bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), m[j],
+                          (uint8_t)(hcv[j] & 0xff), (uint8_t)(hcv[j] >> 8)};
+    }
+  }
+  if (threadIdx.x == 0) {
+    s_tot = btot;
+    s_base = btot ? atomicAdd(&rd->n_cand, btot) : 0;
+  }
+  __syncthreads();
+  const uint32_t base = s_base, tot = s_tot;
+  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
+    const CandRec c = bl[i];
     cand[base + i] = c;
-    emit_one(tb, rd, c.slot, c.bits & 1, (c.bits >> 1) & 1, c.m, c.f, brec, bcount,
-             bsize, sbase, snum, dense, dcap);
+    emit_one(tb, rd, c, brec, bcount, bsize, ltab, dense, dcap);
   }
   if (!brec) return;
-  // ticket (see k_rhist): the last block computes the rank-bin prefixes
+  // ticket: the block's bin atomics have completed (every wave waits for its
+  // own) before one lane takes it; the last block computes the prefixes.
+  // Only memory-side atomics cross blocks here (bin counters, overflow flag,
+  // ticket), so no release / acquire fence is needed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) atomicExch(done, 0u);
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[4] = wall_clock64();
+#endif
   bin_prefix(rd, bcount, bsize, bcnt, bsoff, bpoff);
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[5] = wall_clock64();
+#endif
 }
 
 // ---------------------------------------------------------------- k_rrank
@@ -1289,12 +1393,14 @@ struct RoundC {
   bool p_runs, ovf;
 };
 
-__device__ inline void apply_one(const Table& tb, const RoundC& rc, uint32_t s,
-                                 uint8_t f0) {
-  // every load that depends only on the slot is issued before the first
-  // branch: one memory round trip for all of them (f0: the flags k_remit
-  // loaded; nothing between the two kernels changes a candidate's flags)
-  const CView cv = load_view(tb, s);
+__device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd) {
+  // every load that depends only on the candidate record is issued before
+  // the first branch: one memory round trip for the client record and its
+  // ring entries (the record's head / count and flags are k_remit's;
+  // nothing between the two kernels changes them)
+  const uint32_t s = cd.slot;
+  const uint8_t f0 = cd.f();
+  const CView cv = cand_view(tb, cd);
   Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   if (rc.ovf) {
     if (f0 & F_PMARK) tb.flags[s] = (uint8_t)(f0 & ~F_PMARK);
@@ -1412,7 +1518,7 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, unsigned long long* sched,
   for (uint32_t ci = tid; ci < nc; ci += stride) {
     uint64_t t0 = dbg ? wall_clock64() : 0;
     const CandRec c = cand[ci];
-    apply_one(tb, rc, c.slot, c.f);
+    apply_one(tb, rc, c);
     if (dbg && ci < 262144) {
       dbg[2 * ci] = t0;
       dbg[2 * ci + 1] = wall_clock64();
