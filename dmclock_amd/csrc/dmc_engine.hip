@@ -27,6 +27,7 @@
 
 #include "../../include/dmclock_gpu.h"
 #include "dmc_device.h"
+#include "dmc_add.h"
 #include "dmc_round.h"
 #include "dmc_tracker.h"
 
@@ -157,46 +158,7 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
 }
 
 // ------------------------------------------------------------------ add path
-// A batch (a run of add_request_time calls with no activation inside) is
-// grouped by client without sorting: k_add_link counts each client's requests
-// with one atomic per request and files the first kAddSlots batch positions
-// in the client's slot buffer; k_add_chain then lets one thread per client
-// replay that client's requests in batch order.  Clients with more than
-// kAddSlots requests in the batch (rare: 64K requests over 1M clients is
-// Poisson(1/16)) are replayed by a scan of the batch's slot column, in order.
-constexpr uint32_t kAddSlots = 16;
-
-struct AddParams {
-  const dmc_request* reqs;
-  int32_t* rc;
-  uint64_t tick_base;
-  uint32_t n;
-  uint32_t pad;
-};
-
-// Batched activations (the idle reset of every idle client's first request
-// in one batch, resolved on the device; see k_act_resolve).  Per batch
-// position: the proportion contribution (ordered key) a non-idle client with
-// an empty queue had before its first accepted request there (cold, stored
-// at index n - 1 - position) and has after it (cnew); at an activation position the post-add proportion basis
-// (actp: front p if the client has a request, else prev p).
-struct ActBuf {
-  uint64_t* cold;
-  uint64_t* cnew;
-  double* actp;
-  uint64_t* pre;     // exclusive prefix minima of cnew
-  uint64_t* suf;     // exclusive prefix minima of cold (reversed): suffix minima
-  const uint32_t* idx;  // activation positions, ascending
-  uint32_t m;
-  const uint64_t* parts;  // k_act_base partials
-  uint32_t nparts;
-  uint64_t* extra;   // contributions of touched empty clients left unchanged
-  // device-detected activations (dmc_add_batch_device): k_add_chain flags
-  // each activating position, a compaction builds idx and the count *dm
-  uint32_t* flag = nullptr;
-  const uint32_t* dm = nullptr;
-};
-
+// (per-client replay: dmc_add.h)
 // The first node of an add segment: its arguments are the segment's per-call
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
@@ -215,86 +177,12 @@ __global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
   aslot[i] = s;
   if (s >= tb.n) {
     apos[i] = kNone;
+    p.rc[i] = DMC_ENOTREG;  // (no replay will see this request)
     return;
   }
   uint32_t pos = atomicAdd(&acnt[s], 1u);
   apos[i] = pos;
   if (pos < kAddSlots) abuf[(size_t)s * kAddSlots + pos] = i;
-}
-
-// do_add_request for one client's requests of the batch, in batch order:
-// minus the idle reset (handled before, per activation), initial_tag
-// (:878-907), the Reject check (:989-993), the enqueue and cur_rho/cur_delta
-// (:995-1009).
-struct AddState {
-  Tag3 prev;
-  double rinv, winv, linv;
-  uint32_t head, count, cd, cr;
-  uint64_t last_tick;
-  uint8_t flags;
-  bool front_set;
-  Tag3 front;
-};
-
-__device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
-                               const AddParams& p, uint32_t pos) {
-  const dmc_request rq = p.reqs[pos];
-  uint64_t tick = p.tick_base + pos + 1;  // ++tick, :918
-  if (rq.rho > rq.delta) {  // ReqParams asserts rho <= delta
-    p.rc[pos] = DMC_EBADPARAMS;
-    return;
-  }
-  if (st.count >= tb.q) {  // documented deviation: bounded ring
-    p.rc[pos] = DMC_EQUEUEFULL;
-    return;
-  }
-  Tag3 tag;
-  if (!tb.delayed || st.count == 0) {
-    if (!make_tag(st.prev, st.rinv, st.winv, st.linv, rq.delta, rq.rho, rq.time,
-                  rq.cost, tb.antic, &tag)) {
-      p.rc[pos] = DMC_EBADTAG;
-      return;
-    }
-    // update_req_tag, :405-412
-    assign_unpinned(st.prev.r, tag.r);
-    assign_unpinned(st.prev.l, tag.l);
-    assign_unpinned(st.prev.p, tag.p);
-    st.prev.arrival = tag.arrival;
-    st.last_tick = tick;
-  } else {
-    if (rq.cost == 0) {
-      p.rc[pos] = DMC_EBADTAG;
-      return;
-    }
-    tag = Tag3{0.0, 0.0, 0.0, rq.time};  // placeholder, :880
-  }
-  if (tb.at_limit == DMC_AT_LIMIT_REJECT &&
-      tag.l > __dadd_rn(rq.time, tb.reject_thr)) {
-    p.rc[pos] = DMC_EAGAIN;
-    return;
-  }
-  ReqEntry e;
-  e.r = tag.r;
-  e.p = tag.p;
-  e.l = tag.l;
-  e.arrival = tag.arrival;
-  e.handle = rq.handle;
-  e.cost = rq.cost;
-  e.delta = (tb.delayed && st.count > 0) ? 0u : rq.delta;
-  e.rho = (tb.delayed && st.count > 0) ? 0u : rq.rho;
-  e.dec = kNoDec;
-  e.tie = 0;
-  e.pad = 0;
-  ring[(st.head + st.count) & tb.qmask] = e;
-  if (st.count == 0) {
-    st.front = tag;
-    st.front_set = true;
-    st.flags &= (uint8_t)~F_READY;  // a new tag is not ready, :155
-  }
-  ++st.count;
-  st.cd = rq.delta;
-  st.cr = rq.rho;
-  p.rc[pos] = DMC_OK;
 }
 
 __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
@@ -313,88 +201,11 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
   uint32_t m = acnt[s];
   acnt[s] = 0;  // ready for the next batch
   if (!(tb.flags[s] & F_REG)) {
-    if (m <= kAddSlots) {
-      for (uint32_t j = 0; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
-    } else {
-      for (uint32_t j = 0; j < p.n; ++j)
-        if (aslot[j] == s) p.rc[j] = DMC_ENOTREG;
-    }
+    add_chain_notreg(p, s, m, abuf, aslot);
     return;
   }
   AddState st;
-  st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
-  st.rinv = tb.rec[s].r_inv;
-  st.winv = tb.rec[s].w_inv;
-  st.linv = tb.rec[s].l_inv;
-  st.head = tb.qs[s].head;
-  st.count = tb.qs[s].count;
-  st.cd = tb.qs[s].cur_delta;
-  st.cr = tb.qs[s].cur_rho;
-  st.last_tick = tb.rec[s].last_tick;
-  st.flags = tb.flags[s];
-  st.front_set = false;
-  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  // batched activations: this client's contribution to the idle reset before
-  // and after its requests (see ActBuf)
-  const bool idle0 = (st.flags & F_IDLE) != 0;
-  const uint32_t count0 = st.count;
-  const double pd = act.cold ? tb.fr[s].pd : 0.0;
-  const double front_p0 = (act.cold && count0) ? tb.fr[s].p : 0.0;
-  const double prev_p0 = st.prev.p;
-  bool act_done = false, chg_done = false;
-  auto step = [&](uint32_t pos) {
-    add_one(tb, st, ring, p, pos);
-    if (!act.cold) return;
-    if (idle0) {
-      const dmc_request& rq = p.reqs[pos];
-      if (!act_done && rq.rho <= rq.delta) {  // the activating request
-        act_done = true;
-        act.actp[pos] = st.count ? (count0 ? front_p0 : st.front.p) : st.prev.p;
-        if (act.flag) act.flag[pos] = 1;
-      }
-    } else if (count0 == 0 && !chg_done && st.count) {
-      chg_done = true;
-      act.cold[p.n - 1 - pos] = okey(__dadd_rn(prev_p0, pd));  // reversed order
-      act.cnew[pos] = okey(__dadd_rn(st.front.p, pd));
-    }
-  };
-  if (m == 1) {
-    step(i);
-  } else if (m <= kAddSlots) {
-    // the client's batch positions in ascending order, by repeated selection
-    // over its (L2-resident) slot-buffer row
-    const uint32_t* row = abuf + (size_t)s * kAddSlots;
-    uint32_t last = 0;
-    for (uint32_t j = 0; j < m; ++j) {
-      uint32_t next = 0xffffffffu;
-      for (uint32_t k = 0; k < m; ++k) {
-        uint32_t v = row[k];
-        if ((j == 0 || v > last) && v < next) next = v;
-      }
-      step(next);
-      last = next;
-    }
-  } else {
-    for (uint32_t j = 0; j < p.n; ++j)
-      if (aslot[j] == s) step(j);
-  }
-  if (act.cold && !idle0 && count0 == 0 && !chg_done)  // nothing accepted
-    atomicMin((unsigned long long*)act.extra,
-              (unsigned long long)okey(__dadd_rn(prev_p0, pd)));
-  tb.rec[s].prev_r = st.prev.r;
-  tb.rec[s].prev_p = st.prev.p;
-  tb.rec[s].prev_l = st.prev.l;
-  tb.rec[s].prev_arr = st.prev.arrival;
-  tb.qs[s].count = st.count;
-  tb.qs[s].cur_delta = st.cd;
-  tb.qs[s].cur_rho = st.cr;
-  tb.rec[s].last_tick = st.last_tick;
-  tb.flags[s] = st.flags;
-  if (st.front_set) {
-    tb.fr[s].r = st.front.r;
-    tb.fr[s].p = st.front.p;
-    tb.fr[s].l = st.front.l;
-  }
+  add_chain_slot(tb, p, s, m, i, abuf, aslot, act, &st);
 }
 
 // idle reset, :937-985: L = min over non-idle clients of
@@ -1706,8 +1517,9 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
 // 8-13 kernel launches, which takes the host's per-launch cost off the
 // critical path.  A shape is captured the second time it is seen; profiling
 // runs eagerly (the stage timers are events between kernels).
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) {
-  prof_gate(q);
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future,
+                   const AddFuse& af = AddFuse{}) {
+  if (!af.pblk) prof_gate(q);
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
@@ -1716,7 +1528,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
   pb(q, DMC_PROF_SCAN);
   hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
-                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp);
+                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp, af);
   pe(q);
   pb(q, DMC_PROF_SELECT);
   hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
@@ -1795,7 +1607,8 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
     return DMC_OK;
   }
   Table tb = q->tb;
-  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp};
+  AddFuse none{};
+  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp, &none};
   return graph_replay(q, *g, args);
 }
 
@@ -1913,9 +1726,13 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (!radix && c.bin_max[1] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[1];
 #ifdef DMC_TAIL_TIMING
     if (q->debug)
-      std::fprintf(stderr, "dmc tails (us): hist body %.2f pick %.2f | emit body %.2f prefix %.2f\n",
+      std::fprintf(stderr, "dmc tails (us): hist body %.2f pick %.2f [reads %.2f scan %.2f thr %.2f rest %.2f] | emit body %.2f prefix %.2f [reads %.2f scan %.2f rest %.2f]\n",
                    (c.tdbg[1] - c.tdbg[0]) / 100.0, (c.tdbg[2] - c.tdbg[1]) / 100.0,
-                   (c.tdbg[4] - c.tdbg[3]) / 100.0, (c.tdbg[5] - c.tdbg[4]) / 100.0);
+                   (c.tdbg[6] - c.tdbg[1]) / 100.0, (c.tdbg[7] - c.tdbg[6]) / 100.0,
+                   (c.tdbg[8] - c.tdbg[7]) / 100.0, (c.tdbg[2] - c.tdbg[8]) / 100.0,
+                   (c.tdbg[4] - c.tdbg[3]) / 100.0, (c.tdbg[5] - c.tdbg[4]) / 100.0,
+                   (c.tdbg[9] - c.tdbg[4]) / 100.0, (c.tdbg[10] - c.tdbg[9]) / 100.0,
+                   (c.tdbg[11] - c.tdbg[10]) / 100.0);
 #endif
     if (c.overflow == 1) {  // dense entries: grow and retry
       ++q->ctr.dense_overflows;
@@ -2489,9 +2306,14 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       const bool future = q->p.at_limit != DMC_AT_LIMIT_ALLOW;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
       CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq};
+      // k_add_link files the batch per slot; the round's scan replays each
+      // slot's requests (add_chain_slot) right before scanning it
+      const AddFuse af{q->apblk, q->acnt, q->abuf, q->aslot};
       auto enqueue = [&] {
-        enqueue_add(q, ap);
-        enqueue_round(q, cp, false, future);
+        hipLaunchKernelGGL(k_add_link, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                           q->stream, ap, q->tb, q->acnt, q->abuf, q->apos, q->aslot,
+                           q->apblk, ActBuf{});
+        enqueue_round(q, cp, false, future, af);
       };
       ++q->ctr.fused_calls;
       uint64_t key = (4ull << 56) | ((uint64_t)n << 1) | (future ? 1 : 0);
@@ -2504,7 +2326,9 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         ActBuf noact{};
         void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk,
                       &noact};
-        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp};
+        AddFuse af2 = af;
+        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp,
+                      &af2};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }

@@ -44,6 +44,7 @@
 // 32-bit radix sort + exact fix-up).
 #pragma once
 
+#include "dmc_add.h"
 #include "dmc_device.h"
 
 namespace dmc {
@@ -114,7 +115,7 @@ struct Round {
   // last-block tail: [0] first k_rhist block start, [1] its last block's
   // ticket, [2] pick done; [3] first k_remit block start, [4] its last
   // block's ticket, [5] bin prefixes done
-  unsigned long long tdbg[6];
+  unsigned long long tdbg[12];  // [6..8] pick steps, [9..11] bin_prefix steps
   // per-call parameters, published by k_rscan (the graph's parameter node)
   double now;
   dmc_decision* out;
@@ -351,9 +352,21 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // Scan.  Per-block counts and key ranges (parts), staged in LDS and combined
 // by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
 // for a RoundPart, too many to run in every wave of the block).
+// An add batch replayed by the scan (dmc_add_pull_batch_device with no idle
+// client): k_add_link has filed the batch's positions per slot; the scan
+// thread that owns a slot with requests in the batch replays them (the
+// add_chain_slot of k_add_chain) before scanning the slot.  pblk == nullptr:
+// no batch.
+struct AddFuse {
+  const AddParams* pblk;
+  uint32_t* acnt;
+  const uint32_t* abuf;
+  const uint32_t* aslot;
+};
+
 __global__ void __launch_bounds__(kScanBlock)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
-        RoundPart* parts, Round* rd, CallParams cp) {
+        RoundPart* parts, Round* rd, CallParams cp, AddFuse af) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -372,10 +385,12 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
   RoundPart acc = rpart_ident();
   const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
   ScanCols x[kScanSlots];
+  uint32_t am[kScanSlots];
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
     x[j].c = 0;
+    am[j] = 0;
     if (s < tb.n) {
       x[j].c = tb.qs[s].count;
       x[j].h = tb.qs[s].head;
@@ -384,6 +399,32 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
       x[j].fl = tb.fr[s].l;
       x[j].pd = tb.fr[s].pd;
       x[j].f = tb.flags[s];
+      if (af.pblk) am[j] = af.acnt[s];
+    }
+  }
+  if (af.pblk) {
+    // the batch's requests of this thread's slots, replayed first
+    const AddParams ap = *af.pblk;
+#pragma unroll
+    for (int j = 0; j < kScanSlots; ++j) {
+      const uint32_t s = base + j * blockDim.x;
+      const uint32_t m = am[j];
+      if (!m) continue;
+      af.acnt[s] = 0;  // ready for the next batch
+      if (!(x[j].f & F_REG)) {
+        add_chain_notreg(ap, s, m, af.abuf, af.aslot);
+        continue;
+      }
+      AddState st;
+      const uint32_t i1 = m == 1 ? af.abuf[(size_t)s * kAddSlots] : 0u;
+      add_chain_slot(tb, ap, s, m, i1, af.abuf, af.aslot, ActBuf{}, &st);
+      x[j].c = st.count;
+      x[j].f = st.flags;
+      if (st.front_set) {
+        x[j].fr = st.front.r;
+        x[j].fp = st.front.p;
+        x[j].fl = st.front.l;
+      }
     }
   }
 #pragma unroll
@@ -479,10 +520,13 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
       if (s + stride < n) load(s + stride);
     }
     __syncthreads();
-    uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
+    // one 64-bit atomic per bin carries both phases' counts (phase 0 in the
+    // low half; a phase's total stays below 2^32): half the flush atomics
+    unsigned long long* hs = reinterpret_cast<unsigned long long*>(hist) +
+                             (blockIdx.x % kShards) * kHistBinsR;
     for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
-      if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
-      if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
+      const unsigned long long v = lh[0][b] | ((unsigned long long)lh[1][b] << 32);
+      if (v) atomicAdd(&hs[b], v);
     }
   }
   // ticket: the block's histogram atomics have completed (every wave waits
@@ -495,7 +539,15 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
   if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) atomicExch(done, 0u);  // ready for the next round
+  if (threadIdx.x == 0) {
+    atomicExch(done, 0u);  // ready for the next round
+    // the consumer side of MI355X_MICROARCH.md's cross-XCD hand-off: one
+    // agent-scope acquire, its wait, a block barrier, then plain loads of
+    // the shards (which every block updated with memory-side atomics)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
 #endif
@@ -538,34 +590,46 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
-  uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
+  // shard i, bin b: hist64[i * kHistBinsR + b], phase p in half p
+  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(hist);
   if (t == 0) {
     *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
     *s_C = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
   }
-  // the shards were filled by every k_rhist block with device-scope atomics
-  // (performed at the memory side): read them the same way, clearing them
-  // for the next round in the same operation (no plain load can see a stale
-  // L2 line of another XCD's, and no plain store is left to write back)
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0;
   {
-    uint32_t v[kBinsPerThreadR][kShards];
+    unsigned long long v[kBinsPerThreadR][kShards];
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j)
 #pragma unroll
       for (int i = 0; i < kShards; ++i)
-        v[j][i] = atomicExch(&hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j], 0u);
+        v[j][i] = h64[i * kHistBinsR + t * kBinsPerThreadR + j];
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       h[j] = 0;
 #pragma unroll
-      for (int i = 0; i < kShards; ++i) h[j] += v[j][i];
+      for (int i = 0; i < kShards; ++i) h[j] += (uint32_t)(v[j][i] >> (32 * p));
       local += h[j];
     }
   }
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[6] = wall_clock64();
+#endif
   const uint32_t before = half_excl_scan(local, wsum);
+  // both halves have read the shards (the scan's barriers): phase 0's half
+  // clears them for the next round (plain stores, written back at the
+  // kernel's end, before the next round's atomics)
+  if (p == 0) {
+#pragma unroll
+    for (int j = 0; j < kBinsPerThreadR; ++j)
+#pragma unroll
+      for (int i = 0; i < kShards; ++i) h64[i * kHistBinsR + t * kBinsPerThreadR + j] = 0;
+  }
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[7] = wall_clock64();
+#endif
   if (need && ne > need && before < need && before + local >= need) {
     uint32_t cum = before;
 #pragma unroll
@@ -597,6 +661,9 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
     }
   }
   __syncthreads();
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[8] = wall_clock64();
+#endif
   const uint32_t C = *s_C > 0 ? *s_C : 1;
   const uint32_t S = kNBPhase - (tb + 1);
   // spare rank bins in proportion to the counts, h * S / C in single
@@ -866,8 +933,15 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 #pragma unroll
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
+#ifdef DMC_PLAIN_TAIL_READS  // measurement only
+    c[j] = bcount[b];
+    z[j] = bsize[b];
+    bcount[b] = 0;
+    bsize[b] = 0;
+#else
     c[j] = atomicExch(&bcount[b], 0u);
     z[j] = atomicExch(&bsize[b], 0u);
+#endif
   }
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
@@ -876,6 +950,9 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
   }
   const bool ovf = atomicOr(&rd->bin_ovf, 0u) != 0;
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[9] = wall_clock64();
+#endif
   uint32_t ic = lc, iz = lz, ip = lp;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d);
@@ -913,6 +990,9 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     }
     return;
   }
+#ifdef DMC_TAIL_TIMING
+  if (threadIdx.x == 0) rd->tdbg[10] = wall_clock64();
+#endif
   uint32_t oz = bz + iz - lz, op = bp + ip - lp;
   (void)bc;
   for (int j = 0; j < per; ++j) {
@@ -951,6 +1031,9 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
       else m1 = wc[i] > m1 ? wc[i] : m1;
       S += ((unsigned long long)wp[i] << 32) | wz[i];
     }
+#ifdef DMC_TAIL_TIMING
+    rd->tdbg[11] = wall_clock64();
+#endif
     rd->bin_max[0] = m0;
     rd->bin_max[1] = m1;
     rd->bin_sq = S;
