@@ -33,6 +33,7 @@ OPT_SMALL_K = 1
 OPT_FORCE_RADIX = 2
 OPT_GRAPHS = 3
 OPT_ACT_SPLIT = 4
+OPT_SAMPLE = 5
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0
@@ -120,6 +121,7 @@ class Counters(ctypes.Structure):
         ("decisions", ctypes.c_uint64),
         ("graph_replays", ctypes.c_uint64),
         ("fused_calls", ctypes.c_uint64),
+        ("sample_retries", ctypes.c_uint64),
         ("max_bin", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
     ]

@@ -867,6 +867,9 @@ struct dmc_queue {
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
   uint32_t* sbn = nullptr;    // rank-bin table per phase and histogram bin (k_rhist's pick)
   uint16_t* hc = nullptr;     // N: ring head | count << 8 as k_rscan saw them
+  uint64_t *skr = nullptr, *skp = nullptr;  // N / kSample: the threshold histogram's sample
+  bool exact_next = false;    // re-run a round whose sampled threshold failed exactly
+  int sample_mode = 1;        // DMC_OPT_SAMPLE: 0 exact, 1 sampled, 2 sampled (test: no margin)
   uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics)
   uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
   uint32_t* hist_done = nullptr;  // k_rhist's block ticket counter
@@ -1517,9 +1520,15 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
 // 8-13 kernel launches, which takes the host's per-launch cost off the
 // critical path.  A shape is captured the second time it is seen; profiling
 // runs eagerly (the stage timers are events between kernels).
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future,
-                   const AddFuse& af = AddFuse{}) {
-  if (!af.pblk) prof_gate(q);
+// Sampled thresholds (kSample) for tables of at least kSampleMinN slots on
+// the bin-rank path, unless the previous round's sample failed validation.
+bool use_sample(const dmc_queue* q, bool radix) {
+  return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
+}
+
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) {
+  prof_gate(q);
+  const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
@@ -1528,13 +1537,20 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future,
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
   pb(q, DMC_PROF_SCAN);
   hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
-                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp, af);
+                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp,
+                     sampled ? q->skr : nullptr, sampled ? q->skp : nullptr);
   pe(q);
   pb(q, DMC_PROF_SELECT);
-  hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
-                     (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                     (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn,
-                     q->hist_done);
+  if (sampled)
+    hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0, q->stream,
+                       (N + kSample - 1) / kSample, (const uint64_t*)q->skr,
+                       (const uint64_t*)q->skp, (const RoundPart*)q->rparts, gN, q->rd,
+                       q->hist, q->sbn, q->hist_done, q->sample_mode == 2 ? 2 : 1);
+  else
+    hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
+                       (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
+                       (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn,
+                       q->hist_done, 0);
   pe(q);
   pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk), dim3(kEmitThreads),
@@ -1597,8 +1613,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future,
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
                  dmc_pull_result* d_result, bool radix, bool future) {
-  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 2) | (radix ? 2 : 0) |
-                 (future ? 1 : 0);
+  const bool sampled = use_sample(q, radix);
+  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 3) | (sampled ? 4 : 0) |
+                 (radix ? 2 : 0) | (future ? 1 : 0);
   CallParams cp{kk, 0, now, out, q->tick, d_result, ++q->round_seq};
   GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, future); });
   if (!g) {
@@ -1607,8 +1624,10 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
     return DMC_OK;
   }
   Table tb = q->tb;
-  AddFuse none{};
-  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp, &none};
+  uint64_t* skr = sampled ? q->skr : nullptr;
+  uint64_t* skp = sampled ? q->skp : nullptr;
+  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp,
+                  &skr, &skp};
   return graph_replay(q, *g, args);
 }
 
@@ -1743,6 +1762,13 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       retry_radix = retry;
       continue;
     }
+    if (c.overflow == 3) {
+      // the sampled threshold admitted too few first keys (k_remit's exact
+      // count): this round is re-run with the exact histogram
+      ++q->ctr.sample_retries;
+      q->exact_next = true;
+      continue;
+    }
     if (c.overflow == 2) {
       // a rank bin outgrew kBinCapR: this round is re-run on the radix path.
       // An isolated skewed round costs only that; massively tied keys
@@ -1758,6 +1784,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       continue;
     }
     if (!radix) q->ovf_streak = 0;
+    q->exact_next = false;
     q->ctr.candidates += c.n_cand;
     q->ctr.entries += radix ? c.dense_n : c.n_emit;
     q->ctr.decisions += c.n_dec;
@@ -1853,6 +1880,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->hist, kShards * 2 * kHistBinsR);
   rc |= A(&q->sbn, 2 * kHistBinsR);
   rc |= A(&q->hc, N);
+  rc |= A(&q->skr, (N + kSample - 1) / kSample);
+  rc |= A(&q->skp, (N + kSample - 1) / kSample);
   q->step_grid = grid_for(N, 1024);
   rc |= A(&q->red, q->step_grid + 1);
   rc |= A(&q->sctl, 1);
@@ -1913,7 +1942,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
                   t.ring,
                   q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbn,
-                  q->hc, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->hc, q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
@@ -2306,17 +2335,13 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       const bool future = q->p.at_limit != DMC_AT_LIMIT_ALLOW;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
       CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq};
-      // k_add_link files the batch per slot; the round's scan replays each
-      // slot's requests (add_chain_slot) right before scanning it
-      const AddFuse af{q->apblk, q->acnt, q->abuf, q->aslot};
       auto enqueue = [&] {
-        hipLaunchKernelGGL(k_add_link, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                           q->stream, ap, q->tb, q->acnt, q->abuf, q->apos, q->aslot,
-                           q->apblk, ActBuf{});
-        enqueue_round(q, cp, false, future, af);
+        enqueue_add(q, ap);
+        enqueue_round(q, cp, false, future);
       };
       ++q->ctr.fused_calls;
-      uint64_t key = (4ull << 56) | ((uint64_t)n << 1) | (future ? 1 : 0);
+      uint64_t key = (4ull << 56) | ((uint64_t)n << 2) | (use_sample(q, false) ? 2 : 0) |
+                     (future ? 1 : 0);
       GraphRec* gr = graph_for(q, key, enqueue, (const void*)k_rscan);
       if (!gr) {
         enqueue();
@@ -2326,9 +2351,11 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         ActBuf noact{};
         void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk,
                       &noact};
-        AddFuse af2 = af;
+        const bool sampled = use_sample(q, false);
+        uint64_t* skr = sampled ? q->skr : nullptr;
+        uint64_t* skp = sampled ? q->skp : nullptr;
         void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp,
-                      &af2};
+                      &skr, &skp};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }
@@ -2481,6 +2508,11 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_ACT_SPLIT:
       q->act_split = value != 0;
+      return DMC_OK;
+    case DMC_OPT_SAMPLE:
+      if (value < 0 || value > 2) return DMC_EINVAL;
+      q->sample_mode = (int)value;
+      invalidate_graphs(q);
       return DMC_OK;
     default:
       return DMC_EINVAL;

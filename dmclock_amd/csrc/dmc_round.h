@@ -44,7 +44,6 @@
 // 32-bit radix sort + exact fix-up).
 #pragma once
 
-#include "dmc_add.h"
 #include "dmc_device.h"
 
 namespace dmc {
@@ -108,6 +107,8 @@ struct Round {
   uint32_t n_cand;       // candidate clients (k_rcand)
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
   uint32_t n_emit;       // rank records emitted (k_rbscan)
+  uint32_t sampled;      // the thresholds came from a 1/8 sample of the first keys
+  uint32_t ccnt[2];      // sampled rounds: first keys at or below T, per phase (k_remit)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
   unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
@@ -198,6 +199,14 @@ struct CountV {
 constexpr int kScanSlots = DMC_SCAN_SLOTS;
 constexpr int kScanBlock = DMC_SCAN_BLOCK;
 
+// Sampled thresholds: for large tables the round's threshold histogram is
+// built from every kSample-th slot's first keys (k_rscan writes them
+// compactly), with a margin on the needed count; k_remit counts the exact
+// first keys at or below each threshold and a round whose sampled threshold
+// admits too few is re-run with the exact histogram (overflow = 3).
+constexpr uint32_t kSample = 8;
+constexpr uint32_t kSampleMinN = 1u << 16;
+
 struct ScanCols {
   uint32_t c, h;
   double fr, fp, fl, pd;
@@ -206,7 +215,8 @@ struct ScanCols {
 
 __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
                                  double now, uint64_t* keyr, uint64_t* keyp,
-                                 uint8_t* mr, uint16_t* hc, RoundPart& acc) {
+                                 uint8_t* mr, uint16_t* hc, uint64_t* skr, uint64_t* skp,
+                                 RoundPart& acc) {
   uint64_t kr = kMaxKey, kp = kMaxKey;
   uint32_t m = 0;
   if (x.c) {
@@ -244,6 +254,10 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
   }
   keyr[s] = kr;
   keyp[s] = kp;
+  if (skr && (s & (kSample - 1)) == 0) {  // the threshold histogram's sample
+    skr[s / kSample] = kr;
+    skp[s / kSample] = kp;
+  }
   mr[s] = (uint8_t)m;
   hc[s] = (uint16_t)((x.c ? x.h : 0u) | (x.c << 8));
   if (kr != kMaxKey) {
@@ -352,21 +366,9 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // Scan.  Per-block counts and key ranges (parts), staged in LDS and combined
 // by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
 // for a RoundPart, too many to run in every wave of the block).
-// An add batch replayed by the scan (dmc_add_pull_batch_device with no idle
-// client): k_add_link has filed the batch's positions per slot; the scan
-// thread that owns a slot with requests in the batch replays them (the
-// add_chain_slot of k_add_chain) before scanning the slot.  pblk == nullptr:
-// no batch.
-struct AddFuse {
-  const AddParams* pblk;
-  uint32_t* acnt;
-  const uint32_t* abuf;
-  const uint32_t* aslot;
-};
-
 __global__ void __launch_bounds__(kScanBlock)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
-        RoundPart* parts, Round* rd, CallParams cp, AddFuse af) {
+        RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -385,12 +387,10 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
   RoundPart acc = rpart_ident();
   const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
   ScanCols x[kScanSlots];
-  uint32_t am[kScanSlots];
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
     x[j].c = 0;
-    am[j] = 0;
     if (s < tb.n) {
       x[j].c = tb.qs[s].count;
       x[j].h = tb.qs[s].head;
@@ -399,38 +399,12 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
       x[j].fl = tb.fr[s].l;
       x[j].pd = tb.fr[s].pd;
       x[j].f = tb.flags[s];
-      if (af.pblk) am[j] = af.acnt[s];
-    }
-  }
-  if (af.pblk) {
-    // the batch's requests of this thread's slots, replayed first
-    const AddParams ap = *af.pblk;
-#pragma unroll
-    for (int j = 0; j < kScanSlots; ++j) {
-      const uint32_t s = base + j * blockDim.x;
-      const uint32_t m = am[j];
-      if (!m) continue;
-      af.acnt[s] = 0;  // ready for the next batch
-      if (!(x[j].f & F_REG)) {
-        add_chain_notreg(ap, s, m, af.abuf, af.aslot);
-        continue;
-      }
-      AddState st;
-      const uint32_t i1 = m == 1 ? af.abuf[(size_t)s * kAddSlots] : 0u;
-      add_chain_slot(tb, ap, s, m, i1, af.abuf, af.aslot, ActBuf{}, &st);
-      x[j].c = st.count;
-      x[j].f = st.flags;
-      if (st.front_set) {
-        x[j].fr = st.front.r;
-        x[j].fp = st.front.p;
-        x[j].fl = st.front.l;
-      }
     }
   }
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, hc, acc);
+    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, hc, skr, skp, acc);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
@@ -464,12 +438,15 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // iteration with every key load issued before the first LDS atomic; the
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
+constexpr int kHistBlocksSampled = 32;  // 131,072 sampled slots of 1M: 4 per thread
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbn);
+                          uint32_t* sbn, int sampled);
+// n keys per phase: every slot's first keys (keyr / keyp, exact), or the
+// scan's 1/kSample sample of them (sampled)
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
         uint32_t nparts, Round* rd, uint32_t* hist, uint32_t* sbn,
-        uint32_t* done) {
+        uint32_t* done, int sampled) {
   __shared__ uint32_t lh[2][kHistBinsR];
   __shared__ uint32_t s_last;
 #ifdef DMC_TAIL_TIMING
@@ -506,6 +483,7 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
     rd->tot = tot;
     rd->n_r = tot.n_r;
     rd->p_runs = p_runs ? 1 : 0;
+    rd->sampled = sampled ? 1 : 0;
   }
   if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
     const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
@@ -520,13 +498,10 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
       if (s + stride < n) load(s + stride);
     }
     __syncthreads();
-    // one 64-bit atomic per bin carries both phases' counts (phase 0 in the
-    // low half; a phase's total stays below 2^32): half the flush atomics
-    unsigned long long* hs = reinterpret_cast<unsigned long long*>(hist) +
-                             (blockIdx.x % kShards) * kHistBinsR;
+    uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
     for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
-      const unsigned long long v = lh[0][b] | ((unsigned long long)lh[1][b] << 32);
-      if (v) atomicAdd(&hs[b], v);
+      if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
+      if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
     }
   }
   // ticket: the block's histogram atomics have completed (every wave waits
@@ -551,7 +526,7 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
 #endif
-  pick_both(rd, tot, hist, sbn);
+  pick_both(rd, tot, hist, sbn, sampled);
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[2] = wall_clock64();
 #endif
@@ -583,15 +558,15 @@ __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
   return wbase + incl - v;
 }
 
-__device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
-                                  const KeyMap& km, uint32_t sh1, Round* rd,
+__device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
+                                  const RoundPart& tot, const KeyMap& km, uint32_t sh1,
+                                  Round* rd,
                                   uint32_t* hist, uint32_t* sbn, uint32_t* wsum,
                                   uint32_t* s_tb, uint32_t* s_C, uint64_t* s_T) {
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
-  // shard i, bin b: hist64[i * kHistBinsR + b], phase p in half p
-  unsigned long long* h64 = reinterpret_cast<unsigned long long*>(hist);
+  uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   if (t == 0) {
     *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
     *s_C = 0;
@@ -600,17 +575,17 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0;
   {
-    unsigned long long v[kBinsPerThreadR][kShards];
+    uint32_t v[kBinsPerThreadR][kShards];
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j)
 #pragma unroll
       for (int i = 0; i < kShards; ++i)
-        v[j][i] = h64[i * kHistBinsR + t * kBinsPerThreadR + j];
+        v[j][i] = hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       h[j] = 0;
 #pragma unroll
-      for (int i = 0; i < kShards; ++i) h[j] += (uint32_t)(v[j][i] >> (32 * p));
+      for (int i = 0; i < kShards; ++i) h[j] += v[j][i];
       local += h[j];
     }
   }
@@ -618,24 +593,21 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
   if (threadIdx.x == 0) rd->tdbg[6] = wall_clock64();
 #endif
   const uint32_t before = half_excl_scan(local, wsum);
-  // both halves have read the shards (the scan's barriers): phase 0's half
-  // clears them for the next round (plain stores, written back at the
-  // kernel's end, before the next round's atomics)
-  if (p == 0) {
+  // clear this phase's shards for the next round (plain stores, written
+  // back at the kernel's end, before the next round's atomics)
 #pragma unroll
-    for (int j = 0; j < kBinsPerThreadR; ++j)
+  for (int j = 0; j < kBinsPerThreadR; ++j)
 #pragma unroll
-      for (int i = 0; i < kShards; ++i) h64[i * kHistBinsR + t * kBinsPerThreadR + j] = 0;
-  }
+    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j] = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[7] = wall_clock64();
 #endif
-  if (need && ne > need && before < need && before + local >= need) {
+  if (need && ne > need && before < need_h && before + local >= need_h) {
     uint32_t cum = before;
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       cum += h[j];
-      if (cum >= need) {
+      if (cum >= need_h) {
         // the bin's upper edge: the largest key mapped into it, the same
         // candidate set as its largest key present (the open-ended last
         // bin: the largest key)
@@ -721,8 +693,21 @@ __device__ inline void pick_phase(int p, uint32_t need, const RoundPart& tot,
 
 // Thresholds and rank-bin tables of both phases, by the last k_rhist block
 // (1024 threads): phase 0 in threads [0, 512), phase 1 in [512, 1024).
+// needed first keys -> histogram units: exact, or for a 1/kSample sample
+// need / kSample plus a margin of 2 % + 4 standard deviations + 16 (a
+// sampled threshold admitting fewer than `need` first keys is caught by
+// k_remit's exact count and the round re-run exactly)
+// (sampled == 2, a test mode: 3 % below the expected count, so that
+// validation fails and rounds are re-run)
+__device__ inline uint32_t need_hist(uint32_t need, int sampled) {
+  if (!sampled || need == 0xffffffffu) return need;
+  const double m = (double)need / kSample;
+  const double v = sampled == 2 ? m * 0.97 : m * 1.02 + 4.0 * __dsqrt_rn(m) + 16.0;
+  return v >= 4294967295.0 ? 0xffffffffu : (uint32_t)v;
+}
+
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbn) {
+                          uint32_t* sbn, int sampled) {
   __shared__ uint32_t wsum[2][kPickHalf / 64];
   __shared__ uint32_t s_tb[2], s_C[2];
   __shared__ uint64_t s_T[2];
@@ -735,8 +720,8 @@ __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
   const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
   const KeyMap km(tot.mn[p], tot.mx[p]);
-  pick_phase(p, need, tot, km, hist_shift_r(km(tot.mx[p])), rd, hist, sbn, wsum[p],
-             &s_tb[p], &s_C[p], &s_T[p]);
+  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), rd,
+             hist, sbn, wsum[p], &s_tb[p], &s_C[p], &s_T[p]);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -933,15 +918,8 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 #pragma unroll
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
-#ifdef DMC_PLAIN_TAIL_READS  // measurement only
-    c[j] = bcount[b];
-    z[j] = bsize[b];
-    bcount[b] = 0;
-    bsize[b] = 0;
-#else
     c[j] = atomicExch(&bcount[b], 0u);
     z[j] = atomicExch(&bsize[b], 0u);
-#endif
   }
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
@@ -949,7 +927,19 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     lz += z[j];
     lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
   }
-  const bool ovf = atomicOr(&rd->bin_ovf, 0u) != 0;
+  bool ovf = atomicOr(&rd->bin_ovf, 0u) != 0;
+  bool bad_sample = false;
+  if (rd->sampled) {
+    // a sampled threshold must admit at least the needed first keys (then
+    // every entry the k pulls can take has a key at or below it)
+    const uint32_t k = rd->k_total;
+    const uint32_t needR = rd->p_runs ? 0xffffffffu : k;
+    const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
+    const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
+    const uint32_t c0 = atomicOr(&rd->ccnt[0], 0u), c1 = atomicOr(&rd->ccnt[1], 0u);
+    bad_sample = (TR && TR != kMaxKey - 1 && c0 < needR) ||
+                 (TP && TP != kMaxKey - 1 && c1 < needP);
+  }
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[9] = wall_clock64();
 #endif
@@ -978,6 +968,11 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     tc += wc[i];
     tz += wz[i];
     tp += wp[i];
+  }
+  if (bad_sample) {
+    // the round is re-run with the exact histogram (nothing applied yet)
+    if (t == 0) rd->overflow = 3;
+    return;
   }
   if (ovf) {
     // the round is re-run on the radix path: report how many entries it
@@ -1118,9 +1113,23 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
       tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, nr = 0, np = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) cnt += ((bits >> (2 * j)) & 3u) ? 1u : 0u;
+  for (int j = 0; j < 4; ++j) {
+    cnt += ((bits >> (2 * j)) & 3u) ? 1u : 0u;
+    nr += (bits >> (2 * j)) & 1u;
+    np += (bits >> (2 * j + 1)) & 1u;
+  }
+  if (rd->sampled) {
+    // the exact number of first keys at or below each threshold (validates
+    // the sampled thresholds in the last block)
+    nr = wsum32(nr);
+    np = wsum32(np);
+    if (lane == 0) {
+      if (nr) atomicAdd(&rd->ccnt[0], nr);
+      if (np) atomicAdd(&rd->ccnt[1], np);
+    }
+  }
   // block compaction (static indices only: no private-memory arrays)
   uint32_t incl = cnt;
   for (int d = 1; d < 64; d <<= 1) {

@@ -267,6 +267,9 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
 #define DMC_OPT_GRAPHS 3       /* 0: launch every kernel eagerly (default 1: replay captured hipGraphs) */
 #define DMC_OPT_ACT_SPLIT 4    /* 1: resolve each activation's idle reset by splitting the batch on the
                                   host (default 0: all of a batch's activations on the device) */
+#define DMC_OPT_SAMPLE 5       /* pull-round thresholds for tables of >= 65,536 slots: 1 (default) from
+                                  a 1/8 sample of the first keys, validated exactly (a failing round is
+                                  re-run exactly); 0 always exact; 2 a test mode with no sampling margin */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
 /* Engine path counters since creation (or the last reset): which ranking
@@ -283,6 +286,7 @@ typedef struct dmc_counters {
   uint64_t decisions;       /* decisions of completed rounds                         */
   uint64_t graph_replays;   /* captured hipGraphs replayed (add segments, rounds, fused calls) */
   uint64_t fused_calls;     /* dmc_add_pull_batch_device calls run as one add + round launch */
+  uint64_t sample_retries;  /* rounds re-run because a sampled threshold admitted too few keys */
   uint32_t max_bin;         /* largest rank bin of a bin-ranked round (records)     */
   uint32_t reserved;
 } dmc_counters;

@@ -29,11 +29,15 @@ def mk_gpu(**kw):
 def mk_variant(variant):
     """engine paths: default (bin-rank batches, single steps for k <= 8),
     radix-sorted batches, and single steps for every pull"""
-    from dmclock_amd._abi import OPT_FORCE_RADIX, OPT_GRAPHS, OPT_SMALL_K
+    from dmclock_amd._abi import OPT_FORCE_RADIX, OPT_GRAPHS, OPT_SAMPLE, OPT_SMALL_K
 
     def mk(**kw):
         q = mk_gpu(**kw)
-        if variant == "radix":
+        if variant == "exact":
+            q.set_option(OPT_SAMPLE, 0)
+        elif variant == "sample_retry":
+            q.set_option(OPT_SAMPLE, 2)
+        elif variant == "radix":
             q.set_option(OPT_FORCE_RADIX, 1)
         elif variant == "steps":
             q.set_option(OPT_SMALL_K, 1 << 30)
@@ -168,13 +172,22 @@ def bench_shaped_trace(seed, n_clients, n_steps, batch, depth=4):
     return tr
 
 
-@pytest.mark.parametrize("variant", ["default", "radix", "eager"])
+@pytest.mark.parametrize("variant", ["default", "exact", "sample_retry", "radix", "eager"])
 def test_bench_shaped_parity(variant):
-    """The benchmark's own key distributions, 64K clients, bit-exact."""
+    """The benchmark's own key distributions, 64K clients, bit-exact: with
+    the thresholds from a 1/8 sample of the first keys (default), from the
+    exact histogram, and from a sample without its margin (validation fails
+    and the rounds are re-run exactly: the counters show the retries)."""
     tr = bench_shaped_trace(42, 1 << 16, 4, 1 << 12)
     n, qg, qo = run_parity(tr, mk_variant(variant),
                            dict(at_limit=AT_LIMIT_WAIT), state_sample=256)
     assert n > 100000
+    c = qg.counters()
+    print(variant, c)
+    if variant == "sample_retry":
+        assert c["sample_retries"] >= 1, c
+    elif variant in ("default", "exact"):
+        assert c["sample_retries"] == 0, c
 
 
 def test_full_size_parity_1m_clients():
