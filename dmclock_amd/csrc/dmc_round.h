@@ -108,7 +108,8 @@ struct Round {
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
   uint32_t n_emit;       // rank records emitted (k_rbscan)
   uint32_t sampled;      // the thresholds came from a 1/8 sample of the first keys
-  uint32_t ccnt[2];      // sampled rounds: first keys at or below T, per phase (k_remit)
+  uint32_t ccnt[2 * kShards];  // sampled rounds: first keys at or below T, per
+                               // phase, in XCD shards (k_remit)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
   unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
@@ -936,7 +937,11 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     const uint32_t needR = rd->p_runs ? 0xffffffffu : k;
     const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
     const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
-    const uint32_t c0 = atomicOr(&rd->ccnt[0], 0u), c1 = atomicOr(&rd->ccnt[1], 0u);
+    uint32_t c0 = 0, c1 = 0;
+    for (int i = 0; i < kShards; ++i) {
+      c0 += atomicOr(&rd->ccnt[2 * i], 0u);
+      c1 += atomicOr(&rd->ccnt[2 * i + 1], 0u);
+    }
     bad_sample = (TR && TR != kMaxKey - 1 && c0 < needR) ||
                  (TP && TP != kMaxKey - 1 && c1 < needP);
   }
@@ -1065,6 +1070,8 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t s_base, s_tot, s_last;
+  __shared__ uint32_t s_cnt[2];
+  if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
@@ -1075,6 +1082,7 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (brec)
     for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
+  __syncthreads();  // s_cnt zeroed before any wave adds to it
   uint64_t kr[4], kp[4];
   uint8_t f[4], m[4];
   uint16_t hcv[4];
@@ -1120,14 +1128,16 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
     nr += (bits >> (2 * j)) & 1u;
     np += (bits >> (2 * j + 1)) & 1u;
   }
-  if (rd->sampled) {
+  const bool sampled = rd->sampled != 0;
+  if (sampled) {
     // the exact number of first keys at or below each threshold (validates
-    // the sampled thresholds in the last block)
+    // the sampled thresholds in the last block): per block, then one atomic
+    // per phase into the block's XCD shard (same-address atomics serialise)
     nr = wsum32(nr);
     np = wsum32(np);
     if (lane == 0) {
-      if (nr) atomicAdd(&rd->ccnt[0], nr);
-      if (np) atomicAdd(&rd->ccnt[1], np);
+      atomicAdd(&s_cnt[0], nr);
+      atomicAdd(&s_cnt[1], np);
     }
   }
   // block compaction (static indices only: no private-memory arrays)
@@ -1158,6 +1168,11 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
     s_base = btot ? atomicAdd(&rd->n_cand, btot) : 0;
   }
   __syncthreads();
+  if (sampled && threadIdx.x == 0) {
+    uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kShards);
+    if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
+    if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
+  }
   const uint32_t base = s_base, tot = s_tot;
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
     const CandRec c = bl[i];
