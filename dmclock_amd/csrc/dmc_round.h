@@ -888,6 +888,14 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
   uint32_t fc;
   const CView cv = cand_view(tb, c);
   const uint32_t h = cv.h;
+  // the first queued entries are requested with the client record (the
+  // P walk after an R prefix would otherwise start a second round trip)
+  double touched = 0.0;
+  {
+    const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+    const uint32_t nt = c.c < 4u ? c.c : 4u;
+    for (uint32_t j = 0; j < nt; ++j) touched += ring[(h + j) & tb.qmask].arrival;
+  }
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
@@ -902,6 +910,7 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
     walk_p(tb, s, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
   }
+  keep(touched);
 }
 
 // Exclusive prefixes over the rank bins of the record counts, the group
@@ -916,11 +925,20 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   __shared__ uint32_t wc[16], wz[16], wp[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
+  // plain loads behind the last block's agent-scope acquire (the counters
+  // were filled with memory-side atomics), cleared with plain stores for
+  // the next round (written back at the kernel's end)
 #pragma unroll
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
-    c[j] = atomicExch(&bcount[b], 0u);
-    z[j] = atomicExch(&bsize[b], 0u);
+    c[j] = bcount[b];
+    z[j] = bsize[b];
+  }
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    const uint32_t b = t * per + j;
+    bcount[b] = 0;
+    bsize[b] = 0;
   }
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
@@ -928,7 +946,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     lz += z[j];
     lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
   }
-  bool ovf = atomicOr(&rd->bin_ovf, 0u) != 0;
+  bool ovf = rd->bin_ovf != 0;
   bool bad_sample = false;
   if (rd->sampled) {
     // a sampled threshold must admit at least the needed first keys (then
@@ -939,8 +957,8 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
     uint32_t c0 = 0, c1 = 0;
     for (int i = 0; i < kShards; ++i) {
-      c0 += atomicOr(&rd->ccnt[2 * i], 0u);
-      c1 += atomicOr(&rd->ccnt[2 * i + 1], 0u);
+      c0 += rd->ccnt[2 * i];
+      c1 += rd->ccnt[2 * i + 1];
     }
     bad_sample = (TR && TR != kMaxKey - 1 && c0 < needR) ||
                  (TP && TP != kMaxKey - 1 && c1 < needP);
@@ -1189,7 +1207,13 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) atomicExch(done, 0u);
+  if (threadIdx.x == 0) {
+    atomicExch(done, 0u);
+    // consumer side of the cross-XCD hand-off (as in k_rhist): one acquire
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[4] = wall_clock64();
 #endif
@@ -1263,31 +1287,41 @@ __device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
 // instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
 // ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
 // branchless (wave-uniform trip counts, broadcast LDS reads).
-constexpr int kRankBlocksR = kNBR;
-__global__ void __launch_bounds__(kBlockR)
+// One wave per rank bin, four bins per block.  The bin's records are
+// staged in the wave's LDS slice; each record is ranked against all of them
+// by `parts` adjacent lanes, each comparing a slice (parts = the largest
+// power of two with cnt * parts <= 64): a bin of more than 64 records
+// (skewed keys) takes ceil(cnt / 64) passes of one record per lane.  The
+// comparison is branchless (wave-uniform trip counts, broadcast LDS reads).
+constexpr int kRankWaves = 4;
+constexpr int kRankBlocksR = kNBR / kRankWaves;
+__global__ void __launch_bounds__(64 * kRankWaves)
 k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
         const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
         uint64_t* wtime = nullptr) {
-  __shared__ BRecR sh[kBinCapR];
+  __shared__ BRecR sh_all[kRankWaves][kBinCapR];
   uint64_t t0 = wall_clock64();
-  const uint32_t b = blockIdx.x;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t b = blockIdx.x * kRankWaves + w;
   const uint32_t cnt = bcnt[b];
   if (cnt == 0 || rd->overflow) return;
+  BRecR* sh = sh_all[w];
   const uint32_t k = rd->k_total;
   const uint32_t n_pgroups = rd->n_pgroups;
   const bool isp = b >= (uint32_t)kNBPhase;
   const uint32_t soff = bsoff[b], poff = bpoff[b];
   const BRecR* src = brec + (size_t)b * kBinCapR;
-  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
+  for (uint32_t i = lane; i < cnt; i += 64) sh[i] = src[i];
   uint32_t parts = 1;
-  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
+  while (parts < 64 && cnt * parts * 2 <= 64u) parts <<= 1;
   const uint32_t per = (cnt + parts - 1) / parts;
-  __syncthreads();
-  const uint32_t t = threadIdx.x;
-  for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
-    rank_rec(rd, sh, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (uint32_t rb = 0; rb < cnt; rb += 64 / parts)
+    rank_rec(rd, sh, cnt, parts, per, rb + lane / parts, lane % parts, isp, k, n_pgroups,
              soff, poff, ring);
-  if (wtime && threadIdx.x == 0) {
+  if (wtime && lane == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
   }
