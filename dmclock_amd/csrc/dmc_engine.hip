@@ -1565,7 +1565,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
-    hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(64 * kRankWaves), 0, q->stream,
+    hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
                        q->rd, (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff,
                        (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
                        q->debug ? q->dbg_wtime : nullptr);

@@ -888,14 +888,6 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
   uint32_t fc;
   const CView cv = cand_view(tb, c);
   const uint32_t h = cv.h;
-  // the first queued entries are requested with the client record (the
-  // P walk after an R prefix would otherwise start a second round trip)
-  double touched = 0.0;
-  {
-    const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-    const uint32_t nt = c.c < 4u ? c.c : 4u;
-    for (uint32_t j = 0; j < nt; ++j) touched += ring[(h + j) & tb.qmask].arrival;
-  }
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
@@ -910,7 +902,6 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
     walk_p(tb, s, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
   }
-  keep(touched);
 }
 
 // Exclusive prefixes over the rank bins of the record counts, the group
@@ -1287,41 +1278,40 @@ __device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
 // instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
 // ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
 // branchless (wave-uniform trip counts, broadcast LDS reads).
-// One wave per rank bin, four bins per block.  The bin's records are
-// staged in the wave's LDS slice; each record is ranked against all of them
-// by `parts` adjacent lanes, each comparing a slice (parts = the largest
-// power of two with cnt * parts <= 64): a bin of more than 64 records
-// (skewed keys) takes ceil(cnt / 64) passes of one record per lane.  The
-// comparison is branchless (wave-uniform trip counts, broadcast LDS reads).
-constexpr int kRankWaves = 4;
-constexpr int kRankBlocksR = kNBR / kRankWaves;
-__global__ void __launch_bounds__(64 * kRankWaves)
+// One block per rank bin.  The bin's records are staged in LDS; each record
+// is ranked against all of them by `parts` adjacent lanes, each comparing a
+// slice (parts = the largest power of two with cnt * parts <= 256, at most
+// 64): a big bin (skewed keys) costs cnt^2 / 256 compare steps per lane
+// instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
+// ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
+// branchless (wave-uniform trip counts, broadcast LDS reads).  (One wave per
+// bin, four bins per block, was measured slower: the skewed P bins of up to
+// ~190 records then take three serial passes in one wave.)
+constexpr int kRankBlocksR = kNBR;
+__global__ void __launch_bounds__(kBlockR)
 k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
         const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
         uint64_t* wtime = nullptr) {
-  __shared__ BRecR sh_all[kRankWaves][kBinCapR];
+  __shared__ BRecR sh[kBinCapR];
   uint64_t t0 = wall_clock64();
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t b = blockIdx.x * kRankWaves + w;
+  const uint32_t b = blockIdx.x;
   const uint32_t cnt = bcnt[b];
   if (cnt == 0 || rd->overflow) return;
-  BRecR* sh = sh_all[w];
   const uint32_t k = rd->k_total;
   const uint32_t n_pgroups = rd->n_pgroups;
   const bool isp = b >= (uint32_t)kNBPhase;
   const uint32_t soff = bsoff[b], poff = bpoff[b];
   const BRecR* src = brec + (size_t)b * kBinCapR;
-  for (uint32_t i = lane; i < cnt; i += 64) sh[i] = src[i];
+  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
   uint32_t parts = 1;
-  while (parts < 64 && cnt * parts * 2 <= 64u) parts <<= 1;
+  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
   const uint32_t per = (cnt + parts - 1) / parts;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (uint32_t rb = 0; rb < cnt; rb += 64 / parts)
-    rank_rec(rd, sh, cnt, parts, per, rb + lane / parts, lane % parts, isp, k, n_pgroups,
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
+    rank_rec(rd, sh, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
              soff, poff, ring);
-  if (wtime && lane == 0) {
+  if (wtime && threadIdx.x == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
   }
