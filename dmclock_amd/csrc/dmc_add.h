@@ -141,20 +141,20 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   st.rinv = tb.rec[s].r_inv;
   st.winv = tb.rec[s].w_inv;
   st.linv = tb.rec[s].l_inv;
-  st.head = tb.qs[s].head;
-  st.count = tb.qs[s].count;
-  st.cd = tb.qs[s].cur_delta;
-  st.cr = tb.qs[s].cur_rho;
-  st.last_tick = tb.rec[s].last_tick;
-  st.flags = tb.flags[s];
+  const double pd = tb.rec[s].pd;
+  st.head = tb.sc[s].head;
+  st.count = tb.sc[s].count;
+  st.flags = tb.sc[s].flags;
+  st.cd = tb.aux[s].cur_delta;
+  st.cr = tb.aux[s].cur_rho;
+  st.last_tick = tb.aux[s].last_tick;
   st.front_set = false;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   // batched activations: this client's contribution to the idle reset before
   // and after its requests (see ActBuf)
   const bool idle0 = (st.flags & F_IDLE) != 0;
   const uint32_t count0 = st.count;
-  const double pd = act.cold ? tb.fr[s].pd : 0.0;
-  const double front_p0 = (act.cold && count0) ? tb.fr[s].p : 0.0;
+  const double front_p0 = (act.cold && count0) ? ring[st.head & tb.qmask].p : 0.0;
   const double prev_p0 = st.prev.p;
   bool act_done = false, chg_done = false;
   auto step = [&](uint32_t pos) {
@@ -200,15 +200,17 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   tb.rec[s].prev_p = st.prev.p;
   tb.rec[s].prev_l = st.prev.l;
   tb.rec[s].prev_arr = st.prev.arrival;
-  tb.qs[s].count = st.count;
-  tb.qs[s].cur_delta = st.cd;
-  tb.qs[s].cur_rho = st.cr;
-  tb.rec[s].last_tick = st.last_tick;
-  tb.flags[s] = st.flags;
+  tb.sc[s].count = (uint8_t)st.count;
+  tb.sc[s].flags = st.flags;
+  tb.aux[s].cur_delta = st.cd;
+  tb.aux[s].cur_rho = st.cr;
+  tb.aux[s].last_tick = st.last_tick;
   if (st.front_set) {
-    tb.fr[s].r = st.front.r;
-    tb.fr[s].p = st.front.p;
-    tb.fr[s].l = st.front.l;
+    // the new front's heap keys (pk with the prop_delta it has now; an
+    // activation later in the batch rewrites it, k_act_resolve)
+    tb.sc[s].r = st.front.r;
+    tb.sc[s].pk = __dadd_rn(st.front.p, pd);
+    tb.sc[s].l = st.front.l;
   }
   *out = st;
 }

@@ -6,11 +6,15 @@
 // and the library is built with -ffp-contract=off).
 //
 // Layout (per queue, N client slots, ring capacity Q):
-//   random-access records: ClientRec (64 B: prev tag, inverses, last_tick)
-//     and QState (16 B: head, count, cur_delta, cur_rho) per client;
-//   scanned columns: FrontRec (32 B: front r/p/l -- the heap keys of the
-//     reference, cached -- and prop_delta) and flags;
+//   ScanRec (32 B per slot, struct of arrays): the front request's heap keys
+//     -- reservation r, proportion key pk = p + prop_delta, limit l -- the
+//     ring cursor and the flags: everything a pass over the whole table
+//     reads, one coalesced 32-byte record per slot;
+//   ClientRec (64 B, random access): prev tag, inverses, prop_delta;
+//   ClientAux (16 B, random access): cur_delta / cur_rho, last_tick;
 //   request rings: ring[slot * Q + i], one 64-byte ReqEntry per request.
+// A client a walker or the add path visits costs its ClientRec line, its
+// ScanRec line and the ring lines it uses.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -37,28 +41,35 @@ struct alignas(16) ReqEntry {
 };
 static_assert(sizeof(ReqEntry) == 64, "ReqEntry must be 64 bytes");
 
-// Per-client state touched at random by the add, emit and apply kernels,
-// kept together so that one client costs one or two cache lines (the
-// struct-of-arrays columns below are the ones the table scans stream).
+// Per-client state the add, emit and apply kernels reach at random: one
+// line (the scanned columns are ScanRec's).
 struct alignas(64) ClientRec {
   double prev_r, prev_p, prev_l, prev_arr;  // ClientRec::prev_tag
   double r_inv, w_inv, l_inv;                // ClientInfo inverses
-  uint64_t last_tick;
+  double pd;                                 // ClientRec::prop_delta
 };
 static_assert(sizeof(ClientRec) == 64, "ClientRec must be 64 bytes");
-struct alignas(16) QState {
-  uint32_t head, count;         // request ring cursor
-  uint32_t cur_delta, cur_rho;  // last ReqParams
-};
-static_assert(sizeof(QState) == 16, "QState must be 16 bytes");
 
-// The front request's tag (the three heaps' keys, cached) and the client's
-// prop_delta: every pull scan streams all four; the add and apply kernels
-// rewrite them together.
-struct alignas(32) FrontRec {
-  double r, p, l, pd;
+// Per-client state only the add path (and delayed pops) touch.
+struct alignas(16) ClientAux {
+  uint32_t cur_delta, cur_rho;  // last ReqParams
+  uint64_t last_tick;
 };
-static_assert(sizeof(FrontRec) == 32, "FrontRec must be 32 bytes");
+static_assert(sizeof(ClientAux) == 16, "ClientAux must be 16 bytes");
+
+// The front request's heap keys (the reference's three heaps order clients
+// by these, dmclock_server.h:722-757), the ring cursor and the flags.  pk is
+// the ready heap's key p + prop_delta (:734-735), cached: it changes with
+// the front and with prop_delta (activations), and its writers compute it
+// with the reference's arithmetic (__dadd_rn).
+struct alignas(32) ScanRec {
+  double r, pk, l;
+  uint8_t head, count;  // request ring cursor (ring capacity <= 64)
+  uint8_t flags;        // F_*
+  uint8_t pad0;
+  uint32_t pad1;
+};
+static_assert(sizeof(ScanRec) == 32, "ScanRec must be 32 bytes");
 
 // Client table pointers (passed by value to kernels).
 struct Table {
@@ -70,9 +81,8 @@ struct Table {
   double reject_thr;
   double antic;
   ClientRec* rec;  // N
-  QState* qs;      // N
-  FrontRec* fr;    // N: front tag + prop_delta (scanned; one line per 4)
-  uint8_t* flags;
+  ScanRec* sc;     // N
+  ClientAux* aux;  // N
   ReqEntry* ring;
 };
 
@@ -153,16 +163,15 @@ struct CView {
 };
 
 __device__ inline CView load_view(const Table& tb, uint32_t s) {
-  const QState q = tb.qs[s];
   CView v;
-  v.h = q.head;
-  v.c = q.count;
-  v.cd = q.cur_delta;
-  v.cr = q.cur_rho;
+  v.h = tb.sc[s].head;
+  v.c = tb.sc[s].count;
+  v.cd = tb.aux[s].cur_delta;
+  v.cr = tb.aux[s].cur_rho;
   v.rinv = tb.rec[s].r_inv;
   v.winv = tb.rec[s].w_inv;
   v.linv = tb.rec[s].l_inv;
-  v.pd = tb.fr[s].pd;
+  v.pd = tb.rec[s].pd;
   return v;
 }
 

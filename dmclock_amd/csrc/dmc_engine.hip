@@ -138,23 +138,9 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
   uint32_t s = slots[i];
   if (s >= tb.n) return;
   // ClientRec(client, info, tick), dmclock_server.h:381-393
-  tb.rec[s].prev_r = 0.0;
-  tb.rec[s].prev_p = 0.0;
-  tb.rec[s].prev_l = 0.0;
-  tb.rec[s].prev_arr = 0.0;
-  tb.rec[s].r_inv = rinv[i];
-  tb.rec[s].w_inv = winv[i];
-  tb.rec[s].l_inv = linv[i];
-  tb.fr[s].pd = 0.0;
-  tb.fr[s].r = 0.0;
-  tb.fr[s].p = 0.0;
-  tb.fr[s].l = 0.0;
-  tb.qs[s].head = 0;
-  tb.qs[s].count = 0;
-  tb.qs[s].cur_delta = 1;
-  tb.qs[s].cur_rho = 1;
-  tb.rec[s].last_tick = tick;
-  tb.flags[s] = F_REG | (active ? 0 : F_IDLE);
+  tb.rec[s] = ClientRec{0.0, 0.0, 0.0, 0.0, rinv[i], winv[i], linv[i], 0.0};
+  tb.sc[s] = ScanRec{0.0, 0.0, 0.0, 0, 0, (uint8_t)(F_REG | (active ? 0 : F_IDLE)), 0, 0};
+  tb.aux[s] = ClientAux{1, 1, tick};
 }
 
 // ------------------------------------------------------------------ add path
@@ -200,12 +186,22 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
   uint32_t s = aslot[i];
   uint32_t m = acnt[s];
   acnt[s] = 0;  // ready for the next batch
-  if (!(tb.flags[s] & F_REG)) {
+  if (!(tb.sc[s].flags & F_REG)) {
     add_chain_notreg(p, s, m, abuf, aslot);
     return;
   }
   AddState st;
   add_chain_slot(tb, p, s, m, i, abuf, aslot, act, &st);
+}
+
+// The end of an idle reset (:981-984): the client's new prop_delta, its
+// front's cached proportion key recomputed with it, idle cleared.
+__device__ inline void activate_slot(const Table& tb, uint32_t s, double pd) {
+  tb.rec[s].pd = pd;
+  const ScanRec r = tb.sc[s];
+  if (r.count)
+    tb.sc[s].pk = __dadd_rn(tb.ring[(size_t)s * tb.q + (r.head & tb.qmask)].p, pd);
+  tb.sc[s].flags = (uint8_t)(r.flags & ~F_IDLE);
 }
 
 // idle reset, :937-985: L = min over non-idle clients of
@@ -214,10 +210,10 @@ __global__ void k_contrib_min(Table tb, uint64_t* parts) {
   uint64_t m = kMaxKey;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    uint8_t f = tb.flags[s];
-    if ((f & F_REG) && !(f & F_IDLE)) {
-      double p = tb.qs[s].count ? tb.fr[s].p : tb.rec[s].prev_p;
-      uint64_t k = okey(__dadd_rn(p, tb.fr[s].pd));
+    const ScanRec r = tb.sc[s];
+    if ((r.flags & F_REG) && !(r.flags & F_IDLE)) {
+      // (has_request ? front.p : prev.p) + prop_delta; pk is the former
+      uint64_t k = okey(r.count ? r.pk : __dadd_rn(tb.rec[s].prev_p, tb.rec[s].pd));
       m = k < m ? k : m;
     }
   }
@@ -252,8 +248,7 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
     double L = from_okey(*lmin);
     if (L < lowest) lowest = L;
   }
-  if (lowest < trigger) tb.fr[s].pd = __dsub_rn(lowest, t);
-  tb.flags[s] &= (uint8_t)~F_IDLE;
+  activate_slot(tb, s, lowest < trigger ? __dsub_rn(lowest, t) : tb.rec[s].pd);
 }
 
 // Batched activations, step 1 (after k_add_link, before k_add_chain): the
@@ -263,12 +258,10 @@ __global__ void k_act_base(Table tb, const uint32_t* acnt, uint64_t* parts) {
   uint64_t m = kMaxKey;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    uint8_t f = tb.flags[s];
-    if ((f & F_REG) && !(f & F_IDLE)) {
-      uint32_t c = tb.qs[s].count;
-      if (c == 0 && acnt[s]) continue;  // changes inside the batch: positions
-      double p = c ? tb.fr[s].p : tb.rec[s].prev_p;
-      uint64_t k = okey(__dadd_rn(p, tb.fr[s].pd));
+    const ScanRec r = tb.sc[s];
+    if ((r.flags & F_REG) && !(r.flags & F_IDLE)) {
+      if (r.count == 0 && acnt[s]) continue;  // changes inside the batch: positions
+      uint64_t k = okey(r.count ? r.pk : __dadd_rn(tb.rec[s].prev_p, tb.rec[s].pd));
       m = k < m ? k : m;
     }
   }
@@ -342,7 +335,7 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
     ap[k] = act.actp[q];
     at[k] = rq.time;
     aslot[k] = rq.slot;
-    apd[k] = tb.fr[rq.slot].pd;
+    apd[k] = tb.rec[rq.slot].pd;
   }
 }
 
@@ -393,8 +386,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
     __syncthreads();
     const uint32_t fail = s_fail;
     if (in && k < fail) {
-      tb.fr[aslot[k]].pd = pd;
-      tb.flags[aslot[k]] &= (uint8_t)~F_IDLE;
+      activate_slot(tb, aslot[k], pd);
     }
     if (fail != 0xffffffffu) {
       if (fail > k0 && t == fail - k0 - 1) s_minpre = incl;
@@ -465,8 +457,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
       }
       __syncthreads();
       if (k < m) {
-        tb.fr[aslot[k]].pd = cpd[t];
-        tb.flags[aslot[k]] &= (uint8_t)~F_IDLE;
+        activate_slot(tb, aslot[k], cpd[t]);
       }
       __syncthreads();
     }
@@ -490,14 +481,15 @@ __device__ inline void step_scan_body(const Table& tb, double now, StepRed* part
   uint32_t nany = 0, nrd = 0, nnr = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    if (!tb.qs[s].count) continue;
+    const ScanRec sr = tb.sc[s];
+    if (!sr.count) continue;
     ++nany;
-    ArgMin a{okey(tb.fr[s].r), s, 1};
+    ArgMin a{okey(sr.r), s, 1};
     r = argmin_combine(r, a);
-    double l = tb.fr[s].l;
-    bool rdy = (tb.flags[s] & F_READY) || l <= now;
-    double pv = tb.fr[s].p;
-    uint64_t kp = okey(__dadd_rn(pv, tb.fr[s].pd));
+    double l = sr.l;
+    bool rdy = (sr.flags & F_READY) || l <= now;
+    double pv = sr.pk;  // p + prop_delta: p < inf iff pv < inf
+    uint64_t kp = okey(pv);
     uint64_t kl = okey(l);
     if (rdy) {
       ++nrd;
@@ -725,8 +717,9 @@ __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
   if (!sc->mark) return;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
-    if (tb.qs[s].count && !(tb.flags[s] & F_READY) && tb.fr[s].l <= now)
-      tb.flags[s] |= F_READY;
+    const ScanRec sr = tb.sc[s];
+    if (sr.count && !(sr.flags & F_READY) && sr.l <= now)
+      tb.sc[s].flags = sr.flags | F_READY;
   }
 }
 
@@ -740,7 +733,8 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
   uint32_t s = sc->slot;
   bool prio = sc->prio != 0;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  uint32_t h = tb.qs[s].head, c = tb.qs[s].count;
+  const ScanRec sr = tb.sc[s];
+  uint32_t h = sr.head, c = sr.count;
   ReqEntry popped = ring[h];
   dmc_decision d;
   d.handle = popped.handle;
@@ -758,7 +752,7 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
     ReqEntry& f = ring[nh];
     Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
     Tag3 nt;
-    uint32_t cd = tb.qs[s].cur_delta, cr = tb.qs[s].cur_rho;
+    uint32_t cd = tb.aux[s].cur_delta, cr = tb.aux[s].cur_rho;
     if (make_tag(pt, rinv, tb.rec[s].w_inv, tb.rec[s].l_inv, cd, cr, f.arrival, f.cost,
                  tb.antic, &nt)) {
       f.r = nt.r;
@@ -774,7 +768,7 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
       tb.rec[s].prev_p = pp;
       tb.rec[s].prev_l = pl;
       tb.rec[s].prev_arr = nt.arrival;
-      tb.rec[s].last_tick = tick;
+      tb.aux[s].last_tick = tick;
     }
   }
   if (prio) {  // reduce_reservation_tags, :1077-1111
@@ -789,15 +783,14 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
     }
     tb.rec[s].prev_r = __dsub_rn(tb.rec[s].prev_r, o);
   }
-  tb.qs[s].head = nh;
-  tb.qs[s].count = nc;
-  tb.flags[s] &= (uint8_t)~F_READY;
+  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc, (uint8_t)(sr.flags & ~F_READY), 0, 0};
   if (nc) {
     const ReqEntry& f = ring[nh];
-    tb.fr[s].r = f.r;
-    tb.fr[s].p = f.p;
-    tb.fr[s].l = f.l;
+    o.r = f.r;
+    o.pk = __dadd_rn(f.p, tb.rec[s].pd);
+    o.l = f.l;
   }
+  tb.sc[s] = o;
   atomicAdd(&sched[prio ? 1 : 0], 1ull);
 }
 
@@ -806,7 +799,7 @@ __global__ void k_count_requests(Table tb, unsigned long long* out) {
   unsigned long long t = 0;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x)
-    t += tb.qs[s].count;
+    t += tb.sc[s].count;
   for (int d = 32; d > 0; d >>= 1) t += shfl_down_u64(t, d);
   __shared__ unsigned long long sh[kBlock / 64];
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = t;
@@ -856,7 +849,7 @@ struct dmc_queue {
   // device scratch
   CandRec* cand = nullptr;    // N: candidates of the round (k_remit)
   uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
-  uint8_t* mr = nullptr;      // N: R prefix length
+  uint32_t* meta = nullptr;   // N: k_rscan's per-slot R-prefix length, flags, head, count
   RoundPart* rparts = nullptr; // k_rscan's per-block partials
   Round* rd = nullptr;
   Round h_rd_copy{};          // host copy of the last round's summary
@@ -866,7 +859,6 @@ struct dmc_queue {
   uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
   uint32_t* sbn = nullptr;    // rank-bin table per phase and histogram bin (k_rhist's pick)
-  uint16_t* hc = nullptr;     // N: ring head | count << 8 as k_rscan saw them
   uint64_t *skr = nullptr, *skp = nullptr;  // N / kSample: the threshold histogram's sample
   bool exact_next = false;    // re-run a round whose sampled threshold failed exactly
   int sample_mode = 1;        // DMC_OPT_SAMPLE: 0 exact, 1 sampled, 2 sampled (test: no margin)
@@ -1537,7 +1529,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
   pb(q, DMC_PROF_SCAN);
   hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
-                     q->keyp, q->mr, q->hc, q->rparts, q->rd, cp,
+                     q->keyp, q->meta, q->rparts, q->rd, cp,
                      sampled ? q->skr : nullptr, sampled ? q->skp : nullptr);
   pe(q);
   pb(q, DMC_PROF_SELECT);
@@ -1555,8 +1547,8 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   pb(q, DMC_PROF_EMIT);
   hipLaunchKernelGGL(k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk), dim3(kEmitThreads),
                      0, q->stream, tb, q->rd, (const uint64_t*)q->keyr,
-                     (const uint64_t*)q->keyp, (const uint8_t*)q->mr,
-                     (const uint16_t*)q->hc, q->cand, radix ? nullptr : q->brec,
+                     (const uint64_t*)q->keyp, (const uint32_t*)q->meta,
+                     q->cand, radix ? nullptr : q->brec,
                      q->bcount, q->bsize, (const uint32_t*)q->sbn, q->dense, q->ecap,
                      q->bcnt, q->bsoff, q->bpoff, q->emit_done);
   pe(q);
@@ -1626,7 +1618,7 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   Table tb = q->tb;
   uint64_t* skr = sampled ? q->skr : nullptr;
   uint64_t* skp = sampled ? q->skp : nullptr;
-  void* args[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp,
+  void* args[] = {&tb, &q->keyr, &q->keyp, &q->meta, &q->rparts, &q->rd, &cp,
                   &skr, &skp};
   return graph_replay(q, *g, args);
 }
@@ -1870,16 +1862,14 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
                ? DMC_OK : DMC_EDEVICE;
   };
   int rc = 0;
-  rc |= A(&t.rec, N); rc |= A(&t.qs, N);
-  rc |= A(&t.fr, N); rc |= A(&t.flags, N);
+  rc |= A(&t.rec, N); rc |= A(&t.sc, N); rc |= A(&t.aux, N);
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
   rc |= A(&q->cand, N);
   rc |= A(&q->keyr, N);
   rc |= A(&q->keyp, N);
-  rc |= A(&q->mr, N);
+  rc |= A(&q->meta, N);
   rc |= A(&q->hist, kShards * 2 * kHistBinsR);
   rc |= A(&q->sbn, 2 * kHistBinsR);
-  rc |= A(&q->hc, N);
   rc |= A(&q->skr, (N + kSample - 1) / kSample);
   rc |= A(&q->skp, (N + kSample - 1) / kSample);
   q->step_grid = grid_for(N, 1024);
@@ -1939,10 +1929,10 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
-  void* ptrs[] = {t.rec, t.qs, t.fr, t.flags,
+  void* ptrs[] = {t.rec, t.sc, t.aux,
                   t.ring,
-                  q->cand, q->keyr, q->keyp, q->mr, q->hist, q->sbn,
-                  q->hc, q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->cand, q->keyr, q->keyp, q->meta, q->hist, q->sbn,
+                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
@@ -2043,10 +2033,10 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   if (int rc0 = settle_act(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   uint8_t f;
-  HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&f, &q->tb.sc[slot].flags, 1, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   f |= F_IDLE;
-  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(&q->tb.sc[slot].flags, &f, 1, hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   if (!q->idle_h[slot]) {
     q->idle_h[slot] = 1;
@@ -2057,7 +2047,7 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
 
 __global__ void k_mark_idle(Table tb, uint32_t n, const uint32_t* slots) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) tb.flags[slots[i]] |= F_IDLE;
+  if (i < n) tb.sc[slots[i]].flags |= F_IDLE;
 }
 
 int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) {
@@ -2109,11 +2099,11 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
 
 static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
                         uint32_t* head) {
-  QState qs;
-  HIP_OK(hipMemcpyAsync(&qs, q->tb.qs + slot, sizeof(qs), hipMemcpyDeviceToHost,
+  ScanRec sr;
+  HIP_OK(hipMemcpyAsync(&sr, q->tb.sc + slot, sizeof(sr), hipMemcpyDeviceToHost,
                         q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
-  uint32_t h = qs.head, c = qs.count;
+  uint32_t h = sr.head, c = sr.count;
   std::vector<ReqEntry> ring(q->p.ring_capacity);
   HIP_OK(hipMemcpyAsync(ring.data(), q->tb.ring + (size_t)slot * q->p.ring_capacity,
                         sizeof(ReqEntry) * q->p.ring_capacity, hipMemcpyDeviceToHost,
@@ -2126,7 +2116,9 @@ static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents
 }
 
 // rewrite a client's queue (after filtering), keeping the front's ready flag
-// only if the front survived
+// only if the front survived; the new front's keys with the client's
+// prop_delta (an IEEE double add on the host, no contraction: the same
+// value as the device's __dadd_rn)
 static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>& ents,
                        bool front_kept) {
   uint32_t Q = q->p.ring_capacity;
@@ -2134,20 +2126,21 @@ static int write_queue(dmc_queue* q, uint32_t slot, const std::vector<ReqEntry>&
   for (size_t i = 0; i < ents.size(); ++i) ring[i] = ents[i];
   HIP_OK(hipMemcpyAsync(q->tb.ring + (size_t)slot * Q, ring.data(), sizeof(ReqEntry) * Q,
                         hipMemcpyHostToDevice, q->stream));
-  uint32_t hc[2] = {0, (uint32_t)ents.size()};  // head, count
-  uint32_t c = hc[1];
-  HIP_OK(hipMemcpyAsync(&q->tb.qs[slot].head, hc, sizeof(hc), hipMemcpyHostToDevice,
-                        q->stream));
-  if (c) {
-    // r, p, l are contiguous in FrontRec and in ReqEntry
-    HIP_OK(hipMemcpyAsync(&q->tb.fr[slot].r, &ring[0].r, 24, hipMemcpyHostToDevice,
-                          q->stream));
-  }
-  uint8_t f;
-  HIP_OK(hipMemcpyAsync(&f, q->tb.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  ScanRec sr;
+  double pd = 0.0;
+  HIP_OK(hipMemcpyAsync(&sr, q->tb.sc + slot, sizeof(sr), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&pd, &q->tb.rec[slot].pd, 8, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
-  if (!front_kept || !c) f &= (uint8_t)~F_READY;
-  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  const uint32_t c = (uint32_t)ents.size();
+  ScanRec o{0.0, 0.0, 0.0, 0, (uint8_t)c, sr.flags, 0, 0};
+  if (c) {
+    o.r = ring[0].r;
+    volatile double pk = ring[0].p + pd;
+    o.pk = pk;
+    o.l = ring[0].l;
+  }
+  if (!front_kept || !c) o.flags &= (uint8_t)~F_READY;
+  HIP_OK(hipMemcpyAsync(q->tb.sc + slot, &o, sizeof(o), hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
 }
@@ -2165,10 +2158,8 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
   for (size_t i = 0; i < ents.size() && i < cap; ++i)
     if (handles_out) handles_out[i] = ents[i].handle;
   if (n_out) *n_out = (uint32_t)ents.size();
-  uint32_t z = 0;
-  uint8_t f = 0;
-  HIP_OK(hipMemcpyAsync(&q->tb.qs[slot].count, &z, 4, hipMemcpyHostToDevice, q->stream));
-  HIP_OK(hipMemcpyAsync(q->tb.flags + slot, &f, 1, hipMemcpyHostToDevice, q->stream));
+  const ScanRec z{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};  // no requests, not registered
+  HIP_OK(hipMemcpyAsync(q->tb.sc + slot, &z, sizeof(z), hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   if (q->idle_h[slot]) --q->n_idle;
   q->reg_h[slot] = 0;
@@ -2184,17 +2175,14 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   const Table& t = q->tb;
   uint8_t f = 0;
   ClientRec cr;
-  QState qs;
+  ScanRec sr;
+  ClientAux ax;
   HIP_OK(hipMemcpyAsync(&cr, t.rec + slot, sizeof(cr), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&qs, t.qs + slot, sizeof(qs), hipMemcpyDeviceToHost, q->stream));
-  FrontRec fr;
-  HIP_OK(hipMemcpyAsync(&fr, t.fr + slot, sizeof(fr), hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(&f, t.flags + slot, 1, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&sr, t.sc + slot, sizeof(sr), hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipMemcpyAsync(&ax, t.aux + slot, sizeof(ax), hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
-  s->prop_delta = fr.pd;
-  s->front_r = fr.r;
-  s->front_p = fr.p;
-  s->front_l = fr.l;
+  f = sr.flags;
+  s->prop_delta = cr.pd;
   s->prev_r = cr.prev_r;
   s->prev_p = cr.prev_p;
   s->prev_l = cr.prev_l;
@@ -2202,16 +2190,20 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   s->r_inv = cr.r_inv;
   s->w_inv = cr.w_inv;
   s->l_inv = cr.l_inv;
-  s->last_tick = cr.last_tick;
-  s->count = qs.count;
-  s->cur_delta = qs.cur_delta;
-  s->cur_rho = qs.cur_rho;
-  uint32_t head = qs.head;
+  s->last_tick = ax.last_tick;
+  s->count = sr.count;
+  s->cur_delta = ax.cur_delta;
+  s->cur_rho = ax.cur_rho;
+  uint32_t head = sr.head;
   if (s->count) {
+    // the front's tag is its ring entry's (ScanRec caches r, p + pd, l)
     ReqEntry e;
     HIP_OK(hipMemcpyAsync(&e, t.ring + (size_t)slot * t.q + head, sizeof(e),
                           hipMemcpyDeviceToHost, q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
+    s->front_r = e.r;
+    s->front_p = e.p;
+    s->front_l = e.l;
     s->front_arrival = e.arrival;
   } else {
     s->front_r = s->front_p = s->front_l = 0.0;
@@ -2226,8 +2218,8 @@ int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
   if (!q || !out || n > q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
   if (n)
-    HIP_OK(hipMemcpy2DAsync(out, sizeof(uint64_t), &q->tb.rec[0].last_tick,
-                            sizeof(ClientRec), sizeof(uint64_t), n,
+    HIP_OK(hipMemcpy2DAsync(out, sizeof(uint64_t), &q->tb.aux[0].last_tick,
+                            sizeof(ClientAux), sizeof(uint64_t), n,
                             hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
@@ -2354,7 +2346,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         const bool sampled = use_sample(q, false);
         uint64_t* skr = sampled ? q->skr : nullptr;
         uint64_t* skp = sampled ? q->skp : nullptr;
-        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->mr, &q->hc, &q->rparts, &q->rd, &cp,
+        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->meta, &q->rparts, &q->rd, &cp,
                       &skr, &skp};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;

@@ -210,19 +210,21 @@ constexpr uint32_t kSampleMinN = 1u << 16;
 
 struct ScanCols {
   uint32_t c, h;
-  double fr, fp, fl, pd;
+  double fr, pk, fl;  // the front's heap keys (ScanRec)
   uint8_t f;
 };
 
 __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
                                  double now, uint64_t* keyr, uint64_t* keyp,
-                                 uint8_t* mr, uint16_t* hc, uint64_t* skr, uint64_t* skp,
+                                 uint32_t* meta, uint64_t* skr, uint64_t* skp,
                                  RoundPart& acc) {
   uint64_t kr = kMaxKey, kp = kMaxKey;
   uint32_t m = 0;
+  uint8_t f = x.f;
   if (x.c) {
     Tag3 pf;
     bool have_pf = true, ready;
+    double pkv = kInf;
     if (x.fr <= now) {
       kr = okey(x.fr);
       if (!tb.delayed) {
@@ -245,13 +247,18 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
       }
       have_pf = m < x.c;
       ready = pf.l <= now;
+      // the post-R front's key, with the client's prop_delta (ClientRec)
+      if (have_pf && ready) pkv = __dadd_rn(pf.p, tb.rec[s].pd);
     } else {
-      pf.p = x.fp;
-      pf.l = x.fl;
-      ready = (x.f & F_READY) || pf.l <= now;
-      if (!(x.f & F_READY) && pf.l <= now) tb.flags[s] = x.f | F_PMARK;
+      pkv = x.pk;
+      ready = (x.f & F_READY) || x.fl <= now;
+      if (!(x.f & F_READY) && x.fl <= now) {
+        f = x.f | F_PMARK;
+        tb.sc[s].flags = f;
+      }
     }
-    if (have_pf && ready && pf.p < kInf) kp = okey(__dadd_rn(pf.p, x.pd));
+    // p < inf iff p + prop_delta < inf (prop_delta is finite)
+    if (have_pf && ready && pkv < kInf) kp = okey(pkv);
   }
   keyr[s] = kr;
   keyp[s] = kp;
@@ -259,8 +266,9 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
     skr[s / kSample] = kr;
     skp[s / kSample] = kp;
   }
-  mr[s] = (uint8_t)m;
-  hc[s] = (uint16_t)((x.c ? x.h : 0u) | (x.c << 8));
+  // the candidate record's fields for k_remit: R-prefix length, flags (with
+  // a pending mark this scan set), ring head and count
+  meta[s] = (m & 0xffu) | ((uint32_t)f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
   if (kr != kMaxKey) {
     ++acc.cnt[0];
     acc.n_r += m;
@@ -368,7 +376,7 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
 // for a RoundPart, too many to run in every wave of the block).
 __global__ void __launch_bounds__(kScanBlock)
-k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
+k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
         RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
@@ -393,19 +401,19 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint8_t* mr, uint16_t* hc,
     uint32_t s = base + j * blockDim.x;
     x[j].c = 0;
     if (s < tb.n) {
-      x[j].c = tb.qs[s].count;
-      x[j].h = tb.qs[s].head;
-      x[j].fr = tb.fr[s].r;
-      x[j].fp = tb.fr[s].p;
-      x[j].fl = tb.fr[s].l;
-      x[j].pd = tb.fr[s].pd;
-      x[j].f = tb.flags[s];
+      const ScanRec r = tb.sc[s];
+      x[j].c = r.count;
+      x[j].h = r.head;
+      x[j].fr = r.r;
+      x[j].pk = r.pk;
+      x[j].fl = r.l;
+      x[j].f = r.flags;
     }
   }
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, mr, hc, skr, skp, acc);
+    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, meta, skr, skp, acc);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
@@ -864,14 +872,13 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
   v.c = cr.c;
   v.cd = v.cr = 0;
   if (tb.delayed) {
-    const QState q = tb.qs[s];
-    v.cd = q.cur_delta;
-    v.cr = q.cur_rho;
+    v.cd = tb.aux[s].cur_delta;
+    v.cr = tb.aux[s].cur_rho;
   }
   v.rinv = tb.rec[s].r_inv;
   v.winv = tb.rec[s].w_inv;
   v.linv = tb.rec[s].l_inv;
-  v.pd = tb.fr[s].pd;
+  v.pd = tb.rec[s].pd;
   return v;
 }
 
@@ -1071,7 +1078,7 @@ constexpr int kEmitThreads = 1024;
 constexpr uint32_t kEmitChunk = kEmitThreads * 4;
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
-        const uint8_t* mr, const uint16_t* hc, CandRec* cand, BRecR* brec,
+        const uint32_t* meta, CandRec* cand, BRecR* brec,
         uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
         uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
         uint32_t* done) {
@@ -1093,31 +1100,27 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
     for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
   __syncthreads();  // s_cnt zeroed before any wave adds to it
   uint64_t kr[4], kp[4];
-  uint8_t f[4], m[4];
-  uint16_t hcv[4];
+  uint32_t mt[4];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   if (s0 + 4 <= n) {
     const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
     const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
     ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
-    uchar4 f4 = *reinterpret_cast<const uchar4*>(tb.flags + s0);
-    uchar4 m4 = *reinterpret_cast<const uchar4*>(mr + s0);
-    ushort4 h4 = *reinterpret_cast<const ushort4*>(hc + s0);
+    uint4 m4 = *reinterpret_cast<const uint4*>(meta + s0);
     kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
     kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
-    f[0] = f4.x; f[1] = f4.y; f[2] = f4.z; f[3] = f4.w;
-    m[0] = m4.x; m[1] = m4.y; m[2] = m4.z; m[3] = m4.w;
-    hcv[0] = h4.x; hcv[1] = h4.y; hcv[2] = h4.z; hcv[3] = h4.w;
+    mt[0] = m4.x; mt[1] = m4.y; mt[2] = m4.z; mt[3] = m4.w;
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bool in = s0 + j < n;
       kr[j] = in ? keyr[s0 + j] : kMaxKey;
       kp[j] = in ? keyp[s0 + j] : kMaxKey;
-      f[j] = in ? tb.flags[s0 + j] : 0;
-      m[j] = in ? mr[s0 + j] : 0;
-      hcv[j] = in ? hc[s0 + j] : 0;
+      mt[j] = in ? meta[s0 + j] : 0;
     }
   }
+  uint8_t f[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = (uint8_t)(mt[j] >> 8);
   uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1127,7 +1130,7 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
     if (cr || cp) {
       bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
     } else if (f[j] & F_PMARK) {
-      tb.flags[s0 + j] = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
+      tb.sc[s0 + j].flags = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
   uint32_t cnt = 0, nr = 0, np = 0;
@@ -1168,8 +1171,8 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
     for (int j = 0; j < 4; ++j) {
       const uint32_t b = (bits >> (2 * j)) & 3u;
       if (b)
-        bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), m[j],
-                          (uint8_t)(hcv[j] & 0xff), (uint8_t)(hcv[j] >> 8)};
+        bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), (uint8_t)mt[j],
+                          (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
     }
   }
   if (threadIdx.x == 0) {
@@ -1534,7 +1537,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   const CView cv = cand_view(tb, cd);
   Tag3 prev{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   if (rc.ovf) {
-    if (f0 & F_PMARK) tb.flags[s] = (uint8_t)(f0 & ~F_PMARK);
+    if (f0 & F_PMARK) tb.sc[s].flags = (uint8_t)(f0 & ~F_PMARK);
     return;
   }
   const double now = rc.now;
@@ -1568,7 +1571,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   uint32_t pops = popsR + popsP;
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
-      tb.flags[s] = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
+      tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
     return;
   }
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
@@ -1604,20 +1607,21 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     tb.rec[s].prev_p = prev.p;
     tb.rec[s].prev_l = prev.l;
     tb.rec[s].prev_arr = prev.arrival;
-    if (c >= 2) tb.rec[s].last_tick = tick;
+    if (c >= 2) tb.aux[s].last_tick = tick;
   }
-  tb.qs[s].head = nh;
-  tb.qs[s].count = nc2;
+  // the new front's heap keys, cursor and flags: one 32-byte ScanRec store
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
+  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
   if (nc2) {
-    tb.fr[s].r = front.r;
-    tb.fr[s].p = front.p;
-    tb.fr[s].l = front.l;
+    o.r = front.r;
+    o.pk = __dadd_rn(front.p, cv.pd);
+    o.l = front.l;
     bool seen = popsP ? (terminal || (g_last != kNoneR && v.last_idx < g_last))
                       : p_runs;
     if (seen && front.l <= now) f |= F_READY;
   }
-  tb.flags[s] = f;
+  o.flags = f;
+  tb.sc[s] = o;
 }
 
 // Candidates (the dense list) with dispatched pops replay their walks for
