@@ -175,20 +175,71 @@ __device__ inline CView load_view(const Table& tb, uint32_t s) {
   return v;
 }
 
-// Touch the client's queued entries past the first two (up to kTouch) so
-// that their lines are requested together with the walk's first loads: the
-// walkers, reduced_r and the apply reductions then hit the cache instead of
-// paying one dependent memory round trip per entry.  Returns a value the
-// caller consumes once the walk is done (keeps the loads alive).
-constexpr uint32_t kTouch = 8;
-__device__ inline double touch_ring(const Table& tb, uint32_t s, uint32_t h,
-                                    uint32_t c) {
-  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  const uint32_t n = c < kTouch ? c : kTouch;
-  double acc = 0.0;
-  for (uint32_t j = 2; j < n; ++j) acc += ring[(h + j) & tb.qmask].arrival;
-  return acc;
+// A client's queue as the walkers read it: queue position i (0 = front) is
+// ring entry (h + i) & qmask.  The first `ns` positions may be staged (LDS)
+// by the caller: one burst of wide loads before the walk instead of one
+// dependent 64-byte read per visit (on gfx950 every wait for a load also
+// waits for the wave's earlier stores, so interleaved entry reads and
+// decision stores serialise).
+struct RingView {
+  const ReqEntry* g;   // the client's ring
+  const ReqEntry* st;  // staged positions [0, ns)
+  uint32_t h, qmask, ns;
+  __device__ ReqEntry at(uint32_t i) const {
+    if (i < ns) return st[i];
+    return g[(h + i) & qmask];
+  }
+  __device__ double r_at(uint32_t i) const {
+    if (i < ns) return st[i].r;
+    return g[(h + i) & qmask].r;
+  }
+  // reduce_reservation_tags' offset of position i (:1090-1091)
+  __device__ double offset_at(uint32_t i, double rinv) const {
+    uint32_t cost, rho;
+    if (i < ns) {
+      cost = st[i].cost;
+      rho = st[i].rho;
+    } else {
+      cost = g[(h + i) & qmask].cost;
+      rho = g[(h + i) & qmask].rho;
+    }
+    return resv_offset(rinv, cost, rho);
+  }
+};
+
+__device__ inline RingView ring_view(const Table& tb, uint32_t s, uint32_t h) {
+  return RingView{tb.ring + (size_t)s * tb.q, nullptr, h, tb.qmask, 0};
 }
+
+// Stage the first min(c, K) queue positions of slot s into st (this
+// thread's LDS slice): all loads issued before the first store.
+template <int K>
+__device__ inline RingView stage_ring(const Table& tb, uint32_t s, uint32_t h,
+                                      uint32_t c, ReqEntry* st) {
+  RingView v = ring_view(tb, s, h);
+  if (!st) return v;
+  const uint32_t ns = c < (uint32_t)K ? c : (uint32_t)K;
+  // 16-byte chunks: every load of the burst is issued before the first
+  // LDS store (the copies go through registers, never a private array)
+  uint4 x[K][4];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint4* src = reinterpret_cast<const uint4*>(v.g + ((h + j) & v.qmask));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[j][k] = (uint32_t)j < ns ? src[k] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    uint4* dst = reinterpret_cast<uint4*>(st + j);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((uint32_t)j < ns) dst[k] = x[j][k];
+  }
+  v.st = st;
+  v.ns = ns;
+  return v;
+}
+
 __device__ inline void keep(double v) { asm volatile("" ::"v"(v)); }
 
 // Visitor callbacks: pop(i, tag, cost, handle, prio, dec, tie) for each pop
@@ -207,25 +258,21 @@ struct NullVisit {
 // Returns the number of pops; leaves the final prev tag in *prev (delayed).
 // `stamped` (apply): walk exactly the entries the ranking stamped.
 template <typename V>
-__device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
+__device__ inline uint32_t walk_r(const Table& tb, const RingView& rv, const CView& cv,
                                   double now, uint64_t T, uint32_t limit, V& vis,
                                   Tag3* prev_io, Tag3* front_out,
                                   uint32_t* front_cost, bool stamped = false) {
-  const uint32_t h = cv.h, c = cv.c;
+  const uint32_t c = cv.c;
   uint32_t n = 0;
   if (c == 0) return 0;
-  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   if (!tb.delayed) {
-    // one entry loaded ahead: the walk's loads are not a dependent chain
-    ReqEntry e = ring[h & tb.qmask];
-    ReqEntry nx = ring[(h + 1) & tb.qmask];
+    ReqEntry e = rv.at(0);
     while (n < c && n < limit) {
       if (!(e.r <= now) || okey(e.r) > T || (stamped && e.dec == kNoDec)) break;
       vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false, e.dec,
               e.tie);
       ++n;
-      e = nx;
-      nx = ring[(h + n + 1) & tb.qmask];
+      if (n < c) e = rv.at(n);
     }
     if (front_out && n < c) {
       *front_out = Tag3{e.r, e.p, e.l, e.arrival};
@@ -234,7 +281,7 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
     return n;
   }
   // delayed: front tag is stored; later tags are computed at pop time
-  ReqEntry e0 = ring[h & tb.qmask];
+  ReqEntry e0 = rv.at(0);
   Tag3 cur{e0.r, e0.p, e0.l, e0.arrival};
   uint32_t cur_cost = e0.cost, cur_dec = e0.dec, cur_tie = e0.tie;
   uint64_t cur_h = e0.handle;
@@ -243,7 +290,7 @@ __device__ inline uint32_t walk_r(const Table& tb, uint32_t s, const CView& cv,
     vis.pop(n, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
     ++n;
     if (n < c) {
-      const ReqEntry e = ring[(h + n) & tb.qmask];
+      const ReqEntry e = rv.at(n);
       Tag3 nt;
       if (!make_tag(cur, cv.rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival,
                     e.cost, tb.antic, &nt))
@@ -284,48 +331,43 @@ struct WalkP {
 
 // immediate-mode reservation tag of entry i after the reductions of the
 // priority pops before it, applied in order (:1088-1095)
-__device__ inline double reduced_r(const ReqEntry* ring, uint32_t h,
-                                   uint32_t qmask, uint32_t i, uint64_t pmask,
+__device__ inline double reduced_r(const RingView& rv, uint32_t i, uint64_t pmask,
                                    double rinv) {
-  double r = ring[(h + i) & qmask].r;
+  double r = rv.r_at(i);
   for (uint32_t j = 0; j < i; ++j)
-    if ((pmask >> j) & 1ull) {
-      const ReqEntry& ej = ring[(h + j) & qmask];
-      r = __dsub_rn(r, resv_offset(rinv, ej.cost, ej.rho));
-    }
+    if ((pmask >> j) & 1ull) r = __dsub_rn(r, rv.offset_at(j, rinv));
   return r;
 }
 
-// The walk starts at ring offset `start` (the front left after the round's
-// reservation pops); `start_tag` is that entry's tag in delayed mode (the
-// walk_r front, used iff use_start_tag), `ready0` its ready flag (only the
-// untouched front can carry one: a front exposed by a reservation pop is ready
-// iff limit <= now).
+// The walk starts at queue position `start` (the front left after the
+// round's reservation pops); `start_tag` is that entry's tag in delayed mode
+// (the walk_r front, used iff use_start_tag), `ready0` its ready flag (only
+// the untouched front can carry one: a front exposed by a reservation pop is
+// ready iff limit <= now).
 // `kstamp` != 0 (apply, kstamp = the round's k): walk exactly the groups the
 // ranking stamped; a group stamped at decision offset o keeps at most
 // kstamp - o pops (the round's last group can be cut inside its run).
 template <typename V>
-__device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
+__device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView& cv,
                                double now, uint64_t T, uint32_t limit, V& vis,
                                Tag3* prev_io, Tag3* front_out,
                                uint32_t* front_cost, uint32_t start,
                                Tag3 start_tag, bool use_start_tag, bool ready0,
                                uint32_t kstamp = 0) {
   WalkP w{0, 0, 0};
-  const uint32_t h = cv.h, c = cv.c;
+  const uint32_t c = cv.c;
   if (start >= c) return w;
-  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   const double pdv = cv.pd, rinv = cv.rinv;
   if (!tb.delayed) {
     uint32_t i = start;
     while (i < c && w.pops < limit) {
-      const ReqEntry e = ring[(h + i) & tb.qmask];
+      const ReqEntry e = rv.at(i);
       bool rdy = (i == start) ? (ready0 || e.l <= now) : (e.l <= now);
       if (!rdy || !(e.p < kInf)) break;
       uint64_t key = okey(__dadd_rn(e.p, pdv));
       if (key > T || (kstamp && e.dec == kNoDec)) break;
       const uint32_t glim = kstamp ? kstamp - e.dec : 0xffffffffu;  // pops in group
-      double r_now = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
+      double r_now = reduced_r(rv, i, w.pmask, rinv);
       vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true, e.dec,
               e.tie);
       w.pmask |= 1ull << i;
@@ -333,9 +375,9 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
       ++w.pops;
       uint32_t run = 0;
       while (i < c && w.pops < limit && run + 1 < glim) {
-        double ri = reduced_r(ring, h, tb.qmask, i, w.pmask, rinv);
+        double ri = reduced_r(rv, i, w.pmask, rinv);
         if (!(ri <= now)) break;
-        const ReqEntry er = ring[(h + i) & tb.qmask];
+        const ReqEntry er = rv.at(i);
         vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, false,
                 er.dec, er.tie);
         ++i;
@@ -346,15 +388,14 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
       ++w.groups;
     }
     if (front_out && i < c) {
-      const ReqEntry& e = ring[(h + i) & tb.qmask];
-      *front_out = Tag3{reduced_r(ring, h, tb.qmask, i, w.pmask, rinv), e.p,
-                        e.l, e.arrival};
+      const ReqEntry e = rv.at(i);
+      *front_out = Tag3{reduced_r(rv, i, w.pmask, rinv), e.p, e.l, e.arrival};
       *front_cost = e.cost;
     }
     return w;
   }
   // delayed mode
-  const ReqEntry e0 = ring[(h + start) & tb.qmask];
+  const ReqEntry e0 = rv.at(start);
   Tag3 cur = use_start_tag ? start_tag : Tag3{e0.r, e0.p, e0.l, e0.arrival};
   uint32_t cur_cost = e0.cost, cur_dec = e0.dec, cur_tie = e0.tie;
   uint32_t cur_rho = start ? cv.cr : e0.rho;  // a recomputed front carries cur_rho
@@ -366,7 +407,7 @@ __device__ inline WalkP walk_p(const Table& tb, uint32_t s, const CView& cv,
     double off = prio ? resv_offset(rinv, cur_cost, cur_rho) : 0.0;
     ++i;
     if (i < c) {
-      const ReqEntry e = ring[(h + i) & tb.qmask];
+      const ReqEntry e = rv.at(i);
       Tag3 nt;
       if (!make_tag(cur, rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival, e.cost,
                     tb.antic, &nt))

@@ -242,8 +242,9 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
       } else {
         CountV v;
         uint32_t fc;
-        m = walk_r(tb, s, load_view(tb, s), now, kMaxKey, 0xffffffffu, v, nullptr,
-                   &pf, &fc);
+        const CView cvx = load_view(tb, s);
+        m = walk_r(tb, ring_view(tb, s, cvx.h), cvx, now, kMaxKey, 0xffffffffu, v,
+                   nullptr, &pf, &fc);
       }
       have_pf = m < x.c;
       ready = pf.l <= now;
@@ -885,9 +886,12 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // One candidate's entries: R pops with r <= min(now, T_R); then, if the
 // priority pulls run, the P groups with key <= T_P from the post-R state.
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
+constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS)
+constexpr int kEmitStageThreads = 512;  // walkers with a staging slice
 __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 BRecR* brec, uint32_t* bcount, uint32_t* bsize,
-                                const uint32_t* sbn, DEnt* dense, uint32_t dcap) {
+                                const uint32_t* sbn, DEnt* dense, uint32_t dcap,
+                                ReqEntry* st) {
   const uint32_t s = c.slot;
   const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
   const double now = rd->now;
@@ -895,10 +899,11 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
   uint32_t fc;
   const CView cv = cand_view(tb, c);
   const uint32_t h = cv.h;
+  const RingView rv = stage_ring<kEmitStage>(tb, s, h, cv.c, st);
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
-    walk_r(tb, s, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
+    walk_r(tb, rv, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
   if (c.cp()) {
     // the priority pulls run only after every R pop
@@ -906,7 +911,7 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
     bool ready0 = m == 0 && (c.f() & F_READY);
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
-    walk_p(tb, s, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
+    walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
   }
 }
@@ -1084,6 +1089,7 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
         uint32_t* done) {
   __shared__ CandRec bl[kEmitChunk];
   __shared__ uint32_t ltab[2 * kHistBinsR];
+  __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
   __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t s_base, s_tot, s_last;
   __shared__ uint32_t s_cnt[2];
@@ -1189,7 +1195,9 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
     const CandRec c = bl[i];
     cand[base + i] = c;
-    emit_one(tb, rd, c, brec, bcount, bsize, ltab, dense, dcap);
+    emit_one(tb, rd, c, brec, bcount, bsize, ltab, dense, dcap,
+             threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
+                                                       : nullptr);
   }
   if (!brec) return;
   // ticket: the block's bin atomics have completed (every wave waits for its
@@ -1527,7 +1535,9 @@ struct RoundC {
   bool p_runs, ovf;
 };
 
-__device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd) {
+constexpr int kApplyStage = 4;  // queue positions staged per candidate (LDS)
+__device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd,
+                                 ReqEntry* st) {
   // every load that depends only on the candidate record is issued before
   // the first branch: one memory round trip for the client record and its
   // ring entries (the record's head / count and flags are k_remit's;
@@ -1546,7 +1556,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   const uint32_t terminal = rc.terminal;
   const bool p_runs = rc.p_runs;
   const uint32_t c = cv.c, h = cv.h;
-  const double touched = touch_ring(tb, s, h, c);
+  const RingView rv = stage_ring<kApplyStage>(tb, s, h, c, st);
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s};
   Tag3 front{};
@@ -1556,18 +1566,17 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   // exactly the pops the ranking stamped: the R prefix's, then the P groups'
   {
     ApplyVR vr{&v};
-    popsR = walk_r(tb, s, cv, now, kMaxKey, 0xffffffffu, vr, &prev, &front, &fcost,
+    popsR = walk_r(tb, rv, cv, now, kMaxKey, 0xffffffffu, vr, &prev, &front, &fcost,
                    true);
   }
   if (p_runs) {
     ApplyVP vp{&v};
     bool ready0 = popsR == 0 && (f0 & F_READY);
-    WalkP w = walk_p(tb, s, cv, now, kMaxKey, 0xffffffffu, vp, &prev, &front, &fcost,
+    WalkP w = walk_p(tb, rv, cv, now, kMaxKey, 0xffffffffu, vp, &prev, &front, &fcost,
                      popsR, front, popsR && tb.delayed, ready0, rc.k);
     popsP = w.pops;
     pmask = w.pmask;
   }
-  keep(touched);
   uint32_t pops = popsR + popsP;
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
@@ -1576,22 +1585,24 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   }
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
   if (!tb.delayed) {
+    double front_r = 0.0;
     if (pmask) {
-      double rinv = cv.rinv;
-      // remaining requests: all reductions, in order
-      for (uint32_t k = pops; k < c; ++k)
-        ring[(h + k) & tb.qmask].r = reduced_r(ring, h, tb.qmask, k, pmask, rinv);
+      const double rinv = cv.rinv;
+      // remaining requests: all reductions, in order (from the entries as
+      // they were: the staged copy is not rewritten)
+      for (uint32_t k = pops; k < c; ++k) {
+        const double rk = reduced_r(rv, k, pmask, rinv);
+        ring[(h + k) & tb.qmask].r = rk;
+        if (k == pops) front_r = rk;
+      }
       double pr = prev.r;
       for (uint32_t j = 0; j < pops; ++j)
-        if ((pmask >> j) & 1ull) {
-          const ReqEntry& ej = ring[(h + j) & tb.qmask];
-          pr = __dsub_rn(pr, resv_offset(rinv, ej.cost, ej.rho));
-        }
+        if ((pmask >> j) & 1ull) pr = __dsub_rn(pr, rv.offset_at(j, rinv));
       tb.rec[s].prev_r = pr;
     }
     if (nc2) {
-      const ReqEntry& fe = ring[nh];
-      front = Tag3{fe.r, fe.p, fe.l, fe.arrival};
+      const ReqEntry fe = rv.at(pops);
+      front = Tag3{pmask ? front_r : fe.r, fe.p, fe.l, fe.arrival};
     }
   } else {
     // delayed: the walks recomputed the new front and prev
@@ -1650,10 +1661,11 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, unsigned long long* sched,
   const uint32_t stride = gridDim.x * blockDim.x;
   const RoundC rc{rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
                   rd->p_runs != 0, rd->overflow != 0};
+  __shared__ ReqEntry stage[kBlockR * kApplyStage];
   for (uint32_t ci = tid; ci < nc; ci += stride) {
     uint64_t t0 = dbg ? wall_clock64() : 0;
     const CandRec c = cand[ci];
-    apply_one(tb, rc, c);
+    apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
     if (dbg && ci < 262144) {
       dbg[2 * ci] = t0;
       dbg[2 * ci + 1] = wall_clock64();
