@@ -334,8 +334,9 @@ struct WalkP {
 __device__ inline double reduced_r(const RingView& rv, uint32_t i, uint64_t pmask,
                                    double rinv) {
   double r = rv.r_at(i);
-  for (uint32_t j = 0; j < i; ++j)
-    if ((pmask >> j) & 1ull) r = __dsub_rn(r, rv.offset_at(j, rinv));
+  // the priority pops before i, ascending (i <= 63: queue capacity <= 64)
+  for (uint64_t m = pmask & ((1ull << i) - 1ull); m; m &= m - 1ull)
+    r = __dsub_rn(r, rv.offset_at((uint32_t)__ffsll((unsigned long long)m) - 1u, rinv));
   return r;
 }
 

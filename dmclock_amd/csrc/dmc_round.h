@@ -1491,9 +1491,22 @@ struct ApplyV {
     d.cost = cost;
     d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
     d.flags = tie;
-    out[idx] = d;
+    // the first decision is held back and stored with the client's state at
+    // the end (flush): no store sits ahead of the walk's and the reductions'
+    // loads (a load wait also waits for the wave's earlier stores)
+    if (!any) {
+      first = d;
+      first_idx = idx;
+    } else {
+      out[idx] = d;
+    }
     last_idx = idx;
     any = true;
+  }
+  dmc_decision first;
+  uint32_t first_idx = 0;
+  __device__ void flush() {
+    if (any) out[first_idx] = first;
   }
 };
 struct ApplyVR {
@@ -1527,6 +1540,7 @@ struct ApplyVP {
 // The round's scalars, read once per thread (stores through the table could
 // alias the round record, which would force re-loads inside the walks).
 struct RoundC {
+  uint64_t* dbg;  // debug: per-candidate stage clocks (8 per candidate) or null
   double now;
   uint64_t tick;
   dmc_decision* out;
@@ -1557,6 +1571,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   const bool p_runs = rc.p_runs;
   const uint32_t c = cv.c, h = cv.h;
   const RingView rv = stage_ring<kApplyStage>(tb, s, h, c, st);
+  if (rc.dbg) rc.dbg[1] = wall_clock64();
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s};
   Tag3 front{};
@@ -1578,6 +1593,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     pmask = w.pmask;
   }
   uint32_t pops = popsR + popsP;
+  if (rc.dbg) rc.dbg[2] = wall_clock64();
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
       tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
@@ -1620,6 +1636,8 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     tb.rec[s].prev_arr = prev.arrival;
     if (c >= 2) tb.aux[s].last_tick = tick;
   }
+  if (rc.dbg) rc.dbg[3] = wall_clock64();
+  v.flush();
   // the new front's heap keys, cursor and flags: one 32-byte ScanRec store
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
   ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
@@ -1659,16 +1677,18 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, unsigned long long* sched,
   const uint32_t nc = rd->n_cand;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  const RoundC rc{rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
-                  rd->p_runs != 0, rd->overflow != 0};
+  RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
+            rd->p_runs != 0, rd->overflow != 0};
   __shared__ ReqEntry stage[kBlockR * kApplyStage];
   for (uint32_t ci = tid; ci < nc; ci += stride) {
     uint64_t t0 = dbg ? wall_clock64() : 0;
     const CandRec c = cand[ci];
+    rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
+    if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;
     apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
-    if (dbg && ci < 262144) {
-      dbg[2 * ci] = t0;
-      dbg[2 * ci + 1] = wall_clock64();
+    if (rc.dbg) {
+      rc.dbg[0] = t0;
+      rc.dbg[4] = wall_clock64();
     }
   }
 }
