@@ -57,7 +57,9 @@ struct ActBuf {
 // (:995-1009).
 struct AddState {
   Tag3 prev;
-  double rinv, winv, linv;
+  double rinv, winv, linv;  // client.info (U1: replaced at each tag calculation)
+  BoundInfo bound;          // U1: what client_info_f returns now
+  bool fetched;             // U1: a tag calculation fetched the bound info
   uint32_t head, count, cd, cr;
   uint64_t last_tick;
   uint8_t flags;
@@ -79,6 +81,12 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   }
   Tag3 tag;
   if (!tb.delayed || st.count == 0) {
+    if (tb.binfo) {  // get_cli_info, :870-875
+      st.rinv = st.bound.r_inv;
+      st.winv = st.bound.w_inv;
+      st.linv = st.bound.l_inv;
+      st.fetched = true;
+    }
     if (!make_tag(st.prev, st.rinv, st.winv, st.linv, rq.delta, rq.rho, rq.time,
                   rq.cost, tb.antic, &tag)) {
       p.rc[pos] = DMC_EBADTAG;
@@ -141,6 +149,8 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   st.rinv = tb.rec[s].r_inv;
   st.winv = tb.rec[s].w_inv;
   st.linv = tb.rec[s].l_inv;
+  st.fetched = false;
+  if (tb.binfo) st.bound = tb.binfo[s];
   const double pd = tb.rec[s].pd;
   st.head = tb.sc[s].head;
   st.count = tb.sc[s].count;
@@ -200,6 +210,11 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   tb.rec[s].prev_p = st.prev.p;
   tb.rec[s].prev_l = st.prev.l;
   tb.rec[s].prev_arr = st.prev.arrival;
+  if (st.fetched) {
+    tb.rec[s].r_inv = st.rinv;
+    tb.rec[s].w_inv = st.winv;
+    tb.rec[s].l_inv = st.linv;
+  }
   tb.sc[s].count = (uint8_t)st.count;
   tb.sc[s].flags = st.flags;
   tb.aux[s].cur_delta = st.cd;

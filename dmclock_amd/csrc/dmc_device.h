@@ -71,6 +71,16 @@ struct alignas(32) ScanRec {
 };
 static_assert(sizeof(ScanRec) == 32, "ScanRec must be 32 bytes");
 
+// The ClientInfo client_info_f returns for a client now (its inverses): the
+// caller publishes it with dmc_client_bind_info_batch.  With dynamic_info
+// (U1) every tag calculation reads it and makes it the client's cached info
+// (get_cli_info, dmclock_server.h:870-875); the reductions use the cached
+// info (:1083-1109), as the reference's client.info.
+struct alignas(32) BoundInfo {
+  double r_inv, w_inv, l_inv, pad;
+};
+static_assert(sizeof(BoundInfo) == 32, "BoundInfo must be 32 bytes");
+
 // Client table pointers (passed by value to kernels).
 struct Table {
   uint32_t n;      // slots
@@ -84,6 +94,7 @@ struct Table {
   ScanRec* sc;     // N
   ClientAux* aux;  // N
   ReqEntry* ring;
+  const BoundInfo* binfo;  // U1 (dynamic_info): read at every tag; else null
 };
 
 __host__ __device__ inline uint64_t dbits(double x) {
@@ -158,9 +169,30 @@ __device__ inline double resv_offset(double rinv, uint32_t cost,
 struct CView {
   uint32_t h, c;          // ring head, queued requests
   uint32_t cd, cr;        // cur_delta, cur_rho (delayed mode)
-  double rinv, winv, linv;
+  double rinv, winv, linv;  // the cached ClientInfo (client.info)
   double pd;              // prop_delta
+  double tr, tw, tl;      // the info a delayed tag calculation reads (U1: bound)
+  // reduce_reservation_tags' inverse after a pop at queue position i of a
+  // batch (delayed mode): the pop fetched the info if an entry follows it,
+  // and so did every earlier pop of the batch (:1021-1036, 1077-1111)
+  __device__ double red_rinv(uint32_t i) const {
+    return (i > 0 || i + 1 < c) ? tr : rinv;
+  }
 };
+
+// the tag-calculation info of a view: U1 reads the bound info
+__device__ inline void view_tag_info(const Table& tb, uint32_t s, CView& v) {
+  if (tb.delayed && tb.binfo) {
+    const BoundInfo b = tb.binfo[s];
+    v.tr = b.r_inv;
+    v.tw = b.w_inv;
+    v.tl = b.l_inv;
+  } else {
+    v.tr = v.rinv;
+    v.tw = v.winv;
+    v.tl = v.linv;
+  }
+}
 
 __device__ inline CView load_view(const Table& tb, uint32_t s) {
   CView v;
@@ -172,6 +204,7 @@ __device__ inline CView load_view(const Table& tb, uint32_t s) {
   v.winv = tb.rec[s].w_inv;
   v.linv = tb.rec[s].l_inv;
   v.pd = tb.rec[s].pd;
+  view_tag_info(tb, s, v);
   return v;
 }
 
@@ -292,7 +325,7 @@ __device__ inline uint32_t walk_r(const Table& tb, const RingView& rv, const CVi
     if (n < c) {
       const ReqEntry e = rv.at(n);
       Tag3 nt;
-      if (!make_tag(cur, cv.rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival,
+      if (!make_tag(cur, cv.tr, cv.tw, cv.tl, cv.cd, cv.cr, e.arrival,
                     e.cost, tb.antic, &nt))
         nt = Tag3{e.r, e.p, e.l, e.arrival};
       if (prev_io) {
@@ -405,12 +438,12 @@ __device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView&
   auto advance = [&](bool prio) {
     // pop entry i (tag `cur`), compute the next front by update_next_tag and,
     // after a priority pop, reduce it and prev (:1021-1036, :1077-1085)
-    double off = prio ? resv_offset(rinv, cur_cost, cur_rho) : 0.0;
+    double off = prio ? resv_offset(cv.red_rinv(i), cur_cost, cur_rho) : 0.0;
     ++i;
     if (i < c) {
       const ReqEntry e = rv.at(i);
       Tag3 nt;
-      if (!make_tag(cur, rinv, cv.winv, cv.linv, cv.cd, cv.cr, e.arrival, e.cost,
+      if (!make_tag(cur, cv.tr, cv.tw, cv.tl, cv.cd, cv.cr, e.arrival, e.cost,
                     tb.antic, &nt))
         nt = Tag3{e.r, e.p, e.l, e.arrival};
       if (prev_io) {

@@ -130,7 +130,7 @@ __device__ inline uint32_t wave_sum_u32(uint32_t v) {
 }
 
 // ------------------------------------------------------------------ register
-__global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
+__global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_t* slots,
                            const double* rinv, const double* winv,
                            const double* linv, int active, uint64_t tick) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -139,6 +139,7 @@ __global__ void k_register(Table tb, uint32_t n, const uint32_t* slots,
   if (s >= tb.n) return;
   // ClientRec(client, info, tick), dmclock_server.h:381-393
   tb.rec[s] = ClientRec{0.0, 0.0, 0.0, 0.0, rinv[i], winv[i], linv[i], 0.0};
+  binfo[s] = BoundInfo{rinv[i], winv[i], linv[i], 0.0};
   tb.sc[s] = ScanRec{0.0, 0.0, 0.0, 0, 0, (uint8_t)(F_REG | (active ? 0 : F_IDLE)), 0, 0};
   tb.aux[s] = ClientAux{1, 1, tick};
 }
@@ -753,7 +754,17 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
     Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
     Tag3 nt;
     uint32_t cd = tb.aux[s].cur_delta, cr = tb.aux[s].cur_rho;
-    if (make_tag(pt, rinv, tb.rec[s].w_inv, tb.rec[s].l_inv, cd, cr, f.arrival, f.cost,
+    double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
+    if (tb.binfo) {  // U1: get_cli_info (:870-875) becomes client.info
+      const BoundInfo b = tb.binfo[s];
+      rinv = b.r_inv;
+      winv = b.w_inv;
+      linv = b.l_inv;
+      tb.rec[s].r_inv = rinv;
+      tb.rec[s].w_inv = winv;
+      tb.rec[s].l_inv = linv;
+    }
+    if (make_tag(pt, rinv, winv, linv, cd, cr, f.arrival, f.cost,
                  tb.antic, &nt)) {
       f.r = nt.r;
       f.p = nt.p;
@@ -843,6 +854,15 @@ struct dmc_queue {
   std::mutex mtx;  // C-ABI calls on one handle are serialised (data_mtx, :762)
   // host mirrors
   std::vector<uint8_t> reg_h, idle_h;
+  // the bound ClientInfo (U1, dmc_client_bind_info_batch): device column and
+  // its host shadow (3 inverses per slot, to skip unchanged pushes)
+  BoundInfo* binfo = nullptr;
+  std::vector<double> binfo_h;
+  dmc_info_fn info_fn = nullptr;  // dmc_queue_set_info_fn
+  void* info_ctx = nullptr;
+  // queue-content generation (bumped by every call that can change a queue)
+  // and the one dmc_queue_requests read, for dmc_queue_filter's check
+  uint64_t gen = 0, maint_gen = ~0ull, maint_total = 0;
   uint32_t n_registered = 0;
   uint32_t n_idle = 0;
   uint64_t tick = 0;
@@ -1479,6 +1499,89 @@ void launch_future(dmc_queue* q) {
   pe(q);
 }
 
+// bound infos of distinct slots (dmc_client_bind_info_batch)
+__global__ void k_bind_info(BoundInfo* binfo, uint32_t n, const uint32_t* slots,
+                            const BoundInfo* v) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) binfo[slots[i]] = v[i];
+}
+
+double inv_of(double x) { return x == 0.0 ? 0.0 : 1.0 / x; }  // :115-117
+
+// Publish bound infos (U1): slots whose inverses differ from the host shadow
+// are written, a few by direct copies, many by one staged kernel (a slot
+// repeated in the batch takes its last values).
+int bind_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, const double* r,
+               const double* w, const double* l) {
+  std::vector<uint32_t> ch;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = slots[i];
+    const double v[3] = {inv_of(r[i]), inv_of(w[i]), inv_of(l[i])};
+    double* h = &q->binfo_h[3ull * s];
+    if (std::memcmp(h, v, sizeof(v)) == 0) continue;
+    std::memcpy(h, v, sizeof(v));
+    ch.push_back(s);
+  }
+  if (ch.empty()) return DMC_OK;
+  std::sort(ch.begin(), ch.end());
+  ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
+  std::vector<BoundInfo> v(ch.size());
+  for (size_t i = 0; i < ch.size(); ++i) {
+    const double* h = &q->binfo_h[3ull * ch[i]];
+    v[i] = BoundInfo{h[0], h[1], h[2], 0.0};
+  }
+  if (ch.size() <= 16) {
+    for (size_t i = 0; i < ch.size(); ++i)
+      HIP_OK(hipMemcpyAsync(q->binfo + ch[i], &v[i], sizeof(BoundInfo),
+                            hipMemcpyHostToDevice, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    return DMC_OK;
+  }
+  const uint32_t m = (uint32_t)ch.size();
+  uint32_t* d_s = nullptr;
+  BoundInfo* d_v = nullptr;
+  HIP_OK(hipMalloc(&d_s, 4ull * m));
+  HIP_OK(hipMalloc(&d_v, sizeof(BoundInfo) * m));
+  HIP_OK(hipMemcpyAsync(d_s, ch.data(), 4ull * m, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemcpyAsync(d_v, v.data(), sizeof(BoundInfo) * m, hipMemcpyHostToDevice,
+                        q->stream));
+  hipLaunchKernelGGL(k_bind_info, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->binfo, m, (const uint32_t*)d_s, (const BoundInfo*)d_v);
+  HIP_OK(hipStreamSynchronize(q->stream));
+  dfree(d_s);
+  dfree(d_v);
+  return DMC_OK;
+}
+
+// U1 with a host client_info_f (dmc_queue_set_info_fn): fetch and bind the
+// infos of n slots (unregistered slots are skipped)
+int fetch_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, size_t stride) {
+  if (!q->info_fn || !q->tb.binfo || !n) return DMC_OK;
+  std::vector<uint32_t> sl;
+  std::vector<double> r, w, l;
+  sl.reserve(n);
+  uint32_t last = 0xffffffffu;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = *reinterpret_cast<const uint32_t*>(
+        reinterpret_cast<const char*>(slots) + stride * i);
+    if (s == last || s >= q->p.max_clients || !q->reg_h[s]) continue;
+    last = s;
+    double a = 0, b = 0, c = 0;
+    if (q->info_fn(q->info_ctx, s, &a, &b, &c) != 0) return DMC_EINVAL;
+    sl.push_back(s);
+    r.push_back(a);
+    w.push_back(b);
+    l.push_back(c);
+  }
+  return bind_infos(q, (uint32_t)sl.size(), sl.data(), r.data(), w.data(), l.data());
+}
+
+// U1 + delayed with a host client_info_f: pulls run one at a time, each
+// fetching the dispatched client's info between selection and pop
+bool info_steps(const dmc_queue* q) {
+  return q->info_fn && q->tb.binfo && q->tb.delayed;
+}
+
 // one general pull_request(now); returns the NextReqType in *type
 int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
               int* type, double* when) {
@@ -1490,6 +1593,16 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlock), 0, q->stream,
                      q->step_grid, (const StepRed*)q->red, now, q->p.at_limit,
                      q->n_registered, q->sctl, (Round*)nullptr, (HostRound*)nullptr);
+  if (info_steps(q)) {
+    // get_cli_info of the client this pull pops (update_next_tag, :1021-1036)
+    HIP_OK(hipMemcpyAsync(q->h_sctl, q->sctl, sizeof(StepCtl), hipMemcpyDeviceToHost,
+                          q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    if (q->h_sctl->type == DMC_NEXT_RETURNING) {
+      const uint32_t s = q->h_sctl->slot;
+      if (int rc = fetch_infos(q, 1, &s, sizeof(uint32_t))) return rc;
+    }
+  }
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
                      q->stream, tb, now, (const StepCtl*)q->sctl);
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
@@ -1666,7 +1779,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       break;
     }
     uint32_t kk = k - n_dec;
-    if (kk <= q->small_k && !pre_launched) {
+    if ((kk <= q->small_k || info_steps(q)) && !pre_launched) {
       int type;
       double when;
       int rc = step_once(q, now, d_out, n_dec, &type, &when);
@@ -1863,6 +1976,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   };
   int rc = 0;
   rc |= A(&t.rec, N); rc |= A(&t.sc, N); rc |= A(&t.aux, N);
+  rc |= A(&q->binfo, N);
+  t.binfo = p.dynamic_info ? q->binfo : nullptr;
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
   rc |= A(&q->cand, N);
   rc |= A(&q->keyr, N);
@@ -1915,6 +2030,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   }
   q->reg_h.assign(N, 0);
   q->idle_h.assign(N, 0);
+  q->binfo_h.assign(3ull * N, 0.0);
   if (hipStreamSynchronize(q->stream) != hipSuccess) {
     dmc_queue_destroy(q);
     return DMC_EDEVICE;
@@ -1929,7 +2045,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
-  void* ptrs[] = {t.rec, t.sc, t.aux,
+  void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
                   q->cand, q->keyr, q->keyp, q->meta, q->hist, q->sbn,
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
@@ -1967,13 +2083,12 @@ int dmc_queue_sync(dmc_queue* q) {
   return DMC_OK;
 }
 
-static double inv_of(double x) { return x == 0.0 ? 0.0 : 1.0 / x; }  // :115-117
-
 int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                               const double* r, const double* w, const double* l,
                               int active) {
   if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
@@ -1995,11 +2110,14 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   HIP_OK(hipMemcpyAsync(d_w, wi.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipMemcpyAsync(d_l, li.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
   hipLaunchKernelGGL(k_register, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                     q->stream, q->tb, n, d_slots, d_r, d_w, d_l, active, q->tick);
+                     q->stream, q->tb, q->binfo, n, d_slots, d_r, d_w, d_l, active, q->tick);
   HIP_OK(hipStreamSynchronize(q->stream));
   dfree(d_slots); dfree(d_r); dfree(d_w); dfree(d_l);
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s = slots[i];
+    q->binfo_h[3ull * s] = ri[i];
+    q->binfo_h[3ull * s + 1] = wi[i];
+    q->binfo_h[3ull * s + 2] = li[i];
     if (!q->reg_h[s]) ++q->n_registered;
     if (q->idle_h[s]) --q->n_idle;
     q->reg_h[s] = 1;
@@ -2020,10 +2138,30 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
   QueueLock g(q);
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   double v[3] = {inv_of(r), inv_of(w), inv_of(l)};
-  // r_inv, w_inv, l_inv are contiguous in ClientRec
+  // r_inv, w_inv, l_inv are contiguous in ClientRec and in BoundInfo
   HIP_OK(hipMemcpyAsync(&q->tb.rec[slot].r_inv, v, sizeof(v), hipMemcpyHostToDevice,
                         q->stream));
+  HIP_OK(hipMemcpyAsync(&q->binfo[slot].r_inv, v, sizeof(v), hipMemcpyHostToDevice,
+                        q->stream));
+  std::memcpy(&q->binfo_h[3ull * slot], v, sizeof(v));
   HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_client_bind_info_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                               const double* r, const double* w, const double* l) {
+  if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
+  QueueLock g(q);
+  for (uint32_t i = 0; i < n; ++i)
+    if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
+  return bind_infos(q, n, slots, r, w, l);
+}
+
+int dmc_queue_set_info_fn(dmc_queue* q, dmc_info_fn fn, void* ctx) {
+  if (!q) return DMC_EINVAL;
+  QueueLock g(q);
+  q->info_fn = fn;
+  q->info_ctx = ctx;
   return DMC_OK;
 }
 
@@ -2097,6 +2235,113 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
   return DMC_OK;
 }
 
+// ------------------------------------------------------------------ maintenance
+// Whole-queue maintenance in a fixed number of device passes: one slot list
+// (null: every slot), queued counts, their exclusive scan, then one pass that
+// gathers the handles, filters, or clears.  One thread per listed slot; a
+// slot's ring is walked in FIFO order.
+__device__ inline uint32_t list_slot(const uint32_t* slots, uint32_t i) {
+  return slots ? slots[i] : i;
+}
+
+__global__ void k_list_counts(Table tb, uint32_t n, const uint32_t* slots,
+                              uint32_t* counts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) counts[i] = tb.sc[list_slot(slots, i)].count;
+}
+
+__global__ void k_list_gather(Table tb, uint32_t n, const uint32_t* slots,
+                              const uint32_t* offs, uint64_t* handles) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = list_slot(slots, i);
+  const ScanRec sr = tb.sc[s];
+  const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  uint64_t* out = handles + offs[i];
+  for (uint32_t j = 0; j < sr.count; ++j) out[j] = ring[(sr.head + j) & tb.qmask].handle;
+}
+
+// ClientRec::remove_by_req_filter's erase (:440-480): the kept requests keep
+// their order and tags (a removed delayed-mode front leaves the next
+// request's stored tag as the front tag, as the reference's deque does); the
+// front's ready flag survives only with the front; the heap keys follow the
+// new front.  *any != 0 if anything was removed.
+__global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
+                              const uint32_t* offs, const uint8_t* keep,
+                              uint32_t* any) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = list_slot(slots, i);
+  const ScanRec sr = tb.sc[s];
+  const uint8_t* kp = keep + offs[i];
+  uint32_t c = sr.count, m = 0;
+  for (uint32_t j = 0; j < c; ++j) m += kp[j] != 0;
+  if (m == c) return;
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  uint32_t w = 0;
+  for (uint32_t j = 0; j < c; ++j) {
+    if (!kp[j]) continue;
+    if (w != j) ring[(sr.head + w) & tb.qmask] = ring[(sr.head + j) & tb.qmask];
+    ++w;
+  }
+  ScanRec o = sr;
+  o.count = (uint8_t)m;
+  if (!kp[0] || m == 0) o.flags = (uint8_t)(o.flags & ~F_READY);
+  if (m) {
+    const ReqEntry& f = ring[sr.head & tb.qmask];
+    o.r = f.r;
+    o.pk = __dadd_rn(f.p, tb.rec[s].pd);
+    o.l = f.l;
+  } else {
+    o.r = o.pk = o.l = 0.0;
+  }
+  tb.sc[s] = o;
+  atomicOr(any, 1u);
+}
+
+// do_clean's erase (:1244-1255) of the listed clients: queue dropped, slot
+// unregistered
+__global__ void k_list_erase(Table tb, uint32_t n, const uint32_t* slots) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tb.sc[list_slot(slots, i)] = ScanRec{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
+}
+
+// Counts and offsets of a slot list, on the device and on the host; the
+// total in *total.
+static int list_offsets(dmc_queue* q, uint32_t n, const uint32_t* d_slots,
+                        uint32_t* d_counts, uint32_t* d_offs,
+                        std::vector<uint32_t>* h_counts, uint64_t* total) {
+  hipLaunchKernelGGL(k_list_counts, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, n, d_slots, d_counts);
+  h_counts->resize(n);
+  HIP_OK(hipMemcpyAsync(h_counts->data(), d_counts, 4ull * n, hipMemcpyDeviceToHost,
+                        q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  // offsets on the host (n * 4 bytes each way; ring capacity <= 64 keeps the
+  // total below 2^32 for any table that fits in HBM)
+  std::vector<uint32_t> offs(n);
+  uint64_t t = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    offs[i] = (uint32_t)t;
+    t += (*h_counts)[i];
+  }
+  HIP_OK(hipMemcpyAsync(d_offs, offs.data(), 4ull * n, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  *total = t;
+  return DMC_OK;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() { dfree(p); }
+  int alloc(size_t bytes) {
+    return hipMalloc(&p, bytes ? bytes : 1) == hipSuccess ? DMC_OK : DMC_ENOMEM;
+  }
+  uint32_t* u32() const { return static_cast<uint32_t*>(p); }
+  uint64_t* u64() const { return static_cast<uint64_t*>(p); }
+  uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
 static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
                         uint32_t* head) {
   ScanRec sr;
@@ -2149,6 +2394,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
@@ -2229,9 +2475,13 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
                   int32_t* rc_out) {
   if (!q || (n && !reqs)) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
+  if (rc) return rc;
+  // U1 with a host client_info_f: the infos the batch's tags read
+  rc = fetch_infos(q, n, &reqs[0].slot, sizeof(dmc_request));
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(q->d_reqs, reqs, sizeof(dmc_request) * n,
                         hipMemcpyHostToDevice, q->stream));
@@ -2250,6 +2500,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
                          int32_t* d_rc_out) {
   if (!q || (n && (!d_reqs || !d_rc_out))) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
@@ -2277,6 +2528,7 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                    dmc_pull_result* result) {
   if (!q || (k && !out)) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   int rc = ensure_dec(q, k);
   if (rc) return rc;
   dmc_pull_result r{};
@@ -2294,6 +2546,7 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
                           dmc_decision* d_out, dmc_pull_result* d_result) {
   if (!q || (k && !d_out)) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   dmc_pull_result r{};
   bool dev_wrote = false;
   int rc = pull_impl(q, now, k, d_out, &r, d_result, &dev_wrote);
@@ -2316,6 +2569,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
   bool fuse;
   {
     QueueLock g(q);
+  ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
     fuse = n && k && q->n_idle == 0 && q->n_registered > 0 && k > q->small_k &&
            !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
@@ -2372,6 +2626,7 @@ int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
                          uint64_t* handles_out, uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (!q->reg_h[slot]) {
     if (n_out) *n_out = 0;
     return DMC_OK;  // client_map.find fails -> return, :599-601
@@ -2406,6 +2661,7 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  ++q->gen;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -2417,6 +2673,115 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
     if (keep[i]) kept.push_back(ents[i]);
   if (kept.size() == ents.size()) return DMC_OK;
   return write_queue(q, slot, kept, n > 0 && keep[0]);
+}
+
+int dmc_queue_requests(dmc_queue* q, uint32_t* counts_out, uint64_t* handles_out,
+                       uint64_t cap, uint64_t* n_out) {
+  if (!q || !n_out) return DMC_EINVAL;
+  QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
+  const uint32_t N = q->tb.n;
+  DevBuf counts, offs, hs;
+  if (counts.alloc(4ull * N) || offs.alloc(4ull * N)) return DMC_ENOMEM;
+  std::vector<uint32_t> hc;
+  uint64_t total = 0;
+  if (int rc = list_offsets(q, N, nullptr, counts.u32(), offs.u32(),
+                            &hc, &total))
+    return rc;
+  if (counts_out) std::memcpy(counts_out, hc.data(), 4ull * N);
+  *n_out = total;
+  q->maint_gen = q->gen;
+  q->maint_total = total;
+  if (!handles_out || cap < total || !total) return DMC_OK;
+  if (hs.alloc(8ull * total)) return DMC_ENOMEM;
+  hipLaunchKernelGGL(k_list_gather, dim3((N + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, N, (const uint32_t*)nullptr,
+                     (const uint32_t*)offs.u32(), hs.u64());
+  HIP_OK(hipMemcpyAsync(handles_out, hs.p, 8ull * total, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  return DMC_OK;
+}
+
+int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_removed) {
+  if (!q || (n && !keep)) return DMC_EINVAL;
+  QueueLock g(q);
+  // the queue must be the one the last dmc_queue_requests read
+  if (q->maint_gen != q->gen || n != q->maint_total) return DMC_EINVAL;
+  ++q->gen;
+  if (any_removed) *any_removed = 0;
+  if (!n) return DMC_OK;
+  const uint32_t N = q->tb.n;
+  DevBuf counts, offs, kp, any;
+  if (counts.alloc(4ull * N) || offs.alloc(4ull * N) || kp.alloc(n) || any.alloc(4))
+    return DMC_ENOMEM;
+  std::vector<uint32_t> hc;
+  uint64_t total = 0;
+  if (int rc = list_offsets(q, N, nullptr, counts.u32(), offs.u32(),
+                            &hc, &total))
+    return rc;
+  if (total != n) return DMC_EINVAL;
+  HIP_OK(hipMemcpyAsync(kp.p, keep, n, hipMemcpyHostToDevice, q->stream));
+  HIP_OK(hipMemsetAsync(any.p, 0, 4, q->stream));
+  hipLaunchKernelGGL(k_list_filter, dim3((N + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, N, (const uint32_t*)nullptr,
+                     (const uint32_t*)offs.u32(), (const uint8_t*)kp.u8(),
+                     any.u32());
+  uint32_t a = 0;
+  HIP_OK(hipMemcpyAsync(&a, any.p, 4, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  if (any_removed) *any_removed = a != 0;
+  return DMC_OK;
+}
+
+int dmc_client_erase_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                           uint32_t* counts_out, uint64_t* handles_out, uint64_t cap,
+                           uint64_t* n_out) {
+  if (!q || (n && !slots)) return DMC_EINVAL;
+  QueueLock g(q);
+  if (int rc0 = settle_act(q)) return rc0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
+    if (!q->reg_h[slots[i]]) return DMC_ENOTREG;
+  }
+  {  // distinct slots (a repeat would be erased twice)
+    std::vector<uint32_t> v(slots, slots + n);
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end()) return DMC_EINVAL;
+  }
+  if (n_out) *n_out = 0;
+  if (!n) return DMC_OK;
+  ++q->gen;
+  DevBuf ds, counts, offs, hs;
+  if (ds.alloc(4ull * n) || counts.alloc(4ull * n) || offs.alloc(4ull * n)) return DMC_ENOMEM;
+  HIP_OK(hipMemcpyAsync(ds.p, slots, 4ull * n, hipMemcpyHostToDevice, q->stream));
+  std::vector<uint32_t> hc;
+  uint64_t total = 0;
+  if (int rc = list_offsets(q, n, ds.u32(), counts.u32(),
+                            offs.u32(), &hc, &total))
+    return rc;
+  if (counts_out) std::memcpy(counts_out, hc.data(), 4ull * n);
+  if (n_out) *n_out = total;
+  const uint32_t gb = (n + kBlock - 1) / kBlock;
+  if (handles_out && total) {
+    if (cap < total) return DMC_EINVAL;
+    if (hs.alloc(8ull * total)) return DMC_ENOMEM;
+    hipLaunchKernelGGL(k_list_gather, dim3(gb), dim3(kBlock), 0, q->stream, q->tb, n,
+                       (const uint32_t*)ds.u32(),
+                       (const uint32_t*)offs.u32(), hs.u64());
+    HIP_OK(hipMemcpyAsync(handles_out, hs.p, 8ull * total, hipMemcpyDeviceToHost,
+                          q->stream));
+  }
+  hipLaunchKernelGGL(k_list_erase, dim3(gb), dim3(kBlock), 0, q->stream, q->tb, n,
+                     (const uint32_t*)ds.u32());
+  HIP_OK(hipStreamSynchronize(q->stream));
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = slots[i];
+    if (q->idle_h[s]) --q->n_idle;
+    q->reg_h[s] = 0;
+    q->idle_h[s] = 0;
+    --q->n_registered;
+  }
+  return DMC_OK;
 }
 
 int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,

@@ -880,6 +880,7 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
   v.winv = tb.rec[s].w_inv;
   v.linv = tb.rec[s].l_inv;
   v.pd = tb.rec[s].pd;
+  view_tag_info(tb, s, v);
   return v;
 }
 
@@ -1634,7 +1635,14 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     tb.rec[s].prev_p = prev.p;
     tb.rec[s].prev_l = prev.l;
     tb.rec[s].prev_arr = prev.arrival;
-    if (c >= 2) tb.aux[s].last_tick = tick;
+    if (c >= 2) {
+      tb.aux[s].last_tick = tick;
+      if (tb.binfo) {  // U1: the first pop's get_cli_info became client.info
+        tb.rec[s].r_inv = cv.tr;
+        tb.rec[s].w_inv = cv.tw;
+        tb.rec[s].l_inv = cv.tl;
+      }
+    }
   }
   if (rc.dbg) rc.dbg[3] = wall_clock64();
   v.flush();

@@ -37,6 +37,8 @@ EXPORTS = {
     "dmc_client_register": (_i32, [_vp, _u32, _f64, _f64, _f64, _i32]),
     "dmc_client_register_batch": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _i32]),
     "dmc_client_update_info": (_i32, [_vp, _u32, _f64, _f64, _f64]),
+    "dmc_client_bind_info_batch": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "dmc_queue_set_info_fn": (_i32, [_vp, _vp, _vp]),
     "dmc_client_mark_idle": (_i32, [_vp, _u32]),
     "dmc_client_mark_idle_batch": (_i32, [_vp, _u32, _vp]),
     "dmc_client_erase": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
@@ -51,6 +53,11 @@ EXPORTS = {
                                     ctypes.POINTER(_u32)]),
     "dmc_client_requests": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
     "dmc_client_filter": (_i32, [_vp, _u32, _u32, _vp]),
+    "dmc_queue_requests": (_i32, [_vp, _vp, _vp, ctypes.c_uint64,
+                                  ctypes.POINTER(ctypes.c_uint64)]),
+    "dmc_queue_filter": (_i32, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(_i32)]),
+    "dmc_client_erase_batch": (_i32, [_vp, _u32, _vp, _vp, _vp, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64)]),
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "dmc_queue_set_option": (_i32, [_vp, _i32, ctypes.c_int64]),
     "dmc_queue_counters": (_i32, [_vp, ctypes.POINTER(Counters), _i32]),
@@ -66,6 +73,10 @@ EXPORTS = {
     "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
 PROF_NSTAGES = 12
+
+# dmc_info_fn: int (*)(void* ctx, uint32_t slot, double* r, double* w, double* l)
+INFO_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _u32, ctypes.POINTER(_f64),
+                           ctypes.POINTER(_f64), ctypes.POINTER(_f64))
 
 
 class DmcError(RuntimeError):
@@ -105,7 +116,10 @@ class GpuQueue:
     def __init__(self, max_clients=1024, ring_capacity=64, max_batch=1 << 16,
                  delayed=False, dynamic_info=False, at_limit=0,
                  reject_threshold=0.0, anticipation=0.0, device=0,
-                 branching=2, track_ties=True):
+                 branching=2, track_ties=True, info_callback=True):
+        """info_callback (U1 only): client_info_f through the engine's
+        dmc_info_fn; False: the caller publishes changes with bind_info
+        (explicit_bind), the device-API callers' contract."""
         del branching, track_ties  # no heaps on the device
         self.L = lib()
         p = QueueParams()
@@ -127,7 +141,22 @@ class GpuQueue:
         self.slot_of = {}      # client id -> slot
         self.client_of = []    # slot -> client id
         self.info_cur = {}     # client -> (r, w, l) client_info_f returns now
-        self.info_dev = {}     # client -> (r, w, l) the device uses
+        self.info_dev = {}     # client -> (r, w, l) last pushed by update_info
+        self._info_fn = None
+        self.explicit_bind = self.dynamic and not info_callback
+        if self.dynamic and info_callback:
+            # U1: the engine asks for client_info_f(client) right before each
+            # tag calculation of a host-API call (dmc_queue_set_info_fn)
+            def info_fn(ctx, slot, r, w, l):
+                try:
+                    v = self.info_cur[self.client_of[slot]]
+                except (KeyError, IndexError):
+                    return 1
+                r[0], w[0], l[0] = v
+                return 0
+            self._info_fn = INFO_FN(info_fn)  # keep the closure alive
+            _check(self.L.dmc_queue_set_info_fn(self.h, ctypes.cast(self._info_fn, _vp),
+                                                None), "set_info_fn")
 
     def close(self):
         if getattr(self, "h", None):
@@ -144,11 +173,24 @@ class GpuQueue:
     def set_info(self, client, r, w, l, fresh=False):
         self.info_cur[client] = (float(r), float(w), float(l))
         if not fresh and client in self.slot_of:
-            self._push_info(client)
+            self._push_info(client, force=self.dynamic)
 
-    def _push_info(self, client):
+    def bind_info(self, slots, r, w, l):
+        """dmc_client_bind_info_batch: what client_info_f returns for these
+        slots from now on (read at every tag calculation under U1)"""
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        l = np.ascontiguousarray(l, dtype=np.float64)
+        _check(self.L.dmc_client_bind_info_batch(self.h, len(slots), _ptr(slots),
+                                                 _ptr(r), _ptr(w), _ptr(l)),
+               "bind_info_batch")
+
+    def _push_info(self, client, force=False):
+        # under U1 the device's cached info also changes at tag calculations,
+        # so update_client_info always pushes
         v = self.info_cur[client]
-        if self.info_dev.get(client) != v:
+        if force or self.info_dev.get(client) != v:
             _check(self.L.dmc_client_update_info(self.h, self.slot_of[client],
                                                  *v), "update_info")
             self.info_dev[client] = v
@@ -201,8 +243,6 @@ class GpuQueue:
     # ---- hot path
     def add(self, client, time, delta=1, rho=1, cost=1, handle=0):
         s = self._slot(client)
-        if self.dynamic:
-            self._push_info(client)
         req = make_requests([s], [time], [cost], [delta], [rho], [handle])
         return int(self.add_batch(req)[0])
 
@@ -214,11 +254,6 @@ class GpuQueue:
                "add_batch")
         return rc
 
-    def _refresh_dynamic(self):
-        if self.dynamic:
-            for c in self.slot_of:
-                self._push_info(c)
-
     def pull(self, now):
         d, res = self.pull_batch(now, 1)
         if res.n_decisions:
@@ -228,7 +263,6 @@ class GpuQueue:
         return res.next_type, None, res.when
 
     def pull_batch(self, now, k):
-        self._refresh_dynamic()
         # a reused output buffer (first-touch page faults on a fresh 3 MB
         # array per call cost as much as the transfer); callers get a copy
         if getattr(self, "_out", None) is None or len(self._out) < max(k, 1):
@@ -311,11 +345,11 @@ class GpuQueue:
 
     def update_client_info(self, client):
         if client in self.slot_of:
-            self._push_info(client)
+            self._push_info(client, force=self.dynamic)
 
     def update_client_infos(self):
         for c in self.slot_of:
-            self._push_info(c)
+            self._push_info(c, force=self.dynamic)
 
     def remove_by_client(self, client, reverse=False):
         if client not in self.slot_of:
@@ -337,25 +371,53 @@ class GpuQueue:
                "client_requests")
         return out[:n.value].copy()
 
+    def queue_requests(self):
+        """dmc_queue_requests: (counts per slot, every queued handle in slot
+        order, FIFO per slot) in one device pass and one readback"""
+        n = ctypes.c_uint64(0)
+        counts = np.zeros(self.params.max_clients, dtype=np.uint32)
+        _check(self.L.dmc_queue_requests(self.h, _ptr(counts), None, 0,
+                                         ctypes.byref(n)), "queue_requests")
+        hs = np.zeros(max(n.value, 1), dtype=np.uint64)
+        _check(self.L.dmc_queue_requests(self.h, None, _ptr(hs), n.value,
+                                         ctypes.byref(n)), "queue_requests")
+        return counts, hs[:n.value]
+
     def remove_by_req_filter(self, fn, backwards=False):
         """remove_by_req_filter (dmclock_server.h:567-585): clients visited in
         ascending client-id order (std::map), each client's requests front to
-        back, or back to front when `backwards`."""
-        any_removed = False
+        back, or back to front when `backwards`.  One readback of every queued
+        handle, the filter on the host, one device compaction pass."""
+        counts, hs = self.queue_requests()
+        if not len(hs):
+            return False
+        offs = np.concatenate([[0], np.cumsum(counts, dtype=np.int64)]).astype(np.int64)
+        keep = np.ones(len(hs), dtype=np.uint8)
+        hl = hs.tolist()
         for c in sorted(self.slot_of):
-            hs = self.client_requests(c).tolist()
-            if not hs:
-                continue
-            keep = np.ones(len(hs), dtype=np.uint8)
-            order = range(len(hs) - 1, -1, -1) if backwards else range(len(hs))
+            s = self.slot_of[c]
+            a, b = int(offs[s]), int(offs[s + 1])
+            order = range(b - 1, a - 1, -1) if backwards else range(a, b)
             for i in order:
-                if fn(int(hs[i])):
+                if fn(int(hl[i])):
                     keep[i] = 0
-            if not keep.all():
-                any_removed = True
-                _check(self.L.dmc_client_filter(self.h, self.slot_of[c],
-                                                len(hs), _ptr(keep)), "filter")
-        return any_removed
+        if keep.all():
+            return False
+        anyr = _i32(0)
+        _check(self.L.dmc_queue_filter(self.h, _ptr(keep), len(keep), ctypes.byref(anyr)),
+               "queue_filter")
+        return bool(anyr.value)
+
+    def erase_batch(self, clients):
+        """dmc_client_erase_batch: do_clean's erase of several clients in one
+        pass; returns their queued handles (list order, FIFO per client)"""
+        sl = np.ascontiguousarray([self.slot_of[c] for c in clients], dtype=np.uint32)
+        n = ctypes.c_uint64(0)
+        cap = len(sl) * self.params.ring_capacity
+        hs = np.zeros(max(cap, 1), dtype=np.uint64)
+        _check(self.L.dmc_client_erase_batch(self.h, len(sl), _ptr(sl), None, _ptr(hs),
+                                             cap, ctypes.byref(n)), "erase_batch")
+        return hs[:n.value].copy()
 
     def mark_idle_batch(self, slots):
         slots = np.ascontiguousarray(slots, dtype=np.uint32)

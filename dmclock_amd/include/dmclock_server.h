@@ -15,14 +15,17 @@
 //  * requests R stay on the host, keyed by a 64-bit handle; the device sees
 //    handles only;
 //  * client_info_f is called at the reference's moments: at client creation,
-//    on update_client_info(s), and before every tag when U1 is set;
+//    on update_client_info(s), and, when U1 is set, by the engine (its
+//    dmc_info_fn) right before each tag calculation: per added request and,
+//    in delayed mode, for each popped client between selection and pop --
+//    O(1) host work per call, no per-pull sweep over the clients;
 //  * the idle/erase cleaner runs on a thread every check_time (the reference's
 //    RunEvery job, :858-861 / :1206-1255), erasing in client-id order.
 //
 // Deviations:
 //  * in-place mutation of a ClientInfo object the queue cached is seen at the
 //    next add of that client or update_client_info(s) (the reference also sees
-//    it at pops);
+//    it at pops); under U1 at the client's next tag calculation;
 //  * a client's queue is a bounded ring (GpuQueueOptions::ring_capacity);
 //    add_request returns DMC_EQUEUEFULL (< 0) when it is full;
 //  * the push queue's sched-ahead timer waits on the right clock (the
@@ -136,37 +139,40 @@ class PriorityQueueBase {
 
   // :567-585 -- clients in ascending C order; each client front to back (or
   // back to front); the filter receives the request and returns true to
-  // remove it.
+  // remove it.  One readback of every queued handle (dmc_queue_requests), the
+  // filter on the host, one device compaction pass (dmc_queue_filter).
   bool remove_by_req_filter(std::function<bool(RequestRef&&)> filter_accum,
                             bool visit_backwards = false) {
     std::lock_guard<std::mutex> g(data_mtx);
-    bool any = false;
-    std::vector<uint64_t> hs(opts_.ring_capacity);
+    std::vector<uint32_t> counts(opts_.max_clients);
+    uint64_t total = 0;
+    detail::check(dmc_queue_requests(q_, counts.data(), nullptr, 0, &total),
+                  "dmc_queue_requests");
+    if (!total) return false;
+    std::vector<uint64_t> hs(total);
+    detail::check(dmc_queue_requests(q_, nullptr, hs.data(), total, &total),
+                  "dmc_queue_requests");
+    std::vector<uint64_t> offs(counts.size() + 1, 0);
+    for (size_t s = 0; s < counts.size(); ++s) offs[s + 1] = offs[s] + counts[s];
+    std::vector<uint8_t> keep(total, 1);
+    bool modified = false;
     for (auto& kv : slot_of_) {
-      uint32_t n = 0;
-      detail::check(dmc_client_requests(q_, kv.second, hs.data(),
-                                        (uint32_t)hs.size(), &n),
-                    "dmc_client_requests");
-      if (!n) continue;
-      std::vector<uint8_t> keep(n, 1);
-      bool modified = false;
-      for (uint32_t j = 0; j < n; ++j) {
-        uint32_t i = visit_backwards ? n - 1 - j : j;
+      const uint64_t a = offs[kv.second], n = counts[kv.second];
+      for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t i = a + (visit_backwards ? n - 1 - j : j);
         auto it = requests_.find(hs[i]);
         if (filter_accum(std::move(it->second))) {
           keep[i] = 0;
           modified = true;
         }
       }
-      if (modified) {
-        for (uint32_t i = 0; i < n; ++i)
-          if (!keep[i]) requests_.erase(hs[i]);
-        detail::check(dmc_client_filter(q_, kv.second, n, keep.data()),
-                      "dmc_client_filter");
-        any = true;
-      }
     }
-    return any;
+    if (!modified) return false;
+    for (uint64_t i = 0; i < total; ++i)
+      if (!keep[i]) requests_.erase(hs[i]);
+    int any = 0;
+    detail::check(dmc_queue_filter(q_, keep.data(), total, &any), "dmc_queue_filter");
+    return any != 0;
   }
 
   static void request_sink(RequestRef&&) {}
@@ -242,6 +248,9 @@ class PriorityQueueBase {
     p.anticipation_timeout = anticipation;
     p.device = opts_.device;
     detail::check(dmc_queue_create(&p, &q_), "dmc_queue_create");
+    if (U1)  // get_cli_info (:870-875): the engine asks right before each tag
+      detail::check(dmc_queue_set_info_fn(q_, &PriorityQueueBase::info_fn, this),
+                    "dmc_queue_set_info_fn");
     info_of_.assign(opts_.max_clients, nullptr);
     dev_info_.assign(opts_.max_clients, ClientInfo(0, 0, 0));
     cleaner_ = std::thread([this] { clean_loop(); });
@@ -290,6 +299,20 @@ class PriorityQueueBase {
     return s;
   }
 
+  // U1: client_info_f for the engine (dmc_info_fn), called inside engine
+  // calls made under data_mtx, as the reference calls it under data_mtx
+  static int info_fn(void* ctx, uint32_t slot, double* r, double* w, double* l) {
+    auto* self = static_cast<PriorityQueueBase*>(ctx);
+    if (slot >= self->client_of_.size()) return 1;
+    const ClientInfo* ci = self->client_info_f(self->client_of_[slot]);
+    if (!ci) return 1;
+    self->info_of_[slot] = ci;
+    *r = ci->reservation;
+    *w = ci->weight;
+    *l = ci->limit;
+    return 0;
+  }
+
   // data_mtx held: make the device copy of a slot's ClientInfo current
   void push_info(uint32_t s) {
     const ClientInfo* ci = info_of_[s];
@@ -308,8 +331,9 @@ class PriorityQueueBase {
   int do_add_request(RequestRef&& request, const C& client_id,
                      const ReqParams& req_params, Time time, Cost cost) {
     uint32_t s = slot_for(client_id);
-    if (U1) info_of_[s] = client_info_f(client_id);  // get_cli_info, :870-875
-    push_info(s);
+    // U1: the engine fetches the info through info_fn at the tag calculation;
+    // otherwise values changed in place through the cached pointer are pushed
+    if (!U1) push_info(s);
     uint64_t h = next_handle_++;
     dmc_request rq{s, cost, time, req_params.delta, req_params.rho, h};
     int32_t rc = 0;
@@ -322,11 +346,7 @@ class PriorityQueueBase {
 
   // data_mtx held: one pull_request(now) on the engine
   int do_pull(Time now, dmc_decision* d, dmc_pull_result* res) {
-    if (U1)  // get_cli_info at pop time (delayed tags, reductions)
-      for (auto& kv : slot_of_) {
-        info_of_[kv.second] = client_info_f(kv.first);
-        push_info(kv.second);
-      }
+    // U1, delayed: the engine calls info_fn for the client it pops
     detail::check(dmc_pull_batch(q_, now, 1, d, res), "dmc_pull_batch");
     return res->n_decisions ? 0 : (int)res->next_type;
   }
@@ -363,23 +383,35 @@ class PriorityQueueBase {
       if (next_slot_)
         detail::check(dmc_client_last_ticks(q_, next_slot_, ticks.data()),
                       "dmc_client_last_ticks");
-      std::vector<uint64_t> hs(opts_.ring_capacity);
+      // one pass over the clients in C order, then one erase batch and one
+      // idle-marking batch on the engine
+      std::vector<uint32_t> to_erase, to_idle;
       for (auto i = slot_of_.begin(); i != slot_of_.end();) {
         auto i2 = i++;
         uint32_t s = i2->second;
         if (erase_point && erased < erase_max_ && ticks[s] <= erase_point) {
-          uint32_t n = 0;
-          detail::check(dmc_client_erase(q_, s, hs.data(), (uint32_t)hs.size(), &n),
-                        "dmc_client_erase");
-          for (uint32_t j = 0; j < n; ++j) requests_.erase(hs[j]);
+          to_erase.push_back(s);
           free_slots_.push_back(s);
           info_of_[s] = nullptr;
           slot_of_.erase(i2);
           ++erased;
         } else if (idle_point && ticks[s] <= idle_point) {
-          detail::check(dmc_client_mark_idle(q_, s), "dmc_client_mark_idle");
+          to_idle.push_back(s);
         }
       }
+      if (!to_erase.empty()) {
+        std::vector<uint64_t> hs((size_t)to_erase.size() * opts_.ring_capacity);
+        uint64_t n = 0;
+        detail::check(dmc_client_erase_batch(q_, (uint32_t)to_erase.size(),
+                                             to_erase.data(), nullptr, hs.data(),
+                                             hs.size(), &n),
+                      "dmc_client_erase_batch");
+        for (uint64_t j = 0; j < n; ++j) requests_.erase(hs[j]);
+      }
+      if (!to_idle.empty())
+        detail::check(dmc_client_mark_idle_batch(q_, (uint32_t)to_idle.size(),
+                                                 to_idle.data()),
+                      "dmc_client_mark_idle_batch");
       next_period_ = erased >= erase_max_
                          ? std::chrono::duration_cast<std::chrono::milliseconds>(
                                aggressive_check_time)

@@ -7,6 +7,9 @@ the HIP engine and on the CPU restatement:
     ("pull", now, k)         up to k pull_request(now)
     ("idle", slots)          do_clean's idle marking for these clients
     ("info", slot, r, w, l)  client_info_f changes + update_client_info
+    ("bind", slots, r, w, l) client_info_f returns fresh ClientInfo objects for
+                             these clients (seen under U1 at the next tag
+                             calculation, dmclock_server.h:870-875)
 
 Time base t0 = 1.0 s (epoch-scale times create rounding
 ties between tags).  Client ids are slots.
@@ -182,6 +185,25 @@ def config4_trace(seed, n_clients, n_steps, batch, depth=4, idle_frac=0.10,
     return tr
 
 
+def dynamic_trace(seed, n_clients, n_steps, adds_per_step, change_frac=0.2,
+                  k_choices=(1, 3, 16, 64, 256), depth=3):
+    """U1 (dynamic client info) trace: steady_trace with random delta/rho and,
+    before every pull, fresh ClientInfo for a random `change_frac` of the
+    clients (ClientInfo re-read at every tag, reductions with the cached one)."""
+    rng = np.random.default_rng(seed + 1000)
+    base = steady_trace(seed, n_clients, n_steps, adds_per_step, 0, depth=depth,
+                        delta_rho="random", k_choices=k_choices)
+    tr = Trace(base.clients, params=dict(base.params, dynamic=True))
+    for op in base.ops:
+        if op[0] == "pull":
+            m = max(1, int(change_frac * n_clients))
+            sl = np.sort(rng.choice(n_clients, m, replace=False)).astype(np.uint32)
+            t = client_table(rng, m)
+            tr.ops.append(("bind", sl, t.r, t.w, t.l))
+        tr.ops.append(op)
+    return tr
+
+
 def replay(q, trace, check=None):
     """Replay a trace on a queue exposing register/add_batch/pull_batch/
     mark_idle/set_info/update_client_info.  Yields per-op outputs."""
@@ -207,6 +229,13 @@ def replay(q, trace, check=None):
             q.set_info(s, r, w, l)
             q.update_client_info(s)
             outs.append(("info", None))
+        elif op[0] == "bind":
+            _, sl, r, w, l = op
+            for i, s in enumerate(sl.tolist()):
+                q.set_info(s, r[i], w[i], l[i], fresh=True)
+            if getattr(q, "explicit_bind", False):
+                q.bind_info(sl, r, w, l)  # dirty pushes instead of a callback
+            outs.append(("bind", None))
         if check is not None:
             check(op, outs[-1])
     return outs

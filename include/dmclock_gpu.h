@@ -71,7 +71,9 @@ typedef struct dmc_queue_params {
   uint32_t ring_capacity;    /* per-client request ring, power of two        */
   uint32_t max_batch;        /* max requests per add batch and decisions per pull batch */
   int32_t delayed;           /* IsDelayed (DelayedTagCalc), :277-280          */
-  int32_t dynamic_info;      /* U1: ClientInfo re-read at every tag, :870-875 */
+  int32_t dynamic_info;      /* U1: every tag calculation reads the bound
+                                ClientInfo (dmc_client_bind_info_batch or the
+                                dmc_info_fn) and caches it, :870-875          */
   int32_t at_limit;          /* DMC_AT_LIMIT_*                                */
   double reject_threshold;   /* RejectThreshold (AtLimitParam variant), :86-93 */
   double anticipation_timeout; /* :151-161                                    */
@@ -167,9 +169,37 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                               const double* reservation, const double* weight,
                               const double* limit, int active);
 /* update_client_info(s) after client_info_f returns new values
- * (dmclock_server.h:633-648; ClientInfo::update :111-118). */
+ * (dmclock_server.h:633-648; ClientInfo::update :111-118): the values become
+ * both what client_info_f returns (the bound info) and the cached
+ * client.info. */
 int dmc_client_update_info(dmc_queue* q, uint32_t slot, double reservation,
                            double weight, double limit);
+
+/* U1, get_cli_info (dmclock_server.h:870-875).  The engine models
+ * client_info_f as a per-client "bound" ClientInfo: what client_info_f(c)
+ * would return now.  With dynamic_info, every tag calculation (initial_tag
+ * :878-907, update_next_tag :1021-1036) reads the bound info and stores it as
+ * the client's cached info, which the reservation reductions use
+ * (:1077-1111), exactly as the reference's `client.info = client_info_f(...)`.
+ * Without dynamic_info the bound info is recorded and unused.
+ *
+ * dmc_client_bind_info_batch publishes new bound values (dirty pushes: only
+ * the clients whose ClientInfo changed need one).  Unchanged values cost no
+ * device work. */
+int dmc_client_bind_info_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                               const double* reservation, const double* weight,
+                               const double* limit);
+/* A host client_info_f for callers that cannot push changes: with
+ * dynamic_info the engine calls fn(ctx, slot, ...) on the calling thread
+ * right before each tag calculation a host-API call may perform -- for every
+ * request of dmc_add_batch, and in delayed mode for the client each
+ * pull_request of dmc_pull_batch dispatches, between its selection and its
+ * pop (such a dmc_pull_batch runs one pull at a time).  fn returns 0, or
+ * non-zero to fail the call with DMC_EINVAL.  The *_device entry points never
+ * call fn: their callers bind first.  fn == NULL removes it. */
+typedef int (*dmc_info_fn)(void* ctx, uint32_t slot, double* reservation,
+                           double* weight, double* limit);
+int dmc_queue_set_info_fn(dmc_queue* q, dmc_info_fn fn, void* ctx);
 /* do_clean's idle marking and erase, as explicit calls (dmclock_server.h
  * :1206-1255): mark_idle sets idle=true; erase drops the client and its
  * queued requests (their handles are written to handles_out, capacity cap). */
@@ -220,6 +250,28 @@ int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
  * ClientRec::remove_by_req_filter's erase (:440-480). */
 int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep);
+/* Whole-queue maintenance in a fixed number of device passes (no per-client
+ * round trips).  remove_by_req_filter (dmclock_server.h:567-585) is
+ *   dmc_queue_requests -> host filter over the handles -> dmc_queue_filter.
+ * dmc_queue_requests: counts_out[s] (max_clients entries, may be NULL) = the
+ * queued requests of slot s; handles_out = every queued handle, slots in
+ * ascending order, each client's FIFO order; *n_out = their total.  With
+ * handles_out NULL or cap < total only the counts and *n_out are written
+ * (size the buffer and call again). */
+int dmc_queue_requests(dmc_queue* q, uint32_t* counts_out, uint64_t* handles_out,
+                       uint64_t cap, uint64_t* n_out);
+/* ClientRec::remove_by_req_filter's erase for every client at once
+ * (:440-480): keep[i] != 0 keeps the i-th handle of the last
+ * dmc_queue_requests readback (n = its total); DMC_EINVAL if the queue
+ * changed since.  *any_removed (may be NULL): whether a request was removed. */
+int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_removed);
+/* do_clean's erase (:1244-1255) of n distinct registered clients in one pass:
+ * counts_out[i] (may be NULL) = slot i's queued requests, handles_out = their
+ * handles (list order, FIFO per client; cap >= total or DMC_EINVAL), *n_out =
+ * the total. */
+int dmc_client_erase_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
+                           uint32_t* counts_out, uint64_t* handles_out, uint64_t cap,
+                           uint64_t* n_out);
 int dmc_stats_get(dmc_queue* q, dmc_stats* out);
 
 /* ------------------------------------------------------------ client side

@@ -23,13 +23,17 @@ def compare_decisions(dg, do, where):
         assert bad.size == 0, (where, f, int(bad[0]), dg[bad[0]], do[bad[0]])
 
 
-def compare_states(qg, qo, slots, where=""):
+INFO_FIELDS = ("r_inv", "w_inv", "l_inv")  # the cached client.info
+
+
+def compare_states(qg, qo, slots, where="", info=False):
+    fields = STATE_FIELDS + (INFO_FIELDS if info else ())
     for s in slots:
         sg, so = qg.client_state(int(s)), qo.client_state(int(s))
         assert (sg is None) == (so is None), (where, s)
         if sg is None:
             continue
-        for f in STATE_FIELDS:
+        for f in fields:
             a, b = getattr(sg, f), getattr(so, f)
             if isinstance(a, float):
                 if f.startswith("front") and not so.count:
@@ -40,11 +44,13 @@ def compare_states(qg, qo, slots, where=""):
                 assert a == b, (where, s, f, a, b)
 
 
-def run_parity(trace, mk_gpu, queue_kw=None, state_sample=64, require_tie_free=True):
+def run_parity(trace, mk_gpu, queue_kw=None, state_sample=64, require_tie_free=True,
+               gpu_kw=None, info=False):
     """Replay `trace` on both engines op by op and compare every output."""
     queue_kw = queue_kw or {}
     qo = pyoracle.OracleQueue(**queue_kw)
-    qg = mk_gpu(max_clients=int(trace.clients.slots.max()) + 1, **queue_kw)
+    qg = mk_gpu(max_clients=int(trace.clients.slots.max()) + 1, **queue_kw,
+                **(gpu_kw or {}))
     outs_o = workloads.replay(qo, trace)
     ties = qo.ties
     if require_tie_free:
@@ -62,7 +68,7 @@ def run_parity(trace, mk_gpu, queue_kw=None, state_sample=64, require_tie_free=T
     rng = np.random.default_rng(0)
     slots = trace.clients.slots
     sample = rng.choice(slots, min(state_sample, len(slots)), replace=False)
-    compare_states(qg, qo, sample, "final")
+    compare_states(qg, qo, sample, "final", info=info)
     assert qg.request_count() == qo.request_count()
     assert tuple(qg.sched_counts()) == tuple(qo.sched_counts())
     return n_dec, qg, qo

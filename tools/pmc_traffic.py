@@ -16,14 +16,30 @@ from collections import defaultdict
 
 STAGES = {
     "scan": ["k_rscan"],
-    "select": ["k_rhist", "k_rpick"],
-    "cand": ["k_rcand"],
+    "select": ["k_rhist"],
     "emit": ["k_remit"],
-    "rank": ["k_rbscan", "k_rrank"],
+    "rank": ["k_rrank"],
     "apply": ["k_rapply"],
+    "future": ["k_round_future"],
     "add_link": ["k_add_link"],
     "add_chain": ["k_add_chain"],
 }
+CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
+
+
+def calibrate(fetch_csv, known_json):
+    """bytes-per-FETCH_SIZE-byte factors from tools/fetch_calib (each
+    repetition: 10 dispatches, the measured kernels at odd positions)"""
+    known = json.load(open(known_json))
+    rows = sorted(csv.DictReader(open(fetch_csv)), key=lambda x: int(x["Dispatch_Id"]))
+    vals = [float(r["Counter_Value"]) * 1024.0 for r in rows]
+    out = {}
+    for j, name in enumerate(CALIB):
+        got = [vals[10 * rep + 2 * j + 1] for rep in range(len(vals) // 10)]
+        avg = sum(got) / max(len(got), 1)
+        out[name] = {"known_bytes": known[name], "fetch_size_bytes": round(avg),
+                     "known_per_counted": known[name] / avg if avg else None}
+    return out
 
 
 def per_kernel(path, steps):
@@ -44,8 +60,17 @@ def main():
     ap.add_argument("--fetch", default="gpurun_out/pmc_FETCH_SIZE/run_counter_collection.csv")
     ap.add_argument("--write", default="gpurun_out/pmc_WRITE_SIZE/run_counter_collection.csv")
     ap.add_argument("--steps", type=int, default=6)
-    ap.add_argument("--out", default="profiles/traffic_r01.json")
+    ap.add_argument("--out", default="profiles/traffic_r02.json")
+    ap.add_argument("--calib", default=None,
+                    help="tools/fetch_calib FETCH_SIZE csv (with --known): print factors")
+    ap.add_argument("--known", default=None)
     a = ap.parse_args()
+    if a.calib:
+        out = calibrate(a.calib, a.known)
+        json.dump(out, open(a.out, "w"), indent=1)
+        for k, v in out.items():
+            print(k, v)
+        return
     fe = per_kernel(a.fetch, a.steps)
     wr = per_kernel(a.write, a.steps)
     out = {}
