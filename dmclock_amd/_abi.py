@@ -34,6 +34,7 @@ OPT_FORCE_RADIX = 2
 OPT_GRAPHS = 3
 OPT_ACT_SPLIT = 4
 OPT_SAMPLE = 5
+OPT_SINGLE_OP = 6
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0

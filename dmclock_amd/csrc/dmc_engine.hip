@@ -475,14 +475,29 @@ __device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
 // General do_next_request(now) one pull at a time (used for small k and for
 // AtLimit::Allow limit breaks, :1157-1165).  Reductions are per block, then
 // one block combines them.
-template <int THREADS = kBlock>
+// ATOMIC: the block's partial is stored with device-scope atomics (performed
+// at the memory side, visible to a last block after its acquire with no
+// release fence: an agent-scope release writes back the whole L2)
+template <int THREADS = kBlock, bool ATOMIC = false>
 __device__ inline void step_scan_body(const Table& tb, double now, StepRed* part) {
   ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
   uint64_t lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nrd = 0, nnr = 0;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    const ScanRec sr = tb.sc[s];
+  // four records per thread in flight (their loads issued before the first
+  // is used: the pass is bound by memory latency, not bandwidth)
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < tb.n; s0 += 4 * stride) {
+    ScanRec rs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t su = s0 + u * stride;
+      if (su < tb.n) rs[u] = tb.sc[su];
+      else rs[u].count = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const uint32_t s = s0 + u * stride;
+    const ScanRec sr = rs[u];
     if (!sr.count) continue;
     ++nany;
     ArgMin a{okey(sr.r), s, 1};
@@ -500,6 +515,7 @@ __device__ inline void step_scan_body(const Table& tb, double now, StepRed* part
       ++nnr;
       lnr = kl < lnr ? kl : lnr;
       pnr = argmin_combine(pnr, ArgMin{kp, s, 1});
+    }
     }
   }
   r = wave_argmin(r);
@@ -535,7 +551,16 @@ __device__ inline void step_scan_body(const Table& tb, double now, StepRed* part
       o.n_ready += sh[i].n_ready;
       o.n_notready += sh[i].n_notready;
     }
-    part[blockIdx.x] = o;
+    if (ATOMIC) {
+      static_assert(sizeof(StepRed) % 8 == 0, "StepRed is stored in 8-byte words");
+      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&o);
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(part + blockIdx.x);
+#pragma unroll
+      for (int i = 0; i < (int)(sizeof(StepRed) / 8); ++i) atomicExch(dst + i, src[i]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      part[blockIdx.x] = o;
+    }
   }
 }
 
@@ -556,10 +581,69 @@ __device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
 
 // launched with one block of kBlock threads; combines the per-block partials
 // (tree reduction in LDS), then thread 0 decides
+// do_next_request's decision from the combined reduction (:1115-1200)
+__device__ inline StepCtl step_decision(const StepRed& o, double now, int at_limit,
+                                        uint32_t nregistered) {
+  StepCtl c{};
+  c.type = DMC_NEXT_NONE;
+  c.slot = kNone;
+  if (nregistered == 0) return c;  // resv_heap.empty(), :1118-1120
+  double rtop = o.n_any ? from_okey(o.r.key) : kInf;
+  if (o.n_any && rtop <= now) {  // :1124-1128
+    c.type = DMC_NEXT_RETURNING;
+    c.prio = 0;
+    c.slot = o.r.slot;
+    c.tie = o.r.cnt > 1;
+    return c;
+  }
+  c.mark = 1;  // the limit scan ran
+  if (o.p.slot != kNone) {  // :1146-1151
+    c.type = DMC_NEXT_RETURNING;
+    c.prio = 1;
+    c.slot = o.p.slot;
+    c.tie = o.p.cnt > 1;
+    return c;
+  }
+  if (at_limit == DMC_AT_LIMIT_ALLOW && o.n_any) {  // :1157-1165
+    // ready-heap top: ready fronts first (all have p == inf here), else the
+    // min p+pd over not-ready fronts
+    bool top_ready = o.n_ready > 0;
+    if (!top_ready && o.pnr.slot != kNone && from_okey(o.pnr.key) < kInf) {
+      c.type = DMC_NEXT_RETURNING;
+      c.prio = 1;
+      c.slot = o.pnr.slot;
+      c.tie = o.pnr.cnt > 1;
+      return c;
+    }
+    if (rtop < kInf) {
+      c.type = DMC_NEXT_RETURNING;
+      c.prio = 0;
+      c.slot = o.r.slot;
+      c.tie = o.r.cnt > 1;
+      return c;
+    }
+  }
+  const double tmax = 1.7976931348623157e308;
+  double next = tmax;
+  if (o.n_any) {
+    next = min_not_0(next, rtop);
+    double lt = o.n_notready ? from_okey(o.lmin_nr) : from_okey(o.lmin_rd);
+    next = min_not_0(next, lt);
+  }
+  if (next < tmax) {
+    c.type = DMC_NEXT_FUTURE;
+    c.when = next;
+  }
+  return c;
+}
+
+// launched with one block of THREADS threads; combines the per-block
+// partials (tree reduction in LDS), then thread 0 decides (hsc: an optional
+// host-mapped mirror of the decision)
 template <int THREADS = kBlock>
 __device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
                             int at_limit, uint32_t nregistered,
-                            StepCtl* sc, Round* ctl) {
+                            StepCtl* sc, Round* ctl, StepCtl* hsc = nullptr) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
   if (ctl) now = ctl->now;
   __shared__ StepRed sh[THREADS];
@@ -580,86 +664,9 @@ __device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
     __syncthreads();
   }
   if (threadIdx.x) return;
-  StepRed o = sh[0];
-  StepCtl c{};
-  c.type = DMC_NEXT_NONE;
-  c.slot = kNone;
-  if (nregistered == 0) {  // resv_heap.empty(), :1118-1120
-    *sc = c;
-    if (ctl) {
-      ctl->next_type = c.type;
-      ctl->when = c.when;
-    }
-    return;
-  }
-  double rtop = o.n_any ? from_okey(o.r.key) : kInf;
-  if (o.n_any && rtop <= now) {  // :1124-1128
-    c.type = DMC_NEXT_RETURNING;
-    c.prio = 0;
-    c.slot = o.r.slot;
-    c.tie = o.r.cnt > 1;
-    *sc = c;
-    if (ctl) {
-      ctl->next_type = c.type;
-      ctl->when = c.when;
-    }
-    return;
-  }
-  c.mark = 1;  // the limit scan ran
-  if (o.p.slot != kNone) {  // :1146-1151
-    c.type = DMC_NEXT_RETURNING;
-    c.prio = 1;
-    c.slot = o.p.slot;
-    c.tie = o.p.cnt > 1;
-    *sc = c;
-    if (ctl) {
-      ctl->next_type = c.type;
-      ctl->when = c.when;
-    }
-    return;
-  }
-  if (at_limit == DMC_AT_LIMIT_ALLOW && o.n_any) {  // :1157-1165
-    // ready-heap top: ready fronts first (all have p == inf here), else the
-    // min p+pd over not-ready fronts
-    bool top_ready = o.n_ready > 0;
-    if (!top_ready && o.pnr.slot != kNone &&
-        from_okey(o.pnr.key) < kInf) {
-      c.type = DMC_NEXT_RETURNING;
-      c.prio = 1;
-      c.slot = o.pnr.slot;
-      c.tie = o.pnr.cnt > 1;
-      *sc = c;
-      if (ctl) {
-        ctl->next_type = c.type;
-        ctl->when = c.when;
-      }
-      return;
-    }
-    if (rtop < kInf) {
-      c.type = DMC_NEXT_RETURNING;
-      c.prio = 0;
-      c.slot = o.r.slot;
-      c.tie = o.r.cnt > 1;
-      *sc = c;
-      if (ctl) {
-        ctl->next_type = c.type;
-        ctl->when = c.when;
-      }
-      return;
-    }
-  }
-  const double tmax = 1.7976931348623157e308;
-  double next = tmax;
-  if (o.n_any) {
-    next = min_not_0(next, rtop);
-    double lt = o.n_notready ? from_okey(o.lmin_nr) : from_okey(o.lmin_rd);
-    next = min_not_0(next, lt);
-  }
-  if (next < tmax) {
-    c.type = DMC_NEXT_FUTURE;
-    c.when = next;
-  }
+  const StepCtl c = step_decision(sh[0], now, at_limit, nregistered);
   *sc = c;
+  if (hsc) *hsc = c;
   if (ctl) {
     ctl->next_type = c.type;
     ctl->when = c.when;
@@ -678,15 +685,15 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
   }
 }
 
-// A round's terminal pull in one kernel: one block of kFutThreads per CU
-// scans the table and writes its partial, and the last block to finish (one
-// ticket counter; lane-0 agent-scope release before the ticket, acquire after
-// it: MI355X_MICROARCH.md, inter-workgroup visibility) combines the partials,
-// decides and ends the round.  When the round did not run out of work (the
+// A round's terminal pull in one kernel: the blocks scan the table and store
+// their partials with memory-side atomics, and the last block to finish (one
+// ticket counter; agent-scope acquire after it: MI355X_MICROARCH.md,
+// inter-workgroup visibility) combines the partials, decides and ends the
+// round.  When the round did not run out of work (the
 // common case) block 0 only ends the round: one kernel boundary per round
 // instead of two.
-constexpr int kFutThreads = 1024;
-constexpr uint32_t kFutBlocks = 256;
+constexpr int kFutThreads = 256;  // (1024-thread blocks spill the reductions to scratch)
+constexpr uint32_t kFutBlocks = 1024;
 __global__ void __launch_bounds__(kFutThreads)
 k_round_future(Table tb, StepRed* part, int at_limit, uint32_t nregistered,
                StepCtl* sc, Round* ctl, HostRound* h, uint32_t* done) {
@@ -694,11 +701,10 @@ k_round_future(Table tb, StepRed* part, int at_limit, uint32_t nregistered,
     if (blockIdx.x == 0) rfinish_body(ctl, h);
     return;
   }
-  step_scan_body<kFutThreads>(tb, ctl->now, part);  // thread 0 stores the partial
+  // thread 0 stores the partial with memory-side atomics
+  step_scan_body<kFutThreads, true>(tb, ctl->now, part);
   __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool last = atomicAdd(done, 1u) == gridDim.x - 1;
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -726,10 +732,9 @@ __global__ void k_step_mark(Table tb, double now, const StepCtl* sc) {
 
 // pop_process_request (+ reduce_reservation_tags for ready-heap pops) of the
 // chosen client, :1046-1111.
-__global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
-                             dmc_decision* out, uint32_t out_idx,
-                             unsigned long long* sched) {
-  if (threadIdx.x || blockIdx.x) return;
+__device__ void step_apply_body(const Table& tb, uint64_t tick, const StepCtl* sc,
+                                dmc_decision* out, uint32_t out_idx,
+                                unsigned long long* sched) {
   if (sc->type != DMC_NEXT_RETURNING) return;
   uint32_t s = sc->slot;
   bool prio = sc->prio != 0;
@@ -805,6 +810,77 @@ __global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
   atomicAdd(&sched[prio ? 1 : 0], 1ull);
 }
 
+__global__ void k_step_apply(Table tb, uint64_t tick, const StepCtl* sc,
+                             dmc_decision* out, uint32_t out_idx,
+                             unsigned long long* sched) {
+  if (threadIdx.x || blockIdx.x) return;
+  step_apply_body(tb, tick, sc, out, out_idx, sched);
+}
+
+// ------------------------------------------------------------------ single-op path
+// One pull_request(now) in two kernels and one host round trip (the facade's
+// per-call path): k_fast_decide scans and, in its last block, decides
+// (mirrored to host-mapped memory); k_fast_apply commits the limit scan's
+// ready marks (grid) and, in its last block, pops the chosen client, writing
+// the decision to host-mapped memory.  Cross-block hand-off as k_round_future:
+// agent-scope release before the ticket, acquire in the last block.
+// (the blocks' partials were stored with memory-side atomics, completed
+// before the ticket: no release fence)
+__device__ inline bool last_block(uint32_t* done) {
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    const bool last = atomicAdd(done, 1u) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *done = 0;  // ready for the next call (no other block touches it now)
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+__global__ void __launch_bounds__(kFutThreads)
+k_fast_decide(Table tb, double now, StepRed* part, int at_limit, uint32_t nregistered,
+              StepCtl* sc, StepCtl* hsc, uint32_t* done) {
+  step_scan_body<kFutThreads, true>(tb, now, part);
+  if (!last_block(done)) return;
+  step_decide<kFutThreads>(gridDim.x, part, now, at_limit, nregistered, sc, nullptr, hsc);
+}
+
+// The marks and the pop touch disjoint state (the popped client's own mark
+// is moot: its new front is not ready), so block 0 pops while the grid marks.
+__global__ void k_fast_apply(Table tb, double now, uint64_t tick, const StepCtl* sc,
+                             dmc_decision* out, uint32_t out_idx,
+                             unsigned long long* sched) {
+  const StepCtl c = *sc;
+  if (blockIdx.x == 0 && threadIdx.x == 0) step_apply_body(tb, tick, sc, out, out_idx, sched);
+  if (!c.mark) return;
+  const uint32_t skip = c.type == DMC_NEXT_RETURNING ? c.slot : kNone;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {  // k_step_mark
+    if (s == skip) continue;
+    const ScanRec sr = tb.sc[s];
+    if (sr.count && !(sr.flags & F_READY) && sr.l <= now)
+      tb.sc[s].flags = sr.flags | F_READY;
+  }
+}
+
+// One add_request of a client that needs no idle reset (the facade's
+// per-call path): the request and its status in host-mapped memory.
+__global__ void k_add_one(Table tb, const dmc_request* req, int32_t* rc, uint64_t tick) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint32_t s = req->slot;
+  if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
+    *rc = DMC_ENOTREG;
+    return;
+  }
+  AddParams p{req, rc, tick, 1, 0};
+  AddState st;
+  add_chain_slot(tb, p, s, 1, 0, nullptr, nullptr, ActBuf{}, &st);
+}
+
 // ------------------------------------------------------------------ stats
 __global__ void k_count_requests(Table tb, unsigned long long* out) {
   unsigned long long t = 0;
@@ -847,6 +923,16 @@ struct GraphRec {
   hipKernelNodeParams kp2{};
 };
 
+// host-mapped I/O of the single-op path
+constexpr uint32_t kFastK = 8;
+struct FastIO {
+  StepCtl sc;
+  dmc_decision dec[kFastK];
+  dmc_request req;
+  int32_t rc;
+  int32_t pad;
+};
+
 struct dmc_queue {
   dmc_queue_params p{};
   hipStream_t stream = nullptr;
@@ -860,6 +946,12 @@ struct dmc_queue {
   std::vector<double> binfo_h;
   dmc_info_fn info_fn = nullptr;  // dmc_queue_set_info_fn
   void* info_ctx = nullptr;
+  // single-op path (DMC_OPT_SINGLE_OP): host-mapped request / status /
+  // decisions and the two kernels' ticket counters
+  bool single_op = true;
+  FastIO* h_fast = nullptr;
+  FastIO* d_fast = nullptr;
+  uint32_t* fast_done = nullptr;
   // queue-content generation (bumped by every call that can change a queue)
   // and the one dmc_queue_requests read, for dmc_queue_filter's check
   uint64_t gen = 0, maint_gen = ~0ull, maint_total = 0;
@@ -1756,6 +1848,46 @@ int wait_round(dmc_queue* q, uint64_t seq) {
   return DMC_OK;
 }
 
+// The single-op path: k <= kFastK pulls, each two kernels and one round
+// trip, decisions straight to the caller's buffer from host-mapped memory.
+bool fast_pull_ok(const dmc_queue* q, uint32_t k) {
+  return q->single_op && k <= q->small_k && k <= kFastK && !info_steps(q) && !q->prof_on;
+}
+
+int fast_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
+              dmc_pull_result* res) {
+  dmc_pull_result r{};
+  r.next_type = DMC_NEXT_RETURNING;
+  uint32_t n = 0;
+  const uint32_t gd = std::min(q->step_grid, kFutBlocks);
+  const uint32_t ga = grid_for(q->tb.n, 1024);
+  while (n < k) {
+    if (q->n_registered == 0) {
+      r.next_type = DMC_NEXT_NONE;
+      break;
+    }
+    hipLaunchKernelGGL(k_fast_decide, dim3(gd), dim3(kFutThreads), 0, q->stream, q->tb,
+                       now, q->red, q->p.at_limit, q->n_registered, q->sctl,
+                       &q->d_fast->sc, q->fast_done);
+    hipLaunchKernelGGL(k_fast_apply, dim3(ga), dim3(kBlock), 0, q->stream, q->tb, now,
+                       q->tick, (const StepCtl*)q->sctl, q->d_fast->dec, n, q->sched);
+    HIP_OK(hipStreamSynchronize(q->stream));
+    ++q->ctr.single_steps;
+    const StepCtl c = q->h_fast->sc;  // written before the stream sync
+    if (c.type != DMC_NEXT_RETURNING) {
+      r.next_type = c.type;
+      r.when = c.when;
+      break;
+    }
+    (c.prio ? r.n_priority : r.n_reservation)++;
+    ++n;
+  }
+  if (n) std::memcpy(out, (const void*)q->h_fast->dec, sizeof(dmc_decision) * n);
+  r.n_decisions = n;
+  if (res) *res = r;
+  return DMC_OK;
+}
+
 // k successive pull_request(now).  Each round is one graph launch and one
 // host round trip; a round ends the batch unless the radix path's dense
 // buffer overflowed (retry with more capacity), a rank bin overflowed (retry
@@ -2010,11 +2142,15 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->abuf, (size_t)N * kAddSlots);
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
+  rc |= A(&q->fast_done, 2);
   rc |= A(&q->reqcount, 1);
   if (hipHostMalloc((void**)&q->h_round, sizeof(HostRound),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&q->d_hround, q->h_round, 0) != hipSuccess ||
-      hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess)
+      hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess ||
+      hipHostMalloc((void**)&q->h_fast, sizeof(FastIO),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&q->d_fast, q->h_fast, 0) != hipSuccess)
     rc |= DMC_ENOMEM;
   else
     std::memset((void*)q->h_round, 0, sizeof(HostRound));
@@ -2066,6 +2202,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->h_mark) (void)hipHostFree(q->h_mark);
   if (q->mark_ev) (void)hipEventDestroy(q->mark_ev);
   if (q->h_sctl) (void)hipHostFree(q->h_sctl);
+  if (q->h_fast) (void)hipHostFree(q->h_fast);
+  dfree(q->fast_done);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -2483,6 +2621,17 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   // U1 with a host client_info_f: the infos the batch's tags read
   rc = fetch_infos(q, n, &reqs[0].slot, sizeof(dmc_request));
   if (rc) return rc;
+  if (n == 1 && q->single_op && !q->prof_on &&
+      (reqs[0].slot >= q->p.max_clients || !q->idle_h[reqs[0].slot])) {
+    // the single-op path: one kernel, request and status in host-mapped memory
+    q->h_fast->req = reqs[0];
+    hipLaunchKernelGGL(k_add_one, dim3(1), dim3(64), 0, q->stream, q->tb,
+                       (const dmc_request*)&q->d_fast->req, &q->d_fast->rc, q->tick);
+    HIP_OK(hipStreamSynchronize(q->stream));
+    q->tick += 1;
+    if (rc_out) rc_out[0] = q->h_fast->rc;
+    return DMC_OK;
+  }
   HIP_OK(hipMemcpyAsync(q->d_reqs, reqs, sizeof(dmc_request) * n,
                         hipMemcpyHostToDevice, q->stream));
   rc = q->n_idle ? add_with_idle(q, reqs, n, q->d_reqs, q->d_rc)
@@ -2529,6 +2678,7 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
   if (!q || (k && !out)) return DMC_EINVAL;
   QueueLock g(q);
   ++q->gen;
+  if (fast_pull_ok(q, k)) return fast_pull(q, now, k, out, result);
   int rc = ensure_dec(q, k);
   if (rc) return rc;
   dmc_pull_result r{};
@@ -2865,6 +3015,9 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_ACT_SPLIT:
       q->act_split = value != 0;
+      return DMC_OK;
+    case DMC_OPT_SINGLE_OP:
+      q->single_op = value != 0;
       return DMC_OK;
     case DMC_OPT_SAMPLE:
       if (value < 0 || value > 2) return DMC_EINVAL;

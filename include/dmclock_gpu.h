@@ -322,6 +322,10 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
 #define DMC_OPT_SAMPLE 5       /* pull-round thresholds for tables of >= 65,536 slots: 1 (default) from
                                   a 1/8 sample of the first keys, validated exactly (a failing round is
                                   re-run exactly); 0 always exact; 2 a test mode with no sampling margin */
+#define DMC_OPT_SINGLE_OP 6    /* 1 (default): host-API adds of one request of a non-idle client and
+                                  pulls with k <= SMALL_K run the single-op path (one kernel per add,
+                                  two per pull, results in host-mapped memory, one round trip);
+                                  0: the general launch sequence */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
 /* Engine path counters since creation (or the last reset): which ranking

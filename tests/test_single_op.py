@@ -1,0 +1,57 @@
+"""The single-op path (DMC_OPT_SINGLE_OP): host-API adds of one request of a
+non-idle client (one kernel, k_add_one) and pulls of k <= 8 (two kernels per
+pull_request, k_fast_decide / k_fast_apply, results in host-mapped memory)
+-- the facade's per-call path -- against the oracle, and the general step
+path (option off) on the same traces.  Modes as the reference's
+do_next_request branches (dmclock_server.h:1115-1200): AtLimit::Wait,
+AtLimit::Allow (limit breaks), delayed tags, non-monotone `now`."""
+import numpy as np
+import pytest
+
+from dmclock_amd import workloads
+from dmclock_amd._abi import AT_LIMIT_ALLOW, AT_LIMIT_WAIT, OPT_SINGLE_OP
+from parity import run_parity
+
+pytestmark = pytest.mark.gpu
+
+MODES = [dict(at_limit=AT_LIMIT_WAIT), dict(at_limit=AT_LIMIT_WAIT, delayed=True),
+         dict(at_limit=AT_LIMIT_ALLOW)]
+
+
+def _mk(single_op):
+    def mk(**kw):
+        from dmclock_amd.gpu import GpuQueue
+        q = GpuQueue(ring_capacity=64, **kw)
+        q.set_option(OPT_SINGLE_OP, int(single_op))
+        return q
+    return mk
+
+
+def _single_add_trace(seed, n, steps, delta_rho="random"):
+    """adds one request per op (the facade's add_request) between pulls of
+    k in 1..8 at sometimes decreasing `now`"""
+    rng = np.random.default_rng(seed)
+    base = workloads.steady_trace(seed, n, steps, 24, 0, depth=2, delta_rho=delta_rho,
+                                  k_choices=[1, 2, 3, 5, 8])
+    tr = workloads.Trace(base.clients, params=base.params)
+    for op in base.ops:
+        if op[0] == "add" and len(op[1]) <= 64:
+            for i in range(len(op[1])):
+                tr.ops.append(("add", op[1][i:i + 1].copy()))
+        elif op[0] == "pull":
+            now = op[1] - (0.3 if rng.random() < 0.2 else 0.0)  # non-monotone
+            tr.ops.append(("pull", now, op[2]))
+        else:
+            tr.ops.append(op)
+    return tr
+
+
+@pytest.mark.parametrize("single_op", [True, False])
+@pytest.mark.parametrize("mode", range(len(MODES)))
+def test_single_op_parity(mode, single_op):
+    tr = _single_add_trace(3 + mode, 512, 80)
+    n, qg, qo = run_parity(tr, _mk(single_op), queue_kw=MODES[mode], state_sample=512)
+    assert n > 250, n
+    c = qg.counters()
+    assert c["rounds"] == 0 and c["single_steps"] >= n, c
+    qg.close()
