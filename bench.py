@@ -155,6 +155,9 @@ def parse():
                          "and 10%% limit-throttled tenants; 5: multi-server "
                          "dmClock, --servers queues per GPU with device client "
                          "trackers and a per-epoch all-reduce")
+    ap.add_argument("--host-idle", action="store_true",
+                    help="config 4: mark idle from host lists (dmc_client_mark_idle_batch) "
+                         "instead of HBM-resident lists")
     ap.add_argument("--idle-frac", type=float, default=0.10,
                     help="config 4: fraction of the clients marked idle before "
                          "each step, drawn from those without an arrival in "
@@ -360,6 +363,12 @@ def main():
 
     dev = torch.device("cuda", local)
     d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r in steps]
+    # config 4: the idle lists resident in HBM like the requests (device-side
+    # marking, dmc_client_mark_idle_batch_device); --host-idle: host lists
+    d_idle = None
+    if idle is not None and not args.host_api and not args.host_idle:
+        d_idle = [torch.from_numpy(np.ascontiguousarray(x, dtype=np.uint32).view(np.int32))
+                  .to(dev) for x in idle]
     d_rc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
     d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8,
                         device=dev)
@@ -374,7 +383,10 @@ def main():
     def step(i):
         if idle is not None:
             t_a = time.perf_counter()
-            q.mark_idle_batch(idle[i])
+            if d_idle is not None:
+                q.mark_idle_batch_device(d_idle[i].data_ptr(), len(idle[i]))
+            else:
+                q.mark_idle_batch(idle[i])
             if timing:
                 host_t["mark_idle"] += time.perf_counter() - t_a
         t_b = time.perf_counter()

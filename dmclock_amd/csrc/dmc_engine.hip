@@ -340,6 +340,191 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
   }
 }
 
+// The sequential part of the idle resets, from activation j0 on with the
+// exact running minimum *M of the earlier activations' contributions:
+//   L_j = min(X_j, M_j), pd_j = L_j - t_j, c_j = p_j + pd_j,
+//   M_{j+1} = min(M_j, c_j)                                   (:957-984)
+// evaluated in windows of kActThreads activations, one per thread:
+//  1. speculate: on the integer grid g of M's binade every rounded
+//     operation above is an integer add (x - t rounds to x/g - rint(t/g)
+//     when the result stays in the binade), so the recurrence becomes the
+//     min-plus affine map m_{j+1} = min(m_j + min(0, d_j), rint(X_j/g) + d_j),
+//     d_j = rint(p_j/g) - rint(t_j/g), whose composition is associative: one
+//     block scan gives every M_j of the window;
+//  2. verify: every thread evaluates its activation exactly (the reference's
+//     double arithmetic) from the speculated M_j and checks that it yields the
+//     speculated M_{j+1}.  Up to and including the first failing activation
+//     the values are exact (its M_j was verified by its predecessor); the
+//     window commits them and the next one starts after it.
+// Binade crossings, rounding ties and X-restarts off the grid fail a
+// check, which costs one window; a window that advances less than 64
+// activations hands the next kActThreads to the wave-stepped recurrence
+// (act_wave_steps), whose cost is the number of new minima.
+__device__ inline double act_grid(double ref) {
+  int e = 0;
+  (void)frexp(ref, &e);  // ref = f * 2^e, 0.5 <= |f| < 1
+  return ldexp(1.0, e - 53);
+}
+
+struct AffMin {  // y -> min(y + a, b) on the grid (integer-valued doubles)
+  double a, b;
+};
+__device__ inline AffMin aff_then(AffMin f, AffMin g) {  // g after f
+  return AffMin{f.a + g.a, fmin(f.b + g.a, g.b)};
+}
+
+__device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
+                                      const uint64_t* ax, const double* ap,
+                                      const double* at, double* apd, double* s_M) {
+  // one wave steps the recurrence: with M fixed, every lane evaluates its
+  // activation; the first lane whose contribution undercuts M (a new
+  // minimum) ends the step, lanes up to it commit (their M was exact), and
+  // M takes that lane's value.  Steps: the new minima plus e / 64.
+  const uint32_t t = threadIdx.x;
+  if (t < 64) {
+    constexpr double dmax = 1.7976931348623157e308;  // :960
+    constexpr double trigger = dmax / 3.0;            // :957
+    double M = *s_M;
+    for (uint32_t j0 = 0; j0 < e; j0 += 64) {
+      const uint32_t j = c0 + j0 + t;
+      const bool in = j0 + t < e;
+      double rx = kInf, rp = 0.0, rt = 0.0, rpd0 = 0.0;
+      if (in) {
+        const uint64_t x = ax[j] < base ? ax[j] : base;
+        rx = x == kMaxKey ? kInf : from_okey(x);
+        rp = ap[j];
+        rt = at[j];
+        rpd0 = apd[j];
+      }
+      const uint32_t w = e - j0 < 64u ? e - j0 : 64u;
+      double out = rpd0;
+      for (uint32_t done = 0; done < w;) {
+        const bool act = in && t >= done;
+        double L = M < rx ? M : rx;
+        double lowest = L < dmax ? L : dmax;
+        const double pd = lowest < trigger ? __dsub_rn(lowest, rt) : rpd0;
+        const double c = __dadd_rn(rp, pd);
+        const uint64_t rec = __ballot(act && c < M);
+        const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
+        if (act && t <= r) out = pd;
+        if (rec) M = __shfl(c, (int)r);
+        done = r == 64u ? 64u : r + 1;
+      }
+      if (in) apd[j] = out;  // committed by k_act_commit
+    }
+    if (t == 0) *s_M = M;
+  }
+  __syncthreads();
+}
+
+constexpr int kChainK = 4;  // activations per thread and window (4096 per window)
+
+__device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t* ax,
+                          const double* ap, const double* at, double* apd, double* s_M,
+                          uint64_t* dbg) {
+  constexpr double dmax = 1.7976931348623157e308;
+  constexpr double trigger = dmax / 3.0;
+  __shared__ double s_ref, s_last[kActThreads];
+  __shared__ AffMin s_w[kActThreads / 64];
+  __shared__ uint32_t s_f;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  constexpr uint32_t WW = kActThreads * kChainK;
+  while (j0 < m) {
+    const uint32_t W = m - j0 < WW ? m - j0 : WW;
+    // this thread's activations: j0 + kChainK * t + u
+    double rx[kChainK], rp[kChainK], rt[kChainK], rpd0[kChainK];
+#pragma unroll
+    for (int u = 0; u < kChainK; ++u) {
+      const uint32_t i = kChainK * t + u;
+      rx[u] = kInf;
+      rp[u] = rt[u] = rpd0[u] = 0.0;
+      if (i < W) {
+        const uint64_t x = ax[j0 + i] < base ? ax[j0 + i] : base;
+        rx[u] = x == kMaxKey ? kInf : from_okey(x);
+        rp[u] = ap[j0 + i];
+        rt[u] = at[j0 + i];
+        rpd0[u] = apd[j0 + i];
+      }
+    }
+    const double M0 = *s_M;
+    if (t == 0) {
+      s_ref = M0 < kInf ? M0 : rx[0];  // the chain's binade (else the first X's)
+      s_f = W;
+      if (dbg) ++dbg[5];
+    }
+    __syncthreads();
+    const double g = act_grid(s_ref);
+    // 1. speculate: the thread's composed map, then a block scan of the maps
+    AffMin fu[kChainK];
+    AffMin f{0.0, kInf};
+#pragma unroll
+    for (int u = 0; u < kChainK; ++u) {
+      const bool in = kChainK * t + u < W;
+      const double d = rint(rp[u] / g) - rint(rt[u] / g);
+      fu[u] = AffMin{in ? fmin(0.0, d) : 0.0, in && rx[u] < kInf ? rint(rx[u] / g) + d : kInf};
+      f = aff_then(f, fu[u]);
+    }
+    AffMin incl = f;
+    for (int o = 1; o < 64; o <<= 1) {
+      AffMin v{__shfl_up(incl.a, o), __shfl_up(incl.b, o)};
+      if ((int)lane >= o) incl = aff_then(v, incl);
+    }
+    if (lane == 63) s_w[wv] = incl;
+    AffMin exw{__shfl_up(incl.a, 1), __shfl_up(incl.b, 1)};
+    if (lane == 0) exw = AffMin{0.0, kInf};
+    __syncthreads();
+    AffMin pre{0.0, kInf};
+    for (uint32_t i = 0; i < wv; ++i) pre = aff_then(pre, s_w[i]);
+    const AffMin ex = aff_then(pre, exw);  // everything before this thread
+    // this thread's speculated M after each of its activations, stepwise
+    // from the exclusive prefix; the last one is the next thread's start
+    double cur = fmin(M0 / g + ex.a, ex.b);
+    double spec[kChainK];
+#pragma unroll
+    for (int u = 0; u < kChainK; ++u) {
+      cur = fmin(cur + fu[u].a, fu[u].b);
+      spec[u] = cur * g;
+    }
+    s_last[t] = spec[kChainK - 1];
+    __syncthreads();
+    // 2. verify, in order (the reference's arithmetic from the speculated
+    // M_j; a thread starts from its predecessor's last verified value)
+    double Mj = t ? s_last[t - 1] : M0;
+    double pd[kChainK], Mn[kChainK];
+    uint32_t bad = 0xffffffffu;
+#pragma unroll
+    for (int u = 0; u < kChainK; ++u) {
+      const uint32_t i = kChainK * t + u;
+      const double L = Mj < rx[u] ? Mj : rx[u];
+      const double lowest = L < dmax ? L : dmax;
+      pd[u] = lowest < trigger ? __dsub_rn(lowest, rt[u]) : rpd0[u];
+      const double c = __dadd_rn(rp[u], pd[u]);
+      Mn[u] = c < Mj ? c : Mj;
+      if (i < W && bad == 0xffffffffu && dbits(Mn[u]) != dbits(spec[u])) bad = i;
+      Mj = spec[u];
+    }
+    if (bad != 0xffffffffu) atomicMin(&s_f, bad);
+    __syncthreads();
+    const uint32_t fl = s_f;  // first failing activation (W: none)
+#pragma unroll
+    for (int u = 0; u < kChainK; ++u) {
+      const uint32_t i = kChainK * t + u;
+      if (i < W && i <= fl) apd[j0 + i] = pd[u];  // committed by k_act_commit
+      if (i == (fl < W ? fl : W - 1)) *s_M = Mn[u];
+    }
+    __syncthreads();
+    const uint32_t adv = fl < W ? fl + 1 : W;
+    j0 += adv;
+    if (adv < 64 && j0 < m) {
+      // the grid does not describe this stretch: step it exactly
+      const uint32_t e = m - j0 < (uint32_t)kActThreads ? m - j0 : kActThreads;
+      act_wave_steps(j0, e, base, ax, ap, at, apd, s_M);
+      if (dbg && t == 0) ++dbg[6];
+      j0 += e;
+    }
+  }
+}
+
 // Step 3 (one block): only the M term is sequential.  Every L_k is first
 // taken as X_k = min(unchanged, pre, suf), which is exact as long as
 // M_{k-1} >= X_k for all k (checked chunk by chunk); from the first k where
@@ -348,7 +533,11 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
 // on one thread over LDS-staged inputs.
 __global__ void __launch_bounds__(kActThreads)
 k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
-              const double* at, const double* apd, const uint32_t* aslot) {
+              const double* at, double* apd, const uint32_t* aslot,
+              uint64_t* dbg = nullptr) {
+  // dbg (debug): [0] start [1] base [2] first pass [3] end clocks, [4] first
+  // undercut, [5] windows, [6] wave fallbacks, [7] activations
+  if (dbg && threadIdx.x == 0) dbg[0] = wall_clock64();
   __shared__ uint64_t wpart[kActThreads / 64];
   __shared__ uint64_t s_base, s_carry, s_minpre;
   __shared__ uint32_t s_fail;
@@ -365,6 +554,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
   }
   __syncthreads();
   const uint64_t base = s_base;
+  if (dbg && t == 0) dbg[1] = wall_clock64();
   uint32_t k0 = 0;
   // speculative: L_k = X_k
   for (; k0 < m; k0 += kActThreads) {
@@ -386,9 +576,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
     if (in && mprev < x) atomicMin(&s_fail, k);
     __syncthreads();
     const uint32_t fail = s_fail;
-    if (in && k < fail) {
-      activate_slot(tb, aslot[k], pd);
-    }
+    if (in && k < fail) apd[k] = pd;  // committed by k_act_commit
     if (fail != 0xffffffffu) {
       if (fail > k0 && t == fail - k0 - 1) s_minpre = incl;
       break;
@@ -399,10 +587,6 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
   __syncthreads();
   const uint32_t fail = s_fail;
   if (fail != 0xffffffffu) {
-    // the recurrence in doubles (okey order is the double order): a short
-    // dependent chain of min / compare / sub / add per activation
-    __shared__ double cx[kActThreads], cp[kActThreads], ct[kActThreads],
-        cpd[kActThreads];
     __shared__ double s_M;
     if (t == 0) {
       uint64_t M = s_carry;
@@ -410,60 +594,26 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
       s_M = M == kMaxKey ? kInf : from_okey(M);
     }
     __syncthreads();
-    for (uint32_t c0 = fail; c0 < m; c0 += kActThreads) {
-      const uint32_t k = c0 + t;
-      if (k < m) {
-        uint64_t x = ax[k] < base ? ax[k] : base;
-        cx[t] = x == kMaxKey ? kInf : from_okey(x);
-        cp[t] = ap[k];
-        ct[t] = at[k];
-        cpd[t] = apd[k];
-      }
-      __syncthreads();
-      if (t < 64) {
-        // one wave steps the recurrence: with M fixed, every lane evaluates
-        // its activation; the first lane whose contribution undercuts M (a
-        // new minimum) ends the step, lanes up to it commit (their M was
-        // exact), and M takes that lane's value.  The number of steps is the
-        // number of new minima plus e / 64, not e.  Each lane keeps its
-        // activation's inputs in registers for the whole 64-wide window, so
-        // a step's critical path is the arithmetic, the ballot and one
-        // readlane (no LDS round trip).
-        constexpr double dmax = 1.7976931348623157e308;  // :960
-        constexpr double trigger = dmax / 3.0;            // :957
-        double M = s_M;
-        const uint32_t e = m - c0 < (uint32_t)kActThreads ? m - c0 : kActThreads;
-        for (uint32_t j0 = 0; j0 < e; j0 += 64) {
-          const uint32_t j = j0 + t;
-          const bool in = j < e;
-          const double rx = in ? cx[j] : kInf, rp = in ? cp[j] : 0.0,
-                       rt = in ? ct[j] : 0.0, rpd0 = in ? cpd[j] : 0.0;
-          const uint32_t w = e - j0 < 64u ? e - j0 : 64u;
-          double out = rpd0;
-          for (uint32_t done = 0; done < w;) {
-            const bool act = in && t >= done;
-            double L = M < rx ? M : rx;
-            double lowest = L < dmax ? L : dmax;
-            const double pd = lowest < trigger ? __dsub_rn(lowest, rt) : rpd0;
-            const double c = __dadd_rn(rp, pd);
-            const uint64_t rec = __ballot(act && c < M);
-            const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
-            if (act && t <= r) out = pd;
-            if (rec) M = __shfl(c, (int)r);
-            done = r == 64u ? 64u : r + 1;
-          }
-          if (in) cpd[j] = out;
-        }
-        if (t == 0) s_M = M;
-      }
-      __syncthreads();
-      if (k < m) {
-        activate_slot(tb, aslot[k], cpd[t]);
-      }
-      __syncthreads();
-    }
+    if (dbg && t == 0) dbg[2] = wall_clock64();
+    act_chain(fail, m, base, ax, ap, at, apd, &s_M, dbg);
+  }
+  if (dbg && t == 0) {
+    dbg[3] = wall_clock64();
+    dbg[4] = fail;
+    dbg[7] = m;
   }
   if (t == 0) *act.extra = kMaxKey;  // ready for the next batch
+}
+
+// Step 4 (grid): every activation's idle reset takes effect -- prop_delta,
+// its front's cached key, idle cleared (k_act_resolve left the resolved
+// prop_deltas in apd; the resolution reads none of the state written here)
+__global__ void k_act_commit(Table tb, const uint32_t* dm, uint32_t m0, const double* apd,
+                             const uint32_t* aslot) {
+  const uint32_t m = dm ? *dm : m0;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m;
+       k += gridDim.x * blockDim.x)
+    activate_slot(tb, aslot[k], apd[k]);
 }
 
 // ------------------------------------------------------------------ future
@@ -952,6 +1102,9 @@ struct dmc_queue {
   FastIO* h_fast = nullptr;
   FastIO* d_fast = nullptr;
   uint32_t* fast_done = nullptr;
+  // dmc_client_mark_idle_batch_device: the host idle mirror (idle_h /
+  // n_idle) is stale until sync_idle reads the flags back
+  bool idle_unknown = false;
   // queue-content generation (bumped by every call that can change a queue)
   // and the one dmc_queue_requests read, for dmc_queue_filter's check
   uint64_t gen = 0, maint_gen = ~0ull, maint_total = 0;
@@ -1479,7 +1632,10 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
                      q->act_it, q->act_ipd, q->act_islot);
   hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
                      act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
-                     (const double*)q->act_it, (const double*)q->act_ipd,
+                     (const double*)q->act_it, q->act_ipd,
+                     (const uint32_t*)q->act_islot);
+  hipLaunchKernelGGL(k_act_commit, dim3(grid_for(act.m, 1024)), dim3(kBlock), 0, q->stream,
+                     q->tb, (const uint32_t*)nullptr, act.m, (const double*)q->act_ipd,
                      (const uint32_t*)q->act_islot);
   pe(q);
   HIP_OK(hipGetLastError());
@@ -1530,12 +1686,54 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
                      (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
                      q->act_it, q->act_ipd, q->act_islot);
+  static int dumps = 0;
+  const char* dump = q->debug ? getenv("DMC_DUMP_ACT") : nullptr;
+  if (dump && dumps < 4) {
+    // debug: the resolve's inputs (tools/act_chain_study.py)
+    HIP_OK(hipStreamSynchronize(q->stream));
+    uint32_t m = 0;
+    HIP_OK(hipMemcpy(&m, q->act_dm, 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> parts(gb + 1), ax(m);
+    std::vector<double> apv(m), atv(m), apdv(m);
+    HIP_OK(hipMemcpy(parts.data(), q->act_parts, 8ull * gb, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&parts[gb], q->act_extra, 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(ax.data(), q->act_x, 8ull * m, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(apv.data(), q->act_ip, 8ull * m, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(atv.data(), q->act_it, 8ull * m, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(apdv.data(), q->act_ipd, 8ull * m, hipMemcpyDeviceToHost));
+    uint64_t base = kMaxKey;
+    for (uint64_t v : parts) base = v < base ? v : base;
+    if (FILE* f = std::fopen(dump, "ab")) {
+      std::fwrite(&m, 4, 1, f);
+      std::fwrite(&base, 8, 1, f);
+      std::fwrite(ax.data(), 8, m, f);
+      std::fwrite(apv.data(), 8, m, f);
+      std::fwrite(atv.data(), 8, m, f);
+      std::fwrite(apdv.data(), 8, m, f);
+      std::fclose(f);
+    }
+    ++dumps;
+  }
   hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
                      act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
-                     (const double*)q->act_it, (const double*)q->act_ipd,
+                     (const double*)q->act_it, q->act_ipd,
+                     (const uint32_t*)q->act_islot, q->debug ? q->dbg_atime : nullptr);
+  hipLaunchKernelGGL(k_act_commit, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
+                     q->tb, (const uint32_t*)q->act_dm, n, (const double*)q->act_ipd,
                      (const uint32_t*)q->act_islot);
   pe(q);
   HIP_OK(hipGetLastError());
+  if (q->debug) {
+    std::vector<uint64_t> d(8);
+    HIP_OK(hipMemcpyAsync(d.data(), q->dbg_atime, 64, hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipMemsetAsync(q->dbg_atime, 0, 64, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    std::fprintf(stderr, "dmc act_resolve: m=%llu base %.2f us first pass %.2f us chain %.2f us "
+                 "(first undercut %llu, windows %llu, wave fallbacks %llu)\n",
+                 (unsigned long long)d[7], (d[1] - d[0]) / 100.0, (d[2] - d[1]) / 100.0,
+                 (d[3] - d[2]) / 100.0, (unsigned long long)d[4], (unsigned long long)d[5],
+                 (unsigned long long)d[6]);
+  }
   HIP_OK(hipMemcpyAsync(q->h_actm, q->act_dm, 4, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipMemcpyAsync(q->h_act, q->act_islot, 4ull * n, hipMemcpyDeviceToHost,
                         q->stream));
@@ -1548,6 +1746,7 @@ int settle_act(dmc_queue* q) {
   if (!q->act_pending) return DMC_OK;
   HIP_OK(hipStreamSynchronize(q->stream));
   q->act_pending = false;
+  if (q->idle_unknown) return DMC_OK;  // sync_idle rebuilds the mirror
   const uint32_t m = *q->h_actm;
   for (uint32_t k = 0; k < m; ++k) {
     const uint32_t s = q->h_act[k];
@@ -1558,6 +1757,37 @@ int settle_act(dmc_queue* q) {
   }
   return DMC_OK;
 }
+
+__global__ void k_idle_flags(Table tb, uint8_t* out) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
+       s += gridDim.x * blockDim.x) {
+    const uint8_t f = tb.sc[s].flags;
+    out[s] = (f & F_REG) && (f & F_IDLE) ? 1 : 0;
+  }
+}
+
+// The host idle mirror, rebuilt from the device flags after device-side
+// idle marking (one pass over the flags, N bytes back).
+int sync_idle(dmc_queue* q) {
+  if (!q->idle_unknown) return DMC_OK;
+  if (int rc = settle_act(q)) return rc;
+  const uint32_t N = q->tb.n;
+  uint8_t* d = nullptr;
+  HIP_OK(hipMalloc(&d, N));
+  hipLaunchKernelGGL(k_idle_flags, dim3(grid_for(N, 2048)), dim3(kBlock), 0, q->stream,
+                     q->tb, d);
+  HIP_OK(hipMemcpyAsync(q->idle_h.data(), d, N, hipMemcpyDeviceToHost, q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  dfree(d);
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < N; ++s) n += q->idle_h[s];
+  q->n_idle = n;
+  q->idle_unknown = false;
+  return DMC_OK;
+}
+
+// whether an add batch may contain an activation
+bool maybe_idle(const dmc_queue* q) { return q->n_idle || q->idle_unknown; }
 
 int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
                   const dmc_request* d_reqs, int32_t* d_rc) {
@@ -2228,6 +2458,7 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   QueueLock g(q);
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
   if (!n) return DMC_OK;
@@ -2307,6 +2538,7 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   uint8_t f;
   HIP_OK(hipMemcpyAsync(&f, &q->tb.sc[slot].flags, 1, hipMemcpyDeviceToHost, q->stream));
@@ -2330,6 +2562,7 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
   if (!q || (n && !slots)) return DMC_EINVAL;
   QueueLock g(q);
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s = slots[i];
     if (s >= q->p.max_clients) return DMC_EINVAL;
@@ -2480,6 +2713,24 @@ struct DevBuf {
   uint8_t* u8() const { return static_cast<uint8_t*>(p); }
 };
 
+__global__ void k_mark_idle_dev(Table tb, uint32_t n, const uint32_t* slots) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slots[i];
+  if (s < tb.n && (tb.sc[s].flags & F_REG)) tb.sc[s].flags |= F_IDLE;
+}
+
+int dmc_client_mark_idle_batch_device(dmc_queue* q, uint32_t n, const uint32_t* d_slots) {
+  if (!q || (n && !d_slots)) return DMC_EINVAL;
+  QueueLock g(q);
+  if (!n) return DMC_OK;
+  hipLaunchKernelGGL(k_mark_idle_dev, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     q->stream, q->tb, n, d_slots);
+  HIP_OK(hipGetLastError());
+  q->idle_unknown = true;
+  return DMC_OK;
+}
+
 static int read_handles(dmc_queue* q, uint32_t slot, std::vector<ReqEntry>* ents,
                         uint32_t* head) {
   ScanRec sr;
@@ -2534,6 +2785,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
   QueueLock g(q);
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -2615,6 +2867,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   QueueLock g(q);
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
   if (rc) return rc;
@@ -2655,8 +2908,10 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   if (rc) return rc;
   rc = settle_act(q);
   if (rc) return rc;
-  if (q->n_idle && !q->act_split && q->p.at_limit != DMC_AT_LIMIT_REJECT) {
+  if (maybe_idle(q) && !q->act_split && q->p.at_limit != DMC_AT_LIMIT_REJECT) {
     rc = add_act_batch_dev(q, n, d_reqs, d_rc_out);
+  } else if (maybe_idle(q) && (rc = sync_idle(q)) != DMC_OK) {
+    return rc;
   } else if (q->n_idle) {
     // the host split (Reject, or forced): stage the batch on the host
     std::vector<dmc_request> h(n);
@@ -2721,7 +2976,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
     QueueLock g(q);
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
-    fuse = n && k && q->n_idle == 0 && q->n_registered > 0 && k > q->small_k &&
+    fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
            !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
            q->use_graphs && !q->prof_on;
     if (fuse) {
@@ -2889,6 +3144,7 @@ int dmc_client_erase_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   if (!q || (n && !slots)) return DMC_EINVAL;
   QueueLock g(q);
   if (int rc0 = settle_act(q)) return rc0;
+  if (int rc0 = sync_idle(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
     if (!q->reg_h[slots[i]]) return DMC_ENOTREG;

@@ -41,6 +41,7 @@ EXPORTS = {
     "dmc_queue_set_info_fn": (_i32, [_vp, _vp, _vp]),
     "dmc_client_mark_idle": (_i32, [_vp, _u32]),
     "dmc_client_mark_idle_batch": (_i32, [_vp, _u32, _vp]),
+    "dmc_client_mark_idle_batch_device": (_i32, [_vp, _u32, _vp]),
     "dmc_client_erase": (_i32, [_vp, _u32, _vp, _u32, ctypes.POINTER(_u32)]),
     "dmc_client_get_state": (_i32, [_vp, _u32, ctypes.POINTER(ClientState)]),
     "dmc_client_last_ticks": (_i32, [_vp, _u32, _vp]),
@@ -423,6 +424,11 @@ class GpuQueue:
         slots = np.ascontiguousarray(slots, dtype=np.uint32)
         _check(self.L.dmc_client_mark_idle_batch(self.h, len(slots), _ptr(slots)),
                "mark_idle_batch")
+
+    def mark_idle_batch_device(self, d_slots_ptr, n):
+        """dmc_client_mark_idle_batch_device: the slot list in HBM"""
+        _check(self.L.dmc_client_mark_idle_batch_device(self.h, n, d_slots_ptr),
+               "mark_idle_batch_device")
 
     def mark_idle(self, client):
         _check(self.L.dmc_client_mark_idle(self.h, self.slot_of[client]),

@@ -207,6 +207,11 @@ int dmc_client_mark_idle(dmc_queue* q, uint32_t slot);
 /* The same for n registered clients (do_clean's idle pass over a client
  * set, :1230-1250); slots in host memory. */
 int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots);
+/* The same with the slot list in device memory, ordered on the queue's stream
+ * (no host round trip; unregistered slots are ignored).  The engine's host
+ * view of which clients are idle is re-read from the device when a later
+ * host-API call needs it; device-API adds detect activations on the device. */
+int dmc_client_mark_idle_batch_device(dmc_queue* q, uint32_t n, const uint32_t* d_slots);
 int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out);
 int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* out);

@@ -27,7 +27,7 @@ from parity import compare_decisions, compare_states
 pytestmark = pytest.mark.gpu
 
 
-def replay_device(q, trace, fuse=True):
+def replay_device(q, trace, fuse=True, host_ops=False):
     """workloads.replay through the device API: an add followed by a pull is
     one dmc_add_pull_batch_device call (fuse) -- bench.py's step -- other ops
     dmc_add_batch_device / dmc_pull_batch_device; inputs are copied to HBM
@@ -54,7 +54,13 @@ def replay_device(q, trace, fuse=True):
     i = 0
     while i < len(ops):
         op = ops[i]
-        if op[0] == "add":
+        if host_ops and op[0] == "add":  # host API after device-side idle marking
+            outs.append(("add", q.add_batch(op[1])))
+        elif host_ops and op[0] == "pull":
+            d, res = q.pull_batch(op[1], op[2])
+            outs.append(("pull", d, (res.n_decisions, res.next_type,
+                                     res.when if res.next_type == 1 else 0.0)))
+        elif op[0] == "add":
             reqs = torch.from_numpy(op[1].view(np.uint8).copy()).to(dev)
             n = len(op[1])
             torch.cuda.synchronize()  # the copy ran on torch's stream
@@ -75,7 +81,12 @@ def replay_device(q, trace, fuse=True):
             q.sync()
             outs.append(pull_out())
         elif op[0] == "idle":
-            q.mark_idle_batch(op[1])
+            # bench.py's config-4 marking: the list resident in HBM
+            d_idle = torch.from_numpy(np.ascontiguousarray(op[1], dtype=np.uint32)
+                                      .view(np.int32)).to(dev)
+            torch.cuda.synchronize()
+            q.mark_idle_batch_device(d_idle.data_ptr(), len(op[1]))
+            q.sync()
             outs.append(("idle", None))
         else:
             raise ValueError(op[0])
@@ -83,7 +94,7 @@ def replay_device(q, trace, fuse=True):
     return outs
 
 
-def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True):
+def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True, host_ops=False):
     from dmclock_amd.gpu import GpuQueue
     queue_kw = queue_kw or {}
     qo = pyoracle.OracleQueue(**queue_kw)
@@ -92,7 +103,7 @@ def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True):
     n = int(trace.clients.slots.max()) + 1
     maxb = max(len(op[1]) for op in trace.ops if op[0] == "add")
     qg = GpuQueue(max_clients=n, ring_capacity=64, max_batch=maxb, **queue_kw)
-    outs_g = replay_device(qg, trace, fuse=fuse)
+    outs_g = replay_device(qg, trace, fuse=fuse, host_ops=host_ops)
     n_dec = 0
     for i, (a, b) in enumerate(zip(outs_g, outs_o)):
         assert a[0] == b[0], i
@@ -127,13 +138,13 @@ def test_fused_bench_call_parity_1m_clients():
 
 
 @pytest.mark.parametrize("seed", [1, 2])
-@pytest.mark.parametrize("api", ["device", "host"])
+@pytest.mark.parametrize("api", ["device", "host", "mixed"])
 def test_config4_churn_throttled_parity_64k(seed, api):
     """BASELINE config 4 at 65,536 clients: before each of four steps of 4096
     adds + 4096 pulls, 10 % of the clients (those without an arrival in the
     two previous steps) are marked idle; 10 % of the tenants are limited
     below their arrival rate (AtLimit::Wait).  Seeds 1 and 2 are tie-free
-    under the oracle.  Both APIs bit-exact, hundreds of activations per step."""
+    under the oracle.  Every API bit-exact, hundreds of activations per step."""
     from parity import run_parity
     tr = workloads.config4_trace(seed, 1 << 16, 4, 1 << 12)
     idle = np.zeros(1 << 16, bool)
@@ -146,8 +157,10 @@ def test_config4_churn_throttled_parity_64k(seed, api):
             acts += int(idle[u].sum())
             idle[u] = False
     assert acts > 500, acts
-    if api == "device":
-        n, qg, qo = device_parity(tr)
+    if api in ("device", "mixed"):
+        # mixed: HBM idle lists, then host-API adds / pulls (the engine
+        # re-reads its idle view from the device)
+        n, qg, qo = device_parity(tr, host_ops=api == "mixed")
     else:
         from test_gpu_parity import mk_gpu
         n, qg, qo = run_parity(tr, mk_gpu, state_sample=4096)
