@@ -454,14 +454,15 @@ __device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t
     }
     __syncthreads();
     const double g = act_grid(s_ref);
+    const double gi = 1.0 / g;  // a power of two: x * gi == x / g exactly
     // 1. speculate: the thread's composed map, then a block scan of the maps
     AffMin fu[kChainK];
     AffMin f{0.0, kInf};
 #pragma unroll
     for (int u = 0; u < kChainK; ++u) {
       const bool in = kChainK * t + u < W;
-      const double d = rint(rp[u] / g) - rint(rt[u] / g);
-      fu[u] = AffMin{in ? fmin(0.0, d) : 0.0, in && rx[u] < kInf ? rint(rx[u] / g) + d : kInf};
+      const double d = rint(rp[u] * gi) - rint(rt[u] * gi);
+      fu[u] = AffMin{in ? fmin(0.0, d) : 0.0, in && rx[u] < kInf ? rint(rx[u] * gi) + d : kInf};
       f = aff_then(f, fu[u]);
     }
     AffMin incl = f;
@@ -478,7 +479,7 @@ __device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t
     const AffMin ex = aff_then(pre, exw);  // everything before this thread
     // this thread's speculated M after each of its activations, stepwise
     // from the exclusive prefix; the last one is the next thread's start
-    double cur = fmin(M0 / g + ex.a, ex.b);
+    double cur = fmin(M0 * gi + ex.a, ex.b);
     double spec[kChainK];
 #pragma unroll
     for (int u = 0; u < kChainK; ++u) {
@@ -1734,10 +1735,14 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
                  (d[3] - d[2]) / 100.0, (unsigned long long)d[4], (unsigned long long)d[5],
                  (unsigned long long)d[6]);
   }
-  HIP_OK(hipMemcpyAsync(q->h_actm, q->act_dm, 4, hipMemcpyDeviceToHost, q->stream));
-  HIP_OK(hipMemcpyAsync(q->h_act, q->act_islot, 4ull * n, hipMemcpyDeviceToHost,
-                        q->stream));
-  q->act_pending = true;
+  // the host idle mirror learns the activated slots (not needed while it is
+  // stale anyway: device-side idle marking, sync_idle rebuilds it)
+  if (!q->idle_unknown) {
+    HIP_OK(hipMemcpyAsync(q->h_actm, q->act_dm, 4, hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipMemcpyAsync(q->h_act, q->act_islot, 4ull * n, hipMemcpyDeviceToHost,
+                          q->stream));
+    q->act_pending = true;
+  }
   return DMC_OK;
 }
 
