@@ -13,6 +13,7 @@
 // struct-of-arrays client table plus a per-batch radix sort of the candidate
 // pops; see DESIGN.md for why the result is the reference's dispatch order.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -1231,8 +1232,8 @@ void prof_gate(dmc_queue* q) {
     hipLaunchKernelGGL(k_prof_gate, dim3(1), dim3(64), 0, q->stream, 50u);  // ~170 us
 }
 
-void pb(dmc_queue* q, int stage) {
-  if (!q->prof_on) return;
+bool prof_slot(dmc_queue* q, int stage) {
+  if (!q->prof_on) return false;
   if (q->prof_n == q->prof_pool.size()) {
     ProfRec r;
     // timing-only events: no system-scope fence (no L2 writeback/invalidate
@@ -1240,12 +1241,31 @@ void pb(dmc_queue* q, int stage) {
     if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
         hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
       q->prof_on = false;
-      return;
+      return false;
     }
     q->prof_pool.push_back(r);
   }
   q->prof_pool[q->prof_n].stage = stage;
-  (void)hipEventRecord(q->prof_pool[q->prof_n].a, q->stream);
+  return true;
+}
+
+void pb(dmc_queue* q, int stage) {
+  if (prof_slot(q, stage)) (void)hipEventRecord(q->prof_pool[q->prof_n].a, q->stream);
+}
+
+// A stage that is one kernel.  Profiling: the kernel's own dispatch records
+// the stage's events at its start and end (hipExtLaunchKernel), so the stage
+// time is the kernel's execution, as rocprofv3 reports it, without the
+// launch gap a pair of stream events around it would add.
+template <typename F, typename... Args>
+void klaunch(dmc_queue* q, int stage, F kernel, dim3 g, dim3 b, uint32_t sh, Args... args) {
+  if (!prof_slot(q, stage)) {
+    hipLaunchKernelGGL(kernel, g, b, sh, q->stream, args...);
+    return;
+  }
+  const ProfRec& r = q->prof_pool[q->prof_n];
+  hipExtLaunchKernelGGL(kernel, g, b, sh, q->stream, r.a, r.b, 0, args...);
+  ++q->prof_n;
 }
 
 void pe(dmc_queue* q) {
@@ -1469,15 +1489,11 @@ int slot_bits(uint32_t n) {
 void enqueue_add(dmc_queue* q, const AddParams& ap) {
   prof_gate(q);
   uint32_t g = (ap.n + kBlock - 1) / kBlock;
-  pb(q, DMC_PROF_ADD_LINK);
-  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
-                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk);
-  pe(q);
-  pb(q, DMC_PROF_ADD_CHAIN);
-  hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
-                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot);
-  pe(q);
+  klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, q->tb, q->acnt,
+          q->abuf, q->apos, q->aslot, q->apblk, ActBuf{});
+  klaunch(q, DMC_PROF_ADD_CHAIN, k_add_chain, dim3(g), dim3(kBlock), 0, q->tb,
+          (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+          (const uint32_t*)q->apos, (const uint32_t*)q->aslot, ActBuf{});
 }
 
 int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
@@ -1817,13 +1833,10 @@ uint32_t pow2_at_least(uint32_t x) {
 // limit-heap tops, :1170-1185.  No-op unless the round is terminal.
 void launch_future(dmc_queue* q) {
   const double now = 0.0;  // read from the round by the kernels
-  pb(q, DMC_PROF_FUTURE);
   (void)now;
-  hipLaunchKernelGGL(k_round_future, dim3(std::min(q->step_grid, kFutBlocks)),
-                     dim3(kFutThreads), 0, q->stream,
-                     q->tb, q->red, q->p.at_limit, q->n_registered, q->sctl, q->rd,
-                     q->d_hround, q->fut_done);
-  pe(q);
+  klaunch(q, DMC_PROF_FUTURE, k_round_future, dim3(std::min(q->step_grid, kFutBlocks)),
+          dim3(kFutThreads), 0, q->tb, q->red, q->p.at_limit, q->n_registered, q->sctl,
+          q->rd, q->d_hround, q->fut_done);
 }
 
 // bound infos of distinct slots (dmc_client_bind_info_batch)
@@ -1967,41 +1980,30 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   // walking kernels: grid-stride over the candidate list, sized so that
   // a typical round's candidates are resident at once
   uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
-  pb(q, DMC_PROF_SCAN);
-  hipLaunchKernelGGL(k_rscan, dim3(gN), dim3(kScanBlock), 0, q->stream, tb, q->keyr,
-                     q->keyp, q->meta, q->rparts, q->rd, cp,
-                     sampled ? q->skr : nullptr, sampled ? q->skp : nullptr);
-  pe(q);
-  pb(q, DMC_PROF_SELECT);
+  klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb, q->keyr,
+          q->keyp, q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
+          sampled ? q->skp : nullptr);
   if (sampled)
-    hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0, q->stream,
-                       (N + kSample - 1) / kSample, (const uint64_t*)q->skr,
-                       (const uint64_t*)q->skp, (const RoundPart*)q->rparts, gN, q->rd,
-                       q->hist, q->sbn, q->hist_done, q->sample_mode == 2 ? 2 : 1);
+    klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
+            (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
+            (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn, q->hist_done,
+            q->sample_mode == 2 ? 2 : 1);
   else
-    hipLaunchKernelGGL(k_rhist, dim3(kHistBlocksR), dim3(1024), 0, q->stream, N,
-                       (const uint64_t*)q->keyr, (const uint64_t*)q->keyp,
-                       (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn,
-                       q->hist_done, 0);
-  pe(q);
-  pb(q, DMC_PROF_EMIT);
-  hipLaunchKernelGGL(k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk), dim3(kEmitThreads),
-                     0, q->stream, tb, q->rd, (const uint64_t*)q->keyr,
-                     (const uint64_t*)q->keyp, (const uint32_t*)q->meta,
-                     q->cand, radix ? nullptr : q->brec,
-                     q->bcount, q->bsize, (const uint32_t*)q->sbn, q->dense, q->ecap,
-                     q->bcnt, q->bsoff, q->bpoff, q->emit_done);
-  pe(q);
+    klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
+            (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
+            gN, q->rd, q->hist, q->sbn, q->hist_done, 0);
+  klaunch(q, DMC_PROF_EMIT, k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk),
+          dim3(kEmitThreads), 0, tb, q->rd, (const uint64_t*)q->keyr,
+          (const uint64_t*)q->keyp, (const uint32_t*)q->meta, q->cand,
+          radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
+          q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done);
   if (!radix) {
-    pb(q, DMC_PROF_RANK);
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
-    hipLaunchKernelGGL(k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->stream,
-                       q->rd, (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff,
-                       (const uint32_t*)q->bpoff, (const BRecR*)q->brec, tb.ring,
-                       q->debug ? q->dbg_wtime : nullptr);
-    pe(q);
+    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
+            (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
+            (const BRecR*)q->brec, tb.ring, q->debug ? q->dbg_wtime : nullptr);
   } else {
     uint32_t E = q->ecap;
     uint32_t gE = grid_for(E, 1024);
@@ -2032,10 +2034,8 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                        (const uint32_t*)q->gpoff, tb.ring);
     pe(q);
   }
-  pb(q, DMC_PROF_APPLY);
-  hipLaunchKernelGGL(k_rapply, dim3(gW), dim3(kBlockR), 0, q->stream, tb, q->rd,
-                     (const CandRec*)q->cand, q->sched, q->debug ? q->dbg_atime : nullptr);
-  pe(q);
+  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(gW), dim3(kBlockR), 0, tb, q->rd,
+          (const CandRec*)q->cand, q->sched, q->debug ? q->dbg_atime : nullptr);
   if (future)
     launch_future(q);  // its decide kernel ends the round
   else

@@ -25,19 +25,33 @@ STAGES = {
     "add_chain": ["k_add_chain"],
 }
 CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
+STREAMING = {"scan", "select", "future"}
 
 
 def calibrate(fetch_csv, known_json):
-    """bytes-per-FETCH_SIZE-byte factors from tools/fetch_calib (each
-    repetition: 10 dispatches, the measured kernels at odd positions)"""
+    """bytes-per-FETCH_SIZE-byte factors from tools/fetch_calib: per
+    repetition six stream16 dispatches (the 2nd is the measured 512 MiB, the
+    others 2 GiB evict passes) and one of each random-access kernel"""
     known = json.load(open(known_json))
     rows = sorted(csv.DictReader(open(fetch_csv)), key=lambda x: int(x["Dispatch_Id"]))
-    vals = [float(r["Counter_Value"]) * 1024.0 for r in rows]
+    by = defaultdict(list)
+    for r in rows:
+        name = r["Kernel_Name"]
+        key = ("rand64" if "rand_rec<4>" in name else "rand32" if "rand_rec<2>" in name
+               else "rand16" if name.startswith("rand16") else "rand8"
+               if name.startswith("rand8") else "stream16" if name.startswith("stream16")
+               else None)
+        if key:
+            by[key].append(float(r["Counter_Value"]) * 1024.0)
+    by["evict"] = [v for i, v in enumerate(by["stream16"]) if i % 6 != 1]
+    by["stream16"] = [v for i, v in enumerate(by["stream16"]) if i % 6 == 1]
+    known = dict(known, evict=known["evict_pass_bytes"])
     out = {}
-    for j, name in enumerate(CALIB):
-        got = [vals[10 * rep + 2 * j + 1] for rep in range(len(vals) // 10)]
+    for name in CALIB + ["evict"]:
+        got = by.get(name, [])
         avg = sum(got) / max(len(got), 1)
         out[name] = {"known_bytes": known[name], "fetch_size_bytes": round(avg),
+                     "dispatches": len(got),
                      "known_per_counted": known[name] / avg if avg else None}
     return out
 
@@ -77,8 +91,16 @@ def main():
     for stage, ks in STAGES.items():
         f = sum(sum(fe.get(k, [])) / max(len(fe.get(k, [])), 1) for k in ks)
         w = sum(sum(wr.get(k, [])) / max(len(wr.get(k, [])), 1) for k in ks)
+        # calibrated on known byte counts (tools/fetch_calib.hip, profiles/
+        # r02_fetch_calib.json): FETCH_SIZE counts 64 B per memory request; a
+        # coalesced stream requests 128 B (bytes = 2 x FETCH_SIZE), a random
+        # access of <= 64 B one 64-B request (bytes = FETCH_SIZE).  Streaming
+        # stages take 2x; the walkers mix both, so their traffic is bracketed
+        # by 1x (all random) and 2x (all streamed), 1x being reported
+        fac = 2.0 if stage in STREAMING else 1.0
         out[stage] = {"fetch_size_bytes_raw": round(f), "write_size_bytes": round(w),
-                      "hbm_bytes": round(2 * f + w),
+                      "hbm_bytes": round(fac * f + w), "fetch_factor": fac,
+                      "hbm_bytes_if_all_streamed": round(2 * f + w),
                       "kernels": ks, "launches_averaged": a.steps}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out.items():
