@@ -1103,9 +1103,6 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (brec)
-    for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
-  __syncthreads();  // s_cnt zeroed before any wave adds to it
   uint64_t kr[4], kp[4];
   uint32_t mt[4];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   if (s0 + 4 <= n) {
@@ -1125,6 +1122,10 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
       mt[j] = in ? meta[s0 + j] : 0;
     }
   }
+  // the rank-bin table staged while the keys are in flight
+  if (brec)
+    for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
+  __syncthreads();  // s_cnt zeroed before any wave adds to it
   uint8_t f[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) f[j] = (uint8_t)(mt[j] >> 8);
