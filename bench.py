@@ -543,10 +543,12 @@ def main():
         "stages_ms_per_step": {n: round(ms / max(prof_steps, 1), 4)
                                for n, (c, ms) in prof.items() if c},
         "stages_note": "stage times from a second pass of prof_steps steps "
-                       "launched eagerly behind a GPU-side gate (all of a "
-                       "call's kernels queued before the first starts) with "
-                       "HIP events around each stage; the timed region "
-                       "replays captured hipGraphs",
+                       "launched eagerly on the engine's stream: one-kernel "
+                       "stages with HIP events recorded by the kernel's own "
+                       "dispatch (hipExtLaunchKernel: execution time, as "
+                       "rocprofv3 reports it), multi-kernel stages with "
+                       "event pairs; the timed region replays captured "
+                       "hipGraphs",
         "prof_steps": prof_steps,
         "engine_counters": ctr_timed,
     }
