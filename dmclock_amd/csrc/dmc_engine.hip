@@ -1129,7 +1129,8 @@ struct dmc_queue {
   uint64_t *skr = nullptr, *skp = nullptr;  // N / kSample: the threshold histogram's sample
   bool exact_next = false;    // re-run a round whose sampled threshold failed exactly
   int sample_mode = 1;        // DMC_OPT_SAMPLE: 0 exact, 1 sampled, 2 sampled (test: no margin)
-  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics)
+  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics;
+                                                  // bcount: 8 bytes per bin)
   uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
   uint32_t* hist_done = nullptr;  // k_rhist's block ticket counter
   uint32_t* emit_done = nullptr;  // k_remit's block ticket counter
@@ -1188,6 +1189,7 @@ struct dmc_queue {
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
   uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
   uint64_t* dbg_atime = nullptr; // debug: per-candidate apply start/end clocks
+  uint64_t* dbg_etime = nullptr; // debug: per-block k_remit phase clocks (5 per block)
   uint32_t radix_batches = 0;  // rounds left on the fallback path
   uint32_t ovf_streak = 0;     // bin-rank rounds in a row that overflowed (saturates at 5)
   dmc_counters ctr{};          // dmc_queue_counters
@@ -1996,7 +1998,8 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
           dim3(kEmitThreads), 0, tb, q->rd, (const uint64_t*)q->keyr,
           (const uint64_t*)q->keyp, (const uint32_t*)q->meta, q->cand,
           radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
-          q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done);
+          q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
+          q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
@@ -2199,6 +2202,22 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
         std::fclose(f);
       }
     }
+    if (q->debug && getenv("DMC_EMIT_CLOCKS")) {
+      const uint32_t nb = (q->tb.n + kEmitChunk - 1) / kEmitChunk;
+      std::vector<uint64_t> e(5ull * nb + 1);
+      (void)hipMemcpy(e.data(), q->dbg_etime, 8ull * e.size(), hipMemcpyDeviceToHost);
+      uint64_t t0 = ~0ull;
+      for (uint32_t b = 0; b < nb; ++b) t0 = std::min(t0, e[5ull * b]);
+      // per phase: median and max over blocks, in us from the first block's start
+      for (int ph = 0; ph < 5; ++ph) {
+        std::vector<double> v(nb);
+        for (uint32_t b = 0; b < nb; ++b) v[b] = (e[5ull * b + ph] - t0) / 100.0;
+        std::sort(v.begin(), v.end());
+        std::fprintf(stderr, "emit clock %d: min %.2f med %.2f max %.2f us\n", ph, v[0],
+                     v[nb / 2], v[nb - 1]);
+      }
+      std::fprintf(stderr, "emit clock tail end: %.2f us\n", (e[5ull * nb] - t0) / 100.0);
+    }
     if (q->debug)
       std::fprintf(stderr,
                    "dmc round: k=%u n_r=%llu p_runs=%u cand=%u R(elig=%u T=%s) "
@@ -2360,7 +2379,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
-  rc |= A(&q->bcount, kNBR);
+  rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsize, kNBR);
   rc |= A(&q->bcnt, kNBR);
   rc |= A(&q->hist_done, 1);
@@ -2370,6 +2389,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
+  if (q->debug) rc |= A(&q->dbg_etime, 5 * 4096 + 1);
   // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
   // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan

@@ -795,8 +795,12 @@ struct EmitV {
     uint32_t ridx = rbase + ((head + pos) & qmask);
     if (brec) {
       uint32_t b = rank_bin_r(key, *ps, ph, sbn);
-      uint32_t at = atomicAdd(&bcount[b], 1u);
-      atomicAdd(&bsize[b], ph == 0 ? 1u : 1u + run);
+      // one 64-bit atomic per record: the bin's record count in the low word,
+      // its group sizes in the high word (bcount: kNBR 8-byte counters)
+      const unsigned long long inc =
+          ((unsigned long long)(ph == 0 ? 1u : 1u + run) << 32) | 1ull;
+      const uint32_t at = (uint32_t)atomicAdd(
+          reinterpret_cast<unsigned long long*>(bcount) + b, inc);
       if (at < kBinCapR)
         brec[(size_t)b * kBinCapR + at] = BRecR{key, slot, pos, run, ridx};
       else
@@ -888,7 +892,7 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // priority pulls run, the P groups with key <= T_P from the post-R state.
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
 constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS)
-constexpr int kEmitStageThreads = 512;  // walkers with a staging slice
+constexpr int kEmitStageThreads = 512;  // walkers with a staging slice (all of a block)
 __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
@@ -923,27 +927,27 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
 // counters every block filled with memory-side atomics, read and cleared the
 // same way (atomicExch).  A rank bin past kBinCapR aborts the round
 // (overflow = 2): the host re-runs it on the radix path.
+template <int THREADS>
 __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
                            uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff) {
-  constexpr int per = kNBR / 1024;
-  __shared__ uint32_t wc[16], wz[16], wp[16];
+  constexpr int per = kNBR / THREADS;
+  constexpr int NW = THREADS / 64;
+  __shared__ uint32_t wc[NW], wz[NW], wp[NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
   // plain loads behind the last block's agent-scope acquire (the counters
   // were filled with memory-side atomics), cleared with plain stores for
   // the next round (written back at the kernel's end)
+  unsigned long long* bc64 = reinterpret_cast<unsigned long long*>(bcount);
 #pragma unroll
   for (int j = 0; j < per; ++j) {
-    const uint32_t b = t * per + j;
-    c[j] = bcount[b];
-    z[j] = bsize[b];
+    const unsigned long long v = bc64[t * per + j];
+    c[j] = (uint32_t)v;
+    z[j] = (uint32_t)(v >> 32);
   }
 #pragma unroll
-  for (int j = 0; j < per; ++j) {
-    const uint32_t b = t * per + j;
-    bcount[b] = 0;
-    bsize[b] = 0;
-  }
+  for (int j = 0; j < per; ++j) bc64[t * per + j] = 0ull;
+  (void)bsize;
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
     lc += c[j];
@@ -986,7 +990,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   }
   __syncthreads();
   uint32_t bc = 0, bz = 0, bp = 0, tc = 0, tz = 0, tp = 0;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NW; ++i) {
     if (i < w) {
       bc += wc[i];
       bz += wz[i];
@@ -1048,8 +1052,8 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   if (t == 0) {
     uint32_t m0 = 0, m1 = 0;
     unsigned long long S = 0;
-    for (int i = 0; i < 16; ++i) {
-      if (i < 8) m0 = wc[i] > m0 ? wc[i] : m0;  // threads 0..511: R bins
+    for (int i = 0; i < NW; ++i) {
+      if (i < NW / 2) m0 = wc[i] > m0 ? wc[i] : m0;  // the first half: R bins
       else m1 = wc[i] > m1 ? wc[i] : m1;
       S += ((unsigned long long)wp[i] << 32) | wz[i];
     }
@@ -1081,13 +1085,18 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
 constexpr int kEmitThreads = 1024;
-constexpr uint32_t kEmitChunk = kEmitThreads * 4;
+constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster,
+                             // and a slower last-block tail)
+constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
         const uint32_t* meta, CandRec* cand, BRecR* brec,
         uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
         uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
-        uint32_t* done) {
+        uint32_t* done, uint64_t* eclk = nullptr) {
+  // eclk (debug): per block [0] start [1] keys + table staged [2] candidates
+  // compacted [3] walks done [4] ticket taken
+  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
   __shared__ CandRec bl[kEmitChunk];
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
@@ -1099,23 +1108,30 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
   const uint32_t n = tb.n;
-  const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * 4;
+  const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
   const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t kr[4], kp[4];
-  uint32_t mt[4];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
-  if (s0 + 4 <= n) {
+  uint64_t kr[kEmitPer], kp[kEmitPer];
+  uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
+  if (s0 + kEmitPer <= n) {
     const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
     const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
-    ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
-    uint4 m4 = *reinterpret_cast<const uint4*>(meta + s0);
-    kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
-    kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
-    mt[0] = m4.x; mt[1] = m4.y; mt[2] = m4.z; mt[3] = m4.w;
+    const uint4* m4 = reinterpret_cast<const uint4*>(meta + s0);
+#pragma unroll
+    for (int j = 0; j < kEmitPer / 2; ++j) {
+      const ulonglong2 a = r2[j], c = p2[j];
+      kr[2 * j] = a.x; kr[2 * j + 1] = a.y;
+      kp[2 * j] = c.x; kp[2 * j + 1] = c.y;
+    }
+#pragma unroll
+    for (int j = 0; j < kEmitPer / 4; ++j) {
+      const uint4 m = m4[j];
+      mt[4 * j] = m.x; mt[4 * j + 1] = m.y; mt[4 * j + 2] = m.z; mt[4 * j + 3] = m.w;
+    }
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < kEmitPer; ++j) {
       bool in = s0 + j < n;
       kr[j] = in ? keyr[s0 + j] : kMaxKey;
       kp[j] = in ? keyp[s0 + j] : kMaxKey;
@@ -1126,24 +1142,21 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   if (brec)
     for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
   __syncthreads();  // s_cnt zeroed before any wave adds to it
-  uint8_t f[4];
+  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
+  uint8_t f[kEmitPer];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) f[j] = (uint8_t)(mt[j] >> 8);
+  for (int j = 0; j < kEmitPer; ++j) f[j] = (uint8_t)(mt[j] >> 8);
   uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < kEmitPer; ++j) {
     if (s0 + j >= n) continue;
     const bool cr = pred.TR && kr[j] <= pred.TR;
     const bool cp = pred.TP && kp[j] <= pred.TP;
-    if (cr || cp) {
-      bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
-    } else if (f[j] & F_PMARK) {
-      tb.sc[s0 + j].flags = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
-    }
+    if (cr || cp) bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
   }
   uint32_t cnt = 0, nr = 0, np = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < kEmitPer; ++j) {
     cnt += ((bits >> (2 * j)) & 3u) ? 1u : 0u;
     nr += (bits >> (2 * j)) & 1u;
     np += (bits >> (2 * j + 1)) & 1u;
@@ -1176,31 +1189,46 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   {
     uint32_t o = wbase + incl - cnt;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < kEmitPer; ++j) {
       const uint32_t b = (bits >> (2 * j)) & 3u;
       if (b)
         bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), (uint8_t)mt[j],
                           (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
     }
   }
-  if (threadIdx.x == 0) {
-    s_tot = btot;
-    s_base = btot ? atomicAdd(&rd->n_cand, btot) : 0;
-  }
+  if (threadIdx.x == 0) s_tot = btot;
   __syncthreads();
-  if (sampled && threadIdx.x == 0) {
-    uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kShards);
-    if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
-    if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
+  // The block's segment of the candidate list is allocated (a same-address
+  // atomic, serialised over the grid) and the sampled counts published by
+  // the last wave, which rarely walks, while the walks run: on gfx950 a
+  // wave's load waits also wait for its earlier memory operations.
+  constexpr uint32_t kAllocT = kEmitThreads - 64;
+  uint32_t abase = 0;
+  if (threadIdx.x == kAllocT) {
+    if (btot) abase = atomicAdd(&rd->n_cand, btot);
+    if (sampled) {
+      uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kShards);
+      if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
+      if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
+    }
   }
-  const uint32_t base = s_base, tot = s_tot;
-  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
-    const CandRec c = bl[i];
-    cand[base + i] = c;
-    emit_one(tb, rd, c, brec, bcount, bsize, ltab, dense, dcap,
+  const uint32_t tot = s_tot;
+  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 2] = wall_clock64();
+  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads)
+    emit_one(tb, rd, bl[i], brec, bcount, bsize, ltab, dense, dcap,
              threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
                                                        : nullptr);
-  }
+  if (threadIdx.x == kAllocT) s_base = abase;
+  __syncthreads();
+  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 3] = wall_clock64();
+  // the block's candidates, copied from LDS in one coalesced pass
+  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) cand[s_base + i] = bl[i];
+  // non-candidates settle their pending limit-scan marks (after the walks:
+  // a store ahead of a walk's loads would delay them)
+#pragma unroll
+  for (int j = 0; j < kEmitPer; ++j)
+    if (s0 + j < n && !((bits >> (2 * j)) & 3u) && (f[j] & F_PMARK))
+      tb.sc[s0 + j].flags = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
   if (!brec) return;
   // ticket: the block's bin atomics have completed (every wave waits for its
   // own) before one lane takes it; the last block computes the prefixes.
@@ -1209,6 +1237,7 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) {
@@ -1221,7 +1250,8 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[4] = wall_clock64();
 #endif
-  bin_prefix(rd, bcount, bsize, bcnt, bsoff, bpoff);
+  bin_prefix<kEmitThreads>(rd, bcount, bsize, bcnt, bsoff, bpoff);
+  if (eclk && threadIdx.x == 0) eclk[5 * gridDim.x] = wall_clock64();
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[5] = wall_clock64();
 #endif
