@@ -201,6 +201,30 @@ def test_full_size_parity_1m_clients():
     assert n > 1_000_000
 
 
+def test_full_size_parity_1m_clients_delayed():
+    """The same at full size with DelayedTagCalc (the Ceph configuration:
+    tags computed at pop time, update_next_tag :1021-1036, front-only
+    reductions): 1,048,576 clients, every decision and add status
+    bit-exact, the trace tie-free."""
+    tr = bench_shaped_trace(42, 1 << 20, 2, 1 << 16, depth=2)
+    n, qg, qo = run_parity(tr, mk_variant("default"),
+                           dict(at_limit=AT_LIMIT_WAIT, delayed=True), state_sample=4096)
+    assert n > 1_000_000
+
+
+def test_dynamic_info_rounds_64k():
+    """U1 through batched rounds at 65,536 clients: 20 % of the clients get a
+    fresh ClientInfo before every pull (published with
+    dmc_client_bind_info_batch), delayed tags, pulls of 4096 -- every
+    decision and every client's cached inverses bit-exact."""
+    from dmclock_amd import workloads as wl
+    tr = wl.dynamic_trace(7, 1 << 16, 4, 1 << 12, k_choices=(1 << 12,), depth=2)
+    n, qg, qo = run_parity(tr, mk_gpu, dict(delayed=True, dynamic_info=True),
+                           state_sample=4096, gpu_kw=dict(info_callback=False), info=True)
+    assert n > 10_000, n
+    assert qg.counters()["rounds"] >= 4
+
+
 # ------------------------------------------------ batched activations
 MODES_ACT = [dict(at_limit=AT_LIMIT_WAIT), dict(at_limit=AT_LIMIT_WAIT, delayed=True),
              dict(at_limit=AT_LIMIT_ALLOW)]
