@@ -2217,6 +2217,25 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
                      v[nb / 2], v[nb - 1]);
       }
       std::fprintf(stderr, "emit clock tail end: %.2f us\n", (e[5ull * nb] - t0) / 100.0);
+      // per candidate: staging and walk durations
+      std::vector<uint64_t> ck(4ull * nb * 512);
+      (void)hipMemcpy(ck.data(), q->dbg_etime + 5 * 4096 + 8, 8ull * ck.size(),
+                      hipMemcpyDeviceToHost);
+      (void)hipMemset(q->dbg_etime + 5 * 4096 + 8, 0, 8ull * ck.size());
+      std::vector<double> a, b, st;
+      for (size_t i = 0; i < ck.size() / 4; ++i) {
+        if (!ck[4 * i]) continue;
+        a.push_back((ck[4 * i + 1] - ck[4 * i]) / 100.0);
+        b.push_back((ck[4 * i + 2] - ck[4 * i + 1]) / 100.0);
+        st.push_back((ck[4 * i] - t0) / 100.0);
+      }
+      std::sort(a.begin(), a.end());
+      std::sort(b.begin(), b.end());
+      std::sort(st.begin(), st.end());
+      if (!a.empty())
+        std::fprintf(stderr, "emit cand (%zu): start p50 %.2f | stage p50 %.2f p90 %.2f | walk+records p50 %.2f p90 %.2f us\n",
+                     a.size(), st[st.size() / 2], a[a.size() / 2], a[a.size() * 9 / 10],
+                     b[b.size() / 2], b[b.size() * 9 / 10]);
     }
     if (q->debug)
       std::fprintf(stderr,
@@ -2389,7 +2408,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
-  if (q->debug) rc |= A(&q->dbg_etime, 5 * 4096 + 1);
+  if (q->debug) rc |= A(&q->dbg_etime, 5 * 4096 + 8 + 4 * 4096 * 512);
   // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
   // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan

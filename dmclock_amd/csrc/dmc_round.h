@@ -891,12 +891,15 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // One candidate's entries: R pops with r <= min(now, T_R); then, if the
 // priority pulls run, the P groups with key <= T_P from the post-R state.
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
-constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS)
+constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2: no faster)
 constexpr int kEmitStageThreads = 512;  // walkers with a staging slice (all of a block)
 __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
-                                ReqEntry* st) {
+                                ReqEntry* st, uint64_t* ck = nullptr) {
+  // ck (debug): [0] entry, [1] client record and ring staged, [2] walks and
+  // their rank records done
+  if (ck) ck[0] = wall_clock64();
   const uint32_t s = c.slot;
   const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
   const double now = rd->now;
@@ -905,6 +908,11 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
   const CView cv = cand_view(tb, c);
   const uint32_t h = cv.h;
   const RingView rv = stage_ring<kEmitStage>(tb, s, h, cv.c, st);
+  if (ck) {
+    keep(cv.rinv);
+    keep(cv.pd);
+    ck[1] = wall_clock64();
+  }
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask};
@@ -918,6 +926,10 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
             s * tb.q, h, tb.qmask};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
+  }
+  if (ck) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ck[2] = wall_clock64();
   }
 }
 
@@ -1217,7 +1229,8 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads)
     emit_one(tb, rd, bl[i], brec, bcount, bsize, ltab, dense, dcap,
              threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
-                                                       : nullptr);
+                                                       : nullptr,
+             eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
   if (threadIdx.x == kAllocT) s_base = abase;
   __syncthreads();
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 3] = wall_clock64();
