@@ -28,6 +28,24 @@ CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
 STREAMING = {"scan", "select", "future"}
 
 
+def calib_rates(stats_csv, out):
+    """add each pattern's measured rate (rocprofv3 --stats of fetch_calib):
+    GB/s of its known bytes and 64-B memory requests per second"""
+    names = {"stream16": "stream16(", "rand64": "rand_rec<4>", "rand32": "rand_rec<2>",
+             "rand16": "rand16(", "rand8": "rand8("}
+    for r in csv.DictReader(open(stats_csv)):
+        for k, pat in names.items():
+            if pat in r["Name"] and k in out:
+                ns = float(r["AverageNs"])
+                if k == "stream16" and int(r["Calls"]) > 3:
+                    continue  # the evict passes share the name
+                out[k]["avg_ns"] = ns
+                out[k]["GBps"] = round(out[k]["known_bytes"] / ns, 1)
+                req = out[k]["fetch_size_bytes"] / 64.0
+                out[k]["requests_per_s"] = round(req / (ns * 1e-9))
+    return out
+
+
 def calibrate(fetch_csv, known_json):
     """bytes-per-FETCH_SIZE-byte factors from tools/fetch_calib: per
     repetition six stream16 dispatches (the 2nd is the measured 512 MiB, the
@@ -78,9 +96,13 @@ def main():
     ap.add_argument("--calib", default=None,
                     help="tools/fetch_calib FETCH_SIZE csv (with --known): print factors")
     ap.add_argument("--known", default=None)
+    ap.add_argument("--calib-stats", default=None,
+                    help="rocprofv3 --stats csv of the same calibration run: rates")
     a = ap.parse_args()
     if a.calib:
         out = calibrate(a.calib, a.known)
+        if a.calib_stats:
+            out = calib_rates(a.calib_stats, out)
         json.dump(out, open(a.out, "w"), indent=1)
         for k, v in out.items():
             print(k, v)
