@@ -944,9 +944,9 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
                            uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff) {
   constexpr int per = kNBR / THREADS;
   constexpr int NW = THREADS / 64;
-  __shared__ uint32_t wc[NW], wz[NW], wp[NW];
+  __shared__ uint32_t wc[NW], wz[NW], wp[NW], wm[NW];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0;
+  uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0, lm = 0;
   // plain loads behind the last block's agent-scope acquire (the counters
   // were filled with memory-side atomics), cleared with plain stores for
   // the next round (written back at the kernel's end)
@@ -965,6 +965,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     lc += c[j];
     lz += z[j];
     lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
+    lm = c[j] > lm ? c[j] : lm;  // a thread's bins are all R or all P
   }
   bool ovf = rd->bin_ovf != 0;
   bool bad_sample = false;
@@ -986,25 +987,29 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[9] = wall_clock64();
 #endif
-  uint32_t ic = lc, iz = lz, ip = lp;
+  // one pass of wave scans: record counts, group sizes, P groups (sums) and
+  // the largest bin (max); lane 63 holds the wave totals
+  uint32_t ic = lc, iz = lz, ip = lp, im = lm;
   for (int d = 1; d < 64; d <<= 1) {
-    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d);
+    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d),
+             om = __shfl_up(im, d);
     if (lane >= d) {
       ic += oc;
       iz += oz;
       ip += op;
+      im = om > im ? om : im;
     }
   }
   if (lane == 63) {
     wc[w] = ic;
     wz[w] = iz;
     wp[w] = ip;
+    wm[w] = im;
   }
   __syncthreads();
-  uint32_t bc = 0, bz = 0, bp = 0, tc = 0, tz = 0, tp = 0;
+  uint32_t bz = 0, bp = 0, tc = 0, tz = 0, tp = 0;
   for (int i = 0; i < NW; ++i) {
     if (i < w) {
-      bc += wc[i];
       bz += wz[i];
       bp += wp[i];
     }
@@ -1032,7 +1037,6 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   if (threadIdx.x == 0) rd->tdbg[10] = wall_clock64();
 #endif
   uint32_t oz = bz + iz - lz, op = bp + ip - lp;
-  (void)bc;
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
     bcnt[b] = c[j];
@@ -1041,40 +1045,20 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     oz += z[j];
     if (b >= (uint32_t)kNBPhase) op += c[j];
   }
-  // diagnostics: largest bin per phase, sum of squared bin counts (the rank
-  // pass's work), reduced through the wave partial slots
-  uint32_t mx = 0;
-  unsigned long long sq = 0;
-  for (int j = 0; j < per; ++j) {
-    mx = c[j] > mx ? c[j] : mx;
-    sq += (unsigned long long)c[j] * c[j];
-  }
-  for (int d = 32; d > 0; d >>= 1) {
-    uint32_t o = __shfl_down(mx, d);
-    mx = o > mx ? o : mx;
-    sq += shfl_down_u64r(sq, d);
-  }
-  __syncthreads();
-  if (lane == 0) {
-    wc[w] = mx;
-    wz[w] = (uint32_t)sq;
-    wp[w] = (uint32_t)(sq >> 32);
-  }
-  __syncthreads();
   if (t == 0) {
+    // the largest bin per phase (diagnostics): the first half of the waves
+    // holds the R bins
     uint32_t m0 = 0, m1 = 0;
-    unsigned long long S = 0;
     for (int i = 0; i < NW; ++i) {
-      if (i < NW / 2) m0 = wc[i] > m0 ? wc[i] : m0;  // the first half: R bins
-      else m1 = wc[i] > m1 ? wc[i] : m1;
-      S += ((unsigned long long)wp[i] << 32) | wz[i];
+      if (i < NW / 2) m0 = wm[i] > m0 ? wm[i] : m0;
+      else m1 = wm[i] > m1 ? wm[i] : m1;
     }
 #ifdef DMC_TAIL_TIMING
     rd->tdbg[11] = wall_clock64();
 #endif
     rd->bin_max[0] = m0;
     rd->bin_max[1] = m1;
-    rd->bin_sq = S;
+    rd->bin_sq = 0;  // (not computed)
     const uint32_t k = rd->k_total;
     rd->n_dec = tz < k ? tz : k;
     rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
