@@ -34,10 +34,6 @@
 
 using namespace dmc;
 
-#ifndef DMC_WALK_GRID_CAP
-#define DMC_WALK_GRID_CAP 1024
-#endif
-
 namespace {
 
 constexpr int kBlock = 256;
@@ -1114,7 +1110,11 @@ struct dmc_queue {
   uint32_t n_idle = 0;
   uint64_t tick = 0;
   // device scratch
-  CandRec* cand = nullptr;    // N: candidates of the round (k_remit)
+  CandRec* cand = nullptr;    // N (rounded up to emit blocks): candidates of the
+                              // round, kEmitChunk per k_remit block
+  uint32_t* bcand = nullptr;  // per k_remit block: its candidates
+  PostRec* post = nullptr;    // per candidate: a fast candidate's state after its pop
+  uint32_t* decof = nullptr;  // per candidate: kSlowCand, kNoDec or its decision offset
   uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
   uint32_t* meta = nullptr;   // N: k_rscan's per-slot R-prefix length, flags, head, count
   RoundPart* rparts = nullptr; // k_rscan's per-block partials
@@ -1979,9 +1979,8 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
-  // walking kernels: grid-stride over the candidate list, sized so that
-  // a typical round's candidates are resident at once
-  uint32_t gW = std::min<uint32_t>((N + kBlockR - 1) / kBlockR, DMC_WALK_GRID_CAP);
+  // k_remit blocks (kEmitChunk slots each); k_rapply takes two per emit block
+  const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
   klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb, q->keyr,
           q->keyp, q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
           sampled ? q->skp : nullptr);
@@ -1994,10 +1993,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
             gN, q->rd, q->hist, q->sbn, q->hist_done, 0);
-  klaunch(q, DMC_PROF_EMIT, k_remit, dim3((N + kEmitChunk - 1) / kEmitChunk),
+  klaunch(q, DMC_PROF_EMIT, k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint64_t*)q->keyr,
-          (const uint64_t*)q->keyp, (const uint32_t*)q->meta, q->cand,
-          radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
+          (const uint64_t*)q->keyp, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
+          q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
           q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
           q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
@@ -2006,7 +2005,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                            hipMemcpyDeviceToDevice, q->stream);
     klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
             (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
-            (const BRecR*)q->brec, tb.ring, q->debug ? q->dbg_wtime : nullptr);
+            (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
   } else {
     uint32_t E = q->ecap;
     uint32_t gE = grid_for(E, 1024);
@@ -2037,8 +2036,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                        (const uint32_t*)q->gpoff, tb.ring);
     pe(q);
   }
-  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(gW), dim3(kBlockR), 0, tb, q->rd,
-          (const CandRec*)q->cand, q->sched, q->debug ? q->dbg_atime : nullptr);
+  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(2 * gEm), dim3(kBlockR), 0, tb, q->rd,
+          (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
+          (const PostRec*)q->post, q->sched, q->debug ? q->dbg_atime : nullptr);
   if (future)
     launch_future(q);  // its decide kernel ends the round
   else
@@ -2242,13 +2242,14 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
                    "dmc round: k=%u n_r=%llu p_runs=%u cand=%u R(elig=%u T=%s) "
                    "P(elig=%u) dec=%u prio=%u bins max R %u P %u sumsq %llu "
                    "ovf=%u radix=%d dense=%u pgroups=%u P keys [%.9g, %.9g] T %.9g "
-                   "now %.9g\n",
+                   "now %.9g fast %u multi %u run %u slow %u\n",
                    kk, (unsigned long long)c.n_r, c.p_runs, c.n_cand,
                    c.ph[0].n_elig, c.ph[0].T == kMaxKey - 1 ? "all" : "thr",
                    c.ph[1].n_elig, c.n_dec, c.n_prio, c.bin_max[0], c.bin_max[1],
                    c.bin_sq, c.overflow, (int)radix, c.dense_n, c.n_pgroups,
                    from_okey(c.ph[1].kmin), from_okey(c.ph[1].kmax),
-                   c.ph[1].T ? from_okey(c.ph[1].T) : 0.0, c.now);
+                   c.ph[1].T ? from_okey(c.ph[1].T) : 0.0, c.now, c.ecnt[0], c.ecnt[1],
+                   c.ecnt[2], c.ecnt[3]);
     ++q->ctr.rounds;
     if (radix) ++q->ctr.radix_rounds;
     if (!radix && c.bin_max[0] > q->ctr.max_bin) q->ctr.max_bin = c.bin_max[0];
@@ -2384,7 +2385,13 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->binfo, N);
   t.binfo = p.dynamic_info ? q->binfo : nullptr;
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
-  rc |= A(&q->cand, N);
+  {
+    const size_t nb = (N + kEmitChunk - 1) / kEmitChunk, nc = nb * kEmitChunk;
+    rc |= A(&q->cand, nc);
+    rc |= A(&q->bcand, nb);
+    rc |= A(&q->post, nc);
+    rc |= A(&q->decof, nc);
+  }
   rc |= A(&q->keyr, N);
   rc |= A(&q->keyp, N);
   rc |= A(&q->meta, N);
@@ -2457,7 +2464,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   Table& t = q->tb;
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
-                  q->cand, q->keyr, q->keyp, q->meta, q->hist, q->sbn,
+                  q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->meta, q->hist, q->sbn,
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,

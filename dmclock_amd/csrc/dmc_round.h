@@ -111,6 +111,8 @@ struct Round {
   uint32_t ccnt[2 * kShards];  // sampled rounds: first keys at or below T, per
                                // phase, in XCD shards (k_remit)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
+  uint32_t ecnt[4];      // diagnostics: candidates fast / several records /
+                         // one P group with a run / other slow (k_remit)
   unsigned long long bin_sq;  // diagnostics: sum of squared bin counts
   RoundPart tot;         // reduced scan partials (k_rreduce)
   // diagnostics (DMC_TAIL_TIMING builds): wall clocks of the kernels with a
@@ -760,13 +762,51 @@ __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
 // queue position), the group's run (P) and the entry's ring index.  The
 // decision offset and tie flag are written into the ring entry itself
 // (ReqEntry::dec / ::tie), where k_rapply's walk reads them.
-struct BRecR {
+struct BKey {
   uint64_t okey;
   uint32_t slot;
   uint32_t seq;
   uint32_t run;
   uint32_t ridx;  // slot * q + ring index
 };
+
+// The record as k_remit writes it (one 64-byte line): the order key, then
+// the candidate index and, for a *fast* record (kFastRec: its candidate's
+// only record, a single pop at queue position 0, immediate mode), the pop's
+// decision payload, which k_rrank writes straight to the decision array; a
+// slow record's pop is stamped into its ring entry for k_rapply's re-walk.
+constexpr uint32_t kFastRec = 0x80000000u;
+struct BRecR {
+  BKey k;
+  uint32_t ci;  // candidate index | kFastRec
+  uint32_t cost;
+  uint64_t handle;
+  double r, p, l;
+};
+static_assert(sizeof(BRecR) == 64, "BRecR must be one 64-byte line");
+
+// A fast candidate's state after its pops (k_remit computes it from the
+// walk; k_rapply stores it iff k_rrank dispatched the whole group): the new
+// front's keys, the reduced prev r and the reduction offset (priority pop),
+// queue position 2's reduced r (no run); and, for a priority pop followed by
+// a one-pop reservation run, that pop's decision payload (second line).
+// decof[ci]: kSlowCand (re-walk), kNoDec (not dispatched) or the first
+// pop's decision offset.
+constexpr uint32_t kSlowCand = 0xfffffffeu;
+struct PostRec {
+  double fr, fpk, fl;  // new front r, p + prop_delta, l (queue position 1 + run)
+  double prev_r;       // prev r after the pop's reduction
+  double off;          // reduce_reservation_tags offset (priority pop)
+  double r2;           // queue position 2's reduced r (run 0)
+  uint32_t bits;       // 1: priority pop, 2: the new front's l <= now, 4: run of one
+  uint32_t pad[3];
+  // the run's pop (queue position 1), bits & 4
+  uint64_t handle1;
+  double r1, p1, l1;
+  uint32_t cost1;
+  uint32_t pad1[7];
+};
+static_assert(sizeof(PostRec) == 128, "PostRec must be two 64-byte lines");
 
 // Dense entry (radix path).
 struct DEnt {
@@ -775,6 +815,21 @@ struct DEnt {
   uint32_t seq;   // queue position | phase << 31
   uint32_t run;
   uint32_t ridx;  // slot * q + ring index
+};
+
+// What a candidate's walks emitted: its record count, the first record
+// (held back until the walks end, when it is known whether the candidate is
+// fast) and its first pop.
+// (A fast candidate's pop is queue position 0, whose staged entry holds its
+// decision payload: nothing of it is kept in registers through the walks.)
+struct EmitAcc {
+  uint32_t ci;
+  uint32_t nrec = 0, npops = 0;
+  uint32_t b0 = 0, at0 = kBinCapR;  // the first record's bin and place
+  uint64_t key0 = 0;                // its key
+  uint32_t run0 = 0;                // its run (P group)
+  uint32_t pos0 = 0;                // the first pop's queue position
+  bool prio0 = false;               // ... and kind
 };
 
 struct EmitV {
@@ -791,6 +846,7 @@ struct EmitV {
   DEnt* dense;
   uint32_t dcap;
   uint32_t rbase, head, qmask;  // ring index of queue position i
+  EmitAcc* acc;
   __device__ void put(uint64_t key, uint32_t pos, uint32_t run) {
     uint32_t ridx = rbase + ((head + pos) & qmask);
     if (brec) {
@@ -801,10 +857,19 @@ struct EmitV {
           ((unsigned long long)(ph == 0 ? 1u : 1u + run) << 32) | 1ull;
       const uint32_t at = (uint32_t)atomicAdd(
           reinterpret_cast<unsigned long long*>(bcount) + b, inc);
-      if (at < kBinCapR)
-        brec[(size_t)b * kBinCapR + at] = BRecR{key, slot, pos, run, ridx};
-      else
+      if (at >= kBinCapR) {
         atomicOr(&rd->bin_ovf, 1u);  // read by the last block (memory side)
+      } else if (acc->nrec == 0) {
+        acc->b0 = b;  // written by emit_one once the walks have ended
+        acc->at0 = at;
+        acc->key0 = key;
+        acc->run0 = run;
+      } else {
+        // a second record: the candidate is slow (both go out now)
+        if (acc->nrec == 1 && acc->at0 < kBinCapR) first_slow();
+        brec[(size_t)b * kBinCapR + at] = BRecR{BKey{key, slot, pos, run, ridx}, acc->ci};
+      }
+      ++acc->nrec;
     } else {
       // wave-aggregated: one counter add and one max per phase per wave
       // (massively tied rounds emit every entry here; per-entry atomics on
@@ -831,9 +896,21 @@ struct EmitV {
       if (at < dcap) dense[at] = DEnt{key, slot, pos | ((uint32_t)ph << 31), run, ridx};
     }
   }
+  // the held-back first record, written as a slow one (its queue position
+  // is the first pop's)
+  __device__ void first_slow() {
+    brec[(size_t)acc->b0 * kBinCapR + acc->at0] =
+        BRecR{BKey{acc->key0, slot, acc->pos0, acc->run0,
+                   rbase + ((head + acc->pos0) & qmask)},
+              acc->ci};
+  }
   uint32_t gpos = 0;
   __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, bool prio,
                       uint32_t, uint32_t) {
+    if (acc->npops++ == 0) {
+      acc->pos0 = i;
+      acc->prio0 = prio;
+    }
     if (ph == 0) put(okey(t.r), i, 0);
     else if (prio) gpos = i;
   }
@@ -893,9 +970,10 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
 constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2: no faster)
 constexpr int kEmitStageThreads = 512;  // walkers with a staging slice (all of a block)
-__device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
-                                BRecR* brec, uint32_t* bcount, uint32_t* bsize,
+__device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c,
+                                uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
+                                PostRec* post, uint32_t* decof,
                                 ReqEntry* st, uint64_t* ck = nullptr) {
   // ck (debug): [0] entry, [1] client record and ring staged, [2] walks and
   // their rank records done
@@ -906,6 +984,7 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
   Tag3 pf;
   uint32_t fc;
   const CView cv = cand_view(tb, c);
+  const double prev_r = tb.rec[s].prev_r;  // (the inverses' line)
   const uint32_t h = cv.h;
   const RingView rv = stage_ring<kEmitStage>(tb, s, h, cv.c, st);
   if (ck) {
@@ -913,9 +992,11 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
     keep(cv.pd);
     ck[1] = wall_clock64();
   }
+  EmitAcc acc;
+  acc.ci = ci;
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
-            s * tb.q, h, tb.qmask};
+            s * tb.q, h, tb.qmask, &acc};
     walk_r(tb, rv, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
   if (c.cp()) {
@@ -923,14 +1004,73 @@ __device__ inline void emit_one(const Table& tb, Round* rd, const CandRec& c,
     const uint32_t m = c.m;
     bool ready0 = m == 0 && (c.f() & F_READY);
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
-            s * tb.q, h, tb.qmask};
+            s * tb.q, h, tb.qmask, &acc};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0);
+  }
+  // Fast candidate: one record at queue position 0 in immediate mode -- one
+  // reservation pop, or a priority pop with a reservation run of at most one
+  // pop.  Its first decision goes out with its record (k_rrank writes it);
+  // its state after the group (apply_one's arithmetic for that case) and the
+  // run's decision are stored here.
+  const uint32_t run = acc.npops - 1;  // (a one-record candidate: its group's run)
+  const bool fast = brec && !tb.delayed && acc.nrec == 1 && acc.pos0 == 0 &&
+                    acc.at0 < kBinCapR && (run == 0 || (run == 1 && acc.prio0));
+  if (fast) {
+    PostRec pr;
+    const uint32_t cc = cv.c;
+    const bool prio = acc.prio0;
+    // the pop's payload: queue position 0 as stored (immediate mode: a
+    // priority pop with no earlier one has its stored r)
+    const ReqEntry e0 = rv.at(0);
+    const double off = prio ? resv_offset(cv.rinv, e0.cost, e0.rho) : 0.0;
+    pr.fr = pr.fpk = pr.fl = pr.r2 = 0.0;
+    pr.bits = (prio ? 1u : 0u) | (run ? 4u : 0u);
+    if (run) {
+      // the run's pop: queue position 1 with its reduced r (its decision tag)
+      const ReqEntry e1 = rv.at(1);
+      pr.handle1 = e1.handle;
+      pr.r1 = __dsub_rn(e1.r, off);
+      pr.p1 = e1.p;
+      pr.l1 = e1.l;
+      pr.cost1 = e1.cost;
+    }
+    if (cc >= 2 + run) {
+      const ReqEntry ef = rv.at(1 + run);  // staged: 1 + run < kEmitStage
+      pr.fr = prio ? __dsub_rn(ef.r, off) : ef.r;
+      pr.fpk = __dadd_rn(ef.p, cv.pd);
+      pr.fl = ef.l;
+      if (ef.l <= now) pr.bits |= 2u;
+    }
+    if (prio && !run && cc >= 3) pr.r2 = __dsub_rn(rv.r_at(2), off);
+    pr.prev_r = prio ? __dsub_rn(prev_r, off) : prev_r;
+    pr.off = off;
+    pr.pad[0] = pr.pad[1] = pr.pad[2] = 0;
+    brec[(size_t)acc.b0 * kBinCapR + acc.at0] =
+        BRecR{BKey{acc.key0, s, 0u, run, s * tb.q + h}, ci | kFastRec, e0.cost, e0.handle,
+              e0.r, e0.p, e0.l};
+    {
+      // the second line only with a run
+      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&pr);
+      ulonglong2* dst = reinterpret_cast<ulonglong2*>(post + ci);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < 4 || run) dst[j] = src[j];
+    }
+    decof[ci] = kNoDec;
+  } else {
+    if (brec && acc.nrec == 1 && acc.at0 < kBinCapR) {
+      EmitV v{0, s, nullptr, brec, bcount, bsize, sbn, rd, dense, dcap, s * tb.q, h,
+              tb.qmask, &acc};
+      v.first_slow();
+    }
+    decof[ci] = kSlowCand;
   }
   if (ck) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ck[2] = wall_clock64();
   }
+  return fast ? 0u : acc.nrec > 1 ? 1u : acc.npops > 1 ? 2u : 3u;
 }
 
 // Exclusive prefixes over the rank bins of the record counts, the group
@@ -1086,7 +1226,8 @@ constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no f
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
-        const uint32_t* meta, CandRec* cand, BRecR* brec,
+        const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
+        uint32_t* decof, BRecR* brec,
         uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
         uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
         uint32_t* done, uint64_t* eclk = nullptr) {
@@ -1097,9 +1238,10 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
   __shared__ uint32_t wsum[kEmitThreads / 64];
-  __shared__ uint32_t s_base, s_tot, s_last;
-  __shared__ uint32_t s_cnt[2];
+  __shared__ uint32_t s_tot, s_last;
+  __shared__ uint32_t s_cnt[2], s_ec[4];
   if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
+  if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
@@ -1194,14 +1336,14 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   }
   if (threadIdx.x == 0) s_tot = btot;
   __syncthreads();
-  // The block's segment of the candidate list is allocated (a same-address
-  // atomic, serialised over the grid) and the sampled counts published by
-  // the last wave, which rarely walks, while the walks run: on gfx950 a
-  // wave's load waits also wait for its earlier memory operations.
+  // The candidate count (a statistic) and the sampled counts are published
+  // (same-address atomics, serialised over the grid) by the last wave, which
+  // rarely walks, while the walks run: on gfx950 a wave's load waits also
+  // wait for its earlier memory operations.
   constexpr uint32_t kAllocT = kEmitThreads - 64;
-  uint32_t abase = 0;
   if (threadIdx.x == kAllocT) {
-    if (btot) abase = atomicAdd(&rd->n_cand, btot);
+    // (the total is a statistic: the candidate arrays are per block)
+    if (btot) atomicAdd(&rd->n_cand, btot);
     if (sampled) {
       uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kShards);
       if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
@@ -1210,16 +1352,23 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   }
   const uint32_t tot = s_tot;
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 2] = wall_clock64();
-  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads)
-    emit_one(tb, rd, bl[i], brec, bcount, bsize, ltab, dense, dcap,
-             threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
-                                                       : nullptr,
-             eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
-  if (threadIdx.x == kAllocT) s_base = abase;
+  // candidate index: the block's segment of the candidate arrays (kEmitChunk
+  // per block; k_rapply's blocks take their emit block's segment)
+  const uint32_t cbase = blockIdx.x * kEmitChunk;
+  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
+    const uint32_t cat = emit_one(
+        tb, rd, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
+        threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
+                                                  : nullptr,
+        eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
+    atomicAdd(&s_ec[cat], 1u);
+  }
   __syncthreads();
+  if (threadIdx.x < 4 && s_ec[threadIdx.x]) atomicAdd(&rd->ecnt[threadIdx.x], s_ec[threadIdx.x]);
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 3] = wall_clock64();
   // the block's candidates, copied from LDS in one coalesced pass
-  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) cand[s_base + i] = bl[i];
+  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) cand[cbase + i] = bl[i];
+  if (threadIdx.x == 0) bcand[blockIdx.x] = tot;
   // non-candidates settle their pending limit-scan marks (after the walks:
   // a store ahead of a walk's loads would delay them)
 #pragma unroll
@@ -1258,27 +1407,41 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
 // One block per rank bin ranks it in LDS by (okey, slot, position); R bins
 // precede P bins, so the decision offset of an entry is the sum of the group
 // sizes (1 for R pops, 1 + run for P groups) of all earlier bins (bin_prefix)
-// plus those of its own bin that precede it.  Decides: entry ids slot * q +
-// position get their decision offset and tie flag, stamped into the ring
-// entry (the priority pop's entry for a P group).
+// plus those of its own bin that precede it.  Decides: a fast record's
+// decision is written (and its offset recorded for k_rapply); a slow record's
+// entry (slot * q + position) gets its decision offset and tie flag stamped
+// into the ring entry (the priority pop's entry for a P group).
 
 // Rank of record i of a bin among all `cnt` of them, compared in `parts`
 // slices of `per` records by adjacent lanes whose counts are summed by
-// shuffles; lanes with i >= cnt take part in the shuffles only.  Decides:
-// the entry's decision offset and tie flag stamped into its ring entry.
-__device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
+// shuffles; lanes with i >= cnt take part in the shuffles only.
+__device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
                                 uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, bool isp, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
-                                ReqEntry* ring) {
+                                ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
   const bool valid = i < cnt;
-  BRecR me = sh[valid ? i : 0];
+  BKey me = sh[valid ? i : 0];
+  // the writer lane's payload (an L2 hit: the block staged the line), in
+  // flight during the comparisons
+  uint32_t ci = 0, cost = 0;
+  uint64_t handle = 0;
+  double tr = 0.0, tp = 0.0, tl = 0.0;
+  if (valid && part == 0) {
+    const BRecR& x = src[i];
+    ci = x.ci;
+    cost = x.cost;
+    handle = x.handle;
+    tr = x.r;
+    tp = x.p;
+    tl = x.l;
+  }
   uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
   if (!valid) f1 = f0;
   uint32_t rank = 0, gl = 0, tie = 0;
 #pragma unroll 4
   for (uint32_t f = f0; f < f1; ++f) {
-    const BRecR o = sh[f];
+    const BKey o = sh[f];
     uint32_t eqk = o.okey == me.okey;
     uint32_t less = (uint32_t)(o.okey < me.okey) |
                     (eqk & ((uint32_t)(o.slot < me.slot) |
@@ -1296,8 +1459,29 @@ __device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
     uint32_t goff = soff + gl;
     uint32_t size = isp ? 1u + me.run : 1u;
     if (goff < k) {
-      ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
-      ring[me.ridx].tie = tie;
+      if ((ci & kFastRec) && goff + size > k) {
+        // a fast group cut by the round's end: k_rapply re-walks it
+        ring[me.ridx].dec = goff;
+        ring[me.ridx].tie = tie;
+        decof[ci & ~kFastRec] = kSlowCand;
+      } else if (ci & kFastRec) {
+        // a fast record: its first pop's decision, and its offset for
+        // k_rapply (which writes the run's pop)
+        dmc_decision d;
+        d.handle = handle;
+        d.tag_r = tr;
+        d.tag_p = tp;
+        d.tag_l = tl;
+        d.slot = me.slot;
+        d.cost = cost;
+        d.phase = isp ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+        d.flags = tie;
+        out[goff] = d;
+        decof[ci & ~kFastRec] = goff;
+      } else {
+        ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
+        ring[me.ridx].tie = tie;
+      }
       if (isp) {
         uint32_t prank = poff + rank;  // among P groups
         if (goff + size >= k || prank == n_pgroups - 1) {
@@ -1311,46 +1495,42 @@ __device__ inline void rank_rec(Round* rd, const BRecR* sh, uint32_t cnt,
   }
 }
 
-// One block per rank bin.  The bin's records are staged in LDS; each record
-// is ranked against all of them by `parts` adjacent lanes, each comparing a
-// slice (parts = the largest power of two with cnt * parts <= 256, at most
-// 64): a big bin (skewed keys) costs cnt^2 / 256 compare steps per lane
-// instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
-// ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
-// branchless (wave-uniform trip counts, broadcast LDS reads).
-// One block per rank bin.  The bin's records are staged in LDS; each record
-// is ranked against all of them by `parts` adjacent lanes, each comparing a
-// slice (parts = the largest power of two with cnt * parts <= 256, at most
-// 64): a big bin (skewed keys) costs cnt^2 / 256 compare steps per lane
-// instead of cnt.  A bin of more than kBlockR records (parts = 1) takes
-// ceil(cnt / kBlockR) passes of one record per thread.  The comparison is
-// branchless (wave-uniform trip counts, broadcast LDS reads).  (One wave per
-// bin, four bins per block, was measured slower: the skewed P bins of up to
-// ~190 records then take three serial passes in one wave.)
+// One block per rank bin.  The bin's order keys are staged in LDS; each
+// record is ranked against all of them by `parts` adjacent lanes, each
+// comparing a slice (parts = the largest power of two with cnt * parts <=
+// 256, at most 64): a big bin (skewed keys) costs cnt^2 / 256 compare steps
+// per lane instead of cnt.  A bin of more than kBlockR records (parts = 1)
+// takes ceil(cnt / kBlockR) passes of one record per thread.  The comparison
+// is branchless (wave-uniform trip counts, broadcast LDS reads).  (One wave
+// per bin, four bins per block, was measured slower: the skewed P bins of up
+// to ~190 records then take three serial passes in one wave.)  A bin's
+// records take consecutive decision offsets, so fast records' decision
+// stores from one block fill one stretch of the decision array.
 constexpr int kRankBlocksR = kNBR;
 __global__ void __launch_bounds__(kBlockR)
 k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
-        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring,
+        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring, uint32_t* decof,
         uint64_t* wtime = nullptr) {
-  __shared__ BRecR sh[kBinCapR];
+  __shared__ BKey sh[kBinCapR];
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
   const uint32_t cnt = bcnt[b];
   if (cnt == 0 || rd->overflow) return;
   const uint32_t k = rd->k_total;
   const uint32_t n_pgroups = rd->n_pgroups;
+  dmc_decision* out = rd->out;
   const bool isp = b >= (uint32_t)kNBPhase;
   const uint32_t soff = bsoff[b], poff = bpoff[b];
   const BRecR* src = brec + (size_t)b * kBinCapR;
-  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i];
+  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
   uint32_t parts = 1;
   while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
   const uint32_t per = (cnt + parts - 1) / parts;
   __syncthreads();
   const uint32_t t = threadIdx.x;
   for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
-    rank_rec(rd, sh, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
-             soff, poff, ring);
+    rank_rec(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
+             soff, poff, ring, out, decof);
   if (wtime && threadIdx.x == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
@@ -1579,6 +1759,7 @@ struct RoundC {
 };
 
 constexpr int kApplyStage = 4;  // queue positions staged per candidate (LDS)
+constexpr int kDeepBatch = 8;   // queued requests reduced per batch of loads
 __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd,
                                  ReqEntry* st) {
   // every load that depends only on the candidate record is issued before
@@ -1635,10 +1816,16 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
       const double rinv = cv.rinv;
       // remaining requests: all reductions, in order (from the entries as
       // they were: the staged copy is not rewritten)
-      for (uint32_t k = pops; k < c; ++k) {
-        const double rk = reduced_r(rv, k, pmask, rinv);
-        ring[(h + k) & tb.qmask].r = rk;
-        if (k == pops) front_r = rk;
+      // (kDeepBatch at a time: the batch's loads before its stores)
+      for (uint32_t k0 = pops; k0 < c; k0 += kDeepBatch) {
+        double v[kDeepBatch];
+#pragma unroll
+        for (int j = 0; j < kDeepBatch; ++j)
+          if (k0 + j < c) v[j] = reduced_r(rv, k0 + j, pmask, rinv);
+#pragma unroll
+        for (int j = 0; j < kDeepBatch; ++j)
+          if (k0 + j < c) ring[(h + k0 + j) & tb.qmask].r = v[j];
+        if (k0 == pops) front_r = v[0];
       }
       double pr = prev.r;
       for (uint32_t j = 0; j < pops; ++j)
@@ -1700,25 +1887,117 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
 // (Non-candidates settled their pending marks in k_remit.)  Block 0 also
 // counts the round's decisions (sched[0] reservation, sched[1] priority,
 // :1469,1479).
+// A fast candidate (k_remit precomputed its state after its group: a pop at
+// queue position 0 and at most one run pop; decof: kNoDec if it was not
+// dispatched, else its first decision's offset): the stores apply_one would
+// make for that case, with no walk -- the run pop's decision, the reduced
+// reservation tags of the queued requests (the new front's and position
+// 2's precomputed; from position 3 on read, reduced and written, every load
+// issued before the first store), prev r, and the new front's ScanRec with
+// its ready flag.
+__device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandRec& cd,
+                                  uint32_t d, const PostRec& pr) {
+  const uint32_t s = cd.slot;
+  const uint8_t f0 = cd.f();
+  if (d == kNoDec) {  // not dispatched: the pending mark settles
+    if (f0 & F_PMARK)
+      tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (rc.p_runs ? F_READY : 0));
+    return;
+  }
+  const uint32_t bits = pr.bits;
+  const bool prio = bits & 1u;
+  const uint32_t run = (bits >> 2) & 1u;
+  const uint32_t c = cd.c, h = cd.h;
+  const uint32_t pops = 1 + run;
+  const uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
+  if (prio) {
+    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+    const double off = pr.off;
+    // positions >= 3, kDeepBatch at a time: loads, then stores
+    for (uint32_t k0 = 3; k0 < c; k0 += kDeepBatch) {
+      double v[kDeepBatch];
+#pragma unroll
+      for (int j = 0; j < kDeepBatch; ++j)
+        if (k0 + j < c) v[j] = ring[(h + k0 + j) & tb.qmask].r;
+#pragma unroll
+      for (int j = 0; j < kDeepBatch; ++j)
+        if (k0 + j < c) ring[(h + k0 + j) & tb.qmask].r = __dsub_rn(v[j], off);
+    }
+    if (nc2) ring[nh].r = pr.fr;
+    if (!run && c >= 3) ring[(h + 2) & tb.qmask].r = pr.r2;
+    tb.rec[s].prev_r = pr.prev_r;
+  }
+  if (run) {
+    dmc_decision x;
+    x.handle = pr.handle1;
+    x.tag_r = pr.r1;
+    x.tag_p = pr.p1;
+    x.tag_l = pr.l1;
+    x.slot = s;
+    x.cost = pr.cost1;
+    x.phase = DMC_PHASE_RESERVATION;
+    x.flags = 0;
+    rc.out[d + 1] = x;
+  }
+  uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
+  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
+  if (nc2) {
+    o.r = pr.fr;
+    o.pk = pr.fpk;
+    o.l = pr.fl;
+    const uint32_t last = d + run;  // the group's last decision
+    const bool seen =
+        prio ? (rc.terminal || (rc.g_last != kNoneR && last < rc.g_last)) : rc.p_runs;
+    if (seen && (bits & 2u)) f |= F_READY;
+  }
+  o.flags = f;
+  tb.sc[s] = o;
+}
+
+// Candidates, one thread each; k_rapply's blocks 2j and 2j + 1 take emit
+// block j's segment of the candidate arrays.  Fast candidates store their
+// precomputed state (apply_fast); the others (several records, a P group
+// with a reservation run, delayed mode, the radix path) replay their walks
+// for exactly the pops the ranking stamped (R pops, then P groups from the
+// post-R state), write the decision records and store the new state: ring
+// head/count, front cache, reduced reservation tags (immediate: every queued
+// request, in order, :1088-1095; delayed: the front, :1077-1085), prev tag,
+// and the front's ready flag: a front left by reservation pops only was seen
+// by the round's first limit scan iff the priority pulls ran; one left by
+// priority pops iff a later limit-scanning pull happened (or the round's
+// terminal pull).  (Non-candidates settled their pending marks in k_remit.)
+// Block 0 also counts the round's decisions (sched[0] reservation, sched[1]
+// priority, :1469,1479).
 #ifndef DMC_APPLY_MINB
 #define DMC_APPLY_MINB 5
 #endif
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
-k_rapply(Table tb, Round* rd, const CandRec* cand, unsigned long long* sched,
+k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
+         const uint32_t* decof, const PostRec* post, unsigned long long* sched,
          uint64_t* dbg = nullptr) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow) {
     sched[0] += rd->n_dec - rd->n_prio;
     sched[1] += rd->n_prio;
   }
-  const uint32_t nc = rd->n_cand;
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t eb = blockIdx.x >> 1;
+  const uint32_t nc = bcand[eb];
+  const uint32_t base = eb * kEmitChunk;
   RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
             rd->p_runs != 0, rd->overflow != 0};
   __shared__ ReqEntry stage[kBlockR * kApplyStage];
-  for (uint32_t ci = tid; ci < nc; ci += stride) {
+  for (uint32_t i = (blockIdx.x & 1) * kBlockR + threadIdx.x; i < nc; i += 2 * kBlockR) {
+    const uint32_t ci = base + i;
     uint64_t t0 = dbg ? wall_clock64() : 0;
+    // one level of coalesced loads: the candidate, its decision offset and
+    // its precomputed state (both lines: a run's second line is no further
+    // round trip)
     const CandRec c = cand[ci];
+    const uint32_t d = decof[ci];
+    const PostRec pr = post[ci];
+    if (d != kSlowCand && !rc.ovf) {
+      apply_fast(tb, rc, c, d, pr);
+      continue;
+    }
     rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
     if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;
     apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
