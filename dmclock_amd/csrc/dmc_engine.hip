@@ -837,18 +837,13 @@ __global__ void k_step_decide(uint32_t nparts, const StepRed* part, double now,
 // their partials with memory-side atomics, and the last block to finish (one
 // ticket counter; agent-scope acquire after it: MI355X_MICROARCH.md,
 // inter-workgroup visibility) combines the partials, decides and ends the
-// round.  When the round did not run out of work (the
-// common case) block 0 only ends the round: one kernel boundary per round
-// instead of two.
+// round again under `seq`.  The host launches it only after a round that
+// ran out of work (k_rapply's last block published that round's summary).
 constexpr int kFutThreads = 256;  // (1024-thread blocks spill the reductions to scratch)
 constexpr uint32_t kFutBlocks = 1024;
 __global__ void __launch_bounds__(kFutThreads)
 k_round_future(Table tb, StepRed* part, int at_limit, uint32_t nregistered,
-               StepCtl* sc, Round* ctl, HostRound* h, uint32_t* done) {
-  if (ctl->overflow || !ctl->terminal) {
-    if (blockIdx.x == 0) rfinish_body(ctl, h);
-    return;
-  }
+               StepCtl* sc, Round* ctl, HostRound* h, uint32_t* done, uint64_t seq) {
   // thread 0 stores the partial with memory-side atomics
   step_scan_body<kFutThreads, true>(tb, ctl->now, part);
   __shared__ uint32_t s_last;
@@ -863,6 +858,7 @@ k_round_future(Table tb, StepRed* part, int at_limit, uint32_t nregistered,
   __syncthreads();
   if (!s_last) return;
   step_decide<kFutThreads>(gridDim.x, part, 0.0, at_limit, nregistered, sc, ctl);
+  if (threadIdx.x == 0) ctl->seq = seq;  // the summary's second publication
   __syncthreads();
   if (threadIdx.x == 0) *done = 0;  // ready for the next round
   rfinish_body(ctl, h);
@@ -1833,12 +1829,10 @@ uint32_t pow2_at_least(uint32_t x) {
 // Terminal pull of a Wait/Reject batch: one general do_next_request, which
 // (nothing being eligible) computes min_not_0 over the reservation- and
 // limit-heap tops, :1170-1185.  No-op unless the round is terminal.
-void launch_future(dmc_queue* q) {
-  const double now = 0.0;  // read from the round by the kernels
-  (void)now;
+void launch_future(dmc_queue* q, uint64_t seq) {
   klaunch(q, DMC_PROF_FUTURE, k_round_future, dim3(std::min(q->step_grid, kFutBlocks)),
           dim3(kFutThreads), 0, q->tb, q->red, q->p.at_limit, q->n_registered, q->sctl,
-          q->rd, q->d_hround, q->fut_done);
+          q->rd, q->d_hround, q->fut_done, seq);
 }
 
 // bound infos of distinct slots (dmc_client_bind_info_batch)
@@ -1973,7 +1967,7 @@ bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
 
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) {
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   prof_gate(q);
   const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
@@ -2036,25 +2030,23 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool future) 
                        (const uint32_t*)q->gpoff, tb.ring);
     pe(q);
   }
-  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(2 * gEm), dim3(kBlockR), 0, tb, q->rd,
+  // (its last block ends the round: a round that ran out of work under
+  // Wait / Reject is followed by the terminal pull, launched by the host)
+  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(2 * gEm + 1), dim3(kBlockR), 0, tb, q->rd,
           (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
-          (const PostRec*)q->post, q->sched, q->debug ? q->dbg_atime : nullptr);
-  if (future)
-    launch_future(q);  // its decide kernel ends the round
-  else
-    hipLaunchKernelGGL(k_rfinish, dim3(1), dim3(64), 0, q->stream, (const Round*)q->rd,
-                       q->d_hround);
+          (const PostRec*)q->post, q->sched, q->d_hround,
+          q->debug ? q->dbg_atime : nullptr);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
-                 dmc_pull_result* d_result, bool radix, bool future) {
+                 dmc_pull_result* d_result, bool radix) {
   const bool sampled = use_sample(q, radix);
   uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 3) | (sampled ? 4 : 0) |
-                 (radix ? 2 : 0) | (future ? 1 : 0);
+                 (radix ? 2 : 0);
   CallParams cp{kk, 0, now, out, q->tick, d_result, ++q->round_seq};
-  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, future); });
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); });
   if (!g) {
-    enqueue_round(q, cp, radix, future);
+    enqueue_round(q, cp, radix);
     HIP_OK(hipGetLastError());
     return DMC_OK;
   }
@@ -2176,12 +2168,21 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       if (q->radix_batches && !retry) --q->radix_batches;
       rc = radix ? ensure_entries(q, q->dense_hint) : ensure_brec(q);
       if (rc) return rc;
-      rc = launch_round(q, now, kk, d_out + n_dec, dres, radix, !allow);
+      rc = launch_round(q, now, kk, d_out + n_dec, dres, radix);
       if (rc) return rc;
     }
     // one host round trip per round, through host-mapped memory
     rc = wait_round(q, q->round_seq);
     if (rc) return rc;
+    if (!allow && q->h_rd->terminal && !q->h_rd->overflow) {
+      // the round ran out of work: the terminal pull (do_next_request's
+      // future / none, :1170-1185) ends it
+      launch_future(q, ++q->round_seq);
+      rc = wait_round(q, q->round_seq);
+      if (rc) return rc;
+    }
+    // (debug readbacks below: k_rapply's other blocks may still run)
+    if (q->debug) HIP_OK(hipStreamSynchronize(q->stream));
     pflush(q);
     const Round c = *q->h_rd;
     bool wrote = dres && !c.overflow;
@@ -3034,16 +3035,14 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       int rc = ensure_batch(q, n);
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
-      const bool future = q->p.at_limit != DMC_AT_LIMIT_ALLOW;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
       CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq};
       auto enqueue = [&] {
         enqueue_add(q, ap);
-        enqueue_round(q, cp, false, future);
+        enqueue_round(q, cp, false);
       };
       ++q->ctr.fused_calls;
-      uint64_t key = (4ull << 56) | ((uint64_t)n << 2) | (use_sample(q, false) ? 2 : 0) |
-                     (future ? 1 : 0);
+      uint64_t key = (4ull << 56) | ((uint64_t)n << 2) | (use_sample(q, false) ? 2 : 0);
       GraphRec* gr = graph_for(q, key, enqueue, (const void*)k_rscan);
       if (!gr) {
         enqueue();

@@ -1887,6 +1887,30 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
 // (Non-candidates settled their pending marks in k_remit.)  Block 0 also
 // counts the round's decisions (sched[0] reservation, sched[1] priority,
 // :1469,1479).
+// Round end (one block of 64): the device-API result record when the host
+// expects this round to end the call (no overflow retry; a terminal round
+// under AtLimit::Allow is followed by host-driven steps, which rewrite it),
+// then the Round summary to host memory and its sequence number last.
+__device__ inline void rfinish_body(const Round* rd, HostRound* h) {
+  constexpr uint32_t W = sizeof(Round) / 4;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x == 0 && rd->res && !rd->overflow) {
+    dmc_pull_result r{};
+    r.n_decisions = rd->n_dec;
+    bool stop = rd->terminal && rd->n_dec < rd->k_total;
+    r.next_type = stop ? rd->next_type : DMC_NEXT_RETURNING;
+    r.when = stop ? rd->when : 0.0;
+    r.n_priority = rd->n_prio;
+    r.n_reservation = rd->n_dec - rd->n_prio;
+    *rd->res = r;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&h->seq, rd->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // A fast candidate (k_remit precomputed its state after its group: a pop at
 // queue position 0 and at most one run pop; decof: kNoDec if it was not
 // dispatched, else its first decision's offset): the stores apply_one would
@@ -1955,7 +1979,8 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 }
 
 // Candidates, one thread each; k_rapply's blocks 2j and 2j + 1 take emit
-// block j's segment of the candidate arrays.  Fast candidates store their
+// block j's segment of the candidate arrays, its last block ends the round
+// (the summary to host memory, the device-API result record).  Fast candidates store their
 // precomputed state (apply_fast); the others (several records, a P group
 // with a reservation run, delayed mode, the radix path) replay their walks
 // for exactly the pops the ranking stamped (R pops, then P groups from the
@@ -1974,7 +1999,14 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
          const uint32_t* decof, const PostRec* post, unsigned long long* sched,
-         uint64_t* dbg = nullptr) {
+         HostRound* h, uint64_t* dbg = nullptr) {
+  if (blockIdx.x == gridDim.x - 1) {
+    // the extra block publishes the round's summary (complete since k_rrank)
+    // to host memory at once: the host learns the outcome while the other
+    // blocks store the state, and its next launch is stream-ordered behind them
+    rfinish_body(rd, h);
+    return;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow) {
     sched[0] += rd->n_dec - rd->n_prio;
     sched[1] += rd->n_prio;
@@ -2008,30 +2040,6 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
   }
 }
 
-// Round end (one block of 64): the device-API result record when the host
-// expects this round to end the call (no overflow retry; a terminal round
-// under AtLimit::Allow is followed by host-driven steps, which rewrite it),
-// then the Round summary to host memory and its sequence number last.
-__device__ inline void rfinish_body(const Round* rd, HostRound* h) {
-  constexpr uint32_t W = sizeof(Round) / 4;
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
-  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
-  if (threadIdx.x == 0 && rd->res && !rd->overflow) {
-    dmc_pull_result r{};
-    r.n_decisions = rd->n_dec;
-    bool stop = rd->terminal && rd->n_dec < rd->k_total;
-    r.next_type = stop ? rd->next_type : DMC_NEXT_RETURNING;
-    r.when = stop ? rd->when : 0.0;
-    r.n_priority = rd->n_prio;
-    r.n_reservation = rd->n_dec - rd->n_prio;
-    *rd->res = r;
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&h->seq, rd->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __global__ void k_rfinish(const Round* rd, HostRound* h) { rfinish_body(rd, h); }
 
 // device-API result written by the host's view of a multi-round call
