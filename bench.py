@@ -35,31 +35,32 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 # Algorithmic bytes of each stage per step, from the step's counts: N client
 # slots, R added requests, D decisions, C candidate clients, E rank records
-# emitted, A activations (DESIGN.md section 6).  The pull-round stages stream
+# emitted, A activations (DESIGN.md section 3.2).  The pull-round stages stream
 # the client-table columns they need once per kernel and touch the
 # candidates' state and rings; the add path touches one client record per
-# request.
-def _stage_bytes(N, R, D, C, E, A):
+# request.  Bytes a kernel needs, not the lines it moves (the PMC traffic,
+# roofline.traffic, is the lines).
+def _stage_bytes(N, R, D, C, E, A, sampled=True):
     return {
-        # k_rscan: count 4 + head 4 + front r/p/l 24 + prop_delta 8 + flags 1
-        #   read; keyr 8 + keyp 8 + R-prefix length 1 written
-        "scan": 58 * N,
-        # k_rhist + k_rpick: keyr + keyp read
-        "select": 16 * N,
-        # k_rcand: keyr + keyp + flags read per slot; candidate slot written
-        "cand": 17 * N + 4 * C,
-        # k_remit: per candidate its slot 4, keyr/keyp 16, R-prefix length 1,
-        #   QState 16, inverses 24, prop_delta 8, flags 1 read; per record its
-        #   ring entry 64 read and the 24-byte rank record written
-        "emit": 70 * C + 88 * E,
-        # k_rbscan + k_rrank: rank records read, the decision offset and tie
-        #   flag (8) stamped into each dispatched ring entry
-        "rank": 24 * E + 8 * D,
-        # k_rapply: per candidate its slot 4, flags 1, QState 16, ClientRec
-        #   64, prop_delta 8 read; per decision its ring entry 64 read and the
-        #   48-byte decision written, and the popped client's new state
-        #   (head/count 8, front r/p/l 24, prev r 8, flags 1) written
-        "apply": 93 * C + 153 * D,
+        # k_rscan: ScanRec 32 read; keyr 8 + keyp 8 + meta 4 written; the
+        #   1/8 key sample 2
+        "scan": 54 * N,
+        # k_rhist: the sampled first keys (2 x 8 B per 8 slots), or every
+        #   slot's keyr + keyp (exact)
+        "select": (2 if sampled else 16) * N,
+        # k_remit: keyr 8 + keyp 8 + meta 4 streamed per slot; per candidate
+        #   its ClientRec fields 40 (inverses, prop_delta, prev r), two ring
+        #   entries 128 and position 2's r 8 read, its CandRec 8, PostRec 64
+        #   and decision offset 4 written; per record the bin atomic 8 and the
+        #   64-byte record
+        "emit": 20 * N + 252 * C + 72 * E,
+        # k_rrank: the records 64 read; per decision the 48-byte record and
+        #   the candidate's decision offset 4 written
+        "rank": 64 * E + 52 * D,
+        # k_rapply: per candidate CandRec 8, decision offset 4, PostRec 128
+        #   read; ScanRec 32, prev r 8 and the queued requests' reduced r
+        #   (about 2 x 8) written
+        "apply": 196 * C,
         # k_add_link: request slot 4 read, apos/aslot 8 written, the
         #   client's counter 4 (atomic) and slot-buffer entry 4
         "add_link": 20 * R,
@@ -90,7 +91,10 @@ def roofline(args, prof, prof_steps, ctr, k, n_clients=None, n_adds=None,
     per_step = lambda key: ctr[key] / prof_steps
     D, C, E = per_step("decisions"), per_step("candidates"), per_step("entries")
     A = activations or 0.0
-    model = _stage_bytes(N, R, D, C, E, A)
+    # sampled thresholds: tables of >= 65,536 slots (kSampleMinN) unless a
+    # round's sample failed validation (counted)
+    sampled = N >= (1 << 16) and not ctr.get("sample_retries", 0)
+    model = _stage_bytes(N, R, D, C, E, A, sampled)
     cand = [(ms, name) for ms, name in cand if name in model]
     if not cand:
         return None
