@@ -134,16 +134,32 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   p.rc[pos] = DMC_OK;
 }
 
-// The replay of slot s's m requests of the batch (m = its batch count, its
-// batch positions in abuf, or found by a scan of the slot column when m >
-// kAddSlots; i1: the position when m == 1), in batch order, with the
-// activation bookkeeping of ActBuf when act.cold is set.  Leaves the slot's
-// new state in *out (count, flags, front when set).
+// Slot s of the batch is not registered: every request of it gets ENOTREG.
+__device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t m,
+                                        const uint32_t* abuf, const uint32_t* aslot) {
+  if (m <= kAddSlots) {
+    for (uint32_t j = 0; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
+  } else {
+    for (uint32_t j = 0; j < p.n; ++j)
+      if (aslot[j] == s) p.rc[j] = DMC_ENOTREG;
+  }
+}
+
+// The replay of slot s's m requests of the batch (m = its batch count, read
+// from *acnt with the client's state when acnt is set, which is then reset
+// for the next batch; its batch positions in abuf, or found by a scan of the
+// slot column when m > kAddSlots; i1: the position when m == 1), in batch
+// order, with the activation bookkeeping of ActBuf when act.cold is set.  An
+// unregistered slot (checked here when acnt is set) rejects its requests.
+// Leaves the slot's new state in *out (count, flags, front when set).  Every
+// load is issued before the first store (on gfx950 a load's wait also waits
+// for the wave's earlier stores).
 __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint32_t s,
                                       uint32_t m, uint32_t i1, const uint32_t* abuf,
                                       const uint32_t* aslot, const ActBuf& act,
-                                      AddState* out) {
+                                      AddState* out, uint32_t* acnt = nullptr) {
   const uint32_t i = i1;
+  if (acnt) m = acnt[s];
   AddState st;
   st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   st.rinv = tb.rec[s].r_inv;
@@ -162,6 +178,11 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   // batched activations: this client's contribution to the idle reset before
   // and after its requests (see ActBuf)
+  if (acnt && !(st.flags & F_REG)) {
+    acnt[s] = 0;  // ready for the next batch
+    add_chain_notreg(p, s, m, abuf, aslot);
+    return;
+  }
   const bool idle0 = (st.flags & F_IDLE) != 0;
   const uint32_t count0 = st.count;
   const double front_p0 = (act.cold && count0) ? ring[st.head & tb.qmask].p : 0.0;
@@ -227,18 +248,8 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
     tb.sc[s].pk = __dadd_rn(st.front.p, pd);
     tb.sc[s].l = st.front.l;
   }
+  if (acnt) acnt[s] = 0;  // ready for the next batch
   *out = st;
-}
-
-// Slot s of the batch is not registered: every request of it gets ENOTREG.
-__device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t m,
-                                        const uint32_t* abuf, const uint32_t* aslot) {
-  if (m <= kAddSlots) {
-    for (uint32_t j = 0; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
-  } else {
-    for (uint32_t j = 0; j < p.n; ++j)
-      if (aslot[j] == s) p.rc[j] = DMC_ENOTREG;
-  }
 }
 
 }  // namespace dmc

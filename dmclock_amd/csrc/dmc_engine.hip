@@ -172,24 +172,21 @@ __global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
 __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
                             const uint32_t* abuf, const uint32_t* apos,
                             const uint32_t* aslot, ActBuf act = ActBuf{}) {
-  const AddParams p = *pblk;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // one level of loads: the call's parameters and this position's filing
+  // (apos / aslot are padded to whole blocks: in bounds for the grid)
+  const AddParams p = *pblk;
+  const uint32_t pos0 = apos[i];
+  const uint32_t s = aslot[i];
   if (i >= p.n) return;
-  uint32_t pos0 = apos[i];
   if (pos0 == kNone) {
     p.rc[i] = DMC_ENOTREG;
     return;
   }
   if (pos0 != 0) return;  // the client's first filer replays its requests
-  uint32_t s = aslot[i];
-  uint32_t m = acnt[s];
-  acnt[s] = 0;  // ready for the next batch
-  if (!(tb.sc[s].flags & F_REG)) {
-    add_chain_notreg(p, s, m, abuf, aslot);
-    return;
-  }
+  // the next: the client's batch count with its state
   AddState st;
-  add_chain_slot(tb, p, s, m, i, abuf, aslot, act, &st);
+  add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, acnt);
 }
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
@@ -1457,8 +1454,9 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
   dfree(q->d_reqs); dfree(q->d_rc); dfree(q->apos); dfree(q->aslot);
   HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
   HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
-  HIP_OK(hipMalloc(&q->apos, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->aslot, sizeof(uint32_t) * cap));
+  // (padded to whole blocks: k_add_chain loads them before its bounds check)
+  HIP_OK(hipMalloc(&q->apos, sizeof(uint32_t) * (cap + kBlock)));
+  HIP_OK(hipMalloc(&q->aslot, sizeof(uint32_t) * (cap + kBlock)));
   q->bcap = cap;
   return DMC_OK;
 }

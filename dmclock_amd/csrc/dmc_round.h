@@ -490,13 +490,6 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
   };
   if (s < n) load(s);
   const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    bool p_runs = tot.n_r < (uint64_t)rd->k_total;
-    rd->tot = tot;
-    rd->n_r = tot.n_r;
-    rd->p_runs = p_runs ? 1 : 0;
-    rd->sampled = sampled ? 1 : 0;
-  }
   if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
     const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
     const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
@@ -539,6 +532,14 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
   if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
 #endif
   pick_both(rd, tot, hist, sbn, sampled);
+  if (threadIdx.x == 0) {
+    // the round's totals (stored by the last block, after its barriers: a
+    // barrier waits for the thread's outstanding stores)
+    rd->tot = tot;
+    rd->n_r = tot.n_r;
+    rd->p_runs = tot.n_r < (uint64_t)rd->k_total ? 1 : 0;
+    rd->sampled = sampled ? 1 : 0;
+  }
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[2] = wall_clock64();
 #endif
@@ -605,12 +606,6 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   if (threadIdx.x == 0) rd->tdbg[6] = wall_clock64();
 #endif
   const uint32_t before = half_excl_scan(local, wsum);
-  // clear this phase's shards for the next round (plain stores, written
-  // back at the kernel's end, before the next round's atomics)
-#pragma unroll
-  for (int j = 0; j < kBinsPerThreadR; ++j)
-#pragma unroll
-    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j] = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[7] = wall_clock64();
 #endif
@@ -679,6 +674,13 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     sbn[p * kHistBinsR + b] = (p * kNBPhase + first) | (num << 16);
     nb += ns[j];
   }
+  // clear this phase's shards for the next round (plain stores, written
+  // back at the kernel's end, before the next round's atomics; last, since a
+  // block barrier waits for the thread's outstanding stores)
+#pragma unroll
+  for (int j = 0; j < kBinsPerThreadR; ++j)
+#pragma unroll
+    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j] = 0;
   if (t == 0) {
     PhaseSel z{};
     z.kmin = tot.mn[p];
@@ -1097,8 +1099,12 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     c[j] = (uint32_t)v;
     z[j] = (uint32_t)(v >> 32);
   }
+  // (cleared for the next round last: a block barrier waits for the
+  // thread's outstanding stores)
+  auto clear = [&] {
 #pragma unroll
-  for (int j = 0; j < per; ++j) bc64[t * per + j] = 0ull;
+    for (int j = 0; j < per; ++j) bc64[t * per + j] = 0ull;
+  };
   (void)bsize;
   for (int j = 0; j < per; ++j) {
     const uint32_t b = t * per + j;
@@ -1160,6 +1166,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   if (bad_sample) {
     // the round is re-run with the exact histogram (nothing applied yet)
     if (t == 0) rd->overflow = 3;
+    clear();
     return;
   }
   if (ovf) {
@@ -1171,6 +1178,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
       rd->dense_n = tc;
       rd->overflow = 2;
     }
+    clear();
     return;
   }
 #ifdef DMC_TAIL_TIMING
@@ -1205,6 +1213,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     rd->n_pgroups = tp;
     rd->n_emit = tc;
   }
+  clear();
 }
 
 // ---------------------------------------------------------------- k_remit
