@@ -26,6 +26,9 @@ STAGES = {
 }
 CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
 STREAMING = {"scan", "select", "future"}
+# walkers that also stream columns with 16-B-per-lane loads: bytes per slot
+# (k_remit: keyr 8 + keyp 8 + meta 4), counted 2x; the rest of their fetch 1x
+STREAM_PART = {"emit": 20}
 
 
 def calib_rates(stats_csv, out):
@@ -96,6 +99,8 @@ def main():
     ap.add_argument("--calib", default=None,
                     help="tools/fetch_calib FETCH_SIZE csv (with --known): print factors")
     ap.add_argument("--known", default=None)
+    ap.add_argument("--slots", type=int, default=1 << 20,
+                    help="client slots of the profiled bench (STREAM_PART)")
     ap.add_argument("--calib-stats", default=None,
                     help="rocprofv3 --stats csv of the same calibration run: rates")
     a = ap.parse_args()
@@ -117,11 +122,16 @@ def main():
         # r02_fetch_calib.json): FETCH_SIZE counts 64 B per memory request; a
         # coalesced stream requests 128 B (bytes = 2 x FETCH_SIZE), a random
         # access of <= 64 B one 64-B request (bytes = FETCH_SIZE).  Streaming
-        # stages take 2x; the walkers mix both, so their traffic is bracketed
-        # by 1x (all random) and 2x (all streamed), 1x being reported
+        # stages take 2x; the walkers' random accesses 1x, k_remit's streamed
+        # key columns 2x (STREAM_PART); the all-streamed bound is kept beside
         fac = 2.0 if stage in STREAMING else 1.0
+        hbm = fac * f + w
+        if stage in STREAM_PART and f > 0:
+            # the streamed columns' raw count is half their bytes
+            streamed_raw = min(f, STREAM_PART[stage] * a.slots / 2.0)
+            hbm = 2.0 * streamed_raw + (f - streamed_raw) + w
         out[stage] = {"fetch_size_bytes_raw": round(f), "write_size_bytes": round(w),
-                      "hbm_bytes": round(fac * f + w), "fetch_factor": fac,
+                      "hbm_bytes": round(hbm), "fetch_factor": fac,
                       "hbm_bytes_if_all_streamed": round(2 * f + w),
                       "kernels": ks, "launches_averaged": a.steps}
     json.dump(out, open(a.out, "w"), indent=1)
