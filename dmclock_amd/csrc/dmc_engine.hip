@@ -1385,6 +1385,7 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = n
   GraphRec* slot = &q->graphs[0];
   for (auto& g : q->graphs)
     if (!g.exec || g.last_use < slot->last_use) slot = &g;
+  if (slot->exec) (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
   graph_destroy(*slot);
   if (graph_capture(q, *slot, enqueue, func2) != DMC_OK) {
     graph_destroy(*slot);
@@ -1396,8 +1397,12 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = n
   return slot;
 }
 
-// Buffers captured into graphs are about to move: drop every graph.
+// Buffers captured into graphs are about to move: drop every graph.  The
+// stream drains first: a call returns once its round's summary is published,
+// while that round's last kernel may still run (and a graph, its kernel
+// arguments or a buffer must not go away under it).
 void invalidate_graphs(dmc_queue* q) {
+  (void)hipStreamSynchronize(q->stream);
   pflush(q);
   for (auto& g : q->graphs) graph_destroy(g);
 }
@@ -1463,6 +1468,7 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
 
 int ensure_dec(dmc_queue* q, uint32_t n) {
   if (n <= q->dcap) return DMC_OK;
+  (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
   dfree(q->d_dec);
   uint32_t cap = std::max<uint32_t>(n, 1024);
   HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
@@ -1545,6 +1551,7 @@ int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
 
 int ensure_act(dmc_queue* q, uint32_t n) {
   if (n <= q->acap) return DMC_OK;
+  (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
   uint32_t cap = std::max<uint32_t>(n, 4096);
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
@@ -2625,6 +2632,7 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
     q->mark_ev_live = false;
   }
   if (n > q->mark_cap) {
+    (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
     if (q->h_mark) (void)hipHostFree(q->h_mark);
     dfree(q->d_mark);
     q->h_mark = nullptr;

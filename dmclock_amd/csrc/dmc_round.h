@@ -644,10 +644,21 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   if (threadIdx.x == 0) rd->tdbg[8] = wall_clock64();
 #endif
   const uint32_t C = *s_C > 0 ? *s_C : 1;
-  const uint32_t S = kNBPhase - (tb + 1);
-  // spare rank bins in proportion to the counts, h * S / C in single
-  // precision (any split is correct; only the balance depends on it), each
-  // clipped to S so that the phase cannot pass its kNBPhase rank bins
+  // Every non-empty histogram bin up to T's gets one rank bin, and the
+  // spare ones go in proportion to the counts, h * S / C in single precision
+  // (any split is correct; only the balance depends on it), each clipped to
+  // S so that the phase cannot pass its kNBPhase rank bins.  An empty bin
+  // gets none: its keys (a sample's empty bin may hold a few) share the next
+  // bin's first rank bin, which keeps the map monotone.
+  uint32_t lnz = 0;
+#pragma unroll
+  for (int j = 0; j < kBinsPerThreadR; ++j)
+    lnz += ((uint32_t)(t * kBinsPerThreadR + j) <= tb && h[j]) ? 1u : 0u;
+  (void)half_excl_scan(lnz, wsum);
+  uint32_t nz = 0;
+  for (int i = 0; i < kPickHalf / 64; ++i) nz += wsum[i];
+  __syncthreads();  // (wsum is reused below)
+  const uint32_t S = kNBPhase > nz ? kNBPhase - nz : 0;
   const float q = (float)S / (float)C;
   uint32_t ns[kBinsPerThreadR], lns = 0;
 #pragma unroll
@@ -655,7 +666,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     const uint32_t b = t * kBinsPerThreadR + j;
     uint32_t e = (uint32_t)((float)h[j] * q);
     e = e > S ? S : e;
-    ns[j] = b <= tb ? 1u + e : 0u;
+    ns[j] = (b <= tb && h[j]) ? 1u + e : 0u;
     lns += ns[j];
   }
   uint32_t nb = half_excl_scan(lns, wsum);
