@@ -42,18 +42,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # roofline.traffic, is the lines).
 def _stage_bytes(N, R, D, C, E, A, sampled=True):
     return {
-        # k_rscan: ScanRec 32 read; keyr 8 + keyp 8 + meta 4 written; the
-        #   1/8 key sample 2
-        "scan": 54 * N,
+        # k_rscan: ScanRec 32 read; the quantized first keys 8 + meta 4
+        #   written; the 1/8 key sample 2 (unsampled rounds: + the 64-bit
+        #   keys 16)
+        "scan": (46 if sampled else 62) * N,
         # k_rhist: the sampled first keys (2 x 8 B per 8 slots), or every
         #   slot's keyr + keyp (exact)
         "select": (2 if sampled else 16) * N,
-        # k_remit: keyr 8 + keyp 8 + meta 4 streamed per slot; per candidate
+        # k_remit: quantized keys 8 + meta 4 streamed per slot; per candidate
         #   its ClientRec fields 40 (inverses, prop_delta, prev r), two ring
         #   entries 128 and position 2's r 8 read, its CandRec 8, PostRec 64
         #   and decision offset 4 written; per record the bin atomic 8 and the
         #   64-byte record
-        "emit": 20 * N + 252 * C + 72 * E,
+        "emit": 12 * N + 252 * C + 72 * E,
         # k_rrank: the records 64 read; per decision the 48-byte record and
         #   the candidate's decision offset 4 written
         "rank": 64 * E + 52 * D,

@@ -1108,7 +1108,8 @@ struct dmc_queue {
   uint32_t* bcand = nullptr;  // per k_remit block: its candidates
   PostRec* post = nullptr;    // per candidate: a fast candidate's state after its pop
   uint32_t* decof = nullptr;  // per candidate: kSlowCand, kNoDec or its decision offset
-  uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase
+  uint64_t *keyr = nullptr, *keyp = nullptr;  // N: first keys per phase (unsampled rounds)
+  uint2* k32 = nullptr;       // N: 32-bit quantized first keys (R, P), k_remit's stream
   uint32_t* meta = nullptr;   // N: k_rscan's per-slot R-prefix length, flags, head, count
   RoundPart* rparts = nullptr; // k_rscan's per-block partials
   Round* rd = nullptr;
@@ -1980,9 +1981,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes two per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb, q->keyr,
-          q->keyp, q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
-          sampled ? q->skp : nullptr);
+  klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb,
+          sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
+          q->rd, cp, sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
@@ -1993,8 +1994,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
             gN, q->rd, q->hist, q->sbn, q->hist_done, 0);
   klaunch(q, DMC_PROF_EMIT, k_remit, dim3(gEm),
-          dim3(kEmitThreads), 0, tb, q->rd, (const uint64_t*)q->keyr,
-          (const uint64_t*)q->keyp, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
+          dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
           q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
           q->debug ? q->dbg_etime : nullptr);
@@ -2058,8 +2058,10 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   Table tb = q->tb;
   uint64_t* skr = sampled ? q->skr : nullptr;
   uint64_t* skp = sampled ? q->skp : nullptr;
-  void* args[] = {&tb, &q->keyr, &q->keyp, &q->meta, &q->rparts, &q->rd, &cp,
-                  &skr, &skp};
+  uint64_t* kr = sampled ? nullptr : q->keyr;
+  uint64_t* kp = sampled ? nullptr : q->keyp;
+  void* args[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
+                  &skr, &skp, &q->k32};
   return graph_replay(q, *g, args);
 }
 
@@ -2400,6 +2402,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   }
   rc |= A(&q->keyr, N);
   rc |= A(&q->keyp, N);
+  rc |= A(&q->k32, N);
   rc |= A(&q->meta, N);
   rc |= A(&q->hist, kShards * 2 * kHistBinsR);
   rc |= A(&q->sbn, 2 * kHistBinsR);
@@ -2470,7 +2473,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   Table& t = q->tb;
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
-                  q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->meta, q->hist, q->sbn,
+                  q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist, q->sbn,
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
                   q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
@@ -3061,8 +3064,10 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         const bool sampled = use_sample(q, false);
         uint64_t* skr = sampled ? q->skr : nullptr;
         uint64_t* skp = sampled ? q->skp : nullptr;
-        void* a2[] = {&tb, &q->keyr, &q->keyp, &q->meta, &q->rparts, &q->rd, &cp,
-                      &skr, &skp};
+        uint64_t* kr = sampled ? nullptr : q->keyr;
+        uint64_t* kp = sampled ? nullptr : q->keyp;
+        void* a2[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
+                      &skr, &skp, &q->k32};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }

@@ -210,6 +210,18 @@ constexpr int kScanBlock = DMC_SCAN_BLOCK;
 constexpr uint32_t kSample = 8;
 constexpr uint32_t kSampleMinN = 1u << 16;
 
+// k_remit's candidate test streams a 32-bit quantized first key per phase
+// (the ordered key's top half, capped at 0xfffffffe; 0xffffffff: no key) and
+// compares it with the threshold's; the pick rounds every finite threshold up
+// to the end of its quantum (T | 0xffffffff: any T at or above the needed key
+// is exact), so that key <= T  <=>  key32 <= T32 exactly.  (Finite and
+// infinite keys have top halves <= 0xfff00000.)
+__device__ inline uint32_t key32(uint64_t k) {
+  if (k == kMaxKey) return 0xffffffffu;
+  const uint32_t h = (uint32_t)(k >> 32);
+  return h > 0xfffffffeu ? 0xfffffffeu : h;
+}
+
 struct ScanCols {
   uint32_t c, h;
   double fr, pk, fl;  // the front's heap keys (ScanRec)
@@ -219,7 +231,7 @@ struct ScanCols {
 __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
                                  double now, uint64_t* keyr, uint64_t* keyp,
                                  uint32_t* meta, uint64_t* skr, uint64_t* skp,
-                                 RoundPart& acc) {
+                                 uint2* k32, RoundPart& acc) {
   uint64_t kr = kMaxKey, kp = kMaxKey;
   uint32_t m = 0;
   uint8_t f = x.f;
@@ -263,8 +275,11 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
     // p < inf iff p + prop_delta < inf (prop_delta is finite)
     if (have_pf && ready && pkv < kInf) kp = okey(pkv);
   }
-  keyr[s] = kr;
-  keyp[s] = kp;
+  if (keyr) {  // the exact histogram's keys (unsampled rounds)
+    keyr[s] = kr;
+    keyp[s] = kp;
+  }
+  k32[s] = make_uint2(key32(kr), key32(kp));
   if (skr && (s & (kSample - 1)) == 0) {  // the threshold histogram's sample
     skr[s / kSample] = kr;
     skp[s / kSample] = kp;
@@ -380,7 +395,8 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // for a RoundPart, too many to run in every wave of the block).
 __global__ void __launch_bounds__(kScanBlock)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
-        RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp) {
+        RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
+        uint2* k32) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -416,7 +432,7 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, meta, skr, skp, acc);
+    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, meta, skr, skp, k32, acc);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
@@ -623,7 +639,8 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                             ? tot.mx[p]
                             : km.max_key_at(sat_add_u64(hmin, ((uint64_t)(b + 1) << sh1) - 1),
                                             tot.mx[p]);
-        *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : edge;
+        // (rounded up to the end of its 32-bit quantum: see key32)
+        *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : (edge | 0xffffffffull);
         *s_tb = b;
         break;
       }
@@ -934,15 +951,16 @@ struct EmitV {
 // pulls run and) its first P key is <= T_P.
 struct CandPred {
   uint64_t TR, TP;  // 0: no candidates in that phase
+  uint32_t TR32, TP32;
   __device__ explicit CandPred(const Round* rd)
-      : TR(rd->ph[0].T), TP(rd->p_runs ? rd->ph[1].T : 0) {}
-  __device__ bool operator()(uint64_t kr, uint64_t kp) const {
-    return (TR && kr <= TR) || (TP && kp <= TP);
+      : TR(rd->ph[0].T), TP(rd->p_runs ? rd->ph[1].T : 0),
+        TR32(key32(TR) > 0xfffffffeu ? 0xfffffffeu : key32(TR)),
+        TP32(key32(TP) > 0xfffffffeu ? 0xfffffffeu : key32(TP)) {}
+  // exact: T is kMaxKey - 1 or the end of its quantum (see key32)
+  __device__ bool operator()(uint32_t kr32, uint32_t kp32) const {
+    return (TR && kr32 <= TR32) || (TP && kp32 <= TP32);
   }
 };
-__device__ inline bool is_cand(const Round* rd, uint64_t kr, uint64_t kp) {
-  return CandPred(rd)(kr, kp);
-}
 
 // A candidate as compacted by k_remit: slot; flags (low nibble) and its
 // first-key predicates (bit 4: R, bit 5: P); R-prefix length; ring head and
@@ -1245,7 +1263,7 @@ constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no f
                              // and a slower last-block tail)
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
 __global__ void __launch_bounds__(kEmitThreads)
-k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
+k_remit(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
@@ -1270,17 +1288,15 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
   const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t kr[kEmitPer], kp[kEmitPer];
+  uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   if (s0 + kEmitPer <= n) {
-    const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
-    const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
+    const uint4* k4 = reinterpret_cast<const uint4*>(k32 + s0);
     const uint4* m4 = reinterpret_cast<const uint4*>(meta + s0);
 #pragma unroll
     for (int j = 0; j < kEmitPer / 2; ++j) {
-      const ulonglong2 a = r2[j], c = p2[j];
-      kr[2 * j] = a.x; kr[2 * j + 1] = a.y;
-      kp[2 * j] = c.x; kp[2 * j + 1] = c.y;
+      const uint4 a = k4[j];
+      kr[2 * j] = a.x; kp[2 * j] = a.y; kr[2 * j + 1] = a.z; kp[2 * j + 1] = a.w;
     }
 #pragma unroll
     for (int j = 0; j < kEmitPer / 4; ++j) {
@@ -1291,8 +1307,9 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
 #pragma unroll
     for (int j = 0; j < kEmitPer; ++j) {
       bool in = s0 + j < n;
-      kr[j] = in ? keyr[s0 + j] : kMaxKey;
-      kp[j] = in ? keyp[s0 + j] : kMaxKey;
+      const uint2 k = in ? k32[s0 + j] : make_uint2(0xffffffffu, 0xffffffffu);
+      kr[j] = k.x;
+      kp[j] = k.y;
       mt[j] = in ? meta[s0 + j] : 0;
     }
   }
@@ -1308,8 +1325,8 @@ k_remit(Table tb, Round* rd, const uint64_t* keyr, const uint64_t* keyp,
 #pragma unroll
   for (int j = 0; j < kEmitPer; ++j) {
     if (s0 + j >= n) continue;
-    const bool cr = pred.TR && kr[j] <= pred.TR;
-    const bool cp = pred.TP && kp[j] <= pred.TP;
+    const bool cr = pred.TR && kr[j] <= pred.TR32;
+    const bool cp = pred.TP && kp[j] <= pred.TP32;
     if (cr || cp) bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
   }
   uint32_t cnt = 0, nr = 0, np = 0;

@@ -27,8 +27,9 @@ STAGES = {
 CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
 STREAMING = {"scan", "select", "future"}
 # walkers that also stream columns with 16-B-per-lane loads: bytes per slot
-# (k_remit: keyr 8 + keyp 8 + meta 4), counted 2x; the rest of their fetch 1x
-STREAM_PART = {"emit": 20}
+# (k_remit: the quantized keys 8 + meta 4), counted 2x; the rest of their
+# fetch 1x
+STREAM_PART = {"emit": 12}
 
 
 def calib_rates(stats_csv, out):
