@@ -169,9 +169,10 @@ def main(args):
         for i in range(i0, i1):
             d = d_steps[s][i]
             trk.fill(s, d.data_ptr(), args.batch)
-            q.add_batch_device(d.data_ptr(), args.batch, d_rc[s].data_ptr())
-            q.pull_batch_device(nows[s][i], k, d_out[s].data_ptr(),
-                                d_res[s, i].data_ptr())
+            # the add batch and the pull batch in one graph launch
+            q.add_pull_batch_device(d.data_ptr(), args.batch, d_rc[s].data_ptr(),
+                                    nows[s][i], k, d_out[s].data_ptr(),
+                                    d_res[s, i].data_ptr())
             trk.tally(s, d_out[s].data_ptr(), d_res[s, i].data_ptr(), k)
         q.sync()
 
