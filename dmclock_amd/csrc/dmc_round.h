@@ -194,7 +194,7 @@ struct CountV {
 // (counts, key ranges) stay few.
 // (build-time overridable for launch-shape sweeps: results do not depend on them)
 #ifndef DMC_SCAN_SLOTS
-#define DMC_SCAN_SLOTS 2
+#define DMC_SCAN_SLOTS 1
 #endif
 #ifndef DMC_SCAN_BLOCK
 #define DMC_SCAN_BLOCK 1024
@@ -228,53 +228,88 @@ struct ScanCols {
   uint8_t f;
 };
 
-__device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
-                                 double now, uint64_t* keyr, uint64_t* keyp,
-                                 uint32_t* meta, uint64_t* skr, uint64_t* skp,
-                                 uint2* k32, RoundPart& acc) {
-  uint64_t kr = kMaxKey, kp = kMaxKey;
-  uint32_t m = 0;
-  uint8_t f = x.f;
-  if (x.c) {
-    Tag3 pf;
-    bool have_pf = true, ready;
-    double pkv = kInf;
-    if (x.fr <= now) {
-      kr = okey(x.fr);
-      if (!tb.delayed) {
-        // the front (r == fr) is in the prefix; walk on from entry 1
-        const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-        m = 1;
-        while (m < x.c) {
-          const ReqEntry& e = ring[(x.h + m) & tb.qmask];
-          if (!(e.r <= now)) {
-            pf = Tag3{e.r, e.p, e.l, e.arrival};
-            break;
+// A slot's first R prefix step, requested for all of a thread's slots
+// before any of them is walked (immediate mode, front r <= now): queue
+// position 1's tag and the client's prop_delta, one level of loads.
+struct ScanPre {
+  double r1, p1, l1, pd;
+};
+
+struct ScanOut {
+  uint64_t kr, kp;
+  uint32_t m;
+  uint8_t f;
+  bool mark;  // a pending limit-scan mark to store
+};
+
+// The slot's keys from its ScanRec columns (and, for an R prefix, its ring):
+// no stores (scan_store makes them after every slot of the thread is done,
+// since a load's wait also waits for the wave's earlier stores).
+__device__ inline ScanOut scan_compute(const Table& tb, uint32_t s, const ScanCols& x,
+                                       const ScanPre& pre, double now) {
+  ScanOut o{kMaxKey, kMaxKey, 0, x.f, false};
+  if (!x.c) return o;
+  Tag3 pf;
+  bool have_pf = true, ready;
+  double pkv = kInf;
+  if (x.fr <= now) {
+    o.kr = okey(x.fr);
+    double pd;
+    uint32_t m;
+    if (!tb.delayed) {
+      // the front (r == fr) is in the prefix; position 1 was requested up
+      // front, a longer prefix walks on from position 2
+      pd = pre.pd;
+      m = 1;
+      if (m < x.c) {
+        if (!(pre.r1 <= now)) {
+          pf = Tag3{pre.r1, pre.p1, pre.l1, 0.0};
+        } else {
+          const ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+          m = 2;
+          while (m < x.c) {
+            const ReqEntry& e = ring[(x.h + m) & tb.qmask];
+            if (!(e.r <= now)) {
+              pf = Tag3{e.r, e.p, e.l, e.arrival};
+              break;
+            }
+            ++m;
           }
-          ++m;
         }
-      } else {
-        CountV v;
-        uint32_t fc;
-        const CView cvx = load_view(tb, s);
-        m = walk_r(tb, ring_view(tb, s, cvx.h), cvx, now, kMaxKey, 0xffffffffu, v,
-                   nullptr, &pf, &fc);
       }
-      have_pf = m < x.c;
-      ready = pf.l <= now;
-      // the post-R front's key, with the client's prop_delta (ClientRec)
-      if (have_pf && ready) pkv = __dadd_rn(pf.p, tb.rec[s].pd);
     } else {
-      pkv = x.pk;
-      ready = (x.f & F_READY) || x.fl <= now;
-      if (!(x.f & F_READY) && x.fl <= now) {
-        f = x.f | F_PMARK;
-        tb.sc[s].flags = f;
-      }
+      CountV v;
+      uint32_t fc;
+      const CView cvx = load_view(tb, s);
+      pd = cvx.pd;
+      m = walk_r(tb, ring_view(tb, s, cvx.h), cvx, now, kMaxKey, 0xffffffffu, v,
+                 nullptr, &pf, &fc);
     }
-    // p < inf iff p + prop_delta < inf (prop_delta is finite)
-    if (have_pf && ready && pkv < kInf) kp = okey(pkv);
+    o.m = m;
+    have_pf = m < x.c;
+    ready = pf.l <= now;
+    // the post-R front's key, with the client's prop_delta
+    if (have_pf && ready) pkv = __dadd_rn(pf.p, pd);
+  } else {
+    pkv = x.pk;
+    ready = (x.f & F_READY) || x.fl <= now;
+    if (!(x.f & F_READY) && x.fl <= now) {
+      o.f = x.f | F_PMARK;
+      o.mark = true;
+    }
   }
+  // p < inf iff p + prop_delta < inf (prop_delta is finite)
+  if (have_pf && ready && pkv < kInf) o.kp = okey(pkv);
+  return o;
+}
+
+__device__ inline void scan_store(const Table& tb, uint32_t s, const ScanCols& x,
+                                  const ScanOut& o, uint64_t* keyr, uint64_t* keyp,
+                                  uint32_t* meta, uint64_t* skr, uint64_t* skp,
+                                  uint2* k32, RoundPart& acc) {
+  const uint64_t kr = o.kr, kp = o.kp;
+  const uint32_t m = o.m;
+  if (o.mark) tb.sc[s].flags = o.f;
   if (keyr) {  // the exact histogram's keys (unsampled rounds)
     keyr[s] = kr;
     keyp[s] = kp;
@@ -286,7 +321,7 @@ __device__ inline void scan_slot(const Table& tb, uint32_t s, const ScanCols& x,
   }
   // the candidate record's fields for k_remit: R-prefix length, flags (with
   // a pending mark this scan set), ring head and count
-  meta[s] = (m & 0xffu) | ((uint32_t)f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
+  meta[s] = (m & 0xffu) | ((uint32_t)o.f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
   if (kr != kMaxKey) {
     ++acc.cnt[0];
     acc.n_r += m;
@@ -393,7 +428,11 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // Scan.  Per-block counts and key ranges (parts), staged in LDS and combined
 // by wave 0 (cross-lane shuffles are ds_bpermute round trips: 12 per level
 // for a RoundPart, too many to run in every wave of the block).
-__global__ void __launch_bounds__(kScanBlock)
+// (DMC_SCAN_MINW waves per SIMD: 8 = two blocks per CU, at most 64 VGPRs)
+#ifndef DMC_SCAN_MINW
+#define DMC_SCAN_MINW 8
+#endif
+__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
 k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
         RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
         uint2* k32) {
@@ -429,10 +468,33 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
       x[j].f = r.flags;
     }
   }
+  // every slot's first R prefix step in one level of loads
+  ScanPre pre[kScanSlots];
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_slot(tb, s, x[j], now, keyr, keyp, meta, skr, skp, k32, acc);
+    pre[j] = ScanPre{0.0, 0.0, 0.0, 0.0};
+    if (s < tb.n && x[j].c && x[j].fr <= now && !tb.delayed) {
+      pre[j].pd = tb.rec[s].pd;
+      if (x[j].c > 1) {
+        const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x[j].h + 1) & tb.qmask)];
+        pre[j].r1 = e.r;
+        pre[j].p1 = e.p;
+        pre[j].l1 = e.l;
+      }
+    }
+  }
+  ScanOut o[kScanSlots];
+#pragma unroll
+  for (int j = 0; j < kScanSlots; ++j) {
+    uint32_t s = base + j * blockDim.x;
+    o[j] = s < tb.n ? scan_compute(tb, s, x[j], pre[j], now)
+                    : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
+  }
+#pragma unroll
+  for (int j = 0; j < kScanSlots; ++j) {
+    uint32_t s = base + j * blockDim.x;
+    if (s < tb.n) scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
