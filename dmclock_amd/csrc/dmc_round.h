@@ -513,7 +513,17 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
   __shared__ RoundPart sh_tot;
   if (threadIdx.x < 64) {
     RoundPart o = rpart_ident();
-    for (uint32_t i = threadIdx.x; i < nparts; i += 64) rpart_combine(o, parts[i]);
+    // four partials per lane in flight at a time (independent loads, not a
+    // chain of 16 dependent ones for 1024 partials)
+    uint32_t i = threadIdx.x;
+    for (; i + 3 * 64 < nparts; i += 4 * 64) {
+      const RoundPart a = parts[i], b = parts[i + 64], c = parts[i + 128], d = parts[i + 192];
+      rpart_combine(o, a);
+      rpart_combine(o, b);
+      rpart_combine(o, c);
+      rpart_combine(o, d);
+    }
+    for (; i < nparts; i += 64) rpart_combine(o, parts[i]);
     o = wave_reduce_rpart(o);
     if (threadIdx.x == 0) sh_tot = o;
   }
@@ -529,6 +539,7 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
 constexpr int kHistBlocksSampled = 32;  // 131,072 sampled slots of 1M: 4 per thread
+                                        // (16 and 64 blocks measured no faster)
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
                           uint32_t* sbn, int sampled);
 // n keys per phase: every slot's first keys (keyr / keyp, exact), or the
