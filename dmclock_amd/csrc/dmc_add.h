@@ -68,8 +68,9 @@ struct AddState {
 };
 
 __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
-                               const AddParams& p, uint32_t pos) {
-  const dmc_request rq = p.reqs[pos];
+                               const AddParams& p, uint32_t pos,
+                               const dmc_request* pre = nullptr) {
+  const dmc_request rq = pre ? *pre : p.reqs[pos];
   uint64_t tick = p.tick_base + pos + 1;  // ++tick, :918
   if (rq.rho > rq.delta) {  // ReqParams asserts rho <= delta
     p.rc[pos] = DMC_EBADPARAMS;
@@ -159,6 +160,9 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
                                       const uint32_t* aslot, const ActBuf& act,
                                       AddState* out, uint32_t* acnt = nullptr) {
   const uint32_t i = i1;
+  // position i1's request, requested with the client's state (the usual
+  // case, m == 1, needs nothing else from the batch)
+  const dmc_request rq1 = p.reqs[i];
   if (acnt) m = acnt[s];
   AddState st;
   st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
@@ -189,7 +193,7 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   const double prev_p0 = st.prev.p;
   bool act_done = false, chg_done = false;
   auto step = [&](uint32_t pos) {
-    add_one(tb, st, ring, p, pos);
+    add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
     if (!act.cold) return;
     if (idle0) {
       const dmc_request& rq = p.reqs[pos];
