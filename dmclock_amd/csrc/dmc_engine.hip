@@ -1979,7 +1979,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
-  // k_remit blocks (kEmitChunk slots each); k_rapply takes two per emit block
+  // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
   klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb,
           sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
@@ -2037,7 +2037,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   }
   // (its last block ends the round: a round that ran out of work under
   // Wait / Reject is followed by the terminal pull, launched by the host)
-  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(2 * gEm + 1), dim3(kBlockR), 0, tb, q->rd,
+  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(kApplyPerEmit * gEm + 1), dim3(kBlockR), 0, tb, q->rd,
           (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
           (const PostRec*)q->post, q->sched, q->d_hround,
           q->debug ? q->dbg_atime : nullptr);

@@ -1073,7 +1073,10 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // priority pulls run, the P groups with key <= T_P from the post-R state.
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
 constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2: no faster)
-constexpr int kEmitStageThreads = 512;  // walkers with a staging slice (all of a block)
+#ifndef DMC_EMIT_STAGE_THREADS
+#define DMC_EMIT_STAGE_THREADS 512
+#endif
+constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a staging slice
 __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
@@ -1331,7 +1334,10 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 // rank-bin table staged in LDS.  Bin-rank path: the last block to finish
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
-constexpr int kEmitThreads = 1024;
+#ifndef DMC_EMIT_THREADS
+#define DMC_EMIT_THREADS 1024
+#endif
+constexpr int kEmitThreads = DMC_EMIT_THREADS;
 constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster,
                              // and a slower last-block tail)
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
@@ -2103,6 +2109,9 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 // terminal pull).  (Non-candidates settled their pending marks in k_remit.)
 // Block 0 also counts the round's decisions (sched[0] reservation, sched[1]
 // priority, :1469,1479).
+// apply blocks per emit block (about 70 candidates per 1024 slots in a
+// config-3 round)
+constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 #ifndef DMC_APPLY_MINB
 #define DMC_APPLY_MINB 5
 #endif
@@ -2121,13 +2130,17 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
     sched[0] += rd->n_dec - rd->n_prio;
     sched[1] += rd->n_prio;
   }
-  const uint32_t eb = blockIdx.x >> 1;
+  // (kApplyPerEmit apply blocks per emit block)
+  const uint32_t eb = blockIdx.x / kApplyPerEmit;
   const uint32_t nc = bcand[eb];
   const uint32_t base = eb * kEmitChunk;
   RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
             rd->p_runs != 0, rd->overflow != 0};
   __shared__ ReqEntry stage[kBlockR * kApplyStage];
-  for (uint32_t i = (blockIdx.x & 1) * kBlockR + threadIdx.x; i < nc; i += 2 * kBlockR) {
+  // (interleaved: the emit block's candidates, about 280, split evenly over
+  // its apply blocks rather than filling the first one)
+  for (uint32_t i = threadIdx.x * kApplyPerEmit + (blockIdx.x % kApplyPerEmit); i < nc;
+       i += kApplyPerEmit * kBlockR) {
     const uint32_t ci = base + i;
     uint64_t t0 = dbg ? wall_clock64() : 0;
     // one level of coalesced loads: the candidate, its decision offset and
