@@ -1,14 +1,14 @@
 #!/bin/bash
-# fused histogram: bench-shaped and full-size parity, the round parity subset, default bench
+# Round-2 closing checks at HEAD: GPU suite, 2-rank rehearsals (one GPU,
+# gloo) of config 3 and config 5, each step under its own limit
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-/root/repo}
-cd $R
+cd ${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "bench_shaped" -s > gpurun_out/pytest_k1.log 2>&1
-rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_k1.log; grep "hint_misses" gpurun_out/pytest_k1.log | sed 's/.*sample_retries/sample_retries/' | head -8; tail -2 gpurun_out/pytest_k1.log
-[ $rc -eq 0 ] || { grep -n "Error\|assert\|FAIL" gpurun_out/pytest_k1.log | head -30; exit $rc; }
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_k.json 2> gpurun_out/bench_k.err || { tail -20 gpurun_out/bench_k.err; exit 1; }
-python -c "import json; d=json.load(open('gpurun_out/bench_k.json')); print('ms_per_step', d['ms_per_step'], d['value']/1e6, d['stages_ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_us'], d['roofline']['frac'], d['engine_counters'])"
-timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_device_parity.py tests/test_device_api.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_k2.log 2>&1
-rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_k2.log; tail -2 gpurun_out/pytest_k2.log
-[ $rc -eq 0 ] || { grep -n "Error\|assert\|FAIL" gpurun_out/pytest_k2.log | head -30; exit $rc; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/k_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/k_pytest.log; [ $rc -eq 0 ] || exit $rc
+BENCH_SHARE_DEVICE=1 timeout -k 10 300 python bench.py --gpus 2 --clients 262144 --batch 16384 --steps 10 --warmup 2 --no-cpu-baseline --no-profile > gpurun_out/k_w2.json 2> gpurun_out/k_w2.err
+rc=$?; [ $rc -eq 0 ] || { echo "bench w2 failed $rc"; tail -20 gpurun_out/k_w2.err; exit $rc; }
+tail -1 gpurun_out/k_w2.json
+BENCH_SHARE_DEVICE=1 timeout -k 10 400 python bench.py --config 5 --gpus 2 --servers 2 --steps 32 --warmup 16 --no-cpu-baseline --no-profile > gpurun_out/k_c5w2.json 2> gpurun_out/k_c5w2.err
+rc=$?; [ $rc -eq 0 ] || { echo "bench c5 w2 failed $rc"; tail -20 gpurun_out/k_c5w2.err; exit $rc; }
+tail -1 gpurun_out/k_c5w2.json
