@@ -2113,7 +2113,9 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 // config-3 round)
 constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 #ifndef DMC_APPLY_MINB
-#define DMC_APPLY_MINB 5
+// (apply_one needs ≈164 VGPRs: 2 waves per SIMD, which the grid of two
+// 256-thread blocks per CU needs; a higher bound only warns)
+#define DMC_APPLY_MINB 2
 #endif
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
