@@ -14,7 +14,6 @@
 // pops; see DESIGN.md for why the result is the reference's dispatch order.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -30,6 +29,7 @@
 #include "dmc_device.h"
 #include "dmc_add.h"
 #include "dmc_round.h"
+#include "dmc_sort.h"
 #include "dmc_tracker.h"
 
 using namespace dmc;
@@ -272,12 +272,6 @@ __global__ void k_act_base(Table tb, const uint32_t* acnt, uint64_t* parts) {
 
 constexpr int kActThreads = 1024;
 
-struct MinKey {
-  __host__ __device__ uint64_t operator()(uint64_t a, uint64_t b) const {
-    return a < b ? a : b;
-  }
-};
-
 // block-wide inclusive min-scan of one value per thread (u64 ordered keys)
 __device__ inline uint64_t block_incl_min(uint64_t v, uint64_t* wpart) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -332,6 +326,116 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
     aslot[k] = rq.slot;
     apd[k] = tb.rec[rq.slot].pd;
   }
+}
+
+// The batch positions' scans of the activation bookkeeping, in three
+// launches (dmc_sort.h's scan scheme, fused over the three arrays): pre =
+// exclusive prefix minima of cnew, suf = exclusive prefix minima of cold
+// (stored in reversed position order: suffix minima), and, for activations
+// the device detected (act.flag), the flagged positions compacted into idx,
+// ascending, with their count in *dm.
+struct ActScanPart {
+  uint64_t mn, mo;
+  uint32_t c, pad;
+};
+
+__global__ void __launch_bounds__(kScT)
+k_act_scan_reduce(ActBuf act, uint32_t n, ActScanPart* parts) {
+  __shared__ uint64_t w64[kScT / 64];
+  __shared__ uint32_t w32[kScT / 64];
+  const uint32_t base = blockIdx.x * kScTile;
+  uint64_t a = kMaxKey, b = kMaxKey;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kScItems; ++j) {
+    const uint32_t i = base + j * kScT + threadIdx.x;
+    if (i < n) {
+      a = MinU64::op(a, act.cnew[i]);
+      b = MinU64::op(b, act.cold[i]);
+      if (act.flag) c += act.flag[i];
+    }
+  }
+  uint64_t ta, tb;
+  uint32_t tc;
+  (void)block_excl<MinU64>(a, w64, &ta);
+  (void)block_excl<MinU64>(b, w64, &tb);
+  (void)block_excl<SumU32>(c, w32, &tc);
+  if (threadIdx.x == 0) parts[blockIdx.x] = ActScanPart{ta, tb, tc, 0};
+}
+
+__global__ void __launch_bounds__(kScT) k_act_scan_top(ActScanPart* parts, uint32_t np) {
+  __shared__ uint64_t w64[kScT / 64];
+  __shared__ uint32_t w32[kScT / 64];
+  uint64_t ca = kMaxKey, cb = kMaxKey;
+  uint32_t cc = 0;
+  for (uint32_t c0 = 0; c0 < np; c0 += kScT) {
+    const uint32_t i = c0 + threadIdx.x;
+    const ActScanPart v = i < np ? parts[i] : ActScanPart{kMaxKey, kMaxKey, 0, 0};
+    uint64_t ta, tb;
+    uint32_t tc;
+    const uint64_t ea = block_excl<MinU64>(v.mn, w64, &ta);
+    const uint64_t eb = block_excl<MinU64>(v.mo, w64, &tb);
+    const uint32_t ec = block_excl<SumU32>(v.c, w32, &tc);
+    if (i < np) parts[i] = ActScanPart{MinU64::op(ca, ea), MinU64::op(cb, eb), cc + ec, 0};
+    ca = MinU64::op(ca, ta);
+    cb = MinU64::op(cb, tb);
+    cc += tc;
+  }
+}
+
+__global__ void __launch_bounds__(kScT)
+k_act_scan_down(ActBuf act, uint32_t n, const ActScanPart* parts, uint32_t* idx,
+                uint32_t* dm) {
+  __shared__ uint64_t ta[kScTile], tb[kScTile];
+  __shared__ uint32_t tc[kScTile];
+  __shared__ uint64_t w64[kScT / 64];
+  __shared__ uint32_t w32[kScT / 64];
+  const uint32_t base = blockIdx.x * kScTile;
+#pragma unroll
+  for (int j = 0; j < kScItems; ++j) {
+    const uint32_t i = base + j * kScT + threadIdx.x, l = j * kScT + threadIdx.x;
+    const bool in = i < n;
+    ta[l] = in ? act.cnew[i] : kMaxKey;
+    tb[l] = in ? act.cold[i] : kMaxKey;
+    tc[l] = in && idx ? act.flag[i] : 0u;
+  }
+  __syncthreads();
+  uint64_t va[kScItems], vb[kScItems];
+  uint32_t vc[kScItems];
+  uint64_t a = kMaxKey, b = kMaxKey;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kScItems; ++j) {
+    const uint32_t l = threadIdx.x * kScItems + j;
+    va[j] = a;
+    vb[j] = b;
+    vc[j] = c;
+    a = MinU64::op(a, ta[l]);
+    b = MinU64::op(b, tb[l]);
+    c += tc[l];
+  }
+  const ActScanPart cin = parts[blockIdx.x];
+  uint32_t tot;
+  const uint64_t ea = MinU64::op(cin.mn, block_excl<MinU64>(a, w64));
+  const uint64_t eb = MinU64::op(cin.mo, block_excl<MinU64>(b, w64));
+  const uint32_t ec = cin.c + block_excl<SumU32>(c, w32, &tot);
+#pragma unroll
+  for (int j = 0; j < kScItems; ++j) {
+    const uint32_t l = threadIdx.x * kScItems + j;
+    if (idx && tc[l]) idx[ec + vc[j]] = base + l;  // (flags are 0 / 1)
+    ta[l] = MinU64::op(ea, va[j]);
+    tb[l] = MinU64::op(eb, vb[j]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScItems; ++j) {
+    const uint32_t i = base + j * kScT + threadIdx.x, l = j * kScT + threadIdx.x;
+    if (i < n) {
+      act.pre[i] = ta[l];
+      act.suf[i] = tb[l];
+    }
+  }
+  if (dm && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *dm = cin.c + tot;
 }
 
 // The sequential part of the idle resets, from activation j0 on with the
@@ -1057,7 +1161,11 @@ struct GraphRec {
   uint64_t key = 0;
   uint64_t last_use = 0;
   hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  // two instances, launched alternately: a call returns while its launch's
+  // last kernel may still run, so the next call updates and launches the
+  // other one and never touches an instance in flight
+  hipGraphExec_t exec = nullptr, exec2 = nullptr;
+  bool flip = false;
   hipGraphNode_t param_node = nullptr;
   hipKernelNodeParams kp{};
   hipGraphNode_t param_node2 = nullptr;  // fused add + pull: the round's k_rscan
@@ -1145,9 +1253,13 @@ struct dmc_queue {
   double *act_ip = nullptr, *act_it = nullptr, *act_ipd = nullptr;
   uint32_t* act_islot = nullptr;
   uint32_t* act_flag = nullptr;  // device-detected activations: position flags
+  ActScanPart* act_sparts = nullptr;  // the bookkeeping scans' tile partials
   uint32_t* act_dm = nullptr;    // and their count
   uint32_t* h_actm = nullptr;    // pinned copy of the count
-  bool act_pending = false;      // h_act / h_actm hold a batch the idle mirror has not seen
+  bool act_pending = false;
+  int act_dumps = 0;             // debug: resolve inputs dumped (DMC_DUMP_ACT)
+  void* stage = nullptr;         // small host-to-device lists (ensure_stage)
+  size_t stage_cap = 0;      // h_act / h_actm hold a batch the idle mirror has not seen
   // dmc_client_mark_idle_batch staging (pinned) and device list
   uint32_t* h_mark = nullptr;
   uint32_t* d_mark = nullptr;
@@ -1161,8 +1273,8 @@ struct dmc_queue {
   // radix path (grown on demand)
   uint32_t ecap = 0, dense_hint = 1u << 16;
   DEnt* dense = nullptr;
-  uint32_t *ek32 = nullptr, *sk32 = nullptr;  // 32-bit sort keys
-  uint32_t *eval = nullptr, *sval = nullptr;
+  uint32_t *sa = nullptr, *sb = nullptr;  // the LSD sort's index buffers
+  uint32_t *lcnt = nullptr, *sparts = nullptr;  // its digit counts; scan partials
   uint32_t *gsz = nullptr, *goff = nullptr, *gisp = nullptr, *gpoff = nullptr;
   // add batch buffers
   uint32_t bcap = 0;
@@ -1174,8 +1286,6 @@ struct dmc_queue {
   // decisions (host API)
   uint32_t dcap = 0;
   dmc_decision* d_dec = nullptr;
-  void* temp = nullptr;
-  size_t temp_bytes = 0;
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
@@ -1289,23 +1399,31 @@ void pflush(dmc_queue* q) {
   q->prof_n = 0;
 }
 
-void dfree(void* p) {
-  if (p) (void)hipFree(p);
+int dfree(void* p) {
+  if (!p) return DMC_OK;
+  const hipError_t e = hipFree(p);
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "dmclock_gpu: hipFree failed: %s\n", hipGetErrorString(e));
+    return DMC_EDEVICE;
+  }
+  return DMC_OK;
 }
 
 int graph_replay(dmc_queue* q, GraphRec& g, void** args, void** args2 = nullptr) {
   ++q->ctr.graph_replays;
+  hipGraphExec_t ex = g.flip ? g.exec2 : g.exec;
+  g.flip = !g.flip;
   hipKernelNodeParams kp = g.kp;
   kp.kernelParams = args;
   kp.extra = nullptr;
-  HIP_OK(hipGraphExecKernelNodeSetParams(g.exec, g.param_node, &kp));
+  HIP_OK(hipGraphExecKernelNodeSetParams(ex, g.param_node, &kp));
   if (args2) {
     hipKernelNodeParams kp2 = g.kp2;
     kp2.kernelParams = args2;
     kp2.extra = nullptr;
-    HIP_OK(hipGraphExecKernelNodeSetParams(g.exec, g.param_node2, &kp2));
+    HIP_OK(hipGraphExecKernelNodeSetParams(ex, g.param_node2, &kp2));
   }
-  HIP_OK(hipGraphLaunch(g.exec, q->stream));
+  HIP_OK(hipGraphLaunch(ex, q->stream));
   return DMC_OK;
 }
 
@@ -1353,14 +1471,16 @@ int graph_capture(dmc_queue* q, GraphRec& g, F enqueue, const void* func2 = null
       return DMC_EDEVICE;
     }
   }
-  HIP_OK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
   g.graph = graph;
+  HIP_OK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+  HIP_OK(hipGraphInstantiate(&g.exec2, graph, nullptr, nullptr, 0));
   g.param_node = root;
   return DMC_OK;
 }
 
 void graph_destroy(GraphRec& g) {
   if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.exec2) (void)hipGraphExecDestroy(g.exec2);
   if (g.graph) (void)hipGraphDestroy(g.graph);
   g = GraphRec{};
 }
@@ -1368,7 +1488,8 @@ void graph_destroy(GraphRec& g) {
 // Find (or, on the second sighting, build) the graph for `key`; nullptr if the
 // caller should launch eagerly this time.
 template <typename F>
-GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = nullptr) {
+GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, int* err,
+                    const void* func2 = nullptr) {
   // stage timers run eagerly: event-record nodes inside a replayed graph do
   // not bracket the kernels they were captured between
   if (!q->use_graphs || q->prof_on) return nullptr;
@@ -1386,7 +1507,10 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = n
   GraphRec* slot = &q->graphs[0];
   for (auto& g : q->graphs)
     if (!g.exec || g.last_use < slot->last_use) slot = &g;
-  if (slot->exec) (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
+  if (slot->exec && hipStreamSynchronize(q->stream) != hipSuccess) {  // (see invalidate_graphs)
+    *err = DMC_EDEVICE;
+    return nullptr;
+  }
   graph_destroy(*slot);
   if (graph_capture(q, *slot, enqueue, func2) != DMC_OK) {
     graph_destroy(*slot);
@@ -1402,46 +1526,45 @@ GraphRec* graph_for(dmc_queue* q, uint64_t key, F enqueue, const void* func2 = n
 // stream drains first: a call returns once its round's summary is published,
 // while that round's last kernel may still run (and a graph, its kernel
 // arguments or a buffer must not go away under it).
-void invalidate_graphs(dmc_queue* q) {
-  (void)hipStreamSynchronize(q->stream);
+int invalidate_graphs(dmc_queue* q) {
+  const hipError_t e = hipStreamSynchronize(q->stream);
   pflush(q);
   for (auto& g : q->graphs) graph_destroy(g);
-}
-
-int ensure_temp(dmc_queue* q, size_t need) {
-  if (need <= q->temp_bytes) return DMC_OK;
-  invalidate_graphs(q);
-  if (q->temp) dfree(q->temp);
-  q->temp = nullptr;
-  size_t sz = need + (need >> 2) + 4096;
-  HIP_OK(hipMalloc(&q->temp, sz));
-  q->temp_bytes = sz;
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "dmclock_gpu: stream drain failed: %s\n", hipGetErrorString(e));
+    return DMC_EDEVICE;
+  }
   return DMC_OK;
 }
 
+// The radix path's buffers for `n` dense entries (grown on demand): the
+// entries, the sort's two index buffers, its per-(digit, tile) counts, the
+// scans' tile partials and the group sizes / offsets.
 int ensure_entries(dmc_queue* q, uint32_t n) {
   if (n <= q->ecap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n, 1u << 16);
-  invalidate_graphs(q);
-  dfree(q->dense); dfree(q->ek32); dfree(q->sk32); dfree(q->eval);
-  dfree(q->sval); dfree(q->gsz); dfree(q->goff); dfree(q->gisp); dfree(q->gpoff);
+  int rc = invalidate_graphs(q);
+  for (void** p : {(void**)&q->dense, (void**)&q->sa, (void**)&q->sb, (void**)&q->lcnt,
+                   (void**)&q->sparts, (void**)&q->gsz, (void**)&q->goff,
+                   (void**)&q->gisp, (void**)&q->gpoff}) {
+    if (int e = dfree(*p)) rc = e;
+    *p = nullptr;
+  }
   q->ecap = 0;
+  if (rc) return rc;
+  const uint32_t nblk = scan_tiles(cap);
+  const uint32_t ncnt = 256u * nblk;
   HIP_OK(hipMalloc(&q->dense, sizeof(DEnt) * cap));
-  HIP_OK(hipMalloc(&q->ek32, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->sk32, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->eval, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->sval, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sa, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->sb, sizeof(uint32_t) * cap));
+  HIP_OK(hipMalloc(&q->lcnt, sizeof(uint32_t) * ncnt));
+  HIP_OK(hipMalloc(&q->sparts, sizeof(uint32_t) * scan_tiles(std::max(ncnt, cap))));
   HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->gisp, sizeof(uint32_t) * cap));
   HIP_OK(hipMalloc(&q->gpoff, sizeof(uint32_t) * cap));
   q->ecap = cap;
-  size_t t1 = 0, t2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, q->ek32, q->sk32, q->eval,
-                                           q->sval, (int)cap, 0, 32, q->stream);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, q->gsz, q->goff, (int)cap,
-                                         q->stream);
-  return ensure_temp(q, std::max(t1, t2));
+  return DMC_OK;
 }
 
 // The rank-bin records (kNBR x kBinCapR x 24 B = 48 MiB per queue), allocated
@@ -1456,8 +1579,12 @@ int ensure_brec(dmc_queue* q) {
 int ensure_batch(dmc_queue* q, uint32_t n) {
   if (n <= q->bcap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n, 1024);
-  invalidate_graphs(q);
-  dfree(q->d_reqs); dfree(q->d_rc); dfree(q->apos); dfree(q->aslot);
+  if (int rc = invalidate_graphs(q)) return rc;
+  for (void** p : {(void**)&q->d_reqs, (void**)&q->d_rc, (void**)&q->apos, (void**)&q->aslot}) {
+    if (int rc = dfree(*p)) return rc;
+    *p = nullptr;
+  }
+  q->bcap = 0;
   HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
   HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
   // (padded to whole blocks: k_add_chain loads them before its bounds check)
@@ -1469,8 +1596,10 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
 
 int ensure_dec(dmc_queue* q, uint32_t n) {
   if (n <= q->dcap) return DMC_OK;
-  (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
-  dfree(q->d_dec);
+  HIP_OK(hipStreamSynchronize(q->stream));  // (see invalidate_graphs)
+  if (int rc = dfree(q->d_dec)) return rc;
+  q->d_dec = nullptr;
+  q->dcap = 0;
   uint32_t cap = std::max<uint32_t>(n, 1024);
   HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
   q->dcap = cap;
@@ -1504,7 +1633,9 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
   if (!n) return DMC_OK;
   AddParams ap{d_reqs, d_rc, tick_base, n, 0};
   uint64_t key = (2ull << 56) | n;
-  GraphRec* g = graph_for(q, key, [&] { enqueue_add(q, ap); });
+  int err = DMC_OK;
+  GraphRec* g = graph_for(q, key, [&] { enqueue_add(q, ap); }, &err);
+  if (err) return err;
   if (!g) {
     enqueue_add(q, ap);
     HIP_OK(hipGetLastError());
@@ -1524,6 +1655,7 @@ int activate(dmc_queue* q, uint32_t slot, double t) {
   hipLaunchKernelGGL(k_activate, dim3(1), dim3(kBlock), 0, q->stream, q->tb, slot,
                      t, (const uint64_t*)q->act_min, g);
   pe(q);
+  HIP_OK(hipGetLastError());
   return DMC_OK;
 }
 
@@ -1552,11 +1684,13 @@ int add_host_split(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
 
 int ensure_act(dmc_queue* q, uint32_t n) {
   if (n <= q->acap) return DMC_OK;
-  (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
+  HIP_OK(hipStreamSynchronize(q->stream));  // (see invalidate_graphs)
+  q->acap = 0;
   uint32_t cap = std::max<uint32_t>(n, 4096);
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
   dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot); dfree(q->act_flag);
+  dfree(q->act_sparts);
   if (q->h_act) (void)hipHostFree(q->h_act);
   q->h_act = nullptr;
   HIP_OK(hipMalloc(&q->act_cold, 8ull * cap));
@@ -1576,20 +1710,7 @@ int ensure_act(dmc_queue* q, uint32_t n) {
     HIP_OK(hipMalloc(&q->act_dm, 4));
     HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
   }
-  {
-    size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveScan(nullptr, tb, q->act_cnew, q->act_pre,
-                                            MinKey{}, kMaxKey, (int)cap, q->stream);
-    int rc = ensure_temp(q, tb);
-    if (rc) return rc;
-    tb = 0;
-    (void)hipcub::DeviceSelect::Flagged(nullptr, tb,
-                                        hipcub::CountingInputIterator<uint32_t>(0),
-                                        q->act_flag, q->act_idx, q->act_dm, (int)cap,
-                                        q->stream);
-    rc = ensure_temp(q, tb);
-    if (rc) return rc;
-  }
+  HIP_OK(hipMalloc(&q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap)));
   if (!q->act_extra) {
     HIP_OK(hipMalloc(&q->act_extra, 8));
     const uint64_t mx = kMaxKey;
@@ -1599,6 +1720,18 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   if (!q->act_parts) HIP_OK(hipMalloc(&q->act_parts, 8ull * 2048));
   q->acap = cap;
   return DMC_OK;
+}
+
+// the activation bookkeeping's scans (and, flagged, the compaction) of an
+// n-position batch: three launches
+void act_scans(dmc_queue* q, const ActBuf& act, uint32_t n, bool flagged) {
+  const uint32_t nb = scan_tiles(n);
+  hipLaunchKernelGGL(k_act_scan_reduce, dim3(nb), dim3(kScT), 0, q->stream, act, n,
+                     q->act_sparts);
+  hipLaunchKernelGGL(k_act_scan_top, dim3(1), dim3(kScT), 0, q->stream, q->act_sparts, nb);
+  hipLaunchKernelGGL(k_act_scan_down, dim3(nb), dim3(kScT), 0, q->stream, act, n,
+                     (const ActScanPart*)q->act_sparts, flagged ? q->act_idx : nullptr,
+                     flagged ? q->act_dm : nullptr);
 }
 
 // A batch with activations in one pass (AtLimit Wait / Allow): the host only
@@ -1642,12 +1775,7 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
                      (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
-  size_t tbytes = q->temp_bytes;
-  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cnew, q->act_pre,
-                                          MinKey{}, kMaxKey, (int)n, q->stream);
-  tbytes = q->temp_bytes;
-  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cold, q->act_suf,
-                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  act_scans(q, act, n, false);
   hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(m, 1024)), dim3(kBlock), 0, q->stream,
                      (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
                      q->act_it, q->act_ipd, q->act_islot);
@@ -1693,23 +1821,12 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
                      (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
-  size_t tbytes = q->temp_bytes;
-  (void)hipcub::DeviceSelect::Flagged(q->temp, tbytes,
-                                      hipcub::CountingInputIterator<uint32_t>(0),
-                                      q->act_flag, q->act_idx, q->act_dm, (int)n,
-                                      q->stream);
-  tbytes = q->temp_bytes;
-  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cnew, q->act_pre,
-                                          MinKey{}, kMaxKey, (int)n, q->stream);
-  tbytes = q->temp_bytes;
-  (void)hipcub::DeviceScan::ExclusiveScan(q->temp, tbytes, q->act_cold, q->act_suf,
-                                          MinKey{}, kMaxKey, (int)n, q->stream);
+  act_scans(q, act, n, true);
   hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
                      (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
                      q->act_it, q->act_ipd, q->act_islot);
-  static int dumps = 0;
   const char* dump = q->debug ? getenv("DMC_DUMP_ACT") : nullptr;
-  if (dump && dumps < 4) {
+  if (dump && q->act_dumps < 4) {
     // debug: the resolve's inputs (tools/act_chain_study.py)
     HIP_OK(hipStreamSynchronize(q->stream));
     uint32_t m = 0;
@@ -1733,7 +1850,7 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
       std::fwrite(apdv.data(), 8, m, f);
       std::fclose(f);
     }
-    ++dumps;
+    ++q->act_dumps;
   }
   hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
                      act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
@@ -1822,8 +1939,9 @@ int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
 }
 
 // --------------------------------------------------------------- pull rounds
-// Larger pulls rank through the radix path: the kNBR x kBinCapR rank bins
-// hold about a million entries when balanced.
+// A pull round takes at most kBinRankMaxK pulls (larger k: several rounds
+// at the same `now`): the kNBR x kBinCapR rank bins hold about a million
+// entries when balanced, and 2^18 decisions keep them at a quarter of that.
 constexpr uint32_t kBinRankMaxK = 1u << 18;
 
 uint32_t pow2_at_least(uint32_t x) {
@@ -1835,10 +1953,12 @@ uint32_t pow2_at_least(uint32_t x) {
 // Terminal pull of a Wait/Reject batch: one general do_next_request, which
 // (nothing being eligible) computes min_not_0 over the reservation- and
 // limit-heap tops, :1170-1185.  No-op unless the round is terminal.
-void launch_future(dmc_queue* q, uint64_t seq) {
+int launch_future(dmc_queue* q, uint64_t seq) {
   klaunch(q, DMC_PROF_FUTURE, k_round_future, dim3(std::min(q->step_grid, kFutBlocks)),
           dim3(kFutThreads), 0, q->tb, q->red, q->p.at_limit, q->n_registered, q->sctl,
           q->rd, q->d_hround, q->fut_done, seq);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
 }
 
 // bound infos of distinct slots (dmc_client_bind_info_batch)
@@ -1848,73 +1968,109 @@ __global__ void k_bind_info(BoundInfo* binfo, uint32_t n, const uint32_t* slots,
   if (i < n) binfo[slots[i]] = v[i];
 }
 
+// queue counts of n slots (U1 + delayed: which clients' next add calculates a tag)
+__global__ void k_slot_counts(Table tb, uint32_t n, const uint32_t* slots, uint8_t* out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = tb.sc[slots[i]].count;
+}
+
 double inv_of(double x) { return x == 0.0 ? 0.0 : 1.0 / x; }  // :115-117
 
+// The queue's persistent device staging for small host-to-device lists
+// (bound infos, slot lists), grown on demand.
+int ensure_stage(dmc_queue* q, size_t bytes) {
+  if (bytes <= q->stage_cap) return DMC_OK;
+  HIP_OK(hipStreamSynchronize(q->stream));  // (its last user may still run)
+  if (int rc = dfree(q->stage)) return rc;
+  q->stage = nullptr;
+  q->stage_cap = 0;
+  const size_t cap = std::max<size_t>(bytes + (bytes >> 1), 4096);
+  HIP_OK(hipMalloc(&q->stage, cap));
+  q->stage_cap = cap;
+  return DMC_OK;
+}
+
 // Publish bound infos (U1): slots whose inverses differ from the host shadow
-// are written, a few by direct copies, many by one staged kernel (a slot
-// repeated in the batch takes its last values).
+// are written by one staged kernel (a slot repeated in the batch takes its
+// last values); the shadow takes the new values only once the device has
+// them, so a failed push is retried by the next bind of the same values.
 int bind_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, const double* r,
                const double* w, const double* l) {
   std::vector<uint32_t> ch;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t s = slots[i];
-    const double v[3] = {inv_of(r[i]), inv_of(w[i]), inv_of(l[i])};
-    double* h = &q->binfo_h[3ull * s];
-    if (std::memcmp(h, v, sizeof(v)) == 0) continue;
-    std::memcpy(h, v, sizeof(v));
+  // the last occurrence of each slot wins
+  std::vector<std::pair<uint32_t, uint32_t>> sl(n);
+  for (uint32_t i = 0; i < n; ++i) sl[i] = {slots[i], i};
+  std::stable_sort(sl.begin(), sl.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<BoundInfo> v;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (j + 1 < n && sl[j + 1].first == sl[j].first) continue;
+    const uint32_t s = sl[j].first, i = sl[j].second;
+    const double x[3] = {inv_of(r[i]), inv_of(w[i]), inv_of(l[i])};
+    if (std::memcmp(&q->binfo_h[3ull * s], x, sizeof(x)) == 0) continue;
     ch.push_back(s);
+    v.push_back(BoundInfo{x[0], x[1], x[2], 0.0});
   }
   if (ch.empty()) return DMC_OK;
-  std::sort(ch.begin(), ch.end());
-  ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
-  std::vector<BoundInfo> v(ch.size());
-  for (size_t i = 0; i < ch.size(); ++i) {
-    const double* h = &q->binfo_h[3ull * ch[i]];
-    v[i] = BoundInfo{h[0], h[1], h[2], 0.0};
-  }
-  if (ch.size() <= 16) {
-    for (size_t i = 0; i < ch.size(); ++i)
-      HIP_OK(hipMemcpyAsync(q->binfo + ch[i], &v[i], sizeof(BoundInfo),
-                            hipMemcpyHostToDevice, q->stream));
-    HIP_OK(hipStreamSynchronize(q->stream));
-    return DMC_OK;
-  }
   const uint32_t m = (uint32_t)ch.size();
-  uint32_t* d_s = nullptr;
-  BoundInfo* d_v = nullptr;
-  HIP_OK(hipMalloc(&d_s, 4ull * m));
-  HIP_OK(hipMalloc(&d_v, sizeof(BoundInfo) * m));
+  const size_t sb = (4ull * m + 63) & ~size_t(63);
+  if (int rc = ensure_stage(q, sb + sizeof(BoundInfo) * m)) return rc;
+  uint32_t* d_s = static_cast<uint32_t*>(q->stage);
+  BoundInfo* d_v = reinterpret_cast<BoundInfo*>(static_cast<char*>(q->stage) + sb);
   HIP_OK(hipMemcpyAsync(d_s, ch.data(), 4ull * m, hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipMemcpyAsync(d_v, v.data(), sizeof(BoundInfo) * m, hipMemcpyHostToDevice,
                         q->stream));
   hipLaunchKernelGGL(k_bind_info, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      q->stream, q->binfo, m, (const uint32_t*)d_s, (const BoundInfo*)d_v);
+  HIP_OK(hipGetLastError());
   HIP_OK(hipStreamSynchronize(q->stream));
-  dfree(d_s);
-  dfree(d_v);
+  for (uint32_t j = 0; j < m; ++j) {
+    double* h = &q->binfo_h[3ull * ch[j]];
+    h[0] = v[j].r_inv;
+    h[1] = v[j].w_inv;
+    h[2] = v[j].l_inv;
+  }
   return DMC_OK;
 }
 
 // U1 with a host client_info_f (dmc_queue_set_info_fn): fetch and bind the
-// infos of n slots (unregistered slots are skipped)
+// infos of the distinct registered slots among n.  Delayed mode calls
+// get_cli_info only for a client whose queue is empty (initial_tag,
+// :878-893): slots with queued requests are skipped (their counts read back
+// from the device).
 int fetch_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, size_t stride) {
   if (!q->info_fn || !q->tb.binfo || !n) return DMC_OK;
   std::vector<uint32_t> sl;
-  std::vector<double> r, w, l;
   sl.reserve(n);
-  uint32_t last = 0xffffffffu;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t s = *reinterpret_cast<const uint32_t*>(
         reinterpret_cast<const char*>(slots) + stride * i);
-    if (s == last || s >= q->p.max_clients || !q->reg_h[s]) continue;
-    last = s;
-    double a = 0, b = 0, c = 0;
-    if (q->info_fn(q->info_ctx, s, &a, &b, &c) != 0) return DMC_EINVAL;
-    sl.push_back(s);
-    r.push_back(a);
-    w.push_back(b);
-    l.push_back(c);
+    if (s < q->p.max_clients && q->reg_h[s]) sl.push_back(s);
   }
+  std::sort(sl.begin(), sl.end());
+  sl.erase(std::unique(sl.begin(), sl.end()), sl.end());
+  if (sl.empty()) return DMC_OK;
+  if (q->tb.delayed) {
+    const uint32_t m = (uint32_t)sl.size();
+    const size_t sb = (4ull * m + 63) & ~size_t(63);
+    if (int rc = ensure_stage(q, sb + m)) return rc;
+    uint32_t* d_s = static_cast<uint32_t*>(q->stage);
+    uint8_t* d_c = static_cast<uint8_t*>(q->stage) + sb;
+    std::vector<uint8_t> cnt(m);
+    HIP_OK(hipMemcpyAsync(d_s, sl.data(), 4ull * m, hipMemcpyHostToDevice, q->stream));
+    hipLaunchKernelGGL(k_slot_counts, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       q->stream, q->tb, m, (const uint32_t*)d_s, d_c);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(cnt.data(), d_c, m, hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    size_t o = 0;
+    for (uint32_t j = 0; j < m; ++j)
+      if (!cnt[j]) sl[o++] = sl[j];
+    sl.resize(o);
+  }
+  std::vector<double> r(sl.size()), w(sl.size()), l(sl.size());
+  for (size_t j = 0; j < sl.size(); ++j)
+    if (q->info_fn(q->info_ctx, sl[j], &r[j], &w[j], &l[j]) != 0) return DMC_EINVAL;
   return bind_infos(q, (uint32_t)sl.size(), sl.data(), r.data(), w.data(), l.data());
 }
 
@@ -1950,6 +2106,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
   hipLaunchKernelGGL(k_step_apply, dim3(1), dim3(64), 0, q->stream, tb, q->tick,
                      (const StepCtl*)q->sctl, d_out, idx, q->sched);
   pe(q);
+  HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(q->h_sctl, q->sctl, sizeof(StepCtl), hipMemcpyDeviceToHost,
                         q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
@@ -2006,33 +2163,37 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
             (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
             (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
   } else {
-    uint32_t E = q->ecap;
-    uint32_t gE = grid_for(E, 1024);
+    // the exact LSD sort of the dense entries (dmc_sort.h), then each
+    // entry's group size, two exclusive sums and the decisions
+    const uint32_t E = q->ecap;
+    const uint32_t gE = grid_for(E, 1024);
+    const uint32_t nblk = scan_tiles(E);
     pb(q, DMC_PROF_SORT);
-    hipLaunchKernelGGL(k_dkey32, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E,
-                       (const DEnt*)q->dense, E, q->ek32, q->eval);
-    size_t tbytes = q->temp_bytes;
-    (void)hipcub::DeviceRadixSort::SortPairs(q->temp, tbytes, q->ek32, q->sk32,
-                                             q->eval, q->sval, (int)E, 0, 32,
-                                             q->stream);
-    hipLaunchKernelGGL(k_dfixup, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Round*)q->rd, E, (const uint32_t*)q->sk32, q->sval,
-                       (const DEnt*)q->dense);
+    hipLaunchKernelGGL(k_dcheck, dim3(1), dim3(64), 0, q->stream, q->rd, E);
+    LsdPass ps[16];
+    const int np = lsd_passes(slot_bits(tb.n), ps);
+    const uint32_t* src = nullptr;
+    for (int i = 0; i < np; ++i) {
+      uint32_t* dst = (i & 1) ? q->sb : q->sa;
+      hipLaunchKernelGGL(k_lsd_count, dim3(nblk), dim3(kScT), 0, q->stream,
+                         (const Round*)q->rd, E, (const DEnt*)q->dense, src, nblk,
+                         ps[i].field, ps[i].shift, q->lcnt);
+      scan_excl<SumU32>(q->lcnt, q->lcnt, 256u * nblk, q->sparts, q->stream);
+      hipLaunchKernelGGL(k_lsd_scatter, dim3(nblk), dim3(kScT), 0, q->stream,
+                         (const Round*)q->rd, E, (const DEnt*)q->dense, src, dst, nblk,
+                         ps[i].field, ps[i].shift, (const uint32_t*)q->lcnt);
+      src = dst;
+    }
     pe(q);
     pb(q, DMC_PROF_RANK);
     hipLaunchKernelGGL(k_dsizes, dim3(gE), dim3(kBlock), 0, q->stream,
-                       (const Round*)q->rd, E, E, (const uint32_t*)q->sval,
-                       (const DEnt*)q->dense, q->gsz, q->gisp);
-    tbytes = q->temp_bytes;
-    (void)hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gsz, q->goff, (int)E,
-                                           q->stream);
-    tbytes = q->temp_bytes;
-    (void)hipcub::DeviceScan::ExclusiveSum(q->temp, tbytes, q->gisp, q->gpoff,
-                                           (int)E, q->stream);
-    hipLaunchKernelGGL(k_ddecide, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E,
-                       (const uint32_t*)q->sval, (const DEnt*)q->dense,
-                       (const uint32_t*)q->gsz, (const uint32_t*)q->goff,
-                       (const uint32_t*)q->gpoff, tb.ring);
+                       (const Round*)q->rd, E, E, src, (const DEnt*)q->dense, q->gsz,
+                       q->gisp);
+    scan_excl<SumU32>(q->gsz, q->goff, E, q->sparts, q->stream);
+    scan_excl<SumU32>(q->gisp, q->gpoff, E, q->sparts, q->stream);
+    hipLaunchKernelGGL(k_ddecide, dim3(gE), dim3(kBlock), 0, q->stream, q->rd, E, src,
+                       (const DEnt*)q->dense, (const uint32_t*)q->gsz,
+                       (const uint32_t*)q->goff, (const uint32_t*)q->gpoff, tb.ring);
     pe(q);
   }
   // (its last block ends the round: a round that ran out of work under
@@ -2049,7 +2210,9 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 3) | (sampled ? 4 : 0) |
                  (radix ? 2 : 0);
   CallParams cp{kk, 0, now, out, q->tick, d_result, ++q->round_seq};
-  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); });
+  int err = DMC_OK;
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); }, &err);
+  if (err) return err;
   if (!g) {
     enqueue_round(q, cp, radix);
     HIP_OK(hipGetLastError());
@@ -2108,6 +2271,7 @@ int fast_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                        &q->d_fast->sc, q->fast_done);
     hipLaunchKernelGGL(k_fast_apply, dim3(ga), dim3(kBlock), 0, q->stream, q->tb, now,
                        q->tick, (const StepCtl*)q->sctl, q->d_fast->dec, n, q->sched);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(q->stream));
     ++q->ctr.single_steps;
     const StepCtl c = q->h_fast->sc;  // written before the stream sync
@@ -2164,9 +2328,13 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     const bool retry = retry_radix;
     retry_radix = false;
-    bool radix = q->force_radix || q->radix_batches > 0 || kk > kBinRankMaxK || retry;
+    bool radix = q->force_radix || q->radix_batches > 0 || retry;
+    // a round takes at most kBinRankMaxK pulls (the rank bins' design
+    // size); k beyond that is the next rounds' at the same `now`, exactly
+    // the reference's sequence of pulls
+    const uint32_t kr = std::min(kk, kBinRankMaxK);
     // the first round of a call may end it: its k_rfinish writes d_result
-    dmc_pull_result* dres = (first_round && n_dec == 0) ? d_result : nullptr;
+    dmc_pull_result* dres = (first_round && n_dec == 0 && kr == k) ? d_result : nullptr;
     int rc = DMC_OK;
     if (pre_launched) {  // the fused add + pull graph launched this round
       pre_launched = false;
@@ -2175,7 +2343,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       if (q->radix_batches && !retry) --q->radix_batches;
       rc = radix ? ensure_entries(q, q->dense_hint) : ensure_brec(q);
       if (rc) return rc;
-      rc = launch_round(q, now, kk, d_out + n_dec, dres, radix);
+      rc = launch_round(q, now, kr, d_out + n_dec, dres, radix);
       if (rc) return rc;
     }
     // one host round trip per round, through host-mapped memory
@@ -2184,7 +2352,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (!allow && q->h_rd->terminal && !q->h_rd->overflow) {
       // the round ran out of work: the terminal pull (do_next_request's
       // future / none, :1170-1185) ends it
-      launch_future(q, ++q->round_seq);
+      rc = launch_future(q, ++q->round_seq);
+      if (rc) return rc;
       rc = wait_round(q, q->round_seq);
       if (rc) return rc;
     }
@@ -2310,10 +2479,11 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     n_dec += c.n_dec;
     r.n_priority += c.n_prio;
     r.n_reservation += c.n_dec - c.n_prio;
-    if (n_dec >= k || !c.terminal) {
+    if (n_dec >= k) {
       if (dev_wrote) *dev_wrote = wrote;
       break;
     }
+    if (!c.terminal) continue;  // a capped round took all kr: the next takes the rest
     if (allow) {
       int type;
       double when;
@@ -2475,10 +2645,10 @@ int dmc_queue_destroy(dmc_queue* q) {
                   t.ring,
                   q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist, q->sbn,
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
-                  q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->ek32,
-                  q->sk32, q->eval, q->sval, q->gsz, q->goff, q->gisp, q->gpoff,
+                  q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
+                  q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
-                  q->apblk, q->d_dec, q->temp};
+                  q->apblk, q->d_dec, q->stage};
   for (void* p : ptrs)
     dfree(p);
   if (q->h_round) (void)hipHostFree(q->h_round);
@@ -2635,7 +2805,7 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
     q->mark_ev_live = false;
   }
   if (n > q->mark_cap) {
-    (void)hipStreamSynchronize(q->stream);  // (see invalidate_graphs)
+    HIP_OK(hipStreamSynchronize(q->stream));  // (see invalidate_graphs)
     if (q->h_mark) (void)hipHostFree(q->h_mark);
     dfree(q->d_mark);
     q->h_mark = nullptr;
@@ -3052,7 +3222,9 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       };
       ++q->ctr.fused_calls;
       uint64_t key = (4ull << 56) | ((uint64_t)n << 2) | (use_sample(q, false) ? 2 : 0);
-      GraphRec* gr = graph_for(q, key, enqueue, (const void*)k_rscan);
+      int err = DMC_OK;
+      GraphRec* gr = graph_for(q, key, enqueue, &err, (const void*)k_rscan);
+      if (err) return err;
       if (!gr) {
         enqueue();
         HIP_OK(hipGetLastError());
@@ -3328,7 +3500,7 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_GRAPHS:
       q->use_graphs = value != 0;
-      if (!q->use_graphs) invalidate_graphs(q);
+      if (!q->use_graphs) return invalidate_graphs(q);
       return DMC_OK;
     case DMC_OPT_ACT_SPLIT:
       q->act_split = value != 0;
@@ -3339,7 +3511,7 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
     case DMC_OPT_SAMPLE:
       if (value < 0 || value > 2) return DMC_EINVAL;
       q->sample_mode = (int)value;
-      invalidate_graphs(q);
+      return invalidate_graphs(q);
       return DMC_OK;
     default:
       return DMC_EINVAL;

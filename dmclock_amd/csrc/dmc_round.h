@@ -103,7 +103,7 @@ struct Round {
   uint32_t overflow;     // 1: dense capacity, 2: rank bin (retry on radix)
   uint32_t next_type;    // DMC_NEXT_* of the stopping pull (terminal)
   double when;
-  unsigned long long dmax[2];  // radix path: largest emitted key per phase
+  unsigned long long rsv0[2];  // (unused)
   uint32_t n_cand;       // candidate clients (k_rcand)
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
   uint32_t n_emit;       // rank records emitted (k_rbscan)
@@ -974,26 +974,13 @@ struct EmitV {
       }
       ++acc->nrec;
     } else {
-      // wave-aggregated: one counter add and one max per phase per wave
-      // (massively tied rounds emit every entry here; per-entry atomics on
-      // two addresses serialise)
+      // wave-aggregated: one counter add per wave (massively tied rounds
+      // emit every entry here; per-entry atomics on one address serialise)
       const uint64_t m = __ballot(1);
       const int lane = threadIdx.x & 63;
       const int leader = __ffsll((unsigned long long)m) - 1;
-      const unsigned long long k0 = ph == 0 ? key : 0ull, k1 = ph == 1 ? key : 0ull;
-      unsigned long long mx0 = 0, mx1 = 0;
-      for (uint64_t mm = m; mm; mm &= mm - 1) {
-        const int l = __ffsll((unsigned long long)mm) - 1;
-        const unsigned long long a = __shfl(k0, l), b = __shfl(k1, l);
-        mx0 = a > mx0 ? a : mx0;
-        mx1 = b > mx1 ? b : mx1;
-      }
       uint32_t base = 0;
-      if (lane == leader) {
-        if (mx0) atomicMax(&rd->dmax[0], mx0);
-        if (mx1) atomicMax(&rd->dmax[1], mx1);
-        base = atomicAdd(&rd->dense_n, (uint32_t)__popcll(m));
-      }
+      if (lane == leader) base = atomicAdd(&rd->dense_n, (uint32_t)__popcll(m));
       base = __shfl(base, leader);
       const uint32_t at = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
       if (at < dcap) dense[at] = DEnt{key, slot, pos | ((uint32_t)ph << 31), run, ridx};
@@ -1654,70 +1641,7 @@ k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
 }
 
 // ---------------------------------------------------------------- radix path
-// 32-bit sort keys: phase in the top bit, then (okey - kmin) >> shift with the
-// smallest shift that keeps every key of the phase below 2^31; padding gets
-// 0xffffffff.  Runs of equal 32-bit keys are ordered exactly by k_dfixup.
-__global__ void k_dkey32(Round* rd, uint32_t dcap, const DEnt* dense,
-                         uint32_t E, uint32_t* ek32, uint32_t* eval) {
-  uint32_t nd = rd->dense_n;
-  bool ovf = nd > dcap || rd->overflow;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0 && ovf && !rd->overflow) rd->overflow = 1;
-  uint32_t shift[2];
-  for (int p = 0; p < 2; ++p) {
-    const PhaseSel& ps = rd->ph[p];
-    uint64_t hi = rd->dmax[p];
-    uint64_t range = hi > ps.kmin ? hi - ps.kmin : 0;
-    uint32_t sh = 0;
-    while ((range >> sh) >= 0x7fffffffull) ++sh;
-    shift[p] = sh;
-  }
-  for (uint32_t e = tid; e < E; e += gridDim.x * blockDim.x) {
-    bool real = !ovf && e < nd;
-    uint32_t k32 = 0xffffffffu;
-    if (real) {
-      const DEnt& d = dense[e];
-      int p = d.seq >> 31;
-      uint64_t km = rd->ph[p].kmin;
-      uint64_t v = d.okey > km ? (d.okey - km) >> shift[p] : 0;
-      if (v > 0x7ffffffeull) v = 0x7ffffffeull;
-      k32 = ((uint32_t)p << 31) | (uint32_t)v;
-    }
-    ek32[e] = k32;
-    eval[e] = e;
-  }
-}
-
-__device__ inline bool dent_less(const DEnt& a, const DEnt& b) {
-  uint32_t pa = a.seq >> 31, pb = b.seq >> 31;
-  if (pa != pb) return pa < pb;
-  if (a.okey != b.okey) return a.okey < b.okey;
-  if (a.slot != b.slot) return a.slot < b.slot;
-  return (a.seq & 0x7fffffffu) < (b.seq & 0x7fffffffu);
-}
-
-__global__ void k_dfixup(const Round* rd, uint32_t dcap, const uint32_t* sk32,
-                         uint32_t* sval, const DEnt* dense) {
-  if (rd->overflow) return;
-  uint32_t n = rd->dense_n;
-  if (n > dcap) return;
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n;
-       p += gridDim.x * blockDim.x) {
-    if (p > 0 && sk32[p - 1] == sk32[p]) continue;
-    uint32_t q = p + 1;
-    while (q < n && sk32[q] == sk32[p]) ++q;
-    for (uint32_t a = p + 1; a < q; ++a) {
-      uint32_t v = sval[a];
-      uint32_t b = a;
-      while (b > p && dent_less(dense[v], dense[sval[b - 1]])) {
-        sval[b] = sval[b - 1];
-        --b;
-      }
-      sval[b] = v;
-    }
-  }
-}
-
+// (the dense entries are sorted by dmc_sort.h's exact LSD passes)
 __global__ void k_dsizes(const Round* rd, uint32_t dcap, uint32_t E,
                          const uint32_t* sval, const DEnt* dense, uint32_t* gsz,
                          uint32_t* isp) {

@@ -20,7 +20,9 @@ from ._abi import (DECISION_DTYPE, REQUEST_DTYPE, ClientState, Counters,
                    PullResult, QueueParams, Stats, make_requests)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdmclock_gpu.so")
+# DMC_LIB: an alternative build of the same C-ABI (A/B runs of variants,
+# scripts/gpu_ab_run.sh); default: the in-tree library
+LIB_PATH = os.environ.get("DMC_LIB") or os.path.join(_HERE, "libdmclock_gpu.so")
 _lib = None
 
 _vp = ctypes.c_void_p

@@ -5,7 +5,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 mkdir -p $T/a/b/csrc $T/a/include $R/dmclock_amd/variants
-for f in dmc_round.h dmc_engine.hip dmc_add.h dmc_device.h dmc_tracker.h; do
+for f in $(git -C $R ls-tree --name-only HEAD dmclock_amd/csrc/ | xargs -n1 basename); do
   git -C $R show HEAD:dmclock_amd/csrc/$f > $T/a/b/csrc/$f
 done
 git -C $R show HEAD:include/dmclock_gpu.h > $T/a/include/dmclock_gpu.h

@@ -137,6 +137,150 @@ def test_fused_bench_call_parity_1m_clients():
     qg.close()
 
 
+def _bench_setup(q, tr):
+    """bench.py's prepare(): bulk registration, the pre-population in 1M
+    chunks and the settle pulls in 1M chunks, through the host API"""
+    c = tr.clients
+    q.register(c.slots, c.r, c.w, c.l, c.active)
+    pre = tr.ops[0][1]
+    rcs = [q.add_batch(pre[i:i + (1 << 20)]) for i in range(0, len(pre), 1 << 20)]
+    now, k = tr.ops[1][1], tr.ops[1][2]
+    outs, done = [], 0
+    while done < k:
+        kk = min(k - done, 1 << 20)
+        d, res = q.pull_batch(now, kk)
+        outs.append((d, (res.n_decisions, res.next_type)))
+        done += kk
+    return rcs, outs
+
+
+def test_bench_exact_trace_parity():
+    """bench.py's own workload, call for call:
+    config3_trace(42, 2^20, 33 steps, 64K, depth 4) is make_workload's trace
+    at the default arguments (seed 42, 4,194,304 pre-populated requests, a
+    2,097,152-pull settle in two host calls, then warmup 3 + timed 20 +
+    profiled 10 steps, each one dmc_add_pull_batch_device of 64K adds + 64K
+    pulls replaying the captured graph).  The oracle replays the same calls
+    concurrently (ctypes releases the GIL).  Every add status, decision and
+    result record bit-exact, 4096 sampled client states, and the engine
+    counters: no radix round, no bin overflow, no sample re-run."""
+    import threading
+    import torch
+    from dmclock_amd.gpu import GpuQueue
+    tr = workloads.config3_trace(42, 1 << 20, 33, 1 << 16, depth=4)
+    steps = [(tr.ops[i][1], tr.ops[i + 1][1], tr.ops[i + 1][2])
+             for i in range(2, len(tr.ops), 2)]
+    want = {}
+
+    def oracle():
+        qo = pyoracle.OracleQueue()
+        want["setup"] = _bench_setup(qo, tr)
+        out = []
+        for reqs, now, k in steps:
+            rc = qo.add_batch(reqs)
+            d, res = qo.pull_batch(now, k)
+            out.append((rc, d, (res.n_decisions, res.next_type)))
+        want["steps"] = out
+        want["q"] = qo
+
+    th = threading.Thread(target=oracle)
+    th.start()
+    dev = torch.device("cuda", 0)
+    qg = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+    got_setup = _bench_setup(qg, tr)
+    d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r, _, _ in steps]
+    k = 1 << 16
+    d_rc = torch.zeros(k, dtype=torch.int32, device=dev)
+    d_out = [torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+             for _ in steps]
+    d_res = torch.zeros((len(steps), 24), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    qg.counters(reset=True)
+    rcs = []
+    for i, (reqs, now, kk) in enumerate(steps):
+        # bench.py's step: no synchronisation between the calls
+        qg.add_pull_batch_device(d_reqs[i].data_ptr(), len(reqs), d_rc.data_ptr(), now,
+                                 kk, d_out[i].data_ptr(), d_res[i].data_ptr())
+        qg.sync()  # (the status copy runs on torch's stream)
+        rcs.append(d_rc.clone())
+    ctr = qg.counters()
+    torch.cuda.synchronize()
+    th.join()
+    assert "q" in want, "oracle thread failed"
+    qo = want["q"]
+    assert qo.ties == 0, f"trace has {qo.ties} tied decisions"
+    for a, b in zip(got_setup[0], want["setup"][0]):
+        assert np.array_equal(a, b)
+    for i, ((dg, rg), (do, ro)) in enumerate(zip(got_setup[1], want["setup"][1])):
+        compare_decisions(dg, do, f"settle call {i}")
+        assert rg == ro, (i, rg, ro)
+    n = 0
+    for i, (rc_o, do, ro) in enumerate(want["steps"]):
+        assert np.array_equal(rcs[i].cpu().numpy(), rc_o), i
+        pr = PullResult.from_buffer_copy(d_res[i].cpu().numpy().tobytes())
+        assert (pr.n_decisions, pr.next_type) == ro, (i, pr.n_decisions, ro)
+        dg = d_out[i][:pr.n_decisions * DECISION_DTYPE.itemsize].cpu().numpy() \
+            .view(DECISION_DTYPE)
+        compare_decisions(dg, do, f"step {i}")
+        n += len(do)
+    assert n > 30 * 60000, n
+    assert ctr["fused_calls"] == len(steps), ctr
+    assert ctr["radix_rounds"] == 0 and ctr["bin_overflows"] == 0, ctr
+    assert ctr["sample_retries"] == 0, ctr
+    rng = np.random.default_rng(1)
+    compare_states(qg, qo, rng.choice(tr.clients.slots, 4096, replace=False), "final")
+    assert qg.request_count() == qo.request_count()
+    assert tuple(qg.sched_counts()) == tuple(qo.sched_counts())
+    qo.close()
+    qg.close()
+
+
+def test_fused_device_vs_host_api_200_steps():
+    """A 200-step horizon at bench.py's shape (the key spread keeps growing,
+    DESIGN.md section 6): the fused device call against the host-buffer API
+    on a second queue, every step's decisions and results bit-exact (a
+    property of the engine: both APIs run the same rounds; the oracle's
+    horizon is test_bench_exact_trace_parity's 33 steps)."""
+    import torch
+    from dmclock_amd.gpu import GpuQueue
+    n_steps = 200
+    tr = workloads.config3_trace(7, 1 << 20, n_steps, 1 << 16, depth=4)
+    steps = [(tr.ops[i][1], tr.ops[i + 1][1], tr.ops[i + 1][2])
+             for i in range(2, len(tr.ops), 2)]
+    dev = torch.device("cuda", 0)
+    qa = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+    qb = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+    for q in (qa, qb):
+        _bench_setup(q, tr)
+    k = 1 << 16
+    d_rc = torch.zeros(k, dtype=torch.int32, device=dev)
+    d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(24, dtype=torch.uint8, device=dev)
+    n = 0
+    for i, (reqs, now, kk) in enumerate(steps):
+        d_reqs = torch.from_numpy(reqs.view(np.uint8)).to(dev)
+        torch.cuda.synchronize()
+        qa.add_pull_batch_device(d_reqs.data_ptr(), len(reqs), d_rc.data_ptr(), now, kk,
+                                 d_out.data_ptr(), d_res.data_ptr())
+        qa.sync()
+        rb = qb.add_batch(reqs)
+        db, resb = qb.pull_batch(now, kk)
+        assert np.array_equal(d_rc.cpu().numpy(), rb), i
+        pr = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+        assert (pr.n_decisions, pr.next_type) == (resb.n_decisions, resb.next_type), i
+        da = d_out[:pr.n_decisions * DECISION_DTYPE.itemsize].cpu().numpy() \
+            .view(DECISION_DTYPE)
+        compare_decisions(da, db, f"step {i}")
+        n += len(db)
+    assert n > n_steps * 60000, n
+    rng = np.random.default_rng(2)
+    sl = rng.choice(tr.clients.slots, 2048, replace=False)
+    compare_states(qa, qb, sl, "final")
+    assert qa.counters()["radix_rounds"] == 0
+    qa.close()
+    qb.close()
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 @pytest.mark.parametrize("api", ["device", "host", "mixed"])
 def test_config4_churn_throttled_parity_64k(seed, api):
