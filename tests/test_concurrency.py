@@ -125,6 +125,9 @@ def _rank(rank, world, port, sh, outdir, out_q):
         with ThreadPoolExecutor(S) as pool:
             list(pool.map(prepare, range(S)))
             trk.deliver()
+            # (the deep settle rounds may overflow rank bins and re-run on
+            # the radix path; the steps' counters start here)
+            settle_ctr = [q.counters(reset=True) for q in qs]
             for e in range(sh["epochs"]):
                 i0 = e * sh["steps"]
                 list(pool.map(lambda j: run(j, i0, i0 + sh["steps"]), range(S)))
@@ -143,8 +146,10 @@ def _rank(rank, world, port, sh, outdir, out_q):
             for f in ("xd", "xr", "known"):
                 out[f] = st[f][j]
             out["gd"], out["gr"] = st["gd"], st["gr"]
-            out["counters"] = np.array([qs[j].counters()["radix_rounds"],
-                                        qs[j].counters()["rounds"]])
+            c = qs[j].counters()
+            out["counters"] = np.array([c["radix_rounds"], c["rounds"],
+                                        settle_ctr[j]["rounds"],
+                                        settle_ctr[j]["radix_rounds"]])
             np.savez(os.path.join(outdir, f"srv{s}.npz"), **out)
         for q in qs:
             q.close()
@@ -227,7 +232,10 @@ def _check(sh, outdir, want, et):
             assert np.array_equal(g[f], getattr(et, f)[sl]), (s, f)
         assert np.array_equal(g["known"].astype(bool), et.known[sl]), s
         assert np.array_equal(g["gd"], et.gd) and np.array_equal(g["gr"], et.gr), s
+        # steps: bin-ranked rounds only; the settle: at least four rounds
+        # (k = 2^20 in rounds of at most 2^18 pulls)
         assert g["counters"][0] == 0, ("radix rounds", s, g["counters"])
+        assert g["counters"][2] >= 4, ("settle rounds", s, g["counters"])
     return n_dec
 
 
@@ -261,12 +269,15 @@ def _spawn(world, sh, outdir):
         assert p.exitcode == 0
 
 
+@pytest.mark.timeout(480)
 @pytest.mark.parametrize("world", [1, 2])
 def test_concurrent_queues_trackers_parity(world):
     """world 1: four queues in one process, four host threads; world 2: two
     processes of two queues each, the epoch all-reduce over gloo.  Every
     delta/rho, decision, result and tracker word bit-exact; the k = 2^20
-    settle ran as bin-ranked rounds (no radix round)."""
+    settle ran as rounds of at most 2^18 pulls (deep queues can overflow a
+    rank bin there: those rounds re-run on the radix path, concurrently on
+    the four streams), the steps as bin-ranked rounds."""
     sh = dict(SHAPE)
     with tempfile.TemporaryDirectory() as outdir:
         _spawn(world, sh, outdir)

@@ -154,6 +154,7 @@ def _bench_setup(q, tr):
     return rcs, outs
 
 
+@pytest.mark.timeout(480)
 def test_bench_exact_trace_parity():
     """bench.py's own workload, call for call:
     config3_trace(42, 2^20, 33 steps, 64K, depth 4) is make_workload's trace
