@@ -9,6 +9,7 @@ os.environ["DMC_DEBUG"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))  # (test_concurrency imports it; unused here)
 import numpy as np  # noqa: E402
 
 
