@@ -125,6 +125,7 @@ class Counters(ctypes.Structure):
         ("sample_retries", ctypes.c_uint64),
         ("max_bin", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+        ("bin_splits", ctypes.c_uint64),
     ]
 
     def as_dict(self):

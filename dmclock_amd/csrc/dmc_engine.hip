@@ -1943,6 +1943,9 @@ int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
 // at the same `now`): the kNBR x kBinCapR rank bins hold about a million
 // entries when balanced, and 2^18 decisions keep them at a quarter of that.
 constexpr uint32_t kBinRankMaxK = 1u << 18;
+// rounds of at least this many pulls whose rank bins overflow are re-run as
+// smaller rounds (pull_impl); smaller ones on the radix path
+constexpr uint32_t kSplitMinK = 4096;
 
 uint32_t pow2_at_least(uint32_t x) {
   uint32_t p = 4096;
@@ -2306,6 +2309,8 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
   r.next_type = DMC_NEXT_RETURNING;
   uint32_t n_dec = 0;
   bool allow = q->p.at_limit == DMC_AT_LIMIT_ALLOW;
+  // this call's round size: kBinRankMaxK, lowered after a rank-bin overflow
+  uint32_t kcap = kBinRankMaxK;
   while (n_dec < k) {
     if (q->n_registered == 0) {
       r.next_type = DMC_NEXT_NONE;
@@ -2332,7 +2337,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     // a round takes at most kBinRankMaxK pulls (the rank bins' design
     // size); k beyond that is the next rounds' at the same `now`, exactly
     // the reference's sequence of pulls
-    const uint32_t kr = std::min(kk, kBinRankMaxK);
+    const uint32_t kr = std::min(kk, kcap);
     // the first round of a call may end it: its k_rfinish writes d_result
     dmc_pull_result* dres = (first_round && n_dec == 0 && kr == k) ? d_result : nullptr;
     int rc = DMC_OK;
@@ -2458,12 +2463,28 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       continue;
     }
     if (c.overflow == 2) {
-      // a rank bin outgrew kBinCapR: this round is re-run on the radix path.
-      // An isolated skewed round costs only that; massively tied keys
-      // (overflows in a row) keep the next 1, 2, 4, then 8 calls on it.
-      // k_rbscan left the round's emitted-entry total in dense_n: the retry's
-      // dense buffer is sized for it up front.
+      // a rank bin outgrew kBinCapR (the bins are spread by the first keys'
+      // histogram; deep queues put more entries near the threshold).  A
+      // round of at least kSplitMinK pulls is re-run with fewer, scaled so
+      // that the largest bin would hold 3/4 of its capacity (at most half,
+      // at least 1/16 of the pulls; the rest are the next rounds' at the
+      // same `now`).  Otherwise it is re-run on the radix path: an isolated
+      // skewed round costs only that; massively tied keys (radix re-runs in
+      // a row) keep the next 1, 2, 4, then 8 calls on it.  The overflowed
+      // round's emitted-entry total (dense_n) sizes the radix retry's dense
+      // buffer up front.
       ++q->ctr.bin_overflows;
+      const uint32_t bmax = std::max(c.bin_max[0], c.bin_max[1]);
+      if (kr >= kSplitMinK && bmax > kBinCapR) {
+        uint64_t kn = (uint64_t)kr * (kBinCapR * 3 / 4) / bmax;
+        kn = std::max<uint64_t>(kn, kr / 16);
+        kn = std::min<uint64_t>(kn, kr / 2);
+        if (kn >= kSplitMinK / 2) {
+          kcap = (uint32_t)kn;
+          ++q->ctr.bin_splits;
+          continue;
+        }
+      }
       retry_radix = true;
       q->dense_hint = std::max(q->dense_hint, pow2_at_least(c.dense_n + (c.dense_n >> 2) + 1));
       q->ovf_streak = std::min<uint32_t>(q->ovf_streak + 1, 5);

@@ -1262,10 +1262,18 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     return;
   }
   if (ovf) {
-    // the round is re-run on the radix path: report how many entries it
-    // emitted (the bin counts, overflowed ones included) so that the retry's
-    // dense buffer is sized for them
+    // the round is re-run with fewer pulls or on the radix path: report
+    // how many entries it emitted (the bin counts, overflowed ones included)
+    // so that a radix retry's dense buffer is sized for them, and the
+    // largest bin per phase, from which the host sizes a smaller round
     if (t == 0) {
+      uint32_t m0 = 0, m1 = 0;
+      for (int i = 0; i < NW; ++i) {
+        if (i < NW / 2) m0 = wm[i] > m0 ? wm[i] : m0;
+        else m1 = wm[i] > m1 ? wm[i] : m1;
+      }
+      rd->bin_max[0] = m0;
+      rd->bin_max[1] = m1;
       rd->bin_ovf = 0;
       rd->dense_n = tc;
       rd->overflow = 2;

@@ -339,7 +339,8 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 typedef struct dmc_counters {
   uint64_t rounds;          /* batched pull rounds run (re-runs included)          */
   uint64_t radix_rounds;    /* of which ranked by the radix path                    */
-  uint64_t bin_overflows;   /* rounds aborted by a rank-bin overflow (re-run on the radix path) */
+  uint64_t bin_overflows;   /* rounds aborted by a rank-bin overflow (re-run with fewer pulls,
+                               bin_splits, or on the radix path)                    */
   uint64_t dense_overflows; /* radix rounds re-run with a larger dense buffer       */
   uint64_t single_steps;    /* general single pull_request steps                    */
   uint64_t candidates;      /* candidate clients visited by completed rounds         */
@@ -350,6 +351,7 @@ typedef struct dmc_counters {
   uint64_t sample_retries;  /* rounds re-run because a sampled threshold admitted too few keys */
   uint32_t max_bin;         /* largest rank bin of a bin-ranked round (records)     */
   uint32_t reserved;
+  uint64_t bin_splits;      /* of the overflowed rounds: re-run as a smaller round   */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 

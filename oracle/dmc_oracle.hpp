@@ -264,6 +264,9 @@ class Queue {
     bool idle = true;
     Counter last_tick = 0;
     uint32_t cur_rho = 1, cur_delta = 1;
+    // tie study only (tools/tie_rules.py): when the current front became the
+    // front (a running count of front changes)
+    uint64_t front_since = 0;
     bool has_request() const { return !requests.empty(); }
     const Tag& front() const { return requests.front().tag; }
   };
@@ -316,6 +319,22 @@ class Queue {
     Tag tag;      // the popped tag (before reduction), for tag-level parity
     bool tie = false;  // another client compared equal to the heap top
   };
+
+  // Tie study (test infrastructure, tools/tie_rules.py): with log_ties, every
+  // tied decision records the heap it came from, the client dispatched and
+  // every client tied with it (slot, front arrival, front_since, last_tick).
+  struct TieMember {
+    uint32_t slot;
+    double arrival;
+    uint64_t front_since, last_tick;
+  };
+  struct TieRec {
+    int heap;  // 0 reservation, 1 ready
+    uint32_t chosen;
+    std::vector<TieMember> members;
+  };
+  bool log_ties = false;
+  std::vector<TieRec> tie_log;
 
   Queue(InfoFn info_of, bool delayed, bool dynamic_info, unsigned branching,
         AtLimit at_limit, double reject_threshold, double anticipation)
@@ -416,6 +435,7 @@ class Queue {
 
     c.requests.push_back(Req{tag, client_id, handle});
     if (c.requests.size() == 1) {
+      c.front_since = ++front_seq_;
       resv_.adjust(c);
       limit_.adjust(c);
       ready_.adjust(c);
@@ -436,6 +456,7 @@ class Queue {
     ClientRec& reserv = resv_.top();
     if (reserv.has_request() && reserv.front().reservation <= now) {
       res.tie = track_ties && top_tied(resv_);
+      if (res.tie) log_tie(resv_, 0);
       pop_into(resv_, Phase::reservation, &res);
       ++reserv_sched_count;
       return res;
@@ -455,6 +476,7 @@ class Queue {
     if (readys.has_request() && readys.front().ready &&
         readys.front().proportion < kMaxTag) {
       res.tie = track_ties && top_tied(ready_);
+      if (res.tie) log_tie(ready_, 1);
       pop_ready_into(&res);
       return res;
     }
@@ -649,6 +671,7 @@ class Queue {
     ClientRec& top = heap.top();
     Req req = top.requests.front();
     top.requests.pop_front();
+    if (top.has_request()) top.front_since = ++front_seq_;
     update_next_tag(top, req.tag);
     resv_.demote(top);
     limit_.adjust(top);
@@ -699,6 +722,36 @@ class Queue {
   // True iff some other element compares equal to the heap top.  Elements
   // equal to the root can only be reached through equal ancestors, so a DFS
   // over equal nodes from the root finds them all.
+  // the clients with a request comparing equal to the heap top (the top
+  // first), logged with the state the study's tie rules read
+  template <typename H>
+  void log_tie(const H& heap, int heap_id) {
+    if (!log_ties) return;
+    TieRec rec;
+    rec.heap = heap_id;
+    const ClientRec& top = heap.at(0);
+    rec.chosen = top.client;
+    auto add = [&](const ClientRec& e) {
+      rec.members.push_back(TieMember{e.client, e.front().arrival, e.front_since,
+                                      e.last_tick});
+    };
+    add(top);
+    std::vector<size_t> stack{0};
+    const size_t k = heap.branching();
+    while (!stack.empty()) {
+      size_t i = stack.back();
+      stack.pop_back();
+      for (size_t c = k * i + 1; c <= k * i + k && c < heap.size(); ++c) {
+        const ClientRec& e = heap.at(c);
+        if (!heap.less(top, e) && !heap.less(e, top)) {
+          if (e.has_request()) add(e);
+          stack.push_back(c);
+        }
+      }
+    }
+    tie_log.push_back(std::move(rec));
+  }
+
   template <typename H>
   bool top_tied(const H& heap) const {
     const ClientRec& top = heap.at(0);
@@ -725,6 +778,7 @@ class Queue {
   double reject_threshold_;
   double antic_;
   Counter tick_ = 0;
+  uint64_t front_seq_ = 0;  // tie study: front changes so far
   std::map<uint32_t, RecRef> client_map_;
   IndHeap<RecRef, ClientRec, ResvCmp> resv_;
   IndHeap<RecRef, ClientRec, LimCmp> limit_;

@@ -155,6 +155,36 @@ int dmo_pull_batch(void* h, double now, uint32_t k, dmc_decision* out,
 
 uint64_t dmo_ties(void* h) { return static_cast<OQueue*>(h)->ties; }
 
+// Tie study (tools/tie_rules.py): log every tied decision's tied set.
+void dmo_tie_log_enable(void* h, int on) { static_cast<OQueue*>(h)->q->log_ties = on != 0; }
+
+// The log since the last read, flattened into 64-bit words: per tie [heap,
+// chosen slot, m] then m members [slot, arrival bits, front_since,
+// last_tick]; returns the words needed (reads and clears only if cap
+// suffices).
+uint64_t dmo_tie_log_read(void* h, uint64_t* out, uint64_t cap) {
+  auto& log = static_cast<OQueue*>(h)->q->tie_log;
+  uint64_t need = 0;
+  for (auto& t : log) need += 3 + 4 * t.members.size();
+  if (!out || cap < need) return need;
+  uint64_t o = 0;
+  for (auto& t : log) {
+    out[o++] = uint64_t(t.heap);
+    out[o++] = t.chosen;
+    out[o++] = t.members.size();
+    for (auto& m : t.members) {
+      uint64_t a;
+      std::memcpy(&a, &m.arrival, 8);
+      out[o++] = m.slot;
+      out[o++] = a;
+      out[o++] = m.front_since;
+      out[o++] = m.last_tick;
+    }
+  }
+  log.clear();
+  return need;
+}
+
 uint64_t dmo_request_count(void* h) {
   return static_cast<OQueue*>(h)->q->request_count();
 }

@@ -50,6 +50,8 @@ def lib():
             "dmo_pull_batch": (_i32, [_vp, _f64, _u32, _vp,
                                       ctypes.POINTER(PullResult)]),
             "dmo_ties": (_u64, [_vp]),
+            "dmo_tie_log_enable": (None, [_vp, _i32]),
+            "dmo_tie_log_read": (_u64, [_vp, _vp, _u64]),
             "dmo_request_count": (_u64, [_vp]),
             "dmo_client_count": (_u64, [_vp]),
             "dmo_empty": (_i32, [_vp]),
@@ -171,6 +173,28 @@ class OracleQueue:
     @property
     def ties(self):
         return self.L.dmo_ties(self.h)
+
+    def tie_log(self, on=True):
+        """tie study: log every tied decision's tied set"""
+        self.L.dmo_tie_log_enable(self.h, int(on))
+
+    def read_tie_log(self):
+        """[(heap, chosen slot, [(slot, front arrival, front_since,
+        last_tick), ...])] since the last read (the top first)"""
+        n = self.L.dmo_tie_log_read(self.h, None, 0)
+        buf = np.zeros(max(n, 1), np.uint64)
+        self.L.dmo_tie_log_read(self.h, _ptr(buf), n)
+        out, i = [], 0
+        while i < n:
+            heap, chosen, m = int(buf[i]), int(buf[i + 1]), int(buf[i + 2])
+            i += 3
+            mem = []
+            for _ in range(m):
+                mem.append((int(buf[i]), float(buf[i + 1:i + 2].view(np.float64)[0]),
+                            int(buf[i + 2]), int(buf[i + 3])))
+                i += 4
+            out.append((heap, chosen, mem))
+        return out
 
     def request_count(self):
         return self.L.dmo_request_count(self.h)

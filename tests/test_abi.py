@@ -69,6 +69,7 @@ int main(void) {
   printf("dmc_stats %zu\n", sizeof(dmc_stats));
   printf("dmc_counters %zu\n", sizeof(dmc_counters));
   P(dmc_counters, single_steps); P(dmc_counters, max_bin);
+  P(dmc_counters, bin_splits);
   P(dmc_request, time); P(dmc_request, delta); P(dmc_request, handle);
   P(dmc_decision, tag_r); P(dmc_decision, slot); P(dmc_decision, flags);
   P(dmc_queue_params, reject_threshold); P(dmc_queue_params, device);
@@ -96,6 +97,7 @@ def test_struct_layouts_match_header(tmp_path):
     assert out["dmc_counters"] == ctypes.sizeof(_abi.Counters)
     assert out["dmc_counters.single_steps"] == _abi.Counters.single_steps.offset
     assert out["dmc_counters.max_bin"] == _abi.Counters.max_bin.offset
+    assert out["dmc_counters.bin_splits"] == _abi.Counters.bin_splits.offset
     assert out["dmc_request.time"] == _abi.REQUEST_DTYPE.fields["time"][1]
     assert out["dmc_request.delta"] == _abi.REQUEST_DTYPE.fields["delta"][1]
     assert out["dmc_request.handle"] == _abi.REQUEST_DTYPE.fields["handle"][1]

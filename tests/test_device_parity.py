@@ -253,6 +253,7 @@ def test_fused_device_vs_host_api_200_steps():
     qb = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
     for q in (qa, qb):
         _bench_setup(q, tr)
+    qa.counters(reset=True)
     k = 1 << 16
     d_rc = torch.zeros(k, dtype=torch.int32, device=dev)
     d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
@@ -277,7 +278,8 @@ def test_fused_device_vs_host_api_200_steps():
     rng = np.random.default_rng(2)
     sl = rng.choice(tr.clients.slots, 2048, replace=False)
     compare_states(qa, qb, sl, "final")
-    assert qa.counters()["radix_rounds"] == 0
+    c = qa.counters()
+    assert c["radix_rounds"] == 0 and c["bin_overflows"] == 0, c
     qa.close()
     qb.close()
 

@@ -127,19 +127,38 @@ def study_sim(conf_path, jitter, t0, seed):
     ties = 0
     firsts = []
     differ = 0
+    # in virtual time, over all servers: the first tied decision and the
+    # first decision where the two dispatch sequences differ (a closed loop
+    # couples the servers through the clients, so a difference on one server
+    # can stem from a tie on another: only a global first difference at or
+    # after the global first tie rules out a non-tie divergence)
+    t_tie = t_diff = None
     for s in range(len(o.log_dec)):
         do = [r for _, r in o.log_dec[s]]
         dg = [r for _, r in g.log_dec[s]]
+        to = [t for t, _ in o.log_dec[s]]
+        tg = [t for t, _ in g.log_dec[s]]
         tf = [i for i, r in enumerate(do) if int(r["flags"]) & 1]
         ties += len(tf)
         n = min(len(do), len(dg))
-        d = [i for i in range(n) if (int(do[i]["slot"]), int(do[i]["phase"])) !=
-             (int(dg[i]["slot"]), int(dg[i]["phase"]))]
-        differ += len(d) + abs(len(do) - len(dg))
+        d = [i for i in range(n) if (int(do[i]["slot"]), int(do[i]["phase"]),
+                                     to[i]) != (int(dg[i]["slot"]), int(dg[i]["phase"]),
+                                                tg[i])]
+        if len(do) != len(dg) and not d:
+            d = [n]
+        differ += len([i for i in d if i < n]) + abs(len(do) - len(dg))
+        if tf:
+            t = to[tf[0]]
+            t_tie = t if t_tie is None else min(t_tie, t)
+        if d:
+            i = d[0]
+            t = min(to[i] if i < len(to) else np.inf, tg[i] if i < len(tg) else np.inf)
+            t_diff = t if t_diff is None else min(t_diff, t)
         if tf or d:
             firsts.append((s, tf[0] if tf else None, d[0] if d else None))
     before_tie_ok = all(fd is None or (ft is not None and fd >= ft)
                         for _, ft, fd in firsts)
+    global_ok = t_diff is None or (t_tie is not None and t_diff >= t_tie)
     so, sg = o.stats(), g.stats()
     l1_res = int(np.abs(so["reservation_ops"] - sg["reservation_ops"]).sum())
     l1_prio = int(np.abs(so["priority_ops"] - sg["priority_ops"]).sum())
@@ -149,6 +168,9 @@ def study_sim(conf_path, jitter, t0, seed):
             "tied_frac": ties / max(total, 1),
             "servers_with_a_tie_or_difference": len(firsts),
             "sequences_identical_until_first_tie": before_tie_ok,
+            "first_tie_virtual_time": t_tie,
+            "first_difference_virtual_time": t_diff,
+            "no_difference_before_the_first_tie_anywhere": global_ok,
             "differ_positions": differ, "differ_positions_frac": differ / max(total, 1),
             "reservation_ops_oracle": int(so["reservation_ops"].sum()),
             "reservation_ops_engine": int(sg["reservation_ops"].sum()),
