@@ -2162,9 +2162,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
-    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
+    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd, tb,
             (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
-            (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
+            (const BRecR*)q->brec, (const PostRec*)q->post, q->decof,
+            q->debug ? q->dbg_wtime : nullptr);
   } else {
     // the exact LSD sort of the dense entries (dmc_sort.h), then each
     // entry's group size, two exclusive sums and the decisions
