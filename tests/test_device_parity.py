@@ -278,8 +278,11 @@ def test_fused_device_vs_host_api_200_steps():
     rng = np.random.default_rng(2)
     sl = rng.choice(tr.clients.slots, 2048, replace=False)
     compare_states(qa, qb, sl, "final")
+    # (over 200 steps the key spread grows: an overflowed rank bin re-runs
+    # the round smaller, bin_splits; none needs the radix path)
     c = qa.counters()
-    assert c["radix_rounds"] == 0 and c["bin_overflows"] == 0, c
+    assert c["radix_rounds"] == 0, c
+    assert c["bin_overflows"] == c["bin_splits"] <= 4, c
     qa.close()
     qb.close()
 
