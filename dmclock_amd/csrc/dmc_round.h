@@ -55,7 +55,10 @@ constexpr int kNBPhase = kNBR / 2;
 // Same-address atomics from every block of a launch serialise at the memory
 // side (~12 ns each): the histogram is sharded 8 ways (block % 8, one shard
 // per XCD) and the pick combines the shards.
-constexpr int kShards = 8;
+#ifndef DMC_HIST_SHARDS
+#define DMC_HIST_SHARDS 8
+#endif
+constexpr int kShards = DMC_HIST_SHARDS;
 constexpr uint32_t kBinCapR = 512;      // entries per rank bin (2 per thread of k_rrank)
 constexpr uint32_t kNoneR = 0xffffffffu;
 constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
@@ -538,7 +541,10 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // iteration with every key load issued before the first LDS atomic; the
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
-constexpr int kHistBlocksSampled = 32;  // 131,072 sampled slots of 1M: 4 per thread
+#ifndef DMC_HIST_BLOCKS
+#define DMC_HIST_BLOCKS 32
+#endif
+constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of 1M: 4 per thread
                                         // (16 and 64 blocks measured no faster)
 __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
                           uint32_t* sbn, int sampled);
