@@ -867,6 +867,14 @@ __device__ inline uint32_t rank_bin_r(uint64_t k, const PhaseSel& ps, int p,
   return (e & 0xffffu) + sub;
 }
 
+// The rank bin of an entry key rounded down to its 32-bit quantum (key32):
+// monotone in the key, and a candidate's first record -- whose key is the
+// first key k_remit streams quantized -- gets its bin before its walk.
+__device__ inline uint32_t rank_bin_q(uint64_t k, const PhaseSel& ps, int p,
+                                      const uint32_t* sbn) {
+  return rank_bin_r(k & 0xffffffff00000000ull, ps, p, sbn);
+}
+
 // Rank-bin record of one entry: the order key (phase by bin, okey, slot,
 // queue position), the group's run (P) and the entry's ring index.  The
 // decision offset and tie flag are written into the ring entry itself
@@ -918,6 +926,12 @@ struct PostRec {
   uint32_t pad1[7];
 };
 static_assert(sizeof(PostRec) == 128, "PostRec must be two 64-byte lines");
+// (k_remit stores it in 16-byte pieces in this order)
+static_assert(offsetof(PostRec, prev_r) == 24 && offsetof(PostRec, r2) == 40 &&
+                  offsetof(PostRec, bits) == 48 && offsetof(PostRec, cand) == 52 &&
+                  offsetof(PostRec, handle1) == 64 && offsetof(PostRec, p1) == 80 &&
+                  offsetof(PostRec, cost1) == 96,
+              "PostRec layout");
 
 // Dense entry (radix path).
 struct DEnt {
@@ -941,6 +955,7 @@ struct EmitAcc {
   uint32_t run0 = 0;                // its run (P group)
   uint32_t pos0 = 0;                // the first pop's queue position
   bool prio0 = false;               // ... and kind
+  bool pre = false;                 // b0 / at0 reserved before the walk
 };
 
 struct EmitV {
@@ -961,13 +976,26 @@ struct EmitV {
   __device__ void put(uint64_t key, uint32_t pos, uint32_t run) {
     uint32_t ridx = rbase + ((head + pos) & qmask);
     if (brec) {
-      uint32_t b = rank_bin_r(key, *ps, ph, sbn);
+      const uint32_t b = rank_bin_q(key, *ps, ph, sbn);
+      unsigned long long* bc = reinterpret_cast<unsigned long long*>(bcount);
+      if (acc->nrec == 0 && acc->pre) {
+        // the first record: its place was reserved before the walk with a
+        // group size of 1; a P group's run is added now (rare), and a bin
+        // that differs from the reserved one (cannot happen: the same
+        // quantized key) fails the round safely
+        if (b != acc->b0) atomicOr(&rd->bin_ovf, 1u);
+        if (ph == 1 && run) atomicAdd(bc + b, (unsigned long long)run << 32);
+        if (acc->at0 >= kBinCapR) atomicOr(&rd->bin_ovf, 1u);
+        acc->key0 = key;
+        acc->run0 = run;
+        ++acc->nrec;
+        return;
+      }
       // one 64-bit atomic per record: the bin's record count in the low word,
       // its group sizes in the high word (bcount: kNBR 8-byte counters)
       const unsigned long long inc =
           ((unsigned long long)(ph == 0 ? 1u : 1u + run) << 32) | 1ull;
-      const uint32_t at = (uint32_t)atomicAdd(
-          reinterpret_cast<unsigned long long*>(bcount) + b, inc);
+      const uint32_t at = (uint32_t)atomicAdd(bc + b, inc);
       if (at >= kBinCapR) {
         atomicOr(&rd->bin_ovf, 1u);  // read by the last block (memory side)
       } else if (acc->nrec == 0) {
@@ -1069,14 +1097,14 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
 constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2: no faster)
 #ifndef DMC_EMIT_STAGE_THREADS
-#define DMC_EMIT_STAGE_THREADS 512
+#define DMC_EMIT_STAGE_THREADS 448  // (LDS: 160 KB per block with the key array)
 #endif
 constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a staging slice
 __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
                                 PostRec* post, uint32_t* decof,
-                                ReqEntry* st, uint64_t* ck = nullptr) {
+                                ReqEntry* st, uint32_t key32_0, uint64_t* ck = nullptr) {
   // ck (debug): [0] entry, [1] client record and ring staged, [2] walks and
   // their rank records done
   if (ck) ck[0] = wall_clock64();
@@ -1085,17 +1113,30 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
   const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
+  EmitAcc acc;
+  acc.ci = ci;
   const CView cv = cand_view(tb, c);
   const double prev_r = tb.rec[s].prev_r;  // (the inverses' line)
   const uint32_t h = cv.h;
   const RingView rv = stage_ring<kEmitStage>(tb, s, h, cv.c, st);
+#ifndef DMC_EMIT_PRERESERVE
+#define DMC_EMIT_PRERESERVE 1
+#endif
+  if (DMC_EMIT_PRERESERVE && brec) {
+    // the first record's rank-bin place, reserved before the walk (its key
+    // is the first key of the candidate's first phase, key32_0 is its
+    // quantum): the atomic's latency overlaps the walk
+    const int ph0 = c.cr() ? 0 : 1;
+    acc.b0 = rank_bin_q((uint64_t)key32_0 << 32, rd->ph[ph0], ph0, sbn);
+    acc.at0 = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long*>(bcount) + acc.b0,
+                                  (1ull << 32) | 1ull);
+    acc.pre = true;
+  }
   if (ck) {
     keep(cv.rinv);
     keep(cv.pd);
     ck[1] = wall_clock64();
   }
-  EmitAcc acc;
-  acc.ci = ci;
   if (c.cr()) {
     EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
@@ -1119,47 +1160,49 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
   const bool fast = brec && !tb.delayed && acc.nrec == 1 && acc.pos0 == 0 &&
                     acc.at0 < kBinCapR && (run == 0 || (run == 1 && acc.prio0));
   if (fast) {
-    PostRec pr;
+    // (stored piecewise as computed: the record, then the PostRec's lines --
+    // a whole PostRec and BRecR held in registers at once spill)
     const uint32_t cc = cv.c;
     const bool prio = acc.prio0;
-    // the pop's payload: queue position 0 as stored (immediate mode: a
-    // priority pop with no earlier one has its stored r)
-    const ReqEntry e0 = rv.at(0);
-    const double off = prio ? resv_offset(cv.rinv, e0.cost, e0.rho) : 0.0;
-    pr.fr = pr.fpk = pr.fl = pr.r2 = 0.0;
-    pr.bits = (prio ? 1u : 0u) | (run ? 4u : 0u);
-    if (run) {
-      // the run's pop: queue position 1 with its reduced r (its decision tag)
-      const ReqEntry e1 = rv.at(1);
-      pr.handle1 = e1.handle;
-      pr.r1 = __dsub_rn(e1.r, off);
-      pr.p1 = e1.p;
-      pr.l1 = e1.l;
-      pr.cost1 = e1.cost;
-    }
-    if (cc >= 2 + run) {
-      const ReqEntry ef = rv.at(1 + run);  // staged: 1 + run < kEmitStage
-      pr.fr = prio ? __dsub_rn(ef.r, off) : ef.r;
-      pr.fpk = __dadd_rn(ef.p, cv.pd);
-      pr.fl = ef.l;
-      if (ef.l <= now) pr.bits |= 2u;
-    }
-    if (prio && !run && cc >= 3) pr.r2 = __dsub_rn(rv.r_at(2), off);
-    pr.prev_r = prio ? __dsub_rn(prev_r, off) : prev_r;
-    pr.off = off;
-    pr.cand = (uint32_t)c.fb | ((uint32_t)c.m << 8) | ((uint32_t)c.h << 16) |
-              ((uint32_t)c.c << 24);
-    pr.pad[0] = pr.pad[1] = 0;
-    brec[(size_t)acc.b0 * kBinCapR + acc.at0] =
-        BRecR{BKey{acc.key0, s, 0u, run, s * tb.q + h}, ci | kFastRec, e0.cost, e0.handle,
-              e0.r, e0.p, e0.l};
+    double off = 0.0;
     {
-      // the second line only with a run
-      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&pr);
-      ulonglong2* dst = reinterpret_cast<ulonglong2*>(post + ci);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < 4 || run) dst[j] = src[j];
+      // the pop's payload: queue position 0 as stored (immediate mode: a
+      // priority pop with no earlier one has its stored r)
+      const ReqEntry e0 = rv.at(0);
+      if (prio) off = resv_offset(cv.rinv, e0.cost, e0.rho);
+      brec[(size_t)acc.b0 * kBinCapR + acc.at0] =
+          BRecR{BKey{acc.key0, s, 0u, run, s * tb.q + h}, ci | kFastRec, e0.cost, e0.handle,
+                e0.r, e0.p, e0.l};
+    }
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(post + ci);
+    {
+      double fr = 0.0, fpk = 0.0, fl = 0.0, r2 = 0.0;
+      uint32_t bits = (prio ? 1u : 0u) | (run ? 4u : 0u);
+      if (cc >= 2 + run) {
+        const ReqEntry ef = rv.at(1 + run);  // staged: 1 + run < kEmitStage
+        fr = prio ? __dsub_rn(ef.r, off) : ef.r;
+        fpk = __dadd_rn(ef.p, cv.pd);
+        fl = ef.l;
+        if (ef.l <= now) bits |= 2u;
+      }
+      if (prio && !run && cc >= 3) r2 = __dsub_rn(rv.r_at(2), off);
+      const double pr_prev = prio ? __dsub_rn(prev_r, off) : prev_r;
+      const uint32_t cw = (uint32_t)c.fb | ((uint32_t)c.m << 8) | ((uint32_t)c.h << 16) |
+                          ((uint32_t)c.c << 24);
+      // PostRec line 1: fr, fpk | fl, prev_r | off, r2 | bits, cand, pad
+      dst[0] = make_ulonglong2(dbits(fr), dbits(fpk));
+      dst[1] = make_ulonglong2(dbits(fl), dbits(pr_prev));
+      dst[2] = make_ulonglong2(dbits(off), dbits(r2));
+      dst[3] = make_ulonglong2((unsigned long long)bits | ((unsigned long long)cw << 32), 0ull);
+    }
+    if (run) {
+      // line 2, the run's pop: queue position 1 with its reduced r (its
+      // decision tag): handle1, r1 | p1, l1 | cost1
+      const ReqEntry e1 = rv.at(1);
+      dst[4] = make_ulonglong2(e1.handle, dbits(__dsub_rn(e1.r, off)));
+      dst[5] = make_ulonglong2(dbits(e1.p), dbits(e1.l));
+      dst[6] = make_ulonglong2((unsigned long long)e1.cost, 0ull);
+      dst[7] = make_ulonglong2(0ull, 0ull);
     }
     decof[ci] = kNoDec;
   } else {
@@ -1189,7 +1232,12 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   constexpr int per = kNBR / THREADS;
   constexpr int NW = THREADS / 64;
   __shared__ uint32_t wc[NW], wz[NW], wp[NW], wm[NW];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, w = t >> 6;
+  // (opaque here: the shuffles' lane addresses are computed in this tail,
+  // not hoisted to the kernel's start and held -- spilled -- across k_remit's
+  // walks)
+  int lane = t & 63;
+  asm volatile("" : "+v"(lane));
   uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0, lm = 0;
   // plain loads behind the last block's agent-scope acquire (the counters
   // were filled with memory-side atomics), cleared with plain stores for
@@ -1239,8 +1287,12 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   // the largest bin (max); lane 63 holds the wave totals
   uint32_t ic = lc, iz = lz, ip = lp, im = lm;
   for (int d = 1; d < 64; d <<= 1) {
-    uint32_t oc = __shfl_up(ic, d), oz = __shfl_up(iz, d), op = __shfl_up(ip, d),
-             om = __shfl_up(im, d);
+    // (ds_bpermute from this tail's own lane id: see `lane` above)
+    const int src = (lane >= d ? lane - d : lane) << 2;
+    uint32_t oc = __builtin_amdgcn_ds_bpermute(src, ic),
+             oz = __builtin_amdgcn_ds_bpermute(src, iz),
+             op = __builtin_amdgcn_ds_bpermute(src, ip),
+             om = __builtin_amdgcn_ds_bpermute(src, im);
     if (lane >= d) {
       ic += oc;
       iz += oz;
@@ -1336,7 +1388,8 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 // The block compacts its candidates in LDS (about 270 of its 4096 slots in
 // a config-3 round) and appends them to the candidate list with one atomic;
 // its first threads then walk one candidate each, full waves, with the
-// rank-bin table staged in LDS.  Bin-rank path: the last block to finish
+// rank-bin table staged in LDS; a candidate's first record reserves its
+// rank-bin place before its walk (rank_bin_q).  Bin-rank path: the last block to finish
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
 #ifndef DMC_EMIT_THREADS
@@ -1357,6 +1410,10 @@ k_remit(Table tb, Round* rd, const uint2* k32,
   // compacted [3] walks done [4] ticket taken
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
   __shared__ CandRec bl[kEmitChunk];
+  __shared__ uint32_t bk[kEmitChunk];  // their first phase's quantized first key
+  // each thread's slot predicates and flags, parked for the mark settling
+  // after the walks (fewer registers live across them: no spills)
+  __shared__ uint2 s_fb[kEmitThreads];
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
   __shared__ uint32_t wsum[kEmitThreads / 64];
@@ -1450,12 +1507,20 @@ k_remit(Table tb, Round* rd, const uint2* k32,
 #pragma unroll
     for (int j = 0; j < kEmitPer; ++j) {
       const uint32_t b = (bits >> (2 * j)) & 3u;
-      if (b)
+      if (b) {
+        bk[o] = (b & 1u) ? kr[j] : kp[j];
         bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), (uint8_t)mt[j],
                           (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
+      }
     }
   }
   if (threadIdx.x == 0) s_tot = btot;
+  {
+    uint32_t fw = 0;
+#pragma unroll
+    for (int j = 0; j < kEmitPer; ++j) fw |= (uint32_t)f[j] << (8 * j);
+    s_fb[threadIdx.x] = make_uint2(bits, fw);
+  }
   __syncthreads();
   // The candidate count (a statistic) and the sampled counts are published
   // (same-address atomics, serialised over the grid) by the last wave, which
@@ -1481,7 +1546,7 @@ k_remit(Table tb, Round* rd, const uint2* k32,
         tb, rd, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
         threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
                                                   : nullptr,
-        eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
+        bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
     atomicAdd(&s_ec[cat], 1u);
   }
   __syncthreads();
@@ -1492,10 +1557,18 @@ k_remit(Table tb, Round* rd, const uint2* k32,
   if (threadIdx.x == 0) bcand[blockIdx.x] = tot;
   // non-candidates settle their pending limit-scan marks (after the walks:
   // a store ahead of a walk's loads would delay them)
+  {
+    uint32_t ti = threadIdx.x;
+    asm volatile("" : "+v"(ti));  // (its LDS address recomputed here, not held)
+    const uint2 fb = s_fb[ti];
+    const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
 #pragma unroll
-  for (int j = 0; j < kEmitPer; ++j)
-    if (s0 + j < n && !((bits >> (2 * j)) & 3u) && (f[j] & F_PMARK))
-      tb.sc[s0 + j].flags = (uint8_t)((f[j] & ~F_PMARK) | (p_runs ? F_READY : 0));
+    for (int j = 0; j < kEmitPer; ++j) {
+      const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
+      if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
+        tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
+    }
+  }
   if (!brec) return;
   // ticket: the block's bin atomics have completed (every wave waits for its
   // own) before one lane takes it; the last block computes the prefixes.
