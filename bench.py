@@ -522,13 +522,14 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": ("config3: single server queue, synthetic 1M "
-                                "clients mixed r/w/l, 64K adds + 64K pulls "
-                                "per step") if args.config == 3 else
-                               ("config4: config 3 + do_clean idle marking of "
-                                f"{args.idle_frac:.0%} of the clients before each "
-                                "step (activations with the prop_delta reset) "
-                                "+ 10% limit-throttled tenants"),
+        "config": {"workload": (f"config3: single server queue, synthetic "
+                                f"{args.clients} clients mixed r/w/l, {args.batch} "
+                                f"adds + {k} pulls per step") if args.config == 3 else
+                               (f"config4: config 3 ({args.clients} clients, "
+                                f"{args.batch} adds + {k} pulls per step) + "
+                                f"do_clean idle marking of {args.idle_frac:.0%} of "
+                                "the clients before each step (activations with the "
+                                "prop_delta reset) + 10% limit-throttled tenants"),
                    "clients": args.clients, "adds_per_step": args.batch,
                    "pulls_per_step": k, "prepopulated": len(pre),
                    "settle_pulls": settle,

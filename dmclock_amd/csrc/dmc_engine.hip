@@ -2037,11 +2037,13 @@ int bind_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, const double* r,
 }
 
 // U1 with a host client_info_f (dmc_queue_set_info_fn): fetch and bind the
-// infos of the distinct registered slots among n.  Delayed mode calls
-// get_cli_info only for a client whose queue is empty (initial_tag,
-// :878-893): slots with queued requests are skipped (their counts read back
-// from the device).
-int fetch_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, size_t stride) {
+// infos of the distinct registered slots among n.  For an add batch
+// (adding) in delayed mode, get_cli_info runs only for a client whose queue
+// is empty (initial_tag, :878-893): slots with queued requests are skipped
+// (their counts read back from the device).  A delayed pop's
+// update_next_tag (:1021-1036) always fetches.
+int fetch_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, size_t stride,
+                bool adding) {
   if (!q->info_fn || !q->tb.binfo || !n) return DMC_OK;
   std::vector<uint32_t> sl;
   sl.reserve(n);
@@ -2053,7 +2055,7 @@ int fetch_infos(dmc_queue* q, uint32_t n, const uint32_t* slots, size_t stride) 
   std::sort(sl.begin(), sl.end());
   sl.erase(std::unique(sl.begin(), sl.end()), sl.end());
   if (sl.empty()) return DMC_OK;
-  if (q->tb.delayed) {
+  if (adding && q->tb.delayed) {
     const uint32_t m = (uint32_t)sl.size();
     const size_t sb = (4ull * m + 63) & ~size_t(63);
     if (int rc = ensure_stage(q, sb + m)) return rc;
@@ -2101,7 +2103,7 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
     HIP_OK(hipStreamSynchronize(q->stream));
     if (q->h_sctl->type == DMC_NEXT_RETURNING) {
       const uint32_t s = q->h_sctl->slot;
-      if (int rc = fetch_infos(q, 1, &s, sizeof(uint32_t))) return rc;
+      if (int rc = fetch_infos(q, 1, &s, sizeof(uint32_t), false)) return rc;
     }
   }
   hipLaunchKernelGGL(k_step_mark, dim3(grid_for(tb.n, 2048)), dim3(kBlock), 0,
@@ -3125,7 +3127,7 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   int rc = ensure_batch(q, n);
   if (rc) return rc;
   // U1 with a host client_info_f: the infos the batch's tags read
-  rc = fetch_infos(q, n, &reqs[0].slot, sizeof(dmc_request));
+  rc = fetch_infos(q, n, &reqs[0].slot, sizeof(dmc_request), true);
   if (rc) return rc;
   if (n == 1 && q->single_op && !q->prof_on &&
       (reqs[0].slot >= q->p.max_clients || !q->idle_h[reqs[0].slot])) {
