@@ -35,6 +35,7 @@ OPT_GRAPHS = 3
 OPT_ACT_SPLIT = 4
 OPT_SAMPLE = 5
 OPT_SINGLE_OP = 6
+OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0

@@ -1288,6 +1288,7 @@ struct dmc_queue {
   dmc_decision* d_dec = nullptr;
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
+  int fail_allocs = 0;   // DMC_OPT_FAIL_ALLOC (test hook): device allocations to fail
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
   bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
@@ -1537,6 +1538,29 @@ int invalidate_graphs(dmc_queue* q) {
   return DMC_OK;
 }
 
+// Device allocation of a queue buffer: DMC_OPT_FAIL_ALLOC (a test hook)
+// makes the next n of them fail as an exhausted device would; a failed
+// growth leaves the buffer absent (its capacity 0) and the call returns
+// DMC_ENOMEM before launching anything that would use it.
+int dalloc(dmc_queue* q, void** p, size_t bytes) {
+  *p = nullptr;
+  if (q->fail_allocs > 0) {
+    --q->fail_allocs;
+    return DMC_ENOMEM;
+  }
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    *p = nullptr;
+    (void)hipGetLastError();  // (not sticky: the queue stays usable)
+    return DMC_ENOMEM;
+  }
+  return DMC_OK;
+}
+#define DALLOC(q, ptr, bytes)                                         \
+  do {                                                                \
+    if (int e_ = dalloc((q), reinterpret_cast<void**>(ptr), (bytes))) \
+      return e_;                                                      \
+  } while (0)
+
 // The radix path's buffers for `n` dense entries (grown on demand): the
 // entries, the sort's two index buffers, its per-(digit, tile) counts, the
 // scans' tile partials and the group sizes / offsets.
@@ -1554,15 +1578,15 @@ int ensure_entries(dmc_queue* q, uint32_t n) {
   if (rc) return rc;
   const uint32_t nblk = scan_tiles(cap);
   const uint32_t ncnt = 256u * nblk;
-  HIP_OK(hipMalloc(&q->dense, sizeof(DEnt) * cap));
-  HIP_OK(hipMalloc(&q->sa, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->sb, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->lcnt, sizeof(uint32_t) * ncnt));
-  HIP_OK(hipMalloc(&q->sparts, sizeof(uint32_t) * scan_tiles(std::max(ncnt, cap))));
-  HIP_OK(hipMalloc(&q->gsz, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->goff, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->gisp, sizeof(uint32_t) * cap));
-  HIP_OK(hipMalloc(&q->gpoff, sizeof(uint32_t) * cap));
+  DALLOC(q, &q->dense, sizeof(DEnt) * cap);
+  DALLOC(q, &q->sa, sizeof(uint32_t) * cap);
+  DALLOC(q, &q->sb, sizeof(uint32_t) * cap);
+  DALLOC(q, &q->lcnt, sizeof(uint32_t) * ncnt);
+  DALLOC(q, &q->sparts, sizeof(uint32_t) * scan_tiles(std::max(ncnt, cap)));
+  DALLOC(q, &q->gsz, sizeof(uint32_t) * cap);
+  DALLOC(q, &q->goff, sizeof(uint32_t) * cap);
+  DALLOC(q, &q->gisp, sizeof(uint32_t) * cap);
+  DALLOC(q, &q->gpoff, sizeof(uint32_t) * cap);
   q->ecap = cap;
   return DMC_OK;
 }
@@ -1572,7 +1596,7 @@ int ensure_entries(dmc_queue* q, uint32_t n) {
 // the radix path do not pay for them.
 int ensure_brec(dmc_queue* q) {
   if (q->brec) return DMC_OK;
-  HIP_OK(hipMalloc(&q->brec, sizeof(BRecR) * (size_t)kNBR * kBinCapR));
+  DALLOC(q, &q->brec, sizeof(BRecR) * (size_t)kNBR * kBinCapR);
   return DMC_OK;
 }
 
@@ -1585,11 +1609,11 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
     *p = nullptr;
   }
   q->bcap = 0;
-  HIP_OK(hipMalloc(&q->d_reqs, sizeof(dmc_request) * cap));
-  HIP_OK(hipMalloc(&q->d_rc, sizeof(int32_t) * cap));
+  DALLOC(q, &q->d_reqs, sizeof(dmc_request) * cap);
+  DALLOC(q, &q->d_rc, sizeof(int32_t) * cap);
   // (padded to whole blocks: k_add_chain loads them before its bounds check)
-  HIP_OK(hipMalloc(&q->apos, sizeof(uint32_t) * (cap + kBlock)));
-  HIP_OK(hipMalloc(&q->aslot, sizeof(uint32_t) * (cap + kBlock)));
+  DALLOC(q, &q->apos, sizeof(uint32_t) * (cap + kBlock));
+  DALLOC(q, &q->aslot, sizeof(uint32_t) * (cap + kBlock));
   q->bcap = cap;
   return DMC_OK;
 }
@@ -1601,7 +1625,7 @@ int ensure_dec(dmc_queue* q, uint32_t n) {
   q->d_dec = nullptr;
   q->dcap = 0;
   uint32_t cap = std::max<uint32_t>(n, 1024);
-  HIP_OK(hipMalloc(&q->d_dec, sizeof(dmc_decision) * cap));
+  DALLOC(q, &q->d_dec, sizeof(dmc_decision) * cap);
   q->dcap = cap;
   return DMC_OK;
 }
@@ -1693,31 +1717,31 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   dfree(q->act_sparts);
   if (q->h_act) (void)hipHostFree(q->h_act);
   q->h_act = nullptr;
-  HIP_OK(hipMalloc(&q->act_cold, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_cnew, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_pre, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_suf, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_p, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_idx, 4ull * cap));
-  HIP_OK(hipMalloc(&q->act_x, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_ip, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_it, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_ipd, 8ull * cap));
-  HIP_OK(hipMalloc(&q->act_islot, 4ull * cap));
-  HIP_OK(hipMalloc(&q->act_flag, 4ull * cap));
+  DALLOC(q, &q->act_cold, 8ull * cap);
+  DALLOC(q, &q->act_cnew, 8ull * cap);
+  DALLOC(q, &q->act_pre, 8ull * cap);
+  DALLOC(q, &q->act_suf, 8ull * cap);
+  DALLOC(q, &q->act_p, 8ull * cap);
+  DALLOC(q, &q->act_idx, 4ull * cap);
+  DALLOC(q, &q->act_x, 8ull * cap);
+  DALLOC(q, &q->act_ip, 8ull * cap);
+  DALLOC(q, &q->act_it, 8ull * cap);
+  DALLOC(q, &q->act_ipd, 8ull * cap);
+  DALLOC(q, &q->act_islot, 4ull * cap);
+  DALLOC(q, &q->act_flag, 4ull * cap);
   HIP_OK(hipHostMalloc((void**)&q->h_act, 4ull * cap, 0));
   if (!q->act_dm) {
-    HIP_OK(hipMalloc(&q->act_dm, 4));
+    DALLOC(q, &q->act_dm, 4);
     HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
   }
-  HIP_OK(hipMalloc(&q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap)));
+  DALLOC(q, &q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap));
   if (!q->act_extra) {
-    HIP_OK(hipMalloc(&q->act_extra, 8));
+    DALLOC(q, &q->act_extra, 8);
     const uint64_t mx = kMaxKey;
     HIP_OK(hipMemcpyAsync(q->act_extra, &mx, 8, hipMemcpyHostToDevice, q->stream));
     HIP_OK(hipStreamSynchronize(q->stream));
   }
-  if (!q->act_parts) HIP_OK(hipMalloc(&q->act_parts, 8ull * 2048));
+  if (!q->act_parts) DALLOC(q, &q->act_parts, 8ull * 2048);
   q->acap = cap;
   return DMC_OK;
 }
@@ -1988,7 +2012,7 @@ int ensure_stage(dmc_queue* q, size_t bytes) {
   q->stage = nullptr;
   q->stage_cap = 0;
   const size_t cap = std::max<size_t>(bytes + (bytes >> 1), 4096);
-  HIP_OK(hipMalloc(&q->stage, cap));
+  DALLOC(q, &q->stage, cap);
   q->stage_cap = cap;
   return DMC_OK;
 }
@@ -2837,7 +2861,7 @@ int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) 
     q->mark_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 4096);
     HIP_OK(hipHostMalloc((void**)&q->h_mark, 4ull * cap, 0));
-    HIP_OK(hipMalloc(&q->d_mark, 4ull * cap));
+    DALLOC(q, &q->d_mark, 4ull * cap);
     q->mark_cap = cap;
   }
   if (!q->mark_ev) HIP_OK(hipEventCreateWithFlags(&q->mark_ev, hipEventDisableTiming));
@@ -3531,6 +3555,10 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_SINGLE_OP:
       q->single_op = value != 0;
+      return DMC_OK;
+    case DMC_OPT_FAIL_ALLOC:
+      if (value < 0) return DMC_EINVAL;
+      q->fail_allocs = (int)value;
       return DMC_OK;
     case DMC_OPT_SAMPLE:
       if (value < 0 || value > 2) return DMC_EINVAL;

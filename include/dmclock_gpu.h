@@ -331,6 +331,9 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   pulls with k <= SMALL_K run the single-op path (one kernel per add,
                                   two per pull, results in host-mapped memory, one round trip);
                                   0: the general launch sequence */
+#define DMC_OPT_FAIL_ALLOC 7    /* test hook: the queue's next `value` device buffer allocations
+                                  (growth of its batch, decision, radix and activation buffers)
+                                  fail; the call returns DMC_ENOMEM, the queue stays usable */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
 
 /* Engine path counters since creation (or the last reset): which ranking
