@@ -36,6 +36,7 @@ OPT_ACT_SPLIT = 4
 OPT_SAMPLE = 5
 OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
+OPT_BREAK_ROUNDS = 8
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0
@@ -127,6 +128,8 @@ class Counters(ctypes.Structure):
         ("max_bin", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
         ("bin_splits", ctypes.c_uint64),
+        ("brk_rounds", ctypes.c_uint64),
+        ("brk_fallbacks", ctypes.c_uint64),
     ]
 
     def as_dict(self):

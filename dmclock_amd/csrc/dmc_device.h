@@ -275,11 +275,16 @@ __device__ inline RingView stage_ring(const Table& tb, uint32_t s, uint32_t h,
 
 __device__ inline void keep(double v) { asm volatile("" ::"v"(v)); }
 
-// Visitor callbacks: pop(i, tag, cost, handle, prio, dec, tie) for each pop
-// (i = queue position, dec/tie = the ring entry's round scratch), and
-// group(key, run) after each priority group.
+// Visitor callbacks: pop(i, tag, cost, handle, kind, dec, tie) for each pop
+// (i = queue position, dec/tie = the ring entry's round scratch; kind: a
+// PopKind), and group(key, run) after each priority group.
+enum PopKind : uint32_t {
+  kPopR = 0,      // reservation pop
+  kPopHead = 1,   // priority pop opening a group (the group's key)
+  kPopChain = 2,  // priority pop inside a limit-break group's run (walk_p, brk)
+};
 struct NullVisit {
-  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool, uint32_t,
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, uint32_t, uint32_t,
                       uint32_t) {}
   __device__ void group(uint64_t, uint32_t) {}
 };
@@ -302,7 +307,7 @@ __device__ inline uint32_t walk_r(const Table& tb, const RingView& rv, const CVi
     ReqEntry e = rv.at(0);
     while (n < c && n < limit) {
       if (!(e.r <= now) || okey(e.r) > T || (stamped && e.dec == kNoDec)) break;
-      vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, false, e.dec,
+      vis.pop(n, Tag3{e.r, e.p, e.l, e.arrival}, e.cost, e.handle, kPopR, e.dec,
               e.tie);
       ++n;
       if (n < c) e = rv.at(n);
@@ -320,7 +325,7 @@ __device__ inline uint32_t walk_r(const Table& tb, const RingView& rv, const CVi
   uint64_t cur_h = e0.handle;
   while (n < c && n < limit) {
     if (!(cur.r <= now) || okey(cur.r) > T || (stamped && cur_dec == kNoDec)) break;
-    vis.pop(n, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
+    vis.pop(n, cur, cur_cost, cur_h, kPopR, cur_dec, cur_tie);
     ++n;
     if (n < c) {
       const ReqEntry e = rv.at(n);
@@ -356,6 +361,13 @@ __device__ inline uint32_t walk_r(const Table& tb, const RingView& rv, const CVi
 // `limit` bounds the total pops (apply mode).  On return *pmask has bit i set
 // for every entry popped by priority (immediate mode), used to recompute the
 // reduced reservation tags of the entries behind them.
+// brk (limit-break rounds, AtLimit::Allow, immediate mode): the pulls after
+// the eligible work ran out (no front with r <= now, none ready) pop the
+// ready-heap top regardless of its limit (:1157-1165); each such group's
+// run then takes the pops its reduction exposes to the next pulls: a front
+// with r <= now (reservation) or with l <= now (readied by the next limit
+// scan and popped as the only ready front, kPopChain), until the front has
+// neither.
 struct WalkP {
   uint32_t pops;
   uint32_t groups;
@@ -387,7 +399,7 @@ __device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView&
                                Tag3* prev_io, Tag3* front_out,
                                uint32_t* front_cost, uint32_t start,
                                Tag3 start_tag, bool use_start_tag, bool ready0,
-                               uint32_t kstamp = 0) {
+                               uint32_t kstamp = 0, bool brk = false) {
   WalkP w{0, 0, 0};
   const uint32_t c = cv.c;
   if (start >= c) return w;
@@ -396,13 +408,14 @@ __device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView&
     uint32_t i = start;
     while (i < c && w.pops < limit) {
       const ReqEntry e = rv.at(i);
-      bool rdy = (i == start) ? (ready0 || e.l <= now) : (e.l <= now);
+      // (a limit-break group's head needs no readiness: brk)
+      bool rdy = brk || ((i == start) ? (ready0 || e.l <= now) : (e.l <= now));
       if (!rdy || !(e.p < kInf)) break;
       uint64_t key = okey(__dadd_rn(e.p, pdv));
       if (key > T || (kstamp && e.dec == kNoDec)) break;
       const uint32_t glim = kstamp ? kstamp - e.dec : 0xffffffffu;  // pops in group
       double r_now = reduced_r(rv, i, w.pmask, rinv);
-      vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, true, e.dec,
+      vis.pop(i, Tag3{r_now, e.p, e.l, e.arrival}, e.cost, e.handle, kPopHead, e.dec,
               e.tie);
       w.pmask |= 1ull << i;
       ++i;
@@ -410,10 +423,19 @@ __device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView&
       uint32_t run = 0;
       while (i < c && w.pops < limit && run + 1 < glim) {
         double ri = reduced_r(rv, i, w.pmask, rinv);
-        if (!(ri <= now)) break;
         const ReqEntry er = rv.at(i);
-        vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, false,
-                er.dec, er.tie);
+        if (ri <= now) {  // the next pull's reservation pop
+          vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, kPopR,
+                  er.dec, er.tie);
+        } else if (brk && er.l <= now && er.p < kInf) {
+          // limit breaks: the next pull's limit scan readies this front and
+          // pops it (the only ready front, :1135-1151), with its reduction
+          vis.pop(i, Tag3{ri, er.p, er.l, er.arrival}, er.cost, er.handle, kPopChain,
+                  er.dec, er.tie);
+          w.pmask |= 1ull << i;
+        } else {
+          break;
+        }
         ++i;
         ++w.pops;
         ++run;
@@ -468,13 +490,13 @@ __device__ inline WalkP walk_p(const Table& tb, const RingView& rv, const CView&
     uint64_t key = okey(__dadd_rn(cur.p, pdv));
     if (key > T || (kstamp && cur_dec == kNoDec)) break;
     const uint32_t glim = kstamp ? kstamp - cur_dec : 0xffffffffu;  // pops in group
-    vis.pop(i, cur, cur_cost, cur_h, true, cur_dec, cur_tie);
+    vis.pop(i, cur, cur_cost, cur_h, kPopHead, cur_dec, cur_tie);
     advance(true);
     ++w.pops;
     uint32_t run = 0;
     while (i < c && w.pops < limit && run + 1 < glim) {
       if (!(cur.r <= now)) break;
-      vis.pop(i, cur, cur_cost, cur_h, false, cur_dec, cur_tie);
+      vis.pop(i, cur, cur_cost, cur_h, kPopR, cur_dec, cur_tie);
       advance(false);
       ++w.pops;
       ++run;

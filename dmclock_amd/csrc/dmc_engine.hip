@@ -1289,6 +1289,7 @@ struct dmc_queue {
   uint32_t step_grid = 0;
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   int fail_allocs = 0;   // DMC_OPT_FAIL_ALLOC (test hook): device allocations to fail
+  bool brk_rounds = true;  // DMC_OPT_BREAK_ROUNDS: Allow's limit breaks as rounds
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
   bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
@@ -2155,6 +2156,13 @@ int step_once(dmc_queue* q, double now, dmc_decision* d_out, uint32_t idx,
 // runs eagerly (the stage timers are events between kernels).
 // Sampled thresholds (kSample) for tables of at least kSampleMinN slots on
 // the bin-rank path, unless the previous round's sample failed validation.
+// limit-break rounds: AtLimit::Allow, immediate mode (walk_p's brk groups),
+// no host client_info_f between selection and pop (DMC_OPT_BREAK_ROUNDS)
+bool brk_ok(const dmc_queue* q) {
+  return q->brk_rounds && q->p.at_limit == DMC_AT_LIMIT_ALLOW && !q->tb.delayed &&
+         !info_steps(q);
+}
+
 bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
@@ -2235,11 +2243,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
-                 dmc_pull_result* d_result, bool radix) {
+                 dmc_pull_result* d_result, bool radix, bool brk = false) {
   const bool sampled = use_sample(q, radix);
   uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 3) | (sampled ? 4 : 0) |
                  (radix ? 2 : 0);
-  CallParams cp{kk, 0, now, out, q->tick, d_result, ++q->round_seq};
+  CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq};
   int err = DMC_OK;
   GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); }, &err);
   if (err) return err;
@@ -2338,6 +2346,11 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
   bool allow = q->p.at_limit == DMC_AT_LIMIT_ALLOW;
   // this call's round size: kBinRankMaxK, lowered after a rank-bin overflow
   uint32_t kcap = kBinRankMaxK;
+  // the next round is a limit-break round (AtLimit::Allow, after a round ran
+  // out of eligible work: walk_p's brk groups instead of single steps);
+  // after one found the state not break-ready, none until a general round
+  // has made progress
+  bool brk = false, brk_fallback = false;
   while (n_dec < k) {
     if (q->n_registered == 0) {
       r.next_type = DMC_NEXT_NONE;
@@ -2375,7 +2388,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       if (q->radix_batches && !retry) --q->radix_batches;
       rc = radix ? ensure_entries(q, q->dense_hint) : ensure_brec(q);
       if (rc) return rc;
-      rc = launch_round(q, now, kr, d_out + n_dec, dres, radix);
+      rc = launch_round(q, now, kr, d_out + n_dec, dres, radix, brk);
       if (rc) return rc;
     }
     // one host round trip per round, through host-mapped memory
@@ -2482,6 +2495,15 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       retry_radix = retry;
       continue;
     }
+    if (c.overflow == 5) {
+      // a limit-break round found the state not break-ready (a front with
+      // r <= now or l <= now, or a weight-0 client's infinite p): nothing of
+      // it took effect; general rounds and steps take over
+      ++q->ctr.brk_fallbacks;
+      brk = false;
+      brk_fallback = true;
+      continue;
+    }
     if (c.overflow == 3) {
       // the sampled threshold admitted too few first keys (k_remit's exact
       // count): this round is re-run with the exact histogram
@@ -2524,6 +2546,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     q->ctr.candidates += c.n_cand;
     q->ctr.entries += radix ? c.dense_n : c.n_emit;
     q->ctr.decisions += c.n_dec;
+    if (!brk && c.n_dec) brk_fallback = false;
     n_dec += c.n_dec;
     r.n_priority += c.n_prio;
     r.n_reservation += c.n_dec - c.n_prio;
@@ -2532,9 +2555,16 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       break;
     }
     if (!c.terminal) continue;  // a capped round took all kr: the next takes the rest
+    if (allow && !brk && !brk_fallback && brk_ok(q)) {
+      // the eligible work ran out: the limit breaks (:1157-1165) as rounds
+      brk = true;
+      ++q->ctr.brk_rounds;
+      continue;
+    }
     if (allow) {
       int type;
       double when;
+      brk = false;
       rc = step_once(q, now, d_out, n_dec, &type, &when);
       if (rc) return rc;
       if (type != DMC_NEXT_RETURNING) {
@@ -3555,6 +3585,9 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_SINGLE_OP:
       q->single_op = value != 0;
+      return DMC_OK;
+    case DMC_OPT_BREAK_ROUNDS:
+      q->brk_rounds = value != 0;
       return DMC_OK;
     case DMC_OPT_FAIL_ALLOC:
       if (value < 0) return DMC_EINVAL;

@@ -111,6 +111,11 @@ struct Round {
   uint32_t n_pgroups;    // P groups emitted (k_rbscan)
   uint32_t n_emit;       // rank records emitted (k_rbscan)
   uint32_t sampled;      // the thresholds came from a 1/8 sample of the first keys
+  uint32_t brk;          // a limit-break round (AtLimit::Allow after the eligible
+                         // work ran out: walk_p's brk groups)
+  uint32_t brk_bad;      // ... whose state was not break-ready (overflow = 5)
+  uint32_t brk_prio;     // ... its priority pops (counted by k_rapply)
+  uint32_t brk_done;     // ... k_rapply's block ticket (the summary goes last)
   uint32_t ccnt[2 * kShards];  // sampled rounds: first keys at or below T, per
                                // phase, in XCD shards (k_remit)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
@@ -133,7 +138,7 @@ struct Round {
 
 struct CallParams {
   uint32_t k_total;
-  uint32_t pad;
+  uint32_t brk;  // a limit-break round
   double now;
   dmc_decision* out;
   uint64_t tick;
@@ -179,7 +184,7 @@ __device__ inline uint32_t wsum32(uint32_t v) {
 
 struct CountV {
   uint32_t pops = 0, groups = 0;
-  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, bool, uint32_t,
+  __device__ void pop(uint32_t, const Tag3&, uint32_t, uint64_t, uint32_t, uint32_t,
                       uint32_t) {
     ++pops;
   }
@@ -249,9 +254,19 @@ struct ScanOut {
 // no stores (scan_store makes them after every slot of the thread is done,
 // since a load's wait also waits for the wave's earlier stores).
 __device__ inline ScanOut scan_compute(const Table& tb, uint32_t s, const ScanCols& x,
-                                       const ScanPre& pre, double now) {
+                                       const ScanPre& pre, double now, bool brk = false,
+                                       bool* bad = nullptr) {
   ScanOut o{kMaxKey, kMaxKey, 0, x.f, false};
   if (!x.c) return o;
+  if (brk) {
+    // a limit-break round: every front's key is its p + prop_delta (the
+    // ready-heap order of not-ready fronts); the state must be the one the
+    // eligible work left: no front with r <= now, none ready or with
+    // l <= now, every p finite (else the host runs general pulls)
+    if (x.fr <= now || x.fl <= now || (x.f & F_READY) || !(x.pk < kInf)) *bad = true;
+    else o.kp = okey(x.pk);
+    return o;
+  }
   Tag3 pf;
   bool have_pf = true, ready;
   double pkv = kInf;
@@ -442,6 +457,7 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
+    z.brk = cp.brk;
     z.g_last = kNoneR;
     z.next_type = DMC_NEXT_RETURNING;
     z.now = cp.now;
@@ -473,11 +489,12 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   }
   // every slot's first R prefix step in one level of loads
   ScanPre pre[kScanSlots];
+  const bool brk = cp.brk != 0;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
     pre[j] = ScanPre{0.0, 0.0, 0.0, 0.0};
-    if (s < tb.n && x[j].c && x[j].fr <= now && !tb.delayed) {
+    if (s < tb.n && x[j].c && x[j].fr <= now && !tb.delayed && !brk) {
       pre[j].pd = tb.rec[s].pd;
       if (x[j].c > 1) {
         const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x[j].h + 1) & tb.qmask)];
@@ -488,12 +505,16 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
     }
   }
   ScanOut o[kScanSlots];
+  bool bad = false;  // a limit-break round's state is not break-ready
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    o[j] = s < tb.n ? scan_compute(tb, s, x[j], pre[j], now)
+    o[j] = s < tb.n ? scan_compute(tb, s, x[j], pre[j], now, brk, &bad)
                     : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
   }
+  // (a limit-break round has no reservation entries: its n_r counts the
+  // slots that are not break-ready, for k_rhist's last block)
+  if (bad) acc.n_r += 1;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
@@ -626,14 +647,23 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
 #endif
-  pick_both(rd, tot, hist, sbn, sampled);
+  const bool brk_bad = rd->brk && tot.n_r;
+  RoundPart t2 = tot;
+  if (rd->brk) t2.n_r = 0;  // (brk: no reservation entries)
+  pick_both(rd, t2, hist, sbn, sampled);
   if (threadIdx.x == 0) {
     // the round's totals (stored by the last block, after its barriers: a
     // barrier waits for the thread's outstanding stores)
-    rd->tot = tot;
-    rd->n_r = tot.n_r;
-    rd->p_runs = tot.n_r < (uint64_t)rd->k_total ? 1 : 0;
+    rd->tot = t2;
+    rd->n_r = t2.n_r;
+    rd->p_runs = t2.n_r < (uint64_t)rd->k_total ? 1 : 0;
     rd->sampled = sampled ? 1 : 0;
+    if (brk_bad) {
+      // the state is not the one a limit-break round assumes: nothing of
+      // the round takes effect, the host runs general pulls instead
+      rd->brk_bad = 1;
+      rd->overflow = 5;
+    }
   }
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[2] = wall_clock64();
@@ -1031,14 +1061,14 @@ struct EmitV {
               acc->ci};
   }
   uint32_t gpos = 0;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, bool prio,
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t, uint64_t, uint32_t kind,
                       uint32_t, uint32_t) {
     if (acc->npops++ == 0) {
       acc->pos0 = i;
-      acc->prio0 = prio;
+      acc->prio0 = kind != kPopR;
     }
     if (ph == 0) put(okey(t.r), i, 0);
-    else if (prio) gpos = i;
+    else if (kind == kPopHead) gpos = i;
   }
   __device__ void group(uint64_t key, uint32_t run) { put(key, gpos, run); }
 };
@@ -1149,7 +1179,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
-           pf, m && tb.delayed, ready0);
+           pf, m && tb.delayed, ready0, 0, rd->brk != 0);
   }
   // Fast candidate: one record at queue position 0 in immediate mode -- one
   // reservation pop, or a priority pop with a reservation run of at most one
@@ -1157,7 +1187,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
   // its state after the group (apply_one's arithmetic for that case) and the
   // run's decision are stored here.
   const uint32_t run = acc.npops - 1;  // (a one-record candidate: its group's run)
-  const bool fast = brec && !tb.delayed && acc.nrec == 1 && acc.pos0 == 0 &&
+  const bool fast = brec && !tb.delayed && !rd->brk && acc.nrec == 1 && acc.pos0 == 0 &&
                     acc.at0 < kBinCapR && (run == 0 || (run == 1 && acc.prio0));
   if (fast) {
     // (stored piecewise as computed: the record, then the PostRec's lines --
@@ -1265,6 +1295,10 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
   }
   bool ovf = rd->bin_ovf != 0;
   bool bad_sample = false;
+  if (rd->overflow) {  // (failed before emission: a limit-break round's state)
+    clear();
+    return;
+  }
   if (rd->sampled) {
     // a sampled threshold must admit at least the needed first keys (then
     // every entry the k pulls can take has a key at or below it)
@@ -1895,22 +1929,25 @@ struct ApplyV {
   uint32_t slot;
   uint32_t inrun = 0, gidx = 0;
   uint32_t last_idx = 0;
+  uint32_t nprio = 0;  // priority pops (limit-break rounds count them here)
   bool any = false;
   __device__ void pop(uint32_t, const Tag3& t, uint32_t cost, uint64_t h,
-                      bool prio, bool pphase, uint32_t edec, uint32_t etie) {
+                      uint32_t kind, bool pphase, uint32_t edec, uint32_t etie) {
     uint32_t idx, tie;
+    const bool prio = kind != kPopR;
     if (!pphase) {
       idx = edec;
       tie = etie;
     } else {
-      if (prio) {
+      if (kind == kPopHead) {
         gidx = edec;
         inrun = 0;
       }
       idx = gidx + inrun;
-      tie = prio ? etie : 0;
+      tie = kind == kPopHead ? etie : 0;
       ++inrun;
     }
+    nprio += prio ? 1u : 0u;
     dmc_decision d;
     d.handle = h;
     d.tag_r = t.r;
@@ -1940,17 +1977,17 @@ struct ApplyV {
 };
 struct ApplyVR {
   ApplyV* a;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p,
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, uint32_t k,
                       uint32_t d, uint32_t ti) {
-    a->pop(i, t, c, h, p, false, d, ti);
+    a->pop(i, t, c, h, k, false, d, ti);
   }
   __device__ void group(uint64_t, uint32_t) {}
 };
 struct ApplyVP {
   ApplyV* a;
-  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, bool p,
+  __device__ void pop(uint32_t i, const Tag3& t, uint32_t c, uint64_t h, uint32_t k,
                       uint32_t d, uint32_t ti) {
-    a->pop(i, t, c, h, p, true, d, ti);
+    a->pop(i, t, c, h, k, true, d, ti);
   }
   __device__ void group(uint64_t, uint32_t) {}
 };
@@ -1975,7 +2012,8 @@ struct RoundC {
   dmc_decision* out;
   uint32_t g_last, terminal;
   uint32_t k;
-  bool p_runs, ovf;
+  bool p_runs, ovf, brk;
+  uint32_t* brk_prio;  // limit-break rounds: the priority pops' count
 };
 
 constexpr int kApplyStage = 4;  // queue positions staged per candidate (LDS)
@@ -2017,7 +2055,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     ApplyVP vp{&v};
     bool ready0 = popsR == 0 && (f0 & F_READY);
     WalkP w = walk_p(tb, rv, cv, now, kMaxKey, 0xffffffffu, vp, &prev, &front, &fcost,
-                     popsR, front, popsR && tb.delayed, ready0, rc.k);
+                     popsR, front, popsR && tb.delayed, ready0, rc.k, rc.brk);
     popsP = w.pops;
     pmask = w.pmask;
   }
@@ -2080,6 +2118,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   }
   if (rc.dbg) rc.dbg[3] = wall_clock64();
   v.flush();
+  if (rc.brk && v.nprio) atomicAdd(rc.brk_prio, v.nprio);
   // the new front's heap keys, cursor and flags: one 32-byte ScanRec store
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
   ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
@@ -2087,8 +2126,11 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     o.r = front.r;
     o.pk = __dadd_rn(front.p, cv.pd);
     o.l = front.l;
-    bool seen = popsP ? (terminal || (g_last != kNoneR && v.last_idx < g_last))
-                      : p_runs;
+    // (a limit-break group's run ends at a front with l > now, or at the
+    // round's end before any pull scanned it: never ready)
+    bool seen = rc.brk ? false
+                       : popsP ? (terminal || (g_last != kNoneR && v.last_idx < g_last))
+                               : p_runs;
     if (seen && front.l <= now) f |= F_READY;
   }
   o.flags = f;
@@ -2158,44 +2200,65 @@ __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
          const uint32_t* decof, const PostRec* post, unsigned long long* sched,
          HostRound* h, uint64_t* dbg = nullptr) {
-  if (blockIdx.x == gridDim.x - 1) {
+  // A limit-break round's priority pops (group heads and their runs'
+  // readied fronts) are counted here: its summary goes out once every block
+  // has counted (a ticket), not from the extra block at once
+  const bool brk = rd->brk && !rd->overflow;
+  if (blockIdx.x == gridDim.x - 1 && !brk) {
     // the extra block publishes the round's summary (complete since k_rrank)
     // to host memory at once: the host learns the outcome while the other
     // blocks store the state, and its next launch is stream-ordered behind them
     rfinish_body(rd, h);
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow && !brk) {
     sched[0] += rd->n_dec - rd->n_prio;
     sched[1] += rd->n_prio;
   }
-  // (kApplyPerEmit apply blocks per emit block)
-  const uint32_t eb = blockIdx.x / kApplyPerEmit;
-  const uint32_t nc = bcand[eb];
-  const uint32_t base = eb * kEmitChunk;
-  RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
-            rd->p_runs != 0, rd->overflow != 0};
-  __shared__ ReqEntry stage[kBlockR * kApplyStage];
-  // (interleaved: the emit block's candidates, about 280, split evenly over
-  // its apply blocks rather than filling the first one)
-  for (uint32_t i = threadIdx.x * kApplyPerEmit + (blockIdx.x % kApplyPerEmit); i < nc;
-       i += kApplyPerEmit * kBlockR) {
-    const uint32_t ci = base + i;
-    uint64_t t0 = dbg ? wall_clock64() : 0;
-    // one level of coalesced loads: the candidate, its decision offset and
-    // its precomputed state (both lines: a run's second line is no further
-    // round trip)
-    const uint32_t d = decof[ci];
-    if (d != kSlowCand && !rc.ovf) continue;  // a fast candidate: k_rrank applied it
-    const CandRec c = cand[ci];
-    rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
-    if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;
-    apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
-    if (rc.dbg) {
-      rc.dbg[0] = t0;
-      rc.dbg[4] = wall_clock64();
+  if (blockIdx.x < gridDim.x - 1) {
+    // (kApplyPerEmit apply blocks per emit block)
+    const uint32_t eb = blockIdx.x / kApplyPerEmit;
+    const uint32_t nc = bcand[eb];
+    const uint32_t base = eb * kEmitChunk;
+    RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
+              rd->p_runs != 0, rd->overflow != 0, brk, &rd->brk_prio};
+    __shared__ ReqEntry stage[kBlockR * kApplyStage];
+    // (interleaved: the emit block's candidates, about 280, split evenly over
+    // its apply blocks rather than filling the first one)
+    for (uint32_t i = threadIdx.x * kApplyPerEmit + (blockIdx.x % kApplyPerEmit); i < nc;
+         i += kApplyPerEmit * kBlockR) {
+      const uint32_t ci = base + i;
+      uint64_t t0 = dbg ? wall_clock64() : 0;
+      const uint32_t d = decof[ci];
+      if (d != kSlowCand && !rc.ovf) continue;  // a fast candidate: k_rrank applied it
+      const CandRec c = cand[ci];
+      rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
+      if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;
+      apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
+      if (rc.dbg) {
+        rc.dbg[0] = t0;
+        rc.dbg[4] = wall_clock64();
+      }
     }
   }
+  if (!brk) return;
+  // ticket: the block's count atomics have completed (memory side) before
+  // one lane takes it; the last block publishes
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&rd->brk_done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t np = atomicAdd(&rd->brk_prio, 0u);
+    rd->n_prio = np;
+    sched[0] += rd->n_dec - np;
+    sched[1] += np;
+  }
+  __syncthreads();
+  rfinish_body(rd, h);
 }
 
 __global__ void k_rfinish(const Round* rd, HostRound* h) { rfinish_body(rd, h); }

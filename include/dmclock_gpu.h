@@ -331,6 +331,9 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   pulls with k <= SMALL_K run the single-op path (one kernel per add,
                                   two per pull, results in host-mapped memory, one round trip);
                                   0: the general launch sequence */
+#define DMC_OPT_BREAK_ROUNDS 8  /* 1 (default): AtLimit::Allow's limit breaks (dmclock_server.h:1157-1165)
+                                  run as batched rounds after the eligible work ran out (immediate
+                                  mode); 0: one general pull_request step each */
 #define DMC_OPT_FAIL_ALLOC 7    /* test hook: the queue's next `value` device buffer allocations
                                   (growth of its batch, decision, radix and activation buffers)
                                   fail; the call returns DMC_ENOMEM, the queue stays usable */
@@ -355,6 +358,8 @@ typedef struct dmc_counters {
   uint32_t max_bin;         /* largest rank bin of a bin-ranked round (records)     */
   uint32_t reserved;
   uint64_t bin_splits;      /* of the overflowed rounds: re-run as a smaller round   */
+  uint64_t brk_rounds;      /* limit-break rounds started (AtLimit::Allow)           */
+  uint64_t brk_fallbacks;   /* limit-break rounds whose state was not break-ready    */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 
