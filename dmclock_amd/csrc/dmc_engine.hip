@@ -2175,8 +2175,8 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  klaunch(q, DMC_PROF_SCAN, k_rscan, dim3(gN), dim3(kScanBlock), 0, tb,
-          sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
+  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN), dim3(kScanBlock), 0,
+          tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
           q->rd, cp, sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
@@ -2245,7 +2245,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
                  dmc_pull_result* d_result, bool radix, bool brk = false) {
   const bool sampled = use_sample(q, radix);
-  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 3) | (sampled ? 4 : 0) |
+  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 4) | (brk ? 8 : 0) | (sampled ? 4 : 0) |
                  (radix ? 2 : 0);
   CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq};
   int err = DMC_OK;

@@ -450,10 +450,13 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #ifndef DMC_SCAN_MINW
 #define DMC_SCAN_MINW 8
 #endif
+// (BRK: a limit-break round's scan, its own instantiation: the general
+// scan sits at its 64-register bound)
+template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
-k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
-        RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
-        uint2* k32) {
+k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
+          RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
+          uint2* k32) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -489,7 +492,7 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   }
   // every slot's first R prefix step in one level of loads
   ScanPre pre[kScanSlots];
-  const bool brk = cp.brk != 0;
+  constexpr bool brk = BRK;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
@@ -529,6 +532,10 @@ k_rscan(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
     if (threadIdx.x == 0) parts[blockIdx.x] = o;
   }
 }
+
+// the general scan (the graphs' parameter node) and the limit-break scan
+constexpr auto k_rscan = k_rscan_t<false>;
+constexpr auto k_rscan_brk = k_rscan_t<true>;
 
 // The round's totals from the scan's per-block partials (every thread gets
 // them): wave 0 combines them, 8 per lane for 512 partials with the loads in
