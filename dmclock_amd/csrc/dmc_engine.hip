@@ -2187,7 +2187,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
             gN, q->rd, q->hist, q->sbn, q->hist_done, 0);
-  klaunch(q, DMC_PROF_EMIT, k_remit, dim3(gEm),
+  klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
           q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
@@ -2196,10 +2196,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     if (q->debug)
       (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, q->stream);
-    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd, tb,
+    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
             (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
-            (const BRecR*)q->brec, (const PostRec*)q->post, q->decof,
-            q->debug ? q->dbg_wtime : nullptr);
+            (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
   } else {
     // the exact LSD sort of the dense entries (dmc_sort.h), then each
     // entry's group size, two exclusive sums and the decisions

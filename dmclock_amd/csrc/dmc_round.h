@@ -1137,6 +1137,9 @@ constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2:
 #define DMC_EMIT_STAGE_THREADS 448  // (LDS: 160 KB per block with the key array)
 #endif
 constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a staging slice
+// (BRK: a limit-break round, its own instantiation of k_remit: the general
+// walkers carry none of walk_p's break-mode code)
+template <bool BRK>
 __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c,
                                 uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
@@ -1186,7 +1189,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
     EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
-           pf, m && tb.delayed, ready0, 0, rd->brk != 0);
+           pf, m && tb.delayed, ready0, 0, BRK);
   }
   // Fast candidate: one record at queue position 0 in immediate mode -- one
   // reservation pop, or a priority pop with a reservation run of at most one
@@ -1194,7 +1197,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
   // its state after the group (apply_one's arithmetic for that case) and the
   // run's decision are stored here.
   const uint32_t run = acc.npops - 1;  // (a one-record candidate: its group's run)
-  const bool fast = brec && !tb.delayed && !rd->brk && acc.nrec == 1 && acc.pos0 == 0 &&
+  const bool fast = brec && !tb.delayed && !BRK && acc.nrec == 1 && acc.pos0 == 0 &&
                     acc.at0 < kBinCapR && (run == 0 || (run == 1 && acc.prio0));
   if (fast) {
     // (stored piecewise as computed: the record, then the PostRec's lines --
@@ -1440,8 +1443,9 @@ constexpr int kEmitThreads = DMC_EMIT_THREADS;
 constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster,
                              // and a slower last-block tail)
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
+template <bool BRK>
 __global__ void __launch_bounds__(kEmitThreads)
-k_remit(Table tb, Round* rd, const uint2* k32,
+k_remit_t(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
@@ -1583,7 +1587,7 @@ k_remit(Table tb, Round* rd, const uint2* k32,
   // per block; k_rapply's blocks take their emit block's segment)
   const uint32_t cbase = blockIdx.x * kEmitChunk;
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
-    const uint32_t cat = emit_one(
+    const uint32_t cat = emit_one<BRK>(
         tb, rd, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
         threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
                                                   : nullptr,
@@ -1638,6 +1642,10 @@ k_remit(Table tb, Round* rd, const uint2* k32,
 #endif
 }
 
+// the general emission and the limit-break rounds' emission
+constexpr auto k_remit = k_remit_t<false>;
+constexpr auto k_remit_brk = k_remit_t<true>;
+
 // ---------------------------------------------------------------- k_rrank
 // One block per rank bin ranks it in LDS by (okey, slot, position); R bins
 // precede P bins, so the decision offset of an entry is the sum of the group
@@ -1649,94 +1657,26 @@ k_remit(Table tb, Round* rd, const uint2* k32,
 
 constexpr int kDeepBatch = 8;   // queued requests reduced per batch of loads
 
-// A fast candidate's stores (k_remit precomputed its state after its group:
-// a pop at queue position 0 and at most one run pop), made by the k_rrank
-// lane that ranked its record: d = kNoDec if the group was not dispatched
-// (then only the pending limit-scan mark settles), else its first
-// decision's offset -- the run pop's decision, the reduced reservation tags
-// of the queued requests (the new front's and position 2's precomputed; from
-// position 3 on read, reduced and written, every load issued before the
-// first store), prev r, and the new front's ScanRec with its ready flag.  A
-// front left by a priority pop was seen by a later limit-scanning pull iff
-// this group is not the round's last priority pull (or the round is
-// terminal); one left by a reservation pop iff the priority pulls ran.
-__device__ inline void apply_fast(const Table& tb, uint32_t s, uint32_t d, const PostRec& pr,
-                                  dmc_decision* out, bool p_runs, bool terminal,
-                                  bool is_last) {
-  const uint8_t f0 = (uint8_t)(pr.cand & 0x0fu);
-  if (d == kNoDec) {  // not dispatched: the pending mark settles
-    if (f0 & F_PMARK) tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
-    return;
-  }
-  const uint32_t bits = pr.bits;
-  const bool prio = bits & 1u;
-  const uint32_t run = (bits >> 2) & 1u;
-  const uint32_t c = pr.cand >> 24, h = (pr.cand >> 16) & 0xffu;
-  const uint32_t pops = 1 + run;
-  const uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
-  if (prio) {
-    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-    const double off = pr.off;
-    // positions >= 3, kDeepBatch at a time: loads, then stores
-    for (uint32_t k0 = 3; k0 < c; k0 += kDeepBatch) {
-      double v[kDeepBatch];
-#pragma unroll
-      for (int j = 0; j < kDeepBatch; ++j)
-        if (k0 + j < c) v[j] = ring[(h + k0 + j) & tb.qmask].r;
-#pragma unroll
-      for (int j = 0; j < kDeepBatch; ++j)
-        if (k0 + j < c) ring[(h + k0 + j) & tb.qmask].r = __dsub_rn(v[j], off);
-    }
-    if (nc2) ring[nh].r = pr.fr;
-    if (!run && c >= 3) ring[(h + 2) & tb.qmask].r = pr.r2;
-    tb.rec[s].prev_r = pr.prev_r;
-  }
-  if (run) {
-    dmc_decision x;
-    x.handle = pr.handle1;
-    x.tag_r = pr.r1;
-    x.tag_p = pr.p1;
-    x.tag_l = pr.l1;
-    x.slot = s;
-    x.cost = pr.cost1;
-    x.phase = DMC_PHASE_RESERVATION;
-    x.flags = 0;
-    out[d + 1] = x;
-  }
-  uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
-  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
-  if (nc2) {
-    o.r = pr.fr;
-    o.pk = pr.fpk;
-    o.l = pr.fl;
-    const bool seen = prio ? (terminal || !is_last) : p_runs;
-    if (seen && (bits & 2u)) f |= F_READY;
-  }
-  o.flags = f;
-  tb.sc[s] = o;
-}
-
 // Rank of record i of a bin among all `cnt` of them, compared in `parts`
 // slices of `per` records by adjacent lanes whose counts are summed by
 // shuffles; lanes with i >= cnt take part in the shuffles only.  The lane
 // that owns a record then decides it: a fast record's decision is written
-// and its candidate's state stored (apply_fast: k_rapply only re-walks the
-// slow candidates); a slow record's pop is stamped into its ring entry.
-__device__ inline void rank_rec(Round* rd, const Table& tb, const BKey* sh, const BRecR* src,
-                                const PostRec* post, uint32_t cnt,
+// and its offset recorded for k_rapply (which stores the candidate's
+// precomputed state); a slow record's pop is stamped into its ring entry.
+// (Storing the fast candidates' state here instead, in the rank lanes, was
+// measured slower: rank 9.8 -> 21.2 us for apply 11.5 -> 6.3, §10.)
+__device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
                                 uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, bool isp, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
-                                dmc_decision* out, uint32_t* decof, bool p_runs,
-                                bool terminal) {
+                                ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
   const bool valid = i < cnt;
   BKey me = sh[valid ? i : 0];
-  // the writer lane's payload (an L2 hit: the block staged the line) and a
-  // fast record's post state, in flight during the comparisons
+  // the writer lane's payload (an L2 hit: the block staged the line), in
+  // flight during the comparisons
   uint32_t ci = 0, cost = 0;
   uint64_t handle = 0;
   double tr = 0.0, tp = 0.0, tl = 0.0;
-  PostRec pr;
   if (valid && part == 0) {
     const BRecR& x = src[i];
     ci = x.ci;
@@ -1745,14 +1685,6 @@ __device__ inline void rank_rec(Round* rd, const Table& tb, const BKey* sh, cons
     tr = x.r;
     tp = x.p;
     tl = x.l;
-    if (ci & kFastRec) {
-      // (the second line only with a run)
-      const ulonglong2* ps = reinterpret_cast<const ulonglong2*>(post + (ci & ~kFastRec));
-      ulonglong2* pd = reinterpret_cast<ulonglong2*>(&pr);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < 4 || me.run) pd[j] = ps[j];
-    }
   }
   uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
   if (!valid) f1 = f0;
@@ -1776,26 +1708,15 @@ __device__ inline void rank_rec(Round* rd, const Table& tb, const BKey* sh, cons
   if (valid && part == 0) {
     uint32_t goff = soff + gl;
     uint32_t size = isp ? 1u + me.run : 1u;
-    bool is_last = false;
     if (goff < k) {
-      if (isp) {
-        uint32_t prank = poff + rank;  // among P groups
-        if (goff + size >= k || prank == n_pgroups - 1) {
-          // the last applied group: its priority pop is the round's last
-          // limit-scanning pull
-          is_last = true;
-          rd->g_last = goff;
-          rd->n_prio = prank + 1;
-        }
-      }
       if ((ci & kFastRec) && goff + size > k) {
         // a fast group cut by the round's end: k_rapply re-walks it
-        ReqEntry* e = tb.ring + me.ridx;
-        e->dec = goff;
-        e->tie = tie;
+        ring[me.ridx].dec = goff;
+        ring[me.ridx].tie = tie;
         decof[ci & ~kFastRec] = kSlowCand;
       } else if (ci & kFastRec) {
-        // a fast record: its first pop's decision and its candidate's state
+        // a fast record: its first pop's decision, and its offset for
+        // k_rapply (which writes the run's pop and the candidate's state)
         dmc_decision d;
         d.handle = handle;
         d.tag_r = tr;
@@ -1806,14 +1727,20 @@ __device__ inline void rank_rec(Round* rd, const Table& tb, const BKey* sh, cons
         d.phase = isp ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
         d.flags = tie;
         out[goff] = d;
-        apply_fast(tb, me.slot, goff, pr, out, p_runs, terminal, is_last);
+        decof[ci & ~kFastRec] = goff;
       } else {
-        ReqEntry* e = tb.ring + me.ridx;
-        e->dec = goff;  // the stamp k_rapply's walk follows
-        e->tie = tie;
+        ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
+        ring[me.ridx].tie = tie;
       }
-    } else if (ci & kFastRec) {
-      apply_fast(tb, me.slot, kNoDec, pr, out, p_runs, terminal, false);
+      if (isp) {
+        uint32_t prank = poff + rank;  // among P groups
+        if (goff + size >= k || prank == n_pgroups - 1) {
+          // the last applied group: its priority pop is the round's last
+          // limit-scanning pull
+          rd->g_last = goff;
+          rd->n_prio = prank + 1;
+        }
+      }
     }
   }
 }
@@ -1831,8 +1758,8 @@ __device__ inline void rank_rec(Round* rd, const Table& tb, const BKey* sh, cons
 // stores from one block fill one stretch of the decision array.
 constexpr int kRankBlocksR = kNBR;
 __global__ void __launch_bounds__(kBlockR)
-k_rrank(Round* rd, Table tb, const uint32_t* bcnt, const uint32_t* bsoff,
-        const uint32_t* bpoff, const BRecR* brec, const PostRec* post, uint32_t* decof,
+k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
+        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring, uint32_t* decof,
         uint64_t* wtime = nullptr) {
   __shared__ BKey sh[kBinCapR];
   uint64_t t0 = wall_clock64();
@@ -1841,7 +1768,6 @@ k_rrank(Round* rd, Table tb, const uint32_t* bcnt, const uint32_t* bsoff,
   if (cnt == 0 || rd->overflow) return;
   const uint32_t k = rd->k_total;
   const uint32_t n_pgroups = rd->n_pgroups;
-  const bool p_runs = rd->p_runs != 0, terminal = rd->terminal != 0;
   dmc_decision* out = rd->out;
   const bool isp = b >= (uint32_t)kNBPhase;
   const uint32_t soff = bsoff[b], poff = bpoff[b];
@@ -1853,8 +1779,8 @@ k_rrank(Round* rd, Table tb, const uint32_t* bcnt, const uint32_t* bsoff,
   __syncthreads();
   const uint32_t t = threadIdx.x;
   for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
-    rank_rec(rd, tb, sh, src, post, cnt, parts, per, rb + t / parts, t % parts, isp, k,
-             n_pgroups, soff, poff, out, decof, p_runs, terminal);
+    rank_rec(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
+             soff, poff, ring, out, decof);
   if (wtime && threadIdx.x == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
@@ -2179,12 +2105,82 @@ __device__ inline void rfinish_body(const Round* rd, HostRound* h) {
   if (threadIdx.x == 0)
     __hip_atomic_store(&h->seq, rd->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// A fast candidate (k_remit precomputed its state after its group: a pop at
+// queue position 0 and at most one run pop; decof: kNoDec if it was not
+// dispatched, else its first decision's offset): the stores apply_one would
+// make for that case, with no walk -- the run pop's decision, the reduced
+// reservation tags of the queued requests (the new front's and position 2's
+// precomputed; from position 3 on read, reduced and written, every load
+// issued before the first store), prev r, and the new front's ScanRec with
+// its ready flag.  A front left by a priority pop was seen by a later
+// limit-scanning pull iff the group's last decision precedes the round's
+// last priority pull (or the round is terminal); one left by a reservation
+// pop iff the priority pulls ran.
+__device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandRec& cd,
+                                  uint32_t d, const PostRec& pr) {
+  const uint32_t s = cd.slot;
+  const uint8_t f0 = cd.f();
+  if (d == kNoDec) {  // not dispatched: the pending mark settles
+    if (f0 & F_PMARK)
+      tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (rc.p_runs ? F_READY : 0));
+    return;
+  }
+  const uint32_t bits = pr.bits;
+  const bool prio = bits & 1u;
+  const uint32_t run = (bits >> 2) & 1u;
+  const uint32_t c = cd.c, h = cd.h;
+  const uint32_t pops = 1 + run;
+  const uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
+  if (prio) {
+    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+    const double off = pr.off;
+    // positions >= 3, kDeepBatch at a time: loads, then stores
+    for (uint32_t k0 = 3; k0 < c; k0 += kDeepBatch) {
+      double v[kDeepBatch];
+#pragma unroll
+      for (int j = 0; j < kDeepBatch; ++j)
+        if (k0 + j < c) v[j] = ring[(h + k0 + j) & tb.qmask].r;
+#pragma unroll
+      for (int j = 0; j < kDeepBatch; ++j)
+        if (k0 + j < c) ring[(h + k0 + j) & tb.qmask].r = __dsub_rn(v[j], off);
+    }
+    if (nc2) ring[nh].r = pr.fr;
+    if (!run && c >= 3) ring[(h + 2) & tb.qmask].r = pr.r2;
+    tb.rec[s].prev_r = pr.prev_r;
+  }
+  if (run) {
+    dmc_decision x;
+    x.handle = pr.handle1;
+    x.tag_r = pr.r1;
+    x.tag_p = pr.p1;
+    x.tag_l = pr.l1;
+    x.slot = s;
+    x.cost = pr.cost1;
+    x.phase = DMC_PHASE_RESERVATION;
+    x.flags = 0;
+    rc.out[d + 1] = x;
+  }
+  uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
+  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
+  if (nc2) {
+    o.r = pr.fr;
+    o.pk = pr.fpk;
+    o.l = pr.fl;
+    const uint32_t last = d + run;  // the group's last decision
+    const bool seen =
+        prio ? (rc.terminal || (rc.g_last != kNoneR && last < rc.g_last)) : rc.p_runs;
+    if (seen && (bits & 2u)) f |= F_READY;
+  }
+  o.flags = f;
+  tb.sc[s] = o;
+}
+
 // Candidates, one thread each; k_rapply's blocks 2j and 2j + 1 take emit
 // block j's segment of the candidate arrays, its last block ends the round
 // (the summary to host memory, the device-API result record).  Fast
-// candidates were applied by k_rrank (apply_fast) and are skipped here; the
-// others (several records, a fast group cut by the round's end, delayed
-// mode, the radix path) replay their walks
+// candidates store their precomputed state (apply_fast); the others
+// (several records, a fast group cut by the round's end, delayed mode,
+// limit-break rounds, the radix path) replay their walks
 // for exactly the pops the ranking stamped (R pops, then P groups from the
 // post-R state), write the decision records and store the new state: ring
 // head/count, front cache, reduced reservation tags (immediate: every queued
@@ -2236,9 +2232,16 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
          i += kApplyPerEmit * kBlockR) {
       const uint32_t ci = base + i;
       uint64_t t0 = dbg ? wall_clock64() : 0;
-      const uint32_t d = decof[ci];
-      if (d != kSlowCand && !rc.ovf) continue;  // a fast candidate: k_rrank applied it
+      // one level of coalesced loads: the candidate, its decision offset and
+      // its precomputed state (both lines: a run's second line is no further
+      // round trip)
       const CandRec c = cand[ci];
+      const uint32_t d = decof[ci];
+      const PostRec pr = post[ci];
+      if (d != kSlowCand && !rc.ovf) {
+        apply_fast(tb, rc, c, d, pr);
+        continue;
+      }
       rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
       if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;
       apply_one(tb, rc, c, stage + threadIdx.x * kApplyStage);
