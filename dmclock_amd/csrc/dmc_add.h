@@ -13,11 +13,13 @@ namespace dmc {
 
 // A batch (a run of add_request_time calls with no activation inside) is
 // grouped by client without sorting: k_add_link counts each client's requests
-// with one atomic per request and files the first kAddSlots batch positions
-// in the client's slot buffer; k_add_chain then lets one thread per client
-// replay that client's requests in batch order.  Clients with more than
-// kAddSlots requests in the batch (rare: 64K requests over 1M clients is
-// Poisson(1/16)) are replayed by a scan of the batch's slot column, in order.
+// with one atomic per request on the client's ScanRec line (ScanRec::nadd,
+// the line k_add_chain reads anyway) and files the batch positions of the
+// client's later filers (filing order 1 .. kAddSlots - 1) in its slot buffer;
+// k_add_chain then lets the first filer replay that client's requests in
+// batch order.  Clients with more than kAddSlots requests in the batch (rare:
+// 64K requests over 1M clients is Poisson(1/16)) are replayed by a scan of
+// the batch's slot column, in order.
 constexpr uint32_t kAddSlots = 16;
 
 struct AddParams {
@@ -64,6 +66,8 @@ struct AddState {
   uint64_t last_tick;
   uint8_t flags;
   bool front_set;
+  bool cd_set, tick_set;    // cur_delta / cur_rho, last_tick changed (ClientAux is
+                            // written, never read, by the add path)
   Tag3 front;
 };
 
@@ -99,6 +103,7 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
     assign_unpinned(st.prev.p, tag.p);
     st.prev.arrival = tag.arrival;
     st.last_tick = tick;
+    st.tick_set = true;
   } else {
     if (rq.cost == 0) {
       p.rc[pos] = DMC_EBADTAG;
@@ -132,14 +137,17 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   ++st.count;
   st.cd = rq.delta;
   st.cr = rq.rho;
+  st.cd_set = true;
   p.rc[pos] = DMC_OK;
 }
 
 // Slot s of the batch is not registered: every request of it gets ENOTREG.
 __device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t m,
-                                        const uint32_t* abuf, const uint32_t* aslot) {
+                                        uint32_t i1, const uint32_t* abuf,
+                                        const uint32_t* aslot) {
   if (m <= kAddSlots) {
-    for (uint32_t j = 0; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
+    p.rc[i1] = DMC_ENOTREG;
+    for (uint32_t j = 1; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
   } else {
     for (uint32_t j = 0; j < p.n; ++j)
       if (aslot[j] == s) p.rc[j] = DMC_ENOTREG;
@@ -147,23 +155,27 @@ __device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t
 }
 
 // The replay of slot s's m requests of the batch (m = its batch count, read
-// from *acnt with the client's state when acnt is set, which is then reset
-// for the next batch; its batch positions in abuf, or found by a scan of the
-// slot column when m > kAddSlots; i1: the position when m == 1), in batch
-// order, with the activation bookkeeping of ActBuf when act.cold is set.  An
-// unregistered slot (checked here when acnt is set) rejects its requests.
-// Leaves the slot's new state in *out (count, flags, front when set).  Every
-// load is issued before the first store (on gfx950 a load's wait also waits
-// for the wave's earlier stores).
+// with the client's state from ScanRec::nadd when `counted`, which is then
+// reset for the next batch; i1: the first filer's batch position, the other
+// positions in abuf, or found by a scan of the slot column when m >
+// kAddSlots), in batch order, with the activation bookkeeping of ActBuf when
+// act.cold is set.  An unregistered slot (checked here when counted) rejects
+// its requests.  Leaves the slot's new state in *out (count, flags, front
+// when set).  Every load is issued before the first store (on gfx950 a
+// load's wait also waits for the wave's earlier stores); ClientAux is only
+// written.
 __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint32_t s,
                                       uint32_t m, uint32_t i1, const uint32_t* abuf,
                                       const uint32_t* aslot, const ActBuf& act,
-                                      AddState* out, uint32_t* acnt = nullptr) {
+                                      AddState* out, bool counted = false) {
   const uint32_t i = i1;
   // position i1's request, requested with the client's state (the usual
   // case, m == 1, needs nothing else from the batch)
   const dmc_request rq1 = p.reqs[i];
-  if (acnt) m = acnt[s];
+  // the ScanRec's cursor word: head, count, flags and the batch count
+  uint64_t* cw = reinterpret_cast<uint64_t*>(&tb.sc[s].head);
+  const uint64_t cur = *cw;
+  if (counted) m = (uint32_t)(cur >> 32);
   AddState st;
   st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
   st.rinv = tb.rec[s].r_inv;
@@ -172,19 +184,24 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   st.fetched = false;
   if (tb.binfo) st.bound = tb.binfo[s];
   const double pd = tb.rec[s].pd;
-  st.head = tb.sc[s].head;
-  st.count = tb.sc[s].count;
-  st.flags = tb.sc[s].flags;
-  st.cd = tb.aux[s].cur_delta;
-  st.cr = tb.aux[s].cur_rho;
-  st.last_tick = tb.aux[s].last_tick;
+  st.head = (uint32_t)(cur & 0xffu);
+  st.count = (uint32_t)((cur >> 8) & 0xffu);
+  st.flags = (uint8_t)(cur >> 16);
+  st.cd = st.cr = 0;
+  st.last_tick = 0;
+  st.cd_set = st.tick_set = false;
   st.front_set = false;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   // batched activations: this client's contribution to the idle reset before
   // and after its requests (see ActBuf)
-  if (acnt && !(st.flags & F_REG)) {
-    acnt[s] = 0;  // ready for the next batch
-    add_chain_notreg(p, s, m, abuf, aslot);
+  // the cursor word as stored back: the batch count cleared for the next batch
+  auto store_cursor = [&] {
+    *cw = (uint64_t)(st.head & 0xffu) | ((uint64_t)(st.count & 0xffu) << 8) |
+          ((uint64_t)st.flags << 16) | (cur & 0xff000000ull);
+  };
+  if (counted && !(st.flags & F_REG)) {
+    store_cursor();  // (unchanged; the batch count cleared)
+    add_chain_notreg(p, s, m, i, abuf, aslot);
     return;
   }
   const bool idle0 = (st.flags & F_IDLE) != 0;
@@ -213,12 +230,13 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   } else if (m <= kAddSlots) {
     // the client's batch positions in ascending order, by repeated selection
     // over its (L2-resident) slot-buffer row
+    // (filing order 0 is this thread's own position i)
     const uint32_t* row = abuf + (size_t)s * kAddSlots;
     uint32_t last = 0;
     for (uint32_t j = 0; j < m; ++j) {
       uint32_t next = 0xffffffffu;
       for (uint32_t k = 0; k < m; ++k) {
-        uint32_t v = row[k];
+        uint32_t v = k == 0 ? i : row[k];
         if ((j == 0 || v > last) && v < next) next = v;
       }
       step(next);
@@ -240,11 +258,15 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
     tb.rec[s].w_inv = st.winv;
     tb.rec[s].l_inv = st.linv;
   }
-  tb.sc[s].count = (uint8_t)st.count;
-  tb.sc[s].flags = st.flags;
-  tb.aux[s].cur_delta = st.cd;
-  tb.aux[s].cur_rho = st.cr;
-  tb.aux[s].last_tick = st.last_tick;
+  store_cursor();
+  if (st.cd_set && st.tick_set) {
+    tb.aux[s] = ClientAux{st.cd, st.cr, st.last_tick};
+  } else if (st.cd_set) {
+    tb.aux[s].cur_delta = st.cd;
+    tb.aux[s].cur_rho = st.cr;
+  } else if (st.tick_set) {
+    tb.aux[s].last_tick = st.last_tick;
+  }
   if (st.front_set) {
     // the new front's heap keys (pk with the prop_delta it has now; an
     // activation later in the batch rewrites it, k_act_resolve)
@@ -252,7 +274,6 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
     tb.sc[s].pk = __dadd_rn(st.front.p, pd);
     tb.sc[s].l = st.front.l;
   }
-  if (acnt) acnt[s] = 0;  // ready for the next batch
   *out = st;
 }
 

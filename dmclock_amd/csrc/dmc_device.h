@@ -67,7 +67,9 @@ struct alignas(32) ScanRec {
   uint8_t head, count;  // request ring cursor (ring capacity <= 64)
   uint8_t flags;        // F_*
   uint8_t pad0;
-  uint32_t pad1;
+  uint32_t nadd;        // the add batch in flight: the client's requests in it
+                        // (k_add_link's atomic; k_add_chain resets it; 0
+                        // outside a batch)
 };
 static_assert(sizeof(ScanRec) == 32, "ScanRec must be 32 bytes");
 

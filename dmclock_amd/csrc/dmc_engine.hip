@@ -146,7 +146,7 @@ __global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_
 // The first node of an add segment: its arguments are the segment's per-call
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
-__global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
+__global__ void k_add_link(AddParams p, Table tb,
                            uint32_t* abuf, uint32_t* apos, uint32_t* aslot,
                            AddParams* pblk, ActBuf act = ActBuf{}) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,12 +164,13 @@ __global__ void k_add_link(AddParams p, Table tb, uint32_t* acnt,
     p.rc[i] = DMC_ENOTREG;  // (no replay will see this request)
     return;
   }
-  uint32_t pos = atomicAdd(&acnt[s], 1u);
+  uint32_t pos = atomicAdd(&tb.sc[s].nadd, 1u);
   apos[i] = pos;
-  if (pos < kAddSlots) abuf[(size_t)s * kAddSlots + pos] = i;
+  // (filing order 0 replays the client's requests and knows its own position)
+  if (pos - 1u < kAddSlots - 1u) abuf[(size_t)s * kAddSlots + pos] = i;
 }
 
-__global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
+__global__ void k_add_chain(Table tb, const AddParams* pblk,
                             const uint32_t* abuf, const uint32_t* apos,
                             const uint32_t* aslot, ActBuf act = ActBuf{}) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -186,7 +187,7 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk, uint32_t* acnt,
   if (pos0 != 0) return;  // the client's first filer replays its requests
   // the next: the client's batch count with its state
   AddState st;
-  add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, acnt);
+  add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, true);
 }
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
@@ -249,13 +250,13 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
 // Batched activations, step 1 (after k_add_link, before k_add_chain): the
 // idle reset's minimum over the clients whose contribution the batch does
 // not change: registered, non-idle, and not (empty and touched by the batch).
-__global__ void k_act_base(Table tb, const uint32_t* acnt, uint64_t* parts) {
+__global__ void k_act_base(Table tb, uint64_t* parts) {
   uint64_t m = kMaxKey;
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
        s += gridDim.x * blockDim.x) {
     const ScanRec r = tb.sc[s];
     if ((r.flags & F_REG) && !(r.flags & F_IDLE)) {
-      if (r.count == 0 && acnt[s]) continue;  // changes inside the batch: positions
+      if (r.count == 0 && r.nadd) continue;  // changes inside the batch: positions
       uint64_t k = okey(r.count ? r.pk : __dadd_rn(tb.rec[s].prev_p, tb.rec[s].pd));
       m = k < m ? k : m;
     }
@@ -1281,7 +1282,7 @@ struct dmc_queue {
   dmc_request* d_reqs = nullptr;
   int32_t* d_rc = nullptr;
   uint32_t *apos = nullptr, *aslot = nullptr;   // per batch request
-  uint32_t *acnt = nullptr, *abuf = nullptr;    // per client (N, N * kAddSlots)
+  uint32_t* abuf = nullptr;  // per client: later filers' batch positions (N * kAddSlots)
   AddParams* apblk = nullptr;
   // decisions (host API)
   uint32_t dcap = 0;
@@ -1646,10 +1647,10 @@ int slot_bits(uint32_t n) {
 void enqueue_add(dmc_queue* q, const AddParams& ap) {
   prof_gate(q);
   uint32_t g = (ap.n + kBlock - 1) / kBlock;
-  klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, q->tb, q->acnt,
+  klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, q->tb,
           q->abuf, q->apos, q->aslot, q->apblk, ActBuf{});
   klaunch(q, DMC_PROF_ADD_CHAIN, k_add_chain, dim3(g), dim3(kBlock), 0, q->tb,
-          (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+          (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
           (const uint32_t*)q->apos, (const uint32_t*)q->aslot, ActBuf{});
 }
 
@@ -1668,7 +1669,7 @@ int add_segment(dmc_queue* q, const dmc_request* d_reqs, uint32_t n,
   }
   Table tb = q->tb;
   ActBuf noact{};
-  void* args[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk, &noact};
+  void* args[] = {&ap, &tb, &q->abuf, &q->apos, &q->aslot, &q->apblk, &noact};
   return graph_replay(q, *g, args);
 }
 
@@ -1788,15 +1789,15 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   uint32_t g = (n + kBlock - 1) / kBlock;
   pb(q, DMC_PROF_ADD_LINK);
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
-                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk, act);
+                     q->abuf, q->apos, q->aslot, q->apblk, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
   hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
-                     (const uint32_t*)q->acnt, q->act_parts);
+                     q->act_parts);
   pe(q);
   pb(q, DMC_PROF_ADD_CHAIN);
   hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+                     (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
                      (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
@@ -1834,15 +1835,15 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   uint32_t g = (n + kBlock - 1) / kBlock;
   pb(q, DMC_PROF_ADD_LINK);
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
-                     q->acnt, q->abuf, q->apos, q->aslot, q->apblk, act);
+                     q->abuf, q->apos, q->aslot, q->apblk, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
   hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
-                     (const uint32_t*)q->acnt, q->act_parts);
+                     q->act_parts);
   pe(q);
   pb(q, DMC_PROF_ADD_CHAIN);
   hipLaunchKernelGGL(k_add_chain, dim3(g), dim3(kBlock), 0, q->stream, q->tb,
-                     (const AddParams*)q->apblk, q->acnt, (const uint32_t*)q->abuf,
+                     (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
                      (const uint32_t*)q->apos, (const uint32_t*)q->aslot, act);
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
@@ -2675,7 +2676,6 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
   // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
-  rc |= A(&q->acnt, N);
   rc |= A(&q->abuf, (size_t)N * kAddSlots);
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
@@ -2724,7 +2724,7 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
-                  q->d_reqs, q->d_rc, q->apos, q->aslot, q->acnt, q->abuf,
+                  q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
                   q->apblk, q->d_dec, q->stage};
   for (void* p : ptrs)
     dfree(p);
@@ -3308,7 +3308,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       } else {
         Table tb = q->tb;
         ActBuf noact{};
-        void* a1[] = {&ap, &tb, &q->acnt, &q->abuf, &q->apos, &q->aslot, &q->apblk,
+        void* a1[] = {&ap, &tb, &q->abuf, &q->apos, &q->aslot, &q->apblk,
                       &noact};
         const bool sampled = use_sample(q, false);
         uint64_t* skr = sampled ? q->skr : nullptr;
