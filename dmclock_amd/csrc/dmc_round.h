@@ -52,13 +52,16 @@ constexpr int kBlockR = 256;
 constexpr int kHistBinsR = 2048;        // per phase
 constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
 constexpr int kNBPhase = kNBR / 2;
-// Same-address atomics from every block of a launch serialise at the memory
-// side (~12 ns each): the histogram is sharded 8 ways (block % 8, one shard
-// per XCD) and the pick combines the shards.
+// The histogram's shards (block % kShards): one, measured fastest (select
+// 15.9 -> 13.4 us against 8 XCD shards): the pick's loads of every shard
+// cost more than the same-address flush atomics of k_rhist's 32 blocks.
 #ifndef DMC_HIST_SHARDS
-#define DMC_HIST_SHARDS 8
+#define DMC_HIST_SHARDS 1
 #endif
 constexpr int kShards = DMC_HIST_SHARDS;
+// k_remit's sampled-threshold counts: one per XCD (256 blocks' same-address
+// atomics would serialise)
+constexpr int kCntShards = 8;
 constexpr uint32_t kBinCapR = 512;      // entries per rank bin (2 per thread of k_rrank)
 constexpr uint32_t kNoneR = 0xffffffffu;
 constexpr uint8_t F_PMARK = 8;          // pending limit-scan mark (this round)
@@ -116,7 +119,7 @@ struct Round {
   uint32_t brk_bad;      // ... whose state was not break-ready (overflow = 5)
   uint32_t brk_prio;     // ... its priority pops (counted by k_rapply)
   uint32_t brk_done;     // ... k_rapply's block ticket (the summary goes last)
-  uint32_t ccnt[2 * kShards];  // sampled rounds: first keys at or below T, per
+  uint32_t ccnt[2 * kCntShards];  // sampled rounds: first keys at or below T, per
                                // phase, in XCD shards (k_remit)
   uint32_t bin_max[2];   // diagnostics: largest rank bin per phase
   uint32_t ecnt[4];      // diagnostics: candidates fast / several records /
@@ -1317,7 +1320,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
     const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
     uint32_t c0 = 0, c1 = 0;
-    for (int i = 0; i < kShards; ++i) {
+    for (int i = 0; i < kCntShards; ++i) {
       c0 += rd->ccnt[2 * i];
       c1 += rd->ccnt[2 * i + 1];
     }
@@ -1429,11 +1432,11 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
 // coalesced.  A slot is a candidate iff its first R key is <= T_R or (the
 // priority pulls run and) its first P key is <= T_P; non-candidates settle
 // their pending limit-scan marks here (k_rapply settles the candidates').
-// The block compacts its candidates in LDS (about 270 of its 4096 slots in
-// a config-3 round) and appends them to the candidate list with one atomic;
-// its first threads then walk one candidate each, full waves, with the
-// rank-bin table staged in LDS; a candidate's first record reserves its
-// rank-bin place before its walk (rank_bin_q).  Bin-rank path: the last block to finish
+// Each wave compacts its candidates (about 17 of its 256 slots in a
+// config-3 round) into the block's list in LDS, at a base one LDS atomic
+// hands it, and its lanes walk them at once, with the rank-bin table staged
+// in LDS; a candidate's first record reserves its rank-bin place before its
+// walk (rank_bin_q).  Bin-rank path: the last block to finish
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
 #ifndef DMC_EMIT_THREADS
@@ -1443,6 +1446,9 @@ constexpr int kEmitThreads = DMC_EMIT_THREADS;
 constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster,
                              // and a slower last-block tail)
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
+// walkers with a staging slice per wave: its first lanes (a wave with more
+// candidates walks the rest from global memory)
+constexpr int kEmitStageLanes = kEmitStageThreads / (kEmitThreads / 64);
 template <bool BRK>
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
@@ -1461,11 +1467,11 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   __shared__ uint2 s_fb[kEmitThreads];
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
-  __shared__ uint32_t wsum[kEmitThreads / 64];
   __shared__ uint32_t s_tot, s_last;
   __shared__ uint32_t s_cnt[2], s_ec[4];
   if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
   if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_tot = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
@@ -1534,19 +1540,19 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
       atomicAdd(&s_cnt[1], np);
     }
   }
-  // block compaction (static indices only: no private-memory arrays)
+  // Wave-local compaction (static indices only: no private-memory arrays):
+  // each wave appends its candidates to the block's list at a base one LDS
+  // atomic hands it, and its lanes walk them at once -- no block barrier
+  // between a wave's key loads and its walkers' first loads.
   uint32_t incl = cnt;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t o = __shfl_up(incl, d);
     if (lane >= d) incl += o;
   }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint32_t wbase = 0, btot = 0;
-  for (int i = 0; i < kEmitThreads / 64; ++i) {
-    wbase += i < w ? wsum[i] : 0u;
-    btot += wsum[i];
-  }
+  const uint32_t wtot = __shfl(incl, 63);
+  uint32_t wbase = 0;
+  if (lane == 0 && wtot) wbase = atomicAdd(&s_tot, wtot);
+  wbase = __shfl(wbase, 0);
   {
     uint32_t o = wbase + incl - cnt;
 #pragma unroll
@@ -1559,43 +1565,43 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
       }
     }
   }
-  if (threadIdx.x == 0) s_tot = btot;
   {
     uint32_t fw = 0;
 #pragma unroll
     for (int j = 0; j < kEmitPer; ++j) fw |= (uint32_t)f[j] << (8 * j);
     s_fb[threadIdx.x] = make_uint2(bits, fw);
   }
-  __syncthreads();
-  // The candidate count (a statistic) and the sampled counts are published
-  // (same-address atomics, serialised over the grid) by the last wave, which
-  // rarely walks, while the walks run: on gfx950 a wave's load waits also
-  // wait for its earlier memory operations.
-  constexpr uint32_t kAllocT = kEmitThreads - 64;
-  if (threadIdx.x == kAllocT) {
-    // (the total is a statistic: the candidate arrays are per block)
-    if (btot) atomicAdd(&rd->n_cand, btot);
-    if (sampled) {
-      uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kShards);
-      if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
-      if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
-    }
-  }
-  const uint32_t tot = s_tot;
+  // (the wave's list entries, written by its lanes, are read by other lanes
+  // of the same wave: LDS operations of one wave complete in order)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 2] = wall_clock64();
   // candidate index: the block's segment of the candidate arrays (kEmitChunk
   // per block; k_rapply's blocks take their emit block's segment)
   const uint32_t cbase = blockIdx.x * kEmitChunk;
-  for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) {
+  for (uint32_t j = lane; j < wtot; j += 64) {
+    const uint32_t i = wbase + j;
     const uint32_t cat = emit_one<BRK>(
         tb, rd, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
-        threadIdx.x < (uint32_t)kEmitStageThreads ? stage + threadIdx.x * kEmitStage
-                                                  : nullptr,
+        lane < kEmitStageLanes ? stage + (w * kEmitStageLanes + lane) * kEmitStage : nullptr,
         bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
     atomicAdd(&s_ec[cat], 1u);
   }
   __syncthreads();
+  const uint32_t tot = s_tot;
   if (threadIdx.x < 4 && s_ec[threadIdx.x]) atomicAdd(&rd->ecnt[threadIdx.x], s_ec[threadIdx.x]);
+  // the candidate count (a statistic) and the sampled counts, published
+  // after the walks (same-address atomics, serialised over the grid; on
+  // gfx950 a wave's load waits also wait for its earlier memory operations)
+  if (threadIdx.x == 64) {
+    if (tot) atomicAdd(&rd->n_cand, tot);
+    if (sampled) {
+      uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kCntShards);
+      if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
+      if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
+    }
+  }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 3] = wall_clock64();
   // the block's candidates, copied from LDS in one coalesced pass
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) cand[cbase + i] = bl[i];
