@@ -1228,14 +1228,12 @@ struct dmc_queue {
   HostRound* d_hround = nullptr; // its device address
   uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
-  uint32_t* sbn = nullptr;    // rank-bin table per phase and histogram bin (k_rhist's pick)
   uint64_t *skr = nullptr, *skp = nullptr;  // N / kSample: the threshold histogram's sample
   bool exact_next = false;    // re-run a round whose sampled threshold failed exactly
   int sample_mode = 1;        // DMC_OPT_SAMPLE: 0 exact, 1 sampled, 2 sampled (test: no margin)
   uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics;
                                                   // bcount: 8 bytes per bin)
   uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
-  uint32_t* hist_done = nullptr;  // k_rhist's block ticket counter
   uint32_t* emit_done = nullptr;  // k_remit's block ticket counter
   uint32_t *bsoff = nullptr, *bpoff = nullptr;   // their prefixes (k_rbscan)
   BRecR* brec = nullptr;      // kNBR * kBinCapR rank-bin records
@@ -2178,19 +2176,19 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
   klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN), dim3(kScanBlock), 0,
           tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
-          q->rd, cp, sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32);
+          q->rd, cp, sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32, q->hist);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
-            (const RoundPart*)q->rparts, gN, q->rd, q->hist, q->sbn, q->hist_done,
+            (const RoundPart*)q->rparts, gN, q->rd, q->hist,
             q->sample_mode == 2 ? 2 : 1);
   else
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
-            gN, q->rd, q->hist, q->sbn, q->hist_done, 0);
+            gN, q->rd, q->hist, 0);
   klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
-          q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->sbn,
+          q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->hist,
           q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
           q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
@@ -2262,7 +2260,7 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   uint64_t* kr = sampled ? nullptr : q->keyr;
   uint64_t* kp = sampled ? nullptr : q->keyp;
   void* args[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                  &skr, &skp, &q->k32};
+                  &skr, &skp, &q->k32, &q->hist};
   return graph_replay(q, *g, args);
 }
 
@@ -2653,7 +2651,6 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->k32, N);
   rc |= A(&q->meta, N);
   rc |= A(&q->hist, kShards * 2 * kHistBinsR);
-  rc |= A(&q->sbn, 2 * kHistBinsR);
   rc |= A(&q->skr, (N + kSample - 1) / kSample);
   rc |= A(&q->skp, (N + kSample - 1) / kSample);
   q->step_grid = grid_for(N, 1024);
@@ -2665,7 +2662,6 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsize, kNBR);
   rc |= A(&q->bcnt, kNBR);
-  rc |= A(&q->hist_done, 1);
   rc |= A(&q->emit_done, 1);
   rc |= A(&q->bsoff, kNBR);
   rc |= A(&q->bpoff, kNBR);
@@ -2720,8 +2716,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   Table& t = q->tb;
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
-                  q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist, q->sbn,
-                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->hist_done, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist,
+                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
@@ -3316,7 +3312,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         uint64_t* kr = sampled ? nullptr : q->keyr;
         uint64_t* kp = sampled ? nullptr : q->keyp;
         void* a2[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                      &skr, &skp, &q->k32};
+                      &skr, &skp, &q->k32, &q->hist};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }

@@ -459,7 +459,7 @@ template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
 k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
           RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
-          uint2* k32) {
+          uint2* k32, uint32_t* hist) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.k_total = cp.k_total;
@@ -519,7 +519,7 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
                     : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
   }
   // (a limit-break round has no reservation entries: its n_r counts the
-  // slots that are not break-ready, for k_rhist's last block)
+  // slots that are not break-ready, for k_rhist's block 0)
   if (bad) acc.n_r += 1;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
@@ -527,6 +527,13 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
     if (s < tb.n) scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
   sh[threadIdx.x] = acc;
+  // the threshold histogram k_rhist fills, cleared (the previous round's
+  // k_remit blocks have read it)
+  {
+    for (uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
+         gi < (uint32_t)(kShards * 2 * kHistBinsR); gi += gridDim.x * blockDim.x)
+      hist[gi] = 0;
+  }
   __syncthreads();
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
@@ -577,19 +584,15 @@ constexpr int kHistBlocksR = 256;
 #endif
 constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of 1M: 4 per thread
                                         // (16 and 64 blocks measured no faster)
-__device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbn, int sampled);
 // n keys per phase: every slot's first keys (keyr / keyp, exact), or the
-// scan's 1/kSample sample of them (sampled)
+// scan's 1/kSample sample of them (sampled: 1, or 2 in the test mode of
+// need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
+// every k_remit block picks the thresholds and rank bins from it (no block
+// ticket, no last-block tail here).  Block 0 stores the round's totals.
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist, uint32_t* sbn,
-        uint32_t* done, int sampled) {
+        uint32_t nparts, Round* rd, uint32_t* hist, int sampled) {
   __shared__ uint32_t lh[2][kHistBinsR];
-  __shared__ uint32_t s_last;
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) atomicMin(&rd->tdbg[0], (unsigned long long)wall_clock64());
-#endif
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
     lh[0][b] = 0;
     lh[1][b] = 0;
@@ -616,6 +619,23 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
   };
   if (s < n) load(s);
   const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the round's totals (a limit-break round has no reservation entries: its
+    // scan's n_r counts the slots that are not break-ready)
+    const bool brk_bad = rd->brk && tot.n_r;
+    RoundPart t2 = tot;
+    if (rd->brk) t2.n_r = 0;
+    rd->tot = t2;
+    rd->n_r = t2.n_r;
+    rd->p_runs = t2.n_r < (uint64_t)rd->k_total ? 1 : 0;
+    rd->sampled = (uint32_t)sampled;
+    if (brk_bad) {
+      // the state is not the one a limit-break round assumes: nothing of
+      // the round takes effect, the host runs general pulls instead
+      rd->brk_bad = 1;
+      rd->overflow = 5;
+    }
+  }
   if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
     const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
     const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
@@ -635,54 +655,12 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
       if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
     }
   }
-  // ticket: the block's histogram atomics have completed (every wave waits
-  // for its own) before one lane takes it; the last block picks.  Only
-  // memory-side atomics cross blocks here (the shards, the ticket), so no
-  // release / acquire fence is needed (MI355X_MICROARCH.md, inter-workgroup
-  // visibility: nothing this kernel hands over sits in an L2)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  if (threadIdx.x == 0) {
-    atomicExch(done, 0u);  // ready for the next round
-    // the consumer side of MI355X_MICROARCH.md's cross-XCD hand-off: one
-    // agent-scope acquire, its wait, a block barrier, then plain loads of
-    // the shards (which every block updated with memory-side atomics)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[1] = wall_clock64();
-#endif
-  const bool brk_bad = rd->brk && tot.n_r;
-  RoundPart t2 = tot;
-  if (rd->brk) t2.n_r = 0;  // (brk: no reservation entries)
-  pick_both(rd, t2, hist, sbn, sampled);
-  if (threadIdx.x == 0) {
-    // the round's totals (stored by the last block, after its barriers: a
-    // barrier waits for the thread's outstanding stores)
-    rd->tot = t2;
-    rd->n_r = t2.n_r;
-    rd->p_runs = t2.n_r < (uint64_t)rd->k_total ? 1 : 0;
-    rd->sampled = sampled ? 1 : 0;
-    if (brk_bad) {
-      // the state is not the one a limit-break round assumes: nothing of
-      // the round takes effect, the host runs general pulls instead
-      rd->brk_bad = 1;
-      rd->overflow = 5;
-    }
-  }
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[2] = wall_clock64();
-#endif
 }
 
 // Threshold and rank-bin table of one phase, by one half (kPickHalf
-// threads) of the last k_rhist block; the other half does the other phase
-// at the same time (the block barriers line up: both halves run this code).
+// threads) of a k_remit block (every block, from the same histogram: the
+// same result); the other half does the other phase at the same time (the
+// block barriers line up: both halves run this code).
 // T: the largest key of the bin holding the need-th first key (any T at or
 // above the k-th smallest entry key is exact; a bin edge only admits extra
 // candidates).  The phase's kNBPhase rank bins are spread over the
@@ -708,13 +686,13 @@ __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
 
 __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                                   const RoundPart& tot, const KeyMap& km, uint32_t sh1,
-                                  Round* rd,
-                                  uint32_t* hist, uint32_t* sbn, uint32_t* wsum,
-                                  uint32_t* s_tb, uint32_t* s_C, uint64_t* s_T) {
+                                  const uint32_t* hist, uint32_t* sbn, PhaseSel* ps,
+                                  uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
+                                  uint64_t* s_T) {
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
-  uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
+  const uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   if (t == 0) {
     *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
     *s_C = 0;
@@ -737,13 +715,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
       local += h[j];
     }
   }
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[6] = wall_clock64();
-#endif
   const uint32_t before = half_excl_scan(local, wsum);
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[7] = wall_clock64();
-#endif
   if (need && ne > need && before < need_h && before + local >= need_h) {
     uint32_t cum = before;
 #pragma unroll
@@ -776,9 +748,6 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     }
   }
   __syncthreads();
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[8] = wall_clock64();
-#endif
   const uint32_t C = *s_C > 0 ? *s_C : 1;
   // Every non-empty histogram bin up to T's gets one rank bin, and the
   // spare ones go in proportion to the counts, h * S / C in single precision
@@ -821,13 +790,6 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     sbn[p * kHistBinsR + b] = (p * kNBPhase + first) | (num << 16);
     nb += ns[j];
   }
-  // clear this phase's shards for the next round (plain stores, written
-  // back at the kernel's end, before the next round's atomics; last, since a
-  // block barrier waits for the thread's outstanding stores)
-#pragma unroll
-  for (int j = 0; j < kBinsPerThreadR; ++j)
-#pragma unroll
-    for (int i = 0; i < kShards; ++i) hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j] = 0;
   if (t == 0) {
     PhaseSel z{};
     z.kmin = tot.mn[p];
@@ -848,12 +810,12 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     // last bin spans [top, hitop]
     z.inv_w = bitsd((uint64_t)(1023 - sh1) << 52);
     z.inv_last = 1.0 / ((double)(z.hitop - top) + 1.0);
-    rd->ph[p] = z;
+    *ps = z;
   }
 }
 
-// Thresholds and rank-bin tables of both phases, by the last k_rhist block
-// (1024 threads): phase 0 in threads [0, 512), phase 1 in [512, 1024).
+// Thresholds and rank-bin tables of both phases, by a k_remit block (1024
+// threads): phase 0 in threads [0, 512), phase 1 in [512, 1024).
 // needed first keys -> histogram units: exact, or for a 1/kSample sample
 // need / kSample plus a margin of 2 % + 4 standard deviations + 16 (a
 // sampled threshold admitting fewer than `need` first keys is caught by
@@ -867,12 +829,12 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
   return v >= 4294967295.0 ? 0xffffffffu : (uint32_t)v;
 }
 
-__device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
-                          uint32_t* sbn, int sampled) {
+// (sbn, ps: LDS; the results are complete after the last barrier inside)
+__device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist,
+                          uint32_t* sbn, PhaseSel* ps, int sampled) {
   __shared__ uint32_t wsum[2][kPickHalf / 64];
   __shared__ uint32_t s_tb[2], s_C[2];
   __shared__ uint64_t s_T[2];
-  const uint32_t k = rd->k_total;
   const bool p_runs = tot.n_r < (uint64_t)k;
   const int p = threadIdx.x / kPickHalf;
   // R: all prefixes when they hold fewer than k entries; else every client
@@ -881,8 +843,9 @@ __device__ void pick_both(Round* rd, const RoundPart& tot, uint32_t* hist,
   const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
   const KeyMap km(tot.mn[p], tot.mx[p]);
-  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), rd,
-             hist, sbn, wsum[p], &s_tb[p], &s_C[p], &s_T[p]);
+  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hist,
+             sbn, &ps[p], wsum[p], &s_tb[p], &s_C[p], &s_T[p]);
+  __syncthreads();  // (ps, written by thread 0 of each half)
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -1085,11 +1048,17 @@ struct EmitV {
 
 // A client is a candidate iff its first R key is <= T_R or (the priority
 // pulls run and) its first P key is <= T_P.
+// (the thresholds are read from LDS: wave-uniform, moved to scalar registers)
+__device__ inline uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 struct CandPred {
   uint64_t TR, TP;  // 0: no candidates in that phase
   uint32_t TR32, TP32;
-  __device__ explicit CandPred(const Round* rd)
-      : TR(rd->ph[0].T), TP(rd->p_runs ? rd->ph[1].T : 0),
+  __device__ CandPred(const PhaseSel* ph, bool p_runs)
+      : TR(uniform_u64(ph[0].T)), TP(p_runs ? uniform_u64(ph[1].T) : 0),
         TR32(key32(TR) > 0xfffffffeu ? 0xfffffffeu : key32(TR)),
         TP32(key32(TP) > 0xfffffffeu ? 0xfffffffeu : key32(TP)) {}
   // exact: T is kMaxKey - 1 or the end of its quantum (see key32)
@@ -1143,7 +1112,8 @@ constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a sta
 // (BRK: a limit-break round, its own instantiation of k_remit: the general
 // walkers carry none of walk_p's break-mode code)
 template <bool BRK>
-__device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c,
+__device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* ph,
+                                const CandRec& c,
                                 uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
                                 PostRec* post, uint32_t* decof,
@@ -1152,7 +1122,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
   // their rank records done
   if (ck) ck[0] = wall_clock64();
   const uint32_t s = c.slot;
-  const uint64_t TR = rd->ph[0].T, TP = rd->ph[1].T;
+  const uint64_t TR = uniform_u64(ph[0].T), TP = uniform_u64(ph[1].T);
   const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
@@ -1170,7 +1140,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
     // is the first key of the candidate's first phase, key32_0 is its
     // quantum): the atomic's latency overlaps the walk
     const int ph0 = c.cr() ? 0 : 1;
-    acc.b0 = rank_bin_q((uint64_t)key32_0 << 32, rd->ph[ph0], ph0, sbn);
+    acc.b0 = rank_bin_q((uint64_t)key32_0 << 32, ph[ph0], ph0, sbn);
     acc.at0 = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long*>(bcount) + acc.b0,
                                   (1ull << 32) | 1ull);
     acc.pre = true;
@@ -1181,7 +1151,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
     ck[1] = wall_clock64();
   }
   if (c.cr()) {
-    EmitV v{0, s, &rd->ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
+    EmitV v{0, s, &ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_r(tb, rv, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
@@ -1189,7 +1159,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
     // the priority pulls run only after every R pop
     const uint32_t m = c.m;
     bool ready0 = m == 0 && (c.f() & F_READY);
-    EmitV v{1, s, &rd->ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
+    EmitV v{1, s, &ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0, 0, BRK);
@@ -1270,7 +1240,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const CandRec& c
 // same way (atomicExch).  A rank bin past kBinCapR aborts the round
 // (overflow = 2): the host re-runs it on the radix path.
 template <int THREADS>
-__device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
+__device__ void bin_prefix(Round* rd, const PhaseSel* ph, uint32_t* bcount, uint32_t* bsize,
                            uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff) {
   constexpr int per = kNBR / THREADS;
   constexpr int NW = THREADS / 64;
@@ -1318,7 +1288,7 @@ __device__ void bin_prefix(Round* rd, uint32_t* bcount, uint32_t* bsize,
     const uint32_t k = rd->k_total;
     const uint32_t needR = rd->p_runs ? 0xffffffffu : k;
     const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
-    const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
+    const uint64_t TR = ph[0].T, TP = rd->p_runs ? ph[1].T : 0;
     uint32_t c0 = 0, c1 = 0;
     for (int i = 0; i < kCntShards; ++i) {
       c0 += rd->ccnt[2 * i];
@@ -1454,7 +1424,7 @@ __global__ void __launch_bounds__(kEmitThreads)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
-        uint32_t* bcount, uint32_t* bsize, const uint32_t* sbn, DEnt* dense,
+        uint32_t* bcount, uint32_t* bsize, const uint32_t* hist, DEnt* dense,
         uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
         uint32_t* done, uint64_t* eclk = nullptr) {
   // eclk (debug): per block [0] start [1] keys + table staged [2] candidates
@@ -1469,6 +1439,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
   __shared__ uint32_t s_tot, s_last;
   __shared__ uint32_t s_cnt[2], s_ec[4];
+  __shared__ PhaseSel s_ph[2];
   if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
   if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_tot = 0;
@@ -1477,9 +1448,8 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
 #endif
   const uint32_t n = tb.n;
   const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
-  const CandPred pred(rd);
   const bool p_runs = rd->p_runs != 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   if (s0 + kEmitPer <= n) {
@@ -1505,10 +1475,12 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
       mt[j] = in ? meta[s0 + j] : 0;
     }
   }
-  // the rank-bin table staged while the keys are in flight
-  if (brec)
-    for (int i = threadIdx.x; i < 2 * kHistBinsR; i += kEmitThreads) ltab[i] = sbn[i];
-  __syncthreads();  // s_cnt zeroed before any wave adds to it
+  // the thresholds and the rank-bin table, picked from the round's
+  // histogram while the keys are in flight (its barriers also order the
+  // zeroing of s_cnt / s_tot before any wave adds to them)
+  pick_both(rd->k_total, rd->tot, hist, ltab, s_ph, (int)rd->sampled);
+  if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
+  const CandPred pred(s_ph, p_runs);
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
   uint8_t f[kEmitPer];
 #pragma unroll
@@ -1580,11 +1552,15 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   // candidate index: the block's segment of the candidate arrays (kEmitChunk
   // per block; k_rapply's blocks take their emit block's segment)
   const uint32_t cbase = blockIdx.x * kEmitChunk;
+  // this lane's staging slice (its address computed here, not held -- and
+  // spilled -- from the kernel's start)
+  uint32_t sli = (threadIdx.x >> 6) * kEmitStageLanes + lane;
+  asm volatile("" : "+v"(sli));
   for (uint32_t j = lane; j < wtot; j += 64) {
     const uint32_t i = wbase + j;
     const uint32_t cat = emit_one<BRK>(
-        tb, rd, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
-        lane < kEmitStageLanes ? stage + (w * kEmitStageLanes + lane) * kEmitStage : nullptr,
+        tb, rd, s_ph, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
+        lane < kEmitStageLanes ? stage + sli * kEmitStage : nullptr,
         bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
     atomicAdd(&s_ec[cat], 1u);
   }
@@ -1641,7 +1617,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[4] = wall_clock64();
 #endif
-  bin_prefix<kEmitThreads>(rd, bcount, bsize, bcnt, bsoff, bpoff);
+  bin_prefix<kEmitThreads>(rd, s_ph, bcount, bsize, bcnt, bsoff, bpoff);
   if (eclk && threadIdx.x == 0) eclk[5 * gridDim.x] = wall_clock64();
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) rd->tdbg[5] = wall_clock64();
