@@ -1231,11 +1231,9 @@ struct dmc_queue {
   uint64_t *skr = nullptr, *skp = nullptr;  // N / kSample: the threshold histogram's sample
   bool exact_next = false;    // re-run a round whose sampled threshold failed exactly
   int sample_mode = 1;        // DMC_OPT_SAMPLE: 0 exact, 1 sampled, 2 sampled (test: no margin)
-  uint32_t *bcount = nullptr, *bsize = nullptr;  // kNBR rank-bin counters (atomics;
-                                                  // bcount: 8 bytes per bin)
-  uint32_t* bcnt = nullptr;   // kNBR: their counts as the last k_remit block read them
-  uint32_t* emit_done = nullptr;  // k_remit's block ticket counter
-  uint32_t *bsoff = nullptr, *bpoff = nullptr;   // their prefixes (k_rbscan)
+  uint32_t* bcount = nullptr;  // kNBR rank-bin counters, 8 bytes each (k_remit's atomics:
+                               // records | group sizes << 32)
+  unsigned long long* bsup = nullptr;  // kNSup super-bin sums of them (k_remit's blocks)
   BRecR* brec = nullptr;      // kNBR * kBinCapR rank-bin records
   StepRed* red = nullptr;     // step partials (grid) + future record
   StepCtl* sctl = nullptr;
@@ -2181,22 +2179,21 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
             (const RoundPart*)q->rparts, gN, q->rd, q->hist,
-            q->sample_mode == 2 ? 2 : 1);
+            q->sample_mode == 2 ? 2 : 1, (unsigned long long*)q->bcount, q->bsup);
   else
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
-            gN, q->rd, q->hist, 0);
+            gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup);
   klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
-          q->decof, radix ? nullptr : q->brec, q->bcount, q->bsize, (const uint32_t*)q->hist,
-          q->dense, q->ecap, q->bcnt, q->bsoff, q->bpoff, q->emit_done,
-          q->debug ? q->dbg_etime : nullptr);
+          q->decof, radix ? nullptr : q->brec, q->bcount, q->bsup, (const uint32_t*)q->hist,
+          q->dense, q->ecap, q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
-    if (q->debug)
-      (void)hipMemcpyAsync(q->dbg_bins, q->bcnt, kNBR * sizeof(uint32_t),
-                           hipMemcpyDeviceToDevice, q->stream);
+    if (q->debug)  // (the record counts: the rank-bin counters' low words)
+      (void)hipMemcpy2DAsync(q->dbg_bins, sizeof(uint32_t), q->bcount, 2 * sizeof(uint32_t),
+                             sizeof(uint32_t), kNBR, hipMemcpyDeviceToDevice, q->stream);
     klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
-            (const uint32_t*)q->bcnt, (const uint32_t*)q->bsoff, (const uint32_t*)q->bpoff,
+            (const unsigned long long*)q->bcount, (const unsigned long long*)q->bsup,
             (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
   } else {
     // the exact LSD sort of the dense entries (dmc_sort.h), then each
@@ -2436,7 +2433,6 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
         std::fprintf(stderr, "emit clock %d: min %.2f med %.2f max %.2f us\n", ph, v[0],
                      v[nb / 2], v[nb - 1]);
       }
-      std::fprintf(stderr, "emit clock tail end: %.2f us\n", (e[5ull * nb] - t0) / 100.0);
       // per candidate: staging and walk durations
       std::vector<uint64_t> ck(4ull * nb * 512);
       (void)hipMemcpy(ck.data(), q->dbg_etime + 5 * 4096 + 8, 8ull * ck.size(),
@@ -2660,11 +2656,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->rd, 1);
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
-  rc |= A(&q->bsize, kNBR);
-  rc |= A(&q->bcnt, kNBR);
-  rc |= A(&q->emit_done, 1);
-  rc |= A(&q->bsoff, kNBR);
-  rc |= A(&q->bpoff, kNBR);
+  rc |= A(&q->bsup, kNSup);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
@@ -2717,8 +2709,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
                   q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist,
-                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsize, q->bcnt, q->emit_done, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
-                  q->bsoff, q->bpoff, q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
+                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
                   q->apblk, q->d_dec, q->stage};

@@ -52,6 +52,12 @@ constexpr int kBlockR = 256;
 constexpr int kHistBinsR = 2048;        // per phase
 constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
 constexpr int kNBPhase = kNBR / 2;
+// super-bins of 64 rank bins: k_remit's blocks sum their records per
+// super-bin in LDS and flush the sums, so that each k_rrank block finds its
+// bin's offsets from 64 super-bin sums and the <= 63 bins before it in its
+// super-bin (no prefix pass over all 4096 bins)
+constexpr int kSupBins = 64;
+constexpr int kNSup = kNBR / kSupBins;
 // The histogram's shards (block % kShards): one, measured fastest (select
 // 15.9 -> 13.4 us against 8 XCD shards): the pick's loads of every shard
 // cost more than the same-address flush atomics of k_rhist's 32 blocks.
@@ -591,8 +597,10 @@ constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of
 // ticket, no last-block tail here).  Block 0 stores the round's totals.
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist, int sampled) {
+        uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
+        unsigned long long* bcount, unsigned long long* gsup) {
   __shared__ uint32_t lh[2][kHistBinsR];
+
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
     lh[0][b] = 0;
     lh[1][b] = 0;
@@ -654,6 +662,14 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
       if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
       if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
     }
+  }
+  // the rank-bin counters and super-bin sums k_remit fills, cleared (the
+  // previous round's k_rrank has read them; last: a load's wait also waits
+  // for the wave's earlier stores)
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)(kNBR + kNSup);
+       i += gridDim.x * blockDim.x) {
+    if (i < (uint32_t)kNBR) bcount[i] = 0ull;
+    else gsup[i - kNBR] = 0ull;
   }
 }
 
@@ -968,7 +984,7 @@ struct EmitV {
   // bin-rank path
   BRecR* brec;
   uint32_t* bcount;
-  uint32_t* bsize;
+  unsigned long long* ssup;  // the block's super-bin sums (LDS)
   const uint32_t* sbn;  // the rank-bin table, staged in LDS
   Round* rd;
   // radix path
@@ -987,7 +1003,10 @@ struct EmitV {
         // that differs from the reserved one (cannot happen: the same
         // quantized key) fails the round safely
         if (b != acc->b0) atomicOr(&rd->bin_ovf, 1u);
-        if (ph == 1 && run) atomicAdd(bc + b, (unsigned long long)run << 32);
+        if (ph == 1 && run) {
+          atomicAdd(bc + b, (unsigned long long)run << 32);
+          atomicAdd(&ssup[b / kSupBins], (unsigned long long)run << 32);
+        }
         if (acc->at0 >= kBinCapR) atomicOr(&rd->bin_ovf, 1u);
         acc->key0 = key;
         acc->run0 = run;
@@ -999,6 +1018,7 @@ struct EmitV {
       const unsigned long long inc =
           ((unsigned long long)(ph == 0 ? 1u : 1u + run) << 32) | 1ull;
       const uint32_t at = (uint32_t)atomicAdd(bc + b, inc);
+      atomicAdd(&ssup[b / kSupBins], inc);
       if (at >= kBinCapR) {
         atomicOr(&rd->bin_ovf, 1u);  // read by the last block (memory side)
       } else if (acc->nrec == 0) {
@@ -1114,7 +1134,8 @@ constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a sta
 template <bool BRK>
 __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* ph,
                                 const CandRec& c,
-                                uint32_t ci, BRecR* brec, uint32_t* bcount, uint32_t* bsize,
+                                uint32_t ci, BRecR* brec, uint32_t* bcount,
+                                unsigned long long* ssup,
                                 const uint32_t* sbn, DEnt* dense, uint32_t dcap,
                                 PostRec* post, uint32_t* decof,
                                 ReqEntry* st, uint32_t key32_0, uint64_t* ck = nullptr) {
@@ -1143,6 +1164,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     acc.b0 = rank_bin_q((uint64_t)key32_0 << 32, ph[ph0], ph0, sbn);
     acc.at0 = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long*>(bcount) + acc.b0,
                                   (1ull << 32) | 1ull);
+    atomicAdd(&ssup[acc.b0 / kSupBins], (1ull << 32) | 1ull);
     acc.pre = true;
   }
   if (ck) {
@@ -1151,7 +1173,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     ck[1] = wall_clock64();
   }
   if (c.cr()) {
-    EmitV v{0, s, &ph[0], brec, bcount, bsize, sbn, rd, dense, dcap,
+    EmitV v{0, s, &ph[0], brec, bcount, ssup, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_r(tb, rv, cv, now, TR, 0xffffffffu, v, nullptr, &pf, &fc);
   }
@@ -1159,7 +1181,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     // the priority pulls run only after every R pop
     const uint32_t m = c.m;
     bool ready0 = m == 0 && (c.f() & F_READY);
-    EmitV v{1, s, &ph[1], brec, bcount, bsize, sbn, rd, dense, dcap,
+    EmitV v{1, s, &ph[1], brec, bcount, ssup, sbn, rd, dense, dcap,
             s * tb.q, h, tb.qmask, &acc};
     walk_p(tb, rv, cv, now, TP, 0xffffffffu, v, nullptr, nullptr, nullptr, m,
            pf, m && tb.delayed, ready0, 0, BRK);
@@ -1220,7 +1242,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     decof[ci] = kNoDec;
   } else {
     if (brec && acc.nrec == 1 && acc.at0 < kBinCapR) {
-      EmitV v{0, s, nullptr, brec, bcount, bsize, sbn, rd, dense, dcap, s * tb.q, h,
+      EmitV v{0, s, nullptr, brec, bcount, ssup, sbn, rd, dense, dcap, s * tb.q, h,
               tb.qmask, &acc};
       v.first_slow();
     }
@@ -1231,168 +1253,6 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     ck[2] = wall_clock64();
   }
   return fast ? 0u : acc.nrec > 1 ? 1u : acc.npops > 1 ? 2u : 3u;
-}
-
-// Exclusive prefixes over the rank bins of the record counts, the group
-// sizes and the P-group counts; the round's decision count and terminal
-// flag; diagnostics.  Run by the last k_remit block (1024 threads) over the
-// counters every block filled with memory-side atomics, read and cleared the
-// same way (atomicExch).  A rank bin past kBinCapR aborts the round
-// (overflow = 2): the host re-runs it on the radix path.
-template <int THREADS>
-__device__ void bin_prefix(Round* rd, const PhaseSel* ph, uint32_t* bcount, uint32_t* bsize,
-                           uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff) {
-  constexpr int per = kNBR / THREADS;
-  constexpr int NW = THREADS / 64;
-  __shared__ uint32_t wc[NW], wz[NW], wp[NW], wm[NW];
-  const int t = threadIdx.x, w = t >> 6;
-  // (opaque here: the shuffles' lane addresses are computed in this tail,
-  // not hoisted to the kernel's start and held -- spilled -- across k_remit's
-  // walks)
-  int lane = t & 63;
-  asm volatile("" : "+v"(lane));
-  uint32_t c[per], z[per], lc = 0, lz = 0, lp = 0, lm = 0;
-  // plain loads behind the last block's agent-scope acquire (the counters
-  // were filled with memory-side atomics), cleared with plain stores for
-  // the next round (written back at the kernel's end)
-  unsigned long long* bc64 = reinterpret_cast<unsigned long long*>(bcount);
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    const unsigned long long v = bc64[t * per + j];
-    c[j] = (uint32_t)v;
-    z[j] = (uint32_t)(v >> 32);
-  }
-  // (cleared for the next round last: a block barrier waits for the
-  // thread's outstanding stores)
-  auto clear = [&] {
-#pragma unroll
-    for (int j = 0; j < per; ++j) bc64[t * per + j] = 0ull;
-  };
-  (void)bsize;
-  for (int j = 0; j < per; ++j) {
-    const uint32_t b = t * per + j;
-    lc += c[j];
-    lz += z[j];
-    lp += b >= (uint32_t)kNBPhase ? c[j] : 0;
-    lm = c[j] > lm ? c[j] : lm;  // a thread's bins are all R or all P
-  }
-  bool ovf = rd->bin_ovf != 0;
-  bool bad_sample = false;
-  if (rd->overflow) {  // (failed before emission: a limit-break round's state)
-    clear();
-    return;
-  }
-  if (rd->sampled) {
-    // a sampled threshold must admit at least the needed first keys (then
-    // every entry the k pulls can take has a key at or below it)
-    const uint32_t k = rd->k_total;
-    const uint32_t needR = rd->p_runs ? 0xffffffffu : k;
-    const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
-    const uint64_t TR = ph[0].T, TP = rd->p_runs ? ph[1].T : 0;
-    uint32_t c0 = 0, c1 = 0;
-    for (int i = 0; i < kCntShards; ++i) {
-      c0 += rd->ccnt[2 * i];
-      c1 += rd->ccnt[2 * i + 1];
-    }
-    bad_sample = (TR && TR != kMaxKey - 1 && c0 < needR) ||
-                 (TP && TP != kMaxKey - 1 && c1 < needP);
-  }
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[9] = wall_clock64();
-#endif
-  // one pass of wave scans: record counts, group sizes, P groups (sums) and
-  // the largest bin (max); lane 63 holds the wave totals
-  uint32_t ic = lc, iz = lz, ip = lp, im = lm;
-  for (int d = 1; d < 64; d <<= 1) {
-    // (ds_bpermute from this tail's own lane id: see `lane` above)
-    const int src = (lane >= d ? lane - d : lane) << 2;
-    uint32_t oc = __builtin_amdgcn_ds_bpermute(src, ic),
-             oz = __builtin_amdgcn_ds_bpermute(src, iz),
-             op = __builtin_amdgcn_ds_bpermute(src, ip),
-             om = __builtin_amdgcn_ds_bpermute(src, im);
-    if (lane >= d) {
-      ic += oc;
-      iz += oz;
-      ip += op;
-      im = om > im ? om : im;
-    }
-  }
-  if (lane == 63) {
-    wc[w] = ic;
-    wz[w] = iz;
-    wp[w] = ip;
-    wm[w] = im;
-  }
-  __syncthreads();
-  uint32_t bz = 0, bp = 0, tc = 0, tz = 0, tp = 0;
-  for (int i = 0; i < NW; ++i) {
-    if (i < w) {
-      bz += wz[i];
-      bp += wp[i];
-    }
-    tc += wc[i];
-    tz += wz[i];
-    tp += wp[i];
-  }
-  if (bad_sample) {
-    // the round is re-run with the exact histogram (nothing applied yet)
-    if (t == 0) rd->overflow = 3;
-    clear();
-    return;
-  }
-  if (ovf) {
-    // the round is re-run with fewer pulls or on the radix path: report
-    // how many entries it emitted (the bin counts, overflowed ones included)
-    // so that a radix retry's dense buffer is sized for them, and the
-    // largest bin per phase, from which the host sizes a smaller round
-    if (t == 0) {
-      uint32_t m0 = 0, m1 = 0;
-      for (int i = 0; i < NW; ++i) {
-        if (i < NW / 2) m0 = wm[i] > m0 ? wm[i] : m0;
-        else m1 = wm[i] > m1 ? wm[i] : m1;
-      }
-      rd->bin_max[0] = m0;
-      rd->bin_max[1] = m1;
-      rd->bin_ovf = 0;
-      rd->dense_n = tc;
-      rd->overflow = 2;
-    }
-    clear();
-    return;
-  }
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[10] = wall_clock64();
-#endif
-  uint32_t oz = bz + iz - lz, op = bp + ip - lp;
-  for (int j = 0; j < per; ++j) {
-    const uint32_t b = t * per + j;
-    bcnt[b] = c[j];
-    bsoff[b] = oz;
-    bpoff[b] = op;
-    oz += z[j];
-    if (b >= (uint32_t)kNBPhase) op += c[j];
-  }
-  if (t == 0) {
-    // the largest bin per phase (diagnostics): the first half of the waves
-    // holds the R bins
-    uint32_t m0 = 0, m1 = 0;
-    for (int i = 0; i < NW; ++i) {
-      if (i < NW / 2) m0 = wm[i] > m0 ? wm[i] : m0;
-      else m1 = wm[i] > m1 ? wm[i] : m1;
-    }
-#ifdef DMC_TAIL_TIMING
-    rd->tdbg[11] = wall_clock64();
-#endif
-    rd->bin_max[0] = m0;
-    rd->bin_max[1] = m1;
-    rd->bin_sq = 0;  // (not computed)
-    const uint32_t k = rd->k_total;
-    rd->n_dec = tz < k ? tz : k;
-    rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
-    rd->n_pgroups = tp;
-    rd->n_emit = tc;
-  }
-  clear();
 }
 
 // ---------------------------------------------------------------- k_remit
@@ -1424,11 +1284,10 @@ __global__ void __launch_bounds__(kEmitThreads)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
-        uint32_t* bcount, uint32_t* bsize, const uint32_t* hist, DEnt* dense,
-        uint32_t dcap, uint32_t* bcnt, uint32_t* bsoff, uint32_t* bpoff,
-        uint32_t* done, uint64_t* eclk = nullptr) {
-  // eclk (debug): per block [0] start [1] keys + table staged [2] candidates
-  // compacted [3] walks done [4] ticket taken
+        uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
+        uint32_t dcap, uint64_t* eclk = nullptr) {
+  // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
+  // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
   __shared__ CandRec bl[kEmitChunk];
   __shared__ uint32_t bk[kEmitChunk];  // their first phase's quantized first key
@@ -1437,12 +1296,14 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   __shared__ uint2 s_fb[kEmitThreads];
   __shared__ uint32_t ltab[2 * kHistBinsR];
   __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
-  __shared__ uint32_t s_tot, s_last;
+  __shared__ uint32_t s_tot;
   __shared__ uint32_t s_cnt[2], s_ec[4];
   __shared__ PhaseSel s_ph[2];
+  __shared__ unsigned long long s_sup[kNSup];
   if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
   if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_tot = 0;
+  if (threadIdx.x < kNSup) s_sup[threadIdx.x] = 0;
 #ifdef DMC_TAIL_TIMING
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
@@ -1559,7 +1420,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   for (uint32_t j = lane; j < wtot; j += 64) {
     const uint32_t i = wbase + j;
     const uint32_t cat = emit_one<BRK>(
-        tb, rd, s_ph, bl[i], cbase + i, brec, bcount, bsize, ltab, dense, dcap, post, decof,
+        tb, rd, s_ph, bl[i], cbase + i, brec, bcount, s_sup, ltab, dense, dcap, post, decof,
         lane < kEmitStageLanes ? stage + sli * kEmitStage : nullptr,
         bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
     atomicAdd(&s_ec[cat], 1u);
@@ -1567,6 +1428,9 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   __syncthreads();
   const uint32_t tot = s_tot;
   if (threadIdx.x < 4 && s_ec[threadIdx.x]) atomicAdd(&rd->ecnt[threadIdx.x], s_ec[threadIdx.x]);
+  // the block's super-bin sums (memory-side atomics, read by k_rrank)
+  if (brec && threadIdx.x < kNSup && s_sup[threadIdx.x])
+    atomicAdd(&gsup[threadIdx.x], s_sup[threadIdx.x]);
   // the candidate count (a statistic) and the sampled counts, published
   // after the walks (same-address atomics, serialised over the grid; on
   // gfx950 a wave's load waits also wait for its earlier memory operations)
@@ -1596,32 +1460,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
         tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
-  if (!brec) return;
-  // ticket: the block's bin atomics have completed (every wave waits for its
-  // own) before one lane takes it; the last block computes the prefixes.
-  // Only memory-side atomics cross blocks here (bin counters, overflow flag,
-  // ticket), so no release / acquire fence is needed
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
-  __syncthreads();
-  if (!s_last) return;
-  if (threadIdx.x == 0) {
-    atomicExch(done, 0u);
-    // consumer side of the cross-XCD hand-off (as in k_rhist): one acquire
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[4] = wall_clock64();
-#endif
-  bin_prefix<kEmitThreads>(rd, s_ph, bcount, bsize, bcnt, bsoff, bpoff);
-  if (eclk && threadIdx.x == 0) eclk[5 * gridDim.x] = wall_clock64();
-#ifdef DMC_TAIL_TIMING
-  if (threadIdx.x == 0) rd->tdbg[5] = wall_clock64();
-#endif
 }
 
 // the general emission and the limit-break rounds' emission
@@ -1631,7 +1470,8 @@ constexpr auto k_remit_brk = k_remit_t<true>;
 // ---------------------------------------------------------------- k_rrank
 // One block per rank bin ranks it in LDS by (okey, slot, position); R bins
 // precede P bins, so the decision offset of an entry is the sum of the group
-// sizes (1 for R pops, 1 + run for P groups) of all earlier bins (bin_prefix)
+// sizes (1 for R pops, 1 + run for P groups) of all earlier bins (the
+// super-bin sums before its super-bin and the bins before it in its own)
 // plus those of its own bin that precede it.  Decides: a fast record's
 // decision is written (and its offset recorded for k_rapply); a slow record's
 // entry (slot * q + position) gets its decision offset and tie flag stamped
@@ -1739,20 +1579,87 @@ __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uin
 // records take consecutive decision offsets, so fast records' decision
 // stores from one block fill one stretch of the decision array.
 constexpr int kRankBlocksR = kNBR;
+
+// A sampled round whose thresholds admitted fewer first keys than needed
+// (k_remit's exact counts): it is re-run with the exact histogram (nothing
+// of it is applied); every entry the k pulls take has a key at or below an
+// admitted threshold otherwise
+__device__ inline bool sample_failed(const Round* rd) {
+  if (!rd->sampled) return false;
+  const uint32_t k = rd->k_total;
+  const uint32_t needR = rd->p_runs ? 0xffffffffu : k;
+  const uint32_t needP = rd->p_runs ? k - (uint32_t)rd->n_r : 0u;
+  const uint64_t TR = rd->ph[0].T, TP = rd->p_runs ? rd->ph[1].T : 0;
+  uint32_t c0 = 0, c1 = 0;
+  for (int i = 0; i < kCntShards; ++i) {
+    c0 += rd->ccnt[2 * i];
+    c1 += rd->ccnt[2 * i + 1];
+  }
+  return (TR && TR != kMaxKey - 1 && c0 < needR) || (TP && TP != kMaxKey - 1 && c1 < needP);
+}
+
+// Rank diagnostics: the largest bin per phase, recorded by the bins above
+// this size only (a handful per round; an overflowing bin always)
+constexpr uint32_t kBinMaxReport = 128;
+
 __global__ void __launch_bounds__(kBlockR)
-k_rrank(Round* rd, const uint32_t* bcnt, const uint32_t* bsoff,
-        const uint32_t* bpoff, const BRecR* brec, ReqEntry* ring, uint32_t* decof,
-        uint64_t* wtime = nullptr) {
+k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup,
+        const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime = nullptr) {
   __shared__ BKey sh[kBinCapR];
+  __shared__ uint32_t s_hdr[4];  // the bin's records, its group and P-group offsets, P groups
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
-  const uint32_t cnt = bcnt[b];
-  if (cnt == 0 || rd->overflow) return;
-  const uint32_t k = rd->k_total;
-  const uint32_t n_pgroups = rd->n_pgroups;
-  dmc_decision* out = rd->out;
   const bool isp = b >= (uint32_t)kNBPhase;
-  const uint32_t soff = bsoff[b], poff = bpoff[b];
+  if (threadIdx.x < 64) {
+    // one level of loads: the 64 super-bin sums and the 64 bins of this
+    // bin's super-bin (the rank-bin counters k_remit's walkers filled:
+    // records | group sizes << 32)
+    const uint32_t lane = threadIdx.x, sb = b / kSupBins, ib = b % kSupBins;
+    const unsigned long long sv = gsup[lane];
+    const unsigned long long bv = bcount[sb * kSupBins + lane];
+    const uint32_t sc = (uint32_t)sv, sz = (uint32_t)(sv >> 32);
+    const uint32_t bc = (uint32_t)bv, bz = (uint32_t)(bv >> 32);
+    const bool psup = lane >= (uint32_t)(kNSup / 2);  // (P bins: super-bins 32..63)
+    const uint32_t zoff = wsum32((lane < sb ? sz : 0u) + (lane < ib ? bz : 0u));
+    const uint32_t poff =
+        wsum32((lane < sb && psup ? sc : 0u) + (isp && lane < ib ? bc : 0u));
+    const uint32_t tp = wsum32(psup ? sc : 0u);
+    const uint32_t cnt = __shfl(bc, (int)ib);
+    if (b == 0) {
+      // the round's totals and outcome (the summary k_rapply publishes)
+      const uint32_t tc = wsum32(sc), tz = wsum32(sz);
+      if (lane == 0 && !rd->overflow) {
+        if (sample_failed(rd)) {
+          rd->overflow = 3;  // re-run with the exact histogram
+        } else if (rd->bin_ovf) {
+          // re-run with fewer pulls or on the radix path: the emitted
+          // entries (overflowed bins included) size a radix retry's dense
+          // buffer, bin_max (below) a smaller round
+          rd->dense_n = tc;
+          rd->overflow = 2;
+        } else {
+          const uint32_t k = rd->k_total;
+          rd->n_dec = tz < k ? tz : k;
+          rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
+          rd->n_pgroups = tp;
+          rd->n_emit = tc;
+        }
+      }
+    }
+    if (lane == 0) {
+      s_hdr[0] = cnt;
+      s_hdr[1] = zoff;
+      s_hdr[2] = poff;
+      s_hdr[3] = tp;
+      if (cnt > kBinMaxReport) atomicMax(&rd->bin_max[isp ? 1 : 0], cnt);
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = s_hdr[0];
+  if (cnt == 0 || rd->overflow || rd->bin_ovf || sample_failed(rd)) return;
+  const uint32_t k = rd->k_total;
+  const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
+  dmc_decision* out = rd->out;
   const BRecR* src = brec + (size_t)b * kBinCapR;
   for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
   uint32_t parts = 1;
