@@ -700,43 +700,91 @@ __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
   return wbase + incl - v;
 }
 
+// The same for a pair of counts (the histogram's keys and non-empty bins),
+// with the half's total of the first (wsum: 2 x kPickHalf / 64 words)
+__device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, uint32_t* ev,
+                                       uint32_t* ez, uint32_t* tv) {
+  constexpr int NW = kPickHalf / 64;
+  const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
+  uint32_t iv = v, iz = z;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ov = __shfl_up(iv, d), oz = __shfl_up(iz, d);
+    if (lane >= d) {
+      iv += ov;
+      iz += oz;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = iv;
+    wsum[NW + w] = iz;
+  }
+  __syncthreads();
+  uint32_t bv = 0, bz = 0, tt = 0;
+  for (int i = 0; i < NW; ++i) {
+    if (i < w) {
+      bv += wsum[i];
+      bz += wsum[NW + i];
+    }
+    tt += wsum[i];
+  }
+  __syncthreads();
+  *ev = bv + iv - v;
+  *ez = bz + iz - z;
+  *tv = tt;
+}
+
+// (s_sel: tb, C, nz, found -- T's histogram bin, the keys and the non-empty
+// bins up to it, whether the need-th key was found; s_def: C and nz up to
+// the default tb, the top bin)
 __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                                   const RoundPart& tot, const KeyMap& km, uint32_t sh1,
                                   const uint32_t* hist, uint32_t* sbn, PhaseSel* ps,
-                                  uint32_t* wsum, uint32_t* s_tb, uint32_t* s_C,
+                                  uint32_t* wsum, uint32_t* s_sel, uint32_t* s_def,
                                   uint64_t* s_T) {
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
   const uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
+  // the default: every key (T = all, or none) up to the top bin
+  const uint32_t tb0 = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
   if (t == 0) {
-    *s_tb = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
-    *s_C = 0;
+    s_sel[3] = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
   }
   uint32_t h[kBinsPerThreadR];
-  uint32_t local = 0;
+  uint32_t local = 0, lz = 0;
   {
     uint32_t v[kBinsPerThreadR][kShards];
+    if (kShards == 1 && kBinsPerThreadR == 4) {
+      const uint4 x = reinterpret_cast<const uint4*>(hp)[t];
+      v[0][0] = x.x;
+      v[1][0] = x.y;
+      v[2][0] = x.z;
+      v[3][0] = x.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < kBinsPerThreadR; ++j)
+      for (int j = 0; j < kBinsPerThreadR; ++j)
 #pragma unroll
-      for (int i = 0; i < kShards; ++i)
-        v[j][i] = hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
+        for (int i = 0; i < kShards; ++i)
+          v[j][i] = hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
+    }
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       h[j] = 0;
 #pragma unroll
       for (int i = 0; i < kShards; ++i) h[j] += v[j][i];
       local += h[j];
+      lz += h[j] ? 1u : 0u;
     }
   }
-  const uint32_t before = half_excl_scan(local, wsum);
+  uint32_t before, zbefore, total;
+  half_excl_scan2(local, lz, wsum, &before, &zbefore, &total);
   if (need && ne > need && before < need_h && before + local >= need_h) {
-    uint32_t cum = before;
+    uint32_t cum = before, cz = zbefore;
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
       cum += h[j];
+      cz += h[j] ? 1u : 0u;
       if (cum >= need_h) {
         // the bin's upper edge: the largest key mapped into it, the same
         // candidate set as its largest key present (the open-ended last
@@ -748,37 +796,39 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                                             tot.mx[p]);
         // (rounded up to the end of its 32-bit quantum: see key32)
         *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : (edge | 0xffffffffull);
-        *s_tb = b;
+        s_sel[0] = b;
+        s_sel[1] = cum;
+        s_sel[2] = cz;
+        s_sel[3] = 1;
         break;
       }
     }
   }
-  __syncthreads();
-  const uint32_t tb = *s_tb;
-  {
-    uint32_t cum = before;
+  if ((uint32_t)t == tb0 / kBinsPerThreadR) {
+    uint32_t cum = before, cz = zbefore;
 #pragma unroll
     for (int j = 0; j < kBinsPerThreadR; ++j) {
-      cum += h[j];
-      if ((uint32_t)(t * kBinsPerThreadR + j) == tb) *s_C = cum;
+      if ((uint32_t)(t * kBinsPerThreadR + j) <= tb0) {
+        cum += h[j];
+        cz += h[j] ? 1u : 0u;
+      }
     }
+    s_def[0] = cum;
+    s_def[1] = cz;
   }
   __syncthreads();
-  const uint32_t C = *s_C > 0 ? *s_C : 1;
+  const bool found = s_sel[3] != 0;
+  const uint32_t tb = found ? s_sel[0] : tb0;
+  const uint32_t C0 = found ? s_sel[1] : s_def[0];
+  const uint32_t nz = found ? s_sel[2] : s_def[1];
+  (void)total;
+  const uint32_t C = C0 > 0 ? C0 : 1;
   // Every non-empty histogram bin up to T's gets one rank bin, and the
   // spare ones go in proportion to the counts, h * S / C in single precision
   // (any split is correct; only the balance depends on it), each clipped to
   // S so that the phase cannot pass its kNBPhase rank bins.  An empty bin
   // gets none: its keys (a sample's empty bin may hold a few) share the next
   // bin's first rank bin, which keeps the map monotone.
-  uint32_t lnz = 0;
-#pragma unroll
-  for (int j = 0; j < kBinsPerThreadR; ++j)
-    lnz += ((uint32_t)(t * kBinsPerThreadR + j) <= tb && h[j]) ? 1u : 0u;
-  (void)half_excl_scan(lnz, wsum);
-  uint32_t nz = 0;
-  for (int i = 0; i < kPickHalf / 64; ++i) nz += wsum[i];
-  __syncthreads();  // (wsum is reused below)
   const uint32_t S = kNBPhase > nz ? kNBPhase - nz : 0;
   const float q = (float)S / (float)C;
   uint32_t ns[kBinsPerThreadR], lns = 0;
@@ -848,8 +898,8 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
 // (sbn, ps: LDS; the results are complete after the last barrier inside)
 __device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist,
                           uint32_t* sbn, PhaseSel* ps, int sampled) {
-  __shared__ uint32_t wsum[2][kPickHalf / 64];
-  __shared__ uint32_t s_tb[2], s_C[2];
+  __shared__ uint32_t wsum[2][2 * kPickHalf / 64];
+  __shared__ uint32_t s_sel[2][4], s_def[2][2];
   __shared__ uint64_t s_T[2];
   const bool p_runs = tot.n_r < (uint64_t)k;
   const int p = threadIdx.x / kPickHalf;
@@ -860,7 +910,7 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
   const KeyMap km(tot.mn[p], tot.mx[p]);
   pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hist,
-             sbn, &ps[p], wsum[p], &s_tb[p], &s_C[p], &s_T[p]);
+             sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p]);
   __syncthreads();  // (ps, written by thread 0 of each half)
 }
 
@@ -1610,6 +1660,7 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
   const bool isp = b >= (uint32_t)kNBPhase;
+  const BRecR* src = brec + (size_t)b * kBinCapR;
   if (threadIdx.x < 64) {
     // one level of loads: the 64 super-bin sums and the 64 bins of this
     // bin's super-bin (the rank-bin counters k_remit's walkers filled:
@@ -1660,7 +1711,6 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   const uint32_t k = rd->k_total;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
   dmc_decision* out = rd->out;
-  const BRecR* src = brec + (size_t)b * kBinCapR;
   for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
   uint32_t parts = 1;
   while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
