@@ -474,7 +474,8 @@ __device__ inline AffMin aff_then(AffMin f, AffMin g) {  // g after f
 
 __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
                                       const uint64_t* ax, const double* ap,
-                                      const double* at, double* apd, double* s_M) {
+                                      const double* at, double* apd, double* s_M,
+                                      uint64_t* mout = nullptr) {
   // one wave steps the recurrence: with M fixed, every lane evaluates its
   // activation; the first lane whose contribution undercuts M (a new
   // minimum) ends the step, lanes up to it commit (their M was exact), and
@@ -496,7 +497,7 @@ __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
         rpd0 = apd[j];
       }
       const uint32_t w = e - j0 < 64u ? e - j0 : 64u;
-      double out = rpd0;
+      double out = rpd0, mo = 0.0;
       for (uint32_t done = 0; done < w;) {
         const bool act = in && t >= done;
         double L = M < rx ? M : rx;
@@ -505,11 +506,15 @@ __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
         const double c = __dadd_rn(rp, pd);
         const uint64_t rec = __ballot(act && c < M);
         const uint32_t r = rec ? (uint32_t)(__ffsll((unsigned long long)rec) - 1) : 64u;
-        if (act && t <= r) out = pd;
+        if (act && t <= r) {
+          out = pd;
+          mo = t == r ? c : M;
+        }
         if (rec) M = __shfl(c, (int)r);
         done = r == 64u ? 64u : r + 1;
       }
       if (in) apd[j] = out;  // committed by k_act_commit
+      if (in && mout) mout[j] = mo == kInf ? kMaxKey : okey(mo);
     }
     if (t == 0) *s_M = M;
   }
@@ -518,9 +523,13 @@ __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
 
 constexpr int kChainK = 4;  // activations per thread and window (4096 per window)
 
+// (mout: M after each activation, as an ordered key; wave_below: a window
+// that advances less than this many activations hands the next kActThreads
+// to the wave-stepped recurrence)
 __device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t* ax,
                           const double* ap, const double* at, double* apd, double* s_M,
-                          uint64_t* dbg) {
+                          uint64_t* dbg, uint64_t* mout = nullptr, uint32_t wave_below = 64,
+                          uint32_t wave_len = kActThreads) {
   constexpr double dmax = 1.7976931348623157e308;
   constexpr double trigger = dmax / 3.0;
   __shared__ double s_ref, s_last[kActThreads];
@@ -609,16 +618,19 @@ __device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t
 #pragma unroll
     for (int u = 0; u < kChainK; ++u) {
       const uint32_t i = kChainK * t + u;
-      if (i < W && i <= fl) apd[j0 + i] = pd[u];  // committed by k_act_commit
+      if (i < W && i <= fl) {
+        apd[j0 + i] = pd[u];  // committed by k_act_commit
+        if (mout) mout[j0 + i] = Mn[u] == kInf ? kMaxKey : okey(Mn[u]);
+      }
       if (i == (fl < W ? fl : W - 1)) *s_M = Mn[u];
     }
     __syncthreads();
     const uint32_t adv = fl < W ? fl + 1 : W;
     j0 += adv;
-    if (adv < 64 && j0 < m) {
+    if (adv < wave_below && j0 < m) {
       // the grid does not describe this stretch: step it exactly
-      const uint32_t e = m - j0 < (uint32_t)kActThreads ? m - j0 : kActThreads;
-      act_wave_steps(j0, e, base, ax, ap, at, apd, s_M);
+      const uint32_t e = m - j0 < wave_len ? m - j0 : wave_len;
+      act_wave_steps(j0, e, base, ax, ap, at, apd, s_M, mout);
       if (dbg && t == 0) ++dbg[6];
       j0 += e;
     }
@@ -703,6 +715,350 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
     dbg[7] = m;
   }
   if (t == 0) *act.extra = kMaxKey;  // ready for the next batch
+}
+
+// ------------------------------------------------ segmented resolution
+// The recurrence above, M_{j+1} = min(M_j, c_j(M_j)) with c_j(M) the
+// contribution p_j + pd_j for L_j = min(X_j, M), resolved in tiles of
+// kActTile activations:
+//  * a "simple" activation -- X_j finite and p_j - t_j well above the
+//    rounding of the operands -- has c_j(M) >= M for every M < X_j and
+//    c_j(M) = K_j := c_j(X_j) for M >= X_j: its step is M -> min(M, K_j),
+//    independent of M (config 4: about 98 % of them);
+//  * so between two "complex" ones (an idle client whose proportion tag lies
+//    behind the clock, p_j <= t_j, or X_j infinite) M only takes the minimum
+//    of the run's K values, a segmented min-scan (k_act_keys, per tile);
+//  * the complex ones are stepped in order by one wave (k_act_seq), with
+//    the runs' minima between them: a lane per complex activation evaluates
+//    its step with M fixed, and the first lane that changes M ends the
+//    step, so the cost is the number of changes plus one step per 64;
+//  * k_act_apply gives every activation its exact M_j (its segment's entry
+//    and the run's minimum before it), evaluates it with the reference's
+//    arithmetic, checks the simple ones' step (exact M_j and a holding step
+//    prove M_{j+1}; the first failing activation, if any, is re-resolved
+//    from its exact M by k_act_fixup's speculated min-plus chain) and
+//    commits the idle reset.
+constexpr uint32_t kActTile = kActThreads;
+constexpr uint32_t kActItems = kActTile + 1;  // per tile: its complex steps and the tail
+
+// The sequential steps, per tile (at t * kActItems): the tile's complex
+// activations in order, each with the minimum of the simple run before it
+// (S), then the tail pseudo-step (S = the run after the last one, X = none,
+// no contribution: M -> min(M, S)).
+struct ActTiles {
+  uint64_t* K;      // n: c_j(X_j) (ordered key)
+  uint32_t* nst;    // tiles: steps per tile (complex ones + 1)
+  uint64_t* sS;     // tiles * kActItems: each step's run minimum
+  uint64_t* sX;     // ... its X (kMaxKey: the tail)
+  double *sP, *sT, *sPd0;  // ... its p, t, old prop_delta
+  uint64_t* Mtile;  // tiles + 1: M entering each tile (k_act_seq)
+  uint64_t* Mout;   // tiles * kActItems: M after each step (k_act_seq)
+  uint64_t* Mj;     // n: M entering each activation (k_act_apply)
+  uint64_t* cX;     // n: the complex steps, concatenated (k_act_seq's scratch)
+  double *cP, *cT, *cPd;
+  uint64_t* cMo;    // n: M after each of them
+  uint64_t* xbase;  // 1: the unchanged clients' minimum (k_act_keys, block 0)
+  uint32_t* fail;   // 1: the first activation whose simple step failed (~0: none)
+};
+
+// p + pd for L (ordered keys in, ordered key out): the reference's arithmetic
+__device__ inline uint64_t act_contrib(uint64_t L, double p, double t, double pd0,
+                                       double* pd_out) {
+  const double pd = act_pd(L, t, pd0);
+  if (pd_out) *pd_out = pd;
+  return okey(__dadd_rn(p, pd));
+}
+
+__device__ inline bool act_simple(uint64_t X, double p, double t) {
+  constexpr double trigger = 1.7976931348623157e308 / 3.0;
+  if (X == kMaxKey) return false;
+  const double x = from_okey(X);
+  if (!(x < trigger)) return false;
+  const double d = __dsub_rn(p, t);
+  return d > 0x1p-40 * (fabs(x) + fabs(t) + fabs(p) + 1.0);
+}
+
+// segmented inclusive min-scan over a block (1024 threads): a reset element
+// (a complex activation) starts a new run with its own value
+struct SegMin {
+  uint32_t r;
+  uint64_t m;
+};
+__device__ inline SegMin seg_op(SegMin a, SegMin b) {  // a then b
+  return b.r ? b : SegMin{a.r, a.m < b.m ? a.m : b.m};
+}
+__device__ inline SegMin block_seg_min(SegMin v, SegMin* wpart) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    SegMin o{(uint32_t)__shfl_up((int)v.r, d), shfl_up_u64(v.m, d)};
+    if (lane >= d) v = seg_op(o, v);
+  }
+  if (lane == 63) wpart[w] = v;
+  __syncthreads();
+  SegMin b{0, kMaxKey};
+  for (int i = 0; i < w; ++i) b = seg_op(b, wpart[i]);
+  __syncthreads();
+  return seg_op(b, v);
+}
+
+// the tile's activations: X, K, classification, the complex ones compacted
+// with the runs' minima before them
+__global__ void __launch_bounds__(kActThreads)
+k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
+           const double* apd, ActTiles tl) {
+  __shared__ uint64_t wmin[kActThreads / 64];
+  __shared__ SegMin wseg[kActThreads / 64];
+  __shared__ uint32_t wcnt[kActThreads / 64];
+  __shared__ uint64_t s_incl[kActThreads];
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  const uint32_t t = blockIdx.x, j0 = t * kActTile;
+  if (j0 >= m) return;
+  // the unchanged clients' minimum (every block; block 0 publishes it)
+  uint64_t b = kMaxKey;
+  for (uint32_t i = threadIdx.x; i < act.nparts; i += kActThreads)
+    b = act.parts[i] < b ? act.parts[i] : b;
+  b = block_incl_min(b, wmin);
+  __shared__ uint64_t s_base;
+  if (threadIdx.x == kActThreads - 1) {
+    const uint64_t e = *act.extra;
+    s_base = e < b ? e : b;
+    if (t == 0) *tl.xbase = s_base;
+  }
+  __syncthreads();
+  const uint64_t base = s_base;
+  const uint32_t j = j0 + threadIdx.x;
+  const bool in = j < m;
+  uint64_t K = kMaxKey;
+  bool cx = false;
+  if (in) {
+    const uint64_t X = ax[j] < base ? ax[j] : base;
+    const double p = ap[j], tt = at[j];
+    K = act_contrib(X, p, tt, apd[j], nullptr);
+    cx = !act_simple(X, p, tt);
+    tl.K[j] = K;
+  }
+  const SegMin incl = block_seg_min(SegMin{cx ? 1u : 0u, cx ? kMaxKey : K}, wseg);
+  s_incl[threadIdx.x] = incl.m;
+  // the complex ones' ranks in the tile
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(in && cx);
+  if (lane == 0) wcnt[w] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+  for (int i = 0; i < kActThreads / 64; ++i) {
+    rank += i < w ? wcnt[i] : 0u;
+    tot += wcnt[i];
+  }
+  const uint32_t o = t * kActItems;
+  if (in && cx) {
+    tl.sS[o + rank] = threadIdx.x ? s_incl[threadIdx.x - 1] : kMaxKey;
+    tl.sX[o + rank] = ax[j] < base ? ax[j] : base;
+    tl.sP[o + rank] = ap[j];
+    tl.sT[o + rank] = at[j];
+    tl.sPd0[o + rank] = apd[j];
+  }
+  const uint32_t last = (m - j0 < kActTile ? m - j0 : kActTile) - 1;
+  if (threadIdx.x == last) {
+    // the tail pseudo-step (a complex last one: its own run, empty)
+    tl.nst[t] = tot + 1;
+    tl.sS[o + tot] = incl.m;
+    tl.sX[o + tot] = kMaxKey;
+    tl.sP[o + tot] = 0.0;
+    tl.sT[o + tot] = 0.0;
+    tl.sPd0[o + tot] = 0.0;
+  }
+}
+
+// The complex steps in order (one block): concatenated over the tiles, then
+// resolved by act_chain's speculated min-plus scan (windows of up to 4096
+// steps checked with the reference's arithmetic; a window advancing fewer
+// than 8 steps hands the next 64 to the wave-stepped recurrence), starting
+// from the minimum of every simple run before the first one.  The runs'
+// minima between later complex steps are not applied here (they lie above M
+// in practice): k_act_apply checks each step from its exact entry, and a
+// run minimum below M fails that check (the batch is re-resolved from
+// there).  Each tile's entry M is then stepped over the tiles exactly.
+constexpr uint32_t kActMaxTiles = 1024;  // (batches of up to 2^20 activations)
+__global__ void __launch_bounds__(kActThreads)
+k_act_seq(ActBuf act, ActTiles tl) {
+  __shared__ uint32_t s_off[kActMaxTiles + 1];  // complex steps before each tile
+  __shared__ uint32_t wsum[kActThreads / 64];
+  __shared__ uint64_t s_tail[kActMaxTiles];     // each tile's tail run minimum
+  __shared__ uint64_t wmin[kActThreads / 64];
+  __shared__ double s_M;
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  const uint32_t T = (m + kActTile - 1) / kActTile;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  {
+    const uint32_t v = tid < T ? tl.nst[tid] - 1u : 0u;
+    uint32_t incl = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d);
+      if ((int)lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t b = 0, tot = 0;
+    for (int i = 0; i < kActThreads / 64; ++i) {
+      b += i < (int)w ? wsum[i] : 0u;
+      tot += wsum[i];
+    }
+    if (tid < T) {
+      s_off[tid] = b + incl - v;
+      s_tail[tid] = tl.sS[tid * kActItems + v];
+    }
+    if (tid == 0) s_off[T] = tot;
+  }
+  __syncthreads();
+  const uint32_t nc = s_off[T];
+  {
+    // M entering the first complex step: every simple run before it (the
+    // tails of the tiles before its tile, and its own run)
+    uint64_t mn = kMaxKey;
+    if (tid < T && s_off[tid + 1] == 0) mn = s_tail[tid];  // (no complex step up to it)
+    if (nc && tid < T && s_off[tid] == 0 && s_off[tid + 1] > 0) {
+      const uint64_t s0 = tl.sS[tid * kActItems];
+      mn = s0 < mn ? s0 : mn;
+    }
+    mn = block_incl_min(mn, wmin);
+    if (tid == kActThreads - 1) s_M = mn == kMaxKey ? kInf : from_okey(mn);
+  }
+  __syncthreads();
+  auto tile_of = [&](uint32_t g) -> uint32_t {  // s_off[t] <= g < s_off[t + 1]
+    uint32_t lo = 0, hi = T;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_off[mid] <= g) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  };
+  for (uint32_t g = tid; g < nc; g += kActThreads) {
+    const uint32_t t = tile_of(g), at = t * kActItems + (g - s_off[t]);
+    tl.cX[g] = tl.sX[at];
+    tl.cP[g] = tl.sP[at];
+    tl.cT[g] = tl.sT[at];
+    tl.cPd[g] = tl.sPd0[at];
+  }
+  __threadfence();
+  __syncthreads();
+  if (nc) act_chain(0, nc, kMaxKey, tl.cX, tl.cP, tl.cT, tl.cPd, &s_M, nullptr, tl.cMo, 8, 64);
+  __threadfence();
+  __syncthreads();
+  for (uint32_t g = tid; g < nc; g += kActThreads) {
+    const uint32_t t = tile_of(g);
+    tl.Mout[t * kActItems + (g - s_off[t])] = tl.cMo[g];
+  }
+  // M entering each tile, stepped over the tiles: after a tile's last
+  // complex step (if any), then its tail run
+  __shared__ uint64_t s_last[kActMaxTiles];
+  for (uint32_t t = tid; t < T; t += kActThreads)
+    s_last[t] = s_off[t + 1] > s_off[t] ? tl.cMo[s_off[t + 1] - 1] : kMaxKey;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t M = kMaxKey;
+    for (uint32_t t = 0; t < T; ++t) {
+      tl.Mtile[t] = M;
+      if (s_off[t + 1] > s_off[t]) M = s_last[t];
+      M = s_tail[t] < M ? s_tail[t] : M;
+    }
+    tl.Mtile[T] = M;
+  }
+}
+
+// Every activation's exact M_j, its idle reset evaluated and committed; the
+// simple ones' steps checked (the first failure: k_act_fixup)
+__global__ void __launch_bounds__(kActThreads)
+k_act_apply(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const double* at,
+            const double* apd, const uint32_t* aslot, ActTiles tl) {
+  __shared__ SegMin wseg[kActThreads / 64];
+  __shared__ uint32_t wcnt[kActThreads / 64];
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  const uint32_t t = blockIdx.x, j0 = t * kActTile;
+  if (j0 >= m) return;
+  const uint64_t base = *tl.xbase;
+  const uint32_t j = j0 + threadIdx.x;
+  const bool in = j < m;
+  uint64_t X = kMaxKey, K = kMaxKey;
+  double p = 0.0, tt = 0.0, pd0 = 0.0;
+  uint32_t slot = 0;
+  bool cx = false;
+  ScanRec sr{};
+  double fp = 0.0;
+  if (in) {
+    X = ax[j] < base ? ax[j] : base;
+    p = ap[j];
+    tt = at[j];
+    pd0 = apd[j];
+    K = tl.K[j];
+    slot = aslot[j];
+    cx = !act_simple(X, p, tt);
+    // the idle reset's own loads (activate_slot's), issued ahead of the scan
+    sr = tb.sc[slot];
+    if (sr.count) fp = tb.ring[(size_t)slot * tb.q + (sr.head & tb.qmask)].p;
+  }
+  // exclusive run minimum before j (a complex j: its run's, cxS)
+  const SegMin incl = block_seg_min(SegMin{cx ? 1u : 0u, cx ? kMaxKey : K}, wseg);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  SegMin ex{(uint32_t)__shfl_up((int)incl.r, 1), shfl_up_u64(incl.m, 1)};
+  __shared__ SegMin s_wlast[kActThreads / 64];
+  if (lane == 63) s_wlast[w] = incl;
+  // complex ones strictly before j in the tile: the segment's entry is the
+  // last one's M after it, else the tile's entry
+  const uint64_t bal = __ballot(in && cx);
+  if (lane == 0) wcnt[w] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  if (lane == 0) ex = w ? s_wlast[w - 1] : SegMin{0, kMaxKey};
+  uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+  for (int i = 0; i < w; ++i) before += wcnt[i];
+  if (!in) return;
+  // (a run's minimum restarts after each complex one: ex.m is the current
+  // run's minimum before j, at a complex j the run before it)
+  const uint64_t run = threadIdx.x ? ex.m : kMaxKey;
+  const uint64_t entry = before ? tl.Mout[t * kActItems + before - 1] : tl.Mtile[t];
+  uint64_t Mj = run < entry ? run : entry;
+  double pd;
+  const uint64_t L = X < Mj ? X : Mj;
+  const uint64_t c = act_contrib(L, p, tt, pd0, &pd);
+  if (!cx) {
+    // a simple step: min(M, c(M)) must be min(M, K)
+    const uint64_t a = c < Mj ? c : Mj, b2 = K < Mj ? K : Mj;
+    if (a != b2) atomicMin(tl.fail, j);
+  } else {
+    // a complex step: k_act_seq's M after it, from this exact entry
+    const uint64_t a = c < Mj ? c : Mj;
+    if (a != tl.Mout[t * kActItems + before]) atomicMin(tl.fail, j);
+  }
+  tl.Mj[j] = Mj;
+  // activate_slot with its loads made above
+  tb.rec[slot].pd = pd;
+  if (sr.count) tb.sc[slot].pk = __dadd_rn(fp, pd);
+  tb.sc[slot].flags = (uint8_t)(sr.flags & ~F_IDLE);
+}
+
+// The first activation whose simple step failed (if any): from its exact M
+// the rest of the batch is resolved by act_chain and committed again (the
+// idle reset is idempotent: k_act_apply's commits of these are overwritten)
+__global__ void __launch_bounds__(kActThreads)
+k_act_fixup(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const double* at,
+            double* apd, const uint32_t* aslot, ActTiles tl) {
+  const uint32_t f = *tl.fail;
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  if (f != 0xffffffffu && f < m) {
+    __shared__ double s_M;
+    if (threadIdx.x == 0) {
+      const uint64_t M = tl.Mj[f];
+      s_M = M == kMaxKey ? kInf : from_okey(M);
+    }
+    __syncthreads();
+    act_chain(f, m, *tl.xbase, ax, ap, at, apd, &s_M, nullptr);
+    for (uint32_t j = f + threadIdx.x; j < m; j += kActThreads) activate_slot(tb, aslot[j], apd[j]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *tl.fail = 0xffffffffu;
+    *act.extra = kMaxKey;  // ready for the next batch
+  }
 }
 
 // Step 4 (grid): every activation's idle reset takes effect -- prop_delta,
@@ -1246,6 +1602,9 @@ struct dmc_queue {
            *act_suf = nullptr, *act_extra = nullptr, *act_parts = nullptr;
   double* act_p = nullptr;
   uint32_t* act_idx = nullptr;
+  ActTiles atl{};              // the segmented resolution's buffers (ensure_act)
+  uint64_t* act_xbase = nullptr;
+  uint32_t* act_fail = nullptr;
   uint64_t* act_x = nullptr;   // per activation: X_k without the unchanged term
   double *act_ip = nullptr, *act_it = nullptr, *act_ipd = nullptr;
   uint32_t* act_islot = nullptr;
@@ -1713,6 +2072,13 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
   dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot); dfree(q->act_flag);
   dfree(q->act_sparts);
+  {
+    ActTiles& a = q->atl;
+    dfree(a.K); dfree(a.nst); dfree(a.sS); dfree(a.sX); dfree(a.sP); dfree(a.sT);
+    dfree(a.sPd0); dfree(a.Mtile); dfree(a.Mout); dfree(a.Mj);
+    dfree(a.cX); dfree(a.cP); dfree(a.cT); dfree(a.cPd); dfree(a.cMo);
+    a = ActTiles{};
+  }
   if (q->h_act) (void)hipHostFree(q->h_act);
   q->h_act = nullptr;
   DALLOC(q, &q->act_cold, 8ull * cap);
@@ -1733,6 +2099,33 @@ int ensure_act(dmc_queue* q, uint32_t n) {
     HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
   }
   DALLOC(q, &q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap));
+  {
+    ActTiles& a = q->atl;
+    const uint32_t T = (cap + kActTile - 1) / kActTile;
+    DALLOC(q, &a.K, 8ull * cap);
+    DALLOC(q, &a.nst, 4ull * T);
+    DALLOC(q, &a.sS, 8ull * T * kActItems);
+    DALLOC(q, &a.sX, 8ull * T * kActItems);
+    DALLOC(q, &a.sP, 8ull * T * kActItems);
+    DALLOC(q, &a.sT, 8ull * T * kActItems);
+    DALLOC(q, &a.sPd0, 8ull * T * kActItems);
+    DALLOC(q, &a.Mtile, 8ull * (T + 1));
+    DALLOC(q, &a.Mout, 8ull * T * kActItems);
+    DALLOC(q, &a.Mj, 8ull * cap);
+    DALLOC(q, &a.cX, 8ull * cap);
+    DALLOC(q, &a.cP, 8ull * cap);
+    DALLOC(q, &a.cT, 8ull * cap);
+    DALLOC(q, &a.cPd, 8ull * cap);
+    DALLOC(q, &a.cMo, 8ull * cap);
+    if (!q->act_xbase) {
+      DALLOC(q, &q->act_xbase, 8);
+      DALLOC(q, &q->act_fail, 4);
+      HIP_OK(hipMemsetAsync(q->act_fail, 0xff, 4, q->stream));
+      HIP_OK(hipStreamSynchronize(q->stream));
+    }
+    a.xbase = q->act_xbase;
+    a.fail = q->act_fail;
+  }
   if (!q->act_extra) {
     DALLOC(q, &q->act_extra, 8);
     const uint64_t mx = kMaxKey;
@@ -1742,6 +2135,31 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   if (!q->act_parts) DALLOC(q, &q->act_parts, 8ull * 2048);
   q->acap = cap;
   return DMC_OK;
+}
+
+// The idle resets of a batch's activations (m of them, at most n: the
+// device count act.dm, or act.m), resolved and committed (see k_act_keys)
+void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
+  if (!n) return;
+  const uint32_t T = (n + kActTile - 1) / kActTile;
+  const uint64_t* ax = q->act_x;
+  const double *ap = q->act_ip, *at = q->act_it;
+  if (T > kActMaxTiles) {
+    // (more than 2^20 activations in one batch: the one-block resolution)
+    hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
+                       act, ax, ap, at, q->act_ipd, (const uint32_t*)q->act_islot);
+    hipLaunchKernelGGL(k_act_commit, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
+                       q->tb, (const uint32_t*)act.dm, n, (const double*)q->act_ipd,
+                       (const uint32_t*)q->act_islot);
+    return;
+  }
+  hipLaunchKernelGGL(k_act_keys, dim3(T), dim3(kActThreads), 0, q->stream, act, ax, ap, at,
+                     (const double*)q->act_ipd, q->atl);
+  hipLaunchKernelGGL(k_act_seq, dim3(1), dim3(kActThreads), 0, q->stream, act, q->atl);
+  hipLaunchKernelGGL(k_act_apply, dim3(T), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
+                     ap, at, (const double*)q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
+  hipLaunchKernelGGL(k_act_fixup, dim3(1), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
+                     ap, at, q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
 }
 
 // the activation bookkeeping's scans (and, flagged, the compaction) of an
@@ -1801,13 +2219,7 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(m, 1024)), dim3(kBlock), 0, q->stream,
                      (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
                      q->act_it, q->act_ipd, q->act_islot);
-  hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
-                     act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
-                     (const double*)q->act_it, q->act_ipd,
-                     (const uint32_t*)q->act_islot);
-  hipLaunchKernelGGL(k_act_commit, dim3(grid_for(act.m, 1024)), dim3(kBlock), 0, q->stream,
-                     q->tb, (const uint32_t*)nullptr, act.m, (const double*)q->act_ipd,
-                     (const uint32_t*)q->act_islot);
+  act_resolve(q, act, act.m);
   pe(q);
   HIP_OK(hipGetLastError());
   // the pinned staging is reused by the next batch: wait for the copy
@@ -1874,26 +2286,9 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
     }
     ++q->act_dumps;
   }
-  hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
-                     act, (const uint64_t*)q->act_x, (const double*)q->act_ip,
-                     (const double*)q->act_it, q->act_ipd,
-                     (const uint32_t*)q->act_islot, q->debug ? q->dbg_atime : nullptr);
-  hipLaunchKernelGGL(k_act_commit, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
-                     q->tb, (const uint32_t*)q->act_dm, n, (const double*)q->act_ipd,
-                     (const uint32_t*)q->act_islot);
+  act_resolve(q, act, n);
   pe(q);
   HIP_OK(hipGetLastError());
-  if (q->debug) {
-    std::vector<uint64_t> d(8);
-    HIP_OK(hipMemcpyAsync(d.data(), q->dbg_atime, 64, hipMemcpyDeviceToHost, q->stream));
-    HIP_OK(hipMemsetAsync(q->dbg_atime, 0, 64, q->stream));
-    HIP_OK(hipStreamSynchronize(q->stream));
-    std::fprintf(stderr, "dmc act_resolve: m=%llu base %.2f us first pass %.2f us chain %.2f us "
-                 "(first undercut %llu, windows %llu, wave fallbacks %llu)\n",
-                 (unsigned long long)d[7], (d[1] - d[0]) / 100.0, (d[2] - d[1]) / 100.0,
-                 (d[3] - d[2]) / 100.0, (unsigned long long)d[4], (unsigned long long)d[5],
-                 (unsigned long long)d[6]);
-  }
   // the host idle mirror learns the activated slots (not needed while it is
   // stale anyway: device-side idle marking, sync_idle rebuilds it)
   if (!q->idle_unknown) {
@@ -1955,6 +2350,14 @@ bool maybe_idle(const dmc_queue* q) { return q->n_idle || q->idle_unknown; }
 
 int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
                   const dmc_request* d_reqs, int32_t* d_rc) {
+  // (AtLimit::Reject: the host split.  A rejected request still updates the
+  // client's prev tag (update_req_tag precedes the reject check, :899-906,
+  // :988-992), so an empty client's contribution to later idle resets can
+  // change at every request of the batch, not only at its first accepted
+  // one as k_add_chain's bookkeeping assumes.  And a rejected activating
+  // request returns before the heap adjustments (:992 vs :995-1015): the
+  // reference keeps that client at its pre-reset heap position, which no
+  // heap-free engine reproduces -- DESIGN section 8)
   if (q->act_split || q->p.at_limit == DMC_AT_LIMIT_REJECT)
     return add_host_split(q, h_reqs, n, d_reqs, d_rc);
   return add_act_batch(q, h_reqs, n, d_reqs, d_rc);
@@ -2722,6 +3125,11 @@ int dmc_queue_destroy(dmc_queue* q) {
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_extra); dfree(q->act_parts);
   dfree(q->act_x); dfree(q->act_ip); dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot);
   dfree(q->act_flag); dfree(q->act_dm);
+  dfree(q->atl.K); dfree(q->atl.nst); dfree(q->atl.sS); dfree(q->atl.sX); dfree(q->atl.sP);
+  dfree(q->atl.sT); dfree(q->atl.sPd0); dfree(q->atl.Mtile); dfree(q->atl.Mout);
+  dfree(q->atl.Mj); dfree(q->atl.cX); dfree(q->atl.cP); dfree(q->atl.cT); dfree(q->atl.cPd);
+  dfree(q->atl.cMo);
+  dfree(q->act_xbase); dfree(q->act_fail);
   if (q->h_actm) (void)hipHostFree(q->h_actm);
   dfree(q->d_mark);
   if (q->h_mark) (void)hipHostFree(q->h_mark);

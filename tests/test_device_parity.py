@@ -366,3 +366,4 @@ def test_config4_1m_device_activations_vs_host_split():
     qa.close()
     qb.close()
     torch.cuda.synchronize()
+
