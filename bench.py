@@ -152,7 +152,7 @@ def parse():
                          "HIP events between kernels; run after the timed "
                          "region, on the following batches)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles",
-                                                      "traffic_r02.json"))
+                                                      "traffic_r03.json"))
     ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5),
                     help="3: one server queue (default); 4: config 3 with "
                          "idle/active churn (do_clean idle marking before "

@@ -86,7 +86,7 @@ def per_kernel(path, steps):
         name = r["Kernel_Name"]
         for ks in STAGES.values():
             for k in ks:
-                if k + "(" in name or name.endswith(k):
+                if k + "(" in name or k + "_t<" in name or name.endswith(k):
                     vals[k].append(float(r["Counter_Value"]) * 1024.0)
     return {k: v[-steps:] for k, v in vals.items()}
 
@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--fetch", default="gpurun_out/pmc_FETCH_SIZE/run_counter_collection.csv")
     ap.add_argument("--write", default="gpurun_out/pmc_WRITE_SIZE/run_counter_collection.csv")
     ap.add_argument("--steps", type=int, default=6)
-    ap.add_argument("--out", default="profiles/traffic_r02.json")
+    ap.add_argument("--out", default="profiles/traffic_r03.json")
     ap.add_argument("--calib", default=None,
                     help="tools/fetch_calib FETCH_SIZE csv (with --known): print factors")
     ap.add_argument("--known", default=None)
