@@ -526,7 +526,9 @@ constexpr int kChainK = 4;  // activations per thread and window (4096 per windo
 // (mout: M after each activation, as an ordered key; wave_below: a window
 // that advances less than this many activations hands the next kActThreads
 // to the wave-stepped recurrence)
-__device__ void act_chain(uint32_t j0, uint32_t m, uint64_t base, const uint64_t* ax,
+// (always inlined: three kernels call it, and a call frame is scratch)
+__device__ __attribute__((always_inline)) inline void act_chain(
+    uint32_t j0, uint32_t m, uint64_t base, const uint64_t* ax,
                           const double* ap, const double* at, double* apd, double* s_M,
                           uint64_t* dbg, uint64_t* mout = nullptr, uint32_t wave_below = 64,
                           uint32_t wave_len = kActThreads) {
