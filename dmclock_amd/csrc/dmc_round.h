@@ -1661,6 +1661,14 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   const uint32_t b = blockIdx.x;
   const bool isp = b >= (uint32_t)kNBPhase;
   const BRecR* src = brec + (size_t)b * kBinCapR;
+  // the round's inputs, read once before any store (block 0 writes the
+  // outcome into the same record)
+  const uint32_t ovf0 = rd->overflow, bovf = rd->bin_ovf;
+  const bool sfail = sample_failed(rd);
+  const uint32_t k = rd->k_total;
+  const uint32_t p_runs = rd->p_runs;
+  dmc_decision* const out = rd->out;
+  const bool fail = ovf0 || bovf || sfail;
   if (threadIdx.x < 64) {
     // one level of loads: the 64 super-bin sums and the 64 bins of this
     // bin's super-bin (the rank-bin counters k_remit's walkers filled:
@@ -1679,19 +1687,18 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
     if (b == 0) {
       // the round's totals and outcome (the summary k_rapply publishes)
       const uint32_t tc = wsum32(sc), tz = wsum32(sz);
-      if (lane == 0 && !rd->overflow) {
-        if (sample_failed(rd)) {
+      if (lane == 0 && !ovf0) {
+        if (sfail) {
           rd->overflow = 3;  // re-run with the exact histogram
-        } else if (rd->bin_ovf) {
+        } else if (bovf) {
           // re-run with fewer pulls or on the radix path: the emitted
           // entries (overflowed bins included) size a radix retry's dense
           // buffer, bin_max (below) a smaller round
           rd->dense_n = tc;
           rd->overflow = 2;
         } else {
-          const uint32_t k = rd->k_total;
           rd->n_dec = tz < k ? tz : k;
-          rd->terminal = (rd->p_runs && tz < k) ? 1 : 0;
+          rd->terminal = (p_runs && tz < k) ? 1 : 0;
           rd->n_pgroups = tp;
           rd->n_emit = tc;
         }
@@ -1707,10 +1714,8 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   }
   __syncthreads();
   const uint32_t cnt = s_hdr[0];
-  if (cnt == 0 || rd->overflow || rd->bin_ovf || sample_failed(rd)) return;
-  const uint32_t k = rd->k_total;
+  if (cnt == 0 || fail) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
-  dmc_decision* out = rd->out;
   for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
   uint32_t parts = 1;
   while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
