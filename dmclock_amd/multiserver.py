@@ -107,8 +107,9 @@ class DeviceTrackers:
         for q in self.queues:
             q.sync()
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and \
-                dist.get_world_size(group) > 1:
+        # (any initialized group: at world size 1 the all-reduce is the
+        # identity, and RCCL still runs it on the device buffers)
+        if dist.is_available() and dist.is_initialized():
             both = torch.stack([self.sum_d, self.sum_r])
             if dist.get_backend(group) == "gloo":
                 host = both.cpu()

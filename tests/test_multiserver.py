@@ -206,19 +206,20 @@ def _w2_workload():
     return cmap, tab, eps
 
 
-def _device_trackers_worker(rank, world, port, out_q):
+def _device_trackers_worker(rank, world, port, out_q, backend="gloo"):
     """One rank: servers [rank * S, (rank + 1) * S) as GPU queues on cuda:0
-    with DeviceTrackers, the per-epoch delivery all-reducing over gloo (the
-    product's DeviceTrackers.deliver, host-staged)."""
+    with DeviceTrackers, the per-epoch delivery all-reducing over `backend`
+    (the product's DeviceTrackers.deliver: host-staged under gloo, on the
+    device buffers under nccl = RCCL)."""
     import torch
     import torch.distributed as dist
     from dmclock_amd._abi import PullResult
     from dmclock_amd.multiserver import DeviceTrackers, make_queues
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
-        torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         cmap, tab, eps = _w2_workload()
         S = W2["S_total"] // world
@@ -259,6 +260,67 @@ def _device_trackers_worker(rank, world, port, out_q):
             q.close()
     finally:
         dist.destroy_process_group()
+
+
+def _oracle_reference(world):
+    """all four servers on the oracle with the epoch restatement"""
+    cmap, tab, eps = _w2_workload()
+    S_total, N, G, k = W2["S_total"], W2["N"], W2["G"], W2["k"]
+    qo = [pyoracle.OracleQueue() for _ in range(S_total)]
+    for q in qo:
+        q.register(tab.slots, tab.r, tab.w, tab.l, True)
+    et = EpochTrackers(S_total, N, G, cmap)
+    want = {}
+    for e, (t, ep) in enumerate(eps):
+        for s in range(S_total):
+            reqs = ep[s].copy()
+            et.fill(s, reqs)
+            want[("req", e, s)] = (reqs["delta"].copy(), reqs["rho"].copy())
+            assert (qo[s].add_batch(reqs) == 0).all()
+        for s in range(S_total):
+            do, _ = qo[s].pull_batch(t, k)
+            et.tally(s, do)
+            want[("dec", e, s)] = do
+        et.deliver()
+    return eps, et, want
+
+
+@pytest.mark.gpu
+def test_device_trackers_world1_rccl():
+    """The RCCL branch of DeviceTrackers.deliver: one rank on GPU 0 in an
+    `nccl` (RCCL) process group holding all four servers -- every epoch's
+    all-reduce runs through RCCL on the device buffers (the identity at
+    world size 1; the 8-GPU runs reduce over xGMI) -- against the oracle
+    queues with the epoch restatement: every request's delta/rho, every
+    decision and the final tracker state bit-exact."""
+    import torch.multiprocessing as mp
+    from parity import compare_decisions
+    ctx = mp.get_context("spawn")
+    out_q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    p = ctx.Process(target=_device_trackers_worker, args=(0, 1, port, out_q, "nccl"))
+    p.start()
+    try:
+        rank, st, decs = out_q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    eps, et, want = _oracle_reference(1)
+    n_dec = 0
+    it = iter(decs)
+    S = W2["S_total"]
+    for e in range(len(eps)):
+        for _ in range(S):
+            kind, s, d, r = next(it)
+            wd, wr = want[("req", e, s)]
+            assert np.array_equal(d, wd) and np.array_equal(r, wr), (e, s)
+        for _ in range(S):
+            kind, s, dg = next(it)
+            compare_decisions(dg, want[("dec", e, s)], f"epoch {e} server {s}")
+            n_dec += len(dg)
+    for f in ("gd", "gr", "xd", "xr", "known"):
+        assert np.array_equal(st[f], getattr(et, f)), f
+    assert n_dec > 1000
 
 
 @pytest.mark.gpu
