@@ -37,6 +37,7 @@ OPT_SAMPLE = 5
 OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
+OPT_PREDICT = 9
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0
@@ -130,6 +131,8 @@ class Counters(ctypes.Structure):
         ("bin_splits", ctypes.c_uint64),
         ("brk_rounds", ctypes.c_uint64),
         ("brk_fallbacks", ctypes.c_uint64),
+        ("pred_rounds", ctypes.c_uint64),
+        ("pred_misses", ctypes.c_uint64),
     ]
 
     def as_dict(self):

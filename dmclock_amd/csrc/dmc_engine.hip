@@ -1648,6 +1648,14 @@ struct dmc_queue {
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   int fail_allocs = 0;   // DMC_OPT_FAIL_ALLOC (test hook): device allocations to fail
   bool brk_rounds = true;  // DMC_OPT_BREAK_ROUNDS: Allow's limit breaks as rounds
+  // predicted-candidate rounds (DMC_OPT_PREDICT): the last sampled bin-ranked
+  // rounds' thresholds per phase ([0] the latest), their k, how many
+  bool pred_on = false;  // measured slower at config 3
+  bool pred_skip = false;     // the next round runs unpredicted (after a miss)
+  uint64_t thrT[2][2] = {{0, 0}, {0, 0}};
+  uint32_t thrK = 0, thrN = 0;
+  ScanEnt* slist = nullptr;   // k_rscan blocks x kListCap predicted-candidate entries
+  uint32_t* slcnt = nullptr;  // per k_rscan block: its list's length
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
   bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
@@ -2569,7 +2577,7 @@ bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
 
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = false) {
   prof_gate(q);
   const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
@@ -2577,9 +2585,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN), dim3(kScanBlock), 0,
-          tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta, q->rparts,
-          q->rd, cp, sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32, q->hist);
+  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : pred ? k_rscan_pred : k_rscan, dim3(gN),
+          dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
+          q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
+          sampled ? q->skp : nullptr, q->k32, q->hist, q->slist, q->slcnt);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
@@ -2589,10 +2598,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
             gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup);
-  klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
+  klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : pred ? k_remit_pred : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsup, (const uint32_t*)q->hist,
-          q->dense, q->ecap, q->debug ? q->dbg_etime : nullptr);
+          q->dense, q->ecap, (const ScanEnt*)q->slist, (const uint32_t*)q->slcnt,
+          q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
     if (q->debug)  // (the record counts: the rank-bin counters' low words)
       (void)hipMemcpy2DAsync(q->dbg_bins, sizeof(uint32_t), q->bcount, 2 * sizeof(uint32_t),
@@ -2642,17 +2652,67 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
           q->debug ? q->dbg_atime : nullptr);
 }
 
+// Predicted thresholds for a round of kk pulls (DMC_OPT_PREDICT): the last
+// round's, widened by three times its last drift and 2^-20 relative, for a
+// sampled bin-ranked round of the same k as the last ones.  R: "all" stays
+// all (and none predicts all: the R-eligible slots are few); P: none
+// predicts nothing (no prediction).
+bool predict(dmc_queue* q, uint32_t kk, bool radix, bool brk, uint64_t pT[2]) {
+  if (!q->pred_on || q->pred_skip || radix || brk || !use_sample(q, radix) ||
+      q->thrN == 0 || q->thrK != kk)
+    return false;
+  for (int p = 0; p < 2; ++p) {
+    const uint64_t T0 = q->thrT[p][0];
+    if (T0 == kMaxKey - 1 || (p == 0 && T0 == 0)) {
+      pT[p] = kMaxKey - 1;
+      continue;
+    }
+    if (T0 == 0) return false;
+    const double d0 = from_okey(T0);
+    double drift = 0.0;
+    const uint64_t T1 = q->thrT[p][1];
+    if (q->thrN >= 2 && T1 != 0 && T1 != kMaxKey - 1) drift = d0 - from_okey(T1);
+    const double w = 3.0 * std::fabs(drift) + std::ldexp(std::fabs(d0) + 1.0, -20);
+    const double dp = d0 + w;
+    if (!(dp < kInf)) {
+      pT[p] = kMaxKey - 1;
+      continue;
+    }
+    const uint64_t kp = okey(dp) | 0xffffffffull;  // (the end of its 32-bit quantum)
+    pT[p] = kp < kMaxKey - 1 ? kp : kMaxKey - 1;
+  }
+  return true;
+}
+
+// after a completed round: its thresholds for the next predictions
+void record_thresholds(dmc_queue* q, const Round& c, uint32_t kk, bool radix, bool brk) {
+  q->pred_skip = false;
+  if (radix || brk || !c.sampled) {
+    q->thrN = 0;
+    return;
+  }
+  if (q->thrK != kk) q->thrN = 0;
+  for (int p = 0; p < 2; ++p) {
+    q->thrT[p][1] = q->thrT[p][0];
+    q->thrT[p][0] = c.ph[p].T;
+  }
+  q->thrK = kk;
+  q->thrN = std::min<uint32_t>(q->thrN + 1, 2);
+}
+
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
                  dmc_pull_result* d_result, bool radix, bool brk = false) {
   const bool sampled = use_sample(q, radix);
-  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 4) | (brk ? 8 : 0) | (sampled ? 4 : 0) |
-                 (radix ? 2 : 0);
-  CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq};
+  CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq, {0, 0}};
+  const bool pred = predict(q, kk, radix, brk, cp.pT);
+  if (pred) ++q->ctr.pred_rounds;
+  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 5) | (pred ? 16 : 0) | (brk ? 8 : 0) |
+                 (sampled ? 4 : 0) | (radix ? 2 : 0);
   int err = DMC_OK;
-  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); }, &err);
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, pred); }, &err);
   if (err) return err;
   if (!g) {
-    enqueue_round(q, cp, radix);
+    enqueue_round(q, cp, radix, pred);
     HIP_OK(hipGetLastError());
     return DMC_OK;
   }
@@ -2662,7 +2722,7 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   uint64_t* kr = sampled ? nullptr : q->keyr;
   uint64_t* kp = sampled ? nullptr : q->keyp;
   void* args[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                  &skr, &skp, &q->k32, &q->hist};
+                  &skr, &skp, &q->k32, &q->hist, &q->slist, &q->slcnt};
   return graph_replay(q, *g, args);
 }
 
@@ -2894,6 +2954,18 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       retry_radix = retry;
       continue;
     }
+    if (c.overflow == 6) {
+      // a predicted round's threshold lay above its prediction (or a list
+      // outgrew its capacity): nothing of it took effect; re-run unpredicted
+      ++q->ctr.pred_misses;
+      q->pred_skip = true;
+      if (q->debug || getenv("DMC_PRED_LOG"))
+        std::fprintf(stderr, "dmc pred miss: T %.9g %.9g predicted %.9g %.9g\n",
+                     c.ph[0].T ? from_okey(c.ph[0].T) : 0.0,
+                     c.ph[1].T ? from_okey(c.ph[1].T) : 0.0,
+                     c.pT[0] ? from_okey(c.pT[0]) : 0.0, c.pT[1] ? from_okey(c.pT[1]) : 0.0);
+      continue;
+    }
     if (c.overflow == 5) {
       // a limit-break round found the state not break-ready (a front with
       // r <= now or l <= now, or a weight-0 client's infinite p): nothing of
@@ -2942,6 +3014,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     if (!radix) q->ovf_streak = 0;
     q->exact_next = false;
+    record_thresholds(q, c, kr, radix, brk);
     q->ctr.candidates += c.n_cand;
     q->ctr.entries += radix ? c.dense_n : c.n_emit;
     q->ctr.decisions += c.n_dec;
@@ -3060,6 +3133,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
+  rc |= A(&q->slist, (size_t)((N + kScanBlock - 1) / kScanBlock) * kListCap);
+  rc |= A(&q->slcnt, (N + kScanBlock - 1) / kScanBlock);
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsup, kNSup);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
@@ -3114,7 +3189,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
                   q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist,
-                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->slist, q->slcnt, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
@@ -3690,15 +3765,19 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
-      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq};
+      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq, {0, 0}};
+      const bool pred = predict(q, k, false, false, cp.pT);
+      if (pred) ++q->ctr.pred_rounds;
       auto enqueue = [&] {
         enqueue_add(q, ap);
-        enqueue_round(q, cp, false);
+        enqueue_round(q, cp, false, pred);
       };
       ++q->ctr.fused_calls;
-      uint64_t key = (4ull << 56) | ((uint64_t)n << 2) | (use_sample(q, false) ? 2 : 0);
+      uint64_t key = (4ull << 56) | ((uint64_t)n << 3) | (pred ? 4 : 0) |
+                     (use_sample(q, false) ? 2 : 0);
       int err = DMC_OK;
-      GraphRec* gr = graph_for(q, key, enqueue, &err, (const void*)k_rscan);
+      GraphRec* gr = graph_for(q, key, enqueue, &err,
+                               pred ? (const void*)k_rscan_pred : (const void*)k_rscan);
       if (err) return err;
       if (!gr) {
         enqueue();
@@ -3714,7 +3793,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         uint64_t* kr = sampled ? nullptr : q->keyr;
         uint64_t* kp = sampled ? nullptr : q->keyp;
         void* a2[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                      &skr, &skp, &q->k32, &q->hist};
+                      &skr, &skp, &q->k32, &q->hist, &q->slist, &q->slcnt};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }
@@ -3985,6 +4064,10 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_BREAK_ROUNDS:
       q->brk_rounds = value != 0;
+      return DMC_OK;
+    case DMC_OPT_PREDICT:
+      q->pred_on = value != 0;
+      q->thrN = 0;
       return DMC_OK;
     case DMC_OPT_FAIL_ALLOC:
       if (value < 0) return DMC_EINVAL;

@@ -143,6 +143,8 @@ struct Round {
   uint64_t tick;
   dmc_pull_result* res;  // device-API result record (null: the host writes it)
   uint64_t seq;          // round sequence number, published to the host
+  uint64_t pT[2];        // predicted thresholds (pred rounds: k_rscan listed every
+                         // slot whose first key is at or below them)
 };
 
 struct CallParams {
@@ -153,7 +155,22 @@ struct CallParams {
   uint64_t tick;
   dmc_pull_result* res;
   uint64_t seq;
+  uint64_t pT[2];  // predicted thresholds (the host's, from the last rounds'
+                   // thresholds; used by the PRED instantiations only)
 };
+
+// Predicted-candidate rounds (PRED): instead of every slot's quantized keys
+// and meta word (12 B per slot written by k_rscan and streamed by k_remit),
+// k_rscan lists, per block in slot order, the slots whose first key is at or
+// below the host's predicted thresholds and those it gave a pending
+// limit-scan mark; k_remit reads its four scan blocks' lists.  The list is
+// exact for every threshold at or below the predicted one: a round whose
+// picked threshold lies above it, or a list that outgrew kListCap, fails
+// (overflow = 6) before anything is applied and is re-run unpredicted.
+struct ScanEnt {
+  uint32_t slot, kr32, kp32, meta;
+};
+constexpr uint32_t kListCap = 512;  // entries per k_rscan block (of 1024 slots)
 
 // Host-mapped (fine-grained pinned) round summary: the round's last kernel
 // copies Round here and then publishes seq, so the host learns the outcome
@@ -330,6 +347,11 @@ __device__ inline ScanOut scan_compute(const Table& tb, uint32_t s, const ScanCo
   return o;
 }
 
+__device__ inline uint32_t scan_meta(const ScanCols& x, const ScanOut& o) {
+  return (o.m & 0xffu) | ((uint32_t)o.f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
+}
+
+template <bool FULL = true>
 __device__ inline void scan_store(const Table& tb, uint32_t s, const ScanCols& x,
                                   const ScanOut& o, uint64_t* keyr, uint64_t* keyp,
                                   uint32_t* meta, uint64_t* skr, uint64_t* skp,
@@ -337,18 +359,18 @@ __device__ inline void scan_store(const Table& tb, uint32_t s, const ScanCols& x
   const uint64_t kr = o.kr, kp = o.kp;
   const uint32_t m = o.m;
   if (o.mark) tb.sc[s].flags = o.f;
-  if (keyr) {  // the exact histogram's keys (unsampled rounds)
+  if (FULL && keyr) {  // the exact histogram's keys (unsampled rounds)
     keyr[s] = kr;
     keyp[s] = kp;
   }
-  k32[s] = make_uint2(key32(kr), key32(kp));
+  if (FULL) k32[s] = make_uint2(key32(kr), key32(kp));
   if (skr && (s & (kSample - 1)) == 0) {  // the threshold histogram's sample
     skr[s / kSample] = kr;
     skp[s / kSample] = kp;
   }
   // the candidate record's fields for k_remit: R-prefix length, flags (with
   // a pending mark this scan set), ring head and count
-  meta[s] = (m & 0xffu) | ((uint32_t)o.f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
+  if (FULL) meta[s] = scan_meta(x, o);
   if (kr != kMaxKey) {
     ++acc.cnt[0];
     acc.n_r += m;
@@ -461,13 +483,16 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
-template <bool BRK>
+template <bool BRK, bool PRED>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
 k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
           RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
-          uint2* k32, uint32_t* hist) {
+          uint2* k32, uint32_t* hist, ScanEnt* lst, uint32_t* lcnt) {
+  static_assert(!PRED || kScanSlots == 1, "predicted lists: one slot per thread");
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
+    z.pT[0] = cp.pT[0];
+    z.pT[1] = cp.pT[1];
     z.k_total = cp.k_total;
     z.brk = cp.brk;
     z.g_last = kNoneR;
@@ -530,7 +555,20 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
-    if (s < tb.n) scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
+    if (s < tb.n)
+      scan_store<!PRED>(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
+  }
+  // PRED: this block's list, in slot order (wave counts parked in LDS for
+  // the offsets after the block barrier below)
+  __shared__ uint32_t s_wc[kScanBlock / 64];
+  bool ent = false;
+  uint64_t bal = 0;
+  if (PRED) {
+    const uint64_t kr = o[0].kr, kp = o[0].kp;
+    ent = base < tb.n && ((kr != kMaxKey && kr <= cp.pT[0]) ||
+                          (kp != kMaxKey && kp <= cp.pT[1]) || o[0].mark);
+    bal = __ballot(ent);
+    if ((threadIdx.x & 63) == 0) s_wc[threadIdx.x >> 6] = (uint32_t)__popcll(bal);
   }
   sh[threadIdx.x] = acc;
   // the threshold histogram k_rhist fills, cleared (the previous round's
@@ -541,6 +579,18 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
       hist[gi] = 0;
   }
   __syncthreads();
+  if (PRED) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t at = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+    for (int i = 0; i < kScanBlock / 64; ++i) {
+      at += i < w ? s_wc[i] : 0u;
+      tot += s_wc[i];
+    }
+    if (ent && at < kListCap)
+      lst[(size_t)blockIdx.x * kListCap + at] =
+          ScanEnt{base, key32(o[0].kr), key32(o[0].kp), scan_meta(x[0], o[0])};
+    if (threadIdx.x == 0) lcnt[blockIdx.x] = tot;  // (> kListCap: the round fails)
+  }
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
     for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
@@ -549,9 +599,11 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   }
 }
 
-// the general scan (the graphs' parameter node) and the limit-break scan
-constexpr auto k_rscan = k_rscan_t<false>;
-constexpr auto k_rscan_brk = k_rscan_t<true>;
+// the general scan (the graphs' parameter node), the limit-break scan, and
+// the predicted-candidate scan
+constexpr auto k_rscan = k_rscan_t<false, false>;
+constexpr auto k_rscan_brk = k_rscan_t<true, false>;
+constexpr auto k_rscan_pred = k_rscan_t<false, true>;
 
 // The round's totals from the scan's per-block partials (every thread gets
 // them): wave 0 combines them, 8 per lane for 512 partials with the loads in
@@ -1329,13 +1381,19 @@ constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
 // walkers with a staging slice per wave: its first lanes (a wave with more
 // candidates walks the rest from global memory)
 constexpr int kEmitStageLanes = kEmitStageThreads / (kEmitThreads / 64);
-template <bool BRK>
+// (PRED: the slots come from the four k_rscan blocks' lists of this block's
+// chunk, at most 2 x kEmitThreads entries: two per thread)
+constexpr uint32_t kScanPerEmit = kEmitChunk / kScanBlock;
+template <bool BRK, bool PRED>
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
-        uint32_t dcap, uint64_t* eclk = nullptr) {
+        uint32_t dcap, const ScanEnt* lst, const uint32_t* lcnt,
+        uint64_t* eclk = nullptr) {
+  static_assert(!PRED || (kScanPerEmit * kListCap <= 2 * kEmitThreads && kEmitPer >= 2),
+                "predicted lists: two entries per thread");
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
@@ -1363,7 +1421,56 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
-  if (s0 + kEmitPer <= n) {
+  // PRED: the list's segment sizes (the four scan blocks), the entries'
+  // slots, and whether a list overflowed
+  uint32_t seg[kScanPerEmit];
+  uint32_t sl[2] = {0, 0};
+  uint32_t nent = 0;
+  // list entry e of this block: (segment, offset) by the segment sizes
+  // (static indices only: seg[] stays in registers)
+  static_assert(kScanPerEmit == 4, "four scan blocks per emit block");
+  auto ent_at = [&](uint32_t e) -> const ScanEnt& {
+    uint32_t sg = 0;
+    if (e >= seg[0]) {
+      e -= seg[0];
+      sg = 1;
+      if (e >= seg[1]) {
+        e -= seg[1];
+        sg = 2;
+        if (e >= seg[2]) {
+          e -= seg[2];
+          sg = 3;
+        }
+      }
+    }
+    return lst[(size_t)(blockIdx.x * kScanPerEmit + sg) * kListCap + e];
+  };
+  if (PRED) {
+#pragma unroll
+    for (int i = 0; i < (int)kScanPerEmit; ++i) {
+      const uint32_t c = blockIdx.x * kScanPerEmit + i < (n + kScanBlock - 1) / kScanBlock
+                             ? lcnt[blockIdx.x * kScanPerEmit + i]
+                             : 0u;
+      seg[i] = c < kListCap ? c : kListCap;
+      nent += seg[i];
+    }
+#pragma unroll
+    for (int j = 0; j < kEmitPer; ++j) {
+      kr[j] = kp[j] = 0xffffffffu;
+      mt[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t e = threadIdx.x + j * kEmitThreads;
+      if (e < nent) {
+        const ScanEnt x = ent_at(e);
+        sl[j] = x.slot;
+        kr[j] = x.kr32;
+        kp[j] = x.kp32;
+        mt[j] = x.meta;
+      }
+    }
+  } else if (s0 + kEmitPer <= n) {
     const uint4* k4 = reinterpret_cast<const uint4*>(k32 + s0);
     const uint4* m4 = reinterpret_cast<const uint4*>(meta + s0);
 #pragma unroll
@@ -1392,6 +1499,25 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   pick_both(rd->k_total, rd->tot, hist, ltab, s_ph, (int)rd->sampled);
   if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   const CandPred pred(s_ph, p_runs);
+  if (PRED) {
+    // the lists hold every slot at or below the predicted thresholds: the
+    // picked ones must not lie above them (wave-uniform: every block picks
+    // the same) and no list may have overflowed (any block's: read by all)
+    bool miss = (pred.TR && pred.TR > rd->pT[0]) || (pred.TP && pred.TP > rd->pT[1]);
+    if (!miss) {
+      const uint32_t nsb = (n + kScanBlock - 1) / kScanBlock;
+      for (uint32_t i = threadIdx.x; i < nsb; i += kEmitThreads)
+        if (lcnt[i] > kListCap) miss = true;
+      miss = __syncthreads_or(miss);
+    }
+    if (miss) {
+      // nothing of the round takes effect (the pending marks this scan set
+      // are set again by the unpredicted re-run at the same `now`)
+      if (blockIdx.x == 0 && threadIdx.x == 0) rd->overflow = 6;
+      if (threadIdx.x == 0) bcand[blockIdx.x] = 0;
+      return;
+    }
+  }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
   uint8_t f[kEmitPer];
 #pragma unroll
@@ -1399,7 +1525,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
   for (int j = 0; j < kEmitPer; ++j) {
-    if (s0 + j >= n) continue;
+    if (PRED ? (j >= 2 || threadIdx.x + j * kEmitThreads >= nent) : s0 + j >= n) continue;
     const bool cr = pred.TR && kr[j] <= pred.TR32;
     const bool cp = pred.TP && kp[j] <= pred.TP32;
     if (cr || cp) bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
@@ -1443,8 +1569,8 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
       const uint32_t b = (bits >> (2 * j)) & 3u;
       if (b) {
         bk[o] = (b & 1u) ? kr[j] : kp[j];
-        bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)), (uint8_t)mt[j],
-                          (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
+        bl[o++] = CandRec{PRED ? sl[j < 2 ? j : 0] : s0 + j, (uint8_t)(f[j] | (b << 4)),
+                          (uint8_t)mt[j], (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
       }
     }
   }
@@ -1502,20 +1628,59 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
     uint32_t ti = threadIdx.x;
     asm volatile("" : "+v"(ti));  // (its LDS address recomputed here, not held)
     const uint2 fb = s_fb[ti];
-    const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
+    if (PRED) {
+      // (the entries' slots and the segment sizes reloaded: not held --
+      // spilled -- across the walks)
+      const uint32_t* lc = lcnt;
+      asm volatile("" : "+s"(lc));
+      uint32_t sz[kScanPerEmit], ne = 0;
 #pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
-      const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
-      if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
-        tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
+      for (int i = 0; i < (int)kScanPerEmit; ++i) {
+        const uint32_t c = blockIdx.x * kScanPerEmit + i < (n + kScanBlock - 1) / kScanBlock
+                               ? lc[blockIdx.x * kScanPerEmit + i]
+                               : 0u;
+        sz[i] = c < kListCap ? c : kListCap;
+        ne += sz[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
+        uint32_t e = ti + j * kEmitThreads;
+        if (e < ne && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK)) {
+          uint32_t sg = 0;
+          if (e >= sz[0]) {
+            e -= sz[0];
+            sg = 1;
+            if (e >= sz[1]) {
+              e -= sz[1];
+              sg = 2;
+              if (e >= sz[2]) {
+                e -= sz[2];
+                sg = 3;
+              }
+            }
+          }
+          const uint32_t slot = lst[(size_t)(blockIdx.x * kScanPerEmit + sg) * kListCap + e].slot;
+          tb.sc[slot].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
+        }
+      }
+    } else {
+      const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
+#pragma unroll
+      for (int j = 0; j < kEmitPer; ++j) {
+        const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
+        if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
+          tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
+      }
     }
   }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
 }
 
-// the general emission and the limit-break rounds' emission
-constexpr auto k_remit = k_remit_t<false>;
-constexpr auto k_remit_brk = k_remit_t<true>;
+// the general emission, the limit-break rounds' and the predicted rounds'
+constexpr auto k_remit = k_remit_t<false, false>;
+constexpr auto k_remit_brk = k_remit_t<true, false>;
+constexpr auto k_remit_pred = k_remit_t<false, true>;
 
 // ---------------------------------------------------------------- k_rrank
 // One block per rank bin ranks it in LDS by (okey, slot, position); R bins

@@ -331,6 +331,11 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   pulls with k <= SMALL_K run the single-op path (one kernel per add,
                                   two per pull, results in host-mapped memory, one round trip);
                                   0: the general launch sequence */
+#define DMC_OPT_PREDICT 9       /* 1: a sampled bin-ranked round of the same k as the last ones
+                                  lists its candidates against thresholds predicted from theirs
+                                  (k_remit walks the lists, not the key columns; a miss re-runs the
+                                  round unpredicted); 0 (default): never -- measured slower at
+                                  config 3 */
 #define DMC_OPT_BREAK_ROUNDS 8  /* 1 (default): AtLimit::Allow's limit breaks (dmclock_server.h:1157-1165)
                                   run as batched rounds after the eligible work ran out (immediate
                                   mode); 0: one general pull_request step each */
@@ -360,6 +365,9 @@ typedef struct dmc_counters {
   uint64_t bin_splits;      /* of the overflowed rounds: re-run as a smaller round   */
   uint64_t brk_rounds;      /* limit-break rounds started (AtLimit::Allow)           */
   uint64_t brk_fallbacks;   /* limit-break rounds whose state was not break-ready    */
+  uint64_t pred_rounds;     /* rounds run with predicted thresholds (DMC_OPT_PREDICT) */
+  uint64_t pred_misses;     /* ... re-run unpredicted (a threshold above the prediction,
+                               or a candidate list past its capacity)               */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 

@@ -94,7 +94,8 @@ def replay_device(q, trace, fuse=True, host_ops=False):
     return outs
 
 
-def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True, host_ops=False):
+def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True, host_ops=False,
+                  options=()):
     from dmclock_amd.gpu import GpuQueue
     queue_kw = queue_kw or {}
     qo = pyoracle.OracleQueue(**queue_kw)
@@ -103,6 +104,8 @@ def device_parity(trace, queue_kw=None, state_sample=4096, fuse=True, host_ops=F
     n = int(trace.clients.slots.max()) + 1
     maxb = max(len(op[1]) for op in trace.ops if op[0] == "add")
     qg = GpuQueue(max_clients=n, ring_capacity=64, max_batch=maxb, **queue_kw)
+    for opt, val in options:
+        qg.set_option(opt, val)
     outs_g = replay_device(qg, trace, fuse=fuse, host_ops=host_ops)
     n_dec = 0
     for i, (a, b) in enumerate(zip(outs_g, outs_o)):
@@ -134,6 +137,23 @@ def test_fused_bench_call_parity_1m_clients():
     c = qg.counters()
     assert c["fused_calls"] == 4, c
     assert c["graph_replays"] >= 3, c
+    qg.close()
+
+
+def test_predicted_rounds_parity():
+    """DMC_OPT_PREDICT (off by default: measured slower): the
+    fused call's round lists, in k_rscan, the slots whose keys fall under
+    thresholds predicted from the previous rounds, and k_remit walks those
+    lists instead of the key columns; a round whose picked thresholds exceed
+    the prediction re-runs unpredicted.  Config 3 at full size, every
+    decision bit-exact, and the predicted rounds counted."""
+    from dmclock_amd._abi import OPT_PREDICT
+    tr = workloads.config3_trace(42, 1 << 20, 8, 1 << 16, depth=2)
+    n, qg, qo = device_parity(tr, options=[(OPT_PREDICT, 1)])
+    c = qg.counters()
+    assert c["fused_calls"] == 8, c
+    assert c["pred_rounds"] >= 5, c
+    assert c["pred_misses"] < c["pred_rounds"], c
     qg.close()
 
 
