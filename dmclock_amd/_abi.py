@@ -38,6 +38,7 @@ OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
 OPT_PREDICT = 9
+OPT_SERVE = 10
 
 # PhaseType (dmclock_recs.h:33)
 PHASE_RESERVATION = 0
@@ -133,6 +134,8 @@ class Counters(ctypes.Structure):
         ("brk_fallbacks", ctypes.c_uint64),
         ("pred_rounds", ctypes.c_uint64),
         ("pred_misses", ctypes.c_uint64),
+        ("serve_calls", ctypes.c_uint64),
+        ("serve_launches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

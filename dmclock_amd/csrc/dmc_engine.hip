@@ -1176,7 +1176,7 @@ __global__ void k_step_scan(Table tb, double now, StepRed* part) {
   step_scan_body(tb, now, part);
 }
 
-__device__ inline void stepred_combine(StepRed& o, const StepRed& b) {
+__device__ __attribute__((always_inline)) inline void stepred_combine(StepRed& o, const StepRed& b) {
   o.r = argmin_combine(o.r, b.r);
   o.p = argmin_combine(o.p, b.p);
   o.pnr = argmin_combine(o.pnr, b.pnr);
@@ -1541,6 +1541,10 @@ struct FastIO {
   int32_t pad;
 };
 
+namespace {
+#include "dmc_serve.h"
+}  // namespace
+
 struct dmc_queue {
   dmc_queue_params p{};
   hipStream_t stream = nullptr;
@@ -1560,6 +1564,24 @@ struct dmc_queue {
   FastIO* h_fast = nullptr;
   FastIO* d_fast = nullptr;
   uint32_t* fast_done = nullptr;
+  // the serve path (DMC_OPT_SERVE, dmc_serve.h): k_serve running on the
+  // queue's stream; the group summaries are valid while no other call has
+  // run since k_serve last wrote them
+  bool serve_on = false;
+  bool serving = false;
+  bool gsum_valid = false;
+  ServeIO* h_serve = nullptr;
+  ServeIO* d_serve = nullptr;
+  StepRed* gsum = nullptr;
+  uint32_t gshift = 10, ngroups = 0;
+  uint64_t serve_seq = 0;
+  uint64_t serve_idle_ticks = 200000;  // 2 ms of the 100 MHz wall clock
+  // DMC_SERVE_TRACE: per-call phases (k_serve's wall-clock stamps), printed
+  // at destroy: read, work, publish (ticks) and the host's call time (ns)
+  bool serve_trace = getenv("DMC_SERVE_TRACE") != nullptr;
+  double serve_tr[4] = {0, 0, 0, 0};
+  double serve_ph[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // [add, pull]: phases, calls
+  double serve_mhz = 0;
   // dmc_client_mark_idle_batch_device: the host idle mirror (idle_h /
   // n_idle) is stale until sync_idle reads the flags back
   bool idle_unknown = false;
@@ -1682,9 +1704,26 @@ struct dmc_queue {
 // Every entry point of a queue holds its mutex (the reference's data_mtx) and
 // makes the queue's device current for the calling thread, so that servers
 // of one rank can be driven from one host thread each.
+// Stops k_serve (its summaries written back) before a call that launches
+// other work on the queue's stream or changes the table; the summaries are
+// then stale until rebuilt.
+void serve_quiesce(dmc_queue* q) {
+  q->gsum_valid = false;
+  if (!q->serving) return;
+  q->h_serve->op = kServeStop;
+  __atomic_store_n(&q->h_serve->req_seq, ++q->serve_seq, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(q->stream);
+  q->serving = false;
+}
+
+// Every C-ABI call holds the queue's lock; all but the serve path's calls
+// quiesce k_serve first.
 struct QueueLock {
   std::lock_guard<std::mutex> l;
-  explicit QueueLock(dmc_queue* q) : l(q->mtx) { (void)hipSetDevice(q->p.device); }
+  explicit QueueLock(dmc_queue* q, bool serve = false) : l(q->mtx) {
+    (void)hipSetDevice(q->p.device);
+    if (!serve) serve_quiesce(q);
+  }
 };
 
 namespace {
@@ -2787,6 +2826,112 @@ int fast_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
   return DMC_OK;
 }
 
+// ------------------------------------------------------------------ serve path
+int serve_start(dmc_queue* q, uint64_t seq0) {
+  if (!q->gsum_valid) {
+    hipLaunchKernelGGL(k_gsum_build, dim3(q->ngroups), dim3(kServeThreads), 0, q->stream,
+                       q->tb, q->gsum, q->gshift);
+    q->gsum_valid = true;
+  }
+  __atomic_store_n(&q->h_serve->state, (uint32_t)kServeRunning, __ATOMIC_RELEASE);
+  hipLaunchKernelGGL(k_serve, dim3(1), dim3(kServeThreads), 0, q->stream, q->tb, q->gsum,
+                     q->ngroups, q->gshift, q->d_serve, q->p.at_limit, q->n_registered,
+                     q->sched, seq0, q->serve_idle_ticks);
+  if (hipGetLastError() != hipSuccess) {
+    q->gsum_valid = false;
+    return DMC_EDEVICE;
+  }
+  q->serving = true;
+  ++q->ctr.serve_launches;
+  return DMC_OK;
+}
+
+// One command to k_serve (the command fields already written): launch it if
+// it is not running, post, and wait for the answer.  A kernel that idled out
+// just before the post is relaunched to take the posted command.
+int serve_call(dmc_queue* q) {
+  ServeIO* io = q->h_serve;
+  if (!q->serving) {
+    int rc = serve_start(q, q->serve_seq);
+    if (rc) return rc;
+  }
+  const uint64_t seq = ++q->serve_seq;
+  __atomic_store_n(&io->req_seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&io->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 255) == 0) {
+      if (__atomic_load_n(&io->state, __ATOMIC_ACQUIRE) == kServeExited &&
+          __atomic_load_n(&io->done_seq, __ATOMIC_ACQUIRE) != seq) {
+        HIP_OK(hipStreamSynchronize(q->stream));
+        q->serving = false;
+        int rc = serve_start(q, seq - 1);
+        if (rc) return rc;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        serve_quiesce(q);
+        return DMC_EDEVICE;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  ++q->ctr.serve_calls;
+  if (q->serve_trace) {
+    q->serve_tr[0] += (double)(io->clk[1] - io->clk[0]);
+    q->serve_tr[1] += (double)(io->clk[2] - io->clk[1]);
+    q->serve_tr[2] += (double)(io->clk[3] - io->clk[2]);
+    q->serve_tr[3] += std::chrono::duration<double, std::nano>(
+                          std::chrono::steady_clock::now() - t0).count();
+    double* ph = q->serve_ph[io->op == kServePull ? 1 : 0];
+    ph[0] += (double)(io->phase[0] - io->clk[1]);
+    ph[1] += (double)(io->phase[1] - io->phase[0]);
+    ph[2] += (double)(io->phase[2] - (io->op == kServePull ? io->phase[1] : io->phase[0]));
+    ph[3] += 1;
+    q->serve_tr[2] += 0;  // (publish stamp unused: the fence is not observable)
+    q->serve_mhz += 100.0 * (double)(io->cyc[1] - io->cyc[0]) /
+                    (double)std::max<uint64_t>(1, io->clk[2] - io->clk[1]);
+  }
+  return DMC_OK;
+}
+
+bool serve_add_ok(const dmc_queue* q, const dmc_request& r) {
+  return q->serve_on && q->single_op && !q->prof_on && !q->act_pending && !q->idle_unknown &&
+         !(q->info_fn && q->tb.binfo) && (r.slot >= q->p.max_clients || !q->idle_h[r.slot]);
+}
+
+int serve_add(dmc_queue* q, const dmc_request& r, int32_t* rc_out) {
+  ServeIO* io = q->h_serve;
+  io->op = kServeAdd;
+  io->tick = q->tick;
+  io->req = r;
+  int rc = serve_call(q);
+  if (rc) return rc;
+  q->tick += 1;
+  if (rc_out) rc_out[0] = io->rc;
+  return DMC_OK;
+}
+
+int serve_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
+               dmc_pull_result* res) {
+  ServeIO* io = q->h_serve;
+  io->op = kServePull;
+  io->k = k;
+  io->now = now;
+  io->tick = q->tick;
+  int rc = serve_call(q);
+  if (rc) return rc;
+  dmc_pull_result r{};
+  r.n_decisions = io->n;
+  r.n_reservation = io->n_res;
+  r.n_priority = io->n_prio;
+  r.next_type = io->type;
+  if (io->type == DMC_NEXT_FUTURE) r.when = io->when;
+  q->ctr.single_steps += io->n + (io->type != DMC_NEXT_RETURNING ? 1 : 0);
+  if (io->n) std::memcpy(out, (const void*)io->dec, sizeof(dmc_decision) * io->n);
+  if (res) *res = r;
+  return DMC_OK;
+}
+
 // k successive pull_request(now).  Each round is one graph launch and one
 // host round trip; a round ends the batch unless the radix path's dense
 // buffer overflowed (retry with more capacity), a rank bin overflowed (retry
@@ -3148,6 +3293,15 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->apblk, 1);
   rc |= A(&q->sched, 2);
   rc |= A(&q->fast_done, 2);
+  while (((uint64_t)N + (1ull << q->gshift) - 1) >> q->gshift > kServeMaxG) ++q->gshift;
+  q->ngroups = (uint32_t)(((uint64_t)N + (1ull << q->gshift) - 1) >> q->gshift);
+  rc |= A(&q->gsum, q->ngroups);
+  {
+    int khz = 0;  // the wall clock k_serve's idle limit counts
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p.device) == hipSuccess &&
+        khz > 0)
+      q->serve_idle_ticks = 2ull * (uint64_t)khz;
+  }
   rc |= A(&q->reqcount, 1);
   if (hipHostMalloc((void**)&q->h_round, sizeof(HostRound),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -3155,10 +3309,15 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
       hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess ||
       hipHostMalloc((void**)&q->h_fast, sizeof(FastIO),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&q->d_fast, q->h_fast, 0) != hipSuccess)
+      hipHostGetDevicePointer((void**)&q->d_fast, q->h_fast, 0) != hipSuccess ||
+      hipHostMalloc((void**)&q->h_serve, sizeof(ServeIO),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&q->d_serve, q->h_serve, 0) != hipSuccess)
     rc |= DMC_ENOMEM;
-  else
+  else {
     std::memset((void*)q->h_round, 0, sizeof(HostRound));
+    std::memset((void*)q->h_serve, 0, sizeof(ServeIO));
+  }
   if (rc) {
     dmc_queue_destroy(q);
     return DMC_ENOMEM;
@@ -3183,6 +3342,22 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   (void)hipSetDevice(q->p.device);
+  if (q->h_serve) serve_quiesce(q);
+  if (q->serve_trace && q->ctr.serve_calls) {
+    const double c = (double)q->ctr.serve_calls;
+    std::fprintf(stderr, "dmc serve: %llu calls, %llu launches; per call: read %.0f, work %.0f, "
+                 "publish %.0f wall-clock ticks; host %.0f ns\n",
+                 (unsigned long long)q->ctr.serve_calls,
+                 (unsigned long long)q->ctr.serve_launches, q->serve_tr[0] / c,
+                 q->serve_tr[1] / c, q->serve_tr[2] / c, q->serve_tr[3] / c);
+    std::fprintf(stderr, "dmc serve: shader clock %.0f MHz while answering\n",
+                 q->serve_mhz / c);
+    for (int o = 0; o < 2; ++o)
+      if (q->serve_ph[o][3] > 0)
+        std::fprintf(stderr, "dmc serve %s: first phase %.0f, pop %.0f, summary %.0f ticks\n",
+                     o ? "pull" : "add", q->serve_ph[o][0] / q->serve_ph[o][3],
+                     q->serve_ph[o][1] / q->serve_ph[o][3], q->serve_ph[o][2] / q->serve_ph[o][3]);
+  }
   if (q->stream) (void)hipStreamSynchronize(q->stream);
   invalidate_graphs(q);
   Table& t = q->tb;
@@ -3214,6 +3389,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   if (q->h_sctl) (void)hipHostFree(q->h_sctl);
   if (q->h_fast) (void)hipHostFree(q->h_fast);
   dfree(q->fast_done);
+  if (q->h_serve) (void)hipHostFree(q->h_serve);
+  dfree(q->gsum);
   for (auto& r : q->prof_pool) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -3223,10 +3400,15 @@ int dmc_queue_destroy(dmc_queue* q) {
   return DMC_OK;
 }
 
-void* dmc_queue_stream(dmc_queue* q) { return q ? (void*)q->stream : nullptr; }
+void* dmc_queue_stream(dmc_queue* q) {
+  if (!q) return nullptr;
+  QueueLock g(q);  // (work the caller queues on it must not wait behind k_serve)
+  return (void*)q->stream;
+}
 
 int dmc_queue_sync(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
+  QueueLock g(q);
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
 }
@@ -3645,8 +3827,10 @@ int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
 int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
                   int32_t* rc_out) {
   if (!q || (n && !reqs)) return DMC_EINVAL;
-  QueueLock g(q);
+  QueueLock g(q, true);
   ++q->gen;
+  if (n == 1 && serve_add_ok(q, reqs[0])) return serve_add(q, reqs[0], rc_out);
+  serve_quiesce(q);
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
   if (!n) return DMC_OK;
@@ -3712,8 +3896,10 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
 int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                    dmc_pull_result* result) {
   if (!q || (k && !out)) return DMC_EINVAL;
-  QueueLock g(q);
+  QueueLock g(q, true);
   ++q->gen;
+  if (q->serve_on && fast_pull_ok(q, k)) return serve_pull(q, now, k, out, result);
+  serve_quiesce(q);
   if (fast_pull_ok(q, k)) return fast_pull(q, now, k, out, result);
   int rc = ensure_dec(q, k);
   if (rc) return rc;
@@ -4064,6 +4250,9 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_BREAK_ROUNDS:
       q->brk_rounds = value != 0;
+      return DMC_OK;
+    case DMC_OPT_SERVE:
+      q->serve_on = value != 0;
       return DMC_OK;
     case DMC_OPT_PREDICT:
       q->pred_on = value != 0;

@@ -1,0 +1,340 @@
+// The serve path: one-at-a-time add_request / pull_request (the drop-in
+// caller's calling convention, dmclock_server.h:1425-1489 pull_request and
+// :1627-1660 add_request of a Pull queue) without a kernel launch per call.
+//
+// A persistent single-workgroup kernel (k_serve) polls a host-mapped command
+// block; the host writes a command and its sequence number and polls for the
+// matching completion.  The pull decision needs the three heap tops
+// (reservation, ready proportion, limit) over every client; instead of the
+// single-op path's scan of all N fronts, the table is cut into G <= 1024
+// groups of 2^gshift slots and each group's StepRed summary (the same
+// reduction step_scan_body computes, with readiness taken from the F_READY
+// flag alone) is kept in LDS.  A decision reduces the G summaries; an add or
+// a pop changes one client, whose group is re-summarised (2^gshift fronts);
+// the limit scan's ready marks (:1131-1143, committed when the reservation
+// phase did not dispatch, exactly as k_fast_apply commits them) re-summarise
+// only the groups whose earliest not-ready limit has passed.  The decision is
+// step_decision's, the pop step_apply_body's, the add add_chain_slot's: the
+// same arithmetic as every other path.
+//
+// Exit conditions every wave reaches: a stop command, or no command for
+// `idle_ticks` of the 100 MHz wall clock (the host relaunches on demand).
+// The summaries are written back to HBM at exit (valid until any other call
+// changes the table; the host then rebuilds them with k_gsum_build).
+#pragma once
+
+constexpr int kServeThreads = 256;
+constexpr uint32_t kServeMaxG = 1024;
+enum : uint32_t { kServeNone = 0, kServeAdd = 1, kServePull = 2, kServeStop = 3 };
+enum : uint32_t { kServeRunning = 1, kServeExited = 2 };
+
+// Host-mapped command block.  The host writes the command fields, then
+// req_seq (release); the kernel answers in the second cache line, then
+// done_seq (system-scope release).
+struct alignas(64) ServeIO {
+  uint64_t req_seq;  // word 0; the command in words 1..7
+  uint32_t op, k;
+  double now;
+  uint64_t tick;
+  dmc_request req;
+  // device -> host
+  alignas(64) uint64_t done_seq;
+  uint32_t state;
+  int32_t rc;
+  uint32_t n, n_res, n_prio;
+  int32_t type;
+  double when;
+  uint64_t clk[4];  // wall clock: command seen, command read, answered, published
+  uint64_t phase[3];  // wall clock inside the first step: add/total, pop, summary
+  uint64_t cyc[2];    // shader clock at command read and at answer (the clock rate)
+  dmc_decision dec[kFastK];
+};
+static_assert(offsetof(ServeIO, done_seq) == 64, "the command is one 64-byte line");
+constexpr int kServeCmdWords = 7;
+
+__device__ inline uint64_t sys_load_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline uint32_t sys_load_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __attribute__((always_inline)) inline void stepred_clear(StepRed& a) {
+  a.r = ArgMin{kMaxKey, kNone, 0};
+  a.p = a.r;
+  a.pnr = a.r;
+  a.lmin_nr = kMaxKey;
+  a.lmin_rd = kMaxKey;
+  a.n_any = a.n_ready = a.n_notready = 0;
+  a.pad = 0;
+}
+
+// Wave reductions on the DPP network (row shifts within 16-lane rows, then
+// the row broadcasts of lane 15 and lane 31): a few ALU cycles a step, where
+// a shuffle is an LDS round trip.  Every lane starts with its own value; the
+// wave's result is in lane 63.  Lanes a step has no source for receive the
+// identity.
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline uint32_t dpp32(uint32_t v, uint32_t idn) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)idn, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline void stepred_dpp_step(StepRed& a) {
+  auto k64 = [](uint64_t v) {
+    return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32), 0xffffffffu) << 32) |
+           dpp32<CTRL, ROWS>((uint32_t)v, 0xffffffffu);
+  };
+  auto am = [&](const ArgMin& x) {
+    return ArgMin{k64(x.key), dpp32<CTRL, ROWS>(x.slot, kNone), dpp32<CTRL, ROWS>(x.cnt, 0u)};
+  };
+  StepRed b;
+  b.r = am(a.r);
+  b.p = am(a.p);
+  b.pnr = am(a.pnr);
+  b.lmin_nr = k64(a.lmin_nr);
+  b.lmin_rd = k64(a.lmin_rd);
+  b.n_any = dpp32<CTRL, ROWS>(a.n_any, 0u);
+  b.n_ready = dpp32<CTRL, ROWS>(a.n_ready, 0u);
+  b.n_notready = dpp32<CTRL, ROWS>(a.n_notready, 0u);
+  stepred_combine(a, b);
+}
+__device__ __attribute__((always_inline)) inline void wave_stepred(StepRed& a) {
+  stepred_dpp_step<0x111, 0xf>(a);  // row_shr:1
+  stepred_dpp_step<0x112, 0xf>(a);  // row_shr:2
+  stepred_dpp_step<0x114, 0xf>(a);  // row_shr:4
+  stepred_dpp_step<0x118, 0xf>(a);  // row_shr:8 (lane 15 of a row: the row's)
+  stepred_dpp_step<0x142, 0xa>(a);  // row_bcast:15 into rows 1 and 3
+  stepred_dpp_step<0x143, 0xc>(a);  // row_bcast:31 into rows 2 and 3
+}
+
+// block-wide combine of per-thread StepReds into sh[kServeRes] (visible to
+// every thread on return; sh: kServeRes + 1 entries of LDS).  The result is
+// read from LDS: a StepRed held across the barriers would go to scratch.
+constexpr int kServeRes = kServeThreads / 64;
+__device__ __attribute__((always_inline)) inline void serve_block_reduce(StepRed a, StepRed* sh) {
+  wave_stepred(a);
+  __syncthreads();  // (the previous result has been read)
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) sh[w] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kServeRes; ++i) stepred_combine(sh[0], sh[i]);
+    sh[kServeRes] = sh[0];
+  }
+  __syncthreads();
+}
+
+// one front's contribution to a summary (step_scan_body's classification)
+__device__ __attribute__((always_inline)) inline void summary_add(StepRed& a, const ScanRec& sr,
+                                                                  uint32_t s, bool rdy) {
+  ++a.n_any;
+  a.r = argmin_combine(a.r, ArgMin{okey(sr.r), s, 1});
+  const uint64_t kp = okey(sr.pk), kl = okey(sr.l);
+  if (rdy) {
+    ++a.n_ready;
+    a.lmin_rd = kl < a.lmin_rd ? kl : a.lmin_rd;
+    if (sr.pk < kInf) a.p = argmin_combine(a.p, ArgMin{kp, s, 1});
+  } else {
+    ++a.n_notready;
+    a.lmin_nr = kl < a.lmin_nr ? kl : a.lmin_nr;
+    a.pnr = argmin_combine(a.pnr, ArgMin{kp, s, 1});
+  }
+}
+
+// One group's summary (step_scan_body's reduction over slots
+// [g << gshift, (g + 1) << gshift)), into sh[kServeRes].  MARK: the limit
+// scan's ready marks for fronts with l <= now are committed first;
+// otherwise readiness is the flag alone.  The fronts are loaded kSumBatch
+// per lane before the first is used (one memory latency per batch).
+constexpr int kSumBatch = 8;
+template <bool MARK>
+__device__ __attribute__((always_inline)) inline void group_summary(const Table& tb, uint32_t g,
+                                                                    uint32_t gshift, double now,
+                                                                    StepRed* sh) {
+  StepRed a;
+  stepred_clear(a);
+  const uint32_t s0 = g << gshift;
+  const uint32_t s1 = min(tb.n, s0 + (1u << gshift));
+  for (uint32_t b = s0 + threadIdx.x; b < s1; b += kSumBatch * kServeThreads) {
+    ScanRec rs[kSumBatch];
+#pragma unroll
+    for (int u = 0; u < kSumBatch; ++u) {
+      const uint32_t s = b + u * kServeThreads;
+      if (s < s1) rs[u] = tb.sc[s];
+      else rs[u].count = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kSumBatch; ++u) {
+      const ScanRec& sr = rs[u];
+      if (!sr.count) continue;
+      const uint32_t s = b + u * kServeThreads;
+      bool rdy = (sr.flags & F_READY) != 0;
+      if (MARK && !rdy && sr.l <= now) {  // k_step_mark
+        tb.sc[s].flags = sr.flags | F_READY;
+        rdy = true;
+      }
+      summary_add(a, sr, s, rdy);
+    }
+  }
+  serve_block_reduce(a, sh);
+}
+
+// every group's summary, one workgroup per group
+__global__ void __launch_bounds__(kServeThreads)
+k_gsum_build(Table tb, StepRed* gs, uint32_t gshift) {
+  __shared__ StepRed sh[kServeRes + 1];
+  group_summary<false>(tb, blockIdx.x, gshift, 0.0, sh);
+  if (threadIdx.x == 0) gs[blockIdx.x] = sh[kServeRes];
+}
+
+// the summaries' combine (into sh[kServeRes])
+__device__ __attribute__((always_inline)) inline void serve_total(const StepRed* sg, uint32_t G, StepRed* sh) {
+  StepRed a;
+  stepred_clear(a);
+  for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) stepred_combine(a, sg[i]);
+  serve_block_reduce(a, sh);
+}
+
+__global__ void __launch_bounds__(kServeThreads)
+k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_limit,
+        uint32_t nregistered, unsigned long long* sched, uint64_t seq0,
+        uint64_t idle_ticks) {
+  __shared__ StepRed sg[kServeMaxG];
+  __shared__ StepRed sh[kServeRes + 1];
+  __shared__ uint32_t s_nst;
+  __shared__ uint16_t s_stale[kServeMaxG];
+  __shared__ uint64_t s_cmd[8];  // the command line's words (s_cmd[0]: the op, 0 = stop)
+  __shared__ int32_t s_rc;
+  __shared__ StepCtl s_c;
+  for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) sg[i] = gs[i];
+  uint64_t seen = seq0;  // (wave 0's)
+  uint64_t c_seen = 0, c_read = 0;
+  __syncthreads();
+  for (;;) {
+    if (threadIdx.x < 64) {  // wave 0 polls: one request per poll
+      const uint64_t t0 = wall_clock64();
+      bool got = false;
+      for (;;) {
+        const uint64_t sq = __hip_atomic_load(&io->req_seq, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sq != seen) {
+          seen = sq;
+          got = true;
+          break;
+        }
+        if (wall_clock64() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      c_seen = wall_clock64();
+      uint64_t w = 0;
+      if (got) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // the command's words in one round trip (a lane each)
+        const uint32_t lane = threadIdx.x;
+        if (lane < kServeCmdWords)
+          w = sys_load_u64(reinterpret_cast<const uint64_t*>(io) + 1 + lane);
+      }
+      if (threadIdx.x < kServeCmdWords) s_cmd[threadIdx.x] = w;
+      c_read = wall_clock64();
+      if (threadIdx.x == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
+    }
+    __syncthreads();
+    const uint32_t op = (uint32_t)s_cmd[0];
+    if (op != kServeAdd && op != kServePull) break;
+    const uint32_t s_k = (uint32_t)(s_cmd[0] >> 32);
+    const double s_now = __builtin_bit_cast(double, s_cmd[1]);
+    const uint64_t s_tick = s_cmd[2];
+    const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
+    const double now = s_now;
+    if (op == kServeAdd) {  // k_add_one
+      // a request for a client with no request is its new front: inserted
+      // into the group's summary (exact: nothing leaves it); otherwise the
+      // fronts, and the summary, are unchanged
+      if (threadIdx.x == 0) {
+        const uint32_t s = s_reqp->slot;
+        if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
+          s_rc = DMC_ENOTREG;
+        } else {
+          AddParams p{s_reqp, &s_rc, s_tick, 1, 0};
+          AddState st;
+          add_chain_slot(tb, p, s, 1, 0, nullptr, nullptr, ActBuf{}, &st);
+          if (st.front_set) {
+            const ScanRec sr = tb.sc[s];
+            summary_add(sg[s >> gshift], sr, s, (sr.flags & F_READY) != 0);
+          }
+        }
+        io->phase[0] = wall_clock64();
+        io->phase[2] = io->phase[0];
+        io->rc = s_rc;
+      }
+    } else {
+      uint32_t n = 0, nres = 0, nprio = 0;
+      int32_t type = DMC_NEXT_RETURNING;
+      double when = 0.0;
+      while (n < s_k) {
+        const StepRed& o = sh[kServeRes];
+        serve_total(sg, G, sh);
+        if (threadIdx.x == 0 && n == 0) io->phase[0] = wall_clock64();
+        const bool rfires = o.n_any && from_okey(o.r.key) <= now;
+        if (!rfires && nregistered) {
+          // the limit scan: re-summarise the groups holding a not-ready
+          // front whose limit has passed, committing its ready mark
+          if (threadIdx.x == 0) s_nst = 0;
+          __syncthreads();  // (and every thread has read rfires)
+          for (uint32_t i = threadIdx.x; i < G; i += kServeThreads)
+            if (sg[i].n_notready && from_okey(sg[i].lmin_nr) <= now)
+              s_stale[atomicAdd(&s_nst, 1u)] = (uint16_t)i;
+          __syncthreads();
+          const uint32_t nst = s_nst;
+          for (uint32_t j = 0; j < nst; ++j) {
+            const uint32_t g = s_stale[j];
+            group_summary<true>(tb, g, gshift, now, sh);
+            if (threadIdx.x == 0) sg[g] = sh[kServeRes];
+          }
+          __syncthreads();
+          if (nst) serve_total(sg, G, sh);
+        }
+        const StepCtl c = step_decision(o, now, at_limit, nregistered);
+        if (c.type != DMC_NEXT_RETURNING) {
+          type = c.type;
+          when = c.when;
+          break;
+        }
+        if (threadIdx.x == 0) {
+          s_c = c;
+          step_apply_body(tb, s_tick, &s_c, io->dec, n, sched);
+          if (n == 0) io->phase[1] = wall_clock64();
+        }
+        __syncthreads();
+        group_summary<false>(tb, c.slot >> gshift, gshift, now, sh);
+        if (threadIdx.x == 0) sg[c.slot >> gshift] = sh[kServeRes];
+        if (threadIdx.x == 0 && n == 0) io->phase[2] = wall_clock64();
+        __syncthreads();
+        ++n;
+        (c.prio ? nprio : nres)++;
+      }
+      if (threadIdx.x == 0) {
+        io->n = n;
+        io->n_res = nres;
+        io->n_prio = nprio;
+        io->type = type;
+        io->when = when;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      io->clk[0] = c_seen;
+      io->clk[1] = c_read;
+      io->clk[2] = wall_clock64();
+      io->cyc[1] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      io->clk[3] = wall_clock64();
+      __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) gs[i] = sg[i];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&io->state, (uint32_t)kServeExited, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}

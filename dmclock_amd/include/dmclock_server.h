@@ -94,11 +94,15 @@ struct GpuQueueOptions {
   uint32_t ring_capacity = 64;
   uint32_t max_batch = 1u << 16;
   int device = 0;
+  // single add_request / pull_request calls answered by the engine's
+  // persistent serve kernel (DMC_OPT_SERVE): no kernel launch per call
+  bool serve = false;
   static GpuQueueOptions from_env() {
     GpuQueueOptions o;
     if (const char* s = std::getenv("DMCLOCK_GPU_MAX_CLIENTS")) o.max_clients = std::atoi(s);
     if (const char* s = std::getenv("DMCLOCK_GPU_RING")) o.ring_capacity = std::atoi(s);
     if (const char* s = std::getenv("DMCLOCK_GPU_DEVICE")) o.device = std::atoi(s);
+    if (const char* s = std::getenv("DMCLOCK_GPU_SERVE")) o.serve = std::atoi(s) != 0;
     return o;
   }
 };
@@ -248,6 +252,8 @@ class PriorityQueueBase {
     p.anticipation_timeout = anticipation;
     p.device = opts_.device;
     detail::check(dmc_queue_create(&p, &q_), "dmc_queue_create");
+    if (opts_.serve)
+      detail::check(dmc_queue_set_option(q_, DMC_OPT_SERVE, 1), "dmc_queue_set_option");
     if (U1)  // get_cli_info (:870-875): the engine asks right before each tag
       detail::check(dmc_queue_set_info_fn(q_, &PriorityQueueBase::info_fn, this),
                     "dmc_queue_set_info_fn");

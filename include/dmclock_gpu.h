@@ -336,6 +336,12 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   (k_remit walks the lists, not the key columns; a miss re-runs the
                                   round unpredicted); 0 (default): never -- measured slower at
                                   config 3 */
+#define DMC_OPT_SERVE 10        /* 1: single-op adds and pulls (as DMC_OPT_SINGLE_OP) are served by a
+                                  persistent one-workgroup kernel polling host-mapped commands: no
+                                  launch per call; the pull reduces per-group summaries of the
+                                  fronts instead of scanning every client.  Any other call stops
+                                  it; it exits by itself after 2 ms without a command.
+                                  0 (default): the single-op kernels */
 #define DMC_OPT_BREAK_ROUNDS 8  /* 1 (default): AtLimit::Allow's limit breaks (dmclock_server.h:1157-1165)
                                   run as batched rounds after the eligible work ran out (immediate
                                   mode); 0: one general pull_request step each */
@@ -368,6 +374,8 @@ typedef struct dmc_counters {
   uint64_t pred_rounds;     /* rounds run with predicted thresholds (DMC_OPT_PREDICT) */
   uint64_t pred_misses;     /* ... re-run unpredicted (a threshold above the prediction,
                                or a candidate list past its capacity)               */
+  uint64_t serve_calls;     /* single adds / pulls answered by the serve kernel (DMC_OPT_SERVE) */
+  uint64_t serve_launches;  /* serve kernel launches (first call, after another call or idling) */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 

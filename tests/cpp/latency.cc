@@ -14,7 +14,10 @@
 // facade registers each at its first add, idle, as the reference does).
 // Prints one JSON line with p50 / p99 / mean per call in microseconds.
 //
-// usage: latency N M [--no-oracle] [--no-facade]
+// --serve: the facade and engine legs with DMC_OPT_SERVE (the persistent
+// serve kernel answers each single call; no launch per call).
+//
+// usage: latency N M [--no-oracle] [--no-facade] [--serve]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -83,13 +86,14 @@ struct Op {
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    std::fprintf(stderr, "usage: latency N M [--no-oracle] [--no-facade]\n");
+    std::fprintf(stderr, "usage: latency N M [--no-oracle] [--no-facade] [--serve]\n");
     return 2;
   }
   const uint32_t N = (uint32_t)std::atol(argv[1]);
   const uint32_t M = (uint32_t)std::atol(argv[2]);
-  bool oracle = true, facade = true;
+  bool oracle = true, facade = true, serve = false;
   for (int i = 3; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--serve")) serve = true;
     if (!std::strcmp(argv[i], "--no-oracle")) oracle = false;
     if (!std::strcmp(argv[i], "--no-facade")) facade = false;
   }
@@ -116,6 +120,7 @@ int main(int argc, char** argv) {
     dmc::GpuQueueOptions opts;
     opts.max_clients = N;
     opts.ring_capacity = 64;
+    opts.serve = serve;
     dmc::PullPriorityQueue<uint32_t, Req> pq(
         [&](const uint32_t& c) -> const dmc::ClientInfo* { return &ci[c]; },
         dmc::AtLimit::Wait, 0.0, opts);
@@ -154,6 +159,7 @@ int main(int argc, char** argv) {
       l[c] = infos[c].l;
     }
     dmc_client_register_batch(q, N, sl.data(), r.data(), w.data(), l.data(), 1);
+    if (serve) dmc_queue_set_option(q, DMC_OPT_SERVE, 1);
     std::vector<dmc_request> rq(N);
     for (uint32_t c = 0; c < N; ++c) rq[c] = dmc_request{c, 1, pre[c].t, 1, 1, c};
     for (uint32_t a = 0; a < N; a += 1u << 16) {
@@ -209,11 +215,11 @@ int main(int argc, char** argv) {
     dmo_queue_destroy(q);
   }
 
-  std::printf("{\"clients\": %u, \"rounds\": %u, \"facade_prepop_s\": %.3f, "
+  std::printf("{\"serve\": %s, \"clients\": %u, \"rounds\": %u, \"facade_prepop_s\": %.3f, "
               "\"oracle_prepop_s\": %.3f, \"facade_add_us\": %s, \"facade_pull_us\": %s, "
               "\"engine_add_us\": %s, \"engine_pull_us\": %s, \"oracle_add_us\": %s, "
               "\"oracle_pull_us\": %s}\n",
-              N, M, f_pre_s, o_pre_s, f_add.json().c_str(), f_pull.json().c_str(),
+              serve ? "true" : "false", N, M, f_pre_s, o_pre_s, f_add.json().c_str(), f_pull.json().c_str(),
               e_add.json().c_str(), e_pull.json().c_str(), o_add.json().c_str(),
               o_pull.json().c_str());
   return 0;

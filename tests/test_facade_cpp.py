@@ -31,3 +31,14 @@ def test_facade_gpu():
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failures" in out.stdout
+
+
+@pytest.mark.gpu
+def test_facade_gpu_serve():
+    """the same KATs with every facade queue on the serve path
+    (DMCLOCK_GPU_SERVE=1: DMC_OPT_SERVE, single calls answered by k_serve)"""
+    env = dict(os.environ, DMCLOCK_GPU_SERVE="1")
+    out = subprocess.run([_build()], capture_output=True, text=True, timeout=300, env=env)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 failures" in out.stdout

@@ -1,15 +1,17 @@
 """The single-op path (DMC_OPT_SINGLE_OP): host-API adds of one request of a
 non-idle client (one kernel, k_add_one) and pulls of k <= 8 (two kernels per
 pull_request, k_fast_decide / k_fast_apply, results in host-mapped memory)
--- the facade's per-call path -- against the oracle, and the general step
-path (option off) on the same traces.  Modes as the reference's
+-- the facade's per-call path -- against the oracle, the serve path
+(DMC_OPT_SERVE: the same calls answered by the persistent k_serve from
+per-group summaries) and the general step path (option off) on the same
+traces.  Modes as the reference's
 do_next_request branches (dmclock_server.h:1115-1200): AtLimit::Wait,
 AtLimit::Allow (limit breaks), delayed tags, non-monotone `now`."""
 import numpy as np
 import pytest
 
 from dmclock_amd import workloads
-from dmclock_amd._abi import AT_LIMIT_ALLOW, AT_LIMIT_WAIT, OPT_SINGLE_OP
+from dmclock_amd._abi import AT_LIMIT_ALLOW, AT_LIMIT_WAIT, OPT_SERVE, OPT_SINGLE_OP
 from parity import run_parity
 
 pytestmark = pytest.mark.gpu
@@ -22,7 +24,8 @@ def _mk(single_op):
     def mk(**kw):
         from dmclock_amd.gpu import GpuQueue
         q = GpuQueue(ring_capacity=64, **kw)
-        q.set_option(OPT_SINGLE_OP, int(single_op))
+        q.set_option(OPT_SINGLE_OP, int(bool(single_op)))
+        q.set_option(OPT_SERVE, int(single_op == "serve"))
         return q
     return mk
 
@@ -46,7 +49,7 @@ def _single_add_trace(seed, n, steps, delta_rho="random"):
     return tr
 
 
-@pytest.mark.parametrize("single_op", [True, False])
+@pytest.mark.parametrize("single_op", ["serve", True, False])
 @pytest.mark.parametrize("mode", range(len(MODES)))
 def test_single_op_parity(mode, single_op):
     tr = _single_add_trace(3 + mode, 512, 80)
@@ -54,4 +57,21 @@ def test_single_op_parity(mode, single_op):
     assert n > 250, n
     c = qg.counters()
     assert c["rounds"] == 0 and c["single_steps"] >= n, c
+    if single_op == "serve":
+        assert c["serve_calls"] > 500 and c["serve_launches"] >= 1, c
+    qg.close()
+
+
+@pytest.mark.parametrize("mode", range(len(MODES)))
+def test_serve_many_groups(mode):
+    """k_serve over 300,000 slots: 293 group summaries (the last one partial),
+    the limit scan's marks re-summarising only the stale groups; a run of
+    single adds and pulls between the trace's batch adds (each batch call
+    stops k_serve; the next single call rebuilds the summaries and
+    relaunches it)"""
+    tr = _single_add_trace(11 + mode, 300_000, 40)
+    n, qg, qo = run_parity(tr, _mk("serve"), queue_kw=MODES[mode], state_sample=4096)
+    assert n > 100, n
+    c = qg.counters()
+    assert c["serve_calls"] > 300 and c["serve_launches"] >= 1, c
     qg.close()
