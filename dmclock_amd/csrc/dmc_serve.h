@@ -78,6 +78,10 @@ template <int CTRL, int ROWS>
 __device__ __attribute__((always_inline)) inline uint32_t dpp32(uint32_t v, uint32_t idn) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)idn, (int)v, CTRL, ROWS, 0xf, false);
 }
+template <int C, int R>
+struct DppStep {
+  static constexpr int ctrl = C, rows = R;
+};
 template <int CTRL, int ROWS>
 __device__ __attribute__((always_inline)) inline void stepred_dpp_step(StepRed& a) {
   auto k64 = [](uint64_t v) {
@@ -107,19 +111,116 @@ __device__ __attribute__((always_inline)) inline void wave_stepred(StepRed& a) {
   stepred_dpp_step<0x143, 0xc>(a);  // row_bcast:31 into rows 2 and 3
 }
 
-// block-wide combine of per-thread StepReds into sh[kServeRes] (visible to
-// every thread on return; sh: kServeRes + 1 entries of LDS).  The result is
-// read from LDS: a StepRed held across the barriers would go to scratch.
-constexpr int kServeRes = kServeThreads / 64;
-__device__ __attribute__((always_inline)) inline void serve_block_reduce(StepRed a, StepRed* sh) {
-  wave_stepred(a);
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline uint64_t dpp64(uint64_t v, uint64_t idn) {
+  return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32), (uint32_t)(idn >> 32)) << 32) |
+         dpp32<CTRL, ROWS>((uint32_t)v, (uint32_t)idn);
+}
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline void argmin_dpp_step(ArgMin& a) {
+  const ArgMin b{dpp64<CTRL, ROWS>(a.key, kMaxKey), dpp32<CTRL, ROWS>(a.slot, kNone),
+                 dpp32<CTRL, ROWS>(a.cnt, 0u)};
+  a = argmin_combine(a, b);
+}
+__device__ __attribute__((always_inline)) inline void wave_argmin_dpp(ArgMin& a) {
+  argmin_dpp_step<0x111, 0xf>(a);
+  argmin_dpp_step<0x112, 0xf>(a);
+  argmin_dpp_step<0x114, 0xf>(a);
+  argmin_dpp_step<0x118, 0xf>(a);
+  argmin_dpp_step<0x142, 0xa>(a);
+  argmin_dpp_step<0x143, 0xc>(a);
+}
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline void minsum_dpp_step(uint64_t& m0, uint64_t& m1,
+                                                                       uint32_t& c0, uint32_t& c1,
+                                                                       uint32_t& c2) {
+  const uint64_t b0 = dpp64<CTRL, ROWS>(m0, kMaxKey), b1 = dpp64<CTRL, ROWS>(m1, kMaxKey);
+  m0 = b0 < m0 ? b0 : m0;
+  m1 = b1 < m1 ? b1 : m1;
+  c0 += dpp32<CTRL, ROWS>(c0, 0u);
+  c1 += dpp32<CTRL, ROWS>(c1, 0u);
+  c2 += dpp32<CTRL, ROWS>(c2, 0u);
+}
+
+// Block-wide combine of per-thread StepReds into *out (visible to every
+// thread on return): the 256 partials go to LDS and each wave reduces one
+// part of the record over all of them -- wave 0 the r argmin, wave 1 p,
+// wave 2 pnr, wave 3 the limit minima and the counts -- four short
+// reductions side by side instead of one long one per wave.
+constexpr int kServeRes = kServeThreads;  // the result's index in the LDS array
+__device__ __attribute__((always_inline)) inline void serve_block_reduce(const StepRed& a,
+                                                                         StepRed* part) {
+  StepRed* out = part + kServeRes;
+  static_assert(kServeThreads == 256, "one wave per part of the record");
   __syncthreads();  // (the previous result has been read)
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) sh[w] = a;
+  part[threadIdx.x] = a;
+  __syncthreads();
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < 3) {
+    auto f = [&](const StepRed& x) { return w == 0 ? x.r : w == 1 ? x.p : x.pnr; };
+    ArgMin m = f(part[lane]);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) m = argmin_combine(m, f(part[lane + 64 * j]));
+    wave_argmin_dpp(m);
+    if (lane == 63) {
+      if (w == 0) out->r = m;
+      else if (w == 1) out->p = m;
+      else out->pnr = m;
+    }
+  } else {
+    uint64_t m0 = kMaxKey, m1 = kMaxKey;
+    uint32_t c0 = 0, c1 = 0, c2 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const StepRed& x = part[lane + 64 * j];
+      m0 = x.lmin_nr < m0 ? x.lmin_nr : m0;
+      m1 = x.lmin_rd < m1 ? x.lmin_rd : m1;
+      c0 += x.n_any;
+      c1 += x.n_ready;
+      c2 += x.n_notready;
+    }
+    minsum_dpp_step<0x111, 0xf>(m0, m1, c0, c1, c2);
+    minsum_dpp_step<0x112, 0xf>(m0, m1, c0, c1, c2);
+    minsum_dpp_step<0x114, 0xf>(m0, m1, c0, c1, c2);
+    minsum_dpp_step<0x118, 0xf>(m0, m1, c0, c1, c2);
+    minsum_dpp_step<0x142, 0xa>(m0, m1, c0, c1, c2);
+    minsum_dpp_step<0x143, 0xc>(m0, m1, c0, c1, c2);
+    if (lane == 63) {
+      out->lmin_nr = m0;
+      out->lmin_rd = m1;
+      out->n_any = c0;
+      out->n_ready = c1;
+      out->n_notready = c2;
+      out->pad = 0;
+    }
+  }
+  __syncthreads();
+}
+
+// block-wide argmin into sha[0] (visible to every thread on return)
+__device__ __attribute__((always_inline)) inline void serve_block_argmin(ArgMin a, ArgMin* sha) {
+  auto step = [&](auto ctrl_rows) {
+    constexpr int CTRL = decltype(ctrl_rows)::ctrl, ROWS = decltype(ctrl_rows)::rows;
+    ArgMin b;
+    b.key = ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(a.key >> 32), 0xffffffffu) << 32) |
+            dpp32<CTRL, ROWS>((uint32_t)a.key, 0xffffffffu);
+    b.slot = dpp32<CTRL, ROWS>(a.slot, kNone);
+    b.cnt = dpp32<CTRL, ROWS>(a.cnt, 0u);
+    a = argmin_combine(a, b);
+  };
+  step(DppStep<0x111, 0xf>{});
+  step(DppStep<0x112, 0xf>{});
+  step(DppStep<0x114, 0xf>{});
+  step(DppStep<0x118, 0xf>{});
+  step(DppStep<0x142, 0xa>{});
+  step(DppStep<0x143, 0xc>{});
+  __syncthreads();  // (the previous result has been read)
+  if ((threadIdx.x & 63) == 63) sha[1 + (threadIdx.x >> 6)] = a;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < kServeRes; ++i) stepred_combine(sh[0], sh[i]);
-    sh[kServeRes] = sh[0];
+    ArgMin o = sha[1];
+    for (int i = 2; i <= kServeThreads / 64; ++i) o = argmin_combine(o, sha[i]);
+    sha[0] = o;
   }
   __syncthreads();
 }
@@ -146,7 +247,7 @@ __device__ __attribute__((always_inline)) inline void summary_add(StepRed& a, co
 // scan's ready marks for fronts with l <= now are committed first;
 // otherwise readiness is the flag alone.  The fronts are loaded kSumBatch
 // per lane before the first is used (one memory latency per batch).
-constexpr int kSumBatch = 8;
+constexpr int kSumBatch = 4;  // (1024-slot groups: one batch)
 template <bool MARK>
 __device__ __attribute__((always_inline)) inline void group_summary(const Table& tb, uint32_t g,
                                                                     uint32_t gshift, double now,
@@ -201,6 +302,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         uint64_t idle_ticks) {
   __shared__ StepRed sg[kServeMaxG];
   __shared__ StepRed sh[kServeRes + 1];
+  __shared__ ArgMin sha[kServeThreads / 64 + 1];
   __shared__ uint32_t s_nst;
   __shared__ uint16_t s_stale[kServeMaxG];
   __shared__ uint64_t s_cmd[8];  // the command line's words (s_cmd[0]: the op, 0 = stop)
@@ -272,15 +374,26 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       int32_t type = DMC_NEXT_RETURNING;
       double when = 0.0;
       while (n < s_k) {
-        const StepRed& o = sh[kServeRes];
-        serve_total(sg, G, sh);
+        // the reservation heap's top: the group argmin of the groups' r
+        // minima (lowest group on equal keys is the lowest slot; the tied
+        // fronts' count is the sum)
+        ArgMin ar{kMaxKey, kNone, 0};
+        for (uint32_t i = threadIdx.x; i < G; i += kServeThreads)
+          ar = argmin_combine(ar, ArgMin{sg[i].r.key, i, sg[i].r.cnt});
+        serve_block_argmin(ar, sha);
         if (threadIdx.x == 0 && n == 0) io->phase[0] = wall_clock64();
-        const bool rfires = o.n_any && from_okey(o.r.key) <= now;
-        if (!rfires && nregistered) {
+        StepCtl c{};
+        c.type = -1;
+        if (sha[0].key != kMaxKey && from_okey(sha[0].key) <= now) {
+          c.type = DMC_NEXT_RETURNING;  // :1124-1128
+          c.prio = 0;
+          c.slot = sg[sha[0].slot].r.slot;
+          c.tie = sha[0].cnt > 1;
+        } else if (nregistered) {
           // the limit scan: re-summarise the groups holding a not-ready
           // front whose limit has passed, committing its ready mark
           if (threadIdx.x == 0) s_nst = 0;
-          __syncthreads();  // (and every thread has read rfires)
+          __syncthreads();  // (and every thread has read the r top)
           for (uint32_t i = threadIdx.x; i < G; i += kServeThreads)
             if (sg[i].n_notready && from_okey(sg[i].lmin_nr) <= now)
               s_stale[atomicAdd(&s_nst, 1u)] = (uint16_t)i;
@@ -292,9 +405,23 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
             if (threadIdx.x == 0) sg[g] = sh[kServeRes];
           }
           __syncthreads();
-          if (nst) serve_total(sg, G, sh);
+          // the ready heap's top (:1146-1151)
+          ArgMin ap{kMaxKey, kNone, 0};
+          for (uint32_t i = threadIdx.x; i < G; i += kServeThreads)
+            ap = argmin_combine(ap, ArgMin{sg[i].p.key, i, sg[i].p.cnt});
+          serve_block_argmin(ap, sha);
+          if (sha[0].key != kMaxKey) {
+            c.type = DMC_NEXT_RETURNING;
+            c.prio = 1;
+            c.mark = 1;
+            c.slot = sg[sha[0].slot].p.slot;
+            c.tie = sha[0].cnt > 1;
+          }
         }
-        const StepCtl c = step_decision(o, now, at_limit, nregistered);
+        if (c.type < 0) {  // no work now: the full reduction decides
+          serve_total(sg, G, sh);
+          c = step_decision(sh[kServeRes], now, at_limit, nregistered);
+        }
         if (c.type != DMC_NEXT_RETURNING) {
           type = c.type;
           when = c.when;
@@ -306,8 +433,9 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
           if (n == 0) io->phase[1] = wall_clock64();
         }
         __syncthreads();
-        group_summary<false>(tb, c.slot >> gshift, gshift, now, sh);
-        if (threadIdx.x == 0) sg[c.slot >> gshift] = sh[kServeRes];
+        const uint32_t g = c.slot >> gshift;
+        group_summary<false>(tb, g, gshift, now, sh);
+        if (threadIdx.x == 0) sg[g] = sh[kServeRes];
         if (threadIdx.x == 0 && n == 0) io->phase[2] = wall_clock64();
         __syncthreads();
         ++n;

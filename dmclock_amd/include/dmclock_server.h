@@ -96,7 +96,8 @@ struct GpuQueueOptions {
   int device = 0;
   // single add_request / pull_request calls answered by the engine's
   // persistent serve kernel (DMC_OPT_SERVE): no kernel launch per call
-  bool serve = false;
+  // (DMCLOCK_GPU_SERVE=0: the single-op kernels)
+  bool serve = true;
   static GpuQueueOptions from_env() {
     GpuQueueOptions o;
     if (const char* s = std::getenv("DMCLOCK_GPU_MAX_CLIENTS")) o.max_clients = std::atoi(s);

@@ -1,7 +1,8 @@
 """Runs the C++ facade test (tests/cpp/test_facade.cc): the reference's KATs
 written against the drop-in crimson::dmclock API of
 dmclock_amd/include/dmclock_server.h.  On CPU only the host-side tracker
-tests run; with a GPU, every server KAT runs through the engine."""
+tests run; with a GPU, every server KAT runs through the engine, with the
+facade's default serve kernel (DMC_OPT_SERVE) and with it off."""
 import os
 import subprocess
 
@@ -34,10 +35,10 @@ def test_facade_gpu():
 
 
 @pytest.mark.gpu
-def test_facade_gpu_serve():
-    """the same KATs with every facade queue on the serve path
-    (DMCLOCK_GPU_SERVE=1: DMC_OPT_SERVE, single calls answered by k_serve)"""
-    env = dict(os.environ, DMCLOCK_GPU_SERVE="1")
+def test_facade_gpu_kernels():
+    """the same KATs with the facade's serve kernel off (DMCLOCK_GPU_SERVE=0:
+    every single call launches the single-op kernels)"""
+    env = dict(os.environ, DMCLOCK_GPU_SERVE="0")
     out = subprocess.run([_build()], capture_output=True, text=True, timeout=300, env=env)
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
