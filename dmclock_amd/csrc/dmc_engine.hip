@@ -2851,6 +2851,10 @@ int serve_start(dmc_queue* q, uint64_t seq0) {
 // just before the post is relaunched to take the posted command.
 int serve_call(dmc_queue* q) {
   ServeIO* io = q->h_serve;
+  if (q->serving && __atomic_load_n(&io->state, __ATOMIC_ACQUIRE) == kServeExited) {
+    HIP_OK(hipStreamSynchronize(q->stream));  // (it idled out or its lifetime ended)
+    q->serving = false;
+  }
   if (!q->serving) {
     int rc = serve_start(q, q->serve_seq);
     if (rc) return rc;

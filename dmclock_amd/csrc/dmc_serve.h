@@ -17,8 +17,11 @@
 // step_decision's, the pop step_apply_body's, the add add_chain_slot's: the
 // same arithmetic as every other path.
 //
-// Exit conditions every wave reaches: a stop command, or no command for
-// `idle_ticks` of the 100 MHz wall clock (the host relaunches on demand).
+// Exit conditions every wave reaches: a stop command, no command for
+// `idle_ticks` of the 100 MHz wall clock, or, after an answer, a lifetime of
+// 5 x `idle_ticks` (the host relaunches on demand).  The lifetime bounds how
+// long a queue's k_serve can hold a hardware queue that another queue's
+// k_serve waits behind (more queues than hardware queues in a process).
 // The summaries are written back to HBM at exit (valid until any other call
 // changes the table; the host then rebuilds them with k_gsum_build).
 #pragma once
@@ -310,6 +313,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
   __shared__ StepCtl s_c;
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) sg[i] = gs[i];
   uint64_t seen = seq0;  // (wave 0's)
+  const uint64_t born = wall_clock64();
   uint64_t c_seen = 0, c_read = 0;
   __syncthreads();
   for (;;) {
@@ -458,7 +462,10 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       io->clk[3] = wall_clock64();
       __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_cmd[0] = wall_clock64() - born > 5 * idle_ticks ? kServeStop : kServeNone;
     }
+    __syncthreads();
+    if (s_cmd[0] == kServeStop) break;  // lifetime over
   }
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) gs[i] = sg[i];
   __syncthreads();

@@ -75,3 +75,47 @@ def test_serve_many_groups(mode):
     c = qg.counters()
     assert c["serve_calls"] > 300 and c["serve_launches"] >= 1, c
     qg.close()
+
+
+def test_serve_concurrent_queues():
+    """six queues on the serve path driven from six host threads at once:
+    more k_serve kernels than the process's hardware queues (4), so some
+    wait behind others; each one's lifetime lets them through.  Every add
+    status and decision of every queue against the oracle."""
+    import threading
+
+    import pyoracle
+    from parity import compare_decisions
+    traces = [_single_add_trace(21 + i, 2000, 30) for i in range(6)]
+    want = []
+    for tr in traces:
+        qo = pyoracle.OracleQueue(**MODES[0])
+        want.append(workloads.replay(qo, tr))
+        assert qo.ties == 0
+    qs = [_mk("serve")(max_clients=2000, **MODES[0]) for _ in traces]
+    got, errs = [None] * len(qs), []
+
+    def drive(i):
+        try:
+            got[i] = workloads.replay(qs[i], traces[i])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = [threading.Thread(target=drive, args=(i,)) for i in range(len(qs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert len(g) == len(w)
+        for j, (a, b) in enumerate(zip(g, w)):
+            assert a[0] == b[0]
+            if a[0] == "add":
+                assert np.array_equal(a[1], b[1]), (i, j)
+            elif a[0] == "pull":
+                compare_decisions(a[1], b[1], f"queue {i} op {j}")
+                assert a[2] == b[2], (i, j, a[2], b[2])
+        c = qs[i].counters()
+        assert c["serve_calls"] > 500, c
+        qs[i].close()
