@@ -2697,7 +2697,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = f
 // all (and none predicts all: the R-eligible slots are few); P: none
 // predicts nothing (no prediction).
 bool predict(dmc_queue* q, uint32_t kk, bool radix, bool brk, uint64_t pT[2]) {
-  if (!q->pred_on || q->pred_skip || radix || brk || !use_sample(q, radix) ||
+  if (kScanPerEmit != 4 || !q->pred_on || q->pred_skip || radix || brk || !use_sample(q, radix) ||
       q->thrN == 0 || q->thrK != kk)
     return false;
   for (int p = 0; p < 2; ++p) {

@@ -1384,6 +1384,9 @@ constexpr int kEmitStageLanes = kEmitStageThreads / (kEmitThreads / 64);
 // (PRED: the slots come from the four k_rscan blocks' lists of this block's
 // chunk, at most 2 x kEmitThreads entries: two per thread)
 constexpr uint32_t kScanPerEmit = kEmitChunk / kScanBlock;
+// (the host's grids, the apply blocks and the candidate buffers assume this
+// chunk: 2048-slot emit blocks ran slower, and 1024-slot ones faulted)
+static_assert(kEmitChunk == 4096, "emit blocks of 4096 slots");
 template <bool BRK, bool PRED>
 __global__ void __launch_bounds__(kEmitThreads)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
@@ -1423,12 +1426,12 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   // PRED: the list's segment sizes (the four scan blocks), the entries'
   // slots, and whether a list overflowed
-  uint32_t seg[kScanPerEmit];
+  uint32_t seg[4] = {0, 0, 0, 0};
   uint32_t sl[2] = {0, 0};
   uint32_t nent = 0;
   // list entry e of this block: (segment, offset) by the segment sizes
   // (static indices only: seg[] stays in registers)
-  static_assert(kScanPerEmit == 4, "four scan blocks per emit block");
+  // (four scan blocks per emit block; the host predicts only then)
   auto ent_at = [&](uint32_t e) -> const ScanEnt& {
     uint32_t sg = 0;
     if (e >= seg[0]) {

@@ -16,7 +16,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "dmclock_amd", "libdmclock_gpu.so")
+LIB = os.environ.get("DMC_LIB") or os.path.join(ROOT, "dmclock_amd", "libdmclock_gpu.so")
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 
