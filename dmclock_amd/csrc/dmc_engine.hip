@@ -1710,8 +1710,14 @@ struct dmc_queue {
 void serve_quiesce(dmc_queue* q) {
   q->gsum_valid = false;
   if (!q->serving) return;
-  q->h_serve->op = kServeStop;
-  __atomic_store_n(&q->h_serve->req_seq, ++q->serve_seq, __ATOMIC_RELEASE);
+  {  // the stop command
+    ServeIO* io = q->h_serve;
+    const uint64_t seq = ++q->serve_seq;
+    io->now = 0.0;
+    std::memset((void*)&io->req, 0, sizeof(io->req));
+    io->cmd = (uint64_t)kServeStop | (serve_check(seq, kServeStop, 0, 0, 0, 0, 0) << 16);
+    __atomic_store_n(&io->req_seq, seq, __ATOMIC_RELEASE);
+  }
   (void)hipStreamSynchronize(q->stream);
   q->serving = false;
 }
@@ -2836,7 +2842,7 @@ int serve_start(dmc_queue* q, uint64_t seq0) {
   __atomic_store_n(&q->h_serve->state, (uint32_t)kServeRunning, __ATOMIC_RELEASE);
   hipLaunchKernelGGL(k_serve, dim3(1), dim3(kServeThreads), 0, q->stream, q->tb, q->gsum,
                      q->ngroups, q->gshift, q->d_serve, q->p.at_limit, q->n_registered,
-                     q->sched, seq0, q->serve_idle_ticks);
+                     q->sched, seq0, q->serve_idle_ticks, q->tick);
   if (hipGetLastError() != hipSuccess) {
     q->gsum_valid = false;
     return DMC_EDEVICE;
@@ -2849,7 +2855,7 @@ int serve_start(dmc_queue* q, uint64_t seq0) {
 // One command to k_serve (the command fields already written): launch it if
 // it is not running, post, and wait for the answer.  A kernel that idled out
 // just before the post is relaunched to take the posted command.
-int serve_call(dmc_queue* q) {
+int serve_call(dmc_queue* q, uint32_t op, uint32_t k) {
   ServeIO* io = q->h_serve;
   if (q->serving && __atomic_load_n(&io->state, __ATOMIC_ACQUIRE) == kServeExited) {
     HIP_OK(hipStreamSynchronize(q->stream));  // (it idled out or its lifetime ended)
@@ -2860,6 +2866,11 @@ int serve_call(dmc_queue* q) {
     if (rc) return rc;
   }
   const uint64_t seq = ++q->serve_seq;
+  uint64_t rw[4];
+  std::memcpy(rw, (const void*)&io->req, sizeof(rw));
+  const uint64_t opk = (uint64_t)op | ((uint64_t)k << 8);
+  io->cmd = opk | (serve_check(seq, opk, __builtin_bit_cast(uint64_t, io->now), rw[0], rw[1],
+                               rw[2], rw[3]) << 16);
   __atomic_store_n(&io->req_seq, seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; ++spin) {
@@ -2886,10 +2897,10 @@ int serve_call(dmc_queue* q) {
     q->serve_tr[2] += (double)(io->clk[3] - io->clk[2]);
     q->serve_tr[3] += std::chrono::duration<double, std::nano>(
                           std::chrono::steady_clock::now() - t0).count();
-    double* ph = q->serve_ph[io->op == kServePull ? 1 : 0];
+    double* ph = q->serve_ph[op == kServePull ? 1 : 0];
     ph[0] += (double)(io->phase[0] - io->clk[1]);
     ph[1] += (double)(io->phase[1] - io->phase[0]);
-    ph[2] += (double)(io->phase[2] - (io->op == kServePull ? io->phase[1] : io->phase[0]));
+    ph[2] += (double)(io->phase[2] - (op == kServePull ? io->phase[1] : io->phase[0]));
     ph[3] += 1;
     q->serve_tr[2] += 0;  // (publish stamp unused: the fence is not observable)
     q->serve_mhz += 100.0 * (double)(io->cyc[1] - io->cyc[0]) /
@@ -2905,10 +2916,9 @@ bool serve_add_ok(const dmc_queue* q, const dmc_request& r) {
 
 int serve_add(dmc_queue* q, const dmc_request& r, int32_t* rc_out) {
   ServeIO* io = q->h_serve;
-  io->op = kServeAdd;
-  io->tick = q->tick;
+  io->now = 0.0;
   io->req = r;
-  int rc = serve_call(q);
+  int rc = serve_call(q, kServeAdd, 0);
   if (rc) return rc;
   q->tick += 1;
   if (rc_out) rc_out[0] = io->rc;
@@ -2918,11 +2928,9 @@ int serve_add(dmc_queue* q, const dmc_request& r, int32_t* rc_out) {
 int serve_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
                dmc_pull_result* res) {
   ServeIO* io = q->h_serve;
-  io->op = kServePull;
-  io->k = k;
   io->now = now;
-  io->tick = q->tick;
-  int rc = serve_call(q);
+  std::memset((void*)&io->req, 0, sizeof(io->req));
+  int rc = serve_call(q, kServePull, k);
   if (rc) return rc;
   dmc_pull_result r{};
   r.n_decisions = io->n;

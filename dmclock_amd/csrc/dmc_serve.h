@@ -31,15 +31,20 @@ constexpr uint32_t kServeMaxG = 1024;
 enum : uint32_t { kServeNone = 0, kServeAdd = 1, kServePull = 2, kServeStop = 3 };
 enum : uint32_t { kServeRunning = 1, kServeExited = 2 };
 
-// Host-mapped command block.  The host writes the command fields, then
-// req_seq (release); the kernel answers in the second cache line, then
-// done_seq (system-scope release).
+// Host-mapped command block.  The command is words 0-6 of one 64-byte line:
+// the sequence number, op | k << 8 | check << 16, now, the request.  The
+// host writes words 1-6, then the sequence number (release); k_serve reads
+// all seven words with one load per poll (a lane each) and takes a new
+// sequence number only with a matching check, a 48-bit hash of the other
+// words (a read torn by the host's stores fails it and is polled again).
+// The answer is in the second line, then done_seq (system-scope release).
+// The tick (:918) is k_serve's own: the launch's, plus one per add.
 struct alignas(64) ServeIO {
-  uint64_t req_seq;  // word 0; the command in words 1..7
-  uint32_t op, k;
+  uint64_t req_seq;
+  uint64_t cmd;
   double now;
-  uint64_t tick;
   dmc_request req;
+  uint64_t pad0;
   // device -> host
   alignas(64) uint64_t done_seq;
   uint32_t state;
@@ -53,7 +58,22 @@ struct alignas(64) ServeIO {
   dmc_decision dec[kFastK];
 };
 static_assert(offsetof(ServeIO, done_seq) == 64, "the command is one 64-byte line");
+static_assert(sizeof(dmc_request) == 32, "the request is words 3-6");
 constexpr int kServeCmdWords = 7;
+
+// the command's check: a hash of its sequence number, op, k, now and request
+__host__ __device__ inline uint64_t serve_check(uint64_t seq, uint64_t opk, uint64_t now,
+                                                uint64_t r0, uint64_t r1, uint64_t r2,
+                                                uint64_t r3) {
+  uint64_t h = seq * 0x9E3779B97F4A7C15ull;
+  const uint64_t w[6] = {opk & 0xffffull, now, r0, r1, r2, r3};
+  for (int i = 0; i < 6; ++i) {
+    h ^= w[i];
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
+  }
+  return h >> 16;  // 48 bits
+}
 
 __device__ inline uint64_t sys_load_u64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -302,13 +322,14 @@ __device__ __attribute__((always_inline)) inline void serve_total(const StepRed*
 __global__ void __launch_bounds__(kServeThreads)
 k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_limit,
         uint32_t nregistered, unsigned long long* sched, uint64_t seq0,
-        uint64_t idle_ticks) {
+        uint64_t idle_ticks, uint64_t tick) {
   __shared__ StepRed sg[kServeMaxG];
   __shared__ StepRed sh[kServeRes + 1];
   __shared__ ArgMin sha[kServeThreads / 64 + 1];
   __shared__ uint32_t s_nst;
   __shared__ uint16_t s_stale[kServeMaxG];
-  __shared__ uint64_t s_cmd[8];  // the command line's words (s_cmd[0]: the op, 0 = stop)
+  __shared__ uint64_t s_cmd[8];  // the command line's words (op 0: exit)
+  __shared__ uint32_t s_life;
   __shared__ int32_t s_rc;
   __shared__ StepCtl s_c;
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) sg[i] = gs[i];
@@ -317,40 +338,41 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
   uint64_t c_seen = 0, c_read = 0;
   __syncthreads();
   for (;;) {
-    if (threadIdx.x < 64) {  // wave 0 polls: one request per poll
+    if (threadIdx.x < 64) {  // wave 0 polls: the command line, one load per poll
+      const uint32_t lane = threadIdx.x;
       const uint64_t t0 = wall_clock64();
+      const uint64_t* line = reinterpret_cast<const uint64_t*>(io);
       bool got = false;
+      uint64_t w = 0;
       for (;;) {
-        const uint64_t sq = __hip_atomic_load(&io->req_seq, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        w = lane < kServeCmdWords ? sys_load_u64(line + lane) : 0;
+        const uint64_t sq = shfl_u64(w, 0);
         if (sq != seen) {
-          seen = sq;
-          got = true;
-          break;
+          const uint64_t opk = shfl_u64(w, 1);
+          if ((opk >> 16) == serve_check(sq, opk, shfl_u64(w, 2), shfl_u64(w, 3),
+                                         shfl_u64(w, 4), shfl_u64(w, 5), shfl_u64(w, 6))) {
+            seen = sq;
+            got = true;
+            break;
+          }
         }
         if (wall_clock64() - t0 > idle_ticks) break;
         __builtin_amdgcn_s_sleep(1);
       }
       c_seen = wall_clock64();
-      uint64_t w = 0;
-      if (got) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        // the command's words in one round trip (a lane each)
-        const uint32_t lane = threadIdx.x;
-        if (lane < kServeCmdWords)
-          w = sys_load_u64(reinterpret_cast<const uint64_t*>(io) + 1 + lane);
-      }
-      if (threadIdx.x < kServeCmdWords) s_cmd[threadIdx.x] = w;
-      c_read = wall_clock64();
-      if (threadIdx.x == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
+      if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (lane < kServeCmdWords) s_cmd[lane] = got ? w : 0;
+      c_read = c_seen;
+      if (lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
-    const uint32_t op = (uint32_t)s_cmd[0];
+    const uint32_t op = (uint32_t)(s_cmd[1] & 0xff);
     if (op != kServeAdd && op != kServePull) break;
-    const uint32_t s_k = (uint32_t)(s_cmd[0] >> 32);
-    const double s_now = __builtin_bit_cast(double, s_cmd[1]);
-    const uint64_t s_tick = s_cmd[2];
+    const uint32_t s_k = (uint32_t)((s_cmd[1] >> 8) & 0xff);
+    const double s_now = __builtin_bit_cast(double, s_cmd[2]);
+    const uint64_t s_tick = tick;
     const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
+    if (op == kServeAdd) ++tick;  // (++tick, :918: the host's count follows)
     const double now = s_now;
     if (op == kServeAdd) {  // k_add_one
       // a request for a client with no request is its new front: inserted
@@ -462,10 +484,10 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       io->clk[3] = wall_clock64();
       __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      s_cmd[0] = wall_clock64() - born > 5 * idle_ticks ? kServeStop : kServeNone;
+      s_life = wall_clock64() - born > 5 * idle_ticks;
     }
     __syncthreads();
-    if (s_cmd[0] == kServeStop) break;  // lifetime over
+    if (s_life) break;  // lifetime over
   }
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) gs[i] = sg[i];
   __syncthreads();
