@@ -1705,6 +1705,51 @@ constexpr int kDeepBatch = 8;   // queued requests reduced per batch of loads
 // precomputed state); a slow record's pop is stamped into its ring entry.
 // (Storing the fast candidates' state here instead, in the rank lanes, was
 // measured slower: rank 9.8 -> 21.2 us for apply 11.5 -> 6.3, §10.)
+// A ranked record's stores: its decision offset goff (the group sizes of
+// the bin's records before it plus the bin's offset), stamped or written.
+__device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_t cost,
+                                 uint64_t handle, double tr, double tp, double tl,
+                                 uint32_t rank, uint32_t gl, uint32_t tie, bool isp, uint32_t k,
+                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
+                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
+  uint32_t goff = soff + gl;
+  uint32_t size = isp ? 1u + me.run : 1u;
+  if (goff < k) {
+    if ((ci & kFastRec) && goff + size > k) {
+      // a fast group cut by the round's end: k_rapply re-walks it
+      ring[me.ridx].dec = goff;
+      ring[me.ridx].tie = tie;
+      decof[ci & ~kFastRec] = kSlowCand;
+    } else if (ci & kFastRec) {
+      // a fast record: its first pop's decision, and its offset for
+      // k_rapply (which writes the run's pop and the candidate's state)
+      dmc_decision d;
+      d.handle = handle;
+      d.tag_r = tr;
+      d.tag_p = tp;
+      d.tag_l = tl;
+      d.slot = me.slot;
+      d.cost = cost;
+      d.phase = isp ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+      d.flags = tie;
+      out[goff] = d;
+      decof[ci & ~kFastRec] = goff;
+    } else {
+      ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
+      ring[me.ridx].tie = tie;
+    }
+    if (isp) {
+      uint32_t prank = poff + rank;  // among P groups
+      if (goff + size >= k || prank == n_pgroups - 1) {
+        // the last applied group: its priority pop is the round's last
+        // limit-scanning pull
+        rd->g_last = goff;
+        rd->n_prio = prank + 1;
+      }
+    }
+  }
+}
+
 __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
                                 uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, bool isp, uint32_t k,
@@ -1745,44 +1790,9 @@ __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uin
     gl += __shfl_xor(gl, d);
     tie |= __shfl_xor(tie, d);
   }
-  if (valid && part == 0) {
-    uint32_t goff = soff + gl;
-    uint32_t size = isp ? 1u + me.run : 1u;
-    if (goff < k) {
-      if ((ci & kFastRec) && goff + size > k) {
-        // a fast group cut by the round's end: k_rapply re-walks it
-        ring[me.ridx].dec = goff;
-        ring[me.ridx].tie = tie;
-        decof[ci & ~kFastRec] = kSlowCand;
-      } else if (ci & kFastRec) {
-        // a fast record: its first pop's decision, and its offset for
-        // k_rapply (which writes the run's pop and the candidate's state)
-        dmc_decision d;
-        d.handle = handle;
-        d.tag_r = tr;
-        d.tag_p = tp;
-        d.tag_l = tl;
-        d.slot = me.slot;
-        d.cost = cost;
-        d.phase = isp ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
-        d.flags = tie;
-        out[goff] = d;
-        decof[ci & ~kFastRec] = goff;
-      } else {
-        ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
-        ring[me.ridx].tie = tie;
-      }
-      if (isp) {
-        uint32_t prank = poff + rank;  // among P groups
-        if (goff + size >= k || prank == n_pgroups - 1) {
-          // the last applied group: its priority pop is the round's last
-          // limit-scanning pull
-          rd->g_last = goff;
-          rd->n_prio = prank + 1;
-        }
-      }
-    }
-  }
+  if (valid && part == 0)
+    place_rec(rd, me, ci, cost, handle, tr, tp, tl, rank, gl, tie, isp, k, n_pgroups, soff,
+              poff, ring, out, decof);
 }
 
 // One block per rank bin.  The bin's order keys are staged in LDS; each
@@ -1797,6 +1807,79 @@ __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uin
 // records take consecutive decision offsets, so fast records' decision
 // stores from one block fill one stretch of the decision array.
 constexpr int kRankBlocksR = kNBR;
+
+// A bin of more than kRankSortMin records (skewed keys: config 4's activated
+// clients emit several P groups each) is sorted instead: a bitonic sort of
+// the record indices by the same order (okey, slot, queue position) in LDS,
+// one compare-exchange per thread per step (45 steps for 512), then the
+// group offsets by a block scan of the sizes in sorted order, and a tie
+// where the record's run of equal keys holds another slot.  Counting costs
+// cnt^2 / 256 compare steps per lane: 973 for a full bin.
+constexpr uint32_t kRankSortMin = 192;
+__device__ inline bool bkey_less(const BKey& x, const BKey& y) {
+  return x.okey < y.okey ||
+         (x.okey == y.okey && (x.slot < y.slot || (x.slot == y.slot && x.seq < y.seq)));
+}
+__device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
+                                   bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
+                                   uint32_t poff, ReqEntry* ring, dmc_decision* out,
+                                   uint32_t* decof) {
+  static_assert(kBinCapR == 2 * kBlockR, "two records per thread");
+  __shared__ uint16_t ord[kBinCapR];
+  __shared__ uint32_t wsum[kBlockR / 64];
+  const uint32_t t = threadIdx.x;
+  uint32_t P = 2;
+  while (P < cnt) P <<= 1;
+  for (uint32_t i = t; i < P; i += kBlockR) ord[i] = (uint16_t)i;
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i | j;
+      if (l < P) {
+        const uint32_t a = ord[i], c = ord[l];
+        // indices >= cnt (padding) order after every record
+        const bool c_lt_a = c < cnt && (a >= cnt || bkey_less(sh[c], sh[a]));
+        const bool a_lt_c = a < cnt && (c >= cnt || bkey_less(sh[a], sh[c]));
+        if ((i & kk) == 0 ? c_lt_a : a_lt_c) {
+          ord[i] = (uint16_t)c;
+          ord[l] = (uint16_t)a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // positions 2t, 2t + 1: their records, sizes, and the exclusive prefix
+  const uint32_t r0 = 2 * t, r1 = r0 + 1;
+  const uint32_t i0 = r0 < cnt ? ord[r0] : 0u, i1 = r1 < cnt ? ord[r1] : 0u;
+  const uint32_t z0 = r0 < cnt ? (isp ? 1u + sh[i0].run : 1u) : 0u;
+  const uint32_t z1 = r1 < cnt ? (isp ? 1u + sh[i1].run : 1u) : 0u;
+  const uint32_t lane = t & 63, w = t >> 6;
+  uint32_t incl = z0 + z1;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
+  const uint32_t ex = pre + incl - (z0 + z1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t r = h ? r1 : r0;
+    if (r >= cnt) continue;
+    const uint32_t i = h ? i1 : i0;
+    const BKey me = sh[i];
+    uint32_t tie = 0;
+    for (uint32_t q = r; q > 0 && sh[ord[q - 1]].okey == me.okey; --q)
+      tie |= sh[ord[q - 1]].slot != me.slot;
+    for (uint32_t q = r + 1; q < cnt && sh[ord[q]].okey == me.okey; ++q)
+      tie |= sh[ord[q]].slot != me.slot;
+    const BRecR& x = src[i];
+    place_rec(rd, me, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, h ? ex + z0 : ex, tie, isp, k,
+              n_pgroups, soff, poff, ring, out, decof);
+  }
+}
 
 // A sampled round whose thresholds admitted fewer first keys than needed
 // (k_remit's exact counts): it is re-run with the exact histogram (nothing
@@ -1885,6 +1968,14 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   if (cnt == 0 || fail) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
   for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
+  if (cnt > kRankSortMin) {
+    rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof);
+    if (wtime && threadIdx.x == 0) {
+      wtime[2 * b] = t0;
+      wtime[2 * b + 1] = wall_clock64();
+    }
+    return;
+  }
   uint32_t parts = 1;
   while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
   const uint32_t per = (cnt + parts - 1) / parts;
