@@ -329,8 +329,9 @@ __global__ void k_act_inputs(const AddParams* pblk, Table tb, ActBuf act,
   }
 }
 
-// The batch positions' scans of the activation bookkeeping, in three
-// launches (dmc_sort.h's scan scheme, fused over the three arrays): pre =
+// The batch positions' scans of the activation bookkeeping, in two launches
+// (tile totals, then each tile's scan with its carry-in from the totals
+// before it, fused over the three arrays): pre =
 // exclusive prefix minima of cnew, suf = exclusive prefix minima of cold
 // (stored in reversed position order: suffix minima), and, for activations
 // the device detected (act.flag), the flagged positions compacted into idx,
@@ -364,25 +365,6 @@ k_act_scan_reduce(ActBuf act, uint32_t n, ActScanPart* parts) {
   if (threadIdx.x == 0) parts[blockIdx.x] = ActScanPart{ta, tb, tc, 0};
 }
 
-__global__ void __launch_bounds__(kScT) k_act_scan_top(ActScanPart* parts, uint32_t np) {
-  __shared__ uint64_t w64[kScT / 64];
-  __shared__ uint32_t w32[kScT / 64];
-  uint64_t ca = kMaxKey, cb = kMaxKey;
-  uint32_t cc = 0;
-  for (uint32_t c0 = 0; c0 < np; c0 += kScT) {
-    const uint32_t i = c0 + threadIdx.x;
-    const ActScanPart v = i < np ? parts[i] : ActScanPart{kMaxKey, kMaxKey, 0, 0};
-    uint64_t ta, tb;
-    uint32_t tc;
-    const uint64_t ea = block_excl<MinU64>(v.mn, w64, &ta);
-    const uint64_t eb = block_excl<MinU64>(v.mo, w64, &tb);
-    const uint32_t ec = block_excl<SumU32>(v.c, w32, &tc);
-    if (i < np) parts[i] = ActScanPart{MinU64::op(ca, ea), MinU64::op(cb, eb), cc + ec, 0};
-    ca = MinU64::op(ca, ta);
-    cb = MinU64::op(cb, tb);
-    cc += tc;
-  }
-}
 
 __global__ void __launch_bounds__(kScT)
 k_act_scan_down(ActBuf act, uint32_t n, const ActScanPart* parts, uint32_t* idx,
@@ -415,7 +397,39 @@ k_act_scan_down(ActBuf act, uint32_t n, const ActScanPart* parts, uint32_t* idx,
     b = MinU64::op(b, tb[l]);
     c += tc[l];
   }
-  const ActScanPart cin = parts[blockIdx.x];
+  // the carry-in: the tile totals of the blocks before this one (k_act_scan_
+  // reduce's), combined here by every block (no separate top-level launch)
+  ActScanPart cin;
+  {
+    uint64_t ma = kMaxKey, mb = kMaxKey;
+    uint32_t mc = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kScT) {
+      const ActScanPart v = parts[i];
+      ma = MinU64::op(ma, v.mn);
+      mb = MinU64::op(mb, v.mo);
+      mc += v.c;
+    }
+    ma = wave_min_u64(ma);
+    mb = wave_min_u64(mb);
+    mc = wave_sum_u32(mc);
+    if ((threadIdx.x & 63) == 0) {
+      w64[threadIdx.x >> 6] = ma;
+      w32[threadIdx.x >> 6] = mc;
+    }
+    __syncthreads();
+    cin.mn = w64[0];
+    cin.c = w32[0];
+    for (int i = 1; i < kScT / 64; ++i) {
+      cin.mn = MinU64::op(cin.mn, w64[i]);
+      cin.c += w32[i];
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) w64[threadIdx.x >> 6] = mb;
+    __syncthreads();
+    cin.mo = w64[0];
+    for (int i = 1; i < kScT / 64; ++i) cin.mo = MinU64::op(cin.mo, w64[i]);
+    __syncthreads();  // (w64 is reused by the scans below)
+  }
   uint32_t tot;
   const uint64_t ea = MinU64::op(cin.mn, block_excl<MinU64>(a, w64));
   const uint64_t eb = MinU64::op(cin.mo, block_excl<MinU64>(b, w64));
@@ -2218,12 +2232,11 @@ void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
 }
 
 // the activation bookkeeping's scans (and, flagged, the compaction) of an
-// n-position batch: three launches
+// n-position batch: two launches
 void act_scans(dmc_queue* q, const ActBuf& act, uint32_t n, bool flagged) {
   const uint32_t nb = scan_tiles(n);
   hipLaunchKernelGGL(k_act_scan_reduce, dim3(nb), dim3(kScT), 0, q->stream, act, n,
                      q->act_sparts);
-  hipLaunchKernelGGL(k_act_scan_top, dim3(1), dim3(kScT), 0, q->stream, q->act_sparts, nb);
   hipLaunchKernelGGL(k_act_scan_down, dim3(nb), dim3(kScT), 0, q->stream, act, n,
                      (const ActScanPart*)q->act_sparts, flagged ? q->act_idx : nullptr,
                      flagged ? q->act_dm : nullptr);
