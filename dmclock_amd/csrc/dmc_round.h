@@ -1815,7 +1815,10 @@ constexpr int kRankBlocksR = kNBR;
 // group offsets by a block scan of the sizes in sorted order, and a tie
 // where the record's run of equal keys holds another slot.  Counting costs
 // cnt^2 / 256 compare steps per lane: 973 for a full bin.
-constexpr uint32_t kRankSortMin = 192;
+#ifndef DMC_RANK_SORT_MIN
+#define DMC_RANK_SORT_MIN 192
+#endif
+constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
 __device__ inline bool bkey_less(const BKey& x, const BKey& y) {
   return x.okey < y.okey ||
          (x.okey == y.okey && (x.slot < y.slot || (x.slot == y.slot && x.seq < y.seq)));
