@@ -252,13 +252,27 @@ __global__ void k_activate(Table tb, uint32_t s, double t, const uint64_t* parts
 // not change: registered, non-idle, and not (empty and touched by the batch).
 __global__ void k_act_base(Table tb, uint64_t* parts) {
   uint64_t m = kMaxKey;
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < tb.n;
-       s += gridDim.x * blockDim.x) {
-    const ScanRec r = tb.sc[s];
-    if ((r.flags & F_REG) && !(r.flags & F_IDLE)) {
-      if (r.count == 0 && r.nadd) continue;  // changes inside the batch: positions
-      uint64_t k = okey(r.count ? r.pk : __dadd_rn(tb.rec[s].prev_p, tb.rec[s].pd));
-      m = k < m ? k : m;
+  // kBaseUnroll records per thread in flight before the first is used
+  constexpr int kBaseUnroll = 4;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t s0 = blockIdx.x * blockDim.x + threadIdx.x; s0 < tb.n;
+       s0 += kBaseUnroll * stride) {
+    ScanRec rs[kBaseUnroll];
+#pragma unroll
+    for (int u = 0; u < kBaseUnroll; ++u) {
+      const uint32_t s = s0 + u * stride;
+      if (s < tb.n) rs[u] = tb.sc[s];
+      else rs[u].flags = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kBaseUnroll; ++u) {
+      const ScanRec& r = rs[u];
+      const uint32_t s = s0 + u * stride;
+      if ((r.flags & F_REG) && !(r.flags & F_IDLE)) {
+        if (r.count == 0 && r.nadd) continue;  // changes inside the batch: positions
+        uint64_t k = okey(r.count ? r.pk : __dadd_rn(tb.rec[s].prev_p, tb.rec[s].pd));
+        m = k < m ? k : m;
+      }
     }
   }
   m = wave_min_u64(m);
@@ -2264,7 +2278,7 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   HIP_OK(hipMemcpyAsync(q->act_idx, q->h_act, 4ull * m, hipMemcpyHostToDevice,
                         q->stream));
   prof_gate(q);
-  const uint32_t gb = grid_for(q->tb.n, 2048);
+  const uint32_t gb = grid_for(q->tb.n, 1024);  // (k_act_base: four records per thread at 1M)
   ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
              q->act_idx, m, q->act_parts, gb, q->act_extra};
   AddParams ap{d_reqs, d_rc, q->tick, n, 0};
@@ -2304,7 +2318,7 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   int rc = ensure_act(q, n);
   if (rc) return rc;
   prof_gate(q);
-  const uint32_t gb = grid_for(q->tb.n, 2048);
+  const uint32_t gb = grid_for(q->tb.n, 1024);  // (k_act_base: four records per thread at 1M)
   ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
              q->act_idx, 0, q->act_parts, gb, q->act_extra, q->act_flag, q->act_dm};
   AddParams ap{d_reqs, d_rc, q->tick, n, 0};
