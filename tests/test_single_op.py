@@ -119,3 +119,17 @@ def test_serve_concurrent_queues():
         c = qs[i].counters()
         assert c["serve_calls"] > 500, c
         qs[i].close()
+
+
+@pytest.mark.timeout(300)
+def test_serve_1m_clients():
+    """the serve path at the latency benchmark's size: 1,048,576 clients
+    (1,024 group summaries of 1,024 slots), 2M pre-populated requests, then
+    single adds and pulls with sometimes decreasing `now`; every decision,
+    status and sampled state against the oracle"""
+    tr = _single_add_trace(31, 1 << 20, 60)
+    n, qg, qo = run_parity(tr, _mk("serve"), queue_kw=MODES[0], state_sample=4096)
+    assert n > 100, n
+    c = qg.counters()
+    assert c["serve_calls"] > 1000, c
+    qg.close()
