@@ -152,7 +152,9 @@ typedef struct dmc_queue dmc_queue;
  * (dmclock_server.h:1314-1341).  Allocates the HBM client table and rings. */
 int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out);
 int dmc_queue_destroy(dmc_queue* q);
-/* The HIP stream (hipStream_t) every *_device call runs on. */
+/* The HIP stream (hipStream_t) every *_device call runs on (the serve
+ * kernel, DMC_OPT_SERVE, is stopped first: work queued on the stream does
+ * not wait behind it).  dmc_queue_sync waits for the stream. */
 void* dmc_queue_stream(dmc_queue* q);
 int dmc_queue_sync(dmc_queue* q);
 const char* dmc_strerror(int code);
