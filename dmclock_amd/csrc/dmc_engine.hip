@@ -2869,7 +2869,7 @@ int serve_start(dmc_queue* q, uint64_t seq0) {
   __atomic_store_n(&q->h_serve->state, (uint32_t)kServeRunning, __ATOMIC_RELEASE);
   hipLaunchKernelGGL(k_serve, dim3(1), dim3(kServeThreads), 0, q->stream, q->tb, q->gsum,
                      q->ngroups, q->gshift, q->d_serve, q->p.at_limit, q->n_registered,
-                     q->sched, seq0, q->serve_idle_ticks, q->tick);
+                     q->sched, seq0, q->serve_idle_ticks, q->tick, q->serve_trace);
   if (hipGetLastError() != hipSuccess) {
     q->gsum_valid = false;
     return DMC_EDEVICE;

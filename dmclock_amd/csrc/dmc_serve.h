@@ -322,7 +322,7 @@ __device__ __attribute__((always_inline)) inline void serve_total(const StepRed*
 __global__ void __launch_bounds__(kServeThreads)
 k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_limit,
         uint32_t nregistered, unsigned long long* sched, uint64_t seq0,
-        uint64_t idle_ticks, uint64_t tick) {
+        uint64_t idle_ticks, uint64_t tick, bool trace) {
   __shared__ StepRed sg[kServeMaxG];
   __shared__ StepRed sh[kServeRes + 1];
   __shared__ ArgMin sha[kServeThreads / 64 + 1];
@@ -363,7 +363,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (lane < kServeCmdWords) s_cmd[lane] = got ? w : 0;
       c_read = c_seen;
-      if (lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
+      if (trace && lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
     const uint32_t op = (uint32_t)(s_cmd[1] & 0xff);
@@ -391,8 +391,10 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
             summary_add(sg[s >> gshift], sr, s, (sr.flags & F_READY) != 0);
           }
         }
-        io->phase[0] = wall_clock64();
-        io->phase[2] = io->phase[0];
+        if (trace) {
+          io->phase[0] = wall_clock64();
+          io->phase[2] = io->phase[0];
+        }
         io->rc = s_rc;
       }
     } else {
@@ -407,7 +409,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         for (uint32_t i = threadIdx.x; i < G; i += kServeThreads)
           ar = argmin_combine(ar, ArgMin{sg[i].r.key, i, sg[i].r.cnt});
         serve_block_argmin(ar, sha);
-        if (threadIdx.x == 0 && n == 0) io->phase[0] = wall_clock64();
+        if (trace && threadIdx.x == 0 && n == 0) io->phase[0] = wall_clock64();
         StepCtl c{};
         c.type = -1;
         if (sha[0].key != kMaxKey && from_okey(sha[0].key) <= now) {
@@ -456,13 +458,13 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         if (threadIdx.x == 0) {
           s_c = c;
           step_apply_body(tb, s_tick, &s_c, io->dec, n, sched);
-          if (n == 0) io->phase[1] = wall_clock64();
+          if (trace && n == 0) io->phase[1] = wall_clock64();
         }
         __syncthreads();
         const uint32_t g = c.slot >> gshift;
         group_summary<false>(tb, g, gshift, now, sh);
         if (threadIdx.x == 0) sg[g] = sh[kServeRes];
-        if (threadIdx.x == 0 && n == 0) io->phase[2] = wall_clock64();
+        if (trace && threadIdx.x == 0 && n == 0) io->phase[2] = wall_clock64();
         __syncthreads();
         ++n;
         (c.prio ? nprio : nres)++;
@@ -477,12 +479,14 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      io->clk[0] = c_seen;
-      io->clk[1] = c_read;
-      io->clk[2] = wall_clock64();
-      io->cyc[1] = __builtin_amdgcn_s_memtime();
+      if (trace) {
+        io->clk[0] = c_seen;
+        io->clk[1] = c_read;
+        io->clk[2] = wall_clock64();
+        io->cyc[1] = __builtin_amdgcn_s_memtime();
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      io->clk[3] = wall_clock64();
+      if (trace) io->clk[3] = wall_clock64();
       __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       s_life = wall_clock64() - born > 5 * idle_ticks;
     }
