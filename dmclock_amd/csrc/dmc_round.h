@@ -1816,7 +1816,7 @@ constexpr int kRankBlocksR = kNBR;
 // where the record's run of equal keys holds another slot.  Counting costs
 // cnt^2 / 256 compare steps per lane: 973 for a full bin.
 #ifndef DMC_RANK_SORT_MIN
-#define DMC_RANK_SORT_MIN 192
+#define DMC_RANK_SORT_MIN 256
 #endif
 constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
 __device__ inline bool bkey_less(const BKey& x, const BKey& y) {
