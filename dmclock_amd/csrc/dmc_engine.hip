@@ -972,7 +972,15 @@ k_act_seq(ActBuf act, ActTiles tl) {
   }
   __threadfence();
   __syncthreads();
-  if (nc) act_chain(0, nc, kMaxKey, tl.cX, tl.cP, tl.cT, tl.cPd, &s_M, nullptr, tl.cMo, 8, 64);
+#ifndef DMC_ACT_WAVE_BELOW
+#define DMC_ACT_WAVE_BELOW 8
+#endif
+#ifndef DMC_ACT_WAVE_LEN
+#define DMC_ACT_WAVE_LEN 64
+#endif
+  if (nc)
+    act_chain(0, nc, kMaxKey, tl.cX, tl.cP, tl.cT, tl.cPd, &s_M, nullptr, tl.cMo,
+              DMC_ACT_WAVE_BELOW, DMC_ACT_WAVE_LEN);
   __threadfence();
   __syncthreads();
   for (uint32_t g = tid; g < nc; g += kActThreads) {
