@@ -37,7 +37,7 @@ OPT_SAMPLE = 5
 OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
-OPT_PREDICT = 9
+OPT_FAULT = 9
 OPT_SERVE = 10
 
 # PhaseType (dmclock_recs.h:33)
@@ -132,8 +132,8 @@ class Counters(ctypes.Structure):
         ("bin_splits", ctypes.c_uint64),
         ("brk_rounds", ctypes.c_uint64),
         ("brk_fallbacks", ctypes.c_uint64),
-        ("pred_rounds", ctypes.c_uint64),
-        ("pred_misses", ctypes.c_uint64),
+        ("bad_rounds", ctypes.c_uint64),
+        ("serve_yields", ctypes.c_uint64),
         ("serve_calls", ctypes.c_uint64),
         ("serve_launches", ctypes.c_uint64),
     ]

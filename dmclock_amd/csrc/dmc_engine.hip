@@ -1611,7 +1611,12 @@ struct dmc_queue {
   StepRed* gsum = nullptr;
   uint32_t gshift = 10, ngroups = 0;
   uint64_t serve_seq = 0;
-  uint64_t serve_idle_ticks = 200000;  // 2 ms of the 100 MHz wall clock
+  uint64_t serve_idle_ticks = 20000;  // 0.2 ms of the 100 MHz wall clock (lifetime: 5x)
+  bool serve_reg = false;  // listed in the process's serve registry (serve_registry)
+  // k_serve did not exit within kServeStopWait of a stop command: the
+  // queue's stream is presumed wedged and every later call returns
+  // DMC_EDEVICE instead of blocking on it
+  bool wedged = false;
   // DMC_SERVE_TRACE: per-call phases (k_serve's wall-clock stamps), printed
   // at destroy: read, work, publish (ticks) and the host's call time (ns)
   bool serve_trace = getenv("DMC_SERVE_TRACE") != nullptr;
@@ -1706,14 +1711,7 @@ struct dmc_queue {
   uint32_t small_k = 8;  // pulls with k <= small_k run the single-step path
   int fail_allocs = 0;   // DMC_OPT_FAIL_ALLOC (test hook): device allocations to fail
   bool brk_rounds = true;  // DMC_OPT_BREAK_ROUNDS: Allow's limit breaks as rounds
-  // predicted-candidate rounds (DMC_OPT_PREDICT): the last sampled bin-ranked
-  // rounds' thresholds per phase ([0] the latest), their k, how many
-  bool pred_on = false;  // measured slower at config 3
-  bool pred_skip = false;     // the next round runs unpredicted (after a miss)
-  uint64_t thrT[2][2] = {{0, 0}, {0, 0}};
-  uint32_t thrK = 0, thrN = 0;
-  ScanEnt* slist = nullptr;   // k_rscan blocks x kListCap predicted-candidate entries
-  uint32_t* slcnt = nullptr;  // per k_rscan block: its list's length
+  uint32_t fault = 0;          // DMC_OPT_FAULT (test hook): CallParams::fault of the next round
   bool force_radix = false;    // DMC_OPT_FORCE_RADIX
   bool debug = getenv("DMC_DEBUG") != nullptr;  // per-round diagnostics
   uint32_t* dbg_bins = nullptr;  // debug: bin counts of the last round
@@ -1740,31 +1738,99 @@ struct dmc_queue {
 // Every entry point of a queue holds its mutex (the reference's data_mtx) and
 // makes the queue's device current for the calling thread, so that servers
 // of one rank can be driven from one host thread each.
-// Stops k_serve (its summaries written back) before a call that launches
-// other work on the queue's stream or changes the table; the summaries are
-// then stale until rebuilt.
-void serve_quiesce(dmc_queue* q) {
-  q->gsum_valid = false;
-  if (!q->serving) return;
+//
+// Stopping k_serve: a stop command, then a bounded wait for the kernel to
+// report its exit (it reads the command at its next poll, writes the
+// summaries back and exits); only then the stream synchronisation.  A
+// kernel that does not exit in time marks the queue wedged (DMC_EDEVICE
+// from then on) rather than blocking the caller forever.
+constexpr auto kServeStopWait = std::chrono::seconds(1);
+int serve_stop(dmc_queue* q) {
+  if (!q->serving) return DMC_OK;
+  ServeIO* io = q->h_serve;
   {  // the stop command
-    ServeIO* io = q->h_serve;
     const uint64_t seq = ++q->serve_seq;
     io->now = 0.0;
     std::memset((void*)&io->req, 0, sizeof(io->req));
     io->cmd = (uint64_t)kServeStop | (serve_check(seq, kServeStop, 0, 0, 0, 0, 0) << 16);
     __atomic_store_n(&io->req_seq, seq, __ATOMIC_RELEASE);
   }
-  (void)hipStreamSynchronize(q->stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&io->state, __ATOMIC_ACQUIRE) != kServeExited) {
+    if (std::chrono::steady_clock::now() - t0 > kServeStopWait) {
+      q->wedged = true;
+      std::fprintf(stderr, "dmclock_gpu: k_serve did not stop; queue marked failed\n");
+      return DMC_EDEVICE;
+    }
+    __builtin_ia32_pause();
+  }
   q->serving = false;
+  return hipStreamSynchronize(q->stream) == hipSuccess ? DMC_OK : DMC_EDEVICE;
+}
+
+// Stops k_serve before a call that launches other work on the queue's
+// stream or changes the table; the summaries are then stale until rebuilt.
+int serve_quiesce(dmc_queue* q) {
+  q->gsum_valid = false;
+  return serve_stop(q);
+}
+
+// The process's serving queues (DMC_OPT_SERVE).  A persistent k_serve holds
+// its stream's hardware queue; a process has few of them (HIP's
+// GPU_MAX_HW_QUEUES, 4 by default) and streams share them round-robin, so
+// work queued behind another queue's k_serve waits until that kernel exits
+// (idle timeout or lifetime).  Before any call launches work, every other
+// serving queue of the device that is not in a call of its own (its mutex is
+// free) is stopped -- its summaries stay valid, its next serve call
+// relaunches it (a few microseconds) -- so that at most the queues busy in
+// other threads hold a hardware queue.  DMCLOCK_SERVE_SHARED=1 turns this
+// off (callers that know their streams map to distinct hardware queues).
+struct ServeRegistry {
+  std::mutex m;
+  std::vector<dmc_queue*> qs;
+  bool shared = getenv("DMCLOCK_SERVE_SHARED") && std::atoi(getenv("DMCLOCK_SERVE_SHARED"));
+};
+ServeRegistry& serve_registry() {
+  static ServeRegistry r;
+  return r;
+}
+void serve_register(dmc_queue* q, bool on) {
+  ServeRegistry& r = serve_registry();
+  std::lock_guard<std::mutex> g(r.m);
+  auto it = std::find(r.qs.begin(), r.qs.end(), q);
+  if (on && it == r.qs.end()) r.qs.push_back(q);
+  if (!on && it != r.qs.end()) r.qs.erase(it);
+  q->serve_reg = on;
+}
+void serve_yield_others(dmc_queue* q) {
+  ServeRegistry& r = serve_registry();
+  if (r.shared) return;
+  std::lock_guard<std::mutex> g(r.m);
+  for (dmc_queue* o : r.qs) {
+    if (o == q || o->p.device != q->p.device) continue;
+    if (!__atomic_load_n(&o->serving, __ATOMIC_RELAXED)) continue;
+    std::unique_lock<std::mutex> l(o->mtx, std::try_to_lock);
+    if (!l.owns_lock()) continue;  // in a call of its own (another thread)
+    if (o->serving) {
+      ++o->ctr.serve_yields;
+      (void)serve_stop(o);  // (its summaries stay valid)
+    }
+  }
 }
 
 // Every C-ABI call holds the queue's lock; all but the serve path's calls
-// quiesce k_serve first.
+// quiesce k_serve first.  rc: DMC_EDEVICE once the queue is wedged.
 struct QueueLock {
   std::lock_guard<std::mutex> l;
+  int rc = DMC_OK;
   explicit QueueLock(dmc_queue* q, bool serve = false) : l(q->mtx) {
     (void)hipSetDevice(q->p.device);
-    if (!serve) serve_quiesce(q);
+    if (q->wedged) {
+      rc = DMC_EDEVICE;
+      return;
+    }
+    if (!serve) rc = serve_quiesce(q);
+    if (serve_registry().qs.size() > (q->serve_reg ? 1u : 0u)) serve_yield_others(q);
   }
 };
 
@@ -2185,10 +2251,10 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   DALLOC(q, &q->act_islot, 4ull * cap);
   DALLOC(q, &q->act_flag, 4ull * cap);
   HIP_OK(hipHostMalloc((void**)&q->h_act, 4ull * cap, 0));
-  if (!q->act_dm) {
-    DALLOC(q, &q->act_dm, 4);
-    HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
-  }
+  // (each one-time buffer guarded by its own pointer: a failed allocation
+  // is retried by the next call, never skipped because its pair exists)
+  if (!q->act_dm) DALLOC(q, &q->act_dm, 4);
+  if (!q->h_actm) HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
   DALLOC(q, &q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap));
   {
     ActTiles& a = q->atl;
@@ -2208,8 +2274,8 @@ int ensure_act(dmc_queue* q, uint32_t n) {
     DALLOC(q, &a.cT, 8ull * cap);
     DALLOC(q, &a.cPd, 8ull * cap);
     DALLOC(q, &a.cMo, 8ull * cap);
-    if (!q->act_xbase) {
-      DALLOC(q, &q->act_xbase, 8);
+    if (!q->act_xbase) DALLOC(q, &q->act_xbase, 8);
+    if (!q->act_fail) {
       DALLOC(q, &q->act_fail, 4);
       HIP_OK(hipMemsetAsync(q->act_fail, 0xff, 4, q->stream));
       HIP_OK(hipStreamSynchronize(q->stream));
@@ -2657,7 +2723,7 @@ bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
 
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = false) {
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
   prof_gate(q);
   const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
@@ -2665,10 +2731,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = f
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : pred ? k_rscan_pred : k_rscan, dim3(gN),
+  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN),
           dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
           q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
-          sampled ? q->skp : nullptr, q->k32, q->hist, q->slist, q->slcnt);
+          sampled ? q->skp : nullptr, q->k32, q->hist);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
@@ -2678,11 +2744,10 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = f
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
             gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup);
-  klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : pred ? k_remit_pred : k_remit, dim3(gEm),
+  klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsup, (const uint32_t*)q->hist,
-          q->dense, q->ecap, (const ScanEnt*)q->slist, (const uint32_t*)q->slcnt,
-          q->debug ? q->dbg_etime : nullptr);
+          q->dense, q->ecap, q->debug ? q->dbg_etime : nullptr);
   if (!radix) {
     if (q->debug)  // (the record counts: the rank-bin counters' low words)
       (void)hipMemcpy2DAsync(q->dbg_bins, sizeof(uint32_t), q->bcount, 2 * sizeof(uint32_t),
@@ -2732,67 +2797,17 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, bool pred = f
           q->debug ? q->dbg_atime : nullptr);
 }
 
-// Predicted thresholds for a round of kk pulls (DMC_OPT_PREDICT): the last
-// round's, widened by three times its last drift and 2^-20 relative, for a
-// sampled bin-ranked round of the same k as the last ones.  R: "all" stays
-// all (and none predicts all: the R-eligible slots are few); P: none
-// predicts nothing (no prediction).
-bool predict(dmc_queue* q, uint32_t kk, bool radix, bool brk, uint64_t pT[2]) {
-  if (kScanPerEmit != 4 || !q->pred_on || q->pred_skip || radix || brk || !use_sample(q, radix) ||
-      q->thrN == 0 || q->thrK != kk)
-    return false;
-  for (int p = 0; p < 2; ++p) {
-    const uint64_t T0 = q->thrT[p][0];
-    if (T0 == kMaxKey - 1 || (p == 0 && T0 == 0)) {
-      pT[p] = kMaxKey - 1;
-      continue;
-    }
-    if (T0 == 0) return false;
-    const double d0 = from_okey(T0);
-    double drift = 0.0;
-    const uint64_t T1 = q->thrT[p][1];
-    if (q->thrN >= 2 && T1 != 0 && T1 != kMaxKey - 1) drift = d0 - from_okey(T1);
-    const double w = 3.0 * std::fabs(drift) + std::ldexp(std::fabs(d0) + 1.0, -20);
-    const double dp = d0 + w;
-    if (!(dp < kInf)) {
-      pT[p] = kMaxKey - 1;
-      continue;
-    }
-    const uint64_t kp = okey(dp) | 0xffffffffull;  // (the end of its 32-bit quantum)
-    pT[p] = kp < kMaxKey - 1 ? kp : kMaxKey - 1;
-  }
-  return true;
-}
-
-// after a completed round: its thresholds for the next predictions
-void record_thresholds(dmc_queue* q, const Round& c, uint32_t kk, bool radix, bool brk) {
-  q->pred_skip = false;
-  if (radix || brk || !c.sampled) {
-    q->thrN = 0;
-    return;
-  }
-  if (q->thrK != kk) q->thrN = 0;
-  for (int p = 0; p < 2; ++p) {
-    q->thrT[p][1] = q->thrT[p][0];
-    q->thrT[p][0] = c.ph[p].T;
-  }
-  q->thrK = kk;
-  q->thrN = std::min<uint32_t>(q->thrN + 1, 2);
-}
-
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
                  dmc_pull_result* d_result, bool radix, bool brk = false) {
   const bool sampled = use_sample(q, radix);
-  CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq, {0, 0}};
-  const bool pred = predict(q, kk, radix, brk, cp.pT);
-  if (pred) ++q->ctr.pred_rounds;
-  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 5) | (pred ? 16 : 0) | (brk ? 8 : 0) |
+  CallParams cp{kk, brk ? 1u : 0u, now, out, q->tick, d_result, ++q->round_seq, q->fault, 0};
+  uint64_t key = (3ull << 56) | ((uint64_t)q->ecap << 5) | (brk ? 8 : 0) |
                  (sampled ? 4 : 0) | (radix ? 2 : 0);
   int err = DMC_OK;
-  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix, pred); }, &err);
+  GraphRec* g = graph_for(q, key, [&] { enqueue_round(q, cp, radix); }, &err);
   if (err) return err;
   if (!g) {
-    enqueue_round(q, cp, radix, pred);
+    enqueue_round(q, cp, radix);
     HIP_OK(hipGetLastError());
     return DMC_OK;
   }
@@ -2802,7 +2817,7 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
   uint64_t* kr = sampled ? nullptr : q->keyr;
   uint64_t* kp = sampled ? nullptr : q->keyp;
   void* args[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                  &skr, &skp, &q->k32, &q->hist, &q->slist, &q->slcnt};
+                  &skr, &skp, &q->k32, &q->hist};
   return graph_replay(q, *g, args);
 }
 
@@ -2919,7 +2934,10 @@ int serve_call(dmc_queue* q, uint32_t op, uint32_t k) {
         if (rc) return rc;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-        serve_quiesce(q);
+        // no answer: a bounded stop (a kernel that does not take it marks
+        // the queue wedged); never an unbounded wait on the stream
+        q->gsum_valid = false;
+        (void)serve_stop(q);
         return DMC_EDEVICE;
       }
     }
@@ -3146,17 +3164,15 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       retry_radix = retry;
       continue;
     }
-    if (c.overflow == 6) {
-      // a predicted round's threshold lay above its prediction (or a list
-      // outgrew its capacity): nothing of it took effect; re-run unpredicted
-      ++q->ctr.pred_misses;
-      q->pred_skip = true;
-      if (q->debug || getenv("DMC_PRED_LOG"))
-        std::fprintf(stderr, "dmc pred miss: T %.9g %.9g predicted %.9g %.9g\n",
-                     c.ph[0].T ? from_okey(c.ph[0].T) : 0.0,
-                     c.ph[1].T ? from_okey(c.ph[1].T) : 0.0,
-                     c.pT[0] ? from_okey(c.pT[0]) : 0.0, c.pT[1] ? from_okey(c.pT[1]) : 0.0);
-      continue;
+    if (c.overflow == 7) {
+      // the round failed its outcome check (k_rrank: a phase's selection
+      // unset, R-prefix entries not emitted, or fewer decisions than the
+      // eligible work allows): nothing of it was applied; an engine fault,
+      // reported, never a short dispatch
+      ++q->ctr.bad_rounds;
+      std::fprintf(stderr, "dmclock_gpu: round %llu failed its outcome check (k=%u)\n",
+                   (unsigned long long)c.seq, kr);
+      return DMC_EDEVICE;
     }
     if (c.overflow == 5) {
       // a limit-break round found the state not break-ready (a front with
@@ -3206,7 +3222,6 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     if (!radix) q->ovf_streak = 0;
     q->exact_next = false;
-    record_thresholds(q, c, kr, radix, brk);
     q->ctr.candidates += c.n_cand;
     q->ctr.entries += radix ? c.dense_n : c.n_emit;
     q->ctr.decisions += c.n_dec;
@@ -3325,8 +3340,6 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
   rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
-  rc |= A(&q->slist, (size_t)((N + kScanBlock - 1) / kScanBlock) * kListCap);
-  rc |= A(&q->slcnt, (N + kScanBlock - 1) / kScanBlock);
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsup, kNSup);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
@@ -3347,7 +3360,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
     int khz = 0;  // the wall clock k_serve's idle limit counts
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p.device) == hipSuccess &&
         khz > 0)
-      q->serve_idle_ticks = 2ull * (uint64_t)khz;
+      q->serve_idle_ticks = (uint64_t)khz / 5;  // 0.2 ms
   }
   rc |= A(&q->reqcount, 1);
   if (hipHostMalloc((void**)&q->h_round, sizeof(HostRound),
@@ -3389,7 +3402,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   (void)hipSetDevice(q->p.device);
-  if (q->h_serve) serve_quiesce(q);
+  if (q->serve_reg) serve_register(q, false);
+  if (q->h_serve && !q->wedged) (void)serve_quiesce(q);
   if (q->serve_trace && q->ctr.serve_calls) {
     const double c = (double)q->ctr.serve_calls;
     std::fprintf(stderr, "dmc serve: %llu calls, %llu launches; per call: read %.0f, work %.0f, "
@@ -3411,7 +3425,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   void* ptrs[] = {t.rec, t.sc, t.aux, q->binfo,
                   t.ring,
                   q->cand, q->bcand, q->post, q->decof, q->keyr, q->keyp, q->k32, q->meta, q->hist,
-                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->slist, q->slcnt, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
+                  q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
                   q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
@@ -3456,6 +3470,7 @@ void* dmc_queue_stream(dmc_queue* q) {
 int dmc_queue_sync(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   HIP_OK(hipStreamSynchronize(q->stream));
   return DMC_OK;
 }
@@ -3465,6 +3480,7 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                               int active) {
   if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
@@ -3514,6 +3530,7 @@ int dmc_client_update_info(dmc_queue* q, uint32_t slot, double r, double w,
                            double l) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   double v[3] = {inv_of(r), inv_of(w), inv_of(l)};
   // r_inv, w_inv, l_inv are contiguous in ClientRec and in BoundInfo
@@ -3530,6 +3547,7 @@ int dmc_client_bind_info_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                                const double* r, const double* w, const double* l) {
   if (!q || (n && (!slots || !r || !w || !l))) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
   return bind_infos(q, n, slots, r, w, l);
@@ -3538,6 +3556,7 @@ int dmc_client_bind_info_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
 int dmc_queue_set_info_fn(dmc_queue* q, dmc_info_fn fn, void* ctx) {
   if (!q) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   q->info_fn = fn;
   q->info_ctx = ctx;
   return DMC_OK;
@@ -3546,6 +3565,7 @@ int dmc_queue_set_info_fn(dmc_queue* q, dmc_info_fn fn, void* ctx) {
 int dmc_client_mark_idle(dmc_queue* q, uint32_t slot) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
@@ -3570,6 +3590,7 @@ __global__ void k_mark_idle(Table tb, uint32_t n, const uint32_t* slots) {
 int dmc_client_mark_idle_batch(dmc_queue* q, uint32_t n, const uint32_t* slots) {
   if (!q || (n && !slots)) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -3733,6 +3754,7 @@ __global__ void k_mark_idle_dev(Table tb, uint32_t n, const uint32_t* slots) {
 int dmc_client_mark_idle_batch_device(dmc_queue* q, uint32_t n, const uint32_t* d_slots) {
   if (!q || (n && !d_slots)) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (!n) return DMC_OK;
   hipLaunchKernelGGL(k_mark_idle_dev, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      q->stream, q->tb, n, d_slots);
@@ -3793,6 +3815,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                      uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
@@ -3817,6 +3840,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
 int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
   if (!q || !s || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   std::memset(s, 0, sizeof(*s));
   const Table& t = q->tb;
   uint8_t f = 0;
@@ -3863,6 +3887,7 @@ int dmc_client_get_state(dmc_queue* q, uint32_t slot, dmc_client_state* s) {
 int dmc_client_last_ticks(dmc_queue* q, uint32_t n, uint64_t* out) {
   if (!q || !out || n > q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (n)
     HIP_OK(hipMemcpy2DAsync(out, sizeof(uint64_t), &q->tb.aux[0].last_tick,
                             sizeof(ClientAux), sizeof(uint64_t), n,
@@ -3876,8 +3901,9 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   if (!q || (n && !reqs)) return DMC_EINVAL;
   QueueLock g(q, true);
   ++q->gen;
+  if (g.rc) return g.rc;
   if (n == 1 && serve_add_ok(q, reqs[0])) return serve_add(q, reqs[0], rc_out);
-  serve_quiesce(q);
+  if (int rc0 = serve_quiesce(q)) return rc0;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
   if (!n) return DMC_OK;
@@ -3914,6 +3940,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
                          int32_t* d_rc_out) {
   if (!q || (n && (!d_reqs || !d_rc_out))) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   if (!n) return DMC_OK;
   int rc = ensure_batch(q, n);
@@ -3945,8 +3972,9 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
   if (!q || (k && !out)) return DMC_EINVAL;
   QueueLock g(q, true);
   ++q->gen;
+  if (g.rc) return g.rc;
   if (q->serve_on && fast_pull_ok(q, k)) return serve_pull(q, now, k, out, result);
-  serve_quiesce(q);
+  if (int rc0 = serve_quiesce(q)) return rc0;
   if (fast_pull_ok(q, k)) return fast_pull(q, now, k, out, result);
   int rc = ensure_dec(q, k);
   if (rc) return rc;
@@ -3965,6 +3993,7 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
                           dmc_decision* d_out, dmc_pull_result* d_result) {
   if (!q || (k && !d_out)) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   dmc_pull_result r{};
   bool dev_wrote = false;
@@ -3988,6 +4017,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
   bool fuse;
   {
     QueueLock g(q);
+    if (g.rc) return g.rc;
   ++q->gen;
   if (int rc0 = settle_act(q)) return rc0;
     fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
@@ -3998,19 +4028,15 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
-      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq, {0, 0}};
-      const bool pred = predict(q, k, false, false, cp.pT);
-      if (pred) ++q->ctr.pred_rounds;
+      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault, 0};
       auto enqueue = [&] {
         enqueue_add(q, ap);
-        enqueue_round(q, cp, false, pred);
+        enqueue_round(q, cp, false);
       };
       ++q->ctr.fused_calls;
-      uint64_t key = (4ull << 56) | ((uint64_t)n << 3) | (pred ? 4 : 0) |
-                     (use_sample(q, false) ? 2 : 0);
+      uint64_t key = (4ull << 56) | ((uint64_t)n << 3) | (use_sample(q, false) ? 2 : 0);
       int err = DMC_OK;
-      GraphRec* gr = graph_for(q, key, enqueue, &err,
-                               pred ? (const void*)k_rscan_pred : (const void*)k_rscan);
+      GraphRec* gr = graph_for(q, key, enqueue, &err, (const void*)k_rscan);
       if (err) return err;
       if (!gr) {
         enqueue();
@@ -4026,7 +4052,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         uint64_t* kr = sampled ? nullptr : q->keyr;
         uint64_t* kp = sampled ? nullptr : q->keyp;
         void* a2[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
-                      &skr, &skp, &q->k32, &q->hist, &q->slist, &q->slcnt};
+                      &skr, &skp, &q->k32, &q->hist};
         int rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }
@@ -4051,6 +4077,7 @@ int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
                          uint64_t* handles_out, uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   if (!q->reg_h[slot]) {
     if (n_out) *n_out = 0;
@@ -4071,6 +4098,7 @@ int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
                         uint32_t cap, uint32_t* n_out) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
   uint32_t h;
@@ -4086,6 +4114,7 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
                       const uint8_t* keep) {
   if (!q || slot >= q->p.max_clients) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   ++q->gen;
   if (!q->reg_h[slot]) return DMC_ENOTREG;
   std::vector<ReqEntry> ents;
@@ -4104,6 +4133,7 @@ int dmc_queue_requests(dmc_queue* q, uint32_t* counts_out, uint64_t* handles_out
                        uint64_t cap, uint64_t* n_out) {
   if (!q || !n_out) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (int rc0 = settle_act(q)) return rc0;
   const uint32_t N = q->tb.n;
   DevBuf counts, offs, hs;
@@ -4130,6 +4160,7 @@ int dmc_queue_requests(dmc_queue* q, uint32_t* counts_out, uint64_t* handles_out
 int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_removed) {
   if (!q || (n && !keep)) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   // the queue must be the one the last dmc_queue_requests read
   if (q->maint_gen != q->gen || n != q->maint_total) return DMC_EINVAL;
   ++q->gen;
@@ -4163,6 +4194,7 @@ int dmc_client_erase_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
                            uint64_t* n_out) {
   if (!q || (n && !slots)) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (int rc0 = settle_act(q)) return rc0;
   if (int rc0 = sync_idle(q)) return rc0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -4277,6 +4309,7 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
   if (!q) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   switch (option) {
     case DMC_OPT_SMALL_K:
       if (value < 0) return DMC_EINVAL;
@@ -4300,10 +4333,11 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       return DMC_OK;
     case DMC_OPT_SERVE:
       q->serve_on = value != 0;
+      if (q->serve_on != q->serve_reg) serve_register(q, q->serve_on);
       return DMC_OK;
-    case DMC_OPT_PREDICT:
-      q->pred_on = value != 0;
-      q->thrN = 0;
+    case DMC_OPT_FAULT:
+      if (value < 0) return DMC_EINVAL;
+      q->fault = (uint32_t)value;
       return DMC_OK;
     case DMC_OPT_FAIL_ALLOC:
       if (value < 0) return DMC_EINVAL;
@@ -4322,6 +4356,7 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset) {
   if (!q || !out) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   *out = q->ctr;
   if (reset) q->ctr = dmc_counters{};
   return DMC_OK;
@@ -4330,6 +4365,7 @@ int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset) {
 int dmc_profile_enable(dmc_queue* q, int on) {
   if (!q) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   q->prof_on = on != 0;
   q->prof_n = 0;
   return DMC_OK;
@@ -4338,6 +4374,7 @@ int dmc_profile_enable(dmc_queue* q, int on) {
 int dmc_profile_reset(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   for (int i = 0; i < DMC_PROF_NSTAGES; ++i) {
     q->prof_ms[i] = 0.0;
     q->prof_cnt[i] = 0;
@@ -4349,6 +4386,7 @@ int dmc_profile_read(dmc_queue* q, uint32_t stage, uint64_t* count,
                      double* total_ms) {
   if (!q || stage >= DMC_PROF_NSTAGES) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   if (count) *count = q->prof_cnt[stage];
   if (total_ms) *total_ms = q->prof_ms[stage];
   return DMC_OK;
@@ -4361,6 +4399,7 @@ const char* dmc_profile_stage_name(uint32_t stage) {
 int dmc_stats_get(dmc_queue* q, dmc_stats* out) {
   if (!q || !out) return DMC_EINVAL;
   QueueLock g(q);
+  if (g.rc) return g.rc;
   unsigned long long sc[2];
   HIP_OK(hipMemsetAsync(q->reqcount, 0, 8, q->stream));
   hipLaunchKernelGGL(k_count_requests, dim3(grid_for(q->tb.n, 1024)), dim3(kBlock),

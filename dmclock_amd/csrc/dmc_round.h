@@ -79,7 +79,7 @@ struct PhaseSel {
   uint32_t n_elig;      // clients with an eligible first key
   uint32_t hshift;      // histogram bin of key k: hist_bin(k, hmin, hshift)
   uint32_t tbin;        // histogram bin holding T (last bin of the table)
-  uint32_t pad;
+  uint32_t valid;       // kSelValid once the pick wrote it (k_rscan zeroes it)
   uint64_t hmin;        // histogram base (histogram coordinates, KeyMap)
   uint64_t lo0, hitop;  // coordinate span of the open-ended first / last bin
   double vmin, scale;   // the phase's KeyMap (with kmin)
@@ -143,8 +143,8 @@ struct Round {
   uint64_t tick;
   dmc_pull_result* res;  // device-API result record (null: the host writes it)
   uint64_t seq;          // round sequence number, published to the host
-  uint64_t pT[2];        // predicted thresholds (pred rounds: k_rscan listed every
-                         // slot whose first key is at or below them)
+  uint32_t fault;        // test hook (CallParams::fault)
+  uint32_t pad2;
 };
 
 struct CallParams {
@@ -155,22 +155,9 @@ struct CallParams {
   uint64_t tick;
   dmc_pull_result* res;
   uint64_t seq;
-  uint64_t pT[2];  // predicted thresholds (the host's, from the last rounds'
-                   // thresholds; used by the PRED instantiations only)
+  uint32_t fault;  // test hook (DMC_OPT_FAULT): 1 = phase 1's selection left unset
+  uint32_t pad;
 };
-
-// Predicted-candidate rounds (PRED): instead of every slot's quantized keys
-// and meta word (12 B per slot written by k_rscan and streamed by k_remit),
-// k_rscan lists, per block in slot order, the slots whose first key is at or
-// below the host's predicted thresholds and those it gave a pending
-// limit-scan mark; k_remit reads its four scan blocks' lists.  The list is
-// exact for every threshold at or below the predicted one: a round whose
-// picked threshold lies above it, or a list that outgrew kListCap, fails
-// (overflow = 6) before anything is applied and is re-run unpredicted.
-struct ScanEnt {
-  uint32_t slot, kr32, kp32, meta;
-};
-constexpr uint32_t kListCap = 512;  // entries per k_rscan block (of 1024 slots)
 
 // Host-mapped (fine-grained pinned) round summary: the round's last kernel
 // copies Round here and then publishes seq, so the host learns the outcome
@@ -351,7 +338,6 @@ __device__ inline uint32_t scan_meta(const ScanCols& x, const ScanOut& o) {
   return (o.m & 0xffu) | ((uint32_t)o.f << 8) | ((x.c ? x.h : 0u) << 16) | (x.c << 24);
 }
 
-template <bool FULL = true>
 __device__ inline void scan_store(const Table& tb, uint32_t s, const ScanCols& x,
                                   const ScanOut& o, uint64_t* keyr, uint64_t* keyp,
                                   uint32_t* meta, uint64_t* skr, uint64_t* skp,
@@ -359,18 +345,18 @@ __device__ inline void scan_store(const Table& tb, uint32_t s, const ScanCols& x
   const uint64_t kr = o.kr, kp = o.kp;
   const uint32_t m = o.m;
   if (o.mark) tb.sc[s].flags = o.f;
-  if (FULL && keyr) {  // the exact histogram's keys (unsampled rounds)
+  if (keyr) {  // the exact histogram's keys (unsampled rounds)
     keyr[s] = kr;
     keyp[s] = kp;
   }
-  if (FULL) k32[s] = make_uint2(key32(kr), key32(kp));
+  k32[s] = make_uint2(key32(kr), key32(kp));
   if (skr && (s & (kSample - 1)) == 0) {  // the threshold histogram's sample
     skr[s / kSample] = kr;
     skp[s / kSample] = kp;
   }
   // the candidate record's fields for k_remit: R-prefix length, flags (with
   // a pending mark this scan set), ring head and count
-  if (FULL) meta[s] = scan_meta(x, o);
+  meta[s] = scan_meta(x, o);
   if (kr != kMaxKey) {
     ++acc.cnt[0];
     acc.n_r += m;
@@ -483,16 +469,14 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
-template <bool BRK, bool PRED>
+template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
 k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
           RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
-          uint2* k32, uint32_t* hist, ScanEnt* lst, uint32_t* lcnt) {
-  static_assert(!PRED || kScanSlots == 1, "predicted lists: one slot per thread");
+          uint2* k32, uint32_t* hist) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
-    z.pT[0] = cp.pT[0];
-    z.pT[1] = cp.pT[1];
+    z.fault = cp.fault;
     z.k_total = cp.k_total;
     z.brk = cp.brk;
     z.g_last = kNoneR;
@@ -556,19 +540,7 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
     if (s < tb.n)
-      scan_store<!PRED>(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
-  }
-  // PRED: this block's list, in slot order (wave counts parked in LDS for
-  // the offsets after the block barrier below)
-  __shared__ uint32_t s_wc[kScanBlock / 64];
-  bool ent = false;
-  uint64_t bal = 0;
-  if (PRED) {
-    const uint64_t kr = o[0].kr, kp = o[0].kp;
-    ent = base < tb.n && ((kr != kMaxKey && kr <= cp.pT[0]) ||
-                          (kp != kMaxKey && kp <= cp.pT[1]) || o[0].mark);
-    bal = __ballot(ent);
-    if ((threadIdx.x & 63) == 0) s_wc[threadIdx.x >> 6] = (uint32_t)__popcll(bal);
+      scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
   sh[threadIdx.x] = acc;
   // the threshold histogram k_rhist fills, cleared (the previous round's
@@ -579,18 +551,6 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
       hist[gi] = 0;
   }
   __syncthreads();
-  if (PRED) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t at = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
-    for (int i = 0; i < kScanBlock / 64; ++i) {
-      at += i < w ? s_wc[i] : 0u;
-      tot += s_wc[i];
-    }
-    if (ent && at < kListCap)
-      lst[(size_t)blockIdx.x * kListCap + at] =
-          ScanEnt{base, key32(o[0].kr), key32(o[0].kp), scan_meta(x[0], o[0])};
-    if (threadIdx.x == 0) lcnt[blockIdx.x] = tot;  // (> kListCap: the round fails)
-  }
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
     for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
@@ -599,11 +559,9 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
   }
 }
 
-// the general scan (the graphs' parameter node), the limit-break scan, and
-// the predicted-candidate scan
-constexpr auto k_rscan = k_rscan_t<false, false>;
-constexpr auto k_rscan_brk = k_rscan_t<true, false>;
-constexpr auto k_rscan_pred = k_rscan_t<false, true>;
+// the general scan (the graphs' parameter node) and the limit-break scan
+constexpr auto k_rscan = k_rscan_t<false>;
+constexpr auto k_rscan_brk = k_rscan_t<true>;
 
 // The round's totals from the scan's per-block partials (every thread gets
 // them): wave 0 combines them, 8 per lane for 512 partials with the loads in
@@ -735,8 +693,25 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
 // histogram bins up to T's bin in proportion to their counts (each gets 1 +
 // its share), so that the rank bins stay small however the keys are
 // distributed.  Table entry: first rank bin | rank bins << 16.
-constexpr int kPickHalf = 512;
+// k_remit's block size (1024: the measured best; 512 and 256 build and pass
+// the same parity): pick_both splits it into two halves, one per phase, each
+// taking kBinsPerThreadR histogram bins per thread.  Everything the pick
+// writes (both phases' PhaseSel, both rank-bin tables) is a function of the
+// block size, so no variant leaves a phase unset.
+#ifndef DMC_EMIT_THREADS
+#define DMC_EMIT_THREADS 1024
+#endif
+constexpr int kEmitThreads = DMC_EMIT_THREADS;
+static_assert(kEmitThreads == 256 || kEmitThreads == 512 || kEmitThreads == 1024,
+              "k_remit blocks of 256, 512 or 1024 threads");
+constexpr int kPickHalf = kEmitThreads / 2;
+static_assert(kEmitThreads == 2 * kPickHalf && kPickHalf % 64 == 0 &&
+                  kHistBinsR % kPickHalf == 0 && (kPickHalf & (kPickHalf - 1)) == 0,
+              "pick_both: two power-of-two halves of whole waves, one per phase");
 constexpr int kBinsPerThreadR = kHistBinsR / kPickHalf;
+// PhaseSel::valid of a phase the pick wrote (k_rrank fails a round whose
+// selections are not both written: DMC_EDEVICE, never a short dispatch)
+constexpr uint32_t kSelValid = 0x5e1ec7edu;
 __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
   uint32_t incl = v;
@@ -928,12 +903,14 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     // last bin spans [top, hitop]
     z.inv_w = bitsd((uint64_t)(1023 - sh1) << 52);
     z.inv_last = 1.0 / ((double)(z.hitop - top) + 1.0);
+    z.valid = kSelValid;
     *ps = z;
   }
 }
 
-// Thresholds and rank-bin tables of both phases, by a k_remit block (1024
-// threads): phase 0 in threads [0, 512), phase 1 in [512, 1024).
+// Thresholds and rank-bin tables of both phases, by a k_remit block of
+// kEmitThreads threads: phase 0 in threads [0, kPickHalf), phase 1 in
+// [kPickHalf, kEmitThreads).
 // needed first keys -> histogram units: exact, or for a 1/kSample sample
 // need / kSample plus a margin of 2 % + 4 standard deviations + 16 (a
 // sampled threshold admitting fewer than `need` first keys is caught by
@@ -949,7 +926,7 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
 
 // (sbn, ps: LDS; the results are complete after the last barrier inside)
 __device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist,
-                          uint32_t* sbn, PhaseSel* ps, int sampled) {
+                          uint32_t* sbn, PhaseSel* ps, int sampled, uint32_t fault) {
   __shared__ uint32_t wsum[2][2 * kPickHalf / 64];
   __shared__ uint32_t s_sel[2][4], s_def[2][2];
   __shared__ uint64_t s_T[2];
@@ -964,6 +941,10 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist
   pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hist,
              sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p]);
   __syncthreads();  // (ps, written by thread 0 of each half)
+  // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset, as a pick
+  // that misses a phase would leave it; k_rrank must fail the round
+  if ((fault & 1u) && threadIdx.x == 0) ps[1].valid = 0;
+  __syncthreads();
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -1371,32 +1352,26 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
 // walk (rank_bin_q).  Bin-rank path: the last block to finish
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
-#ifndef DMC_EMIT_THREADS
-#define DMC_EMIT_THREADS 1024
-#endif
-constexpr int kEmitThreads = DMC_EMIT_THREADS;
-constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster,
-                             // and a slower last-block tail)
+constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster)
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
 // walkers with a staging slice per wave: its first lanes (a wave with more
 // candidates walks the rest from global memory)
-constexpr int kEmitStageLanes = kEmitStageThreads / (kEmitThreads / 64);
-// (PRED: the slots come from the four k_rscan blocks' lists of this block's
-// chunk, at most 2 x kEmitThreads entries: two per thread)
-constexpr uint32_t kScanPerEmit = kEmitChunk / kScanBlock;
-// (the host's grids, the apply blocks and the candidate buffers assume this
-// chunk: 2048-slot emit blocks ran slower, and 1024-slot ones faulted)
-static_assert(kEmitChunk == 4096, "emit blocks of 4096 slots");
-template <bool BRK, bool PRED>
-__global__ void __launch_bounds__(kEmitThreads)
+constexpr int kEmitStageLanes0 = kEmitStageThreads / (kEmitThreads / 64);
+constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
+// (the host sizes its grids, the apply blocks and the candidate buffers from
+// kEmitChunk and kApplyPerEmit; pick_both from kEmitThreads)
+// (4 waves per SIMD: at most 128 VGPRs, 16 waves per CU -- one 1024-thread
+// block, or two 512-thread blocks when their LDS fits twice)
+#ifndef DMC_EMIT_MINW
+#define DMC_EMIT_MINW 4
+#endif
+template <bool BRK>
+__global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW)
 k_remit_t(Table tb, Round* rd, const uint2* k32,
         const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
-        uint32_t dcap, const ScanEnt* lst, const uint32_t* lcnt,
-        uint64_t* eclk = nullptr) {
-  static_assert(!PRED || (kScanPerEmit * kListCap <= 2 * kEmitThreads && kEmitPer >= 2),
-                "predicted lists: two entries per thread");
+        uint32_t dcap, uint64_t* eclk = nullptr) {
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
@@ -1424,56 +1399,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
-  // PRED: the list's segment sizes (the four scan blocks), the entries'
-  // slots, and whether a list overflowed
-  uint32_t seg[4] = {0, 0, 0, 0};
-  uint32_t sl[2] = {0, 0};
-  uint32_t nent = 0;
-  // list entry e of this block: (segment, offset) by the segment sizes
-  // (static indices only: seg[] stays in registers)
-  // (four scan blocks per emit block; the host predicts only then)
-  auto ent_at = [&](uint32_t e) -> const ScanEnt& {
-    uint32_t sg = 0;
-    if (e >= seg[0]) {
-      e -= seg[0];
-      sg = 1;
-      if (e >= seg[1]) {
-        e -= seg[1];
-        sg = 2;
-        if (e >= seg[2]) {
-          e -= seg[2];
-          sg = 3;
-        }
-      }
-    }
-    return lst[(size_t)(blockIdx.x * kScanPerEmit + sg) * kListCap + e];
-  };
-  if (PRED) {
-#pragma unroll
-    for (int i = 0; i < (int)kScanPerEmit; ++i) {
-      const uint32_t c = blockIdx.x * kScanPerEmit + i < (n + kScanBlock - 1) / kScanBlock
-                             ? lcnt[blockIdx.x * kScanPerEmit + i]
-                             : 0u;
-      seg[i] = c < kListCap ? c : kListCap;
-      nent += seg[i];
-    }
-#pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
-      kr[j] = kp[j] = 0xffffffffu;
-      mt[j] = 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t e = threadIdx.x + j * kEmitThreads;
-      if (e < nent) {
-        const ScanEnt x = ent_at(e);
-        sl[j] = x.slot;
-        kr[j] = x.kr32;
-        kp[j] = x.kp32;
-        mt[j] = x.meta;
-      }
-    }
-  } else if (s0 + kEmitPer <= n) {
+  if (s0 + kEmitPer <= n) {
     const uint4* k4 = reinterpret_cast<const uint4*>(k32 + s0);
     const uint4* m4 = reinterpret_cast<const uint4*>(meta + s0);
 #pragma unroll
@@ -1499,28 +1425,9 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   // the thresholds and the rank-bin table, picked from the round's
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
-  pick_both(rd->k_total, rd->tot, hist, ltab, s_ph, (int)rd->sampled);
+  pick_both(rd->k_total, rd->tot, hist, ltab, s_ph, (int)rd->sampled, rd->fault);
   if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   const CandPred pred(s_ph, p_runs);
-  if (PRED) {
-    // the lists hold every slot at or below the predicted thresholds: the
-    // picked ones must not lie above them (wave-uniform: every block picks
-    // the same) and no list may have overflowed (any block's: read by all)
-    bool miss = (pred.TR && pred.TR > rd->pT[0]) || (pred.TP && pred.TP > rd->pT[1]);
-    if (!miss) {
-      const uint32_t nsb = (n + kScanBlock - 1) / kScanBlock;
-      for (uint32_t i = threadIdx.x; i < nsb; i += kEmitThreads)
-        if (lcnt[i] > kListCap) miss = true;
-      miss = __syncthreads_or(miss);
-    }
-    if (miss) {
-      // nothing of the round takes effect (the pending marks this scan set
-      // are set again by the unpredicted re-run at the same `now`)
-      if (blockIdx.x == 0 && threadIdx.x == 0) rd->overflow = 6;
-      if (threadIdx.x == 0) bcand[blockIdx.x] = 0;
-      return;
-    }
-  }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
   uint8_t f[kEmitPer];
 #pragma unroll
@@ -1528,7 +1435,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
   uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
   for (int j = 0; j < kEmitPer; ++j) {
-    if (PRED ? (j >= 2 || threadIdx.x + j * kEmitThreads >= nent) : s0 + j >= n) continue;
+    if (s0 + j >= n) continue;
     const bool cr = pred.TR && kr[j] <= pred.TR32;
     const bool cp = pred.TP && kp[j] <= pred.TP32;
     if (cr || cp) bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
@@ -1572,7 +1479,7 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
       const uint32_t b = (bits >> (2 * j)) & 3u;
       if (b) {
         bk[o] = (b & 1u) ? kr[j] : kp[j];
-        bl[o++] = CandRec{PRED ? sl[j < 2 ? j : 0] : s0 + j, (uint8_t)(f[j] | (b << 4)),
+        bl[o++] = CandRec{s0 + j, (uint8_t)(f[j] | (b << 4)),
                           (uint8_t)mt[j], (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
       }
     }
@@ -1631,59 +1538,20 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
     uint32_t ti = threadIdx.x;
     asm volatile("" : "+v"(ti));  // (its LDS address recomputed here, not held)
     const uint2 fb = s_fb[ti];
-    if (PRED) {
-      // (the entries' slots and the segment sizes reloaded: not held --
-      // spilled -- across the walks)
-      const uint32_t* lc = lcnt;
-      asm volatile("" : "+s"(lc));
-      uint32_t sz[kScanPerEmit], ne = 0;
+    const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
 #pragma unroll
-      for (int i = 0; i < (int)kScanPerEmit; ++i) {
-        const uint32_t c = blockIdx.x * kScanPerEmit + i < (n + kScanBlock - 1) / kScanBlock
-                               ? lc[blockIdx.x * kScanPerEmit + i]
-                               : 0u;
-        sz[i] = c < kListCap ? c : kListCap;
-        ne += sz[i];
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
-        uint32_t e = ti + j * kEmitThreads;
-        if (e < ne && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK)) {
-          uint32_t sg = 0;
-          if (e >= sz[0]) {
-            e -= sz[0];
-            sg = 1;
-            if (e >= sz[1]) {
-              e -= sz[1];
-              sg = 2;
-              if (e >= sz[2]) {
-                e -= sz[2];
-                sg = 3;
-              }
-            }
-          }
-          const uint32_t slot = lst[(size_t)(blockIdx.x * kScanPerEmit + sg) * kListCap + e].slot;
-          tb.sc[slot].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
-        }
-      }
-    } else {
-      const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
-#pragma unroll
-      for (int j = 0; j < kEmitPer; ++j) {
-        const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
-        if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
-          tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
-      }
+    for (int j = 0; j < kEmitPer; ++j) {
+      const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
+      if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
+        tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
 }
 
-// the general emission, the limit-break rounds' and the predicted rounds'
-constexpr auto k_remit = k_remit_t<false, false>;
-constexpr auto k_remit_brk = k_remit_t<true, false>;
-constexpr auto k_remit_pred = k_remit_t<false, true>;
+// the general emission and the limit-break rounds'
+constexpr auto k_remit = k_remit_t<false>;
+constexpr auto k_remit_brk = k_remit_t<true>;
 
 // ---------------------------------------------------------------- k_rrank
 // One block per rank bin ranks it in LDS by (okey, slot, position); R bins
@@ -1910,7 +1778,9 @@ __global__ void __launch_bounds__(kBlockR)
 k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup,
         const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime = nullptr) {
   __shared__ BKey sh[kBinCapR];
-  __shared__ uint32_t s_hdr[4];  // the bin's records, its group and P-group offsets, P groups
+  // the bin's records, its group and P-group offsets, P groups, the round's
+  // outcome check
+  __shared__ uint32_t s_hdr[5];
   uint64_t t0 = wall_clock64();
   const uint32_t b = blockIdx.x;
   const bool isp = b >= (uint32_t)kNBPhase;
@@ -1922,7 +1792,7 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
   const uint32_t k = rd->k_total;
   const uint32_t p_runs = rd->p_runs;
   dmc_decision* const out = rd->out;
-  const bool fail = ovf0 || bovf || sfail;
+  const bool fail0 = ovf0 || bovf || sfail;
   if (threadIdx.x < 64) {
     // one level of loads: the 64 super-bin sums and the 64 bins of this
     // bin's super-bin (the rank-bin counters k_remit's walkers filled:
@@ -1938,11 +1808,33 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
         wsum32((lane < sb && psup ? sc : 0u) + (isp && lane < ib ? bc : 0u));
     const uint32_t tp = wsum32(psup ? sc : 0u);
     const uint32_t cnt = __shfl(bc, (int)ib);
+    // The round's outcome check (every block, from the same inputs: all
+    // agree): both phases' selections written by the pick; with the priority
+    // pulls running, every R-prefix entry emitted, and a round short of k
+    // only if the P threshold admitted every eligible client; without them,
+    // at least k R records.  A violation fails the round (overflow = 7:
+    // nothing is applied, the call returns DMC_EDEVICE) instead of
+    // dispatching short.  (dmclock_server.h:1115-1186: k pulls take
+    // min(k, eligible) requests.)
+    const uint32_t tz = wsum32(sz), tcr = wsum32(psup ? 0u : sc);
+    bool bad = false;
+    if (!fail0) {
+      const PhaseSel& p1 = rd->ph[1];
+      bad = rd->ph[0].valid != kSelValid || p1.valid != kSelValid;
+      if (!bad && p_runs) {
+        bad = (uint64_t)tcr != rd->n_r ||
+              (tz < k && !(p1.T == kMaxKey - 1 || (p1.T == 0 && p1.n_elig == 0)));
+      } else if (!bad) {
+        bad = tcr < k;
+      }
+    }
     if (b == 0) {
       // the round's totals and outcome (the summary k_rapply publishes)
-      const uint32_t tc = wsum32(sc), tz = wsum32(sz);
+      const uint32_t tc = wsum32(sc);
       if (lane == 0 && !ovf0) {
-        if (sfail) {
+        if (bad) {
+          rd->overflow = 7;
+        } else if (sfail) {
           rd->overflow = 3;  // re-run with the exact histogram
         } else if (bovf) {
           // re-run with fewer pulls or on the radix path: the emitted
@@ -1963,12 +1855,13 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
       s_hdr[1] = zoff;
       s_hdr[2] = poff;
       s_hdr[3] = tp;
+      s_hdr[4] = bad ? 1u : 0u;
       if (cnt > kBinMaxReport) atomicMax(&rd->bin_max[isp ? 1 : 0], cnt);
     }
   }
   __syncthreads();
   const uint32_t cnt = s_hdr[0];
-  if (cnt == 0 || fail) return;
+  if (cnt == 0 || fail0 || s_hdr[4]) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
   for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
   if (cnt > kRankSortMin) {

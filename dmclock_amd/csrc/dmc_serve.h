@@ -319,6 +319,22 @@ __device__ __attribute__((always_inline)) inline void serve_total(const StepRed*
   serve_block_reduce(a, sh);
 }
 
+// The answer: the command's sequence number after a release fence (the
+// decisions and counts in host-mapped memory before it); thread 0.
+__device__ __attribute__((always_inline)) inline void serve_publish(ServeIO* io, uint64_t seen,
+                                                                    uint64_t c_seen,
+                                                                    uint64_t c_read, bool trace) {
+  if (trace) {
+    io->clk[0] = c_seen;
+    io->clk[1] = c_read;
+    io->clk[2] = wall_clock64();
+    io->cyc[1] = __builtin_amdgcn_s_memtime();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (trace) io->clk[3] = wall_clock64();
+  __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(kServeThreads)
 k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_limit,
         uint32_t nregistered, unsigned long long* sched, uint64_t seq0,
@@ -336,6 +352,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
   uint64_t seen = seq0;  // (wave 0's)
   const uint64_t born = wall_clock64();
   uint64_t c_seen = 0, c_read = 0;
+  bool published = false;  // this command's answer is out (a pull's last decision)
   __syncthreads();
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0 polls: the command line, one load per poll
@@ -374,6 +391,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
     const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
     if (op == kServeAdd) ++tick;  // (++tick, :918: the host's count follows)
     const double now = s_now;
+    published = false;
     if (op == kServeAdd) {  // k_add_one
       // a request for a client with no request is its new front: inserted
       // into the group's summary (exact: nothing leaves it); otherwise the
@@ -401,6 +419,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       uint32_t n = 0, nres = 0, nprio = 0;
       int32_t type = DMC_NEXT_RETURNING;
       double when = 0.0;
+      published = false;
       while (n < s_k) {
         // the reservation heap's top: the group argmin of the groups' r
         // minima (lowest group on equal keys is the lowest slot; the tied
@@ -455,21 +474,32 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
           when = c.when;
           break;
         }
+        ++n;
+        (c.prio ? nprio : nres)++;
         if (threadIdx.x == 0) {
           s_c = c;
-          step_apply_body(tb, s_tick, &s_c, io->dec, n, sched);
-          if (trace && n == 0) io->phase[1] = wall_clock64();
+          step_apply_body(tb, s_tick, &s_c, io->dec, n - 1, sched);
+          if (trace && n == 1) io->phase[1] = wall_clock64();
+          if (n == s_k) {
+            // the call's last decision: answer first, re-summarise after
+            // (the host's next command waits for this loop anyway)
+            io->n = n;
+            io->n_res = nres;
+            io->n_prio = nprio;
+            io->type = type;
+            io->when = when;
+            serve_publish(io, seen, c_seen, c_read, trace);
+          }
         }
+        published = n == s_k;
         __syncthreads();
         const uint32_t g = c.slot >> gshift;
         group_summary<false>(tb, g, gshift, now, sh);
         if (threadIdx.x == 0) sg[g] = sh[kServeRes];
-        if (trace && threadIdx.x == 0 && n == 0) io->phase[2] = wall_clock64();
+        if (trace && threadIdx.x == 0 && n == 1) io->phase[2] = wall_clock64();
         __syncthreads();
-        ++n;
-        (c.prio ? nprio : nres)++;
       }
-      if (threadIdx.x == 0) {
+      if (threadIdx.x == 0 && !published) {
         io->n = n;
         io->n_res = nres;
         io->n_prio = nprio;
@@ -479,15 +509,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (trace) {
-        io->clk[0] = c_seen;
-        io->clk[1] = c_read;
-        io->clk[2] = wall_clock64();
-        io->cyc[1] = __builtin_amdgcn_s_memtime();
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      if (trace) io->clk[3] = wall_clock64();
-      __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (!published) serve_publish(io, seen, c_seen, c_read, trace);
       s_life = wall_clock64() - born > 5 * idle_ticks;
     }
     __syncthreads();

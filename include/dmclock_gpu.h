@@ -333,11 +333,9 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   pulls with k <= SMALL_K run the single-op path (one kernel per add,
                                   two per pull, results in host-mapped memory, one round trip);
                                   0: the general launch sequence */
-#define DMC_OPT_PREDICT 9       /* 1: a sampled bin-ranked round of the same k as the last ones
-                                  lists its candidates against thresholds predicted from theirs
-                                  (k_remit walks the lists, not the key columns; a miss re-runs the
-                                  round unpredicted); 0 (default): never -- measured slower at
-                                  config 3 */
+#define DMC_OPT_FAULT 9         /* test hook: 1 = the next rounds' pick leaves phase 1's selection
+                                  unset (each such round must fail its outcome check: DMC_EDEVICE,
+                                  never a short dispatch); 0 (default): off */
 #define DMC_OPT_SERVE 10        /* 1: single-op adds and pulls (as DMC_OPT_SINGLE_OP) are served by a
                                   persistent one-workgroup kernel polling host-mapped commands: no
                                   launch per call; the pull reduces per-group summaries of the
@@ -373,9 +371,9 @@ typedef struct dmc_counters {
   uint64_t bin_splits;      /* of the overflowed rounds: re-run as a smaller round   */
   uint64_t brk_rounds;      /* limit-break rounds started (AtLimit::Allow)           */
   uint64_t brk_fallbacks;   /* limit-break rounds whose state was not break-ready    */
-  uint64_t pred_rounds;     /* rounds run with predicted thresholds (DMC_OPT_PREDICT) */
-  uint64_t pred_misses;     /* ... re-run unpredicted (a threshold above the prediction,
-                               or a candidate list past its capacity)               */
+  uint64_t bad_rounds;      /* rounds that failed their outcome check (DMC_EDEVICE returned) */
+  uint64_t serve_yields;    /* times this queue's idle k_serve was stopped so that another
+                               queue's call need not wait behind it (DMC_OPT_SERVE) */
   uint64_t serve_calls;     /* single adds / pulls answered by the serve kernel (DMC_OPT_SERVE) */
   uint64_t serve_launches;  /* serve kernel launches (first call, after another call or idling) */
 } dmc_counters;

@@ -17,7 +17,12 @@
 // --serve: the facade and engine legs with DMC_OPT_SERVE (the persistent
 // serve kernel answers each single call; no launch per call).
 //
-// usage: latency N M [--no-oracle] [--no-facade] [--serve]
+// --queues Q: the engine leg on Q queues of N clients each, the rounds
+// dealt round-robin over them from this one thread (more serving queues than
+// the process's hardware queues: each call first stops the other queues'
+// idle serve kernels).
+//
+// usage: latency N M [--no-oracle] [--no-facade] [--serve] [--queues Q]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -92,7 +97,9 @@ int main(int argc, char** argv) {
   const uint32_t N = (uint32_t)std::atol(argv[1]);
   const uint32_t M = (uint32_t)std::atol(argv[2]);
   bool oracle = true, facade = true, serve = false;
+  uint32_t nq = 1;
   for (int i = 3; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--queues") && i + 1 < argc) nq = (uint32_t)std::atol(argv[++i]);
     if (!std::strcmp(argv[i], "--serve")) serve = true;
     if (!std::strcmp(argv[i], "--no-oracle")) oracle = false;
     if (!std::strcmp(argv[i], "--no-facade")) facade = false;
@@ -145,11 +152,12 @@ int main(int argc, char** argv) {
     p.ring_capacity = 64;
     p.max_batch = 1u << 16;
     p.at_limit = DMC_AT_LIMIT_WAIT;
-    dmc_queue* q = nullptr;
-    if (dmc_queue_create(&p, &q)) {
-      std::fprintf(stderr, "dmc_queue_create failed\n");
-      return 1;
-    }
+    std::vector<dmc_queue*> qs(nq, nullptr);
+    for (auto& q : qs)
+      if (dmc_queue_create(&p, &q)) {
+        std::fprintf(stderr, "dmc_queue_create failed\n");
+        return 1;
+      }
     std::vector<uint32_t> sl(N);
     std::vector<double> r(N), w(N), l(N);
     for (uint32_t c = 0; c < N; ++c) {
@@ -158,18 +166,22 @@ int main(int argc, char** argv) {
       w[c] = infos[c].w;
       l[c] = infos[c].l;
     }
-    dmc_client_register_batch(q, N, sl.data(), r.data(), w.data(), l.data(), 1);
-    if (serve) dmc_queue_set_option(q, DMC_OPT_SERVE, 1);
     std::vector<dmc_request> rq(N);
     for (uint32_t c = 0; c < N; ++c) rq[c] = dmc_request{c, 1, pre[c].t, 1, 1, c};
-    for (uint32_t a = 0; a < N; a += 1u << 16) {
-      uint32_t n = std::min<uint32_t>(1u << 16, N - a);
-      dmc_add_batch(q, n, rq.data() + a, nullptr);
+    for (auto q : qs) {
+      dmc_client_register_batch(q, N, sl.data(), r.data(), w.data(), l.data(), 1);
+      if (serve) dmc_queue_set_option(q, DMC_OPT_SERVE, 1);
+      for (uint32_t a = 0; a < N; a += 1u << 16) {
+        uint32_t n = std::min<uint32_t>(1u << 16, N - a);
+        dmc_add_batch(q, n, rq.data() + a, nullptr);
+      }
     }
     uint64_t h = N;
     dmc_decision d;
     dmc_pull_result res;
+    uint32_t i = 0;
     for (auto& o : ops) {
+      dmc_queue* q = qs[i++ % nq];
       dmc_request one{o.client, 1, o.t, 1, 1, h++};
       int32_t rc = 0;
       auto t0 = Clock::now();
@@ -180,7 +192,15 @@ int main(int argc, char** argv) {
       e_add.add(t0, t1);
       e_pull.add(t1, t2);
     }
-    dmc_queue_destroy(q);
+    for (auto q : qs) {
+      dmc_counters c{};
+      dmc_queue_counters(q, &c, 0);
+      if (nq > 1) std::fprintf(stderr, "queue: serve calls %llu launches %llu yields %llu\n",
+                               (unsigned long long)c.serve_calls,
+                               (unsigned long long)c.serve_launches,
+                               (unsigned long long)c.serve_yields);
+      dmc_queue_destroy(q);
+    }
   }
 
   if (oracle) {
@@ -215,11 +235,11 @@ int main(int argc, char** argv) {
     dmo_queue_destroy(q);
   }
 
-  std::printf("{\"serve\": %s, \"clients\": %u, \"rounds\": %u, \"facade_prepop_s\": %.3f, "
+  std::printf("{\"serve\": %s, \"queues\": %u, \"clients\": %u, \"rounds\": %u, \"facade_prepop_s\": %.3f, "
               "\"oracle_prepop_s\": %.3f, \"facade_add_us\": %s, \"facade_pull_us\": %s, "
               "\"engine_add_us\": %s, \"engine_pull_us\": %s, \"oracle_add_us\": %s, "
               "\"oracle_pull_us\": %s}\n",
-              serve ? "true" : "false", N, M, f_pre_s, o_pre_s, f_add.json().c_str(), f_pull.json().c_str(),
+              serve ? "true" : "false", nq, N, M, f_pre_s, o_pre_s, f_add.json().c_str(), f_pull.json().c_str(),
               e_add.json().c_str(), e_pull.json().c_str(), o_add.json().c_str(),
               o_pull.json().c_str());
   return 0;

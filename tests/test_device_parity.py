@@ -140,21 +140,35 @@ def test_fused_bench_call_parity_1m_clients():
     qg.close()
 
 
-def test_predicted_rounds_parity():
-    """DMC_OPT_PREDICT (off by default: measured slower): the
-    fused call's round lists, in k_rscan, the slots whose keys fall under
-    thresholds predicted from the previous rounds, and k_remit walks those
-    lists instead of the key columns; a round whose picked thresholds exceed
-    the prediction re-runs unpredicted.  Config 3 at full size, every
-    decision bit-exact, and the predicted rounds counted."""
-    from dmclock_amd._abi import OPT_PREDICT
-    tr = workloads.config3_trace(42, 1 << 20, 8, 1 << 16, depth=2)
-    n, qg, qo = device_parity(tr, options=[(OPT_PREDICT, 1)])
-    c = qg.counters()
-    assert c["fused_calls"] == 8, c
-    assert c["pred_rounds"] >= 5, c
-    assert c["pred_misses"] < c["pred_rounds"], c
-    qg.close()
+def test_unset_phase_selection_fails_loudly():
+    """A round whose pick leaves a phase's selection unset (the failure a
+    k_remit block-size mismatch once caused: a 512-thread build dispatched
+    469,585 of 1,310,720 decisions with status OK) must fail its outcome
+    check in k_rrank: the call returns DMC_EDEVICE, nothing is dispatched,
+    and bad_rounds counts it.  DMC_OPT_FAULT=1 injects exactly that (phase
+    1's PhaseSel left unwritten) in both the eager and the graph path; with
+    the hook off, the same queue dispatches again."""
+    import torch
+    from dmclock_amd._abi import OPT_FAULT
+    from dmclock_amd.gpu import DmcError, GpuQueue
+    tr = workloads.config3_trace(7, 1 << 16, 3, 1 << 12, depth=2)
+    c = tr.clients
+    q = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 16)
+    q.register(c.slots, c.r, c.w, c.l, c.active)
+    q.add_batch(tr.ops[0][1])
+    q.set_option(OPT_FAULT, 1)
+    now = tr.ops[1][1]
+    for _ in range(3):  # eager, then the captured graph (second sighting on)
+        with pytest.raises(DmcError, match=r"\(-3\)"):
+            q.pull_batch(now, 4096)
+    cnt = q.counters()
+    assert cnt["bad_rounds"] == 3, cnt
+    assert cnt["decisions"] == 0, cnt
+    q.set_option(OPT_FAULT, 0)
+    d, res = q.pull_batch(now, 4096)
+    assert res.n_decisions == 4096 and len(d) == 4096
+    torch.cuda.synchronize()
+    q.close()
 
 
 def _bench_setup(q, tr):
