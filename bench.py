@@ -169,6 +169,9 @@ def parse():
                          "the previous two steps")
     ap.add_argument("--servers", type=int, default=8,
                     help="config 5: server queues per GPU")
+    ap.add_argument("--separate-queues", action="store_true",
+                    help="config 5: drive each server queue from its own host "
+                         "thread and stream instead of one queue-group step")
     ap.add_argument("--epoch-steps", type=int, default=16,
                     help="config 5: steps per delta/rho epoch (16 x 64K = 1M "
                          "decisions per server)")

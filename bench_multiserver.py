@@ -15,9 +15,11 @@ is filled by get_req_params on the device right before its add; every
 decision is tallied per slot; every --epoch-steps steps the per-client
 response sums are collected, all-reduced over the ranks (RCCL over xGMI,
 int32 sum of 2 x 16M counters) and delivered.  A "step" is, on every server
-of every rank concurrently (one host thread per server, one HIP stream per
-queue): fill delta/rho for the next 64K arrivals, add them, pull 64K
-decisions at the batch's last arrival, tally.  The epoch delivery
+of every rank: fill delta/rho for the next 64K arrivals, add them, pull 64K
+decisions at the batch's last arrival, tally -- by default one queue-group
+step (dmc_group_step_device: one launch per kernel over the rank's S server
+tables, one graph), with --separate-queues one host thread and HIP stream
+per queue, each server its own fill + fused call + tally.  The epoch delivery
 (collect + all-reduce + advance) is inside the timed region.
 
 value = (adds + decisions) of all servers of all ranks / max-over-ranks time.
@@ -105,7 +107,7 @@ def cpu_baseline_multi(args, wl, n_steps):
 def main(args):
     import torch
     from dmclock_amd._abi import DECISION_DTYPE, PullResult
-    from dmclock_amd.multiserver import DeviceTrackers, make_queues
+    from dmclock_amd.multiserver import DeviceTrackers, GpuGroup, make_queues
     from bench import METRIC
 
     from bench import rank_env
@@ -177,9 +179,21 @@ def main(args):
         q.sync()
 
     pool = ThreadPoolExecutor(S)
+    group = None if args.separate_queues else GpuGroup(queues)
+    gtrk = trk.group_trackers()
+    g_args = [([d_steps[s][i].data_ptr() for s in range(S)], [nows[s][i] for s in range(S)],
+               [d_res[s, i].data_ptr() for s in range(S)])
+              for i in range(n_steps + n_prof)]
+    g_rc = [d_rc[s].data_ptr() for s in range(S)]
+    g_out = [d_out[s].data_ptr() for s in range(S)]
 
     def segment(i0, i1):
-        list(pool.map(lambda s: run(s, i0, i1), range(S)))
+        if group is None:
+            list(pool.map(lambda s: run(s, i0, i1), range(S)))
+            return
+        for i in range(i0, i1):
+            reqs, nw, res = g_args[i]
+            group.step(args.batch, reqs, g_rc, nw, k, g_out, res, gtrk)
 
     t_prep = time.perf_counter()
     settle = list(pool.map(prepare, range(S)))[0]
@@ -212,6 +226,10 @@ def main(args):
         dist.barrier()
     dt = time.perf_counter() - t0
     pool.shutdown()
+    grp_ctr = None
+    if group is not None:
+        grp_ctr = {"fused_calls": sum(q.counters()["fused_calls"] for q in queues),
+                   "graph_replays": sum(q.counters()["graph_replays"] for q in queues)}
 
     # roofline: server 0's next n_prof steps alone (no other queue running),
     # stage-timed like config 3 (HIP events around each stage on its stream)
@@ -280,8 +298,10 @@ def main(args):
                    "adds_per_step_per_server": args.batch,
                    "pulls_per_step_per_server": k, "epoch_steps": E,
                    "ring_capacity": args.ring, "settle_pulls": settle,
-                   "parallelism": f"{world} rank(s) x {S} queues, one host "
-                                  f"thread + HIP stream per queue"},
+                   "parallelism": (f"{world} rank(s) x {S} queues, one host "
+                                   f"thread + HIP stream per queue" if group is None else
+                                   f"{world} rank(s) x one queue group of {S} tables "
+                                   f"(one launch per kernel over all tables)")},
         "decisions_per_s": round(n_dec / dt, 1),
         "tag_updates_per_s": round(n_adds / dt, 1),
         "epochs_timed": len(epochs),
@@ -290,6 +310,7 @@ def main(args):
         "tracker_known_frac": round(float(st["known"].mean()), 4),
         "setup_s": {"generate": round(t_gen, 1), "prepopulate": round(t_prep, 1)},
         "roofline": roof,
+        "group_counters": grp_ctr,
         "cpu_baseline": (None if args.no_cpu_baseline or world > 1 else
                          cpu_baseline_multi(args, wl, n_steps)),
     }

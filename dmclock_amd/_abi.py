@@ -157,3 +157,10 @@ def make_requests(slots, times, costs=1, deltas=1, rhos=1, handles=None):
         handles = np.arange(n, dtype=np.uint64)
     out["handle"] = np.broadcast_to(np.asarray(handles, dtype=np.uint64), (n,))
     return out
+
+
+class GroupTracker(ctypes.Structure):
+    """dmc_group_tracker: one server's device tracker state for a group step"""
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "client_of_slot", "gdelta", "grho", "xd", "xr", "known", "first",
+        "comp_delta", "comp_rho")]

@@ -146,9 +146,7 @@ __global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_
 // The first node of an add segment: its arguments are the segment's per-call
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
-__global__ void k_add_link(AddParams p, Table tb,
-                           uint32_t* abuf, uint32_t* apos, uint32_t* aslot,
-                           AddParams* pblk, ActBuf act = ActBuf{}) {
+__device__ __attribute__((always_inline)) inline void add_link_body(AddParams p, Table tb, uint32_t* abuf, uint32_t* apos, uint32_t* aslot, AddParams* pblk, ActBuf act) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *pblk = p;
   if (i >= p.n) return;
@@ -169,10 +167,14 @@ __global__ void k_add_link(AddParams p, Table tb,
   // (filing order 0 replays the client's requests and knows its own position)
   if (pos - 1u < kAddSlots - 1u) abuf[(size_t)s * kAddSlots + pos] = i;
 }
+__global__ void 
+k_add_link(AddParams p, Table tb,
+                           uint32_t* abuf, uint32_t* apos, uint32_t* aslot,
+                           AddParams* pblk, ActBuf act = ActBuf{}) {
+  add_link_body(p, tb, abuf, apos, aslot, pblk, act);
+}
 
-__global__ void k_add_chain(Table tb, const AddParams* pblk,
-                            const uint32_t* abuf, const uint32_t* apos,
-                            const uint32_t* aslot, ActBuf act = ActBuf{}) {
+__device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // one level of loads: the call's parameters and this position's filing
   // (apos / aslot are padded to whole blocks: in bounds for the grid)
@@ -188,6 +190,29 @@ __global__ void k_add_chain(Table tb, const AddParams* pblk,
   // the next: the client's batch count with its state
   AddState st;
   add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, true);
+}
+__global__ void 
+k_add_chain(Table tb, const AddParams* pblk,
+                            const uint32_t* abuf, const uint32_t* apos,
+                            const uint32_t* aslot, ActBuf act = ActBuf{}) {
+  add_chain_body(tb, pblk, abuf, apos, aslot, act);
+}
+
+// (multi-table: per-table arguments of a queue group's add kernels, indexed
+// by blockIdx.y; dmc_round.h's multi-table rounds)
+struct AddArgs {
+  AddParams p;
+  Table tb;
+  uint32_t *abuf, *apos, *aslot;
+  AddParams* pblk;
+};
+__global__ void k_add_link_m(const AddArgs* a) {
+  const AddArgs& x = a[blockIdx.y];
+  add_link_body(x.p, x.tb, x.abuf, x.apos, x.aslot, x.pblk, ActBuf{});
+}
+__global__ void k_add_chain_m(const AddArgs* a) {
+  const AddArgs& x = a[blockIdx.y];
+  add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{});
 }
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
@@ -1584,6 +1609,10 @@ namespace {
 struct dmc_queue {
   dmc_queue_params p{};
   hipStream_t stream = nullptr;
+  // a member of a queue group (dmc_group_create) runs on the group's stream;
+  // its own is kept here and restored when the group is destroyed
+  hipStream_t own_stream = nullptr;
+  dmc_group* group = nullptr;
   Table tb{};
   std::mutex mtx;  // C-ABI calls on one handle are serialised (data_mtx, :762)
   // host mirrors
@@ -1734,6 +1763,35 @@ struct dmc_queue {
   double prof_ms[DMC_PROF_NSTAGES] = {};
   uint64_t prof_cnt[DMC_PROF_NSTAGES] = {};
 };
+
+// A queue group (dmc_group_create, dmc_group_step_device below).
+struct dmc_group {
+  std::vector<dmc_queue*> qs;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // per-step kernel arguments: pinned staging and its device copy (one
+  // memcpy per step, the graph's first node), S entries per kernel
+  uint8_t* h_blob = nullptr;
+  uint8_t* d_blob = nullptr;
+  size_t bytes = 0, o_trk = 0, o_add = 0, o_scan = 0, o_hist = 0, o_emit = 0, o_rank = 0,
+         o_apply = 0, o_tally = 0, tally_bytes = 0;
+  struct G {
+    uint64_t key = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  } graphs[4];
+  uint64_t seen[4] = {0, 0, 0, 0};
+  uint32_t seen_pos = 0, graph_next = 0;
+  uint64_t steps = 0, fused_steps = 0, graph_launches = 0;
+};
+
+void group_graphs_destroy(dmc_group* g) {
+  for (auto& x : g->graphs) {
+    if (x.exec) (void)hipGraphExecDestroy(x.exec);
+    if (x.graph) (void)hipGraphDestroy(x.graph);
+    x = dmc_group::G{};
+  }
+}
 
 // Every entry point of a queue holds its mutex (the reference's data_mtx) and
 // makes the queue's device current for the calling thread, so that servers
@@ -3402,6 +3460,14 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   (void)hipSetDevice(q->p.device);
+  if (q->group) {  // (the group keeps running its other members)
+    dmc_group* g = q->group;
+    (void)hipStreamSynchronize(q->stream);
+    g->qs.erase(std::find(g->qs.begin(), g->qs.end(), q));
+    group_graphs_destroy(g);
+    q->stream = q->own_stream;
+    q->group = nullptr;
+  }
   if (q->serve_reg) serve_register(q, false);
   if (q->h_serve && !q->wedged) (void)serve_quiesce(q);
   if (q->serve_trace && q->ctr.serve_calls) {
@@ -4071,6 +4137,288 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
   int rc = dmc_add_batch_device(q, n, d_reqs, d_rc_out);
   if (rc) return rc;
   return dmc_pull_batch_device(q, now, k, d_out, d_result);
+}
+
+
+// ================================================================ queue groups
+// S server queues of one device driven as one: a group step is, for every
+// member, get_req_params for the batch (optional device trackers), n
+// add_request_time and k pull_request(now) -- each member exactly what
+// dmc_tracker_fill + dmc_add_pull_batch_device + dmc_tracker_tally do on
+// it alone -- with one launch per kernel over all members (blockIdx.y =
+// member, dmc_round.h's multi-table kernels) captured as one hipGraph.
+// Members run on the group's stream while they belong to it.
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// the members' locks, in member order (a group's members are locked together
+// only here; every other call locks one queue)
+struct GroupLock {
+  std::vector<std::unique_lock<std::mutex>> ls;
+  int rc = DMC_OK;
+  explicit GroupLock(dmc_group* g) {
+    (void)hipSetDevice(g->device);
+    for (dmc_queue* q : g->qs) ls.emplace_back(q->mtx);
+    for (dmc_queue* q : g->qs) {
+      if (q->wedged) rc = DMC_EDEVICE;
+      else if (int e = serve_quiesce(q)) rc = e;
+    }
+  }
+};
+
+}  // namespace
+
+int dmc_group_create(dmc_queue* const* queues, uint32_t n, dmc_group** out) {
+  if (!queues || !n || !out) return DMC_EINVAL;
+  const dmc_queue_params& p0 = queues[0]->p;
+  for (uint32_t i = 0; i < n; ++i) {
+    const dmc_queue* q = queues[i];
+    if (!q || q->group || q->p.device != p0.device || q->p.max_clients != p0.max_clients ||
+        q->p.ring_capacity != p0.ring_capacity)
+      return DMC_EINVAL;
+    for (uint32_t j = 0; j < i; ++j)
+      if (queues[j] == q) return DMC_EINVAL;
+  }
+  dmc_group* g = new dmc_group();
+  g->device = p0.device;
+  g->qs.assign(queues, queues + n);
+  (void)hipSetDevice(g->device);
+  const size_t S = n;
+  size_t o = 0;
+  auto take = [&](size_t sz) {
+    const size_t at = o;
+    o = align_up(o + sz * S, 64);
+    return at;
+  };
+  g->o_trk = take(sizeof(TrackArgs));
+  g->o_add = take(sizeof(AddArgs));
+  g->o_scan = take(sizeof(RScanArgs));
+  g->o_hist = take(sizeof(RHistArgs));
+  g->o_emit = take(sizeof(REmitArgs));
+  g->o_rank = take(sizeof(RRankArgs));
+  g->o_apply = take(sizeof(RApplyArgs));
+  g->bytes = o;
+  g->o_tally = take(sizeof(TallyArgs));
+  g->tally_bytes = o - g->o_tally;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&g->h_blob, o, 0) != hipSuccess ||
+      hipMalloc((void**)&g->d_blob, o) != hipSuccess) {
+    dmc_group_destroy(g);
+    return DMC_ENOMEM;
+  }
+  std::memset(g->h_blob, 0, o);
+  for (dmc_queue* q : g->qs) {
+    QueueLock l(q);
+    if (l.rc || hipStreamSynchronize(q->stream) != hipSuccess) {
+      dmc_group_destroy(g);
+      return DMC_EDEVICE;
+    }
+    q->own_stream = q->stream;
+    q->stream = g->stream;
+    q->group = g;
+  }
+  *out = g;
+  return DMC_OK;
+}
+
+int dmc_group_destroy(dmc_group* g) {
+  if (!g) return DMC_EINVAL;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (dmc_queue* q : g->qs) {
+    if (!q || q->group != g) continue;
+    std::lock_guard<std::mutex> l(q->mtx);
+    q->stream = q->own_stream;
+    q->own_stream = nullptr;
+    q->group = nullptr;
+  }
+  group_graphs_destroy(g);
+  if (g->h_blob) (void)hipHostFree(g->h_blob);
+  dfree(g->d_blob);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+  return DMC_OK;
+}
+
+void* dmc_group_stream(dmc_group* g) { return g ? (void*)g->stream : nullptr; }
+
+int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
+                          int32_t* const* d_rc, const double* now, uint32_t k,
+                          dmc_decision* const* d_out, dmc_pull_result* const* d_result,
+                          const dmc_group_tracker* trk) {
+  if (!g || !now || (n && (!d_reqs || !d_rc)) || (k && !d_out)) return DMC_EINVAL;
+  const uint32_t S = (uint32_t)g->qs.size();
+  for (uint32_t i = 0; i < S; ++i)
+    if ((n && (!d_reqs[i] || !d_rc[i])) || (k && !d_out[i])) return DMC_EINVAL;
+  bool fuse = n && k;
+  {
+    GroupLock gl(g);
+    if (gl.rc) return gl.rc;
+    ++g->steps;
+    for (dmc_queue* q : g->qs) {
+      ++q->gen;
+      if (int rc0 = settle_act(q)) return rc0;
+      fuse = fuse && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k && !q->force_radix &&
+             q->radix_batches == 0 && k <= kBinRankMaxK && q->use_graphs && !q->prof_on;
+    }
+    if (fuse) {
+      for (dmc_queue* q : g->qs) {
+        int rc = ensure_batch(q, n);
+        if (!rc) rc = ensure_brec(q);
+        if (rc) return rc;
+      }
+      TrackArgs* ta = reinterpret_cast<TrackArgs*>(g->h_blob + g->o_trk);
+      AddArgs* aa = reinterpret_cast<AddArgs*>(g->h_blob + g->o_add);
+      RScanArgs* sa = reinterpret_cast<RScanArgs*>(g->h_blob + g->o_scan);
+      RHistArgs* ha = reinterpret_cast<RHistArgs*>(g->h_blob + g->o_hist);
+      REmitArgs* ea = reinterpret_cast<REmitArgs*>(g->h_blob + g->o_emit);
+      RRankArgs* ra = reinterpret_cast<RRankArgs*>(g->h_blob + g->o_rank);
+      RApplyArgs* pa = reinterpret_cast<RApplyArgs*>(g->h_blob + g->o_apply);
+      bool all_sampled = true;
+      uint32_t gN = 0, gEm = 0;
+      for (uint32_t i = 0; i < S; ++i) {
+        dmc_queue* q = g->qs[i];
+        const Table& tb = q->tb;
+        const uint32_t N = tb.n;
+        gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
+        gEm = (N + kEmitChunk - 1) / kEmitChunk;
+        const bool sampled = use_sample(q, false);
+        all_sampled = all_sampled && sampled;
+        ta[i] = trk ? TrackArgs{d_reqs[i], n, q->p.max_clients, trk[i].client_of_slot,
+                                trk[i].gdelta, trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
+                                trk[i].first}
+                    : TrackArgs{};
+        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, 0}, tb, q->abuf, q->apos,
+                        q->aslot, q->apblk};
+        const CallParams cp{k, 0, now[i], d_out[i], q->tick + n,
+                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, 0};
+        sa[i] = RScanArgs{tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
+                          q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
+                          sampled ? q->skp : nullptr, q->k32, q->hist};
+        ha[i] = sampled ? RHistArgs{(N + kSample - 1) / kSample, gN, q->skr, q->skp, q->rparts,
+                                    q->rd, q->hist, q->sample_mode == 2 ? 2 : 1,
+                                    (unsigned long long*)q->bcount, q->bsup}
+                        : RHistArgs{N, gN, q->keyr, q->keyp, q->rparts, q->rd, q->hist, 0,
+                                    (unsigned long long*)q->bcount, q->bsup};
+        ea[i] = REmitArgs{tb, q->rd, q->k32, q->meta, q->cand, q->bcand, q->post, q->decof,
+                          q->brec, q->bcount, q->bsup, q->hist, q->dense, q->ecap};
+        ra[i] = RRankArgs{q->rd, (const unsigned long long*)q->bcount, q->bsup, q->brec, tb.ring,
+                          q->decof};
+        pa[i] = RApplyArgs{tb, q->rd, q->cand, q->bcand, q->decof, q->post, q->sched,
+                           q->d_hround};
+      }
+      const uint32_t gHist = all_sampled ? kHistBlocksSampled : kHistBlocksR;
+      const uint32_t gAdd = (n + kBlock - 1) / kBlock;
+      uint8_t* d = g->d_blob;
+      auto enqueue = [&] {
+        (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, g->stream);
+        if (trk) {
+          hipLaunchKernelGGL(k_track_first_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+                             (const TrackArgs*)(d + g->o_trk));
+          hipLaunchKernelGGL(k_track_params_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+                             (const TrackArgs*)(d + g->o_trk));
+        }
+        hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+                           (const AddArgs*)(d + g->o_add));
+        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+                           (const AddArgs*)(d + g->o_add));
+        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, g->stream,
+                           (const RScanArgs*)(d + g->o_scan));
+        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, g->stream,
+                           (const RHistArgs*)(d + g->o_hist));
+        hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, g->stream,
+                           (const REmitArgs*)(d + g->o_emit));
+        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kBlockR), 0, g->stream,
+                           (const RRankArgs*)(d + g->o_rank));
+        hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmit * gEm + 1, S), dim3(kBlockR), 0,
+                           g->stream, (const RApplyArgs*)(d + g->o_apply));
+      };
+      // the step's graph: captured at the second sighting of its shape, then
+      // replayed (the arguments travel in the blob, no node updates)
+      const uint64_t key = ((uint64_t)n << 8) | (trk ? 1 : 0) | (all_sampled ? 2 : 0) |
+                           ((uint64_t)k << 36);
+      dmc_group::G* gr = nullptr;
+      for (auto& x : g->graphs)
+        if (x.exec && x.key == key) gr = &x;
+      if (!gr) {
+        bool seen = false;
+        for (uint64_t s0 : g->seen) seen |= s0 == key;
+        if (seen) {
+          dmc_group::G& x = g->graphs[g->graph_next++ % 4];
+          if (x.exec) HIP_OK(hipStreamSynchronize(g->stream));
+          if (x.exec) (void)hipGraphExecDestroy(x.exec);
+          if (x.graph) (void)hipGraphDestroy(x.graph);
+          x = dmc_group::G{};
+          HIP_OK(hipStreamBeginCapture(g->stream, hipStreamCaptureModeThreadLocal));
+          enqueue();
+          HIP_OK(hipStreamEndCapture(g->stream, &x.graph));
+          HIP_OK(hipGraphInstantiate(&x.exec, x.graph, nullptr, nullptr, 0));
+          x.key = key;
+          gr = &x;
+        } else {
+          g->seen[g->seen_pos++ % 4] = key;
+        }
+      }
+      if (gr) {
+        HIP_OK(hipGraphLaunch(gr->exec, g->stream));
+        ++g->graph_launches;
+      } else {
+        enqueue();
+      }
+      HIP_OK(hipGetLastError());
+      ++g->fused_steps;
+      for (dmc_queue* q : g->qs) {
+        q->tick += n;
+        ++q->ctr.fused_calls;
+      }
+      // each member's round: its outcome, and any follow-up (a re-run, the
+      // terminal pull) on the group stream
+      for (uint32_t i = 0; i < S; ++i) {
+        dmc_queue* q = g->qs[i];
+        dmc_pull_result r{};
+        bool dev_wrote = false;
+        dmc_pull_result* dres = d_result ? d_result[i] : nullptr;
+        int rc = pull_impl(q, now[i], k, d_out[i], &r, dres, &dev_wrote, true);
+        if (rc) return rc;
+        if (dres && !dev_wrote) {
+          hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, dres, r);
+          HIP_OK(hipGetLastError());
+        }
+      }
+      if (trk && d_result) {
+        TallyArgs* la = reinterpret_cast<TallyArgs*>(g->h_blob + g->o_tally);
+        for (uint32_t i = 0; i < S; ++i)
+          la[i] = TallyArgs{d_out[i], d_result[i], k, trk[i].comp_delta, trk[i].comp_rho};
+        HIP_OK(hipMemcpyAsync(g->d_blob + g->o_tally, la, g->tally_bytes, hipMemcpyHostToDevice,
+                              g->stream));
+        hipLaunchKernelGGL(k_tally_m, dim3(grid_for(k, 1024), S), dim3(kBlock), 0, g->stream,
+                           (const TallyArgs*)(g->d_blob + g->o_tally));
+        HIP_OK(hipGetLastError());
+      }
+      return DMC_OK;
+    }
+  }
+  // not fusable (activations pending, small k, ...): each member on its own,
+  // the same calls in the same order, on the group stream
+  for (uint32_t i = 0; i < S; ++i) {
+    dmc_queue* q = g->qs[i];
+    if (trk && n) {
+      int rc = dmc_tracker_fill(q, d_reqs[i], n, trk[i].client_of_slot, trk[i].gdelta,
+                                trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known, trk[i].first);
+      if (rc) return rc;
+    }
+    int rc = dmc_add_pull_batch_device(q, n, d_reqs[i], d_rc ? d_rc[i] : nullptr, now[i], k,
+                                       d_out ? d_out[i] : nullptr,
+                                       d_result ? d_result[i] : nullptr);
+    if (rc) return rc;
+    if (trk && k && d_result) {
+      rc = dmc_tracker_tally(q, d_out[i], d_result[i], k, trk[i].comp_delta, trk[i].comp_rho);
+      if (rc) return rc;
+    }
+  }
+  return DMC_OK;
 }
 
 int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,

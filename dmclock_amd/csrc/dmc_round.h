@@ -470,10 +470,7 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
 template <bool BRK>
-__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
-k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
-          RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
-          uint2* k32, uint32_t* hist) {
+__device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.fault = cp.fault;
@@ -558,6 +555,13 @@ k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
     if (threadIdx.x == 0) parts[blockIdx.x] = o;
   }
 }
+template <bool BRK>
+__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
+k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
+          RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp,
+          uint2* k32, uint32_t* hist) {
+  rscan_t_body<BRK>(tb, keyr, keyp, meta, parts, rd, cp, skr, skp, k32, hist);
+}
 
 // the general scan (the graphs' parameter node) and the limit-break scan
 constexpr auto k_rscan = k_rscan_t<false>;
@@ -605,10 +609,7 @@ constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of
 // need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
 // every k_remit block picks the thresholds and rank bins from it (no block
 // ticket, no last-block tail here).  Block 0 stores the round's totals.
-__global__ void __launch_bounds__(1024)
-k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
-        unsigned long long* bcount, unsigned long long* gsup) {
+__device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
   __shared__ uint32_t lh[2][kHistBinsR];
 
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
@@ -681,6 +682,12 @@ k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart*
     if (i < (uint32_t)kNBR) bcount[i] = 0ull;
     else gsup[i - kNBR] = 0ull;
   }
+}
+__global__ void __launch_bounds__(1024)
+k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
+        uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
+        unsigned long long* bcount, unsigned long long* gsup) {
+  rhist_body(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
 }
 
 // Threshold and rank-bin table of one phase, by one half (kPickHalf
@@ -1366,12 +1373,7 @@ constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
 #define DMC_EMIT_MINW 4
 #endif
 template <bool BRK>
-__global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW)
-k_remit_t(Table tb, Round* rd, const uint2* k32,
-        const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
-        uint32_t* decof, BRecR* brec,
-        uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
-        uint32_t dcap, uint64_t* eclk = nullptr) {
+__device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap, uint64_t* eclk) {
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
@@ -1547,6 +1549,15 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
     }
   }
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
+}
+template <bool BRK>
+__global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW)
+k_remit_t(Table tb, Round* rd, const uint2* k32,
+        const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post,
+        uint32_t* decof, BRecR* brec,
+        uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
+        uint32_t dcap, uint64_t* eclk = nullptr) {
+  remit_t_body<BRK>(tb, rd, k32, meta, cand, bcand, post, decof, brec, bcount, gsup, hist, dense, dcap, eclk);
 }
 
 // the general emission and the limit-break rounds'
@@ -1774,9 +1785,7 @@ __device__ inline bool sample_failed(const Round* rd) {
 // this size only (a handful per round; an overflowing bin always)
 constexpr uint32_t kBinMaxReport = 128;
 
-__global__ void __launch_bounds__(kBlockR)
-k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup,
-        const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime = nullptr) {
+__device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime) {
   __shared__ BKey sh[kBinCapR];
   // the bin's records, its group and P-group offsets, P groups, the round's
   // outcome check
@@ -1884,6 +1893,11 @@ k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* g
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
   }
+}
+__global__ void __launch_bounds__(kBlockR)
+k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup,
+        const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime = nullptr) {
+  rrank_body(rd, bcount, gsup, brec, ring, decof, wtime);
 }
 
 // ---------------------------------------------------------------- radix path
@@ -2298,10 +2312,7 @@ constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 // 256-thread blocks per CU needs; a higher bound only warns)
 #define DMC_APPLY_MINB 2
 #endif
-__global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
-k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
-         const uint32_t* decof, const PostRec* post, unsigned long long* sched,
-         HostRound* h, uint64_t* dbg = nullptr) {
+__device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg) {
   // A limit-break round's priority pops (group heads and their runs'
   // readied fronts) are counted here: its summary goes out once every block
   // has counted (a ticket), not from the extra block at once
@@ -2369,8 +2380,98 @@ k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
   __syncthreads();
   rfinish_body(rd, h);
 }
+__global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
+k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
+         const uint32_t* decof, const PostRec* post, unsigned long long* sched,
+         HostRound* h, uint64_t* dbg = nullptr) {
+  rapply_body(tb, rd, cand, bcand, decof, post, sched, h, dbg);
+}
 
 __global__ void k_rfinish(const Round* rd, HostRound* h) { rfinish_body(rd, h); }
+
+// ------------------------------------------------------- multi-table rounds
+// One launch per kernel over the S server tables of a queue group
+// (dmc_group, config 5's per-GPU shape: servers are independent queues,
+// sim/src/simulate.h:118-136): blockIdx.y selects the table, whose arguments
+// the kernel reads from a device array; blockIdx.x / gridDim.x keep their
+// per-table meaning, so each body is exactly the single-table kernel's.
+// The latency-bound walkers of all tables overlap, and a step of S servers
+// is one graph of seven launches instead of S x seven.
+struct RScanArgs {
+  Table tb;
+  uint64_t *keyr, *keyp;
+  uint32_t* meta;
+  RoundPart* parts;
+  Round* rd;
+  CallParams cp;
+  uint64_t *skr, *skp;
+  uint2* k32;
+  uint32_t* hist;
+};
+struct RHistArgs {
+  uint32_t n, nparts;
+  const uint64_t *keyr, *keyp;
+  const RoundPart* parts;
+  Round* rd;
+  uint32_t* hist;
+  int sampled;
+  unsigned long long *bcount, *gsup;
+};
+struct REmitArgs {
+  Table tb;
+  Round* rd;
+  const uint2* k32;
+  const uint32_t* meta;
+  CandRec* cand;
+  uint32_t* bcand;
+  PostRec* post;
+  uint32_t* decof;
+  BRecR* brec;
+  uint32_t* bcount;
+  unsigned long long* gsup;
+  const uint32_t* hist;
+  DEnt* dense;
+  uint32_t dcap;
+};
+struct RRankArgs {
+  Round* rd;
+  const unsigned long long *bcount, *gsup;
+  const BRecR* brec;
+  ReqEntry* ring;
+  uint32_t* decof;
+};
+struct RApplyArgs {
+  Table tb;
+  Round* rd;
+  const CandRec* cand;
+  const uint32_t *bcand, *decof;
+  const PostRec* post;
+  unsigned long long* sched;
+  HostRound* h;
+};
+
+__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_m(const RScanArgs* a) {
+  const RScanArgs& x = a[blockIdx.y];
+  rscan_t_body<false>(x.tb, x.keyr, x.keyp, x.meta, x.parts, x.rd, x.cp, x.skr, x.skp, x.k32,
+                      x.hist);
+}
+__global__ void __launch_bounds__(1024) k_rhist_m(const RHistArgs* a) {
+  const RHistArgs& x = a[blockIdx.y];
+  rhist_body(x.n, x.keyr, x.keyp, x.parts, x.nparts, x.rd, x.hist, x.sampled, x.bcount, x.gsup);
+}
+__global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const REmitArgs* a) {
+  const REmitArgs& x = a[blockIdx.y];
+  remit_t_body<false>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof, x.brec,
+                      x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
+}
+__global__ void __launch_bounds__(kBlockR) k_rrank_m(const RRankArgs* a) {
+  const RRankArgs& x = a[blockIdx.y];
+  rrank_body(x.rd, x.bcount, x.gsup, x.brec, x.ring, x.decof, nullptr);
+}
+__global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB) k_rapply_m(const RApplyArgs* a) {
+  const RApplyArgs& x = a[blockIdx.y];
+  rapply_body(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr);
+}
 
 // device-API result written by the host's view of a multi-round call
 __global__ void k_put_result(dmc_pull_result* res, dmc_pull_result r) { *res = r; }

@@ -32,8 +32,8 @@
 namespace dmc {
 
 // per-slot completion tallies of one server's decisions (track_resp's cost)
-__global__ void k_tally(const dmc_decision* dec, const dmc_pull_result* res,
-                        uint32_t cap, uint32_t* comp_d, uint32_t* comp_r) {
+__device__ inline void tally_body(const dmc_decision* dec, const dmc_pull_result* res,
+                                  uint32_t cap, uint32_t* comp_d, uint32_t* comp_r) {
   uint32_t n = res->n_decisions < cap ? res->n_decisions : cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += gridDim.x * blockDim.x) {
@@ -41,6 +41,10 @@ __global__ void k_tally(const dmc_decision* dec, const dmc_pull_result* res,
     atomicAdd(&comp_d[d.slot], d.cost);
     if (d.phase == DMC_PHASE_RESERVATION) atomicAdd(&comp_r[d.slot], d.cost);
   }
+}
+__global__ void k_tally(const dmc_decision* dec, const dmc_pull_result* res,
+                        uint32_t cap, uint32_t* comp_d, uint32_t* comp_r) {
+  tally_body(dec, res, cap, comp_d, comp_r);
 }
 
 // first batch position of each (server, client) in the batch
@@ -53,12 +57,11 @@ __global__ void k_track_first(const dmc_request* reqs, uint32_t n, uint32_t nslo
 }
 
 // get_req_params for every request of the batch (one server)
-__global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
-                               const uint32_t* client_of_slot,
-                               const uint32_t* gd, const uint32_t* gr,
-                               uint32_t* xd, uint32_t* xr, uint8_t* known,
-                               uint32_t* first) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ inline void track_params_one(dmc_request* reqs, uint32_t n, uint32_t nslots,
+                                        const uint32_t* client_of_slot,
+                                        const uint32_t* gd, const uint32_t* gr,
+                                        uint32_t* xd, uint32_t* xr, uint8_t* known,
+                                        uint32_t* first, uint32_t i) {
   if (i >= n) return;
   uint32_t s = reqs[i].slot;
   if (s >= nslots) return;
@@ -80,6 +83,14 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
   }
   reqs[i].delta = delta;
   reqs[i].rho = rho;
+}
+__global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
+                               const uint32_t* client_of_slot,
+                               const uint32_t* gd, const uint32_t* gr,
+                               uint32_t* xd, uint32_t* xr, uint8_t* known,
+                               uint32_t* first) {
+  track_params_one(reqs, n, nslots, client_of_slot, gd, gr, xd, xr, known, first,
+                   blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // epoch end, per server: my_delta / my_rho of its responses (X += own) and
@@ -114,6 +125,41 @@ __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
     sum_d[c] = 0;
     sum_r[c] = 0;
   }
+}
+
+// multi-table forms (a queue group's step, dmc_group_step_device): the
+// per-server arguments indexed by blockIdx.y, the bodies the same kernels'
+struct TrackArgs {
+  dmc_request* reqs;
+  uint32_t n, nslots;
+  const uint32_t *cmap, *gd, *gr;
+  uint32_t *xd, *xr;
+  uint8_t* known;
+  uint32_t* first;
+};
+__global__ void k_track_first_m(const TrackArgs* a) {
+  const TrackArgs& x = a[blockIdx.y];
+  if (!x.reqs) return;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= x.n) return;
+  const uint32_t s = x.reqs[i].slot;
+  if (s < x.nslots) atomicMin(&x.first[s], i);
+}
+__global__ void k_track_params_m(const TrackArgs* a) {
+  const TrackArgs& x = a[blockIdx.y];
+  if (!x.reqs) return;
+  track_params_one(x.reqs, x.n, x.nslots, x.cmap, x.gd, x.gr, x.xd, x.xr, x.known, x.first,
+                   blockIdx.x * blockDim.x + threadIdx.x);
+}
+struct TallyArgs {
+  const dmc_decision* dec;
+  const dmc_pull_result* res;
+  uint32_t cap;
+  uint32_t *comp_d, *comp_r;
+};
+__global__ void k_tally_m(const TallyArgs* a) {
+  const TallyArgs& x = a[blockIdx.y];
+  if (x.dec) tally_body(x.dec, x.res, x.cap, x.comp_d, x.comp_r);
 }
 
 }  // namespace dmc

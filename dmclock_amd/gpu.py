@@ -69,6 +69,10 @@ EXPORTS = {
                                 _vp]),
     "dmc_tracker_collect": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dmc_tracker_advance": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "dmc_group_create": (_i32, [_vp, _u32, ctypes.POINTER(_vp)]),
+    "dmc_group_destroy": (_i32, [_vp]),
+    "dmc_group_stream": (_vp, [_vp]),
+    "dmc_group_step_device": (_i32, [_vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "dmc_profile_enable": (_i32, [_vp, _i32]),
     "dmc_profile_reset": (_i32, [_vp]),
     "dmc_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),

@@ -126,11 +126,60 @@ class DeviceTrackers:
                "dmc_tracker_advance")
         q0.sync()
 
+    def group_trackers(self):
+        """the dmc_group_tracker array (one per server) for GpuGroup.step"""
+        from ._abi import GroupTracker
+        arr = (GroupTracker * len(self.queues))()
+        for s in range(len(self.queues)):
+            m = self.cmap[s].data_ptr() if self.cmap is not None else None
+            arr[s] = GroupTracker(m, self.gd.data_ptr(), self.gr.data_ptr(),
+                                  self.xd[s].data_ptr(), self.xr[s].data_ptr(),
+                                  self.known[s].data_ptr(), self.first[s].data_ptr(),
+                                  self.comp_d[s].data_ptr(), self.comp_r[s].data_ptr())
+        return arr
+
     def state(self):
         """host copies (tests)"""
         f = lambda t: t.cpu().numpy().view(np.uint32)
         return {"gd": f(self.gd), "gr": f(self.gr), "xd": f(self.xd),
                 "xr": f(self.xr), "known": self.known.cpu().numpy().astype(bool)}
+
+
+class GpuGroup:
+    """The S server queues of one device driven as one (dmc_group): a step is,
+    for every member, the tracker fill (optional), n adds and k pulls --
+    what fill + add_pull_batch_device + tally do on each queue alone, bit for
+    bit -- as one launch per kernel over all members (blockIdx.y = member),
+    one graph per step."""
+
+    def __init__(self, queues):
+        self.queues = list(queues)
+        self.L = lib()
+        arr = (ctypes.c_void_p * len(self.queues))(*[q.h for q in self.queues])
+        h = ctypes.c_void_p()
+        _check(self.L.dmc_group_create(arr, len(self.queues), ctypes.byref(h)),
+               "dmc_group_create")
+        self.h = h
+
+    def step(self, n, d_reqs, d_rc, nows, k, d_out, d_res, trackers=None):
+        """per-member device pointers (lists of ints), per-member `now`;
+        trackers: DeviceTrackers.group_trackers() or None"""
+        S = len(self.queues)
+        vp = ctypes.c_void_p * S
+        f = (ctypes.c_double * S)(*nows)
+        _check(self.L.dmc_group_step_device(
+            self.h, n, vp(*d_reqs), vp(*d_rc), f, k, vp(*d_out),
+            vp(*d_res) if d_res is not None else None,
+            ctypes.cast(trackers, ctypes.c_void_p) if trackers is not None else None),
+            "dmc_group_step_device")
+
+    def stream(self):
+        return self.L.dmc_group_stream(self.h)
+
+    def close(self):
+        if self.h:
+            _check(self.L.dmc_group_destroy(self.h), "dmc_group_destroy")
+            self.h = None
 
 
 def make_queues(n_servers, n_clients, device=0, **kw):

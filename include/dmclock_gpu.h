@@ -244,6 +244,40 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
                               int32_t* d_rc, double now, uint32_t k,
                               dmc_decision* d_out, dmc_pull_result* d_result);
 
+/* ------------------------------------------------------------ queue groups
+ * S server queues of one device driven as one (BASELINE config 5's per-GPU
+ * shape: dmClock servers are independent queues, sim/src/simulate.h:118-136,
+ * one per server, sim/src/sim_server.h:84,123-130).  A group step does, for
+ * every member s, exactly what dmc_tracker_fill (when trk is given) +
+ * dmc_add_pull_batch_device + dmc_tracker_tally do on it alone -- the same
+ * results, bit for bit -- with one launch per kernel over all members (one
+ * graph per step).  Members must share device, max_clients and
+ * ring_capacity; while in a group a member runs on the group's stream (its
+ * other calls stay valid and are ordered with the group's steps).  A member
+ * destroyed before its group leaves it. */
+typedef struct dmc_group dmc_group;
+typedef struct dmc_group_tracker {  /* one server's device tracker state (see dmc_tracker_*) */
+  const uint32_t* client_of_slot;   /* NULL: identity */
+  const uint32_t* gdelta;
+  const uint32_t* grho;
+  uint32_t* xd;
+  uint32_t* xr;
+  uint8_t* known;
+  uint32_t* first;
+  uint32_t* comp_delta;             /* tallied after the step (needs d_result) */
+  uint32_t* comp_rho;
+} dmc_group_tracker;
+int dmc_group_create(dmc_queue* const* queues, uint32_t n, dmc_group** out);
+int dmc_group_destroy(dmc_group* g);
+void* dmc_group_stream(dmc_group* g);
+/* Per member s: requests d_reqs[s][0..n) (delta/rho filled first when trk),
+ * statuses d_rc[s], pull time now[s], k pulls into d_out[s], result record
+ * d_result[s]; trk: NULL or one entry per member. */
+int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
+                          int32_t* const* d_rc, const double* now, uint32_t k,
+                          dmc_decision* const* d_out, dmc_pull_result* const* d_result,
+                          const dmc_group_tracker* trk);
+
 /* ------------------------------------------------------------ maintenance */
 
 /* remove_by_client (dmclock_server.h:594-625): queued handles in FIFO order

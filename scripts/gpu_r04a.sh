@@ -20,4 +20,6 @@ run suite 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeo
 for v in e512 e512s e256; do
   DMC_LIB=$R/dmclock_amd/variants/$v.so run exact_$v 400 python -u -m pytest tests/test_device_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "exact_trace or unset_phase" || exit 1
 done &&
+run c5 500 python bench.py --config 5 --no-cpu-baseline &&
+run c5sep 500 python bench.py --config 5 --no-cpu-baseline --separate-queues &&
 VARIANTS="${VARIANTS:-base e512 e512s e256}" ROUNDS=2 timeout -k 10 900 bash scripts/gpu_variants.sh > gpurun_out/r04a_variants.log 2>&1; rc=$?; cat gpurun_out/r04a_variants.log; exit $rc

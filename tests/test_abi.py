@@ -68,6 +68,8 @@ int main(void) {
   printf("dmc_client_state %zu\n", sizeof(dmc_client_state));
   printf("dmc_stats %zu\n", sizeof(dmc_stats));
   printf("dmc_counters %zu\n", sizeof(dmc_counters));
+  printf("dmc_group_tracker %zu\n", sizeof(dmc_group_tracker));
+  P(dmc_group_tracker, comp_rho);
   P(dmc_counters, single_steps); P(dmc_counters, max_bin);
   P(dmc_counters, bin_splits);
   P(dmc_request, time); P(dmc_request, delta); P(dmc_request, handle);
@@ -95,6 +97,8 @@ def test_struct_layouts_match_header(tmp_path):
     assert out["dmc_client_state"] == ctypes.sizeof(_abi.ClientState)
     assert out["dmc_stats"] == ctypes.sizeof(_abi.Stats)
     assert out["dmc_counters"] == ctypes.sizeof(_abi.Counters)
+    assert out["dmc_group_tracker"] == ctypes.sizeof(_abi.GroupTracker)
+    assert out["dmc_group_tracker.comp_rho"] == _abi.GroupTracker.comp_rho.offset
     assert out["dmc_counters.single_steps"] == _abi.Counters.single_steps.offset
     assert out["dmc_counters.max_bin"] == _abi.Counters.max_bin.offset
     assert out["dmc_counters.bin_splits"] == _abi.Counters.bin_splits.offset

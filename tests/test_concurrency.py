@@ -82,6 +82,10 @@ def _rank(rank, world, port, sh, outdir, out_q):
         N, k = sh["N"], sh["batch"]
         qs = make_queues(S, N, device=0, ring_capacity=64, max_batch=sh["chunk"])
         trk = DeviceTrackers(qs, N, dev, n_clients=sh["G"], client_of_slot=cmap[mine])
+        group = None
+        if sh.get("group"):
+            from dmclock_amd.multiserver import GpuGroup
+            group = GpuGroup(qs)  # (members run on the group's stream from here)
         # every device buffer lives to the end: no call waits for another
         d_pre = [[torch.from_numpy(c.view(np.uint8)).to(dev) for c in srv[s][0]]
                  for s in mine]
@@ -111,6 +115,17 @@ def _rank(rank, world, port, sh, outdir, out_q):
             trk.tally(j, d_set[j].data_ptr(), d_res[j, n_steps].data_ptr(), sh["settle"])
             q.sync()
 
+        def run_group(i0, i1):
+            gtrk = trk.group_trackers()
+            for i in range(i0, i1):
+                bs = [srv[mine[j]][2][i] for j in range(S)]
+                group.step(len(bs[0]), [d_steps[j][i].data_ptr() for j in range(S)],
+                           [d_rc[j].data_ptr() for j in range(S)],
+                           [float(b["time"][-1]) for b in bs], k,
+                           [d_out[j][i].data_ptr() for j in range(S)],
+                           [d_res[j, i].data_ptr() for j in range(S)], gtrk)
+            qs[0].sync()
+
         def run(j, i0, i1):
             q = qs[j]
             for i in range(i0, i1):
@@ -130,7 +145,10 @@ def _rank(rank, world, port, sh, outdir, out_q):
             settle_ctr = [q.counters(reset=True) for q in qs]
             for e in range(sh["epochs"]):
                 i0 = e * sh["steps"]
-                list(pool.map(lambda j: run(j, i0, i0 + sh["steps"]), range(S)))
+                if group is not None:
+                    run_group(i0, i0 + sh["steps"])
+                else:
+                    list(pool.map(lambda j: run(j, i0, i0 + sh["steps"]), range(S)))
                 trk.deliver()
         torch.cuda.synchronize()
         assert sum(rc_bad) == 0, rc_bad
@@ -149,8 +167,10 @@ def _rank(rank, world, port, sh, outdir, out_q):
             c = qs[j].counters()
             out["counters"] = np.array([c["radix_rounds"], c["rounds"],
                                         settle_ctr[j]["rounds"],
-                                        settle_ctr[j]["radix_rounds"]])
+                                        settle_ctr[j]["radix_rounds"], c["fused_calls"]])
             np.savez(os.path.join(outdir, f"srv{s}.npz"), **out)
+        if group is not None:
+            group.close()
         for q in qs:
             q.close()
         out_q.put((rank, "ok"))
@@ -235,7 +255,8 @@ def _check(sh, outdir, want, et):
         # steps: bin-ranked rounds only; the settle: at least four rounds
         # (k = 2^20 in rounds of at most 2^18 pulls)
         assert g["counters"][0] == 0, ("radix rounds", s, g["counters"])
-        assert g["counters"][2] >= 4, ("settle rounds", s, g["counters"])
+        assert g["counters"][2] >= sh["settle"] >> 18, ("settle rounds", s, g["counters"])
+        assert g["counters"][4] == n_steps, ("fused steps", s, g["counters"])
     return n_dec
 
 
@@ -281,6 +302,23 @@ def test_concurrent_queues_trackers_parity(world):
     sh = dict(SHAPE)
     with tempfile.TemporaryDirectory() as outdir:
         _spawn(world, sh, outdir)
+        want, et, ties = oracle_run(sh)
+        assert ties == 0, f"{ties} tied decisions: pick another seed"
+        n = _check(sh, outdir, want, et)
+    assert n > sh["S_total"] * sh["settle"]
+
+
+@pytest.mark.timeout(480)
+def test_group_queues_trackers_parity_8():
+    """The multi-table path: eight server queues in
+    one queue group (dmc_group_step_device: one launch per kernel over the
+    eight tables, blockIdx.y = table, one graph per step, device trackers'
+    fill and tally inside the step), after the same per-queue preparation and
+    settle; every delta/rho, decision, result and tracker word bit-exact
+    against eight oracle queues and the epoch restatement."""
+    sh = dict(SHAPE, S_total=8, N=1 << 17, G=1 << 19, settle=1 << 19, group=True)
+    with tempfile.TemporaryDirectory() as outdir:
+        _spawn(1, sh, outdir)
         want, et, ties = oracle_run(sh)
         assert ties == 0, f"{ties} tied decisions: pick another seed"
         n = _check(sh, outdir, want, et)
