@@ -16,10 +16,13 @@ run() {  # name, seconds, command...
   echo "$n exit $rc"; tail -2 gpurun_out/r04a_$n.log | cut -c1-300
   return $rc
 }
-run suite 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
+if [ -z "$VARIANTS_ONLY" ]; then
+run suite 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
+run c5 300 python bench.py --config 5 --no-cpu-baseline &&
+run c5sep 300 python bench.py --config 5 --no-cpu-baseline --separate-queues
+exit $?
+fi
 for v in e512 e512s e256; do
   DMC_LIB=$R/dmclock_amd/variants/$v.so run exact_$v 400 python -u -m pytest tests/test_device_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "exact_trace or unset_phase" || exit 1
 done &&
-run c5 500 python bench.py --config 5 --no-cpu-baseline &&
-run c5sep 500 python bench.py --config 5 --no-cpu-baseline --separate-queues &&
 VARIANTS="${VARIANTS:-base e512 e512s e256}" ROUNDS=2 timeout -k 10 900 bash scripts/gpu_variants.sh > gpurun_out/r04a_variants.log 2>&1; rc=$?; cat gpurun_out/r04a_variants.log; exit $rc
