@@ -1613,6 +1613,10 @@ struct dmc_queue {
   // its own is kept here and restored when the group is destroyed
   hipStream_t own_stream = nullptr;
   dmc_group* group = nullptr;
+  // graphs are captured on a stream of their own (created on first use):
+  // a group's members share their execution stream with other host threads,
+  // whose launches must never land in (or break) a capture
+  hipStream_t cap_stream = nullptr;
   Table tb{};
   std::mutex mtx;  // C-ABI calls on one handle are serialised (data_mtx, :762)
   // host mirrors
@@ -1768,7 +1772,7 @@ struct dmc_queue {
 struct dmc_group {
   std::vector<dmc_queue*> qs;
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, cap_stream = nullptr;
   // per-step kernel arguments: pinned staging and its device copy (one
   // memcpy per step, the graph's first node), S entries per kernel
   uint8_t* h_blob = nullptr;
@@ -2003,10 +2007,23 @@ int graph_replay(dmc_queue* q, GraphRec& g, void** args, void** args2 = nullptr)
 // Capture `enqueue` (which must start with the parameter kernel) as a graph.
 template <typename F>
 int graph_capture(dmc_queue* q, GraphRec& g, F enqueue, const void* func2 = nullptr) {
-  HIP_OK(hipStreamBeginCapture(q->stream, hipStreamCaptureModeThreadLocal));
+  if (!q->cap_stream)
+    HIP_OK(hipStreamCreateWithFlags(&q->cap_stream, hipStreamNonBlocking));
+  // (enqueue launches on q->stream: pointed at the capture stream meanwhile)
+  hipStream_t exec = q->stream;
+  q->stream = q->cap_stream;
+  if (hipStreamBeginCapture(q->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    q->stream = exec;
+    return DMC_EDEVICE;
+  }
   enqueue();
   hipGraph_t graph = nullptr;
-  HIP_OK(hipStreamEndCapture(q->stream, &graph));
+  const hipError_t ce = hipStreamEndCapture(q->stream, &graph);
+  q->stream = exec;
+  if (ce != hipSuccess) {
+    std::fprintf(stderr, "dmclock_gpu: hipStreamEndCapture failed: %s\n", hipGetErrorString(ce));
+    return DMC_EDEVICE;
+  }
   size_t nroot = 0;
   HIP_OK(hipGraphGetRootNodes(graph, nullptr, &nroot));
   if (nroot != 1) {
@@ -3523,6 +3540,7 @@ int dmc_queue_destroy(dmc_queue* q) {
     (void)hipEventDestroy(r.b);
   }
   if (q->stream) (void)hipStreamDestroy(q->stream);
+  if (q->cap_stream) (void)hipStreamDestroy(q->cap_stream);
   delete q;
   return DMC_OK;
 }
@@ -4238,6 +4256,7 @@ int dmc_group_destroy(dmc_group* g) {
   if (g->h_blob) (void)hipHostFree(g->h_blob);
   dfree(g->d_blob);
   if (g->stream) (void)hipStreamDestroy(g->stream);
+  if (g->cap_stream) (void)hipStreamDestroy(g->cap_stream);
   delete g;
   return DMC_OK;
 }
@@ -4312,28 +4331,28 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       const uint32_t gHist = all_sampled ? kHistBlocksSampled : kHistBlocksR;
       const uint32_t gAdd = (n + kBlock - 1) / kBlock;
       uint8_t* d = g->d_blob;
-      auto enqueue = [&] {
-        (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, g->stream);
+      auto enqueue = [&](hipStream_t st) {
+        (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, st);
         if (trk) {
-          hipLaunchKernelGGL(k_track_first_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+          hipLaunchKernelGGL(k_track_first_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                              (const TrackArgs*)(d + g->o_trk));
-          hipLaunchKernelGGL(k_track_params_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+          hipLaunchKernelGGL(k_track_params_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                              (const TrackArgs*)(d + g->o_trk));
         }
-        hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+        hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                            (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, g->stream,
+        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                            (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, g->stream,
+        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
                            (const RScanArgs*)(d + g->o_scan));
-        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, g->stream,
+        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, st,
                            (const RHistArgs*)(d + g->o_hist));
-        hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, g->stream,
+        hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
                            (const REmitArgs*)(d + g->o_emit));
-        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kBlockR), 0, g->stream,
+        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kBlockR), 0, st,
                            (const RRankArgs*)(d + g->o_rank));
         hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmit * gEm + 1, S), dim3(kBlockR), 0,
-                           g->stream, (const RApplyArgs*)(d + g->o_apply));
+                           st, (const RApplyArgs*)(d + g->o_apply));
       };
       // the step's graph: captured at the second sighting of its shape, then
       // replayed (the arguments travel in the blob, no node updates)
@@ -4351,9 +4370,11 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
           if (x.exec) (void)hipGraphExecDestroy(x.exec);
           if (x.graph) (void)hipGraphDestroy(x.graph);
           x = dmc_group::G{};
-          HIP_OK(hipStreamBeginCapture(g->stream, hipStreamCaptureModeThreadLocal));
-          enqueue();
-          HIP_OK(hipStreamEndCapture(g->stream, &x.graph));
+          if (!g->cap_stream)
+            HIP_OK(hipStreamCreateWithFlags(&g->cap_stream, hipStreamNonBlocking));
+          HIP_OK(hipStreamBeginCapture(g->cap_stream, hipStreamCaptureModeThreadLocal));
+          enqueue(g->cap_stream);
+          HIP_OK(hipStreamEndCapture(g->cap_stream, &x.graph));
           HIP_OK(hipGraphInstantiate(&x.exec, x.graph, nullptr, nullptr, 0));
           x.key = key;
           gr = &x;
@@ -4365,7 +4386,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         HIP_OK(hipGraphLaunch(gr->exec, g->stream));
         ++g->graph_launches;
       } else {
-        enqueue();
+        enqueue(g->stream);
       }
       HIP_OK(hipGetLastError());
       ++g->fused_steps;
