@@ -169,6 +169,10 @@ def parse():
                          "the previous two steps")
     ap.add_argument("--servers", type=int, default=8,
                     help="config 5: server queues per GPU")
+    ap.add_argument("--sequential-epochs", action="store_true",
+                    help="config 5: deliver each epoch's responses at its end "
+                         "(collect, all-reduce, advance in sequence) instead of "
+                         "overlapping the all-reduce with the next epoch")
     ap.add_argument("--separate-queues", action="store_true",
                     help="config 5: drive each server queue from its own host "
                          "thread and stream instead of one queue-group step")

@@ -132,7 +132,8 @@ def main(args):
     queues = make_queues(S, N, device=local, ring_capacity=args.ring,
                          max_batch=max(args.batch, k, 1 << 20))
     cmap = np.stack([w[1] for w in wl])
-    trk = DeviceTrackers(queues, N, dev, n_clients=S * N, client_of_slot=cmap)
+    trk = DeviceTrackers(queues, N, dev, n_clients=S * N, client_of_slot=cmap,
+                         lagged=not args.sequential_epochs)
 
     chunk = 1 << 20
     d_rc = [torch.zeros(chunk, dtype=torch.int32, device=dev) for _ in range(S)]
@@ -180,7 +181,6 @@ def main(args):
 
     pool = ThreadPoolExecutor(S)
     group = None if args.separate_queues else GpuGroup(queues)
-    gtrk = trk.group_trackers()
     g_args = [([d_steps[s][i].data_ptr() for s in range(S)], [nows[s][i] for s in range(S)],
                [d_res[s, i].data_ptr() for s in range(S)])
               for i in range(n_steps + n_prof)]
@@ -193,7 +193,7 @@ def main(args):
             return
         for i in range(i0, i1):
             reqs, nw, res = g_args[i]
-            group.step(args.batch, reqs, g_rc, nw, k, g_out, res, gtrk)
+            group.step(args.batch, reqs, g_rc, nw, k, g_out, res, trk.group_trackers())
 
     t_prep = time.perf_counter()
     settle = list(pool.map(prepare, range(S)))[0]
@@ -219,6 +219,7 @@ def main(args):
     epochs = []
     t0 = time.perf_counter()
     steps_with_epochs(args.warmup, n_steps, epochs)
+    trk.finish()  # (the last epoch's overlapped delivery)
     for q in queues:
         q.sync()
     torch.cuda.synchronize()
@@ -275,6 +276,10 @@ def main(args):
 
     # all-reduce bytes per epoch: 2 x int32 per global client
     ar_bytes = 2 * 4 * S * N
+    # a ring all-reduce moves 2 (n - 1) / n of the buffer over each GPU's
+    # busiest link; xGMI: ~153 GB/s per link (MI355X_MICROARCH.md)
+    ring_ms = 2.0 * (world - 1) / world * ar_bytes / 153e9 * 1e3
+    ar_ms = trk.allreduce_ms[-len(epochs):] if epochs and trk.allreduce_ms else []
     out = {
         "metric": METRIC,
         "value": round(local_ops / dt, 1),
@@ -307,6 +312,11 @@ def main(args):
         "epochs_timed": len(epochs),
         "epoch_delivery_ms": None if ep_ms is None else round(ep_ms, 3),
         "allreduce_bytes_per_epoch": ar_bytes,
+        "allreduce_ms_per_epoch": round(float(np.mean(ar_ms)), 4) if ar_ms else None,
+        "allreduce_ring_bound_ms": round(ring_ms, 4),
+        "epoch_exchange": ("sequential" if args.sequential_epochs else
+                           "overlapped: an epoch's sums all-reduced during the next "
+                           "epoch's steps, delivered at its end"),
         "tracker_known_frac": round(float(st["known"].mean()), 4),
         "setup_s": {"generate": round(t_gen, 1), "prepopulate": round(t_prep, 1)},
         "roofline": roof,

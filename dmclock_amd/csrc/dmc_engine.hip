@@ -4616,6 +4616,7 @@ int dmc_tracker_tally(dmc_queue* q, const dmc_decision* d_dec,
                       uint32_t* d_comp_delta, uint32_t* d_comp_rho) {
   if (!q) return DMC_EINVAL;
   QueueLock lk(q);
+  if (lk.rc) return lk.rc;
   if (!q || !d_result || (cap && (!d_dec || !d_comp_delta || !d_comp_rho)))
     return DMC_EINVAL;
   if (!cap) return DMC_OK;
@@ -4631,6 +4632,7 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
                      uint8_t* d_known, uint32_t* d_first) {
   if (!q) return DMC_EINVAL;
   QueueLock lk(q);
+  if (lk.rc) return lk.rc;
   if (!q || (n && (!d_reqs || !d_gdelta || !d_grho || !d_xd || !d_xr ||
                    !d_known || !d_first)))
     return DMC_EINVAL;
@@ -4645,12 +4647,43 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
   return DMC_OK;
 }
 
+int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_client_of_slot,
+                             const uint32_t* d_comp_delta, const uint32_t* d_comp_rho,
+                             uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
+  if (lk.rc) return lk.rc;
+  if (n_slots > q->p.max_clients) return DMC_EINVAL;
+  if (!n_slots) return DMC_OK;
+  if (!d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
+  hipLaunchKernelGGL(k_track_sums, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
+                     n_slots, d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta,
+                     d_sum_rho);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
+}
+
+int dmc_tracker_commit(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd, uint32_t* d_xr,
+                       uint32_t* d_comp_delta, uint32_t* d_comp_rho) {
+  if (!q) return DMC_EINVAL;
+  QueueLock lk(q);
+  if (lk.rc) return lk.rc;
+  if (n_slots > q->p.max_clients) return DMC_EINVAL;
+  if (!n_slots) return DMC_OK;
+  if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho) return DMC_EINVAL;
+  hipLaunchKernelGGL(k_track_commit, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
+                     n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho);
+  HIP_OK(hipGetLastError());
+  return DMC_OK;
+}
+
 int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
                         const uint32_t* d_client_of_slot, uint32_t* d_xd,
                         uint32_t* d_xr, uint32_t* d_comp_delta, uint32_t* d_comp_rho,
                         uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
   if (!q) return DMC_EINVAL;
   QueueLock lk(q);
+  if (lk.rc) return lk.rc;
   if (!q || n_slots > q->p.max_clients) return DMC_EINVAL;
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho)
@@ -4666,6 +4699,7 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                         uint32_t* d_grho, uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
   if (!q) return DMC_EINVAL;
   QueueLock lk(q);
+  if (lk.rc) return lk.rc;
   if (!q) return DMC_EINVAL;
   if (!n_clients) return DMC_OK;
   if (!d_gdelta || !d_grho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;

@@ -114,6 +114,37 @@ __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
   }
 }
 
+// Overlapped (lagged) delivery, split in two: at an epoch's end only the
+// per-client sums of its responses are formed (the all-reduce of them runs
+// during the next epoch); at the next epoch's end its own-response part
+// commits (X += comp, comp cleared) together with the all-reduced sums
+// (k_track_advance).
+__global__ void k_track_sums(uint32_t nslots, const uint32_t* client_of_slot,
+                             const uint32_t* comp_d, const uint32_t* comp_r,
+                             uint32_t* sum_d, uint32_t* sum_r) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    const uint32_t cd = comp_d[s];
+    if (!cd) continue;
+    const uint32_t cr = comp_r[s];
+    const uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    atomicAdd(&sum_d[c], cd);
+    if (cr) atomicAdd(&sum_r[c], cr);
+  }
+}
+__global__ void k_track_commit(uint32_t nslots, uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
+                               uint32_t* comp_r) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    const uint32_t cd = comp_d[s];
+    if (!cd) continue;
+    xd[s] += cd;
+    xr[s] += comp_r[s];
+    comp_d[s] = 0;
+    comp_r[s] = 0;
+  }
+}
+
 // after the all-reduce of the sums: the global counters advance (D += all
 // servers' responses to the client), sums cleared for the next epoch
 __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,

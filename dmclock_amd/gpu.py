@@ -69,6 +69,8 @@ EXPORTS = {
                                 _vp]),
     "dmc_tracker_collect": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dmc_tracker_advance": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "dmc_tracker_collect_sums": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "dmc_tracker_commit": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "dmc_group_create": (_i32, [_vp, _u32, ctypes.POINTER(_vp)]),
     "dmc_group_destroy": (_i32, [_vp]),
     "dmc_group_stream": (_vp, [_vp]),

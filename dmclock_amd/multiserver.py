@@ -36,9 +36,18 @@ class DeviceTrackers:
     Each server table has n_slots client slots; client_of_slot (S x n_slots,
     int32, optional; identity when None) names the global client of each
     slot, of n_clients global clients (default n_slots).  Per (server, slot):
-    X_delta, X_rho, known; per global client: the delta/rho counters."""
+    X_delta, X_rho, known; per global client: the delta/rho counters.
 
-    def __init__(self, queues, n_slots, device, n_clients=None, client_of_slot=None):
+    lagged=False: deliver() hands each epoch's responses to the clients at
+    that epoch's end (collect, all-reduce, advance, in sequence).
+    lagged=True (the overlapped exchange): deliver()
+    forms the epoch's per-client sums and starts their all-reduce, which runs
+    while the next epoch's steps do; the responses reach the clients' counters
+    at the next deliver() (finish() flushes the last one).  Per-slot tallies
+    are double-buffered so that the next epoch tallies into the other half."""
+
+    def __init__(self, queues, n_slots, device, n_clients=None, client_of_slot=None,
+                 lagged=False):
         import torch
         self.torch = torch
         self.queues = list(queues)
@@ -46,6 +55,7 @@ class DeviceTrackers:
         G = n_clients if n_clients is not None else n_slots
         i32 = torch.int32
         self.N, self.G = N, G
+        self.lagged = lagged
         if client_of_slot is not None:
             client_of_slot = torch.as_tensor(client_of_slot, dtype=i32).to(device)
             if tuple(client_of_slot.shape) != (S, N):
@@ -55,16 +65,36 @@ class DeviceTrackers:
         self.cmap = client_of_slot
         self.gd = torch.ones(G, dtype=i32, device=device)
         self.gr = torch.ones(G, dtype=i32, device=device)
-        self.sum_d = torch.zeros(G, dtype=i32, device=device)
-        self.sum_r = torch.zeros(G, dtype=i32, device=device)
+        # persistent all-reduce buffers: [half][delta, rho][client] (one
+        # collective on a contiguous (2, G) block, no per-epoch stack)
+        self.sums = torch.zeros((2, 2, G), dtype=i32, device=device)
         self.xd = torch.zeros((S, N), dtype=i32, device=device)
         self.xr = torch.zeros((S, N), dtype=i32, device=device)
         self.known = torch.zeros((S, N), dtype=torch.uint8, device=device)
         self.first = torch.full((S, N), U32_NONE, dtype=i32, device=device)
-        self.comp_d = torch.zeros((S, N), dtype=i32, device=device)
-        self.comp_r = torch.zeros((S, N), dtype=i32, device=device)
+        self.comp = torch.zeros((2, 2, S, N), dtype=i32, device=device)
+        self.cur = 0
+        self.pending = None  # lagged: (half, all-reduce work or None)
+        self.allreduce_ms = []  # lagged: measured all-reduce time per epoch
         self.L = lib()
+        self._gt = [None, None]
         torch.cuda.synchronize(device)
+
+    @property
+    def comp_d(self):
+        return self.comp[self.cur, 0]
+
+    @property
+    def comp_r(self):
+        return self.comp[self.cur, 1]
+
+    @property
+    def sum_d(self):
+        return self.sums[0, 0]
+
+    @property
+    def sum_r(self):
+        return self.sums[0, 1]
 
     def _map(self, s):
         return None if self.cmap is None else _p(self.cmap[s])
@@ -96,47 +126,107 @@ class DeviceTrackers:
                                               _p(self.sum_d), _p(self.sum_r)),
                    "dmc_tracker_collect")
 
-    def deliver(self, group=None):
-        """Epoch boundary: collect, one all-reduce of the per-client sums over
-        the ranks (sum, modular int32), then the global counters advance.
-        Under RCCL ("nccl") the all-reduce runs on the device buffers over
-        xGMI; under gloo (CPU tests, or ranks sharing one GPU) the sums are
-        staged through host memory."""
-        torch = self.torch
-        self.collect()
+    def _sync_queues(self):
         for q in self.queues:
             q.sync()
+
+    def _allreduce(self, buf, group, async_op):
+        """the exchange step: RCCL on the device buffer (async: its work
+        handle), gloo through host memory (blocking)"""
+        torch = self.torch
         import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
         # (any initialized group: at world size 1 the all-reduce is the
         # identity, and RCCL still runs it on the device buffers)
-        if dist.is_available() and dist.is_initialized():
-            both = torch.stack([self.sum_d, self.sum_r])
-            if dist.get_backend(group) == "gloo":
-                host = both.cpu()
-                dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-                both.copy_(host)
-            else:
-                dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
-            self.sum_d.copy_(both[0])
-            self.sum_r.copy_(both[1])
+        if dist.get_backend(group) == "gloo":
+            host = buf.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(host)
             torch.cuda.synchronize(self.gd.device)
+            return None
+        if not async_op:
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+            torch.cuda.synchronize(self.gd.device)
+            return None
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        work.wait()  # (the current stream waits for it; the host does not)
+        ev1.record()
+        return (work, ev0, ev1)
+
+    def _advance(self, half):
         q0 = self.queues[0]
         _check(self.L.dmc_tracker_advance(q0.h, self.G, _p(self.gd), _p(self.gr),
-                                          _p(self.sum_d), _p(self.sum_r)),
+                                          _p(self.sums[half, 0]), _p(self.sums[half, 1])),
                "dmc_tracker_advance")
-        q0.sync()
+
+    def deliver(self, group=None):
+        """Epoch boundary.  Sequential: collect, one all-reduce of the
+        per-client sums over the ranks (sum, modular int32), then the global
+        counters advance.  Lagged: the previous epoch's delivery completes
+        (commit + advance) and this epoch's sums start their all-reduce."""
+        if self.lagged:
+            return self._deliver_lagged(group)
+        self.collect()
+        self._sync_queues()
+        self._allreduce(self.sums[0], group, async_op=False)
+        self._advance(0)
+        self.queues[0].sync()
+
+    def _finish_pending(self):
+        torch = self.torch
+        half, work = self.pending
+        if work is not None:
+            w, ev0, ev1 = work
+            ev1.synchronize()
+            self.allreduce_ms.append(ev0.elapsed_time(ev1))
+        for s, q in enumerate(self.queues):
+            _check(self.L.dmc_tracker_commit(q.h, self.N, _p(self.xd[s]), _p(self.xr[s]),
+                                             _p(self.comp[half, 0, s]),
+                                             _p(self.comp[half, 1, s])),
+                   "dmc_tracker_commit")
+        self._advance(half)
+        self.pending = None
+        del torch
+
+    def _deliver_lagged(self, group):
+        if self.pending is not None:
+            self._finish_pending()
+        h = self.cur
+        for s, q in enumerate(self.queues):
+            _check(self.L.dmc_tracker_collect_sums(q.h, self.N, self._map(s),
+                                                   _p(self.comp[h, 0, s]),
+                                                   _p(self.comp[h, 1, s]),
+                                                   _p(self.sums[h, 0]), _p(self.sums[h, 1])),
+                   "dmc_tracker_collect_sums")
+        self._sync_queues()
+        self.pending = (h, self._allreduce(self.sums[h], group, async_op=True))
+        self.cur = 1 - h  # the next epoch tallies into the other half
+
+    def finish(self):
+        """lagged: deliver the last epoch's pending responses"""
+        if self.pending is not None:
+            self._finish_pending()
+            self._sync_queues()
 
     def group_trackers(self):
-        """the dmc_group_tracker array (one per server) for GpuGroup.step"""
+        """the dmc_group_tracker array (one per server) for GpuGroup.step,
+        pointing at the current tally half"""
         from ._abi import GroupTracker
-        arr = (GroupTracker * len(self.queues))()
-        for s in range(len(self.queues)):
-            m = self.cmap[s].data_ptr() if self.cmap is not None else None
-            arr[s] = GroupTracker(m, self.gd.data_ptr(), self.gr.data_ptr(),
-                                  self.xd[s].data_ptr(), self.xr[s].data_ptr(),
-                                  self.known[s].data_ptr(), self.first[s].data_ptr(),
-                                  self.comp_d[s].data_ptr(), self.comp_r[s].data_ptr())
-        return arr
+        if self._gt[self.cur] is None:
+            arr = (GroupTracker * len(self.queues))()
+            for s in range(len(self.queues)):
+                m = self.cmap[s].data_ptr() if self.cmap is not None else None
+                arr[s] = GroupTracker(m, self.gd.data_ptr(), self.gr.data_ptr(),
+                                      self.xd[s].data_ptr(), self.xr[s].data_ptr(),
+                                      self.known[s].data_ptr(), self.first[s].data_ptr(),
+                                      self.comp[self.cur, 0, s].data_ptr(),
+                                      self.comp[self.cur, 1, s].data_ptr())
+            self._gt[self.cur] = arr
+        return self._gt[self.cur]
 
     def state(self):
         """host copies (tests)"""

@@ -339,6 +339,17 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
                      const uint32_t* d_client_of_slot, const uint32_t* d_gdelta,
                      const uint32_t* d_grho, uint32_t* d_xd, uint32_t* d_xr,
                      uint8_t* d_known, uint32_t* d_first);
+/* Overlapped delivery, the two halves of
+ * dmc_tracker_collect: at an epoch's end sum_*[client_of_slot[s]] += comp_*
+ * only (the all-reduce of the sums then runs during the next epoch); at the
+ * next epoch's end dmc_tracker_commit moves that epoch's own responses into
+ * the server's tracker state (xd += comp_delta, xr += comp_rho, comp_* = 0)
+ * beside dmc_tracker_advance of the all-reduced sums. */
+int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_client_of_slot,
+                             const uint32_t* d_comp_delta, const uint32_t* d_comp_rho,
+                             uint32_t* d_sum_delta, uint32_t* d_sum_rho);
+int dmc_tracker_commit(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd, uint32_t* d_xr,
+                       uint32_t* d_comp_delta, uint32_t* d_comp_rho);
 /* Epoch end for one server (track_resp, :221-235): xd += comp_delta, xr +=
  * comp_rho (my_delta / my_rho), sum_*[client_of_slot[s]] += comp_* (atomic;
  * the servers of a rank may collect concurrently), comp_* = 0. */

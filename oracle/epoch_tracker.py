@@ -18,7 +18,12 @@ import numpy as np
 
 
 class EpochTrackers:
-    def __init__(self, n_servers, n_slots, n_clients=None, client_of_slot=None):
+    """lag=True: the overlapped exchange of dmclock_amd/multiserver.py
+    (DeviceTrackers(lagged=True)): an epoch's responses are handed to the
+    clients at the *next* epoch boundary (its sums all-reduced meanwhile);
+    finish() flushes the last one."""
+
+    def __init__(self, n_servers, n_slots, n_clients=None, client_of_slot=None, lag=False):
         G = n_slots if n_clients is None else n_clients
         self.S, self.N, self.G = n_servers, n_slots, G
         if client_of_slot is None:
@@ -31,6 +36,8 @@ class EpochTrackers:
         self.known = np.zeros((n_servers, n_slots), bool)
         self.comp_d = np.zeros((n_servers, n_slots), np.uint32)
         self.comp_r = np.zeros((n_servers, n_slots), np.uint32)
+        self.lag = lag
+        self.pend = None  # lag: (sum_d, sum_r, comp_d, comp_r) of the last epoch
 
     def fill(self, s, reqs):
         """get_req_params(s) for every request of `reqs` (batch order); sets
@@ -73,13 +80,31 @@ class EpochTrackers:
     def deliver(self, sum_d=None, sum_r=None):
         """Epoch boundary: the global counters advance by every server's
         responses (sum_d/sum_r: the all-ranks sums; default: this object's
-        servers), each server's X by its own (my_delta / my_rho)."""
+        servers), each server's X by its own (my_delta / my_rho).  lag: the
+        previous epoch's responses are applied, this epoch's held back."""
         if sum_d is None:
             sum_d, sum_r = self.local_sums()
+        if self.lag:
+            prev = self.pend
+            self.pend = (sum_d.copy(), sum_r.copy(), self.comp_d.copy(), self.comp_r.copy())
+            self.comp_d[:] = 0
+            self.comp_r[:] = 0
+            if prev is not None:
+                self._apply(*prev)
+            return
+        self._apply(sum_d, sum_r, self.comp_d, self.comp_r)
+        self.comp_d[:] = 0
+        self.comp_r[:] = 0
+
+    def finish(self):
+        """lag: apply the last epoch's held-back responses"""
+        if self.lag and self.pend is not None:
+            self._apply(*self.pend)
+            self.pend = None
+
+    def _apply(self, sum_d, sum_r, comp_d, comp_r):
         with np.errstate(over="ignore"):
             self.gd += sum_d
             self.gr += sum_r
-            self.xd += self.comp_d
-            self.xr += self.comp_r
-        self.comp_d[:] = 0
-        self.comp_r[:] = 0
+            self.xd += comp_d
+            self.xr += comp_r

@@ -75,7 +75,54 @@ def test_epoch_restatement_matches_sequential_tracker(mapped):
         et.deliver()
 
 
-def _gloo_worker(rank, world, port, q):
+def test_lagged_restatement_matches_sequential_tracker():
+    """The overlapped exchange (lag=True): epoch e's responses reach the
+    clients at boundary e + 1, i.e. the sequential ServiceTracker receives
+    its track_resp calls one epoch late -- otherwise the same arithmetic
+    (dmclock_client.h:221-251); finish() flushes the last epoch."""
+    rng = np.random.default_rng(4)
+    S, N, G = 3, 40, 70
+    cmap = client_maps(rng, S, N, G)
+    et = EpochTrackers(S, N, G, cmap, lag=True)
+    seq = [pyoracle.Tracker("orig") for _ in range(G)]
+    held = []  # the responses of the epoch whose delivery is pending
+    asked = [[] for _ in range(S)]
+    for epoch in range(7):
+        for s in range(S):
+            reqs = np.zeros(rng.integers(5, 60), dtype=REQUEST_DTYPE)
+            reqs["slot"] = rng.integers(0, N, len(reqs))
+            asked[s] = sorted(set(asked[s]) | set(reqs["slot"].tolist()))
+            et.fill(s, reqs)
+            for i in range(len(reqs)):
+                d, r = seq[cmap[s, reqs["slot"][i]]].get_req_params(s)
+                assert (d, r) == (reqs["delta"][i], reqs["rho"][i]), (epoch, s, i)
+        cur = []
+        for s in range(S):
+            # (responses answer requests: the slots this server was asked by)
+            n = int(rng.integers(5, 40))
+            dec = np.zeros(n, dtype=DECISION_DTYPE)
+            dec["slot"] = rng.choice(asked[s], n)
+            dec["cost"] = rng.integers(1, 4, n)
+            dec["phase"] = rng.integers(0, 2, n)
+            et.tally(s, dec)
+            cur += [(s, x) for x in dec]
+        et.deliver()
+        for s, x in held:  # the previous epoch's responses arrive now
+            seq[cmap[s, x["slot"]]].track_resp(s, int(x["phase"]), int(x["cost"]))
+        held = cur
+    et.finish()
+    for s, x in held:
+        seq[cmap[s, x["slot"]]].track_resp(s, int(x["phase"]), int(x["cost"]))
+    for s in range(S):  # one more request each: every counter delivered
+        for slot in range(N):
+            reqs = np.zeros(1, dtype=REQUEST_DTYPE)
+            reqs["slot"] = slot
+            et.fill(s, reqs)
+            d, r = seq[cmap[s, slot]].get_req_params(s)
+            assert (d, r) == (reqs["delta"][0], reqs["rho"][0]), (s, slot)
+
+
+def _gloo_worker(rank, world, port, q, lag=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -85,7 +132,7 @@ def _gloo_worker(rank, world, port, q):
         rng = np.random.default_rng(11)
         S_total, N = 4, 64
         S = S_total // world
-        et = EpochTrackers(S, N)
+        et = EpochTrackers(S, N, lag=lag)
         for epoch in range(4):
             for s in range(S):
                 gs = rank * S + s
@@ -100,18 +147,22 @@ def _gloo_worker(rank, world, port, q):
             dist.all_reduce(both, op=dist.ReduceOp.SUM)
             allr = both.numpy().view(np.uint32)
             et.deliver(allr[0], allr[1])
+        et.finish()
         q.put((rank, et.gd.copy(), et.gr.copy(), et.xd.copy()))
     finally:
         dist.destroy_process_group()
 
 
-def test_epoch_allreduce_gloo_world2():
-    """Per-rank sums + all-reduce == one process holding every server."""
+@pytest.mark.parametrize("lag", [False, True])
+def test_epoch_allreduce_gloo_world2(lag):
+    """Per-rank sums + all-reduce == one process holding every server (both
+    delivery schedules)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port + int(lag), q, lag))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = dict()
@@ -123,7 +174,7 @@ def test_epoch_allreduce_gloo_world2():
         assert p.exitcode == 0
     # single process, all 4 servers
     S_total, N = 4, 64
-    et = EpochTrackers(S_total, N)
+    et = EpochTrackers(S_total, N, lag=lag)
     for epoch in range(4):
         for gs in range(S_total):
             r2 = np.random.default_rng(100 * epoch + gs)
@@ -133,6 +184,7 @@ def test_epoch_allreduce_gloo_world2():
             dec["phase"] = r2.integers(0, 2, 50)
             et.tally(gs, dec)
         et.deliver()
+    et.finish()
     for rank in (0, 1):
         gd, gr, xd = res[rank]
         assert np.array_equal(gd, et.gd) and np.array_equal(gr, et.gr)
@@ -206,7 +258,7 @@ def _w2_workload():
     return cmap, tab, eps
 
 
-def _device_trackers_worker(rank, world, port, out_q, backend="gloo"):
+def _device_trackers_worker(rank, world, port, out_q, backend="gloo", lagged=False):
     """One rank: servers [rank * S, (rank + 1) * S) as GPU queues on cuda:0
     with DeviceTrackers, the per-epoch delivery all-reducing over `backend`
     (the product's DeviceTrackers.deliver: host-staged under gloo, on the
@@ -228,7 +280,7 @@ def _device_trackers_worker(rank, world, port, out_q, backend="gloo"):
         for q in qg:
             q.register(tab.slots, tab.r, tab.w, tab.l, True)
         dt = DeviceTrackers(qg, W2["N"], dev, n_clients=W2["G"],
-                            client_of_slot=cmap[mine])
+                            client_of_slot=cmap[mine], lagged=lagged)
         decs = []
         k = W2["k"]
         for t, ep in eps:
@@ -254,22 +306,23 @@ def _device_trackers_worker(rank, world, port, out_q, backend="gloo"):
                 dg = d_out.cpu().numpy().view(DECISION_DTYPE)[:res.n_decisions].copy()
                 decs.append(("dec", s, dg))
             dt.deliver()
+        dt.finish()
         st = dt.state()
-        out_q.put((rank, st, decs))
+        out_q.put((rank, st, decs, dt.allreduce_ms))
         for q in qg:
             q.close()
     finally:
         dist.destroy_process_group()
 
 
-def _oracle_reference(world):
+def _oracle_reference(world, lag=False):
     """all four servers on the oracle with the epoch restatement"""
     cmap, tab, eps = _w2_workload()
     S_total, N, G, k = W2["S_total"], W2["N"], W2["G"], W2["k"]
     qo = [pyoracle.OracleQueue() for _ in range(S_total)]
     for q in qo:
         q.register(tab.slots, tab.r, tab.w, tab.l, True)
-    et = EpochTrackers(S_total, N, G, cmap)
+    et = EpochTrackers(S_total, N, G, cmap, lag=lag)
     want = {}
     for e, (t, ep) in enumerate(eps):
         for s in range(S_total):
@@ -282,11 +335,13 @@ def _oracle_reference(world):
             et.tally(s, do)
             want[("dec", e, s)] = do
         et.deliver()
+    et.finish()
     return eps, et, want
 
 
 @pytest.mark.gpu
-def test_device_trackers_world1_rccl():
+@pytest.mark.parametrize("lagged", [False, True])
+def test_device_trackers_world1_rccl(lagged):
     """The RCCL branch of DeviceTrackers.deliver: one rank on GPU 0 in an
     `nccl` (RCCL) process group holding all four servers -- every epoch's
     all-reduce runs through RCCL on the device buffers (the identity at
@@ -298,14 +353,17 @@ def test_device_trackers_world1_rccl():
     ctx = mp.get_context("spawn")
     out_q = ctx.Queue()
     port = 31500 + os.getpid() % 1000
-    p = ctx.Process(target=_device_trackers_worker, args=(0, 1, port, out_q, "nccl"))
+    p = ctx.Process(target=_device_trackers_worker,
+                    args=(0, 1, port + int(lagged), out_q, "nccl", lagged))
     p.start()
     try:
-        rank, st, decs = out_q.get(timeout=240)
+        rank, st, decs, ar_ms = out_q.get(timeout=240)
     finally:
         p.join(timeout=60)
     assert p.exitcode == 0
-    eps, et, want = _oracle_reference(1)
+    if lagged:  # the overlapped all-reduce ran (and was timed) every epoch
+        assert len(ar_ms) == W2["epochs"], ar_ms
+    eps, et, want = _oracle_reference(1, lag=lagged)
     n_dec = 0
     it = iter(decs)
     S = W2["S_total"]
@@ -324,7 +382,8 @@ def test_device_trackers_world1_rccl():
 
 
 @pytest.mark.gpu
-def test_device_trackers_world2_gloo():
+@pytest.mark.parametrize("lagged", [False, True])
+def test_device_trackers_world2_gloo(lagged):
     """Two ranks sharing GPU 0, two server queues each, device trackers with
     the per-epoch all-reduce of DeviceTrackers.deliver over gloo: every
     request's delta/rho, every decision and the final tracker state equal one
@@ -334,14 +393,15 @@ def test_device_trackers_world2_gloo():
     ctx = mp.get_context("spawn")
     out_q = ctx.Queue()
     port = 30500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_device_trackers_worker, args=(r, 2, port, out_q))
+    procs = [ctx.Process(target=_device_trackers_worker,
+                         args=(r, 2, port + int(lagged), out_q, "gloo", lagged))
              for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     try:
         for _ in procs:
-            rank, st, decs = out_q.get(timeout=240)
+            rank, st, decs, _ = out_q.get(timeout=240)
             res[rank] = (st, decs)
     finally:
         for p in procs:
@@ -354,7 +414,7 @@ def test_device_trackers_world2_gloo():
     qo = [pyoracle.OracleQueue() for _ in range(S_total)]
     for q in qo:
         q.register(tab.slots, tab.r, tab.w, tab.l, True)
-    et = EpochTrackers(S_total, N, G, cmap)
+    et = EpochTrackers(S_total, N, G, cmap, lag=lagged)
     want = {}
     for e, (t, ep) in enumerate(eps):
         for s in range(S_total):
@@ -367,6 +427,7 @@ def test_device_trackers_world2_gloo():
             et.tally(s, do)
             want[("dec", e, s)] = do
         et.deliver()
+    et.finish()
     n_dec = 0
     for rank, (st, decs) in res.items():
         S = S_total // 2
