@@ -38,6 +38,7 @@ OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
 OPT_FAULT = 9
+OPT_HEAP_ORDER = 11
 OPT_SERVE = 10
 
 # PhaseType (dmclock_recs.h:33)

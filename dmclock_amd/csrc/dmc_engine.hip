@@ -1604,6 +1604,7 @@ struct FastIO {
 
 namespace {
 #include "dmc_serve.h"
+#include "dmc_heap.h"
 }  // namespace
 
 struct dmc_queue {
@@ -1650,6 +1651,12 @@ struct dmc_queue {
   // queue's stream is presumed wedged and every later call returns
   // DMC_EDEVICE instead of blocking on it
   bool wedged = false;
+  // DMC_OPT_HEAP_ORDER (dmc_heap.h): the reference's heaps on the device,
+  // every add and pull in call order
+  bool heap = false;
+  HeapDev hd{};
+  HeapPullRes* h_hres = nullptr;  // pinned
+  HeapPullRes* d_hres = nullptr;
   // DMC_SERVE_TRACE: per-call phases (k_serve's wall-clock stamps), printed
   // at destroy: read, work, publish (ticks) and the host's call time (ns)
   bool serve_trace = getenv("DMC_SERVE_TRACE") != nullptr;
@@ -3340,6 +3347,113 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
   return DMC_OK;
 }
 
+// ------------------------------------------------------------ heap order
+// (DMC_OPT_HEAP_ORDER: dmc_heap.h)
+int heap_enable(dmc_queue* q, uint32_t k) {
+  if (q->n_registered || k < 2 || k > 64) return DMC_EINVAL;
+  if (q->heap) return DMC_OK;
+  const size_t N = q->p.max_clients;
+  DALLOC(q, &q->hd.hp, 3 * 4 * N);
+  DALLOC(q, &q->hd.hix, 3 * 4 * N);
+  DALLOC(q, &q->hd.cnt, 4 * 4);
+  HIP_OK(hipMemsetAsync(q->hd.cnt, 0, 16, q->stream));
+  if (!q->h_hres) HIP_OK(hipHostMalloc((void**)&q->h_hres, sizeof(HeapPullRes), 0));
+  DALLOC(q, &q->d_hres, sizeof(HeapPullRes));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  q->hd.n = (uint32_t)N;
+  q->hd.k = k;
+  q->heap = true;
+  return DMC_OK;
+}
+
+// n adds in call order (d_reqs, d_rc device-resident)
+int heap_add(dmc_queue* q, uint32_t n, const dmc_request* d_reqs, int32_t* d_rc) {
+  if (!n) return DMC_OK;
+  AddParams p{d_reqs, d_rc, q->tick, n, 0};
+  hipLaunchKernelGGL(k_heap_add, dim3(1), dim3(kHeapThreads), 0, q->stream, q->tb, q->hd, p);
+  HIP_OK(hipGetLastError());
+  q->tick += n;
+  if (q->n_idle) q->idle_unknown = true;  // (activations happened on the device)
+  return DMC_OK;
+}
+
+// k pulls at `now` into d_out; the result (also to d_result when given)
+int heap_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
+              dmc_pull_result* d_result, dmc_pull_result* r) {
+  if (info_steps(q)) {
+    // U1 + delayed with a host client_info_f: one pull at a time, the
+    // popped client's info fetched between its selection and its pop
+    dmc_pull_result acc{};
+    acc.next_type = DMC_NEXT_RETURNING;
+    uint32_t n = 0;
+    while (n < k) {
+      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, 1u,
+                         q->p.at_limit, q->tick, d_out + n, q->d_hres,
+                         (dmc_pull_result*)nullptr, q->sched, 1);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(q->h_hres, q->d_hres, sizeof(HeapPullRes), hipMemcpyDeviceToHost,
+                            q->stream));
+      HIP_OK(hipStreamSynchronize(q->stream));
+      const HeapPullRes h = *q->h_hres;
+      if (h.type != DMC_NEXT_RETURNING) {
+        acc.next_type = h.type;
+        acc.when = h.type == DMC_NEXT_FUTURE ? h.when : 0.0;
+        break;
+      }
+      const uint32_t s = h.pend_slot;
+      if (int rc = fetch_infos(q, 1, &s, sizeof(uint32_t), false)) return rc;
+      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, 1u,
+                         q->p.at_limit, q->tick, d_out + n, q->d_hres,
+                         (dmc_pull_result*)nullptr, q->sched, 2);
+      HIP_OK(hipGetLastError());
+      ++n;
+      (h.pend_prio ? acc.n_priority : acc.n_reservation)++;
+    }
+    HIP_OK(hipStreamSynchronize(q->stream));
+    acc.n_decisions = n;
+    q->ctr.decisions += n;
+    q->ctr.single_steps += n;
+    if (d_result) {
+      hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, d_result, acc);
+      HIP_OK(hipGetLastError());
+    }
+    if (r) *r = acc;
+    return DMC_OK;
+  }
+  hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, k,
+                     q->p.at_limit, q->tick, d_out, q->d_hres, d_result, q->sched, 0);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(q->h_hres, q->d_hres, sizeof(HeapPullRes), hipMemcpyDeviceToHost,
+                        q->stream));
+  HIP_OK(hipStreamSynchronize(q->stream));
+  const HeapPullRes h = *q->h_hres;
+  dmc_pull_result x{};
+  x.n_decisions = h.n;
+  x.next_type = h.type;
+  x.when = h.type == DMC_NEXT_FUTURE ? h.when : 0.0;
+  x.n_priority = h.n_prio;
+  x.n_reservation = h.n_res;
+  q->ctr.decisions += h.n;
+  q->ctr.single_steps += h.n;
+  if (r) *r = x;
+  return DMC_OK;
+}
+
+// a host list of slots to one of the heap kernels
+int heap_list(dmc_queue* q, void (*kern)(Table, HeapDev, const uint32_t*, uint32_t),
+              const std::vector<uint32_t>& slots) {
+  if (slots.empty()) return DMC_OK;
+  uint32_t* d = nullptr;
+  HIP_OK(hipMalloc(&d, 4 * slots.size()));
+  HIP_OK(hipMemcpyAsync(d, slots.data(), 4 * slots.size(), hipMemcpyHostToDevice, q->stream));
+  hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, (const uint32_t*)d,
+                     (uint32_t)slots.size());
+  const hipError_t e = hipGetLastError();
+  HIP_OK(hipStreamSynchronize(q->stream));
+  dfree(d);
+  return e == hipSuccess ? DMC_OK : DMC_EDEVICE;
+}
+
 }  // namespace
 
 // ====================================================================== C-ABI
@@ -3526,6 +3640,8 @@ int dmc_queue_destroy(dmc_queue* q) {
   dfree(q->atl.Mj); dfree(q->atl.cX); dfree(q->atl.cP); dfree(q->atl.cT); dfree(q->atl.cPd);
   dfree(q->atl.cMo);
   dfree(q->act_xbase); dfree(q->act_fail);
+  dfree(q->hd.hp); dfree(q->hd.hix); dfree(q->hd.cnt); dfree(q->d_hres);
+  if (q->h_hres) (void)hipHostFree(q->h_hres);
   if (q->h_actm) (void)hipHostFree(q->h_actm);
   dfree(q->d_mark);
   if (q->h_mark) (void)hipHostFree(q->h_mark);
@@ -3571,6 +3687,13 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   for (uint32_t i = 0; i < n; ++i)
     if (slots[i] >= q->p.max_clients) return DMC_EINVAL;
   if (!n) return DMC_OK;
+  if (q->heap) {  // heap order: new, distinct clients only (client_map.emplace)
+    std::vector<uint32_t> v(slots, slots + n);
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end()) return DMC_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+      if (q->reg_h[slots[i]]) return DMC_EINVAL;
+  }
   std::vector<double> ri(n), wi(n), li(n);
   for (uint32_t i = 0; i < n; ++i) {
     ri[i] = inv_of(r[i]);
@@ -3589,6 +3712,9 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   HIP_OK(hipMemcpyAsync(d_l, li.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
   hipLaunchKernelGGL(k_register, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      q->stream, q->tb, q->binfo, n, d_slots, d_r, d_w, d_l, active, q->tick);
+  if (q->heap)  // three pushes per client, in the given order (:925-931)
+    hipLaunchKernelGGL(k_heap_push, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd,
+                       (const uint32_t*)d_slots, n);
   HIP_OK(hipStreamSynchronize(q->stream));
   dfree(d_slots); dfree(d_r); dfree(d_w); dfree(d_l);
   for (uint32_t i = 0; i < n; ++i) {
@@ -3911,6 +4037,7 @@ int dmc_client_erase(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
   for (size_t i = 0; i < ents.size() && i < cap; ++i)
     if (handles_out) handles_out[i] = ents[i].handle;
   if (n_out) *n_out = (uint32_t)ents.size();
+  if (q->heap && (rc = heap_list(q, k_heap_remove, {slot}))) return rc;
   const ScanRec z{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};  // no requests, not registered
   HIP_OK(hipMemcpyAsync(q->tb.sc + slot, &z, sizeof(z), hipMemcpyHostToDevice, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
@@ -3986,6 +4113,24 @@ int dmc_add_batch(dmc_queue* q, uint32_t n, const dmc_request* reqs,
   QueueLock g(q, true);
   ++q->gen;
   if (g.rc) return g.rc;
+  if (q->heap) {  // heap order: every add in call order on the device
+    if (int rc0 = serve_quiesce(q)) return rc0;
+    if (!n) return DMC_OK;
+    int rc = ensure_batch(q, n);
+    if (rc) return rc;
+    // U1 with a host client_info_f: the infos the batch's tags read
+    rc = fetch_infos(q, n, &reqs[0].slot, sizeof(dmc_request), true);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(q->d_reqs, reqs, sizeof(dmc_request) * n, hipMemcpyHostToDevice,
+                          q->stream));
+    rc = heap_add(q, n, q->d_reqs, q->d_rc);
+    if (rc) return rc;
+    std::vector<int32_t> rcs(n);
+    HIP_OK(hipMemcpyAsync(rcs.data(), q->d_rc, 4ull * n, hipMemcpyDeviceToHost, q->stream));
+    HIP_OK(hipStreamSynchronize(q->stream));
+    if (rc_out) std::memcpy(rc_out, rcs.data(), 4ull * n);
+    return DMC_OK;
+  }
   if (n == 1 && serve_add_ok(q, reqs[0])) return serve_add(q, reqs[0], rc_out);
   if (int rc0 = serve_quiesce(q)) return rc0;
   if (int rc0 = settle_act(q)) return rc0;
@@ -4027,6 +4172,7 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   if (g.rc) return g.rc;
   ++q->gen;
   if (!n) return DMC_OK;
+  if (q->heap) return heap_add(q, n, d_reqs, d_rc_out);
   int rc = ensure_batch(q, n);
   if (rc) return rc;
   rc = settle_act(q);
@@ -4057,6 +4203,21 @@ int dmc_pull_batch(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
   QueueLock g(q, true);
   ++q->gen;
   if (g.rc) return g.rc;
+  if (q->heap) {
+    if (int rc0 = serve_quiesce(q)) return rc0;
+    int rc = ensure_dec(q, k);
+    if (rc) return rc;
+    dmc_pull_result r{};
+    rc = heap_pull(q, now, k, q->d_dec, nullptr, &r);
+    if (rc) return rc;
+    if (r.n_decisions) {
+      HIP_OK(hipMemcpyAsync(out, q->d_dec, sizeof(dmc_decision) * r.n_decisions,
+                            hipMemcpyDeviceToHost, q->stream));
+      HIP_OK(hipStreamSynchronize(q->stream));
+    }
+    if (result) *result = r;
+    return DMC_OK;
+  }
   if (q->serve_on && fast_pull_ok(q, k)) return serve_pull(q, now, k, out, result);
   if (int rc0 = serve_quiesce(q)) return rc0;
   if (fast_pull_ok(q, k)) return fast_pull(q, now, k, out, result);
@@ -4079,6 +4240,7 @@ int dmc_pull_batch_device(dmc_queue* q, double now, uint32_t k,
   QueueLock g(q);
   if (g.rc) return g.rc;
   ++q->gen;
+  if (q->heap) return heap_pull(q, now, k, d_out, d_result, nullptr);
   dmc_pull_result r{};
   bool dev_wrote = false;
   int rc = pull_impl(q, now, k, d_out, &r, d_result, &dev_wrote);
@@ -4103,6 +4265,10 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
     QueueLock g(q);
     if (g.rc) return g.rc;
   ++q->gen;
+  if (q->heap) {
+    if (int rc = heap_add(q, n, d_reqs, d_rc_out)) return rc;
+    return heap_pull(q, now, k, d_out, d_result, nullptr);
+  }
   if (int rc0 = settle_act(q)) return rc0;
     fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
            !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
@@ -4193,7 +4359,8 @@ int dmc_group_create(dmc_queue* const* queues, uint32_t n, dmc_group** out) {
   const dmc_queue_params& p0 = queues[0]->p;
   for (uint32_t i = 0; i < n; ++i) {
     const dmc_queue* q = queues[i];
-    if (!q || q->group || q->p.device != p0.device || q->p.max_clients != p0.max_clients ||
+    if (!q || q->group || q->heap || q->p.device != p0.device ||
+        q->p.max_clients != p0.max_clients ||
         q->p.ring_capacity != p0.ring_capacity)
       return DMC_EINVAL;
     for (uint32_t j = 0; j < i; ++j)
@@ -4460,7 +4627,9 @@ int dmc_remove_by_client(dmc_queue* q, uint32_t slot, int reverse,
   for (uint32_t i = 0; i < n && i < cap; ++i)
     if (handles_out) handles_out[i] = ents[reverse ? n - 1 - i : i].handle;
   if (n_out) *n_out = n;
-  return write_queue(q, slot, {}, false);
+  rc = write_queue(q, slot, {}, false);
+  if (!rc && q->heap) rc = heap_list(q, k_heap_adjust, {slot});  // (:621-625)
+  return rc;
 }
 
 int dmc_client_requests(dmc_queue* q, uint32_t slot, uint64_t* handles_out,
@@ -4495,7 +4664,9 @@ int dmc_client_filter(dmc_queue* q, uint32_t slot, uint32_t n,
   for (uint32_t i = 0; i < n; ++i)
     if (keep[i]) kept.push_back(ents[i]);
   if (kept.size() == ents.size()) return DMC_OK;
-  return write_queue(q, slot, kept, n > 0 && keep[0]);
+  rc = write_queue(q, slot, kept, n > 0 && keep[0]);
+  if (!rc && q->heap) rc = heap_list(q, k_heap_adjust, {slot});  // (:580-584)
+  return rc;
 }
 
 int dmc_queue_requests(dmc_queue* q, uint32_t* counts_out, uint64_t* handles_out,
@@ -4555,6 +4726,17 @@ int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_rem
   HIP_OK(hipMemcpyAsync(&a, any.p, 4, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   if (any_removed) *any_removed = a != 0;
+  if (q->heap && a) {  // adjust x 3 for every modified client, ascending (:580-584)
+    std::vector<uint32_t> mod;
+    uint64_t at = 0;
+    for (uint32_t s = 0; s < N; ++s) {
+      bool m = false;
+      for (uint32_t j = 0; j < hc[s]; ++j) m |= !keep[at + j];
+      at += hc[s];
+      if (m) mod.push_back(s);
+    }
+    if (int rc = heap_list(q, k_heap_adjust, mod)) return rc;
+  }
   return DMC_OK;
 }
 
@@ -4578,6 +4760,9 @@ int dmc_client_erase_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   if (n_out) *n_out = 0;
   if (!n) return DMC_OK;
   ++q->gen;
+  if (q->heap) {  // delete_from_heaps, in the given order, before the state goes
+    if (int rc = heap_list(q, k_heap_remove, std::vector<uint32_t>(slots, slots + n))) return rc;
+  }
   DevBuf ds, counts, offs, hs;
   if (ds.alloc(4ull * n) || counts.alloc(4ull * n) || offs.alloc(4ull * n)) return DMC_ENOMEM;
   HIP_OK(hipMemcpyAsync(ds.p, slots, 4ull * n, hipMemcpyHostToDevice, q->stream));
@@ -4738,6 +4923,9 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       q->serve_on = value != 0;
       if (q->serve_on != q->serve_reg) serve_register(q, q->serve_on);
       return DMC_OK;
+    case DMC_OPT_HEAP_ORDER:
+      if (value == 0) return q->heap ? DMC_EINVAL : DMC_OK;
+      return heap_enable(q, (uint32_t)value);
     case DMC_OPT_FAULT:
       if (value < 0) return DMC_EINVAL;
       q->fault = (uint32_t)value;

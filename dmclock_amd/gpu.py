@@ -125,11 +125,13 @@ class GpuQueue:
     def __init__(self, max_clients=1024, ring_capacity=64, max_batch=1 << 16,
                  delayed=False, dynamic_info=False, at_limit=0,
                  reject_threshold=0.0, anticipation=0.0, device=0,
-                 branching=2, track_ties=True, info_callback=True):
+                 branching=2, track_ties=True, info_callback=True, heap_order=False):
         """info_callback (U1 only): client_info_f through the engine's
         dmc_info_fn; False: the caller publishes changes with bind_info
-        (explicit_bind), the device-API callers' contract."""
-        del branching, track_ties  # no heaps on the device
+        (explicit_bind), the device-API callers' contract.  heap_order:
+        tie-exact dispatch (DMC_OPT_HEAP_ORDER, the reference's `branching`-ary
+        heaps on the device); otherwise branching has no meaning (no heaps)."""
+        del track_ties
         self.L = lib()
         p = QueueParams()
         p.max_clients = max_clients
@@ -146,6 +148,10 @@ class GpuQueue:
                "dmc_queue_create")
         self.h = h
         self.params = p
+        if heap_order:
+            from ._abi import OPT_HEAP_ORDER
+            _check(self.L.dmc_queue_set_option(self.h, OPT_HEAP_ORDER, int(branching)),
+                   "set_option(HEAP_ORDER)")
         self.dynamic = bool(dynamic_info)
         self.slot_of = {}      # client id -> slot
         self.client_of = []    # slot -> client id

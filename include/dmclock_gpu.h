@@ -390,6 +390,14 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
 #define DMC_OPT_BREAK_ROUNDS 8  /* 1 (default): AtLimit::Allow's limit breaks (dmclock_server.h:1157-1165)
                                   run as batched rounds after the eligible work ran out (immediate
                                   mode); 0: one general pull_request step each */
+#define DMC_OPT_HEAP_ORDER 11   /* K >= 2: tie-exact dispatch -- the reference's three indirect
+                                  K-ary heaps (IndIntruHeap, dmclock_server.h:768-797) kept on the
+                                  device and driven in the reference's order; among equal keys the
+                                  reference's heap top wins (default: lowest slot, flagged).  Every
+                                  add and pull then runs in call order on one workgroup (exact, not
+                                  fast).  Set before the first client is registered; clients may
+                                  be registered once; queue groups do not take such queues.
+                                  0: off (default) */
 #define DMC_OPT_FAIL_ALLOC 7    /* test hook: the queue's next `value` device buffer allocations
                                   (growth of its batch, decision, radix and activation buffers)
                                   fail; the call returns DMC_ENOMEM, the queue stays usable */
