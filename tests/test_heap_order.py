@@ -62,7 +62,7 @@ def test_config2_without_jitter_tie_exact():
         return pyoracle.OracleQueue(at_limit=at_limit, anticipation=antic)
 
     def gpu(at_limit, antic):
-        return GpuQueue(max_clients=ncl, ring_capacity=128, max_batch=1024,
+        return GpuQueue(max_clients=ncl, ring_capacity=64, max_batch=1024,
                         at_limit=at_limit, anticipation=antic, heap_order=True)
 
     o = sim.Simulation(conf, ora, seed=7, jitter=0.0).run(max_events=10_000_000)
