@@ -53,6 +53,44 @@ struct ActBuf {
   const uint32_t* dm = nullptr;
 };
 
+// Client trackers fused into the add (a queue group's step, config 5):
+// get_req_params (dmclock_client.h:241-251) for every request of the batch,
+// written into the request before its tag is calculated -- the first request
+// of a (server, client) pair in batch order gets the responses since its
+// previous request (or (1, 1) from a server it never asked), later ones
+// (0, 0) -- exactly what dmc_tracker_fill's two kernels compute, without
+// their separate passes over the batch.
+struct TrackFill {
+  dmc_request* reqs;  // the batch (delta / rho written back)
+  const uint32_t *cmap, *gd, *gr;
+  uint32_t *xd, *xr;
+  uint8_t* known;
+  uint32_t nslots;
+};
+
+// (the pair's state, loaded ahead: *c the global client; its counters next)
+struct TrackSlot {
+  uint32_t xd, xr, c;
+  uint8_t known;
+};
+__device__ inline TrackSlot track_load(const TrackFill& t, uint32_t s) {
+  return TrackSlot{t.xd[s], t.xr[s], t.cmap ? t.cmap[s] : s, t.known[s]};
+}
+// the first request's parameters; the pair's state moves to the counters
+__device__ inline void track_first(const TrackFill& t, uint32_t s, const TrackSlot& ts,
+                                   uint32_t D, uint32_t R, uint32_t* delta, uint32_t* rho) {
+  if (!ts.known) {
+    t.known[s] = 1;
+    *delta = 1;
+    *rho = 1;
+  } else {
+    *delta = D - ts.xd;
+    *rho = R - ts.xr;
+  }
+  t.xd[s] = D;
+  t.xr[s] = R;
+}
+
 // do_add_request for one client's requests of the batch, in batch order:
 // minus the idle reset (handled before, per activation), initial_tag
 // (:878-907), the Reject check (:989-993), the enqueue and cur_rho/cur_delta
@@ -141,10 +179,38 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   p.rc[pos] = DMC_OK;
 }
 
-// Slot s of the batch is not registered: every request of it gets ENOTREG.
+// Slot s of the batch is not registered: every request of it gets ENOTREG
+// (with fused trackers its requests still get their parameters, as
+// dmc_tracker_fill gives them to every request of a table slot).
 __device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t m,
                                         uint32_t i1, const uint32_t* abuf,
-                                        const uint32_t* aslot) {
+                                        const uint32_t* aslot, const TrackFill* tf = nullptr) {
+  if (tf && s < tf->nslots) {
+    uint32_t first = i1;
+    if (m <= kAddSlots) {
+      for (uint32_t j = 1; j < m; ++j) first = min(first, abuf[(size_t)s * kAddSlots + j]);
+    } else {
+      for (uint32_t j = 0; j < p.n; ++j)
+        if (aslot[j] == s) {
+          first = j;
+          break;
+        }
+    }
+    const TrackSlot ts = track_load(*tf, s);
+    uint32_t d0, r0;
+    track_first(*tf, s, ts, tf->gd[ts.c], tf->gr[ts.c], &d0, &r0);
+    auto put = [&](uint32_t pos) {
+      tf->reqs[pos].delta = pos == first ? d0 : 0u;
+      tf->reqs[pos].rho = pos == first ? r0 : 0u;
+    };
+    if (m <= kAddSlots) {
+      put(i1);
+      for (uint32_t j = 1; j < m; ++j) put(abuf[(size_t)s * kAddSlots + j]);
+    } else {
+      for (uint32_t j = 0; j < p.n; ++j)
+        if (aslot[j] == s) put(j);
+    }
+  }
   if (m <= kAddSlots) {
     p.rc[i1] = DMC_ENOTREG;
     for (uint32_t j = 1; j < m; ++j) p.rc[abuf[(size_t)s * kAddSlots + j]] = DMC_ENOTREG;
@@ -167,11 +233,20 @@ __device__ inline void add_chain_notreg(const AddParams& p, uint32_t s, uint32_t
 __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint32_t s,
                                       uint32_t m, uint32_t i1, const uint32_t* abuf,
                                       const uint32_t* aslot, const ActBuf& act,
-                                      AddState* out, bool counted = false) {
+                                      AddState* out, bool counted = false,
+                                      const TrackFill* tf = nullptr) {
   const uint32_t i = i1;
   // position i1's request, requested with the client's state (the usual
   // case, m == 1, needs nothing else from the batch)
   const dmc_request rq1 = p.reqs[i];
+  // fused trackers: the pair's state with the client's, its counters next
+  TrackSlot ts{};
+  uint32_t tD = 0, tR = 0;
+  if (tf) {
+    ts = track_load(*tf, s);
+    tD = tf->gd[ts.c];
+    tR = tf->gr[ts.c];
+  }
   // the ScanRec's cursor word: head, count, flags and the batch count
   uint64_t* cw = reinterpret_cast<uint64_t*>(&tb.sc[s].head);
   const uint64_t cur = *cw;
@@ -201,16 +276,28 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   };
   if (counted && !(st.flags & F_REG)) {
     store_cursor();  // (unchanged; the batch count cleared)
-    add_chain_notreg(p, s, m, i, abuf, aslot);
+    add_chain_notreg(p, s, m, i, abuf, aslot, tf);
     return;
   }
   const bool idle0 = (st.flags & F_IDLE) != 0;
   const uint32_t count0 = st.count;
   const double front_p0 = (act.cold && count0) ? ring[st.head & tb.qmask].p : 0.0;
   const double prev_p0 = st.prev.p;
-  bool act_done = false, chg_done = false;
+  bool act_done = false, chg_done = false, tf_done = false;
   auto step = [&](uint32_t pos) {
-    add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
+    if (tf) {  // get_req_params, batch order
+      dmc_request rq = pos == i ? rq1 : p.reqs[pos];
+      rq.delta = rq.rho = 0;
+      if (!tf_done) {
+        tf_done = true;
+        track_first(*tf, s, ts, tD, tR, &rq.delta, &rq.rho);
+      }
+      tf->reqs[pos].delta = rq.delta;
+      tf->reqs[pos].rho = rq.rho;
+      add_one(tb, st, ring, p, pos, &rq);
+    } else {
+      add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
+    }
     if (!act.cold) return;
     if (idle0) {
       const dmc_request& rq = p.reqs[pos];

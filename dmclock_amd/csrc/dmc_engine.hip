@@ -174,7 +174,7 @@ k_add_link(AddParams p, Table tb,
   add_link_body(p, tb, abuf, apos, aslot, pblk, act);
 }
 
-__device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act) {
+__device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act, const TrackFill* tf = nullptr) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // one level of loads: the call's parameters and this position's filing
   // (apos / aslot are padded to whole blocks: in bounds for the grid)
@@ -189,7 +189,7 @@ __device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, c
   if (pos0 != 0) return;  // the client's first filer replays its requests
   // the next: the client's batch count with its state
   AddState st;
-  add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, true);
+  add_chain_slot(tb, p, s, 0, i, abuf, aslot, act, &st, true, tf);
 }
 __global__ void 
 k_add_chain(Table tb, const AddParams* pblk,
@@ -205,6 +205,7 @@ struct AddArgs {
   Table tb;
   uint32_t *abuf, *apos, *aslot;
   AddParams* pblk;
+  TrackFill tf;  // the server's trackers, fused into the add (tf.reqs null: none)
 };
 __global__ void k_add_link_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
@@ -212,7 +213,7 @@ __global__ void k_add_link_m(const AddArgs* a) {
 }
 __global__ void k_add_chain_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
-  add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{});
+  add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{}, x.tf.reqs ? &x.tf : nullptr);
 }
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
@@ -4477,7 +4478,11 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                                 trk[i].first}
                     : TrackArgs{};
         aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, 0}, tb, q->abuf, q->apos,
-                        q->aslot, q->apblk};
+                        q->aslot, q->apblk,
+                        trk ? TrackFill{d_reqs[i], trk[i].client_of_slot, trk[i].gdelta,
+                                        trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
+                                        q->p.max_clients}
+                            : TrackFill{}};
         const CallParams cp{k, 0, now[i], d_out[i], q->tick + n,
                             d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, 0};
         sa[i] = RScanArgs{tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
@@ -4500,12 +4505,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       uint8_t* d = g->d_blob;
       auto enqueue = [&](hipStream_t st) {
         (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, st);
-        if (trk) {
-          hipLaunchKernelGGL(k_track_first_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                             (const TrackArgs*)(d + g->o_trk));
-          hipLaunchKernelGGL(k_track_params_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                             (const TrackArgs*)(d + g->o_trk));
-        }
+        // (the trackers' get_req_params run inside k_add_chain_m: TrackFill)
         hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                            (const AddArgs*)(d + g->o_add));
         hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,

@@ -91,8 +91,8 @@ def test_epoch_time_ties_tie_exact(mode):
     whose prop_delta aligns keys exactly, :957-985), random delta/rho, pulls
     of k in 1..64: many ties, every decision and state equal to the oracle's"""
     rng = np.random.default_rng(5)
-    tr = workloads.churn_trace(5, 700, 30, 150, 0, idle_frac=0.05, t0=1.7e9,
-                               k_choices=[1, 3, 17, 64])
+    tr = workloads.churn_trace(5, 700, 60, 150, 0, idle_frac=0.05, t0=1.7e9,
+                               k_choices=[1, 3, 17, 64, 128])
     if mode.get("at_limit") == AT_LIMIT_REJECT:
         tr.clients.l = np.where(rng.random(700) < 0.5, rng.uniform(0.3, 1.5, 700), 0.0)
     n, qg, qo = run_parity(tr, mk_heap(mode.get("branching", 2)), queue_kw=mode,
