@@ -207,11 +207,11 @@ struct AddArgs {
   AddParams* pblk;
   TrackFill tf;  // the server's trackers, fused into the add (tf.reqs null: none)
 };
-__global__ void k_add_link_m(const AddArgs* a) {
+__global__ void __launch_bounds__(kBlock) k_add_link_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
   add_link_body(x.p, x.tb, x.abuf, x.apos, x.aslot, x.pblk, ActBuf{});
 }
-__global__ void k_add_chain_m(const AddArgs* a) {
+__global__ void __launch_bounds__(kBlock) k_add_chain_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
   add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{}, x.tf.reqs ? &x.tf : nullptr);
 }

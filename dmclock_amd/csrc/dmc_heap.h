@@ -364,23 +364,16 @@ __global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at
     const HeapPullRes pr = *res;
     heap_pop(tb, H, pr.pend_slot, pr.pend_prio != 0, tick, out, sched);
     r.n = 1;
-    (pr.pend_prio ? r.n_prio : r.n_res) = 1;
+    if (pr.pend_prio) r.n_prio = 1;
+    else r.n_res = 1;
     *res = r;
     return;
   }
-  // (mode 1: the decided pop is recorded instead of made)
-  auto pop = [&](uint32_t s, bool prio) {
-    if (mode == 1) {
-      r.pend_slot = s;
-      r.pend_prio = prio ? 1u : 0u;
-      return false;
-    }
-    heap_pop(tb, H, s, prio, tick, out + r.n, sched);
-    ++r.n;
-    ++(prio ? r.n_prio : r.n_res);
-    return true;
-  };
+  // each iteration decides one pull (pop_slot / pop_prio) or stops; the pop
+  // is made at its end (mode 1: recorded for mode 2 instead)
   while (r.n < k) {
+    uint32_t pop_slot = kNone;
+    bool pop_prio = false;
     if (*H.resv.cnt == 0) {  // no clients: none (:1118-1120)
       r.type = DMC_NEXT_NONE;
       break;
@@ -388,57 +381,59 @@ __global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at
     const uint32_t rs = H.resv.top();
     const ScanRec rsr = tb.sc[rs];
     if (rsr.count && rsr.r <= now) {
-      if (pop(rs, false)) continue;
-      break;
-    }
-    for (;;) {  // the limit loop
-      const uint32_t ls = H.lim.top();
-      const ScanRec lr = tb.sc[ls];
-      if (!(lr.count && !(lr.flags & F_READY) && lr.l <= now)) break;
-      tb.sc[ls].flags = (uint8_t)(lr.flags | F_READY);
-      H.ready.promote(ls);
-      H.lim.demote(ls);
-    }
-    const uint32_t ps = H.ready.top();
-    const ScanRec pr = tb.sc[ps];
-    if (pr.count && (pr.flags & F_READY) && pr.pk < kInf) {
-      if (pop(ps, true)) continue;
-      break;
-    }
-    if (at_limit == DMC_AT_LIMIT_ALLOW) {
-      if (pr.count && pr.pk < kInf) {
-        if (pop(ps, true)) continue;
-        break;
-      }
-      if (rsr.count && rsr.r < kInf) {
-        if (pop(rs, false)) continue;
-        break;
-      }
-    }
-    // future / none (:1170-1185; min_not_0_time excludes exact 0, :1192-1195)
-    // (kMaxTime = DBL_MAX: an infinite tag is no future, :1170-1185)
-    constexpr double kTimeMax = 1.7976931348623157e308;
-    double next = kTimeMax;
-    bool have = false;
-    const uint32_t rt = H.resv.top(), lt = H.lim.top();
-    if (tb.sc[rt].count) {
-      const double v = tb.sc[rt].r;
-      if (v != 0.0) next = v < next ? v : next;
-      have = true;
-    }
-    if (tb.sc[lt].count) {
-      const double v = tb.sc[lt].l;
-      if (v != 0.0) next = v < next ? v : next;
-      have = true;
-    }
-    (void)have;
-    if (next < kTimeMax) {
-      r.type = DMC_NEXT_FUTURE;
-      r.when = next;
+      pop_slot = rs;
     } else {
-      r.type = DMC_NEXT_NONE;
+      for (;;) {  // the limit loop
+        const uint32_t ls = H.lim.top();
+        const ScanRec lr = tb.sc[ls];
+        if (!(lr.count && !(lr.flags & F_READY) && lr.l <= now)) break;
+        tb.sc[ls].flags = (uint8_t)(lr.flags | F_READY);
+        H.ready.promote(ls);
+        H.lim.demote(ls);
+      }
+      const uint32_t ps = H.ready.top();
+      const ScanRec pr = tb.sc[ps];
+      if (pr.count && (pr.flags & F_READY) && pr.pk < kInf) {
+        pop_slot = ps;
+        pop_prio = true;
+      } else if (at_limit == DMC_AT_LIMIT_ALLOW && pr.count && pr.pk < kInf) {
+        pop_slot = ps;
+        pop_prio = true;
+      } else if (at_limit == DMC_AT_LIMIT_ALLOW && rsr.count && rsr.r < kInf) {
+        pop_slot = rs;
+      }
     }
-    break;
+    if (pop_slot == kNone) {
+      // future / none (:1170-1185; min_not_0_time excludes exact 0,
+      // :1192-1195; kTimeMax = DBL_MAX: an infinite tag is no future)
+      constexpr double kTimeMax = 1.7976931348623157e308;
+      double next = kTimeMax;
+      const uint32_t rt = H.resv.top(), lt = H.lim.top();
+      if (tb.sc[rt].count) {
+        const double v = tb.sc[rt].r;
+        if (v != 0.0) next = v < next ? v : next;
+      }
+      if (tb.sc[lt].count) {
+        const double v = tb.sc[lt].l;
+        if (v != 0.0) next = v < next ? v : next;
+      }
+      if (next < kTimeMax) {
+        r.type = DMC_NEXT_FUTURE;
+        r.when = next;
+      } else {
+        r.type = DMC_NEXT_NONE;
+      }
+      break;
+    }
+    if (mode == 1) {
+      r.pend_slot = pop_slot;
+      r.pend_prio = pop_prio ? 1u : 0u;
+      break;
+    }
+    heap_pop(tb, H, pop_slot, pop_prio, tick, out + r.n, sched);
+    ++r.n;
+    if (pop_prio) ++r.n_prio;
+    else ++r.n_res;
   }
   *res = r;
   if (d_result) {
