@@ -2835,7 +2835,7 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
     if (q->debug)  // (the record counts: the rank-bin counters' low words)
       (void)hipMemcpy2DAsync(q->dbg_bins, sizeof(uint32_t), q->bcount, 2 * sizeof(uint32_t),
                              sizeof(uint32_t), kNBR, hipMemcpyDeviceToDevice, q->stream);
-    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kBlockR), 0, q->rd,
+    klaunch(q, DMC_PROF_RANK, k_rrank, dim3(kRankBlocksR), dim3(kRankThreads), 0, q->rd,
             (const unsigned long long*)q->bcount, (const unsigned long long*)q->bsup,
             (const BRecR*)q->brec, tb.ring, q->decof, q->debug ? q->dbg_wtime : nullptr);
   } else {
@@ -4516,7 +4516,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                            (const RHistArgs*)(d + g->o_hist));
         hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
                            (const REmitArgs*)(d + g->o_emit));
-        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kBlockR), 0, st,
+        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads), 0, st,
                            (const RRankArgs*)(d + g->o_rank));
         hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmit * gEm + 1, S), dim3(kBlockR), 0,
                            st, (const RApplyArgs*)(d + g->o_apply));

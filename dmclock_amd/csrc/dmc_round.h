@@ -49,6 +49,12 @@
 namespace dmc {
 
 constexpr int kBlockR = 256;
+// k_rrank's block (one rank bin each): 256 threads, or 128 so that all
+// 4096 bins' blocks are resident at once (16 per CU; build knob for A/B)
+#ifndef DMC_RANK_THREADS
+#define DMC_RANK_THREADS 256
+#endif
+constexpr int kRankThreads = DMC_RANK_THREADS;
 constexpr int kHistBinsR = 2048;        // per phase
 constexpr int kNBR = 4096;              // rank bins: R [0, 2048), P [2048, 4096)
 constexpr int kNBPhase = kNBR / 2;
@@ -512,9 +518,10 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
   for (int j = 0; j < kScanSlots; ++j) {
     uint32_t s = base + j * blockDim.x;
     pre[j] = ScanPre{0.0, 0.0, 0.0, 0.0};
-    if (s < tb.n && x[j].c && x[j].fr <= now && !tb.delayed && !brk) {
+    // (prop_delta only for a post-R front: a queue of one has none)
+    if (s < tb.n && x[j].c > 1 && x[j].fr <= now && !tb.delayed && !brk) {
       pre[j].pd = tb.rec[s].pd;
-      if (x[j].c > 1) {
+      {
         const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x[j].h + 1) & tb.qmask)];
         pre[j].r1 = e.r;
         pre[j].p1 = e.p;
@@ -1706,18 +1713,19 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
                                    bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
                                    uint32_t poff, ReqEntry* ring, dmc_decision* out,
                                    uint32_t* decof) {
-  static_assert(kBinCapR == 2 * kBlockR, "two records per thread");
+  constexpr uint32_t RP = kBinCapR / kRankThreads;  // sorted positions per thread
+  static_assert(kBinCapR % kRankThreads == 0 && RP <= 8, "whole positions per thread");
   __shared__ uint16_t ord[kBinCapR];
-  __shared__ uint32_t wsum[kBlockR / 64];
+  __shared__ uint32_t wsum[kRankThreads / 64];
   const uint32_t t = threadIdx.x;
   uint32_t P = 2;
   while (P < cnt) P <<= 1;
-  for (uint32_t i = t; i < P; i += kBlockR) ord[i] = (uint16_t)i;
+  for (uint32_t i = t; i < P; i += kRankThreads) ord[i] = (uint16_t)i;
   __syncthreads();
   for (uint32_t kk = 2; kk <= P; kk <<= 1) {
     for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-      const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i | j;
-      if (l < P) {
+      for (uint32_t u = t; u < P / 2; u += kRankThreads) {
+        const uint32_t i = ((u & ~(j - 1)) << 1) | (u & (j - 1)), l = i | j;
         const uint32_t a = ord[i], c = ord[l];
         // indices >= cnt (padding) order after every record
         const bool c_lt_a = c < cnt && (a >= cnt || bkey_less(sh[c], sh[a]));
@@ -1730,13 +1738,17 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
       __syncthreads();
     }
   }
-  // positions 2t, 2t + 1: their records, sizes, and the exclusive prefix
-  const uint32_t r0 = 2 * t, r1 = r0 + 1;
-  const uint32_t i0 = r0 < cnt ? ord[r0] : 0u, i1 = r1 < cnt ? ord[r1] : 0u;
-  const uint32_t z0 = r0 < cnt ? (isp ? 1u + sh[i0].run : 1u) : 0u;
-  const uint32_t z1 = r1 < cnt ? (isp ? 1u + sh[i1].run : 1u) : 0u;
+  // positions RP t .. RP t + RP - 1: their records, sizes, the exclusive prefix
+  uint32_t z[RP], ix[RP], zs = 0;
+#pragma unroll
+  for (uint32_t h = 0; h < RP; ++h) {
+    const uint32_t r = RP * t + h;
+    ix[h] = r < cnt ? ord[r] : 0u;
+    z[h] = r < cnt ? (isp ? 1u + sh[ix[h]].run : 1u) : 0u;
+    zs += z[h];
+  }
   const uint32_t lane = t & 63, w = t >> 6;
-  uint32_t incl = z0 + z1;
+  uint32_t incl = zs;
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint32_t o = __shfl_up(incl, d);
     if (lane >= d) incl += o;
@@ -1745,12 +1757,14 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
-  const uint32_t ex = pre + incl - (z0 + z1);
+  uint32_t ex = pre + incl - zs;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t r = h ? r1 : r0;
+  for (uint32_t h = 0; h < RP; ++h) {
+    const uint32_t r = RP * t + h;
+    const uint32_t exh = ex;
+    ex += z[h];
     if (r >= cnt) continue;
-    const uint32_t i = h ? i1 : i0;
+    const uint32_t i = ix[h];
     const BKey me = sh[i];
     uint32_t tie = 0;
     for (uint32_t q = r; q > 0 && sh[ord[q - 1]].okey == me.okey; --q)
@@ -1758,7 +1772,7 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
     for (uint32_t q = r + 1; q < cnt && sh[ord[q]].okey == me.okey; ++q)
       tie |= sh[ord[q]].slot != me.slot;
     const BRecR& x = src[i];
-    place_rec(rd, me, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, h ? ex + z0 : ex, tie, isp, k,
+    place_rec(rd, me, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, exh, tie, isp, k,
               n_pgroups, soff, poff, ring, out, decof);
   }
 }
@@ -1872,7 +1886,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
   const uint32_t cnt = s_hdr[0];
   if (cnt == 0 || fail0 || s_hdr[4]) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
-  for (uint32_t i = threadIdx.x; i < cnt; i += kBlockR) sh[i] = src[i].k;
+  for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) sh[i] = src[i].k;
   if (cnt > kRankSortMin) {
     rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof);
     if (wtime && threadIdx.x == 0) {
@@ -1882,11 +1896,11 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     return;
   }
   uint32_t parts = 1;
-  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kBlockR) parts <<= 1;
+  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kRankThreads) parts <<= 1;
   const uint32_t per = (cnt + parts - 1) / parts;
   __syncthreads();
   const uint32_t t = threadIdx.x;
-  for (uint32_t rb = 0; rb < cnt; rb += kBlockR / parts)
+  for (uint32_t rb = 0; rb < cnt; rb += kRankThreads / parts)
     rank_rec(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
              soff, poff, ring, out, decof);
   if (wtime && threadIdx.x == 0) {
@@ -1894,7 +1908,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     wtime[2 * b + 1] = wall_clock64();
   }
 }
-__global__ void __launch_bounds__(kBlockR)
+__global__ void __launch_bounds__(kRankThreads)
 k_rrank(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup,
         const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime = nullptr) {
   rrank_body(rd, bcount, gsup, brec, ring, decof, wtime);
@@ -2464,7 +2478,7 @@ __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const R
   remit_t_body<false>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof, x.brec,
                       x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
 }
-__global__ void __launch_bounds__(kBlockR) k_rrank_m(const RRankArgs* a) {
+__global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
   const RRankArgs& x = a[blockIdx.y];
   rrank_body(x.rd, x.bcount, x.gsup, x.brec, x.ring, x.decof, nullptr);
 }
