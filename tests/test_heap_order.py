@@ -123,7 +123,8 @@ def test_tied_trace_tie_exact(mode):
     qg.close()
 
 
-def test_maintenance_in_heap_order():
+@pytest.mark.parametrize("ops", ["erase", "remove_by_client", "filter", "all"])
+def test_maintenance_in_heap_order(ops):
     """erase (delete_from_heaps), remove_by_client and remove_by_req_filter
     (adjust x 3 per modified client) between tied pulls: the heaps stay the
     reference's"""
@@ -144,15 +145,18 @@ def test_maintenance_in_heap_order():
     h = int(tr.ops[0][1]["handle"].max()) + 1
     gone = set()
     for step in range(12):
-        if step % 3 == 0:
+        kind = ["erase", "remove_by_client", "filter"][step % 3]
+        if ops not in ("all", kind):
+            kind = None
+        if kind == "erase":
             gone |= {3 * step + 1, 3 * step + 2}
         for q in (qo, qg):
-            if step % 3 == 0:
+            if kind == "erase":
                 for cl in (3 * step + 1, 3 * step + 2):
                     assert q.erase(cl)
-            if step % 3 == 1:
+            if kind == "remove_by_client":
                 q.remove_by_client(5 * step, reverse=bool(step & 2))
-            if step % 3 == 2:
+            if kind == "filter":
                 q.remove_by_req_filter(lambda hd: hd % 7 == step % 7, backwards=bool(step & 4))
         reqs = workloads.arrivals(rng, 300, 200, t, 600.0, handle_base=h)
         reqs["time"] = np.round(reqs["time"], 2)
