@@ -3879,17 +3879,12 @@ __global__ void k_list_gather(Table tb, uint32_t n, const uint32_t* slots,
 // request's stored tag as the front tag, as the reference's deque does); the
 // front's ready flag survives only with the front; the heap keys follow the
 // new front.  *any != 0 if anything was removed.
-__global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
-                              const uint32_t* offs, const uint8_t* keep,
-                              uint32_t* any) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t s = list_slot(slots, i);
+// one client's compaction (kp: its keep flags, FIFO order); false: nothing removed
+__device__ inline bool list_filter_slot(const Table& tb, uint32_t s, const uint8_t* kp) {
   const ScanRec sr = tb.sc[s];
-  const uint8_t* kp = keep + offs[i];
   uint32_t c = sr.count, m = 0;
   for (uint32_t j = 0; j < c; ++j) m += kp[j] != 0;
-  if (m == c) return;
+  if (m == c) return false;
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   uint32_t w = 0;
   for (uint32_t j = 0; j < c; ++j) {
@@ -3909,7 +3904,29 @@ __global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
     o.r = o.pk = o.l = 0.0;
   }
   tb.sc[s] = o;
-  atomicOr(any, 1u);
+  return true;
+}
+
+__global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
+                              const uint32_t* offs, const uint8_t* keep,
+                              uint32_t* any) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (list_filter_slot(tb, list_slot(slots, i), keep + offs[i])) atomicOr(any, 1u);
+}
+
+// heap order (dmc_heap.h): remove_by_req_filter's loop (:567-585) in client
+// order -- each modified client filtered, then adjusted in the three heaps,
+// before the next one is filtered (a later client's adjust must see the
+// earlier clients' new fronts and the later ones' old ones)
+__global__ void k_heap_filter(Table tb, HeapDev hd, uint32_t n, const uint32_t* slots,
+                              const uint32_t* offs, const uint8_t* keep) {
+  if (threadIdx.x) return;
+  Heaps H(tb, hd);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = slots[i];
+    if (list_filter_slot(tb, s, keep + offs[s])) H.adjust3(s);
+  }
 }
 
 // do_clean's erase (:1244-1255) of the listed clients: queue dropped, slot
@@ -4717,6 +4734,27 @@ int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_rem
     return rc;
   if (total != n) return DMC_EINVAL;
   HIP_OK(hipMemcpyAsync(kp.p, keep, n, hipMemcpyHostToDevice, q->stream));
+  if (q->heap) {  // sequential, client order: filter, adjust, next client
+    std::vector<uint32_t> mod;
+    uint64_t at = 0;
+    for (uint32_t s = 0; s < N; ++s) {
+      bool m = false;
+      for (uint32_t j = 0; j < hc[s]; ++j) m |= !keep[at + j];
+      at += hc[s];
+      if (m) mod.push_back(s);
+    }
+    if (any_removed) *any_removed = !mod.empty();
+    if (mod.empty()) return DMC_OK;
+    DevBuf dm;
+    if (dm.alloc(4ull * mod.size())) return DMC_ENOMEM;
+    HIP_OK(hipMemcpyAsync(dm.p, mod.data(), 4ull * mod.size(), hipMemcpyHostToDevice, q->stream));
+    hipLaunchKernelGGL(k_heap_filter, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd,
+                       (uint32_t)mod.size(), (const uint32_t*)dm.u32(),
+                       (const uint32_t*)offs.u32(), (const uint8_t*)kp.u8());
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(q->stream));
+    return DMC_OK;
+  }
   HIP_OK(hipMemsetAsync(any.p, 0, 4, q->stream));
   hipLaunchKernelGGL(k_list_filter, dim3((N + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      q->stream, q->tb, N, (const uint32_t*)nullptr,
@@ -4726,17 +4764,6 @@ int dmc_queue_filter(dmc_queue* q, const uint8_t* keep, uint64_t n, int* any_rem
   HIP_OK(hipMemcpyAsync(&a, any.p, 4, hipMemcpyDeviceToHost, q->stream));
   HIP_OK(hipStreamSynchronize(q->stream));
   if (any_removed) *any_removed = a != 0;
-  if (q->heap && a) {  // adjust x 3 for every modified client, ascending (:580-584)
-    std::vector<uint32_t> mod;
-    uint64_t at = 0;
-    for (uint32_t s = 0; s < N; ++s) {
-      bool m = false;
-      for (uint32_t j = 0; j < hc[s]; ++j) m |= !keep[at + j];
-      at += hc[s];
-      if (m) mod.push_back(s);
-    }
-    if (int rc = heap_list(q, k_heap_adjust, mod)) return rc;
-  }
   return DMC_OK;
 }
 
