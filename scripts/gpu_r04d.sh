@@ -14,6 +14,6 @@ run() {  # name, seconds, command...
   echo "$n exit $rc"; tail -2 gpurun_out/r04d_$n.log | cut -c1-300
   return $rc
 }
-run heap 700 python -u -m pytest tests/test_heap_order.py tests/test_group.py tests/test_concurrency.py -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread &&
+run heap 700 python -u -m pytest tests/test_group.py tests/test_concurrency.py -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread &&
 run c5 300 python bench.py --config 5 --no-cpu-baseline &&
 run c5prof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04d_c5prof -o run --output-format csv -- python3 $R/bench.py --config 5 --no-cpu-baseline --no-profile --steps 6 --warmup 2
