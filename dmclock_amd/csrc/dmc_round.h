@@ -1221,7 +1221,10 @@ __device__ inline CView cand_view(const Table& tb, const CandRec& cr) {
 // One candidate's entries: R pops with r <= min(now, T_R); then, if the
 // priority pulls run, the P groups with key <= T_P from the post-R state.
 // Bin-rank path: into the rank bins; radix path: appended to the dense list.
-constexpr int kEmitStage = 3;      // queue positions staged per walker (LDS; 2: no faster)
+#ifndef DMC_EMIT_STAGE
+#define DMC_EMIT_STAGE 3
+#endif
+constexpr int kEmitStage = DMC_EMIT_STAGE;  // queue positions staged per walker (LDS; 2: no faster)
 #ifndef DMC_EMIT_STAGE_THREADS
 #define DMC_EMIT_STAGE_THREADS 448  // (LDS: 160 KB per block with the key array)
 #endif
