@@ -18,6 +18,10 @@ run() {  # name, seconds, command...
 }
 run clocks 300 bash scripts/gpu_emit_clocks.sh &&
 cp gpurun_out/emit_clocks.log gpurun_out/r04e_emit_clocks_full.log &&
+for v in base e512s base e512s; do
+  DMC_LIB=$R/dmclock_amd/variants/$v.so timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --no-profile --steps 10 > gpurun_out/r04e_c5_$v.json 2> gpurun_out/r04e_c5_$v.err || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/r04e_c5_$v.json')); print('c5 $v', d['ms_per_step'], d['decisions_per_s'])"
+done &&
 run lat1m 300 tests/cpp/latency 1048576 2000 --serve &&
 run lat6q 300 tests/cpp/latency 100000 3000 --serve --no-oracle --no-facade --queues 6 &&
 for v in ${PARITY_VARIANTS:-r128}; do
