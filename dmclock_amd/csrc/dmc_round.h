@@ -402,6 +402,41 @@ __device__ inline RoundPart wave_reduce_rpart(const RoundPart& a) {
   return o;
 }
 
+// The same on the DPP network (row shifts within 16-lane rows, then the row
+// broadcasts of lanes 15 and 31): ALU steps instead of LDS round trips, so
+// every wave of a block reduces its own partials; the wave's result is in
+// lane 63 (lanes a step has no source for receive the identity).
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline uint32_t rdpp32(uint32_t v, uint32_t idn) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)idn, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline uint64_t rdpp64(uint64_t v, uint64_t idn) {
+  return ((uint64_t)rdpp32<CTRL, ROWS>((uint32_t)(v >> 32), (uint32_t)(idn >> 32)) << 32) |
+         rdpp32<CTRL, ROWS>((uint32_t)v, (uint32_t)idn);
+}
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline void rpart_dpp_step(RoundPart& a) {
+  RoundPart b;
+  b.cnt[0] = rdpp32<CTRL, ROWS>(a.cnt[0], 0u);
+  b.cnt[1] = rdpp32<CTRL, ROWS>(a.cnt[1], 0u);
+  b.n_r = rdpp64<CTRL, ROWS>(a.n_r, 0ull);
+  b.mn[0] = rdpp64<CTRL, ROWS>(a.mn[0], kMaxKey);
+  b.mn[1] = rdpp64<CTRL, ROWS>(a.mn[1], kMaxKey);
+  b.mx[0] = rdpp64<CTRL, ROWS>(a.mx[0], 0ull);
+  b.mx[1] = rdpp64<CTRL, ROWS>(a.mx[1], 0ull);
+  rpart_combine(a, b);
+}
+__device__ __attribute__((always_inline)) inline RoundPart wave_rpart_dpp(RoundPart a) {
+  rpart_dpp_step<0x111, 0xf>(a);  // row_shr:1
+  rpart_dpp_step<0x112, 0xf>(a);  // row_shr:2
+  rpart_dpp_step<0x114, 0xf>(a);  // row_shr:4
+  rpart_dpp_step<0x118, 0xf>(a);  // row_shr:8
+  rpart_dpp_step<0x142, 0xa>(a);  // row_bcast:15 into rows 1 and 3
+  rpart_dpp_step<0x143, 0xc>(a);  // row_bcast:31 into rows 2 and 3
+  return a;
+}
+
 __device__ inline uint32_t hist_shift_r(uint64_t range) {
   // smallest shift with (range >> shift) < kHistBinsR
   uint32_t bits = range ? 64 - __clzll((long long)range) : 0;
@@ -473,6 +508,11 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #ifndef DMC_SCAN_MINW
 #define DMC_SCAN_MINW 8
 #endif
+// the block's partials reduced wave by wave on the DPP network (1), or all
+// staged in LDS and combined by wave 0 (0, rounds 1-3)
+#ifndef DMC_SCAN_RED_DPP
+#define DMC_SCAN_RED_DPP 1
+#endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
 template <bool BRK>
@@ -492,7 +532,11 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     z.tdbg[0] = z.tdbg[3] = ~0ull;
     *rd = z;
   }
+#if DMC_SCAN_RED_DPP
+  __shared__ RoundPart sh[kScanBlock / 64];
+#else
   __shared__ RoundPart sh[kScanBlock];
+#endif
   const double now = cp.now;
   RoundPart acc = rpart_ident();
   const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
@@ -546,7 +590,14 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     if (s < tb.n)
       scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
+#if DMC_SCAN_RED_DPP
+  // every wave reduces its partials on the DPP network; wave 0 combines the
+  // waves' (one LDS word group each)
+  acc = wave_rpart_dpp(acc);
+  if ((threadIdx.x & 63) == 63) sh[threadIdx.x >> 6] = acc;
+#else
   sh[threadIdx.x] = acc;
+#endif
   // the threshold histogram k_rhist fills, cleared (the previous round's
   // k_remit blocks have read it)
   {
@@ -555,12 +606,20 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
       hist[gi] = 0;
   }
   __syncthreads();
+#if DMC_SCAN_RED_DPP
+  if (threadIdx.x < 64) {
+    RoundPart o = threadIdx.x < (uint32_t)(kScanBlock / 64) ? sh[threadIdx.x] : rpart_ident();
+    o = wave_rpart_dpp(o);
+    if (threadIdx.x == 63) parts[blockIdx.x] = o;
+  }
+#else
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
     for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
     o = wave_reduce_rpart(o);
     if (threadIdx.x == 0) parts[blockIdx.x] = o;
   }
+#endif
 }
 template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)

@@ -24,7 +24,7 @@ for v in base e512s base e512s; do
 done &&
 run lat1m 300 tests/cpp/latency 1048576 2000 --serve &&
 run lat6q 300 tests/cpp/latency 100000 3000 --serve --no-oracle --no-facade --queues 6 &&
-for v in ${PARITY_VARIANTS:-r128}; do
+for v in ${PARITY_VARIANTS:-r128 base}; do
   DMC_LIB=$R/dmclock_amd/variants/$v.so run par_$v 500 python -u -m pytest tests/test_device_parity.py tests/test_gpu_parity.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "exact_trace or tied_rank or bench_shaped or churn_activations" || exit 1
 done &&
-VARIANTS="${VARIANTS:-base r128 sc2 sc512 st2}" ROUNDS=2 timeout -k 10 900 bash scripts/gpu_variants.sh > gpurun_out/r04e_variants.log 2>&1; rc=$?; cat gpurun_out/r04e_variants.log; exit $rc
+VARIANTS="${VARIANTS:-base nodpp r128 sc2 st2}" ROUNDS=2 timeout -k 10 900 bash scripts/gpu_variants.sh > gpurun_out/r04e_variants.log 2>&1; rc=$?; cat gpurun_out/r04e_variants.log; exit $rc
