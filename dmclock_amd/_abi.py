@@ -137,6 +137,8 @@ class Counters(ctypes.Structure):
         ("serve_yields", ctypes.c_uint64),
         ("serve_calls", ctypes.c_uint64),
         ("serve_launches", ctypes.c_uint64),
+        ("act_batches", ctypes.c_uint64),
+        ("act_seq_batches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -31,11 +31,20 @@ struct AddParams {
 };
 
 // Batched activations (the idle reset of every idle client's first request
-// in one batch, resolved on the device; see k_act_resolve).  Per batch
-// position: the proportion contribution (ordered key) a non-idle client with
-// an empty queue had before its first accepted request there (cold, stored
-// at index n - 1 - position) and has after it (cnew); at an activation position the post-add proportion basis
-// (actp: front p if the client has a request, else prev p).
+// in one batch, resolved on the device; see k_act_resolve).  A non-idle
+// client with an empty queue contributes (prev p) + prop_delta until its
+// first accepted request, then (front p) + prop_delta; each of its requests
+// up to that one may change it (under AtLimit::Reject a rejected request
+// still moves prev p, :899-906), and the values never decrease (a tag is
+// max(time, prev + increment) >= prev, or the max_tag a weight of 0 gives).
+// Per batch position where the contribution changed: the value before the
+// change (cold, stored at index n - 1 - position); at the client's last change
+// the value after it (cnew).  An activation at position q then sees the
+// client's current value as min(suffix minimum of cold over positions > q,
+// prefix minimum of cnew over positions < q) -- the value before the first
+// later change, or after the last one.  At an activation position the
+// post-add proportion basis (actp: front p if the client has a request, else
+// prev p).
 struct ActBuf {
   uint64_t* cold;
   uint64_t* cnew;
@@ -51,6 +60,16 @@ struct ActBuf {
   // each activating position, a compaction builds idx and the count *dm
   uint32_t* flag = nullptr;
   const uint32_t* dm = nullptr;
+  // AtLimit::Reject: an activated client whose activating request was
+  // rejected stays empty, and each later request of the batch may move its
+  // proportion basis until one is accepted.  At such a change (position r):
+  // hev_q[r] = the client's activation position, hev_p[r] = its new basis;
+  // hard[activation position] = 1 and *anyhard = 1 (k_act_hard resolves the
+  // batch).  hev_q is kNone elsewhere.
+  uint32_t* hev_q = nullptr;
+  double* hev_p = nullptr;
+  uint32_t* hard = nullptr;
+  uint32_t* anyhard = nullptr;
 };
 
 // Client trackers fused into the add (a queue group's step, config 5):
@@ -284,6 +303,11 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   const double front_p0 = (act.cold && count0) ? ring[st.head & tb.qmask].p : 0.0;
   const double prev_p0 = st.prev.p;
   bool act_done = false, chg_done = false, tf_done = false;
+  // (the empty client's proportion basis as of the last step, and the batch
+  // position of its last change; an activated client left empty: its
+  // activation position, while it stays empty)
+  double cur_p = prev_p0;
+  uint32_t chg_last = 0xffffffffu, act_q = 0xffffffffu;
   auto step = [&](uint32_t pos) {
     if (tf) {  // get_req_params, batch order
       dmc_request rq = pos == i ? rq1 : p.reqs[pos];
@@ -303,13 +327,31 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
       const dmc_request& rq = p.reqs[pos];
       if (!act_done && rq.rho <= rq.delta) {  // the activating request
         act_done = true;
-        act.actp[pos] = st.count ? (count0 ? front_p0 : st.front.p) : st.prev.p;
+        cur_p = st.count ? (count0 ? front_p0 : st.front.p) : st.prev.p;
+        act.actp[pos] = cur_p;
         if (act.flag) act.flag[pos] = 1;
+        if (!st.count) act_q = pos;  // rejected (or no tag): still empty
+      } else if (act_q != 0xffffffffu) {
+        const double np = st.count ? st.front.p : st.prev.p;
+        if (dbits(np) != dbits(cur_p)) {
+          cur_p = np;
+          act.hev_q[pos] = act_q;
+          act.hev_p[pos] = np;
+          if (!act.hard[act_q]) {
+            act.hard[act_q] = 1u;
+            *act.anyhard = 1u;
+          }
+        }
+        if (st.count) act_q = 0xffffffffu;
       }
-    } else if (count0 == 0 && !chg_done && st.count) {
-      chg_done = true;
-      act.cold[p.n - 1 - pos] = okey(__dadd_rn(prev_p0, pd));  // reversed order
-      act.cnew[pos] = okey(__dadd_rn(st.front.p, pd));
+    } else if (count0 == 0 && !chg_done) {
+      const double np = st.count ? st.front.p : st.prev.p;
+      if (dbits(np) != dbits(cur_p)) {
+        act.cold[p.n - 1 - pos] = okey(__dadd_rn(cur_p, pd));  // reversed order
+        cur_p = np;
+        chg_last = pos;
+      }
+      chg_done = st.count != 0;
     }
   };
   if (m == 1) {
@@ -333,9 +375,13 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
     for (uint32_t j = 0; j < p.n; ++j)
       if (aslot[j] == s) step(j);
   }
-  if (act.cold && !idle0 && count0 == 0 && !chg_done)  // nothing accepted
-    atomicMin((unsigned long long*)act.extra,
-              (unsigned long long)okey(__dadd_rn(prev_p0, pd)));
+  if (act.cold && !idle0 && count0 == 0) {
+    if (chg_last != 0xffffffffu)
+      act.cnew[chg_last] = okey(__dadd_rn(cur_p, pd));
+    else  // unchanged by the batch
+      atomicMin((unsigned long long*)act.extra,
+                (unsigned long long)okey(__dadd_rn(prev_p0, pd)));
+  }
   tb.rec[s].prev_r = st.prev.r;
   tb.rec[s].prev_p = st.prev.p;
   tb.rec[s].prev_l = st.prev.l;

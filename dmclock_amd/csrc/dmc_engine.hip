@@ -154,6 +154,9 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
     act.cold[i] = kMaxKey;
     act.cnew[i] = kMaxKey;
     if (act.flag) act.flag[i] = 0;
+    act.hev_q[i] = kNone;
+    act.hard[i] = 0u;
+    if (i == 0) *act.anyhard = 0u;
   }
   uint32_t s = p.reqs[i].slot;
   aslot[i] = s;
@@ -705,6 +708,7 @@ k_act_resolve(Table tb, ActBuf act, const uint64_t* ax, const double* ap,
               uint64_t* dbg = nullptr) {
   // dbg (debug): [0] start [1] base [2] first pass [3] end clocks, [4] first
   // undercut, [5] windows, [6] wave fallbacks, [7] activations
+  if (*act.anyhard) return;  // (k_act_hard's batch: it resolved and committed)
   if (dbg && threadIdx.x == 0) dbg[0] = wall_clock64();
   __shared__ uint64_t wpart[kActThreads / 64];
   __shared__ uint64_t s_base, s_carry, s_minpre;
@@ -868,7 +872,7 @@ k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
   __shared__ uint64_t s_incl[kActThreads];
   const uint32_t m = act.dm ? *act.dm : act.m;
   const uint32_t t = blockIdx.x, j0 = t * kActTile;
-  if (j0 >= m) return;
+  if (j0 >= m || *act.anyhard) return;  // (anyhard: k_act_hard's batch)
   // the unchanged clients' minimum (every block; block 0 publishes it)
   uint64_t b = kMaxKey;
   for (uint32_t i = threadIdx.x; i < act.nparts; i += kActThreads)
@@ -937,6 +941,7 @@ k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
 constexpr uint32_t kActMaxTiles = 1024;  // (batches of up to 2^20 activations)
 __global__ void __launch_bounds__(kActThreads)
 k_act_seq(ActBuf act, ActTiles tl) {
+  if (*act.anyhard) return;
   __shared__ uint32_t s_off[kActMaxTiles + 1];  // complex steps before each tile
   __shared__ uint32_t wsum[kActThreads / 64];
   __shared__ uint64_t s_tail[kActMaxTiles];     // each tile's tail run minimum
@@ -1039,7 +1044,7 @@ k_act_apply(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const do
   __shared__ uint32_t wcnt[kActThreads / 64];
   const uint32_t m = act.dm ? *act.dm : act.m;
   const uint32_t t = blockIdx.x, j0 = t * kActTile;
-  if (j0 >= m) return;
+  if (j0 >= m || *act.anyhard) return;
   const uint64_t base = *tl.xbase;
   const uint32_t j = j0 + threadIdx.x;
   const bool in = j < m;
@@ -1100,15 +1105,161 @@ k_act_apply(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const do
   tb.sc[slot].flags = (uint8_t)(sr.flags & ~F_IDLE);
 }
 
+// AtLimit::Reject: the batches where an activated client's activating
+// request was rejected (it stays non-idle and empty, :969-993) and later
+// requests of the batch move its proportion basis (ActBuf::hev_q).  Such a
+// "hard" client contributes basis + its new prop_delta, a value that rises
+// at each change, which the tile resolution's running minimum cannot
+// express.  One wave resolves these batches in activation order instead:
+//   L_k = min(X_k, M, Mh),  pd_k = L_k - t_k (or unchanged above the trigger),
+//   c_k = p_k + pd_k, then M = min(M, c_k), or for a hard client Mh (the
+//   minimum over the hard clients' current values) takes c_k,
+// and before activation k every basis change at a position below q_k
+// raises its client's value to P + pd (Mh recomputed when the raised value
+// was the minimum).  X_k is the tile path's (base, cold / cnew scans).  The
+// per-activation inputs come from k_act_inputs; the wave loads 64 of them
+// at a time and steps through them with uniform (readlane) values.
+// Commits the idle resets; the tile kernels see *anyhard and do nothing.
+// Run by wave 0 of k_act_fixup (no launch of its own), or by k_act_hard
+// before the one-block k_act_resolve.  (Any mode: an activating request
+// whose tag calculation failed leaves its client empty too.)
+__device__ __attribute__((always_inline)) inline double rl_d(double v, uint32_t l) {
+  const uint64_t b = dbits(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), (int)l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __attribute__((always_inline)) inline uint64_t rl_u64(uint64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline double wave_min_d(double v) {
+  for (int d = 32; d > 0; d >>= 1) {
+    const double o = __shfl_xor(v, d);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+struct ActHard {
+  uint32_t* hmap;   // per batch position: the hard client's activation index
+  uint32_t* hlist;  // the hard clients' activation indices, in order
+  double *hval, *hpd;  // per activation index: current value, prop_delta
+  uint64_t* nhard;  // batches resolved here (counter)
+};
+
+__device__ inline void act_hard_body(const Table& tb, const ActBuf& act, const uint64_t* ax,
+                                     const double* ap, const double* at, double* apd,
+                                     const uint32_t* aslot, const ActHard& hs) {
+  constexpr double dmax = 1.7976931348623157e308;  // :960
+  constexpr double trigger = dmax / 3.0;            // :957
+  const uint32_t lane = threadIdx.x;
+  const uint32_t m = act.dm ? *act.dm : act.m;
+  uint64_t b = kMaxKey;
+  for (uint32_t i = lane; i < act.nparts; i += 64) b = act.parts[i] < b ? act.parts[i] : b;
+  b = rl_u64(wave_min_u64(b), 0);
+  const uint64_t e = *act.extra;
+  const uint64_t base = e < b ? e : b;
+  double M = kInf, Mh = kInf;
+  uint32_t H = 0, pos = 0;
+  for (uint32_t k0 = 0; k0 < m; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const bool in = k < m;
+    uint32_t q = 0, hd = 0;
+    uint64_t x = kMaxKey;
+    double p = 0.0, t = 0.0, pd0 = 0.0;
+    if (in) {
+      q = act.idx[k];
+      x = ax[k] < base ? ax[k] : base;
+      p = ap[k];
+      t = at[k];
+      pd0 = apd[k];
+      hd = act.hard[q];
+    }
+    double mypd = pd0;
+    const uint32_t cnt = m - k0 < 64u ? m - k0 : 64u;
+    for (uint32_t u = 0; u < cnt; ++u) {
+      const uint32_t qu = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)u);
+      // the hard clients' basis changes at positions below qu
+      while (pos < qu && H) {
+        const uint32_t r = pos + lane;
+        const uint32_t hq = r < qu ? act.hev_q[r] : kNone;
+        uint64_t bal = __ballot(hq != kNone);
+        while (bal) {
+          const uint32_t j = (uint32_t)(__ffsll((unsigned long long)bal) - 1);
+          bal &= bal - 1;
+          const uint32_t aq = (uint32_t)__builtin_amdgcn_readlane((int)hq, (int)j);
+          const uint32_t h = hs.hmap[aq];
+          const double old = hs.hval[h];
+          const double nv = __dadd_rn(act.hev_p[pos + j], hs.hpd[h]);
+          if (lane == 0) hs.hval[h] = nv;
+          __threadfence_block();
+          if (nv < Mh) {
+            Mh = nv;
+          } else if (old == Mh && nv != old) {
+            double mn = kInf;
+            for (uint32_t i = lane; i < H; i += 64) {
+              const double v = hs.hval[hs.hlist[i]];
+              mn = v < mn ? v : mn;
+            }
+            Mh = rl_d(wave_min_d(mn), 0);
+          }
+        }
+        pos = pos + 64 < qu ? pos + 64 : qu;
+      }
+      if (!H) pos = qu;  // (no hard client yet: nothing to raise)
+      pos = qu + 1 > pos ? qu + 1 : pos;
+      const uint64_t xu = rl_u64(x, u);
+      const double rx = xu == kMaxKey ? kInf : from_okey(xu);
+      double L = M < rx ? M : rx;
+      L = Mh < L ? Mh : L;
+      const double lowest = L < dmax ? L : dmax;
+      const double pd = lowest < trigger ? __dsub_rn(lowest, rl_d(t, u)) : rl_d(pd0, u);
+      const double c = __dadd_rn(rl_d(p, u), pd);
+      if (lane == u) mypd = pd;
+      if (__builtin_amdgcn_readlane((int)hd, (int)u)) {
+        const uint32_t ku = k0 + u;
+        if (lane == 0) {
+          hs.hmap[qu] = ku;
+          hs.hlist[H] = ku;
+          hs.hval[ku] = c;
+          hs.hpd[ku] = pd;
+        }
+        __threadfence_block();
+        ++H;
+        Mh = c < Mh ? c : Mh;
+      } else {
+        M = c < M ? c : M;
+      }
+    }
+    if (in) {
+      apd[k] = mypd;
+      activate_slot(tb, aslot[k], mypd);
+    }
+  }
+  if (lane == 0) ++*hs.nhard;
+}
+
+__global__ void __launch_bounds__(64)
+k_act_hard(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const double* at,
+           double* apd, const uint32_t* aslot, ActHard hs) {
+  if (!*act.anyhard) return;
+  act_hard_body(tb, act, ax, ap, at, apd, aslot, hs);
+  __threadfence_block();
+  if (threadIdx.x == 0) *act.extra = kMaxKey;  // ready for the next batch
+}
+
 // The first activation whose simple step failed (if any): from its exact M
 // the rest of the batch is resolved by act_chain and committed again (the
 // idle reset is idempotent: k_act_apply's commits of these are overwritten)
 __global__ void __launch_bounds__(kActThreads)
 k_act_fixup(Table tb, ActBuf act, const uint64_t* ax, const double* ap, const double* at,
-            double* apd, const uint32_t* aslot, ActTiles tl) {
+            double* apd, const uint32_t* aslot, ActTiles tl, ActHard hs) {
+  if (threadIdx.x < 64 && *act.anyhard) act_hard_body(tb, act, ax, ap, at, apd, aslot, hs);
   const uint32_t f = *tl.fail;
   const uint32_t m = act.dm ? *act.dm : act.m;
-  if (f != 0xffffffffu && f < m) {
+  if (f != 0xffffffffu && f < m && !*act.anyhard) {
     __shared__ double s_M;
     if (threadIdx.x == 0) {
       const uint64_t M = tl.Mj[f];
@@ -1718,6 +1869,15 @@ struct dmc_queue {
   ActScanPart* act_sparts = nullptr;  // the bookkeeping scans' tile partials
   uint32_t* act_dm = nullptr;    // and their count
   uint32_t* h_actm = nullptr;    // pinned copy of the count
+  // AtLimit::Reject's rejected activations that move their client's basis
+  // again later in the batch (k_act_hard): per batch position the change
+  // events and the activation flags, per activation the sequential
+  // resolution's scratch, the any-flag and the count of such batches
+  uint32_t *act_hev_q = nullptr, *act_hard = nullptr, *act_hmap = nullptr,
+           *act_hlist = nullptr, *act_anyhard = nullptr;
+  double *act_hev_p = nullptr, *act_hval = nullptr, *act_hpd = nullptr;
+  uint64_t* h_nhard = nullptr;   // (host-mapped: read by dmc_queue_counters)
+  uint64_t* act_nhard = nullptr;  // its device pointer
   bool act_pending = false;
   int act_dumps = 0;             // debug: resolve inputs dumped (DMC_DUMP_ACT)
   void* stage = nullptr;         // small host-to-device lists (ensure_stage)
@@ -2312,6 +2472,8 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_x); dfree(q->act_ip);
   dfree(q->act_it); dfree(q->act_ipd); dfree(q->act_islot); dfree(q->act_flag);
   dfree(q->act_sparts);
+  dfree(q->act_hev_q); dfree(q->act_hard); dfree(q->act_hmap); dfree(q->act_hlist);
+  dfree(q->act_hev_p); dfree(q->act_hval); dfree(q->act_hpd);
   {
     ActTiles& a = q->atl;
     dfree(a.K); dfree(a.nst); dfree(a.sS); dfree(a.sX); dfree(a.sP); dfree(a.sT);
@@ -2333,11 +2495,24 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   DALLOC(q, &q->act_ipd, 8ull * cap);
   DALLOC(q, &q->act_islot, 4ull * cap);
   DALLOC(q, &q->act_flag, 4ull * cap);
+  DALLOC(q, &q->act_hev_q, 4ull * cap);
+  DALLOC(q, &q->act_hard, 4ull * cap);
+  DALLOC(q, &q->act_hmap, 4ull * cap);
+  DALLOC(q, &q->act_hlist, 4ull * cap);
+  DALLOC(q, &q->act_hev_p, 8ull * cap);
+  DALLOC(q, &q->act_hval, 8ull * cap);
+  DALLOC(q, &q->act_hpd, 8ull * cap);
   HIP_OK(hipHostMalloc((void**)&q->h_act, 4ull * cap, 0));
   // (each one-time buffer guarded by its own pointer: a failed allocation
   // is retried by the next call, never skipped because its pair exists)
   if (!q->act_dm) DALLOC(q, &q->act_dm, 4);
   if (!q->h_actm) HIP_OK(hipHostMalloc((void**)&q->h_actm, 4, 0));
+  if (!q->act_anyhard) DALLOC(q, &q->act_anyhard, 4);
+  if (!q->h_nhard) {
+    HIP_OK(hipHostMalloc((void**)&q->h_nhard, 8, hipHostMallocMapped | hipHostMallocCoherent));
+    *q->h_nhard = 0;
+    HIP_OK(hipHostGetDevicePointer((void**)&q->act_nhard, q->h_nhard, 0));
+  }
   DALLOC(q, &q->act_sparts, sizeof(ActScanPart) * scan_tiles(cap));
   {
     ActTiles& a = q->atl;
@@ -2377,15 +2552,26 @@ int ensure_act(dmc_queue* q, uint32_t n) {
   return DMC_OK;
 }
 
+// the Reject bookkeeping's buffers (ActBuf::hev_q ...)
+void act_hard_bufs(dmc_queue* q, ActBuf& act) {
+  act.hev_q = q->act_hev_q;
+  act.hev_p = q->act_hev_p;
+  act.hard = q->act_hard;
+  act.anyhard = q->act_anyhard;
+}
+
 // The idle resets of a batch's activations (m of them, at most n: the
 // device count act.dm, or act.m), resolved and committed (see k_act_keys)
 void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
   if (!n) return;
+  const ActHard hs{q->act_hmap, q->act_hlist, q->act_hval, q->act_hpd, q->act_nhard};
   const uint32_t T = (n + kActTile - 1) / kActTile;
   const uint64_t* ax = q->act_x;
   const double *ap = q->act_ip, *at = q->act_it;
   if (T > kActMaxTiles) {
     // (more than 2^20 activations in one batch: the one-block resolution)
+    hipLaunchKernelGGL(k_act_hard, dim3(1), dim3(64), 0, q->stream, q->tb, act, ax, ap, at,
+                       q->act_ipd, (const uint32_t*)q->act_islot, hs);
     hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
                        act, ax, ap, at, q->act_ipd, (const uint32_t*)q->act_islot);
     hipLaunchKernelGGL(k_act_commit, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
@@ -2399,7 +2585,7 @@ void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
   hipLaunchKernelGGL(k_act_apply, dim3(T), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
                      ap, at, (const double*)q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
   hipLaunchKernelGGL(k_act_fixup, dim3(1), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
-                     ap, at, q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
+                     ap, at, q->act_ipd, (const uint32_t*)q->act_islot, q->atl, hs);
 }
 
 // the activation bookkeeping's scans (and, flagged, the compaction) of an
@@ -2413,7 +2599,7 @@ void act_scans(dmc_queue* q, const ActBuf& act, uint32_t n, bool flagged) {
                      flagged ? q->act_dm : nullptr);
 }
 
-// A batch with activations in one pass (AtLimit Wait / Allow): the host only
+// A batch with activations in one pass: the host only
 // finds the activating requests (to keep its idle mirror); the idle resets
 // are resolved on the device by k_act_base + k_add_chain's bookkeeping +
 // k_act_resolve, exactly as a sequential replay would compute them.
@@ -2438,12 +2624,14 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   const uint32_t gb = grid_for(q->tb.n, 1024);  // (k_act_base: four records per thread at 1M)
   ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
              q->act_idx, m, q->act_parts, gb, q->act_extra};
+  act_hard_bufs(q, act);
   AddParams ap{d_reqs, d_rc, q->tick, n, 0};
   uint32_t g = (n + kBlock - 1) / kBlock;
   pb(q, DMC_PROF_ADD_LINK);
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
                      q->abuf, q->apos, q->aslot, q->apblk, act);
   pe(q);
+  ++q->ctr.act_batches;
   pb(q, DMC_PROF_ACTIVATE);
   hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
                      q->act_parts);
@@ -2478,12 +2666,14 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   const uint32_t gb = grid_for(q->tb.n, 1024);  // (k_act_base: four records per thread at 1M)
   ActBuf act{q->act_cold, q->act_cnew, q->act_p, q->act_pre, q->act_suf,
              q->act_idx, 0, q->act_parts, gb, q->act_extra, q->act_flag, q->act_dm};
+  act_hard_bufs(q, act);
   AddParams ap{d_reqs, d_rc, q->tick, n, 0};
   uint32_t g = (n + kBlock - 1) / kBlock;
   pb(q, DMC_PROF_ADD_LINK);
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, q->tb,
                      q->abuf, q->apos, q->aslot, q->apblk, act);
   pe(q);
+  ++q->ctr.act_batches;
   pb(q, DMC_PROF_ACTIVATE);
   hipLaunchKernelGGL(k_act_base, dim3(gb), dim3(kBlock), 0, q->stream, q->tb,
                      q->act_parts);
@@ -2589,16 +2779,15 @@ bool maybe_idle(const dmc_queue* q) { return q->n_idle || q->idle_unknown; }
 
 int add_with_idle(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
                   const dmc_request* d_reqs, int32_t* d_rc) {
-  // (AtLimit::Reject: the host split.  A rejected request still updates the
-  // client's prev tag (update_req_tag precedes the reject check, :899-906,
-  // :988-992), so an empty client's contribution to later idle resets can
-  // change at every request of the batch, not only at its first accepted
-  // one as k_add_chain's bookkeeping assumes.  And a rejected activating
-  // request returns before the heap adjustments (:992 vs :995-1015): the
-  // reference keeps that client at its pre-reset heap position, which no
-  // heap-free engine reproduces -- DESIGN section 8)
-  if (q->act_split || q->p.at_limit == DMC_AT_LIMIT_REJECT)
-    return add_host_split(q, h_reqs, n, d_reqs, d_rc);
+  // (AtLimit::Reject: on the device too.  A rejected request still updates
+  // the client's prev tag (update_req_tag precedes the reject check,
+  // :899-906, :988-992), so an empty client's contribution can change at
+  // every request of the batch -- k_add_chain's bookkeeping records each
+  // change; a rejected activation followed by more requests of its client
+  // sends the batch to the host split (k_act_reject_check).  A rejected
+  // activating request also returns before the heap adjustments (:992 vs
+  // :995-1015), which only the heap-order mode models -- DESIGN section 8)
+  if (q->act_split) return add_host_split(q, h_reqs, n, d_reqs, d_rc);
   return add_act_batch(q, h_reqs, n, d_reqs, d_rc);
 }
 
@@ -3641,6 +3830,9 @@ int dmc_queue_destroy(dmc_queue* q) {
   dfree(q->atl.Mj); dfree(q->atl.cX); dfree(q->atl.cP); dfree(q->atl.cT); dfree(q->atl.cPd);
   dfree(q->atl.cMo);
   dfree(q->act_xbase); dfree(q->act_fail);
+  dfree(q->act_hev_q); dfree(q->act_hard); dfree(q->act_hmap); dfree(q->act_hlist);
+  dfree(q->act_anyhard); dfree(q->act_hev_p); dfree(q->act_hval); dfree(q->act_hpd);
+  if (q->h_nhard) (void)hipHostFree(q->h_nhard);
   dfree(q->hd.hp); dfree(q->hd.hix); dfree(q->hd.cnt); dfree(q->d_hres);
   if (q->h_hres) (void)hipHostFree(q->h_hres);
   if (q->h_actm) (void)hipHostFree(q->h_actm);
@@ -4195,12 +4387,12 @@ int dmc_add_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   if (rc) return rc;
   rc = settle_act(q);
   if (rc) return rc;
-  if (maybe_idle(q) && !q->act_split && q->p.at_limit != DMC_AT_LIMIT_REJECT) {
+  if (maybe_idle(q) && !q->act_split) {
     rc = add_act_batch_dev(q, n, d_reqs, d_rc_out);
   } else if (maybe_idle(q) && (rc = sync_idle(q)) != DMC_OK) {
     return rc;
   } else if (q->n_idle) {
-    // the host split (Reject, or forced): stage the batch on the host
+    // the host split (forced): stage the batch on the host
     std::vector<dmc_request> h(n);
     HIP_OK(hipMemcpyAsync(h.data(), d_reqs, sizeof(dmc_request) * n,
                           hipMemcpyDeviceToHost, q->stream));
@@ -4975,8 +5167,13 @@ int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset) {
   if (!q || !out) return DMC_EINVAL;
   QueueLock g(q);
   if (g.rc) return g.rc;
+  // (k_act_hard's count, host-mapped: current once the adds have completed)
+  if (q->h_nhard) q->ctr.act_seq_batches = *(volatile uint64_t*)q->h_nhard;
   *out = q->ctr;
-  if (reset) q->ctr = dmc_counters{};
+  if (reset) {
+    q->ctr = dmc_counters{};
+    if (q->h_nhard) *(volatile uint64_t*)q->h_nhard = 0;
+  }
   return DMC_OK;
 }
 

@@ -49,10 +49,10 @@
 namespace dmc {
 
 constexpr int kBlockR = 256;
-// k_rrank's block (one rank bin each): 256 threads, or 128 so that all
-// 4096 bins' blocks are resident at once (16 per CU; build knob for A/B)
+// k_rrank's block (one rank bin each): 128 threads, so that all 4096 bins'
+// blocks are resident at once (16 per CU; r04e: 12.6 vs 14.7 us at 256)
 #ifndef DMC_RANK_THREADS
-#define DMC_RANK_THREADS 256
+#define DMC_RANK_THREADS 128
 #endif
 constexpr int kRankThreads = DMC_RANK_THREADS;
 constexpr int kHistBinsR = 2048;        // per phase
@@ -427,6 +427,35 @@ __device__ __attribute__((always_inline)) inline void rpart_dpp_step(RoundPart& 
   b.mx[1] = rdpp64<CTRL, ROWS>(a.mx[1], 0ull);
   rpart_combine(a, b);
 }
+// the wave's inclusive prefix sum on the same network (lane i: lanes 0..i),
+// and the wave's sum in every lane
+// (DMC_WAVE_DPP 0: the shuffle loops of rounds 1-3, for A/B)
+#ifndef DMC_WAVE_DPP
+#define DMC_WAVE_DPP 1
+#endif
+__device__ __attribute__((always_inline)) inline uint32_t wscan_u32(uint32_t v) {
+#if !DMC_WAVE_DPP
+  const int lane = threadIdx.x & 63;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+#endif
+  v += rdpp32<0x111, 0xf>(v, 0u);
+  v += rdpp32<0x112, 0xf>(v, 0u);
+  v += rdpp32<0x114, 0xf>(v, 0u);
+  v += rdpp32<0x118, 0xf>(v, 0u);
+  v += rdpp32<0x142, 0xa>(v, 0u);
+  v += rdpp32<0x143, 0xc>(v, 0u);
+  return v;
+}
+__device__ __attribute__((always_inline)) inline uint32_t wsum_all(uint32_t v) {
+#if !DMC_WAVE_DPP
+  return __shfl(wsum32(v), 0);
+#endif
+  return (uint32_t)__builtin_amdgcn_readlane((int)wscan_u32(v), 63);
+}
 __device__ __attribute__((always_inline)) inline RoundPart wave_rpart_dpp(RoundPart a) {
   rpart_dpp_step<0x111, 0xf>(a);  // row_shr:1
   rpart_dpp_step<0x112, 0xf>(a);  // row_shr:2
@@ -511,7 +540,7 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // the block's partials reduced wave by wave on the DPP network (1), or all
 // staged in LDS and combined by wave 0 (0, rounds 1-3)
 #ifndef DMC_SCAN_RED_DPP
-#define DMC_SCAN_RED_DPP 1
+#define DMC_SCAN_RED_DPP 0
 #endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
@@ -651,8 +680,13 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
       rpart_combine(o, d);
     }
     for (; i < nparts; i += 64) rpart_combine(o, parts[i]);
+#if DMC_WAVE_DPP
+    o = wave_rpart_dpp(o);
+    if (threadIdx.x == 63) sh_tot = o;
+#else
     o = wave_reduce_rpart(o);
     if (threadIdx.x == 0) sh_tot = o;
+#endif
   }
   __syncthreads();
   RoundPart r = sh_tot;
@@ -787,11 +821,7 @@ constexpr int kBinsPerThreadR = kHistBinsR / kPickHalf;
 constexpr uint32_t kSelValid = 0x5e1ec7edu;
 __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
-  uint32_t incl = v;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
+  const uint32_t incl = wscan_u32(v);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   uint32_t wbase = 0;
@@ -806,14 +836,7 @@ __device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, u
                                        uint32_t* ez, uint32_t* tv) {
   constexpr int NW = kPickHalf / 64;
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
-  uint32_t iv = v, iz = z;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t ov = __shfl_up(iv, d), oz = __shfl_up(iz, d);
-    if (lane >= d) {
-      iv += ov;
-      iz += oz;
-    }
-  }
+  const uint32_t iv = wscan_u32(v), iz = wscan_u32(z);
   if (lane == 63) {
     wsum[w] = iv;
     wsum[NW + w] = iz;
@@ -1523,8 +1546,8 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
     // the exact number of first keys at or below each threshold (validates
     // the sampled thresholds in the last block): per block, then one atomic
     // per phase into the block's XCD shard (same-address atomics serialise)
-    nr = wsum32(nr);
-    np = wsum32(np);
+    nr = wsum_all(nr);
+    np = wsum_all(np);
     if (lane == 0) {
       atomicAdd(&s_cnt[0], nr);
       atomicAdd(&s_cnt[1], np);
@@ -1534,12 +1557,8 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // each wave appends its candidates to the block's list at a base one LDS
   // atomic hands it, and its lanes walk them at once -- no block barrier
   // between a wave's key loads and its walkers' first loads.
-  uint32_t incl = cnt;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
-  const uint32_t wtot = __shfl(incl, 63);
+  const uint32_t incl = wscan_u32(cnt);
+  const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   uint32_t wbase = 0;
   if (lane == 0 && wtot) wbase = atomicAdd(&s_tot, wtot);
   wbase = __shfl(wbase, 0);
@@ -1810,11 +1829,7 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
     zs += z[h];
   }
   const uint32_t lane = t & 63, w = t >> 6;
-  uint32_t incl = zs;
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
-  }
+  const uint32_t incl = wscan_u32(zs);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   uint32_t pre = 0;
@@ -1888,10 +1903,10 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     const uint32_t sc = (uint32_t)sv, sz = (uint32_t)(sv >> 32);
     const uint32_t bc = (uint32_t)bv, bz = (uint32_t)(bv >> 32);
     const bool psup = lane >= (uint32_t)(kNSup / 2);  // (P bins: super-bins 32..63)
-    const uint32_t zoff = wsum32((lane < sb ? sz : 0u) + (lane < ib ? bz : 0u));
+    const uint32_t zoff = wsum_all((lane < sb ? sz : 0u) + (lane < ib ? bz : 0u));
     const uint32_t poff =
-        wsum32((lane < sb && psup ? sc : 0u) + (isp && lane < ib ? bc : 0u));
-    const uint32_t tp = wsum32(psup ? sc : 0u);
+        wsum_all((lane < sb && psup ? sc : 0u) + (isp && lane < ib ? bc : 0u));
+    const uint32_t tp = wsum_all(psup ? sc : 0u);
     const uint32_t cnt = __shfl(bc, (int)ib);
     // The round's outcome check (every block, from the same inputs: all
     // agree): both phases' selections written by the pick; with the priority
@@ -1901,7 +1916,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     // nothing is applied, the call returns DMC_EDEVICE) instead of
     // dispatching short.  (dmclock_server.h:1115-1186: k pulls take
     // min(k, eligible) requests.)
-    const uint32_t tz = wsum32(sz), tcr = wsum32(psup ? 0u : sc);
+    const uint32_t tz = wsum_all(sz), tcr = wsum_all(psup ? 0u : sc);
     bool bad = false;
     if (!fail0) {
       const PhaseSel& p1 = rd->ph[1];
@@ -1915,7 +1930,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     }
     if (b == 0) {
       // the round's totals and outcome (the summary k_rapply publishes)
-      const uint32_t tc = wsum32(sc);
+      const uint32_t tc = wsum_all(sc);
       if (lane == 0 && !ovf0) {
         if (bad) {
           rd->overflow = 7;

@@ -185,6 +185,40 @@ def config4_trace(seed, n_clients, n_steps, batch, depth=4, idle_frac=0.10,
     return tr
 
 
+def reject_churn_trace(seed, n_clients, n_steps, batch, idle_frac=0.3, throttled=0.4,
+                       t0=1.0, delta_rho="random"):
+    """AtLimit::Reject with activations: config 4's churn with `throttled` of
+    the tenants limited far below their arrival rate (l ~ U[0.2, 1] against
+    2 req/s, so their limit tags run ahead of the clock) and idle marking
+    drawn from all clients: activating requests of throttled clients are
+    rejected -- the idle reset still applies and prev moves
+    (dmclock_server.h:937-993) -- and clients emptied by the pulls see
+    rejected requests move their proportion basis before one is accepted.
+    batch >= n_clients gives clients several requests per batch (a rejected
+    activation followed by more requests: the host split); smaller batches
+    mostly one."""
+    rng = np.random.default_rng(seed)
+    tab = client_table(rng, n_clients)
+    thr = rng.random(n_clients) < throttled
+    tab.l = np.where(thr, rng.uniform(0.2, 1.0, n_clients), tab.l)
+    rate = 2.0 * n_clients
+    tr = Trace(tab, params=dict(seed=seed, reject=True))
+    pre = arrivals(rng, n_clients, 2 * n_clients, t0, rate, delta_rho=delta_rho)
+    t = float(pre["time"][-1])
+    tr.ops.append(("add", pre))
+    tr.ops.append(("pull", t, n_clients))
+    h = len(pre)
+    for _ in range(n_steps):
+        sel = rng.choice(n_clients, int(idle_frac * n_clients), replace=False)
+        tr.ops.append(("idle", np.sort(sel).astype(np.uint32)))
+        reqs = arrivals(rng, n_clients, batch, t, rate, delta_rho=delta_rho, handle_base=h)
+        h += batch
+        t = float(reqs["time"][-1])
+        tr.ops.append(("add", reqs))
+        tr.ops.append(("pull", t, batch))
+    return tr
+
+
 def dynamic_trace(seed, n_clients, n_steps, adds_per_step, change_frac=0.2,
                   k_choices=(1, 3, 16, 64, 256), depth=3):
     """U1 (dynamic client info) trace: steady_trace with random delta/rho and,

@@ -429,6 +429,10 @@ typedef struct dmc_counters {
                                queue's call need not wait behind it (DMC_OPT_SERVE) */
   uint64_t serve_calls;     /* single adds / pulls answered by the serve kernel (DMC_OPT_SERVE) */
   uint64_t serve_launches;  /* serve kernel launches (first call, after another call or idling) */
+  uint64_t act_batches;     /* add batches whose activations were resolved on the device */
+  uint64_t act_seq_batches; /* of those, resolved in order by one wave (k_act_hard: an
+                               activated client left empty -- AtLimit::Reject rejected its
+                               request -- whose basis later requests of the batch moved) */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 

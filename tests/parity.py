@@ -72,3 +72,51 @@ def run_parity(trace, mk_gpu, queue_kw=None, state_sample=64, require_tie_free=T
     assert qg.request_count() == qo.request_count()
     assert tuple(qg.sched_counts()) == tuple(qo.sched_counts())
     return n_dec, qg, qo
+
+
+
+def activation_batches(trace, queue_kw):
+    """Replays `trace` on the oracle one request at a time and returns (add
+    batches holding an activation, of those the batches with a "hard" one:
+    an activated client left with an empty queue -- its activating request
+    rejected under AtLimit::Reject -- whose proportion basis a later request
+    of the same batch moves; the engine resolves those batches in order with
+    one wave, k_act_hard, and counts them in act_seq_batches)."""
+    qo = pyoracle.OracleQueue(**queue_kw)
+    c = trace.clients
+    qo.register(c.slots, c.r, c.w, c.l, c.active)
+    n_act = n_hard = 0
+    for op in trace.ops:
+        if op[0] == "add":
+            reqs = op[1]
+            act = hard = False
+            watched = {}  # activated, still empty: slot -> basis bits
+            for i in range(len(reqs)):
+                s = int(reqs["slot"][i])
+                pre = qo.client_state(s)
+                qo.add_batch(reqs[i:i + 1])
+                if pre is None or not pre.registered:
+                    continue
+                post = qo.client_state(s)
+                basis = post.front_p if post.count else post.prev_p
+                if pre.idle and reqs["rho"][i] <= reqs["delta"][i]:
+                    act = True
+                    if post.count == 0:
+                        watched[s] = np.float64(basis).view(np.uint64)
+                elif s in watched:
+                    if np.float64(basis).view(np.uint64) != watched[s]:
+                        hard = True
+                    if post.count:
+                        del watched[s]
+                    else:
+                        watched[s] = np.float64(basis).view(np.uint64)
+            n_act += act
+            n_hard += hard
+        elif op[0] == "pull":
+            qo.pull_batch(op[1], op[2])
+        elif op[0] == "idle":
+            for s in op[1].tolist():
+                qo.mark_idle(s)
+        else:
+            raise ValueError(op[0])
+    return n_act, n_hard

@@ -401,3 +401,17 @@ def test_config4_1m_device_activations_vs_host_split():
     qb.close()
     torch.cuda.synchronize()
 
+
+def test_reject_activations_device_api():
+    """AtLimit::Reject through the device API: activations detected by
+    k_add_chain on the device, rejected activations whose client's basis
+    moves again in the batch resolved in order (k_act_hard), the host's idle
+    mirror never consulted.  Every add status, decision, result record and
+    sampled client state bit-exact against the oracle (tie-free seed)."""
+    from dmclock_amd._abi import AT_LIMIT_REJECT
+    tr = workloads.reject_churn_trace(4, 2000, 6, 4000, idle_frac=0.1)
+    n, qg, qo = device_parity(tr, queue_kw=dict(at_limit=AT_LIMIT_REJECT,
+                                                reject_threshold=0.5))
+    c = qg.counters()
+    assert c["act_batches"] == 6 and c["act_seq_batches"] >= 1, c
+    qg.close()

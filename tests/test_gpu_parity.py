@@ -279,6 +279,68 @@ def test_churn_activations_parity(mode, seed):
         assert qo.ties > 0, seed
 
 
+REJECT = dict(at_limit=AT_LIMIT_REJECT, reject_threshold=0.5)
+
+
+def device_vs_split(tr, n, mode):
+    """The trace on the device-resolved activations and on the host split (one
+    activation at a time): every add status, decision, result and final
+    client state equal.  Returns both queues and the device run's outputs."""
+    from parity import compare_decisions, compare_states
+    qa = mk_act(0)(max_clients=n, **mode)
+    qb = mk_act(1)(max_clients=n, **mode)
+    oa, ob = workloads.replay(qa, tr), workloads.replay(qb, tr)
+    for i, (a, b) in enumerate(zip(oa, ob)):
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), (i, np.nonzero(a[1] != b[1]))
+        elif a[0] == "pull":
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], i
+    compare_states(qa, qb, np.arange(n), "final")
+    return qa, qb, oa
+
+
+@pytest.mark.parametrize("n,batch,seed,oracle", [
+    (2000, 250, 1, True), (2000, 250, 2, False), (2000, 4000, 1, True),
+    (2000, 4000, 4, True), (2000, 4000, 2, False)])
+def test_reject_activations_parity(n, batch, seed, oracle):
+    """AtLimit::Reject batches with activations resolved on the device (no
+    host split): 40 % of the tenants limited far below their arrival rate,
+    10 % of the clients marked idle before every step, so activating requests
+    are rejected (the idle reset still applies, :937-993) and emptied clients
+    see rejected requests move their proportion basis.  Every add status,
+    decision and client state equals the host split's; the engine's counters
+    show every activation batch resolved on the device, and exactly the
+    batches the oracle's request-by-request replay finds "hard" (a rejected
+    activation whose basis moves again in the batch) resolved in order by
+    k_act_hard; on the tie-free seeds everything equals the oracle."""
+    from parity import activation_batches
+    tr = workloads.reject_churn_trace(seed, n, 6, batch, idle_frac=0.1)
+    qa, qb, oa = device_vs_split(tr, n, REJECT)
+    rejected = sum(int((o[1] == 11).sum()) for o in oa if o[0] == "add")
+    assert rejected > 1000, rejected
+    n_act, n_hard = activation_batches(tr, REJECT)
+    c = qa.counters()
+    print(f"n={n} batch={batch} seed={seed} rejected={rejected} predicted "
+          f"{n_act}/{n_hard} counters {c['act_batches']}/{c['act_seq_batches']}")
+    assert (c["act_batches"], c["act_seq_batches"]) == (n_act, n_hard), c
+    assert qb.counters()["act_batches"] == 0
+    if oracle:
+        run_parity(tr, mk_act(0), REJECT, state_sample=n)
+
+
+def test_reject_activations_64k():
+    """The same at 65,536 clients with 8,192-request batches: device
+    resolution equal to the host split in every output and client state,
+    the in-order resolution (k_act_hard) taken (oracle leg: the CPU
+    restatement's idle resets are O(N) each, 2 minutes here)."""
+    n = 1 << 16
+    tr = workloads.reject_churn_trace(1, n, 6, 8192, idle_frac=0.1)
+    qa, qb, oa = device_vs_split(tr, n, REJECT)
+    c = qa.counters()
+    assert c["act_batches"] == 6 and c["act_seq_batches"] >= 1, c
+
+
 def test_activation_undercut_by_earlier_activation():
     """An activated client's contribution undercuts the minimum a later
     activation sees once the former minimum client gets its first request
