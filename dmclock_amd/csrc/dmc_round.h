@@ -389,22 +389,9 @@ __device__ inline RoundPart rpart_ident() {
   return RoundPart{{0, 0}, 0, {kMaxKey, kMaxKey}, {0, 0}};
 }
 
-// one wave's partials combined across its lanes (result in every lane)
-__device__ inline RoundPart wave_reduce_rpart(const RoundPart& a) {
-  RoundPart o;
-  o.cnt[0] = wsum32(a.cnt[0]);
-  o.cnt[1] = wsum32(a.cnt[1]);
-  o.n_r = wsum64(a.n_r);
-  o.mn[0] = wmin64(a.mn[0]);
-  o.mn[1] = wmin64(a.mn[1]);
-  o.mx[0] = wmax64(a.mx[0]);
-  o.mx[1] = wmax64(a.mx[1]);
-  return o;
-}
-
-// The same on the DPP network (row shifts within 16-lane rows, then the row
-// broadcasts of lanes 15 and 31): ALU steps instead of LDS round trips, so
-// every wave of a block reduces its own partials; the wave's result is in
+// One wave's partials combined across its lanes on the DPP network (row
+// shifts within 16-lane rows, then the row broadcasts of lanes 15 and 31):
+// ALU steps instead of ds_bpermute round trips; the wave's result is in
 // lane 63 (lanes a step has no source for receive the identity).
 template <int CTRL, int ROWS>
 __device__ __attribute__((always_inline)) inline uint32_t rdpp32(uint32_t v, uint32_t idn) {
@@ -429,19 +416,9 @@ __device__ __attribute__((always_inline)) inline void rpart_dpp_step(RoundPart& 
 }
 // the wave's inclusive prefix sum on the same network (lane i: lanes 0..i),
 // and the wave's sum in every lane
-// (DMC_WAVE_DPP 0: the shuffle loops of rounds 1-3, for A/B)
-#ifndef DMC_WAVE_DPP
-#define DMC_WAVE_DPP 1
-#endif
+// (against the shuffle loops of rounds 1-3: emit 27.0 vs 28.2 us, pick
+// 6.8 vs 7.1, rank 12.2 vs 12.6, r04g)
 __device__ __attribute__((always_inline)) inline uint32_t wscan_u32(uint32_t v) {
-#if !DMC_WAVE_DPP
-  const int lane = threadIdx.x & 63;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d);
-    if (lane >= d) v += o;
-  }
-  return v;
-#endif
   v += rdpp32<0x111, 0xf>(v, 0u);
   v += rdpp32<0x112, 0xf>(v, 0u);
   v += rdpp32<0x114, 0xf>(v, 0u);
@@ -451,9 +428,6 @@ __device__ __attribute__((always_inline)) inline uint32_t wscan_u32(uint32_t v) 
   return v;
 }
 __device__ __attribute__((always_inline)) inline uint32_t wsum_all(uint32_t v) {
-#if !DMC_WAVE_DPP
-  return __shfl(wsum32(v), 0);
-#endif
   return (uint32_t)__builtin_amdgcn_readlane((int)wscan_u32(v), 63);
 }
 __device__ __attribute__((always_inline)) inline RoundPart wave_rpart_dpp(RoundPart a) {
@@ -537,11 +511,6 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #ifndef DMC_SCAN_MINW
 #define DMC_SCAN_MINW 8
 #endif
-// the block's partials reduced wave by wave on the DPP network (1), or all
-// staged in LDS and combined by wave 0 (0, rounds 1-3)
-#ifndef DMC_SCAN_RED_DPP
-#define DMC_SCAN_RED_DPP 0
-#endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound)
 template <bool BRK>
@@ -561,11 +530,7 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     z.tdbg[0] = z.tdbg[3] = ~0ull;
     *rd = z;
   }
-#if DMC_SCAN_RED_DPP
-  __shared__ RoundPart sh[kScanBlock / 64];
-#else
   __shared__ RoundPart sh[kScanBlock];
-#endif
   const double now = cp.now;
   RoundPart acc = rpart_ident();
   const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
@@ -619,14 +584,9 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     if (s < tb.n)
       scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
-#if DMC_SCAN_RED_DPP
-  // every wave reduces its partials on the DPP network; wave 0 combines the
-  // waves' (one LDS word group each)
-  acc = wave_rpart_dpp(acc);
-  if ((threadIdx.x & 63) == 63) sh[threadIdx.x >> 6] = acc;
-#else
+  // (staged in LDS and combined by wave 0: reducing every wave's partials
+  // on the DPP network first measured slower, 14.6 vs 14.3 us, r04g)
   sh[threadIdx.x] = acc;
-#endif
   // the threshold histogram k_rhist fills, cleared (the previous round's
   // k_remit blocks have read it)
   {
@@ -635,20 +595,12 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
       hist[gi] = 0;
   }
   __syncthreads();
-#if DMC_SCAN_RED_DPP
-  if (threadIdx.x < 64) {
-    RoundPart o = threadIdx.x < (uint32_t)(kScanBlock / 64) ? sh[threadIdx.x] : rpart_ident();
-    o = wave_rpart_dpp(o);
-    if (threadIdx.x == 63) parts[blockIdx.x] = o;
-  }
-#else
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
     for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
-    o = wave_reduce_rpart(o);
-    if (threadIdx.x == 0) parts[blockIdx.x] = o;
+    o = wave_rpart_dpp(o);
+    if (threadIdx.x == 63) parts[blockIdx.x] = o;
   }
-#endif
 }
 template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
@@ -680,13 +632,8 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
       rpart_combine(o, d);
     }
     for (; i < nparts; i += 64) rpart_combine(o, parts[i]);
-#if DMC_WAVE_DPP
     o = wave_rpart_dpp(o);
     if (threadIdx.x == 63) sh_tot = o;
-#else
-    o = wave_reduce_rpart(o);
-    if (threadIdx.x == 0) sh_tot = o;
-#endif
   }
   __syncthreads();
   RoundPart r = sh_tot;
