@@ -136,6 +136,11 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=30)
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="config 4: seconds of oracle work in the CPU sample")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="each dmc_add_pull_batch_device call waits for its round "
+                         "(default: DMC_OPT_PIPELINE, a call queues its graph behind the "
+                         "previous one and returns; the timed region ends with "
+                         "dmc_queue_sync, which finishes the last call)")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -372,6 +377,10 @@ def main():
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
                  max_batch=max(args.batch, k, 1 << 20), device=local)
     settle = prepare(q, args, tab, pre)
+    pipelined = not (args.no_pipeline or args.host_api or args.separate_calls)
+    if pipelined:
+        from dmclock_amd._abi import OPT_PIPELINE
+        q.set_option(OPT_PIPELINE, 1)
 
     dev = torch.device("cuda", local)
     d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r in steps]
@@ -426,6 +435,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    q.sync()
     st_t0 = q.stats()
     q.counters(reset=True)
     if dist:
@@ -434,6 +444,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
+    q.sync()  # (the last call's round read: with pipelining it is finished here)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -543,7 +554,8 @@ def main():
                    "ring_capacity": args.ring,
                    "api": ("host buffers (dmc_add_batch + dmc_pull_batch, PCIe "
                            "inclusive)" if args.host_api else
-                           "device buffers (dmc_add_pull_batch_device)"),
+                           "device buffers (dmc_add_pull_batch_device"
+                           + (", pipelined: DMC_OPT_PIPELINE)" if pipelined else ")")),
                    "parallelism": f"{world} independent server queue(s)"
                                   + ("" if backend == "nccl" else
                                      " (rehearsal: ranks share device 0, gloo)")},

@@ -39,6 +39,7 @@ OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
 OPT_FAULT = 9
 OPT_HEAP_ORDER = 11
+OPT_PIPELINE = 12
 OPT_SERVE = 10
 
 # PhaseType (dmclock_recs.h:33)

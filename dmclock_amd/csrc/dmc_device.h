@@ -97,6 +97,10 @@ struct Table {
   ClientAux* aux;  // N
   ReqEntry* ring;
   const BoundInfo* binfo;  // U1 (dynamic_info): read at every tag; else null
+  // DMC_OPT_PIPELINE: the gate word a pipelined round's end sets when the
+  // host must finish its call first; the next call's graph, already queued,
+  // then does nothing (every kernel of it checks); else null
+  const uint32_t* gate;
 };
 
 __host__ __device__ inline uint64_t dbits(double x) {

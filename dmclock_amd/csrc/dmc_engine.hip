@@ -147,6 +147,7 @@ __global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
 __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p, Table tb, uint32_t* abuf, uint32_t* apos, uint32_t* aslot, AddParams* pblk, ActBuf act) {
+  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *pblk = p;
   if (i >= p.n) return;
@@ -178,6 +179,7 @@ k_add_link(AddParams p, Table tb,
 }
 
 __device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act, const TrackFill* tf = nullptr) {
+  if (tb.gate && *tb.gate) return;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // one level of loads: the call's parameters and this position's filing
   // (apos / aslot are padded to whole blocks: in bounds for the grid)
@@ -1837,7 +1839,7 @@ struct dmc_queue {
   Round* rd = nullptr;
   Round h_rd_copy{};          // host copy of the last round's summary
   Round* h_rd = &h_rd_copy;
-  HostRound* h_round = nullptr;  // fine-grained pinned, written by k_rfinish
+  HostRound* h_round = nullptr;  // fine-grained pinned, written by k_rfinish (two: seq parity)
   HostRound* d_hround = nullptr; // its device address
   uint64_t round_seq = 0;
   uint32_t* hist = nullptr;   // 2 x kHistBinsR
@@ -1890,6 +1892,17 @@ struct dmc_queue {
   bool mark_ev_live = false;
   uint32_t* h_act = nullptr;  // pinned staging of the activation positions
   bool act_split = false;     // DMC_OPT_ACT_SPLIT: one host split per activation
+  // DMC_OPT_PIPELINE: the gate word (Table::gate) and the call left pending
+  bool pipeline = false;
+  uint32_t* gate = nullptr;
+  struct PendCall {
+    bool on = false;
+    uint64_t seq = 0;  // its round's sequence number
+    uint32_t k = 0;
+    double now = 0.0;
+    dmc_decision* out = nullptr;
+    dmc_pull_result* res = nullptr;
+  } pend;
   unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
   unsigned long long* reqcount = nullptr;
   // radix path (grown on demand)
@@ -2050,10 +2063,16 @@ void serve_yield_others(dmc_queue* q) {
 
 // Every C-ABI call holds the queue's lock; all but the serve path's calls
 // quiesce k_serve first.  rc: DMC_EDEVICE once the queue is wedged.
+namespace {
+int settle_pending(dmc_queue* q, bool* clean_out = nullptr);
+}  // namespace
+
+// (settle: finish a pipelined call left pending, DMC_OPT_PIPELINE -- every
+// entry point but dmc_add_pull_batch_device, which does it after its launch)
 struct QueueLock {
   std::lock_guard<std::mutex> l;
   int rc = DMC_OK;
-  explicit QueueLock(dmc_queue* q, bool serve = false) : l(q->mtx) {
+  explicit QueueLock(dmc_queue* q, bool serve = false, bool settle = true) : l(q->mtx) {
     (void)hipSetDevice(q->p.device);
     if (q->wedged) {
       rc = DMC_EDEVICE;
@@ -2061,6 +2080,7 @@ struct QueueLock {
     }
     if (!serve) rc = serve_quiesce(q);
     if (serve_registry().qs.size() > (q->serve_reg ? 1u : 0u)) serve_yield_others(q);
+    if (!rc && settle && q->pend.on) rc = settle_pending(q);
   }
 };
 
@@ -3097,7 +3117,8 @@ int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
 // 2 ms (a long round, or a device fault) blocks on the stream instead, which
 // reports errors.
 int wait_round(dmc_queue* q, uint64_t seq) {
-  const volatile uint64_t* flag = &q->h_round->seq;
+  const HostRound* hr = q->h_round + (seq & 1);
+  const volatile uint64_t* flag = &hr->seq;
   auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; ++spin) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
@@ -3109,7 +3130,7 @@ int wait_round(dmc_queue* q, uint64_t seq) {
     }
     __builtin_ia32_pause();
   }
-  std::memcpy(q->h_rd, (const void*)&q->h_round->r, sizeof(Round));
+  std::memcpy(q->h_rd, (const void*)&hr->r, sizeof(Round));
   return DMC_OK;
 }
 
@@ -3276,9 +3297,11 @@ int serve_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* out,
 // general limit-break step, then another round).  d_result (device API) is
 // written by the first round's k_rfinish when that round ends the call;
 // *dev_wrote says so.
+// (pre_seq: the pre-launched round's sequence number when later rounds were
+// launched since -- a pipelined call's, DMC_OPT_PIPELINE)
 int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
               dmc_pull_result* res, dmc_pull_result* d_result = nullptr,
-              bool* dev_wrote = nullptr, bool pre_launched = false) {
+              bool* dev_wrote = nullptr, bool pre_launched = false, uint64_t pre_seq = 0) {
   if (dev_wrote) *dev_wrote = false;
   bool first_round = true;
   bool retry_radix = false;  // re-run an overflowed round on the radix path
@@ -3323,9 +3346,11 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     // the first round of a call may end it: its k_rfinish writes d_result
     dmc_pull_result* dres = (first_round && n_dec == 0 && kr == k) ? d_result : nullptr;
     int rc = DMC_OK;
+    uint64_t wseq = 0;
     if (pre_launched) {  // the fused add + pull graph launched this round
       pre_launched = false;
       radix = false;
+      wseq = pre_seq;
     } else {
       if (q->radix_batches && !retry) --q->radix_batches;
       rc = radix ? ensure_entries(q, q->dense_hint) : ensure_brec(q);
@@ -3334,7 +3359,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       if (rc) return rc;
     }
     // one host round trip per round, through host-mapped memory
-    rc = wait_round(q, q->round_seq);
+    rc = wait_round(q, wseq ? wseq : q->round_seq);
     if (rc) return rc;
     if (!allow && q->h_rd->terminal && !q->h_rd->overflow) {
       // the round ran out of work: the terminal pull (do_next_request's
@@ -3534,6 +3559,32 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
   }
   r.n_decisions = n_dec;
   if (res) *res = r;
+  return DMC_OK;
+}
+
+// DMC_OPT_PIPELINE: finish the call left pending -- its round's outcome
+// read; a round that needs the host (re-runs, the terminal pull, further
+// rounds) shut the gate, which is opened again before pull_impl goes on.
+// *clean_out: the round ended its call (the gate stayed open, so a graph
+// queued behind it ran).
+int settle_pending(dmc_queue* q, bool* clean_out) {
+  if (clean_out) *clean_out = true;
+  if (!q->pend.on) return DMC_OK;
+  const dmc_queue::PendCall p = q->pend;
+  q->pend.on = false;
+  int rc = wait_round(q, p.seq);
+  if (rc) return rc;
+  const bool clean = !q->h_rd->overflow && q->h_rd->n_dec >= q->h_rd->k_total;
+  if (clean_out) *clean_out = clean;
+  if (!clean) HIP_OK(hipMemsetAsync(q->gate, 0, 4, q->stream));
+  dmc_pull_result r{};
+  bool dev_wrote = false;
+  rc = pull_impl(q, p.now, p.k, p.out, &r, p.res, &dev_wrote, true, p.seq);
+  if (rc) return rc;
+  if (p.res && !dev_wrote) {
+    hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, p.res, r);
+    HIP_OK(hipGetLastError());
+  }
   return DMC_OK;
 }
 
@@ -3742,7 +3793,9 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
       q->serve_idle_ticks = (uint64_t)khz / 5;  // 0.2 ms
   }
   rc |= A(&q->reqcount, 1);
-  if (hipHostMalloc((void**)&q->h_round, sizeof(HostRound),
+  t.gate = nullptr;
+  rc |= A(&q->gate, 1);
+  if (hipHostMalloc((void**)&q->h_round, 2 * sizeof(HostRound),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&q->d_hround, q->h_round, 0) != hipSuccess ||
       hipHostMalloc((void**)&q->h_sctl, sizeof(StepCtl), 0) != hipSuccess ||
@@ -3754,7 +3807,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
       hipHostGetDevicePointer((void**)&q->d_serve, q->h_serve, 0) != hipSuccess)
     rc |= DMC_ENOMEM;
   else {
-    std::memset((void*)q->h_round, 0, sizeof(HostRound));
+    std::memset((void*)q->h_round, 0, 2 * sizeof(HostRound));
     std::memset((void*)q->h_serve, 0, sizeof(ServeIO));
   }
   if (rc) {
@@ -3781,6 +3834,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
 int dmc_queue_destroy(dmc_queue* q) {
   if (!q) return DMC_EINVAL;
   (void)hipSetDevice(q->p.device);
+  if (q->pend.on) (void)settle_pending(q);  // (DMC_OPT_PIPELINE: its work completes)
   if (q->group) {  // (the group keeps running its other members)
     dmc_group* g = q->group;
     (void)hipStreamSynchronize(q->stream);
@@ -3820,6 +3874,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   for (void* p : ptrs)
     dfree(p);
   if (q->h_round) (void)hipHostFree(q->h_round);
+  dfree(q->gate);
   if (q->h_act) (void)hipHostFree(q->h_act);
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_extra); dfree(q->act_parts);
@@ -4470,25 +4525,31 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
                               int32_t* d_rc_out, double now, uint32_t k,
                               dmc_decision* d_out, dmc_pull_result* d_result) {
   if (!q || (n && (!d_reqs || !d_rc_out)) || (k && !d_out)) return DMC_EINVAL;
-  bool fuse;
   {
-    QueueLock g(q);
+    // (a pipelined call left pending is finished after this call's launch)
+    QueueLock g(q, false, false);
     if (g.rc) return g.rc;
-  ++q->gen;
-  if (q->heap) {
-    if (int rc = heap_add(q, n, d_reqs, d_rc_out)) return rc;
-    return heap_pull(q, now, k, d_out, d_result, nullptr);
-  }
-  if (int rc0 = settle_act(q)) return rc0;
-    fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
-           !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
-           q->use_graphs && !q->prof_on;
-    if (fuse) {
+    ++q->gen;
+    for (;;) {
+      if (q->heap) {
+        if (int rc = settle_pending(q)) return rc;
+        if (int rc = heap_add(q, n, d_reqs, d_rc_out)) return rc;
+        return heap_pull(q, now, k, d_out, d_result, nullptr);
+      }
+      if (int rc0 = settle_act(q)) return rc0;
+      const bool fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
+                        !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
+                        q->use_graphs && !q->prof_on;
+      if (!fuse) {
+        if (int rc = settle_pending(q)) return rc;
+        break;  // the two calls
+      }
       int rc = ensure_batch(q, n);
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
-      CallParams cp{k, 0, now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault, 0};
+      CallParams cp{k,     0,   now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault,
+                    0,     q->pipeline ? q->gate : nullptr};
       auto enqueue = [&] {
         enqueue_add(q, ap);
         enqueue_round(q, cp, false);
@@ -4513,10 +4574,30 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         uint64_t* kp = sampled ? nullptr : q->keyp;
         void* a2[] = {&tb, &kr, &kp, &q->meta, &q->rparts, &q->rd, &cp,
                       &skr, &skp, &q->k32, &q->hist};
-        int rc = graph_replay(q, *gr, a1, a2);
+        rc = graph_replay(q, *gr, a1, a2);
         if (rc) return rc;
       }
       q->tick += n;
+      if (q->pipeline) {
+        // the previous call, finished now that this one is queued behind it
+        bool clean = true;
+        if ((rc = settle_pending(q, &clean))) return rc;
+        if (!clean) {
+          // it needed the host: the graph just queued found the gate shut
+          // and did nothing -- launched again, behind the previous call's
+          // remaining work
+          q->tick -= n;
+          --q->ctr.fused_calls;
+          continue;
+        }
+        q->pend.on = true;
+        q->pend.seq = cp.seq;
+        q->pend.k = k;
+        q->pend.now = now;
+        q->pend.out = d_out;
+        q->pend.res = d_result;
+        return DMC_OK;
+      }
       dmc_pull_result r{};
       bool dev_wrote = false;
       rc = pull_impl(q, now, k, d_out, &r, d_result, &dev_wrote, true);
@@ -4558,6 +4639,7 @@ struct GroupLock {
     for (dmc_queue* q : g->qs) {
       if (q->wedged) rc = DMC_EDEVICE;
       else if (int e = serve_quiesce(q)) rc = e;
+      else if (int e2 = settle_pending(q)) rc = e2;
     }
   }
 };
@@ -5145,6 +5227,12 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
     case DMC_OPT_HEAP_ORDER:
       if (value == 0) return q->heap ? DMC_EINVAL : DMC_OK;
       return heap_enable(q, (uint32_t)value);
+    case DMC_OPT_PIPELINE:
+      if ((value != 0) == q->pipeline) return DMC_OK;
+      if (int rc = invalidate_graphs(q)) return rc;  // (the graphs hold the table's gate)
+      q->pipeline = value != 0;
+      q->tb.gate = q->pipeline ? q->gate : nullptr;
+      return DMC_OK;
     case DMC_OPT_FAULT:
       if (value < 0) return DMC_EINVAL;
       q->fault = (uint32_t)value;

@@ -150,7 +150,8 @@ struct Round {
   dmc_pull_result* res;  // device-API result record (null: the host writes it)
   uint64_t seq;          // round sequence number, published to the host
   uint32_t fault;        // test hook (CallParams::fault)
-  uint32_t pad2;
+  uint32_t skip;         // this round's kernels do nothing (its k_rscan found the gate shut)
+  uint32_t* gate;        // a pipelined round: its end sets the gate (CallParams::gate)
 };
 
 struct CallParams {
@@ -163,12 +164,15 @@ struct CallParams {
   uint64_t seq;
   uint32_t fault;  // test hook (DMC_OPT_FAULT): 1 = phase 1's selection left unset
   uint32_t pad;
+  uint32_t* gate;  // DMC_OPT_PIPELINE: a pipelined call's round (its end sets the gate)
 };
 
 // Host-mapped (fine-grained pinned) round summary: the round's last kernel
 // copies Round here and then publishes seq, so the host learns the outcome
 // by polling host memory instead of a device-to-host copy and a stream
-// synchronisation (two command-processor round trips per call).
+// synchronisation (two command-processor round trips per call).  Two of
+// them, by seq parity: with DMC_OPT_PIPELINE the next round may end while
+// the host reads this one's.
 struct HostRound {
   Round r;
   uint64_t seq;
@@ -515,6 +519,10 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // scan sits at its 64-register bound)
 template <bool BRK>
 __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+  if (tb.gate && *tb.gate) {  // (DMC_OPT_PIPELINE: the host finishes the last call first)
+    if (blockIdx.x == 0 && threadIdx.x == 0) rd->skip = 1u;
+    return;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Round z{};
     z.fault = cp.fault;
@@ -527,6 +535,7 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     z.tick = cp.tick;
     z.res = cp.res;
     z.seq = cp.seq;
+    z.gate = cp.gate;
     z.tdbg[0] = z.tdbg[3] = ~0ull;
     *rd = z;
   }
@@ -657,6 +666,7 @@ constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of
 // every k_remit block picks the thresholds and rank bins from it (no block
 // ticket, no last-block tail here).  Block 0 stores the round's totals.
 __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
+  if (rd->skip) return;
   __shared__ uint32_t lh[2][kHistBinsR];
 
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
@@ -1413,6 +1423,7 @@ constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
 #endif
 template <bool BRK>
 __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap, uint64_t* eclk) {
+  if (rd->skip) return;
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
@@ -1824,6 +1835,7 @@ __device__ inline bool sample_failed(const Round* rd) {
 constexpr uint32_t kBinMaxReport = 128;
 
 __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime) {
+  if (rd->skip) return;
   __shared__ BKey sh[kBinCapR];
   // the bin's records, its group and P-group offsets, P groups, the round's
   // outcome check
@@ -2236,7 +2248,14 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
 // expects this round to end the call (no overflow retry; a terminal round
 // under AtLimit::Allow is followed by host-driven steps, which rewrite it),
 // then the Round summary to host memory and its sequence number last.
-__device__ inline void rfinish_body(const Round* rd, HostRound* h) {
+// (from k_rapply: `round_end`; the terminal pull's re-publication leaves
+// the gate alone)
+__device__ inline void rfinish_body(const Round* rd, HostRound* h, bool round_end = false) {
+  h += rd->seq & 1;
+  // a pipelined round (DMC_OPT_PIPELINE): the gate stays open iff the round
+  // ends its call (the host has nothing left to do for it)
+  if (round_end && threadIdx.x == 0 && rd->gate)
+    *rd->gate = (!rd->overflow && rd->n_dec >= rd->k_total) ? 0u : 1u;
   constexpr uint32_t W = sizeof(Round) / 4;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
@@ -2351,6 +2370,7 @@ constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 #define DMC_APPLY_MINB 2
 #endif
 __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg) {
+  if (rd->skip) return;
   // A limit-break round's priority pops (group heads and their runs'
   // readied fronts) are counted here: its summary goes out once every block
   // has counted (a ticket), not from the extra block at once
@@ -2359,7 +2379,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
     // the extra block publishes the round's summary (complete since k_rrank)
     // to host memory at once: the host learns the outcome while the other
     // blocks store the state, and its next launch is stream-ordered behind them
-    rfinish_body(rd, h);
+    rfinish_body(rd, h, true);
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow && !brk) {
@@ -2416,7 +2436,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
     sched[1] += np;
   }
   __syncthreads();
-  rfinish_body(rd, h);
+  rfinish_body(rd, h, true);
 }
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,

@@ -398,6 +398,15 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   fast).  Set before the first client is registered; clients may
                                   be registered once; queue groups do not take such queues.
                                   0: off (default) */
+#define DMC_OPT_PIPELINE 12     /* 1: dmc_add_pull_batch_device calls are pipelined -- a call queues its
+                                  graph behind the previous call's and returns; the previous call is
+                                  finished (its round's outcome read, re-runs if it needed any) after
+                                  that launch, so the device runs the calls back to back.  A call's
+                                  results are complete once the next call on the queue, or any other
+                                  call such as dmc_queue_sync, has returned; an error of a call is
+                                  reported by that next call.  A round that needs the host shuts a
+                                  device-side gate and the next call's queued graph does nothing (it
+                                  is launched again).  0 (default): each call waits for its round */
 #define DMC_OPT_FAIL_ALLOC 7    /* test hook: the queue's next `value` device buffer allocations
                                   (growth of its batch, decision, radix and activation buffers)
                                   fail; the call returns DMC_ENOMEM, the queue stays usable */

@@ -415,3 +415,130 @@ def test_reject_activations_device_api():
     c = qg.counters()
     assert c["act_batches"] == 6 and c["act_seq_batches"] >= 1, c
     qg.close()
+
+
+def replay_pipelined(q, trace):
+    """The trace's add + pull pairs as dmc_add_pull_batch_device calls with
+    DMC_OPT_PIPELINE on, issued back to back with no synchronisation between
+    them (each call its own status, decision and result buffers, as a caller
+    overlapping its calls would hold them); other ops through the device
+    API.  One dmc_queue_sync at the end, then every output read back."""
+    import torch
+    from dmclock_amd._abi import OPT_PIPELINE
+    dev = torch.device("cuda", 0)
+    c = trace.clients
+    q.register(c.slots, c.r, c.w, c.l, c.active)
+    q.set_option(OPT_PIPELINE, 1)
+    ops = trace.ops
+    pending = []  # (kind, buffers)
+    keep = []
+    i = 0
+    while i < len(ops):
+        op = ops[i]
+        if op[0] == "add":
+            reqs = torch.from_numpy(op[1].view(np.uint8).copy()).to(dev)
+            n = len(op[1])
+            d_rc = torch.zeros(n, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()  # (the copies ran on torch's stream)
+            keep.append(reqs)
+            if i + 1 < len(ops) and ops[i + 1][0] == "pull":
+                now, k = ops[i + 1][1], ops[i + 1][2]
+                d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+                d_res = torch.zeros(24, dtype=torch.uint8, device=dev)
+                q.add_pull_batch_device(reqs.data_ptr(), n, d_rc.data_ptr(), now, k,
+                                        d_out.data_ptr(), d_res.data_ptr())
+                pending.append(("add", d_rc))
+                pending.append(("pull", (d_out, d_res)))
+                i += 2
+                continue
+            q.add_batch_device(reqs.data_ptr(), n, d_rc.data_ptr())
+            pending.append(("add", d_rc))
+        elif op[0] == "pull":
+            k = op[2]
+            d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            d_res = torch.zeros(24, dtype=torch.uint8, device=dev)
+            q.pull_batch_device(op[1], k, d_out.data_ptr(), d_res.data_ptr())
+            pending.append(("pull", (d_out, d_res)))
+        else:
+            raise ValueError(op[0])
+        i += 1
+    q.sync()
+    outs = []
+    for kind, buf in pending:
+        if kind == "add":
+            outs.append(("add", buf.cpu().numpy().copy()))
+        else:
+            d_out, d_res = buf
+            res = PullResult.from_buffer_copy(d_res.cpu().numpy().tobytes())
+            dec = d_out[:res.n_decisions * DECISION_DTYPE.itemsize].cpu().numpy() \
+                .view(DECISION_DTYPE).copy()
+            outs.append(("pull", dec, (res.n_decisions, res.next_type,
+                                       res.when if res.next_type == 1 else 0.0)))
+    return outs
+
+
+@pytest.mark.parametrize("variant", ["default", "sample_retry", "terminal"])
+def test_pipelined_calls_parity(variant):
+    """DMC_OPT_PIPELINE (bench.py's default): config-3 steps at 65,536
+    clients issued as back-to-back pipelined calls.  `sample_retry` runs the
+    sampled thresholds with no margin, so that every round fails validation
+    and needs the host (a re-run): each such round shuts the device-side gate,
+    the next call's already-queued graph does nothing and is launched again
+    -- the path a caller never sees.  `terminal` puts a step that pulls more
+    than is queued in the middle (a terminal round: the host's terminal pull,
+    then the next call's graph launched again).
+    Every add status, decision and result record bit-exact against the
+    oracle."""
+    from dmclock_amd._abi import OPT_SAMPLE
+    from dmclock_amd.gpu import GpuQueue
+    tr = workloads.config3_trace(42, 1 << 16, 6, 1 << 12, depth=2)
+    if variant == "terminal":
+        # a step in the middle pulls more than is queued (a terminal round)
+        t = float(tr.ops[7][1])
+        reqs = workloads.arrivals(np.random.default_rng(5), 1 << 16, 1 << 12, t, 2.0 * (1 << 16),
+                                  handle_base=10 ** 7)
+        tr.ops[8:8] = [("add", reqs), ("pull", float(reqs["time"][-1]), 1 << 18)]
+    qo = pyoracle.OracleQueue()
+    outs_o = workloads.replay(qo, tr)
+    assert qo.ties == 0
+    qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 18)
+    if variant == "sample_retry":
+        qg.set_option(OPT_SAMPLE, 2)
+    outs_g = replay_pipelined(qg, tr)
+    assert len(outs_g) == len(outs_o)
+    for i, (a, b) in enumerate(zip(outs_g, outs_o)):
+        assert a[0] == b[0], i
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), (i, np.nonzero(a[1] != b[1]))
+        else:
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], (i, a[2], b[2])
+    compare_states(qg, qo, np.random.default_rng(3).choice(1 << 16, 2048, replace=False),
+                   "final")
+    c = qg.counters()
+    print(variant, c)
+    assert c["fused_calls"] >= 6, c
+    if variant == "sample_retry":
+        assert c["sample_retries"] >= 6, c
+    qg.close()
+
+
+def test_pipelined_bench_call_parity_1m_clients():
+    """bench.py's timed call as it runs by default (DMC_OPT_PIPELINE) at
+    full size: 1,048,576 clients, four pipelined steps of 64K adds + 64K
+    pulls after the pre-population and settle; every output bit-exact."""
+    from dmclock_amd.gpu import GpuQueue
+    tr = workloads.config3_trace(42, 1 << 20, 4, 1 << 16, depth=2)
+    qo = pyoracle.OracleQueue()
+    outs_o = workloads.replay(qo, tr)
+    assert qo.ties == 0
+    qg = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+    outs_g = replay_pipelined(qg, tr)
+    for i, (a, b) in enumerate(zip(outs_g, outs_o)):
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), i
+        else:
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], (i, a[2], b[2])
+    assert qg.counters()["fused_calls"] >= 4
+    qg.close()
