@@ -141,6 +141,9 @@ def parse():
                          "(default: DMC_OPT_PIPELINE, a call queues its graph behind the "
                          "previous one and returns; the timed region ends with "
                          "dmc_queue_sync, which finishes the last call)")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="DMC_OPT_GRAPHS 0: every kernel launched eagerly (A/B of the "
+                         "host's launch cost)")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -377,6 +380,9 @@ def main():
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
                  max_batch=max(args.batch, k, 1 << 20), device=local)
     settle = prepare(q, args, tab, pre)
+    if args.no_graphs:
+        from dmclock_amd._abi import OPT_GRAPHS
+        q.set_option(OPT_GRAPHS, 0)
     pipelined = not (args.no_pipeline or args.host_api or args.separate_calls)
     if pipelined:
         from dmclock_amd._abi import OPT_PIPELINE
