@@ -624,14 +624,30 @@ constexpr auto k_rscan = k_rscan_t<false>;
 constexpr auto k_rscan_brk = k_rscan_t<true>;
 
 // The round's totals from the scan's per-block partials (every thread gets
-// them): wave 0 combines them, 8 per lane for 512 partials with the loads in
-// flight together, and reduces across its lanes; the other waves wait.
+// them).  Wide (default): every thread of the block loads its share (one
+// round trip for up to blockDim partials), each wave reduces on the DPP
+// network, wave 0 combines the waves'.  Narrow (rounds 1-3, A/B): wave 0
+// alone, four partials per lane in flight (four round trips for 1024).
+#ifndef DMC_RPARTS_WIDE
+#define DMC_RPARTS_WIDE 1
+#endif
 __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t nparts) {
   __shared__ RoundPart sh_tot;
+#if DMC_RPARTS_WIDE
+  __shared__ RoundPart sh_w[1024 / 64];
+  RoundPart o = rpart_ident();
+  for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) rpart_combine(o, parts[i]);
+  o = wave_rpart_dpp(o);
+  if ((threadIdx.x & 63) == 63) sh_w[threadIdx.x >> 6] = o;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    RoundPart x = threadIdx.x < (blockDim.x >> 6) ? sh_w[threadIdx.x] : rpart_ident();
+    x = wave_rpart_dpp(x);
+    if (threadIdx.x == 63) sh_tot = x;
+  }
+#else
   if (threadIdx.x < 64) {
     RoundPart o = rpart_ident();
-    // four partials per lane in flight at a time (independent loads, not a
-    // chain of 16 dependent ones for 1024 partials)
     uint32_t i = threadIdx.x;
     for (; i + 3 * 64 < nparts; i += 4 * 64) {
       const RoundPart a = parts[i], b = parts[i + 64], c = parts[i + 128], d = parts[i + 192];
@@ -644,6 +660,7 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
     o = wave_rpart_dpp(o);
     if (threadIdx.x == 63) sh_tot = o;
   }
+#endif
   __syncthreads();
   RoundPart r = sh_tot;
   __syncthreads();

@@ -14,3 +14,4 @@ for v in pipe nopipe nographs; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $R/gpurun_out/r04i_rt -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-profile --steps 10 > gpurun_out/r04i_rt.log 2>&1 || { echo "rt trace failed"; tail -5 gpurun_out/r04i_rt.log; exit 1; }
 ls gpurun_out/r04i_rt
+VARIANTS="${VARIANTS:-base rpnarrow}" ROUNDS=3 timeout -k 10 600 bash scripts/gpu_variants.sh > gpurun_out/r04i_variants.log 2>&1; rc=$?; cat gpurun_out/r04i_variants.log; exit $rc
