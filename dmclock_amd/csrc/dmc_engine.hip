@@ -4537,9 +4537,11 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         return heap_pull(q, now, k, d_out, d_result, nullptr);
       }
       if (int rc0 = settle_act(q)) return rc0;
+      // (pipelined calls also fuse with graphs off: the kernels launched
+      // eagerly, still queued behind the previous call's)
       const bool fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
                         !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
-                        q->use_graphs && !q->prof_on;
+                        (q->use_graphs || q->pipeline) && !q->prof_on;
       if (!fuse) {
         if (int rc = settle_pending(q)) return rc;
         break;  // the two calls
