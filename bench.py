@@ -142,8 +142,12 @@ def parse():
                          "previous one and returns; the timed region ends with "
                          "dmc_queue_sync, which finishes the last call)")
     ap.add_argument("--no-graphs", action="store_true",
-                    help="DMC_OPT_GRAPHS 0: every kernel launched eagerly (A/B of the "
-                         "host's launch cost)")
+                    help="DMC_OPT_GRAPHS 0: every kernel launched eagerly (the default "
+                         "for pipelined calls)")
+    ap.add_argument("--graphs", action="store_true",
+                    help="pipelined calls replay captured hipGraphs (default: launched "
+                         "eagerly -- a replayed graph starts 8.5 us after the previous "
+                         "one ends, eager kernels back to back, r04j)")
     ap.add_argument("--separate-calls", action="store_true",
                     help="dmc_add_batch_device + dmc_pull_batch_device per step "
                          "instead of dmc_add_pull_batch_device")
@@ -380,10 +384,10 @@ def main():
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
                  max_batch=max(args.batch, k, 1 << 20), device=local)
     settle = prepare(q, args, tab, pre)
-    if args.no_graphs:
+    pipelined = not (args.no_pipeline or args.host_api or args.separate_calls)
+    if args.no_graphs or (pipelined and not args.graphs):
         from dmclock_amd._abi import OPT_GRAPHS
         q.set_option(OPT_GRAPHS, 0)
-    pipelined = not (args.no_pipeline or args.host_api or args.separate_calls)
     if pipelined:
         from dmclock_amd._abi import OPT_PIPELINE
         q.set_option(OPT_PIPELINE, 1)
@@ -561,7 +565,9 @@ def main():
                    "api": ("host buffers (dmc_add_batch + dmc_pull_batch, PCIe "
                            "inclusive)" if args.host_api else
                            "device buffers (dmc_add_pull_batch_device"
-                           + (", pipelined: DMC_OPT_PIPELINE)" if pipelined else ")")),
+                           + (", pipelined: DMC_OPT_PIPELINE" if pipelined else "")
+                           + (", kernels launched eagerly)" if (args.no_graphs or
+                              (pipelined and not args.graphs)) else ", hipGraphs)")),
                    "parallelism": f"{world} independent server queue(s)"
                                   + ("" if backend == "nccl" else
                                      " (rehearsal: ranks share device 0, gloo)")},

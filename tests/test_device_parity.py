@@ -189,8 +189,12 @@ def _bench_setup(q, tr):
 
 
 @pytest.mark.timeout(480)
-def test_bench_exact_trace_parity():
-    """bench.py's own workload, call for call:
+@pytest.mark.parametrize("mode", ["bench", "graphs"])
+def test_bench_exact_trace_parity(mode):
+    """bench.py's own workload, call for call,
+    `bench`: as bench.py runs it (DMC_OPT_PIPELINE, kernels launched
+    eagerly, no synchronisation between the calls, one status buffer per
+    step); `graphs`: unpipelined calls replaying the captured graph:
     config3_trace(42, 2^20, 33 steps, 64K, depth 4) is make_workload's trace
     at the default arguments (seed 42, 4,194,304 pre-populated requests, a
     2,097,152-pull settle in two host calls, then warmup 3 + timed 20 +
@@ -223,9 +227,13 @@ def test_bench_exact_trace_parity():
     dev = torch.device("cuda", 0)
     qg = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
     got_setup = _bench_setup(qg, tr)
+    if mode == "bench":
+        from dmclock_amd._abi import OPT_GRAPHS, OPT_PIPELINE
+        qg.set_option(OPT_PIPELINE, 1)
+        qg.set_option(OPT_GRAPHS, 0)
     d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r, _, _ in steps]
     k = 1 << 16
-    d_rc = torch.zeros(k, dtype=torch.int32, device=dev)
+    d_rcs = [torch.zeros(k, dtype=torch.int32, device=dev) for _ in steps]
     d_out = [torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
              for _ in steps]
     d_res = torch.zeros((len(steps), 24), dtype=torch.uint8, device=dev)
@@ -233,11 +241,12 @@ def test_bench_exact_trace_parity():
     qg.counters(reset=True)
     rcs = []
     for i, (reqs, now, kk) in enumerate(steps):
-        # bench.py's step: no synchronisation between the calls
-        qg.add_pull_batch_device(d_reqs[i].data_ptr(), len(reqs), d_rc.data_ptr(), now,
+        qg.add_pull_batch_device(d_reqs[i].data_ptr(), len(reqs), d_rcs[i].data_ptr(), now,
                                  kk, d_out[i].data_ptr(), d_res[i].data_ptr())
-        qg.sync()  # (the status copy runs on torch's stream)
-        rcs.append(d_rc.clone())
+        if mode != "bench":
+            qg.sync()
+    qg.sync()
+    rcs = d_rcs
     ctr = qg.counters()
     torch.cuda.synchronize()
     th.join()
@@ -477,7 +486,8 @@ def replay_pipelined(q, trace):
     return outs
 
 
-@pytest.mark.parametrize("variant", ["default", "sample_retry", "terminal"])
+@pytest.mark.parametrize("variant", ["default", "sample_retry", "terminal", "eager",
+                                     "eager_retry"])
 def test_pipelined_calls_parity(variant):
     """DMC_OPT_PIPELINE (bench.py's default): config-3 steps at 65,536
     clients issued as back-to-back pipelined calls.  `sample_retry` runs the
@@ -486,7 +496,9 @@ def test_pipelined_calls_parity(variant):
     the next call's already-queued graph does nothing and is launched again
     -- the path a caller never sees.  `terminal` puts a step that pulls more
     than is queued in the middle (a terminal round: the host's terminal pull,
-    then the next call's graph launched again).
+    then the next call's graph launched again).  `eager` / `eager_retry`:
+    the same with graphs off (each call's kernels launched eagerly, still
+    queued behind the previous call's).
     Every add status, decision and result record bit-exact against the
     oracle."""
     from dmclock_amd._abi import OPT_SAMPLE
@@ -502,8 +514,11 @@ def test_pipelined_calls_parity(variant):
     outs_o = workloads.replay(qo, tr)
     assert qo.ties == 0
     qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 18)
-    if variant == "sample_retry":
+    if variant in ("sample_retry", "eager_retry"):
         qg.set_option(OPT_SAMPLE, 2)
+    if variant.startswith("eager"):
+        from dmclock_amd._abi import OPT_GRAPHS
+        qg.set_option(OPT_GRAPHS, 0)
     outs_g = replay_pipelined(qg, tr)
     assert len(outs_g) == len(outs_o)
     for i, (a, b) in enumerate(zip(outs_g, outs_o)):
@@ -518,14 +533,14 @@ def test_pipelined_calls_parity(variant):
     c = qg.counters()
     print(variant, c)
     assert c["fused_calls"] >= 6, c
-    if variant == "sample_retry":
+    if variant in ("sample_retry", "eager_retry"):
         assert c["sample_retries"] >= 6, c
     qg.close()
 
 
 def test_pipelined_bench_call_parity_1m_clients():
-    """bench.py's timed call as it runs by default (DMC_OPT_PIPELINE) at
-    full size: 1,048,576 clients, four pipelined steps of 64K adds + 64K
+    """bench.py's timed call as it runs by default (DMC_OPT_PIPELINE, kernels
+    launched eagerly) at full size: 1,048,576 clients, four pipelined steps of 64K adds + 64K
     pulls after the pre-population and settle; every output bit-exact."""
     from dmclock_amd.gpu import GpuQueue
     tr = workloads.config3_trace(42, 1 << 20, 4, 1 << 16, depth=2)
@@ -533,6 +548,8 @@ def test_pipelined_bench_call_parity_1m_clients():
     outs_o = workloads.replay(qo, tr)
     assert qo.ties == 0
     qg = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+    from dmclock_amd._abi import OPT_GRAPHS
+    qg.set_option(OPT_GRAPHS, 0)  # (bench.py's launch mode)
     outs_g = replay_pipelined(qg, tr)
     for i, (a, b) in enumerate(zip(outs_g, outs_o)):
         if a[0] == "add":
