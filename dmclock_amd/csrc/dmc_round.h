@@ -833,15 +833,39 @@ __device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, u
 // (s_sel: tb, C, nz, found -- T's histogram bin, the keys and the non-empty
 // bins up to it, whether the need-th key was found; s_def: C and nz up to
 // the default tb, the top bin)
+// (hv: this thread's kBinsPerThreadR bins, loaded by pick_load ahead of the
+// caller's other loads)
+struct PickBins {
+  uint32_t h[kBinsPerThreadR];
+};
+__device__ inline PickBins pick_load(const uint32_t* hist) {
+  const int t = threadIdx.x & (kPickHalf - 1), p = threadIdx.x / kPickHalf;
+  const uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
+  PickBins b;
+  if (kShards == 1 && kBinsPerThreadR == 4) {
+    const uint4 x = reinterpret_cast<const uint4*>(hp)[t];
+    b.h[0] = x.x;
+    b.h[1] = x.y;
+    b.h[2] = x.z;
+    b.h[3] = x.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kBinsPerThreadR; ++j) {
+      b.h[j] = 0;
+#pragma unroll
+      for (int i = 0; i < kShards; ++i) b.h[j] += hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
+    }
+  }
+  return b;
+}
 __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                                   const RoundPart& tot, const KeyMap& km, uint32_t sh1,
-                                  const uint32_t* hist, uint32_t* sbn, PhaseSel* ps,
+                                  const PickBins& hv, uint32_t* sbn, PhaseSel* ps,
                                   uint32_t* wsum, uint32_t* s_sel, uint32_t* s_def,
                                   uint64_t* s_T) {
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
-  const uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   // the default: every key (T = all, or none) up to the top bin
   const uint32_t tb0 = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
   if (t == 0) {
@@ -850,29 +874,11 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   }
   uint32_t h[kBinsPerThreadR];
   uint32_t local = 0, lz = 0;
-  {
-    uint32_t v[kBinsPerThreadR][kShards];
-    if (kShards == 1 && kBinsPerThreadR == 4) {
-      const uint4 x = reinterpret_cast<const uint4*>(hp)[t];
-      v[0][0] = x.x;
-      v[1][0] = x.y;
-      v[2][0] = x.z;
-      v[3][0] = x.w;
-    } else {
 #pragma unroll
-      for (int j = 0; j < kBinsPerThreadR; ++j)
-#pragma unroll
-        for (int i = 0; i < kShards; ++i)
-          v[j][i] = hp[i * 2 * kHistBinsR + t * kBinsPerThreadR + j];
-    }
-#pragma unroll
-    for (int j = 0; j < kBinsPerThreadR; ++j) {
-      h[j] = 0;
-#pragma unroll
-      for (int i = 0; i < kShards; ++i) h[j] += v[j][i];
-      local += h[j];
-      lz += h[j] ? 1u : 0u;
-    }
+  for (int j = 0; j < kBinsPerThreadR; ++j) {
+    h[j] = hv.h[j];
+    local += h[j];
+    lz += h[j] ? 1u : 0u;
   }
   uint32_t before, zbefore, total;
   half_excl_scan2(local, lz, wsum, &before, &zbefore, &total);
@@ -995,7 +1001,7 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
 }
 
 // (sbn, ps: LDS; the results are complete after the last barrier inside)
-__device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist,
+__device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
                           uint32_t* sbn, PhaseSel* ps, int sampled, uint32_t fault) {
   __shared__ uint32_t wsum[2][2 * kPickHalf / 64];
   __shared__ uint32_t s_sel[2][4], s_def[2][2];
@@ -1008,7 +1014,7 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const uint32_t* hist
   const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
   const KeyMap km(tot.mn[p], tot.mx[p]);
-  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hist,
+  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hv,
              sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p]);
   __syncthreads();  // (ps, written by thread 0 of each half)
   // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset, as a pick
@@ -1464,6 +1470,9 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
 #endif
   const uint32_t n = tb.n;
   const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
+  // the pick's histogram bins first: its compute then waits for them only,
+  // while the slots' keys below are still in flight
+  const PickBins hv = pick_load(hist);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
@@ -1494,7 +1503,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // the thresholds and the rank-bin table, picked from the round's
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
-  pick_both(rd->k_total, rd->tot, hist, ltab, s_ph, (int)rd->sampled, rd->fault);
+  pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault);
   if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   const CandPred pred(s_ph, p_runs);
   if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
