@@ -27,7 +27,7 @@ struct AddParams {
   int32_t* rc;
   uint64_t tick_base;
   uint32_t n;
-  uint32_t pad;
+  uint32_t keep;  // 1: the batch counts stay for k_scan_fix (k_chain_scan's batches)
 };
 
 // Batched activations (the idle reset of every idle client's first request
@@ -291,7 +291,7 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   // the cursor word as stored back: the batch count cleared for the next batch
   auto store_cursor = [&] {
     *cw = (uint64_t)(st.head & 0xffu) | ((uint64_t)(st.count & 0xffu) << 8) |
-          ((uint64_t)st.flags << 16) | (cur & 0xff000000ull);
+          ((uint64_t)st.flags << 16) | (cur & (p.keep ? 0xffffffffff000000ull : 0xff000000ull));
   };
   if (counted && !(st.flags & F_REG)) {
     store_cursor();  // (unchanged; the batch count cleared)

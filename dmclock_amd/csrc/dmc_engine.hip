@@ -178,9 +178,9 @@ k_add_link(AddParams p, Table tb,
   add_link_body(p, tb, abuf, apos, aslot, pblk, act);
 }
 
-__device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act, const TrackFill* tf = nullptr) {
+__device__ __attribute__((always_inline)) inline void add_chain_body(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos, const uint32_t* aslot, ActBuf act, const TrackFill* tf = nullptr, int bid = -1) {
   if (tb.gate && *tb.gate) return;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i = (bid < 0 ? blockIdx.x : (uint32_t)bid) * blockDim.x + threadIdx.x;
   // one level of loads: the call's parameters and this position's filing
   // (apos / aslot are padded to whole blocks: in bounds for the grid)
   const AddParams p = *pblk;
@@ -201,6 +201,22 @@ k_add_chain(Table tb, const AddParams* pblk,
                             const uint32_t* abuf, const uint32_t* apos,
                             const uint32_t* aslot, ActBuf act = ActBuf{}) {
   add_chain_body(tb, pblk, abuf, apos, aslot, act);
+}
+
+// A fused call's add chain and its round's scan in one launch, side by side
+// (blocks [0, nchain): the chain, the rest: the scan, which leaves the
+// batch's slots to k_scan_fix): the chain's random client accesses and the
+// scan's stream overlap instead of running one after the other.
+__global__ void __launch_bounds__(kBlock)
+k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
+             const uint32_t* aslot, uint32_t nchain, uint64_t* keyr, uint64_t* keyp,
+             uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr,
+             uint64_t* skp, uint2* k32, uint32_t* hist) {
+  if (blockIdx.x < nchain)
+    add_chain_body(tb, pblk, abuf, apos, aslot, ActBuf{}, nullptr, (int)blockIdx.x);
+  else
+    rscan_body_g<false, kBlock, true>(tb, keyr, keyp, meta, parts, rd, cp, skr, skp, k32, hist,
+                                      blockIdx.x - nchain, gridDim.x - nchain);
 }
 
 // (multi-table: per-table arguments of a queue group's add kernels, indexed
@@ -3015,18 +3031,23 @@ bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
 
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
-  prof_gate(q);
+// (scanned: the scan already ran with that many partials -- k_chain_scan +
+// k_scan_fix, enqueue_add_round_overlap)
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scanned = 0) {
+  if (!scanned) prof_gate(q);
   const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
   uint32_t N = tb.n;
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN),
-          dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
-          q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
-          sampled ? q->skp : nullptr, q->k32, q->hist);
+  if (scanned)
+    gN = scanned;
+  else
+    klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN),
+            dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
+            q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
+            sampled ? q->skp : nullptr, q->k32, q->hist);
   if (sampled)
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
@@ -3087,6 +3108,40 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix) {
           (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
           (const PostRec*)q->post, q->sched, q->d_hround,
           q->debug ? q->dbg_atime : nullptr);
+}
+
+// A fused call's add + round launched eagerly with the add chain and the
+// scan side by side (k_chain_scan), then the batch's slots scanned
+// (k_scan_fix) and the rest of the round.
+constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
+#ifndef DMC_OVERLAP
+#define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
+#endif
+bool overlap_ok(const dmc_queue* q, uint32_t n) {
+  return DMC_OVERLAP && !q->use_graphs && !q->prof_on &&
+         (n + kFixThreads - 1) / kFixThreads <= kFixPartsMax;
+}
+void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
+  const bool sampled = use_sample(q, false);
+  const Table& tb = q->tb;
+  ap.keep = 1;
+  const uint32_t g = (ap.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, tb, q->abuf,
+                     q->apos, q->aslot, q->apblk, ActBuf{});
+  const uint32_t nS = (tb.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_chain_scan, dim3(g + nS), dim3(kBlock), 0, q->stream, tb,
+                     (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
+                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, g,
+                     sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
+                     q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
+                     sampled ? q->skp : nullptr, q->k32, q->hist);
+  const uint32_t nF = (ap.n + kFixThreads - 1) / kFixThreads;
+  hipLaunchKernelGGL(k_scan_fix, dim3(nF), dim3(kFixThreads), 0, q->stream, tb,
+                     (const AddParams*)q->apblk, (const uint32_t*)q->apos,
+                     (const uint32_t*)q->aslot, sampled ? nullptr : q->keyr,
+                     sampled ? nullptr : q->keyp, q->meta, q->rparts + nS, q->rd,
+                     sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32);
+  enqueue_round(q, cp, false, nS + nF);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
@@ -3769,7 +3824,8 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->sctl, 1);
   rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
-  rc |= A(&q->rparts, (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots));
+  // (k_rscan's partials, or k_chain_scan's and k_scan_fix's)
+  rc |= A(&q->rparts, (N + kBlock - 1) / kBlock + kFixPartsMax);
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsup, kNSup);
   if (q->debug) rc |= A(&q->dbg_bins, kNBR);
@@ -4553,8 +4609,12 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       CallParams cp{k,     0,   now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault,
                     0,     q->pipeline ? q->gate : nullptr};
       auto enqueue = [&] {
-        enqueue_add(q, ap);
-        enqueue_round(q, cp, false);
+        if (overlap_ok(q, n)) {
+          enqueue_add_round_overlap(q, ap, cp);
+        } else {
+          enqueue_add(q, ap);
+          enqueue_round(q, cp, false);
+        }
       };
       ++q->ctr.fused_calls;
       uint64_t key = (4ull << 56) | ((uint64_t)n << 3) | (use_sample(q, false) ? 2 : 0);

@@ -516,14 +516,18 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 #define DMC_SCAN_MINW 8
 #endif
 // (BRK: a limit-break round's scan, its own instantiation: the general
-// scan sits at its 64-register bound)
-template <bool BRK>
-__device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+// scan sits at its 64-register bound.  T: threads per block; bid / nblk:
+// the block's index and count among the scan's blocks.  TOUCHED: slots
+// the running add batch files (ScanRec::nadd != 0) are left to
+// k_scan_fix, which scans them once the batch's adds are in -- the scan
+// then runs beside the add chain, k_chain_scan)
+template <bool BRK, int T = kScanBlock, bool TOUCHED = false>
+__device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist, uint32_t bid, uint32_t nblk) {
   if (tb.gate && *tb.gate) {  // (DMC_OPT_PIPELINE: the host finishes the last call first)
-    if (blockIdx.x == 0 && threadIdx.x == 0) rd->skip = 1u;
+    if (bid == 0 && threadIdx.x == 0) rd->skip = 1u;
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bid == 0 && threadIdx.x == 0) {
     Round z{};
     z.fault = cp.fault;
     z.k_total = cp.k_total;
@@ -539,18 +543,21 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
     z.tdbg[0] = z.tdbg[3] = ~0ull;
     *rd = z;
   }
-  __shared__ RoundPart sh[kScanBlock];
+  __shared__ RoundPart sh[T];
   const double now = cp.now;
   RoundPart acc = rpart_ident();
-  const uint32_t base = blockIdx.x * blockDim.x * kScanSlots + threadIdx.x;
+  const uint32_t base = bid * T * kScanSlots + threadIdx.x;
   ScanCols x[kScanSlots];
+  bool mine[kScanSlots];
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
-    uint32_t s = base + j * blockDim.x;
+    uint32_t s = base + j * T;
     x[j].c = 0;
+    mine[j] = s < tb.n;
     if (s < tb.n) {
       const ScanRec r = tb.sc[s];
-      x[j].c = r.count;
+      if (TOUCHED && r.nadd) mine[j] = false;  // (k_scan_fix's)
+      x[j].c = mine[j] ? r.count : 0;
       x[j].h = r.head;
       x[j].fr = r.r;
       x[j].pk = r.pk;
@@ -563,10 +570,10 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
   constexpr bool brk = BRK;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
-    uint32_t s = base + j * blockDim.x;
+    uint32_t s = base + j * T;
     pre[j] = ScanPre{0.0, 0.0, 0.0, 0.0};
     // (prop_delta only for a post-R front: a queue of one has none)
-    if (s < tb.n && x[j].c > 1 && x[j].fr <= now && !tb.delayed && !brk) {
+    if (mine[j] && x[j].c > 1 && x[j].fr <= now && !tb.delayed && !brk) {
       pre[j].pd = tb.rec[s].pd;
       {
         const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x[j].h + 1) & tb.qmask)];
@@ -580,17 +587,17 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
   bool bad = false;  // a limit-break round's state is not break-ready
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
-    uint32_t s = base + j * blockDim.x;
-    o[j] = s < tb.n ? scan_compute(tb, s, x[j], pre[j], now, brk, &bad)
-                    : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
+    uint32_t s = base + j * T;
+    o[j] = mine[j] ? scan_compute(tb, s, x[j], pre[j], now, brk, &bad)
+                   : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
   }
   // (a limit-break round has no reservation entries: its n_r counts the
   // slots that are not break-ready, for k_rhist's block 0)
   if (bad) acc.n_r += 1;
 #pragma unroll
   for (int j = 0; j < kScanSlots; ++j) {
-    uint32_t s = base + j * blockDim.x;
-    if (s < tb.n)
+    uint32_t s = base + j * T;
+    if (mine[j])
       scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
   }
   // (staged in LDS and combined by wave 0: reducing every wave's partials
@@ -599,14 +606,74 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
   // the threshold histogram k_rhist fills, cleared (the previous round's
   // k_remit blocks have read it)
   {
-    for (uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
-         gi < (uint32_t)(kShards * 2 * kHistBinsR); gi += gridDim.x * blockDim.x)
+    for (uint32_t gi = bid * T + threadIdx.x; gi < (uint32_t)(kShards * 2 * kHistBinsR);
+         gi += nblk * T)
       hist[gi] = 0;
   }
   __syncthreads();
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
-    for (int i = threadIdx.x + 64; i < kScanBlock; i += 64) rpart_combine(o, sh[i]);
+    for (int i = threadIdx.x + 64; i < T; i += 64) rpart_combine(o, sh[i]);
+    o = wave_rpart_dpp(o);
+    if (threadIdx.x == 63) parts[bid] = o;
+  }
+}
+template <bool BRK>
+__device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+  rscan_body_g<BRK>(tb, keyr, keyp, meta, parts, rd, cp, skr, skp, k32, hist, blockIdx.x,
+                    gridDim.x);
+}
+
+// The slots an add batch filed, scanned after its adds (k_chain_scan's scan
+// left them): one thread per batch position, the client's first filer
+// scans its slot exactly as k_rscan would and clears the batch count;
+// per-block partials after the scan's.
+constexpr int kFixThreads = 256;
+__global__ void __launch_bounds__(kFixThreads)
+k_scan_fix(Table tb, const AddParams* pblk, const uint32_t* apos, const uint32_t* aslot,
+           uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd,
+           uint64_t* skr, uint64_t* skp, uint2* k32) {
+  if (rd->skip) return;  // (DMC_OPT_PIPELINE: the round does nothing)
+  __shared__ RoundPart sh[kFixThreads];
+  const uint32_t n = pblk->n;
+  const uint32_t i = blockIdx.x * kFixThreads + threadIdx.x;
+  const double now = rd->now;
+  RoundPart acc = rpart_ident();
+  uint32_t s = 0;
+  bool own = false;
+  if (i < n) {
+    s = aslot[i];
+    own = apos[i] == 0 && s < tb.n;
+  }
+  ScanCols x;
+  x.c = 0;
+  if (own) {
+    const ScanRec r = tb.sc[s];
+    x.c = r.count;
+    x.h = r.head;
+    x.fr = r.r;
+    x.pk = r.pk;
+    x.fl = r.l;
+    x.f = r.flags;
+  }
+  ScanPre pre{0.0, 0.0, 0.0, 0.0};
+  if (own && x.c > 1 && x.fr <= now && !tb.delayed) {
+    pre.pd = tb.rec[s].pd;
+    const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x.h + 1) & tb.qmask)];
+    pre.r1 = e.r;
+    pre.p1 = e.p;
+    pre.l1 = e.l;
+  }
+  if (own) {
+    const ScanOut o = scan_compute(tb, s, x, pre, now);
+    scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
+    tb.sc[s].nadd = 0;  // (the batch count, kept by the add chain)
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    RoundPart o = sh[threadIdx.x];
+    for (int j = threadIdx.x + 64; j < kFixThreads; j += 64) rpart_combine(o, sh[j]);
     o = wave_rpart_dpp(o);
     if (threadIdx.x == 63) parts[blockIdx.x] = o;
   }
