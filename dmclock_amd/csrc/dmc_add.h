@@ -27,7 +27,7 @@ struct AddParams {
   int32_t* rc;
   uint64_t tick_base;
   uint32_t n;
-  uint32_t keep;  // 1: the batch counts stay for k_scan_fix (k_chain_scan's batches)
+  uint32_t keep;  // 1: the batch counts stay until k_rhist (k_chain_scan's batches)
 };
 
 // Batched activations (the idle reset of every idle client's first request

@@ -204,19 +204,41 @@ k_add_chain(Table tb, const AddParams* pblk,
 }
 
 // A fused call's add chain and its round's scan in one launch, side by side
-// (blocks [0, nchain): the chain, the rest: the scan, which leaves the
-// batch's slots to k_scan_fix): the chain's random client accesses and the
-// scan's stream overlap instead of running one after the other.
+// (blocks [0, nchain): the chain; the rest: the scan, kScanChainSlots slots
+// per thread, which leaves the batch's slots to the chain -- each client's
+// first filer scans its slot once its adds are in): the chain's random
+// client accesses and the scan's stream overlap instead of running one
+// after the other.  Partials: the scan's nscan blocks', then the chain's.
+constexpr int kScanChainSlots = 4;
 __global__ void __launch_bounds__(kBlock)
 k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
-             const uint32_t* aslot, uint32_t nchain, uint64_t* keyr, uint64_t* keyp,
-             uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr,
-             uint64_t* skp, uint2* k32, uint32_t* hist) {
-  if (blockIdx.x < nchain)
-    add_chain_body(tb, pblk, abuf, apos, aslot, ActBuf{}, nullptr, (int)blockIdx.x);
-  else
-    rscan_body_g<false, kBlock, true>(tb, keyr, keyp, meta, parts, rd, cp, skr, skp, k32, hist,
-                                      blockIdx.x - nchain, gridDim.x - nchain);
+             const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
+             uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
+             uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+  if (blockIdx.x >= nchain) {
+    rscan_body_g<false, kBlock, true, kScanChainSlots>(tb, keyr, keyp, meta, parts, rd, cp, skr,
+                                                       skp, k32, hist, blockIdx.x - nchain,
+                                                       nscan);
+    return;
+  }
+  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  // (one level of loads: the call's parameters and this position's filing;
+  // apos / aslot are padded to whole blocks)
+  const AddParams p = *pblk;
+  const uint32_t pos0 = apos[i];
+  const uint32_t s = aslot[i];
+  RoundPart acc = rpart_ident();
+  if (i < p.n) {
+    if (pos0 == kNone) {
+      p.rc[i] = DMC_ENOTREG;
+    } else if (pos0 == 0) {
+      AddState st;
+      add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, nullptr);
+      scan_slot(tb, s, cp.now, keyr, keyp, meta, skr, skp, k32, acc);
+    }
+  }
+  block_rpart_store<kBlock>(acc, parts + nscan + blockIdx.x);
 }
 
 // (multi-table: per-table arguments of a queue group's add kernels, indexed
@@ -3041,9 +3063,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  if (scanned)
+  NaddClear nc{};
+  if (scanned) {
     gN = scanned;
-  else
+    nc = NaddClear{&((const AddParams*)q->apblk)->n, q->apos, q->aslot, tb.sc, tb.n};
+  } else
     klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN),
             dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
             q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
@@ -3052,11 +3076,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
             (const RoundPart*)q->rparts, gN, q->rd, q->hist,
-            q->sample_mode == 2 ? 2 : 1, (unsigned long long*)q->bcount, q->bsup);
+            q->sample_mode == 2 ? 2 : 1, (unsigned long long*)q->bcount, q->bsup, nc);
   else
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
-            gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup);
+            gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup, nc);
   klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsup, (const uint32_t*)q->hist,
@@ -3119,7 +3143,7 @@ constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 #endif
 bool overlap_ok(const dmc_queue* q, uint32_t n) {
   return DMC_OVERLAP && !q->use_graphs && !q->prof_on &&
-         (n + kFixThreads - 1) / kFixThreads <= kFixPartsMax;
+         (n + kBlock - 1) / kBlock <= kFixPartsMax;
 }
 void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
   const bool sampled = use_sample(q, false);
@@ -3128,20 +3152,14 @@ void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp)
   const uint32_t g = (ap.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, tb, q->abuf,
                      q->apos, q->aslot, q->apblk, ActBuf{});
-  const uint32_t nS = (tb.n + kBlock - 1) / kBlock;
+  const uint32_t nS = (tb.n + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
   hipLaunchKernelGGL(k_chain_scan, dim3(g + nS), dim3(kBlock), 0, q->stream, tb,
                      (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
-                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, g,
+                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, g, nS,
                      sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
                      q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
                      sampled ? q->skp : nullptr, q->k32, q->hist);
-  const uint32_t nF = (ap.n + kFixThreads - 1) / kFixThreads;
-  hipLaunchKernelGGL(k_scan_fix, dim3(nF), dim3(kFixThreads), 0, q->stream, tb,
-                     (const AddParams*)q->apblk, (const uint32_t*)q->apos,
-                     (const uint32_t*)q->aslot, sampled ? nullptr : q->keyr,
-                     sampled ? nullptr : q->keyp, q->meta, q->rparts + nS, q->rd,
-                     sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32);
-  enqueue_round(q, cp, false, nS + nF);
+  enqueue_round(q, cp, false, nS + g);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,

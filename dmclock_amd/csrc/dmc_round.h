@@ -518,10 +518,10 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound.  T: threads per block; bid / nblk:
 // the block's index and count among the scan's blocks.  TOUCHED: slots
-// the running add batch files (ScanRec::nadd != 0) are left to
-// k_scan_fix, which scans them once the batch's adds are in -- the scan
-// then runs beside the add chain, k_chain_scan)
-template <bool BRK, int T = kScanBlock, bool TOUCHED = false>
+// the running add batch files (ScanRec::nadd != 0) are left to the add
+// chain, which scans each once its adds are in (scan_slot) -- the scan then
+// runs beside the add chain, k_chain_scan)
+template <bool BRK, int T = kScanBlock, bool TOUCHED = false, int SL = kScanSlots>
 __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist, uint32_t bid, uint32_t nblk) {
   if (tb.gate && *tb.gate) {  // (DMC_OPT_PIPELINE: the host finishes the last call first)
     if (bid == 0 && threadIdx.x == 0) rd->skip = 1u;
@@ -546,17 +546,17 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
   __shared__ RoundPart sh[T];
   const double now = cp.now;
   RoundPart acc = rpart_ident();
-  const uint32_t base = bid * T * kScanSlots + threadIdx.x;
-  ScanCols x[kScanSlots];
-  bool mine[kScanSlots];
+  const uint32_t base = bid * T * SL + threadIdx.x;
+  ScanCols x[SL];
+  bool mine[SL];
 #pragma unroll
-  for (int j = 0; j < kScanSlots; ++j) {
+  for (int j = 0; j < SL; ++j) {
     uint32_t s = base + j * T;
     x[j].c = 0;
     mine[j] = s < tb.n;
     if (s < tb.n) {
       const ScanRec r = tb.sc[s];
-      if (TOUCHED && r.nadd) mine[j] = false;  // (k_scan_fix's)
+      if (TOUCHED && r.nadd) mine[j] = false;  // (the add chain's)
       x[j].c = mine[j] ? r.count : 0;
       x[j].h = r.head;
       x[j].fr = r.r;
@@ -566,10 +566,10 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
     }
   }
   // every slot's first R prefix step in one level of loads
-  ScanPre pre[kScanSlots];
+  ScanPre pre[SL];
   constexpr bool brk = BRK;
 #pragma unroll
-  for (int j = 0; j < kScanSlots; ++j) {
+  for (int j = 0; j < SL; ++j) {
     uint32_t s = base + j * T;
     pre[j] = ScanPre{0.0, 0.0, 0.0, 0.0};
     // (prop_delta only for a post-R front: a queue of one has none)
@@ -583,10 +583,10 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
       }
     }
   }
-  ScanOut o[kScanSlots];
+  ScanOut o[SL];
   bool bad = false;  // a limit-break round's state is not break-ready
 #pragma unroll
-  for (int j = 0; j < kScanSlots; ++j) {
+  for (int j = 0; j < SL; ++j) {
     uint32_t s = base + j * T;
     o[j] = mine[j] ? scan_compute(tb, s, x[j], pre[j], now, brk, &bad)
                    : ScanOut{kMaxKey, kMaxKey, 0, 0, false};
@@ -595,7 +595,7 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
   // slots that are not break-ready, for k_rhist's block 0)
   if (bad) acc.n_r += 1;
 #pragma unroll
-  for (int j = 0; j < kScanSlots; ++j) {
+  for (int j = 0; j < SL; ++j) {
     uint32_t s = base + j * T;
     if (mine[j])
       scan_store(tb, s, x[j], o[j], keyr, keyp, meta, skr, skp, k32, acc);
@@ -624,60 +624,46 @@ __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uin
                     gridDim.x);
 }
 
-// The slots an add batch filed, scanned after its adds (k_chain_scan's scan
-// left them): one thread per batch position, the client's first filer
-// scans its slot exactly as k_rscan would and clears the batch count;
-// per-block partials after the scan's.
-constexpr int kFixThreads = 256;
-__global__ void __launch_bounds__(kFixThreads)
-k_scan_fix(Table tb, const AddParams* pblk, const uint32_t* apos, const uint32_t* aslot,
-           uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd,
-           uint64_t* skr, uint64_t* skp, uint2* k32) {
-  if (rd->skip) return;  // (DMC_OPT_PIPELINE: the round does nothing)
-  __shared__ RoundPart sh[kFixThreads];
-  const uint32_t n = pblk->n;
-  const uint32_t i = blockIdx.x * kFixThreads + threadIdx.x;
-  const double now = rd->now;
-  RoundPart acc = rpart_ident();
-  uint32_t s = 0;
-  bool own = false;
-  if (i < n) {
-    s = aslot[i];
-    own = apos[i] == 0 && s < tb.n;
-  }
+// A slot an add batch filed, scanned after its adds by the thread that
+// replayed them (k_chain_scan's scan leaves such slots, TOUCHED above): exactly what
+// k_rscan computes and stores for it, accumulated into acc.
+__device__ inline void scan_slot(const Table& tb, uint32_t s, double now, uint64_t* keyr,
+                                 uint64_t* keyp, uint32_t* meta, uint64_t* skr, uint64_t* skp,
+                                 uint2* k32, RoundPart& acc) {
+  const ScanRec r = tb.sc[s];
   ScanCols x;
-  x.c = 0;
-  if (own) {
-    const ScanRec r = tb.sc[s];
-    x.c = r.count;
-    x.h = r.head;
-    x.fr = r.r;
-    x.pk = r.pk;
-    x.fl = r.l;
-    x.f = r.flags;
-  }
+  x.c = r.count;
+  x.h = r.head;
+  x.fr = r.r;
+  x.pk = r.pk;
+  x.fl = r.l;
+  x.f = r.flags;
   ScanPre pre{0.0, 0.0, 0.0, 0.0};
-  if (own && x.c > 1 && x.fr <= now && !tb.delayed) {
+  if (x.c > 1 && x.fr <= now && !tb.delayed) {
     pre.pd = tb.rec[s].pd;
     const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x.h + 1) & tb.qmask)];
     pre.r1 = e.r;
     pre.p1 = e.p;
     pre.l1 = e.l;
   }
-  if (own) {
-    const ScanOut o = scan_compute(tb, s, x, pre, now);
-    scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
-    tb.sc[s].nadd = 0;  // (the batch count, kept by the add chain)
-  }
+  const ScanOut o = scan_compute(tb, s, x, pre, now);
+  scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
+}
+
+// a block's partials (T threads' acc) combined into parts[i]
+template <int T>
+__device__ inline void block_rpart_store(RoundPart acc, RoundPart* out) {
+  __shared__ RoundPart sh[T];
   sh[threadIdx.x] = acc;
   __syncthreads();
   if (threadIdx.x < 64) {
     RoundPart o = sh[threadIdx.x];
-    for (int j = threadIdx.x + 64; j < kFixThreads; j += 64) rpart_combine(o, sh[j]);
+    for (int j = threadIdx.x + 64; j < T; j += 64) rpart_combine(o, sh[j]);
     o = wave_rpart_dpp(o);
-    if (threadIdx.x == 63) parts[blockIdx.x] = o;
+    if (threadIdx.x == 63) *out = o;
   }
 }
+
 template <bool BRK>
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW)
 k_rscan_t(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta,
@@ -824,10 +810,24 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
     else gsup[i - kNBR] = 0ull;
   }
 }
+// (after k_chain_scan: the batch counts its add chain kept, so that its scan
+// could tell the batch's slots, cleared)
+struct NaddClear {
+  const uint32_t* n;  // the batch size (AddParams::n, published by k_add_link)
+  const uint32_t* apos;
+  const uint32_t* aslot;
+  ScanRec* sc;
+  uint32_t nslots;
+};
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
         uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
-        unsigned long long* bcount, unsigned long long* gsup) {
+        unsigned long long* bcount, unsigned long long* gsup, NaddClear nc = NaddClear{}) {
+  if (nc.sc && !rd->skip) {
+    const uint32_t nb = *nc.n;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x)
+      if (nc.apos[i] == 0 && nc.aslot[i] < nc.nslots) nc.sc[nc.aslot[i]].nadd = 0;
+  }
   rhist_body(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
 }
 

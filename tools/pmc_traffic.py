@@ -23,13 +23,16 @@ STAGES = {
     "future": ["k_round_future"],
     "add_link": ["k_add_link"],
     "add_chain": ["k_add_chain"],
+    # (bench.py's default launch: the add chain beside the scan, then the
+    # batch's slots scanned)
+    "chain_scan": ["k_chain_scan", "k_scan_fix"],
 }
 CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
 STREAMING = {"scan", "select", "future"}
 # walkers that also stream columns with 16-B-per-lane loads: bytes per slot
 # (k_remit: the quantized keys 8 + meta 4), counted 2x; the rest of their
 # fetch 1x
-STREAM_PART = {"emit": 12}
+STREAM_PART = {"emit": 12, "chain_scan": 32}
 
 
 def calib_rates(stats_csv, out):
