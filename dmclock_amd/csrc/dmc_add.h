@@ -27,7 +27,8 @@ struct AddParams {
   int32_t* rc;
   uint64_t tick_base;
   uint32_t n;
-  uint32_t keep;  // 1: the batch counts stay until k_rhist (k_chain_scan's batches)
+  uint32_t epoch;  // k_chain_scan's batches: k_add_link stamps the batch's slots with it
+                   // (Table::touch) so that the scan beside the chain leaves them; else 0
 };
 
 // Batched activations (the idle reset of every idle client's first request
@@ -126,6 +127,8 @@ struct AddState {
   bool cd_set, tick_set;    // cur_delta / cur_rho, last_tick changed (ClientAux is
                             // written, never read, by the add path)
   Tag3 front;
+  Tag3 last_added;          // the last request enqueued (add_one)
+  Tag3 nt[2];               // the batch's first two enqueued requests (add_chain_slot)
 };
 
 __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
@@ -186,6 +189,7 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   e.tie = 0;
   e.pad = 0;
   ring[(st.head + st.count) & tb.qmask] = e;
+  st.last_added = tag;
   if (st.count == 0) {
     st.front = tag;
     st.front_set = true;
@@ -291,7 +295,7 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   // the cursor word as stored back: the batch count cleared for the next batch
   auto store_cursor = [&] {
     *cw = (uint64_t)(st.head & 0xffu) | ((uint64_t)(st.count & 0xffu) << 8) |
-          ((uint64_t)st.flags << 16) | (cur & (p.keep ? 0xffffffffff000000ull : 0xff000000ull));
+          ((uint64_t)st.flags << 16) | (cur & 0xff000000ull);
   };
   if (counted && !(st.flags & F_REG)) {
     store_cursor();  // (unchanged; the batch count cleared)
@@ -320,7 +324,9 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
       tf->reqs[pos].rho = rq.rho;
       add_one(tb, st, ring, p, pos, &rq);
     } else {
+      const uint32_t c_before = st.count;
       add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
+      if (st.count > c_before && c_before - count0 < 2u) st.nt[c_before - count0] = st.last_added;
     }
     if (!act.cold) return;
     if (idle0) {

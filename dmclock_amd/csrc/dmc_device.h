@@ -101,6 +101,9 @@ struct Table {
   // host must finish its call first; the next call's graph, already queued,
   // then does nothing (every kernel of it checks); else null
   const uint32_t* gate;
+  // per slot: the epoch of the last add batch that filed it with the scan
+  // running beside the add chain (AddParams::epoch, k_chain_scan)
+  uint32_t* touch;
 };
 
 __host__ __device__ inline uint64_t dbits(double x) {

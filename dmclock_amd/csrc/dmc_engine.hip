@@ -168,6 +168,7 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
   }
   uint32_t pos = atomicAdd(&tb.sc[s].nadd, 1u);
   apos[i] = pos;
+  if (p.epoch) tb.touch[s] = p.epoch;  // (k_chain_scan's scan leaves the slot)
   // (filing order 0 replays the client's requests and knows its own position)
   if (pos - 1u < kAddSlots - 1u) abuf[(size_t)s * kAddSlots + pos] = i;
 }
@@ -233,9 +234,47 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
     if (pos0 == kNone) {
       p.rc[i] = DMC_ENOTREG;
     } else if (pos0 == 0) {
+      // the slot's heap keys before the adds (the cursor's line: no extra
+      // request) and its prop_delta, with the chain's own loads
+      const ScanRec r0 = tb.sc[s];
+      const double pd = tb.rec[s].pd;
       AddState st;
       add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, nullptr);
-      scan_slot(tb, s, cp.now, keyr, keyp, meta, skr, skp, k32, acc);
+      // the scan of the slot after its adds, from the chain's registers (what
+      // k_rscan would load): the front is the batch's first request if the
+      // queue was empty, else unchanged; queue position 1 is a request of
+      // the batch unless two were queued before
+      ScanCols x;
+      x.c = st.count;
+      x.h = st.head;
+      x.f = st.flags;
+      if (st.front_set) {
+        x.fr = st.front.r;
+        x.pk = __dadd_rn(st.front.p, pd);
+        x.fl = st.front.l;
+      } else {
+        x.fr = r0.r;
+        x.pk = r0.pk;
+        x.fl = r0.l;
+      }
+      ScanPre pre{0.0, 0.0, 0.0, 0.0};
+      if (x.c > 1 && x.fr <= cp.now && !tb.delayed) {
+        pre.pd = pd;
+        const uint32_t c0 = r0.count;
+        if (c0 >= 2) {
+          const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x.h + 1) & tb.qmask)];
+          pre.r1 = e.r;
+          pre.p1 = e.p;
+          pre.l1 = e.l;
+        } else {
+          const Tag3& t1 = st.nt[1 - c0];
+          pre.r1 = t1.r;
+          pre.p1 = t1.p;
+          pre.l1 = t1.l;
+        }
+      }
+      const ScanOut o = scan_compute(tb, s, x, pre, cp.now);
+      scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
     }
   }
   block_rpart_store<kBlock>(acc, parts + nscan + blockIdx.x);
@@ -1933,6 +1972,7 @@ struct dmc_queue {
   // DMC_OPT_PIPELINE: the gate word (Table::gate) and the call left pending
   bool pipeline = false;
   uint32_t* gate = nullptr;
+  uint32_t epoch = 0;  // k_chain_scan's batches (AddParams::epoch)
   struct PendCall {
     bool on = false;
     uint64_t seq = 0;  // its round's sequence number
@@ -3053,8 +3093,8 @@ bool use_sample(const dmc_queue* q, bool radix) {
   return !radix && q->sample_mode && q->tb.n >= kSampleMinN && !q->exact_next;
 }
 
-// (scanned: the scan already ran with that many partials -- k_chain_scan +
-// k_scan_fix, enqueue_add_round_overlap)
+// (scanned: the scan already ran with that many partials -- k_chain_scan,
+// enqueue_add_round_overlap)
 void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scanned = 0) {
   if (!scanned) prof_gate(q);
   const bool sampled = use_sample(q, radix);
@@ -3063,11 +3103,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
   uint32_t gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
   // k_remit blocks (kEmitChunk slots each); k_rapply takes kApplyPerEmit per emit block
   const uint32_t gEm = (N + kEmitChunk - 1) / kEmitChunk;
-  NaddClear nc{};
-  if (scanned) {
+  if (scanned)
     gN = scanned;
-    nc = NaddClear{&((const AddParams*)q->apblk)->n, q->apos, q->aslot, tb.sc, tb.n};
-  } else
+  else
     klaunch(q, DMC_PROF_SCAN, cp.brk ? k_rscan_brk : k_rscan, dim3(gN),
             dim3(kScanBlock), 0, tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp,
             q->meta, q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
@@ -3076,11 +3114,11 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksSampled), dim3(1024), 0,
             (N + kSample - 1) / kSample, (const uint64_t*)q->skr, (const uint64_t*)q->skp,
             (const RoundPart*)q->rparts, gN, q->rd, q->hist,
-            q->sample_mode == 2 ? 2 : 1, (unsigned long long*)q->bcount, q->bsup, nc);
+            q->sample_mode == 2 ? 2 : 1, (unsigned long long*)q->bcount, q->bsup);
   else
     klaunch(q, DMC_PROF_SELECT, k_rhist, dim3(kHistBlocksR), dim3(1024), 0, N,
             (const uint64_t*)q->keyr, (const uint64_t*)q->keyp, (const RoundPart*)q->rparts,
-            gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup, nc);
+            gN, q->rd, q->hist, 0, (unsigned long long*)q->bcount, q->bsup);
   klaunch(q, DMC_PROF_EMIT, cp.brk ? k_remit_brk : k_remit, dim3(gEm),
           dim3(kEmitThreads), 0, tb, q->rd, (const uint2*)q->k32, (const uint32_t*)q->meta, q->cand, q->bcand, q->post,
           q->decof, radix ? nullptr : q->brec, q->bcount, q->bsup, (const uint32_t*)q->hist,
@@ -3134,9 +3172,9 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
           q->debug ? q->dbg_atime : nullptr);
 }
 
-// A fused call's add + round launched eagerly with the add chain and the
-// scan side by side (k_chain_scan), then the batch's slots scanned
-// (k_scan_fix) and the rest of the round.
+// A fused call's add + round launched eagerly: the add chain and the scan
+// side by side (k_chain_scan: the scan leaves the batch's slots, which the
+// chain scans after their adds), then the rest of the round.
 constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 #ifndef DMC_OVERLAP
 #define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
@@ -3148,7 +3186,7 @@ bool overlap_ok(const dmc_queue* q, uint32_t n) {
 void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
   const bool sampled = use_sample(q, false);
   const Table& tb = q->tb;
-  ap.keep = 1;
+  ap.epoch = cp.epoch;
   const uint32_t g = (ap.n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, tb, q->abuf,
                      q->apos, q->aslot, q->apblk, ActBuf{});
@@ -3842,7 +3880,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->sctl, 1);
   rc |= A(&q->fut_done, 1);
   rc |= A(&q->rd, 1);
-  // (k_rscan's partials, or k_chain_scan's and k_scan_fix's)
+  // (k_rscan's partials, or k_chain_scan's: its scan's and its chain's)
   rc |= A(&q->rparts, (N + kBlock - 1) / kBlock + kFixPartsMax);
   rc |= A(&q->bcount, 2 * kNBR);  // 8-byte counters: records | group sizes << 32
   rc |= A(&q->bsup, kNSup);
@@ -3868,6 +3906,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   }
   rc |= A(&q->reqcount, 1);
   t.gate = nullptr;
+  rc |= A(&t.touch, N);
   rc |= A(&q->gate, 1);
   if (hipHostMalloc((void**)&q->h_round, 2 * sizeof(HostRound),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -3949,6 +3988,7 @@ int dmc_queue_destroy(dmc_queue* q) {
     dfree(p);
   if (q->h_round) (void)hipHostFree(q->h_round);
   dfree(q->gate);
+  dfree(q->tb.touch);
   if (q->h_act) (void)hipHostFree(q->h_act);
   dfree(q->act_cold); dfree(q->act_cnew); dfree(q->act_pre); dfree(q->act_suf);
   dfree(q->act_p); dfree(q->act_idx); dfree(q->act_extra); dfree(q->act_parts);
@@ -4624,8 +4664,10 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
+      // (k_chain_scan: the batch's epoch, never 0)
+      const uint32_t epoch = overlap_ok(q, n) ? (++q->epoch ? q->epoch : ++q->epoch) : 0u;
       CallParams cp{k,     0,   now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault,
-                    0,     q->pipeline ? q->gate : nullptr};
+                    epoch, q->pipeline ? q->gate : nullptr};
       auto enqueue = [&] {
         if (overlap_ok(q, n)) {
           enqueue_add_round_overlap(q, ap, cp);

@@ -163,7 +163,7 @@ struct CallParams {
   dmc_pull_result* res;
   uint64_t seq;
   uint32_t fault;  // test hook (DMC_OPT_FAULT): 1 = phase 1's selection left unset
-  uint32_t pad;
+  uint32_t epoch;  // k_chain_scan: the slots stamped with it are the add chain's to scan
   uint32_t* gate;  // DMC_OPT_PIPELINE: a pipelined call's round (its end sets the gate)
 };
 
@@ -518,8 +518,8 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // (BRK: a limit-break round's scan, its own instantiation: the general
 // scan sits at its 64-register bound.  T: threads per block; bid / nblk:
 // the block's index and count among the scan's blocks.  TOUCHED: slots
-// the running add batch files (ScanRec::nadd != 0) are left to the add
-// chain, which scans each once its adds are in (scan_slot) -- the scan then
+// the running add batch files (Table::touch == the call's epoch) are left
+// to the add chain, which scans each once its adds are in -- the scan then
 // runs beside the add chain, k_chain_scan)
 template <bool BRK, int T = kScanBlock, bool TOUCHED = false, int SL = kScanSlots>
 __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist, uint32_t bid, uint32_t nblk) {
@@ -556,7 +556,7 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
     mine[j] = s < tb.n;
     if (s < tb.n) {
       const ScanRec r = tb.sc[s];
-      if (TOUCHED && r.nadd) mine[j] = false;  // (the add chain's)
+      if (TOUCHED && tb.touch[s] == cp.epoch) mine[j] = false;  // (the add chain's)
       x[j].c = mine[j] ? r.count : 0;
       x[j].h = r.head;
       x[j].fr = r.r;
@@ -622,32 +622,6 @@ template <bool BRK>
 __device__ __attribute__((always_inline)) inline void rscan_t_body(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
   rscan_body_g<BRK>(tb, keyr, keyp, meta, parts, rd, cp, skr, skp, k32, hist, blockIdx.x,
                     gridDim.x);
-}
-
-// A slot an add batch filed, scanned after its adds by the thread that
-// replayed them (k_chain_scan's scan leaves such slots, TOUCHED above): exactly what
-// k_rscan computes and stores for it, accumulated into acc.
-__device__ inline void scan_slot(const Table& tb, uint32_t s, double now, uint64_t* keyr,
-                                 uint64_t* keyp, uint32_t* meta, uint64_t* skr, uint64_t* skp,
-                                 uint2* k32, RoundPart& acc) {
-  const ScanRec r = tb.sc[s];
-  ScanCols x;
-  x.c = r.count;
-  x.h = r.head;
-  x.fr = r.r;
-  x.pk = r.pk;
-  x.fl = r.l;
-  x.f = r.flags;
-  ScanPre pre{0.0, 0.0, 0.0, 0.0};
-  if (x.c > 1 && x.fr <= now && !tb.delayed) {
-    pre.pd = tb.rec[s].pd;
-    const ReqEntry& e = tb.ring[(size_t)s * tb.q + ((x.h + 1) & tb.qmask)];
-    pre.r1 = e.r;
-    pre.p1 = e.p;
-    pre.l1 = e.l;
-  }
-  const ScanOut o = scan_compute(tb, s, x, pre, now);
-  scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
 }
 
 // a block's partials (T threads' acc) combined into parts[i]
@@ -810,24 +784,10 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
     else gsup[i - kNBR] = 0ull;
   }
 }
-// (after k_chain_scan: the batch counts its add chain kept, so that its scan
-// could tell the batch's slots, cleared)
-struct NaddClear {
-  const uint32_t* n;  // the batch size (AddParams::n, published by k_add_link)
-  const uint32_t* apos;
-  const uint32_t* aslot;
-  ScanRec* sc;
-  uint32_t nslots;
-};
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
         uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
-        unsigned long long* bcount, unsigned long long* gsup, NaddClear nc = NaddClear{}) {
-  if (nc.sc && !rd->skip) {
-    const uint32_t nb = *nc.n;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x)
-      if (nc.apos[i] == 0 && nc.aslot[i] < nc.nslots) nc.sc[nc.aslot[i]].nadd = 0;
-  }
+        unsigned long long* bcount, unsigned long long* gsup) {
   rhist_body(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
 }
 
