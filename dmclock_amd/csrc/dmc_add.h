@@ -127,8 +127,10 @@ struct AddState {
   bool cd_set, tick_set;    // cur_delta / cur_rho, last_tick changed (ClientAux is
                             // written, never read, by the add path)
   Tag3 front;
-  Tag3 last_added;          // the last request enqueued (add_one)
-  Tag3 nt[2];               // the batch's first two enqueued requests (add_chain_slot)
+  // the batch's first two enqueued requests' r, p, l (add_chain_slot, for
+  // k_chain_scan's scan of the slot)
+  double n0r, n0p, n0l, n1r, n1p, n1l;
+  uint32_t nq = 0;          // requests enqueued by the batch so far
 };
 
 __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
@@ -189,7 +191,16 @@ __device__ inline void add_one(const Table& tb, AddState& st, ReqEntry* ring,
   e.tie = 0;
   e.pad = 0;
   ring[(st.head + st.count) & tb.qmask] = e;
-  st.last_added = tag;
+  if (st.nq == 0) {
+    st.n0r = tag.r;
+    st.n0p = tag.p;
+    st.n0l = tag.l;
+  } else if (st.nq == 1) {
+    st.n1r = tag.r;
+    st.n1p = tag.p;
+    st.n1l = tag.l;
+  }
+  ++st.nq;
   if (st.count == 0) {
     st.front = tag;
     st.front_set = true;
@@ -324,9 +335,7 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
       tf->reqs[pos].rho = rq.rho;
       add_one(tb, st, ring, p, pos, &rq);
     } else {
-      const uint32_t c_before = st.count;
       add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
-      if (st.count > c_before && c_before - count0 < 2u) st.nt[c_before - count0] = st.last_added;
     }
     if (!act.cold) return;
     if (idle0) {

@@ -266,11 +266,14 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
           pre.r1 = e.r;
           pre.p1 = e.p;
           pre.l1 = e.l;
-        } else {
-          const Tag3& t1 = st.nt[1 - c0];
-          pre.r1 = t1.r;
-          pre.p1 = t1.p;
-          pre.l1 = t1.l;
+        } else if (c0 == 1) {  // position 1: the batch's first request
+          pre.r1 = st.n0r;
+          pre.p1 = st.n0p;
+          pre.l1 = st.n0l;
+        } else {  // the batch's second
+          pre.r1 = st.n1r;
+          pre.p1 = st.n1p;
+          pre.l1 = st.n1l;
         }
       }
       const ScanOut o = scan_compute(tb, s, x, pre, cp.now);
