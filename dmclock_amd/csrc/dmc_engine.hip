@@ -210,7 +210,10 @@ k_add_chain(Table tb, const AddParams* pblk,
 // first filer scans its slot once its adds are in): the chain's random
 // client accesses and the scan's stream overlap instead of running one
 // after the other.  Partials: the scan's nscan blocks', then the chain's.
-constexpr int kScanChainSlots = 4;
+#ifndef DMC_CHAIN_SCAN_SLOTS
+#define DMC_CHAIN_SCAN_SLOTS 4
+#endif
+constexpr int kScanChainSlots = DMC_CHAIN_SCAN_SLOTS;
 __global__ void __launch_bounds__(kBlock)
 k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
              const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
