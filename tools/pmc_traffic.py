@@ -138,6 +138,11 @@ def main():
                       "hbm_bytes": round(hbm), "fetch_factor": fac,
                       "hbm_bytes_if_all_streamed": round(2 * f + w),
                       "kernels": ks, "launches_averaged": a.steps}
+    if out.get("chain_scan", {}).get("fetch_size_bytes_raw"):
+        # the timed steps ran the add chain beside the scan: k_rscan and
+        # k_add_chain ran only outside them (pre-population, settle rounds)
+        out.pop("scan", None)
+        out.pop("add_chain", None)
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out.items():
         print(f"{k:10s} fetch(raw) {v['fetch_size_bytes_raw']/1e6:8.2f} MB  write {v['write_size_bytes']/1e6:8.2f} MB  hbm(corr) {v['hbm_bytes']/1e6:8.2f} MB")
