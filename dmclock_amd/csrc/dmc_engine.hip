@@ -214,19 +214,14 @@ k_add_chain(Table tb, const AddParams* pblk,
 #define DMC_CHAIN_SCAN_SLOTS 4
 #endif
 constexpr int kScanChainSlots = DMC_CHAIN_SCAN_SLOTS;
-__global__ void __launch_bounds__(kBlock)
-k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
-             const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
-             uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
-             uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
-  if (blockIdx.x >= nchain) {
-    rscan_body_g<false, kBlock, true, kScanChainSlots>(tb, keyr, keyp, meta, parts, rd, cp, skr,
-                                                       skp, k32, hist, blockIdx.x - nchain,
-                                                       nscan);
-    return;
-  }
+
+// the chain side: block bid of the batch (tf: a queue group's trackers)
+__device__ __attribute__((always_inline)) inline void chain_scan_chain(
+    const Table& tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
+    const uint32_t* aslot, const TrackFill* tf, double now, uint64_t* keyr, uint64_t* keyp,
+    uint32_t* meta, uint64_t* skr, uint64_t* skp, uint2* k32, RoundPart* part, uint32_t bid) {
   if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = bid * kBlock + threadIdx.x;
   // (one level of loads: the call's parameters and this position's filing;
   // apos / aslot are padded to whole blocks)
   const AddParams p = *pblk;
@@ -235,14 +230,14 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
   RoundPart acc = rpart_ident();
   if (i < p.n) {
     if (pos0 == kNone) {
-      p.rc[i] = DMC_ENOTREG;
+      p.rc[i] = DMC_ENOTREG;  // (as k_add_chain: no replay sees this request)
     } else if (pos0 == 0) {
       // the slot's heap keys before the adds (the cursor's line: no extra
       // request) and its prop_delta, with the chain's own loads
       const ScanRec r0 = tb.sc[s];
       const double pd = tb.rec[s].pd;
       AddState st;
-      add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, nullptr);
+      add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, tf);
       // the scan of the slot after its adds, from the chain's registers (what
       // k_rscan would load): the front is the batch's first request if the
       // queue was empty, else unchanged; queue position 1 is a request of
@@ -261,7 +256,7 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
         x.fl = r0.l;
       }
       ScanPre pre{0.0, 0.0, 0.0, 0.0};
-      if (x.c > 1 && x.fr <= cp.now && !tb.delayed) {
+      if (x.c > 1 && x.fr <= now && !tb.delayed) {
         pre.pd = pd;
         const uint32_t c0 = r0.count;
         if (c0 >= 2) {
@@ -279,11 +274,26 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
           pre.l1 = st.n1l;
         }
       }
-      const ScanOut o = scan_compute(tb, s, x, pre, cp.now);
+      const ScanOut o = scan_compute(tb, s, x, pre, now);
       scan_store(tb, s, x, o, keyr, keyp, meta, skr, skp, k32, acc);
     }
   }
-  block_rpart_store<kBlock>(acc, parts + nscan + blockIdx.x);
+  block_rpart_store<kBlock>(acc, part);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
+             const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
+             uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
+             uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+  if (blockIdx.x >= nchain) {
+    rscan_body_g<false, kBlock, true, kScanChainSlots>(tb, keyr, keyp, meta, parts, rd, cp, skr,
+                                                       skp, k32, hist, blockIdx.x - nchain,
+                                                       nscan);
+    return;
+  }
+  chain_scan_chain(tb, pblk, abuf, apos, aslot, nullptr, cp.now, keyr, keyp, meta, skr, skp,
+                   k32, parts + nscan + blockIdx.x, blockIdx.x);
 }
 
 // (multi-table: per-table arguments of a queue group's add kernels, indexed
@@ -302,6 +312,21 @@ __global__ void __launch_bounds__(kBlock) k_add_link_m(const AddArgs* a) {
 __global__ void __launch_bounds__(kBlock) k_add_chain_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
   add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{}, x.tf.reqs ? &x.tf : nullptr);
+}
+// k_chain_scan over a queue group's tables (blockIdx.y)
+__global__ void __launch_bounds__(kBlock)
+k_chain_scan_m(const AddArgs* a, const RScanArgs* sa, uint32_t nchain, uint32_t nscan) {
+  const RScanArgs& y = sa[blockIdx.y];
+  if (blockIdx.x >= nchain) {
+    rscan_body_g<false, kBlock, true, kScanChainSlots>(y.tb, y.keyr, y.keyp, y.meta, y.parts,
+                                                       y.rd, y.cp, y.skr, y.skp, y.k32, y.hist,
+                                                       blockIdx.x - nchain, nscan);
+    return;
+  }
+  const AddArgs& x = a[blockIdx.y];
+  chain_scan_chain(x.tb, x.pblk, x.abuf, x.apos, x.aslot, x.tf.reqs ? &x.tf : nullptr, y.cp.now,
+                   y.keyr, y.keyp, y.meta, y.skr, y.skp, y.k32, y.parts + nscan + blockIdx.x,
+                   blockIdx.x);
 }
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
@@ -4884,11 +4909,17 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       RApplyArgs* pa = reinterpret_cast<RApplyArgs*>(g->h_blob + g->o_apply);
       bool all_sampled = true;
       uint32_t gN = 0, gEm = 0;
+      const uint32_t gAdd = (n + kBlock - 1) / kBlock;
+      // the add chain beside the scan (k_chain_scan_m) unless DMC_OVERLAP=0
+      const bool over = DMC_OVERLAP && gAdd <= kFixPartsMax;
+      uint32_t nS = 0;
       for (uint32_t i = 0; i < S; ++i) {
         dmc_queue* q = g->qs[i];
         const Table& tb = q->tb;
         const uint32_t N = tb.n;
         gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
+        nS = (N + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
+        const uint32_t epoch = over ? (++q->epoch ? q->epoch : ++q->epoch) : 0u;
         gEm = (N + kEmitChunk - 1) / kEmitChunk;
         const bool sampled = use_sample(q, false);
         all_sampled = all_sampled && sampled;
@@ -4896,21 +4927,22 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                                 trk[i].gdelta, trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                 trk[i].first}
                     : TrackArgs{};
-        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, 0}, tb, q->abuf, q->apos,
+        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, epoch}, tb, q->abuf, q->apos,
                         q->aslot, q->apblk,
                         trk ? TrackFill{d_reqs[i], trk[i].client_of_slot, trk[i].gdelta,
                                         trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                         q->p.max_clients}
                             : TrackFill{}};
         const CallParams cp{k, 0, now[i], d_out[i], q->tick + n,
-                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, 0};
+                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, epoch};
+        const uint32_t np = over ? nS + gAdd : gN;  // (the scan's partials)
         sa[i] = RScanArgs{tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
                           q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
                           sampled ? q->skp : nullptr, q->k32, q->hist};
-        ha[i] = sampled ? RHistArgs{(N + kSample - 1) / kSample, gN, q->skr, q->skp, q->rparts,
+        ha[i] = sampled ? RHistArgs{(N + kSample - 1) / kSample, np, q->skr, q->skp, q->rparts,
                                     q->rd, q->hist, q->sample_mode == 2 ? 2 : 1,
                                     (unsigned long long*)q->bcount, q->bsup}
-                        : RHistArgs{N, gN, q->keyr, q->keyp, q->rparts, q->rd, q->hist, 0,
+                        : RHistArgs{N, np, q->keyr, q->keyp, q->rparts, q->rd, q->hist, 0,
                                     (unsigned long long*)q->bcount, q->bsup};
         ea[i] = REmitArgs{tb, q->rd, q->k32, q->meta, q->cand, q->bcand, q->post, q->decof,
                           q->brec, q->bcount, q->bsup, q->hist, q->dense, q->ecap};
@@ -4920,17 +4952,22 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                            q->d_hround};
       }
       const uint32_t gHist = all_sampled ? kHistBlocksSampled : kHistBlocksR;
-      const uint32_t gAdd = (n + kBlock - 1) / kBlock;
       uint8_t* d = g->d_blob;
       auto enqueue = [&](hipStream_t st) {
         (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, st);
         // (the trackers' get_req_params run inside k_add_chain_m: TrackFill)
         hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                            (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                           (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
-                           (const RScanArgs*)(d + g->o_scan));
+        if (over) {
+          hipLaunchKernelGGL(k_chain_scan_m, dim3(gAdd + nS, S), dim3(kBlock), 0, st,
+                             (const AddArgs*)(d + g->o_add), (const RScanArgs*)(d + g->o_scan),
+                             gAdd, nS);
+        } else {
+          hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
+                             (const AddArgs*)(d + g->o_add));
+          hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
+                             (const RScanArgs*)(d + g->o_scan));
+        }
         hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, st,
                            (const RHistArgs*)(d + g->o_hist));
         hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
@@ -4943,7 +4980,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       // the step's graph: captured at the second sighting of its shape, then
       // replayed (the arguments travel in the blob, no node updates)
       const uint64_t key = ((uint64_t)n << 8) | (trk ? 1 : 0) | (all_sampled ? 2 : 0) |
-                           ((uint64_t)k << 36);
+                           ((uint64_t)k << 36) | (over ? 4 : 0);
       dmc_group::G* gr = nullptr;
       for (auto& x : g->graphs)
         if (x.exec && x.key == key) gr = &x;
