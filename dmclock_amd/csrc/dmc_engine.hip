@@ -313,21 +313,6 @@ __global__ void __launch_bounds__(kBlock) k_add_chain_m(const AddArgs* a) {
   const AddArgs& x = a[blockIdx.y];
   add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{}, x.tf.reqs ? &x.tf : nullptr);
 }
-// k_chain_scan over a queue group's tables (blockIdx.y)
-__global__ void __launch_bounds__(kBlock)
-k_chain_scan_m(const AddArgs* a, const RScanArgs* sa, uint32_t nchain, uint32_t nscan) {
-  const RScanArgs& y = sa[blockIdx.y];
-  if (blockIdx.x >= nchain) {
-    rscan_body_g<false, kBlock, true, kScanChainSlots>(y.tb, y.keyr, y.keyp, y.meta, y.parts,
-                                                       y.rd, y.cp, y.skr, y.skp, y.k32, y.hist,
-                                                       blockIdx.x - nchain, nscan);
-    return;
-  }
-  const AddArgs& x = a[blockIdx.y];
-  chain_scan_chain(x.tb, x.pblk, x.abuf, x.apos, x.aslot, x.tf.reqs ? &x.tf : nullptr, y.cp.now,
-                   y.keyr, y.keyp, y.meta, y.skr, y.skp, y.k32, y.parts + nscan + blockIdx.x,
-                   blockIdx.x);
-}
 
 // The end of an idle reset (:981-984): the client's new prop_delta, its
 // front's cached proportion key recomputed with it, idle cleared.
@@ -4910,16 +4895,13 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       bool all_sampled = true;
       uint32_t gN = 0, gEm = 0;
       const uint32_t gAdd = (n + kBlock - 1) / kBlock;
-      // the add chain beside the scan (k_chain_scan_m) unless DMC_OVERLAP=0
-      const bool over = DMC_OVERLAP && gAdd <= kFixPartsMax;
-      uint32_t nS = 0;
+      // (the add chain and the scan one after the other: k_chain_scan over
+      // all tables measured slower, config 5 1.04 vs 0.93 ms, r04o)
       for (uint32_t i = 0; i < S; ++i) {
         dmc_queue* q = g->qs[i];
         const Table& tb = q->tb;
         const uint32_t N = tb.n;
         gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
-        nS = (N + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
-        const uint32_t epoch = over ? (++q->epoch ? q->epoch : ++q->epoch) : 0u;
         gEm = (N + kEmitChunk - 1) / kEmitChunk;
         const bool sampled = use_sample(q, false);
         all_sampled = all_sampled && sampled;
@@ -4927,15 +4909,15 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                                 trk[i].gdelta, trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                 trk[i].first}
                     : TrackArgs{};
-        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, epoch}, tb, q->abuf, q->apos,
+        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, 0}, tb, q->abuf, q->apos,
                         q->aslot, q->apblk,
                         trk ? TrackFill{d_reqs[i], trk[i].client_of_slot, trk[i].gdelta,
                                         trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                         q->p.max_clients}
                             : TrackFill{}};
         const CallParams cp{k, 0, now[i], d_out[i], q->tick + n,
-                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, epoch};
-        const uint32_t np = over ? nS + gAdd : gN;  // (the scan's partials)
+                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, 0};
+        const uint32_t np = gN;  // (the scan's partials)
         sa[i] = RScanArgs{tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
                           q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
                           sampled ? q->skp : nullptr, q->k32, q->hist};
@@ -4958,16 +4940,10 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         // (the trackers' get_req_params run inside k_add_chain_m: TrackFill)
         hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, st,
                            (const AddArgs*)(d + g->o_add));
-        if (over) {
-          hipLaunchKernelGGL(k_chain_scan_m, dim3(gAdd + nS, S), dim3(kBlock), 0, st,
-                             (const AddArgs*)(d + g->o_add), (const RScanArgs*)(d + g->o_scan),
-                             gAdd, nS);
-        } else {
-          hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                             (const AddArgs*)(d + g->o_add));
-          hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
-                             (const RScanArgs*)(d + g->o_scan));
-        }
+        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
+                           (const AddArgs*)(d + g->o_add));
+        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
+                           (const RScanArgs*)(d + g->o_scan));
         hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, st,
                            (const RHistArgs*)(d + g->o_hist));
         hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
@@ -4980,7 +4956,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       // the step's graph: captured at the second sighting of its shape, then
       // replayed (the arguments travel in the blob, no node updates)
       const uint64_t key = ((uint64_t)n << 8) | (trk ? 1 : 0) | (all_sampled ? 2 : 0) |
-                           ((uint64_t)k << 36) | (over ? 4 : 0);
+                           ((uint64_t)k << 36);
       dmc_group::G* gr = nullptr;
       for (auto& x : g->graphs)
         if (x.exec && x.key == key) gr = &x;
