@@ -487,7 +487,7 @@ def replay_pipelined(q, trace):
 
 
 @pytest.mark.parametrize("variant", ["default", "sample_retry", "terminal", "eager",
-                                     "eager_retry"])
+                                     "eager_retry", "eager_delayed", "eager_exact"])
 def test_pipelined_calls_parity(variant):
     """DMC_OPT_PIPELINE (bench.py's default): config-3 steps at 65,536
     clients issued as back-to-back pipelined calls.  `sample_retry` runs the
@@ -498,7 +498,9 @@ def test_pipelined_calls_parity(variant):
     than is queued in the middle (a terminal round: the host's terminal pull,
     then the next call's graph launched again).  `eager` / `eager_retry`:
     the same with graphs off (each call's kernels launched eagerly, still
-    queued behind the previous call's).
+    queued behind the previous call's -- and the add chain beside the
+    scan, k_chain_scan); `eager_delayed`: DelayedTagCalc; `eager_exact`:
+    the exact threshold histogram (every slot's keys written).
     Every add status, decision and result record bit-exact against the
     oracle."""
     from dmclock_amd._abi import OPT_SAMPLE
@@ -510,12 +512,15 @@ def test_pipelined_calls_parity(variant):
         reqs = workloads.arrivals(np.random.default_rng(5), 1 << 16, 1 << 12, t, 2.0 * (1 << 16),
                                   handle_base=10 ** 7)
         tr.ops[8:8] = [("add", reqs), ("pull", float(reqs["time"][-1]), 1 << 18)]
-    qo = pyoracle.OracleQueue()
+    kw = dict(delayed=True) if variant == "eager_delayed" else {}
+    qo = pyoracle.OracleQueue(**kw)
     outs_o = workloads.replay(qo, tr)
     assert qo.ties == 0
-    qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 18)
+    qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 18, **kw)
     if variant in ("sample_retry", "eager_retry"):
         qg.set_option(OPT_SAMPLE, 2)
+    if variant == "eager_exact":
+        qg.set_option(OPT_SAMPLE, 0)
     if variant.startswith("eager"):
         from dmclock_amd._abi import OPT_GRAPHS
         qg.set_option(OPT_GRAPHS, 0)
