@@ -238,6 +238,9 @@ __device__ __attribute__((always_inline)) inline void chain_scan_chain(
       const double pd = tb.rec[s].pd;
       AddState st;
       add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, tf);
+      // (delayed tags: the walk below reads the ring entries, ClientAux and
+      // ClientRec this thread has just written -- ordered explicitly)
+      if (tb.delayed) __threadfence();
       // the scan of the slot after its adds, from the chain's registers (what
       // k_rscan would load): the front is the batch's first request if the
       // queue was empty, else unchanged; queue position 1 is a request of
@@ -3200,7 +3203,7 @@ constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 // caught by k_rrank, DMC_EDEVICE, never a wrong dispatch -- and delayed
 // queues keep the two launches until that is understood)
 bool overlap_ok(const dmc_queue* q, uint32_t n) {
-  return DMC_OVERLAP && !q->use_graphs && !q->prof_on && !q->tb.delayed &&
+  return DMC_OVERLAP && !q->use_graphs && !q->prof_on &&
          (n + kBlock - 1) / kBlock <= kFixPartsMax;
 }
 void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
