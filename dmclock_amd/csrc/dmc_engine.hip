@@ -3198,10 +3198,6 @@ constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 #ifndef DMC_OVERLAP
 #define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
 #endif
-// (immediate tags only: with DelayedTagCalc the merged launch failed a
-// round's outcome check in test_pipelined_calls_parity[eager_delayed] --
-// caught by k_rrank, DMC_EDEVICE, never a wrong dispatch -- and delayed
-// queues keep the two launches until that is understood)
 bool overlap_ok(const dmc_queue* q, uint32_t n) {
   return DMC_OVERLAP && !q->use_graphs && !q->prof_on &&
          (n + kBlock - 1) / kBlock <= kFixPartsMax;
