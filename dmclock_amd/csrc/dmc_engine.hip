@@ -238,9 +238,6 @@ __device__ __attribute__((always_inline)) inline void chain_scan_chain(
       const double pd = tb.rec[s].pd;
       AddState st;
       add_chain_slot(tb, p, s, 0, i, abuf, aslot, ActBuf{}, &st, true, tf);
-      // (delayed tags: the walk below reads the ring entries, ClientAux and
-      // ClientRec this thread has just written -- ordered explicitly)
-      if (tb.delayed) __threadfence();
       // the scan of the slot after its adds, from the chain's registers (what
       // k_rscan would load): the front is the batch's first request if the
       // queue was empty, else unchanged; queue position 1 is a request of
