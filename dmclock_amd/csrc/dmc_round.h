@@ -1846,6 +1846,48 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
   uint32_t pre = 0;
   for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
   uint32_t ex = pre + incl - zs;
+  // tie flags in O(1) per record: a record ties iff the run of equal keys
+  // holding it (contiguous in the sorted order) holds two slots, i.e. two
+  // adjacent members with different slots -- runs numbered by a prefix
+  // count of their heads, each run's flag set by any such pair (heavily
+  // tied bins, config 4's activated clients, made the scans of the run
+  // from every member quadratic)
+  __shared__ uint32_t runtie[kBinCapR];
+  __shared__ uint32_t wrun[kRankThreads / 64];
+  uint32_t hd = 0, dd = 0, nh = 0;  // per position h: bit h
+#pragma unroll
+  for (uint32_t h = 0; h < RP; ++h) {
+    const uint32_t r = RP * t + h;
+    if (r >= cnt) continue;
+    const BKey me = sh[ix[h]];
+    bool head = true, diff = false;
+    if (r > 0) {
+      const BKey pv = sh[ord[r - 1]];
+      head = pv.okey != me.okey;
+      diff = !head && pv.slot != me.slot;
+    }
+    hd |= (head ? 1u : 0u) << h;
+    dd |= (diff ? 1u : 0u) << h;
+    nh += head ? 1u : 0u;
+    runtie[r] = 0u;
+  }
+  const uint32_t rincl = wscan_u32(nh);
+  if (lane == 63) wrun[w] = rincl;
+  __syncthreads();
+  uint32_t rbase = 0;
+  for (uint32_t q = 0; q < w; ++q) rbase += wrun[q];
+  rbase += rincl - nh;  // heads before this thread's positions
+  uint32_t runid[RP];
+  {
+    uint32_t c = rbase;
+#pragma unroll
+    for (uint32_t h = 0; h < RP; ++h) {
+      c += (hd >> h) & 1u;
+      runid[h] = c - 1u;  // (position 0 is a head: c >= 1 for every position < cnt)
+      if ((dd >> h) & 1u) runtie[c - 1u] = 1u;
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (uint32_t h = 0; h < RP; ++h) {
     const uint32_t r = RP * t + h;
@@ -1854,11 +1896,7 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
     if (r >= cnt) continue;
     const uint32_t i = ix[h];
     const BKey me = sh[i];
-    uint32_t tie = 0;
-    for (uint32_t q = r; q > 0 && sh[ord[q - 1]].okey == me.okey; --q)
-      tie |= sh[ord[q - 1]].slot != me.slot;
-    for (uint32_t q = r + 1; q < cnt && sh[ord[q]].okey == me.okey; ++q)
-      tie |= sh[ord[q]].slot != me.slot;
+    const uint32_t tie = runtie[runid[h]];
     const BRecR& x = src[i];
     place_rec(rd, me, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, exh, tie, isp, k,
               n_pgroups, soff, poff, ring, out, decof);
