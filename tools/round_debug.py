@@ -1,7 +1,7 @@
 """Per-round engine diagnostics (DMC_DEBUG=1 prints one line per round on
 stderr) for one server of tests/test_concurrency.py's workload, or for
 bench.py's config-3 workload (--bench): rank-bin maxima, thresholds,
-candidate kinds.  GPU box only."""
+candidate kinds; --config4: bench.py --config 4's workload.  GPU box only."""
 import os
 import sys
 
@@ -32,6 +32,22 @@ def main():
             print(f"=== step {i // 2 - 1}", file=sys.stderr, flush=True)
             q.add_batch(tr.ops[i][1])
             q.pull_batch(tr.ops[i + 1][1], tr.ops[i + 1][2])
+        print(q.counters(), file=sys.stderr)
+        return
+    if "--config4" in sys.argv:
+        tr = workloads.config4_trace(42, 1 << 20, 6, 1 << 16, depth=4)
+        q = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 20)
+        c = tr.clients
+        q.register(c.slots, c.r, c.w, c.l, c.active)
+        for i, op in enumerate(tr.ops):
+            if op[0] == "add":
+                for j in range(0, len(op[1]), 1 << 20):
+                    q.add_batch(op[1][j:j + (1 << 20)])
+            elif op[0] == "pull":
+                print(f"=== op {i}", file=sys.stderr, flush=True)
+                q.pull_batch(op[1], op[2])
+            elif op[0] == "idle":
+                q.mark_idle_batch(op[1])
         print(q.counters(), file=sys.stderr)
         return
     from test_concurrency import SHAPE, workload
