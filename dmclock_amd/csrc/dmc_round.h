@@ -2203,7 +2203,10 @@ struct RoundC {
   uint32_t* brk_prio;  // limit-break rounds: the priority pops' count
 };
 
-constexpr int kApplyStage = 4;  // queue positions staged per candidate (LDS)
+#ifndef DMC_APPLY_STAGE
+#define DMC_APPLY_STAGE 4
+#endif
+constexpr int kApplyStage = DMC_APPLY_STAGE;  // queue positions staged per candidate (LDS)
 __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd,
                                  ReqEntry* st) {
   // every load that depends only on the candidate record is issued before
