@@ -1034,9 +1034,17 @@ k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
 // run minimum below M fails that check (the batch is re-resolved from
 // there).  Each tile's entry M is then stepped over the tiles exactly.
 constexpr uint32_t kActMaxTiles = 1024;  // (batches of up to 2^20 activations)
+#ifndef DMC_SEQ_LDS
+#define DMC_SEQ_LDS 2048
+#endif
+constexpr uint32_t kSeqLds = DMC_SEQ_LDS;  // complex steps chained in LDS (k_act_seq)
+// (dbg, debug queues: [0..4] clocks -- start, offsets, complex steps
+// gathered, chain done, end; [5] windows, [6] wave fallbacks, [7] complex
+// steps, [8] tiles)
 __global__ void __launch_bounds__(kActThreads)
-k_act_seq(ActBuf act, ActTiles tl) {
+k_act_seq(ActBuf act, ActTiles tl, uint64_t* dbg = nullptr) {
   if (*act.anyhard) return;
+  if (dbg && threadIdx.x == 0) dbg[0] = wall_clock64();
   __shared__ uint32_t s_off[kActMaxTiles + 1];  // complex steps before each tile
   __shared__ uint32_t wsum[kActThreads / 64];
   __shared__ uint64_t s_tail[kActMaxTiles];     // each tile's tail run minimum
@@ -1067,6 +1075,11 @@ k_act_seq(ActBuf act, ActTiles tl) {
   }
   __syncthreads();
   const uint32_t nc = s_off[T];
+  if (dbg && tid == 0) {
+    dbg[1] = wall_clock64();
+    dbg[7] = nc;
+    dbg[8] = T;
+  }
   {
     // M entering the first complex step: every simple run before it (the
     // tails of the tiles before its tile, and its own run)
@@ -1089,35 +1102,50 @@ k_act_seq(ActBuf act, ActTiles tl) {
     }
     return lo;
   };
-  for (uint32_t g = tid; g < nc; g += kActThreads) {
-    const uint32_t t = tile_of(g), at = t * kActItems + (g - s_off[t]);
-    tl.cX[g] = tl.sX[at];
-    tl.cP[g] = tl.sP[at];
-    tl.cT[g] = tl.sT[at];
-    tl.cPd[g] = tl.sPd0[at];
-  }
-  __threadfence();
-  __syncthreads();
 #ifndef DMC_ACT_WAVE_BELOW
 #define DMC_ACT_WAVE_BELOW 8
 #endif
 #ifndef DMC_ACT_WAVE_LEN
 #define DMC_ACT_WAVE_LEN 64
 #endif
-  if (nc)
-    act_chain(0, nc, kMaxKey, tl.cX, tl.cP, tl.cT, tl.cPd, &s_M, nullptr, tl.cMo,
-              DMC_ACT_WAVE_BELOW, DMC_ACT_WAVE_LEN);
-  __threadfence();
-  __syncthreads();
-  for (uint32_t g = tid; g < nc; g += kActThreads) {
-    const uint32_t t = tile_of(g);
-    tl.Mout[t * kActItems + (g - s_off[t])] = tl.cMo[g];
+  // the complex steps gathered in order, chained, their M scattered back
+  // (cx..cmo: LDS for up to kSeqLds of them -- every chain window then reads
+  // and writes LDS instead of waiting on global stores and loads -- else the
+  // global scratch)
+  __shared__ uint64_t s_last[kActMaxTiles];
+  auto run = [&](uint64_t* cx, double* cp, double* ct, double* cpd, uint64_t* cmo) {
+    for (uint32_t g = tid; g < nc; g += kActThreads) {
+      const uint32_t t = tile_of(g), at = t * kActItems + (g - s_off[t]);
+      cx[g] = tl.sX[at];
+      cp[g] = tl.sP[at];
+      ct[g] = tl.sT[at];
+      cpd[g] = tl.sPd0[at];
+    }
+    __threadfence();
+    __syncthreads();
+    if (dbg && tid == 0) dbg[2] = wall_clock64();
+    if (nc)
+      act_chain(0, nc, kMaxKey, cx, cp, ct, cpd, &s_M, dbg, cmo, DMC_ACT_WAVE_BELOW,
+                DMC_ACT_WAVE_LEN);
+    __threadfence();
+    __syncthreads();
+    if (dbg && tid == 0) dbg[3] = wall_clock64();
+    for (uint32_t g = tid; g < nc; g += kActThreads) {
+      const uint32_t t = tile_of(g);
+      tl.Mout[t * kActItems + (g - s_off[t])] = cmo[g];
+    }
+    for (uint32_t t = tid; t < T; t += kActThreads)
+      s_last[t] = s_off[t + 1] > s_off[t] ? cmo[s_off[t + 1] - 1] : kMaxKey;
+  };
+  if (nc <= kSeqLds) {
+    __shared__ uint64_t l_x[kSeqLds], l_mo[kSeqLds];
+    __shared__ double l_p[kSeqLds], l_t[kSeqLds], l_pd[kSeqLds];
+    run(l_x, l_p, l_t, l_pd, l_mo);
+  } else {
+    run(tl.cX, tl.cP, tl.cT, tl.cPd, tl.cMo);
   }
   // M entering each tile, stepped over the tiles: after a tile's last
   // complex step (if any), then its tail run
-  __shared__ uint64_t s_last[kActMaxTiles];
-  for (uint32_t t = tid; t < T; t += kActThreads)
-    s_last[t] = s_off[t + 1] > s_off[t] ? tl.cMo[s_off[t + 1] - 1] : kMaxKey;
   __syncthreads();
   if (tid == 0) {
     uint64_t M = kMaxKey;
@@ -1127,6 +1155,7 @@ k_act_seq(ActBuf act, ActTiles tl) {
       M = s_tail[t] < M ? s_tail[t] : M;
     }
     tl.Mtile[T] = M;
+    if (dbg) dbg[4] = wall_clock64();
   }
 }
 
@@ -2026,6 +2055,7 @@ struct dmc_queue {
   uint64_t* dbg_wtime = nullptr; // debug: per-wave rank start/end clocks
   uint64_t* dbg_atime = nullptr; // debug: per-candidate apply start/end clocks
   uint64_t* dbg_etime = nullptr; // debug: per-block k_remit phase clocks (5 per block)
+  uint64_t* dbg_actseq = nullptr; // debug: k_act_seq's clocks and counts (16)
   uint32_t radix_batches = 0;  // rounds left on the fallback path
   uint32_t ovf_streak = 0;     // bin-rank rounds in a row that overflowed (saturates at 5)
   dmc_counters ctr{};          // dmc_queue_counters
@@ -2695,7 +2725,20 @@ void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
   }
   hipLaunchKernelGGL(k_act_keys, dim3(T), dim3(kActThreads), 0, q->stream, act, ax, ap, at,
                      (const double*)q->act_ipd, q->atl);
-  hipLaunchKernelGGL(k_act_seq, dim3(1), dim3(kActThreads), 0, q->stream, act, q->atl);
+  if (q->debug && q->dbg_actseq)
+    (void)hipMemsetAsync(q->dbg_actseq, 0, 16 * 8, q->stream);
+  hipLaunchKernelGGL(k_act_seq, dim3(1), dim3(kActThreads), 0, q->stream, act, q->atl,
+                     q->debug ? q->dbg_actseq : nullptr);
+  if (q->debug && q->dbg_actseq) {
+    uint64_t d[16];
+    if (hipMemcpy(d, q->dbg_actseq, sizeof d, hipMemcpyDeviceToHost) == hipSuccess && d[0])
+      std::fprintf(stderr,
+                   "act_seq: complex %llu tiles %llu windows %llu wave %llu | offsets %.2f "
+                   "gather %.2f chain %.2f end %.2f us\n",
+                   (unsigned long long)d[7], (unsigned long long)d[8],
+                   (unsigned long long)d[5], (unsigned long long)d[6], (d[1] - d[0]) / 100.0,
+                   (d[2] - d[1]) / 100.0, (d[3] - d[2]) / 100.0, (d[4] - d[3]) / 100.0);
+  }
   hipLaunchKernelGGL(k_act_apply, dim3(T), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
                      ap, at, (const double*)q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
   hipLaunchKernelGGL(k_act_fixup, dim3(1), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
@@ -3520,14 +3563,14 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     }
     if (q->debug && getenv("DMC_EMIT_CLOCKS")) {
       const uint32_t nb = (q->tb.n + kEmitChunk - 1) / kEmitChunk;
-      std::vector<uint64_t> e(5ull * nb + 1);
+      std::vector<uint64_t> e((size_t)kEClk * nb + 1);
       (void)hipMemcpy(e.data(), q->dbg_etime, 8ull * e.size(), hipMemcpyDeviceToHost);
       uint64_t t0 = ~0ull;
-      for (uint32_t b = 0; b < nb; ++b) t0 = std::min(t0, e[5ull * b]);
+      for (uint32_t b = 0; b < nb; ++b) t0 = std::min(t0, e[(size_t)kEClk * b]);
       // per phase: median and max over blocks, in us from the first block's start
-      for (int ph = 0; ph < 5; ++ph) {
+      for (int ph = 0; ph < kEClk; ++ph) {
         std::vector<double> v(nb);
-        for (uint32_t b = 0; b < nb; ++b) v[b] = (e[5ull * b + ph] - t0) / 100.0;
+        for (uint32_t b = 0; b < nb; ++b) v[b] = (e[(size_t)kEClk * b + ph] - t0) / 100.0;
         std::sort(v.begin(), v.end());
         std::fprintf(stderr, "emit clock %d: min %.2f med %.2f max %.2f us\n", ph, v[0],
                      v[nb / 2], v[nb - 1]);
@@ -3904,6 +3947,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
   if (q->debug) rc |= A(&q->dbg_etime, 5 * 4096 + 8 + 4 * 4096 * 512);
+  if (q->debug) rc |= A(&q->dbg_actseq, 16);
   // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
   // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan

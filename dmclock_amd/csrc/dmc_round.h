@@ -862,6 +862,14 @@ __device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, u
 // the default tb, the top bin)
 // (hv: this thread's kBinsPerThreadR bins, loaded by pick_load ahead of the
 // caller's other loads)
+// (debug, DMC_PICK_CLOCKS: k_remit's block clocks [5, 10) inside the pick)
+#ifndef DMC_PICK_CLOCKS
+#define DMC_PICK_CLOCKS 0
+#endif
+constexpr int kEClk = DMC_PICK_CLOCKS ? 10 : 5;  // k_remit block clocks per block
+__device__ inline void pclock(uint64_t* pc, int i) {
+  if (DMC_PICK_CLOCKS && pc && threadIdx.x == 0) pc[i] = wall_clock64();
+}
 struct PickBins {
   uint32_t h[kBinsPerThreadR];
 };
@@ -889,7 +897,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
                                   const RoundPart& tot, const KeyMap& km, uint32_t sh1,
                                   const PickBins& hv, uint32_t* sbn, PhaseSel* ps,
                                   uint32_t* wsum, uint32_t* s_sel, uint32_t* s_def,
-                                  uint64_t* s_T) {
+                                  uint64_t* s_T, uint64_t* pc = nullptr) {
   const int t = threadIdx.x & (kPickHalf - 1);
   const uint32_t ne = tot.cnt[p];
   const uint64_t hmin = 0;
@@ -907,8 +915,11 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     local += h[j];
     lz += h[j] ? 1u : 0u;
   }
+  if (DMC_PICK_CLOCKS) asm volatile("" ::"v"(local));
+  pclock(pc, 7);
   uint32_t before, zbefore, total;
   half_excl_scan2(local, lz, wsum, &before, &zbefore, &total);
+  pclock(pc, 8);
   if (need && ne > need && before < need_h && before + local >= need_h) {
     uint32_t cum = before, cz = zbefore;
 #pragma unroll
@@ -947,6 +958,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     s_def[1] = cz;
   }
   __syncthreads();
+  pclock(pc, 9);
   const bool found = s_sel[3] != 0;
   const uint32_t tb = found ? s_sel[0] : tb0;
   const uint32_t C0 = found ? s_sel[1] : s_def[0];
@@ -1029,7 +1041,8 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
 
 // (sbn, ps: LDS; the results are complete after the last barrier inside)
 __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
-                          uint32_t* sbn, PhaseSel* ps, int sampled, uint32_t fault) {
+                          uint32_t* sbn, PhaseSel* ps, int sampled, uint32_t fault,
+                          uint64_t* pc = nullptr) {
   __shared__ uint32_t wsum[2][2 * kPickHalf / 64];
   __shared__ uint32_t s_sel[2][4], s_def[2][2];
   __shared__ uint64_t s_T[2];
@@ -1040,9 +1053,12 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
   // (each such client contributes at least one entry <= T).  P: the rest.
   const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
+  pclock(pc, 5);
   const KeyMap km(tot.mn[p], tot.mx[p]);
+  if (DMC_PICK_CLOCKS) asm volatile("" ::"v"(km.scale));
+  pclock(pc, 6);
   pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hv,
-             sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p]);
+             sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p], pc);
   __syncthreads();  // (ps, written by thread 0 of each half)
   // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset, as a pick
   // that misses a phase would leave it; k_rrank must fail the round
@@ -1476,7 +1492,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   if (rd->skip) return;
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
-  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x] = wall_clock64();
+  if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x] = wall_clock64();
   __shared__ CandRec bl[kEmitChunk];
   __shared__ uint32_t bk[kEmitChunk];  // their first phase's quantized first key
   // each thread's slot predicates and flags, parked for the mark settling
@@ -1530,10 +1546,11 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // the thresholds and the rank-bin table, picked from the round's
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
-  pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault);
+  pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
+            eclk ? eclk + kEClk * blockIdx.x : nullptr);
   if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   const CandPred pred(s_ph, p_runs);
-  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 1] = wall_clock64();
+  if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 1] = wall_clock64();
   uint8_t f[kEmitPer];
 #pragma unroll
   for (int j = 0; j < kEmitPer; ++j) f[j] = (uint8_t)(mt[j] >> 8);
@@ -1596,7 +1613,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 2] = wall_clock64();
+  if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 2] = wall_clock64();
   // candidate index: the block's segment of the candidate arrays (kEmitChunk
   // per block; k_rapply's blocks take their emit block's segment)
   const uint32_t cbase = blockIdx.x * kEmitChunk;
@@ -1629,7 +1646,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
       if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
     }
   }
-  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 3] = wall_clock64();
+  if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 3] = wall_clock64();
   // the block's candidates, copied from LDS in one coalesced pass
   for (uint32_t i = threadIdx.x; i < tot; i += kEmitThreads) cand[cbase + i] = bl[i];
   if (threadIdx.x == 0) bcand[blockIdx.x] = tot;
@@ -1647,7 +1664,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
         tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
-  if (eclk && threadIdx.x == 0) eclk[5 * blockIdx.x + 4] = wall_clock64();
+  if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 4] = wall_clock64();
 }
 template <bool BRK>
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW)
