@@ -691,6 +691,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
   __shared__ uint32_t s_f;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   constexpr uint32_t WW = kActThreads * kChainK;
+  uint32_t nwin = 0, nwave = 0;  // (debug counts)
   while (j0 < m) {
     const uint32_t W = m - j0 < WW ? m - j0 : WW;
     // this thread's activations: j0 + kChainK * t + u
@@ -712,7 +713,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
     if (t == 0) {
       s_ref = M0 < kInf ? M0 : rx[0];  // the chain's binade (else the first X's)
       s_f = W;
-      if (dbg) ++dbg[5];
+      if (dbg && nwin < 12) dbg[16 + 2 * nwin] = wall_clock64();
     }
     __syncthreads();
     const double g = act_grid(s_ref);
@@ -780,14 +781,21 @@ __device__ __attribute__((always_inline)) inline void act_chain(
     }
     __syncthreads();
     const uint32_t adv = fl < W ? fl + 1 : W;
+    if (dbg && t == 0 && nwin < 12)
+      dbg[17 + 2 * nwin] = (uint64_t)j0 | ((uint64_t)adv << 32) | ((uint64_t)W << 48);
+    ++nwin;
     j0 += adv;
     if (adv < wave_below && j0 < m) {
       // the grid does not describe this stretch: step it exactly
       const uint32_t e = m - j0 < wave_len ? m - j0 : wave_len;
       act_wave_steps(j0, e, base, ax, ap, at, apd, s_M, mout);
-      if (dbg && t == 0) ++dbg[6];
+      ++nwave;
       j0 += e;
     }
+  }
+  if (dbg && t == 0) {
+    dbg[5] = nwin;
+    dbg[6] = nwave;
   }
 }
 
@@ -2726,18 +2734,25 @@ void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
   hipLaunchKernelGGL(k_act_keys, dim3(T), dim3(kActThreads), 0, q->stream, act, ax, ap, at,
                      (const double*)q->act_ipd, q->atl);
   if (q->debug && q->dbg_actseq)
-    (void)hipMemsetAsync(q->dbg_actseq, 0, 16 * 8, q->stream);
+    (void)hipMemsetAsync(q->dbg_actseq, 0, 48 * 8, q->stream);
   hipLaunchKernelGGL(k_act_seq, dim3(1), dim3(kActThreads), 0, q->stream, act, q->atl,
                      q->debug ? q->dbg_actseq : nullptr);
   if (q->debug && q->dbg_actseq) {
-    uint64_t d[16];
-    if (hipMemcpy(d, q->dbg_actseq, sizeof d, hipMemcpyDeviceToHost) == hipSuccess && d[0])
+    uint64_t d[48];
+    if (hipMemcpy(d, q->dbg_actseq, sizeof d, hipMemcpyDeviceToHost) == hipSuccess && d[0]) {
+      for (int k = 0; k < 12 && d[16 + 2 * k]; ++k)
+        std::fprintf(stderr, "act_seq window %d: at %.2f us, from %llu, W %llu, advanced %llu\n",
+                     k, (d[16 + 2 * k] - d[2]) / 100.0,
+                     (unsigned long long)(d[17 + 2 * k] & 0xffffffffu),
+                     (unsigned long long)(d[17 + 2 * k] >> 48),
+                     (unsigned long long)((d[17 + 2 * k] >> 32) & 0xffffu));
       std::fprintf(stderr,
                    "act_seq: complex %llu tiles %llu windows %llu wave %llu | offsets %.2f "
                    "gather %.2f chain %.2f end %.2f us\n",
                    (unsigned long long)d[7], (unsigned long long)d[8],
                    (unsigned long long)d[5], (unsigned long long)d[6], (d[1] - d[0]) / 100.0,
                    (d[2] - d[1]) / 100.0, (d[3] - d[2]) / 100.0, (d[4] - d[3]) / 100.0);
+    }
   }
   hipLaunchKernelGGL(k_act_apply, dim3(T), dim3(kActThreads), 0, q->stream, q->tb, act, ax,
                      ap, at, (const double*)q->act_ipd, (const uint32_t*)q->act_islot, q->atl);
@@ -3947,7 +3962,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   if (q->debug) rc |= A(&q->dbg_wtime, 2 * kNBR);
   if (q->debug) rc |= A(&q->dbg_atime, 2 * 262144);
   if (q->debug) rc |= A(&q->dbg_etime, 5 * 4096 + 8 + 4 * 4096 * 512);
-  if (q->debug) rc |= A(&q->dbg_actseq, 16);
+  if (q->debug) rc |= A(&q->dbg_actseq, 48);
   // q->brec (kNBR x kBinCapR rank-bin records, 48 MiB) is allocated by the
   // first bin-ranked round (ensure_brec)
   rc |= A(&q->act_min, 2048);  // per-block minima of the activation scan
