@@ -624,6 +624,22 @@ __device__ inline AffMin aff_then(AffMin f, AffMin g) {  // g after f
   return AffMin{f.a + g.a, fmin(f.b + g.a, g.b)};
 }
 
+// a barrier over the threads running the chain: the block, or one wave
+// (whose LDS operations complete in order: a fence for the compiler)
+template <uint32_t NT>
+__device__ __attribute__((always_inline)) inline void act_sync() {
+  if constexpr (NT == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+// (NT: the threads that run it -- the block, or wave 0 alone, whose
+// synchronisations are then the wave's)
+template <uint32_t NT = kActThreads>
 __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
                                       const uint64_t* ax, const double* ap,
                                       const double* at, double* apd, double* s_M,
@@ -670,7 +686,7 @@ __device__ inline void act_wave_steps(uint32_t c0, uint32_t e, uint64_t base,
     }
     if (t == 0) *s_M = M;
   }
-  __syncthreads();
+  act_sync<NT>();
 }
 
 constexpr int kChainK = 4;  // activations per thread and window (4096 per window)
@@ -679,6 +695,7 @@ constexpr int kChainK = 4;  // activations per thread and window (4096 per windo
 // that advances less than this many activations hands the next kActThreads
 // to the wave-stepped recurrence)
 // (always inlined: three kernels call it, and a call frame is scratch)
+template <uint32_t NT = kActThreads>
 __device__ __attribute__((always_inline)) inline void act_chain(
     uint32_t j0, uint32_t m, uint64_t base, const uint64_t* ax,
                           const double* ap, const double* at, double* apd, double* s_M,
@@ -686,11 +703,11 @@ __device__ __attribute__((always_inline)) inline void act_chain(
                           uint32_t wave_len = kActThreads) {
   constexpr double dmax = 1.7976931348623157e308;
   constexpr double trigger = dmax / 3.0;
-  __shared__ double s_ref, s_last[kActThreads];
-  __shared__ AffMin s_w[kActThreads / 64];
+  __shared__ double s_ref, s_last[NT];
+  __shared__ AffMin s_w[NT / 64];
   __shared__ uint32_t s_f;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  constexpr uint32_t WW = kActThreads * kChainK;
+  constexpr uint32_t WW = NT * kChainK;
   uint32_t nwin = 0, nwave = 0;  // (debug counts)
   while (j0 < m) {
     const uint32_t W = m - j0 < WW ? m - j0 : WW;
@@ -715,7 +732,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
       s_f = W;
       if (dbg && nwin < 12) dbg[16 + 2 * nwin] = wall_clock64();
     }
-    __syncthreads();
+    act_sync<NT>();
     const double g = act_grid(s_ref);
     const double gi = 1.0 / g;  // a power of two: x * gi == x / g exactly
     // 1. speculate: the thread's composed map, then a block scan of the maps
@@ -736,7 +753,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
     if (lane == 63) s_w[wv] = incl;
     AffMin exw{__shfl_up(incl.a, 1), __shfl_up(incl.b, 1)};
     if (lane == 0) exw = AffMin{0.0, kInf};
-    __syncthreads();
+    act_sync<NT>();
     AffMin pre{0.0, kInf};
     for (uint32_t i = 0; i < wv; ++i) pre = aff_then(pre, s_w[i]);
     const AffMin ex = aff_then(pre, exw);  // everything before this thread
@@ -750,7 +767,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
       spec[u] = cur * g;
     }
     s_last[t] = spec[kChainK - 1];
-    __syncthreads();
+    act_sync<NT>();
     // 2. verify, in order (the reference's arithmetic from the speculated
     // M_j; a thread starts from its predecessor's last verified value)
     double Mj = t ? s_last[t - 1] : M0;
@@ -768,7 +785,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
       Mj = spec[u];
     }
     if (bad != 0xffffffffu) atomicMin(&s_f, bad);
-    __syncthreads();
+    act_sync<NT>();
     const uint32_t fl = s_f;  // first failing activation (W: none)
 #pragma unroll
     for (int u = 0; u < kChainK; ++u) {
@@ -779,7 +796,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
       }
       if (i == (fl < W ? fl : W - 1)) *s_M = Mn[u];
     }
-    __syncthreads();
+    act_sync<NT>();
     const uint32_t adv = fl < W ? fl + 1 : W;
     if (dbg && t == 0 && nwin < 12)
       dbg[17 + 2 * nwin] = (uint64_t)j0 | ((uint64_t)adv << 32) | ((uint64_t)W << 48);
@@ -788,7 +805,7 @@ __device__ __attribute__((always_inline)) inline void act_chain(
     if (adv < wave_below && j0 < m) {
       // the grid does not describe this stretch: step it exactly
       const uint32_t e = m - j0 < wave_len ? m - j0 : wave_len;
-      act_wave_steps(j0, e, base, ax, ap, at, apd, s_M, mout);
+      act_wave_steps<NT>(j0, e, base, ax, ap, at, apd, s_M, mout);
       ++nwave;
       j0 += e;
     }
@@ -1046,6 +1063,9 @@ constexpr uint32_t kActMaxTiles = 1024;  // (batches of up to 2^20 activations)
 #define DMC_SEQ_LDS 2048
 #endif
 constexpr uint32_t kSeqLds = DMC_SEQ_LDS;  // complex steps chained in LDS (k_act_seq)
+#ifndef DMC_SEQ_WAVE
+#define DMC_SEQ_WAVE 1  // ... by wave 0 alone
+#endif
 // (dbg, debug queues: [0..4] clocks -- start, offsets, complex steps
 // gathered, chain done, end; [5] windows, [6] wave fallbacks, [7] complex
 // steps, [8] tiles)
@@ -1121,7 +1141,7 @@ k_act_seq(ActBuf act, ActTiles tl, uint64_t* dbg = nullptr) {
   // and writes LDS instead of waiting on global stores and loads -- else the
   // global scratch)
   __shared__ uint64_t s_last[kActMaxTiles];
-  auto run = [&](uint64_t* cx, double* cp, double* ct, double* cpd, uint64_t* cmo) {
+  auto run = [&](uint64_t* cx, double* cp, double* ct, double* cpd, uint64_t* cmo, bool wave) {
     for (uint32_t g = tid; g < nc; g += kActThreads) {
       const uint32_t t = tile_of(g), at = t * kActItems + (g - s_off[t]);
       cx[g] = tl.sX[at];
@@ -1132,9 +1152,15 @@ k_act_seq(ActBuf act, ActTiles tl, uint64_t* dbg = nullptr) {
     __threadfence();
     __syncthreads();
     if (dbg && tid == 0) dbg[2] = wall_clock64();
-    if (nc)
+    if (nc && wave) {
+      // (wave 0 alone: the windows' barriers and scans are the wave's)
+      if (tid < 64)
+        act_chain<64>(0, nc, kMaxKey, cx, cp, ct, cpd, &s_M, dbg, cmo, DMC_ACT_WAVE_BELOW,
+                      DMC_ACT_WAVE_LEN);
+    } else if (nc) {
       act_chain(0, nc, kMaxKey, cx, cp, ct, cpd, &s_M, dbg, cmo, DMC_ACT_WAVE_BELOW,
                 DMC_ACT_WAVE_LEN);
+    }
     __threadfence();
     __syncthreads();
     if (dbg && tid == 0) dbg[3] = wall_clock64();
@@ -1148,9 +1174,9 @@ k_act_seq(ActBuf act, ActTiles tl, uint64_t* dbg = nullptr) {
   if (nc <= kSeqLds) {
     __shared__ uint64_t l_x[kSeqLds], l_mo[kSeqLds];
     __shared__ double l_p[kSeqLds], l_t[kSeqLds], l_pd[kSeqLds];
-    run(l_x, l_p, l_t, l_pd, l_mo);
+    run(l_x, l_p, l_t, l_pd, l_mo, DMC_SEQ_WAVE != 0);
   } else {
-    run(tl.cX, tl.cP, tl.cT, tl.cPd, tl.cMo);
+    run(tl.cX, tl.cP, tl.cT, tl.cPd, tl.cMo, false);
   }
   // M entering each tile, stepped over the tiles: after a tile's last
   // complex step (if any), then its tail run
