@@ -27,6 +27,8 @@ run stats 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_prof -o run
 python tools/stepstats.py gpurun_out/r04f_prof/run_kernel_trace.csv 20 > gpurun_out/r04f_kernel_stats_timed.csv
 else
 run c4 400 python bench.py --config 4 &&
+run c4stats 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_c4prof -o run --output-format csv -- python3 $R/bench.py --config 4 --no-cpu-baseline --no-profile &&
+python tools/stepstats.py gpurun_out/r04f_c4prof/run_kernel_trace.csv 20 > gpurun_out/r04f_c4_kernel_stats_timed.csv &&
 run c5 400 python bench.py --config 5 --no-cpu-baseline &&
 run c5stats 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_c5prof -o run --output-format csv -- python3 $R/bench.py --config 5 --no-cpu-baseline --no-profile --steps 6 --warmup 2 &&
 run lat1m 300 tests/cpp/latency 1048576 2000 --serve &&
