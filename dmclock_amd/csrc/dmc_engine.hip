@@ -3972,7 +3972,7 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   rc |= A(&q->keyp, N);
   rc |= A(&q->k32, N);
   rc |= A(&q->meta, N);
-  rc |= A(&q->hist, kShards * 2 * kHistBinsR);
+  rc |= A(&q->hist, (kShards + 1) * 2 * kHistBinsR);  // (+ the pre-picked rank-bin tables)
   rc |= A(&q->skr, (N + kSample - 1) / kSample);
   rc |= A(&q->skp, (N + kSample - 1) / kSample);
   q->step_grid = grid_for(N, 1024);

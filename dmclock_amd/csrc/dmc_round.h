@@ -151,6 +151,7 @@ struct Round {
   uint64_t seq;          // round sequence number, published to the host
   uint32_t fault;        // test hook (CallParams::fault)
   uint32_t skip;         // this round's kernels do nothing (its k_rscan found the gate shut)
+  uint32_t hist_done;    // k_rhist's block ticket (pre-picked rounds: its last block picks)
   uint32_t* gate;        // a pipelined round: its end sets the gate (CallParams::gate)
 };
 
@@ -699,97 +700,20 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // iteration with every key load issued before the first LDS atomic; the
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
+// queue groups' rounds: the thresholds and rank-bin tables picked once per
+// table by k_rhist_m's last block (rhist_body<true>) instead of by every
+// k_remit_m block (config 5: 0.9565 vs 0.962 ms/step; single-table rounds
+// keep the pick in k_remit, whose 256 blocks run it beside their key loads:
+// the tail made k_rhist 14-17 µs for 3 µs less emit, r04ab)
+#ifndef DMC_PRE_PICK_M
+#define DMC_PRE_PICK_M 1
+#endif
+constexpr bool kPrePickM = DMC_PRE_PICK_M != 0;
 #ifndef DMC_HIST_BLOCKS
 #define DMC_HIST_BLOCKS 32
 #endif
 constexpr int kHistBlocksSampled = DMC_HIST_BLOCKS;  // 131,072 sampled slots of 1M: 4 per thread
                                         // (16 and 64 blocks measured no faster)
-// n keys per phase: every slot's first keys (keyr / keyp, exact), or the
-// scan's 1/kSample sample of them (sampled: 1, or 2 in the test mode of
-// need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
-// every k_remit block picks the thresholds and rank bins from it (no block
-// ticket, no last-block tail here).  Block 0 stores the round's totals.
-__device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
-  if (rd->skip) return;
-  __shared__ uint32_t lh[2][kHistBinsR];
-
-  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
-    lh[0][b] = 0;
-    lh[1][b] = 0;
-  }
-  // this thread's first keys are loaded before the totals are reduced (the
-  // two latencies overlap); further iterations only when n > 4 x threads
-  const uint32_t stride = gridDim.x * blockDim.x * 4;
-  uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  uint64_t kr[4], kp[4];
-  auto load = [&](uint32_t s0) {
-    if (s0 + 4 <= n) {
-      const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
-      const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
-      ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
-      kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
-      kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        kr[j] = s0 + j < n ? keyr[s0 + j] : kMaxKey;
-        kp[j] = s0 + j < n ? keyp[s0 + j] : kMaxKey;
-      }
-    }
-  };
-  if (s < n) load(s);
-  const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // the round's totals (a limit-break round has no reservation entries: its
-    // scan's n_r counts the slots that are not break-ready)
-    const bool brk_bad = rd->brk && tot.n_r;
-    RoundPart t2 = tot;
-    if (rd->brk) t2.n_r = 0;
-    rd->tot = t2;
-    rd->n_r = t2.n_r;
-    rd->p_runs = t2.n_r < (uint64_t)rd->k_total ? 1 : 0;
-    rd->sampled = (uint32_t)sampled;
-    if (brk_bad) {
-      // the state is not the one a limit-break round assumes: nothing of
-      // the round takes effect, the host runs general pulls instead
-      rd->brk_bad = 1;
-      rd->overflow = 5;
-    }
-  }
-  if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
-    const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
-    const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
-    const uint32_t sh1 = hist_shift_r(m1(tot.mx[1]));
-    for (; s < n; s += stride) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(m0(kr[j]), 0, sh0)], 1u);
-        if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(m1(kp[j]), 0, sh1)], 1u);
-      }
-      if (s + stride < n) load(s + stride);
-    }
-    __syncthreads();
-    uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
-    for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
-      if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
-      if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
-    }
-  }
-  // the rank-bin counters and super-bin sums k_remit fills, cleared (the
-  // previous round's k_rrank has read them; last: a load's wait also waits
-  // for the wave's earlier stores)
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)(kNBR + kNSup);
-       i += gridDim.x * blockDim.x) {
-    if (i < (uint32_t)kNBR) bcount[i] = 0ull;
-    else gsup[i - kNBR] = 0ull;
-  }
-}
-__global__ void __launch_bounds__(1024)
-k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
-        uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
-        unsigned long long* bcount, unsigned long long* gsup) {
-  rhist_body(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
-}
 
 // Threshold and rank-bin table of one phase, by one half (kPickHalf
 // threads) of a k_remit block (every block, from the same histogram: the
@@ -1064,6 +988,130 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
   // that misses a phase would leave it; k_rrank must fail the round
   if ((fault & 1u) && threadIdx.x == 0) ps[1].valid = 0;
   __syncthreads();
+}
+
+// n keys per phase: every slot's first keys (keyr / keyp, exact), or the
+// scan's 1/kSample sample of them (sampled: 1, or 2 in the test mode of
+// need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
+// every k_remit block picks the thresholds and rank bins from it (no block
+// ticket, no last-block tail here).  Block 0 stores the round's totals.
+// PRE: the thresholds and rank-bin tables are picked once, by the last
+// block to finish (a block ticket), into the histogram buffer's tail and the
+// Round's selections, instead of by every k_remit block (the multi-table
+// rounds: 4,096 emit blocks at one per CU, each ≈4 µs in the pick)
+template <bool PRE = false>
+__device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
+  if (rd->skip) return;
+  __shared__ uint32_t lh[2][kHistBinsR];
+
+  for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
+    lh[0][b] = 0;
+    lh[1][b] = 0;
+  }
+  // this thread's first keys are loaded before the totals are reduced (the
+  // two latencies overlap); further iterations only when n > 4 x threads
+  const uint32_t stride = gridDim.x * blockDim.x * 4;
+  uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  uint64_t kr[4], kp[4];
+  auto load = [&](uint32_t s0) {
+    if (s0 + 4 <= n) {
+      const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
+      const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
+      ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
+      kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
+      kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kr[j] = s0 + j < n ? keyr[s0 + j] : kMaxKey;
+        kp[j] = s0 + j < n ? keyp[s0 + j] : kMaxKey;
+      }
+    }
+  };
+  if (s < n) load(s);
+  const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the round's totals (a limit-break round has no reservation entries: its
+    // scan's n_r counts the slots that are not break-ready)
+    const bool brk_bad = rd->brk && tot.n_r;
+    RoundPart t2 = tot;
+    if (rd->brk) t2.n_r = 0;
+    rd->tot = t2;
+    rd->n_r = t2.n_r;
+    rd->p_runs = t2.n_r < (uint64_t)rd->k_total ? 1 : 0;
+    rd->sampled = (uint32_t)sampled;
+    if (brk_bad) {
+      // the state is not the one a limit-break round assumes: nothing of
+      // the round takes effect, the host runs general pulls instead
+      rd->brk_bad = 1;
+      rd->overflow = 5;
+    }
+  }
+  if (tot.cnt[0] != 0 || tot.cnt[1] != 0) {
+    const KeyMap m0(tot.mn[0], tot.mx[0]), m1(tot.mn[1], tot.mx[1]);
+    const uint32_t sh0 = hist_shift_r(m0(tot.mx[0]));
+    const uint32_t sh1 = hist_shift_r(m1(tot.mx[1]));
+    for (; s < n; s += stride) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kr[j] != kMaxKey) atomicAdd(&lh[0][hist_bin(m0(kr[j]), 0, sh0)], 1u);
+        if (kp[j] != kMaxKey) atomicAdd(&lh[1][hist_bin(m1(kp[j]), 0, sh1)], 1u);
+      }
+      if (s + stride < n) load(s + stride);
+    }
+    __syncthreads();
+    uint32_t* hs = hist + (blockIdx.x % kShards) * 2 * kHistBinsR;
+    for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
+      if (lh[0][b]) atomicAdd(&hs[b], lh[0][b]);
+      if (lh[1][b]) atomicAdd(&hs[kHistBinsR + b], lh[1][b]);
+    }
+  }
+  // the rank-bin counters and super-bin sums k_remit fills, cleared (the
+  // previous round's k_rrank has read them; last: a load's wait also waits
+  // for the wave's earlier stores)
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (uint32_t)(kNBR + kNSup);
+       i += gridDim.x * blockDim.x) {
+    if (i < (uint32_t)kNBR) bcount[i] = 0ull;
+    else gsup[i - kNBR] = 0ull;
+  }
+  if constexpr (PRE) {
+    static_assert(kEmitThreads == 1024, "pre-picked tables: k_rhist's blocks are k_remit's");
+    __shared__ uint32_t s_last;
+    __shared__ PhaseSel s_ph[2];
+    // this block's flush atomics performed before its ticket (no release
+    // fence: at agent scope it writes back the whole L2, ≈20 µs after the
+    // scan's stores; the histogram's atomics are device-coherent already)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (and every thread is done with lh)
+    if (threadIdx.x == 0) s_last = atomicAdd(&rd->hist_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (s_last) {
+      // every block's flush is in: the bins read at the coherence point
+      // (agent-scope atomic loads), not from this XCD's L2
+      PickBins hv;
+#pragma unroll
+      for (int j = 0; j < kBinsPerThreadR; ++j) {
+        const int t = threadIdx.x & (kPickHalf - 1), p = threadIdx.x / kPickHalf;
+        hv.h[j] = 0;
+#pragma unroll
+        for (int i = 0; i < kShards; ++i)
+          hv.h[j] += __hip_atomic_load(hist + p * kHistBinsR + i * 2 * kHistBinsR +
+                                           t * kBinsPerThreadR + j,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pick_both(rd->k_total, tot, hv, &lh[0][0], s_ph, sampled, rd->fault);
+      reinterpret_cast<uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x] =
+          reinterpret_cast<const uint4*>(&lh[0][0])[threadIdx.x];
+      if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
+      if (threadIdx.x == 0) rd->hist_done = 0;  // (a re-run round takes tickets again)
+    }
+  }
+}
+__global__ void __launch_bounds__(1024)
+k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
+        uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
+        unsigned long long* bcount, unsigned long long* gsup) {
+  rhist_body<false>(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -1487,7 +1535,7 @@ constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
 #ifndef DMC_EMIT_MINW
 #define DMC_EMIT_MINW 4
 #endif
-template <bool BRK>
+template <bool BRK, bool PRE = false>
 __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap, uint64_t* eclk) {
   if (rd->skip) return;
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
@@ -1515,7 +1563,11 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
   // the pick's histogram bins first: its compute then waits for them only,
   // while the slots' keys below are still in flight
-  const PickBins hv = pick_load(hist);
+  // (PRE: the tables k_rhist's last block picked, this thread's share)
+  PickBins hv;
+  uint4 pt;
+  if constexpr (PRE) pt = reinterpret_cast<const uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x];
+  else hv = pick_load(hist);
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
@@ -1546,9 +1598,16 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // the thresholds and the rank-bin table, picked from the round's
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
-  pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
-            eclk ? eclk + kEClk * blockIdx.x : nullptr);
-  if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
+  if constexpr (PRE) {
+    static_assert(kEmitThreads * 4 == 2 * kHistBinsR, "pre-picked tables: a uint4 per thread");
+    reinterpret_cast<uint4*>(ltab)[threadIdx.x] = pt;
+    if (threadIdx.x < 2) s_ph[threadIdx.x] = rd->ph[threadIdx.x];
+    __syncthreads();  // (also orders the zeroing of s_cnt / s_tot)
+  } else {
+    pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
+              eclk ? eclk + kEClk * blockIdx.x : nullptr);
+    if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
+  }
   const CandPred pred(s_ph, p_runs);
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 1] = wall_clock64();
   uint8_t f[kEmitPer];
@@ -1673,7 +1732,8 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
         uint32_t dcap, uint64_t* eclk = nullptr) {
-  remit_t_body<BRK>(tb, rd, k32, meta, cand, bcand, post, decof, brec, bcount, gsup, hist, dense, dcap, eclk);
+  remit_t_body<BRK>(tb, rd, k32, meta, cand, bcand, post, decof, brec, bcount, gsup, hist,
+                    dense, dcap, eclk);
 }
 
 // the general emission and the limit-break rounds'
@@ -2626,12 +2686,13 @@ __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_m(const RSc
 }
 __global__ void __launch_bounds__(1024) k_rhist_m(const RHistArgs* a) {
   const RHistArgs& x = a[blockIdx.y];
-  rhist_body(x.n, x.keyr, x.keyp, x.parts, x.nparts, x.rd, x.hist, x.sampled, x.bcount, x.gsup);
+  rhist_body<kPrePickM>(x.n, x.keyr, x.keyp, x.parts, x.nparts, x.rd, x.hist, x.sampled, x.bcount,
+                        x.gsup);
 }
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const REmitArgs* a) {
   const REmitArgs& x = a[blockIdx.y];
-  remit_t_body<false>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof, x.brec,
-                      x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
+  remit_t_body<false, kPrePickM>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof,
+                                 x.brec, x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
 }
 __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
   const RRankArgs& x = a[blockIdx.y];
