@@ -1075,7 +1075,7 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
     else gsup[i - kNBR] = 0ull;
   }
   if constexpr (PRE) {
-    static_assert(kEmitThreads == 1024, "pre-picked tables: k_rhist's blocks are k_remit's");
+    // (pick_both's halves: the launch gives these blocks kEmitThreads threads)
     __shared__ uint32_t s_last;
     __shared__ PhaseSel s_ph[2];
     // this block's flush atomics performed before its ticket (no release
@@ -1100,8 +1100,9 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       pick_both(rd->k_total, tot, hv, &lh[0][0], s_ph, sampled, rd->fault);
-      reinterpret_cast<uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x] =
-          reinterpret_cast<const uint4*>(&lh[0][0])[threadIdx.x];
+      for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += blockDim.x)
+        reinterpret_cast<uint4*>(hist + kShards * 2 * kHistBinsR)[i] =
+            reinterpret_cast<const uint4*>(&lh[0][0])[i];
       if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
       if (threadIdx.x == 0) rd->hist_done = 0;  // (a re-run round takes tickets again)
     }
@@ -1564,10 +1565,16 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // the pick's histogram bins first: its compute then waits for them only,
   // while the slots' keys below are still in flight
   // (PRE: the tables k_rhist's last block picked, this thread's share)
+  constexpr int kPT = 2 * kHistBinsR / 4 / kEmitThreads;
   PickBins hv;
-  uint4 pt;
-  if constexpr (PRE) pt = reinterpret_cast<const uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x];
-  else hv = pick_load(hist);
+  uint4 pt[kPT];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < kPT; ++j)
+      pt[j] = reinterpret_cast<const uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x + j * kEmitThreads];
+  } else {
+    hv = pick_load(hist);
+  }
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
@@ -1599,8 +1606,8 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
   if constexpr (PRE) {
-    static_assert(kEmitThreads * 4 == 2 * kHistBinsR, "pre-picked tables: a uint4 per thread");
-    reinterpret_cast<uint4*>(ltab)[threadIdx.x] = pt;
+#pragma unroll
+    for (int j = 0; j < kPT; ++j) reinterpret_cast<uint4*>(ltab)[threadIdx.x + j * kEmitThreads] = pt[j];
     if (threadIdx.x < 2) s_ph[threadIdx.x] = rd->ph[threadIdx.x];
     __syncthreads();  // (also orders the zeroing of s_cnt / s_tot)
   } else {
