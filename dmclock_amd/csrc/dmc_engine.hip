@@ -5029,8 +5029,11 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                            (const AddArgs*)(d + g->o_add));
         hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
                            (const RScanArgs*)(d + g->o_scan));
-        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(kPrePickM ? kEmitThreads : 1024), 0, st,
+        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, st,
                            (const RHistArgs*)(d + g->o_hist));
+        if (kPrePickM)
+          hipLaunchKernelGGL(k_rpick_m, dim3(1, S), dim3(kEmitThreads), 0, st,
+                             (const RHistArgs*)(d + g->o_hist));
         hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
                            (const REmitArgs*)(d + g->o_emit));
         hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads), 0, st,

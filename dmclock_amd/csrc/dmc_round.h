@@ -151,7 +151,6 @@ struct Round {
   uint64_t seq;          // round sequence number, published to the host
   uint32_t fault;        // test hook (CallParams::fault)
   uint32_t skip;         // this round's kernels do nothing (its k_rscan found the gate shut)
-  uint32_t hist_done;    // k_rhist's block ticket (pre-picked rounds: its last block picks)
   uint32_t* gate;        // a pipelined round: its end sets the gate (CallParams::gate)
 };
 
@@ -701,10 +700,9 @@ __device__ inline RoundPart reduce_rparts(const RoundPart* parts, uint32_t npart
 // block's bins flush into shard block % kShards.
 constexpr int kHistBlocksR = 256;
 // queue groups' rounds: the thresholds and rank-bin tables picked once per
-// table by k_rhist_m's last block (rhist_body<true>) instead of by every
-// k_remit_m block (config 5: 0.9565 vs 0.962 ms/step; single-table rounds
-// keep the pick in k_remit, whose 256 blocks run it beside their key loads:
-// the tail made k_rhist 14-17 µs for 3 µs less emit, r04ab)
+// table (k_rpick_m) instead of by every k_remit_m block; single-table rounds
+// keep the pick in k_remit, whose 256 blocks run it beside their key loads
+// (a pick in k_rhist's last block made it 14-17 µs for 3 µs less emit, r04ab)
 #ifndef DMC_PRE_PICK_M
 #define DMC_PRE_PICK_M 1
 #endif
@@ -995,11 +993,6 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
 // need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
 // every k_remit block picks the thresholds and rank bins from it (no block
 // ticket, no last-block tail here).  Block 0 stores the round's totals.
-// PRE: the thresholds and rank-bin tables are picked once, by the last
-// block to finish (a block ticket), into the histogram buffer's tail and the
-// Round's selections, instead of by every k_remit block (the multi-table
-// rounds: 4,096 emit blocks at one per CU, each ≈4 µs in the pick)
-template <bool PRE = false>
 __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
   if (rd->skip) return;
   __shared__ uint32_t lh[2][kHistBinsR];
@@ -1074,45 +1067,12 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
     if (i < (uint32_t)kNBR) bcount[i] = 0ull;
     else gsup[i - kNBR] = 0ull;
   }
-  if constexpr (PRE) {
-    // (pick_both's halves: the launch gives these blocks kEmitThreads threads)
-    __shared__ uint32_t s_last;
-    __shared__ PhaseSel s_ph[2];
-    // this block's flush atomics performed before its ticket (no release
-    // fence: at agent scope it writes back the whole L2, ≈20 µs after the
-    // scan's stores; the histogram's atomics are device-coherent already)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // (and every thread is done with lh)
-    if (threadIdx.x == 0) s_last = atomicAdd(&rd->hist_done, 1u) == gridDim.x - 1 ? 1u : 0u;
-    __syncthreads();
-    if (s_last) {
-      // every block's flush is in: the bins read at the coherence point
-      // (agent-scope atomic loads), not from this XCD's L2
-      PickBins hv;
-#pragma unroll
-      for (int j = 0; j < kBinsPerThreadR; ++j) {
-        const int t = threadIdx.x & (kPickHalf - 1), p = threadIdx.x / kPickHalf;
-        hv.h[j] = 0;
-#pragma unroll
-        for (int i = 0; i < kShards; ++i)
-          hv.h[j] += __hip_atomic_load(hist + p * kHistBinsR + i * 2 * kHistBinsR +
-                                           t * kBinsPerThreadR + j,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      pick_both(rd->k_total, tot, hv, &lh[0][0], s_ph, sampled, rd->fault);
-      for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += blockDim.x)
-        reinterpret_cast<uint4*>(hist + kShards * 2 * kHistBinsR)[i] =
-            reinterpret_cast<const uint4*>(&lh[0][0])[i];
-      if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
-      if (threadIdx.x == 0) rd->hist_done = 0;  // (a re-run round takes tickets again)
-    }
-  }
 }
 __global__ void __launch_bounds__(1024)
 k_rhist(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts,
         uint32_t nparts, Round* rd, uint32_t* hist, int sampled,
         unsigned long long* bcount, unsigned long long* gsup) {
-  rhist_body<false>(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
+  rhist_body(n, keyr, keyp, parts, nparts, rd, hist, sampled, bcount, gsup);
 }
 
 // Rank bin of an entry key (monotone in the key): its histogram bin's share
@@ -1564,7 +1524,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
   // the pick's histogram bins first: its compute then waits for them only,
   // while the slots' keys below are still in flight
-  // (PRE: the tables k_rhist's last block picked, this thread's share)
+  // (PRE: the tables k_rpick_m picked, this thread's share)
   constexpr int kPT = 2 * kHistBinsR / 4 / kEmitThreads;
   PickBins hv;
   uint4 pt[kPT];
@@ -2693,8 +2653,23 @@ __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_m(const RSc
 }
 __global__ void __launch_bounds__(1024) k_rhist_m(const RHistArgs* a) {
   const RHistArgs& x = a[blockIdx.y];
-  rhist_body<kPrePickM>(x.n, x.keyr, x.keyp, x.parts, x.nparts, x.rd, x.hist, x.sampled, x.bcount,
-                        x.gsup);
+  rhist_body(x.n, x.keyr, x.keyp, x.parts, x.nparts, x.rd, x.hist, x.sampled, x.bcount, x.gsup);
+}
+// queue groups (kPrePickM): each table's thresholds and rank-bin tables
+// picked once, by one block per table, into the histogram buffer's tail and
+// the Round's selections, for every k_remit_m block to load
+__global__ void __launch_bounds__(kEmitThreads) k_rpick_m(const RHistArgs* a) {
+  const RHistArgs& x = a[blockIdx.y];
+  Round* rd = x.rd;
+  if (rd->skip) return;
+  __shared__ uint32_t sbn[2 * kHistBinsR];
+  __shared__ PhaseSel s_ph[2];
+  const PickBins hv = pick_load(x.hist);
+  pick_both(rd->k_total, rd->tot, hv, sbn, s_ph, (int)rd->sampled, rd->fault);
+  for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += kEmitThreads)
+    reinterpret_cast<uint4*>(x.hist + kShards * 2 * kHistBinsR)[i] =
+        reinterpret_cast<const uint4*>(sbn)[i];
+  if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
 }
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const REmitArgs* a) {
   const REmitArgs& x = a[blockIdx.y];
