@@ -3,7 +3,8 @@
 # passes, the default bench line, kernel stats of the same bench command
 # (timed steps), config 4, config 5 (queue group), single-call latency;
 # outputs gpurun_out/r04f_* (copied into profiles/ afterwards).
-# PART=a: suite + smoke + PMC + bench + stats; PART=b: configs 4/5 + latency
+# PART=a: suite + smoke + PMC + bench + stats; PART=b: configs 4/5 + latency;
+# PART=c: config 5 and its kernel stats
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
@@ -25,6 +26,10 @@ python tools/pmc_traffic.py --out gpurun_out/traffic_r04f.json > gpurun_out/r04f
 run bench 300 python bench.py --traffic gpurun_out/traffic_r04f.json &&
 run stats 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-profile &&
 python tools/stepstats.py gpurun_out/r04f_prof/run_kernel_trace.csv 20 > gpurun_out/r04f_kernel_stats_timed.csv
+elif [ "${PART}" = c ]; then
+run c5 400 python bench.py --config 5 --no-cpu-baseline &&
+run c5stats 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_c5prof -o run --output-format csv -- python3 $R/bench.py --config 5 --no-cpu-baseline --no-profile --steps 6 --warmup 2 &&
+python tools/stepstats.py gpurun_out/r04f_c5prof/run_kernel_trace.csv 6 > gpurun_out/r04f_c5_kernel_stats_timed.csv
 else
 run c4 400 python bench.py --config 4 &&
 run c4stats 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04f_c4prof -o run --output-format csv -- python3 $R/bench.py --config 4 --no-cpu-baseline --no-profile &&
