@@ -238,7 +238,11 @@ constexpr int kScanBlock = DMC_SCAN_BLOCK;
 // compactly), with a margin on the needed count; k_remit counts the exact
 // first keys at or below each threshold and a round whose sampled threshold
 // admits too few is re-run with the exact histogram (overflow = 3).
-constexpr uint32_t kSample = 8;
+#ifndef DMC_SAMPLE
+#define DMC_SAMPLE 8
+#endif
+constexpr uint32_t kSample = DMC_SAMPLE;  // (a power of two)
+static_assert((kSample & (kSample - 1)) == 0, "kSample: a power of two");
 constexpr uint32_t kSampleMinN = 1u << 16;
 
 // k_remit's candidate test streams a 32-bit quantized first key per phase

@@ -19,6 +19,6 @@ for v in $VARIANTS; do
     echo "variant $v: decisions/bad_rounds $dec differ from the base's $base: wrong result, not timed"
     exit 1
   fi
-  python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); print('$v', d['ms_per_step'], {k: round(v*1e3,1) for k, v in d['stages_ms_per_step'].items()}, 'dec', d['engine_counters']['decisions'])"
+  python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); print('$v', d['ms_per_step'], {k: round(v*1e3,1) for k, v in d['stages_ms_per_step'].items()}, 'dec', d['engine_counters']['decisions'], 'retries', d['engine_counters']['sample_retries'])"
 done
 done
