@@ -335,6 +335,50 @@ __device__ __attribute__((always_inline)) inline void serve_publish(ServeIO* io,
   __hip_atomic_store(&io->done_seq, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One group's summary by waves 1-3 (192 lanes, their fronts kWaveSumBatch
+// per lane in flight): each wave reduces its share on the DPP network, the
+// last one to finish (an LDS ticket) combines the three into *sg_out and
+// sets *done -- no block barrier, so that wave 0 keeps polling and serving
+// adds meanwhile (a pull's deferred re-summary).
+constexpr int kWaveSumBatch = 6;  // (1024-slot groups: one batch)
+__device__ __attribute__((always_inline)) inline void waves_group_summary(
+    const Table& tb, uint32_t g, uint32_t gshift, StepRed* sg_out, StepRed* part,
+    uint32_t* ticket, uint32_t* done) {
+  constexpr uint32_t NL = kServeThreads - 64;
+  const uint32_t li = threadIdx.x - 64, lane = threadIdx.x & 63;
+  StepRed a;
+  stepred_clear(a);
+  const uint32_t s0 = g << gshift;
+  const uint32_t s1 = min(tb.n, s0 + (1u << gshift));
+  for (uint32_t b = s0 + li; b < s1; b += kWaveSumBatch * NL) {
+    ScanRec rs[kWaveSumBatch];
+#pragma unroll
+    for (int u = 0; u < kWaveSumBatch; ++u) {
+      const uint32_t s = b + u * NL;
+      if (s < s1) rs[u] = tb.sc[s];
+      else rs[u].count = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kWaveSumBatch; ++u) {
+      const ScanRec& sr = rs[u];
+      if (!sr.count) continue;
+      summary_add(a, sr, b + u * NL, (sr.flags & F_READY) != 0);
+    }
+  }
+  wave_stepred(a);
+  if (lane == 63) {
+    part[li >> 6] = a;
+    if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+        NL / 64 - 1) {
+      StepRed t = part[0];
+      for (uint32_t w = 1; w < NL / 64; ++w) stepred_combine(t, part[w]);
+      *sg_out = t;
+      *ticket = 0;
+      __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kServeThreads)
 k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_limit,
         uint32_t nregistered, unsigned long long* sched, uint64_t seq0,
@@ -348,74 +392,114 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
   __shared__ uint32_t s_life;
   __shared__ int32_t s_rc;
   __shared__ StepCtl s_c;
+  // a pull's last pop leaves its group's re-summary owed (s_pend): waves
+  // 1-3 run it while wave 0 polls and serves adds, which need no other group's
+  // summary; an add to that group waits for it (s_pdone), a pull for the
+  // block barrier
+  __shared__ uint32_t s_pend;
+  __shared__ uint32_t s_pdone;
+  __shared__ StepRed s_rpart[kServeThreads / 64 - 1];
+  __shared__ uint32_t s_rticket;
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) sg[i] = gs[i];
+  if (threadIdx.x == 0) {
+    s_pend = kNone;
+    s_pdone = 1;
+    s_rticket = 0;
+    s_life = 0;
+  }
   uint64_t seen = seq0;  // (wave 0's)
   const uint64_t born = wall_clock64();
   uint64_t c_seen = 0, c_read = 0;
   bool published = false;  // this command's answer is out (a pull's last decision)
+  uint32_t owed = kNone;   // (every thread's copy of the group this iteration left owed)
   __syncthreads();
   for (;;) {
-    if (threadIdx.x < 64) {  // wave 0 polls: the command line, one load per poll
+    const uint32_t pend = s_pend;
+    if (threadIdx.x < 64) {
+      // wave 0 polls: the command line, one load per poll; adds are served
+      // here, one after another, until a pull (or the end) comes
       const uint32_t lane = threadIdx.x;
-      const uint64_t t0 = wall_clock64();
       const uint64_t* line = reinterpret_cast<const uint64_t*>(io);
-      bool got = false;
-      uint64_t w = 0;
       for (;;) {
-        w = lane < kServeCmdWords ? sys_load_u64(line + lane) : 0;
-        const uint64_t sq = shfl_u64(w, 0);
-        if (sq != seen) {
-          const uint64_t opk = shfl_u64(w, 1);
-          if ((opk >> 16) == serve_check(sq, opk, shfl_u64(w, 2), shfl_u64(w, 3),
-                                         shfl_u64(w, 4), shfl_u64(w, 5), shfl_u64(w, 6))) {
-            seen = sq;
-            got = true;
-            break;
+        const uint64_t t0 = wall_clock64();
+        bool got = false;
+        uint64_t w = 0;
+        for (;;) {
+          w = lane < kServeCmdWords ? sys_load_u64(line + lane) : 0;
+          const uint64_t sq = shfl_u64(w, 0);
+          if (sq != seen) {
+            const uint64_t opk = shfl_u64(w, 1);
+            if ((opk >> 16) == serve_check(sq, opk, shfl_u64(w, 2), shfl_u64(w, 3),
+                                           shfl_u64(w, 4), shfl_u64(w, 5), shfl_u64(w, 6))) {
+              seen = sq;
+              got = true;
+              break;
+            }
           }
+          if (wall_clock64() - t0 > idle_ticks) break;
+          __builtin_amdgcn_s_sleep(1);
         }
-        if (wall_clock64() - t0 > idle_ticks) break;
-        __builtin_amdgcn_s_sleep(1);
+        c_seen = wall_clock64();
+        if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (lane < kServeCmdWords) s_cmd[lane] = got ? w : 0;
+        c_read = c_seen;
+        if (trace && lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t op = (uint32_t)(s_cmd[1] & 0xff);
+        if (op != kServeAdd) break;  // a pull, a stop or the idle end: the block's
+        // k_add_one: a request for a client with no request is its new
+        // front, inserted into the group's summary (exact: nothing leaves
+        // it); otherwise the fronts, and the summary, are unchanged
+        const uint64_t s_tick = tick++;  // (++tick, :918: the host's count follows)
+        uint32_t life = 0;
+        if (lane == 0) {
+          const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
+          const uint32_t s = s_reqp->slot;
+          if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
+            s_rc = DMC_ENOTREG;
+          } else {
+            if (pend != kNone && (s >> gshift) == pend) {
+              // (its group's owed re-summary reads the fronts: first)
+              while (!__hip_atomic_load(&s_pdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))
+                __builtin_amdgcn_s_sleep(1);
+            }
+            AddParams p{s_reqp, &s_rc, s_tick, 1, 0};
+            AddState st;
+            add_chain_slot(tb, p, s, 1, 0, nullptr, nullptr, ActBuf{}, &st);
+            if (st.front_set) {
+              const ScanRec sr = tb.sc[s];
+              summary_add(sg[s >> gshift], sr, s, (sr.flags & F_READY) != 0);
+            }
+          }
+          if (trace) {
+            io->phase[0] = wall_clock64();
+            io->phase[2] = io->phase[0];
+          }
+          io->rc = s_rc;
+          serve_publish(io, seen, c_seen, c_read, trace);
+          life = wall_clock64() - born > 5 * idle_ticks ? 1u : 0u;
+        }
+        if (__builtin_amdgcn_readfirstlane(life)) {  // lifetime over
+          if (lane < kServeCmdWords) s_cmd[lane] = 0;
+          break;
+        }
       }
-      c_seen = wall_clock64();
-      if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      if (lane < kServeCmdWords) s_cmd[lane] = got ? w : 0;
-      c_read = c_seen;
-      if (trace && lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
+    } else if (pend != kNone) {
+      waves_group_summary(tb, pend, gshift, &sg[pend], s_rpart, &s_rticket, &s_pdone);
     }
-    __syncthreads();
+    __syncthreads();  // (the owed re-summary is in)
+    if (threadIdx.x == 0) s_pend = kNone;  // (read again only after the next barriers)
+    owed = kNone;
     const uint32_t op = (uint32_t)(s_cmd[1] & 0xff);
-    if (op != kServeAdd && op != kServePull) break;
+    if (op != kServePull) break;
     const uint32_t s_k = (uint32_t)((s_cmd[1] >> 8) & 0xff);
     const double s_now = __builtin_bit_cast(double, s_cmd[2]);
     const uint64_t s_tick = tick;
-    const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
-    if (op == kServeAdd) ++tick;  // (++tick, :918: the host's count follows)
     const double now = s_now;
     published = false;
-    if (op == kServeAdd) {  // k_add_one
-      // a request for a client with no request is its new front: inserted
-      // into the group's summary (exact: nothing leaves it); otherwise the
-      // fronts, and the summary, are unchanged
-      if (threadIdx.x == 0) {
-        const uint32_t s = s_reqp->slot;
-        if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
-          s_rc = DMC_ENOTREG;
-        } else {
-          AddParams p{s_reqp, &s_rc, s_tick, 1, 0};
-          AddState st;
-          add_chain_slot(tb, p, s, 1, 0, nullptr, nullptr, ActBuf{}, &st);
-          if (st.front_set) {
-            const ScanRec sr = tb.sc[s];
-            summary_add(sg[s >> gshift], sr, s, (sr.flags & F_READY) != 0);
-          }
-        }
-        if (trace) {
-          io->phase[0] = wall_clock64();
-          io->phase[2] = io->phase[0];
-        }
-        io->rc = s_rc;
-      }
-    } else {
+    {
       uint32_t n = 0, nres = 0, nprio = 0;
       int32_t type = DMC_NEXT_RETURNING;
       double when = 0.0;
@@ -482,7 +566,6 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
           if (trace && n == 1) io->phase[1] = wall_clock64();
           if (n == s_k) {
             // the call's last decision: answer first, re-summarise after
-            // (the host's next command waits for this loop anyway)
             io->n = n;
             io->n_res = nres;
             io->n_prio = nprio;
@@ -494,8 +577,18 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         published = n == s_k;
         __syncthreads();
         const uint32_t g = c.slot >> gshift;
-        group_summary<false>(tb, g, gshift, now, sh);
-        if (threadIdx.x == 0) sg[g] = sh[kServeRes];
+        if (published) {
+          // the call's last pop: its group's re-summary is owed (waves
+          // 1-3, beside the next commands' polling)
+          owed = g;
+          if (threadIdx.x == 0) {
+            s_pend = g;
+            s_pdone = 0;
+          }
+        } else {
+          group_summary<false>(tb, g, gshift, now, sh);
+          if (threadIdx.x == 0) sg[g] = sh[kServeRes];
+        }
         if (trace && threadIdx.x == 0 && n == 1) io->phase[2] = wall_clock64();
         __syncthreads();
       }
@@ -514,6 +607,13 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
     }
     __syncthreads();
     if (s_life) break;  // lifetime over
+  }
+  // (a re-summary still owed: the lifetime ended right after a pull)
+  if (owed != kNone) {
+    const uint32_t g = owed;
+    group_summary<false>(tb, g, gshift, 0.0, sh);
+    if (threadIdx.x == 0) sg[g] = sh[kServeRes];
+    __syncthreads();
   }
   for (uint32_t i = threadIdx.x; i < G; i += kServeThreads) gs[i] = sg[i];
   __syncthreads();
