@@ -43,3 +43,28 @@ def test_facade_gpu_kernels():
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failures" in out.stdout
+
+
+def test_facade_client_id_types(tmp_path):
+    """the facade instantiates for client ids with and without std::hash
+    (the per-call lookup uses a hash index only when C is hashable; the
+    reference needs only operator<)"""
+    src = tmp_path / "ids.cc"
+    src.write_text(
+        '#include "dmclock_server.h"\n'
+        "struct NoHashClient {\n"
+        "  int v;\n"
+        "  bool operator<(const NoHashClient& o) const { return v < o.v; }\n"
+        "};\n"
+        "struct Req { int x; };\n"
+        "template class crimson::dmclock::PullPriorityQueue<NoHashClient, Req>;\n"
+        "template class crimson::dmclock::PushPriorityQueue<NoHashClient, Req>;\n"
+        "template class crimson::dmclock::PullPriorityQueue<int, Req>;\n"
+        "static_assert(!crimson::dmclock::detail::has_std_hash<NoHashClient>::value);\n"
+        "static_assert(crimson::dmclock::detail::has_std_hash<int>::value);\n")
+    root = os.path.dirname(HERE)
+    out = subprocess.run(["g++", "-std=c++17", "-fsyntax-only",
+                          "-I", os.path.join(root, "dmclock_amd", "include"),
+                          "-I", os.path.join(root, "include"), str(src)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
