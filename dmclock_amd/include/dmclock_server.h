@@ -120,12 +120,13 @@ namespace detail {
 inline void check(int rc, const char* what) {
   if (rc != DMC_OK) throw GpuError(what, rc);
 }
-// whether std::hash<T> is enabled (a disabled specialization is not
-// default-constructible)
+// whether T can key an unordered_map: std::hash<T> enabled (a disabled
+// specialization is not default-constructible) and T equality-comparable
 template <typename T, typename = void>
 struct has_std_hash : std::false_type {};
 template <typename T>
-struct has_std_hash<T, std::void_t<decltype(std::hash<T>{}(std::declval<const T&>()))>>
+struct has_std_hash<T, std::void_t<decltype(std::hash<T>{}(std::declval<const T&>())),
+                                   decltype(std::declval<const T&>() == std::declval<const T&>())>>
     : std::true_type {};
 }  // namespace detail
 
