@@ -983,16 +983,39 @@ __device__ inline SegMin block_seg_min(SegMin v, SegMin* wpart) {
 
 // the tile's activations: X, K, classification, the complex ones compacted
 // with the runs' minima before them
+// (its inputs gathered here, as k_act_inputs would, and stored for the
+// kernels after it: one launch and one level of loads fewer)
 __global__ void __launch_bounds__(kActThreads)
-k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
-           const double* apd, ActTiles tl) {
+k_act_keys(const AddParams* pblk, Table tb, ActBuf act, uint64_t* ax, double* ap, double* at,
+           double* apd, uint32_t* aslot, ActTiles tl) {
   __shared__ uint64_t wmin[kActThreads / 64];
   __shared__ SegMin wseg[kActThreads / 64];
   __shared__ uint32_t wcnt[kActThreads / 64];
   __shared__ uint64_t s_incl[kActThreads];
   const uint32_t m = act.dm ? *act.dm : act.m;
   const uint32_t t = blockIdx.x, j0 = t * kActTile;
-  if (j0 >= m || *act.anyhard) return;  // (anyhard: k_act_hard's batch)
+  if (j0 >= m) return;
+  // this activation's inputs (k_act_inputs' gather)
+  const uint32_t j = j0 + threadIdx.x;
+  const bool in = j < m;
+  uint64_t xj = kMaxKey;
+  double pj = 0.0, tj = 0.0, pdj = 0.0;
+  if (in) {
+    const AddParams p = *pblk;
+    const uint32_t q = act.idx[j];
+    const uint64_t a = act.pre[q], b = act.suf[p.n - 1 - q];
+    xj = a < b ? a : b;
+    const dmc_request& rq = p.reqs[q];
+    pj = act.actp[q];
+    tj = rq.time;
+    pdj = tb.rec[rq.slot].pd;
+    ax[j] = xj;
+    ap[j] = pj;
+    at[j] = tj;
+    aslot[j] = rq.slot;
+    apd[j] = pdj;
+  }
+  if (*act.anyhard) return;  // (anyhard: k_act_hard's batch, resolved by k_act_fixup)
   // the unchanged clients' minimum (every block; block 0 publishes it)
   uint64_t b = kMaxKey;
   for (uint32_t i = threadIdx.x; i < act.nparts; i += kActThreads)
@@ -1006,15 +1029,12 @@ k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
   }
   __syncthreads();
   const uint64_t base = s_base;
-  const uint32_t j = j0 + threadIdx.x;
-  const bool in = j < m;
   uint64_t K = kMaxKey;
   bool cx = false;
   if (in) {
-    const uint64_t X = ax[j] < base ? ax[j] : base;
-    const double p = ap[j], tt = at[j];
-    K = act_contrib(X, p, tt, apd[j], nullptr);
-    cx = !act_simple(X, p, tt);
+    const uint64_t X = xj < base ? xj : base;
+    K = act_contrib(X, pj, tj, pdj, nullptr);
+    cx = !act_simple(X, pj, tj);
     tl.K[j] = K;
   }
   const SegMin incl = block_seg_min(SegMin{cx ? 1u : 0u, cx ? kMaxKey : K}, wseg);
@@ -1032,10 +1052,10 @@ k_act_keys(ActBuf act, const uint64_t* ax, const double* ap, const double* at,
   const uint32_t o = t * kActItems;
   if (in && cx) {
     tl.sS[o + rank] = threadIdx.x ? s_incl[threadIdx.x - 1] : kMaxKey;
-    tl.sX[o + rank] = ax[j] < base ? ax[j] : base;
-    tl.sP[o + rank] = ap[j];
-    tl.sT[o + rank] = at[j];
-    tl.sPd0[o + rank] = apd[j];
+    tl.sX[o + rank] = xj < base ? xj : base;
+    tl.sP[o + rank] = pj;
+    tl.sT[o + rank] = tj;
+    tl.sPd0[o + rank] = pdj;
   }
   const uint32_t last = (m - j0 < kActTile ? m - j0 : kActTile) - 1;
   if (threadIdx.x == last) {
@@ -2742,12 +2762,15 @@ void act_hard_bufs(dmc_queue* q, ActBuf& act) {
 // device count act.dm, or act.m), resolved and committed (see k_act_keys)
 void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
   if (!n) return;
+  const AddParams* pblk = (const AddParams*)q->apblk;
   const ActHard hs{q->act_hmap, q->act_hlist, q->act_hval, q->act_hpd, q->act_nhard};
   const uint32_t T = (n + kActTile - 1) / kActTile;
   const uint64_t* ax = q->act_x;
   const double *ap = q->act_ip, *at = q->act_it;
   if (T > kActMaxTiles) {
     // (more than 2^20 activations in one batch: the one-block resolution)
+    hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream, pblk,
+                       q->tb, act, q->act_x, q->act_ip, q->act_it, q->act_ipd, q->act_islot);
     hipLaunchKernelGGL(k_act_hard, dim3(1), dim3(64), 0, q->stream, q->tb, act, ax, ap, at,
                        q->act_ipd, (const uint32_t*)q->act_islot, hs);
     hipLaunchKernelGGL(k_act_resolve, dim3(1), dim3(kActThreads), 0, q->stream, q->tb,
@@ -2757,8 +2780,8 @@ void act_resolve(dmc_queue* q, const ActBuf& act, uint32_t n) {
                        (const uint32_t*)q->act_islot);
     return;
   }
-  hipLaunchKernelGGL(k_act_keys, dim3(T), dim3(kActThreads), 0, q->stream, act, ax, ap, at,
-                     (const double*)q->act_ipd, q->atl);
+  hipLaunchKernelGGL(k_act_keys, dim3(T), dim3(kActThreads), 0, q->stream, pblk, q->tb, act,
+                     q->act_x, q->act_ip, q->act_it, q->act_ipd, q->act_islot, q->atl);
   if (q->debug && q->dbg_actseq)
     (void)hipMemsetAsync(q->dbg_actseq, 0, 48 * 8, q->stream);
   hipLaunchKernelGGL(k_act_seq, dim3(1), dim3(kActThreads), 0, q->stream, act, q->atl,
@@ -2841,10 +2864,7 @@ int add_act_batch(dmc_queue* q, const dmc_request* h_reqs, uint32_t n,
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
   act_scans(q, act, n, false);
-  hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(m, 1024)), dim3(kBlock), 0, q->stream,
-                     (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
-                     q->act_it, q->act_ipd, q->act_islot);
-  act_resolve(q, act, act.m);
+  act_resolve(q, act, act.m);  // (its first kernel gathers the inputs)
   pe(q);
   HIP_OK(hipGetLastError());
   // the pinned staging is reused by the next batch: wait for the copy
@@ -2883,12 +2903,13 @@ int add_act_batch_dev(dmc_queue* q, uint32_t n, const dmc_request* d_reqs,
   pe(q);
   pb(q, DMC_PROF_ACTIVATE);
   act_scans(q, act, n, true);
-  hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
-                     (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
-                     q->act_it, q->act_ipd, q->act_islot);
   const char* dump = q->debug ? getenv("DMC_DUMP_ACT") : nullptr;
   if (dump && q->act_dumps < 4) {
-    // debug: the resolve's inputs (tools/act_chain_study.py)
+    // debug: the resolve's inputs (tools/act_chain_study.py; k_act_keys
+    // gathers them again, the same values)
+    hipLaunchKernelGGL(k_act_inputs, dim3(grid_for(n, 1024)), dim3(kBlock), 0, q->stream,
+                       (const AddParams*)q->apblk, q->tb, act, q->act_x, q->act_ip,
+                       q->act_it, q->act_ipd, q->act_islot);
     HIP_OK(hipStreamSynchronize(q->stream));
     uint32_t m = 0;
     HIP_OK(hipMemcpy(&m, q->act_dm, 4, hipMemcpyDeviceToHost));
