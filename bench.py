@@ -76,6 +76,9 @@ def _stage_bytes(N, R, D, C, E, A, sampled=True):
         #   request the cold/new contributions and their two min-scans (4 x 8
         #   written + read); per activation its inputs and result (~56)
         "activate": 33 * N + 64 * R + 56 * A,
+        # k_chain_scan (a fused call's add chain beside the round's scan, one
+        #   launch): the two stages' bytes
+        "chain_scan": (46 if sampled else 62) * N + 278 * R,
     }
 
 
@@ -99,21 +102,40 @@ def roofline(args, prof, prof_steps, ctr, k, n_clients=None, n_adds=None,
     cand = [(ms, name) for ms, name in cand if name in model]
     if not cand:
         return None
+    # every stage's own roofline (algorithmic bytes per launch / mean launch)
+    per = {}
+    for ms_s, nm in cand:
+        c = prof[nm][0]
+        bl = model[nm] / (c / prof_steps)
+        a_s = ms_s / c / 1e3
+        per[nm] = {"bytes_per_launch": int(bl), "avg_launch_us": round(a_s * 1e6, 2),
+                   "launches_per_step": round(c / prof_steps, 2),
+                   "achieved": round(bl / a_s / 1e9, 1),
+                   "frac": round(bl / a_s / 1e9 / HBM_PEAK_GBS, 4)}
     ms, name = max(cand)
-    c = prof[name][0]
-    launches_per_step = c / prof_steps
-    per_launch = model[name] / launches_per_step
-    avg_s = ms / c / 1e3
-    achieved = per_launch / avg_s / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1),
+    r = per[name]
+    return {"bound": "hbm", "achieved": r["achieved"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac": r["frac"],
             "traffic": None, "kernel": name,
-            "bytes_per_launch": int(per_launch),
-            "avg_launch_us": round(avg_s * 1e6, 2),
+            "bytes_per_launch": r["bytes_per_launch"],
+            "avg_launch_us": r["avg_launch_us"],
             "counts_per_step": {"clients": N, "adds": R, "decisions": round(D, 1),
                                 "candidates": round(C, 1), "records": round(E, 1),
-                                "activations": A}}
+                                "activations": A},
+            "stages": per}
+
+
+def latest_traffic():
+    """the newest round's PMC traffic file, profiles/traffic_rNN.json"""
+    import glob
+    import re
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")):
+        m = re.fullmatch(r"traffic_r(\d+)\.json", os.path.basename(f))
+        if m and (best is None or int(m.group(1)) > best[0]):
+            best = (int(m.group(1)), f)
+    return best[1] if best else None
 
 
 def parse():
@@ -157,14 +179,24 @@ def parse():
                          "what the C++ facade uses); a PCIe-inclusive rate, "
                          "never the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--t0", type=float, default=None,
+                    help="time base of the arrivals in seconds (default 1.0; "
+                         "--heap-order: 1.7e9, get_time()'s epoch scale, where "
+                         "rounding makes equal tags)")
+    ap.add_argument("--heap-order", type=int, nargs="?", const=2, default=0,
+                    help="tie-exact dispatch (DMC_OPT_HEAP_ORDER = K, default 2): "
+                         "the reference's three K-ary heaps on the device, every "
+                         "add and pull in call order on one wave; the timed step "
+                         "is the same call.  No stage pass")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the second, stage-timed pass")
     ap.add_argument("--prof-steps", type=int, default=10,
                     help="steps of the stage-timed pass (eager launches with "
                          "HIP events between kernels; run after the timed "
                          "region, on the following batches)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles",
-                                                      "traffic_r03.json"))
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic file (tools/pmc_traffic.py) for roofline.traffic "
+                         "(default: the newest profiles/traffic_rNN.json)")
     ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5),
                     help="3: one server queue (default); 4: config 3 with "
                          "idle/active churn (do_clean idle marking before "
@@ -194,6 +226,10 @@ def parse():
     args = ap.parse_args()
     if args.config == 5 and "--clients" not in sys.argv:
         args.clients = 1 << 21  # 2M client slots per server table
+    if args.t0 is None:
+        args.t0 = 1.7e9 if args.heap_order else 1.0
+    if args.heap_order:
+        args.no_profile = True
     return args
 
 
@@ -207,7 +243,7 @@ def make_workload(args, seed):
         thr = rng.random(n) < 0.10
         tab.l = np.where(thr, rng.uniform(0.5, 1.5, n), tab.l)
     rate = 2.0 * n
-    pre = workloads.arrivals(rng, n, args.depth * n, 1.0, rate)
+    pre = workloads.arrivals(rng, n, args.depth * n, args.t0, rate)
     t = float(pre["time"][-1])
     steps = []
     handle = len(pre)
@@ -265,8 +301,9 @@ def cpu_baseline(args, tab, pre, steps, idle=None):
     timed over --cpu-steps steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    q = pyoracle.OracleQueue(track_ties=False)
+    q = pyoracle.OracleQueue(track_ties=bool(args.heap_order))
     prepare(q, args, tab, pre)
+    ties0 = q.ties if args.heap_order else 0
     k = args.pulls or args.batch
     ops = 0
     if idle is not None:
@@ -277,11 +314,14 @@ def cpu_baseline(args, tab, pre, steps, idle=None):
         d, res = q.pull_batch(float(reqs["time"][-1]), k)
         ops += len(reqs) + res.n_decisions
     dt = time.perf_counter() - t0
-    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
-                       f"the same {args.clients}-client queue after the same "
-                       f"pre-population and settle, {args.cpu_steps} steps of "
-                       f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+    out = {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+           "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
+                      f"the same {args.clients}-client queue after the same "
+                      f"pre-population and settle, {args.cpu_steps} steps of "
+                      f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+    if args.heap_order:  # (tie tracking is on: its cost is in the sample)
+        out["tied_decisions"] = {"setup": int(ties0), "sample": int(q.ties - ties0)}
+    return out
 
 
 def cpu_baseline_churn(args, q, steps, idle):
@@ -382,9 +422,11 @@ def main():
     tab, pre, steps, idle = make_workload(args, args.seed + rank)
     k = args.pulls or args.batch
     q = GpuQueue(max_clients=args.clients, ring_capacity=args.ring,
-                 max_batch=max(args.batch, k, 1 << 20), device=local)
+                 max_batch=max(args.batch, k, 1 << 20), device=local,
+                 heap_order=bool(args.heap_order), branching=args.heap_order or 2)
     settle = prepare(q, args, tab, pre)
-    pipelined = not (args.no_pipeline or args.host_api or args.separate_calls)
+    pipelined = not (args.no_pipeline or args.host_api or args.separate_calls or
+                     args.heap_order)
     if args.no_graphs or (pipelined and not args.graphs):
         from dmclock_amd._abi import OPT_GRAPHS
         q.set_option(OPT_GRAPHS, 0)
@@ -523,13 +565,15 @@ def main():
         # scripts/gpu_pmc.sh (tools/pmc_traffic.py), committed under
         # profiles/; null if that file is absent or lacks the stage
         traffic = None
-        if os.path.exists(args.traffic):
+        tfile = args.traffic or latest_traffic()
+        if tfile and os.path.exists(tfile):
             try:
-                t = json.load(open(args.traffic)).get(roof["kernel"])
+                t = json.load(open(tfile)).get(roof["kernel"])
                 traffic = t["hbm_bytes"] if t else None
             except Exception:
                 traffic = None
         roof["traffic"] = traffic
+        roof["traffic_file"] = os.path.relpath(tfile, ROOT) if tfile else None
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -552,13 +596,18 @@ def main():
         "data": "synthetic",
         "config": {"workload": (f"config3: single server queue, synthetic "
                                 f"{args.clients} clients mixed r/w/l, {args.batch} "
-                                f"adds + {k} pulls per step") if args.config == 3 else
+                                f"adds + {k} pulls per step"
+                                + (f", tie-exact heap order (DMC_OPT_HEAP_ORDER={args.heap_order})"
+                                   if args.heap_order else "")
+                                + (f", arrivals from t0 = {args.t0:g} s" if args.t0 != 1.0
+                                   else "")) if args.config == 3 else
                                (f"config4: config 3 ({args.clients} clients, "
                                 f"{args.batch} adds + {k} pulls per step) + "
                                 f"do_clean idle marking of {args.idle_frac:.0%} of "
                                 "the clients before each step (activations with the "
                                 "prop_delta reset) + 10% limit-throttled tenants"),
                    "clients": args.clients, "adds_per_step": args.batch,
+                   "heap_order": args.heap_order, "t0": args.t0,
                    "pulls_per_step": k, "prepopulated": len(pre),
                    "settle_pulls": settle,
                    "ring_capacity": args.ring,
@@ -580,16 +629,25 @@ def main():
         "priority_decisions": int(st.prop_sched_count - st_t0.prop_sched_count),
         "queued_after": int(st.requests),
         "roofline": roof,
+        "roofline_note": (None if not args.heap_order else
+                          "heap order: one wave's chain of dependent sift round trips "
+                          "(latency-bound, a few hundred bytes per operation): no HBM "
+                          "roofline applies"),
         "cpu_baseline": cpu,
         "stages_ms_per_step": {n: round(ms / max(prof_steps, 1), 4)
                                for n, (c, ms) in prof.items() if c},
         "stages_note": "stage times from a second pass of prof_steps steps "
-                       "launched eagerly on the engine's stream: one-kernel "
-                       "stages with HIP events recorded by the kernel's own "
-                       "dispatch (hipExtLaunchKernel: execution time, as "
-                       "rocprofv3 reports it), multi-kernel stages with "
-                       "event pairs; the timed region replays captured "
-                       "hipGraphs",
+                       "after the timed region, the same calls with the same "
+                       "kernels (fused, pipelined, launched eagerly: add_link, "
+                       "chain_scan, select, emit, rank, apply) behind a "
+                       "GPU-side gate: one-kernel stages timed by HIP events "
+                       "the kernel's own dispatch records "
+                       "(hipExtLaunchKernel: execution time, as rocprofv3 "
+                       "reports it), multi-kernel stages by event pairs; "
+                       + ("the timed region replays captured hipGraphs"
+                          if (not pipelined or args.graphs) and not args.no_graphs
+                          else "the timed region launches the same kernels "
+                               "eagerly, pipelined behind the previous call"),
         "prof_steps": prof_steps,
         "engine_counters": ctr_timed,
     }

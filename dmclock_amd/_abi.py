@@ -17,6 +17,8 @@ DMC_EBADTAG = -1001
 DMC_EBADPARAMS = -1002
 DMC_EQUEUEFULL = -1004
 DMC_ENOTREG = -1005
+DMC_ENOTRUN = -1006  # pipelined: the previous call failed, this one was not executed
+ABI_VERSION = 5  # include/dmclock_gpu.h DMC_ABI_VERSION
 
 # AtLimit (dmclock_server.h:74-84)
 AT_LIMIT_WAIT = 0
@@ -37,7 +39,7 @@ OPT_SAMPLE = 5
 OPT_SINGLE_OP = 6
 OPT_FAIL_ALLOC = 7  # test hook: fail the next n device allocations
 OPT_BREAK_ROUNDS = 8
-OPT_FAULT = 9
+OPT_FAULT = 13
 OPT_HEAP_ORDER = 11
 OPT_PIPELINE = 12
 OPT_SERVE = 10

@@ -15,11 +15,10 @@ DEPS = SOURCES + sorted(
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                # exact IEEE double tag arithmetic: no FMA contraction
                "-ffp-contract=off",
-               # (the ScanRec cursor word is stored and loaded through a
-               # uint64_t pointer beside its byte fields: with type-based
-               # alias analysis a later member load could be moved above
-               # the word's store)
-               "-fno-strict-aliasing", "-Wall", "-Wno-unused-function"]
+               # (strict aliasing holds: every whole-word access to memory
+               # declared with other types goes through ld_as / st_as,
+               # csrc/dmc_device.h)
+               "-Wall", "-Wno-unused-function"]
 
 
 def up_to_date():

@@ -282,8 +282,8 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
     tR = tf->gr[ts.c];
   }
   // the ScanRec's cursor word: head, count, flags and the batch count
-  uint64_t* cw = reinterpret_cast<uint64_t*>(&tb.sc[s].head);
-  const uint64_t cur = *cw;
+  ScanRec* const cw = tb.sc + s;
+  const uint64_t cur = cursor_load(cw);
   if (counted) m = (uint32_t)(cur >> 32);
   AddState st;
   st.prev = Tag3{tb.rec[s].prev_r, tb.rec[s].prev_p, tb.rec[s].prev_l, tb.rec[s].prev_arr};
@@ -305,8 +305,8 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   // and after its requests (see ActBuf)
   // the cursor word as stored back: the batch count cleared for the next batch
   auto store_cursor = [&] {
-    *cw = (uint64_t)(st.head & 0xffu) | ((uint64_t)(st.count & 0xffu) << 8) |
-          ((uint64_t)st.flags << 16) | (cur & 0xff000000ull);
+    cursor_store(cw, (uint64_t)(st.head & 0xffu) | ((uint64_t)(st.count & 0xffu) << 8) |
+                         ((uint64_t)st.flags << 16) | (cur & 0xff000000ull));
   };
   if (counted && !(st.flags & F_REG)) {
     store_cursor();  // (unchanged; the batch count cleared)

@@ -116,6 +116,35 @@ __host__ __device__ inline double bitsd(uint64_t u) {
   __builtin_memcpy(&x, &u, 8);
   return x;
 }
+// Whole-word access to memory declared with other types (a vector load of a
+// scalar column, a record's words, the ScanRec cursor): through
+// __builtin_memcpy, whose byte access may alias any type, so type-based
+// alias analysis can never move it across the members' own loads and stores
+// (an access through a reinterpret_cast pointer of another type could be,
+// and once was: DESIGN.md section 10).  p must be aligned for T; the copy
+// compiles to one access of sizeof(T) bytes.
+template <typename T>
+__device__ inline T ld_as(const void* p) {
+  T v;
+  __builtin_memcpy(&v, __builtin_assume_aligned(p, alignof(T)), sizeof(T));
+  return v;
+}
+template <typename T>
+__device__ inline void st_as(void* p, const T& v) {
+  __builtin_memcpy(__builtin_assume_aligned(p, alignof(T)), &v, sizeof(T));
+}
+
+// The ScanRec cursor word -- head | count << 8 | flags << 16 | pad0 << 24 |
+// nadd << 32 -- read and written whole (8-aligned at offset 24).
+__device__ inline uint64_t cursor_load(const ScanRec* r) {
+  return ld_as<uint64_t>(reinterpret_cast<const char*>(r) + offsetof(ScanRec, head));
+}
+__device__ inline void cursor_store(ScanRec* r, uint64_t w) {
+  st_as<uint64_t>(reinterpret_cast<char*>(r) + offsetof(ScanRec, head), w);
+}
+static_assert(offsetof(ScanRec, head) == 24 && offsetof(ScanRec, nadd) == 28,
+              "the cursor word is ScanRec's last 8 bytes");
+
 // order-preserving map double -> u64 (ascending)
 __host__ __device__ inline uint64_t okey(double x) {
   uint64_t u = dbits(x);
@@ -266,16 +295,17 @@ __device__ inline RingView stage_ring(const Table& tb, uint32_t s, uint32_t h,
   uint4 x[K][4];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    const uint4* src = reinterpret_cast<const uint4*>(v.g + ((h + j) & v.qmask));
+    const char* src = reinterpret_cast<const char*>(v.g + ((h + j) & v.qmask));
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[j][k] = (uint32_t)j < ns ? src[k] : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < 4; ++k)
+      x[j][k] = (uint32_t)j < ns ? ld_as<uint4>(src + 16 * k) : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    uint4* dst = reinterpret_cast<uint4*>(st + j);
+    char* dst = reinterpret_cast<char*>(st + j);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if ((uint32_t)j < ns) dst[k] = x[j][k];
+      if ((uint32_t)j < ns) st_as<uint4>(dst + 16 * k, x[j][k]);
   }
   v.st = st;
   v.ns = ns;

@@ -1552,10 +1552,10 @@ __device__ inline void step_scan_body(const Table& tb, double now, StepRed* part
     }
     if (ATOMIC) {
       static_assert(sizeof(StepRed) % 8 == 0, "StepRed is stored in 8-byte words");
-      const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&o);
       unsigned long long* dst = reinterpret_cast<unsigned long long*>(part + blockIdx.x);
 #pragma unroll
-      for (int i = 0; i < (int)(sizeof(StepRed) / 8); ++i) atomicExch(dst + i, src[i]);
+      for (int i = 0; i < (int)(sizeof(StepRed) / 8); ++i)
+        atomicExch(dst + i, ld_as<unsigned long long>(reinterpret_cast<const char*>(&o) + 8 * i));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       part[blockIdx.x] = o;
@@ -2055,6 +2055,7 @@ struct dmc_queue {
            *act_hlist = nullptr, *act_anyhard = nullptr;
   double *act_hev_p = nullptr, *act_hval = nullptr, *act_hpd = nullptr;
   uint64_t* h_nhard = nullptr;   // (host-mapped: read by dmc_queue_counters)
+  uint64_t nhard_base = 0;       // its value at the last counters reset
   uint64_t* act_nhard = nullptr;  // its device pointer
   bool act_pending = false;
   int act_dumps = 0;             // debug: resolve inputs dumped (DMC_DUMP_ACT)
@@ -2266,7 +2267,7 @@ namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
     "add_link", "add_chain", "activate", "scan", "select", "emit", "sort",
-    "rank", "apply", "step", "future", "cand"};
+    "rank", "apply", "step", "future", "cand", "chain_scan"};
 
 // Profiling launches eagerly; a short GPU-side delay queued ahead of a
 // profiled call lets the host enqueue all of the call's kernels before the
@@ -3301,23 +3302,22 @@ constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 #define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
 #endif
 bool overlap_ok(const dmc_queue* q, uint32_t n) {
-  return DMC_OVERLAP && !q->use_graphs && !q->prof_on &&
-         (n + kBlock - 1) / kBlock <= kFixPartsMax;
+  return DMC_OVERLAP && !q->use_graphs && (n + kBlock - 1) / kBlock <= kFixPartsMax;
 }
 void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
   const bool sampled = use_sample(q, false);
   const Table& tb = q->tb;
   ap.epoch = cp.epoch;
   const uint32_t g = (ap.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_add_link, dim3(g), dim3(kBlock), 0, q->stream, ap, tb, q->abuf,
-                     q->apos, q->aslot, q->apblk, ActBuf{});
+  prof_gate(q);
+  klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, tb, q->abuf,
+          q->apos, q->aslot, q->apblk, ActBuf{});
   const uint32_t nS = (tb.n + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
-  hipLaunchKernelGGL(k_chain_scan, dim3(g + nS), dim3(kBlock), 0, q->stream, tb,
-                     (const AddParams*)q->apblk, (const uint32_t*)q->abuf,
-                     (const uint32_t*)q->apos, (const uint32_t*)q->aslot, g, nS,
-                     sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
-                     q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
-                     sampled ? q->skp : nullptr, q->k32, q->hist);
+  klaunch(q, DMC_PROF_CHAIN_SCAN, k_chain_scan, dim3(g + nS), dim3(kBlock), 0, tb,
+          (const AddParams*)q->apblk, (const uint32_t*)q->abuf, (const uint32_t*)q->apos,
+          (const uint32_t*)q->aslot, g, nS, sampled ? nullptr : q->keyr,
+          sampled ? nullptr : q->keyp, q->meta, q->rparts, q->rd, cp,
+          sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32, q->hist);
   enqueue_round(q, cp, false, nS + g);
 }
 
@@ -3826,7 +3826,7 @@ int heap_enable(dmc_queue* q, uint32_t k) {
   if (q->n_registered || k < 2 || k > 64) return DMC_EINVAL;
   if (q->heap) return DMC_OK;
   const size_t N = q->p.max_clients;
-  DALLOC(q, &q->hd.hp, 3 * 4 * N);
+  DALLOC(q, &q->hd.ent, 3 * sizeof(HEnt) * N);
   DALLOC(q, &q->hd.hix, 3 * 4 * N);
   DALLOC(q, &q->hd.cnt, 4 * 4);
   HIP_OK(hipMemsetAsync(q->hd.cnt, 0, 16, q->stream));
@@ -4124,7 +4124,7 @@ int dmc_queue_destroy(dmc_queue* q) {
   dfree(q->act_hev_q); dfree(q->act_hard); dfree(q->act_hmap); dfree(q->act_hlist);
   dfree(q->act_anyhard); dfree(q->act_hev_p); dfree(q->act_hval); dfree(q->act_hpd);
   if (q->h_nhard) (void)hipHostFree(q->h_nhard);
-  dfree(q->hd.hp); dfree(q->hd.hix); dfree(q->hd.cnt); dfree(q->d_hres);
+  dfree(q->hd.ent); dfree(q->hd.hix); dfree(q->hd.cnt); dfree(q->d_hres);
   if (q->h_hres) (void)hipHostFree(q->h_hres);
   if (q->h_actm) (void)hipHostFree(q->h_actm);
   dfree(q->d_mark);
@@ -4196,9 +4196,11 @@ int dmc_client_register_batch(dmc_queue* q, uint32_t n, const uint32_t* slots,
   HIP_OK(hipMemcpyAsync(d_l, li.data(), 8ull * n, hipMemcpyHostToDevice, q->stream));
   hipLaunchKernelGGL(k_register, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      q->stream, q->tb, q->binfo, n, d_slots, d_r, d_w, d_l, active, q->tick);
-  if (q->heap)  // three pushes per client, in the given order (:925-931)
-    hipLaunchKernelGGL(k_heap_push, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd,
-                       (const uint32_t*)d_slots, n);
+  if (q->heap) {  // three pushes per client, in the given order (:925-931)
+    hipLaunchKernelGGL(k_heap_push, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, q->stream,
+                       q->tb, q->hd, (const uint32_t*)d_slots, n);
+    hipLaunchKernelGGL(k_heap_count_add, dim3(1), dim3(64), 0, q->stream, q->hd, n);
+  }
   HIP_OK(hipStreamSynchronize(q->stream));
   dfree(d_slots); dfree(d_r); dfree(d_w); dfree(d_l);
   for (uint32_t i = 0; i < n; ++i) {
@@ -4402,13 +4404,16 @@ __global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
 // order -- each modified client filtered, then adjusted in the three heaps,
 // before the next one is filtered (a later client's adjust must see the
 // earlier clients' new fronts and the later ones' old ones)
-__global__ void k_heap_filter(Table tb, HeapDev hd, uint32_t n, const uint32_t* slots,
-                              const uint32_t* offs, const uint8_t* keep) {
-  if (threadIdx.x) return;
-  Heaps H(tb, hd);
+__global__ void __launch_bounds__(64) k_heap_filter(Table tb, HeapDev hd, uint32_t n,
+                                                    const uint32_t* slots, const uint32_t* offs,
+                                                    const uint8_t* keep) {
+  WHeaps W(tb, hd);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t s = slots[i];
-    if (list_filter_slot(tb, s, keep + offs[s])) H.adjust3(s);
+    uint32_t mod = 0;
+    if (W.lane == 0) mod = list_filter_slot(tb, s, keep + offs[s]) ? 1u : 0u;
+    wave_sync();
+    if (uread(mod, 0)) W.adjust3(s);
   }
 }
 
@@ -4777,7 +4782,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       // eagerly, still queued behind the previous call's)
       const bool fuse = n && k && !maybe_idle(q) && q->n_registered > 0 && k > q->small_k &&
                         !q->force_radix && q->radix_batches == 0 && k <= kBinRankMaxK &&
-                        (q->use_graphs || q->pipeline) && !q->prof_on;
+                        (q->use_graphs || q->pipeline);
       if (!fuse) {
         if (int rc = settle_pending(q)) return rc;
         break;  // the two calls
@@ -4786,8 +4791,17 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       if (!rc) rc = ensure_brec(q);
       if (rc) return rc;
       AddParams ap{d_reqs, d_rc_out, q->tick, n, 0};
-      // (k_chain_scan: the batch's epoch, never 0)
-      const uint32_t epoch = overlap_ok(q, n) ? (++q->epoch ? q->epoch : ++q->epoch) : 0u;
+      // (k_chain_scan: the batch's epoch, never 0; when the counter wraps the
+      // stamps are cleared first, so that no slot keeps a stamp equal to a
+      // later batch's epoch)
+      uint32_t epoch = 0;
+      if (overlap_ok(q, n)) {
+        if (++q->epoch == 0) {
+          HIP_OK(hipMemsetAsync(q->tb.touch, 0, 4ull * q->p.max_clients, q->stream));
+          q->epoch = 1;
+        }
+        epoch = q->epoch;
+      }
       CallParams cp{k,     0,   now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault,
                     epoch, q->pipeline ? q->gate : nullptr};
       auto enqueue = [&] {
@@ -4825,7 +4839,16 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       if (q->pipeline) {
         // the previous call, finished now that this one is queued behind it
         bool clean = true;
-        if ((rc = settle_pending(q, &clean))) return rc;
+        if ((rc = settle_pending(q, &clean))) {
+          if (clean) return rc;  // (the device failed: this call's state is unknown)
+          // the previous call failed after shutting the gate: this call's
+          // graph, queued behind it, did nothing -- it was not executed
+          // (its statuses, decisions and result untouched), which
+          // DMC_ENOTRUN tells the caller; the gate is open again
+          q->tick -= n;
+          --q->ctr.fused_calls;
+          return DMC_ENOTRUN;
+        }
         if (!clean) {
           // it needed the host: the graph just queued found the gate shut
           // and did nothing -- launched again, behind the previous call's
@@ -5483,6 +5506,8 @@ int dmc_queue_set_option(dmc_queue* q, int option, int64_t value) {
       q->pipeline = value != 0;
       q->tb.gate = q->pipeline ? q->gate : nullptr;
       return DMC_OK;
+    case 9:  // (retired: round 3's DMC_OPT_PREDICT; DMC_ABI_VERSION 5)
+      return DMC_EINVAL;
     case DMC_OPT_FAULT:
       if (value < 0) return DMC_EINVAL;
       q->fault = (uint32_t)value;
@@ -5505,15 +5530,27 @@ int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset) {
   if (!q || !out) return DMC_EINVAL;
   QueueLock g(q);
   if (g.rc) return g.rc;
-  // (k_act_hard's count, host-mapped: current once the adds have completed)
-  if (q->h_nhard) q->ctr.act_seq_batches = *(volatile uint64_t*)q->h_nhard;
+  // (k_act_hard's count, host-mapped: current once the adds have completed;
+  // the device owns the word, a reset moves the host's baseline)
+  const uint64_t nhard = q->h_nhard ? *(volatile uint64_t*)q->h_nhard : 0;
+  q->ctr.act_seq_batches = nhard - q->nhard_base;
   *out = q->ctr;
   if (reset) {
     q->ctr = dmc_counters{};
-    if (q->h_nhard) *(volatile uint64_t*)q->h_nhard = 0;
+    q->nhard_base = nhard;
   }
   return DMC_OK;
 }
+
+int dmc_queue_counters_sized(dmc_queue* q, void* out, uint64_t size, int reset) {
+  if (!q || !out) return DMC_EINVAL;
+  dmc_counters c{};
+  if (int rc = dmc_queue_counters(q, &c, reset)) return rc;
+  std::memcpy(out, &c, size < sizeof(c) ? (size_t)size : sizeof(c));
+  return DMC_OK;
+}
+
+int dmc_abi_version(void) { return DMC_ABI_VERSION; }
 
 int dmc_profile_enable(dmc_queue* q, int on) {
   if (!q) return DMC_EINVAL;

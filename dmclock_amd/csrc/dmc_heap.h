@@ -10,13 +10,27 @@
 // (support/src/indirect_intrusive_heap.h:240-564; comparators
 // src/dmclock_server.h:722-757).  No client attribute predicts it, so a
 // caller that needs the reference's exact dispatch sequence on tie-heavy
-// traces (closed loops of identical clients, config 2 without jitter) turns
-// this mode on: every add and pull then runs in call order on one workgroup
-// of the device, with the heaps as arrays of slots plus each slot's index in
-// each heap, and the same per-client state (ScanRec / ClientRec / ring) and
-// tag arithmetic as every other path.  It trades the rounds' throughput for
-// the heap's sequential semantics; the heaps' top decides, exactly as
-// do_next_request does (:1115-1186).
+// traces turns this mode on: every add and pull then runs in call order on
+// one wave of the device.
+//
+// Layout (per heap h = resv, limit, ready): `ent[h][i]`, the heap array of
+// 16-byte entries {ordered key, class, slot} -- the client's comparison key
+// kept inline, so a compare needs no load of the client's record -- and
+// `hix[h][slot]`, each slot's index (IndIntruHeap's intrusive index).  An
+// entry is a pure function of the slot's ScanRec (hent): whenever a kernel
+// here changes a ScanRec it rewrites the slot's three entries, sifted or in
+// place, before anything compares against them, so every comparison sees
+// what the reference's comparator would read from the client record.
+//
+// Sifts are wave-parallel but make exactly the reference's moves.  A
+// sift_down loads the whole subtree of the next D levels below the moving
+// element at once (62 entries for K = 2: one lane each) and resolves the
+// path in registers, IndIntruHeap's rule at each level (the first smallest
+// child, moved up iff strictly less, :479-548); a sift_up loads every
+// ancestor at once and moves up while strictly less (:462-474); sift
+// (:550-564) loads the ancestors and the first subtree together and picks
+// the direction from the parent.  One dependent memory round trip per D
+// levels instead of two per level.
 //
 // Heap order per operation (what the reference calls, in its order):
 //   register      resv.push, limit.push, ready.push            (:925-931)
@@ -39,159 +53,360 @@
 
 enum : int { kHResv = 0, kHLim = 1, kHReady = 2 };
 
+// A heap entry: ClientCompare's order (:722-757) as (cls, key) ascending.
+//   resv:  cls 0 = has a request, key r
+//   limit: cls 0 = has a request and not ready, 1 = ready (ReadyOption::lowers), key l
+//   ready: cls 0 = has a request and ready, 1 = not ready (raises), key p + prop_delta
+//   no request: cls 3, key 0 (such clients compare equal: neither is less)
+// key = okey(v) with -0.0 read as +0.0 (the comparator's `<` does not order
+// them).  Tags are never NaN (make_tag refuses none of them; a NaN arrival
+// time is outside the reference's contract).
+struct alignas(16) HEnt {
+  uint64_t key;
+  uint32_t cls;
+  uint32_t slot;
+};
+static_assert(sizeof(HEnt) == 16, "HEnt must be 16 bytes");
+constexpr uint32_t kClsNone = 3;
+
 struct HeapDev {
-  uint32_t* hp;   // [3][n] heap arrays (slots)
+  HEnt* ent;      // [3][n] heap arrays
   uint32_t* hix;  // [3][n] each slot's index in each heap
   uint32_t* cnt;  // [3] heap sizes
   uint32_t n, k;  // capacity, branching (IndIntruHeap's K)
 };
 
-// ClientCompare (:722-757): clients with a request precede those without;
-// resv by r; limit: not-ready first (ReadyOption::lowers), then l; ready:
-// ready first (raises), then p + prop_delta (the cached pk, the same double
-// add); strict less.
-__device__ inline bool heap_less(const Table& tb, int h, uint32_t a, uint32_t b) {
-  const ScanRec ra = tb.sc[a], rb = tb.sc[b];
-  if (!ra.count) return false;
-  if (!rb.count) return true;
-  if (h == kHResv) return ra.r < rb.r;
-  const bool rda = (ra.flags & F_READY) != 0, rdb = (rb.flags & F_READY) != 0;
-  if (h == kHLim) return rda == rdb ? ra.l < rb.l : rdb;
-  return rda == rdb ? ra.pk < rb.pk : rda;
+__device__ inline uint64_t okey0(double v) { return okey(v == 0.0 ? 0.0 : v); }
+__device__ inline double hval(const HEnt& e) { return from_okey(e.key); }
+
+__device__ inline HEnt hent(int h, const ScanRec& r, uint32_t s) {
+  HEnt e;
+  e.slot = s;
+  if (!r.count) {
+    e.key = 0;
+    e.cls = kClsNone;
+    return e;
+  }
+  const bool rdy = (r.flags & F_READY) != 0;
+  if (h == kHResv) {
+    e.key = okey0(r.r);
+    e.cls = 0;
+  } else if (h == kHLim) {
+    e.key = okey0(r.l);
+    e.cls = rdy ? 1u : 0u;
+  } else {
+    e.key = okey0(r.pk);
+    e.cls = rdy ? 0u : 1u;
+  }
+  return e;
 }
 
-// One heap, IndIntruHeap's algorithms (indirect_intrusive_heap.h): sift_up
-// moves only on strict less (:462-474); K == 2 sift_down takes the left child
-// unless the right one is strictly smaller (:514-548), K > 2 the first
-// smallest child (:479-510); sift picks the direction (:550-564); remove
-// swaps in the last element and sifts with the count already reduced, the
-// removed element still in the array (:433-445).
-struct HeapRef {
-  const Table& tb;
-  int h;
-  uint32_t* a;  // the heap array
-  uint32_t* x;  // slot -> index
-  uint32_t* cnt;
-  uint32_t k;
-  __device__ HeapRef(const Table& t, const HeapDev& d, int hh)
-      : tb(t), h(hh), a(d.hp + (size_t)hh * d.n), x(d.hix + (size_t)hh * d.n),
-        cnt(d.cnt + hh), k(d.k) {}
-  __device__ bool less(uint32_t i, uint32_t j) const { return heap_less(tb, h, a[i], a[j]); }
-  __device__ void swap(uint32_t i, uint32_t j) {
-    const uint32_t si = a[i], sj = a[j];
-    a[i] = sj;
-    a[j] = si;
-    x[sj] = i;
-    x[si] = j;
-  }
-  __device__ void sift_up(uint32_t i) {
-    while (i > 0) {
-      const uint32_t p = (i - 1) / k;
-      if (!less(i, p)) break;
-      swap(i, p);
-      i = p;
+// strict less (ClientCompare)
+__device__ inline bool hlt(const HEnt& a, const HEnt& b) {
+  return a.cls < b.cls || (a.cls == b.cls && a.key < b.key);
+}
+
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// one lane's entry, wave-uniform
+__device__ inline HEnt hread(const HEnt& e, uint32_t lane) {
+  HEnt o;
+  const uint32_t lo = (uint32_t)e.key, hi = (uint32_t)(e.key >> 32);
+  o.key = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, (int)lane) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)lane) << 32);
+  o.cls = (uint32_t)__builtin_amdgcn_readlane((int)e.cls, (int)lane);
+  o.slot = (uint32_t)__builtin_amdgcn_readlane((int)e.slot, (int)lane);
+  return o;
+}
+__device__ inline uint32_t uread(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+__device__ inline double dread(double v, uint32_t lane) {
+  const uint64_t u = dbits(v);
+  return bitsd((uint64_t)uread((uint32_t)u, lane) | ((uint64_t)uread((uint32_t)(u >> 32), lane) << 32));
+}
+// lane 0's stores before the wave's later loads (same wave, other lanes)
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One heap of IndIntruHeap's algorithms, driven by all 64 lanes of a wave
+// with uniform arguments; every function returns the moving element's final
+// index.  Only lanes' own loads and stores differ.
+struct WHeap {
+  HEnt* a;        // the heap array
+  uint32_t* x;    // slot -> index
+  uint32_t k;     // branching
+  uint32_t lane;
+
+  __device__ void put(uint32_t i, const HEnt& e) const {  // (uniform: lane 0 stores)
+    if (lane == 0) {
+      a[i] = e;
+      x[e.slot] = i;
     }
   }
-  __device__ void sift_down(uint32_t i, uint32_t n) {
-    if (i >= n) return;
-    if (k == 2) {
-      for (;;) {
-        const uint32_t li = 2 * i + 1, ri = li + 1;
-        if (li >= n) break;
-        if (less(li, i)) {
-          if (ri < n && less(ri, li)) {
-            swap(i, ri);
-            i = ri;
-          } else {
-            swap(i, li);
-            i = li;
-          }
-        } else if (ri < n && less(ri, i)) {
-          swap(i, ri);
-          i = ri;
-        } else {
-          break;
+
+  // lanes [base, 64) as the levels 1..D below a root: lane -> (level, offset)
+  // and the node's index from the root's; D = the levels that fit
+  struct Sub {
+    uint32_t lv, off, D;
+    uint64_t pw, g;  // K^lv, 1 + K + ... + K^(lv-1)
+  };
+  __device__ Sub layout(uint32_t base) const {
+    Sub L{0, 0, 0, 1, 0};
+    uint32_t avail = lane >= base ? 64u : 0u;
+    // D: levels whose lanes all fit in [base, 64)
+    uint64_t pw = k, used = 0, g = 1;
+    for (uint32_t l = 1; l <= 32; ++l) {
+      if (used + pw > 64 - base) break;
+      L.D = l;
+      if (avail && lane - base >= used && lane - base < used + pw) {
+        L.lv = l;
+        L.off = lane - base - (uint32_t)used;
+        L.pw = pw;
+        L.g = g;
+      }
+      used += pw;
+      g += pw;
+      pw *= k;
+    }
+    return L;
+  }
+  // first lane of level l's block (levels 1..D, from `base`)
+  __device__ uint32_t level_lane(uint32_t base, uint32_t l) const {
+    uint32_t u = 0;
+    uint64_t pw = k;
+    for (uint32_t t = 1; t < l; ++t) {
+      u += (uint32_t)pw;
+      pw *= k;
+    }
+    return base + u;
+  }
+
+  // the subtree below root r (this lane's node, if any and < n)
+  __device__ HEnt sub_load(const Sub& L, uint32_t r, uint32_t n, uint32_t* idx) const {
+    HEnt e{~0ull, kClsNone + 1, 0};
+    *idx = 0xffffffffu;
+    if (L.lv) {
+      const uint64_t i = L.pw * (uint64_t)r + L.g + L.off;
+      if (i < n) {
+        *idx = (uint32_t)i;
+        e = a[i];
+      }
+    }
+    return e;
+  }
+
+  // sift_down of X from i over the loaded subtree (lanes [base, 64), D
+  // levels): IndIntruHeap's moves; the moved lanes store themselves one
+  // level up.  Returns true when X went below the subtree's last level
+  // (*i is then the node to continue from).
+  __device__ bool down_sub(const Sub& L, uint32_t base, const HEnt& e, uint32_t eidx, uint32_t n,
+                           const HEnt& X, uint32_t* i) const {
+    uint32_t c = *i, co = 0;
+    uint32_t tgt = 0xffffffffu;
+    bool cont = true;
+    for (uint32_t l = 0; l < L.D; ++l) {
+      const uint64_t li = (uint64_t)k * c + 1;
+      if (li >= n) {
+        cont = false;
+        break;
+      }
+      const uint32_t nc = (uint32_t)min((uint64_t)k, n - li);
+      const uint32_t l0 = level_lane(base, l + 1) + co * k;
+      uint32_t mj = 0;
+      HEnt mb = hread(e, l0);
+      for (uint32_t j = 1; j < nc; ++j) {
+        const HEnt cj = hread(e, l0 + j);
+        if (hlt(cj, mb)) {
+          mb = cj;
+          mj = j;
         }
       }
-      return;
+      if (!hlt(mb, X)) {
+        cont = false;
+        break;
+      }
+      if (lane == l0 + mj) tgt = c;
+      c = (uint32_t)li + mj;
+      co = co * k + mj;
     }
-    for (;;) {
-      const uint32_t li = k * i + 1;
-      if (li >= n) break;
-      const uint32_t ri = min(k * i + k, n - 1);
-      uint32_t mi = li;
-      for (uint32_t c = li + 1; c <= ri; ++c)
-        if (less(c, mi)) mi = c;
-      if (!less(mi, i)) break;
-      swap(i, mi);
-      i = mi;
+    if (tgt != 0xffffffffu) {
+      a[tgt] = e;
+      x[e.slot] = tgt;
     }
+    (void)eidx;
+    *i = c;
+    return cont && L.D > 0;
   }
-  __device__ void sift(uint32_t i, uint32_t n) {
-    if (i == 0) sift_down(i, n);
-    else if (less(i, (i - 1) / k)) sift_up(i);
-    else sift_down(i, n);
+
+  // sift_down (:479-548) of X from i, n = the count it sees
+  __device__ uint32_t sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (i < n) {
+      const Sub L = layout(0);
+      for (;;) {
+        uint32_t eidx;
+        const HEnt e = sub_load(L, i, n, &eidx);
+        if (!down_sub(L, 0, e, eidx, n, X, &i)) break;
+      }
+    }
+    put(i, X);
+    return i;
   }
-  __device__ void push(uint32_t s) {
-    const uint32_t i = *cnt;
-    a[i] = s;
-    x[s] = i;
-    *cnt = i + 1;
-    sift_up(i);
+
+  // ancestor t + 1 of i (lanes t < depth): index, and the depth of i
+  __device__ uint32_t ancestors(uint32_t i, uint32_t* anc) const {
+    uint32_t d = 0, p = i, my = 0;
+    while (p > 0) {
+      p = k == 2 ? (p - 1) >> 1 : (p - 1) / k;
+      if (lane == d) my = p;
+      ++d;
+    }
+    *anc = my;
+    return d;
   }
-  __device__ void remove_slot(uint32_t s) {
-    const uint32_t i = x[s], last = *cnt - 1;
-    swap(i, last);
-    sift(i, last);
-    *cnt = last;
+
+  // sift_up (:462-474) of X from i over the loaded ancestors (lane t holds
+  // ancestor t + 1, t < d): X passes the leading run of ancestors it is
+  // strictly less than, each moving down one node of the path
+  __device__ uint32_t up_anc(uint32_t i, const HEnt& X, uint32_t d, uint32_t anc,
+                             const HEnt& ae) const {
+    const bool lt = lane < d && hlt(X, ae);
+    const uint64_t bal = __ballot(lt);
+    const uint32_t m = (uint32_t)__builtin_ctzll(~bal);
+    uint32_t dst = (uint32_t)__shfl_up((int)anc, 1);  // the path's node below it
+    if (lane == 0) dst = i;
+    if (lane < m) {
+      a[dst] = ae;
+      x[ae.slot] = dst;
+    }
+    const uint32_t f = m ? uread(anc, m - 1) : i;
+    put(f, X);
+    return f;
   }
-  __device__ void promote(uint32_t s) { sift_up(x[s]); }
-  __device__ void demote(uint32_t s) { sift_down(x[s], *cnt); }
-  __device__ void adjust(uint32_t s) { sift(x[s], *cnt); }
-  __device__ uint32_t top() const { return a[0]; }
+
+  __device__ uint32_t sift_up(uint32_t i, const HEnt& X) const {
+    uint32_t anc;
+    const uint32_t d = ancestors(i, &anc);
+    HEnt ae{~0ull, kClsNone + 1, 0};
+    if (lane < d) ae = a[anc];
+    return up_anc(i, X, d, anc, ae);
+  }
+
+  // sift (:550-564): up if less than the parent, else down.  The ancestors
+  // and the first subtree below i are loaded together.
+  __device__ uint32_t sift(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (i == 0) return sift_down(i, n, X);
+    uint32_t anc;
+    const uint32_t d = ancestors(i, &anc);
+    const Sub L = layout(d);
+    HEnt ae{~0ull, kClsNone + 1, 0};
+    uint32_t eidx = 0xffffffffu;
+    HEnt e = ae;
+    if (lane < d) ae = a[anc];
+    else if (i < n) e = sub_load(L, i, n, &eidx);
+    if (hlt(X, hread(ae, 0))) return up_anc(i, X, d, anc, ae);
+    if (L.D == 0) return sift_down(i, n, X);  // (no lanes left for a subtree)
+    if (i < n && down_sub(L, d, e, eidx, n, X, &i)) return sift_down(i, n, X);
+    put(i, X);
+    return i;
+  }
 };
 
-struct Heaps {
-  HeapRef resv, lim, ready;
-  __device__ Heaps(const Table& t, const HeapDev& d)
-      : resv(t, d, kHResv), lim(t, d, kHLim), ready(t, d, kHReady) {}
-  __device__ void adjust3(uint32_t s) {
-    resv.adjust(s);
-    lim.adjust(s);
-    ready.adjust(s);
+struct WHeaps {
+  const Table& tb;
+  const HeapDev& hd;
+  WHeap h[3];
+  uint32_t lane;
+  __device__ WHeaps(const Table& t, const HeapDev& d) : tb(t), hd(d) {
+    lane = lane_id();
+    for (int j = 0; j < 3; ++j)
+      h[j] = WHeap{d.ent + (size_t)j * d.n, d.hix + (size_t)j * d.n, d.k, lane};
+  }
+  __device__ uint32_t count() const { return hd.cnt[0]; }
+  __device__ HEnt top(int j) const { return hd.ent[(size_t)j * hd.n]; }
+  // slot s's index in each heap (lanes 0-2 load; uniform)
+  __device__ void index3(uint32_t s, uint32_t* ix) const {
+    uint32_t v = 0;
+    if (lane < 3) v = hd.hix[(size_t)lane * hd.n + s];
+    for (int j = 0; j < 3; ++j) ix[j] = uread(v, j);
+  }
+  // the slot's three entries from its ScanRec (loaded by every lane: one
+  // request) and its three indices
+  __device__ void load3(uint32_t s, HEnt* X, uint32_t* ix) const {
+    const ScanRec r = tb.sc[s];
+    index3(s, ix);
+    for (int j = 0; j < 3; ++j) X[j] = hent(j, r, s);
+  }
+  // adjust x 3 (:996-1016, :567-625): sift in each heap, in heap order
+  __device__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
+    const uint32_t n = count();
+    for (int j = 0; j < 3; ++j) ix[j] = h[j].sift(ix[j], n, X[j]);
+  }
+  __device__ void adjust3(uint32_t s) const {
+    HEnt X[3];
+    uint32_t ix[3];
+    load3(s, X, ix);
+    adjust3(s, X, ix);
+  }
+  // the entries rewritten in place (a key that changed without a heap call:
+  // the idle reset before a Reject, :937-993)
+  __device__ void refresh3(uint32_t s) const {
+    HEnt X[3];
+    uint32_t ix[3];
+    load3(s, X, ix);
+    for (int j = 0; j < 3; ++j) h[j].put(ix[j], X[j]);
+  }
+  // erase (delete_from_heaps): IndIntruHeap::remove (:433-445) -- the last
+  // element swapped in and sifted with the count already reduced
+  __device__ void remove3(uint32_t s) const {
+    uint32_t ix[3];
+    index3(s, ix);
+    const uint32_t last = count() - 1;
+    for (int j = 0; j < 3; ++j) {
+      const HEnt X = h[j].a[last];
+      h[j].sift(ix[j], last, X);
+    }
+    wave_sync();
+    if (lane < 3) hd.cnt[lane] = last;
+    wave_sync();
   }
 };
 
 // ------------------------------------------------------------------ kernels
-// registration (client_map.emplace + three pushes, in the given order)
+// registration (client_map.emplace + three pushes, in the given order): new
+// clients have no request, so each push's sift_up never moves (nothing is
+// strictly greater than a client without a request): the pushes append in
+// order, one thread per client.  `base` = the heaps' count before.
 __global__ void k_heap_push(Table tb, HeapDev hd, const uint32_t* slots, uint32_t n) {
-  if (threadIdx.x) return;
-  Heaps H(tb, hd);
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t s = slots[i];
-    H.resv.push(s);
-    H.lim.push(s);
-    H.ready.push(s);
+  const uint32_t base = hd.cnt[0];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slots[i];
+  const ScanRec r = tb.sc[s];
+  for (int j = 0; j < 3; ++j) {
+    hd.ent[(size_t)j * hd.n + base + i] = hent(j, r, s);
+    hd.hix[(size_t)j * hd.n + s] = base + i;
   }
+}
+__global__ void k_heap_count_add(HeapDev hd, uint32_t n) {
+  if (threadIdx.x < 3) hd.cnt[threadIdx.x] += n;
 }
 
 // erase (delete_from_heaps, before the client's state goes)
-__global__ void k_heap_remove(Table tb, HeapDev hd, const uint32_t* slots, uint32_t n) {
-  if (threadIdx.x) return;
-  Heaps H(tb, hd);
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t s = slots[i];
-    H.resv.remove_slot(s);
-    H.lim.remove_slot(s);
-    H.ready.remove_slot(s);
-  }
+__global__ void __launch_bounds__(64) k_heap_remove(Table tb, HeapDev hd, const uint32_t* slots,
+                                                    uint32_t n) {
+  WHeaps W(tb, hd);
+  for (uint32_t i = 0; i < n; ++i) W.remove3(slots[i]);
 }
 
 // clients whose queues a filter / remove_by_client modified, ascending
-__global__ void k_heap_adjust(Table tb, HeapDev hd, const uint32_t* slots, uint32_t n) {
-  if (threadIdx.x) return;
-  Heaps H(tb, hd);
-  for (uint32_t i = 0; i < n; ++i) H.adjust3(slots[i]);
+__global__ void __launch_bounds__(64) k_heap_adjust(Table tb, HeapDev hd, const uint32_t* slots,
+                                                    uint32_t n) {
+  WHeaps W(tb, hd);
+  for (uint32_t i = 0; i < n; ++i) W.adjust3(slots[i]);
 }
 
 constexpr int kHeapThreads = 256;
@@ -221,20 +436,35 @@ __device__ inline double heap_idle_lowest(const Table& tb, uint64_t* sh) {
   return r == kMaxKey ? 1.7976931348623157e308 : from_okey(r);
 }
 
-// n add_request_time calls in order (do_add_request, :913-1018)
+// n add_request_time calls in order (do_add_request, :913-1018).  Wave 0
+// runs them; waves 1-3 wait at the block barrier and join only for an idle
+// reset's minimum (a scan of every client, as the reference's).
 __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd, AddParams p) {
   __shared__ uint64_t sh[kHeapThreads / 64];
-  __shared__ uint32_t s_idle;
-  Heaps H(tb, hd);
+  __shared__ uint32_t s_cmd;  // 1: an idle reset's minimum, 2: done
+  if (threadIdx.x >= 64) {
+    for (;;) {
+      __syncthreads();
+      if (s_cmd == 2) return;
+      heap_idle_lowest(tb, sh);
+    }
+  }
+  WHeaps W(tb, hd);
+  const uint32_t lane = W.lane;
   for (uint32_t i = 0; i < p.n; ++i) {
     const uint32_t s = p.reqs[i].slot;
-    if (threadIdx.x == 0) s_idle = s < tb.n && (tb.sc[s].flags & (F_REG | F_IDLE)) == (F_REG | F_IDLE);
-    __syncthreads();
-    const bool idle = s_idle != 0;
+    const bool ok = s < tb.n;
+    const uint8_t fl = ok ? tb.sc[s].flags : 0;
+    const bool idle = ok && (fl & (F_REG | F_IDLE)) == (F_REG | F_IDLE);
     double lowest = 0.0;
-    if (idle) lowest = heap_idle_lowest(tb, sh);  // (the client itself is idle: not counted)
-    if (threadIdx.x == 0) {
-      if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
+    if (idle) {  // (the client itself is idle: not counted)
+      if (lane == 0) s_cmd = 1;
+      __syncthreads();
+      lowest = heap_idle_lowest(tb, sh);
+    }
+    uint32_t acc = 0, first = 0;
+    if (lane == 0) {
+      if (!ok || !(fl & F_REG)) {
         p.rc[i] = DMC_ENOTREG;
       } else {
         if (idle) {  // :981-984 (prop_delta kept when the trigger does not fire)
@@ -248,97 +478,138 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
         const uint32_t count0 = tb.sc[s].count;
         AddState st;
         add_chain_slot(tb, p, s, 1, i, nullptr, nullptr, ActBuf{}, &st);
-        if (p.rc[i] == DMC_OK) {
-          if (count0 == 0) H.adjust3(s);  // a first request (:996-1006)
-          H.adjust3(s);                   // (:1011-1016)
-        }
+        acc = p.rc[i] == DMC_OK ? 1u : 0u;
+        first = count0 == 0 ? 1u : 0u;
       }
     }
-    __syncthreads();
+    wave_sync();  // (lane 0's stores above precede the wave's loads below)
+    acc = uread(acc, 0);
+    first = uread(first, 0);
+    if (acc) {
+      HEnt X[3];
+      uint32_t ix[3];
+      W.load3(s, X, ix);
+      if (first) W.adjust3(s, X, ix);  // a first request (:996-1006)
+      W.adjust3(s, X, ix);             // (:1011-1016)
+    } else if (idle) {
+      W.refresh3(s);  // (a rejected activation: prop_delta moved, no heap call)
+    }
   }
+  if (lane == 0) s_cmd = 2;
+  __syncthreads();
 }
 
-// The pop of the top of heap `hsel` (pop_process_request, :1046-1073, with
-// reduce_reservation_tags, :1077-1111, for a priority pop): the decision,
-// the front popped and (delayed) the new front's tag (update_next_tag,
-// :1021-1036), the heap calls with that state, then the reduction and
-// resv.promote.
-__device__ inline void heap_pop(const Table& tb, Heaps& H, uint32_t s, bool prio, uint64_t tick,
-                                dmc_decision* out, unsigned long long* sched) {
-  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  const ScanRec sr = tb.sc[s];
-  const uint32_t h = sr.head, c = sr.count;
-  const ReqEntry popped = ring[h];
-  dmc_decision d;
-  d.handle = popped.handle;
-  d.tag_r = popped.r;
-  d.tag_p = popped.p;
-  d.tag_l = popped.l;
-  d.slot = s;
-  d.cost = popped.cost;
-  d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
-  d.flags = 0;  // (the heap top is the reference's winner: no tie to flag)
-  *out = d;
-  const uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
-  double rinv = tb.rec[s].r_inv;
-  if (tb.delayed && nc) {  // update_next_tag
-    ReqEntry& f = ring[nh];
-    const Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
-    Tag3 nt;
-    const uint32_t cd = tb.aux[s].cur_delta, cr = tb.aux[s].cur_rho;
-    double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
-    if (tb.binfo) {  // U1: get_cli_info (:870-875) becomes client.info
-      const BoundInfo b = tb.binfo[s];
-      rinv = b.r_inv;
-      winv = b.w_inv;
-      linv = b.l_inv;
-      tb.rec[s].r_inv = rinv;
-      tb.rec[s].w_inv = winv;
-      tb.rec[s].l_inv = linv;
-    }
-    if (make_tag(pt, rinv, winv, linv, cd, cr, f.arrival, f.cost, tb.antic, &nt)) {
-      f.r = nt.r;
-      f.p = nt.p;
-      f.l = nt.l;
-      f.delta = cd;
-      f.rho = cr;
-      double pr = tb.rec[s].prev_r, pp = tb.rec[s].prev_p, pl = tb.rec[s].prev_l;
-      assign_unpinned(pr, nt.r);
-      assign_unpinned(pl, nt.l);
-      assign_unpinned(pp, nt.p);
-      tb.rec[s].prev_r = pr;
-      tb.rec[s].prev_p = pp;
-      tb.rec[s].prev_l = pl;
-      tb.rec[s].prev_arr = nt.arrival;
-      tb.aux[s].last_tick = tick;
-    }
-  }
-  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc, (uint8_t)(sr.flags & ~F_READY), 0, 0};
-  if (nc) {
-    const ReqEntry& f = ring[nh];
-    o.r = f.r;
-    o.pk = __dadd_rn(f.p, tb.rec[s].pd);
-    o.l = f.l;
-  }
-  tb.sc[s] = o;
-  H.resv.demote(s);
-  H.lim.adjust(s);
-  H.ready.demote(s);
-  if (prio) {
-    const double off = resv_offset(rinv, popped.cost, popped.rho);
-    if (tb.delayed) {
-      if (nc) ring[nh].r = __dsub_rn(ring[nh].r, off);
-    } else {
-      for (uint32_t i = 1; i < c; ++i) {
-        ReqEntry& e = ring[(h + i) & tb.qmask];
-        e.r = __dsub_rn(e.r, off);
+// The pop of slot s, the top of heap `hsel` (pop_process_request,
+// :1046-1073, with reduce_reservation_tags, :1077-1111, for a priority pop):
+// the decision, the front popped and (delayed) the new front's tag
+// (update_next_tag, :1021-1036), the heap calls with that state, then the
+// reduction and resv.promote.  Lane 0 makes the client's state change; the
+// wave makes the heap calls.
+__device__ inline void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
+                                uint64_t tick, dmc_decision* out, unsigned long long* sched) {
+  const uint32_t lane = W.lane;
+  // the slot's heap indices, requested first (lanes 0-2)
+  const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
+  // lane 0: the client's state change; the front's keys before the
+  // reduction (o: what the demotes see) and its reduced r (the promote's)
+  double o_r = 0.0, o_pk = 0.0, o_l = 0.0, r_red = 0.0;
+  uint32_t o_cf = 0;
+  if (lane == 0) {
+    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+    const ScanRec sr = tb.sc[s];
+    const uint32_t h = sr.head, c = sr.count;
+    const ReqEntry popped = ring[h];
+    dmc_decision d;
+    d.handle = popped.handle;
+    d.tag_r = popped.r;
+    d.tag_p = popped.p;
+    d.tag_l = popped.l;
+    d.slot = s;
+    d.cost = popped.cost;
+    d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
+    d.flags = 0;  // (the heap top is the reference's winner: no tie to flag)
+    *out = d;
+    const uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
+    double rinv = tb.rec[s].r_inv;
+    if (tb.delayed && nc) {  // update_next_tag
+      ReqEntry& f = ring[nh];
+      const Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
+      Tag3 nt;
+      const uint32_t cd = tb.aux[s].cur_delta, cr = tb.aux[s].cur_rho;
+      double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
+      if (tb.binfo) {  // U1: get_cli_info (:870-875) becomes client.info
+        const BoundInfo b = tb.binfo[s];
+        rinv = b.r_inv;
+        winv = b.w_inv;
+        linv = b.l_inv;
+        tb.rec[s].r_inv = rinv;
+        tb.rec[s].w_inv = winv;
+        tb.rec[s].l_inv = linv;
+      }
+      if (make_tag(pt, rinv, winv, linv, cd, cr, f.arrival, f.cost, tb.antic, &nt)) {
+        f.r = nt.r;
+        f.p = nt.p;
+        f.l = nt.l;
+        f.delta = cd;
+        f.rho = cr;
+        double pr = tb.rec[s].prev_r, pp = tb.rec[s].prev_p, pl = tb.rec[s].prev_l;
+        assign_unpinned(pr, nt.r);
+        assign_unpinned(pl, nt.l);
+        assign_unpinned(pp, nt.p);
+        tb.rec[s].prev_r = pr;
+        tb.rec[s].prev_p = pp;
+        tb.rec[s].prev_l = pl;
+        tb.rec[s].prev_arr = nt.arrival;
+        tb.aux[s].last_tick = tick;
       }
     }
-    tb.rec[s].prev_r = __dsub_rn(tb.rec[s].prev_r, off);
-    if (nc) tb.sc[s].r = ring[nh].r;
-    H.resv.promote(s);
+    ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc, (uint8_t)(sr.flags & ~F_READY), 0, 0};
+    if (nc) {
+      const ReqEntry& f = ring[nh];
+      o.r = f.r;
+      o.pk = __dadd_rn(f.p, tb.rec[s].pd);
+      o.l = f.l;
+    }
+    o_r = o.r;
+    o_pk = o.pk;
+    o_l = o.l;
+    o_cf = (uint32_t)o.count | ((uint32_t)o.flags << 8);
+    r_red = o.r;
+    if (prio) {
+      // reduce_reservation_tags (immediate: every queued request; delayed:
+      // the front) and prev r (:1077-1111)
+      const double off = resv_offset(rinv, popped.cost, popped.rho);
+      if (tb.delayed) {
+        if (nc) ring[nh].r = __dsub_rn(ring[nh].r, off);
+      } else {
+        for (uint32_t i = 1; i < c; ++i) {
+          ReqEntry& e = ring[(h + i) & tb.qmask];
+          e.r = __dsub_rn(e.r, off);
+        }
+      }
+      tb.rec[s].prev_r = __dsub_rn(tb.rec[s].prev_r, off);
+      if (nc) r_red = ring[nh].r;
+    }
+    o.r = r_red;
+    tb.sc[s] = o;
+    atomicAdd(&sched[prio ? 1 : 0], 1ull);
   }
-  atomicAdd(&sched[prio ? 1 : 0], 1ull);
+  ScanRec o{dread(o_r, 0), dread(o_pk, 0), dread(o_l, 0), 0, 0, 0, 0, 0};
+  const uint32_t cf = uread(o_cf, 0);
+  o.count = (uint8_t)(cf & 0xffu);
+  o.flags = (uint8_t)(cf >> 8);
+  uint32_t ix[3];
+  for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
+  const uint32_t n = W.count();
+  // pop_process_request's heap calls, on the unreduced front (:1063-1069)
+  ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o, s));
+  ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o, s));
+  ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o, s));
+  if (prio) {  // resv_heap.promote after the reduction (:1110)
+    o.r = dread(r_red, 0);
+    W.h[kHResv].sift_up(ix[kHResv], hent(kHResv, o, s));
+  }
+  wave_sync();
 }
 
 struct HeapPullRes {
@@ -353,54 +624,59 @@ struct HeapPullRes {
 // fetches the popped client's info between selection and pop, :870-875,
 // :1021-1036): one pull decided -- the limit loop's marks made -- and its
 // pop left in res->pend_*; mode 2: that pop.
-__global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at_limit,
-                            uint64_t tick, dmc_decision* out, HeapPullRes* res,
-                            dmc_pull_result* d_result, unsigned long long* sched,
-                            int mode = 0) {
-  if (threadIdx.x) return;
-  Heaps H(tb, hd);
+__global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k,
+                                                  int at_limit, uint64_t tick, dmc_decision* out,
+                                                  HeapPullRes* res, dmc_pull_result* d_result,
+                                                  unsigned long long* sched, int mode = 0) {
+  WHeaps W(tb, hd);
+  const uint32_t lane = W.lane;
   HeapPullRes r{0, 0, 0, DMC_NEXT_RETURNING, 0.0, 0, 0};
   if (mode == 2) {
     const HeapPullRes pr = *res;
-    heap_pop(tb, H, pr.pend_slot, pr.pend_prio != 0, tick, out, sched);
+    heap_pop(tb, W, pr.pend_slot, pr.pend_prio != 0, tick, out, sched);
     r.n = 1;
     if (pr.pend_prio) r.n_prio = 1;
     else r.n_res = 1;
-    *res = r;
+    if (lane == 0) *res = r;
     return;
   }
+  const uint32_t n = W.count();
   // each iteration decides one pull (pop_slot / pop_prio) or stops; the pop
   // is made at its end (mode 1: recorded for mode 2 instead)
   while (r.n < k) {
     uint32_t pop_slot = kNone;
     bool pop_prio = false;
-    if (*H.resv.cnt == 0) {  // no clients: none (:1118-1120)
+    if (n == 0) {  // no clients: none (:1118-1120)
       r.type = DMC_NEXT_NONE;
       break;
     }
-    const uint32_t rs = H.resv.top();
-    const ScanRec rsr = tb.sc[rs];
-    if (rsr.count && rsr.r <= now) {
-      pop_slot = rs;
+    const HEnt rt = W.top(kHResv);
+    if (rt.cls == 0 && hval(rt) <= now) {
+      pop_slot = rt.slot;
     } else {
       for (;;) {  // the limit loop
-        const uint32_t ls = H.lim.top();
-        const ScanRec lr = tb.sc[ls];
-        if (!(lr.count && !(lr.flags & F_READY) && lr.l <= now)) break;
-        tb.sc[ls].flags = (uint8_t)(lr.flags | F_READY);
-        H.ready.promote(ls);
-        H.lim.demote(ls);
+        const HEnt lt = W.top(kHLim);
+        if (!(lt.cls == 0 && hval(lt) <= now)) break;
+        const uint32_t ls = lt.slot;
+        // ready = true (the slot's ready flag: F_READY in its cursor word)
+        if (lane == 0) tb.sc[ls].flags = (uint8_t)(tb.sc[ls].flags | F_READY);
+        wave_sync();
+        HEnt X[3];
+        uint32_t ix[3];
+        W.load3(ls, X, ix);
+        W.h[kHReady].sift_up(ix[kHReady], X[kHReady]);
+        W.h[kHLim].sift_down(0, n, X[kHLim]);
       }
-      const uint32_t ps = H.ready.top();
-      const ScanRec pr = tb.sc[ps];
-      if (pr.count && (pr.flags & F_READY) && pr.pk < kInf) {
-        pop_slot = ps;
+      const HEnt pt = W.top(kHReady);
+      const bool ph = pt.cls != kClsNone && hval(pt) < kInf;
+      if (pt.cls == 0 && ph) {
+        pop_slot = pt.slot;
         pop_prio = true;
-      } else if (at_limit == DMC_AT_LIMIT_ALLOW && pr.count && pr.pk < kInf) {
-        pop_slot = ps;
+      } else if (at_limit == DMC_AT_LIMIT_ALLOW && ph) {
+        pop_slot = pt.slot;
         pop_prio = true;
-      } else if (at_limit == DMC_AT_LIMIT_ALLOW && rsr.count && rsr.r < kInf) {
-        pop_slot = rs;
+      } else if (at_limit == DMC_AT_LIMIT_ALLOW && rt.cls == 0 && hval(rt) < kInf) {
+        pop_slot = rt.slot;
       }
     }
     if (pop_slot == kNone) {
@@ -408,13 +684,13 @@ __global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at
       // :1192-1195; kTimeMax = DBL_MAX: an infinite tag is no future)
       constexpr double kTimeMax = 1.7976931348623157e308;
       double next = kTimeMax;
-      const uint32_t rt = H.resv.top(), lt = H.lim.top();
-      if (tb.sc[rt].count) {
-        const double v = tb.sc[rt].r;
+      const HEnt r0 = W.top(kHResv), l0 = W.top(kHLim);
+      if (r0.cls != kClsNone) {
+        const double v = hval(r0);
         if (v != 0.0) next = v < next ? v : next;
       }
-      if (tb.sc[lt].count) {
-        const double v = tb.sc[lt].l;
+      if (l0.cls != kClsNone) {
+        const double v = hval(l0);
         if (v != 0.0) next = v < next ? v : next;
       }
       if (next < kTimeMax) {
@@ -430,11 +706,12 @@ __global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at
       r.pend_prio = pop_prio ? 1u : 0u;
       break;
     }
-    heap_pop(tb, H, pop_slot, pop_prio, tick, out + r.n, sched);
+    heap_pop(tb, W, pop_slot, pop_prio, tick, out + r.n, sched);
     ++r.n;
     if (pop_prio) ++r.n_prio;
     else ++r.n_res;
   }
+  if (lane) return;
   *res = r;
   if (d_result) {
     dmc_pull_result x{};
@@ -446,4 +723,3 @@ __global__ void k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k, int at
     *d_result = x;
   }
 }
-

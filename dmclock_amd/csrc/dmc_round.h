@@ -804,7 +804,7 @@ __device__ inline PickBins pick_load(const uint32_t* hist) {
   const uint32_t* hp = hist + p * kHistBinsR;  // shard i at hp + i * 2 * kHistBinsR
   PickBins b;
   if (kShards == 1 && kBinsPerThreadR == 4) {
-    const uint4 x = reinterpret_cast<const uint4*>(hp)[t];
+    const uint4 x = ld_as<uint4>(hp + 4 * t);
     b.h[0] = x.x;
     b.h[1] = x.y;
     b.h[2] = x.z;
@@ -1012,9 +1012,8 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
   uint64_t kr[4], kp[4];
   auto load = [&](uint32_t s0) {
     if (s0 + 4 <= n) {
-      const ulonglong2* r2 = reinterpret_cast<const ulonglong2*>(keyr + s0);
-      const ulonglong2* p2 = reinterpret_cast<const ulonglong2*>(keyp + s0);
-      ulonglong2 a = r2[0], b = r2[1], c = p2[0], d = p2[1];
+      const ulonglong2 a = ld_as<ulonglong2>(keyr + s0), b = ld_as<ulonglong2>(keyr + s0 + 2),
+                       c = ld_as<ulonglong2>(keyp + s0), d = ld_as<ulonglong2>(keyp + s0 + 2);
       kr[0] = a.x; kr[1] = a.y; kr[2] = b.x; kr[3] = b.y;
       kp[0] = c.x; kp[1] = c.y; kp[2] = d.x; kp[3] = d.y;
     } else {
@@ -1427,7 +1426,7 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
           BRecR{BKey{acc.key0, s, 0u, run, s * tb.q + h}, ci | kFastRec, e0.cost, e0.handle,
                 e0.r, e0.p, e0.l};
     }
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(post + ci);
+    char* const dst = reinterpret_cast<char*>(post + ci);  // PostRec's 16-byte words
     {
       double fr = 0.0, fpk = 0.0, fl = 0.0, r2 = 0.0;
       uint32_t bits = (prio ? 1u : 0u) | (run ? 4u : 0u);
@@ -1443,19 +1442,19 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
       const uint32_t cw = (uint32_t)c.fb | ((uint32_t)c.m << 8) | ((uint32_t)c.h << 16) |
                           ((uint32_t)c.c << 24);
       // PostRec line 1: fr, fpk | fl, prev_r | off, r2 | bits, cand, pad
-      dst[0] = make_ulonglong2(dbits(fr), dbits(fpk));
-      dst[1] = make_ulonglong2(dbits(fl), dbits(pr_prev));
-      dst[2] = make_ulonglong2(dbits(off), dbits(r2));
-      dst[3] = make_ulonglong2((unsigned long long)bits | ((unsigned long long)cw << 32), 0ull);
+      st_as(dst, make_ulonglong2(dbits(fr), dbits(fpk)));
+      st_as(dst + 16, make_ulonglong2(dbits(fl), dbits(pr_prev)));
+      st_as(dst + 32, make_ulonglong2(dbits(off), dbits(r2)));
+      st_as(dst + 48, make_ulonglong2((unsigned long long)bits | ((unsigned long long)cw << 32), 0ull));
     }
     if (run) {
       // line 2, the run's pop: queue position 1 with its reduced r (its
       // decision tag): handle1, r1 | p1, l1 | cost1
       const ReqEntry e1 = rv.at(1);
-      dst[4] = make_ulonglong2(e1.handle, dbits(__dsub_rn(e1.r, off)));
-      dst[5] = make_ulonglong2(dbits(e1.p), dbits(e1.l));
-      dst[6] = make_ulonglong2((unsigned long long)e1.cost, 0ull);
-      dst[7] = make_ulonglong2(0ull, 0ull);
+      st_as(dst + 64, make_ulonglong2(e1.handle, dbits(__dsub_rn(e1.r, off))));
+      st_as(dst + 80, make_ulonglong2(dbits(e1.p), dbits(e1.l)));
+      st_as(dst + 96, make_ulonglong2((unsigned long long)e1.cost, 0ull));
+      st_as(dst + 112, make_ulonglong2(0ull, 0ull));
     }
     decof[ci] = kNoDec;
   } else {
@@ -1535,7 +1534,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   if constexpr (PRE) {
 #pragma unroll
     for (int j = 0; j < kPT; ++j)
-      pt[j] = reinterpret_cast<const uint4*>(hist + kShards * 2 * kHistBinsR)[threadIdx.x + j * kEmitThreads];
+      pt[j] = ld_as<uint4>(hist + kShards * 2 * kHistBinsR + 4 * (threadIdx.x + j * kEmitThreads));
   } else {
     hv = pick_load(hist);
   }
@@ -1544,16 +1543,14 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
   uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
   if (s0 + kEmitPer <= n) {
-    const uint4* k4 = reinterpret_cast<const uint4*>(k32 + s0);
-    const uint4* m4 = reinterpret_cast<const uint4*>(meta + s0);
 #pragma unroll
     for (int j = 0; j < kEmitPer / 2; ++j) {
-      const uint4 a = k4[j];
+      const uint4 a = ld_as<uint4>(k32 + s0 + 2 * j);
       kr[2 * j] = a.x; kp[2 * j] = a.y; kr[2 * j + 1] = a.z; kp[2 * j + 1] = a.w;
     }
 #pragma unroll
     for (int j = 0; j < kEmitPer / 4; ++j) {
-      const uint4 m = m4[j];
+      const uint4 m = ld_as<uint4>(meta + s0 + 4 * j);
       mt[4 * j] = m.x; mt[4 * j + 1] = m.y; mt[4 * j + 2] = m.z; mt[4 * j + 3] = m.w;
     }
   } else {
@@ -1571,7 +1568,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // zeroing of s_cnt / s_tot before any wave adds to them)
   if constexpr (PRE) {
 #pragma unroll
-    for (int j = 0; j < kPT; ++j) reinterpret_cast<uint4*>(ltab)[threadIdx.x + j * kEmitThreads] = pt[j];
+    for (int j = 0; j < kPT; ++j) st_as(ltab + 4 * (threadIdx.x + j * kEmitThreads), pt[j]);
     if (threadIdx.x < 2) s_ph[threadIdx.x] = rd->ph[threadIdx.x];
     __syncthreads();  // (also orders the zeroing of s_cnt / s_tot)
   } else {
@@ -2399,9 +2396,10 @@ __device__ inline void rfinish_body(const Round* rd, HostRound* h, bool round_en
   if (round_end && threadIdx.x == 0 && rd->gate)
     *rd->gate = (!rd->overflow && rd->n_dec >= rd->k_total) ? 0u : 1u;
   constexpr uint32_t W = sizeof(Round) / 4;
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(rd);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&h->r);
-  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
+  const char* src = reinterpret_cast<const char*>(rd);
+  char* dst = reinterpret_cast<char*>(&h->r);
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x)
+    st_as<uint32_t>(dst + 4 * i, ld_as<uint32_t>(src + 4 * i));
   if (threadIdx.x == 0 && rd->res && !rd->overflow) {
     dmc_pull_result r{};
     r.n_decisions = rd->n_dec;
@@ -2671,8 +2669,7 @@ __global__ void __launch_bounds__(kEmitThreads) k_rpick_m(const RHistArgs* a) {
   const PickBins hv = pick_load(x.hist);
   pick_both(rd->k_total, rd->tot, hv, sbn, s_ph, (int)rd->sampled, rd->fault);
   for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += kEmitThreads)
-    reinterpret_cast<uint4*>(x.hist + kShards * 2 * kHistBinsR)[i] =
-        reinterpret_cast<const uint4*>(sbn)[i];
+    st_as(x.hist + kShards * 2 * kHistBinsR + 4 * i, ld_as<uint4>(sbn + 4 * i));
   if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
 }
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const REmitArgs* a) {

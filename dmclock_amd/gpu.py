@@ -64,6 +64,8 @@ EXPORTS = {
     "dmc_stats_get": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "dmc_queue_set_option": (_i32, [_vp, _i32, ctypes.c_int64]),
     "dmc_queue_counters": (_i32, [_vp, ctypes.POINTER(Counters), _i32]),
+    "dmc_queue_counters_sized": (_i32, [_vp, _vp, ctypes.c_uint64, _i32]),
+    "dmc_abi_version": (_i32, []),
     "dmc_tracker_tally": (_i32, [_vp, _vp, _vp, _u32, _vp, _vp]),
     "dmc_tracker_fill": (_i32, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp,
                                 _vp]),
@@ -81,7 +83,7 @@ EXPORTS = {
                                 ctypes.POINTER(_f64)]),
     "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
-PROF_NSTAGES = 12
+PROF_NSTAGES = 13
 
 # dmc_info_fn: int (*)(void* ctx, uint32_t slot, double* r, double* w, double* l)
 INFO_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _u32, ctypes.POINTER(_f64),

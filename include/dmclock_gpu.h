@@ -44,6 +44,21 @@ extern "C" {
 #define DMC_EQUEUEFULL (-1004) /* the client's request ring is full (documented deviation: the
                                   reference's per-client std::deque is unbounded, :360) */
 #define DMC_ENOTREG (-1005)    /* slot not registered */
+#define DMC_ENOTRUN (-1006)    /* DMC_OPT_PIPELINE: the previous call on the queue failed (its error is
+                                  reported now) and this call was not executed: none of its adds or
+                                  pulls took effect and its outputs were not written */
+
+/* ------------------------------------------------------------ ABI version
+ * Bumped at every incompatible change of this header (option ids, struct
+ * layouts, status codes).  A caller compiled against one header checks
+ * dmc_abi_version() == DMC_ABI_VERSION at start-up; dmc_counters is also
+ * readable size-checked (dmc_queue_counters_sized).
+ *   5: DMC_OPT_FAULT moved from 9 to 13 (9, round 3's DMC_OPT_PREDICT, is
+ *      retired and returns DMC_EINVAL); DMC_ENOTRUN; dmc_counters gained
+ *      act_batches / act_seq_batches (round 4) and renamed pred_* to
+ *      bad_rounds / serve_yields. */
+#define DMC_ABI_VERSION 5
+int dmc_abi_version(void);
 
 /* ------------------------------------------------------------ enums */
 /* AtLimit, dmclock_server.h:74-84 */
@@ -378,9 +393,10 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   pulls with k <= SMALL_K run the single-op path (one kernel per add,
                                   two per pull, results in host-mapped memory, one round trip);
                                   0: the general launch sequence */
-#define DMC_OPT_FAULT 9         /* test hook: 1 = the next rounds' pick leaves phase 1's selection
+#define DMC_OPT_FAULT 13        /* test hook: 1 = the next rounds' pick leaves phase 1's selection
                                   unset (each such round must fail its outcome check: DMC_EDEVICE,
-                                  never a short dispatch); 0 (default): off */
+                                  never a short dispatch); 0 (default): off.  (Option 9, the
+                                  retired DMC_OPT_PREDICT, returns DMC_EINVAL.) */
 #define DMC_OPT_SERVE 10        /* 1: single-op adds and pulls (as DMC_OPT_SINGLE_OP) are served by a
                                   persistent one-workgroup kernel polling host-mapped commands: no
                                   launch per call; the pull reduces per-group summaries of the
@@ -404,7 +420,9 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   that launch, so the device runs the calls back to back.  A call's
                                   results are complete once the next call on the queue, or any other
                                   call such as dmc_queue_sync, has returned; an error of a call is
-                                  reported by that next call.  A round that needs the host shuts a
+                                  reported by that next call, which then was not executed itself
+                                  (DMC_ENOTRUN when the error is the previous call's alone; the
+                                  queue stays usable).  A round that needs the host shuts a
                                   device-side gate and the next call's queued graph does nothing (it
                                   is launched again).  0 (default): each call waits for its round */
 #define DMC_OPT_FAIL_ALLOC 7    /* test hook: the queue's next `value` device buffer allocations
@@ -444,6 +462,9 @@ typedef struct dmc_counters {
                                request -- whose basis later requests of the batch moved) */
 } dmc_counters;
 int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
+/* The same, copying min(size, sizeof(dmc_counters)) bytes: a caller built
+ * against an older, smaller dmc_counters passes its own sizeof. */
+int dmc_queue_counters_sized(dmc_queue* q, void* out, uint64_t size, int reset);
 
 /* ------------------------------------------------------------ profiling
  * Stage timers: HIP events recorded on the queue's stream around each stage
@@ -462,7 +483,8 @@ int dmc_queue_counters(dmc_queue* q, dmc_counters* out, int reset);
 #define DMC_PROF_STEP 9     /* one general pull_request */
 #define DMC_PROF_FUTURE 10  /* a round's terminal pull */
 #define DMC_PROF_CAND 11    /* k_rcand */
-#define DMC_PROF_NSTAGES 12
+#define DMC_PROF_CHAIN_SCAN 12 /* k_chain_scan: a fused call's add chain beside the round's scan */
+#define DMC_PROF_NSTAGES 13
 
 int dmc_profile_enable(dmc_queue* q, int on);
 int dmc_profile_reset(dmc_queue* q);

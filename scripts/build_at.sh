@@ -7,7 +7,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 c=$1; name=$2; shift 2
 mkdir -p $R/dmclock_amd/variants
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-strict-aliasing -Wno-unused-function"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -Wno-unused-function"
 if [ "$c" = "." ]; then
   exec /opt/rocm/bin/hipcc $F "$@" -o $R/dmclock_amd/variants/$name.so $R/dmclock_amd/csrc/dmc_engine.hip
 fi

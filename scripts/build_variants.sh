@@ -6,7 +6,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/dmclock_amd/variants
 mkdir -p $OUT
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-strict-aliasing -Wno-unused-function"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -Wno-unused-function"
 SRC=$R/dmclock_amd/csrc/dmc_engine.hip
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}; [ "$defs" = "$spec" ] && defs=""

@@ -32,6 +32,24 @@ def test_library_exports_every_declared_symbol():
     assert set(names) <= set(gpu.EXPORTS), set(names) - set(gpu.EXPORTS)
 
 
+def test_abi_version_matches_header():
+    """DMC_ABI_VERSION (option ids and dmc_counters changed without
+    a way to detect it): the library, the header and the binding agree."""
+    src = open(HEADER).read()
+    v = int(re.search(r"#define DMC_ABI_VERSION (\d+)", src).group(1))
+    assert gpu.lib().dmc_abi_version() == v == _abi.ABI_VERSION
+    assert "#define DMC_OPT_FAULT 13" in src and _abi.OPT_FAULT == 13
+
+
+def test_retired_option_and_sized_counters_need_a_queue():
+    """option 9 (the retired DMC_OPT_PREDICT) and the size-checked counters
+    query reject a null queue without touching a device"""
+    L = gpu.lib()
+    assert L.dmc_queue_set_option(None, 9, 1) == _abi.DMC_EINVAL
+    buf = ctypes.create_string_buffer(64)
+    assert L.dmc_queue_counters_sized(None, buf, 64, 0) == _abi.DMC_EINVAL
+
+
 def test_queue_create_fails_loudly_without_device():
     """No CPU fallback: without a HIP device queue creation returns an error
     (DMC_EDEVICE) and the binding raises."""

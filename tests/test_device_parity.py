@@ -171,6 +171,72 @@ def test_unset_phase_selection_fails_loudly():
     q.close()
 
 
+def test_pipelined_failure_next_call_not_run():
+    """DMC_OPT_PIPELINE + DMC_OPT_FAULT: call N's round fails its
+    outcome check and shuts the gate, so call N+1's graph, queued behind it,
+    does nothing.  Call N+1 must say so -- DMC_ENOTRUN, its statuses and
+    decisions untouched, the tick not advanced -- and the queue must go on:
+    call N+2 equals the oracle that saw call N's adds (applied before its
+    failed round, which dispatched nothing) and call N+2, not call N+1."""
+    import torch
+    from dmclock_amd._abi import DMC_ENOTRUN, OPT_FAULT, OPT_GRAPHS, OPT_PIPELINE
+    from dmclock_amd.gpu import DmcError, GpuQueue
+    tr = workloads.config3_trace(11, 1 << 16, 3, 1 << 12, depth=2)
+    c = tr.clients
+    steps = [(tr.ops[i][1], tr.ops[i + 1][1], tr.ops[i + 1][2])
+             for i in range(2, len(tr.ops), 2)]
+    qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 16)
+    qo = pyoracle.OracleQueue()
+    for q in (qg, qo):
+        q.register(c.slots, c.r, c.w, c.l, c.active)
+        q.add_batch(tr.ops[0][1])
+        q.pull_batch(tr.ops[1][1], tr.ops[1][2])
+    qg.set_option(OPT_PIPELINE, 1)
+    qg.set_option(OPT_GRAPHS, 0)
+    dev = torch.device("cuda", 0)
+    k = 1 << 12
+    d_reqs = [torch.from_numpy(r.view(np.uint8)).to(dev) for r, _, _ in steps]
+    d_rc = [torch.full((k,), 77, dtype=torch.int32, device=dev) for _ in steps]
+    d_out = [torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+             for _ in steps]
+    d_res = torch.zeros((len(steps), 24), dtype=torch.uint8, device=dev)
+
+    def call(i):
+        reqs, now, kk = steps[i]
+        qg.add_pull_batch_device(d_reqs[i].data_ptr(), len(reqs), d_rc[i].data_ptr(), now,
+                                 kk, d_out[i].data_ptr(), d_res[i].data_ptr())
+
+    qg.set_option(OPT_FAULT, 1)
+    call(0)  # pipelined: its failure is reported by the next call
+    with pytest.raises(DmcError, match=rf"\({DMC_ENOTRUN}\)"):
+        call(1)
+    qg.set_option(OPT_FAULT, 0)
+    call(2)
+    qg.sync()
+    torch.cuda.synchronize()
+    assert (d_rc[1].cpu().numpy() == 77).all()  # call 1 never ran
+    assert qg.counters()["bad_rounds"] >= 1
+    with pytest.raises(DmcError):  # option 9: the retired DMC_OPT_PREDICT
+        qg.set_option(9, 1)
+    import ctypes
+    buf = ctypes.create_string_buffer(16)  # a caller with an older, smaller struct
+    assert qg.L.dmc_queue_counters_sized(qg.h, buf, 16, 0) == 0
+    assert int.from_bytes(buf.raw[:8], "little") == qg.counters()["rounds"]
+    qo.add_batch(steps[0][0])
+    rc_o = qo.add_batch(steps[2][0])
+    do, ro = qo.pull_batch(steps[2][1], steps[2][2])
+    assert qo.ties == 0
+    assert np.array_equal(d_rc[2].cpu().numpy(), rc_o)
+    pr = PullResult.from_buffer_copy(d_res[2].cpu().numpy().tobytes())
+    assert (pr.n_decisions, pr.next_type) == (ro.n_decisions, ro.next_type)
+    dg = d_out[2][:pr.n_decisions * DECISION_DTYPE.itemsize].cpu().numpy().view(DECISION_DTYPE)
+    compare_decisions(dg, do, "call 2")
+    rng = np.random.default_rng(3)
+    compare_states(qg, qo, rng.choice(c.slots, 1024, replace=False), "after")
+    qg.close()
+    qo.close()
+
+
 def _bench_setup(q, tr):
     """bench.py's prepare(): bulk registration, the pre-population in 1M
     chunks and the settle pulls in 1M chunks, through the host API"""

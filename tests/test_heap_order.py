@@ -84,6 +84,44 @@ MODES = [dict(at_limit=AT_LIMIT_WAIT), dict(at_limit=AT_LIMIT_WAIT, delayed=True
          dict(at_limit=AT_LIMIT_WAIT, branching=3), dict(at_limit=AT_LIMIT_WAIT, branching=4)]
 
 
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: "-".join(f"{k}={v}" for k, v in m.items()))
+def test_epoch_time_ties_tie_exact(mode):
+    """open loop at the reference's clock scale (t0 = 1.7e9 s, what
+    get_time() returns: rounding collisions make equal tags), idle marking
+    between steps (activations whose prop_delta aligns keys exactly,
+    :957-985), random delta/rho, pulls of k in 1..128: every decision,
+    status and client state equal to the oracle's (the reference's heaps)"""
+    rng = np.random.default_rng(5)
+    tr = workloads.churn_trace(5, 700, 160, 150, 0, idle_frac=0.05, t0=1.7e9,
+                               k_choices=[1, 3, 17, 64, 128])
+    if mode.get("at_limit") == AT_LIMIT_REJECT:
+        tr.clients.l = np.where(rng.random(700) < 0.5, rng.uniform(0.3, 1.5, 700), 0.0)
+    n, qg, qo = run_parity(tr, mk_heap(mode.get("branching", 2)), queue_kw=mode,
+                           state_sample=700, require_tie_free=False)
+    assert n > 1000, n
+    assert qo.ties > 0, "the trace should tie"
+    qg.close()
+
+
+@pytest.mark.timeout(900)
+def test_heap_order_1m_clients_epoch_time():
+    """A11 at scale: BASELINE config 3 at 1,048,576
+    clients on the reference's clock scale (t0 = 1.7e9 s), in heap order:
+    4,194,304 pre-populated requests, a 2,097,152-pull settle, then two
+    steps of 65,536 adds + 65,536 pulls.  Every add status, every decision
+    (client, phase, cost, handle, tag bits), every result and 4,096 sampled
+    client states equal to the oracle's -- which replays the reference's
+    heaps and counts the tied decisions: there are ties, and each went to
+    the reference's heap top."""
+    tr = workloads.config3_trace(42, 1 << 20, 2, 1 << 16, depth=4, t0=1.7e9)
+    n, qg, qo = run_parity(tr, mk_heap(), state_sample=4096, require_tie_free=False,
+                           gpu_kw=dict(max_batch=1 << 20))
+    assert n > 2_000_000, n
+    assert qo.ties > 0, qo.ties
+    print(f"1M clients in heap order: {n} decisions, {qo.ties} tied, all the reference's")
+    qg.close()
+
+
 def _tie_trace(seed, n, steps, reject=False):
     """churn (idle marking between steps: activations, whose prop_delta
     aligns keys exactly, :957-985) with few distinct client rates and

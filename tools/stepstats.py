@@ -27,7 +27,13 @@ def main():
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
     starts = [i for i, x in enumerate(rows) if "k_add_link" in x["Kernel_Name"]]
-    starts.append(len(rows))
+    # a step runs from its k_add_link to the next one; the trace's last step
+    # ends at its last engine kernel (k_*), so that what runs after the
+    # timed region (the runtime's result copies, copyBuffer) is not counted
+    end = len(rows)
+    while end > starts[-1] + 1 and "k_" not in rows[end - 1]["Kernel_Name"]:
+        end -= 1
+    starts.append(end)
     hi = len(starts) - 1 - a.skip_last
     lo = hi - a.steps
     if lo < 0:
