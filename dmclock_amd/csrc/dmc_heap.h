@@ -322,7 +322,7 @@ struct WHeaps {
   uint32_t lane;
   __device__ WHeaps(const Table& t, const HeapDev& d) : tb(t), hd(d) {
     lane = lane_id();
-    for (int j = 0; j < 3; ++j)
+    _Pragma("unroll") for (int j = 0; j < 3; ++j)
       h[j] = WHeap{d.ent + (size_t)j * d.n, d.hix + (size_t)j * d.n, d.k, lane};
   }
   __device__ uint32_t count() const { return hd.cnt[0]; }
@@ -331,19 +331,19 @@ struct WHeaps {
   __device__ void index3(uint32_t s, uint32_t* ix) const {
     uint32_t v = 0;
     if (lane < 3) v = hd.hix[(size_t)lane * hd.n + s];
-    for (int j = 0; j < 3; ++j) ix[j] = uread(v, j);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(v, j);
   }
   // the slot's three entries from its ScanRec (loaded by every lane: one
   // request) and its three indices
   __device__ void load3(uint32_t s, HEnt* X, uint32_t* ix) const {
     const ScanRec r = tb.sc[s];
     index3(s, ix);
-    for (int j = 0; j < 3; ++j) X[j] = hent(j, r, s);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) X[j] = hent(j, r, s);
   }
   // adjust x 3 (:996-1016, :567-625): sift in each heap, in heap order
   __device__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
     const uint32_t n = count();
-    for (int j = 0; j < 3; ++j) ix[j] = h[j].sift(ix[j], n, X[j]);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = h[j].sift(ix[j], n, X[j]);
   }
   __device__ void adjust3(uint32_t s) const {
     HEnt X[3];
@@ -357,7 +357,7 @@ struct WHeaps {
     HEnt X[3];
     uint32_t ix[3];
     load3(s, X, ix);
-    for (int j = 0; j < 3; ++j) h[j].put(ix[j], X[j]);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) h[j].put(ix[j], X[j]);
   }
   // erase (delete_from_heaps): IndIntruHeap::remove (:433-445) -- the last
   // element swapped in and sifted with the count already reduced
@@ -365,7 +365,7 @@ struct WHeaps {
     uint32_t ix[3];
     index3(s, ix);
     const uint32_t last = count() - 1;
-    for (int j = 0; j < 3; ++j) {
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) {
       const HEnt X = h[j].a[last];
       h[j].sift(ix[j], last, X);
     }
@@ -386,7 +386,7 @@ __global__ void k_heap_push(Table tb, HeapDev hd, const uint32_t* slots, uint32_
   if (i >= n) return;
   const uint32_t s = slots[i];
   const ScanRec r = tb.sc[s];
-  for (int j = 0; j < 3; ++j) {
+  _Pragma("unroll") for (int j = 0; j < 3; ++j) {
     hd.ent[(size_t)j * hd.n + base + i] = hent(j, r, s);
     hd.hix[(size_t)j * hd.n + s] = base + i;
   }
@@ -599,7 +599,7 @@ __device__ inline void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bo
   o.count = (uint8_t)(cf & 0xffu);
   o.flags = (uint8_t)(cf >> 8);
   uint32_t ix[3];
-  for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
+  _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
   const uint32_t n = W.count();
   // pop_process_request's heap calls, on the unreduced front (:1063-1069)
   ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o, s));
