@@ -279,9 +279,13 @@ def prepare(q, args, tab, pre):
     settle pulls."""
     q.register_active(tab.slots, tab.r, tab.w, tab.l)
     chunk = 1 << 20
+    t0 = time.perf_counter()
     for i in range(0, len(pre), chunk):
         rc = q.add_batch(pre[i:i + chunk])
         assert (rc == 0).all(), np.unique(rc)
+        if args.heap_order:  # (minutes in heap order: progress for the log)
+            print(f"prepare: {i + chunk} adds, {time.perf_counter() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
     settle = args.settle if args.settle is not None else \
         args.depth * args.clients // 2
     t_pre = float(pre["time"][-1])
@@ -290,6 +294,9 @@ def prepare(q, args, tab, pre):
         k = min(settle - done, 1 << 20)
         d, res = q.pull_batch(t_pre, k)
         done += k
+        if args.heap_order:
+            print(f"prepare: {done} settle pulls, {time.perf_counter() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
         if res.n_decisions < k:
             break
     return settle
@@ -496,6 +503,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
+        if args.heap_order:
+            print(f"step {i}", file=sys.stderr, flush=True)
     q.sync()  # (the last call's round read: with pipelining it is finished here)
     torch.cuda.synchronize()
     if dist:

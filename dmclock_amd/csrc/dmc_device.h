@@ -20,6 +20,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// k_chain_scan's batch stamp in ScanRec::stamp (1), or a separate 32-bit
+// touch array (0, rounds 4's layout, for A/B)
+#ifndef DMC_STAMP_SC
+#define DMC_STAMP_SC 1
+#endif
+
 namespace dmc {
 
 constexpr double kInf = __builtin_huge_val();
@@ -66,7 +72,10 @@ struct alignas(32) ScanRec {
   double r, pk, l;
   uint8_t head, count;  // request ring cursor (ring capacity <= 64)
   uint8_t flags;        // F_*
-  uint8_t pad0;
+  uint8_t stamp;        // the low byte of the epoch of the last add batch that
+                        // filed the slot with the scan running beside the add
+                        // chain (k_chain_scan's scan leaves such slots to the
+                        // chain); cleared for every slot when the epoch wraps
   uint32_t nadd;        // the add batch in flight: the client's requests in it
                         // (k_add_link's atomic; k_add_chain resets it; 0
                         // outside a batch)
@@ -134,7 +143,7 @@ __device__ inline void st_as(void* p, const T& v) {
   __builtin_memcpy(__builtin_assume_aligned(p, alignof(T)), &v, sizeof(T));
 }
 
-// The ScanRec cursor word -- head | count << 8 | flags << 16 | pad0 << 24 |
+// The ScanRec cursor word -- head | count << 8 | flags << 16 | stamp << 24 |
 // nadd << 32 -- read and written whole (8-aligned at offset 24).
 __device__ inline uint64_t cursor_load(const ScanRec* r) {
   return ld_as<uint64_t>(reinterpret_cast<const char*>(r) + offsetof(ScanRec, head));

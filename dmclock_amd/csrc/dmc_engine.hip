@@ -168,9 +168,19 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
   }
   uint32_t pos = atomicAdd(&tb.sc[s].nadd, 1u);
   apos[i] = pos;
-  if (p.epoch) tb.touch[s] = p.epoch;  // (k_chain_scan's scan leaves the slot)
+  // (k_chain_scan's scan leaves the slot: the stamp on the line the atomic
+  // just took, or the separate touch array)
+  if (p.epoch) {
+    if (DMC_STAMP_SC) tb.sc[s].stamp = (uint8_t)p.epoch;
+    else tb.touch[s] = p.epoch;
+  }
   // (filing order 0 replays the client's requests and knows its own position)
   if (pos - 1u < kAddSlots - 1u) abuf[(size_t)s * kAddSlots + pos] = i;
+}
+// the epoch wrapped: no slot may keep a stamp equal to a later batch's
+__global__ void k_clear_stamps(Table tb) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < tb.n) tb.sc[s].stamp = 0;
 }
 __global__ void 
 k_add_link(AddParams p, Table tb,
@@ -4796,8 +4806,12 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       // later batch's epoch)
       uint32_t epoch = 0;
       if (overlap_ok(q, n)) {
-        if (++q->epoch == 0) {
-          HIP_OK(hipMemsetAsync(q->tb.touch, 0, 4ull * q->p.max_clients, q->stream));
+        if (++q->epoch == (DMC_STAMP_SC ? 256u : 0u)) {
+          if (DMC_STAMP_SC)
+            hipLaunchKernelGGL(k_clear_stamps, dim3((q->tb.n + kBlock - 1) / kBlock),
+                               dim3(kBlock), 0, q->stream, q->tb);
+          else
+            HIP_OK(hipMemsetAsync(q->tb.touch, 0, 4ull * q->p.max_clients, q->stream));
           q->epoch = 1;
         }
         epoch = q->epoch;

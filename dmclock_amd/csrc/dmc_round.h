@@ -560,7 +560,8 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
     mine[j] = s < tb.n;
     if (s < tb.n) {
       const ScanRec r = tb.sc[s];
-      if (TOUCHED && tb.touch[s] == cp.epoch) mine[j] = false;  // (the add chain's)
+      if (TOUCHED && (DMC_STAMP_SC ? r.stamp == (uint8_t)cp.epoch : tb.touch[s] == cp.epoch))
+        mine[j] = false;  // (the add chain's)
       x[j].c = mine[j] ? r.count : 0;
       x[j].h = r.head;
       x[j].fr = r.r;

@@ -17,6 +17,8 @@
 #     heap             bench.py --heap-order (tie-exact mode at config 3)
 #     lat              tests/cpp/latency at 1M clients (serve path)
 #     heaptime         tools/heap_timing.py at $HEAP_N clients (heap order vs oracle)
+#     rankbins         tools/rank_bins.py: k_rrank's per-bin clocks over 40 debug rounds
+#     probe            tools/rand_probe: random-record read rates (64/128-byte shapes)
 #     variants         $VARIANTS alternated $ROUNDS times (scripts/gpu_variants.sh)
 #   $BENCH_ARGS is appended to every bench.py command.
 set -o pipefail
@@ -77,6 +79,8 @@ for step in "$@"; do
     lat) run lat 300 tests/cpp/latency 1048576 2000 --serve || exit 1 ;;
     heaptime) run heaptime_${HEAP_N:-65536} 600 python -u tools/heap_timing.py ${HEAP_N:-65536} 2 ${HEAP_ARGS} || exit 1 ;;
     variants) bash scripts/gpu_variants.sh || exit 1 ;;
+    rankbins) run rankbins 300 python -u tools/rank_bins.py 40 || exit 1 ;;
+    probe) run probe 200 tools/rand_probe || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
