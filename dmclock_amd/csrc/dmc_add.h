@@ -324,6 +324,10 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
   double cur_p = prev_p0;
   uint32_t chg_last = 0xffffffffu, act_q = 0xffffffffu;
   auto step = [&](uint32_t pos) {
+    // (heap order: the reference's heap calls for this request, below)
+    const uint32_t cnt_before = st.count;
+    const bool activating = tb.hev && act.cold && idle0 && !act_done &&
+                            p.reqs[pos].rho <= p.reqs[pos].delta;
     if (tf) {  // get_req_params, batch order
       dmc_request rq = pos == i ? rq1 : p.reqs[pos];
       rq.delta = rq.rho = 0;
@@ -336,6 +340,15 @@ __device__ inline void add_chain_slot(const Table& tb, const AddParams& p, uint3
       add_one(tb, st, ring, p, pos, &rq);
     } else {
       add_one(tb, st, ring, p, pos, pos == i ? &rq1 : nullptr);
+    }
+    if (tb.hev) {
+      // an accepted request: adjust x 3, twice for a client's first (:996-1016);
+      // a refused activation: the idle reset's prop_delta moved the ready
+      // key of a client with requests, and no heap call follows (:989-993)
+      uint8_t e = 0;
+      if (p.rc[pos] == DMC_OK) e = cnt_before == 0 ? 3 : 2;
+      else if (activating && st.count > 0) e = 1;
+      tb.hev[pos] = e;
     }
     if (!act.cold) return;
     if (idle0) {

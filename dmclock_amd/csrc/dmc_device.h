@@ -113,6 +113,11 @@ struct Table {
   // per slot: the epoch of the last add batch that filed it with the scan
   // running beside the add chain (AddParams::epoch, k_chain_scan)
   uint32_t* touch;
+  // DMC_OPT_HEAP_ORDER: per position of the running add batch, the heap calls
+  // the reference makes for it (k_add_chain writes, k_heap_events replays:
+  // 0 none, 1 a key changed with no heap call, 2 adjust x 3, 3 adjust x 3
+  // twice); else null
+  uint8_t* hev;
 };
 
 __host__ __device__ inline uint64_t dbits(double x) {

@@ -159,6 +159,7 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
     act.hard[i] = 0u;
     if (i == 0) *act.anyhard = 0u;
   }
+  if (tb.hev) tb.hev[i] = 0;  // (positions the chain never visits: no heap call)
   uint32_t s = p.reqs[i].slot;
   aslot[i] = s;
   if (s >= tb.n) {
@@ -2104,6 +2105,7 @@ struct dmc_queue {
   dmc_request* d_reqs = nullptr;
   int32_t* d_rc = nullptr;
   uint32_t *apos = nullptr, *aslot = nullptr;   // per batch request
+  uint8_t* d_hev = nullptr;                      // per batch request: heap events (Table::hev)
   uint32_t* abuf = nullptr;  // per client: later filers' batch positions (N * kAddSlots)
   AddParams* apblk = nullptr;
   // decisions (host API)
@@ -2570,7 +2572,8 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
   if (n <= q->bcap) return DMC_OK;
   uint32_t cap = std::max<uint32_t>(n, 1024);
   if (int rc = invalidate_graphs(q)) return rc;
-  for (void** p : {(void**)&q->d_reqs, (void**)&q->d_rc, (void**)&q->apos, (void**)&q->aslot}) {
+  for (void** p : {(void**)&q->d_reqs, (void**)&q->d_rc, (void**)&q->apos, (void**)&q->aslot,
+                   (void**)&q->d_hev}) {
     if (int rc = dfree(*p)) return rc;
     *p = nullptr;
   }
@@ -2580,6 +2583,8 @@ int ensure_batch(dmc_queue* q, uint32_t n) {
   // (padded to whole blocks: k_add_chain loads them before its bounds check)
   DALLOC(q, &q->apos, sizeof(uint32_t) * (cap + kBlock));
   DALLOC(q, &q->aslot, sizeof(uint32_t) * (cap + kBlock));
+  DALLOC(q, &q->d_hev, cap);
+  q->tb.hev = q->heap ? q->d_hev : nullptr;
   q->bcap = cap;
   return DMC_OK;
 }
@@ -3846,17 +3851,39 @@ int heap_enable(dmc_queue* q, uint32_t k) {
   q->hd.n = (uint32_t)N;
   q->hd.k = k;
   q->heap = true;
+  if (int rc = invalidate_graphs(q)) return rc;  // (the captured Table gains hev)
+  q->tb.hev = q->d_hev;
   return DMC_OK;
 }
 
-// n adds in call order (d_reqs, d_rc device-resident)
+// n adds in call order (d_reqs, d_rc device-resident): the batched add path
+// (tags, Reject checks, idle resets: the reference's values, resolved in
+// parallel) leaves each position's heap calls in tb.hev; k_heap_events then
+// makes them in batch order.  (DMC_HEAP_SEQ_ADD: every add and its heap
+// calls in order on one wave, k_heap_add -- round 4's form, for A/B.)
+#ifndef DMC_HEAP_SEQ_ADD
+#define DMC_HEAP_SEQ_ADD 0
+#endif
 int heap_add(dmc_queue* q, uint32_t n, const dmc_request* d_reqs, int32_t* d_rc) {
   if (!n) return DMC_OK;
-  AddParams p{d_reqs, d_rc, q->tick, n, 0};
-  hipLaunchKernelGGL(k_heap_add, dim3(1), dim3(kHeapThreads), 0, q->stream, q->tb, q->hd, p);
+  if (DMC_HEAP_SEQ_ADD) {
+    AddParams p{d_reqs, d_rc, q->tick, n, 0};
+    hipLaunchKernelGGL(k_heap_add, dim3(1), dim3(kHeapThreads), 0, q->stream, q->tb, q->hd, p);
+    HIP_OK(hipGetLastError());
+    q->tick += n;
+    if (q->n_idle) q->idle_unknown = true;  // (activations happened on the device)
+    return DMC_OK;
+  }
+  int rc = ensure_batch(q, n);
+  if (!rc) rc = settle_act(q);
+  if (rc) return rc;
+  rc = maybe_idle(q) ? add_act_batch_dev(q, n, d_reqs, d_rc)
+                     : add_segment(q, d_reqs, n, d_rc, q->tick);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_heap_events, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, d_reqs,
+                     (const uint8_t*)q->d_hev, n);
   HIP_OK(hipGetLastError());
   q->tick += n;
-  if (q->n_idle) q->idle_unknown = true;  // (activations happened on the device)
   return DMC_OK;
 }
 
@@ -4114,7 +4141,7 @@ int dmc_queue_destroy(dmc_queue* q) {
                   q->skr, q->skp, q->red, q->sctl, q->fut_done, q->rd, q->rparts, q->bcount, q->bsup, q->dbg_bins, q->dbg_wtime, q->dbg_atime,
                   q->brec, q->act_min, q->sched, q->reqcount, q->dense, q->sa,
                   q->sb, q->lcnt, q->sparts, q->gsz, q->goff, q->gisp, q->gpoff,
-                  q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf,
+                  q->d_reqs, q->d_rc, q->apos, q->aslot, q->abuf, q->d_hev,
                   q->apblk, q->d_dec, q->stage};
   for (void* p : ptrs)
     dfree(p);
@@ -4387,16 +4414,13 @@ __device__ inline bool list_filter_slot(const Table& tb, uint32_t s, const uint8
     if (w != j) ring[(sr.head + w) & tb.qmask] = ring[(sr.head + j) & tb.qmask];
     ++w;
   }
-  ScanRec o = sr;
-  o.count = (uint8_t)m;
-  if (!kp[0] || m == 0) o.flags = (uint8_t)(o.flags & ~F_READY);
+  const uint8_t fl = (!kp[0] || m == 0) ? (uint8_t)(sr.flags & ~F_READY) : sr.flags;
+  ScanRec o{0.0, 0.0, 0.0, sr.head, (uint8_t)m, fl, sr.stamp, sr.nadd};
   if (m) {
     const ReqEntry& f = ring[sr.head & tb.qmask];
     o.r = f.r;
     o.pk = __dadd_rn(f.p, tb.rec[s].pd);
     o.l = f.l;
-  } else {
-    o.r = o.pk = o.l = 0.0;
   }
   tb.sc[s] = o;
   return true;
@@ -4417,7 +4441,9 @@ __global__ void k_list_filter(Table tb, uint32_t n, const uint32_t* slots,
 __global__ void __launch_bounds__(64) k_heap_filter(Table tb, HeapDev hd, uint32_t n,
                                                     const uint32_t* slots, const uint32_t* offs,
                                                     const uint8_t* keep) {
-  WHeaps W(tb, hd);
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
+  WHeaps W(tb, hd, cache, T);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t s = slots[i];
     uint32_t mod = 0;
@@ -4425,6 +4451,7 @@ __global__ void __launch_bounds__(64) k_heap_filter(Table tb, HeapDev hd, uint32
     wave_sync();
     if (uread(mod, 0)) W.adjust3(s);
   }
+  heap_cache_flush(hd, cache, T);
 }
 
 // do_clean's erase (:1244-1255) of the listed clients: queue dropped, slot

@@ -68,6 +68,13 @@ struct alignas(16) HEnt {
 };
 static_assert(sizeof(HEnt) == 16, "HEnt must be 16 bytes");
 constexpr uint32_t kClsNone = 3;
+// entries of each heap kept in LDS while a heap kernel runs: the top 11
+// levels of a binary heap (3 x 32 KB); a sift from the root then reaches
+// memory only below them
+#ifndef DMC_HEAP_LDS
+#define DMC_HEAP_LDS 2047
+#endif
+constexpr uint32_t kHeapLds = DMC_HEAP_LDS;
 
 struct HeapDev {
   HEnt* ent;      // [3][n] heap arrays
@@ -140,10 +147,20 @@ struct WHeap {
   uint32_t* x;    // slot -> index
   uint32_t k;     // branching
   uint32_t lane;
+  HEnt* c;        // the LDS copy of a[0, T): the heap's top levels (heap_cache_fill)
+  uint32_t T;
 
-  __device__ void put(uint32_t i, const HEnt& e) const {  // (uniform: lane 0 stores)
+  __device__ __forceinline__ HEnt ld(uint32_t i) const {
+    if (i < T) return c[i];
+    return a[i];
+  }
+  __device__ __forceinline__ void st(uint32_t i, const HEnt& e) const {
+    if (i < T) c[i] = e;
+    else a[i] = e;
+  }
+  __device__ __forceinline__ void put(uint32_t i, const HEnt& e) const {  // (uniform: lane 0 stores)
     if (lane == 0) {
-      a[i] = e;
+      st(i, e);
       x[e.slot] = i;
     }
   }
@@ -154,7 +171,7 @@ struct WHeap {
     uint32_t lv, off, D;
     uint64_t pw, g;  // K^lv, 1 + K + ... + K^(lv-1)
   };
-  __device__ Sub layout(uint32_t base) const {
+  __device__ __forceinline__ Sub layout(uint32_t base) const {
     Sub L{0, 0, 0, 1, 0};
     uint32_t avail = lane >= base ? 64u : 0u;
     // D: levels whose lanes all fit in [base, 64)
@@ -175,7 +192,7 @@ struct WHeap {
     return L;
   }
   // first lane of level l's block (levels 1..D, from `base`)
-  __device__ uint32_t level_lane(uint32_t base, uint32_t l) const {
+  __device__ __forceinline__ uint32_t level_lane(uint32_t base, uint32_t l) const {
     uint32_t u = 0;
     uint64_t pw = k;
     for (uint32_t t = 1; t < l; ++t) {
@@ -186,14 +203,14 @@ struct WHeap {
   }
 
   // the subtree below root r (this lane's node, if any and < n)
-  __device__ HEnt sub_load(const Sub& L, uint32_t r, uint32_t n, uint32_t* idx) const {
+  __device__ __forceinline__ HEnt sub_load(const Sub& L, uint32_t r, uint32_t n, uint32_t* idx) const {
     HEnt e{~0ull, kClsNone + 1, 0};
     *idx = 0xffffffffu;
     if (L.lv) {
       const uint64_t i = L.pw * (uint64_t)r + L.g + L.off;
       if (i < n) {
         *idx = (uint32_t)i;
-        e = a[i];
+        e = ld((uint32_t)i);
       }
     }
     return e;
@@ -203,7 +220,7 @@ struct WHeap {
   // levels): IndIntruHeap's moves; the moved lanes store themselves one
   // level up.  Returns true when X went below the subtree's last level
   // (*i is then the node to continue from).
-  __device__ bool down_sub(const Sub& L, uint32_t base, const HEnt& e, uint32_t eidx, uint32_t n,
+  __device__ __forceinline__ bool down_sub(const Sub& L, uint32_t base, const HEnt& e, uint32_t eidx, uint32_t n,
                            const HEnt& X, uint32_t* i) const {
     uint32_t c = *i, co = 0;
     uint32_t tgt = 0xffffffffu;
@@ -234,7 +251,7 @@ struct WHeap {
       co = co * k + mj;
     }
     if (tgt != 0xffffffffu) {
-      a[tgt] = e;
+      st(tgt, e);
       x[e.slot] = tgt;
     }
     (void)eidx;
@@ -243,7 +260,7 @@ struct WHeap {
   }
 
   // sift_down (:479-548) of X from i, n = the count it sees
-  __device__ uint32_t sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
+  __device__ __forceinline__ uint32_t sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
     if (i < n) {
       const Sub L = layout(0);
       for (;;) {
@@ -257,7 +274,7 @@ struct WHeap {
   }
 
   // ancestor t + 1 of i (lanes t < depth): index, and the depth of i
-  __device__ uint32_t ancestors(uint32_t i, uint32_t* anc) const {
+  __device__ __forceinline__ uint32_t ancestors(uint32_t i, uint32_t* anc) const {
     uint32_t d = 0, p = i, my = 0;
     while (p > 0) {
       p = k == 2 ? (p - 1) >> 1 : (p - 1) / k;
@@ -271,7 +288,7 @@ struct WHeap {
   // sift_up (:462-474) of X from i over the loaded ancestors (lane t holds
   // ancestor t + 1, t < d): X passes the leading run of ancestors it is
   // strictly less than, each moving down one node of the path
-  __device__ uint32_t up_anc(uint32_t i, const HEnt& X, uint32_t d, uint32_t anc,
+  __device__ __forceinline__ uint32_t up_anc(uint32_t i, const HEnt& X, uint32_t d, uint32_t anc,
                              const HEnt& ae) const {
     const bool lt = lane < d && hlt(X, ae);
     const uint64_t bal = __ballot(lt);
@@ -279,7 +296,7 @@ struct WHeap {
     uint32_t dst = (uint32_t)__shfl_up((int)anc, 1);  // the path's node below it
     if (lane == 0) dst = i;
     if (lane < m) {
-      a[dst] = ae;
+      st(dst, ae);
       x[ae.slot] = dst;
     }
     const uint32_t f = m ? uread(anc, m - 1) : i;
@@ -287,17 +304,17 @@ struct WHeap {
     return f;
   }
 
-  __device__ uint32_t sift_up(uint32_t i, const HEnt& X) const {
+  __device__ __forceinline__ uint32_t sift_up(uint32_t i, const HEnt& X) const {
     uint32_t anc;
     const uint32_t d = ancestors(i, &anc);
     HEnt ae{~0ull, kClsNone + 1, 0};
-    if (lane < d) ae = a[anc];
+    if (lane < d) ae = ld(anc);
     return up_anc(i, X, d, anc, ae);
   }
 
   // sift (:550-564): up if less than the parent, else down.  The ancestors
   // and the first subtree below i are loaded together.
-  __device__ uint32_t sift(uint32_t i, uint32_t n, const HEnt& X) const {
+  __device__ __forceinline__ uint32_t sift(uint32_t i, uint32_t n, const HEnt& X) const {
     if (i == 0) return sift_down(i, n, X);
     uint32_t anc;
     const uint32_t d = ancestors(i, &anc);
@@ -305,7 +322,7 @@ struct WHeap {
     HEnt ae{~0ull, kClsNone + 1, 0};
     uint32_t eidx = 0xffffffffu;
     HEnt e = ae;
-    if (lane < d) ae = a[anc];
+    if (lane < d) ae = ld(anc);
     else if (i < n) e = sub_load(L, i, n, &eidx);
     if (hlt(X, hread(ae, 0))) return up_anc(i, X, d, anc, ae);
     if (L.D == 0) return sift_down(i, n, X);  // (no lanes left for a subtree)
@@ -320,32 +337,35 @@ struct WHeaps {
   const HeapDev& hd;
   WHeap h[3];
   uint32_t lane;
-  __device__ WHeaps(const Table& t, const HeapDev& d) : tb(t), hd(d) {
+  // (cache: the LDS copy of each heap's first T entries, kHeapLds apart)
+  __device__ WHeaps(const Table& t, const HeapDev& d, HEnt* cache, uint32_t T)
+      : tb(t), hd(d) {
     lane = lane_id();
     _Pragma("unroll") for (int j = 0; j < 3; ++j)
-      h[j] = WHeap{d.ent + (size_t)j * d.n, d.hix + (size_t)j * d.n, d.k, lane};
+      h[j] = WHeap{d.ent + (size_t)j * d.n, d.hix + (size_t)j * d.n, d.k, lane,
+                   cache + j * kHeapLds, T};
   }
   __device__ uint32_t count() const { return hd.cnt[0]; }
-  __device__ HEnt top(int j) const { return hd.ent[(size_t)j * hd.n]; }
+  __device__ HEnt top(int j) const { return h[j].ld(0); }
   // slot s's index in each heap (lanes 0-2 load; uniform)
-  __device__ void index3(uint32_t s, uint32_t* ix) const {
+  __device__ __forceinline__ void index3(uint32_t s, uint32_t* ix) const {
     uint32_t v = 0;
     if (lane < 3) v = hd.hix[(size_t)lane * hd.n + s];
     _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(v, j);
   }
   // the slot's three entries from its ScanRec (loaded by every lane: one
   // request) and its three indices
-  __device__ void load3(uint32_t s, HEnt* X, uint32_t* ix) const {
+  __device__ __forceinline__ void load3(uint32_t s, HEnt* X, uint32_t* ix) const {
     const ScanRec r = tb.sc[s];
     index3(s, ix);
     _Pragma("unroll") for (int j = 0; j < 3; ++j) X[j] = hent(j, r, s);
   }
   // adjust x 3 (:996-1016, :567-625): sift in each heap, in heap order
-  __device__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
+  __device__ __forceinline__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
     const uint32_t n = count();
     _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = h[j].sift(ix[j], n, X[j]);
   }
-  __device__ void adjust3(uint32_t s) const {
+  __device__ __forceinline__ void adjust3(uint32_t s) const {
     HEnt X[3];
     uint32_t ix[3];
     load3(s, X, ix);
@@ -353,7 +373,7 @@ struct WHeaps {
   }
   // the entries rewritten in place (a key that changed without a heap call:
   // the idle reset before a Reject, :937-993)
-  __device__ void refresh3(uint32_t s) const {
+  __device__ __forceinline__ void refresh3(uint32_t s) const {
     HEnt X[3];
     uint32_t ix[3];
     load3(s, X, ix);
@@ -361,12 +381,12 @@ struct WHeaps {
   }
   // erase (delete_from_heaps): IndIntruHeap::remove (:433-445) -- the last
   // element swapped in and sifted with the count already reduced
-  __device__ void remove3(uint32_t s) const {
+  __device__ __forceinline__ void remove3(uint32_t s) const {
     uint32_t ix[3];
     index3(s, ix);
     const uint32_t last = count() - 1;
     _Pragma("unroll") for (int j = 0; j < 3; ++j) {
-      const HEnt X = h[j].a[last];
+      const HEnt X = h[j].ld(last);
       h[j].sift(ix[j], last, X);
     }
     wave_sync();
@@ -374,6 +394,23 @@ struct WHeaps {
     wave_sync();
   }
 };
+
+// The heaps' first entries into LDS at a kernel's start (every thread of the
+// block), and back at its end: T = min(count, kHeapLds).
+__device__ inline uint32_t heap_cache_fill(const HeapDev& hd, HEnt* c) {
+  const uint32_t T = min(hd.cnt[0], kHeapLds);
+  _Pragma("unroll") for (int j = 0; j < 3; ++j)
+    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x)
+      c[j * kHeapLds + i] = hd.ent[(size_t)j * hd.n + i];
+  __syncthreads();
+  return T;
+}
+__device__ inline void heap_cache_flush(const HeapDev& hd, const HEnt* c, uint32_t T) {
+  __syncthreads();
+  _Pragma("unroll") for (int j = 0; j < 3; ++j)
+    for (uint32_t i = threadIdx.x; i < T; i += blockDim.x)
+      hd.ent[(size_t)j * hd.n + i] = c[j * kHeapLds + i];
+}
 
 // ------------------------------------------------------------------ kernels
 // registration (client_map.emplace + three pushes, in the given order): new
@@ -398,15 +435,65 @@ __global__ void k_heap_count_add(HeapDev hd, uint32_t n) {
 // erase (delete_from_heaps, before the client's state goes)
 __global__ void __launch_bounds__(64) k_heap_remove(Table tb, HeapDev hd, const uint32_t* slots,
                                                     uint32_t n) {
-  WHeaps W(tb, hd);
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
+  WHeaps W(tb, hd, cache, T);
   for (uint32_t i = 0; i < n; ++i) W.remove3(slots[i]);
+  heap_cache_flush(hd, cache, T);
 }
 
 // clients whose queues a filter / remove_by_client modified, ascending
 __global__ void __launch_bounds__(64) k_heap_adjust(Table tb, HeapDev hd, const uint32_t* slots,
                                                     uint32_t n) {
-  WHeaps W(tb, hd);
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
+  WHeaps W(tb, hd, cache, T);
   for (uint32_t i = 0; i < n; ++i) W.adjust3(slots[i]);
+  heap_cache_flush(hd, cache, T);
+}
+
+// The heap calls of an add batch, in batch order.  The batched add path
+// (k_add_link, k_add_chain and, with idle clients, the activation kernels)
+// has made every request's state change with the reference's values -- tags,
+// Reject checks, idle resets -- and left in hev[i] the heap calls the
+// reference makes for request i: 3 a client's first request (adjust x 3 at
+// :996-1006 and again at :1011-1016), 2 any other accepted one (:1011-1016),
+// 1 a refused activation of a client with requests (its idle reset moved
+// the ready key, and no heap call follows, :989-993: the entries are
+// rewritten in place), 0 none.  Every call sees the slot's state after the
+// batch, which is its state at each of its events: a client's front changes
+// only at its first accepted request of the batch, its prop_delta only at
+// its activation, before any of its adjusts.  64 events are read at once.
+__global__ void __launch_bounds__(64) k_heap_events(Table tb, HeapDev hd, const dmc_request* reqs,
+                                                    const uint8_t* ev, uint32_t n) {
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
+  WHeaps W(tb, hd, cache, T);
+  const uint32_t lane = W.lane;
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    uint32_t e = 0, sl = 0;
+    if (i < n) {
+      e = ev[i];
+      if (e) sl = reqs[i].slot;
+    }
+    uint64_t m = __ballot(e != 0);
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t ej = uread(e, j), s = uread(sl, j);
+      if (ej == 1) {
+        W.refresh3(s);
+        continue;
+      }
+      HEnt X[3];
+      uint32_t ix[3];
+      W.load3(s, X, ix);
+      if (ej == 3) W.adjust3(s, X, ix);
+      W.adjust3(s, X, ix);
+    }
+  }
+  heap_cache_flush(hd, cache, T);
 }
 
 constexpr int kHeapThreads = 256;
@@ -442,14 +529,18 @@ __device__ inline double heap_idle_lowest(const Table& tb, uint64_t* sh) {
 __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd, AddParams p) {
   __shared__ uint64_t sh[kHeapThreads / 64];
   __shared__ uint32_t s_cmd;  // 1: an idle reset's minimum, 2: done
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
   if (threadIdx.x >= 64) {
     for (;;) {
       __syncthreads();
-      if (s_cmd == 2) return;
+      if (s_cmd == 2) break;
       heap_idle_lowest(tb, sh);
     }
+    heap_cache_flush(hd, cache, T);
+    return;
   }
-  WHeaps W(tb, hd);
+  WHeaps W(tb, hd, cache, T);
   const uint32_t lane = W.lane;
   for (uint32_t i = 0; i < p.n; ++i) {
     const uint32_t s = p.reqs[i].slot;
@@ -497,28 +588,51 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
   }
   if (lane == 0) s_cmd = 2;
   __syncthreads();
+  heap_cache_flush(hd, cache, T);
 }
 
 // The pop of slot s, the top of heap `hsel` (pop_process_request,
 // :1046-1073, with reduce_reservation_tags, :1077-1111, for a priority pop):
 // the decision, the front popped and (delayed) the new front's tag
 // (update_next_tag, :1021-1036), the heap calls with that state, then the
-// reduction and resv.promote.  Lane 0 makes the client's state change; the
-// wave makes the heap calls.
-__device__ inline void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
+// reduction and resv.promote.  Every lane loads the client's record, cursor
+// and the popped and next entries (one request each: the values are
+// uniform) and lane i the queue's entry i (an immediate priority pop reduces
+// every queued request: one lane each), in two levels of loads; lane 0
+// stores what is uniform.
+__device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
                                 uint64_t tick, dmc_decision* out, unsigned long long* sched) {
   const uint32_t lane = W.lane;
-  // the slot's heap indices, requested first (lanes 0-2)
+  // level 1: the slot's heap indices (lanes 0-2), cursor, record, aux, bound info
   const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
-  // lane 0: the client's state change; the front's keys before the
-  // reduction (o: what the demotes see) and its reduced r (the promote's)
-  double o_r = 0.0, o_pk = 0.0, o_l = 0.0, r_red = 0.0;
-  uint32_t o_cf = 0;
+  const ScanRec sr = tb.sc[s];
+  ClientRec cr = tb.rec[s];
+  ClientAux ax{0, 0, 0};
+  BoundInfo bi{0.0, 0.0, 0.0, 0.0};
+  if (tb.delayed) {
+    ax = tb.aux[s];
+    if (tb.binfo) bi = tb.binfo[s];
+  }
+  // level 2: the queue's entries
+  ReqEntry* ring = tb.ring + (size_t)s * tb.q;
+  const uint32_t h = sr.head, c = sr.count;
+  const uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
+  const ReqEntry popped = ring[h];
+  // the new front (delayed: its tag is computed below)
+  double fr = 0.0, fp = 0.0, fl = 0.0, farr = 0.0;
+  uint32_t fcost = 0;
+  if (nc) {
+    const ReqEntry& fe = ring[nh];
+    fr = fe.r;
+    fp = fe.p;
+    fl = fe.l;
+    farr = fe.arrival;
+    fcost = fe.cost;
+  }
+  double er = 0.0;  // lane i: queue position i's r (immediate priority pop, i >= 2)
+  const bool deep = prio && !tb.delayed && lane >= 2 && lane < c;
+  if (deep) er = ring[(h + lane) & tb.qmask].r;
   if (lane == 0) {
-    ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-    const ScanRec sr = tb.sc[s];
-    const uint32_t h = sr.head, c = sr.count;
-    const ReqEntry popped = ring[h];
     dmc_decision d;
     d.handle = popped.handle;
     d.tag_r = popped.r;
@@ -529,86 +643,76 @@ __device__ inline void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bo
     d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
     d.flags = 0;  // (the heap top is the reference's winner: no tie to flag)
     *out = d;
-    const uint32_t nh = (h + 1) & tb.qmask, nc = c - 1;
-    double rinv = tb.rec[s].r_inv;
-    if (tb.delayed && nc) {  // update_next_tag
-      ReqEntry& f = ring[nh];
-      const Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
-      Tag3 nt;
-      const uint32_t cd = tb.aux[s].cur_delta, cr = tb.aux[s].cur_rho;
-      double winv = tb.rec[s].w_inv, linv = tb.rec[s].l_inv;
-      if (tb.binfo) {  // U1: get_cli_info (:870-875) becomes client.info
-        const BoundInfo b = tb.binfo[s];
-        rinv = b.r_inv;
-        winv = b.w_inv;
-        linv = b.l_inv;
-        tb.rec[s].r_inv = rinv;
-        tb.rec[s].w_inv = winv;
-        tb.rec[s].l_inv = linv;
-      }
-      if (make_tag(pt, rinv, winv, linv, cd, cr, f.arrival, f.cost, tb.antic, &nt)) {
-        f.r = nt.r;
-        f.p = nt.p;
-        f.l = nt.l;
-        f.delta = cd;
-        f.rho = cr;
-        double pr = tb.rec[s].prev_r, pp = tb.rec[s].prev_p, pl = tb.rec[s].prev_l;
-        assign_unpinned(pr, nt.r);
-        assign_unpinned(pl, nt.l);
-        assign_unpinned(pp, nt.p);
-        tb.rec[s].prev_r = pr;
-        tb.rec[s].prev_p = pp;
-        tb.rec[s].prev_l = pl;
-        tb.rec[s].prev_arr = nt.arrival;
-        tb.aux[s].last_tick = tick;
-      }
-    }
-    ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc, (uint8_t)(sr.flags & ~F_READY), 0, 0};
-    if (nc) {
-      const ReqEntry& f = ring[nh];
-      o.r = f.r;
-      o.pk = __dadd_rn(f.p, tb.rec[s].pd);
-      o.l = f.l;
-    }
-    o_r = o.r;
-    o_pk = o.pk;
-    o_l = o.l;
-    o_cf = (uint32_t)o.count | ((uint32_t)o.flags << 8);
-    r_red = o.r;
-    if (prio) {
-      // reduce_reservation_tags (immediate: every queued request; delayed:
-      // the front) and prev r (:1077-1111)
-      const double off = resv_offset(rinv, popped.cost, popped.rho);
-      if (tb.delayed) {
-        if (nc) ring[nh].r = __dsub_rn(ring[nh].r, off);
-      } else {
-        for (uint32_t i = 1; i < c; ++i) {
-          ReqEntry& e = ring[(h + i) & tb.qmask];
-          e.r = __dsub_rn(e.r, off);
-        }
-      }
-      tb.rec[s].prev_r = __dsub_rn(tb.rec[s].prev_r, off);
-      if (nc) r_red = ring[nh].r;
-    }
-    o.r = r_red;
-    tb.sc[s] = o;
     atomicAdd(&sched[prio ? 1 : 0], 1ull);
   }
-  ScanRec o{dread(o_r, 0), dread(o_pk, 0), dread(o_l, 0), 0, 0, 0, 0, 0};
-  const uint32_t cf = uread(o_cf, 0);
-  o.count = (uint8_t)(cf & 0xffu);
-  o.flags = (uint8_t)(cf >> 8);
+  double rinv = cr.r_inv;
+  bool f_tagged = false;
+  if (tb.delayed && nc) {  // update_next_tag (every lane computes the same)
+    const Tag3 pt{popped.r, popped.p, popped.l, popped.arrival};
+    Tag3 nt;
+    double winv = cr.w_inv, linv = cr.l_inv;
+    if (tb.binfo) {  // U1: get_cli_info (:870-875) becomes client.info
+      rinv = bi.r_inv;
+      winv = bi.w_inv;
+      linv = bi.l_inv;
+      cr.r_inv = rinv;
+      cr.w_inv = winv;
+      cr.l_inv = linv;
+    }
+    if (make_tag(pt, rinv, winv, linv, ax.cur_delta, ax.cur_rho, farr, fcost, tb.antic, &nt)) {
+      fr = nt.r;
+      fp = nt.p;
+      fl = nt.l;
+      f_tagged = true;
+      assign_unpinned(cr.prev_r, nt.r);
+      assign_unpinned(cr.prev_l, nt.l);
+      assign_unpinned(cr.prev_p, nt.p);
+      cr.prev_arr = nt.arrival;
+      if (lane == 0) tb.aux[s].last_tick = tick;
+    }
+  }
+  // the front's keys before the reduction (what the demotes see)
+  ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc, (uint8_t)(sr.flags & ~F_READY), sr.stamp, 0};
+  if (nc) {
+    o.r = fr;
+    o.pk = __dadd_rn(fp, cr.pd);
+    o.l = fl;
+  }
+  const double r_pre = o.r;
+  if (prio) {
+    // reduce_reservation_tags (immediate: every queued request; delayed: the
+    // front) and prev r (:1077-1111)
+    const double off = resv_offset(rinv, popped.cost, popped.rho);
+    if (nc) fr = __dsub_rn(fr, off);
+    if (deep) ring[(h + lane) & tb.qmask].r = __dsub_rn(er, off);
+    cr.prev_r = __dsub_rn(cr.prev_r, off);
+    if (nc) o.r = fr;
+  }
+  if (lane == 0) {
+    if (nc && (f_tagged || prio)) {
+      ReqEntry& fe = ring[nh];
+      fe.r = fr;
+      if (f_tagged) {
+        fe.p = fp;
+        fe.l = fl;
+        fe.delta = ax.cur_delta;
+        fe.rho = ax.cur_rho;
+      }
+    }
+    if (tb.delayed || prio) tb.rec[s] = cr;
+    tb.sc[s] = o;
+  }
   uint32_t ix[3];
   _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
   const uint32_t n = W.count();
   // pop_process_request's heap calls, on the unreduced front (:1063-1069)
-  ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o, s));
-  ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o, s));
-  ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o, s));
-  if (prio) {  // resv_heap.promote after the reduction (:1110)
-    o.r = dread(r_red, 0);
+  ScanRec o0 = o;
+  o0.r = r_pre;
+  ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
+  ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o0, s));
+  ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o0, s));
+  if (prio)  // resv_heap.promote after the reduction (:1110)
     W.h[kHResv].sift_up(ix[kHResv], hent(kHResv, o, s));
-  }
   wave_sync();
 }
 
@@ -628,7 +732,9 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
                                                   int at_limit, uint64_t tick, dmc_decision* out,
                                                   HeapPullRes* res, dmc_pull_result* d_result,
                                                   unsigned long long* sched, int mode = 0) {
-  WHeaps W(tb, hd);
+  __shared__ HEnt cache[3 * kHeapLds];
+  const uint32_t T = heap_cache_fill(hd, cache);
+  WHeaps W(tb, hd, cache, T);
   const uint32_t lane = W.lane;
   HeapPullRes r{0, 0, 0, DMC_NEXT_RETURNING, 0.0, 0, 0};
   if (mode == 2) {
@@ -637,6 +743,7 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
     r.n = 1;
     if (pr.pend_prio) r.n_prio = 1;
     else r.n_res = 1;
+    heap_cache_flush(hd, cache, T);
     if (lane == 0) *res = r;
     return;
   }
@@ -711,6 +818,7 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
     if (pop_prio) ++r.n_prio;
     else ++r.n_res;
   }
+  heap_cache_flush(hd, cache, T);
   if (lane) return;
   *res = r;
   if (d_result) {
