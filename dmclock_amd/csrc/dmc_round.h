@@ -1774,16 +1774,34 @@ __device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_
   }
 }
 
-__device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
+// A record's order key as k_rrank stages it in LDS: 16 bytes (the queue
+// position and the group's run packed), so that a bin's 512 keys take 8 KB
+// and nearly every non-empty bin's block is resident at once (24-byte keys:
+// 15.9 KB per block, ten per CU -- two generations of blocks per round);
+// the ring index is read from the record when the pop is placed.
+struct BKeyS {
+  uint64_t okey;
+  uint32_t slot;
+  uint32_t sr;  // queue position << 16 | run
+  __device__ uint32_t seq() const { return sr >> 16; }
+  __device__ uint32_t run() const { return sr & 0xffffu; }
+};
+static_assert(sizeof(BKeyS) == 16, "BKeyS must be 16 bytes");
+__device__ inline BKeyS bkey_s(const BKey& k) {
+  return BKeyS{k.okey, k.slot, (k.seq << 16) | (k.run & 0xffffu)};
+}
+
+__device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                 uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, bool isp, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
   const bool valid = i < cnt;
-  BKey me = sh[valid ? i : 0];
+  const BKeyS me = sh[valid ? i : 0];
+  const uint32_t me_seq = me.seq();
   // the writer lane's payload (an L2 hit: the block staged the line), in
   // flight during the comparisons
-  uint32_t ci = 0, cost = 0;
+  uint32_t ci = 0, cost = 0, ridx = 0;
   uint64_t handle = 0;
   double tr = 0.0, tp = 0.0, tl = 0.0;
   if (valid && part == 0) {
@@ -1794,19 +1812,20 @@ __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uin
     tr = x.r;
     tp = x.p;
     tl = x.l;
+    ridx = x.k.ridx;
   }
   uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
   if (!valid) f1 = f0;
   uint32_t rank = 0, gl = 0, tie = 0;
 #pragma unroll 4
   for (uint32_t f = f0; f < f1; ++f) {
-    const BKey o = sh[f];
+    const BKeyS o = sh[f];
     uint32_t eqk = o.okey == me.okey;
     uint32_t less = (uint32_t)(o.okey < me.okey) |
                     (eqk & ((uint32_t)(o.slot < me.slot) |
-                            ((uint32_t)(o.slot == me.slot) & (uint32_t)(o.seq < me.seq))));
+                            ((uint32_t)(o.slot == me.slot) & (uint32_t)(o.seq() < me_seq))));
     rank += less;
-    gl += less * (isp ? 1u + o.run : 1u);
+    gl += less * (isp ? 1u + o.run() : 1u);
     tie |= eqk & (uint32_t)(o.slot != me.slot);
   }
   for (uint32_t d = 1; d < parts; d <<= 1) {
@@ -1815,8 +1834,8 @@ __device__ inline void rank_rec(Round* rd, const BKey* sh, const BRecR* src, uin
     tie |= __shfl_xor(tie, d);
   }
   if (valid && part == 0)
-    place_rec(rd, me, ci, cost, handle, tr, tp, tl, rank, gl, tie, isp, k, n_pgroups, soff,
-              poff, ring, out, decof);
+    place_rec(rd, BKey{me.okey, me.slot, me_seq, me.run(), ridx}, ci, cost, handle, tr, tp, tl,
+              rank, gl, tie, isp, k, n_pgroups, soff, poff, ring, out, decof);
 }
 
 // One block per rank bin.  The bin's order keys are staged in LDS; each
@@ -1843,11 +1862,11 @@ constexpr int kRankBlocksR = kNBR;
 #define DMC_RANK_SORT_MIN 256
 #endif
 constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
-__device__ inline bool bkey_less(const BKey& x, const BKey& y) {
+__device__ inline bool bkey_less(const BKeyS& x, const BKeyS& y) {
   return x.okey < y.okey ||
-         (x.okey == y.okey && (x.slot < y.slot || (x.slot == y.slot && x.seq < y.seq)));
+         (x.okey == y.okey && (x.slot < y.slot || (x.slot == y.slot && x.seq() < y.seq())));
 }
-__device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, uint32_t cnt,
+__device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                    bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
                                    uint32_t poff, ReqEntry* ring, dmc_decision* out,
                                    uint32_t* decof) {
@@ -1882,7 +1901,7 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
   for (uint32_t h = 0; h < RP; ++h) {
     const uint32_t r = RP * t + h;
     ix[h] = r < cnt ? ord[r] : 0u;
-    z[h] = r < cnt ? (isp ? 1u + sh[ix[h]].run : 1u) : 0u;
+    z[h] = r < cnt ? (isp ? 1u + sh[ix[h]].run() : 1u) : 0u;
     zs += z[h];
   }
   const uint32_t lane = t & 63, w = t >> 6;
@@ -1898,24 +1917,24 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
   // count of their heads, each run's flag set by any such pair (heavily
   // tied bins, config 4's activated clients, made the scans of the run
   // from every member quadratic)
-  __shared__ uint32_t runtie[kBinCapR];
+  __shared__ uint8_t runtie[kBinCapR];  // (bytes: the block's LDS stays under 10 KB)
   __shared__ uint32_t wrun[kRankThreads / 64];
   uint32_t hd = 0, dd = 0, nh = 0;  // per position h: bit h
 #pragma unroll
   for (uint32_t h = 0; h < RP; ++h) {
     const uint32_t r = RP * t + h;
     if (r >= cnt) continue;
-    const BKey me = sh[ix[h]];
+    const BKeyS me = sh[ix[h]];
     bool head = true, diff = false;
     if (r > 0) {
-      const BKey pv = sh[ord[r - 1]];
+      const BKeyS pv = sh[ord[r - 1]];
       head = pv.okey != me.okey;
       diff = !head && pv.slot != me.slot;
     }
     hd |= (head ? 1u : 0u) << h;
     dd |= (diff ? 1u : 0u) << h;
     nh += head ? 1u : 0u;
-    runtie[r] = 0u;
+    runtie[r] = 0;
   }
   const uint32_t rincl = wscan_u32(nh);
   if (lane == 63) wrun[w] = rincl;
@@ -1930,7 +1949,7 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
     for (uint32_t h = 0; h < RP; ++h) {
       c += (hd >> h) & 1u;
       runid[h] = c - 1u;  // (position 0 is a head: c >= 1 for every position < cnt)
-      if ((dd >> h) & 1u) runtie[c - 1u] = 1u;
+      if ((dd >> h) & 1u) runtie[c - 1u] = 1;
     }
   }
   __syncthreads();
@@ -1941,10 +1960,9 @@ __device__ inline void rank_sorted(Round* rd, const BKey* sh, const BRecR* src, 
     ex += z[h];
     if (r >= cnt) continue;
     const uint32_t i = ix[h];
-    const BKey me = sh[i];
     const uint32_t tie = runtie[runid[h]];
     const BRecR& x = src[i];
-    place_rec(rd, me, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, exh, tie, isp, k,
+    place_rec(rd, x.k, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, exh, tie, isp, k,
               n_pgroups, soff, poff, ring, out, decof);
   }
 }
@@ -1973,7 +1991,7 @@ constexpr uint32_t kBinMaxReport = 128;
 
 __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime) {
   if (rd->skip) return;
-  __shared__ BKey sh[kBinCapR];
+  __shared__ BKeyS sh[kBinCapR];
   // the bin's records, its group and P-group offsets, P groups, the round's
   // outcome check
   __shared__ uint32_t s_hdr[5];
@@ -2059,7 +2077,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
   const uint32_t cnt = s_hdr[0];
   if (cnt == 0 || fail0 || s_hdr[4]) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
-  for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) sh[i] = src[i].k;
+  for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) sh[i] = bkey_s(src[i].k);
   if (cnt > kRankSortMin) {
     rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof);
     if (wtime && threadIdx.x == 0) {
