@@ -32,10 +32,12 @@ def build(force=False, verbose=True):
     if not force and up_to_date():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + HIPCC_FLAGS + ["-o", LIB] + SOURCES
+    tmp = LIB + ".tmp"
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
+    os.replace(tmp, LIB)  # (atomic: a snapshot never sees a half-written library)
     return LIB
 
 

@@ -261,6 +261,7 @@ struct WHeap {
 
   // sift_down (:479-548) of X from i, n = the count it sees
   __device__ __forceinline__ uint32_t sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (k == 2) return k2_sift_down(i, n, X);
     if (i < n) {
       const Sub L = layout(0);
       for (;;) {
@@ -306,15 +307,109 @@ struct WHeap {
 
   __device__ __forceinline__ uint32_t sift_up(uint32_t i, const HEnt& X) const {
     uint32_t anc;
-    const uint32_t d = ancestors(i, &anc);
+    const uint32_t d = k == 2 ? k2_ancestors(i, &anc) : ancestors(i, &anc);
     HEnt ae{~0ull, kClsNone + 1, 0};
     if (lane < d) ae = ld(anc);
     return up_anc(i, X, d, anc, ae);
   }
 
+  // ---- K = 2 (the reference's default): a fixed subtree layout -- lane j <
+  // 62 holds node (level L = log2(j + 2), offset j + 2 - 2^L) of the five
+  // levels below the root, whose index is ((r + 1) << L) - 1 + offset; lane
+  // j's children are lanes 2j + 2 and 2j + 3, so each lane picks its
+  // smaller child itself (IndIntruHeap's K == 2 rule: the right one only if
+  // strictly less, :514-548) and the path is then four lane reads.
+  __device__ __forceinline__ uint32_t k2_lv() const {
+    return lane < 62 ? 31u - __builtin_clz(lane + 2) : 0u;
+  }
+  // this lane's node below root r (~0: none, or >= n)
+  __device__ __forceinline__ uint32_t k2_idx(uint32_t r, uint32_t n) const {
+    const uint32_t L = k2_lv();
+    if (!L) return 0xffffffffu;
+    const uint64_t i = (((uint64_t)r + 1) << L) - 1 + (lane + 2 - (1u << L));
+    return i < n ? (uint32_t)i : 0xffffffffu;
+  }
+  // the path of X down the loaded subtree below r: the moved lanes store
+  // themselves at their parents; returns true when X passed the subtree's
+  // last level (*r is then the node to continue from), else X's node in *r
+  __device__ __forceinline__ bool k2_down(const HEnt& e, uint32_t idx, uint32_t n, const HEnt& X,
+                                          uint32_t* r) const {
+    // each lane's chosen child and whether it is less than X (lanes < 30)
+    HEnt lc, rc;
+    const int l2 = (int)(2 * lane + 2) & 63, r2 = (int)(2 * lane + 3) & 63;
+    lc.key = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e.key >> 32), l2) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)e.key, l2);
+    lc.cls = (uint32_t)__shfl((int)e.cls, l2);
+    rc.key = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e.key >> 32), r2) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)e.key, r2);
+    rc.cls = (uint32_t)__shfl((int)e.cls, r2);
+    const uint64_t li = 2ull * idx + 1;
+    const bool hasl = idx != 0xffffffffu && li < n, hasr = hasl && li + 1 < n;
+    const bool pickr = hasr && hlt(rc, lc);
+    const uint32_t code = ((hasl && hlt(pickr ? rc : lc, X)) ? 2u : 0u) | (pickr ? 1u : 0u);
+    // the root's own choice (lanes 0 and 1 are its children)
+    const uint64_t rl = 2ull * *r + 1;
+    if (rl >= n) return false;  // (X stays at r)
+    const HEnt c0 = hread(e, 0);
+    bool p1 = false;
+    if (rl + 1 < n) p1 = hlt(hread(e, 1), c0);
+    const HEnt ch = p1 ? hread(e, 1) : c0;
+    if (!hlt(ch, X)) return false;
+    uint32_t c = p1 ? 1u : 0u;
+    uint64_t moved = 1ull << c;
+    bool cont = true;
+    for (int L = 1; L < 5; ++L) {
+      const uint32_t cc = uread(code, c);
+      if (!(cc & 2u)) {
+        cont = false;
+        break;
+      }
+      c = 2 * c + 2 + (cc & 1u);
+      moved |= 1ull << c;
+    }
+    if ((moved >> lane) & 1ull) {
+      const uint32_t pi = (idx - 1) >> 1;
+      st(pi, e);
+      x[e.slot] = pi;
+    }
+    *r = uread(idx, c);
+    return cont;
+  }
+  __device__ __forceinline__ uint32_t k2_sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
+    while (i < n) {
+      const uint32_t idx = k2_idx(i, n);
+      HEnt e{~0ull, kClsNone + 1, 0};
+      if (idx != 0xffffffffu) e = ld(idx);
+      if (!k2_down(e, idx, n, X, &i)) break;
+    }
+    put(i, X);
+    return i;
+  }
+  // ancestors of i: lane t < d holds ancestor t + 1, ((i + 1) >> (t + 1)) - 1
+  __device__ __forceinline__ uint32_t k2_ancestors(uint32_t i, uint32_t* anc) const {
+    const uint32_t d = 31u - __builtin_clz(i + 1);
+    *anc = lane < d ? ((i + 1) >> (lane + 1)) - 1 : 0u;
+    return d;
+  }
+  __device__ __forceinline__ uint32_t k2_sift(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (i == 0) return k2_sift_down(i, n, X);
+    uint32_t anc;
+    const uint32_t d = k2_ancestors(i, &anc);
+    // the ancestors and the first subtree in one round trip (two loads per lane)
+    HEnt ae{~0ull, kClsNone + 1, 0}, e{~0ull, kClsNone + 1, 0};
+    const uint32_t idx = i < n ? k2_idx(i, n) : 0xffffffffu;
+    if (lane < d) ae = ld(anc);
+    if (idx != 0xffffffffu) e = ld(idx);
+    if (hlt(X, hread(ae, 0))) return up_anc(i, X, d, anc, ae);
+    if (i < n && k2_down(e, idx, n, X, &i)) return k2_sift_down(i, n, X);
+    put(i, X);
+    return i;
+  }
+
   // sift (:550-564): up if less than the parent, else down.  The ancestors
   // and the first subtree below i are loaded together.
   __device__ __forceinline__ uint32_t sift(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (k == 2) return k2_sift(i, n, X);
     if (i == 0) return sift_down(i, n, X);
     uint32_t anc;
     const uint32_t d = ancestors(i, &anc);
@@ -470,28 +565,62 @@ __global__ void __launch_bounds__(64) k_heap_events(Table tb, HeapDev hd, const 
   const uint32_t T = heap_cache_fill(hd, cache);
   WHeaps W(tb, hd, cache, T);
   const uint32_t lane = W.lane;
-  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+  const uint32_t cnt = W.count();
+  for (uint32_t i0 = 0; i0 < n;) {
+    // a window of 64 events, one per lane
     const uint32_t i = i0 + lane;
     uint32_t e = 0, sl = 0;
     if (i < n) {
       e = ev[i];
       if (e) sl = reqs[i].slot;
     }
-    uint64_t m = __ballot(e != 0);
-    while (m) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(m);
-      m &= m - 1;
-      const uint32_t ej = uread(e, j), s = uread(sl, j);
-      if (ej == 1) {
-        W.refresh3(s);
-        continue;
+    // Which of them must run in order.  A repeat request of a client (code
+    // 2) whose three entries already hold its key, none less than its parent
+    // and none with a child less than it, makes three sifts that move
+    // nothing (K = 2 checked here; other K run every event): the window's
+    // events before the first that may move are skipped -- each of them saw
+    // the heaps as the window found them, unchanged by the ones before.
+    bool ord = e == 1 || e == 3 || (e == 2 && hd.k != 2);
+    if (e == 2 && hd.k == 2) {
+      const ScanRec r = tb.sc[sl];
+      uint32_t hx[3];
+      _Pragma("unroll") for (int j = 0; j < 3; ++j) hx[j] = hd.hix[(size_t)j * hd.n + sl];
+      _Pragma("unroll") for (int j = 0; j < 3; ++j) {
+        const HEnt X = hent(j, r, sl);
+        const uint32_t v = hx[j];
+        const HEnt own = W.h[j].ld(v);
+        if (own.key != X.key || own.cls != X.cls) ord = true;
+        if (v > 0 && hlt(X, W.h[j].ld((v - 1) >> 1))) ord = true;
+        const uint64_t li = 2ull * v + 1;
+        if (li < cnt) {
+          const HEnt c1 = W.h[j].ld((uint32_t)li);
+          HEnt mc = c1;
+          if (li + 1 < cnt) {
+            const HEnt c2 = W.h[j].ld((uint32_t)li + 1);
+            if (hlt(c2, c1)) mc = c2;
+          }
+          if (hlt(mc, X)) ord = true;
+        }
       }
+    }
+    const uint64_t m = __ballot(ord);
+    if (!m) {
+      i0 += 64;
+      continue;
+    }
+    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+    const uint32_t ej = uread(e, j), s = uread(sl, j);
+    if (ej == 1) {
+      W.refresh3(s);
+    } else {
       HEnt X[3];
       uint32_t ix[3];
       W.load3(s, X, ix);
       if (ej == 3) W.adjust3(s, X, ix);
       W.adjust3(s, X, ix);
     }
+    wave_sync();
+    i0 += j + 1;
   }
   heap_cache_flush(hd, cache, T);
 }
