@@ -5119,8 +5119,15 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         if (kPrePickM)
           hipLaunchKernelGGL(k_rpick_m, dim3(1, S), dim3(kEmitThreads), 0, st,
                              (const RHistArgs*)(d + g->o_hist));
-        hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
-                           (const REmitArgs*)(d + g->o_emit));
+        if (kPrePickM && DMC_SPLIT_EMIT_M) {
+          hipLaunchKernelGGL(k_rsel_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
+                             (const REmitArgs*)(d + g->o_emit));
+          hipLaunchKernelGGL(k_rwalk_m, dim3(gEm, S), dim3(kWalkThreads), 0, st,
+                             (const REmitArgs*)(d + g->o_emit));
+        } else {
+          hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
+                             (const REmitArgs*)(d + g->o_emit));
+        }
         hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads), 0, st,
                            (const RRankArgs*)(d + g->o_rank));
         hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmit * gEm + 1, S), dim3(kBlockR), 0,

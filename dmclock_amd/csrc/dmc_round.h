@@ -2696,6 +2696,156 @@ __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const R
   remit_t_body<false, kPrePickM>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof,
                                  x.brec, x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
 }
+// Queue groups, split emission (DMC_SPLIT_EMIT_M): k_remit_m's two halves
+// as two launches.  A k_remit_m block (one per CU: its candidate list and
+// ring staging fill the LDS) walks the few candidates of its 4,096 slots
+// (about 140 per table block at config 5's 2M slots: eight per wave) before
+// the next block may start, so a group's 4,096 emit blocks ran in sixteen
+// generations, each as long as one walk.  Here the selection streams the
+// keys and writes each block's candidates (and each candidate's first-key
+// quantum, in decof until the walk replaces it) with small LDS, and the
+// walks run in blocks of kWalkThreads with one staging slice per thread:
+// several blocks per CU, many walks in flight.  The records, their order
+// and every state change are k_remit_m's (the same emit_one).
+#ifndef DMC_SPLIT_EMIT_M
+#define DMC_SPLIT_EMIT_M 1
+#endif
+#ifndef DMC_WALK_THREADS
+#define DMC_WALK_THREADS 128
+#endif
+constexpr int kWalkThreads = DMC_WALK_THREADS;
+__device__ __attribute__((always_inline)) inline void rsel_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, uint32_t* decof) {
+  if (rd->skip) return;
+  __shared__ uint32_t s_tot;
+  __shared__ uint32_t s_cnt[2];
+  __shared__ PhaseSel s_ph[2];
+  if (threadIdx.x < 2) {
+    s_cnt[threadIdx.x] = 0;
+    s_ph[threadIdx.x] = rd->ph[threadIdx.x];
+  }
+  if (threadIdx.x == 0) s_tot = 0;
+  const uint32_t n = tb.n;
+  const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
+  const bool p_runs = rd->p_runs != 0;
+  const int lane = threadIdx.x & 63;
+  uint32_t kr[kEmitPer], kp[kEmitPer], mt[kEmitPer];
+  if (s0 + kEmitPer <= n) {
+#pragma unroll
+    for (int j = 0; j < kEmitPer / 2; ++j) {
+      const uint4 a = ld_as<uint4>(k32 + s0 + 2 * j);
+      kr[2 * j] = a.x; kp[2 * j] = a.y; kr[2 * j + 1] = a.z; kp[2 * j + 1] = a.w;
+    }
+#pragma unroll
+    for (int j = 0; j < kEmitPer / 4; ++j) {
+      const uint4 m = ld_as<uint4>(meta + s0 + 4 * j);
+      mt[4 * j] = m.x; mt[4 * j + 1] = m.y; mt[4 * j + 2] = m.z; mt[4 * j + 3] = m.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kEmitPer; ++j) {
+      const bool in = s0 + j < n;
+      const uint2 k = in ? k32[s0 + j] : make_uint2(0xffffffffu, 0xffffffffu);
+      kr[j] = k.x;
+      kp[j] = k.y;
+      mt[j] = in ? meta[s0 + j] : 0;
+    }
+  }
+  __syncthreads();  // (s_ph, s_cnt, s_tot)
+  const CandPred pred(s_ph, p_runs);
+  uint32_t bits = 0, cnt = 0, nr = 0, np = 0;
+#pragma unroll
+  for (int j = 0; j < kEmitPer; ++j) {
+    if (s0 + j >= n) continue;
+    const bool cr = pred.TR && kr[j] <= pred.TR32;
+    const bool cp = pred.TP && kp[j] <= pred.TP32;
+    if (cr || cp) bits |= ((cr ? 1u : 0u) | (cp ? 2u : 0u)) << (2 * j);
+    cnt += (cr || cp) ? 1u : 0u;
+    nr += cr ? 1u : 0u;
+    np += cp ? 1u : 0u;
+  }
+  const bool sampled = rd->sampled != 0;
+  if (sampled) {
+    nr = wsum_all(nr);
+    np = wsum_all(np);
+    if (lane == 0) {
+      atomicAdd(&s_cnt[0], nr);
+      atomicAdd(&s_cnt[1], np);
+    }
+  }
+  const uint32_t incl = wscan_u32(cnt);
+  const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  uint32_t wbase = 0;
+  if (lane == 0 && wtot) wbase = atomicAdd(&s_tot, wtot);
+  wbase = __shfl(wbase, 0);
+  const uint32_t cbase = blockIdx.x * kEmitChunk;
+  uint32_t o = wbase + incl - cnt;
+#pragma unroll
+  for (int j = 0; j < kEmitPer; ++j) {
+    const uint32_t b = (bits >> (2 * j)) & 3u;
+    const uint8_t f = (uint8_t)(mt[j] >> 8);
+    if (b) {
+      cand[cbase + o] = CandRec{s0 + j, (uint8_t)(f | (b << 4)), (uint8_t)mt[j],
+                                (uint8_t)(mt[j] >> 16), (uint8_t)(mt[j] >> 24)};
+      decof[cbase + o] = (b & 1u) ? kr[j] : kp[j];  // (the walk's first-key quantum)
+      ++o;
+    } else if (s0 + j < n && (f & F_PMARK)) {
+      // a non-candidate settles its pending limit-scan mark
+      tb.sc[s0 + j].flags = (uint8_t)((f & ~F_PMARK) | (p_runs ? F_READY : 0));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bcand[blockIdx.x] = s_tot;
+    if (s_tot) atomicAdd(&rd->n_cand, s_tot);
+    if (sampled) {
+      uint32_t* cc = rd->ccnt + 2 * (blockIdx.x % kCntShards);
+      if (s_cnt[0]) atomicAdd(&cc[0], s_cnt[0]);
+      if (s_cnt[1]) atomicAdd(&cc[1], s_cnt[1]);
+    }
+  }
+}
+// the walks of emit block `seg`'s candidates (blockIdx.x = seg)
+__device__ __attribute__((always_inline)) inline void rwalk_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap) {
+  if (rd->skip) return;
+  __shared__ uint32_t ltab[2 * kHistBinsR];
+  __shared__ PhaseSel s_ph[2];
+  __shared__ unsigned long long s_sup[kNSup];
+  __shared__ uint32_t s_ec[4];
+  __shared__ ReqEntry stage[kWalkThreads * kEmitStage];
+  const uint32_t seg = blockIdx.x;
+  const uint32_t tot = bcand[seg];
+  if (tot == 0) return;
+  for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += kWalkThreads)
+    st_as(ltab + 4 * i, ld_as<uint4>(hist + kShards * 2 * kHistBinsR + 4 * i));
+  if (threadIdx.x < 2) s_ph[threadIdx.x] = rd->ph[threadIdx.x];
+  if (threadIdx.x < kNSup) s_sup[threadIdx.x] = 0;
+  if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t cbase = seg * kEmitChunk;
+  for (uint32_t i = threadIdx.x; i < tot; i += kWalkThreads) {
+    const uint32_t ci = cbase + i;
+    const CandRec c = cand[ci];
+    const uint32_t key0 = decof[ci];
+    const uint32_t cat = emit_one<false>(tb, rd, s_ph, c, ci, brec, bcount, s_sup, ltab, dense,
+                                         dcap, post, decof, stage + threadIdx.x * kEmitStage,
+                                         key0);
+    atomicAdd(&s_ec[cat], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 && s_ec[threadIdx.x]) atomicAdd(&rd->ecnt[threadIdx.x], s_ec[threadIdx.x]);
+  if (brec && threadIdx.x < kNSup && s_sup[threadIdx.x])
+    atomicAdd(&gsup[threadIdx.x], s_sup[threadIdx.x]);
+}
+__global__ void __launch_bounds__(kEmitThreads) k_rsel_m(const REmitArgs* a) {
+  const REmitArgs& x = a[blockIdx.y];
+  rsel_body(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.decof);
+}
+__global__ void __launch_bounds__(kWalkThreads) k_rwalk_m(const REmitArgs* a) {
+  const REmitArgs& x = a[blockIdx.y];
+  rwalk_body(x.tb, x.rd, x.cand, x.bcand, x.post, x.decof, x.brec, x.bcount, x.gsup, x.hist,
+             x.dense, x.dcap);
+}
+
 __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
   const RRankArgs& x = a[blockIdx.y];
   rrank_body(x.rd, x.bcount, x.gsup, x.brec, x.ring, x.decof, nullptr);
