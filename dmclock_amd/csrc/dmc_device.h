@@ -26,6 +26,12 @@
 #define DMC_STAMP_SC 1
 #endif
 
+// Kernels request their first data with the gate / skip word they check
+// (one level of loads instead of two; 0: the check first, round 4's form)
+#ifndef DMC_EARLY_LOADS
+#define DMC_EARLY_LOADS 1
+#endif
+
 namespace dmc {
 
 constexpr double kInf = __builtin_huge_val();

@@ -147,8 +147,11 @@ __global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
 __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p, Table tb, uint32_t* abuf, uint32_t* apos, uint32_t* aslot, AddParams* pblk, ActBuf act) {
-  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // (the request's slot requested with the gate word: one level of loads)
+  uint32_t s = 0;
+  if (DMC_EARLY_LOADS && i < p.n) s = p.reqs[i].slot;
+  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
   if (i == 0) *pblk = p;
   if (i >= p.n) return;
   if (act.cold) {
@@ -160,7 +163,7 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
     if (i == 0) *act.anyhard = 0u;
   }
   if (tb.hev) tb.hev[i] = 0;  // (positions the chain never visits: no heap call)
-  uint32_t s = p.reqs[i].slot;
+  if (!DMC_EARLY_LOADS) s = p.reqs[i].slot;
   aslot[i] = s;
   if (s >= tb.n) {
     apos[i] = kNone;
@@ -228,16 +231,24 @@ constexpr int kScanChainSlots = DMC_CHAIN_SCAN_SLOTS;
 
 // the chain side: block bid of the batch (tf: a queue group's trackers)
 __device__ __attribute__((always_inline)) inline void chain_scan_chain(
-    const Table& tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
+    const Table& tb, const AddParams& p, const uint32_t* abuf, const uint32_t* apos,
     const uint32_t* aslot, const TrackFill* tf, double now, uint64_t* keyr, uint64_t* keyp,
     uint32_t* meta, uint64_t* skr, uint64_t* skp, uint2* k32, RoundPart* part, uint32_t bid) {
-  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
+  if (!DMC_EARLY_LOADS && tb.gate && *tb.gate) return;
   const uint32_t i = bid * kBlock + threadIdx.x;
-  // (one level of loads: the call's parameters and this position's filing;
-  // apos / aslot are padded to whole blocks)
-  const AddParams p = *pblk;
+  // (one level of loads: this position's filing, with the request itself --
+  // the call's parameters are kernel arguments; apos / aslot are padded to
+  // whole blocks)
   const uint32_t pos0 = apos[i];
   const uint32_t s = aslot[i];
+  // (this position's request with them: add_chain_slot's first load of it
+  // is then no level of its own)
+  dmc_request rq0{};
+  if (i < p.n) rq0 = p.reqs[i];
+  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate; its word requested with
+  // the loads above)
+  if (DMC_EARLY_LOADS && tb.gate && *tb.gate) return;
+  keep((double)rq0.time);
   RoundPart acc = rpart_ident();
   if (i < p.n) {
     if (pos0 == kNone) {
@@ -293,7 +304,7 @@ __device__ __attribute__((always_inline)) inline void chain_scan_chain(
 }
 
 __global__ void __launch_bounds__(kBlock)
-k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32_t* apos,
+k_chain_scan(Table tb, AddParams ap, const uint32_t* abuf, const uint32_t* apos,
              const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
              uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
              uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
@@ -303,7 +314,7 @@ k_chain_scan(Table tb, const AddParams* pblk, const uint32_t* abuf, const uint32
                                                        nscan);
     return;
   }
-  chain_scan_chain(tb, pblk, abuf, apos, aslot, nullptr, cp.now, keyr, keyp, meta, skr, skp,
+  chain_scan_chain(tb, ap, abuf, apos, aslot, nullptr, cp.now, keyr, keyp, meta, skr, skp,
                    k32, parts + nscan + blockIdx.x, blockIdx.x);
 }
 
@@ -3329,7 +3340,7 @@ void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp)
           q->apos, q->aslot, q->apblk, ActBuf{});
   const uint32_t nS = (tb.n + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
   klaunch(q, DMC_PROF_CHAIN_SCAN, k_chain_scan, dim3(g + nS), dim3(kBlock), 0, tb,
-          (const AddParams*)q->apblk, (const uint32_t*)q->abuf, (const uint32_t*)q->apos,
+          ap, (const uint32_t*)q->abuf, (const uint32_t*)q->apos,
           (const uint32_t*)q->aslot, g, nS, sampled ? nullptr : q->keyr,
           sampled ? nullptr : q->keyp, q->meta, q->rparts, q->rd, cp,
           sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32, q->hist);

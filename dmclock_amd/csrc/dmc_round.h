@@ -527,7 +527,33 @@ __device__ inline uint64_t sat_add_u64(uint64_t a, uint64_t b) {
 // runs beside the add chain, k_chain_scan)
 template <bool BRK, int T = kScanBlock, bool TOUCHED = false, int SL = kScanSlots>
 __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uint64_t* keyr, uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp, uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist, uint32_t bid, uint32_t nblk) {
-  if (tb.gate && *tb.gate) {  // (DMC_OPT_PIPELINE: the host finishes the last call first)
+  if (!DMC_EARLY_LOADS && tb.gate && *tb.gate) {
+    if (bid == 0 && threadIdx.x == 0) rd->skip = 1u;
+    return;
+  }
+  const uint32_t base = bid * T * SL + threadIdx.x;
+  ScanCols x[SL];
+  bool mine[SL];
+#pragma unroll
+  for (int j = 0; j < SL; ++j) {
+    uint32_t s = base + j * T;
+    x[j].c = 0;
+    mine[j] = s < tb.n;
+    if (s < tb.n) {
+      const ScanRec r = tb.sc[s];
+      if (TOUCHED && (DMC_STAMP_SC ? r.stamp == (uint8_t)cp.epoch : tb.touch[s] == cp.epoch))
+        mine[j] = false;  // (the add chain's)
+      x[j].c = mine[j] ? r.count : 0;
+      x[j].h = r.head;
+      x[j].fr = r.r;
+      x[j].pk = r.pk;
+      x[j].fl = r.l;
+      x[j].f = r.flags;
+    }
+  }
+  // (DMC_OPT_PIPELINE: the host finishes the last call first; the gate word
+  // requested with the slots' records)
+  if (DMC_EARLY_LOADS && tb.gate && *tb.gate) {
     if (bid == 0 && threadIdx.x == 0) rd->skip = 1u;
     return;
   }
@@ -550,26 +576,6 @@ __device__ __attribute__((always_inline)) inline void rscan_body_g(Table tb, uin
   __shared__ RoundPart sh[T];
   const double now = cp.now;
   RoundPart acc = rpart_ident();
-  const uint32_t base = bid * T * SL + threadIdx.x;
-  ScanCols x[SL];
-  bool mine[SL];
-#pragma unroll
-  for (int j = 0; j < SL; ++j) {
-    uint32_t s = base + j * T;
-    x[j].c = 0;
-    mine[j] = s < tb.n;
-    if (s < tb.n) {
-      const ScanRec r = tb.sc[s];
-      if (TOUCHED && (DMC_STAMP_SC ? r.stamp == (uint8_t)cp.epoch : tb.touch[s] == cp.epoch))
-        mine[j] = false;  // (the add chain's)
-      x[j].c = mine[j] ? r.count : 0;
-      x[j].h = r.head;
-      x[j].fr = r.r;
-      x[j].pk = r.pk;
-      x[j].fl = r.l;
-      x[j].f = r.flags;
-    }
-  }
   // every slot's first R prefix step in one level of loads
   ScanPre pre[SL];
   constexpr bool brk = BRK;
@@ -999,7 +1005,7 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
 // every k_remit block picks the thresholds and rank bins from it (no block
 // ticket, no last-block tail here).  Block 0 stores the round's totals.
 __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, const uint64_t* keyr, const uint64_t* keyp, const RoundPart* parts, uint32_t nparts, Round* rd, uint32_t* hist, int sampled, unsigned long long* bcount, unsigned long long* gsup) {
-  if (rd->skip) return;
+  if (!DMC_EARLY_LOADS && rd->skip) return;
   __shared__ uint32_t lh[2][kHistBinsR];
 
   for (int b = threadIdx.x; b < kHistBinsR; b += blockDim.x) {
@@ -1026,6 +1032,8 @@ __device__ __attribute__((always_inline)) inline void rhist_body(uint32_t n, con
     }
   };
   if (s < n) load(s);
+  // (the skip word requested with the keys: one level of loads)
+  if (DMC_EARLY_LOADS && rd->skip) return;
   const RoundPart tot = reduce_rparts(parts, nparts);  // (its barriers order the zeroing)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // the round's totals (a limit-break round has no reservation entries: its
@@ -1502,7 +1510,7 @@ constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
 #endif
 template <bool BRK, bool PRE = false>
 __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap, uint64_t* eclk) {
-  if (rd->skip) return;
+  if (!DMC_EARLY_LOADS && rd->skip) return;
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x] = wall_clock64();
@@ -1539,6 +1547,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   } else {
     hv = pick_load(hist);
   }
+  if (DMC_EARLY_LOADS && rd->skip) return;
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
   uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
@@ -1990,6 +1999,12 @@ __device__ inline bool sample_failed(const Round* rd) {
 constexpr uint32_t kBinMaxReport = 128;
 
 __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime) {
+  // the rank-bin counters requested with the skip word (one level of loads)
+  unsigned long long sv = 0, bv = 0;
+  if (threadIdx.x < 64) {
+    sv = gsup[threadIdx.x];
+    bv = bcount[(blockIdx.x / kSupBins) * kSupBins + threadIdx.x];
+  }
   if (rd->skip) return;
   __shared__ BKeyS sh[kBinCapR];
   // the bin's records, its group and P-group offsets, P groups, the round's
@@ -2012,8 +2027,6 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     // bin's super-bin (the rank-bin counters k_remit's walkers filled:
     // records | group sizes << 32)
     const uint32_t lane = threadIdx.x, sb = b / kSupBins, ib = b % kSupBins;
-    const unsigned long long sv = gsup[lane];
-    const unsigned long long bv = bcount[sb * kSupBins + lane];
     const uint32_t sc = (uint32_t)sv, sz = (uint32_t)(sv >> 32);
     const uint32_t bc = (uint32_t)bv, bz = (uint32_t)(bv >> 32);
     const bool psup = lane >= (uint32_t)(kNSup / 2);  // (P bins: super-bins 32..63)
@@ -2445,8 +2458,22 @@ __device__ inline void rfinish_body(const Round* rd, HostRound* h, bool round_en
 // limit-scanning pull iff the group's last decision precedes the round's
 // last priority pull (or the round is terminal); one left by a reservation
 // pop iff the priority pulls ran.
+// A PostRec's first line (everything but a run's pop): what k_rapply loads
+// for every fast candidate; a run's second line is loaded by apply_fast
+// itself (DMC_POST_LINE1; 0: both lines with the first, round 4's form)
+#ifndef DMC_POST_LINE1
+#define DMC_POST_LINE1 1
+#endif
+struct PostL1 {
+  double fr, fpk, fl, prev_r, off, r2;
+  uint32_t bits, cand;
+};
+__device__ inline PostL1 post_l1(const PostRec& p) {
+  return PostL1{p.fr, p.fpk, p.fl, p.prev_r, p.off, p.r2, p.bits, p.cand};
+}
 __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandRec& cd,
-                                  uint32_t d, const PostRec& pr) {
+                                  uint32_t d, const PostL1& pr, const PostRec* pp,
+                                  const PostRec* both) {
   const uint32_t s = cd.slot;
   const uint8_t f0 = cd.f();
   if (d == kNoDec) {  // not dispatched: the pending mark settles
@@ -2478,13 +2505,14 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
     tb.rec[s].prev_r = pr.prev_r;
   }
   if (run) {
+    const PostRec& p2 = both ? *both : *pp;  // (the second line)
     dmc_decision x;
-    x.handle = pr.handle1;
-    x.tag_r = pr.r1;
-    x.tag_p = pr.p1;
-    x.tag_l = pr.l1;
+    x.handle = p2.handle1;
+    x.tag_r = p2.r1;
+    x.tag_p = p2.p1;
+    x.tag_l = p2.l1;
     x.slot = s;
-    x.cost = pr.cost1;
+    x.cost = p2.cost1;
     x.phase = DMC_PHASE_RESERVATION;
     x.flags = 0;
     rc.out[d + 1] = x;
@@ -2564,10 +2592,20 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
       // round trip)
       const CandRec c = cand[ci];
       const uint32_t d = decof[ci];
-      const PostRec pr = post[ci];
-      if (d != kSlowCand && !rc.ovf) {
-        apply_fast(tb, rc, c, d, pr);
-        continue;
+      if (DMC_POST_LINE1) {
+        const PostRec* pp = post + ci;
+        const PostL1 pr{pp->fr, pp->fpk, pp->fl, pp->prev_r, pp->off, pp->r2, pp->bits,
+                        pp->cand};
+        if (d != kSlowCand && !rc.ovf) {
+          apply_fast(tb, rc, c, d, pr, pp, nullptr);
+          continue;
+        }
+      } else {
+        const PostRec pr = post[ci];
+        if (d != kSlowCand && !rc.ovf) {
+          apply_fast(tb, rc, c, d, post_l1(pr), post + ci, &pr);
+          continue;
+        }
       }
       rc.dbg = (dbg && ci < 65536) ? dbg + 8 * ci : nullptr;
       if (rc.dbg) rc.dbg[1] = rc.dbg[2] = rc.dbg[3] = 0;

@@ -13,12 +13,12 @@ base=""
 for round in $(seq ${ROUNDS:-2}); do
 for v in $VARIANTS; do
   DMC_LIB=$R/dmclock_amd/variants/$v.so timeout -k 10 240 python bench.py --no-cpu-baseline --steps 20 ${BENCH_ARGS} > gpurun_out/var_$v.json 2> gpurun_out/var_$v.err || { tail -5 gpurun_out/var_$v.err; exit 1; }
-  dec=$(python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); c=d['engine_counters']; print(c['decisions'], c['bad_rounds'])") || exit 1
+  dec=$(python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); c=d.get('engine_counters') or {}; print(c.get('decisions', d.get('tracker_known_frac')), c.get('bad_rounds'))") || exit 1
   [ -z "$base" ] && base="$dec"
   if [ "$dec" != "$base" ]; then
     echo "variant $v: decisions/bad_rounds $dec differ from the base's $base: wrong result, not timed"
     exit 1
   fi
-  python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); print('$v', d['ms_per_step'], {k: round(v*1e3,1) for k, v in d['stages_ms_per_step'].items()}, 'dec', d['engine_counters']['decisions'], 'retries', d['engine_counters']['sample_retries'])"
+  python -c "import json; d=json.load(open('gpurun_out/var_$v.json')); c=d.get('engine_counters') or {}; print('$v', d['ms_per_step'], {k: round(v*1e3,1) for k, v in (d.get('stages_ms_per_step') or {}).items()}, 'dec', c.get('decisions'), 'retries', c.get('sample_retries'))"
 done
 done
