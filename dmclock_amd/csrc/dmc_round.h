@@ -2746,7 +2746,7 @@ __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const R
 // several blocks per CU, many walks in flight.  The records, their order
 // and every state change are k_remit_m's (the same emit_one).
 #ifndef DMC_SPLIT_EMIT_M
-#define DMC_SPLIT_EMIT_M 1
+#define DMC_SPLIT_EMIT_M 0
 #endif
 #ifndef DMC_WALK_THREADS
 #define DMC_WALK_THREADS 128
