@@ -999,6 +999,161 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
   __syncthreads();
 }
 
+// The same pick by one wave per phase (wave 0: R, wave 1: P), 32 histogram
+// bins per lane: the prefix sums are wave scans and the threshold's bin a
+// ballot, so the only barrier is the one that publishes the result to the
+// block (the half-block pick above has seven, its waves' key loads in
+// flight between them).  Same arithmetic, the same PhaseSel and rank-bin
+// table entry for entry.  (DMC_PICK_WAVE=0: the half-block pick.)
+#ifndef DMC_PICK_WAVE
+#define DMC_PICK_WAVE 1
+#endif
+constexpr int kWBins = kHistBinsR / 64;  // bins per lane
+struct PickW {
+  uint4 h[kWBins / 4];
+  RoundPart tot;
+};
+// (waves 0 and 1 only; issued ahead of the caller's other loads)
+__device__ inline PickW pick_load_w(const uint32_t* hist, const RoundPart* tot) {
+  PickW b;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < 2) {
+    const uint32_t* hp = hist + w * kHistBinsR + lane * kWBins;
+#pragma unroll
+    for (int j = 0; j < kWBins / 4; ++j) {
+      b.h[j] = ld_as<uint4>(hp + 4 * j);
+#pragma unroll
+      for (int i = 1; i < kShards; ++i) {
+        const uint4 x = ld_as<uint4>(hp + i * 2 * kHistBinsR + 4 * j);
+        b.h[j].x += x.x; b.h[j].y += x.y; b.h[j].z += x.z; b.h[j].w += x.w;
+      }
+    }
+    b.tot = *tot;
+  }
+  return b;
+}
+__device__ inline void pick_wave(int p, uint32_t k, const PickW& hw, uint32_t* sbn,
+                                 PhaseSel* ps, int sampled, uint32_t fault) {
+  const uint32_t lane = threadIdx.x & 63;
+  const RoundPart& tot = hw.tot;
+  const bool p_runs = tot.n_r < (uint64_t)k;
+  const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
+                               : (p_runs ? k - (uint32_t)tot.n_r : 0);
+  const uint32_t need_h = need_hist(need, sampled);
+  // (the phase's totals selected, not indexed: no private-memory array)
+  const uint32_t ne = p ? tot.cnt[1] : tot.cnt[0];
+  const uint64_t kmn = p ? tot.mn[1] : tot.mn[0], kmx = p ? tot.mx[1] : tot.mx[0];
+  const KeyMap km(kmn, kmx);
+  const uint32_t sh1 = hist_shift_r(km(kmx));
+  const uint32_t tb0 = ne ? hist_bin(km(kmx), 0, sh1) : 0;
+  uint32_t h[kWBins];
+#pragma unroll
+  for (int j = 0; j < kWBins / 4; ++j) {
+    h[4 * j] = hw.h[j].x;
+    h[4 * j + 1] = hw.h[j].y;
+    h[4 * j + 2] = hw.h[j].z;
+    h[4 * j + 3] = hw.h[j].w;
+  }
+  uint32_t local = 0, lz = 0;
+#pragma unroll
+  for (int j = 0; j < kWBins; ++j) {
+    local += h[j];
+    lz += h[j] ? 1u : 0u;
+  }
+  const uint32_t before = wscan_u32(local) - local, zbefore = wscan_u32(lz) - lz;
+  // T's bin: the first whose inclusive count reaches need_h (one lane holds
+  // the crossing: the prefix sums are monotone); else every key up to tb0
+  const bool mine = need && ne > need && before < need_h && before + local >= need_h;
+  const uint64_t fm = __ballot(mine);
+  const bool found = fm != 0;
+  const int sl = found ? __ffsll((unsigned long long)fm) - 1 : (int)(tb0 / kWBins);
+  uint32_t cb = 0, cum = before, cz = zbefore;
+  bool done = false;
+#pragma unroll
+  for (int j = 0; j < kWBins; ++j) {
+    const uint32_t b = lane * kWBins + j;
+    if (found ? !done : b <= tb0) {
+      cum += h[j];
+      cz += h[j] ? 1u : 0u;
+      if (found && cum >= need_h) {
+        cb = b;
+        done = true;
+      }
+    }
+  }
+  const uint32_t tb = found ? (uint32_t)__builtin_amdgcn_readlane((int)cb, sl) : tb0;
+  const uint32_t C0 = (uint32_t)__builtin_amdgcn_readlane((int)cum, sl);
+  const uint32_t nz = (uint32_t)__builtin_amdgcn_readlane((int)cz, sl);
+  uint64_t T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
+  if (found) {
+    // the bin's upper edge (see pick_phase), rounded up to its quantum's end
+    const uint64_t edge =
+        tb == kHistBinsR - 1
+            ? kmx
+            : km.max_key_at(sat_add_u64(0, ((uint64_t)(tb + 1) << sh1) - 1), kmx);
+    T = edge >= kMaxKey - 1 ? kMaxKey - 1 : (edge | 0xffffffffull);
+  }
+  // the rank-bin table (pick_phase's split)
+  const uint32_t C = C0 > 0 ? C0 : 1;
+  const uint32_t S = kNBPhase > nz ? kNBPhase - nz : 0;
+  const float q = (float)S / (float)C;
+  uint32_t lns = 0;
+#pragma unroll
+  for (int j = 0; j < kWBins; ++j) {
+    const uint32_t b = lane * kWBins + j;
+    uint32_t e = (uint32_t)((float)h[j] * q);
+    e = e > S ? S : e;
+    h[j] = (b <= tb && h[j]) ? 1u + e : 0u;  // (h now holds the rank-bin counts)
+    lns += h[j];
+  }
+  uint32_t nb = wscan_u32(lns) - lns;
+#pragma unroll
+  for (int j = 0; j < kWBins / 4; ++j) {
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint32_t first = nb, num = h[4 * j + u];
+      if (first >= (uint32_t)kNBPhase) {
+        first = kNBPhase - 1;
+        num = num ? 1 : 0;
+      } else if (first + num > (uint32_t)kNBPhase) {
+        num = kNBPhase - first;
+      }
+      v[u] = (p * kNBPhase + first) | (num << 16);
+      nb += h[4 * j + u];
+    }
+    st_as(sbn + p * kHistBinsR + lane * kWBins + 4 * j, make_uint4(v[0], v[1], v[2], v[3]));
+  }
+  if (lane == 0) {
+    PhaseSel z{};
+    z.kmin = kmn;
+    z.kmax = kmx;
+    z.T = T;
+    z.n_elig = ne;
+    z.hshift = sh1;
+    z.tbin = tb;
+    z.hmin = 0;
+    z.lo0 = 0;
+    const uint64_t cmax = km(kmx);
+    const uint64_t top = (uint64_t)(kHistBinsR - 1) << sh1;
+    z.hitop = cmax > top ? cmax : top;
+    z.vmin = km.vmin;
+    z.scale = km.scale;
+    z.inv_w = bitsd((uint64_t)(1023 - sh1) << 52);
+    z.inv_last = 1.0 / ((double)(z.hitop - top) + 1.0);
+    // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset
+    z.valid = (p == 1 && (fault & 1u)) ? 0u : kSelValid;
+    *ps = z;
+  }
+}
+// (sbn, ps: LDS; complete after the barrier inside)
+__device__ inline void pick_both_w(uint32_t k, const PickW& hw, uint32_t* sbn, PhaseSel* ps,
+                                   int sampled, uint32_t fault) {
+  const int w = threadIdx.x >> 6;
+  if (w < 2) pick_wave(w, k, hw, sbn, &ps[w], sampled, fault);
+  __syncthreads();
+}
+
 // n keys per phase: every slot's first keys (keyr / keyp, exact), or the
 // scan's 1/kSample sample of them (sampled: 1, or 2 in the test mode of
 // need_hist).  The histogram k_rscan cleared is complete at the kernel's end;
@@ -1538,14 +1693,22 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // while the slots' keys below are still in flight
   // (PRE: the tables k_rpick_m picked, this thread's share)
   constexpr int kPT = 2 * kHistBinsR / 4 / kEmitThreads;
+#if DMC_PICK_WAVE
+  PickW hv;
+#else
   PickBins hv;
+#endif
   uint4 pt[kPT];
   if constexpr (PRE) {
 #pragma unroll
     for (int j = 0; j < kPT; ++j)
       pt[j] = ld_as<uint4>(hist + kShards * 2 * kHistBinsR + 4 * (threadIdx.x + j * kEmitThreads));
   } else {
+#if DMC_PICK_WAVE
+    hv = pick_load_w(hist, &rd->tot);
+#else
     hv = pick_load(hist);
+#endif
   }
   if (DMC_EARLY_LOADS && rd->skip) return;
   const bool p_runs = rd->p_runs != 0;
@@ -1582,8 +1745,12 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
     if (threadIdx.x < 2) s_ph[threadIdx.x] = rd->ph[threadIdx.x];
     __syncthreads();  // (also orders the zeroing of s_cnt / s_tot)
   } else {
+#if DMC_PICK_WAVE
+    pick_both_w(rd->k_total, hv, ltab, s_ph, (int)rd->sampled, rd->fault);
+#else
     pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
               eclk ? eclk + kEClk * blockIdx.x : nullptr);
+#endif
     if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   }
   const CandPred pred(s_ph, p_runs);
@@ -1790,24 +1957,37 @@ __device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_
 // the ring index is read from the record when the pop is placed.
 struct BKeyS {
   uint64_t okey;
-  uint32_t slot;
-  uint32_t sr;  // queue position << 16 | run
-  __device__ uint32_t seq() const { return sr >> 16; }
-  __device__ uint32_t run() const { return sr & 0xffffu; }
+  uint64_t lo;  // slot << 32 | queue position << 16 | run
+  __device__ uint32_t slot() const { return (uint32_t)(lo >> 32); }
+  __device__ uint32_t seq() const { return (uint32_t)(lo >> 16) & 0xffffu; }
+  __device__ uint32_t run() const { return (uint32_t)lo & 0xffffu; }
 };
 static_assert(sizeof(BKeyS) == 16, "BKeyS must be 16 bytes");
 __device__ inline BKeyS bkey_s(const BKey& k) {
-  return BKeyS{k.okey, k.slot, (k.seq << 16) | (k.run & 0xffffu)};
+  return BKeyS{k.okey, ((uint64_t)k.slot << 32) | ((k.seq & 0xffffu) << 16) | (k.run & 0xffffu)};
 }
 
+// Rank of record i of a bin among all `cnt` of them, compared in `parts`
+// slices of `per` records by adjacent lanes whose counts are summed by
+// shuffles; lanes with i >= cnt take part in the shuffles only.  The order
+// (okey, slot, queue position) is one 128-bit comparison of (okey, lo): two
+// records of a bin never share slot and position, so lo's run bits never
+// decide it -- the borrow of a 128-bit subtraction, added into the rank
+// (VALU-bound: a heavy bin's block runs one wave per SIMD, and the compare
+// chain is most of its time).  The lane that owns a record then decides it:
+// a fast record's decision is written and its offset recorded for k_rapply
+// (which stores the candidate's precomputed state); a slow record's pop is
+// stamped into its ring entry.  (ISP: a P bin, whose records' group sizes
+// 1 + run give the decision offsets; an R bin's offset is its rank.)
+template <bool ISP>
 __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                 uint32_t parts, uint32_t per, uint32_t i,
-                                uint32_t part, bool isp, uint32_t k,
+                                uint32_t part, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
   const bool valid = i < cnt;
   const BKeyS me = sh[valid ? i : 0];
-  const uint32_t me_seq = me.seq();
+  const uint32_t me_slot = me.slot();
   // the writer lane's payload (an L2 hit: the block staged the line), in
   // flight during the comparisons
   uint32_t ci = 0, cost = 0, ridx = 0;
@@ -1829,22 +2009,22 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
 #pragma unroll 4
   for (uint32_t f = f0; f < f1; ++f) {
     const BKeyS o = sh[f];
-    uint32_t eqk = o.okey == me.okey;
-    uint32_t less = (uint32_t)(o.okey < me.okey) |
-                    (eqk & ((uint32_t)(o.slot < me.slot) |
-                            ((uint32_t)(o.slot == me.slot) & (uint32_t)(o.seq() < me_seq))));
-    rank += less;
-    gl += less * (isp ? 1u + o.run() : 1u);
-    tie |= eqk & (uint32_t)(o.slot != me.slot);
+    unsigned long long b0, b1;
+    (void)__builtin_subcll(o.lo, me.lo, 0ull, &b0);
+    (void)__builtin_subcll(o.okey, me.okey, b0, &b1);  // b1: o < me
+    rank += (uint32_t)b1;
+    if (ISP) gl += b1 ? 1u + ((uint32_t)o.lo & 0xffffu) : 0u;
+    tie |= (uint32_t)(o.okey == me.okey) & (uint32_t)((uint32_t)(o.lo >> 32) != me_slot);
   }
   for (uint32_t d = 1; d < parts; d <<= 1) {
     rank += __shfl_xor(rank, d);
-    gl += __shfl_xor(gl, d);
+    if (ISP) gl += __shfl_xor(gl, d);
     tie |= __shfl_xor(tie, d);
   }
+  if (!ISP) gl = rank;
   if (valid && part == 0)
-    place_rec(rd, BKey{me.okey, me.slot, me_seq, me.run(), ridx}, ci, cost, handle, tr, tp, tl,
-              rank, gl, tie, isp, k, n_pgroups, soff, poff, ring, out, decof);
+    place_rec(rd, BKey{me.okey, me_slot, me.seq(), me.run(), ridx}, ci, cost, handle, tr, tp, tl,
+              rank, gl, tie, ISP, k, n_pgroups, soff, poff, ring, out, decof);
 }
 
 // One block per rank bin.  The bin's order keys are staged in LDS; each
@@ -1872,8 +2052,7 @@ constexpr int kRankBlocksR = kNBR;
 #endif
 constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
 __device__ inline bool bkey_less(const BKeyS& x, const BKeyS& y) {
-  return x.okey < y.okey ||
-         (x.okey == y.okey && (x.slot < y.slot || (x.slot == y.slot && x.seq() < y.seq())));
+  return x.okey < y.okey || (x.okey == y.okey && x.lo < y.lo);
 }
 __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                    bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
@@ -1938,7 +2117,7 @@ __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src,
     if (r > 0) {
       const BKeyS pv = sh[ord[r - 1]];
       head = pv.okey != me.okey;
-      diff = !head && pv.slot != me.slot;
+      diff = !head && pv.slot() != me.slot();
     }
     hd |= (head ? 1u : 0u) << h;
     dd |= (diff ? 1u : 0u) << h;
@@ -2099,14 +2278,23 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     }
     return;
   }
-  uint32_t parts = 1;
-  while (parts < 64 && cnt * parts * 2 <= (uint32_t)kRankThreads) parts <<= 1;
-  const uint32_t per = (cnt + parts - 1) / parts;
   __syncthreads();
   const uint32_t t = threadIdx.x;
-  for (uint32_t rb = 0; rb < cnt; rb += kRankThreads / parts)
-    rank_rec(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, isp, k, n_pgroups,
-             soff, poff, ring, out, decof);
+  // passes of kRankThreads / parts records, parts lanes per record, parts
+  // sized per pass (a bin of 190: 128 records with 1 lane each, then 62 with 2)
+  for (uint32_t rb = 0; rb < cnt;) {
+    const uint32_t rem = cnt - rb;
+    uint32_t parts = 1;
+    while (parts < 64 && rem * parts * 2 <= (uint32_t)kRankThreads) parts <<= 1;
+    const uint32_t per = (cnt + parts - 1) / parts;
+    if (isp)
+      rank_rec<true>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
+                     soff, poff, ring, out, decof);
+    else
+      rank_rec<false>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
+                      soff, poff, ring, out, decof);
+    rb += kRankThreads / parts;
+  }
   if (wtime && threadIdx.x == 0) {
     wtime[2 * b] = t0;
     wtime[2 * b + 1] = wall_clock64();
@@ -2723,8 +2911,13 @@ __global__ void __launch_bounds__(kEmitThreads) k_rpick_m(const RHistArgs* a) {
   if (rd->skip) return;
   __shared__ uint32_t sbn[2 * kHistBinsR];
   __shared__ PhaseSel s_ph[2];
+#if DMC_PICK_WAVE
+  const PickW hv = pick_load_w(x.hist, &rd->tot);
+  pick_both_w(rd->k_total, hv, sbn, s_ph, (int)rd->sampled, rd->fault);
+#else
   const PickBins hv = pick_load(x.hist);
   pick_both(rd->k_total, rd->tot, hv, sbn, s_ph, (int)rd->sampled, rd->fault);
+#endif
   for (int i = threadIdx.x; i < 2 * kHistBinsR / 4; i += kEmitThreads)
     st_as(x.hist + kShards * 2 * kHistBinsR + 4 * i, ld_as<uint4>(sbn + 4 * i));
   if (threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];
