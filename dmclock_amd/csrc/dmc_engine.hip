@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <limits>
 #include <mutex>
 #include <vector>
@@ -5465,6 +5466,15 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
   return DMC_OK;
 }
 
+// the epoch kernels' grid: 4 entries per thread, one pass; their uint4 path
+// when every array is 16-byte aligned (a null map has no array)
+static uint32_t grid4(uint32_t n) { return (n + 4 * kBlock - 1) / (4 * kBlock); }
+static bool aligned16(std::initializer_list<const void*> ps) {
+  for (const void* p : ps)
+    if (reinterpret_cast<uintptr_t>(p) & 15u) return false;
+  return true;
+}
+
 int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_client_of_slot,
                              const uint32_t* d_comp_delta, const uint32_t* d_comp_rho,
                              uint32_t* d_sum_delta, uint32_t* d_sum_rho) {
@@ -5474,9 +5484,9 @@ int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_c
   if (n_slots > q->p.max_clients) return DMC_EINVAL;
   if (!n_slots) return DMC_OK;
   if (!d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_sums, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
+  hipLaunchKernelGGL(k_track_sums, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
                      n_slots, d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta,
-                     d_sum_rho);
+                     d_sum_rho, aligned16({d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta, d_sum_rho}));
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5489,8 +5499,8 @@ int dmc_tracker_commit(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd, uint32_t*
   if (n_slots > q->p.max_clients) return DMC_EINVAL;
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_commit, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
-                     n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho);
+  hipLaunchKernelGGL(k_track_commit, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
+                     n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho, aligned16({d_xd, d_xr, d_comp_delta, d_comp_rho}));
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5506,9 +5516,9 @@ int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho)
     return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_collect, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_track_collect, dim3(grid4(n_slots)), dim3(kBlock), 0,
                      q->stream, n_slots, d_client_of_slot, d_xd, d_xr, d_comp_delta,
-                     d_comp_rho, d_sum_delta, d_sum_rho);
+                     d_comp_rho, d_sum_delta, d_sum_rho, aligned16({d_client_of_slot, d_xd, d_xr, d_comp_delta, d_comp_rho, d_sum_delta, d_sum_rho}));
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5521,8 +5531,8 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
   if (!q) return DMC_EINVAL;
   if (!n_clients) return DMC_OK;
   if (!d_gdelta || !d_grho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_advance, dim3(grid_for(n_clients, 2048)), dim3(kBlock), 0,
-                     q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho);
+  hipLaunchKernelGGL(k_track_advance, dim3(grid4(n_clients)), dim3(kBlock), 0,
+                     q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho, aligned16({d_gdelta, d_grho, d_sum_delta, d_sum_rho}));
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }

@@ -93,25 +93,68 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
                    blockIdx.x * blockDim.x + threadIdx.x);
 }
 
+// The epoch kernels below take 4 consecutive entries per thread, loaded at
+// once (one level of loads: uint4 when the host found every array 16-byte
+// aligned), over a grid that covers the arrays in one pass -- a grid-stride
+// loop of single entries waited for each entry's load in turn (config 5's
+// 2M-slot commit: 15 us, its 16M-client advance: 84 us).
+__device__ inline uint4 ld4(const uint32_t* p, uint32_t s0, uint32_t n, bool vec) {
+  if (vec && s0 + 4 <= n) return ld_as<uint4>(p + s0);
+  uint4 v;
+  v.x = s0 < n ? p[s0] : 0u;
+  v.y = s0 + 1 < n ? p[s0 + 1] : 0u;
+  v.z = s0 + 2 < n ? p[s0 + 2] : 0u;
+  v.w = s0 + 3 < n ? p[s0 + 3] : 0u;
+  return v;
+}
+__device__ inline void st4(uint32_t* p, uint32_t s0, uint32_t n, bool vec, uint4 v) {
+  if (vec && s0 + 4 <= n) {
+    st_as(p + s0, v);
+    return;
+  }
+  if (s0 < n) p[s0] = v.x;
+  if (s0 + 1 < n) p[s0 + 1] = v.y;
+  if (s0 + 2 < n) p[s0 + 2] = v.z;
+  if (s0 + 3 < n) p[s0 + 3] = v.w;
+}
+__device__ inline uint32_t u4at(const uint4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+__device__ inline uint4 add4(const uint4& a, const uint4& b) {
+  return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+// the per-client sums of 4 slots' responses (atomics: the servers of a rank
+// collect concurrently on their own streams)
+__device__ inline void sums4(uint32_t s0, uint32_t nslots, const uint32_t* client_of_slot,
+                             const uint4& cd, const uint4& cr, bool vec, uint32_t* sum_d,
+                             uint32_t* sum_r) {
+  const uint4 cm = client_of_slot ? ld4(client_of_slot, s0, nslots, vec)
+                                  : make_uint4(s0, s0 + 1, s0 + 2, s0 + 3);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t d = u4at(cd, j), r = u4at(cr, j), c = u4at(cm, j);
+    if (d) atomicAdd(&sum_d[c], d);
+    if (r) atomicAdd(&sum_r[c], r);
+  }
+}
+
 // epoch end, per server: my_delta / my_rho of its responses (X += own) and
-// the server's contribution to the per-client sums (atomics: the servers of
-// a rank collect concurrently on their own streams)
+// the server's contribution to the per-client sums
+// (a group of 4 entries with every count 0 is skipped; adding and clearing
+// a zero entry is the identity)
 __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
                                 uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
-                                uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r) {
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
-       s += gridDim.x * blockDim.x) {
-    uint32_t cd = comp_d[s];
-    if (!cd) continue;  // comp_r <= comp_d: nothing delivered to this slot
-    uint32_t cr = comp_r[s];
-    xd[s] += cd;
-    xr[s] += cr;
-    comp_d[s] = 0;
-    comp_r[s] = 0;
-    uint32_t c = client_of_slot ? client_of_slot[s] : s;
-    atomicAdd(&sum_d[c], cd);
-    if (cr) atomicAdd(&sum_r[c], cr);
-  }
+                                uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r, bool vec) {
+  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (s0 >= nslots) return;
+  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
+  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
+  const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
+  st4(xd, s0, nslots, vec, add4(a, cd));
+  st4(xr, s0, nslots, vec, add4(b, cr));
+  st4(comp_d, s0, nslots, vec, make_uint4(0, 0, 0, 0));
+  st4(comp_r, s0, nslots, vec, make_uint4(0, 0, 0, 0));
+  sums4(s0, nslots, client_of_slot, cd, cr, vec, sum_d, sum_r);
 }
 
 // Overlapped (lagged) delivery, split in two: at an epoch's end only the
@@ -121,41 +164,39 @@ __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
 // (k_track_advance).
 __global__ void k_track_sums(uint32_t nslots, const uint32_t* client_of_slot,
                              const uint32_t* comp_d, const uint32_t* comp_r,
-                             uint32_t* sum_d, uint32_t* sum_r) {
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
-       s += gridDim.x * blockDim.x) {
-    const uint32_t cd = comp_d[s];
-    if (!cd) continue;
-    const uint32_t cr = comp_r[s];
-    const uint32_t c = client_of_slot ? client_of_slot[s] : s;
-    atomicAdd(&sum_d[c], cd);
-    if (cr) atomicAdd(&sum_r[c], cr);
-  }
+                             uint32_t* sum_d, uint32_t* sum_r, bool vec) {
+  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (s0 >= nslots) return;
+  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
+  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
+  sums4(s0, nslots, client_of_slot, cd, cr, vec, sum_d, sum_r);
 }
 __global__ void k_track_commit(uint32_t nslots, uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
-                               uint32_t* comp_r) {
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
-       s += gridDim.x * blockDim.x) {
-    const uint32_t cd = comp_d[s];
-    if (!cd) continue;
-    xd[s] += cd;
-    xr[s] += comp_r[s];
-    comp_d[s] = 0;
-    comp_r[s] = 0;
-  }
+                               uint32_t* comp_r, bool vec) {
+  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (s0 >= nslots) return;
+  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
+  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
+  const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
+  st4(xd, s0, nslots, vec, add4(a, cd));
+  st4(xr, s0, nslots, vec, add4(b, cr));
+  st4(comp_d, s0, nslots, vec, make_uint4(0, 0, 0, 0));
+  st4(comp_r, s0, nslots, vec, make_uint4(0, 0, 0, 0));
 }
 
 // after the all-reduce of the sums: the global counters advance (D += all
 // servers' responses to the client), sums cleared for the next epoch
 __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
-                                uint32_t* sum_d, uint32_t* sum_r) {
-  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nclients;
-       c += gridDim.x * blockDim.x) {
-    gd[c] += sum_d[c];
-    gr[c] += sum_r[c];
-    sum_d[c] = 0;
-    sum_r[c] = 0;
-  }
+                                uint32_t* sum_d, uint32_t* sum_r, bool vec) {
+  const uint32_t c0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (c0 >= nclients) return;
+  const uint4 sd = ld4(sum_d, c0, nclients, vec), sr = ld4(sum_r, c0, nclients, vec);
+  if (!(sd.x | sd.y | sd.z | sd.w | sr.x | sr.y | sr.z | sr.w)) return;
+  const uint4 a = ld4(gd, c0, nclients, vec), b = ld4(gr, c0, nclients, vec);
+  st4(gd, c0, nclients, vec, add4(a, sd));
+  st4(gr, c0, nclients, vec, add4(b, sr));
+  st4(sum_d, c0, nclients, vec, make_uint4(0, 0, 0, 0));
+  st4(sum_r, c0, nclients, vec, make_uint4(0, 0, 0, 0));
 }
 
 // multi-table forms (a queue group's step, dmc_group_step_device): the
