@@ -2054,6 +2054,87 @@ constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
 __device__ inline bool bkey_less(const BKeyS& x, const BKeyS& y) {
   return x.okey < y.okey || (x.okey == y.okey && x.lo < y.lo);
 }
+// The bin's records sorted in registers: a bitonic network over 512 (key,
+// record index) elements, thread t holding elements 4t..4t+3 -- the
+// compare-exchanges of distance 1 and 2 inside a thread, 4..128 with the
+// partner lane's elements (shuffles), 256 with the other wave's (their
+// indices through LDS, the keys re-read from sh).  Padding (index >= cnt)
+// orders after every record.  ord[r]: the record at sorted position r.
+// (The LDS network before it, one compare-exchange per thread and step with
+// a barrier each, took ~20 us for a full bin: k_rrank's tail.)
+struct SK {
+  uint64_t k, l;
+  uint32_t i;
+};
+__device__ inline SK sk_at(const BKeyS* sh, uint32_t i, uint32_t cnt) {
+  if (i < cnt) {
+    const BKeyS b = sh[i];
+    return SK{b.okey, b.lo, i};
+  }
+  return SK{~0ull, ~0ull, i};
+}
+__device__ inline bool sk_less(const SK& a, const SK& b) {
+  return a.k < b.k || (a.k == b.k && a.l < b.l);
+}
+// a keeps the smaller of (a, b) when `mn`, else the larger
+__device__ inline SK sk_keep(const SK& a, const SK& b, bool mn) {
+  const bool take = mn ? sk_less(b, a) : sk_less(a, b);
+  return SK{take ? b.k : a.k, take ? b.l : a.l, take ? b.i : a.i};
+}
+__device__ inline void sk_cx(SK& a, SK& b, bool asc) {
+  const bool sw = asc ? sk_less(b, a) : sk_less(a, b);
+  const SK x = a, y = b;
+  a = SK{sw ? y.k : x.k, sw ? y.l : x.l, sw ? y.i : x.i};
+  b = SK{sw ? x.k : y.k, sw ? x.l : y.l, sw ? x.i : y.i};
+}
+__device__ inline SK sk_shfl_xor(const SK& a, uint32_t m) {
+  SK o;
+  o.k = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(a.k >> 32), (int)m) << 32) |
+        (uint32_t)__shfl_xor((int)(uint32_t)a.k, (int)m);
+  o.l = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(a.l >> 32), (int)m) << 32) |
+        (uint32_t)__shfl_xor((int)(uint32_t)a.l, (int)m);
+  o.i = (uint32_t)__shfl_xor((int)a.i, (int)m);
+  return o;
+}
+__device__ inline void sort_bin_regs(const BKeyS* sh, uint32_t cnt, uint16_t* ord) {
+  static_assert(kBinCapR == 512 && kRankThreads == 128, "4 elements per thread, 2 waves");
+  const uint32_t t = threadIdx.x;
+  SK v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = sk_at(sh, 4 * t + r, cnt);
+  for (uint32_t k = 2; k <= kBinCapR; k <<= 1) {
+    const bool asc = ((4 * t) & k) == 0;  // (k >= 4: the same for the thread's 4)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j == 1) {
+        sk_cx(v[0], v[1], k == 2 ? true : asc);
+        sk_cx(v[2], v[3], k == 2 ? false : asc);
+      } else if (j == 2) {
+        sk_cx(v[0], v[2], asc);
+        sk_cx(v[1], v[3], asc);
+      } else {
+        const uint32_t m = j >> 2;  // the partner thread: t ^ m
+        const bool mn = ((t & m) == 0) == asc;
+        if (m < 64) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = sk_keep(v[r], sk_shfl_xor(v[r], m), mn);
+        } else {
+          __syncthreads();  // (ord's previous readers)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ord[4 * t + r] = (uint16_t)v[r].i;
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[r] = sk_keep(v[r], sk_at(sh, ord[4 * (t ^ m) + r], cnt), mn);
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ord[4 * t + r] = (uint16_t)v[r].i;
+  __syncthreads();
+}
+
 __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                    bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
                                    uint32_t poff, ReqEntry* ring, dmc_decision* out,
@@ -2063,26 +2144,7 @@ __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src,
   __shared__ uint16_t ord[kBinCapR];
   __shared__ uint32_t wsum[kRankThreads / 64];
   const uint32_t t = threadIdx.x;
-  uint32_t P = 2;
-  while (P < cnt) P <<= 1;
-  for (uint32_t i = t; i < P; i += kRankThreads) ord[i] = (uint16_t)i;
-  __syncthreads();
-  for (uint32_t kk = 2; kk <= P; kk <<= 1) {
-    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-      for (uint32_t u = t; u < P / 2; u += kRankThreads) {
-        const uint32_t i = ((u & ~(j - 1)) << 1) | (u & (j - 1)), l = i | j;
-        const uint32_t a = ord[i], c = ord[l];
-        // indices >= cnt (padding) order after every record
-        const bool c_lt_a = c < cnt && (a >= cnt || bkey_less(sh[c], sh[a]));
-        const bool a_lt_c = a < cnt && (c >= cnt || bkey_less(sh[a], sh[c]));
-        if ((i & kk) == 0 ? c_lt_a : a_lt_c) {
-          ord[i] = (uint16_t)c;
-          ord[l] = (uint16_t)a;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  sort_bin_regs(sh, cnt, ord);
   // positions RP t .. RP t + RP - 1: their records, sizes, the exclusive prefix
   uint32_t z[RP], ix[RP], zs = 0;
 #pragma unroll
