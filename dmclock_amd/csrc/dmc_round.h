@@ -2062,6 +2062,9 @@ __device__ inline bool bkey_less(const BKeyS& x, const BKeyS& y) {
 // orders after every record.  ord[r]: the record at sorted position r.
 // (The LDS network before it, one compare-exchange per thread and step with
 // a barrier each, took ~20 us for a full bin: k_rrank's tail.)
+#ifndef DMC_RANK_REGSORT
+#define DMC_RANK_REGSORT 1
+#endif
 struct SK {
   uint64_t k, l;
   uint32_t i;
@@ -2099,6 +2102,7 @@ __device__ inline SK sk_shfl_xor(const SK& a, uint32_t m) {
 __device__ inline void sort_bin_regs(const BKeyS* sh, uint32_t cnt, uint16_t* ord) {
   static_assert(kBinCapR == 512 && kRankThreads == 128, "4 elements per thread, 2 waves");
   const uint32_t t = threadIdx.x;
+  __syncthreads();  // (sh: staged by the whole block)
   SK v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = sk_at(sh, 4 * t + r, cnt);
@@ -2144,7 +2148,29 @@ __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src,
   __shared__ uint16_t ord[kBinCapR];
   __shared__ uint32_t wsum[kRankThreads / 64];
   const uint32_t t = threadIdx.x;
+#if DMC_RANK_REGSORT
   sort_bin_regs(sh, cnt, ord);
+#else
+  uint32_t P = 2;
+  while (P < cnt) P <<= 1;
+  for (uint32_t i = t; i < P; i += kRankThreads) ord[i] = (uint16_t)i;
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t u = t; u < P / 2; u += kRankThreads) {
+        const uint32_t i = ((u & ~(j - 1)) << 1) | (u & (j - 1)), l = i | j;
+        const uint32_t a = ord[i], c = ord[l];
+        const bool c_lt_a = c < cnt && (a >= cnt || bkey_less(sh[c], sh[a]));
+        const bool a_lt_c = a < cnt && (c >= cnt || bkey_less(sh[a], sh[c]));
+        if ((i & kk) == 0 ? c_lt_a : a_lt_c) {
+          ord[i] = (uint16_t)c;
+          ord[l] = (uint16_t)a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+#endif
   // positions RP t .. RP t + RP - 1: their records, sizes, the exclusive prefix
   uint32_t z[RP], ix[RP], zs = 0;
 #pragma unroll
