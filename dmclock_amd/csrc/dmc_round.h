@@ -1004,9 +1004,12 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
 // ballot, so the only barrier is the one that publishes the result to the
 // block (the half-block pick above has seven, its waves' key loads in
 // flight between them).  Same arithmetic, the same PhaseSel and rank-bin
-// table entry for entry.  (DMC_PICK_WAVE=0: the half-block pick.)
+// table entry for entry.  Measured slower: emit 28.8-28.9 against 27.2-27.3
+// us with the half-block pick (r05k, alternated on one box) -- one wave's
+// 32 bins per lane in sequence cost more than the barriers saved; kept as
+// DMC_PICK_WAVE=1 (its parity tested like the default's).
 #ifndef DMC_PICK_WAVE
-#define DMC_PICK_WAVE 1
+#define DMC_PICK_WAVE 0
 #endif
 constexpr int kWBins = kHistBinsR / 64;  // bins per lane
 struct PickW {
