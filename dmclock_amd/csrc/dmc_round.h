@@ -152,8 +152,6 @@ struct Round {
   uint32_t fault;        // test hook (CallParams::fault)
   uint32_t skip;         // this round's kernels do nothing (its k_rscan found the gate shut)
   uint32_t* gate;        // a pipelined round: its end sets the gate (CallParams::gate)
-  uint64_t tpred[2];     // the last single-table round's thresholds (0: none), k_remit's
-                         // prefetch prediction for the next round (a hint only)
 };
 
 struct CallParams {
@@ -1741,35 +1739,6 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
       mt[j] = in ? meta[s0 + j] : 0;
     }
   }
-  // Prefetch (single-table rounds, whose pick takes several microseconds):
-  // the client records and first ring entries of the slots the previous
-  // round's thresholds would admit -- nearly all of this round's candidates,
-  // as the thresholds move little from round to round -- requested before
-  // the pick, so that the walkers' first level hits the L2 instead of
-  // queueing behind every block's random reads at once.  The loaded words
-  // are folded into pfx, consumed at the kernel's end (waiting for them
-  // costs nothing by then); a wrong prediction only costs its reads.
-  uint32_t pfx = 0;
-#ifndef DMC_EMIT_PREFETCH
-#define DMC_EMIT_PREFETCH 1
-#endif
-  if constexpr (!PRE && DMC_EMIT_PREFETCH) {
-    const uint64_t pTR = rd->tpred[0], pTP = rd->tpred[1];
-    const uint32_t pr32 = key32(pTR) > 0xfffffffeu ? 0xfffffffeu : key32(pTR);
-    const uint32_t pp32 = key32(pTP) > 0xfffffffeu ? 0xfffffffeu : key32(pTP);
-#pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
-      const uint32_t c = mt[j] >> 24;
-      if (s0 + j < n && c && ((pTR && kr[j] <= pr32) || (pTP && kp[j] <= pp32))) {
-        const uint32_t s = s0 + j, h = (mt[j] >> 16) & 0xffu;
-        const ReqEntry* g = tb.ring + (size_t)s * tb.q;
-        pfx ^= ld_as<uint32_t>(&tb.rec[s].r_inv);
-        pfx ^= ld_as<uint32_t>(&g[h & tb.qmask].r);
-        if (c > 1) pfx ^= ld_as<uint32_t>(&g[(h + 1) & tb.qmask].r);
-        if (c > 2) pfx ^= ld_as<uint32_t>(&g[(h + 2) & tb.qmask].r);
-      }
-    }
-  }
   // the thresholds and the rank-bin table, picked from the round's
   // histogram while the keys are in flight (its barriers also order the
   // zeroing of s_cnt / s_tot before any wave adds to them)
@@ -1785,10 +1754,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
     pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
               eclk ? eclk + kEClk * blockIdx.x : nullptr);
 #endif
-    if (blockIdx.x == 0 && threadIdx.x < 2) {
-      rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
-      rd->tpred[threadIdx.x] = (threadIdx.x == 0 || p_runs) ? s_ph[threadIdx.x].T : 0;
-    }
+    if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
   }
   const CandPred pred(s_ph, p_runs);
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 1] = wall_clock64();
@@ -1906,7 +1872,6 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
     }
   }
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 4] = wall_clock64();
-  asm volatile("" ::"v"(pfx));  // (the prefetches: issued, never left pending)
 }
 template <bool BRK>
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW)
