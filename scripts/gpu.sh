@@ -19,6 +19,8 @@
 #     heaptime         tools/heap_timing.py at $HEAP_N clients (heap order vs oracle)
 #     rankbins         tools/rank_bins.py: k_rrank's per-bin clocks over 40 debug rounds
 #     probe            tools/rand_probe: random-record read rates (64/128-byte shapes)
+#     eclk             k_remit's per-block phase clocks and per-candidate walk times
+#                      over a short bench run (DMC_DEBUG rounds, stderr)
 #     variants         $VARIANTS alternated $ROUNDS times (scripts/gpu_variants.sh)
 #   $BENCH_ARGS is appended to every bench.py command.
 set -o pipefail
@@ -83,6 +85,9 @@ for step in "$@"; do
     variants) bash scripts/gpu_variants.sh || exit 1 ;;
     rankbins) run rankbins 300 python -u tools/rank_bins.py 40 || exit 1 ;;
     probe) run probe 200 tools/rand_probe || exit 1 ;;
+    eclk) DMC_DEBUG=1 DMC_EMIT_CLOCKS=1 run eclk 300 python bench.py --steps 3 --warmup 1 \
+              --no-cpu-baseline --no-profile ${BENCH_ARGS} || exit 1
+          grep -c 'emit clock' ${O}_eclk.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
