@@ -107,21 +107,25 @@ __device__ inline uint4 ld4(const uint32_t* p, uint32_t s0, uint32_t n, bool vec
   v.w = s0 + 3 < n ? p[s0 + 3] : 0u;
   return v;
 }
-__device__ inline void st4(uint32_t* p, uint32_t s0, uint32_t n, bool vec, uint4 v) {
-  if (vec && s0 + 4 <= n) {
-    st_as(p + s0, v);
-    return;
-  }
-  if (s0 < n) p[s0] = v.x;
-  if (s0 + 1 < n) p[s0 + 1] = v.y;
-  if (s0 + 2 < n) p[s0 + 2] = v.z;
-  if (s0 + 3 < n) p[s0 + 3] = v.w;
-}
 __device__ inline uint32_t u4at(const uint4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
-__device__ inline uint4 add4(const uint4& a, const uint4& b) {
-  return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+// X += (d, r) and (d, r) cleared, only at the entries with a count: the
+// arrays are ~20 % dense per epoch at config 5, so writing whole groups of 4
+// moved more bytes than the scattered entries (k_track_advance 102 vs 84 us)
+__device__ inline void commit4(uint32_t s0, uint32_t n, const uint4& d, const uint4& r,
+                               const uint4& a, const uint4& b, uint32_t* xd, uint32_t* xr,
+                               uint32_t* cd, uint32_t* cr) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t dj = u4at(d, j), rj = u4at(r, j);
+    if (s0 + j < n && (dj | rj)) {
+      xd[s0 + j] = u4at(a, j) + dj;
+      xr[s0 + j] = u4at(b, j) + rj;
+      cd[s0 + j] = 0;
+      cr[s0 + j] = 0;
+    }
+  }
 }
 // the per-client sums of 4 slots' responses (atomics: the servers of a rank
 // collect concurrently on their own streams)
@@ -150,10 +154,7 @@ __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
   const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
   if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
   const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
-  st4(xd, s0, nslots, vec, add4(a, cd));
-  st4(xr, s0, nslots, vec, add4(b, cr));
-  st4(comp_d, s0, nslots, vec, make_uint4(0, 0, 0, 0));
-  st4(comp_r, s0, nslots, vec, make_uint4(0, 0, 0, 0));
+  commit4(s0, nslots, cd, cr, a, b, xd, xr, comp_d, comp_r);
   sums4(s0, nslots, client_of_slot, cd, cr, vec, sum_d, sum_r);
 }
 
@@ -178,10 +179,7 @@ __global__ void k_track_commit(uint32_t nslots, uint32_t* xd, uint32_t* xr, uint
   const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
   if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
   const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
-  st4(xd, s0, nslots, vec, add4(a, cd));
-  st4(xr, s0, nslots, vec, add4(b, cr));
-  st4(comp_d, s0, nslots, vec, make_uint4(0, 0, 0, 0));
-  st4(comp_r, s0, nslots, vec, make_uint4(0, 0, 0, 0));
+  commit4(s0, nslots, cd, cr, a, b, xd, xr, comp_d, comp_r);
 }
 
 // after the all-reduce of the sums: the global counters advance (D += all
@@ -193,10 +191,7 @@ __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
   const uint4 sd = ld4(sum_d, c0, nclients, vec), sr = ld4(sum_r, c0, nclients, vec);
   if (!(sd.x | sd.y | sd.z | sd.w | sr.x | sr.y | sr.z | sr.w)) return;
   const uint4 a = ld4(gd, c0, nclients, vec), b = ld4(gr, c0, nclients, vec);
-  st4(gd, c0, nclients, vec, add4(a, sd));
-  st4(gr, c0, nclients, vec, add4(b, sr));
-  st4(sum_d, c0, nclients, vec, make_uint4(0, 0, 0, 0));
-  st4(sum_r, c0, nclients, vec, make_uint4(0, 0, 0, 0));
+  commit4(c0, nclients, sd, sr, a, b, gd, gr, sum_d, sum_r);
 }
 
 // multi-table forms (a queue group's step, dmc_group_step_device): the
