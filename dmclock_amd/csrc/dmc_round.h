@@ -488,15 +488,61 @@ struct KeyMap {
     return x < 0x1p63 ? (uint64_t)x : (1ull << 63);
   }
   // the largest ordered key in [kmin, kmax] whose coordinate is <= c
+  // (value map: a search from the map's inverse at c + 1, which lands within
+  // a few keys of the answer, galloping outwards to bracket it, then
+  // bisection -- the same key a bisection of the whole range finds, in a
+  // handful of map evaluations instead of ~64: one thread runs it while its
+  // block waits, 8 us of k_remit's pick in config 4's straddling P ranges)
   __device__ uint64_t max_key_at(uint64_t c, uint64_t kmax) const {
     if ((*this)(kmax) <= c) return kmax;
     if (scale == 0.0) return kmin + c;  // < kmax here
     uint64_t lo = kmin, hi = kmax;  // (*this)(lo) <= c < (*this)(hi)
+    {
+      const double v = __dadd_rn(vmin, __ddiv_rn((double)c + 1.0, scale));
+      uint64_t g = v == v ? okey(v) : lo + (hi - lo) / 2;
+      g = g <= lo ? lo + 1 : g >= hi ? hi - 1 : g;
+      if (g > lo && g < hi) {
+        if ((*this)(g) <= c) {
+          lo = g;
+          for (uint64_t st = 1; hi - lo > st; st <<= 1) {
+            const uint64_t t = lo + st;
+            if ((*this)(t) <= c) {
+              lo = t;
+            } else {
+              hi = t;
+              break;
+            }
+          }
+        } else {
+          hi = g;
+          for (uint64_t st = 1; hi - lo > st; st <<= 1) {
+            const uint64_t t = hi - st;
+            if ((*this)(t) <= c) {
+              lo = t;
+              break;
+            }
+            hi = t;
+          }
+        }
+      }
+    }
     while (hi - lo > 1) {
       const uint64_t mid = lo + (hi - lo) / 2;
       if ((*this)(mid) <= c) lo = mid;
       else hi = mid;
     }
+#ifdef DMC_KEYMAP_CHECK
+    {  // (check builds: the plain bisection of the whole range agrees)
+      uint64_t l2 = kmin, h2 = kmax;
+      while (h2 - l2 > 1) {
+        const uint64_t mid = l2 + (h2 - l2) / 2;
+        if ((*this)(mid) <= c) l2 = mid;
+        else h2 = mid;
+      }
+      if (l2 != lo) printf("KEYMAP MISMATCH c=%llu fast=%llu bisect=%llu\n",
+                           (unsigned long long)c, (unsigned long long)lo, (unsigned long long)l2);
+    }
+#endif
     return lo;
   }
 };
