@@ -21,7 +21,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <initializer_list>
 #include <limits>
 #include <mutex>
 #include <vector>
@@ -5466,14 +5465,8 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
   return DMC_OK;
 }
 
-// the epoch kernels' grid: 4 entries per thread, one pass; their uint4 path
-// when every array is 16-byte aligned (a null map has no array)
-static uint32_t grid4(uint32_t n) { return (n + 4 * kBlock - 1) / (4 * kBlock); }
-static bool aligned16(std::initializer_list<const void*> ps) {
-  for (const void* p : ps)
-    if (reinterpret_cast<uintptr_t>(p) & 15u) return false;
-  return true;
-}
+// the epoch kernels' grid: kEpochPer entries per thread, one pass
+static uint32_t grid4(uint32_t n) { return (n + kEpochPer * kBlock - 1) / (kEpochPer * kBlock); }
 
 int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_client_of_slot,
                              const uint32_t* d_comp_delta, const uint32_t* d_comp_rho,
@@ -5486,7 +5479,7 @@ int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_c
   if (!d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
   hipLaunchKernelGGL(k_track_sums, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
                      n_slots, d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta,
-                     d_sum_rho, aligned16({d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta, d_sum_rho}));
+                     d_sum_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5500,7 +5493,7 @@ int dmc_tracker_commit(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd, uint32_t*
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho) return DMC_EINVAL;
   hipLaunchKernelGGL(k_track_commit, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
-                     n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho, aligned16({d_xd, d_xr, d_comp_delta, d_comp_rho}));
+                     n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5518,7 +5511,7 @@ int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
     return DMC_EINVAL;
   hipLaunchKernelGGL(k_track_collect, dim3(grid4(n_slots)), dim3(kBlock), 0,
                      q->stream, n_slots, d_client_of_slot, d_xd, d_xr, d_comp_delta,
-                     d_comp_rho, d_sum_delta, d_sum_rho, aligned16({d_client_of_slot, d_xd, d_xr, d_comp_delta, d_comp_rho, d_sum_delta, d_sum_rho}));
+                     d_comp_rho, d_sum_delta, d_sum_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }
@@ -5532,7 +5525,7 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
   if (!n_clients) return DMC_OK;
   if (!d_gdelta || !d_grho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
   hipLaunchKernelGGL(k_track_advance, dim3(grid4(n_clients)), dim3(kBlock), 0,
-                     q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho, aligned16({d_gdelta, d_grho, d_sum_delta, d_sum_rho}));
+                     q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
 }

@@ -93,69 +93,42 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
                    blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// The epoch kernels below take 4 consecutive entries per thread, loaded at
-// once (one level of loads: uint4 when the host found every array 16-byte
-// aligned), over a grid that covers the arrays in one pass -- a grid-stride
-// loop of single entries waited for each entry's load in turn (config 5's
-// 2M-slot commit: 15 us, its 16M-client advance: 84 us).
-__device__ inline uint4 ld4(const uint32_t* p, uint32_t s0, uint32_t n, bool vec) {
-  if (vec && s0 + 4 <= n) return ld_as<uint4>(p + s0);
-  uint4 v;
-  v.x = s0 < n ? p[s0] : 0u;
-  v.y = s0 + 1 < n ? p[s0 + 1] : 0u;
-  v.z = s0 + 2 < n ? p[s0 + 2] : 0u;
-  v.w = s0 + 3 < n ? p[s0 + 3] : 0u;
-  return v;
-}
-__device__ inline uint32_t u4at(const uint4& v, int j) {
-  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
-}
-// X += (d, r) and (d, r) cleared, only at the entries with a count: the
-// arrays are ~20 % dense per epoch at config 5, so writing whole groups of 4
-// moved more bytes than the scattered entries (k_track_advance 102 vs 84 us)
-__device__ inline void commit4(uint32_t s0, uint32_t n, const uint4& d, const uint4& r,
-                               const uint4& a, const uint4& b, uint32_t* xd, uint32_t* xr,
-                               uint32_t* cd, uint32_t* cr) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t dj = u4at(d, j), rj = u4at(r, j);
-    if (s0 + j < n && (dj | rj)) {
-      xd[s0 + j] = u4at(a, j) + dj;
-      xr[s0 + j] = u4at(b, j) + rj;
-      cd[s0 + j] = 0;
-      cr[s0 + j] = 0;
-    }
-  }
-}
-// the per-client sums of 4 slots' responses (atomics: the servers of a rank
-// collect concurrently on their own streams)
-__device__ inline void sums4(uint32_t s0, uint32_t nslots, const uint32_t* client_of_slot,
-                             const uint4& cd, const uint4& cr, bool vec, uint32_t* sum_d,
-                             uint32_t* sum_r) {
-  const uint4 cm = client_of_slot ? ld4(client_of_slot, s0, nslots, vec)
-                                  : make_uint4(s0, s0 + 1, s0 + 2, s0 + 3);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t d = u4at(cd, j), r = u4at(cr, j), c = u4at(cm, j);
-    if (d) atomicAdd(&sum_d[c], d);
-    if (r) atomicAdd(&sum_r[c], r);
-  }
-}
+// The epoch kernels below take kEpochPer entries per thread, a block's
+// kEpochPer x blockDim entries in wave-coalesced rows (entry base + j x
+// blockDim + thread), every entry's counts loaded before any is used (one
+// level of loads), over a grid that covers the arrays in one pass.  (A
+// grid-stride loop waited for each entry's load in turn; four consecutive
+// entries per thread, uint4 loads and stores, moved the stores off the
+// coalesced pattern: config 5's 16M-client advance 84 -> 102-140 us.)
+constexpr uint32_t kEpochPer = 4;
+__device__ inline uint32_t epoch_base() { return blockIdx.x * kEpochPer * blockDim.x + threadIdx.x; }
 
 // epoch end, per server: my_delta / my_rho of its responses (X += own) and
-// the server's contribution to the per-client sums
-// (a group of 4 entries with every count 0 is skipped; adding and clearing
-// a zero entry is the identity)
+// the server's contribution to the per-client sums (atomics: the servers of
+// a rank collect concurrently on their own streams)
 __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
                                 uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
-                                uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r, bool vec) {
-  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (s0 >= nslots) return;
-  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
-  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
-  const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
-  commit4(s0, nslots, cd, cr, a, b, xd, xr, comp_d, comp_r);
-  sums4(s0, nslots, client_of_slot, cd, cr, vec, sum_d, sum_r);
+                                uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r) {
+  const uint32_t e0 = epoch_base();
+  uint32_t cd[kEpochPer], cr[kEpochPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    cd[j] = s < nslots ? comp_d[s] : 0u;
+    cr[j] = s < nslots ? comp_r[s] : 0u;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    if (!(cd[j] | cr[j])) continue;  // (nothing delivered to this slot)
+    xd[s] += cd[j];
+    xr[s] += cr[j];
+    comp_d[s] = 0;
+    comp_r[s] = 0;
+    const uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    if (cd[j]) atomicAdd(&sum_d[c], cd[j]);
+    if (cr[j]) atomicAdd(&sum_r[c], cr[j]);
+  }
 }
 
 // Overlapped (lagged) delivery, split in two: at an epoch's end only the
@@ -165,33 +138,54 @@ __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
 // (k_track_advance).
 __global__ void k_track_sums(uint32_t nslots, const uint32_t* client_of_slot,
                              const uint32_t* comp_d, const uint32_t* comp_r,
-                             uint32_t* sum_d, uint32_t* sum_r, bool vec) {
-  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (s0 >= nslots) return;
-  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
-  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
-  sums4(s0, nslots, client_of_slot, cd, cr, vec, sum_d, sum_r);
+                             uint32_t* sum_d, uint32_t* sum_r) {
+  const uint32_t e0 = epoch_base();
+  uint32_t cd[kEpochPer], cr[kEpochPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    cd[j] = s < nslots ? comp_d[s] : 0u;
+    cr[j] = s < nslots ? comp_r[s] : 0u;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    if (!(cd[j] | cr[j])) continue;
+    const uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    if (cd[j]) atomicAdd(&sum_d[c], cd[j]);
+    if (cr[j]) atomicAdd(&sum_r[c], cr[j]);
+  }
+}
+// X += counts and the counts cleared at the entries with any (commit: a
+// server's own responses; advance: after the all-reduce of the sums, the
+// global counters -- D += all servers' responses to the client)
+__device__ inline void epoch_commit(uint32_t n, uint32_t* x0, uint32_t* x1, uint32_t* c0,
+                                    uint32_t* c1) {
+  const uint32_t e0 = epoch_base();
+  uint32_t a[kEpochPer], b[kEpochPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    a[j] = s < n ? c0[s] : 0u;
+    b[j] = s < n ? c1[s] : 0u;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kEpochPer; ++j) {
+    const uint32_t s = e0 + j * blockDim.x;
+    if (!(a[j] | b[j])) continue;
+    x0[s] += a[j];
+    x1[s] += b[j];
+    c0[s] = 0;
+    c1[s] = 0;
+  }
 }
 __global__ void k_track_commit(uint32_t nslots, uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
-                               uint32_t* comp_r, bool vec) {
-  const uint32_t s0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (s0 >= nslots) return;
-  const uint4 cd = ld4(comp_d, s0, nslots, vec), cr = ld4(comp_r, s0, nslots, vec);
-  if (!(cd.x | cd.y | cd.z | cd.w | cr.x | cr.y | cr.z | cr.w)) return;
-  const uint4 a = ld4(xd, s0, nslots, vec), b = ld4(xr, s0, nslots, vec);
-  commit4(s0, nslots, cd, cr, a, b, xd, xr, comp_d, comp_r);
+                               uint32_t* comp_r) {
+  epoch_commit(nslots, xd, xr, comp_d, comp_r);
 }
-
-// after the all-reduce of the sums: the global counters advance (D += all
-// servers' responses to the client), sums cleared for the next epoch
 __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
-                                uint32_t* sum_d, uint32_t* sum_r, bool vec) {
-  const uint32_t c0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (c0 >= nclients) return;
-  const uint4 sd = ld4(sum_d, c0, nclients, vec), sr = ld4(sum_r, c0, nclients, vec);
-  if (!(sd.x | sd.y | sd.z | sd.w | sr.x | sr.y | sr.z | sr.w)) return;
-  const uint4 a = ld4(gd, c0, nclients, vec), b = ld4(gr, c0, nclients, vec);
-  commit4(c0, nclients, sd, sr, a, b, gd, gr, sum_d, sum_r);
+                                uint32_t* sum_d, uint32_t* sum_r) {
+  epoch_commit(nclients, gd, gr, sum_d, sum_r);
 }
 
 // multi-table forms (a queue group's step, dmc_group_step_device): the
