@@ -28,10 +28,14 @@ def main():
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
     starts = [i for i, x in enumerate(rows) if "k_add_link" in x["Kernel_Name"]]
     # a step runs from its k_add_link to the next one; the trace's last step
-    # ends at its last engine kernel (k_*), so that what runs after the
-    # timed region (the runtime's result copies, copyBuffer) is not counted
+    # ends at its last round kernel (a round's apply or terminal pull, a
+    # queue group's tallies and epoch delivery), so that what runs after the
+    # timed region (the bench's queue-size check k_count_requests, the
+    # runtime's result copies) is not counted
+    tail = ("k_rapply", "k_rfinish", "k_round_future", "k_put_result", "k_tally",
+            "k_track_")
     end = len(rows)
-    while end > starts[-1] + 1 and "k_" not in rows[end - 1]["Kernel_Name"]:
+    while end > starts[-1] + 1 and not any(t in rows[end - 1]["Kernel_Name"] for t in tail):
         end -= 1
     starts.append(end)
     hi = len(starts) - 1 - a.skip_last
