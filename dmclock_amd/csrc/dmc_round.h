@@ -799,21 +799,26 @@ constexpr int kBinsPerThreadR = kHistBinsR / kPickHalf;
 // PhaseSel::valid of a phase the pick wrote (k_rrank fails a round whose
 // selections are not both written: DMC_EDEVICE, never a short dispatch)
 constexpr uint32_t kSelValid = 0x5e1ec7edu;
-__device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum) {
+// (trail: a barrier after the reads, for a caller that reuses wsum; the
+// pick gives each of its scans its own words instead)
+#ifndef DMC_PICK_LEAN
+#define DMC_PICK_LEAN 1
+#endif
+__device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum, bool trail = true) {
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
   const uint32_t incl = wscan_u32(v);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   uint32_t wbase = 0;
   for (int i = 0; i < w; ++i) wbase += wsum[i];
-  __syncthreads();
+  if (trail) __syncthreads();
   return wbase + incl - v;
 }
 
 // The same for a pair of counts (the histogram's keys and non-empty bins),
 // with the half's total of the first (wsum: 2 x kPickHalf / 64 words)
 __device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, uint32_t* ev,
-                                       uint32_t* ez, uint32_t* tv) {
+                                       uint32_t* ez, uint32_t* tv, bool trail = true) {
   constexpr int NW = kPickHalf / 64;
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
   const uint32_t iv = wscan_u32(v), iz = wscan_u32(z);
@@ -830,7 +835,7 @@ __device__ inline void half_excl_scan2(uint32_t v, uint32_t z, uint32_t* wsum, u
     }
     tt += wsum[i];
   }
-  __syncthreads();
+  if (trail) __syncthreads();
   *ev = bv + iv - v;
   *ez = bz + iz - z;
   *tv = tt;
@@ -897,7 +902,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   if (DMC_PICK_CLOCKS) asm volatile("" ::"v"(local));
   pclock(pc, 7);
   uint32_t before, zbefore, total;
-  half_excl_scan2(local, lz, wsum, &before, &zbefore, &total);
+  half_excl_scan2(local, lz, wsum, &before, &zbefore, &total, !DMC_PICK_LEAN);
   pclock(pc, 8);
   if (need && ne > need && before < need_h && before + local >= need_h) {
     uint32_t cum = before, cz = zbefore;
@@ -961,7 +966,8 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     ns[j] = (b <= tb && h[j]) ? 1u + e : 0u;
     lns += ns[j];
   }
-  uint32_t nb = half_excl_scan(lns, wsum);
+  uint32_t nb = half_excl_scan(lns, DMC_PICK_LEAN ? wsum + 2 * (kPickHalf / 64) : wsum,
+                               !DMC_PICK_LEAN);
 #pragma unroll
   for (int j = 0; j < kBinsPerThreadR; ++j) {
     const uint32_t b = t * kBinsPerThreadR + j;
@@ -1022,7 +1028,7 @@ __device__ inline uint32_t need_hist(uint32_t need, int sampled) {
 __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
                           uint32_t* sbn, PhaseSel* ps, int sampled, uint32_t fault,
                           uint64_t* pc = nullptr) {
-  __shared__ uint32_t wsum[2][2 * kPickHalf / 64];
+  __shared__ uint32_t wsum[2][3 * kPickHalf / 64];
   __shared__ uint32_t s_sel[2][4], s_def[2][2];
   __shared__ uint64_t s_T[2];
   const bool p_runs = tot.n_r < (uint64_t)k;
@@ -1038,11 +1044,15 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
   pclock(pc, 6);
   pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hv,
              sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p], pc);
-  __syncthreads();  // (ps, written by thread 0 of each half)
   // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset, as a pick
-  // that misses a phase would leave it; k_rrank must fail the round
-  if ((fault & 1u) && threadIdx.x == 0) ps[1].valid = 0;
-  __syncthreads();
+  // that misses a phase would leave it; k_rrank must fail the round (lean:
+  // by the thread that wrote it, before the one barrier)
+  if (DMC_PICK_LEAN && (fault & 1u) && threadIdx.x == kPickHalf) ps[1].valid = 0;
+  __syncthreads();  // (ps, written by thread 0 of each half)
+  if (!DMC_PICK_LEAN) {
+    if ((fault & 1u) && threadIdx.x == 0) ps[1].valid = 0;
+    __syncthreads();
+  }
 }
 
 // The same pick by one wave per phase (wave 0: R, wave 1: P), 32 histogram
