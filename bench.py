@@ -79,6 +79,9 @@ def _stage_bytes(N, R, D, C, E, A, sampled=True):
         # k_chain_scan (a fused call's add chain beside the round's scan, one
         #   launch): the two stages' bytes
         "chain_scan": (46 if sampled else 62) * N + 278 * R,
+        # k_apply_link (pipelined calls: the previous call's deferred apply
+        #   beside this call's filing, one launch): the two stages' bytes
+        "apply_link": 196 * C + 20 * R,
     }
 
 
@@ -647,8 +650,10 @@ def main():
                                for n, (c, ms) in prof.items() if c},
         "stages_note": "stage times from a second pass of prof_steps steps "
                        "after the timed region, the same calls with the same "
-                       "kernels (fused, pipelined, launched eagerly: add_link, "
-                       "chain_scan, select, emit, rank, apply) behind a "
+                       "kernels (fused, pipelined, launched eagerly: "
+                       "apply_link -- the previous call's deferred apply beside "
+                       "this call's add_link, one launch -- chain_scan, select, "
+                       "emit, rank; the pass's last apply alone) behind a "
                        "GPU-side gate: one-kernel stages timed by HIP events "
                        "the kernel's own dispatch records "
                        "(hipExtLaunchKernel: execution time, as rocprofv3 "

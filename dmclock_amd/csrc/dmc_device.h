@@ -87,6 +87,10 @@ struct alignas(32) ScanRec {
                         // outside a batch)
 };
 static_assert(sizeof(ScanRec) == 32, "ScanRec must be 32 bytes");
+static_assert(offsetof(ScanRec, head) == 24 && offsetof(ScanRec, count) == 25 &&
+                  offsetof(ScanRec, flags) == 26 && offsetof(ScanRec, stamp) == 27 &&
+                  offsetof(ScanRec, nadd) == 28,
+              "ScanRec cursor layout");
 
 // The ClientInfo client_info_f returns for a client now (its inverses): the
 // caller publishes it with dmc_client_bind_info_batch.  With dynamic_info

@@ -146,12 +146,21 @@ __global__ void k_register(Table tb, BoundInfo* binfo, uint32_t n, const uint32_
 // The first node of an add segment: its arguments are the segment's per-call
 // parameters (updated in place on graph replays); block 0 publishes them for
 // k_add_chain.
-__device__ __attribute__((always_inline)) inline void add_link_body(AddParams p, Table tb, uint32_t* abuf, uint32_t* apos, uint32_t* aslot, AddParams* pblk, ActBuf act) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// (bid: the block's index among the filing blocks; prev: k_apply_link, where
+// the previous call's round is applied beside this filing -- its gate is
+// being written by that launch, so the round's outcome is read instead:
+// the gate shut before it (the round skipped), or the round failing or
+// needing the host, shuts this call too, exactly as the gate would)
+__device__ __attribute__((always_inline)) inline void add_link_body(AddParams p, Table tb, uint32_t* abuf, uint32_t* apos, uint32_t* aslot, AddParams* pblk, ActBuf act, uint32_t bid = 0xffffffffu, const Round* prev = nullptr) {
+  uint32_t i = (bid == 0xffffffffu ? blockIdx.x : bid) * blockDim.x + threadIdx.x;
   // (the request's slot requested with the gate word: one level of loads)
   uint32_t s = 0;
   if (DMC_EARLY_LOADS && i < p.n) s = p.reqs[i].slot;
-  if (tb.gate && *tb.gate) return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
+  if (prev) {
+    if (prev->skip || prev->overflow || prev->n_dec < prev->k_total) return;
+  } else if (tb.gate && *tb.gate) {
+    return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
+  }
   if (i == 0) *pblk = p;
   if (i >= p.n) return;
   if (act.cold) {
@@ -180,6 +189,23 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
   }
   // (filing order 0 replays the client's requests and knows its own position)
   if (pos - 1u < kAddSlots - 1u) abuf[(size_t)s * kAddSlots + pos] = i;
+}
+// A pipelined call's filing beside the previous call's apply, one launch
+// (DMC_DEFER_APPLY): blocks [0, napply) apply the previous round (its
+// k_rapply, deferred to this launch), the rest file this call's requests
+// (its k_add_link).  The two touch disjoint state: the apply writes a slot's
+// front keys and cursor bytes (sc_store_front), the filing its batch count
+// and stamp (bytes 27-31 of the same ScanRec) and the batch buffers.
+__global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
+k_apply_link(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
+             const uint32_t* decof, const PostRec* post, unsigned long long* sched,
+             HostRound* h, uint32_t napply, AddParams ap, uint32_t* abuf, uint32_t* apos,
+             uint32_t* aslot, AddParams* pblk) {
+  if (blockIdx.x < napply) {
+    rapply_body(tb, rd, cand, bcand, decof, post, sched, h, nullptr, blockIdx.x, napply);
+    return;
+  }
+  add_link_body(ap, tb, abuf, apos, aslot, pblk, ActBuf{}, blockIdx.x - napply, rd);
 }
 // the epoch wrapped: no slot may keep a stamp equal to a later batch's
 __global__ void k_clear_stamps(Table tb) {
@@ -2102,6 +2128,7 @@ struct dmc_queue {
     double now = 0.0;
     dmc_decision* out = nullptr;
     dmc_pull_result* res = nullptr;
+    bool apply = false;  // its round's k_rapply not launched yet (DMC_DEFER_APPLY)
   } pend;
   unsigned long long* sched = nullptr;  // [0] reservation, [1] priority
   unsigned long long* reqcount = nullptr;
@@ -2290,7 +2317,7 @@ namespace {
 
 const char* kStageNames[DMC_PROF_NSTAGES] = {
     "add_link", "add_chain", "activate", "scan", "select", "emit", "sort",
-    "rank", "apply", "step", "future", "cand", "chain_scan"};
+    "rank", "apply", "step", "future", "cand", "chain_scan", "apply_link"};
 
 // Profiling launches eagerly; a short GPU-side delay queued ahead of a
 // profiled call lets the host enqueue all of the call's kernels before the
@@ -3243,7 +3270,9 @@ bool use_sample(const dmc_queue* q, bool radix) {
 
 // (scanned: the scan already ran with that many partials -- k_chain_scan,
 // enqueue_add_round_overlap)
-void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scanned = 0) {
+void launch_apply(dmc_queue* q);
+void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scanned = 0,
+                   bool defer_apply = false) {
   if (!scanned) prof_gate(q);
   const bool sampled = use_sample(q, radix);
   const Table& tb = q->tb;
@@ -3314,7 +3343,13 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
   }
   // (its last block ends the round: a round that ran out of work under
   // Wait / Reject is followed by the terminal pull, launched by the host)
-  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(kApplyPerEmit * gEm + 1), dim3(kBlockR), 0, tb, q->rd,
+  if (!defer_apply) launch_apply(q);
+}
+uint32_t apply_blocks(const dmc_queue* q) {
+  return kApplyPerEmit * ((q->tb.n + kEmitChunk - 1) / kEmitChunk) + 1;
+}
+void launch_apply(dmc_queue* q) {
+  klaunch(q, DMC_PROF_APPLY, k_rapply, dim3(apply_blocks(q)), dim3(kBlockR), 0, q->tb, q->rd,
           (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
           (const PostRec*)q->post, q->sched, q->d_hround,
           q->debug ? q->dbg_atime : nullptr);
@@ -3324,27 +3359,43 @@ void enqueue_round(dmc_queue* q, const CallParams& cp, bool radix, uint32_t scan
 // side by side (k_chain_scan: the scan leaves the batch's slots, which the
 // chain scans after their adds), then the rest of the round.
 constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
+#ifndef DMC_DEFER_APPLY
+#define DMC_DEFER_APPLY 1
+#endif
 #ifndef DMC_OVERLAP
 #define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
 #endif
 bool overlap_ok(const dmc_queue* q, uint32_t n) {
   return DMC_OVERLAP && !q->use_graphs && (n + kBlock - 1) / kBlock <= kFixPartsMax;
 }
-void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp) {
+// (merge_prev: the previous pipelined call's apply, deferred, runs in this
+// call's filing launch, k_apply_link; defer: this call's apply is left to
+// the next call's filing launch or to settle_pending)
+static_assert(kBlock == kBlockR, "k_apply_link: one block size for both parts");
+void enqueue_add_round_overlap(dmc_queue* q, AddParams ap, const CallParams& cp,
+                               bool merge_prev = false, bool defer = false) {
   const bool sampled = use_sample(q, false);
   const Table& tb = q->tb;
   ap.epoch = cp.epoch;
   const uint32_t g = (ap.n + kBlock - 1) / kBlock;
   prof_gate(q);
-  klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, tb, q->abuf,
-          q->apos, q->aslot, q->apblk, ActBuf{});
+  if (merge_prev) {
+    const uint32_t na = apply_blocks(q);
+    klaunch(q, DMC_PROF_APPLY_LINK, k_apply_link, dim3(na + g), dim3(kBlockR), 0, tb, q->rd,
+            (const CandRec*)q->cand, (const uint32_t*)q->bcand, (const uint32_t*)q->decof,
+            (const PostRec*)q->post, q->sched, q->d_hround, na, ap, q->abuf, q->apos,
+            q->aslot, q->apblk);
+  } else {
+    klaunch(q, DMC_PROF_ADD_LINK, k_add_link, dim3(g), dim3(kBlock), 0, ap, tb, q->abuf,
+            q->apos, q->aslot, q->apblk, ActBuf{});
+  }
   const uint32_t nS = (tb.n + kBlock * kScanChainSlots - 1) / (kBlock * kScanChainSlots);
   klaunch(q, DMC_PROF_CHAIN_SCAN, k_chain_scan, dim3(g + nS), dim3(kBlock), 0, tb,
           ap, (const uint32_t*)q->abuf, (const uint32_t*)q->apos,
           (const uint32_t*)q->aslot, g, nS, sampled ? nullptr : q->keyr,
           sampled ? nullptr : q->keyp, q->meta, q->rparts, q->rd, cp,
           sampled ? q->skr : nullptr, sampled ? q->skp : nullptr, q->k32, q->hist);
-  enqueue_round(q, cp, false, nS + g);
+  enqueue_round(q, cp, false, nS + g, defer);
 }
 
 int launch_round(dmc_queue* q, double now, uint32_t kk, dmc_decision* out,
@@ -3830,6 +3881,11 @@ int settle_pending(dmc_queue* q, bool* clean_out) {
   if (!q->pend.on) return DMC_OK;
   const dmc_queue::PendCall p = q->pend;
   q->pend.on = false;
+  if (p.apply) {  // (its round's apply, deferred and not merged: on its own)
+    q->pend.apply = false;
+    launch_apply(q);
+    HIP_OK(hipGetLastError());
+  }
   int rc = wait_round(q, p.seq);
   if (rc) return rc;
   const bool clean = !q->h_rd->overflow && q->h_rd->n_dec >= q->h_rd->k_total;
@@ -4856,9 +4912,20 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
       }
       CallParams cp{k,     0,   now, d_out, q->tick + n, d_result, ++q->round_seq, q->fault,
                     epoch, q->pipeline ? q->gate : nullptr};
+      // DMC_DEFER_APPLY (pipelined calls launched eagerly): this call's
+      // k_rapply is left to the next call's filing launch, where it runs
+      // beside that filing (k_apply_link), or to settle_pending; the previous
+      // call's deferred apply merges into this launch, or -- on any other
+      // path -- is launched first, before this call's work
+      const bool defer = DMC_DEFER_APPLY && q->pipeline && overlap_ok(q, n);
+      const bool merge = defer && q->pend.on && q->pend.apply;
+      if (q->pend.on && q->pend.apply && !merge) {
+        q->pend.apply = false;
+        launch_apply(q);
+      }
       auto enqueue = [&] {
         if (overlap_ok(q, n)) {
-          enqueue_add_round_overlap(q, ap, cp);
+          enqueue_add_round_overlap(q, ap, cp, merge, defer);
         } else {
           enqueue_add(q, ap);
           enqueue_round(q, cp, false);
@@ -4888,6 +4955,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         if (rc) return rc;
       }
       q->tick += n;
+      if (merge) q->pend.apply = false;  // (launched beside this call's filing)
       if (q->pipeline) {
         // the previous call, finished now that this one is queued behind it
         bool clean = true;
@@ -4915,6 +4983,7 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         q->pend.now = now;
         q->pend.out = d_out;
         q->pend.res = d_result;
+        q->pend.apply = defer;
         return DMC_OK;
       }
       dmc_pull_result r{};
@@ -5465,8 +5534,6 @@ int dmc_tracker_fill(dmc_queue* q, dmc_request* d_reqs, uint32_t n,
   return DMC_OK;
 }
 
-// the epoch kernels' grid: kEpochPer entries per thread, one pass
-static uint32_t grid4(uint32_t n) { return (n + kEpochPer * kBlock - 1) / (kEpochPer * kBlock); }
 
 int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_client_of_slot,
                              const uint32_t* d_comp_delta, const uint32_t* d_comp_rho,
@@ -5477,7 +5544,7 @@ int dmc_tracker_collect_sums(dmc_queue* q, uint32_t n_slots, const uint32_t* d_c
   if (n_slots > q->p.max_clients) return DMC_EINVAL;
   if (!n_slots) return DMC_OK;
   if (!d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_sums, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
+  hipLaunchKernelGGL(k_track_sums, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
                      n_slots, d_client_of_slot, d_comp_delta, d_comp_rho, d_sum_delta,
                      d_sum_rho);
   HIP_OK(hipGetLastError());
@@ -5492,7 +5559,7 @@ int dmc_tracker_commit(dmc_queue* q, uint32_t n_slots, uint32_t* d_xd, uint32_t*
   if (n_slots > q->p.max_clients) return DMC_EINVAL;
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_commit, dim3(grid4(n_slots)), dim3(kBlock), 0, q->stream,
+  hipLaunchKernelGGL(k_track_commit, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, q->stream,
                      n_slots, d_xd, d_xr, d_comp_delta, d_comp_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;
@@ -5509,7 +5576,7 @@ int dmc_tracker_collect(dmc_queue* q, uint32_t n_slots,
   if (!n_slots) return DMC_OK;
   if (!d_xd || !d_xr || !d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho)
     return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_collect, dim3(grid4(n_slots)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_track_collect, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0,
                      q->stream, n_slots, d_client_of_slot, d_xd, d_xr, d_comp_delta,
                      d_comp_rho, d_sum_delta, d_sum_rho);
   HIP_OK(hipGetLastError());
@@ -5524,7 +5591,7 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
   if (!q) return DMC_EINVAL;
   if (!n_clients) return DMC_OK;
   if (!d_gdelta || !d_grho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
-  hipLaunchKernelGGL(k_track_advance, dim3(grid4(n_clients)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_track_advance, dim3(grid_for(n_clients, 2048)), dim3(kBlock), 0,
                      q->stream, n_clients, d_gdelta, d_grho, d_sum_delta, d_sum_rho);
   HIP_OK(hipGetLastError());
   return DMC_OK;

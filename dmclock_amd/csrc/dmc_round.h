@@ -2618,7 +2618,19 @@ struct RoundC {
 #ifndef DMC_APPLY_STAGE
 #define DMC_APPLY_STAGE 4
 #endif
-constexpr int kApplyStage = DMC_APPLY_STAGE;  // queue positions staged per candidate (LDS)
+constexpr int kApplyStage = DMC_APPLY_STAGE;
+// A popped slot's new ScanRec: its front keys and cursor bytes (head, count,
+// flags), never its stamp and batch count (bytes 27-31): the next call's
+// filing (k_add_link's atomic on the count, its stamp) may run beside this
+// round's apply in one launch (k_apply_link, the deferred apply of
+// pipelined calls).  Outside a batch the count is 0 already.
+__device__ inline void sc_store_front(const Table& tb, uint32_t s, const ScanRec& o) {
+  char* d = reinterpret_cast<char*>(tb.sc + s);
+  st_as(d, make_ulonglong2(dbits(o.r), dbits(o.pk)));
+  st_as(d + 16, dbits(o.l));
+  st_as(d + 24, (uint16_t)(o.head | ((uint32_t)o.count << 8)));
+  st_as(d + 26, o.flags);
+}  // queue positions staged per candidate (LDS)
 __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd,
                                  ReqEntry* st) {
   // every load that depends only on the candidate record is issued before
@@ -2736,7 +2748,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
     if (seen && front.l <= now) f |= F_READY;
   }
   o.flags = f;
-  tb.sc[s] = o;
+  sc_store_front(tb, s, o);
 }
 
 // Candidates (the dense list) with dispatched pops replay their walks for
@@ -2864,7 +2876,7 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
     if (seen && (bits & 2u)) f |= F_READY;
   }
   o.flags = f;
-  tb.sc[s] = o;
+  sc_store_front(tb, s, o);
 }
 
 // Candidates, one thread each; k_rapply's blocks 2j and 2j + 1 take emit
@@ -2891,26 +2903,28 @@ constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 // 256-thread blocks per CU needs; a higher bound only warns)
 #define DMC_APPLY_MINB 2
 #endif
-__device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg) {
+// (bid / nblk: the block's index among the apply blocks and their count --
+// k_rapply's own grid, or the first nblk blocks of k_apply_link)
+__device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg, uint32_t bid, uint32_t nblk) {
   if (rd->skip) return;
   // A limit-break round's priority pops (group heads and their runs'
   // readied fronts) are counted here: its summary goes out once every block
   // has counted (a ticket), not from the extra block at once
   const bool brk = rd->brk && !rd->overflow;
-  if (blockIdx.x == gridDim.x - 1 && !brk) {
+  if (bid == nblk - 1 && !brk) {
     // the extra block publishes the round's summary (complete since k_rrank)
     // to host memory at once: the host learns the outcome while the other
     // blocks store the state, and its next launch is stream-ordered behind them
     rfinish_body(rd, h, true);
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && !rd->overflow && !brk) {
+  if (bid == 0 && threadIdx.x == 0 && !rd->overflow && !brk) {
     sched[0] += rd->n_dec - rd->n_prio;
     sched[1] += rd->n_prio;
   }
-  if (blockIdx.x < gridDim.x - 1) {
+  if (bid < nblk - 1) {
     // (kApplyPerEmit apply blocks per emit block)
-    const uint32_t eb = blockIdx.x / kApplyPerEmit;
+    const uint32_t eb = bid / kApplyPerEmit;
     const uint32_t nc = bcand[eb];
     const uint32_t base = eb * kEmitChunk;
     RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
@@ -2918,7 +2932,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
     __shared__ ReqEntry stage[kBlockR * kApplyStage];
     // (interleaved: the emit block's candidates, about 280, split evenly over
     // its apply blocks rather than filling the first one)
-    for (uint32_t i = threadIdx.x * kApplyPerEmit + (blockIdx.x % kApplyPerEmit); i < nc;
+    for (uint32_t i = threadIdx.x * kApplyPerEmit + (bid % kApplyPerEmit); i < nc;
          i += kApplyPerEmit * kBlockR) {
       const uint32_t ci = base + i;
       uint64_t t0 = dbg ? wall_clock64() : 0;
@@ -2957,7 +2971,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
   __shared__ uint32_t s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&rd->brk_done, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) s_last = atomicAdd(&rd->brk_done, 1u) == nblk - 1;
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) {
@@ -2974,7 +2988,7 @@ __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB)
 k_rapply(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand,
          const uint32_t* decof, const PostRec* post, unsigned long long* sched,
          HostRound* h, uint64_t* dbg = nullptr) {
-  rapply_body(tb, rd, cand, bcand, decof, post, sched, h, dbg);
+  rapply_body(tb, rd, cand, bcand, decof, post, sched, h, dbg, blockIdx.x, gridDim.x);
 }
 
 __global__ void k_rfinish(const Round* rd, HostRound* h) { rfinish_body(rd, h); }
@@ -3230,7 +3244,8 @@ __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
 }
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB) k_rapply_m(const RApplyArgs* a) {
   const RApplyArgs& x = a[blockIdx.y];
-  rapply_body(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr);
+  rapply_body(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr, blockIdx.x,
+              gridDim.x);
 }
 
 // device-API result written by the host's view of a multi-round call

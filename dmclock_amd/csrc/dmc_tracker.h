@@ -93,41 +93,24 @@ __global__ void k_track_params(dmc_request* reqs, uint32_t n, uint32_t nslots,
                    blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// The epoch kernels below take kEpochPer entries per thread, a block's
-// kEpochPer x blockDim entries in wave-coalesced rows (entry base + j x
-// blockDim + thread), every entry's counts loaded before any is used (one
-// level of loads), over a grid that covers the arrays in one pass.  (A
-// grid-stride loop waited for each entry's load in turn; four consecutive
-// entries per thread, uint4 loads and stores, moved the stores off the
-// coalesced pattern: config 5's 16M-client advance 84 -> 102-140 us.)
-constexpr uint32_t kEpochPer = 4;
-__device__ inline uint32_t epoch_base() { return blockIdx.x * kEpochPer * blockDim.x + threadIdx.x; }
-
 // epoch end, per server: my_delta / my_rho of its responses (X += own) and
 // the server's contribution to the per-client sums (atomics: the servers of
 // a rank collect concurrently on their own streams)
 __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
                                 uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
                                 uint32_t* comp_r, uint32_t* sum_d, uint32_t* sum_r) {
-  const uint32_t e0 = epoch_base();
-  uint32_t cd[kEpochPer], cr[kEpochPer];
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    cd[j] = s < nslots ? comp_d[s] : 0u;
-    cr[j] = s < nslots ? comp_r[s] : 0u;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    if (!(cd[j] | cr[j])) continue;  // (nothing delivered to this slot)
-    xd[s] += cd[j];
-    xr[s] += cr[j];
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    uint32_t cd = comp_d[s];
+    if (!cd) continue;  // comp_r <= comp_d: nothing delivered to this slot
+    uint32_t cr = comp_r[s];
+    xd[s] += cd;
+    xr[s] += cr;
     comp_d[s] = 0;
     comp_r[s] = 0;
-    const uint32_t c = client_of_slot ? client_of_slot[s] : s;
-    if (cd[j]) atomicAdd(&sum_d[c], cd[j]);
-    if (cr[j]) atomicAdd(&sum_r[c], cr[j]);
+    uint32_t c = client_of_slot ? client_of_slot[s] : s;
+    atomicAdd(&sum_d[c], cd);
+    if (cr) atomicAdd(&sum_r[c], cr);
   }
 }
 
@@ -139,53 +122,40 @@ __global__ void k_track_collect(uint32_t nslots, const uint32_t* client_of_slot,
 __global__ void k_track_sums(uint32_t nslots, const uint32_t* client_of_slot,
                              const uint32_t* comp_d, const uint32_t* comp_r,
                              uint32_t* sum_d, uint32_t* sum_r) {
-  const uint32_t e0 = epoch_base();
-  uint32_t cd[kEpochPer], cr[kEpochPer];
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    cd[j] = s < nslots ? comp_d[s] : 0u;
-    cr[j] = s < nslots ? comp_r[s] : 0u;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    if (!(cd[j] | cr[j])) continue;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    const uint32_t cd = comp_d[s];
+    if (!cd) continue;
+    const uint32_t cr = comp_r[s];
     const uint32_t c = client_of_slot ? client_of_slot[s] : s;
-    if (cd[j]) atomicAdd(&sum_d[c], cd[j]);
-    if (cr[j]) atomicAdd(&sum_r[c], cr[j]);
-  }
-}
-// X += counts and the counts cleared at the entries with any (commit: a
-// server's own responses; advance: after the all-reduce of the sums, the
-// global counters -- D += all servers' responses to the client)
-__device__ inline void epoch_commit(uint32_t n, uint32_t* x0, uint32_t* x1, uint32_t* c0,
-                                    uint32_t* c1) {
-  const uint32_t e0 = epoch_base();
-  uint32_t a[kEpochPer], b[kEpochPer];
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    a[j] = s < n ? c0[s] : 0u;
-    b[j] = s < n ? c1[s] : 0u;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kEpochPer; ++j) {
-    const uint32_t s = e0 + j * blockDim.x;
-    if (!(a[j] | b[j])) continue;
-    x0[s] += a[j];
-    x1[s] += b[j];
-    c0[s] = 0;
-    c1[s] = 0;
+    atomicAdd(&sum_d[c], cd);
+    if (cr) atomicAdd(&sum_r[c], cr);
   }
 }
 __global__ void k_track_commit(uint32_t nslots, uint32_t* xd, uint32_t* xr, uint32_t* comp_d,
                                uint32_t* comp_r) {
-  epoch_commit(nslots, xd, xr, comp_d, comp_r);
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nslots;
+       s += gridDim.x * blockDim.x) {
+    const uint32_t cd = comp_d[s];
+    if (!cd) continue;
+    xd[s] += cd;
+    xr[s] += comp_r[s];
+    comp_d[s] = 0;
+    comp_r[s] = 0;
+  }
 }
+
+// after the all-reduce of the sums: the global counters advance (D += all
+// servers' responses to the client), sums cleared for the next epoch
 __global__ void k_track_advance(uint32_t nclients, uint32_t* gd, uint32_t* gr,
                                 uint32_t* sum_d, uint32_t* sum_r) {
-  epoch_commit(nclients, gd, gr, sum_d, sum_r);
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nclients;
+       c += gridDim.x * blockDim.x) {
+    gd[c] += sum_d[c];
+    gr[c] += sum_r[c];
+    sum_d[c] = 0;
+    sum_r[c] = 0;
+  }
 }
 
 // multi-table forms (a queue group's step, dmc_group_step_device): the

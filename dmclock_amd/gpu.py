@@ -83,7 +83,7 @@ EXPORTS = {
                                 ctypes.POINTER(_f64)]),
     "dmc_profile_stage_name": (ctypes.c_char_p, [_u32]),
 }
-PROF_NSTAGES = 13
+PROF_NSTAGES = 14
 
 # dmc_info_fn: int (*)(void* ctx, uint32_t slot, double* r, double* w, double* l)
 INFO_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _u32, ctypes.POINTER(_f64),

@@ -484,7 +484,9 @@ int dmc_queue_counters_sized(dmc_queue* q, void* out, uint64_t size, int reset);
 #define DMC_PROF_FUTURE 10  /* a round's terminal pull */
 #define DMC_PROF_CAND 11    /* k_rcand */
 #define DMC_PROF_CHAIN_SCAN 12 /* k_chain_scan: a fused call's add chain beside the round's scan */
-#define DMC_PROF_NSTAGES 13
+#define DMC_PROF_APPLY_LINK 13 /* k_apply_link: a pipelined call's filing beside the previous
+                                  call's deferred apply */
+#define DMC_PROF_NSTAGES 14
 
 int dmc_profile_enable(dmc_queue* q, int on);
 int dmc_profile_reset(dmc_queue* q);
