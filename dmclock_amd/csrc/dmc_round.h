@@ -877,16 +877,22 @@ __device__ inline PickBins pick_load(const uint32_t* hist) {
   }
   return b;
 }
+// one phase's totals (selected from a RoundPart without indexing it: the
+// caller may hold the RoundPart in registers)
+struct PhaseTot {
+  uint32_t cnt;
+  uint64_t mn, mx;
+};
 __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
-                                  const RoundPart& tot, const KeyMap& km, uint32_t sh1,
+                                  const PhaseTot& tot, const KeyMap& km, uint32_t sh1,
                                   const PickBins& hv, uint32_t* sbn, PhaseSel* ps,
                                   uint32_t* wsum, uint32_t* s_sel, uint32_t* s_def,
                                   uint64_t* s_T, uint64_t* pc = nullptr) {
   const int t = threadIdx.x & (kPickHalf - 1);
-  const uint32_t ne = tot.cnt[p];
+  const uint32_t ne = tot.cnt;
   const uint64_t hmin = 0;
   // the default: every key (T = all, or none) up to the top bin
-  const uint32_t tb0 = ne ? hist_bin(km(tot.mx[p]), hmin, sh1) : 0;
+  const uint32_t tb0 = ne ? hist_bin(km(tot.mx), hmin, sh1) : 0;
   if (t == 0) {
     s_sel[3] = 0;
     *s_T = (need == 0 || ne == 0) ? 0 : kMaxKey - 1;
@@ -916,9 +922,9 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
         // bin: the largest key)
         uint32_t b = t * kBinsPerThreadR + j;
         uint64_t edge = b == kHistBinsR - 1
-                            ? tot.mx[p]
+                            ? tot.mx
                             : km.max_key_at(sat_add_u64(hmin, ((uint64_t)(b + 1) << sh1) - 1),
-                                            tot.mx[p]);
+                                            tot.mx);
         // (rounded up to the end of its 32-bit quantum: see key32)
         *s_T = edge >= kMaxKey - 1 ? kMaxKey - 1 : (edge | 0xffffffffull);
         s_sel[0] = b;
@@ -985,15 +991,15 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   }
   if (t == 0) {
     PhaseSel z{};
-    z.kmin = tot.mn[p];
-    z.kmax = tot.mx[p];
+    z.kmin = tot.mn;
+    z.kmax = tot.mx;
     z.T = *s_T;
     z.n_elig = ne;
     z.hshift = sh1;
     z.tbin = tb;
     z.hmin = hmin;
     z.lo0 = hmin;
-    const uint64_t cmax = km(tot.mx[p]);
+    const uint64_t cmax = km(tot.mx);
     const uint64_t top = sat_add_u64(hmin, (uint64_t)(kHistBinsR - 1) << sh1);
     z.hitop = cmax > top ? cmax : top;
     z.vmin = km.vmin;
@@ -1039,10 +1045,12 @@ __device__ void pick_both(uint32_t k, const RoundPart& tot, const PickBins& hv,
   const uint32_t need = p == 0 ? (p_runs ? 0xffffffffu : k)
                                : (p_runs ? k - (uint32_t)tot.n_r : 0);
   pclock(pc, 5);
-  const KeyMap km(tot.mn[p], tot.mx[p]);
+  const PhaseTot pt{p ? tot.cnt[1] : tot.cnt[0], p ? tot.mn[1] : tot.mn[0],
+                    p ? tot.mx[1] : tot.mx[0]};
+  const KeyMap km(pt.mn, pt.mx);
   if (DMC_PICK_CLOCKS) asm volatile("" ::"v"(km.scale));
   pclock(pc, 6);
-  pick_phase(p, need, need_hist(need, sampled), tot, km, hist_shift_r(km(tot.mx[p])), hv,
+  pick_phase(p, need, need_hist(need, sampled), pt, km, hist_shift_r(km(pt.mx)), hv,
              sbn, &ps[p], wsum[p], s_sel[p], s_def[p], &s_T[p], pc);
   // test hook (DMC_OPT_FAULT 1): phase 1's selection left unset, as a pick
   // that misses a phase would leave it; k_rrank must fail the round (lean:
@@ -1769,6 +1777,16 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
     hv = pick_load(hist);
 #endif
   }
+  // the round's totals and call parameters, requested with the histogram
+  // (the pick's first use of them is then no load level of its own)
+  RoundPart tot_e;
+  uint32_t k_e = 0, sampled_e = 0, fault_e = 0;
+  if constexpr (!PRE) {
+    tot_e = rd->tot;
+    k_e = rd->k_total;
+    sampled_e = rd->sampled;
+    fault_e = rd->fault;
+  }
   if (DMC_EARLY_LOADS && rd->skip) return;
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
@@ -1807,7 +1825,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
 #if DMC_PICK_WAVE
     pick_both_w(rd->k_total, hv, ltab, s_ph, (int)rd->sampled, rd->fault);
 #else
-    pick_both(rd->k_total, rd->tot, hv, ltab, s_ph, (int)rd->sampled, rd->fault,
+    pick_both(k_e, tot_e, hv, ltab, s_ph, (int)sampled_e, fault_e,
               eclk ? eclk + kEClk * blockIdx.x : nullptr);
 #endif
     if (blockIdx.x == 0 && threadIdx.x < 2) rd->ph[threadIdx.x] = s_ph[threadIdx.x];  // (the summary)
