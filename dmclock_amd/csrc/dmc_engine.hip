@@ -334,6 +334,9 @@ k_chain_scan(Table tb, AddParams ap, const uint32_t* abuf, const uint32_t* apos,
              const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
              uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
              uint64_t* skr, uint64_t* skp, uint2* k32, uint32_t* hist) {
+#ifdef DMC_DBG_CS_SIDE  // (timing probe, wrong results: 1 = scan side only, 2 = chain side only)
+  if ((DMC_DBG_CS_SIDE == 1) == (blockIdx.x < nchain)) return;
+#endif
   if (blockIdx.x >= nchain) {
     rscan_body_g<false, kBlock, true, kScanChainSlots>(tb, keyr, keyp, meta, parts, rd, cp, skr,
                                                        skp, k32, hist, blockIdx.x - nchain,
