@@ -329,7 +329,12 @@ __device__ __attribute__((always_inline)) inline void chain_scan_chain(
   block_rpart_store<kBlock>(acc, part);
 }
 
-__global__ void __launch_bounds__(kBlock)
+// (DMC_CHAIN_SCAN_MINW waves per SIMD: its register bound; at 117 VGPRs,
+// 4 waves, the scan's 1,024 blocks and the chain's 256 did not fit at once)
+#ifndef DMC_CHAIN_SCAN_MINW
+#define DMC_CHAIN_SCAN_MINW 4
+#endif
+__global__ void __launch_bounds__(kBlock, DMC_CHAIN_SCAN_MINW)
 k_chain_scan(Table tb, AddParams ap, const uint32_t* abuf, const uint32_t* apos,
              const uint32_t* aslot, uint32_t nchain, uint32_t nscan, uint64_t* keyr,
              uint64_t* keyp, uint32_t* meta, RoundPart* parts, Round* rd, CallParams cp,
