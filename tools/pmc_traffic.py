@@ -26,6 +26,10 @@ STAGES = {
     # (bench.py's default launch: the add chain beside the scan, then the
     # batch's slots scanned)
     "chain_scan": ["k_chain_scan", "k_scan_fix"],
+    # (pipelined calls: the previous call's deferred apply beside this call's
+    # filing, one launch; "apply" and "add_link" then count only the other
+    # phases' launches -- pre-population, settle -- not the bench's steps)
+    "apply_link": ["k_apply_link"],
 }
 CALIB = ["stream16", "rand64", "rand32", "rand16", "rand8"]
 STREAMING = {"scan", "select", "future"}
@@ -143,6 +147,11 @@ def main():
         # k_add_chain ran only outside them (pre-population, settle rounds)
         out.pop("scan", None)
         out.pop("add_chain", None)
+    if out.get("apply_link", {}).get("fetch_size_bytes_raw"):
+        # pipelined steps: the apply ran beside the next call's filing;
+        # k_rapply and k_add_link ran alone only outside them
+        out.pop("apply", None)
+        out.pop("add_link", None)
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out.items():
         print(f"{k:10s} fetch(raw) {v['fetch_size_bytes_raw']/1e6:8.2f} MB  write {v['write_size_bytes']/1e6:8.2f} MB  hbm(corr) {v['hbm_bytes']/1e6:8.2f} MB")

@@ -26,14 +26,17 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
-    starts = [i for i, x in enumerate(rows) if "k_add_link" in x["Kernel_Name"]]
+    # (pipelined calls after the first: k_apply_link, the previous call's
+    # deferred apply beside this call's filing)
+    starts = [i for i, x in enumerate(rows)
+              if "k_add_link" in x["Kernel_Name"] or "k_apply_link" in x["Kernel_Name"]]
     # a step runs from its k_add_link to the next one; the trace's last step
     # ends at its last round kernel (a round's apply or terminal pull, a
     # queue group's tallies and epoch delivery), so that what runs after the
     # timed region (the bench's queue-size check k_count_requests, the
     # runtime's result copies) is not counted
     tail = ("k_rapply", "k_rfinish", "k_round_future", "k_put_result", "k_tally",
-            "k_track_")
+            "k_track_", "k_rrank")
     end = len(rows)
     while end > starts[-1] + 1 and not any(t in rows[end - 1]["Kernel_Name"] for t in tail):
         end -= 1
