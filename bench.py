@@ -109,7 +109,10 @@ def roofline(args, prof, prof_steps, ctr, k, n_clients=None, n_adds=None,
     per = {}
     for ms_s, nm in cand:
         c = prof[nm][0]
-        bl = model[nm] / (c / prof_steps)
+        # (a stage launched several times per step shares the step's bytes;
+        # one launched less than once per step -- the pipelined pass's first
+        # filing alone, its last apply alone -- still does one call's work)
+        bl = model[nm] / max(c / prof_steps, 1.0)
         a_s = ms_s / c / 1e3
         per[nm] = {"bytes_per_launch": int(bl), "avg_launch_us": round(a_s * 1e6, 2),
                    "launches_per_step": round(c / prof_steps, 2),
