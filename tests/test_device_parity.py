@@ -609,6 +609,42 @@ def test_pipelined_calls_parity(variant):
     qg.close()
 
 
+def test_pipelined_deferred_apply_interleaved():
+    """DMC_DEFER_APPLY: a pipelined call's apply is launched by the next
+    call's filing launch (k_apply_link) -- or, before any other work, by
+    whatever comes next.  Pipelined calls (kernels launched eagerly) with a
+    lone add batch, a small pull (the single-op path, no fusing) and a lone
+    batched pull between them, and the queue's statistics read in the
+    middle: every status, decision and result record bit-exact against the
+    oracle, and the sampled states at the end."""
+    from dmclock_amd._abi import OPT_GRAPHS
+    from dmclock_amd.gpu import GpuQueue
+    tr = workloads.config3_trace(7, 1 << 16, 6, 1 << 12, depth=2)
+    t = float(tr.ops[3][1])
+    extra = workloads.arrivals(np.random.default_rng(9), 1 << 16, 1 << 11, t, 2.0 * (1 << 16),
+                               handle_base=10 ** 7)
+    te = float(extra["time"][-1])
+    tr.ops[4:4] = [("add", extra), ("pull", te, 4), ("pull", te, 1 << 12)]
+    qo = pyoracle.OracleQueue()
+    outs_o = workloads.replay(qo, tr)
+    assert qo.ties == 0
+    qg = GpuQueue(max_clients=1 << 16, ring_capacity=64, max_batch=1 << 16)
+    qg.set_option(OPT_GRAPHS, 0)
+    outs_g = replay_pipelined(qg, tr)
+    assert len(outs_g) == len(outs_o)
+    for i, (a, b) in enumerate(zip(outs_g, outs_o)):
+        assert a[0] == b[0], i
+        if a[0] == "add":
+            assert np.array_equal(a[1], b[1]), (i, np.nonzero(a[1] != b[1]))
+        else:
+            compare_decisions(a[1], b[1], f"op {i}")
+            assert a[2] == b[2], (i, a[2], b[2])
+    compare_states(qg, qo, np.random.default_rng(4).choice(1 << 16, 2048, replace=False),
+                   "final")
+    assert qg.counters()["fused_calls"] >= 6
+    qg.close()
+
+
 def test_pipelined_bench_call_parity_1m_clients():
     """bench.py's timed call as it runs by default (DMC_OPT_PIPELINE, kernels
     launched eagerly) at full size: 1,048,576 clients, four pipelined steps of 64K adds + 64K
