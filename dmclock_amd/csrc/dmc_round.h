@@ -804,6 +804,9 @@ constexpr uint32_t kSelValid = 0x5e1ec7edu;
 #ifndef DMC_PICK_LEAN
 #define DMC_PICK_LEAN 1
 #endif
+#ifndef DMC_PICK_ONESCAN
+#define DMC_PICK_ONESCAN 1
+#endif
 __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum, bool trail = true) {
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
   const uint32_t incl = wscan_u32(v);
@@ -963,6 +966,32 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
   // bin's first rank bin, which keeps the map monotone.
   const uint32_t S = kNBPhase > nz ? kNBPhase - nz : 0;
   const float q = (float)S / (float)C;
+#if DMC_PICK_ONESCAN
+  // (one scan: bin b's first rank bin is the non-empty bins before it plus
+  // floor(the keys before it x S / C) -- both prefixes are the first scan's,
+  // so no second scan; monotone, one rank bin at least per non-empty bin,
+  // the spare ones in proportion to the counts as above; bins past T's are
+  // never looked up, rank_bin_r clamps to the table's last bin)
+  {
+    uint32_t cb = before, cz = zbefore;
+#pragma unroll
+    for (int j = 0; j < kBinsPerThreadR; ++j) {
+      const uint32_t b = t * kBinsPerThreadR + j;
+      const uint32_t f0 = cz + (uint32_t)((float)cb * q);
+      cb += h[j];
+      cz += h[j] ? 1u : 0u;
+      const uint32_t f1 = cz + (uint32_t)((float)cb * q);
+      uint32_t first = f0, num = (b <= tb && h[j]) ? f1 - f0 : 0u;
+      if (b > tb || first >= (uint32_t)kNBPhase) {
+        first = kNBPhase - 1;
+        num = num ? 1 : 0;
+      } else if (first + num > (uint32_t)kNBPhase) {
+        num = kNBPhase - first;
+      }
+      sbn[p * kHistBinsR + b] = (p * kNBPhase + first) | (num << 16);
+    }
+  }
+#else
   uint32_t ns[kBinsPerThreadR], lns = 0;
 #pragma unroll
   for (int j = 0; j < kBinsPerThreadR; ++j) {
@@ -989,6 +1018,7 @@ __device__ inline void pick_phase(int p, uint32_t need, uint32_t need_h,
     sbn[p * kHistBinsR + b] = (p * kNBPhase + first) | (num << 16);
     nb += ns[j];
   }
+#endif
   if (t == 0) {
     PhaseSel z{};
     z.kmin = tot.mn;
