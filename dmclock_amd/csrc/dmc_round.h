@@ -804,8 +804,11 @@ constexpr uint32_t kSelValid = 0x5e1ec7edu;
 #ifndef DMC_PICK_LEAN
 #define DMC_PICK_LEAN 1
 #endif
+// (DMC_PICK_ONESCAN=1: the rank-bin table from the first scan's prefixes,
+// no second scan: emit 26.8-27.3 and rank 10.9-11.0 against 26.6 and
+// 10.6-10.7 us, r05x -- its spread is worse)
 #ifndef DMC_PICK_ONESCAN
-#define DMC_PICK_ONESCAN 1
+#define DMC_PICK_ONESCAN 0
 #endif
 __device__ inline uint32_t half_excl_scan(uint32_t v, uint32_t* wsum, bool trail = true) {
   const int t = threadIdx.x & (kPickHalf - 1), lane = t & 63, w = t >> 6;
