@@ -251,7 +251,7 @@ k_add_chain(Table tb, const AddParams* pblk,
 // client accesses and the scan's stream overlap instead of running one
 // after the other.  Partials: the scan's nscan blocks', then the chain's.
 #ifndef DMC_CHAIN_SCAN_SLOTS
-#define DMC_CHAIN_SCAN_SLOTS 4
+#define DMC_CHAIN_SCAN_SLOTS 3
 #endif
 constexpr int kScanChainSlots = DMC_CHAIN_SCAN_SLOTS;
 
