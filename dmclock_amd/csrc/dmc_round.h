@@ -2005,7 +2005,10 @@ constexpr auto k_remit_brk = k_remit_t<true>;
 // entry (slot * q + position) gets its decision offset and tie flag stamped
 // into the ring entry (the priority pop's entry for a P group).
 
-constexpr int kDeepBatch = 8;   // queued requests reduced per batch of loads
+#ifndef DMC_DEEP_BATCH
+#define DMC_DEEP_BATCH 8
+#endif
+constexpr int kDeepBatch = DMC_DEEP_BATCH;   // queued requests reduced per batch of loads
 
 // Rank of record i of a bin among all `cnt` of them, compared in `parts`
 // slices of `per` records by adjacent lanes whose counts are summed by
