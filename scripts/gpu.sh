@@ -21,6 +21,8 @@
 #     probe            tools/rand_probe: random-record read rates (64/128-byte shapes)
 #     eclk             k_remit's per-block phase clocks and per-candidate walk times
 #                      over a short bench run (DMC_DEBUG rounds, stderr)
+#     aclk             k_rapply's slow candidates' clocks over a short bench run
+#                      (DMC_DEBUG_BINS dump, tools/apply_clocks.py)
 #     variants         $VARIANTS alternated $ROUNDS times (scripts/gpu_variants.sh)
 #   $BENCH_ARGS is appended to every bench.py command.
 set -o pipefail
@@ -88,6 +90,11 @@ for step in "$@"; do
     eclk) DMC_DEBUG=1 DMC_EMIT_CLOCKS=1 run eclk 300 python bench.py --steps 3 --warmup 1 \
               --no-cpu-baseline --no-profile ${BENCH_ARGS} || exit 1
           grep -c 'emit clock' ${O}_eclk.log ;;
+    aclk) rm -f /tmp/aclk_$T.bin
+          DMC_DEBUG=1 DMC_DEBUG_BINS=/tmp/aclk_$T.bin run aclk_bench 300 python bench.py --steps 3 \
+              --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS} || exit 1
+          run aclk 60 python tools/apply_clocks.py /tmp/aclk_$T.bin 4 || exit 1
+          cat ${O}_aclk.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
