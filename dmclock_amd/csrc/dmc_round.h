@@ -2673,6 +2673,9 @@ struct RoundC {
 #define DMC_APPLY_STAGE 4
 #endif
 constexpr int kApplyStage = DMC_APPLY_STAGE;
+#ifndef DMC_APPLY_PREFETCH
+#define DMC_APPLY_PREFETCH 28  // queue positions past the staged ones requested up front
+#endif
 // A popped slot's new ScanRec: its front keys and cursor bytes (head, count,
 // flags), never its stamp and batch count (bytes 27-31): the next call's
 // filing (k_add_link's atomic on the count, its stamp) may run beside this
@@ -2706,6 +2709,18 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   const bool p_runs = rc.p_runs;
   const uint32_t c = cv.c, h = cv.h;
   const RingView rv = stage_ring<kApplyStage>(tb, s, h, c, st);
+  // the queue past the staged positions, requested at once (one dword of
+  // each entry's line; the words folded into pfx, consumed at the end): the
+  // walks' reads of those entries, each dependent on the last, then hit the
+  // caches instead of queueing for HBM one at a time (config 4's activated
+  // clients replay tens of pops: a walk of 13-21 us set the kernel's length)
+  uint32_t pfx = 0;
+  if (DMC_APPLY_PREFETCH && c > (uint32_t)kApplyStage) {
+    const ReqEntry* g = tb.ring + (size_t)s * tb.q;
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)DMC_APPLY_PREFETCH; ++i)
+      if (kApplyStage + i < c) pfx ^= ld_as<uint32_t>(&g[(h + kApplyStage + i) & tb.qmask].cost);
+  }
   if (rc.dbg) rc.dbg[1] = wall_clock64();
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s};
@@ -2732,6 +2747,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
       tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
+    asm volatile("" ::"v"(pfx));
     return;
   }
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
@@ -2803,6 +2819,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   }
   o.flags = f;
   sc_store_front(tb, s, o);
+  asm volatile("" ::"v"(pfx));  // (the prefetches: issued, never left pending)
 }
 
 // Candidates (the dense list) with dispatched pops replay their walks for
