@@ -2129,6 +2129,7 @@ struct dmc_queue {
   bool pipeline = false;
   uint32_t* gate = nullptr;
   uint32_t epoch = 0;  // k_chain_scan's batches (AddParams::epoch)
+  uint32_t fused_ndec = 0;  // the pre-launched round's decisions (a group's tallied ones)
   struct PendCall {
     bool on = false;
     uint64_t seq = 0;  // its round's sequence number
@@ -3678,6 +3679,9 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     // one host round trip per round, through host-mapped memory
     rc = wait_round(q, wseq ? wseq : q->round_seq);
     if (rc) return rc;
+    // (a queue group's fused round tallied its own decisions, k_tally_m
+    // skips them; a round that failed wrote none)
+    if (wseq) q->fused_ndec = q->h_rd->overflow ? 0u : q->h_rd->n_dec;
     if (!allow && q->h_rd->terminal && !q->h_rd->overflow) {
       // the round ran out of work: the terminal pull (do_next_request's
       // future / none, :1170-1185) ends it
@@ -5186,10 +5190,13 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                                     (unsigned long long*)q->bcount, q->bsup};
         ea[i] = REmitArgs{tb, q->rd, q->k32, q->meta, q->cand, q->bcand, q->post, q->decof,
                           q->brec, q->bcount, q->bsup, q->hist, q->dense, q->ecap};
+        // (the trackers' tallies made where the decisions are written)
+        const TallyP tp = (trk && d_result) ? TallyP{trk[i].comp_delta, trk[i].comp_rho}
+                                             : TallyP{};
         ra[i] = RRankArgs{q->rd, (const unsigned long long*)q->bcount, q->bsup, q->brec, tb.ring,
-                          q->decof};
+                          q->decof, tp};
         pa[i] = RApplyArgs{tb, q->rd, q->cand, q->bcand, q->decof, q->post, q->sched,
-                           q->d_hround};
+                           q->d_hround, tp};
       }
       const uint32_t gHist = all_sampled ? kHistBlocksSampled : kHistBlocksR;
       uint8_t* d = g->d_blob;
@@ -5263,22 +5270,30 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       }
       // each member's round: its outcome, and any follow-up (a re-run, the
       // terminal pull) on the group stream
+      // (the decisions later rounds wrote -- re-runs, further rounds -- are
+      // tallied by k_tally_m after them; none in a step whose rounds all
+      // ended their calls)
+      bool more = false;
+      TallyArgs* la = reinterpret_cast<TallyArgs*>(g->h_blob + g->o_tally);
       for (uint32_t i = 0; i < S; ++i) {
         dmc_queue* q = g->qs[i];
         dmc_pull_result r{};
         bool dev_wrote = false;
         dmc_pull_result* dres = d_result ? d_result[i] : nullptr;
+        q->fused_ndec = 0;
         int rc = pull_impl(q, now[i], k, d_out[i], &r, dres, &dev_wrote, true);
         if (rc) return rc;
         if (dres && !dev_wrote) {
           hipLaunchKernelGGL(k_put_result, dim3(1), dim3(1), 0, q->stream, dres, r);
           HIP_OK(hipGetLastError());
         }
+        if (trk && d_result) {
+          la[i] = TallyArgs{d_out[i], d_result[i], k, trk[i].comp_delta, trk[i].comp_rho,
+                            q->fused_ndec};
+          more = more || r.n_decisions > q->fused_ndec;
+        }
       }
-      if (trk && d_result) {
-        TallyArgs* la = reinterpret_cast<TallyArgs*>(g->h_blob + g->o_tally);
-        for (uint32_t i = 0; i < S; ++i)
-          la[i] = TallyArgs{d_out[i], d_result[i], k, trk[i].comp_delta, trk[i].comp_rho};
+      if (trk && d_result && more) {
         HIP_OK(hipMemcpyAsync(g->d_blob + g->o_tally, la, g->tally_bytes, hipMemcpyHostToDevice,
                               g->stream));
         hipLaunchKernelGGL(k_tally_m, dim3(grid_for(k, 1024), S), dim3(kBlock), 0, g->stream,

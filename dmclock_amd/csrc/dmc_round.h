@@ -2020,11 +2020,25 @@ constexpr int kDeepBatch = DMC_DEEP_BATCH;   // queued requests reduced per batc
 // measured slower: rank 9.8 -> 21.2 us for apply 11.5 -> 6.3, §10.)
 // A ranked record's stores: its decision offset goff (the group sizes of
 // the bin's records before it plus the bin's offset), stamped or written.
+// A queue group's per-slot completion tallies (the trackers' track_resp,
+// dmc_tracker.h), made where a decision is written -- k_rrank_m's fast
+// records, k_rapply_m's pops -- instead of by a pass over the decisions
+// after the round (k_tally_m then counts only what later, host-driven rounds
+// wrote).  A round that fails writes no decision and tallies nothing.
+struct TallyP {
+  uint32_t* d = nullptr;
+  uint32_t* r = nullptr;
+};
+__device__ inline void tally_one(const TallyP& t, uint32_t slot, uint32_t cost, bool resv) {
+  if (!t.d) return;
+  atomicAdd(&t.d[slot], cost);
+  if (resv) atomicAdd(&t.r[slot], cost);
+}
 __device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_t cost,
                                  uint64_t handle, double tr, double tp, double tl,
                                  uint32_t rank, uint32_t gl, uint32_t tie, bool isp, uint32_t k,
                                  uint32_t n_pgroups, uint32_t soff, uint32_t poff,
-                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
+                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof, const TallyP& tly) {
   uint32_t goff = soff + gl;
   uint32_t size = isp ? 1u + me.run : 1u;
   if (goff < k) {
@@ -2047,6 +2061,7 @@ __device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_
       d.flags = tie;
       out[goff] = d;
       decof[ci & ~kFastRec] = goff;
+      tally_one(tly, me.slot, cost, !isp);
     } else {
       ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
       ring[me.ridx].tie = tie;
@@ -2097,7 +2112,7 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
                                 uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
-                                ReqEntry* ring, dmc_decision* out, uint32_t* decof) {
+                                ReqEntry* ring, dmc_decision* out, uint32_t* decof, const TallyP& tly) {
   const bool valid = i < cnt;
   const BKeyS me = sh[valid ? i : 0];
   const uint32_t me_slot = me.slot();
@@ -2137,7 +2152,7 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
   if (!ISP) gl = rank;
   if (valid && part == 0)
     place_rec(rd, BKey{me.okey, me_slot, me.seq(), me.run(), ridx}, ci, cost, handle, tr, tp, tl,
-              rank, gl, tie, ISP, k, n_pgroups, soff, poff, ring, out, decof);
+              rank, gl, tie, ISP, k, n_pgroups, soff, poff, ring, out, decof, tly);
 }
 
 // One block per rank bin.  The bin's order keys are staged in LDS; each
@@ -2255,7 +2270,7 @@ __device__ inline void sort_bin_regs(const BKeyS* sh, uint32_t cnt, uint16_t* or
 __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
                                    bool isp, uint32_t k, uint32_t n_pgroups, uint32_t soff,
                                    uint32_t poff, ReqEntry* ring, dmc_decision* out,
-                                   uint32_t* decof) {
+                                   uint32_t* decof, const TallyP& tly) {
   constexpr uint32_t RP = kBinCapR / kRankThreads;  // sorted positions per thread
   static_assert(kBinCapR % kRankThreads == 0 && RP <= 8, "whole positions per thread");
   __shared__ uint16_t ord[kBinCapR];
@@ -2352,7 +2367,7 @@ __device__ inline void rank_sorted(Round* rd, const BKeyS* sh, const BRecR* src,
     const uint32_t tie = runtie[runid[h]];
     const BRecR& x = src[i];
     place_rec(rd, x.k, x.ci, x.cost, x.handle, x.r, x.p, x.l, r, exh, tie, isp, k,
-              n_pgroups, soff, poff, ring, out, decof);
+              n_pgroups, soff, poff, ring, out, decof, tly);
   }
 }
 
@@ -2378,7 +2393,7 @@ __device__ inline bool sample_failed(const Round* rd) {
 // this size only (a handful per round; an overflowing bin always)
 constexpr uint32_t kBinMaxReport = 128;
 
-__device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime) {
+__device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, const unsigned long long* bcount, const unsigned long long* gsup, const BRecR* brec, ReqEntry* ring, uint32_t* decof, uint64_t* wtime, TallyP tly = TallyP{}) {
   // the rank-bin counters requested with the skip word (one level of loads)
   unsigned long long sv = 0, bv = 0;
   if (threadIdx.x < 64) {
@@ -2472,7 +2487,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
   for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) sh[i] = bkey_s(src[i].k);
   if (cnt > kRankSortMin) {
-    rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof);
+    rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof, tly);
     if (wtime && threadIdx.x == 0) {
       wtime[2 * b] = t0;
       wtime[2 * b + 1] = wall_clock64();
@@ -2490,10 +2505,10 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     const uint32_t per = (cnt + parts - 1) / parts;
     if (isp)
       rank_rec<true>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
-                     soff, poff, ring, out, decof);
+                     soff, poff, ring, out, decof, tly);
     else
       rank_rec<false>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
-                      soff, poff, ring, out, decof);
+                      soff, poff, ring, out, decof, tly);
     rb += kRankThreads / parts;
   }
   if (wtime && threadIdx.x == 0) {
@@ -2580,6 +2595,7 @@ __global__ void k_ddecide(Round* rd, uint32_t dcap, const uint32_t* sval,
 struct ApplyV {
   dmc_decision* out;
   uint32_t slot;
+  TallyP tp;
   uint32_t inrun = 0, gidx = 0;
   uint32_t last_idx = 0;
   uint32_t nprio = 0;  // priority pops (limit-break rounds count them here)
@@ -2610,6 +2626,7 @@ struct ApplyV {
     d.cost = cost;
     d.phase = prio ? DMC_PHASE_PRIORITY : DMC_PHASE_RESERVATION;
     d.flags = tie;
+    tally_one(tp, slot, cost, !prio);
     // the first decision is held back and stored with the client's state at
     // the end (flush): no store sits ahead of the walk's and the reductions'
     // loads (a load wait also waits for the wave's earlier stores)
@@ -2667,6 +2684,7 @@ struct RoundC {
   uint32_t k;
   bool p_runs, ovf, brk;
   uint32_t* brk_prio;  // limit-break rounds: the priority pops' count
+  TallyP tp;           // a queue group's tallies (null: none)
 };
 
 #ifndef DMC_APPLY_STAGE
@@ -2723,7 +2741,7 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   }
   if (rc.dbg) rc.dbg[1] = wall_clock64();
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
-  ApplyV v{rc.out, s};
+  ApplyV v{rc.out, s, rc.tp};
   Tag3 front{};
   uint32_t fcost = 0;
   uint32_t popsR = 0, popsP = 0;
@@ -2934,6 +2952,7 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
     x.phase = DMC_PHASE_RESERVATION;
     x.flags = 0;
     rc.out[d + 1] = x;
+    tally_one(rc.tp, s, x.cost, true);
   }
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
   ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
@@ -2976,7 +2995,7 @@ constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 #endif
 // (bid / nblk: the block's index among the apply blocks and their count --
 // k_rapply's own grid, or the first nblk blocks of k_apply_link)
-__device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg, uint32_t bid, uint32_t nblk) {
+__device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg, uint32_t bid, uint32_t nblk, TallyP tp = TallyP{}) {
   if (rd->skip) return;
   // A limit-break round's priority pops (group heads and their runs'
   // readied fronts) are counted here: its summary goes out once every block
@@ -2999,7 +3018,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
     const uint32_t nc = bcand[eb];
     const uint32_t base = eb * kEmitChunk;
     RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
-              rd->p_runs != 0, rd->overflow != 0, brk, &rd->brk_prio};
+              rd->p_runs != 0, rd->overflow != 0, brk, &rd->brk_prio, tp};
     __shared__ ReqEntry stage[kBlockR * kApplyStage];
     // (interleaved: the emit block's candidates, about 280, split evenly over
     // its apply blocks rather than filling the first one)
@@ -3114,6 +3133,7 @@ struct RRankArgs {
   const BRecR* brec;
   ReqEntry* ring;
   uint32_t* decof;
+  TallyP tp;  // the member's tallies (trackers), or none
 };
 struct RApplyArgs {
   Table tb;
@@ -3123,6 +3143,7 @@ struct RApplyArgs {
   const PostRec* post;
   unsigned long long* sched;
   HostRound* h;
+  TallyP tp;  // the member's tallies (trackers), or none
 };
 
 __global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_m(const RScanArgs* a) {
@@ -3311,12 +3332,12 @@ __global__ void __launch_bounds__(kWalkThreads) k_rwalk_m(const REmitArgs* a) {
 
 __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
   const RRankArgs& x = a[blockIdx.y];
-  rrank_body(x.rd, x.bcount, x.gsup, x.brec, x.ring, x.decof, nullptr);
+  rrank_body(x.rd, x.bcount, x.gsup, x.brec, x.ring, x.decof, nullptr, x.tp);
 }
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB) k_rapply_m(const RApplyArgs* a) {
   const RApplyArgs& x = a[blockIdx.y];
   rapply_body(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr, blockIdx.x,
-              gridDim.x);
+              gridDim.x, x.tp);
 }
 
 // device-API result written by the host's view of a multi-round call

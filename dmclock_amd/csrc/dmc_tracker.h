@@ -32,10 +32,13 @@
 namespace dmc {
 
 // per-slot completion tallies of one server's decisions (track_resp's cost)
+// (skip: the decisions a queue group's round already tallied where it wrote
+// them, k_rrank_m / k_rapply_m)
 __device__ inline void tally_body(const dmc_decision* dec, const dmc_pull_result* res,
-                                  uint32_t cap, uint32_t* comp_d, uint32_t* comp_r) {
+                                  uint32_t cap, uint32_t* comp_d, uint32_t* comp_r,
+                                  uint32_t skip = 0) {
   uint32_t n = res->n_decisions < cap ? res->n_decisions : cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+  for (uint32_t i = skip + blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += gridDim.x * blockDim.x) {
     const dmc_decision& d = dec[i];
     atomicAdd(&comp_d[d.slot], d.cost);
@@ -187,10 +190,11 @@ struct TallyArgs {
   const dmc_pull_result* res;
   uint32_t cap;
   uint32_t *comp_d, *comp_r;
+  uint32_t skip;  // decisions tallied by the round's own kernels
 };
 __global__ void k_tally_m(const TallyArgs* a) {
   const TallyArgs& x = a[blockIdx.y];
-  if (x.dec) tally_body(x.dec, x.res, x.cap, x.comp_d, x.comp_r);
+  if (x.dec) tally_body(x.dec, x.res, x.cap, x.comp_d, x.comp_r, x.skip);
 }
 
 }  // namespace dmc
