@@ -3665,6 +3665,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     dmc_pull_result* dres = (first_round && n_dec == 0 && kr == k) ? d_result : nullptr;
     int rc = DMC_OK;
     uint64_t wseq = 0;
+    const bool was_pre = pre_launched;
     if (pre_launched) {  // the fused add + pull graph launched this round
       pre_launched = false;
       radix = false;
@@ -3681,7 +3682,7 @@ int pull_impl(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (rc) return rc;
     // (a queue group's fused round tallied its own decisions, k_tally_m
     // skips them; a round that failed wrote none)
-    if (wseq) q->fused_ndec = q->h_rd->overflow ? 0u : q->h_rd->n_dec;
+    if (was_pre) q->fused_ndec = q->h_rd->overflow ? 0u : q->h_rd->n_dec;
     if (!allow && q->h_rd->terminal && !q->h_rd->overflow) {
       // the round ran out of work: the terminal pull (do_next_request's
       // future / none, :1170-1185) ends it
