@@ -1415,7 +1415,8 @@ struct PostRec {
   uint32_t bits;       // 1: priority pop, 2: the new front's l <= now, 4: run of one
   uint32_t cand;       // the candidate's CandRec word: flags (low nibble) | R-prefix
                        // length << 8 | ring head << 16 | queued count << 24
-  uint32_t pad[2];
+  uint32_t cost0;      // the first pop's cost (a queue group's tally, k_rapply_m)
+  uint32_t pad;
   // the run's pop (queue position 1), bits & 4
   uint64_t handle1;
   double r1, p1, l1;
@@ -1426,6 +1427,7 @@ static_assert(sizeof(PostRec) == 128, "PostRec must be two 64-byte lines");
 // (k_remit stores it in 16-byte pieces in this order)
 static_assert(offsetof(PostRec, prev_r) == 24 && offsetof(PostRec, r2) == 40 &&
                   offsetof(PostRec, bits) == 48 && offsetof(PostRec, cand) == 52 &&
+                  offsetof(PostRec, cost0) == 56 &&
                   offsetof(PostRec, handle1) == 64 && offsetof(PostRec, p1) == 80 &&
                   offsetof(PostRec, cost1) == 96,
               "PostRec layout");
@@ -1681,10 +1683,12 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
     const uint32_t cc = cv.c;
     const bool prio = acc.prio0;
     double off = 0.0;
+    uint32_t cost0 = 0;
     {
       // the pop's payload: queue position 0 as stored (immediate mode: a
       // priority pop with no earlier one has its stored r)
       const ReqEntry e0 = rv.at(0);
+      cost0 = e0.cost;
       if (prio) off = resv_offset(cv.rinv, e0.cost, e0.rho);
       brec[(size_t)acc.b0 * kBinCapR + acc.at0] =
           BRecR{BKey{acc.key0, s, 0u, run, s * tb.q + h}, ci | kFastRec, e0.cost, e0.handle,
@@ -1709,7 +1713,8 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
       st_as(dst, make_ulonglong2(dbits(fr), dbits(fpk)));
       st_as(dst + 16, make_ulonglong2(dbits(fl), dbits(pr_prev)));
       st_as(dst + 32, make_ulonglong2(dbits(off), dbits(r2)));
-      st_as(dst + 48, make_ulonglong2((unsigned long long)bits | ((unsigned long long)cw << 32), 0ull));
+      st_as(dst + 48, make_ulonglong2((unsigned long long)bits | ((unsigned long long)cw << 32),
+                                      (unsigned long long)cost0));
     }
     if (run) {
       // line 2, the run's pop: queue position 1 with its reduced r (its
@@ -2061,7 +2066,7 @@ __device__ inline void place_rec(Round* rd, const BKey& me, uint32_t ci, uint32_
       d.flags = tie;
       out[goff] = d;
       decof[ci & ~kFastRec] = goff;
-      tally_one(tly, me.slot, cost, !isp);
+      (void)tly;  // (its tally: k_rapply, with the run's, PostRec::cost0)
     } else {
       ring[me.ridx].dec = goff;  // the stamp k_rapply's walk follows
       ring[me.ridx].tie = tie;
@@ -2902,10 +2907,10 @@ __device__ inline void rfinish_body(const Round* rd, HostRound* h, bool round_en
 #endif
 struct PostL1 {
   double fr, fpk, fl, prev_r, off, r2;
-  uint32_t bits, cand;
+  uint32_t bits, cand, cost0;
 };
 __device__ inline PostL1 post_l1(const PostRec& p) {
-  return PostL1{p.fr, p.fpk, p.fl, p.prev_r, p.off, p.r2, p.bits, p.cand};
+  return PostL1{p.fr, p.fpk, p.fl, p.prev_r, p.off, p.r2, p.bits, p.cand, p.cost0};
 }
 __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandRec& cd,
                                   uint32_t d, const PostL1& pr, const PostRec* pp,
@@ -2940,6 +2945,7 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
     if (!run && c >= 3) ring[(h + 2) & tb.qmask].r = pr.r2;
     tb.rec[s].prev_r = pr.prev_r;
   }
+  uint32_t run_cost = 0;
   if (run) {
     const PostRec& p2 = both ? *both : *pp;  // (the second line)
     dmc_decision x;
@@ -2952,7 +2958,14 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
     x.phase = DMC_PHASE_RESERVATION;
     x.flags = 0;
     rc.out[d + 1] = x;
-    tally_one(rc.tp, s, x.cost, true);
+    run_cost = x.cost;
+  }
+  // (a queue group's tallies: the group's first pop -- priority or
+  // reservation -- and the run's reservation pop, one update per counter)
+  if (rc.tp.d) {
+    atomicAdd(&rc.tp.d[s], pr.cost0 + run_cost);
+    const uint32_t rr = (prio ? 0u : pr.cost0) + run_cost;
+    if (rr) atomicAdd(&rc.tp.r[s], rr);
   }
   uint8_t f = f0 & (uint8_t)~(F_READY | F_PMARK);
   ScanRec o{0.0, 0.0, 0.0, (uint8_t)nh, (uint8_t)nc2, 0, 0, 0};
@@ -3034,7 +3047,7 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
       if (DMC_POST_LINE1) {
         const PostRec* pp = post + ci;
         const PostL1 pr{pp->fr, pp->fpk, pp->fl, pp->prev_r, pp->off, pp->r2, pp->bits,
-                        pp->cand};
+                        pp->cand, pp->cost0};
         if (d != kSlowCand && !rc.ovf) {
           apply_fast(tb, rc, c, d, pr, pp, nullptr);
           continue;
