@@ -2695,10 +2695,7 @@ struct RoundC {
 #ifndef DMC_APPLY_STAGE
 #define DMC_APPLY_STAGE 4
 #endif
-constexpr int kApplyStage = DMC_APPLY_STAGE;
-#ifndef DMC_APPLY_PREFETCH
-#define DMC_APPLY_PREFETCH 28  // queue positions past the staged ones requested up front
-#endif
+constexpr int kApplyStage = DMC_APPLY_STAGE;  // queue positions staged per candidate (LDS)
 // A popped slot's new ScanRec: its front keys and cursor bytes (head, count,
 // flags), never its stamp and batch count (bytes 27-31): the next call's
 // filing (k_add_link's atomic on the count, its stamp) may run beside this
@@ -2710,7 +2707,7 @@ __device__ inline void sc_store_front(const Table& tb, uint32_t s, const ScanRec
   st_as(d + 16, dbits(o.l));
   st_as(d + 24, (uint16_t)(o.head | ((uint32_t)o.count << 8)));
   st_as(d + 26, o.flags);
-}  // queue positions staged per candidate (LDS)
+}
 __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRec& cd,
                                  ReqEntry* st) {
   // every load that depends only on the candidate record is issued before
@@ -2732,18 +2729,6 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   const bool p_runs = rc.p_runs;
   const uint32_t c = cv.c, h = cv.h;
   const RingView rv = stage_ring<kApplyStage>(tb, s, h, c, st);
-  // the queue past the staged positions, requested at once (one dword of
-  // each entry's line; the words folded into pfx, consumed at the end): the
-  // walks' reads of those entries, each dependent on the last, then hit the
-  // caches instead of queueing for HBM one at a time (config 4's activated
-  // clients replay tens of pops: a walk of 13-21 us set the kernel's length)
-  uint32_t pfx = 0;
-  if (DMC_APPLY_PREFETCH && c > (uint32_t)kApplyStage) {
-    const ReqEntry* g = tb.ring + (size_t)s * tb.q;
-#pragma unroll
-    for (uint32_t i = 0; i < (uint32_t)DMC_APPLY_PREFETCH; ++i)
-      if (kApplyStage + i < c) pfx ^= ld_as<uint32_t>(&g[(h + kApplyStage + i) & tb.qmask].cost);
-  }
   if (rc.dbg) rc.dbg[1] = wall_clock64();
   ReqEntry* ring = tb.ring + (size_t)s * tb.q;
   ApplyV v{rc.out, s, rc.tp};
@@ -2770,7 +2755,6 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   if (pops == 0) {  // a candidate none of whose entries was dispatched
     if (f0 & F_PMARK)
       tb.sc[s].flags = (uint8_t)((f0 & ~F_PMARK) | (p_runs ? F_READY : 0));
-    asm volatile("" ::"v"(pfx));
     return;
   }
   uint32_t nc2 = c - pops, nh = (h + pops) & tb.qmask;
@@ -2842,7 +2826,6 @@ __device__ inline void apply_one(const Table& tb, const RoundC& rc, const CandRe
   }
   o.flags = f;
   sc_store_front(tb, s, o);
-  asm volatile("" ::"v"(pfx));  // (the prefetches: issued, never left pending)
 }
 
 // Candidates (the dense list) with dispatched pops replay their walks for
