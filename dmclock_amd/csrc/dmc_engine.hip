@@ -4100,7 +4100,10 @@ int dmc_queue_create(const dmc_queue_params* params, dmc_queue** out) {
   t.binfo = p.dynamic_info ? q->binfo : nullptr;
   rc |= A(&t.ring, (size_t)N * p.ring_capacity);
   {
-    const size_t nb = (N + kEmitChunk - 1) / kEmitChunk, nc = nb * kEmitChunk;
+    // (blocks of kEmitChunk slots, or a queue group's kEmitChunkM: room for either)
+    const size_t nb = (N + kEmitChunk - 1) / kEmitChunk;
+    const size_t nbm = (N + kEmitChunkM - 1) / kEmitChunkM;
+    const size_t nc = std::max(nb * kEmitChunk, nbm * kEmitChunkM);
     rc |= A(&q->cand, nc);
     rc |= A(&q->bcand, nb);
     rc |= A(&q->post, nc);
@@ -5165,7 +5168,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         const Table& tb = q->tb;
         const uint32_t N = tb.n;
         gN = (N + kScanBlock * kScanSlots - 1) / (kScanBlock * kScanSlots);
-        gEm = (N + kEmitChunk - 1) / kEmitChunk;
+        gEm = (N + kEmitChunkM - 1) / kEmitChunkM;
         const bool sampled = use_sample(q, false);
         all_sampled = all_sampled && sampled;
         ta[i] = trk ? TrackArgs{d_reqs[i], n, q->p.max_clients, trk[i].client_of_slot,
@@ -5226,7 +5229,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         }
         hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads), 0, st,
                            (const RRankArgs*)(d + g->o_rank));
-        hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmit * gEm + 1, S), dim3(kBlockR), 0,
+        hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmitM * gEm + 1, S), dim3(kBlockR), 0,
                            st, (const RApplyArgs*)(d + g->o_apply));
       };
       // the step's graph: captured at the second sighting of its shape, then

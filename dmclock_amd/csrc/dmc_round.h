@@ -1755,8 +1755,27 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
 // walk (rank_bin_q).  Bin-rank path: the last block to finish
 // computes the rank-bin prefixes (k_rrank's offsets); radix path: entries go
 // to the dense list.
-constexpr int kEmitPer = 4;  // slots per thread (8 with 512-thread blocks: no faster)
+#ifndef DMC_EMIT_PER
+#define DMC_EMIT_PER 4
+#endif
+constexpr int kEmitPer = DMC_EMIT_PER;  // slots per thread (8 with 512-thread blocks: no faster)
+static_assert(kEmitPer % 4 == 0 && kEmitPer <= 16, "kEmitPer: 4, 8 or 16 (the slot predicates: 2 bits each in a word)");
 constexpr uint32_t kEmitChunk = kEmitThreads * kEmitPer;
+// Queue groups (k_remit_m, with its k_rapply_m): 8 slots per thread, 8,192
+// per block, and 128 staging walkers (LDS): a group's 8 x 2M-slot tables
+// run 16 generations of one block per CU at 4 slots; at 8 each block's fixed
+// costs are paid half as often (config 5 0.787-0.801 against 0.890-0.895
+// ms/step).  A single table keeps 4: its 256 blocks fill the chip once.
+#ifndef DMC_EMIT_PER_M
+#define DMC_EMIT_PER_M 8
+#endif
+#ifndef DMC_EMIT_STAGE_THREADS_M
+#define DMC_EMIT_STAGE_THREADS_M 128
+#endif
+constexpr int kEmitPerM = DMC_EMIT_PER_M;
+static_assert(kEmitPerM % 4 == 0 && kEmitPerM <= 16, "kEmitPerM: 4, 8 or 16");
+constexpr uint32_t kEmitChunkM = kEmitThreads * kEmitPerM;
+constexpr int kEmitStageThreadsM = DMC_EMIT_STAGE_THREADS_M;
 // walkers with a staging slice per wave: its first lanes (a wave with more
 // candidates walks the rest from global memory)
 constexpr int kEmitStageLanes0 = kEmitStageThreads / (kEmitThreads / 64);
@@ -1768,19 +1787,24 @@ constexpr int kEmitStageLanes = kEmitStageLanes0 < 64 ? kEmitStageLanes0 : 64;
 #ifndef DMC_EMIT_MINW
 #define DMC_EMIT_MINW 4
 #endif
-template <bool BRK, bool PRE = false>
+template <bool BRK, bool PRE, int PER, int STH>
 __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Round* rd, const uint2* k32, const uint32_t* meta, CandRec* cand, uint32_t* bcand, PostRec* post, uint32_t* decof, BRecR* brec, uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense, uint32_t dcap, uint64_t* eclk) {
+  // (PER slots per thread, CH per block; STH walkers with a staging slice,
+  // SL lanes of each wave)
+  constexpr uint32_t CH = kEmitThreads * PER;
+  constexpr int SL = STH / (kEmitThreads / 64) < 64 ? STH / (kEmitThreads / 64) : 64;
   if (!DMC_EARLY_LOADS && rd->skip) return;
   // eclk (debug): per block [0] start [1] keys + thresholds picked [2]
   // candidates compacted [3] walks done [4] block done
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x] = wall_clock64();
-  __shared__ CandRec bl[kEmitChunk];
-  __shared__ uint32_t bk[kEmitChunk];  // their first phase's quantized first key
+  __shared__ CandRec bl[CH];
+  __shared__ uint32_t bk[CH];  // their first phase's quantized first key
   // each thread's slot predicates and flags, parked for the mark settling
   // after the walks (fewer registers live across them: no spills)
-  __shared__ uint2 s_fb[kEmitThreads];
+  __shared__ uint32_t s_fbits[kEmitThreads];
+  __shared__ uint32_t s_fw[PER / 4][kEmitThreads];  // (flags, 4 slots a word)
   __shared__ uint32_t ltab[2 * kHistBinsR];
-  __shared__ ReqEntry stage[kEmitStageThreads * kEmitStage];
+  __shared__ ReqEntry stage[STH * kEmitStage];
   __shared__ uint32_t s_tot;
   __shared__ uint32_t s_cnt[2], s_ec[4];
   __shared__ PhaseSel s_ph[2];
@@ -1793,7 +1817,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   if (threadIdx.x == 0) atomicMin(&rd->tdbg[3], (unsigned long long)wall_clock64());
 #endif
   const uint32_t n = tb.n;
-  const uint32_t s0 = blockIdx.x * kEmitChunk + threadIdx.x * kEmitPer;
+  const uint32_t s0 = blockIdx.x * CH + threadIdx.x * PER;
   // the pick's histogram bins first: its compute then waits for them only,
   // while the slots' keys below are still in flight
   // (PRE: the tables k_rpick_m picked, this thread's share)
@@ -1828,22 +1852,22 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   if (DMC_EARLY_LOADS && rd->skip) return;
   const bool p_runs = rd->p_runs != 0;
   const int lane = threadIdx.x & 63;
-  uint32_t kr[kEmitPer], kp[kEmitPer];  // 32-bit quantized first keys (key32)
-  uint32_t mt[kEmitPer];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
-  if (s0 + kEmitPer <= n) {
+  uint32_t kr[PER], kp[PER];  // 32-bit quantized first keys (key32)
+  uint32_t mt[PER];  // k_rscan's meta: R-prefix length | flags << 8 | head << 16 | count << 24
+  if (s0 + PER <= n) {
 #pragma unroll
-    for (int j = 0; j < kEmitPer / 2; ++j) {
+    for (int j = 0; j < PER / 2; ++j) {
       const uint4 a = ld_as<uint4>(k32 + s0 + 2 * j);
       kr[2 * j] = a.x; kp[2 * j] = a.y; kr[2 * j + 1] = a.z; kp[2 * j + 1] = a.w;
     }
 #pragma unroll
-    for (int j = 0; j < kEmitPer / 4; ++j) {
+    for (int j = 0; j < PER / 4; ++j) {
       const uint4 m = ld_as<uint4>(meta + s0 + 4 * j);
       mt[4 * j] = m.x; mt[4 * j + 1] = m.y; mt[4 * j + 2] = m.z; mt[4 * j + 3] = m.w;
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
       bool in = s0 + j < n;
       const uint2 k = in ? k32[s0 + j] : make_uint2(0xffffffffu, 0xffffffffu);
       kr[j] = k.x;
@@ -1870,12 +1894,12 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   }
   const CandPred pred(s_ph, p_runs);
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 1] = wall_clock64();
-  uint8_t f[kEmitPer];
+  uint8_t f[PER];
 #pragma unroll
-  for (int j = 0; j < kEmitPer; ++j) f[j] = (uint8_t)(mt[j] >> 8);
+  for (int j = 0; j < PER; ++j) f[j] = (uint8_t)(mt[j] >> 8);
   uint32_t bits = 0;  // per slot: bit 2j R predicate, bit 2j+1 P predicate
 #pragma unroll
-  for (int j = 0; j < kEmitPer; ++j) {
+  for (int j = 0; j < PER; ++j) {
     if (s0 + j >= n) continue;
     const bool cr = pred.TR && kr[j] <= pred.TR32;
     const bool cp = pred.TP && kp[j] <= pred.TP32;
@@ -1883,7 +1907,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   }
   uint32_t cnt = 0, nr = 0, np = 0;
 #pragma unroll
-  for (int j = 0; j < kEmitPer; ++j) {
+  for (int j = 0; j < PER; ++j) {
     cnt += ((bits >> (2 * j)) & 3u) ? 1u : 0u;
     nr += (bits >> (2 * j)) & 1u;
     np += (bits >> (2 * j + 1)) & 1u;
@@ -1912,7 +1936,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   {
     uint32_t o = wbase + incl - cnt;
 #pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
       const uint32_t b = (bits >> (2 * j)) & 3u;
       if (b) {
         bk[o] = (b & 1u) ? kr[j] : kp[j];
@@ -1921,11 +1945,13 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
       }
     }
   }
-  {
+  s_fbits[threadIdx.x] = bits;
+#pragma unroll
+  for (int q = 0; q < PER / 4; ++q) {
     uint32_t fw = 0;
 #pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) fw |= (uint32_t)f[j] << (8 * j);
-    s_fb[threadIdx.x] = make_uint2(bits, fw);
+    for (int j = 0; j < 4; ++j) fw |= (uint32_t)f[4 * q + j] << (8 * j);
+    s_fw[q][threadIdx.x] = fw;
   }
   // (the wave's list entries, written by its lanes, are read by other lanes
   // of the same wave: LDS operations of one wave complete in order)
@@ -1933,18 +1959,18 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (eclk && threadIdx.x == 0) eclk[kEClk * blockIdx.x + 2] = wall_clock64();
-  // candidate index: the block's segment of the candidate arrays (kEmitChunk
+  // candidate index: the block's segment of the candidate arrays (CH
   // per block; k_rapply's blocks take their emit block's segment)
-  const uint32_t cbase = blockIdx.x * kEmitChunk;
+  const uint32_t cbase = blockIdx.x * CH;
   // this lane's staging slice (its address computed here, not held -- and
   // spilled -- from the kernel's start)
-  uint32_t sli = (threadIdx.x >> 6) * kEmitStageLanes + lane;
+  uint32_t sli = (threadIdx.x >> 6) * SL + lane;
   asm volatile("" : "+v"(sli));
   for (uint32_t j = lane; j < wtot; j += 64) {
     const uint32_t i = wbase + j;
     const uint32_t cat = emit_one<BRK>(
         tb, rd, s_ph, bl[i], cbase + i, brec, bcount, s_sup, ltab, dense, dcap, post, decof,
-        lane < kEmitStageLanes ? stage + sli * kEmitStage : nullptr,
+        lane < SL ? stage + sli * kEmitStage : nullptr,
         bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
     atomicAdd(&s_ec[cat], 1u);
   }
@@ -1974,12 +2000,15 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   {
     uint32_t ti = threadIdx.x;
     asm volatile("" : "+v"(ti));  // (its LDS address recomputed here, not held)
-    const uint2 fb = s_fb[ti];
-    const uint32_t s0b = blockIdx.x * kEmitChunk + ti * kEmitPer;
+    const uint32_t fbits = s_fbits[ti];
+    uint32_t fws[PER / 4];
 #pragma unroll
-    for (int j = 0; j < kEmitPer; ++j) {
-      const uint32_t fj = (fb.y >> (8 * j)) & 0xffu;
-      if (s0b + j < n && !((fb.x >> (2 * j)) & 3u) && (fj & F_PMARK))
+    for (int q = 0; q < PER / 4; ++q) fws[q] = s_fw[q][ti];
+    const uint32_t s0b = blockIdx.x * CH + ti * PER;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t fj = (fws[j / 4] >> (8 * (j % 4))) & 0xffu;
+      if (s0b + j < n && !((fbits >> (2 * j)) & 3u) && (fj & F_PMARK))
         tb.sc[s0b + j].flags = (uint8_t)((fj & ~F_PMARK) | (p_runs ? F_READY : 0));
     }
   }
@@ -1992,7 +2021,8 @@ k_remit_t(Table tb, Round* rd, const uint2* k32,
         uint32_t* decof, BRecR* brec,
         uint32_t* bcount, unsigned long long* gsup, const uint32_t* hist, DEnt* dense,
         uint32_t dcap, uint64_t* eclk = nullptr) {
-  remit_t_body<BRK>(tb, rd, k32, meta, cand, bcand, post, decof, brec, bcount, gsup, hist,
+  remit_t_body<BRK, false, kEmitPer, kEmitStageThreads>(tb, rd, k32, meta, cand, bcand, post,
+                                                         decof, brec, bcount, gsup, hist,
                     dense, dcap, eclk);
 }
 
@@ -2983,7 +3013,9 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 // priority, :1469,1479).
 // apply blocks per emit block (about 70 candidates per 1024 slots in a
 // config-3 round)
-constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
+constexpr uint32_t apply_per_emit(uint32_t chunk) { return chunk >= 4096 ? chunk / 2048 : 1; }
+constexpr uint32_t kApplyPerEmit = apply_per_emit(kEmitChunk);
+constexpr uint32_t kApplyPerEmitM = apply_per_emit(kEmitChunkM);  // (queue groups)
 #ifndef DMC_APPLY_MINB
 // (apply_one needs ≈164 VGPRs: 2 waves per SIMD, which the grid of two
 // 256-thread blocks per CU needs; a higher bound only warns)
@@ -2991,6 +3023,7 @@ constexpr uint32_t kApplyPerEmit = kEmitChunk >= 4096 ? kEmitChunk / 2048 : 1;
 #endif
 // (bid / nblk: the block's index among the apply blocks and their count --
 // k_rapply's own grid, or the first nblk blocks of k_apply_link)
+template <uint32_t CH = kEmitChunk>
 __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg, uint32_t bid, uint32_t nblk, TallyP tp = TallyP{}) {
   if (rd->skip) return;
   // A limit-break round's priority pops (group heads and their runs'
@@ -3009,17 +3042,17 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
     sched[1] += rd->n_prio;
   }
   if (bid < nblk - 1) {
-    // (kApplyPerEmit apply blocks per emit block)
-    const uint32_t eb = bid / kApplyPerEmit;
+    // (APE apply blocks per emit block of CH slots)
+    constexpr uint32_t APE = apply_per_emit(CH);
+    const uint32_t eb = bid / APE;
     const uint32_t nc = bcand[eb];
-    const uint32_t base = eb * kEmitChunk;
+    const uint32_t base = eb * CH;
     RoundC rc{nullptr, rd->now, rd->tick, rd->out, rd->g_last, rd->terminal, rd->k_total,
               rd->p_runs != 0, rd->overflow != 0, brk, &rd->brk_prio, tp};
     __shared__ ReqEntry stage[kBlockR * kApplyStage];
     // (interleaved: the emit block's candidates, about 280, split evenly over
     // its apply blocks rather than filling the first one)
-    for (uint32_t i = threadIdx.x * kApplyPerEmit + (bid % kApplyPerEmit); i < nc;
-         i += kApplyPerEmit * kBlockR) {
+    for (uint32_t i = threadIdx.x * APE + (bid % APE); i < nc; i += APE * kBlockR) {
       const uint32_t ci = base + i;
       uint64_t t0 = dbg ? wall_clock64() : 0;
       // one level of coalesced loads: the candidate, its decision offset and
@@ -3173,7 +3206,7 @@ __global__ void __launch_bounds__(kEmitThreads) k_rpick_m(const RHistArgs* a) {
 }
 __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const REmitArgs* a) {
   const REmitArgs& x = a[blockIdx.y];
-  remit_t_body<false, kPrePickM>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof,
+  remit_t_body<false, kPrePickM, kEmitPerM, kEmitStageThreadsM>(x.tb, x.rd, x.k32, x.meta, x.cand, x.bcand, x.post, x.decof,
                                  x.brec, x.bcount, x.gsup, x.hist, x.dense, x.dcap, nullptr);
 }
 // Queue groups, split emission (DMC_SPLIT_EMIT_M): k_remit_m's two halves
@@ -3190,6 +3223,8 @@ __global__ void __launch_bounds__(kEmitThreads, DMC_EMIT_MINW) k_remit_m(const R
 #ifndef DMC_SPLIT_EMIT_M
 #define DMC_SPLIT_EMIT_M 0
 #endif
+static_assert(!DMC_SPLIT_EMIT_M || kEmitPerM == kEmitPer,
+              "the split emission's blocks are kEmitChunk wide: build it with DMC_EMIT_PER_M = DMC_EMIT_PER");
 #ifndef DMC_WALK_THREADS
 #define DMC_WALK_THREADS 128
 #endif
@@ -3332,8 +3367,8 @@ __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
 }
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB) k_rapply_m(const RApplyArgs* a) {
   const RApplyArgs& x = a[blockIdx.y];
-  rapply_body(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr, blockIdx.x,
-              gridDim.x, x.tp);
+  rapply_body<kEmitChunkM>(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr,
+                           blockIdx.x, gridDim.x, x.tp);
 }
 
 // device-API result written by the host's view of a multi-round call
