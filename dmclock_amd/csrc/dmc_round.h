@@ -3015,7 +3015,10 @@ __device__ inline void apply_fast(const Table& tb, const RoundC& rc, const CandR
 // config-3 round)
 constexpr uint32_t apply_per_emit(uint32_t chunk) { return chunk >= 4096 ? chunk / 2048 : 1; }
 constexpr uint32_t kApplyPerEmit = apply_per_emit(kEmitChunk);
-constexpr uint32_t kApplyPerEmitM = apply_per_emit(kEmitChunkM);  // (queue groups)
+#ifndef DMC_APPLY_PER_EMIT_M
+#define DMC_APPLY_PER_EMIT_M 1  // (one apply block per 8,192-slot emit block: config 5 0.778-0.785 against 0.809-0.837 ms at 4, 0.779-0.791 at 2)
+#endif
+constexpr uint32_t kApplyPerEmitM = DMC_APPLY_PER_EMIT_M;  // (queue groups)
 #ifndef DMC_APPLY_MINB
 // (apply_one needs ≈164 VGPRs: 2 waves per SIMD, which the grid of two
 // 256-thread blocks per CU needs; a higher bound only warns)
@@ -3023,7 +3026,7 @@ constexpr uint32_t kApplyPerEmitM = apply_per_emit(kEmitChunkM);  // (queue grou
 #endif
 // (bid / nblk: the block's index among the apply blocks and their count --
 // k_rapply's own grid, or the first nblk blocks of k_apply_link)
-template <uint32_t CH = kEmitChunk>
+template <uint32_t CH = kEmitChunk, uint32_t APE = kApplyPerEmit>
 __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Round* rd, const CandRec* cand, const uint32_t* bcand, const uint32_t* decof, const PostRec* post, unsigned long long* sched, HostRound* h, uint64_t* dbg, uint32_t bid, uint32_t nblk, TallyP tp = TallyP{}) {
   if (rd->skip) return;
   // A limit-break round's priority pops (group heads and their runs'
@@ -3043,7 +3046,6 @@ __device__ __attribute__((always_inline)) inline void rapply_body(Table tb, Roun
   }
   if (bid < nblk - 1) {
     // (APE apply blocks per emit block of CH slots)
-    constexpr uint32_t APE = apply_per_emit(CH);
     const uint32_t eb = bid / APE;
     const uint32_t nc = bcand[eb];
     const uint32_t base = eb * CH;
@@ -3367,7 +3369,7 @@ __global__ void __launch_bounds__(kRankThreads) k_rrank_m(const RRankArgs* a) {
 }
 __global__ void __launch_bounds__(kBlockR, DMC_APPLY_MINB) k_rapply_m(const RApplyArgs* a) {
   const RApplyArgs& x = a[blockIdx.y];
-  rapply_body<kEmitChunkM>(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr,
+  rapply_body<kEmitChunkM, kApplyPerEmitM>(x.tb, x.rd, x.cand, x.bcand, x.decof, x.post, x.sched, x.h, nullptr,
                            blockIdx.x, gridDim.x, x.tp);
 }
 
