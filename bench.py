@@ -147,7 +147,9 @@ def latest_traffic():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (the queue's key spread grows over a run: "
+                         "a longer window is the steadier, lower number)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clients", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1 << 16)
@@ -161,7 +163,9 @@ def parse():
                          "steady state with both phases")
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-steps", type=int, default=30)
+    ap.add_argument("--cpu-steps", type=int, default=30,
+                    help="steps of the CPU baseline's sample, timed as three "
+                         "consecutive repeats (the median is the value)")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="config 4: seconds of oracle work in the CPU sample")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -308,30 +312,56 @@ def prepare(q, args, tab, pre):
     return settle
 
 
+def cpu_model():
+    """the host CPU's model name (the baseline's cores differ box to box)"""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or None
+
+
 def cpu_baseline(args, tab, pre, steps, idle=None):
     """The oracle (CPU restatement of the reference queue, one core) on a
     bounded sample of the same workload: same 1M clients and pre-population,
-    timed over --cpu-steps steps."""
+    --cpu-steps steps timed as three consecutive repeats; the value is their
+    median (one core's rate moves with the box's other load)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     q = pyoracle.OracleQueue(track_ties=bool(args.heap_order))
     prepare(q, args, tab, pre)
     ties0 = q.ties if args.heap_order else 0
     k = args.pulls or args.batch
-    ops = 0
     if idle is not None:
-        return cpu_baseline_churn(args, q, steps, idle)
-    t0 = time.perf_counter()
-    for i, reqs in enumerate(steps[:args.cpu_steps]):
-        q.add_batch(reqs)
-        d, res = q.pull_batch(float(reqs["time"][-1]), k)
-        ops += len(reqs) + res.n_decisions
-    dt = time.perf_counter() - t0
-    out = {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+        out = cpu_baseline_churn(args, q, steps, idle)
+        out["cpu_model"] = cpu_model()
+        return out
+    reps = 3
+    per = max(1, args.cpu_steps // reps)
+    rates, ops_all, dt_all = [], 0, 0.0
+    for r in range(reps):
+        ops = 0
+        t0 = time.perf_counter()
+        for reqs in steps[r * per:(r + 1) * per]:
+            q.add_batch(reqs)
+            d, res = q.pull_batch(float(reqs["time"][-1]), k)
+            ops += len(reqs) + res.n_decisions
+        dt = time.perf_counter() - t0
+        rates.append(ops / dt)
+        ops_all += ops
+        dt_all += dt
+    out = {"value": float(np.median(rates)), "unit": "ops/s", "cores": 1, "kind": "port",
+           "cpu_model": cpu_model(),
+           "repeats": [round(x, 1) for x in rates],
            "sample": (f"oracle (CPU restatement, std::map + 3 binary heaps) on "
                       f"the same {args.clients}-client queue after the same "
-                      f"pre-population and settle, {args.cpu_steps} steps of "
-                      f"{args.batch} adds + {k} pulls, {dt:.2f} s")}
+                      f"pre-population and settle, {reps} consecutive repeats of "
+                      f"{per} steps of {args.batch} adds + {k} pulls "
+                      f"({dt_all:.2f} s in all); value = their median")}
     if args.heap_order:  # (tie tracking is on: its cost is in the sample)
         out["tied_decisions"] = {"setup": int(ties0), "sample": int(q.ties - ties0)}
     return out
@@ -455,7 +485,9 @@ def main():
     if idle is not None and not args.host_api and not args.host_idle:
         d_idle = [torch.from_numpy(np.ascontiguousarray(x, dtype=np.uint32).view(np.int32))
                   .to(dev) for x in idle]
-    d_rc = torch.zeros(args.batch, dtype=torch.int32, device=dev)
+    # every step's add statuses in a slice of their own (all asserted after
+    # the run, not only the last step's)
+    d_rc = torch.full((len(steps), args.batch), -1, dtype=torch.int32, device=dev)
     d_out = torch.zeros(k * DECISION_DTYPE.itemsize, dtype=torch.uint8,
                         device=dev)
     res_sz = 24
@@ -465,7 +497,8 @@ def main():
     # costs microseconds of Python the engine call does not need)
     p_reqs = [t.data_ptr() for t in d_reqs]
     p_res = [d_res[i].data_ptr() for i in range(len(steps))]
-    p_rc, p_out = d_rc.data_ptr(), d_out.data_ptr()
+    p_rc = [d_rc[i].data_ptr() for i in range(len(steps))]
+    p_out = d_out.data_ptr()
     torch.cuda.synchronize()
 
     host_t = {"mark_idle": 0.0, "add_pull": 0.0}
@@ -493,10 +526,10 @@ def main():
             assert (rc == 0).all()
             _, host_res[i] = q.pull_batch(nows[i], k)
         elif args.separate_calls:
-            q.add_batch_device(p_reqs[i], args.batch, p_rc)
+            q.add_batch_device(p_reqs[i], args.batch, p_rc[i])
             q.pull_batch_device(nows[i], k, p_out, p_res[i])
         else:  # the same two operations, one graph launch
-            q.add_pull_batch_device(p_reqs[i], args.batch, p_rc, nows[i], k, p_out, p_res[i])
+            q.add_pull_batch_device(p_reqs[i], args.batch, p_rc[i], nows[i], k, p_out, p_res[i])
 
     for i in range(args.warmup):
         step(i)
@@ -549,8 +582,11 @@ def main():
         pr = (host_res[args.warmup + j] if args.host_api
               else PullResult.from_buffer_copy(row.tobytes()))
         n_dec += pr.n_decisions
-    rc_last = d_rc.cpu().numpy()
-    assert args.host_api or (rc_last == 0).all(), np.unique(rc_last, return_counts=True)
+    if not args.host_api:
+        # every step that ran (warmup, timed, stage pass): each add accepted
+        ran = args.warmup + args.steps + prof_steps
+        rc_all = d_rc[:ran].cpu().numpy()
+        assert (rc_all == 0).all(), np.unique(rc_all, return_counts=True)
     st = st_t1
     n_adds = args.steps * args.batch
     local_ops = n_dec + n_adds

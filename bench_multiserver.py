@@ -140,6 +140,8 @@ def main(args):
     d_out = [torch.zeros(max(k, chunk) * DECISION_DTYPE.itemsize, dtype=torch.uint8,
                          device=dev) for _ in range(S)]
     d_res = torch.zeros((S, n_steps + n_prof + 64, 24), dtype=torch.uint8, device=dev)
+    # every step's add statuses in a slice of their own (all asserted)
+    d_rcs = torch.full((S, n_steps + n_prof, args.batch), -1, dtype=torch.int32, device=dev)
     d_steps = [[torch.from_numpy(r.view(np.uint8)).to(dev) for r in w[3]] for w in wl]
     nows = [[float(r["time"][-1]) for r in w[3]] for w in wl]
 
@@ -173,7 +175,7 @@ def main(args):
             d = d_steps[s][i]
             trk.fill(s, d.data_ptr(), args.batch)
             # the add batch and the pull batch in one graph launch
-            q.add_pull_batch_device(d.data_ptr(), args.batch, d_rc[s].data_ptr(),
+            q.add_pull_batch_device(d.data_ptr(), args.batch, d_rcs[s, i].data_ptr(),
                                     nows[s][i], k, d_out[s].data_ptr(),
                                     d_res[s, i].data_ptr())
             trk.tally(s, d_out[s].data_ptr(), d_res[s, i].data_ptr(), k)
@@ -182,9 +184,9 @@ def main(args):
     pool = ThreadPoolExecutor(S)
     group = None if args.separate_queues else GpuGroup(queues)
     g_args = [([d_steps[s][i].data_ptr() for s in range(S)], [nows[s][i] for s in range(S)],
-               [d_res[s, i].data_ptr() for s in range(S)])
+               [d_res[s, i].data_ptr() for s in range(S)],
+               [d_rcs[s, i].data_ptr() for s in range(S)])
               for i in range(n_steps + n_prof)]
-    g_rc = [d_rc[s].data_ptr() for s in range(S)]
     g_out = [d_out[s].data_ptr() for s in range(S)]
 
     def segment(i0, i1):
@@ -192,8 +194,8 @@ def main(args):
             list(pool.map(lambda s: run(s, i0, i1), range(S)))
             return
         for i in range(i0, i1):
-            reqs, nw, res = g_args[i]
-            group.step(args.batch, reqs, g_rc, nw, k, g_out, res, trk.group_trackers())
+            reqs, nw, res, rcs = g_args[i]
+            group.step(args.batch, reqs, rcs, nw, k, g_out, res, trk.group_trackers())
 
     t_prep = time.perf_counter()
     settle = list(pool.map(prepare, range(S)))[0]
@@ -232,11 +234,42 @@ def main(args):
         grp_ctr = {"fused_calls": sum(q.counters()["fused_calls"] for q in queues),
                    "graph_replays": sum(q.counters()["graph_replays"] for q in queues)}
 
-    # roofline: server 0's next n_prof steps alone (no other queue running),
-    # stage-timed like config 3 (HIP events around each stage on its stream)
+    # roofline: the kernels the timed steps ran.  Queue group: the group's
+    # next n_prof steps with its stage timers on (the same multi-table
+    # kernels, launched eagerly, each timed by its own dispatch), the
+    # algorithmic bytes of all S tables per launch (_stage_bytes is linear in
+    # the counts: the members' counters summed).  Separate queues: server 0's
+    # next n_prof steps alone, stage-timed like config 3.
     from bench import roofline
     roof = None
-    if n_prof:
+    if n_prof and group is not None:
+        for q in queues:
+            q.counters(reset=True)
+        group.profile(True)
+        torch.cuda.synchronize()
+        epochs_prof = []
+        steps_with_epochs(n_steps, n_steps + n_prof, epochs_prof)
+        for q in queues:
+            q.sync()
+        torch.cuda.synchronize()
+        prof = group.profile_read()
+        group.profile(False)
+        ctr = {}
+        for q in queues:
+            for key, v in q.counters().items():
+                if isinstance(v, (int, float)):
+                    ctr[key] = ctr.get(key, 0) + v
+        roof = roofline(args, prof, n_prof, ctr, k, n_clients=S * N,
+                        n_adds=S * args.batch)
+        if roof is not None:
+            roof["kernel"] = {"emit": "k_remit_m", "scan": "k_rscan_m",
+                              "add_chain": "k_add_chain_m", "add_link": "k_add_link_m",
+                              "select": "k_rhist_m + k_rpick_m", "rank": "k_rrank_m",
+                              "apply": "k_rapply_m"}.get(roof["kernel"], roof["kernel"])
+            roof["note"] = (f"queue group: the multi-table kernels of {n_prof} group "
+                            f"steps after the timed region (eager launches, each "
+                            f"timed by its own dispatch), {S} tables per launch")
+    elif n_prof:
         q0 = queues[0]
         q0.profile(True)
         q0.profile_reset()
@@ -248,16 +281,21 @@ def main(args):
         roof = roofline(args, q0.profile_read(), n_prof, q0.counters(), k,
                         n_clients=N)
         if roof is not None:
-            roof["note"] = ("server 0 alone after the timed region: its "
-                            "dominant stage per launch")
+            roof["note"] = ("separate queues: server 0 alone after the timed "
+                            "region, its dominant stage per launch")
 
     res = d_res[:, args.warmup:n_steps].cpu().numpy()
     n_dec = sum(PullResult.from_buffer_copy(row.tobytes()).n_decisions
                 for srv in res for row in srv)
     n_adds = S * args.steps * args.batch
-    for s in range(S):
-        rc = d_rc[s][:args.batch].cpu().numpy()
-        assert (rc == 0).all(), np.unique(rc, return_counts=True)
+    # every step that ran (warmup, timed, the roofline pass), every server
+    # (separate queues: the roofline pass ran server 0 alone)
+    rc = d_rcs[:, :n_steps].cpu().numpy()
+    assert (rc == 0).all(), np.unique(rc, return_counts=True)
+    if n_prof:
+        rcp = (d_rcs[:, n_steps:n_steps + n_prof] if group is not None
+               else d_rcs[:1, n_steps:n_steps + n_prof]).cpu().numpy()
+        assert (rcp == 0).all(), np.unique(rcp, return_counts=True)
     local_ops = n_dec + n_adds
     ep_ms = 1e3 * float(np.mean(epochs)) if epochs else None
     if dist:

@@ -307,33 +307,67 @@ __device__ inline RingView ring_view(const Table& tb, uint32_t s, uint32_t h) {
 }
 
 // Stage the first min(c, K) queue positions of slot s into st (this
-// thread's LDS slice): all loads issued before the first store.
+// thread's LDS slice): all loads issued before the first store.  In two
+// halves (StageLoads: the burst in registers; stage_put: its LDS stores) so
+// that a caller can issue its other loads of the same level in between.
 template <int K>
-__device__ inline RingView stage_ring(const Table& tb, uint32_t s, uint32_t h,
-                                      uint32_t c, ReqEntry* st) {
-  RingView v = ring_view(tb, s, h);
-  if (!st) return v;
-  const uint32_t ns = c < (uint32_t)K ? c : (uint32_t)K;
-  // 16-byte chunks: every load of the burst is issued before the first
-  // LDS store (the copies go through registers, never a private array)
-  uint4 x[K][4];
+struct StageLoads {
+  uint4 x[K][4];  // 16-byte chunks (registers, never a private array)
+  uint32_t ns;
+};
+// ALL: all K positions, queued or not (every index is masked into the
+// slot's ring: in bounds; positions past the count are staged and never
+// read): no value-or-zero per load, whose merge the compiler resolves with
+// a copy -- and a wait -- right after each load (k_remit's walkers); else
+// only the queued ones (k_rapply)
+template <int K, bool ALL = false>
+__device__ __attribute__((always_inline)) inline StageLoads<K> stage_load(
+    const Table& tb, uint32_t s, uint32_t h, uint32_t c, const ReqEntry* st) {
+  StageLoads<K> L;
+  L.ns = st ? (c < (uint32_t)K ? c : (uint32_t)K) : 0;
+  const ReqEntry* g = tb.ring + (size_t)s * tb.q;
+  if (ALL) {
+    if (st) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const char* src = reinterpret_cast<const char*>(g + ((h + j) & tb.qmask));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) L.x[j][k] = ld_as<uint4>(src + 16 * k);
+      }
+    }
+    return L;
+  }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    const char* src = reinterpret_cast<const char*>(v.g + ((h + j) & v.qmask));
+    const char* src = reinterpret_cast<const char*>(g + ((h + j) & tb.qmask));
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      x[j][k] = (uint32_t)j < ns ? ld_as<uint4>(src + 16 * k) : make_uint4(0, 0, 0, 0);
+      L.x[j][k] = (uint32_t)j < L.ns ? ld_as<uint4>(src + 16 * k) : make_uint4(0, 0, 0, 0);
   }
+  return L;
+}
+template <int K>
+__device__ __attribute__((always_inline)) inline RingView stage_put(
+    const Table& tb, uint32_t s, uint32_t h, const StageLoads<K>& L, ReqEntry* st) {
+  RingView v = ring_view(tb, s, h);
+  if (!st) return v;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     char* dst = reinterpret_cast<char*>(st + j);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if ((uint32_t)j < ns) st_as<uint4>(dst + 16 * k, x[j][k]);
+      if ((uint32_t)j < L.ns) st_as<uint4>(dst + 16 * k, L.x[j][k]);
   }
   v.st = st;
-  v.ns = ns;
+  v.ns = L.ns;
   return v;
+}
+template <int K>
+__device__ inline RingView stage_ring(const Table& tb, uint32_t s, uint32_t h,
+                                      uint32_t c, ReqEntry* st) {
+  if (!st) return ring_view(tb, s, h);
+  const StageLoads<K> L = stage_load<K>(tb, s, h, c, st);
+  return stage_put<K>(tb, s, h, L, st);
 }
 
 __device__ inline void keep(double v) { asm volatile("" ::"v"(v)); }

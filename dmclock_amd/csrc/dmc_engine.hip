@@ -157,7 +157,7 @@ __device__ __attribute__((always_inline)) inline void add_link_body(AddParams p,
   uint32_t s = 0;
   if (DMC_EARLY_LOADS && i < p.n) s = p.reqs[i].slot;
   if (prev) {
-    if (prev->skip || prev->overflow || prev->n_dec < prev->k_total) return;
+    if (!round_ends_call(*prev)) return;
   } else if (tb.gate && *tb.gate) {
     return;  // (DMC_OPT_PIPELINE: a shut gate, see Table::gate)
   }
@@ -2037,6 +2037,10 @@ struct dmc_queue {
   // queue's stream is presumed wedged and every later call returns
   // DMC_EDEVICE instead of blocking on it
   bool wedged = false;
+  // DMC_OPT_PIPELINE: the error of the last pipelined call that failed when
+  // a later call finished it (that later call returned DMC_ENOTRUN or the
+  // error itself); dmc_queue_pipelined_error reads it
+  int pipe_err = 0;
   // DMC_OPT_HEAP_ORDER (dmc_heap.h): the reference's heaps on the device,
   // every add and pull in call order
   bool heap = false;
@@ -2206,7 +2210,33 @@ struct dmc_group {
   uint64_t seen[4] = {0, 0, 0, 0};
   uint32_t seen_pos = 0, graph_next = 0;
   uint64_t steps = 0, fused_steps = 0, graph_launches = 0;
+  // dmc_group_profile_enable: fused steps launched eagerly, each multi-table
+  // kernel's execution timed by its own dispatch (hipExtLaunchKernel) -- the
+  // kernels the group's timed steps run, per launch over all S tables
+  bool prof_on = false;
+  struct PRec {
+    hipEvent_t a = nullptr, b = nullptr;
+    int stage = 0;
+  };
+  std::vector<PRec> prof_pool;
+  size_t prof_n = 0;
+  double prof_ms[DMC_PROF_NSTAGES] = {};
+  uint64_t prof_cnt[DMC_PROF_NSTAGES] = {};
 };
+
+void group_prof_flush(dmc_group* g) {
+  if (!g->prof_n) return;
+  (void)hipEventSynchronize(g->prof_pool[g->prof_n - 1].b);
+  for (size_t i = 0; i < g->prof_n; ++i) {
+    float ms = 0.f;
+    const dmc_group::PRec& r = g->prof_pool[i];
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      g->prof_ms[r.stage] += ms;
+      g->prof_cnt[r.stage] += 1;
+    }
+  }
+  g->prof_n = 0;
+}
 
 void group_graphs_destroy(dmc_group* g) {
   for (auto& x : g->graphs) {
@@ -2318,7 +2348,7 @@ struct QueueLock {
     }
     if (!serve) rc = serve_quiesce(q);
     if (serve_registry().qs.size() > (q->serve_reg ? 1u : 0u)) serve_yield_others(q);
-    if (!rc && settle && q->pend.on) rc = settle_pending(q);
+    if (!rc && settle && q->pend.on && (rc = settle_pending(q))) q->pipe_err = rc;
   }
 };
 
@@ -3901,7 +3931,7 @@ int settle_pending(dmc_queue* q, bool* clean_out) {
   }
   int rc = wait_round(q, p.seq);
   if (rc) return rc;
-  const bool clean = !q->h_rd->overflow && q->h_rd->n_dec >= q->h_rd->k_total;
+  const bool clean = round_ends_call(*q->h_rd);
   if (clean_out) *clean_out = clean;
   if (!clean) HIP_OK(hipMemsetAsync(q->gate, 0, 4, q->stream));
   dmc_pull_result r{};
@@ -4976,7 +5006,15 @@ int dmc_add_pull_batch_device(dmc_queue* q, uint32_t n, const dmc_request* d_req
         // the previous call, finished now that this one is queued behind it
         bool clean = true;
         if ((rc = settle_pending(q, &clean))) {
-          if (clean) return rc;  // (the device failed: this call's state is unknown)
+          q->pipe_err = rc;  // (kept: DMC_ENOTRUN below does not say what it was)
+          if (clean) {
+            // the previous call's round ended its call (the gate stayed
+            // open), so this call's kernels, queued behind it, ran -- but
+            // its deferred apply is not launched, nor its round read: the
+            // queue's state is unknown, and every later call fails
+            q->wedged = true;
+            return rc;
+          }
           // the previous call failed after shutting the gate: this call's
           // graph, queued behind it, did nothing -- it was not executed
           // (its statuses, decisions and result untouched), which
@@ -5116,6 +5154,10 @@ int dmc_group_destroy(dmc_group* g) {
     q->group = nullptr;
   }
   group_graphs_destroy(g);
+  for (auto& r : g->prof_pool) {
+    if (r.a) (void)hipEventDestroy(r.a);
+    if (r.b) (void)hipEventDestroy(r.b);
+  }
   if (g->h_blob) (void)hipHostFree(g->h_blob);
   dfree(g->d_blob);
   if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -5125,6 +5167,29 @@ int dmc_group_destroy(dmc_group* g) {
 }
 
 void* dmc_group_stream(dmc_group* g) { return g ? (void*)g->stream : nullptr; }
+
+int dmc_group_profile_enable(dmc_group* g, int on) {
+  if (!g) return DMC_EINVAL;
+  GroupLock gl(g);
+  if (gl.rc) return gl.rc;
+  group_prof_flush(g);
+  g->prof_on = on != 0;
+  for (int i = 0; i < DMC_PROF_NSTAGES; ++i) {
+    g->prof_ms[i] = 0.0;
+    g->prof_cnt[i] = 0;
+  }
+  return DMC_OK;
+}
+
+int dmc_group_profile_read(dmc_group* g, uint32_t stage, uint64_t* count, double* total_ms) {
+  if (!g || stage >= DMC_PROF_NSTAGES || !count || !total_ms) return DMC_EINVAL;
+  GroupLock gl(g);
+  if (gl.rc) return gl.rc;
+  group_prof_flush(g);
+  *count = g->prof_cnt[stage];
+  *total_ms = g->prof_ms[stage];
+  return DMC_OK;
+}
 
 int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                           int32_t* const* d_rc, const double* now, uint32_t k,
@@ -5204,33 +5269,68 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       }
       const uint32_t gHist = all_sampled ? kHistBlocksSampled : kHistBlocksR;
       uint8_t* d = g->d_blob;
+      // (profiling: eager launches, each kernel's dispatch recording its
+      // stage's events; a stage of two kernels -- select: hist + pick -- gets
+      // its start from the first and its end from the second)
+      hipEvent_t ev_open = nullptr;
+      auto gl = [&](hipStream_t st, int stage, int part, auto kernel, dim3 gr, dim3 bl,
+                    auto arg) {
+        if (!g->prof_on || st != g->stream || stage < 0) {
+          hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg);
+          return;
+        }
+        if (part == 0 || part == 2) {  // (a new record: 0 one kernel, 2 first of two)
+          if (g->prof_n == g->prof_pool.size()) {
+            dmc_group::PRec r;
+            if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
+                hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
+              g->prof_on = false;
+              hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg);
+              return;
+            }
+            g->prof_pool.push_back(r);
+          }
+          g->prof_pool[g->prof_n].stage = stage;
+        }
+        dmc_group::PRec& r = g->prof_pool[g->prof_n];
+        if (part == 0) {
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, r.b, 0, arg);
+          ++g->prof_n;
+        } else if (part == 2) {
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, nullptr, 0, arg);
+          ev_open = r.b;
+        } else {  // part 3: the second of two
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, nullptr, ev_open, 0, arg);
+          ++g->prof_n;
+        }
+      };
       auto enqueue = [&](hipStream_t st) {
         (void)hipMemcpyAsync(d, g->h_blob, g->bytes, hipMemcpyHostToDevice, st);
         // (the trackers' get_req_params run inside k_add_chain_m: TrackFill)
-        hipLaunchKernelGGL(k_add_link_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                           (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_add_chain_m, dim3(gAdd, S), dim3(kBlock), 0, st,
-                           (const AddArgs*)(d + g->o_add));
-        hipLaunchKernelGGL(k_rscan_m, dim3(gN, S), dim3(kScanBlock), 0, st,
-                           (const RScanArgs*)(d + g->o_scan));
-        hipLaunchKernelGGL(k_rhist_m, dim3(gHist, S), dim3(1024), 0, st,
-                           (const RHistArgs*)(d + g->o_hist));
+        gl(st, DMC_PROF_ADD_LINK, 0, k_add_link_m, dim3(gAdd, S), dim3(kBlock),
+           (const AddArgs*)(d + g->o_add));
+        gl(st, DMC_PROF_ADD_CHAIN, 0, k_add_chain_m, dim3(gAdd, S), dim3(kBlock),
+           (const AddArgs*)(d + g->o_add));
+        gl(st, DMC_PROF_SCAN, 0, k_rscan_m, dim3(gN, S), dim3(kScanBlock),
+           (const RScanArgs*)(d + g->o_scan));
+        gl(st, DMC_PROF_SELECT, kPrePickM ? 2 : 0, k_rhist_m, dim3(gHist, S), dim3(1024),
+           (const RHistArgs*)(d + g->o_hist));
         if (kPrePickM)
-          hipLaunchKernelGGL(k_rpick_m, dim3(1, S), dim3(kEmitThreads), 0, st,
-                             (const RHistArgs*)(d + g->o_hist));
+          gl(st, DMC_PROF_SELECT, 3, k_rpick_m, dim3(1, S), dim3(kEmitThreads),
+             (const RHistArgs*)(d + g->o_hist));
         if (kPrePickM && DMC_SPLIT_EMIT_M) {
-          hipLaunchKernelGGL(k_rsel_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
-                             (const REmitArgs*)(d + g->o_emit));
-          hipLaunchKernelGGL(k_rwalk_m, dim3(gEm, S), dim3(kWalkThreads), 0, st,
-                             (const REmitArgs*)(d + g->o_emit));
+          gl(st, -1, 0, k_rsel_m, dim3(gEm, S), dim3(kEmitThreads),
+             (const REmitArgs*)(d + g->o_emit));
+          gl(st, -1, 0, k_rwalk_m, dim3(gEm, S), dim3(kWalkThreads),
+             (const REmitArgs*)(d + g->o_emit));
         } else {
-          hipLaunchKernelGGL(k_remit_m, dim3(gEm, S), dim3(kEmitThreads), 0, st,
-                             (const REmitArgs*)(d + g->o_emit));
+          gl(st, DMC_PROF_EMIT, 0, k_remit_m, dim3(gEm, S), dim3(kEmitThreads),
+             (const REmitArgs*)(d + g->o_emit));
         }
-        hipLaunchKernelGGL(k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads), 0, st,
-                           (const RRankArgs*)(d + g->o_rank));
-        hipLaunchKernelGGL(k_rapply_m, dim3(kApplyPerEmitM * gEm + 1, S), dim3(kBlockR), 0,
-                           st, (const RApplyArgs*)(d + g->o_apply));
+        gl(st, DMC_PROF_RANK, 0, k_rrank_m, dim3(kRankBlocksR, S), dim3(kRankThreads),
+           (const RRankArgs*)(d + g->o_rank));
+        gl(st, DMC_PROF_APPLY, 0, k_rapply_m, dim3(kApplyPerEmitM * gEm + 1, S), dim3(kBlockR),
+           (const RApplyArgs*)(d + g->o_apply));
       };
       // the step's graph: captured at the second sighting of its shape, then
       // replayed (the arguments travel in the blob, no node updates)
@@ -5239,7 +5339,9 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       dmc_group::G* gr = nullptr;
       for (auto& x : g->graphs)
         if (x.exec && x.key == key) gr = &x;
-      if (!gr) {
+      if (g->prof_on) {
+        gr = nullptr;  // (profiled steps launch eagerly)
+      } else if (!gr) {
         bool seen = false;
         for (uint64_t s0 : g->seen) seen |= s0 == key;
         if (seen) {
@@ -5707,6 +5809,14 @@ int dmc_queue_counters_sized(dmc_queue* q, void* out, uint64_t size, int reset) 
 }
 
 int dmc_abi_version(void) { return DMC_ABI_VERSION; }
+
+int dmc_queue_pipelined_error(dmc_queue* q, int clear) {
+  if (!q) return DMC_EINVAL;
+  std::lock_guard<std::mutex> l(q->mtx);
+  const int e = q->pipe_err;
+  if (clear) q->pipe_err = 0;
+  return e;
+}
 
 int dmc_profile_enable(dmc_queue* q, int on) {
   if (!q) return DMC_EINVAL;

@@ -44,6 +44,8 @@
 // 32-bit radix sort + exact fix-up).
 #pragma once
 
+#include <type_traits>
+
 #include "dmc_device.h"
 
 namespace dmc {
@@ -153,6 +155,17 @@ struct Round {
   uint32_t skip;         // this round's kernels do nothing (its k_rscan found the gate shut)
   uint32_t* gate;        // a pipelined round: its end sets the gate (CallParams::gate)
 };
+
+// A pipelined round ends its call (the host has nothing left to do for
+// it): the gate stays open and the next call's queued kernels run.  One
+// formula for its three readers -- the round's last block, which sets the
+// gate (rfinish_body); a filing merged beside the round's apply, which
+// cannot read the gate that launch writes (add_link_body); and the host's
+// settle_pending -- so that they never disagree.  (A skipped round's apply
+// never reaches rfinish_body: its gate stays shut.)
+__host__ __device__ inline bool round_ends_call(const Round& r) {
+  return !r.skip && !r.overflow && r.n_dec >= r.k_total;
+}
 
 struct CallParams {
   uint32_t k_total;
@@ -1613,9 +1626,19 @@ constexpr int kEmitStage = DMC_EMIT_STAGE;  // queue positions staged per walker
 #endif
 constexpr int kEmitStageThreads = DMC_EMIT_STAGE_THREADS;  // walkers with a staging slice
 // (BRK: a limit-break round, its own instantiation of k_remit: the general
-// walkers carry none of walk_p's break-mode code)
-template <bool BRK>
-__device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* ph,
+// walkers carry none of walk_p's break-mode code.  DL: the table's tag mode
+// as a compile-time constant, 0 immediate, 1 delayed, -1 read from the table
+// -- with it fixed, the walker's loads are one straight-line burst, and the
+// compiler's wait counting sees no delayed-mode loads in flight across the
+// candidate loop)
+#ifndef DMC_EMIT_MODE_SPLIT
+#define DMC_EMIT_MODE_SPLIT 1
+#endif
+#ifndef DMC_EMIT_PEEL
+#define DMC_EMIT_PEEL 1
+#endif
+template <bool BRK, int DL = -1>
+__device__ inline uint32_t emit_one(const Table& tb0, Round* rd, double now, const PhaseSel* ph,
                                 const CandRec& c,
                                 uint32_t ci, BRecR* brec, uint32_t* bcount,
                                 unsigned long long* ssup,
@@ -1624,32 +1647,54 @@ __device__ inline uint32_t emit_one(const Table& tb, Round* rd, const PhaseSel* 
                                 ReqEntry* st, uint32_t key32_0, uint64_t* ck = nullptr) {
   // ck (debug): [0] entry, [1] client record and ring staged, [2] walks and
   // their rank records done
+  Table tb = tb0;
+  if (DL >= 0) tb.delayed = DL;
   if (ck) ck[0] = wall_clock64();
   const uint32_t s = c.slot;
   const uint64_t TR = uniform_u64(ph[0].T), TP = uniform_u64(ph[1].T);
-  const double now = rd->now;
   Tag3 pf;
   uint32_t fc;
   EmitAcc acc;
   acc.ci = ci;
-  const CView cv = cand_view(tb, c);
-  const double prev_r = tb.rec[s].prev_r;  // (the inverses' line)
-  const uint32_t h = cv.h;
-  const RingView rv = stage_ring<kEmitStage>(tb, s, h, cv.c, st);
 #ifndef DMC_EMIT_PRERESERVE
 #define DMC_EMIT_PRERESERVE 1
 #endif
-  if (DMC_EMIT_PRERESERVE && brec) {
-    // the first record's rank-bin place, reserved before the walk (its key
-    // is the first key of the candidate's first phase, key32_0 is its
-    // quantum): the atomic's latency overlaps the walk
+  // the first record's rank-bin place, reserved before the walk (its key is
+  // the first key of the candidate's first phase, key32_0 is its quantum;
+  // its bin comes from LDS alone).  DMC_EMIT_RESERVE_FIRST: the returning
+  // atomic is issued ahead of the client record and ring loads, so that its
+  // round trip overlaps theirs (on gfx950 vector memory results return in
+  // issue order: the wait for the staged entries covers it); else after
+  // them (round 5: a second dependent round trip per walker)
+#ifndef DMC_EMIT_RESERVE_FIRST
+#define DMC_EMIT_RESERVE_FIRST 1
+#endif
+  unsigned long long rsv = 0;  // the atomic's whole 64-bit result (below)
+  auto reserve = [&]() {
     const int ph0 = c.cr() ? 0 : 1;
     acc.b0 = rank_bin_q((uint64_t)key32_0 << 32, ph[ph0], ph0, sbn);
-    acc.at0 = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long*>(bcount) + acc.b0,
-                                  (1ull << 32) | 1ull);
+    rsv = atomicAdd(reinterpret_cast<unsigned long long*>(bcount) + acc.b0,
+                    (1ull << 32) | 1ull);
     atomicAdd(&ssup[acc.b0 / kSupBins], (1ull << 32) | 1ull);
     acc.pre = true;
-  }
+  };
+  if (DMC_EMIT_PRERESERVE && DMC_EMIT_RESERVE_FIRST && brec) reserve();
+  // one level of loads: the staged ring entries, then the client record (a
+  // wait for the record's fields is then a wait for the whole level)
+  const StageLoads<kEmitStage> sl = stage_load<kEmitStage, true>(tb, s, c.h, c.c, st);
+  const CView cv = cand_view(tb, c);
+  const double prev_r = tb.rec[s].prev_r;  // (the inverses' line)
+  const uint32_t h = cv.h;
+  const RingView rv = stage_put<kEmitStage>(tb, s, h, sl, st);
+  if (DMC_EMIT_PRERESERVE && !DMC_EMIT_RESERVE_FIRST && brec) reserve();
+  // (both halves of the result stay live to here: a register of the
+  // returning atomic reused before it returns would be a wait for it ahead
+  // of the loads above; and the record's fields are waited for here on
+  // every path, so that no load is in flight across the candidate loop's
+  // back edge -- the compiler would otherwise wait for it, and everything
+  // issued before it, ahead of the next candidate's loads)
+  asm volatile("" ::"v"(rsv), "v"(prev_r), "v"(cv.rinv), "v"(cv.pd));
+  if (acc.pre) acc.at0 = (uint32_t)rsv;
   if (ck) {
     keep(cv.rinv);
     keep(cv.pd);
@@ -1843,6 +1888,7 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // (the pick's first use of them is then no load level of its own)
   RoundPart tot_e;
   uint32_t k_e = 0, sampled_e = 0, fault_e = 0;
+  const double now_e = rd->now;  // (the walkers' clock, requested here too)
   if constexpr (!PRE) {
     tot_e = rd->tot;
     k_e = rd->k_total;
@@ -1966,14 +2012,33 @@ __device__ __attribute__((always_inline)) inline void remit_t_body(Table tb, Rou
   // spilled -- from the kernel's start)
   uint32_t sli = (threadIdx.x >> 6) * SL + lane;
   asm volatile("" : "+v"(sli));
-  for (uint32_t j = lane; j < wtot; j += 64) {
-    const uint32_t i = wbase + j;
-    const uint32_t cat = emit_one<BRK>(
-        tb, rd, s_ph, bl[i], cbase + i, brec, bcount, s_sup, ltab, dense, dcap, post, decof,
-        lane < SL ? stage + sli * kEmitStage : nullptr,
-        bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
-    atomicAdd(&s_ec[cat], 1u);
-  }
+  auto walk_all = [&](auto dl) {
+    auto walk_cand = [&](uint32_t j) {
+      const uint32_t i = wbase + j;
+      const uint32_t cat = emit_one<BRK, decltype(dl)::value>(
+          tb, rd, now_e, s_ph, bl[i], cbase + i, brec, bcount, s_sup, ltab, dense, dcap, post, decof,
+          lane < SL ? stage + sli * kEmitStage : nullptr,
+          bk[i], eclk && i < 512 ? eclk + 5 * 4096 + 8 + 4 * (blockIdx.x * 512 + i) : nullptr);
+      atomicAdd(&s_ec[cat], 1u);
+    };
+    uint32_t j = lane;
+    // immediate mode: a lane's first candidate (most lanes' only one) walked
+    // outside the loop -- straight-line code, whose loads the compiler's wait
+    // counting does not hold behind loads left in flight by a previous
+    // iteration (a wave walks more than 64 candidates rarely)
+    if (decltype(dl)::value == 0 && DMC_EMIT_PEEL && j < wtot) {
+      walk_cand(j);
+      j += 64;
+    }
+    for (; j < wtot; j += 64) walk_cand(j);
+  };
+  // (nothing of the selection is in flight any more; said explicitly, so that
+  // the compiler's wait counting starts the walkers from an empty queue and
+  // holds none of their loads behind a load it cannot see completed)
+  if (DMC_EMIT_PEEL) __builtin_amdgcn_s_waitcnt(0x0f70);  // s_waitcnt vmcnt(0)
+  if (!DMC_EMIT_MODE_SPLIT) walk_all(std::integral_constant<int, -1>{});
+  else if (tb.delayed) walk_all(std::integral_constant<int, 1>{});
+  else walk_all(std::integral_constant<int, 0>{});
   __syncthreads();
   const uint32_t tot = s_tot;
   if (threadIdx.x < 4 && s_ec[threadIdx.x]) atomicAdd(&rd->ecnt[threadIdx.x], s_ec[threadIdx.x]);
@@ -2142,9 +2207,12 @@ __device__ inline BKeyS bkey_s(const BKey& k) {
 // (which stores the candidate's precomputed state); a slow record's pop is
 // stamped into its ring entry.  (ISP: a P bin, whose records' group sizes
 // 1 + run give the decision offsets; an R bin's offset is its rank.)
+#ifndef DMC_RANK_OKEY_FIRST
+#define DMC_RANK_OKEY_FIRST 1
+#endif
 template <bool ISP>
 __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, uint32_t cnt,
-                                uint32_t parts, uint32_t per, uint32_t i,
+                                bool anyrun, uint32_t parts, uint32_t per, uint32_t i,
                                 uint32_t part, uint32_t k,
                                 uint32_t n_pgroups, uint32_t soff, uint32_t poff,
                                 ReqEntry* ring, dmc_decision* out, uint32_t* decof, const TallyP& tly) {
@@ -2153,22 +2221,85 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
   const uint32_t me_slot = me.slot();
   // the writer lane's payload (an L2 hit: the block staged the line), in
   // flight during the comparisons
-  uint32_t ci = 0, cost = 0, ridx = 0;
-  uint64_t handle = 0;
-  double tr = 0.0, tp = 0.0, tl = 0.0;
-  if (valid && part == 0) {
-    const BRecR& x = src[i];
-    ci = x.ci;
-    cost = x.cost;
-    handle = x.handle;
-    tr = x.r;
-    tp = x.p;
-    tl = x.l;
-    ridx = x.k.ridx;
-  }
+  // (every lane loads a record -- its own, or the bin's first -- and only the
+  // writer uses it: a load under a condition merges with a default value,
+  // which the compiler resolves with a copy, and a wait for the load, right
+  // after it, ahead of the comparisons it should overlap)
+  const BRecR& x = src[valid ? i : 0];
+  const uint32_t ci = x.ci, cost = x.cost, ridx = x.k.ridx;
+  const uint64_t handle = x.handle;
+  const double tr = x.r, tp = x.p, tl = x.l;
   uint32_t f0 = part * per, f1 = f0 + per < cnt ? f0 + per : cnt;
   if (!valid) f1 = f0;
   uint32_t rank = 0, gl = 0, tie = 0;
+#if DMC_RANK_OKEY_FIRST
+  // The order key decides unless it is equal: the main pass counts the
+  // records with a smaller okey (and, in a P bin whose records have runs,
+  // their runs) and those with an equal one; only a record whose okey is
+  // shared (eq > 1: itself and another) walks the bin again for the exact
+  // (okey, slot, queue position) order among the equal ones and the tie
+  // flag.  Four VALU operations per compared record instead of eleven, and
+  // the next keys' LDS reads issued before this batch's compares (one wave
+  // per SIMD: nothing else hides their latency).
+  uint32_t lt = 0, eq = 0, rs = 0;
+  {
+    // (okeys only; reads past f1 stay inside sh -- f1 <= cnt <= kRankSortMin,
+    // sh holds kBinCapR -- and are masked)
+    // whole batches of U unmasked (every load of a batch issued before its
+    // compares), then one masked batch
+    constexpr uint32_t U = 8;
+    uint32_t f = f0;
+    for (; f + U <= f1; f += U) {
+      uint64_t cur[U];
+#pragma unroll
+      for (uint32_t j = 0; j < U; ++j) cur[j] = sh[f + j].okey;
+#pragma unroll
+      for (uint32_t j = 0; j < U; ++j) {
+        const bool l = cur[j] < me.okey;
+        lt += l ? 1u : 0u;
+        eq += cur[j] == me.okey ? 1u : 0u;
+        if (ISP && anyrun) rs += l ? ((uint32_t)sh[f + j].lo & 0xffffu) : 0u;
+      }
+    }
+    if (f < f1) {
+      uint64_t cur[U];
+#pragma unroll
+      for (uint32_t j = 0; j < U; ++j) cur[j] = sh[f + j].okey;
+#pragma unroll
+      for (uint32_t j = 0; j < U; ++j) {
+        const bool in = f + j < f1;
+        const bool l = in && cur[j] < me.okey;
+        lt += l ? 1u : 0u;
+        eq += (in && cur[j] == me.okey) ? 1u : 0u;
+        if (ISP && anyrun) rs += l ? ((uint32_t)sh[f + j].lo & 0xffffu) : 0u;
+      }
+    }
+  }
+  for (uint32_t d = 1; d < parts; d <<= 1) {
+    lt += __shfl_xor(lt, d);
+    eq += __shfl_xor(eq, d);
+    if (ISP && anyrun) rs += __shfl_xor(rs, d);
+  }
+  rank = lt;
+  gl = lt + rs;
+#ifndef DMC_RANK_NOSLOW
+#define DMC_RANK_NOSLOW 0  // (A/B probe only: wrong on equal keys)
+#endif
+  if (!DMC_RANK_NOSLOW && valid && part == 0 && eq > 1) {
+    // (rare: keys shared by several records) the equal okeys, in order
+    for (uint32_t f = 0; f < cnt; ++f) {
+      const BKeyS o = sh[f];
+      if (o.okey != me.okey) continue;
+      if (o.lo < me.lo) {
+        ++rank;
+        gl += 1u + (ISP ? ((uint32_t)o.lo & 0xffffu) : 0u);
+      }
+      tie |= (uint32_t)((uint32_t)(o.lo >> 32) != me_slot);
+    }
+  }
+  if (!ISP) gl = rank;
+#else
+  (void)anyrun;
 #pragma unroll 4
   for (uint32_t f = f0; f < f1; ++f) {
     const BKeyS o = sh[f];
@@ -2185,6 +2316,7 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
     tie |= __shfl_xor(tie, d);
   }
   if (!ISP) gl = rank;
+#endif
   if (valid && part == 0)
     place_rec(rd, BKey{me.okey, me_slot, me.seq(), me.run(), ridx}, ci, cost, handle, tr, tp, tl,
               rank, gl, tie, ISP, k, n_pgroups, soff, poff, ring, out, decof, tly);
@@ -2214,6 +2346,8 @@ constexpr int kRankBlocksR = kNBR;
 #define DMC_RANK_SORT_MIN 256
 #endif
 constexpr uint32_t kRankSortMin = DMC_RANK_SORT_MIN;
+// (rank_rec's unmasked okey reads run up to 8 records past a counted bin)
+static_assert(kRankSortMin + 16 <= kBinCapR, "rank reads past the bin stay in sh");
 __device__ inline bool bkey_less(const BKeyS& x, const BKeyS& y) {
   return x.okey < y.okey || (x.okey == y.okey && x.lo < y.lo);
 }
@@ -2516,11 +2650,23 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
       if (cnt > kBinMaxReport) atomicMax(&rd->bin_max[isp ? 1 : 0], cnt);
     }
   }
+  __shared__ uint32_t s_anyrun;
+  if (threadIdx.x == 0) s_anyrun = 0;
   __syncthreads();
   const uint32_t cnt = s_hdr[0];
   if (cnt == 0 || fail0 || s_hdr[4]) return;
   const uint32_t soff = s_hdr[1], poff = s_hdr[2], n_pgroups = s_hdr[3];
-  for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) sh[i] = bkey_s(src[i].k);
+  {
+    // (a P bin's records with runs: their group sizes enter the offsets;
+    // most bins have none, and the rank skips them)
+    uint32_t ar = 0;
+    for (uint32_t i = threadIdx.x; i < cnt; i += kRankThreads) {
+      const BKeyS b = bkey_s(src[i].k);
+      sh[i] = b;
+      ar |= (uint32_t)b.lo & 0xffffu;
+    }
+    if (ar) s_anyrun = 1;  // (benign race: every writer stores 1)
+  }
   if (cnt > kRankSortMin) {
     rank_sorted(rd, sh, src, cnt, isp, k, n_pgroups, soff, poff, ring, out, decof, tly);
     if (wtime && threadIdx.x == 0) {
@@ -2530,6 +2676,7 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     return;
   }
   __syncthreads();
+  const bool anyrun = s_anyrun != 0;
   const uint32_t t = threadIdx.x;
   // passes of kRankThreads / parts records, parts lanes per record, parts
   // sized per pass (a bin of 190: 128 records with 1 lane each, then 62 with 2)
@@ -2539,10 +2686,10 @@ __device__ __attribute__((always_inline)) inline void rrank_body(Round* rd, cons
     while (parts < 64 && rem * parts * 2 <= (uint32_t)kRankThreads) parts <<= 1;
     const uint32_t per = (cnt + parts - 1) / parts;
     if (isp)
-      rank_rec<true>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
+      rank_rec<true>(rd, sh, src, cnt, anyrun, parts, per, rb + t / parts, t % parts, k, n_pgroups,
                      soff, poff, ring, out, decof, tly);
     else
-      rank_rec<false>(rd, sh, src, cnt, parts, per, rb + t / parts, t % parts, k, n_pgroups,
+      rank_rec<false>(rd, sh, src, cnt, false, parts, per, rb + t / parts, t % parts, k, n_pgroups,
                       soff, poff, ring, out, decof, tly);
     rb += kRankThreads / parts;
   }
@@ -2880,7 +3027,7 @@ __device__ inline void rfinish_body(const Round* rd, HostRound* h, bool round_en
   // a pipelined round (DMC_OPT_PIPELINE): the gate stays open iff the round
   // ends its call (the host has nothing left to do for it)
   if (round_end && threadIdx.x == 0 && rd->gate)
-    *rd->gate = (!rd->overflow && rd->n_dec >= rd->k_total) ? 0u : 1u;
+    *rd->gate = round_ends_call(*rd) ? 0u : 1u;
   constexpr uint32_t W = sizeof(Round) / 4;
   const char* src = reinterpret_cast<const char*>(rd);
   char* dst = reinterpret_cast<char*>(&h->r);
@@ -3339,11 +3486,12 @@ __device__ __attribute__((always_inline)) inline void rwalk_body(Table tb, Round
   if (threadIdx.x < 4) s_ec[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t cbase = seg * kEmitChunk;
+  const double now_w = rd->now;
   for (uint32_t i = threadIdx.x; i < tot; i += kWalkThreads) {
     const uint32_t ci = cbase + i;
     const CandRec c = cand[ci];
     const uint32_t key0 = decof[ci];
-    const uint32_t cat = emit_one<false>(tb, rd, s_ph, c, ci, brec, bcount, s_sup, ltab, dense,
+    const uint32_t cat = emit_one<false>(tb, rd, now_w, s_ph, c, ci, brec, bcount, s_sup, ltab, dense,
                                          dcap, post, decof, stage + threadIdx.x * kEmitStage,
                                          key0);
     atomicAdd(&s_ec[cat], 1u);

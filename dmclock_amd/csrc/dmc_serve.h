@@ -389,6 +389,9 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
   __shared__ uint32_t s_nst;
   __shared__ uint16_t s_stale[kServeMaxG];
   __shared__ uint64_t s_cmd[8];  // the command line's words (op 0: exit)
+  // an add's request (words 3-6 of the line), stored into a dmc_request
+  // object byte-wise (st_as): read as its own type, never through s_cmd
+  __shared__ dmc_request s_req;
   __shared__ uint32_t s_life;
   __shared__ int32_t s_rc;
   __shared__ StepCtl s_c;
@@ -419,6 +422,10 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
       // wave 0 polls: the command line, one load per poll; adds are served
       // here, one after another, until a pull (or the end) comes
       const uint32_t lane = threadIdx.x;
+      // (the command words -- seq, op, now, the request -- are written by
+      // the host and only ever read here, as whole words through system-
+      // scope atomic loads, never as their declared members: no access of
+      // another type for alias analysis to order them against)
       const uint64_t* line = reinterpret_cast<const uint64_t*>(io);
       for (;;) {
         const uint64_t t0 = wall_clock64();
@@ -442,6 +449,8 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         c_seen = wall_clock64();
         if (got) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (lane < kServeCmdWords) s_cmd[lane] = got ? w : 0;
+        if (lane >= 3 && lane < 7)
+          st_as<uint64_t>(reinterpret_cast<char*>(&s_req) + 8 * (lane - 3), got ? w : 0);
         c_read = c_seen;
         if (trace && lane == 0) io->cyc[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -455,7 +464,7 @@ k_serve(Table tb, StepRed* gs, uint32_t G, uint32_t gshift, ServeIO* io, int at_
         const uint64_t s_tick = tick++;  // (++tick, :918: the host's count follows)
         uint32_t life = 0;
         if (lane == 0) {
-          const dmc_request* s_reqp = reinterpret_cast<const dmc_request*>(&s_cmd[3]);
+          const dmc_request* s_reqp = &s_req;
           const uint32_t s = s_reqp->slot;
           if (s >= tb.n || !(tb.sc[s].flags & F_REG)) {
             s_rc = DMC_ENOTREG;

@@ -66,6 +66,7 @@ EXPORTS = {
     "dmc_queue_counters": (_i32, [_vp, ctypes.POINTER(Counters), _i32]),
     "dmc_queue_counters_sized": (_i32, [_vp, _vp, ctypes.c_uint64, _i32]),
     "dmc_abi_version": (_i32, []),
+    "dmc_queue_pipelined_error": (_i32, [_vp, _i32]),
     "dmc_tracker_tally": (_i32, [_vp, _vp, _vp, _u32, _vp, _vp]),
     "dmc_tracker_fill": (_i32, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp,
                                 _vp]),
@@ -77,6 +78,9 @@ EXPORTS = {
     "dmc_group_destroy": (_i32, [_vp]),
     "dmc_group_stream": (_vp, [_vp]),
     "dmc_group_step_device": (_i32, [_vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    "dmc_group_profile_enable": (_i32, [_vp, _i32]),
+    "dmc_group_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(_f64)]),
     "dmc_profile_enable": (_i32, [_vp, _i32]),
     "dmc_profile_reset": (_i32, [_vp]),
     "dmc_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),
@@ -104,6 +108,8 @@ def lib():
                 "`python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in EXPORTS.items():
+            if os.environ.get("DMC_LIB") and not hasattr(L, name):
+                continue  # (an A/B variant built before this entry point existed)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -316,6 +322,11 @@ class GpuQueue:
     def set_option(self, option, value):
         _check(self.L.dmc_queue_set_option(self.h, option, int(value)),
                "set_option")
+
+    def pipelined_error(self, clear=True):
+        """DMC_OPT_PIPELINE: the error of the last pipelined call that a
+        later call found failed (0: none) -- what a DMC_ENOTRUN stands for"""
+        return self.L.dmc_queue_pipelined_error(self.h, int(clear))
 
     def counters(self, reset=False):
         """engine path counters (rounds, radix rounds, overflows, largest

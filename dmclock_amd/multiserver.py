@@ -21,7 +21,7 @@ import ctypes
 
 import numpy as np
 
-from .gpu import GpuQueue, _check, lib
+from .gpu import PROF_NSTAGES, GpuQueue, _check, lib
 
 U32_NONE = -1  # 0xffffffff as int32
 
@@ -265,6 +265,23 @@ class GpuGroup:
 
     def stream(self):
         return self.L.dmc_group_stream(self.h)
+
+    def profile(self, on=True):
+        """group stage timers on (reset) / off: profiled steps run eagerly,
+        each multi-table kernel timed by its own dispatch"""
+        _check(self.L.dmc_group_profile_enable(self.h, int(on)), "group_profile_enable")
+
+    def profile_read(self):
+        """{stage name: (launches, total ms)} over every kernel of the
+        group's profiled steps (dmc_profile_stage_name's names)"""
+        out = {}
+        for st in range(PROF_NSTAGES):
+            c, ms = ctypes.c_uint64(0), ctypes.c_double(0.0)
+            _check(self.L.dmc_group_profile_read(self.h, st, ctypes.byref(c),
+                                                 ctypes.byref(ms)), "group_profile_read")
+            if c.value:
+                out[self.L.dmc_profile_stage_name(st).decode()] = (c.value, ms.value)
+        return out
 
     def close(self):
         if self.h:

@@ -44,9 +44,10 @@ extern "C" {
 #define DMC_EQUEUEFULL (-1004) /* the client's request ring is full (documented deviation: the
                                   reference's per-client std::deque is unbounded, :360) */
 #define DMC_ENOTREG (-1005)    /* slot not registered */
-#define DMC_ENOTRUN (-1006)    /* DMC_OPT_PIPELINE: the previous call on the queue failed (its error is
-                                  reported now) and this call was not executed: none of its adds or
-                                  pulls took effect and its outputs were not written */
+#define DMC_ENOTRUN (-1006)    /* DMC_OPT_PIPELINE: the previous call on the queue failed and this
+                                  call was not executed: none of its adds or pulls took effect and
+                                  its outputs were not written; the previous call's own error is
+                                  dmc_queue_pipelined_error()'s */
 
 /* ------------------------------------------------------------ ABI version
  * Bumped at every incompatible change of this header (option ids, struct
@@ -57,7 +58,9 @@ extern "C" {
  *      retired and returns DMC_EINVAL); DMC_ENOTRUN; dmc_counters gained
  *      act_batches / act_seq_batches (round 4) and renamed pred_* to
  *      bad_rounds / serve_yields. */
-#define DMC_ABI_VERSION 5
+/*   6: dmc_queue_pipelined_error (the error a DMC_ENOTRUN stands for);
+ *      dmc_group_profile_enable / dmc_group_profile_read. */
+#define DMC_ABI_VERSION 6
 int dmc_abi_version(void);
 
 /* ------------------------------------------------------------ enums */
@@ -292,6 +295,14 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                           int32_t* const* d_rc, const double* now, uint32_t k,
                           dmc_decision* const* d_out, dmc_pull_result* const* d_result,
                           const dmc_group_tracker* trk);
+/* Group stage timers (an extension, like dmc_profile_*): while on, fused
+ * group steps launch their multi-table kernels eagerly (no graph), each
+ * timed by its own dispatch; dmc_group_profile_read returns, per
+ * DMC_PROF_* stage (ADD_LINK, ADD_CHAIN, SCAN, SELECT = hist + pick, EMIT,
+ * RANK, APPLY), the launches and their total milliseconds since the last
+ * enable (which also resets them). */
+int dmc_group_profile_enable(dmc_group* g, int on);
+int dmc_group_profile_read(dmc_group* g, uint32_t stage, uint64_t* count, double* total_ms);
 
 /* ------------------------------------------------------------ maintenance */
 
@@ -429,6 +440,14 @@ int dmc_tracker_advance(dmc_queue* q, uint32_t n_clients, uint32_t* d_gdelta,
                                   (growth of its batch, decision, radix and activation buffers)
                                   fail; the call returns DMC_ENOMEM, the queue stays usable */
 int dmc_queue_set_option(dmc_queue* q, int option, int64_t value);
+
+/* DMC_OPT_PIPELINE: the status of the last pipelined call that failed when a
+ * later call finished it -- the error that later call reported as
+ * DMC_ENOTRUN (or returned itself) -- 0 if none; clear != 0 resets it.  A
+ * failure whose call's successor had already run (the device failed: the
+ * queue's state is unknown) also marks the queue failed: every later call
+ * returns DMC_EDEVICE. */
+int dmc_queue_pipelined_error(dmc_queue* q, int clear);
 
 /* Engine path counters since creation (or the last reset): which ranking
  * path the batched pull rounds took and how often a round was re-run.  No

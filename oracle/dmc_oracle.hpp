@@ -28,6 +28,9 @@
 #include <cassert>
 #include <cerrno>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <cstdint>
 #include <deque>
 #include <functional>
@@ -350,6 +353,111 @@ class Queue {
 
   bool track_ties = true;
 
+  // ---- the idle reset's minimum (:937-985), exactly, in O(log N)
+  // The reference scans every client for the lowest (front or prev)
+  // proportion + prop_delta of the non-idle ones: an O(N) pass per
+  // activation, which makes a 1M-client churn trace take hours here.  ActMin
+  // keeps the same minimum in a segment tree over client ids (the
+  // client_map_ order): a leaf holds a client's value iff it is non-idle and
+  // not NaN (the scan's `p < lowest` never takes NaN); a node keeps its left
+  // child unless the right one is strictly smaller -- the first client in map
+  // order among the minimal ones, which is exactly the value the scan ends
+  // with (strict `<` keeps the first of values that compare equal, +0.0 and
+  // -0.0 included).  Every mutation of a client's requests, prev tag,
+  // prop_delta or idle flag refreshes its leaf (am_touch).  Client ids above
+  // kActMinMaxId fall back to the scan.  DMO_ACTMIN_CHECK=1 (tests) runs both
+  // and aborts on any difference.
+  static constexpr uint32_t kActMinMaxId = 1u << 24;
+  struct ActMin {
+    uint32_t cap = 0;              // leaves (a power of two)
+    std::vector<double> val;       // 2 cap nodes
+    std::vector<uint8_t> ok;       // a value is present
+    bool disabled = false;         // an id >= kActMinMaxId was seen
+    void grow(uint32_t id) {
+      uint32_t nc = cap ? cap : 1024;
+      while (nc <= id) nc <<= 1;
+      std::vector<double> v2(2 * (size_t)nc, 0.0);
+      std::vector<uint8_t> o2(2 * (size_t)nc, 0);
+      for (uint32_t i = 0; i < cap; ++i) {
+        v2[nc + i] = val[cap + i];
+        o2[nc + i] = ok[cap + i];
+      }
+      cap = nc;
+      val.swap(v2);
+      ok.swap(o2);
+      for (uint32_t n = cap; n-- > 1;) pull(n);
+    }
+    void pull(uint32_t n) {
+      const uint32_t a = 2 * n, b = a + 1;
+      if (ok[a] && (!ok[b] || !(val[b] < val[a]))) {
+        val[n] = val[a];
+        ok[n] = 1;
+      } else {
+        val[n] = val[b];
+        ok[n] = ok[b];
+      }
+    }
+    void set(uint32_t id, bool present, double v) {
+      if (disabled) return;
+      if (id >= kActMinMaxId) {
+        disabled = true;
+        return;
+      }
+      if (id >= cap) {
+        if (!present) return;
+        grow(id);
+      }
+      uint32_t n = cap + id;
+      val[n] = v;
+      ok[n] = present ? 1 : 0;
+      for (n >>= 1; n >= 1; n >>= 1) pull(n);
+    }
+    bool min(double* out) const {  // false: no value present
+      if (!cap || !ok[1]) return false;
+      *out = val[1];
+      return true;
+    }
+  };
+  ActMin am_;
+  bool am_check_ = getenv("DMO_ACTMIN_CHECK") && atoi(getenv("DMO_ACTMIN_CHECK"));
+
+  void am_touch(const ClientRec& c) {
+    const double p = c.has_request() ? c.front().proportion + c.prop_delta
+                                     : c.prev.proportion + c.prop_delta;
+    am_.set(c.client, !c.idle && p == p, p);
+  }
+  void am_forget(uint32_t client) { am_.set(client, false, 0.0); }
+  // the reference's lowest: DBL_MAX, or the smallest value below it
+  double am_lowest() {
+    double lowest = std::numeric_limits<double>::max();
+    double m;
+    const bool tree = !am_.disabled;
+    if (tree && am_.min(&m) && m < lowest) lowest = m;
+    if (!tree || am_check_) {
+      double l2 = std::numeric_limits<double>::max();
+      for (auto const& kv : client_map_) {
+        const ClientRec& o = *kv.second;
+        if (o.idle) continue;
+        double p = o.has_request() ? o.front().proportion + o.prop_delta
+                                   : o.prev.proportion + o.prop_delta;
+        if (p < l2) l2 = p;
+      }
+      if (tree && std::memcmp(&l2, &lowest, sizeof l2) != 0) {
+        std::fprintf(stderr, "dmc_oracle: ActMin %.17g != scan %.17g\n", lowest, l2);
+        std::abort();
+      }
+      lowest = l2;
+    }
+    return lowest;
+  }
+  // refreshes a client's leaf when it goes out of scope (every return path
+  // of a mutating call)
+  struct AmTouch {
+    Queue* q;
+    const ClientRec* c;
+    ~AmTouch() { q->am_touch(*c); }
+  };
+
   // ---- public API mirrors
   size_t client_count() const { return resv_.size(); }  // :551-554
   size_t request_count() const {                         // :557-564
@@ -388,6 +496,7 @@ class Queue {
     resv_.push(rec);
     limit_.push(rec);
     ready_.push(rec);
+    am_touch(*rec);
     ins.first->second = std::move(rec);
     return kOk;
   }
@@ -411,17 +520,12 @@ class Queue {
       ins.first->second = std::move(rec);
     }
     ClientRec& c = *ins.first->second;
+    AmTouch am_guard{this, &c};
 
     if (c.idle) {  // :937-985
       constexpr double trigger = std::numeric_limits<double>::max() / 3.0;
-      double lowest = std::numeric_limits<double>::max();
-      for (auto const& kv : client_map_) {
-        const ClientRec& o = *kv.second;
-        if (o.idle) continue;
-        double p = o.has_request() ? o.front().proportion + o.prop_delta
-                                   : o.prev.proportion + o.prop_delta;
-        if (p < lowest) lowest = p;
-      }
+      // (the lowest over the non-idle clients: am_lowest, the scan's value)
+      const double lowest = am_lowest();
       if (lowest < trigger) c.prop_delta = lowest - time;
       c.idle = false;
     }
@@ -535,6 +639,7 @@ class Queue {
         resv_.adjust(c);
         limit_.adjust(c);
         ready_.adjust(c);
+        am_touch(c);
         any = true;
       }
     }
@@ -556,6 +661,7 @@ class Queue {
     resv_.adjust(c);
     limit_.adjust(c);
     ready_.adjust(c);
+    am_touch(c);
   }
 
   void update_client_info(uint32_t client) {  // :633-640
@@ -576,10 +682,12 @@ class Queue {
         if (erase_point && erased < erase_max &&
             i2->second->last_tick <= erase_point) {
           delete_from_heaps(*i2->second);
+          am_forget(i2->first);
           client_map_.erase(i2);
           ++erased;
         } else if (idle_point && i2->second->last_tick <= idle_point) {
           i2->second->idle = true;
+          am_touch(*i2->second);
         }
       }
     }
@@ -587,12 +695,16 @@ class Queue {
   }
   void mark_idle(uint32_t client) {
     auto it = client_map_.find(client);
-    if (it != client_map_.end()) it->second->idle = true;
+    if (it != client_map_.end()) {
+      it->second->idle = true;
+      am_touch(*it->second);
+    }
   }
   bool erase_client(uint32_t client) {
     auto it = client_map_.find(client);
     if (it == client_map_.end()) return false;
     delete_from_heaps(*it->second);
+    am_forget(it->first);
     client_map_.erase(it);
     return true;
   }
@@ -676,6 +788,7 @@ class Queue {
     resv_.demote(top);
     limit_.adjust(top);
     ready_.demote(top);
+    am_touch(top);
     res->type = NextType::returning;
     res->client = top.client;
     res->handle = req.handle;

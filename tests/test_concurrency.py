@@ -156,10 +156,11 @@ def _rank(rank, world, port, sh, outdir, out_q):
         res = d_res.cpu().numpy()
         for j, s in enumerate(mine):
             out = {"settle": d_set[j].cpu().numpy(), "res": res[j]}
+            # (requests: only the delta / rho the trackers filled in)
             for ci, d in enumerate(d_pre[j]):
-                out[f"pre{ci}"] = d.cpu().numpy()
+                out[f"pre{ci}"] = _dr(d.cpu().numpy().view(REQUEST_DTYPE))
             for i in range(n_steps):
-                out[f"req{i}"] = d_steps[j][i].cpu().numpy()
+                out[f"req{i}"] = _dr(d_steps[j][i].cpu().numpy().view(REQUEST_DTYPE))
                 out[f"dec{i}"] = d_out[j][i].cpu().numpy()
             for f in ("xd", "xr", "known"):
                 out[f] = st[f][j]
@@ -182,6 +183,11 @@ def _rank(rank, world, port, sh, outdir, out_q):
             dist.destroy_process_group()
 
 
+def _dr(reqs):
+    """a batch's delta and rho columns"""
+    return np.stack([reqs["delta"], reqs["rho"]])
+
+
 def oracle_run(sh):
     """all servers on oracle queues + the epoch restatement, the same call
     sequence per server (threads: ctypes releases the GIL in the oracle)"""
@@ -196,7 +202,7 @@ def oracle_run(sh):
         for ci, c in enumerate(srv[s][0]):
             c = c.copy()
             et.fill(s, c)
-            want[s][f"pre{ci}"] = c
+            want[s][f"pre{ci}"] = _dr(c)
             assert (qo[s].add_batch(c) == 0).all()
         d, res = qo[s].pull_batch(srv[s][1], sh["settle"])
         want[s]["settle"] = (d, res)
@@ -206,7 +212,7 @@ def oracle_run(sh):
         for i in range(i0, i1):
             b = srv[s][2][i].copy()
             et.fill(s, b)
-            want[s][f"req{i}"] = b
+            want[s][f"req{i}"] = _dr(b)
             assert (qo[s].add_batch(b) == 0).all()
             d, res = qo[s].pull_batch(float(b["time"][-1]), k)
             want[s][f"dec{i}"] = (d, res)
@@ -235,9 +241,8 @@ def _check(sh, outdir, want, et):
         w = want[s]
         for key in [kk for kk in w if kk.startswith("pre")] + \
                 [f"req{i}" for i in range(n_steps)]:
-            got = g[key].view(REQUEST_DTYPE)
-            assert np.array_equal(got["delta"], w[key]["delta"]), (s, key)
-            assert np.array_equal(got["rho"], w[key]["rho"]), (s, key)
+            assert np.array_equal(g[key][0], w[key][0]), (s, key, "delta")
+            assert np.array_equal(g[key][1], w[key][1]), (s, key, "rho")
         res = g["res"]
         for key, row, buf in [("settle", n_steps, g["settle"])] + \
                 [(f"dec{i}", i, g[f"dec{i}"]) for i in range(n_steps)]:
@@ -280,7 +285,7 @@ def _spawn(world, sh, outdir):
     msgs = {}
     try:
         for _ in procs:
-            rank, msg = out_q.get(timeout=240)
+            rank, msg = out_q.get(timeout=sh.get("wait", 240))
             msgs[rank] = msg
     finally:
         for p in procs:
@@ -306,6 +311,30 @@ def test_concurrent_queues_trackers_parity(world):
         assert ties == 0, f"{ties} tied decisions: pick another seed"
         n = _check(sh, outdir, want, et)
     assert n > sh["S_total"] * sh["settle"]
+
+
+@pytest.mark.timeout(900)
+def test_group_bench_shape_vs_oracle():
+    """BASELINE config 5's per-GPU shape at its full size against the oracle
+    (VERDICT r5, next item 3): eight server tables of 2,097,152 client slots
+    in one queue group (bench.py --config 5), depth 4 (8M queued requests per
+    table), a 2M-pull settle per table, then two steps of 64K adds + 64K
+    pulls per table with the device trackers' fill and tally inside the
+    group step and an epoch delivery after each.  The tables hold different
+    subsets of 4,194,304 global clients (each server's 2M drawn at random:
+    clients shared across servers, G < S * N), so delta/rho carry other
+    servers' responses (dmclock_client.h:59-79).  Every request's delta/rho,
+    every decision (tag bits included), result record and tracker word of
+    all eight tables bit-exact against eight oracle queues (run on eight host
+    threads) and the epoch restatement (simulate.h:118-136)."""
+    sh = dict(SHAPE, S_total=8, N=1 << 21, G=1 << 22, depth=4, settle=1 << 21, epochs=2,
+              steps=1, batch=1 << 16, seed=21, chunk=1 << 20, group=True, wait=600)
+    with tempfile.TemporaryDirectory() as outdir:
+        _spawn(1, sh, outdir)
+        want, et, ties = oracle_run(sh)
+        assert ties == 0, f"{ties} tied decisions: pick another seed"
+        n = _check(sh, outdir, want, et)
+    assert n > sh["S_total"] * (sh["settle"] + 2 * sh["batch"]) * 0.99
 
 
 @pytest.mark.timeout(480)

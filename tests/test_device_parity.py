@@ -210,6 +210,11 @@ def test_pipelined_failure_next_call_not_run():
     call(0)  # pipelined: its failure is reported by the next call
     with pytest.raises(DmcError, match=rf"\({DMC_ENOTRUN}\)"):
         call(1)
+    # (the error DMC_ENOTRUN stands for -- call 0's failed round
+    # -- stays readable)
+    from dmclock_amd._abi import DMC_EDEVICE
+    assert qg.pipelined_error() == DMC_EDEVICE
+    assert qg.pipelined_error() == 0  # (read and cleared)
     qg.set_option(OPT_FAULT, 0)
     call(2)
     qg.sync()
@@ -427,30 +432,24 @@ def test_config4_churn_throttled_parity_64k(seed, api):
     assert n > 100_000 and res > 1000 and prio > 1000, (n, res, prio)
 
 
-@pytest.mark.timeout(600)
-def test_config4_1m_device_activations_vs_host_split():
-    """BASELINE config 4 at its full size, 1,048,576 clients (VERDICT r2, next
-    item 5): the oracle cannot run it (an O(N) scan per activation, about
-    30,000 per step), so this is a property of the engine -- the device path
-    bench.py --config 4 times (HBM idle lists, fused-API adds whose
-    activations are found and resolved on the device, k_act_resolve's
-    speculated min-plus scan) against the exact host split on a second queue
-    (DMC_OPT_ACT_SPLIT: one k_contrib_min grid minimum + k_activate per
-    activation, in batch order, the reference's :937-985 one at a time).
-    Four steps; every add status, decision and result record, and 4096
-    sampled client states (prop_delta included) bit-exact."""
-    import torch
-    from dmclock_amd._abi import OPT_ACT_SPLIT
-    from dmclock_amd.gpu import GpuQueue
+@pytest.mark.timeout(900)
+def test_config4_1m_device_activations_vs_oracle():
+    """BASELINE config 4 at its full size, 1,048,576 clients, against the
+    oracle: the device path bench.py --config 4
+    times -- HBM idle lists, fused-API adds whose activations are found and
+    resolved on the device (the speculated min-plus scan of section 3.1) --
+    replayed beside the reference's queue restated on the CPU.  The oracle's
+    idle reset (dmclock_server.h:937-985) keeps the reference's minimum over
+    the non-idle clients exactly in a segment tree instead of the reference's
+    O(N) scan per activation (oracle/dmc_oracle.hpp ActMin, pinned bit for
+    bit against the scan by tests/test_oracle_actmin.py), which brings the 1M
+    replay from hours to about a minute.  Four steps of 65,536 adds + 65,536
+    pulls, 10 % of the clients marked idle before each: every add status,
+    decision (slot, phase, cost, handle, tag bits) and result record, and
+    4096 sampled client states (prop_delta included) bit-exact; the trace is
+    tie-free under the oracle."""
     tr = workloads.config4_trace(3, 1 << 20, 4, 1 << 16)
-    qa = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 22)
-    qb = GpuQueue(max_clients=1 << 20, ring_capacity=64, max_batch=1 << 22)
-    qb.set_option(OPT_ACT_SPLIT, 1)
-    outs_a = replay_device(qa, tr, fuse=True)
-    # the host split's reference run: host lists, host-API adds split at
-    # every activation
-    outs_b = workloads.replay(qb, tr)
-    n_dec = acts = 0
+    acts = 0
     idle = np.zeros(1 << 20, bool)
     for op in tr.ops:
         if op[0] == "idle":
@@ -459,22 +458,13 @@ def test_config4_1m_device_activations_vs_host_split():
             u = np.unique(op[1]["slot"])
             acts += int(idle[u].sum())
             idle[u] = False
-    for i, (a, b) in enumerate(zip(outs_a, outs_b)):
-        assert a[0] == b[0], i
-        if a[0] == "add":
-            assert np.array_equal(a[1], b[1]), i
-        elif a[0] == "pull":
-            compare_decisions(a[1], b[1], f"op {i}")
-            assert a[2] == b[2], (i, a[2], b[2])
-            n_dec += len(a[1])
-    rng = np.random.default_rng(5)
-    compare_states(qa, qb, rng.choice(tr.clients.slots, 4096, replace=False), "final")
-    assert qa.request_count() == qb.request_count()
     assert acts > 10_000, acts
+    n_dec, qg, qo = device_parity(tr)
     assert n_dec > 4 * 60_000, n_dec
-    qa.close()
-    qb.close()
-    torch.cuda.synchronize()
+    c = qg.counters()
+    assert c["act_batches"] >= 4, c
+    qg.close()
+    qo.close()
 
 
 def test_reject_activations_device_api():

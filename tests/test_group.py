@@ -10,7 +10,8 @@ tests/test_concurrency.py::test_group_queues_trackers_parity_8; here:
   * the bench's own shape, 8 tables of 2,097,152 slots (bench.py --config 5):
     the grouped run and a run of eight separate queues on the same workload
     produce byte-identical decisions, result records, add statuses and
-    tracker state (a property: the oracle would take hours at this size);
+    tracker state (the same shape against eight oracle queues and the epoch
+    restatement: tests/test_concurrency.py::test_group_bench_shape_vs_oracle);
   * a group whose steps cannot be fused (k below the round size, idle
     clients waiting for activation) falls back to per-member calls with the
     same results.
@@ -46,7 +47,7 @@ def _workload(S, N, depth, n_steps, batch, seed):
     return out
 
 
-def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4):
+def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=()):
     """one pass over the workload; returns digests of every output"""
     import torch
     from dmclock_amd.multiserver import DeviceTrackers, GpuGroup, make_queues
@@ -54,6 +55,9 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4):
     S = len(wl)
     chunk = 1 << 20
     qs = make_queues(S, N, device=0, ring_capacity=64, max_batch=chunk)
+    for q in qs:
+        for opt, val in options:
+            q.set_option(opt, val)
     trk = DeviceTrackers(qs, N, dev, n_clients=S * N,
                          client_of_slot=np.stack([w[1] for w in wl]))
     group = GpuGroup(qs) if grouped else None
@@ -84,6 +88,8 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4):
             done += kk
             j += 1
     trk.deliver()
+    for q in qs:
+        q.counters(reset=True)  # (the steps' own)
     d_steps = [[torch.from_numpy(b.view(np.uint8)).to(dev) for b in w[3]] for w in wl]
     torch.cuda.synchronize()
     gtrk = trk.group_trackers()
@@ -123,7 +129,9 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4):
            "trk": hashlib.sha256(b"".join(st[f].tobytes() for f in
                                           ("gd", "gr", "xd", "xr", "known"))).hexdigest(),
            "fused": [c["fused_calls"] for c in ctr],
-           "decisions": [c["decisions"] for c in ctr]}
+           "decisions": [c["decisions"] for c in ctr],
+           "retries": [c["sample_retries"] for c in ctr],
+           "rounds": [c["rounds"] for c in ctr]}
     if group is not None:
         group.close()
     for q in qs:
@@ -161,3 +169,37 @@ def test_group_fallback_steps_match():
         b = _drive(wl, N, k, grouped=False, settle=N, idle_every=2, epoch=3)
         assert a["digest"] == b["digest"], k
         assert a["trk"] == b["trk"], k
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["rerun", "terminal"])
+def test_group_tallies_rerun_and_terminal_rounds(mode):
+    """a group step's tallies are split -- the fused round's
+    decisions tallied where k_rrank_m / k_rapply_m write them, the decisions
+    of rounds the host drives afterwards by k_tally_m.  Pin that split on the
+    two paths the clean steps never take, against separate queues (whose
+    tallies are dmc_tracker_tally's pass over each call's decisions):
+      rerun: sampled thresholds with no margin (DMC_OPT_SAMPLE = 2) -- fused
+        rounds fail their exact count, nothing of them is applied or tallied,
+        and the host re-runs them exactly;
+      terminal: k far above the eligible requests -- every step's round runs
+        out of work and the host's terminal pull follows it.
+    Decisions, result records, statuses and every tracker word identical."""
+    from dmclock_amd._abi import OPT_SAMPLE
+    S, N = 3, 1 << 16  # (sampled thresholds: tables of >= 65,536 slots)
+    if mode == "rerun":
+        wl = _workload(S, N, 2, 6, 1 << 12, seed=13)
+        k, settle, opts = 1 << 12, N, ((OPT_SAMPLE, 2),)
+    else:
+        wl = _workload(S, N, 1, 6, 1 << 11, seed=14)
+        k, settle, opts = 1 << 15, N, ()
+    a = _drive(wl, N, k, grouped=True, settle=settle, epoch=2, options=opts)
+    b = _drive(wl, N, k, grouped=False, settle=settle, epoch=2, options=opts)
+    assert a["fused"] == [6] * S, a["fused"]
+    if mode == "rerun":
+        assert min(a["retries"]) > 0, a["retries"]
+    else:
+        assert all(d < 6 * k for d in a["decisions"]), a["decisions"]
+    assert a["digest"] == b["digest"]
+    assert a["trk"] == b["trk"]
+    assert a["decisions"] == b["decisions"]
