@@ -2246,34 +2246,51 @@ __device__ inline void rank_rec(Round* rd, const BKeyS* sh, const BRecR* src, ui
     // (okeys only; reads past f1 stay inside sh -- f1 <= cnt <= kRankSortMin,
     // sh holds kBinCapR -- and are masked)
     // whole batches of U unmasked (every load of a batch issued before its
-    // compares), then one masked batch
-    constexpr uint32_t U = 8;
-    uint32_t f = f0;
-    for (; f + U <= f1; f += U) {
-      uint64_t cur[U];
+    // compares), then one masked batch.  A P bin whose records have runs
+    // reads the whole 16-byte keys (the run is in lo) in batches of 4,
+    // other bins the okeys in batches of 8 (no LDS read inside a compare)
+    auto batches = [&](auto cu, auto wide) {
+      constexpr uint32_t U = decltype(cu)::value;
+      constexpr bool W = decltype(wide)::value;
+      uint32_t f = f0;
+      for (; f + U <= f1; f += U) {
+        uint64_t ck[U];
+        uint32_t cr[U];
 #pragma unroll
-      for (uint32_t j = 0; j < U; ++j) cur[j] = sh[f + j].okey;
+        for (uint32_t j = 0; j < U; ++j) {
+          if (W) {
+            const BKeyS b = sh[f + j];
+            ck[j] = b.okey;
+            cr[j] = (uint32_t)b.lo & 0xffffu;
+          } else {
+            ck[j] = sh[f + j].okey;
+            cr[j] = 0;
+          }
+        }
 #pragma unroll
-      for (uint32_t j = 0; j < U; ++j) {
-        const bool l = cur[j] < me.okey;
-        lt += l ? 1u : 0u;
-        eq += cur[j] == me.okey ? 1u : 0u;
-        if (ISP && anyrun) rs += l ? ((uint32_t)sh[f + j].lo & 0xffffu) : 0u;
+        for (uint32_t j = 0; j < U; ++j) {
+          const bool l = ck[j] < me.okey;
+          lt += l ? 1u : 0u;
+          eq += ck[j] == me.okey ? 1u : 0u;
+          if (W) rs += l ? cr[j] : 0u;
+        }
       }
-    }
-    if (f < f1) {
-      uint64_t cur[U];
+      if (f < f1) {
 #pragma unroll
-      for (uint32_t j = 0; j < U; ++j) cur[j] = sh[f + j].okey;
-#pragma unroll
-      for (uint32_t j = 0; j < U; ++j) {
-        const bool in = f + j < f1;
-        const bool l = in && cur[j] < me.okey;
-        lt += l ? 1u : 0u;
-        eq += (in && cur[j] == me.okey) ? 1u : 0u;
-        if (ISP && anyrun) rs += l ? ((uint32_t)sh[f + j].lo & 0xffffu) : 0u;
+        for (uint32_t j = 0; j < U; ++j) {
+          const BKeyS b = sh[f + j];
+          const bool in = f + j < f1;
+          const bool l = in && b.okey < me.okey;
+          lt += l ? 1u : 0u;
+          eq += (in && b.okey == me.okey) ? 1u : 0u;
+          if (W) rs += l ? ((uint32_t)b.lo & 0xffffu) : 0u;
+        }
       }
-    }
+    };
+    if (ISP && anyrun)
+      batches(std::integral_constant<uint32_t, 4>{}, std::true_type{});
+    else
+      batches(std::integral_constant<uint32_t, 8>{}, std::false_type{});
   }
   for (uint32_t d = 1; d < parts; d <<= 1) {
     lt += __shfl_xor(lt, d);
