@@ -370,6 +370,35 @@ __global__ void __launch_bounds__(kBlock) k_add_chain_m(const AddArgs* a) {
   add_chain_body(x.tb, x.pblk, x.abuf, x.apos, x.aslot, ActBuf{}, x.tf.reqs ? &x.tf : nullptr);
 }
 
+// Queue groups, DMC_GROUP_OVERLAP: the add chain and the round's scan as
+// two launches that run at the same time (the two branches of the step's
+// graph: one kernel each, so that each keeps its own occupancy -- one
+// merged launch held the scan side to the chain's 162 VGPRs, r05).  As in
+// k_chain_scan, the filing stamps the batch's slots with the call's epoch,
+// the scan (k_rscan_mt) leaves them, and each client's first filer scans
+// its slot once its adds are in (k_chain_scan_m); partials: the scan's
+// nscan blocks', then the chain's.
+__global__ void __launch_bounds__(kBlock) k_chain_scan_m(const AddArgs* a, const RScanArgs* sa,
+                                                         uint32_t nscan) {
+  const AddArgs& x = a[blockIdx.y];
+  const RScanArgs& r = sa[blockIdx.y];
+  chain_scan_chain(x.tb, x.p, x.abuf, x.apos, x.aslot, x.tf.reqs ? &x.tf : nullptr, r.cp.now,
+                   r.keyr, r.keyp, r.meta, r.skr, r.skp, r.k32, r.parts + nscan + blockIdx.x,
+                   blockIdx.x);
+}
+// (nblk: the scan's blocks of slots; a grid of fewer blocks strides over
+// them, leaving CUs to the chain launched beside it, DMC_GROUP_SCAN_BLOCKS)
+__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_mt(const RScanArgs* a,
+                                                                        uint32_t nblk) {
+  const RScanArgs& x = a[blockIdx.y];
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    rscan_body_g<false, kScanBlock, true, kScanSlots>(x.tb, x.keyr, x.keyp, x.meta, x.parts,
+                                                      x.rd, x.cp, x.skr, x.skp, x.k32, x.hist,
+                                                      b, nblk);
+    __syncthreads();  // (the body's LDS partials, reused by the next block)
+  }
+}
+
 // The end of an idle reset (:981-984): the client's new prop_delta, its
 // front's cached proportion key recomputed with it, idle cleared.
 __device__ inline void activate_slot(const Table& tb, uint32_t s, double pd) {
@@ -2196,6 +2225,10 @@ struct dmc_group {
   std::vector<dmc_queue*> qs;
   int device = 0;
   hipStream_t stream = nullptr, cap_stream = nullptr;
+  // DMC_GROUP_OVERLAP: the scan's branch (eager steps, captures) and the
+  // events that fork it from and join it to the step
+  hipStream_t stream2 = nullptr, cap_stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // per-step kernel arguments: pinned staging and its device copy (one
   // memcpy per step, the graph's first node), S entries per kernel
   uint8_t* h_blob = nullptr;
@@ -3400,6 +3433,12 @@ void launch_apply(dmc_queue* q) {
 constexpr uint32_t kFixPartsMax = 4096;  // (batches of up to 2^20 requests)
 #ifndef DMC_DEFER_APPLY
 #define DMC_DEFER_APPLY 1
+#endif
+#ifndef DMC_GROUP_OVERLAP
+#define DMC_GROUP_OVERLAP 0  // (1: a queue group's add chain beside its scan, two graph branches)
+#endif
+#ifndef DMC_GROUP_SCAN_BLOCKS
+#define DMC_GROUP_SCAN_BLOCKS 0  // (overlap: the scan's grid per table; 0: one block per 1,024 slots)
 #endif
 #ifndef DMC_OVERLAP
 #define DMC_OVERLAP 1  // (0: the add kernels then k_rscan, for A/B)
@@ -5122,6 +5161,9 @@ int dmc_group_create(dmc_queue* const* queues, uint32_t n, dmc_group** out) {
   g->o_tally = take(sizeof(TallyArgs));
   g->tally_bytes = o - g->o_tally;
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&g->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&g->h_blob, o, 0) != hipSuccess ||
       hipMalloc((void**)&g->d_blob, o) != hipSuccess) {
     dmc_group_destroy(g);
@@ -5162,6 +5204,10 @@ int dmc_group_destroy(dmc_group* g) {
   dfree(g->d_blob);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   if (g->cap_stream) (void)hipStreamDestroy(g->cap_stream);
+  if (g->stream2) (void)hipStreamDestroy(g->stream2);
+  if (g->cap_stream2) (void)hipStreamDestroy(g->cap_stream2);
+  if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
+  if (g->ev_join) (void)hipEventDestroy(g->ev_join);
   delete g;
   return DMC_OK;
 }
@@ -5226,6 +5272,20 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       bool all_sampled = true;
       uint32_t gN = 0, gEm = 0;
       const uint32_t gAdd = (n + kBlock - 1) / kBlock;
+      // DMC_GROUP_OVERLAP: the chain and the scan side by side, the batch's
+      // slots stamped with each member's epoch (k_chain_scan's scheme; a
+      // wrapped epoch clears its table's stamps first)
+      const bool ovl = DMC_GROUP_OVERLAP && gAdd <= kFixPartsMax;
+      if (ovl) {
+        for (dmc_queue* q : g->qs) {
+          if (++q->epoch == 256u) {
+            hipLaunchKernelGGL(k_clear_stamps, dim3((q->tb.n + kBlock - 1) / kBlock),
+                               dim3(kBlock), 0, g->stream, q->tb);
+            HIP_OK(hipGetLastError());
+            q->epoch = 1;
+          }
+        }
+      }
       // (the add chain and the scan one after the other: k_chain_scan over
       // all tables measured slower, config 5 1.04 vs 0.93 ms, r04o)
       for (uint32_t i = 0; i < S; ++i) {
@@ -5240,15 +5300,16 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
                                 trk[i].gdelta, trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                 trk[i].first}
                     : TrackArgs{};
-        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, 0}, tb, q->abuf, q->apos,
+        const uint32_t epoch = ovl ? q->epoch : 0u;
+        aa[i] = AddArgs{AddParams{d_reqs[i], d_rc[i], q->tick, n, epoch}, tb, q->abuf, q->apos,
                         q->aslot, q->apblk,
                         trk ? TrackFill{d_reqs[i], trk[i].client_of_slot, trk[i].gdelta,
                                         trk[i].grho, trk[i].xd, trk[i].xr, trk[i].known,
                                         q->p.max_clients}
                             : TrackFill{}};
         const CallParams cp{k, 0, now[i], d_out[i], q->tick + n,
-                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, 0};
-        const uint32_t np = gN;  // (the scan's partials)
+                            d_result ? d_result[i] : nullptr, ++q->round_seq, q->fault, epoch};
+        const uint32_t np = ovl ? gN + gAdd : gN;  // (the scan's partials, then the chain's)
         sa[i] = RScanArgs{tb, sampled ? nullptr : q->keyr, sampled ? nullptr : q->keyp, q->meta,
                           q->rparts, q->rd, cp, sampled ? q->skr : nullptr,
                           sampled ? q->skp : nullptr, q->k32, q->hist};
@@ -5274,9 +5335,9 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
       // its start from the first and its end from the second)
       hipEvent_t ev_open = nullptr;
       auto gl = [&](hipStream_t st, int stage, int part, auto kernel, dim3 gr, dim3 bl,
-                    auto arg) {
-        if (!g->prof_on || st != g->stream || stage < 0) {
-          hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg);
+                    auto... arg) {
+        if (!g->prof_on || (st != g->stream && st != g->stream2) || stage < 0) {
+          hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg...);
           return;
         }
         if (part == 0 || part == 2) {  // (a new record: 0 one kernel, 2 first of two)
@@ -5285,7 +5346,7 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
             if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
                 hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
               g->prof_on = false;
-              hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg);
+              hipLaunchKernelGGL(kernel, gr, bl, 0, st, arg...);
               return;
             }
             g->prof_pool.push_back(r);
@@ -5294,13 +5355,13 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         }
         dmc_group::PRec& r = g->prof_pool[g->prof_n];
         if (part == 0) {
-          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, r.b, 0, arg);
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, r.b, 0, arg...);
           ++g->prof_n;
         } else if (part == 2) {
-          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, nullptr, 0, arg);
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, r.a, nullptr, 0, arg...);
           ev_open = r.b;
         } else {  // part 3: the second of two
-          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, nullptr, ev_open, 0, arg);
+          hipExtLaunchKernelGGL(kernel, gr, bl, 0, st, nullptr, ev_open, 0, arg...);
           ++g->prof_n;
         }
       };
@@ -5309,10 +5370,24 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
         // (the trackers' get_req_params run inside k_add_chain_m: TrackFill)
         gl(st, DMC_PROF_ADD_LINK, 0, k_add_link_m, dim3(gAdd, S), dim3(kBlock),
            (const AddArgs*)(d + g->o_add));
-        gl(st, DMC_PROF_ADD_CHAIN, 0, k_add_chain_m, dim3(gAdd, S), dim3(kBlock),
-           (const AddArgs*)(d + g->o_add));
-        gl(st, DMC_PROF_SCAN, 0, k_rscan_m, dim3(gN, S), dim3(kScanBlock),
-           (const RScanArgs*)(d + g->o_scan));
+        if (ovl) {
+          // two branches: the chain on st, the scan on the second stream
+          hipStream_t st2 = st == g->stream ? g->stream2 : g->cap_stream2;
+          (void)hipEventRecord(g->ev_fork, st);
+          (void)hipStreamWaitEvent(st2, g->ev_fork, 0);
+          gl(st, DMC_PROF_ADD_CHAIN, 0, k_chain_scan_m, dim3(gAdd, S), dim3(kBlock),
+             (const AddArgs*)(d + g->o_add), (const RScanArgs*)(d + g->o_scan), gN);
+          const uint32_t gS = DMC_GROUP_SCAN_BLOCKS ? std::min<uint32_t>(gN, DMC_GROUP_SCAN_BLOCKS) : gN;
+          gl(st2, DMC_PROF_SCAN, 0, k_rscan_mt, dim3(gS, S), dim3(kScanBlock),
+             (const RScanArgs*)(d + g->o_scan), gN);
+          (void)hipEventRecord(g->ev_join, st2);
+          (void)hipStreamWaitEvent(st, g->ev_join, 0);
+        } else {
+          gl(st, DMC_PROF_ADD_CHAIN, 0, k_add_chain_m, dim3(gAdd, S), dim3(kBlock),
+             (const AddArgs*)(d + g->o_add));
+          gl(st, DMC_PROF_SCAN, 0, k_rscan_m, dim3(gN, S), dim3(kScanBlock),
+             (const RScanArgs*)(d + g->o_scan));
+        }
         gl(st, DMC_PROF_SELECT, kPrePickM ? 2 : 0, k_rhist_m, dim3(gHist, S), dim3(1024),
            (const RHistArgs*)(d + g->o_hist));
         if (kPrePickM)
@@ -5352,6 +5427,8 @@ int dmc_group_step_device(dmc_group* g, uint32_t n, dmc_request* const* d_reqs,
           x = dmc_group::G{};
           if (!g->cap_stream)
             HIP_OK(hipStreamCreateWithFlags(&g->cap_stream, hipStreamNonBlocking));
+          if (!g->cap_stream2)
+            HIP_OK(hipStreamCreateWithFlags(&g->cap_stream2, hipStreamNonBlocking));
           HIP_OK(hipStreamBeginCapture(g->cap_stream, hipStreamCaptureModeThreadLocal));
           enqueue(g->cap_stream);
           HIP_OK(hipStreamEndCapture(g->cap_stream, &x.graph));
