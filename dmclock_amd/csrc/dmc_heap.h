@@ -720,6 +720,24 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
   heap_cache_flush(hd, cache, T);
 }
 
+// (debug, DMC_HEAP_CLOCKS: where a pull's time goes -- shader-clock cycles
+// per phase accumulated by the pulling wave, printed once per k_heap_pull)
+#ifndef DMC_HEAP_CLOCKS
+#define DMC_HEAP_CLOCKS 0
+#endif
+struct HClk {
+  uint64_t t[10] = {};  // decide, limit sifts, pop loads, pop stores, resv, lim, ready, promote, limit iters, pulls
+  uint64_t last = 0;
+  __device__ void start() { if (DMC_HEAP_CLOCKS) last = __builtin_amdgcn_s_memtime(); }
+  __device__ void lap(int i) {
+    if (DMC_HEAP_CLOCKS) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      t[i] += now - last;
+      last = now;
+    }
+  }
+};
+
 // The pop of slot s, the top of heap `hsel` (pop_process_request,
 // :1046-1073, with reduce_reservation_tags, :1077-1111, for a priority pop):
 // the decision, the front popped and (delayed) the new front's tag
@@ -730,7 +748,8 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
 // every queued request: one lane each), in two levels of loads; lane 0
 // stores what is uniform.
 __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
-                                uint64_t tick, dmc_decision* out, unsigned long long* sched) {
+                                uint64_t tick, dmc_decision* out, unsigned long long* sched,
+                                HClk* ck = nullptr) {
   const uint32_t lane = W.lane;
   // level 1: the slot's heap indices (lanes 0-2), cursor, record, aux, bound info
   const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
@@ -761,6 +780,12 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
   double er = 0.0;  // lane i: queue position i's r (immediate priority pop, i >= 2)
   const bool deep = prio && !tb.delayed && lane >= 2 && lane < c;
   if (deep) er = ring[(h + lane) & tb.qmask].r;
+  if (DMC_HEAP_CLOCKS && ck) {
+    keep(popped.r);
+    keep(fr);
+    keep(er);
+    ck->lap(2);
+  }
   if (lane == 0) {
     dmc_decision d;
     d.handle = popped.handle;
@@ -834,15 +859,23 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
   uint32_t ix[3];
   _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
   const uint32_t n = W.count();
+  if (DMC_HEAP_CLOCKS && ck) {
+    keep(o.r);
+    ck->lap(3);
+  }
   // pop_process_request's heap calls, on the unreduced front (:1063-1069)
   ScanRec o0 = o;
   o0.r = r_pre;
   ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
+  if (DMC_HEAP_CLOCKS && ck) ck->lap(4);
   ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o0, s));
+  if (DMC_HEAP_CLOCKS && ck) ck->lap(5);
   ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o0, s));
+  if (DMC_HEAP_CLOCKS && ck) ck->lap(6);
   if (prio)  // resv_heap.promote after the reduction (:1110)
     W.h[kHResv].sift_up(ix[kHResv], hent(kHResv, o, s));
   wave_sync();
+  if (DMC_HEAP_CLOCKS && ck) ck->lap(7);
 }
 
 struct HeapPullRes {
@@ -877,6 +910,8 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
     return;
   }
   const uint32_t n = W.count();
+  HClk ck;
+  ck.start();
   // each iteration decides one pull (pop_slot / pop_prio) or stops; the pop
   // is made at its end (mode 1: recorded for mode 2 instead)
   while (r.n < k) {
@@ -899,9 +934,12 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
         wave_sync();
         HEnt X[3];
         uint32_t ix[3];
+        ck.lap(0);
         W.load3(ls, X, ix);
         W.h[kHReady].sift_up(ix[kHReady], X[kHReady]);
         W.h[kHLim].sift_down(0, n, X[kHLim]);
+        ck.lap(1);
+        if (DMC_HEAP_CLOCKS) ++ck.t[8];
       }
       const HEnt pt = W.top(kHReady);
       const bool ph = pt.cls != kClsNone && hval(pt) < kInf;
@@ -942,11 +980,18 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
       r.pend_prio = pop_prio ? 1u : 0u;
       break;
     }
-    heap_pop(tb, W, pop_slot, pop_prio, tick, out + r.n, sched);
+    ck.lap(0);
+    heap_pop(tb, W, pop_slot, pop_prio, tick, out + r.n, sched, &ck);
     ++r.n;
     if (pop_prio) ++r.n_prio;
     else ++r.n_res;
   }
+  if (DMC_HEAP_CLOCKS && lane == 0 && r.n > 1000)
+    printf("heap clocks: pulls %u prio %u limit iters %llu | cycles per pull: decide %.0f limit-sifts %.0f "
+           "pop-loads %.0f pop-stores %.0f resv %.0f lim %.0f ready %.0f promote %.0f\n",
+           r.n, r.n_prio, (unsigned long long)ck.t[8], (double)ck.t[0] / r.n, (double)ck.t[1] / r.n,
+           (double)ck.t[2] / r.n, (double)ck.t[3] / r.n, (double)ck.t[4] / r.n, (double)ck.t[5] / r.n,
+           (double)ck.t[6] / r.n, (double)ck.t[7] / r.n);
   heap_cache_flush(hd, cache, T);
   if (lane) return;
   *res = r;
