@@ -158,6 +158,80 @@ __device__ inline void st_as(void* p, const T& v) {
   __builtin_memcpy(__builtin_assume_aligned(p, alignof(T)), &v, sizeof(T));
 }
 
+// The same, through an explicit address space: ld_lds (p in LDS: ds_read)
+// and ld_glb (p in device memory: global_load).  Where one value comes from
+// either an LDS stage or memory, one generic pointer compiles to a flat
+// access, which counts against both of the wave's memory counters (a wait
+// for an LDS read then also waits for it) and which the compiler orders
+// behind pending flat stores.  The words are may_alias (any type, as
+// ld_as's byte copy).
+typedef uint32_t __attribute__((may_alias, address_space(3))) lds_w32;
+typedef unsigned long long __attribute__((may_alias, address_space(3))) lds_w64;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 __attribute__((may_alias, address_space(3))) lds_w128;
+typedef uint32_t __attribute__((may_alias, address_space(1))) glb_w32;
+typedef unsigned long long __attribute__((may_alias, address_space(1))) glb_w64;
+typedef u32x4 __attribute__((may_alias, address_space(1))) glb_w128;
+template <typename T, typename W128, typename W64, typename W32>
+__device__ __forceinline__ T ld_words(const void* p) {
+  T v;
+  if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+    u32x4 t[sizeof(T) / 16];
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 16); ++k) t[k] = ((const W128*)p)[k];
+    __builtin_memcpy(&v, t, sizeof(T));
+  } else if constexpr (sizeof(T) % 8 == 0 && alignof(T) >= 8) {
+    unsigned long long t[sizeof(T) / 8];
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 8); ++k) t[k] = ((const W64*)p)[k];
+    __builtin_memcpy(&v, t, sizeof(T));
+  } else {
+    static_assert(sizeof(T) % 4 == 0 && alignof(T) >= 4, "whole 4-byte words");
+    uint32_t t[sizeof(T) / 4];
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) t[k] = ((const W32*)p)[k];
+    __builtin_memcpy(&v, t, sizeof(T));
+  }
+  return v;
+}
+template <typename T, typename W128, typename W64, typename W32, size_t A = alignof(T)>
+__device__ __forceinline__ void st_words(void* p, const T& v) {
+  if constexpr (sizeof(T) % 16 == 0 && A >= 16) {
+    u32x4 t[sizeof(T) / 16];
+    __builtin_memcpy(t, &v, sizeof(T));
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 16); ++k) ((W128*)p)[k] = t[k];
+  } else if constexpr (sizeof(T) % 8 == 0 && A >= 8) {
+    unsigned long long t[sizeof(T) / 8];
+    __builtin_memcpy(t, &v, sizeof(T));
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 8); ++k) ((W64*)p)[k] = t[k];
+  } else {
+    static_assert(sizeof(T) % 4 == 0 && alignof(T) >= 4, "whole 4-byte words");
+    uint32_t t[sizeof(T) / 4];
+    __builtin_memcpy(t, &v, sizeof(T));
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) ((W32*)p)[k] = t[k];
+  }
+}
+template <typename T, size_t A = alignof(T)>
+__device__ __forceinline__ void st_lds(void* p, const T& v) {
+  st_words<T, lds_w128, lds_w64, lds_w32, A>(p, v);
+}
+// (A: the alignment p has, when more than T's)
+template <typename T, size_t A = alignof(T)>
+__device__ __forceinline__ void st_glb(void* p, const T& v) {
+  st_words<T, glb_w128, glb_w64, glb_w32, A>(p, v);
+}
+template <typename T>
+__device__ __forceinline__ T ld_lds(const void* p) {
+  return ld_words<T, lds_w128, lds_w64, lds_w32>(p);
+}
+template <typename T>
+__device__ __forceinline__ T ld_glb(const void* p) {
+  return ld_words<T, glb_w128, glb_w64, glb_w32>(p);
+}
+
 // The ScanRec cursor word -- head | count << 8 | flags << 16 | stamp << 24 |
 // nadd << 32 -- read and written whole (8-aligned at offset 24).
 __device__ inline uint64_t cursor_load(const ScanRec* r) {
@@ -278,25 +352,26 @@ __device__ inline CView load_view(const Table& tb, uint32_t s) {
 // decision stores serialise).
 struct RingView {
   const ReqEntry* g;   // the client's ring
-  const ReqEntry* st;  // staged positions [0, ns)
+  const ReqEntry* st;  // staged positions [0, ns) (LDS)
   uint32_t h, qmask, ns;
+  // (each side through its own address space: ld_lds / ld_glb)
   __device__ ReqEntry at(uint32_t i) const {
-    if (i < ns) return st[i];
-    return g[(h + i) & qmask];
+    if (i < ns) return ld_lds<ReqEntry>(st + i);
+    return ld_glb<ReqEntry>(g + ((h + i) & qmask));
   }
   __device__ double r_at(uint32_t i) const {
-    if (i < ns) return st[i].r;
-    return g[(h + i) & qmask].r;
+    if (i < ns) return ld_lds<double>(&st[i].r);
+    return ld_glb<double>(&g[(h + i) & qmask].r);
   }
   // reduce_reservation_tags' offset of position i (:1090-1091)
   __device__ double offset_at(uint32_t i, double rinv) const {
     uint32_t cost, rho;
     if (i < ns) {
-      cost = st[i].cost;
-      rho = st[i].rho;
+      cost = ld_lds<uint32_t>(&st[i].cost);
+      rho = ld_lds<uint32_t>(&st[i].rho);
     } else {
-      cost = g[(h + i) & qmask].cost;
-      rho = g[(h + i) & qmask].rho;
+      cost = ld_glb<uint32_t>(&g[(h + i) & qmask].cost);
+      rho = ld_glb<uint32_t>(&g[(h + i) & qmask].rho);
     }
     return resv_offset(rinv, cost, rho);
   }

@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) k_chain_scan_m(const AddArgs* a, const
 }
 // (nblk: the scan's blocks of slots; a grid of fewer blocks strides over
 // them, leaving CUs to the chain launched beside it, DMC_GROUP_SCAN_BLOCKS)
-__global__ void __launch_bounds__(kScanBlock, DMC_SCAN_MINW) k_rscan_mt(const RScanArgs* a,
+__global__ void __launch_bounds__(kScanBlock) k_rscan_mt(const RScanArgs* a,
                                                                         uint32_t nblk) {
   const RScanArgs& x = a[blockIdx.y];
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -1563,7 +1563,7 @@ __device__ inline double min_not_0(double cur, double possible) {  // :1192-1195
 // at the memory side, visible to a last block after its acquire with no
 // release fence: an agent-scope release writes back the whole L2)
 template <int THREADS = kBlock, bool ATOMIC = false>
-__device__ inline void step_scan_body(const Table& tb, double now, StepRed* part) {
+__device__ __forceinline__ void step_scan_body(const Table& tb, double now, StepRed* part) {
   ArgMin r{kMaxKey, kNone, 0}, p{kMaxKey, kNone, 0}, pnr{kMaxKey, kNone, 0};
   uint64_t lnr = kMaxKey, lrd = kMaxKey;
   uint32_t nany = 0, nrd = 0, nnr = 0;
@@ -1725,7 +1725,7 @@ __device__ inline StepCtl step_decision(const StepRed& o, double now, int at_lim
 // partials (tree reduction in LDS), then thread 0 decides (hsc: an optional
 // host-mapped mirror of the decision)
 template <int THREADS = kBlock>
-__device__ void step_decide(uint32_t nparts, const StepRed* part, double now,
+__device__ __forceinline__ void step_decide(uint32_t nparts, const StepRed* part, double now,
                             int at_limit, uint32_t nregistered,
                             StepCtl* sc, Round* ctl, StepCtl* hsc = nullptr) {
   if (ctl && (ctl->overflow || !ctl->terminal)) return;
@@ -4029,7 +4029,7 @@ int heap_add(dmc_queue* q, uint32_t n, const dmc_request* d_reqs, int32_t* d_rc)
   rc = maybe_idle(q) ? add_act_batch_dev(q, n, d_reqs, d_rc)
                      : add_segment(q, d_reqs, n, d_rc, q->tick);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_heap_events, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, d_reqs,
+  hipLaunchKernelGGL(k_heap_events, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, d_reqs,
                      (const uint8_t*)q->d_hev, n);
   HIP_OK(hipGetLastError());
   q->tick += n;
@@ -4046,7 +4046,7 @@ int heap_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     acc.next_type = DMC_NEXT_RETURNING;
     uint32_t n = 0;
     while (n < k) {
-      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, 1u,
+      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, now, 1u,
                          q->p.at_limit, q->tick, d_out + n, q->d_hres,
                          (dmc_pull_result*)nullptr, q->sched, 1);
       HIP_OK(hipGetLastError());
@@ -4061,7 +4061,7 @@ int heap_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
       }
       const uint32_t s = h.pend_slot;
       if (int rc = fetch_infos(q, 1, &s, sizeof(uint32_t), false)) return rc;
-      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, 1u,
+      hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, now, 1u,
                          q->p.at_limit, q->tick, d_out + n, q->d_hres,
                          (dmc_pull_result*)nullptr, q->sched, 2);
       HIP_OK(hipGetLastError());
@@ -4079,7 +4079,7 @@ int heap_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (r) *r = acc;
     return DMC_OK;
   }
-  hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64), 0, q->stream, q->tb, q->hd, now, k,
+  hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, now, k,
                      q->p.at_limit, q->tick, d_out, q->d_hres, d_result, q->sched, 0);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(q->h_hres, q->d_hres, sizeof(HeapPullRes), hipMemcpyDeviceToHost,

@@ -76,6 +76,12 @@ constexpr uint32_t kClsNone = 3;
 #endif
 constexpr uint32_t kHeapLds = DMC_HEAP_LDS;
 
+// (debug, DMC_HEAP_CLOCKS: shader-clock cycles per phase, printed by
+// k_heap_pull)
+#ifndef DMC_HEAP_CLOCKS
+#define DMC_HEAP_CLOCKS 0
+#endif
+
 struct HeapDev {
   HEnt* ent;      // [3][n] heap arrays
   uint32_t* hix;  // [3][n] each slot's index in each heap
@@ -150,13 +156,18 @@ struct WHeap {
   HEnt* c;        // the LDS copy of a[0, T): the heap's top levels (heap_cache_fill)
   uint32_t T;
 
+  // LDS and memory each through its own address space: ds_read / ds_write
+  // and global_load / global_store.  (Through one generic pointer the two
+  // merge into flat accesses, and a flat load may alias a pending flat
+  // store in either memory: every round would wait for the previous round's
+  // stores to complete before issuing its loads.)
   __device__ __forceinline__ HEnt ld(uint32_t i) const {
-    if (i < T) return c[i];
-    return a[i];
+    if (i < T) return ld_lds<HEnt>(c + i);
+    return ld_glb<HEnt>(a + i);
   }
   __device__ __forceinline__ void st(uint32_t i, const HEnt& e) const {
-    if (i < T) c[i] = e;
-    else a[i] = e;
+    if (i < T) st_lds(c + i, e);
+    else st_glb(a + i, e);
   }
   __device__ __forceinline__ void put(uint32_t i, const HEnt& e) const {  // (uniform: lane 0 stores)
     if (lane == 0) {
@@ -316,9 +327,12 @@ struct WHeap {
   // ---- K = 2 (the reference's default): a fixed subtree layout -- lane j <
   // 62 holds node (level L = log2(j + 2), offset j + 2 - 2^L) of the five
   // levels below the root, whose index is ((r + 1) << L) - 1 + offset; lane
-  // j's children are lanes 2j + 2 and 2j + 3, so each lane picks its
-  // smaller child itself (IndIntruHeap's K == 2 rule: the right one only if
-  // strictly less, :514-548) and the path is then four lane reads.
+  // j's children are lanes 2j + 2 and 2j + 3.  Each lane j < 30 loads its
+  // two children as well as its node, and lane 62 the root's two children
+  // (lanes 0 and 1): every lane picks its smaller child (IndIntruHeap's K ==
+  // 2 rule: the right one only if strictly less, :514-548) and whether it
+  // moves up past X, and the path is walked on the two ballots in scalar
+  // registers.
   __device__ __forceinline__ uint32_t k2_lv() const {
     return lane < 62 ? 31u - __builtin_clz(lane + 2) : 0u;
   }
@@ -329,61 +343,93 @@ struct WHeap {
     const uint64_t i = (((uint64_t)r + 1) << L) - 1 + (lane + 2 - (1u << L));
     return i < n ? (uint32_t)i : 0xffffffffu;
   }
-  // the path of X down the loaded subtree below r: the moved lanes store
-  // themselves at their parents; returns true when X passed the subtree's
-  // last level (*r is then the node to continue from), else X's node in *r
-  __device__ __forceinline__ bool k2_down(const HEnt& e, uint32_t idx, uint32_t n, const HEnt& X,
-                                          uint32_t* r) const {
-    // each lane's chosen child and whether it is less than X (lanes < 30)
-    HEnt lc, rc;
-    const int l2 = (int)(2 * lane + 2) & 63, r2 = (int)(2 * lane + 3) & 63;
-    lc.key = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e.key >> 32), l2) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)e.key, l2);
-    lc.cls = (uint32_t)__shfl((int)e.cls, l2);
-    rc.key = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e.key >> 32), r2) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)e.key, r2);
-    rc.cls = (uint32_t)__shfl((int)e.cls, r2);
-    const uint64_t li = 2ull * idx + 1;
-    const bool hasl = idx != 0xffffffffu && li < n, hasr = hasl && li + 1 < n;
-    const bool pickr = hasr && hlt(rc, lc);
-    const uint32_t code = ((hasl && hlt(pickr ? rc : lc, X)) ? 2u : 0u) | (pickr ? 1u : 0u);
-    // the root's own choice (lanes 0 and 1 are its children)
-    const uint64_t rl = 2ull * *r + 1;
-    if (rl >= n) return false;  // (X stays at r)
-    const HEnt c0 = hread(e, 0);
-    bool p1 = false;
-    if (rl + 1 < n) p1 = hlt(hread(e, 1), c0);
-    const HEnt ch = p1 ? hread(e, 1) : c0;
-    if (!hlt(ch, X)) return false;
-    uint32_t c = p1 ? 1u : 0u;
-    uint64_t moved = 1ull << c;
+  // one round's loads below root r: the lane's node and the children it
+  // compares (one round trip: three loads per lane)
+  struct K2Sub {
+    HEnt e, lc, rc;
+    uint32_t idx;
+    bool hasl, hasr;
+  };
+  __device__ __forceinline__ K2Sub k2_load(uint32_t r, uint32_t n) const {
+    K2Sub s;
+    s.e = s.lc = s.rc = HEnt{~0ull, kClsNone + 1, 0};
+    s.idx = k2_idx(r, n);
+    // the node whose children this lane compares (lanes < 30: its own; 62: r)
+    const bool own = lane < 30 && s.idx != 0xffffffffu;
+    const uint64_t li = 2ull * (own ? s.idx : r) + 1;
+    s.hasl = (own || lane == 62) && li < n;
+    s.hasr = s.hasl && li + 1 < n;
+    if (s.idx != 0xffffffffu) s.e = ld(s.idx);
+    if (s.hasl) s.lc = ld((uint32_t)li);
+    if (s.hasr) s.rc = ld((uint32_t)li + 1);
+    return s;
+  }
+  // the path of X down the loaded subtree below r (*moved: its lanes,
+  // which move up one level); returns true when X passed the subtree's last
+  // level (*r is then the node to continue from), else X's node in *r
+  __device__ __forceinline__ bool k2_path(const K2Sub& s, const HEnt& X, uint32_t* r,
+                                          uint64_t* moved) const {
+    const bool pickr = s.hasr && hlt(s.rc, s.lc);
+    const bool mv = s.hasl && hlt(pickr ? s.rc : s.lc, X);
+    const uint64_t M = __ballot(mv), P = __ballot(pickr);
+    *moved = 0;
+    if (!((M >> 62) & 1ull)) return false;  // (X stays at r)
+    uint32_t c = (uint32_t)((P >> 62) & 1ull);
+    uint64_t m = 1ull << c;
     bool cont = true;
     for (int L = 1; L < 5; ++L) {
-      const uint32_t cc = uread(code, c);
-      if (!(cc & 2u)) {
+      if (!((M >> c) & 1ull)) {
         cont = false;
         break;
       }
-      c = 2 * c + 2 + (cc & 1u);
-      moved |= 1ull << c;
+      c = 2 * c + 2 + (uint32_t)((P >> c) & 1ull);
+      m |= 1ull << c;
     }
-    if ((moved >> lane) & 1ull) {
-      const uint32_t pi = (idx - 1) >> 1;
-      st(pi, e);
-      x[e.slot] = pi;
-    }
-    *r = uread(idx, c);
+    *moved = m;
+    *r = uread(s.idx, c);
     return cont;
   }
-  __device__ __forceinline__ uint32_t k2_sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
-    while (i < n) {
-      const uint32_t idx = k2_idx(i, n);
-      HEnt e{~0ull, kClsNone + 1, 0};
-      if (idx != 0xffffffffu) e = ld(idx);
-      if (!k2_down(e, idx, n, X, &i)) break;
+  // the moved lanes' entries one level up
+  __device__ __forceinline__ void k2_move(const K2Sub& s, uint64_t moved) const {
+    if ((moved >> lane) & 1ull) {
+      const uint32_t pi = (s.idx - 1) >> 1;
+      st(pi, s.e);
+      x[s.e.slot] = pi;
+    }
+  }
+  // sift_down of X from i, whose first subtree is loaded (a).  Software
+  // pipelined: a round's path decided, the next round's loads are issued
+  // before the round's moves are stored, into the other of two buffers --
+  // a load into registers that a pending store still reads would first
+  // wait for that store, and a load wait waits for the stores issued before
+  // it (one memory counter for both): so each round costs one round trip,
+  // the stores' and the loads' overlapped.
+  __device__ __forceinline__ uint32_t k2_sift_down_from(K2Sub a, uint32_t i, uint32_t n,
+                                                        const HEnt& X) const {
+    K2Sub b;
+    uint64_t mv;
+    for (;;) {
+      uint32_t ni = i;
+      const bool ca = k2_path(a, X, &ni, &mv);
+      if (ca) b = k2_load(ni, n);
+      k2_move(a, mv);
+      i = ni;
+      if (!ca) break;
+      const bool cb = k2_path(b, X, &ni, &mv);
+      if (cb) a = k2_load(ni, n);
+      k2_move(b, mv);
+      i = ni;
+      if (!cb) break;
     }
     put(i, X);
     return i;
+  }
+  __device__ __forceinline__ uint32_t k2_sift_down(uint32_t i, uint32_t n, const HEnt& X) const {
+    if (i >= n) {
+      put(i, X);
+      return i;
+    }
+    return k2_sift_down_from(k2_load(i, n), i, n, X);
   }
   // ancestors of i: lane t < d holds ancestor t + 1, ((i + 1) >> (t + 1)) - 1
   __device__ __forceinline__ uint32_t k2_ancestors(uint32_t i, uint32_t* anc) const {
@@ -395,15 +441,16 @@ struct WHeap {
     if (i == 0) return k2_sift_down(i, n, X);
     uint32_t anc;
     const uint32_t d = k2_ancestors(i, &anc);
-    // the ancestors and the first subtree in one round trip (two loads per lane)
-    HEnt ae{~0ull, kClsNone + 1, 0}, e{~0ull, kClsNone + 1, 0};
-    const uint32_t idx = i < n ? k2_idx(i, n) : 0xffffffffu;
+    // the ancestors and the first subtree in one round trip
+    HEnt ae{~0ull, kClsNone + 1, 0};
     if (lane < d) ae = ld(anc);
-    if (idx != 0xffffffffu) e = ld(idx);
+    const K2Sub sub = k2_load(i, n);  // (nothing when i >= n)
     if (hlt(X, hread(ae, 0))) return up_anc(i, X, d, anc, ae);
-    if (i < n && k2_down(e, idx, n, X, &i)) return k2_sift_down(i, n, X);
-    put(i, X);
-    return i;
+    if (i >= n) {
+      put(i, X);
+      return i;
+    }
+    return k2_sift_down_from(sub, i, n, X);
   }
 
   // sift (:550-564): up if less than the parent, else down.  The ancestors
@@ -427,21 +474,43 @@ struct WHeap {
   }
 };
 
+// Waves of the pull and event kernels: 3 = one wave per heap (the three
+// heaps' sifts of a pop, a limit-loop step or an add event run side by side;
+// the pull kernel's waves meet at a block barrier after each), 1 = one wave
+// makes all three in turn.
+#ifndef DMC_HEAP_WAVES
+#define DMC_HEAP_WAVES 3
+#endif
+constexpr uint32_t kHeapWaves = DMC_HEAP_WAVES;
+static_assert(kHeapWaves == 1 || kHeapWaves == 3, "DMC_HEAP_WAVES: 1 or 3");
+
 struct WHeaps {
   const Table& tb;
   const HeapDev& hd;
   WHeap h[3];
   uint32_t lane;
+  uint32_t wid;  // split: this wave's heap
+  bool split;    // one wave per heap (else this wave owns all three)
+  bool lead;     // makes the uniform stores (the limit heap's wave, or the only wave)
   // (cache: the LDS copy of each heap's first T entries, kHeapLds apart)
-  __device__ WHeaps(const Table& t, const HeapDev& d, HEnt* cache, uint32_t T)
+  __device__ WHeaps(const Table& t, const HeapDev& d, HEnt* cache, uint32_t T, bool split_ = false)
       : tb(t), hd(d) {
     lane = lane_id();
+    split = split_;
+    wid = split ? threadIdx.x >> 6 : 0u;
+    lead = !split || wid == (uint32_t)kHLim;  // (the limit heap's sifts are the shortest)
     _Pragma("unroll") for (int j = 0; j < 3; ++j)
       h[j] = WHeap{d.ent + (size_t)j * d.n, d.hix + (size_t)j * d.n, d.k, lane,
                    cache + j * kHeapLds, T};
   }
-  __device__ uint32_t count() const { return hd.cnt[0]; }
-  __device__ HEnt top(int j) const { return h[j].ld(0); }
+  __device__ __forceinline__ bool owns(int j) const { return !split || (uint32_t)j == wid; }
+  // the heaps' state (LDS tops, global records) the same for every wave after it
+  __device__ __forceinline__ void sync() const {
+    if (split) __syncthreads();
+    else wave_sync();
+  }
+  __device__ __forceinline__ uint32_t count() const { return hd.cnt[0]; }
+  __device__ __forceinline__ HEnt top(int j) const { return h[j].ld(0); }
   // slot s's index in each heap (lanes 0-2 load; uniform)
   __device__ __forceinline__ void index3(uint32_t s, uint32_t* ix) const {
     uint32_t v = 0;
@@ -455,10 +524,11 @@ struct WHeaps {
     index3(s, ix);
     _Pragma("unroll") for (int j = 0; j < 3; ++j) X[j] = hent(j, r, s);
   }
-  // adjust x 3 (:996-1016, :567-625): sift in each heap, in heap order
+  // adjust x 3 (:996-1016, :567-625): sift in each heap (this wave's), in
+  // heap order
   __device__ __forceinline__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
     const uint32_t n = count();
-    _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = h[j].sift(ix[j], n, X[j]);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) if (owns(j)) ix[j] = h[j].sift(ix[j], n, X[j]);
   }
   __device__ __forceinline__ void adjust3(uint32_t s) const {
     HEnt X[3];
@@ -472,7 +542,7 @@ struct WHeaps {
     HEnt X[3];
     uint32_t ix[3];
     load3(s, X, ix);
-    _Pragma("unroll") for (int j = 0; j < 3; ++j) h[j].put(ix[j], X[j]);
+    _Pragma("unroll") for (int j = 0; j < 3; ++j) if (owns(j)) h[j].put(ix[j], X[j]);
   }
   // erase (delete_from_heaps): IndIntruHeap::remove (:433-445) -- the last
   // element swapped in and sifted with the count already reduced
@@ -559,11 +629,16 @@ __global__ void __launch_bounds__(64) k_heap_adjust(Table tb, HeapDev hd, const 
 // batch, which is its state at each of its events: a client's front changes
 // only at its first accepted request of the batch, its prop_delta only at
 // its activation, before any of its adjusts.  64 events are read at once.
-__global__ void __launch_bounds__(64) k_heap_events(Table tb, HeapDev hd, const dmc_request* reqs,
-                                                    const uint8_t* ev, uint32_t n) {
+//
+// With one wave per heap (kHeapWaves = 3) each wave replays the whole event
+// list on its own heap: the heaps share no state, and a heap's calls are the
+// same calls in the same order whichever wave makes the other heaps'.
+__global__ void __launch_bounds__(64 * kHeapWaves) k_heap_events(Table tb, HeapDev hd,
+                                                                 const dmc_request* reqs,
+                                                                 const uint8_t* ev, uint32_t n) {
   __shared__ HEnt cache[3 * kHeapLds];
   const uint32_t T = heap_cache_fill(hd, cache);
-  WHeaps W(tb, hd, cache, T);
+  WHeaps W(tb, hd, cache, T, kHeapWaves == 3);
   const uint32_t lane = W.lane;
   const uint32_t cnt = W.count();
   for (uint32_t i0 = 0; i0 < n;) {
@@ -575,17 +650,19 @@ __global__ void __launch_bounds__(64) k_heap_events(Table tb, HeapDev hd, const 
       if (e) sl = reqs[i].slot;
     }
     // Which of them must run in order.  A repeat request of a client (code
-    // 2) whose three entries already hold its key, none less than its parent
-    // and none with a child less than it, makes three sifts that move
-    // nothing (K = 2 checked here; other K run every event): the window's
-    // events before the first that may move are skipped -- each of them saw
-    // the heaps as the window found them, unchanged by the ones before.
+    // 2) whose entries (in this wave's heaps) already hold its key, none
+    // less than its parent and none with a child less than it, makes sifts
+    // that move nothing (K = 2 checked here; other K run every event): the
+    // window's events before the first that may move are skipped -- each of
+    // them saw the heaps as the window found them, unchanged by the ones
+    // before.
     bool ord = e == 1 || e == 3 || (e == 2 && hd.k != 2);
     if (e == 2 && hd.k == 2) {
       const ScanRec r = tb.sc[sl];
-      uint32_t hx[3];
-      _Pragma("unroll") for (int j = 0; j < 3; ++j) hx[j] = hd.hix[(size_t)j * hd.n + sl];
+      uint32_t hx[3] = {0, 0, 0};
+      _Pragma("unroll") for (int j = 0; j < 3; ++j) if (W.owns(j)) hx[j] = hd.hix[(size_t)j * hd.n + sl];
       _Pragma("unroll") for (int j = 0; j < 3; ++j) {
+        if (!W.owns(j)) continue;
         const HEnt X = hent(j, r, sl);
         const uint32_t v = hx[j];
         const HEnt own = W.h[j].ld(v);
@@ -722,9 +799,6 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
 
 // (debug, DMC_HEAP_CLOCKS: where a pull's time goes -- shader-clock cycles
 // per phase accumulated by the pulling wave, printed once per k_heap_pull)
-#ifndef DMC_HEAP_CLOCKS
-#define DMC_HEAP_CLOCKS 0
-#endif
 struct HClk {
   uint64_t t[10] = {};  // decide, limit sifts, pop loads, pop stores, resv, lim, ready, promote, limit iters, pulls
   uint64_t last = 0;
@@ -746,11 +820,13 @@ struct HClk {
 // and the popped and next entries (one request each: the values are
 // uniform) and lane i the queue's entry i (an immediate priority pop reduces
 // every queued request: one lane each), in two levels of loads; lane 0
-// stores what is uniform.
+// stores what is uniform.  With one wave per heap every wave computes the
+// same state, the lead wave stores it, and each wave sifts its own heap.
 __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
                                 uint64_t tick, dmc_decision* out, unsigned long long* sched,
                                 HClk* ck = nullptr) {
   const uint32_t lane = W.lane;
+  const bool lead = W.lead;
   // level 1: the slot's heap indices (lanes 0-2), cursor, record, aux, bound info
   const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
   const ScanRec sr = tb.sc[s];
@@ -778,7 +854,7 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     fcost = fe.cost;
   }
   double er = 0.0;  // lane i: queue position i's r (immediate priority pop, i >= 2)
-  const bool deep = prio && !tb.delayed && lane >= 2 && lane < c;
+  const bool deep = lead && prio && !tb.delayed && lane >= 2 && lane < c;
   if (deep) er = ring[(h + lane) & tb.qmask].r;
   if (DMC_HEAP_CLOCKS && ck) {
     keep(popped.r);
@@ -786,7 +862,11 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     keep(er);
     ck->lap(2);
   }
-  if (lane == 0) {
+  if (W.split) {  // every wave's loads done before the lead wave stores
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (lead && lane == 0) {
     dmc_decision d;
     d.handle = popped.handle;
     d.tag_r = popped.r;
@@ -822,7 +902,7 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
       assign_unpinned(cr.prev_l, nt.l);
       assign_unpinned(cr.prev_p, nt.p);
       cr.prev_arr = nt.arrival;
-      if (lane == 0) tb.aux[s].last_tick = tick;
+      if (lead && lane == 0) tb.aux[s].last_tick = tick;
     }
   }
   // the front's keys before the reduction (what the demotes see)
@@ -842,7 +922,7 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     cr.prev_r = __dsub_rn(cr.prev_r, off);
     if (nc) o.r = fr;
   }
-  if (lane == 0) {
+  if (lead && lane == 0) {
     if (nc && (f_tagged || prio)) {
       ReqEntry& fe = ring[nh];
       fe.r = fr;
@@ -866,15 +946,15 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
   // pop_process_request's heap calls, on the unreduced front (:1063-1069)
   ScanRec o0 = o;
   o0.r = r_pre;
-  ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
+  if (W.owns(kHResv)) ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
   if (DMC_HEAP_CLOCKS && ck) ck->lap(4);
-  ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o0, s));
+  if (W.owns(kHLim)) ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o0, s));
   if (DMC_HEAP_CLOCKS && ck) ck->lap(5);
-  ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o0, s));
+  if (W.owns(kHReady)) ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o0, s));
   if (DMC_HEAP_CLOCKS && ck) ck->lap(6);
-  if (prio)  // resv_heap.promote after the reduction (:1110)
+  if (prio && W.owns(kHResv))  // resv_heap.promote after the reduction (:1110)
     W.h[kHResv].sift_up(ix[kHResv], hent(kHResv, o, s));
-  wave_sync();
+  W.sync();
   if (DMC_HEAP_CLOCKS && ck) ck->lap(7);
 }
 
@@ -890,13 +970,19 @@ struct HeapPullRes {
 // fetches the popped client's info between selection and pop, :870-875,
 // :1021-1036): one pull decided -- the limit loop's marks made -- and its
 // pop left in res->pend_*; mode 2: that pop.
-__global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double now, uint32_t k,
-                                                  int at_limit, uint64_t tick, dmc_decision* out,
-                                                  HeapPullRes* res, dmc_pull_result* d_result,
-                                                  unsigned long long* sched, int mode = 0) {
+//
+// With one wave per heap (kHeapWaves = 3) every wave decides each pull from
+// the LDS tops (the same decision), a pop's or limit step's three heap calls
+// run one per wave, and the block barrier after them makes the next decision
+// see all three heaps.
+__global__ void __launch_bounds__(64 * kHeapWaves) k_heap_pull(Table tb, HeapDev hd, double now,
+                                                               uint32_t k, int at_limit, uint64_t tick,
+                                                               dmc_decision* out, HeapPullRes* res,
+                                                               dmc_pull_result* d_result,
+                                                               unsigned long long* sched, int mode = 0) {
   __shared__ HEnt cache[3 * kHeapLds];
   const uint32_t T = heap_cache_fill(hd, cache);
-  WHeaps W(tb, hd, cache, T);
+  WHeaps W(tb, hd, cache, T, kHeapWaves == 3);
   const uint32_t lane = W.lane;
   HeapPullRes r{0, 0, 0, DMC_NEXT_RETURNING, 0.0, 0, 0};
   if (mode == 2) {
@@ -906,7 +992,7 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
     if (pr.pend_prio) r.n_prio = 1;
     else r.n_res = 1;
     heap_cache_flush(hd, cache, T);
-    if (lane == 0) *res = r;
+    if (lane == 0 && W.lead) *res = r;
     return;
   }
   const uint32_t n = W.count();
@@ -929,15 +1015,23 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
         const HEnt lt = W.top(kHLim);
         if (!(lt.cls == 0 && hval(lt) <= now)) break;
         const uint32_t ls = lt.slot;
-        // ready = true (the slot's ready flag: F_READY in its cursor word)
-        if (lane == 0) tb.sc[ls].flags = (uint8_t)(tb.sc[ls].flags | F_READY);
-        wave_sync();
-        HEnt X[3];
-        uint32_t ix[3];
+        // ready = true (the slot's ready flag: F_READY in its cursor word).
+        // The limit entry is the top itself with the ready class (its key
+        // is the record's l already): that sift needs no load.
         ck.lap(0);
-        W.load3(ls, X, ix);
-        W.h[kHReady].sift_up(ix[kHReady], X[kHReady]);
-        W.h[kHLim].sift_down(0, n, X[kHLim]);
+        if (W.owns(kHReady)) {
+          ScanRec lr = tb.sc[ls];
+          const uint32_t ixr = hd.hix[(size_t)kHReady * hd.n + ls];
+          lr.flags = (uint8_t)(lr.flags | F_READY);
+          if (lane == 0) tb.sc[ls].flags = lr.flags;
+          W.h[kHReady].sift_up(ixr, hent(kHReady, lr, ls));
+        }
+        if (W.owns(kHLim)) {
+          HEnt X = lt;
+          X.cls = 1;  // (hent(kHLim, ...) of the record marked ready)
+          W.h[kHLim].sift_down(0, n, X);
+        }
+        W.sync();
         ck.lap(1);
         if (DMC_HEAP_CLOCKS) ++ck.t[8];
       }
@@ -986,14 +1080,14 @@ __global__ void __launch_bounds__(64) k_heap_pull(Table tb, HeapDev hd, double n
     if (pop_prio) ++r.n_prio;
     else ++r.n_res;
   }
-  if (DMC_HEAP_CLOCKS && lane == 0 && r.n > 1000)
+  if (DMC_HEAP_CLOCKS && lane == 0 && r.n > 1000)  // (each wave: its own heap's sifts)
     printf("heap clocks: pulls %u prio %u limit iters %llu | cycles per pull: decide %.0f limit-sifts %.0f "
            "pop-loads %.0f pop-stores %.0f resv %.0f lim %.0f ready %.0f promote %.0f\n",
            r.n, r.n_prio, (unsigned long long)ck.t[8], (double)ck.t[0] / r.n, (double)ck.t[1] / r.n,
            (double)ck.t[2] / r.n, (double)ck.t[3] / r.n, (double)ck.t[4] / r.n, (double)ck.t[5] / r.n,
            (double)ck.t[6] / r.n, (double)ck.t[7] / r.n);
   heap_cache_flush(hd, cache, T);
-  if (lane) return;
+  if (lane || !W.lead) return;
   *res = r;
   if (d_result) {
     dmc_pull_result x{};

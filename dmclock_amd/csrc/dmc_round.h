@@ -2833,7 +2833,7 @@ struct ApplyV {
       first = d;
       first_idx = idx;
     } else {
-      out[idx] = d;
+      st_glb<dmc_decision, 16>(out + idx, d);  // (48-byte records of a 16-aligned buffer)
     }
     last_idx = idx;
     any = true;
@@ -2841,7 +2841,7 @@ struct ApplyV {
   dmc_decision first;
   uint32_t first_idx = 0;
   __device__ void flush() {
-    if (any) out[first_idx] = first;
+    if (any) st_glb<dmc_decision, 16>(out + first_idx, first);
   }
 };
 struct ApplyVR {
