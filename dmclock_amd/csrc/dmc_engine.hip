@@ -4079,8 +4079,12 @@ int heap_pull(dmc_queue* q, double now, uint32_t k, dmc_decision* d_out,
     if (r) *r = acc;
     return DMC_OK;
   }
-  hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, now, k,
-                     q->p.at_limit, q->tick, d_out, q->d_hres, d_result, q->sched, 0);
+  if (DMC_HEAP_ASYNC && q->hd.k == 2)  // (the heap waves decoupled from the decisions)
+    hipLaunchKernelGGL(k_heap_pull_async, dim3(1), dim3(256), 0, q->stream, q->tb, q->hd, now, k,
+                       q->p.at_limit, q->tick, d_out, q->d_hres, d_result, q->sched);
+  else
+    hipLaunchKernelGGL(k_heap_pull, dim3(1), dim3(64 * kHeapWaves), 0, q->stream, q->tb, q->hd, now,
+                       k, q->p.at_limit, q->tick, d_out, q->d_hres, d_result, q->sched, 0);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(q->h_hres, q->d_hres, sizeof(HeapPullRes), hipMemcpyDeviceToHost,
                         q->stream));

@@ -76,6 +76,11 @@ constexpr uint32_t kClsNone = 3;
 #endif
 constexpr uint32_t kHeapLds = DMC_HEAP_LDS;
 
+// (DMC_HEAP_DP: a priority pop's resv demote + promote as one operation,
+// k2_demote_promote; 0: the two sifts in turn)
+#ifndef DMC_HEAP_DP
+#define DMC_HEAP_DP 1
+#endif
 // (debug, DMC_HEAP_CLOCKS: shader-clock cycles per phase, printed by
 // k_heap_pull)
 #ifndef DMC_HEAP_CLOCKS
@@ -301,10 +306,11 @@ struct WHeap {
   // ancestor t + 1, t < d): X passes the leading run of ancestors it is
   // strictly less than, each moving down one node of the path
   __device__ __forceinline__ uint32_t up_anc(uint32_t i, const HEnt& X, uint32_t d, uint32_t anc,
-                             const HEnt& ae) const {
+                             const HEnt& ae, uint32_t* pm = nullptr) const {
     const bool lt = lane < d && hlt(X, ae);
     const uint64_t bal = __ballot(lt);
     const uint32_t m = (uint32_t)__builtin_ctzll(~bal);
+    if (pm) *pm = m;
     uint32_t dst = (uint32_t)__shfl_up((int)anc, 1);  // the path's node below it
     if (lane == 0) dst = i;
     if (lane < m) {
@@ -452,6 +458,190 @@ struct WHeap {
     }
     return k2_sift_down_from(sub, i, n, X);
   }
+  // The moved lanes of one demote round appended to the path registers
+  // (lane k: path node p_k's index and entry before the demote; p_0 = the
+  // start).  A round's moved lanes are one per level, in lane order.
+  __device__ __forceinline__ void k2_rec_path(const K2Sub& s, uint64_t mv, uint32_t* m,
+                                              uint32_t* pI, HEnt* pE) const {
+    while (mv) {
+      const uint32_t c = (uint32_t)__builtin_ctzll(mv);
+      mv &= mv - 1;
+      const uint32_t k = ++*m;
+      const HEnt e = hread(s.e, c);
+      const uint32_t ix = uread(s.idx, c);
+      if (lane == k) {
+        *pE = e;
+        *pI = ix;
+      }
+    }
+  }
+  // resv.demote of the popped client's entry (Xd: its new front, unreduced,
+  // :1063) and then resv.promote of the same entry (Xu: reduced, :1110),
+  // as one operation.  The demote's rounds store nothing and keep the path
+  // in registers; the promote's ancestors are that path (with the values
+  // the demote moved into it) followed by i's ancestors, loaded with the
+  // demote's first subtree -- so the promote needs no round trip -- and
+  // each changed node is stored once, with its value after both calls.
+  // Along the chain N_0 = the demote's end f, N_u = f's ancestor u: after
+  // the demote N_0 holds Xd and N_u (u <= m, m = the levels it moved) the
+  // entry that was at N_{u-1}; the promote passes the first m' of them,
+  // each moving down one node.  So N_u ends with N_{u+1}'s value (u < m'),
+  // Xu (u = m') or its post-demote value (u > m'), and a node is stored
+  // iff that differs from what memory holds: u = m', m' < u <= m, or
+  // m <= u < m' (for u < min(m, m') it is N_u's entry before both).
+  __device__ __forceinline__ uint32_t k2_demote_promote(uint32_t i, uint32_t n, const HEnt& Xd,
+                                                        const HEnt& Xu) const {
+    uint32_t anc;
+    const uint32_t d = k2_ancestors(i, &anc);
+    HEnt ae{~0ull, kClsNone + 1, 0};
+    if (lane < d) ae = ld(anc);
+    uint32_t pI = lane == 0 ? i : 0u, m = 0, f = i;
+    HEnt pE{~0ull, kClsNone + 1, 0};
+    if (i < n) {
+      K2Sub a = k2_load(i, n), b;
+      uint64_t mv;
+      for (;;) {
+        uint32_t ni = f;
+        const bool ca = k2_path(a, Xd, &ni, &mv);
+        if (ca) b = k2_load(ni, n);
+        k2_rec_path(a, mv, &m, &pI, &pE);
+        f = ni;
+        if (!ca) break;
+        const bool cb = k2_path(b, Xd, &ni, &mv);
+        if (cb) a = k2_load(ni, n);
+        k2_rec_path(b, mv, &m, &pI, &pE);
+        f = ni;
+        if (!cb) break;
+      }
+    }
+    // the chain: lane t holds N_{t+1} -- t < m: p_{m-1-t} with p_{m-t}'s
+    // entry; t >= m: i's ancestor t - m + 1 (lane t - m of anc / ae)
+    const uint32_t D = m + d;
+    const bool onp = lane < m;
+    const int s1 = (int)((onp ? m - 1 - lane : 0u) << 2), s2 = (int)((onp ? m - lane : 0u) << 2);
+    const int s3 = (int)((!onp && lane < D ? lane - m : 0u) << 2);
+    auto bp = [](int src, uint32_t v) {
+      return (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v);
+    };
+    auto bpe = [&](int src, const HEnt& e) {
+      HEnt o;
+      o.key = (uint64_t)bp(src, (uint32_t)e.key) | ((uint64_t)bp(src, (uint32_t)(e.key >> 32)) << 32);
+      o.cls = bp(src, e.cls);
+      o.slot = bp(src, e.slot);
+      return o;
+    };
+    const uint32_t pIx = bp(s1, pI), aIx = bp(s3, anc);
+    const HEnt pEx = bpe(s2, pE), aEx = bpe(s3, ae);
+    uint32_t cI = onp ? pIx : aIx;
+    HEnt cV = onp ? pEx : aEx;
+    if (lane >= D) cV = HEnt{~0ull, kClsNone + 1, 0};
+    // the promote: Xu passes the leading run of chain entries it is less than
+    const uint64_t bal = __ballot(lane < D && hlt(Xu, cV));
+    const uint32_t mp = (uint32_t)__builtin_ctzll(~bal);
+    // lane u: node N_u (lane u - 1's chain node; N_0 = f holding Xd)
+    const int su = (int)((lane ? lane - 1 : 0u) << 2);
+    uint32_t nI = bp(su, cI);
+    HEnt nV = bpe(su, cV);
+    if (lane == 0) {
+      nI = f;
+      nV = Xd;
+    }
+    const bool store = lane == mp || (lane > mp && lane <= m) || (lane >= m && lane < mp);
+    const HEnt F = lane < mp ? cV : lane == mp ? Xu : nV;
+    if (store) {
+      st(nI, F);
+      x[F.slot] = nI;
+    }
+    return uread(nI, mp);
+  }
+  // ---- signalled forms (k_heap_pull_async's heap waves): sig() is called
+  // exactly once, as soon as the heap's top (index 0, in LDS) holds its
+  // value after this call; the rest of the sift runs on behind it.
+  // sift_down (:479-548): from i > 0 it cannot change the top
+  template <typename F>
+  __device__ __forceinline__ uint32_t k2_sift_down_sig(uint32_t i, uint32_t n, const HEnt& X,
+                                                       F sig) const {
+    if (i != 0 || i >= n) {
+      sig();
+      return k2_sift_down(i, n, X);
+    }
+    K2Sub a = k2_load(0, n), b;
+    uint32_t ni = 0;
+    uint64_t mv;
+    const bool ca = k2_path(a, X, &ni, &mv);
+    if (ca) b = k2_load(ni, n);
+    k2_move(a, mv);  // (the root's new entry, when X moved)
+    if (!mv) {
+      put(0, X);
+      sig();
+      return 0;
+    }
+    sig();
+    if (!ca) {
+      put(ni, X);
+      return ni;
+    }
+    return k2_sift_down_from(b, ni, n, X);
+  }
+  // sift (:550-564): the top changes only when X climbs to it
+  template <typename F>
+  __device__ __forceinline__ uint32_t k2_sift_sig(uint32_t i, uint32_t n, const HEnt& X, F sig) const {
+    if (i == 0) return k2_sift_down_sig(i, n, X, sig);
+    uint32_t anc;
+    const uint32_t d = k2_ancestors(i, &anc);
+    HEnt ae{~0ull, kClsNone + 1, 0};
+    if (lane < d) ae = ld(anc);
+    const K2Sub sub = k2_load(i, n);
+    if (hlt(X, hread(ae, 0))) {
+      const uint32_t f = up_anc(i, X, d, anc, ae);
+      sig();
+      return f;
+    }
+    sig();
+    if (i >= n) {
+      put(i, X);
+      return i;
+    }
+    return k2_sift_down_from(sub, i, n, X);
+  }
+  // k2_sift, and whether a second sift of the same X right after it
+  // provably moves nothing (*settled; the add path's two adjusts of a
+  // client's first request, :996-1016).  After a sift down (or no move) X's
+  // node has no child less than X (where the walk stopped) and a parent X is
+  // not less than (the entry that moved up past X, or the parent checked
+  // first).  After a sift up to ancestor m its parent stopped the climb, and
+  // its children are the node below it on the path -- now holding the entry
+  // X passed, which X is less than -- and that node's sibling, loaded here
+  // with the ancestors: settled iff the sibling is not less than X.
+  // (Whether the heap is otherwise in order does not matter: only X's own
+  // node and neighbours decide what the second sift does.)
+  __device__ __forceinline__ uint32_t k2_sift_s(uint32_t i, uint32_t n, const HEnt& X,
+                                                bool* settled) const {
+    *settled = true;
+    if (i == 0) return k2_sift_down(i, n, X);
+    uint32_t anc;
+    const uint32_t d = k2_ancestors(i, &anc);
+    HEnt ae{~0ull, kClsNone + 1, 0}, sb = ae;
+    if (lane < d) ae = ld(anc);
+    // lane d + t: the sibling of path node t (i's ancestor t, t = 0: i)
+    if (lane >= d && lane < 2 * d) {
+      const uint32_t a = ((i + 1) >> (lane - d)) - 1;
+      const uint32_t si = (a & 1u) ? a + 1 : a - 1;
+      if (si < n) sb = ld(si);
+    }
+    const K2Sub sub = k2_load(i, n);  // (nothing when i >= n)
+    if (hlt(X, hread(ae, 0))) {
+      uint32_t m;
+      const uint32_t f = up_anc(i, X, d, anc, ae, &m);
+      *settled = !hlt(hread(sb, d + m - 1), X);
+      return f;
+    }
+    if (i >= n) {
+      put(i, X);
+      return i;
+    }
+    return k2_sift_down_from(sub, i, n, X);
+  }
 
   // sift (:550-564): up if less than the parent, else down.  The ancestors
   // and the first subtree below i are loaded together.
@@ -529,6 +719,25 @@ struct WHeaps {
   __device__ __forceinline__ void adjust3(uint32_t s, const HEnt* X, uint32_t* ix) const {
     const uint32_t n = count();
     _Pragma("unroll") for (int j = 0; j < 3; ++j) if (owns(j)) ix[j] = h[j].sift(ix[j], n, X[j]);
+  }
+  // adjust x 3 twice with the same entries (a first request's :996-1006 and
+  // :1011-1016): per heap, the second sift is made only when the first
+  // cannot prove it moves nothing (k2_sift_s; the heaps are independent, so
+  // each heap's two calls may run back to back)
+  template <int J>
+  __device__ __forceinline__ void twice_one(uint32_t n, const HEnt* X, uint32_t* ix) const {
+    if (owns(J)) {
+      bool st = false;
+      if (h[J].k == 2) ix[J] = h[J].k2_sift_s(ix[J], n, X[J], &st);
+      else ix[J] = h[J].sift(ix[J], n, X[J]);
+      if (!st) ix[J] = h[J].sift(ix[J], n, X[J]);
+    }
+  }
+  __device__ __forceinline__ void adjust3_twice(uint32_t s, const HEnt* X, uint32_t* ix) const {
+    const uint32_t n = count();
+    twice_one<0>(n, X, ix);
+    twice_one<1>(n, X, ix);
+    twice_one<2>(n, X, ix);
   }
   __device__ __forceinline__ void adjust3(uint32_t s) const {
     HEnt X[3];
@@ -649,6 +858,14 @@ __global__ void __launch_bounds__(64 * kHeapWaves) k_heap_events(Table tb, HeapD
       e = ev[i];
       if (e) sl = reqs[i].slot;
     }
+    // every event's slot state and indices (the first ordered event's are
+    // taken from here: nothing before it in the window changed them)
+    ScanRec r{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
+    uint32_t hx[3] = {0, 0, 0};
+    if (e) {
+      r = tb.sc[sl];
+      _Pragma("unroll") for (int j = 0; j < 3; ++j) if (W.owns(j)) hx[j] = hd.hix[(size_t)j * hd.n + sl];
+    }
     // Which of them must run in order.  A repeat request of a client (code
     // 2) whose entries (in this wave's heaps) already hold its key, none
     // less than its parent and none with a child less than it, makes sifts
@@ -658,9 +875,6 @@ __global__ void __launch_bounds__(64 * kHeapWaves) k_heap_events(Table tb, HeapD
     // before.
     bool ord = e == 1 || e == 3 || (e == 2 && hd.k != 2);
     if (e == 2 && hd.k == 2) {
-      const ScanRec r = tb.sc[sl];
-      uint32_t hx[3] = {0, 0, 0};
-      _Pragma("unroll") for (int j = 0; j < 3; ++j) if (W.owns(j)) hx[j] = hd.hix[(size_t)j * hd.n + sl];
       _Pragma("unroll") for (int j = 0; j < 3; ++j) {
         if (!W.owns(j)) continue;
         const HEnt X = hent(j, r, sl);
@@ -687,13 +901,25 @@ __global__ void __launch_bounds__(64 * kHeapWaves) k_heap_events(Table tb, HeapD
     }
     const uint32_t j = (uint32_t)__builtin_ctzll(m);
     const uint32_t ej = uread(e, j), s = uread(sl, j);
-    if (ej == 1) {
-      W.refresh3(s);
+    HEnt X[3];
+    uint32_t ix[3];
+    {
+      ScanRec rj{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
+      rj.r = dread(r.r, j);
+      rj.pk = dread(r.pk, j);
+      rj.l = dread(r.l, j);
+      rj.count = (uint8_t)uread(r.count, j);
+      rj.flags = (uint8_t)uread(r.flags, j);
+      _Pragma("unroll") for (int h = 0; h < 3; ++h) {
+        X[h] = hent(h, rj, s);
+        ix[h] = uread(hx[h], j);
+      }
+    }
+    if (ej == 1) {  // (refresh3 with the window's loads)
+      _Pragma("unroll") for (int h = 0; h < 3; ++h) if (W.owns(h)) W.h[h].put(ix[h], X[h]);
+    } else if (ej == 3) {
+      W.adjust3_twice(s, X, ix);
     } else {
-      HEnt X[3];
-      uint32_t ix[3];
-      W.load3(s, X, ix);
-      if (ej == 3) W.adjust3(s, X, ix);
       W.adjust3(s, X, ix);
     }
     wave_sync();
@@ -786,8 +1012,8 @@ __global__ void __launch_bounds__(kHeapThreads) k_heap_add(Table tb, HeapDev hd,
       HEnt X[3];
       uint32_t ix[3];
       W.load3(s, X, ix);
-      if (first) W.adjust3(s, X, ix);  // a first request (:996-1006)
-      W.adjust3(s, X, ix);             // (:1011-1016)
+      if (first) W.adjust3_twice(s, X, ix);  // a first request (:996-1006, :1011-1016)
+      else W.adjust3(s, X, ix);              // (:1011-1016)
     } else if (idle) {
       W.refresh3(s);  // (a rejected activation: prop_delta moved, no heap call)
     }
@@ -822,13 +1048,17 @@ struct HClk {
 // every queued request: one lane each), in two levels of loads; lane 0
 // stores what is uniform.  With one wave per heap every wave computes the
 // same state, the lead wave stores it, and each wave sifts its own heap.
-__device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
-                                uint64_t tick, dmc_decision* out, unsigned long long* sched,
-                                HClk* ck = nullptr) {
-  const uint32_t lane = W.lane;
-  const bool lead = W.lead;
-  // level 1: the slot's heap indices (lanes 0-2), cursor, record, aux, bound info
-  const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
+// The pop's loads, decision and new client state (heap_pop without the
+// heap calls): *po0 the front's keys before the reduction (what the demotes
+// see), *po after it.  split: a block barrier between every wave's loads and
+// the lead wave's stores (each wave computes the same state).
+__device__ __forceinline__ void heap_pop_state(const Table& tb, uint32_t s, bool prio, uint64_t tick,
+                                               dmc_decision* out, unsigned long long* sched,
+                                               uint32_t lane, bool lead, bool split, HClk* ck,
+                                               ScanRec* po0, ScanRec* po) {
+  // level 1: cursor, record, aux, bound info
+  // (the whole ring loaded here instead, lane i its entry i, measured
+  // slower: pop loads 2,200 against 1,850 cycles per pull, r06i)
   const ScanRec sr = tb.sc[s];
   ClientRec cr = tb.rec[s];
   ClientAux ax{0, 0, 0};
@@ -862,7 +1092,7 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     keep(er);
     ck->lap(2);
   }
-  if (W.split) {  // every wave's loads done before the lead wave stores
+  if (split) {  // every wave's loads done before the lead wave stores
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -936,6 +1166,19 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     if (tb.delayed || prio) tb.rec[s] = cr;
     tb.sc[s] = o;
   }
+  *po = o;
+  *po0 = o;
+  po0->r = r_pre;
+}
+
+__device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint32_t s, bool prio,
+                                uint64_t tick, dmc_decision* out, unsigned long long* sched,
+                                HClk* ck = nullptr) {
+  const uint32_t lane = W.lane;
+  // the slot's heap indices (lanes 0-2), with the state's first level
+  const uint32_t hv = lane < 3 ? W.hd.hix[(size_t)lane * W.hd.n + s] : 0u;
+  ScanRec o0, o;
+  heap_pop_state(tb, s, prio, tick, out, sched, lane, W.lead, W.split, ck, &o0, &o);
   uint32_t ix[3];
   _Pragma("unroll") for (int j = 0; j < 3; ++j) ix[j] = uread(hv, j);
   const uint32_t n = W.count();
@@ -944,15 +1187,18 @@ __device__ __forceinline__ void heap_pop(const Table& tb, const WHeaps& W, uint3
     ck->lap(3);
   }
   // pop_process_request's heap calls, on the unreduced front (:1063-1069)
-  ScanRec o0 = o;
-  o0.r = r_pre;
-  if (W.owns(kHResv)) ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
+  // (a priority pop's resv demote and promote as one operation, K = 2)
+  const bool dp = DMC_HEAP_DP && prio && W.hd.k == 2;
+  if (W.owns(kHResv)) {
+    if (dp) ix[kHResv] = W.h[kHResv].k2_demote_promote(ix[kHResv], n, hent(kHResv, o0, s), hent(kHResv, o, s));
+    else ix[kHResv] = W.h[kHResv].sift_down(ix[kHResv], n, hent(kHResv, o0, s));
+  }
   if (DMC_HEAP_CLOCKS && ck) ck->lap(4);
   if (W.owns(kHLim)) ix[kHLim] = W.h[kHLim].sift(ix[kHLim], n, hent(kHLim, o0, s));
   if (DMC_HEAP_CLOCKS && ck) ck->lap(5);
   if (W.owns(kHReady)) ix[kHReady] = W.h[kHReady].sift_down(ix[kHReady], n, hent(kHReady, o0, s));
   if (DMC_HEAP_CLOCKS && ck) ck->lap(6);
-  if (prio && W.owns(kHResv))  // resv_heap.promote after the reduction (:1110)
+  if (prio && !dp && W.owns(kHResv))  // resv_heap.promote after the reduction (:1110)
     W.h[kHResv].sift_up(ix[kHResv], hent(kHResv, o, s));
   W.sync();
   if (DMC_HEAP_CLOCKS && ck) ck->lap(7);
@@ -1098,4 +1344,221 @@ __global__ void __launch_bounds__(64 * kHeapWaves) k_heap_pull(Table tb, HeapDev
     x.n_reservation = r.n_res;
     *d_result = x;
   }
+}
+
+// ---------------------------------------------------------------------------
+// k pull_request(now) calls in order, the heap waves decoupled from the
+// decisions (K = 2, mode 0).  In k_heap_pull every pull ends at a block
+// barrier, so each pull costs its decision, its pop's loads and the slowest
+// of its three heap calls -- a sift from the root through ~20 levels, of
+// which only the first round decides the new top.  Here wave 3 (the
+// coordinator) makes the decisions, the limit loop's marks and the pops'
+// loads and stores, and publishes each heap operation to an LDS ring; waves
+// 0-2 each run every operation on their own heap in order, signalling (an
+// LDS counter per heap) as soon as their heap's top holds its value after
+// it, and finish the sift's deeper rounds while the coordinator already
+// decides the next pull from the three tops.  The operations, their order
+// per heap and every move are the same as k_heap_pull's: only the waiting
+// changes.  The coordinator alone reads and writes the clients' state
+// (ScanRec, record, ring, decisions) -- except the limit loop's ready mark,
+// which the ready heap's wave stores before it signals -- and each heap
+// wave alone its heap's entries and indices (a pop's index of the popped
+// client in the heap it was the top of is 0; the others are looked up by
+// the heap's wave when it runs the operation).
+#ifndef DMC_HEAP_ASYNC
+#define DMC_HEAP_ASYNC 1
+#endif
+struct HOp {
+  uint32_t type;  // kOpLimit, kOpPop, kOpEnd
+  uint32_t s;     // the slot
+  uint32_t prio;  // pop: a priority pop
+  uint32_t pad;
+  HEnt X[3];  // pop: the three heaps' entries on the unreduced front; limit: X[1] the limit entry marked ready
+  HEnt Xu;    // priority pop: the resv entry after the reduction (resv.promote)
+};
+enum : uint32_t { kOpLimit = 1, kOpPop = 2, kOpEnd = 3 };
+constexpr uint32_t kHOps = 4;  // ring slots (at most two operations are ever unread)
+
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
+  while (lds_u32(p) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+__global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, double now, uint32_t k,
+                                                         int at_limit, uint64_t tick, dmc_decision* out,
+                                                         HeapPullRes* res, dmc_pull_result* d_result,
+                                                         unsigned long long* sched) {
+  __shared__ HEnt cache[3 * kHeapLds];
+  __shared__ HOp ring[kHOps];
+  __shared__ uint32_t s_pub;      // operations published
+  __shared__ uint32_t s_done[3];  // per heap: operations whose effect on the top is in place
+  if (threadIdx.x == 0) {
+    s_pub = 0;
+    s_done[0] = s_done[1] = s_done[2] = 0;
+  }
+  const uint32_t T = heap_cache_fill(hd, cache);  // (its barrier publishes the counters)
+  const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
+  const uint32_t n = hd.cnt[0];
+  if (wid < 3) {
+    // a heap's wave: every operation in order
+    const WHeap H{hd.ent + (size_t)wid * hd.n, hd.hix + (size_t)wid * hd.n, 2u, lane,
+                  cache + wid * kHeapLds, T};
+    for (uint32_t op = 0;; ++op) {
+      lds_wait_ge(&s_pub, op + 1);
+      const HOp o = ring[op % kHOps];
+      if (o.type == kOpEnd) break;
+      auto sig = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the top's LDS store)
+        if (lane == 0) __atomic_store_n(&s_done[wid], op + 1, __ATOMIC_RELAXED);
+      };
+      if (o.type == kOpLimit) {
+        // ready = true; ready.promote; limit.demote (:1135-1144)
+        if (wid == kHResv) {
+          sig();
+        } else if (wid == kHLim) {
+          H.k2_sift_down_sig(0, n, o.X[1], sig);
+        } else {
+          ScanRec lr = tb.sc[o.s];
+          const uint32_t ixr = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
+          lr.flags = (uint8_t)(lr.flags | F_READY);
+          if (lane == 0) tb.sc[o.s].flags = lr.flags;
+          const HEnt X = hent(kHReady, lr, o.s);
+          uint32_t anc;
+          const uint32_t d = H.k2_ancestors(ixr, &anc);
+          HEnt ae{~0ull, kClsNone + 1, 0};
+          if (lane < d) ae = H.ld(anc);
+          // (the mark's store completes with these loads: the coordinator
+          // reads the client's cursor only after this signal)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          H.up_anc(ixr, X, d, anc, ae);
+          sig();
+        }
+      } else {
+        // pop_process_request's calls (:1063-1069) and resv.promote (:1110)
+        if (wid == kHResv) {
+          if (o.prio) {
+            const uint32_t ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
+            H.k2_demote_promote(ix, n, o.X[0], o.Xu);
+            sig();
+          } else {
+            H.k2_sift_down_sig(0, n, o.X[0], sig);  // (the resv top)
+          }
+        } else if (wid == kHLim) {
+          H.k2_sift_sig((uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]), n, o.X[1], sig);
+        } else {
+          const uint32_t ix = o.prio ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
+          H.k2_sift_down_sig(ix, n, o.X[2], sig);  // (prio: the ready top)
+        }
+      }
+    }
+  } else {
+    // the coordinator: k_heap_pull's decisions, one pull after another
+    HeapPullRes r{0, 0, 0, DMC_NEXT_RETURNING, 0.0, 0, 0};
+    uint32_t opn = 0;
+    const HEnt* top0 = cache;
+    const HEnt* top1 = cache + kHeapLds;
+    const HEnt* top2 = cache + 2 * kHeapLds;
+    auto wait_tops = [&]() {
+      lds_wait_ge(&s_done[0], opn);
+      lds_wait_ge(&s_done[1], opn);
+      lds_wait_ge(&s_done[2], opn);
+    };
+    auto publish = [&](const HOp& o) {
+      // (the coordinator's client-state stores complete before a heap wave
+      // can read them: the limit mark's cursor load)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) ring[opn % kHOps] = o;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ++opn;
+      if (lane == 0) __atomic_store_n(&s_pub, opn, __ATOMIC_RELAXED);
+    };
+    while (r.n < k) {
+      uint32_t pop_slot = kNone;
+      bool pop_prio = false;
+      if (n == 0) {  // no clients: none (:1118-1120)
+        r.type = DMC_NEXT_NONE;
+        break;
+      }
+      wait_tops();
+      const HEnt rt = ld_lds<HEnt>(top0);
+      if (rt.cls == 0 && hval(rt) <= now) {
+        pop_slot = rt.slot;
+      } else {
+        for (;;) {  // the limit loop
+          const HEnt lt = ld_lds<HEnt>(top1);
+          if (!(lt.cls == 0 && hval(lt) <= now)) break;
+          HOp o{};
+          o.type = kOpLimit;
+          o.s = lt.slot;
+          o.X[1] = lt;
+          o.X[1].cls = 1;  // (hent(kHLim, ...) of the record marked ready)
+          publish(o);
+          wait_tops();
+        }
+        const HEnt pt = ld_lds<HEnt>(top2);
+        const bool ph = pt.cls != kClsNone && hval(pt) < kInf;
+        if (pt.cls == 0 && ph) {
+          pop_slot = pt.slot;
+          pop_prio = true;
+        } else if (at_limit == DMC_AT_LIMIT_ALLOW && ph) {
+          pop_slot = pt.slot;
+          pop_prio = true;
+        } else if (at_limit == DMC_AT_LIMIT_ALLOW && rt.cls == 0 && hval(rt) < kInf) {
+          pop_slot = rt.slot;
+        }
+      }
+      if (pop_slot == kNone) {
+        // future / none (:1170-1185), as k_heap_pull
+        constexpr double kTimeMax = 1.7976931348623157e308;
+        double next = kTimeMax;
+        const HEnt r0 = ld_lds<HEnt>(top0), l0 = ld_lds<HEnt>(top1);
+        if (r0.cls != kClsNone) {
+          const double v = hval(r0);
+          if (v != 0.0) next = v < next ? v : next;
+        }
+        if (l0.cls != kClsNone) {
+          const double v = hval(l0);
+          if (v != 0.0) next = v < next ? v : next;
+        }
+        if (next < kTimeMax) {
+          r.type = DMC_NEXT_FUTURE;
+          r.when = next;
+        } else {
+          r.type = DMC_NEXT_NONE;
+        }
+        break;
+      }
+      ScanRec o0, o1;
+      heap_pop_state(tb, pop_slot, pop_prio, tick, out + r.n, sched, lane, true, false, nullptr,
+                     &o0, &o1);
+      HOp o{};
+      o.type = kOpPop;
+      o.s = pop_slot;
+      o.prio = pop_prio ? 1u : 0u;
+      _Pragma("unroll") for (int j = 0; j < 3; ++j) o.X[j] = hent(j, o0, pop_slot);
+      o.Xu = hent(kHResv, o1, pop_slot);
+      publish(o);
+      ++r.n;
+      if (pop_prio) ++r.n_prio;
+      else ++r.n_res;
+    }
+    HOp e{};
+    e.type = kOpEnd;
+    publish(e);
+    if (lane == 0) {
+      *res = r;
+      if (d_result) {
+        dmc_pull_result x{};
+        x.n_decisions = r.n;
+        x.next_type = r.type;
+        x.when = r.type == DMC_NEXT_FUTURE ? r.when : 0.0;
+        x.n_priority = r.n_prio;
+        x.n_reservation = r.n_res;
+        *d_result = x;
+      }
+    }
+  }
+  heap_cache_flush(hd, cache, T);
 }
