@@ -1372,7 +1372,7 @@ struct HOp {
   uint32_t type;  // kOpLimit, kOpPop, kOpEnd
   uint32_t s;     // the slot
   uint32_t prio;  // pop: a priority pop
-  uint32_t pad;
+  uint32_t pad;   // pop: bit h, the popped client is heap h's top
   HEnt X[3];  // pop: the three heaps' entries on the unreduced front; limit: X[1] the limit entry marked ready
   HEnt Xu;    // priority pop: the resv entry after the reduction (resv.promote)
 };
@@ -1405,14 +1405,23 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
     // a heap's wave: every operation in order
     const WHeap H{hd.ent + (size_t)wid * hd.n, hd.hix + (size_t)wid * hd.n, 2u, lane,
                   cache + wid * kHeapLds, T};
+    HClk ck;
+    ck.start();
     for (uint32_t op = 0;; ++op) {
       lds_wait_ge(&s_pub, op + 1);
+      ck.lap(0);
       const HOp o = ring[op % kHOps];
       if (o.type == kOpEnd) break;
       auto sig = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the top's LDS store)
         if (lane == 0) __atomic_store_n(&s_done[wid], op + 1, __ATOMIC_RELAXED);
       };
+      // An operation that cannot change the heap's top signals before it
+      // starts: a sift down from a node other than the top, or a climb by
+      // an entry not less than the top (it passes only ancestors it is
+      // strictly less than).  The coordinator says which heaps' top the
+      // popped client is (o.pad bit h: its index there is 0).
+      const HEnt root = ld_lds<HEnt>(H.c);
       if (o.type == kOpLimit) {
         // ready = true; ready.promote; limit.demote (:1135-1144)
         if (wid == kHResv) {
@@ -1420,39 +1429,58 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
         } else if (wid == kHLim) {
           H.k2_sift_down_sig(0, n, o.X[1], sig);
         } else {
+          // (the coordinator sets the ready mark in the client's cursor)
           ScanRec lr = tb.sc[o.s];
           const uint32_t ixr = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
           lr.flags = (uint8_t)(lr.flags | F_READY);
-          if (lane == 0) tb.sc[o.s].flags = lr.flags;
           const HEnt X = hent(kHReady, lr, o.s);
+          const bool early = !hlt(X, root);
+          if (early) sig();
           uint32_t anc;
           const uint32_t d = H.k2_ancestors(ixr, &anc);
           HEnt ae{~0ull, kClsNone + 1, 0};
           if (lane < d) ae = H.ld(anc);
-          // (the mark's store completes with these loads: the coordinator
-          // reads the client's cursor only after this signal)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           H.up_anc(ixr, X, d, anc, ae);
-          sig();
+          if (!early) sig();
         }
       } else {
         // pop_process_request's calls (:1063-1069) and resv.promote (:1110)
+        const bool istop = (o.pad >> wid) & 1u;
+        auto index = [&]() {
+          return istop ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
+        };
         if (wid == kHResv) {
           if (o.prio) {
-            const uint32_t ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
-            H.k2_demote_promote(ix, n, o.X[0], o.Xu);
-            sig();
+            const bool early = !istop && !hlt(o.Xu, root);
+            if (early) sig();
+            H.k2_demote_promote(index(), n, o.X[0], o.Xu);
+            if (!early) sig();
           } else {
             H.k2_sift_down_sig(0, n, o.X[0], sig);  // (the resv top)
           }
         } else if (wid == kHLim) {
-          H.k2_sift_sig((uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]), n, o.X[1], sig);
+          if (!istop && !hlt(o.X[1], root)) {
+            sig();
+            H.k2_sift(index(), n, o.X[1]);
+          } else {
+            H.k2_sift_sig(index(), n, o.X[1], sig);
+          }
         } else {
-          const uint32_t ix = o.prio ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)H.x[o.s]);
-          H.k2_sift_down_sig(ix, n, o.X[2], sig);  // (prio: the ready top)
+          if (istop) {
+            H.k2_sift_down_sig(0, n, o.X[2], sig);
+          } else {  // (a sift down from below the top)
+            sig();
+            H.k2_sift_down(index(), n, o.X[2]);
+          }
         }
       }
+      ck.lap(o.type == kOpLimit ? 1 : 2);
+      if (DMC_HEAP_CLOCKS) ++ck.t[o.type == kOpLimit ? 8 : 9];
     }
+    if (DMC_HEAP_CLOCKS && lane == 0 && ck.t[9] > 1000)
+      printf("async heap wave %u: ops limit %llu pop %llu | cycles per pop: waiting %.0f limit ops %.0f pops %.0f\n",
+             wid, (unsigned long long)ck.t[8], (unsigned long long)ck.t[9], (double)ck.t[0] / ck.t[9],
+             (double)ck.t[1] / ck.t[9], (double)ck.t[2] / ck.t[9]);
   } else {
     // the coordinator: k_heap_pull's decisions, one pull after another
     HeapPullRes r{0, 0, 0, DMC_NEXT_RETURNING, 0.0, 0, 0};
@@ -1460,15 +1488,19 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
     const HEnt* top0 = cache;
     const HEnt* top1 = cache + kHeapLds;
     const HEnt* top2 = cache + 2 * kHeapLds;
+    HClk ck;
+    ck.start();
     auto wait_tops = [&]() {
+      ck.lap(1);
       lds_wait_ge(&s_done[0], opn);
       lds_wait_ge(&s_done[1], opn);
       lds_wait_ge(&s_done[2], opn);
+      ck.lap(0);
     };
     auto publish = [&](const HOp& o) {
-      // (the coordinator's client-state stores complete before a heap wave
-      // can read them: the limit mark's cursor load)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (a limit operation's cursor load by the ready heap's wave: the
+      // coordinator's stores to it complete first)
+      if (o.type == kOpLimit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) ring[opn % kHOps] = o;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       ++opn;
@@ -1494,6 +1526,14 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
           o.s = lt.slot;
           o.X[1] = lt;
           o.X[1].cls = 1;  // (hent(kHLim, ...) of the record marked ready)
+          // ready = true: F_READY in the cursor word (head | count << 8 |
+          // flags << 16 | stamp << 24, ScanRec offset 24); no other bit of it
+          // changes until the coordinator's own later stores
+          if (lane == 0)
+            __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tb.sc + lt.slot) +
+                                                              offsetof(ScanRec, head)),
+                                  (uint32_t)F_READY << 16, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
           publish(o);
           wait_tops();
         }
@@ -1531,15 +1571,23 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
         break;
       }
       ScanRec o0, o1;
+      ck.lap(1);
       heap_pop_state(tb, pop_slot, pop_prio, tick, out + r.n, sched, lane, true, false, nullptr,
                      &o0, &o1);
+      ck.lap(2);
       HOp o{};
       o.type = kOpPop;
       o.s = pop_slot;
       o.prio = pop_prio ? 1u : 0u;
       _Pragma("unroll") for (int j = 0; j < 3; ++j) o.X[j] = hent(j, o0, pop_slot);
       o.Xu = hent(kHResv, o1, pop_slot);
+      {  // the heaps whose top the popped client is (its index there: 0)
+        const HEnt t0 = ld_lds<HEnt>(top0), t1 = ld_lds<HEnt>(top1), t2 = ld_lds<HEnt>(top2);
+        o.pad = (t0.slot == pop_slot ? 1u : 0u) | (t1.slot == pop_slot ? 2u : 0u) |
+                (t2.slot == pop_slot ? 4u : 0u);
+      }
       publish(o);
+      ck.lap(3);
       ++r.n;
       if (pop_prio) ++r.n_prio;
       else ++r.n_res;
@@ -1547,6 +1595,9 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
     HOp e{};
     e.type = kOpEnd;
     publish(e);
+    if (DMC_HEAP_CLOCKS && lane == 0 && r.n > 1000)
+      printf("async coordinator: pulls %u | cycles per pull: waiting %.0f deciding %.0f pop state %.0f publish %.0f\n",
+             r.n, (double)ck.t[0] / r.n, (double)ck.t[1] / r.n, (double)ck.t[2] / r.n, (double)ck.t[3] / r.n);
     if (lane == 0) {
       *res = r;
       if (d_result) {
