@@ -614,9 +614,11 @@ def main():
     if roof is not None:
         # HBM bytes per launch of the same stage from the PMC passes of
         # scripts/gpu_pmc.sh (tools/pmc_traffic.py), committed under
-        # profiles/; null if that file is absent or lacks the stage
+        # profiles/; null if that file is absent or lacks the stage.  The
+        # committed passes run config 3's bench: another config's line
+        # carries traffic only from a file given for it (--traffic)
         traffic = None
-        tfile = args.traffic or latest_traffic()
+        tfile = args.traffic or (latest_traffic() if args.config == 3 else None)
         if tfile and os.path.exists(tfile):
             try:
                 t = json.load(open(tfile)).get(roof["kernel"])
