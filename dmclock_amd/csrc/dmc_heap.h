@@ -1095,6 +1095,11 @@ __device__ __forceinline__ void heap_pop_state(const Table& tb, uint32_t s, bool
   if (split) {  // every wave's loads done before the lead wave stores
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
+  } else {
+    // (with the loads, every earlier memory operation of this wave is
+    // complete before the stores below: the decoupled pull's ready-mark
+    // atomics on a client's cursor)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (lead && lane == 0) {
     dmc_decision d;
@@ -1501,15 +1506,20 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
       lds_wait_ge(&s_done[h], opn);
       ck.lap(0);
     };
+    uint32_t taken = 0;  // a lower bound of every heap wave's operations taken
     auto publish = [&](const HOp& o) {
       // (a limit operation's cursor load by the ready heap's wave: the
       // coordinator's stores to it complete first)
       if (o.type == kOpLimit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // a free ring slot: every heap wave has taken operation opn - kHOps
-      if (opn >= kHOps) {
+      // (the counters only grow: re-read only when the last reading is
+      // not enough)
+      if (opn >= kHOps && taken < opn - kHOps + 1) {
         lds_wait_ge(&s_done[0], opn - kHOps + 1);
         lds_wait_ge(&s_done[1], opn - kHOps + 1);
         lds_wait_ge(&s_done[2], opn - kHOps + 1);
+        const uint32_t t0 = lds_u32(&s_done[0]), t1 = lds_u32(&s_done[1]), t2 = lds_u32(&s_done[2]);
+        taken = min(t0, min(t1, t2));
       }
       if (lane == 0) ring[opn % kHOps] = o;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1537,15 +1547,18 @@ __global__ void __launch_bounds__(256) k_heap_pull_async(Table tb, HeapDev hd, d
           o.s = lt.slot;
           o.X[1] = lt;
           o.X[1].cls = 1;  // (hent(kHLim, ...) of the record marked ready)
+          publish(o);
           // ready = true: F_READY in the cursor word (head | count << 8 |
-          // flags << 16 | stamp << 24, ScanRec offset 24); no other bit of it
-          // changes until the coordinator's own later stores
+          // flags << 16 | stamp << 24, ScanRec offset 24), issued after the
+          // publication (its completion is not waited for there: the ready
+          // heap's wave reads the client's keys, not this bit); no other bit
+          // of the word changes before the coordinator's next stores, which
+          // heap_pop_state orders behind it
           if (lane == 0)
             __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tb.sc + lt.slot) +
                                                               offsetof(ScanRec, head)),
                                   (uint32_t)F_READY << 16, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
-          publish(o);
         }
         wait_top(kHReady);
         const HEnt pt = ld_lds<HEnt>(top2);
