@@ -183,6 +183,8 @@ def main(args):
 
     pool = ThreadPoolExecutor(S)
     group = None if args.separate_queues else GpuGroup(queues)
+    if group is not None and trk.lagged:
+        trk.attach_group(group)  # (the epoch's sums beside the next steps)
     g_args = [([d_steps[s][i].data_ptr() for s in range(S)], [nows[s][i] for s in range(S)],
                [d_res[s, i].data_ptr() for s in range(S)],
                [d_rcs[s, i].data_ptr() for s in range(S)])

@@ -2229,6 +2229,12 @@ struct dmc_group {
   // events that fork it from and join it to the step
   hipStream_t stream2 = nullptr, cap_stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // dmc_group_tracker_collect_sums: the epoch's per-client sums on a stream
+  // of their own beside the group's next steps, joined by
+  // dmc_group_tracker_join
+  hipStream_t side = nullptr;
+  hipEvent_t ev_side_in = nullptr, ev_side_out = nullptr;
+  bool side_pending = false;
   // per-step kernel arguments: pinned staging and its device copy (one
   // memcpy per step, the graph's first node), S entries per kernel
   uint8_t* h_blob = nullptr;
@@ -5212,11 +5218,64 @@ int dmc_group_destroy(dmc_group* g) {
   if (g->cap_stream2) (void)hipStreamDestroy(g->cap_stream2);
   if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
   if (g->ev_join) (void)hipEventDestroy(g->ev_join);
+  if (g->side) {
+    (void)hipStreamSynchronize(g->side);
+    (void)hipStreamDestroy(g->side);
+  }
+  if (g->ev_side_in) (void)hipEventDestroy(g->ev_side_in);
+  if (g->ev_side_out) (void)hipEventDestroy(g->ev_side_out);
   delete g;
   return DMC_OK;
 }
 
 void* dmc_group_stream(dmc_group* g) { return g ? (void*)g->stream : nullptr; }
+
+int dmc_group_tracker_collect_sums(dmc_group* g, uint32_t n_slots,
+                                   const uint32_t* const* d_client_of_slot,
+                                   const uint32_t* const* d_comp_delta,
+                                   const uint32_t* const* d_comp_rho, uint32_t* d_sum_delta,
+                                   uint32_t* d_sum_rho) {
+  if (!g || !d_comp_delta || !d_comp_rho || !d_sum_delta || !d_sum_rho) return DMC_EINVAL;
+  const uint32_t S = (uint32_t)g->qs.size();
+  for (uint32_t i = 0; i < S; ++i) {
+    if (!d_comp_delta[i] || !d_comp_rho[i]) return DMC_EINVAL;
+    if (n_slots > g->qs[i]->p.max_clients) return DMC_EINVAL;
+  }
+  if (!n_slots) return DMC_OK;
+  GroupLock gl(g);
+  if (gl.rc) return gl.rc;
+  if (!g->side) {
+    if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_side_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_side_out, hipEventDisableTiming) != hipSuccess)
+      return DMC_ENOMEM;
+  }
+  // (a second collection before a join: the first one's sums are ordered
+  // before this one's reads of the group's stream anyway; join both)
+  HIP_OK(hipEventRecord(g->ev_side_in, g->stream));
+  HIP_OK(hipStreamWaitEvent(g->side, g->ev_side_in, 0));
+  for (uint32_t i = 0; i < S; ++i)
+    hipLaunchKernelGGL(k_track_sums, dim3(grid_for(n_slots, 2048)), dim3(kBlock), 0, g->side,
+                       n_slots, d_client_of_slot ? d_client_of_slot[i] : nullptr,
+                       d_comp_delta[i], d_comp_rho[i], d_sum_delta, d_sum_rho);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(g->ev_side_out, g->side));
+  g->side_pending = true;
+  return DMC_OK;
+}
+
+int dmc_group_tracker_join(dmc_group* g) {
+  if (!g) return DMC_EINVAL;
+  GroupLock gl(g);
+  if (gl.rc) return gl.rc;
+  if (g->side_pending) {
+    HIP_OK(hipStreamWaitEvent(g->stream, g->ev_side_out, 0));
+    g->side_pending = false;
+  }
+  return DMC_OK;
+}
+
+void* dmc_group_side_stream(dmc_group* g) { return g ? (void*)g->side : nullptr; }
 
 int dmc_group_profile_enable(dmc_group* g, int on) {
   if (!g) return DMC_EINVAL;

@@ -77,6 +77,9 @@ EXPORTS = {
     "dmc_group_create": (_i32, [_vp, _u32, ctypes.POINTER(_vp)]),
     "dmc_group_destroy": (_i32, [_vp]),
     "dmc_group_stream": (_vp, [_vp]),
+    "dmc_group_tracker_collect_sums": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "dmc_group_tracker_join": (_i32, [_vp]),
+    "dmc_group_side_stream": (_vp, [_vp]),
     "dmc_group_step_device": (_i32, [_vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "dmc_group_profile_enable": (_i32, [_vp, _i32]),
     "dmc_group_profile_read": (_i32, [_vp, _u32, ctypes.POINTER(ctypes.c_uint64),

@@ -74,6 +74,7 @@ class DeviceTrackers:
         self.first = torch.full((S, N), U32_NONE, dtype=i32, device=device)
         self.comp = torch.zeros((2, 2, S, N), dtype=i32, device=device)
         self.cur = 0
+        self.gg = None  # attach_group: the GpuGroup whose side stream collects
         self.pending = None  # lagged: (half, all-reduce work or None)
         self.allreduce_ms = []  # lagged: measured all-reduce time per epoch
         self.L = lib()
@@ -130,6 +131,19 @@ class DeviceTrackers:
         for q in self.queues:
             q.sync()
 
+    def attach_group(self, group):
+        """the GpuGroup the queues step in: the lagged delivery's per-client
+        sums then run on the group's side stream beside its next steps
+        (dmc_group_tracker_collect_sums), joined before the next commit"""
+        self.gg = group
+
+    def _collective(self, group):
+        """the backend the delivery all-reduces over, None without one"""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        return dist.get_backend(group)
+
     def _allreduce(self, buf, group, async_op):
         """the exchange step: RCCL on the device buffer (async: its work
         handle), gloo through host memory (blocking)"""
@@ -179,6 +193,8 @@ class DeviceTrackers:
     def _finish_pending(self):
         torch = self.torch
         half, work = self.pending
+        if self.gg is not None:  # (the side stream's sums before commit and advance)
+            _check(self.L.dmc_group_tracker_join(self.gg.h), "dmc_group_tracker_join")
         if work is not None:
             w, ev0, ev1 = work
             ev1.synchronize()
@@ -196,13 +212,33 @@ class DeviceTrackers:
         if self.pending is not None:
             self._finish_pending()
         h = self.cur
-        for s, q in enumerate(self.queues):
-            _check(self.L.dmc_tracker_collect_sums(q.h, self.N, self._map(s),
-                                                   _p(self.comp[h, 0, s]),
-                                                   _p(self.comp[h, 1, s]),
-                                                   _p(self.sums[h, 0]), _p(self.sums[h, 1])),
-                   "dmc_tracker_collect_sums")
-        self._sync_queues()
+        if self.gg is not None:
+            # the sums beside the next epoch's steps (they tally into the
+            # other half); a collective on them waits for the side stream
+            S = len(self.queues)
+            vp = ctypes.c_void_p * S
+            maps = vp(*[self.cmap[s].data_ptr() for s in range(S)]) \
+                if self.cmap is not None else None
+            _check(self.L.dmc_group_tracker_collect_sums(
+                self.gg.h, self.N, maps, vp(*[self.comp[h, 0, s].data_ptr() for s in range(S)]),
+                vp(*[self.comp[h, 1, s].data_ptr() for s in range(S)]),
+                _p(self.sums[h, 0]), _p(self.sums[h, 1])), "dmc_group_tracker_collect_sums")
+            if self._collective(group) == "nccl":
+                torch = self.torch
+                side = torch.cuda.ExternalStream(self.L.dmc_group_side_stream(self.gg.h),
+                                                 device=self.gd.device)
+                torch.cuda.current_stream(self.gd.device).wait_stream(side)
+            elif self._collective(group) is not None:  # (gloo: staged through the host)
+                _check(self.L.dmc_group_tracker_join(self.gg.h), "dmc_group_tracker_join")
+                self._sync_queues()
+        else:
+            for s, q in enumerate(self.queues):
+                _check(self.L.dmc_tracker_collect_sums(q.h, self.N, self._map(s),
+                                                       _p(self.comp[h, 0, s]),
+                                                       _p(self.comp[h, 1, s]),
+                                                       _p(self.sums[h, 0]), _p(self.sums[h, 1])),
+                       "dmc_tracker_collect_sums")
+            self._sync_queues()
         self.pending = (h, self._allreduce(self.sums[h], group, async_op=True))
         self.cur = 1 - h  # the next epoch tallies into the other half
 

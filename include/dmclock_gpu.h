@@ -288,6 +288,23 @@ typedef struct dmc_group_tracker {  /* one server's device tracker state (see dm
 int dmc_group_create(dmc_queue* const* queues, uint32_t n, dmc_group** out);
 int dmc_group_destroy(dmc_group* g);
 void* dmc_group_stream(dmc_group* g);
+/* Overlapped delivery for a queue group (no reference counterpart; the
+ * values of dmc_tracker_collect_sums on every member): the members'
+ * per-client sums, sum_*[client_of_slot[s][i]] += comp_*[s][i], run on a
+ * stream of their own behind the group's work so far, beside the group's
+ * next steps (which tally into the other half of the comp arrays).
+ * dmc_group_tracker_join orders the group's stream behind them: call it
+ * before anything on the group's stream reads the sums or clears those comp
+ * arrays (the next epoch's commit and advance).  client_of_slot: NULL, or one
+ * map per member (entries NULL: identity).  dmc_group_side_stream: that
+ * stream (NULL before the first collection), for a collective on the sums. */
+int dmc_group_tracker_collect_sums(dmc_group* g, uint32_t n_slots,
+                                   const uint32_t* const* d_client_of_slot,
+                                   const uint32_t* const* d_comp_delta,
+                                   const uint32_t* const* d_comp_rho, uint32_t* d_sum_delta,
+                                   uint32_t* d_sum_rho);
+int dmc_group_tracker_join(dmc_group* g);
+void* dmc_group_side_stream(dmc_group* g);
 /* Per member s: requests d_reqs[s][0..n) (delta/rho filled first when trk),
  * statuses d_rc[s], pull time now[s], k pulls into d_out[s], result record
  * d_result[s]; trk: NULL or one entry per member. */

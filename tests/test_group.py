@@ -47,7 +47,7 @@ def _workload(S, N, depth, n_steps, batch, seed):
     return out
 
 
-def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=()):
+def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=(), lagged=False):
     """one pass over the workload; returns digests of every output"""
     import torch
     from dmclock_amd.multiserver import DeviceTrackers, GpuGroup, make_queues
@@ -59,8 +59,10 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=()):
         for opt, val in options:
             q.set_option(opt, val)
     trk = DeviceTrackers(qs, N, dev, n_clients=S * N,
-                         client_of_slot=np.stack([w[1] for w in wl]))
+                         client_of_slot=np.stack([w[1] for w in wl]), lagged=lagged)
     group = GpuGroup(qs) if grouped else None
+    if group is not None and lagged:
+        trk.attach_group(group)
     d_rc = [torch.zeros(chunk, dtype=torch.int32, device=dev) for _ in range(S)]
     n_steps = len(wl[0][3])
     d_out = [torch.zeros(max(k, chunk) * DECISION_DTYPE.itemsize, dtype=torch.uint8,
@@ -101,6 +103,8 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=()):
                                       .astype(np.uint32))
         nows = [float(w[3][i]["time"][-1]) for w in wl]
         if grouped:
+            if lagged:  # (the current tally half)
+                gtrk = trk.group_trackers()
             group.step(len(wl[0][3][i]), [d_steps[s][i].data_ptr() for s in range(S)],
                        [d.data_ptr() for d in d_rc], nows, k,
                        [d.data_ptr() for d in d_out],
@@ -123,6 +127,8 @@ def _drive(wl, N, k, grouped, settle, idle_every=0, epoch=4, options=()):
             digest[s].update(d_rc[s][:len(wl[s][3][i])].cpu().numpy().tobytes())
         if (i + 1) % epoch == 0:
             trk.deliver()
+    if lagged:
+        trk.finish()
     st = trk.state()
     ctr = [q.counters() for q in qs]
     out = {"digest": [d.hexdigest() for d in digest],
@@ -152,6 +158,21 @@ def test_group_bench_shape_vs_separate_queues():
     a = _drive(wl, N, k, grouped=True, settle=1 << 21)
     b = _drive(wl, N, k, grouped=False, settle=1 << 21)
     assert a["fused"] == [8] * S, a["fused"]
+    assert a["digest"] == b["digest"]
+    assert a["trk"] == b["trk"]
+    assert a["decisions"] == b["decisions"]
+
+
+@pytest.mark.timeout(300)
+def test_group_lagged_side_stream_sums():
+    """the overlapped (lagged) epoch delivery with the per-client sums on the
+    group's side stream beside the next epoch's steps
+    (dmc_group_tracker_collect_sums / _join): identical bytes and tracker
+    state to separate queues collecting on their own streams"""
+    S, N, k = 4, 1 << 16, 1 << 12
+    wl = _workload(S, N, 4, 9, k, seed=17)
+    a = _drive(wl, N, k, grouped=True, settle=N, epoch=2, lagged=True)
+    b = _drive(wl, N, k, grouped=False, settle=N, epoch=2, lagged=True)
     assert a["digest"] == b["digest"]
     assert a["trk"] == b["trk"]
     assert a["decisions"] == b["decisions"]
