@@ -18,7 +18,7 @@ DMC_EBADPARAMS = -1002
 DMC_EQUEUEFULL = -1004
 DMC_ENOTREG = -1005
 DMC_ENOTRUN = -1006  # pipelined: the previous call failed, this one was not executed
-ABI_VERSION = 6  # include/dmclock_gpu.h DMC_ABI_VERSION
+ABI_VERSION = 7  # include/dmclock_gpu.h DMC_ABI_VERSION
 
 # AtLimit (dmclock_server.h:74-84)
 AT_LIMIT_WAIT = 0

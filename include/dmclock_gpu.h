@@ -59,8 +59,9 @@ extern "C" {
  *      act_batches / act_seq_batches (round 4) and renamed pred_* to
  *      bad_rounds / serve_yields. */
 /*   6: dmc_queue_pipelined_error (the error a DMC_ENOTRUN stands for);
- *      dmc_group_profile_enable / dmc_group_profile_read. */
-#define DMC_ABI_VERSION 6
+ *      dmc_group_profile_enable / dmc_group_profile_read.
+ *   7: dmc_group_tracker_collect_sums / _join / dmc_group_side_stream. */
+#define DMC_ABI_VERSION 7
 int dmc_abi_version(void);
 
 /* ------------------------------------------------------------ enums */
