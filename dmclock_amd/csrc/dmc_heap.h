@@ -850,80 +850,82 @@ __global__ void __launch_bounds__(64 * kHeapWaves) k_heap_events(Table tb, HeapD
   WHeaps W(tb, hd, cache, T, kHeapWaves == 3);
   const uint32_t lane = W.lane;
   const uint32_t cnt = W.count();
-  for (uint32_t i0 = 0; i0 < n;) {
-    // a window of 64 events, one per lane
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    // a window of 64 events, one per lane: the requests and the slots'
+    // states are the kernel's inputs (the batched add path made every state
+    // change; only the heaps change here), loaded once per window
     const uint32_t i = i0 + lane;
     uint32_t e = 0, sl = 0;
     if (i < n) {
       e = ev[i];
       if (e) sl = reqs[i].slot;
     }
-    // every event's slot state and indices (the first ordered event's are
-    // taken from here: nothing before it in the window changed them)
     ScanRec r{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
-    uint32_t hx[3] = {0, 0, 0};
-    if (e) {
-      r = tb.sc[sl];
-      _Pragma("unroll") for (int j = 0; j < 3; ++j) if (W.owns(j)) hx[j] = hd.hix[(size_t)j * hd.n + sl];
-    }
-    // Which of them must run in order.  A repeat request of a client (code
-    // 2) whose entries (in this wave's heaps) already hold its key, none
-    // less than its parent and none with a child less than it, makes sifts
-    // that move nothing (K = 2 checked here; other K run every event): the
-    // window's events before the first that may move are skipped -- each of
-    // them saw the heaps as the window found them, unchanged by the ones
-    // before.
-    bool ord = e == 1 || e == 3 || (e == 2 && hd.k != 2);
-    if (e == 2 && hd.k == 2) {
-      _Pragma("unroll") for (int j = 0; j < 3; ++j) {
-        if (!W.owns(j)) continue;
-        const HEnt X = hent(j, r, sl);
-        const uint32_t v = hx[j];
-        const HEnt own = W.h[j].ld(v);
-        if (own.key != X.key || own.cls != X.cls) ord = true;
-        if (v > 0 && hlt(X, W.h[j].ld((v - 1) >> 1))) ord = true;
-        const uint64_t li = 2ull * v + 1;
-        if (li < cnt) {
-          const HEnt c1 = W.h[j].ld((uint32_t)li);
-          HEnt mc = c1;
-          if (li + 1 < cnt) {
-            const HEnt c2 = W.h[j].ld((uint32_t)li + 1);
-            if (hlt(c2, c1)) mc = c2;
+    if (e) r = tb.sc[sl];
+    // the window's events from `start` on: after each ordered event the
+    // heaps' indices and entries are read again (it moved them), the rest
+    // of the window is not
+    for (uint32_t start = 0; start < 64;) {
+      const bool live = e && lane >= start;
+      uint32_t hx[3] = {0, 0, 0};
+      if (live) {
+        _Pragma("unroll") for (int j = 0; j < 3; ++j) if (W.owns(j)) hx[j] = hd.hix[(size_t)j * hd.n + sl];
+      }
+      // Which of them must run in order.  A repeat request of a client (code
+      // 2) whose entries (in this wave's heaps) already hold its key, none
+      // less than its parent and none with a child less than it, makes sifts
+      // that move nothing (K = 2 checked here; other K run every event): the
+      // events before the first that may move are skipped -- each of them
+      // saw the heaps as the window found them, unchanged by the ones before.
+      bool ord = live && (e == 1 || e == 3 || (e == 2 && hd.k != 2));
+      if (live && e == 2 && hd.k == 2) {
+        _Pragma("unroll") for (int j = 0; j < 3; ++j) {
+          if (!W.owns(j)) continue;
+          const HEnt X = hent(j, r, sl);
+          const uint32_t v = hx[j];
+          const HEnt own = W.h[j].ld(v);
+          if (own.key != X.key || own.cls != X.cls) ord = true;
+          if (v > 0 && hlt(X, W.h[j].ld((v - 1) >> 1))) ord = true;
+          const uint64_t li = 2ull * v + 1;
+          if (li < cnt) {
+            const HEnt c1 = W.h[j].ld((uint32_t)li);
+            HEnt mc = c1;
+            if (li + 1 < cnt) {
+              const HEnt c2 = W.h[j].ld((uint32_t)li + 1);
+              if (hlt(c2, c1)) mc = c2;
+            }
+            if (hlt(mc, X)) ord = true;
           }
-          if (hlt(mc, X)) ord = true;
         }
       }
-    }
-    const uint64_t m = __ballot(ord);
-    if (!m) {
-      i0 += 64;
-      continue;
-    }
-    const uint32_t j = (uint32_t)__builtin_ctzll(m);
-    const uint32_t ej = uread(e, j), s = uread(sl, j);
-    HEnt X[3];
-    uint32_t ix[3];
-    {
-      ScanRec rj{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
-      rj.r = dread(r.r, j);
-      rj.pk = dread(r.pk, j);
-      rj.l = dread(r.l, j);
-      rj.count = (uint8_t)uread(r.count, j);
-      rj.flags = (uint8_t)uread(r.flags, j);
-      _Pragma("unroll") for (int h = 0; h < 3; ++h) {
-        X[h] = hent(h, rj, s);
-        ix[h] = uread(hx[h], j);
+      const uint64_t m = __ballot(ord);
+      if (!m) break;
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      const uint32_t ej = uread(e, j), s = uread(sl, j);
+      HEnt X[3];
+      uint32_t ix[3];
+      {
+        ScanRec rj{0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
+        rj.r = dread(r.r, j);
+        rj.pk = dread(r.pk, j);
+        rj.l = dread(r.l, j);
+        rj.count = (uint8_t)uread(r.count, j);
+        rj.flags = (uint8_t)uread(r.flags, j);
+        _Pragma("unroll") for (int h = 0; h < 3; ++h) {
+          X[h] = hent(h, rj, s);
+          ix[h] = uread(hx[h], j);
+        }
       }
+      if (ej == 1) {  // (refresh3 with the window's loads)
+        _Pragma("unroll") for (int h = 0; h < 3; ++h) if (W.owns(h)) W.h[h].put(ix[h], X[h]);
+      } else if (ej == 3) {
+        W.adjust3_twice(s, X, ix);
+      } else {
+        W.adjust3(s, X, ix);
+      }
+      wave_sync();
+      start = j + 1;
     }
-    if (ej == 1) {  // (refresh3 with the window's loads)
-      _Pragma("unroll") for (int h = 0; h < 3; ++h) if (W.owns(h)) W.h[h].put(ix[h], X[h]);
-    } else if (ej == 3) {
-      W.adjust3_twice(s, X, ix);
-    } else {
-      W.adjust3(s, X, ix);
-    }
-    wave_sync();
-    i0 += j + 1;
   }
   heap_cache_flush(hd, cache, T);
 }
