@@ -258,7 +258,8 @@ def _w2_workload():
     return cmap, tab, eps
 
 
-def _device_trackers_worker(rank, world, port, out_q, backend="gloo", lagged=False):
+def _device_trackers_worker(rank, world, port, out_q, backend="gloo", lagged=False,
+                            grouped=False):
     """One rank: servers [rank * S, (rank + 1) * S) as GPU queues on cuda:0
     with DeviceTrackers, the per-epoch delivery all-reducing over `backend`
     (the product's DeviceTrackers.deliver: host-staged under gloo, on the
@@ -281,6 +282,11 @@ def _device_trackers_worker(rank, world, port, out_q, backend="gloo", lagged=Fal
             q.register(tab.slots, tab.r, tab.w, tab.l, True)
         dt = DeviceTrackers(qg, W2["N"], dev, n_clients=W2["G"],
                             client_of_slot=cmap[mine], lagged=lagged)
+        gg = None
+        if grouped:  # (the members on a group's stream, the sums on its side stream)
+            from dmclock_amd.multiserver import GpuGroup
+            gg = GpuGroup(qg)
+            dt.attach_group(gg)
         decs = []
         k = W2["k"]
         for t, ep in eps:
@@ -309,6 +315,8 @@ def _device_trackers_worker(rank, world, port, out_q, backend="gloo", lagged=Fal
         dt.finish()
         st = dt.state()
         out_q.put((rank, st, decs, dt.allreduce_ms))
+        if gg is not None:
+            gg.close()
         for q in qg:
             q.close()
     finally:
@@ -340,21 +348,24 @@ def _oracle_reference(world, lag=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lagged", [False, True])
-def test_device_trackers_world1_rccl(lagged):
+@pytest.mark.parametrize("lagged,grouped", [(False, False), (True, False), (True, True)])
+def test_device_trackers_world1_rccl(lagged, grouped):
     """The RCCL branch of DeviceTrackers.deliver: one rank on GPU 0 in an
     `nccl` (RCCL) process group holding all four servers -- every epoch's
     all-reduce runs through RCCL on the device buffers (the identity at
     world size 1; the 8-GPU runs reduce over xGMI) -- against the oracle
     queues with the epoch restatement: every request's delta/rho, every
-    decision and the final tracker state bit-exact."""
+    decision and the final tracker state bit-exact.  grouped: the queues in a
+    GpuGroup with the trackers attached -- each epoch's sums on the group's
+    side stream, the RCCL all-reduce waiting for it on the device."""
     import torch.multiprocessing as mp
     from parity import compare_decisions
     ctx = mp.get_context("spawn")
     out_q = ctx.Queue()
     port = 31500 + os.getpid() % 1000
     p = ctx.Process(target=_device_trackers_worker,
-                    args=(0, 1, port + int(lagged), out_q, "nccl", lagged))
+                    args=(0, 1, port + int(lagged) + 2 * int(grouped), out_q, "nccl", lagged,
+                          grouped))
     p.start()
     try:
         rank, st, decs, ar_ms = out_q.get(timeout=240)
@@ -382,19 +393,22 @@ def test_device_trackers_world1_rccl(lagged):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lagged", [False, True])
-def test_device_trackers_world2_gloo(lagged):
+@pytest.mark.parametrize("lagged,grouped", [(False, False), (True, False), (True, True)])
+def test_device_trackers_world2_gloo(lagged, grouped):
     """Two ranks sharing GPU 0, two server queues each, device trackers with
     the per-epoch all-reduce of DeviceTrackers.deliver over gloo: every
     request's delta/rho, every decision and the final tracker state equal one
-    process running all four oracle queues with the epoch restatement."""
+    process running all four oracle queues with the epoch restatement
+    (grouped: each rank's queues in a GpuGroup, the sums on its side
+    stream, joined before the host-staged all-reduce)."""
     import torch.multiprocessing as mp
     from parity import compare_decisions
     ctx = mp.get_context("spawn")
     out_q = ctx.Queue()
     port = 30500 + os.getpid() % 1000
     procs = [ctx.Process(target=_device_trackers_worker,
-                         args=(r, 2, port + int(lagged), out_q, "gloo", lagged))
+                         args=(r, 2, port + int(lagged) + 2 * int(grouped), out_q, "gloo",
+                               lagged, grouped))
              for r in range(2)]
     for p in procs:
         p.start()
